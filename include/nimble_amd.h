@@ -1,0 +1,162 @@
+/*
+ * nimble_amd.h -- C-ABI boundary of the MI355X-native differentiable timestep.
+ *
+ * This is the drop-in boundary for the hot path that the reference exposes as
+ *   python/nimblephysics/timestep.py:13  TimestepLayer (torch.autograd.Function)
+ * whose forward calls
+ *   dart/neural/NeuralUtils.cpp:26       neural::forwardPass(world)  -> World::step
+ *   dart/simulation/World.cpp:221        World::step
+ * and whose backward calls
+ *   dart/neural/BackpropSnapshot.cpp:382 BackpropSnapshot::backpropState
+ *   dart/neural/BackpropSnapshot.cpp:121 BackpropSnapshot::backprop
+ *
+ * The reference binds those through pybind11 on one World object at a time.
+ * Here one call advances a whole batch of independent worlds (same model,
+ * different state) that live in device memory (HBM).  All pointers passed to
+ * nimble_forward / nimble_backward are DEVICE pointers; the stream is a
+ * hipStream_t passed as void* so that this header needs no HIP/torch types.
+ *
+ * Scalar type: double everywhere (the reference's s_t is double,
+ * dart/math/MathTypes.hpp:53).
+ */
+#ifndef NIMBLE_AMD_H_
+#define NIMBLE_AMD_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Joint types (subset of the dart/dynamics Joint classes on the hot path). */
+enum nimble_joint_type {
+  NIMBLE_JOINT_WELD = 0,      /* dart/dynamics/WeldJoint.hpp      0 dof */
+  NIMBLE_JOINT_REVOLUTE = 1,  /* dart/dynamics/RevoluteJoint.cpp  1 dof */
+  NIMBLE_JOINT_PRISMATIC = 2, /* dart/dynamics/PrismaticJoint.cpp 1 dof */
+  NIMBLE_JOINT_FREE = 3       /* dart/dynamics/FreeJoint.cpp      6 dof
+                                 (built with DART_USE_IDENTITY_JACOBIAN,
+                                 dart/CMakeLists.txt:184) */
+};
+
+/* Collision shape types (dart/collision/dart/DARTCollide.cpp:5030 collide()). */
+enum nimble_shape_type {
+  NIMBLE_SHAPE_BOX = 0,
+  NIMBLE_SHAPE_SPHERE = 1
+};
+
+#define NIMBLE_MAX_BODIES 64
+#define NIMBLE_MAX_DOFS 64
+#define NIMBLE_MAX_SHAPES 32
+/* Max contact points per world per step and LCP rows (3 per frictional
+ * contact, dart/constraint/ContactConstraint.cpp:147 mDim = 3). */
+#define NIMBLE_MAX_CONTACTS 16
+#define NIMBLE_MAX_LCP (3 * NIMBLE_MAX_CONTACTS)
+
+/*
+ * Flat description of a World (all skeletons of the world concatenated in
+ * World::addSkeleton order, bodies of each skeleton in DART tree order).
+ * Transforms are 3x4 row-major [R | p] (12 doubles).
+ */
+typedef struct nimble_world_desc {
+  int32_t num_bodies;
+  int32_t num_dofs;
+  int32_t num_shapes;
+  int32_t reserved;
+  double dt;                        /* World::mTimeStep (World.cpp:75)      */
+  double gravity[3];                /* World::mGravity                     */
+  double contact_clipping_depth;    /* World::mContactClippingDepth (0.03) */
+  double fallback_cfm;              /* World::mFallbackConstraintForceMixingConstant (1e-4) */
+  int32_t penetration_correction;   /* World::mPenetrationCorrectionEnabled (false) */
+  int32_t parallel_pos_vel;         /* World::mParallelVelocityAndPositionUpdates (true) */
+
+  /* per body [num_bodies] */
+  const int32_t* parent;            /* parent body index, -1 for a root    */
+  const int32_t* skeleton;          /* skeleton index                      */
+  const int32_t* joint_type;        /* nimble_joint_type of parent joint   */
+  const int32_t* dof_offset;        /* first world dof of the parent joint */
+  const int32_t* skeleton_mobile;   /* 1 if the body's skeleton is mobile  */
+  const double* T_parent_joint;     /* [12] Joint::mT_ParentBodyToJoint    */
+  const double* T_child_joint;      /* [12] Joint::mT_ChildBodyToJoint     */
+  const double* axis;               /* [3]  revolute / prismatic axis      */
+  const double* mass;               /* Inertia::mMass                      */
+  const double* com;                /* [3]  Inertia::mCenterOfMass         */
+  const double* moment;             /* [6]  Ixx Iyy Izz Ixy Ixz Iyz        */
+  const double* friction;           /* BodyNode friction coeff (1.0)       */
+  const double* restitution;        /* BodyNode restitution coeff (0.0)    */
+
+  /* per dof [num_dofs] */
+  const double* damping;
+  const double* spring;
+  const double* rest_position;
+  const double* pos_lower;
+  const double* pos_upper;
+  const double* vel_lower;
+  const double* vel_upper;
+  const double* force_lower;
+  const double* force_upper;
+
+  /* per collision shape [num_shapes] */
+  const int32_t* shape_body;
+  const int32_t* shape_type;        /* nimble_shape_type                   */
+  const double* shape_size;         /* [3] box size, or radius in [0]      */
+  const double* shape_T;            /* [12] ShapeNode relative transform   */
+} nimble_world_desc;
+
+typedef struct nimble_world* nimble_world_t;
+
+/* Error codes. */
+#define NIMBLE_OK 0
+#define NIMBLE_ERR_INVALID 1
+#define NIMBLE_ERR_HIP 2
+#define NIMBLE_ERR_UNSUPPORTED 3
+
+/*
+ * Upload a world description to the device.  Replaces the reference's
+ * World construction + Skeleton loading (dart/simulation/World.cpp:70,
+ * dart/utils/urdf/DartLoader.cpp:199) for the hot path.
+ */
+int nimble_world_create(const nimble_world_desc* desc, nimble_world_t* out);
+int nimble_world_destroy(nimble_world_t world);
+
+/* Number of doubles of per-world snapshot workspace (the batched
+ * BackpropSnapshot, dart/neural/BackpropSnapshot.cpp:34) and of the per-world
+ * LCP warm-start cache (BoxedLcpConstraintSolver::mX,
+ * dart/constraint/BoxedLcpConstraintSolver.cpp:180). */
+int64_t nimble_snapshot_doubles(nimble_world_t world);
+int64_t nimble_lcp_cache_doubles(nimble_world_t world);
+
+/*
+ * Batched differentiable forward step == neural::forwardPass + World::step
+ * on each of `batch` worlds.
+ *   state      [batch][2*num_dofs]  (positions | velocities), device
+ *   forces     [batch][num_dofs]    control forces, device
+ *   lcp_cache  [batch][lcp_cache_doubles] warm start, read + updated, device
+ *   next_state [batch][2*num_dofs]  output, device
+ *   snapshot   [batch][snapshot_doubles]  output, consumed by nimble_backward
+ */
+int nimble_forward(nimble_world_t world, int32_t batch, const double* state,
+                   const double* forces, double* lcp_cache, double* next_state,
+                   double* snapshot, void* stream);
+
+/*
+ * Batched analytic backward == BackpropSnapshot::backpropState on each world
+ * (dart/neural/BackpropSnapshot.cpp:382), with the Jacobian-transpose products
+ * of BackpropSnapshot::backprop (BackpropSnapshot.cpp:161-183) and
+ * clipLossGradientsToBounds (BackpropSnapshot.cpp:425).
+ *   grad_next_state [batch][2*num_dofs]  dL/d(next_state), device
+ *   grad_state      [batch][2*num_dofs]  dL/d(state) output, device
+ *   grad_forces     [batch][num_dofs]    dL/d(forces) output, device
+ */
+int nimble_backward(nimble_world_t world, int32_t batch, const double* state,
+                    const double* forces, const double* snapshot,
+                    const double* grad_next_state, double* grad_state,
+                    double* grad_forces, void* stream);
+
+/* Last error message (thread-local). */
+const char* nimble_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NIMBLE_AMD_H_ */

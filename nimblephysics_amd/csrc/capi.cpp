@@ -1,0 +1,205 @@
+// C-ABI implementation (include/nimble_amd.h): model upload and kernel
+// launches.  Host-side C++ calling HIP; no torch types cross this boundary.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "model.h"
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                        \
+  do {                                                                       \
+    hipError_t _e = (expr);                                                  \
+    if (_e != hipSuccess) return fail(NIMBLE_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+struct nimble_world {
+  ModelDev host;
+  ModelDev* dev = nullptr;
+  Layout fwd, bwd;
+  int snapDoubles = 1;
+  int cacheDoubles = NIMBLE_MAX_LCP + 1;
+  hipFunction_t dummy = nullptr;
+};
+
+extern "C" __global__ void nimble_forward_kernel(const ModelDev*, Layout, int, const double*, const double*, double*,
+                                                 double*, double*, int, int);
+extern "C" __global__ void nimble_backward_kernel(const ModelDev*, Layout, int, const double*, const double*,
+                                                  const double*, int, const double*, double*, double*);
+
+static void isoInverse(const double* T, double* O) {
+  // [R|p]^-1 = [R^T | -R^T p]
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++) O[r * 4 + c] = T[c * 4 + r];
+  for (int r = 0; r < 3; r++) O[r * 4 + 3] = -(O[r * 4] * T[3] + O[r * 4 + 1] * T[7] + O[r * 4 + 2] * T[11]);
+}
+
+static Layout makeLayout(const ModelDev& m, bool backward) {
+  Layout L{};
+  int o = 0;
+  auto take = [&](int count) { int r = o; o += (count + 1) & ~1; return r; };
+  const int n = m.n, nb = m.nb;
+  L.q = take(n); L.v = take(n); L.tau = take(n);
+  L.Tw = take(12 * nb); L.Sw = take(6 * n); L.V = take(6 * nb); L.A = take(6 * nb);
+  L.IC = take(36 * nb); L.F = take(6 * nb); L.M = take(n * n); L.rhs = take(n); L.x = take(n);
+  L.scratch = take(24 * 6);
+  L.ct = take(8);
+  if (backward) {
+    L.B1 = take(36 * nb); L.B23 = take(36 * nb); L.B4 = take(36 * nb);
+    L.P = take(6 * nb); L.H = take(6 * nb); L.w = take(n); L.gp = take(n); L.gv = take(n); L.out = take(3 * n);
+  }
+  L.total = o;
+  return L;
+}
+
+extern "C" {
+
+const char* nimble_last_error(void) { return g_err.c_str(); }
+
+int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
+  if (!d || !out) return fail(NIMBLE_ERR_INVALID, "null argument");
+  if (d->num_bodies <= 0 || d->num_bodies > NB_MAX) return fail(NIMBLE_ERR_INVALID, "num_bodies out of range");
+  if (d->num_dofs < 0 || d->num_dofs > ND_MAX || d->num_dofs > 64)
+    return fail(NIMBLE_ERR_INVALID, "num_dofs out of range");
+  if (d->num_shapes < 0 || d->num_shapes > NS_MAX) return fail(NIMBLE_ERR_INVALID, "num_shapes out of range");
+  auto* w = new nimble_world();
+  ModelDev& m = w->host;
+  std::memset(&m, 0, sizeof(m));
+  m.nb = d->num_bodies;
+  m.n = d->num_dofs;
+  m.ns = d->num_shapes;
+  m.dt = d->dt;
+  for (int i = 0; i < 3; i++) m.g[i] = d->gravity[i];
+  m.clipDepth = d->contact_clipping_depth;
+  m.fallbackCfm = d->fallback_cfm;
+  m.penCorr = d->penetration_correction;
+  m.parallelPosVel = d->parallel_pos_vel;
+  int dofCount = 0;
+  for (int b = 0; b < m.nb; b++) {
+    int p = d->parent[b];
+    if (p >= b) { delete w; return fail(NIMBLE_ERR_INVALID, "bodies must be in topological order"); }
+    m.parent[b] = p;
+    m.jtype[b] = d->joint_type[b];
+    m.dof0[b] = d->dof_offset[b];
+    m.ndof[b] = m.jtype[b] == NIMBLE_JOINT_WELD ? 0 : (m.jtype[b] == NIMBLE_JOINT_FREE ? 6 : 1);
+    m.depth[b] = p >= 0 ? m.depth[p] + 1 : 0;
+    if (m.depth[b] > m.maxDepth) m.maxDepth = m.depth[b];
+    m.anc[b] = (p >= 0 ? m.anc[p] : 0ull) | (1ull << b);
+    m.skel[b] = d->skeleton[b];
+    std::memcpy(m.Tpj[b], d->T_parent_joint + 12 * b, 12 * sizeof(double));
+    std::memcpy(m.Tcj[b], d->T_child_joint + 12 * b, 12 * sizeof(double));
+    isoInverse(m.Tcj[b], m.TcjInv[b]);
+    for (int i = 0; i < 3; i++) m.axis[b][i] = d->axis[3 * b + i];
+    m.mass[b] = d->mass[b];
+    for (int i = 0; i < 3; i++) m.com[b][i] = d->com[3 * b + i];
+    const double* mo = d->moment + 6 * b;
+    double I[9] = {mo[0], mo[3], mo[4], mo[3], mo[1], mo[5], mo[4], mo[5], mo[2]};
+    std::memcpy(m.Ic[b], I, sizeof(I));
+    m.friction[b] = d->friction[b];
+    m.restitution[b] = d->restitution[b];
+    for (int k = 0; k < m.ndof[b]; k++) m.dofBody[m.dof0[b] + k] = b;
+    dofCount += m.ndof[b];
+    if (m.jtype[b] == NIMBLE_JOINT_FREE) {
+      if (m.numFree >= 8) { delete w; return fail(NIMBLE_ERR_UNSUPPORTED, "more than 8 free joints"); }
+      m.freeBody[m.numFree++] = b;
+    }
+  }
+  if (dofCount != m.n) { delete w; return fail(NIMBLE_ERR_INVALID, "dof count mismatch"); }
+  // BodyNode::isReactive (BodyNode.cpp:2384): mobile skeleton with dependent dofs
+  for (int b = 0; b < m.nb; b++) {
+    bool hasDof = false;
+    for (int a = b; a >= 0; a = m.parent[a]) if (m.ndof[a] > 0) { hasDof = true; break; }
+    m.reactive[b] = (d->skeleton_mobile[b] && hasDof) ? 1 : 0;
+  }
+  for (int i = 0; i < m.n; i++) {
+    m.damping[i] = d->damping[i]; m.spring[i] = d->spring[i]; m.rest[i] = d->rest_position[i];
+    m.posLo[i] = d->pos_lower[i]; m.posHi[i] = d->pos_upper[i];
+    m.velLo[i] = d->vel_lower[i]; m.velHi[i] = d->vel_upper[i];
+    m.forceLo[i] = d->force_lower[i]; m.forceHi[i] = d->force_upper[i];
+  }
+  for (int sIdx = 0; sIdx < m.ns; sIdx++) {
+    m.shapeBody[sIdx] = d->shape_body[sIdx];
+    m.shapeType[sIdx] = d->shape_type[sIdx];
+    for (int i = 0; i < 3; i++) m.shapeSize[sIdx][i] = d->shape_size[3 * sIdx + i];
+    std::memcpy(m.shapeT[sIdx], d->shape_T + 12 * sIdx, 12 * sizeof(double));
+  }
+  // Candidate pairs: DARTCollisionDetector::collide (DARTCollisionDetector.cpp:127)
+  // object order i<j filtered by BodyNodeCollisionFilter (CollisionFilter.cpp:105)
+  m.numPairs = 0;
+  for (int i = 0; i < m.ns; i++)
+    for (int j = i + 1; j < m.ns; j++) {
+      int bi = m.shapeBody[i], bj = m.shapeBody[j];
+      if (bi == bj) continue;
+      int si = m.skel[bi], sj = m.skel[bj];
+      if (!d->skeleton_mobile[bi] && !d->skeleton_mobile[bj]) continue;
+      if (si == sj) continue;  // self-collision checking is off by default
+      m.pairA[m.numPairs] = i;
+      m.pairB[m.numPairs] = j;
+      m.numPairs++;
+    }
+  w->fwd = makeLayout(m, false);
+  w->bwd = makeLayout(m, true);
+  if (w->bwd.total * 8 > 160 * 1024) { delete w; return fail(NIMBLE_ERR_UNSUPPORTED, "model too large for LDS"); }
+  hipError_t e = hipMalloc(&w->dev, sizeof(ModelDev));
+  if (e != hipSuccess) { delete w; return fail(NIMBLE_ERR_HIP, std::string("hipMalloc: ") + hipGetErrorString(e)); }
+  e = hipMemcpy(w->dev, &m, sizeof(ModelDev), hipMemcpyHostToDevice);
+  if (e != hipSuccess) { hipFree(w->dev); delete w; return fail(NIMBLE_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e)); }
+  *out = w;
+  return NIMBLE_OK;
+}
+
+int nimble_world_destroy(nimble_world_t w) {
+  if (!w) return NIMBLE_OK;
+  if (w->dev) hipFree(w->dev);
+  delete w;
+  return NIMBLE_OK;
+}
+
+int64_t nimble_snapshot_doubles(nimble_world_t w) { return w ? w->snapDoubles : -1; }
+int64_t nimble_lcp_cache_doubles(nimble_world_t w) { return w ? w->cacheDoubles : -1; }
+
+static int gridFor(int batch) {
+  // one wave per world; cap the grid so every wave loops over several worlds
+  // only when the batch exceeds 64k
+  return batch < 65536 ? batch : 65536;
+}
+
+int nimble_forward(nimble_world_t w, int32_t batch, const double* state, const double* forces, double* lcp_cache,
+                   double* next_state, double* snapshot, void* stream) {
+  if (!w || batch < 0) return fail(NIMBLE_ERR_INVALID, "bad arguments");
+  if (batch == 0) return NIMBLE_OK;
+  if (!state || !forces || !next_state) return fail(NIMBLE_ERR_INVALID, "null buffer");
+  hipStream_t st = (hipStream_t)stream;
+  const size_t lds = (size_t)w->fwd.total * sizeof(double);
+  hipLaunchKernelGGL(nimble_forward_kernel, dim3(gridFor(batch)), dim3(64), lds, st, w->dev, w->fwd, batch, state,
+                     forces, lcp_cache, next_state, snapshot, w->snapDoubles, w->cacheDoubles);
+  HIP_TRY(hipGetLastError());
+  return NIMBLE_OK;
+}
+
+int nimble_backward(nimble_world_t w, int32_t batch, const double* state, const double* forces,
+                    const double* snapshot, const double* grad_next_state, double* grad_state,
+                    double* grad_forces, void* stream) {
+  if (!w || batch < 0) return fail(NIMBLE_ERR_INVALID, "bad arguments");
+  if (batch == 0) return NIMBLE_OK;
+  if (!state || !forces || !grad_next_state || !grad_state || !grad_forces)
+    return fail(NIMBLE_ERR_INVALID, "null buffer");
+  hipStream_t st = (hipStream_t)stream;
+  const size_t lds = (size_t)w->bwd.total * sizeof(double);
+  hipLaunchKernelGGL(nimble_backward_kernel, dim3(gridFor(batch)), dim3(64), lds, st, w->dev, w->bwd, batch, state,
+                     forces, snapshot, w->snapDoubles, grad_next_state, grad_state, grad_forces);
+  HIP_TRY(hipGetLastError());
+  return NIMBLE_OK;
+}
+
+}  // extern "C"

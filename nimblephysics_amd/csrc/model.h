@@ -1,0 +1,51 @@
+// Device-side model constants for the batched differentiable timestep.
+// Built once on the host from nimble_world_desc (include/nimble_amd.h) and read
+// by every world-instance wavefront through the scalar cache (all indices into
+// it are wave-uniform).
+#pragma once
+#include <stdint.h>
+
+#include "../../include/nimble_amd.h"
+
+#define NB_MAX NIMBLE_MAX_BODIES
+#define ND_MAX NIMBLE_MAX_DOFS
+#define NS_MAX NIMBLE_MAX_SHAPES
+
+struct ModelDev {
+  int nb, n, ns, maxDepth;
+  int numFree;
+  int freeBody[8];
+  double dt, g[3], clipDepth, fallbackCfm;
+  int penCorr, parallelPosVel;
+  // per body
+  int parent[NB_MAX], jtype[NB_MAX], dof0[NB_MAX], ndof[NB_MAX], depth[NB_MAX];
+  int skel[NB_MAX], reactive[NB_MAX];
+  unsigned long long anc[NB_MAX];  // bit a set <=> body a is an ancestor-or-self
+  double Tpj[NB_MAX][12];          // [R|p] row-major
+  double Tcj[NB_MAX][12];
+  double TcjInv[NB_MAX][12];
+  double axis[NB_MAX][3];
+  double mass[NB_MAX], com[NB_MAX][3], Ic[NB_MAX][9];
+  double friction[NB_MAX], restitution[NB_MAX];
+  // per dof
+  int dofBody[ND_MAX];
+  double damping[ND_MAX], spring[ND_MAX], rest[ND_MAX];
+  double posLo[ND_MAX], posHi[ND_MAX], velLo[ND_MAX], velHi[ND_MAX], forceLo[ND_MAX], forceHi[ND_MAX];
+  // collision shapes
+  int shapeBody[NS_MAX], shapeType[NS_MAX];
+  double shapeSize[NS_MAX][3];
+  double shapeT[NS_MAX][12];
+  // candidate pairs (i < j) after BodyNodeCollisionFilter, in detector order
+  int numPairs;
+  int pairA[NS_MAX * 4], pairB[NS_MAX * 4];
+};
+
+// LDS layout (in doubles) for one world instance; offsets computed on host.
+struct Layout {
+  int q, v, tau, Tw, Sw, V, A, IC, F, M, rhs, x, scratch;
+  // backward extras
+  int B1, B23, B4, P, H, w, gp, gv, out;
+  // contacts
+  int ct;
+  int total;
+};

@@ -1,0 +1,576 @@
+// Batched differentiable timestep for gfx950 (MI355X).
+//
+// One world instance per 64-lane wavefront (one workgroup = one wave), all of
+// its working set staged in LDS.  The reference advances one World at a time
+// on the CPU (dart/simulation/World.cpp:221 World::step, with the
+// articulated-body recursions of dart/dynamics/Skeleton.cpp:13034); here every
+// quantity is kept in WORLD coordinates, which turns the per-body frame
+// changes of the body-frame recursions into plain sums:
+//   * forward kinematics / velocities / bias accelerations: one lane per body,
+//     level-synchronous over tree depth;
+//   * composite (subtree) inertias and forces: one lane per matrix element,
+//     reverse body order;
+//   * mass matrix M_jk = S_j^T I^C S_k: one lane per (j,k) pair (CRBA);
+//   * M = L L^T and the solves: right-looking Cholesky, lanes over rows;
+//   * backward: one lane per input direction (q_k, v_k, tau_k), each lane
+//     forming its column of dID/dq and dC/dv in closed form from the
+//     world-frame composites and dotting it with Minv * dL/dv'.
+#include <hip/hip_runtime.h>
+
+#include "model.h"
+#include "spatial.cuh"
+
+#define WAVE 64
+
+// ---------------------------------------------------------------------------
+// Forward kinematics + velocities + velocity-product (bias) accelerations.
+//   Tw[b]  world transform of body b
+//   Sw[k]  world-frame motion subspace column of dof k
+//   V[b]   world-frame spatial velocity
+//   A[b]   world-frame acceleration with ddq = `ddq` (nullptr => 0)
+// Reference: BodyNode::updateTransform / updateVelocity /
+// updatePartialAcceleration (dart/dynamics/BodyNode.cpp:1960-1983).
+// ---------------------------------------------------------------------------
+__device__ void kinematics(const ModelDev& md, double* s, const Layout& L, int lane, const double* ddq) {
+  const double* q = s + L.q;
+  const double* v = s + L.v;
+  for (int lev = 0; lev <= md.maxDepth; lev++) {
+    const int b = lane;
+    if (b < md.nb && md.depth[b] == lev) {
+      const int jt = md.jtype[b];
+      const int o = md.dof0[b];
+      double Q[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+      const double* a = md.axis[b];
+      if (jt == NIMBLE_JOINT_REVOLUTE) {
+        // math::expAngular(axis * q) (Geometry.cpp:3414)
+        double c = cos(q[o]), sn = sin(q[o]), t = 1.0 - c;
+        Q[0] = c + t * a[0] * a[0];        Q[1] = t * a[0] * a[1] - sn * a[2]; Q[2] = t * a[0] * a[2] + sn * a[1];
+        Q[4] = t * a[0] * a[1] + sn * a[2]; Q[5] = c + t * a[1] * a[1];        Q[6] = t * a[1] * a[2] - sn * a[0];
+        Q[8] = t * a[0] * a[2] - sn * a[1]; Q[9] = t * a[1] * a[2] + sn * a[0]; Q[10] = c + t * a[2] * a[2];
+      } else if (jt == NIMBLE_JOINT_PRISMATIC) {
+        Q[3] = a[0] * q[o]; Q[7] = a[1] * q[o]; Q[11] = a[2] * q[o];
+      } else if (jt == NIMBLE_JOINT_FREE) {
+        double R[9];
+        expMapRot(q + o, R);
+        Q[0] = R[0]; Q[1] = R[1]; Q[2] = R[2]; Q[3] = q[o + 3];
+        Q[4] = R[3]; Q[5] = R[4]; Q[6] = R[5]; Q[7] = q[o + 4];
+        Q[8] = R[6]; Q[9] = R[7]; Q[10] = R[8]; Q[11] = q[o + 5];
+      }
+      double T[12];
+      tmul(md.Tpj[b], Q, T);
+      tmul(T, md.TcjInv[b], T);
+      double* Tw = s + L.Tw + 12 * b;
+      const int p = md.parent[b];
+      double Vp[6] = {0, 0, 0, 0, 0, 0}, Ap[6] = {0, 0, 0, 0, 0, 0};
+      if (p >= 0) {
+        tmul(s + L.Tw + 12 * p, T, Tw);
+#pragma unroll
+        for (int i = 0; i < 6; i++) { Vp[i] = s[L.V + 6 * p + i]; Ap[i] = s[L.A + 6 * p + i]; }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 12; i++) Tw[i] = T[i];
+      }
+      // motion subspace in world frame: Ad_{Tw * Tcj} * S_local
+      double TwC[12];
+      tmul(Tw, md.Tcj[b], TwC);
+      double vj[6] = {0, 0, 0, 0, 0, 0}, aj[6] = {0, 0, 0, 0, 0, 0};
+      const int nd = md.ndof[b];
+      for (int k = 0; k < nd; k++) {
+        double loc[6] = {0, 0, 0, 0, 0, 0};
+        if (jt == NIMBLE_JOINT_REVOLUTE) { loc[0] = a[0]; loc[1] = a[1]; loc[2] = a[2]; }
+        else if (jt == NIMBLE_JOINT_PRISMATIC) { loc[3] = a[0]; loc[4] = a[1]; loc[5] = a[2]; }
+        else loc[k] = 1.0;
+        double* S = s + L.Sw + 6 * (o + k);
+        adT(TwC, loc, S);
+        const double qd = v[o + k];
+        const double qdd = ddq ? ddq[o + k] : 0.0;
+#pragma unroll
+        for (int i = 0; i < 6; i++) { vj[i] = fma(S[i], qd, vj[i]); aj[i] = fma(S[i], qdd, aj[i]); }
+      }
+      double Vb[6];
+#pragma unroll
+      for (int i = 0; i < 6; i++) Vb[i] = Vp[i] + vj[i];
+      double cr[6];
+      crm(Vb, vj, cr);  // d/dt(S) qdot = V_child x (S qdot)
+#pragma unroll
+      for (int i = 0; i < 6; i++) {
+        s[L.V + 6 * b + i] = Vb[i];
+        s[L.A + 6 * b + i] = Ap[i] + aj[i] + cr[i];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// World-frame spatial inertia of body b (6x6, row-major) at the world origin.
+// dart/dynamics/Inertia.cpp:1368 computeSpatialTensor in world axes.
+__device__ void worldInertia(const ModelDev& md, const double* Tw, int b, double* I) {
+  const double m = md.mass[b];
+  double cw[3], Rc[9], tmp[9];
+  for (int r = 0; r < 3; r++) cw[r] = Tw[r * 4] * md.com[b][0] + Tw[r * 4 + 1] * md.com[b][1] + Tw[r * 4 + 2] * md.com[b][2] + Tw[r * 4 + 3];
+  // R Ic R^T
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++)
+      tmp[r * 3 + c] = Tw[r * 4] * md.Ic[b][c] + Tw[r * 4 + 1] * md.Ic[b][3 + c] + Tw[r * 4 + 2] * md.Ic[b][6 + c];
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++)
+      Rc[r * 3 + c] = tmp[r * 3] * Tw[c * 4] + tmp[r * 3 + 1] * Tw[c * 4 + 1] + tmp[r * 3 + 2] * Tw[c * 4 + 2];
+  const double C[9] = {0, -cw[2], cw[1], cw[2], 0, -cw[0], -cw[1], cw[0], 0};
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++) {
+      // C C^T
+      double cct = C[r * 3] * C[c * 3] + C[r * 3 + 1] * C[c * 3 + 1] + C[r * 3 + 2] * C[c * 3 + 2];
+      I[r * 6 + c] = Rc[r * 3 + c] + m * cct;
+      I[r * 6 + c + 3] = m * C[r * 3 + c];
+      I[(r + 3) * 6 + c] = m * C[c * 3 + r];
+      I[(r + 3) * 6 + c + 3] = (r == c) ? m : 0.0;
+    }
+}
+
+// Composite inertias IC[b] (subtree sums) and bias forces F[b] = sum over the
+// subtree of  I_i (A_i - a_g) + V_i x* (I_i V_i)  -- the world-frame
+// restatement of BodyNode::updateTransmittedForceID (BodyNode.cpp:1994).
+__device__ void composites(const ModelDev& md, double* s, const Layout& L, int lane) {
+  const double ag[6] = {0, 0, 0, md.g[0], md.g[1], md.g[2]};
+  if (lane < md.nb) {
+    const int b = lane;
+    double* I = s + L.IC + 36 * b;
+    worldInertia(md, s + L.Tw + 12 * b, b, I);
+    double u[6], h[6], f[6], vxh[6];
+    for (int i = 0; i < 6; i++) u[i] = s[L.A + 6 * b + i] - ag[i];
+    mv6(I, u, f);
+    mv6(I, s + L.V + 6 * b, h);
+    crf(s + L.V + 6 * b, h, vxh);
+    for (int i = 0; i < 6; i++) s[L.F + 6 * b + i] = f[i] + vxh[i];
+  }
+  __syncthreads();
+  for (int b = md.nb - 1; b > 0; b--) {
+    const int p = md.parent[b];
+    if (p >= 0) {
+      if (lane < 36) s[L.IC + 36 * p + lane] += s[L.IC + 36 * b + lane];
+      else if (lane < 42) s[L.F + 6 * p + lane - 36] += s[L.F + 6 * b + lane - 36];
+    }
+    __syncthreads();
+  }
+}
+
+// M_jk = S_j^T IC_{deeper(j,k)} S_k (composite-rigid-body algorithm), and the
+// generalized bias C_j = S_j . F_body(j).  M is stored full (n x n) at L.M.
+__device__ void massMatrixAndBias(const ModelDev& md, double* s, const Layout& L, int lane, double* C) {
+  const int n = md.n;
+  const int pairs = n * (n + 1) / 2;
+  for (int t = lane; t < pairs; t += WAVE) {
+    // unrank t -> (j >= k)
+    int j = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+    while (j * (j + 1) / 2 > t) j--;
+    while ((j + 1) * (j + 2) / 2 <= t) j++;
+    const int k = t - j * (j + 1) / 2;
+    const int bj = md.dofBody[j], bk = md.dofBody[k];
+    int deep = -1;
+    if ((md.anc[bj] >> bk) & 1ull) deep = bj;
+    else if ((md.anc[bk] >> bj) & 1ull) deep = bk;
+    double val = 0.0;
+    if (deep >= 0) {
+      double tmp[6];
+      mv6(s + L.IC + 36 * deep, s + L.Sw + 6 * k, tmp);
+      val = dot6(s + L.Sw + 6 * j, tmp);
+    }
+    s[L.M + j * n + k] = val;
+    s[L.M + k * n + j] = val;
+  }
+  for (int j = lane; j < n; j += WAVE) C[j] = dot6(s + L.Sw + 6 * j, s + L.F + 6 * md.dofBody[j]);
+  __syncthreads();
+}
+
+// In-place Cholesky of the n x n matrix at A (lower triangle holds L).
+__device__ void cholesky(double* A, int n, int lane) {
+  for (int j = 0; j < n; j++) {
+    if (lane == 0) A[j * n + j] = sqrt(A[j * n + j]);
+    __syncthreads();
+    const double d = A[j * n + j];
+    for (int i = j + 1 + lane; i < n; i += WAVE) A[i * n + j] /= d;
+    __syncthreads();
+    const int m = n - j - 1;
+    const int cnt = m * (m + 1) / 2;
+    for (int t = lane; t < cnt; t += WAVE) {
+      int r = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+      while (r * (r + 1) / 2 > t) r--;
+      while ((r + 1) * (r + 2) / 2 <= t) r++;
+      const int c = t - r * (r + 1) / 2;
+      const int i = j + 1 + r, k = j + 1 + c;
+      A[i * n + k] -= A[i * n + j] * A[k * n + j];
+    }
+    __syncthreads();
+  }
+}
+
+// Solve L L^T x = b in place (x = b on entry).
+__device__ void cholSolve(const double* Lm, double* x, int n, int lane) {
+  for (int j = 0; j < n; j++) {
+    if (lane == 0) x[j] /= Lm[j * n + j];
+    __syncthreads();
+    const double xj = x[j];
+    for (int i = j + 1 + lane; i < n; i += WAVE) x[i] -= Lm[i * n + j] * xj;
+    __syncthreads();
+  }
+  for (int j = n - 1; j >= 0; j--) {
+    if (lane == 0) x[j] /= Lm[j * n + j];
+    __syncthreads();
+    const double xj = x[j];
+    for (int i = lane; i < j; i += WAVE) x[i] -= Lm[j * n + i] * xj;
+    __syncthreads();
+  }
+}
+
+__device__ void loadState(const ModelDev& md, double* s, const Layout& L, int lane, const double* state,
+                          const double* tau) {
+  const int n = md.n;
+  for (int i = lane; i < n; i += WAVE) {
+    s[L.q + i] = state[i];
+    s[L.v + i] = state[n + i];
+    s[L.tau + i] = tau[i];
+  }
+  __syncthreads();
+}
+
+// Everything up to the factored mass matrix; leaves C in s[L.rhs].
+__device__ void coreDynamics(const ModelDev& md, double* s, const Layout& L, int lane) {
+  kinematics(md, s, L, lane, nullptr);
+  composites(md, s, L, lane);
+  massMatrixAndBias(md, s, L, lane, s + L.rhs);
+  cholesky(s + L.M, md.n, lane);
+}
+
+// ---------------------------------------------------------------------------
+// Forward step.
+// ---------------------------------------------------------------------------
+extern "C" __global__ void __launch_bounds__(WAVE)
+nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, const double* __restrict__ state,
+                      const double* __restrict__ forces, double* __restrict__ lcpCache,
+                      double* __restrict__ nextState, double* __restrict__ snapshot, int snapDoubles,
+                      int cacheDoubles) {
+  extern __shared__ double s[];
+  const ModelDev& md = *mdp;
+  const int lane = threadIdx.x;
+  const int n = md.n;
+  for (int env = blockIdx.x; env < batch; env += gridDim.x) {
+    const double* st = state + (size_t)env * 2 * n;
+    loadState(md, s, L, lane, st, forces + (size_t)env * n);
+    coreDynamics(md, s, L, lane);
+    // rhs = tau + spring + damping - C   (GenericJoint::updateTotalForceDynamic)
+    double* x = s + L.x;
+    for (int i = lane; i < n; i += WAVE) {
+      const double qi = s[L.q + i], vi = s[L.v + i];
+      const double springF = -md.spring[i] * (qi - md.rest[i] + vi * md.dt);
+      const double dampF = -md.damping[i] * vi;
+      x[i] = s[L.tau + i] + springF + dampF - s[L.rhs + i];
+    }
+    __syncthreads();
+    cholSolve(s + L.M, x, n, lane);  // x = ddq
+    double* out = nextState + (size_t)env * 2 * n;
+    // integrateVelocities (Skeleton.cpp:9329): v1 = v + dt ddq
+    for (int i = lane; i < n; i += WAVE) out[n + i] = s[L.v + i] + md.dt * x[i];
+    // integratePositions(initialVelocity) (World.cpp:300)
+    if (lane < md.nb) {
+      const int b = lane, o = md.dof0[b];
+      const int jt = md.jtype[b];
+      if (jt == NIMBLE_JOINT_REVOLUTE || jt == NIMBLE_JOINT_PRISMATIC) {
+        out[o] = s[L.q + o] + s[L.v + o] * md.dt;
+      } else if (jt == NIMBLE_JOINT_FREE) {
+        double r[6];
+        freeIntegrate(s + L.q + o, s + L.v + o, md.dt, r);
+        for (int i = 0; i < 6; i++) out[o + i] = r[i];
+      }
+    }
+    (void)lcpCache; (void)snapshot; (void)snapDoubles; (void)cacheDoubles;
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Backward: BackpropSnapshot::backprop (dart/neural/BackpropSnapshot.cpp:121)
+// as vector-Jacobian products, no full Jacobian is ever formed.
+// ---------------------------------------------------------------------------
+
+// Per-body derivative composites at the state (q, v, a*):
+//   P = sum I u,  H = sum I V,  F = sum (I u + V x* I V),
+//   B1 = sum I [V x],  B23 = sum ([V x*] G(h) - G(h) [V x]),  B4 = sum [V x*] I
+// with u = A - a_g, h = I V and G(h) m := m x* h.
+__device__ void derivativeComposites(const ModelDev& md, double* s, const Layout& L, int lane) {
+  const double ag[6] = {0, 0, 0, md.g[0], md.g[1], md.g[2]};
+  if (lane < md.nb) {
+    const int b = lane;
+    double I[36];
+    worldInertia(md, s + L.Tw + 12 * b, b, I);
+    const double* V = s + L.V + 6 * b;
+    double u[6], h[6], Iu[6], vxh[6];
+    for (int i = 0; i < 6; i++) u[i] = s[L.A + 6 * b + i] - ag[i];
+    mv6(I, u, Iu);
+    mv6(I, V, h);
+    crf(V, h, vxh);
+    for (int i = 0; i < 6; i++) {
+      s[L.P + 6 * b + i] = Iu[i];
+      s[L.H + 6 * b + i] = h[i];
+      s[L.F + 6 * b + i] = Iu[i] + vxh[i];
+    }
+    // column-wise products: column c of each matrix is the image of e_c
+    for (int c = 0; c < 6; c++) {
+      double e[6] = {0, 0, 0, 0, 0, 0};
+      e[c] = 1.0;
+      double vxe[6], t1[6], t2[6], t3[6], Gh[6];
+      crm(V, e, vxe);          // [V x] e
+      mv6(I, vxe, t1);         // B1 col
+      // G(h) e = e x* h ;  [V x*] G(h) e
+      crf(e, h, Gh);
+      crf(V, Gh, t2);
+      // G(h) [V x] e = (V x e) x* h
+      crf(vxe, h, t3);
+      double Ie[6], t4[6];
+      for (int r = 0; r < 6; r++) Ie[r] = I[r * 6 + c];
+      crf(V, Ie, t4);          // [V x*] I e
+      for (int r = 0; r < 6; r++) {
+        s[L.B1 + 36 * b + r * 6 + c] = t1[r];
+        s[L.B23 + 36 * b + r * 6 + c] = t2[r] - t3[r];
+        s[L.B4 + 36 * b + r * 6 + c] = t4[r];
+      }
+    }
+  }
+  __syncthreads();
+  for (int b = md.nb - 1; b > 0; b--) {
+    const int p = md.parent[b];
+    if (p >= 0) {
+      for (int t = lane; t < 126; t += WAVE) {
+        int off;
+        if (t < 36) off = L.B1 + t;
+        else if (t < 72) off = L.B23 + (t - 36);
+        else if (t < 108) off = L.B4 + (t - 72);
+        else if (t < 114) off = L.P + (t - 108);
+        else if (t < 120) off = L.H + (t - 114);
+        else off = L.F + (t - 120);
+        const int stride = (t < 108) ? 36 : 6;
+        s[off + stride * p] += s[off + stride * b];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// dF_c for a subtree motion with generator Z and base (V_lambda, u_lambda):
+__device__ void dForcePos(const double* s, const Layout& L, int c, const double* Z, const double* Vl,
+                          const double* ul, const double* Psi, const double* ZxVl, double* out) {
+  const double* IC = s + L.IC + 36 * c;
+  double t[6], a[6], r[6];
+  crf(Z, s + L.P + 6 * c, r);                   //  Z x* P
+  crm(Z, ul, t); mv6(IC, t, a);                 // -IC (Z x u_l)
+  for (int i = 0; i < 6; i++) r[i] -= a[i];
+  mv6(s + L.B1 + 36 * c, Psi, a);               // -B1 Psi
+  for (int i = 0; i < 6; i++) r[i] -= a[i];
+  crm(Psi, Vl, t); mv6(IC, t, a);               // -IC (Psi x V_l)
+  for (int i = 0; i < 6; i++) r[i] -= a[i];
+  mv6(s + L.B23 + 36 * c, Z, a);                // +B23 Z
+  for (int i = 0; i < 6; i++) r[i] += a[i];
+  crf(ZxVl, s + L.H + 6 * c, a);                // -(Z x V_l) x* H
+  for (int i = 0; i < 6; i++) r[i] -= a[i];
+  mv6(s + L.B4 + 36 * c, ZxVl, a);              // -B4 (Z x V_l)
+  for (int i = 0; i < 6; i++) out[i] = r[i] - a[i];
+}
+
+__device__ void dForceVel(const double* s, const Layout& L, int c, const double* S, const double* Vl,
+                          const double* Vb, double* out) {
+  const double* IC = s + L.IC + 36 * c;
+  double t1[6], t2[6], a[6], r[6];
+  crm(Vl, S, t1);
+  crm(S, Vb, t2);
+  for (int i = 0; i < 6; i++) t1[i] -= t2[i];
+  mv6(IC, t1, r);                               // IC (V_l x S - S x V_b)
+  mv6(s + L.B1 + 36 * c, S, a);                 // -B1 S
+  for (int i = 0; i < 6; i++) r[i] -= a[i];
+  crf(S, s + L.H + 6 * c, a);                   // +S x* H
+  for (int i = 0; i < 6; i++) r[i] += a[i];
+  mv6(s + L.B4 + 36 * c, S, a);                 // +B4 S
+  for (int i = 0; i < 6; i++) out[i] = r[i] + a[i];
+}
+
+// Right Jacobian of SO(3) exp (J_r(th) = I - (1-cos)/t^2 [th] + (t-sin)/t^3 [th]^2)
+__device__ void rightJacobianCol(const double* th, int k, double* o) {
+  const double t2 = th[0] * th[0] + th[1] * th[1] + th[2] * th[2];
+  const double t = sqrt(t2);
+  double a, b;
+  if (t < 1e-6) { a = 0.5; b = 1.0 / 6.0; }
+  else { a = (1.0 - cos(t)) / t2; b = (t - sin(t)) / (t2 * t); }
+  const double K[9] = {0, -th[2], th[1], th[2], 0, -th[0], -th[1], th[0], 0};
+  for (int r = 0; r < 3; r++) {
+    double k2 = K[r * 3] * K[k] + K[r * 3 + 1] * K[3 + k] + K[r * 3 + 2] * K[6 + k];
+    o[r] = (r == k ? 1.0 : 0.0) - a * K[r * 3 + k] + b * k2;
+  }
+}
+
+extern "C" __global__ void __launch_bounds__(WAVE)
+nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, const double* __restrict__ state,
+                       const double* __restrict__ forces, const double* __restrict__ snapshot, int snapDoubles,
+                       const double* __restrict__ gradNext, double* __restrict__ gradState,
+                       double* __restrict__ gradForces) {
+  extern __shared__ double s[];
+  const ModelDev& md = *mdp;
+  const int lane = threadIdx.x;
+  const int n = md.n;
+  const double dt = md.dt;
+  for (int env = blockIdx.x; env < batch; env += gridDim.x) {
+    loadState(md, s, L, lane, state + (size_t)env * 2 * n, forces + (size_t)env * n);
+    const double* gN = gradNext + (size_t)env * 2 * n;
+    for (int i = lane; i < n; i += WAVE) {
+      s[L.gp + i] = gN[i];
+      s[L.gv + i] = gN[n + i];
+    }
+    coreDynamics(md, s, L, lane);
+    // z = dt (tau - C - D v - K (q - q0 + dt v))   [+ constraint impulses]
+    double* x = s + L.x;
+    for (int i = lane; i < n; i += WAVE) {
+      const double qi = s[L.q + i], vi = s[L.v + i];
+      const double springF = md.spring[i] * (qi - md.rest[i] + dt * vi);
+      const double dampF = md.damping[i] * vi;
+      x[i] = dt * (s[L.tau + i] - s[L.rhs + i] - dampF - springF);
+    }
+    (void)snapshot; (void)snapDoubles;
+    __syncthreads();
+    cholSolve(s + L.M, x, n, lane);  // x = y = Minv z  => a* = y / dt
+    for (int i = lane; i < n; i += WAVE) x[i] /= dt;
+    __syncthreads();
+    kinematics(md, s, L, lane, x);  // A = accelerations at a*
+    derivativeComposites(md, s, L, lane);
+    // w = Minv gv
+    double* w = s + L.w;
+    for (int i = lane; i < n; i += WAVE) w[i] = s[L.gv + i];
+    __syncthreads();
+    cholSolve(s + L.M, w, n, lane);
+
+    // ---- per-direction columns -------------------------------------------
+    double gq = 0.0, gvOut = 0.0, gt = 0.0;
+    const int k = lane;
+    if (k < n) {
+      const int b = md.dofBody[k];
+      const int lam = md.parent[b];
+      const double ag[6] = {0, 0, 0, md.g[0], md.g[1], md.g[2]};
+      double Vl[6], ul[6];
+      for (int i = 0; i < 6; i++) {
+        Vl[i] = lam >= 0 ? s[L.V + 6 * lam + i] : 0.0;
+        ul[i] = (lam >= 0 ? s[L.A + 6 * lam + i] : 0.0) - ag[i];
+      }
+      // position generator Z (world twist of the subtree per unit q_k)
+      double Z[6];
+      const double* Sk = s + L.Sw + 6 * k;
+      if (md.jtype[b] == NIMBLE_JOINT_FREE) {
+        const int o = md.dof0[b];
+        const int c = k - o;
+        double xi[6] = {0, 0, 0, 0, 0, 0};
+        const double* th = s + L.q + o;
+        if (c < 3) {
+          rightJacobianCol(th, c, xi);
+        } else {
+          double R[9];
+          expMapRot(th, R);
+          for (int r = 0; r < 3; r++) xi[3 + r] = R[(c - 3) * 3 + r];  // R^T e_c
+        }
+        double TwC[12];
+        tmul(s + L.Tw + 12 * b, md.Tcj[b], TwC);
+        adT(TwC, xi, Z);
+      } else {
+        for (int i = 0; i < 6; i++) Z[i] = Sk[i];
+      }
+      double Psi[6], ZxVl[6];
+      crm(Vl, Z, Psi);
+      crm(Z, Vl, ZxVl);
+      double dFb[6], dFbv[6];
+      dForcePos(s, L, b, Z, Vl, ul, Psi, ZxVl, dFb);
+      dForceVel(s, L, b, Sk, Vl, s + L.V + 6 * b, dFbv);
+      double accQ = 0.0, accV = 0.0;
+      for (int c = 0; c < md.nb; c++) {
+        const int nd = md.ndof[c];
+        if (nd == 0) continue;
+        const bool inSub = (md.anc[c] >> b) & 1ull;
+        const bool isAnc = ((md.anc[b] >> c) & 1ull) && c != b;
+        if (!inSub && !isAnc) continue;
+        const int o = md.dof0[c];
+        if (inSub) {
+          double dF[6], dFv[6];
+          if (c == b) {
+            for (int i = 0; i < 6; i++) { dF[i] = dFb[i]; dFv[i] = dFbv[i]; }
+          } else {
+            dForcePos(s, L, c, Z, Vl, ul, Psi, ZxVl, dF);
+            dForceVel(s, L, c, Sk, Vl, s + L.V + 6 * b, dFv);
+          }
+          const double* Fc = s + L.F + 6 * c;
+          for (int j = 0; j < nd; j++) {
+            const double* Sj = s + L.Sw + 6 * (o + j);
+            double zs[6];
+            crm(Z, Sj, zs);
+            accQ += w[o + j] * (dot6(Sj, dF) + dot6(zs, Fc));
+            accV += w[o + j] * dot6(Sj, dFv);
+          }
+        } else {
+          for (int j = 0; j < nd; j++) {
+            const double* Sj = s + L.Sw + 6 * (o + j);
+            accQ += w[o + j] * dot6(Sj, dFb);
+            accV += w[o + j] * dot6(Sj, dFbv);
+          }
+        }
+      }
+      const double wk = w[k];
+      gq = -dt * accQ - dt * md.spring[k] * wk;
+      gvOut = s[L.gv + k] - dt * accV - dt * md.damping[k] * wk - dt * dt * md.spring[k] * wk;
+      gt = dt * wk;
+      // posPos^T gp and velPos^T gp for 1-dof joints: identity / dt * identity
+      if (md.ndof[b] == 1) {
+        gq += s[L.gp + k];
+        gvOut += dt * s[L.gp + k];
+      }
+    }
+    __syncthreads();
+    // FreeJoint posPos / velPos blocks: central differences exactly as
+    // FreeJoint::finiteDifferencePosPosJacobian / VelPosJacobian
+    // (FreeJoint.cpp:965, :987); 24 lanes, one perturbed integration each.
+    double* fd = s + L.scratch;
+    for (int f = 0; f < md.numFree; f++) {
+      const int b = md.freeBody[f], o = md.dof0[b];
+      if (lane < 24) {
+        const int which = lane / 12;      // 0: wrt pos, 1: wrt vel
+        const int i = (lane % 12) / 2;
+        const double sign = (lane % 2) ? -1.0 : 1.0;
+        const double eps = which == 0 ? 1e-6 : 1e-7;
+        double qq[6], vv[6], r[6];
+        for (int j = 0; j < 6; j++) { qq[j] = s[L.q + o + j]; vv[j] = s[L.v + o + j]; }
+        if (which == 0) qq[i] += sign * eps; else vv[i] += sign * eps;
+        freeIntegrate(qq, vv, dt, r);
+        for (int j = 0; j < 6; j++) fd[lane * 6 + j] = r[j];
+      }
+      __syncthreads();
+      if (k >= o && k < o + 6) {
+        const int i = k - o;
+        double pp = 0.0, vp = 0.0;
+        for (int r = 0; r < 6; r++) {
+          const double jp = (fd[(i * 2) * 6 + r] - fd[(i * 2 + 1) * 6 + r]) / (2 * 1e-6);
+          const double jv = (fd[(12 + i * 2) * 6 + r] - fd[(12 + i * 2 + 1) * 6 + r]) / (2 * 1e-7);
+          pp += jp * s[L.gp + o + r];
+          vp += jv * s[L.gp + o + r];
+        }
+        gq += pp;
+        gvOut += vp;
+      }
+      __syncthreads();
+    }
+    if (k < n) {
+      // clipLossGradientsToBounds (BackpropSnapshot.cpp:425)
+      const double qk = s[L.q + k], vk = s[L.v + k], tk = s[L.tau + k];
+      if (qk == md.posLo[k] && gq > 0) gq = 0;
+      if (qk == md.posHi[k] && gq < 0) gq = 0;
+      if (vk == md.velLo[k] && gvOut > 0) gvOut = 0;
+      if (vk == md.velHi[k] && gvOut < 0) gvOut = 0;
+      if (tk == md.forceLo[k] && gt > 0) gt = 0;
+      if (tk == md.forceHi[k] && gt < 0) gt = 0;
+      gradState[(size_t)env * 2 * n + k] = gq;
+      gradState[(size_t)env * 2 * n + n + k] = gvOut;
+      gradForces[(size_t)env * n + k] = gt;
+    }
+    __syncthreads();
+  }
+}

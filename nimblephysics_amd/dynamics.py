@@ -1,0 +1,403 @@
+"""Host-side model description mirroring the reference's dart.dynamics API.
+
+The reference builds skeletons through C++ classes bound with pybind11
+(dart/dynamics/Skeleton.hpp, BodyNode.hpp, RevoluteJoint.hpp, ...; Python
+bindings under python/_nimblephysics/dynamics/).  Only what the differentiable
+timestep reads is mirrored here: the kinematic tree, joint transforms and axes,
+inertia, joint damping/spring/limits, collision shapes and contact
+coefficients.  The numbers are flattened into a ``nimble_world_desc``
+(include/nimble_amd.h) by ``simulation.World``.
+
+Defaults follow the reference:
+  * Inertia: mass 1, COM 0, moment identity    (dart/dynamics/Inertia.hpp:68)
+  * friction 1.0, restitution 0.0              (detail/BodyNodeAspect.hpp:47)
+  * joint limits +-inf, damping/spring 0       (detail/GenericJointAspect.hpp)
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional
+
+import numpy as np
+
+INF = float("inf")
+
+JOINT_WELD = 0
+JOINT_REVOLUTE = 1
+JOINT_PRISMATIC = 2
+JOINT_FREE = 3
+
+SHAPE_BOX = 0
+SHAPE_SPHERE = 1
+
+
+def _iso(R=None, p=None) -> np.ndarray:
+    T = np.eye(4)
+    if R is not None:
+        T[:3, :3] = np.asarray(R, dtype=np.float64)
+    if p is not None:
+        T[:3, 3] = np.asarray(p, dtype=np.float64)
+    return T
+
+
+class Isometry3:
+    """Minimal stand-in for dart.math.Isometry3 (4x4 homogeneous transform)."""
+
+    def __init__(self, matrix: Optional[np.ndarray] = None):
+        self.m = np.eye(4) if matrix is None else np.array(matrix, dtype=np.float64)
+
+    def set_translation(self, p):
+        self.m[:3, 3] = np.asarray(p, dtype=np.float64)
+
+    def set_rotation(self, R):
+        self.m[:3, :3] = np.asarray(R, dtype=np.float64)
+
+    def translation(self):
+        return self.m[:3, 3].copy()
+
+    def rotation(self):
+        return self.m[:3, :3].copy()
+
+    def matrix(self):
+        return self.m.copy()
+
+
+def _as_matrix(T) -> np.ndarray:
+    if isinstance(T, Isometry3):
+        return T.m.copy()
+    return np.array(T, dtype=np.float64)
+
+
+class Shape:
+    def __init__(self, kind: int, size):
+        self.kind = kind
+        self.size = np.zeros(3)
+        s = np.atleast_1d(np.asarray(size, dtype=np.float64))
+        self.size[: len(s)] = s
+
+
+class BoxShape(Shape):
+    """dart/dynamics/BoxShape.hpp"""
+
+    def __init__(self, size):
+        super().__init__(SHAPE_BOX, size)
+
+    def getSize(self):
+        return self.size.copy()
+
+
+class SphereShape(Shape):
+    """dart/dynamics/SphereShape.hpp"""
+
+    def __init__(self, radius: float):
+        super().__init__(SHAPE_SPHERE, [radius, 0, 0])
+
+    def getRadius(self):
+        return float(self.size[0])
+
+
+class ShapeNode:
+    def __init__(self, body: "BodyNode", shape: Shape, collision: bool):
+        self.body = body
+        self.shape = shape
+        self.T = np.eye(4)
+        self.collision = collision
+        self.visual = True
+
+    def setRelativeTransform(self, T):
+        self.T = _as_matrix(T)
+
+    def getShape(self):
+        return self.shape
+
+    def createCollisionAspect(self):
+        self.collision = True
+
+    def createVisualAspect(self):
+        self.visual = True
+        return _VisualAspect()
+
+    def getVisualAspect(self):
+        return _VisualAspect()
+
+
+class _VisualAspect:
+    def setColor(self, *_):
+        pass
+
+    def setCastShadows(self, *_):
+        pass
+
+
+class Joint:
+    def __init__(self, skel: "Skeleton", kind: int, name: str):
+        self.skel = skel
+        self.kind = kind
+        self.name = name
+        self.T_parent = np.eye(4)
+        self.T_child = np.eye(4)
+        self.axis = np.array([1.0, 0.0, 0.0]) if kind == JOINT_REVOLUTE else np.array([1.0, 0.0, 0.0])
+        n = self.getNumDofs()
+        self.damping = np.zeros(n)
+        self.spring = np.zeros(n)
+        self.rest = np.zeros(n)
+        self.pos_lo = np.full(n, -INF)
+        self.pos_hi = np.full(n, INF)
+        self.vel_lo = np.full(n, -INF)
+        self.vel_hi = np.full(n, INF)
+        self.force_lo = np.full(n, -INF)
+        self.force_hi = np.full(n, INF)
+        self.initial_positions = np.zeros(n)
+        self.dof_offset = 0
+
+    def getNumDofs(self) -> int:
+        return {JOINT_WELD: 0, JOINT_REVOLUTE: 1, JOINT_PRISMATIC: 1, JOINT_FREE: 6}[self.kind]
+
+    def getName(self):
+        return self.name
+
+    def setName(self, name):
+        self.name = name
+
+    # RevoluteJoint::setAxis / PrismaticJoint::setAxis normalise the axis
+    def setAxis(self, axis):
+        a = np.asarray(axis, dtype=np.float64)
+        self.axis = a / np.linalg.norm(a)
+
+    def getAxis(self):
+        return self.axis.copy()
+
+    def setTransformFromParentBodyNode(self, T):
+        self.T_parent = _as_matrix(T)
+
+    def setTransformFromChildBodyNode(self, T):
+        self.T_child = _as_matrix(T)
+
+    def setDampingCoefficient(self, i, d):
+        self.damping[i] = d
+
+    def setSpringStiffness(self, i, k):
+        self.spring[i] = k
+
+    def setRestPosition(self, i, q0):
+        self.rest[i] = q0
+
+    def setPositionUpperLimit(self, i, v):
+        self.pos_hi[i] = v
+
+    def setPositionLowerLimit(self, i, v):
+        self.pos_lo[i] = v
+
+    def setVelocityUpperLimit(self, i, v):
+        self.vel_hi[i] = v
+
+    def setVelocityLowerLimit(self, i, v):
+        self.vel_lo[i] = v
+
+    def setControlForceUpperLimit(self, i, v):
+        self.force_hi[i] = v
+
+    def setControlForceLowerLimit(self, i, v):
+        self.force_lo[i] = v
+
+
+class BodyNode:
+    def __init__(self, skel: "Skeleton", name: str, parent: Optional["BodyNode"], joint: Joint):
+        self.skel = skel
+        self.name = name
+        self.parent = parent
+        self.joint = joint
+        self.mass = 1.0
+        self.com = np.zeros(3)
+        self.moment = np.array([1.0, 1.0, 1.0, 0.0, 0.0, 0.0])  # Ixx Iyy Izz Ixy Ixz Iyz
+        self.friction = 1.0
+        self.restitution = 0.0
+        self.shape_nodes: List[ShapeNode] = []
+        self.index = 0
+
+    def getName(self):
+        return self.name
+
+    def getParentJoint(self):
+        return self.joint
+
+    def getParentBodyNode(self):
+        return self.parent
+
+    def setMass(self, m):
+        self.mass = float(m)
+
+    def getMass(self):
+        return self.mass
+
+    def setLocalCOM(self, c):
+        self.com = np.asarray(c, dtype=np.float64).copy()
+
+    def setMomentOfInertia(self, Ixx, Iyy, Izz, Ixy=0.0, Ixz=0.0, Iyz=0.0):
+        self.moment = np.array([Ixx, Iyy, Izz, Ixy, Ixz, Iyz], dtype=np.float64)
+
+    def setFrictionCoeff(self, f):
+        self.friction = float(f)
+
+    def setRestitutionCoeff(self, r):
+        self.restitution = float(r)
+
+    def createShapeNode(self, shape: Shape, collision: bool = False):
+        node = ShapeNode(self, shape, collision)
+        self.shape_nodes.append(node)
+        return node
+
+    def getShapeNode(self, i):
+        return self.shape_nodes[i]
+
+    def getNumShapeNodes(self):
+        return len(self.shape_nodes)
+
+
+class Skeleton:
+    """Subset of dart/dynamics/Skeleton.hpp used by the timestep."""
+
+    def __init__(self, name: str = "skeleton"):
+        self.name = name
+        self.bodies: List[BodyNode] = []
+        self.mobile = True
+        self.world = None
+        self._q = np.zeros(0)
+        self._v = np.zeros(0)
+
+    # --- construction -------------------------------------------------------
+    def _create(self, kind, parent, joint_name=None, body_name=None):
+        j = Joint(self, kind, joint_name or f"joint_{len(self.bodies)}")
+        b = BodyNode(self, body_name or f"body_{len(self.bodies)}", parent, j)
+        b.index = len(self.bodies)
+        self.bodies.append(b)
+        self._reindex()
+        return j, b
+
+    def createRevoluteJointAndBodyNodePair(self, parent=None, joint_name=None, body_name=None):
+        return self._create(JOINT_REVOLUTE, parent, joint_name, body_name)
+
+    def createPrismaticJointAndBodyNodePair(self, parent=None, joint_name=None, body_name=None):
+        return self._create(JOINT_PRISMATIC, parent, joint_name, body_name)
+
+    def createFreeJointAndBodyNodePair(self, parent=None, joint_name=None, body_name=None):
+        return self._create(JOINT_FREE, parent, joint_name, body_name)
+
+    def createWeldJointAndBodyNodePair(self, parent=None, joint_name=None, body_name=None):
+        return self._create(JOINT_WELD, parent, joint_name, body_name)
+
+    def _reindex(self):
+        off = 0
+        for b in self.bodies:
+            b.joint.dof_offset = off
+            off += b.joint.getNumDofs()
+        n = off
+        q = np.zeros(n)
+        v = np.zeros(n)
+        m = min(n, len(self._q))
+        q[:m] = self._q[:m]
+        v[:m] = self._v[:m]
+        # new dofs start at the joint's initial position
+        for b in self.bodies:
+            j = b.joint
+            for k in range(j.getNumDofs()):
+                if j.dof_offset + k >= m:
+                    q[j.dof_offset + k] = j.initial_positions[k]
+        self._q, self._v = q, v
+
+    # --- queries --------------------------------------------------------------
+    def getName(self):
+        return self.name
+
+    def getNumDofs(self) -> int:
+        return sum(b.joint.getNumDofs() for b in self.bodies)
+
+    def getNumBodyNodes(self):
+        return len(self.bodies)
+
+    def getBodyNode(self, key):
+        if isinstance(key, int):
+            return self.bodies[key]
+        for b in self.bodies:
+            if b.name == key:
+                return b
+        raise KeyError(key)
+
+    def getJoint(self, key):
+        if isinstance(key, int):
+            return self.bodies[key].joint
+        for b in self.bodies:
+            if b.joint.name == key:
+                return b.joint
+        raise KeyError(key)
+
+    def getRootBodyNode(self):
+        return self.bodies[0]
+
+    def setMobile(self, mobile: bool):
+        self.mobile = bool(mobile)
+
+    def isMobile(self):
+        return self.mobile
+
+    # --- state ------------------------------------------------------------------
+    def getPositions(self):
+        return self._q.copy()
+
+    def setPositions(self, q):
+        self._q = np.asarray(q, dtype=np.float64).copy()
+
+    def getVelocities(self):
+        return self._v.copy()
+
+    def setVelocities(self, v):
+        self._v = np.asarray(v, dtype=np.float64).copy()
+
+    def setPosition(self, i, x):
+        self._q[i] = x
+
+    def getPosition(self, i):
+        return float(self._q[i])
+
+    def setVelocity(self, i, x):
+        self._v[i] = x
+
+    def _per_dof(self, attr):
+        out = []
+        for b in self.bodies:
+            out.extend(list(getattr(b.joint, attr)))
+        return np.array(out, dtype=np.float64)
+
+    def getPositionLowerLimits(self):
+        return self._per_dof("pos_lo")
+
+    def getPositionUpperLimits(self):
+        return self._per_dof("pos_hi")
+
+    def setControlForceUpperLimits(self, lim):
+        lim = np.asarray(lim, dtype=np.float64)
+        for b in self.bodies:
+            j = b.joint
+            j.force_hi[:] = lim[j.dof_offset:j.dof_offset + j.getNumDofs()]
+
+    def setControlForceLowerLimits(self, lim):
+        lim = np.asarray(lim, dtype=np.float64)
+        for b in self.bodies:
+            j = b.joint
+            j.force_lo[:] = lim[j.dof_offset:j.dof_offset + j.getNumDofs()]
+
+    def getControlForceUpperLimits(self):
+        return self._per_dof("force_hi")
+
+    def getControlForceLowerLimits(self):
+        return self._per_dof("force_lo")
+
+
+def rpy_to_matrix(rpy) -> np.ndarray:
+    """URDF fixed-axis roll/pitch/yaw -> rotation (Rz(yaw) Ry(pitch) Rx(roll))."""
+    r, p, y = [float(x) for x in rpy]
+    cr, sr, cp, sp, cy, sy = math.cos(r), math.sin(r), math.cos(p), math.sin(p), math.cos(y), math.sin(y)
+    Rx = np.array([[1, 0, 0], [0, cr, -sr], [0, sr, cr]])
+    Ry = np.array([[cp, 0, sp], [0, 1, 0], [-sp, 0, cp]])
+    Rz = np.array([[cy, -sy, 0], [sy, cy, 0], [0, 0, 1]])
+    return Rz @ Ry @ Rx

@@ -1,0 +1,266 @@
+"""World: the reference's dart.simulation.World surface for the timestep.
+
+Mirrors dart/simulation/World.hpp/.cpp: construction defaults (World.cpp:70:
+gravity (0,0,-9.81), dt 0.001, parallel pos/vel updates on, fallback CFM 1e-4,
+contact clipping depth 0.03, penetration correction off), skeleton loading,
+state/action accessors (World.cpp:2024-2130).  A World describes ONE model;
+its state vectors are the single-world state.  The batched device path
+(``timestep`` with a 2-D state) advances many independent copies of the same
+model at once; the per-copy LCP warm-start caches live in ``BatchState``.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from . import dynamics as dyn
+from . import urdf as _urdf
+from ._desc import NIMBLE_MAX_BODIES, NIMBLE_MAX_DOFS, NIMBLE_MAX_SHAPES, build_desc
+
+
+class World:
+    def __init__(self, name: str = "world"):
+        self.name = name
+        self.skeletons: List[dyn.Skeleton] = []
+        self.gravity = np.array([0.0, 0.0, -9.81])
+        self.dt = 0.001
+        self.penetration_correction = False
+        self.parallel_pos_vel = True
+        self.fallback_cfm = 1e-4
+        self.clipping_depth = 0.03
+        self.action_space: Optional[List[int]] = None
+        self._forces: Optional[np.ndarray] = None
+        self._version = 0
+        self._native = None  # (version, handle)
+
+    # --- model ------------------------------------------------------------------
+    def addSkeleton(self, skel: dyn.Skeleton):
+        skel.world = self
+        self.skeletons.append(skel)
+        self._touch()
+        return skel
+
+    def loadSkeleton(self, path: str, ignore_mesh_collisions: bool = False):
+        skel = _urdf.load_urdf(path, ignore_mesh_collisions=ignore_mesh_collisions)
+        return self.addSkeleton(skel)
+
+    def getSkeleton(self, key):
+        if isinstance(key, int):
+            return self.skeletons[key]
+        for s in self.skeletons:
+            if s.name == key:
+                return s
+        raise KeyError(key)
+
+    def getNumSkeletons(self):
+        return len(self.skeletons)
+
+    def getNumDofs(self) -> int:
+        return sum(s.getNumDofs() for s in self.skeletons)
+
+    def _touch(self):
+        self._version += 1
+        n = self.getNumDofs()
+        if self._forces is None or len(self._forces) != n:
+            self._forces = np.zeros(n)
+        if self.action_space is not None and any(a >= n for a in self.action_space):
+            self.action_space = None
+
+    # --- parameters -----------------------------------------------------------------
+    def setGravity(self, g):
+        self.gravity = np.asarray(g, dtype=np.float64).copy()
+        self._version += 1
+
+    def getGravity(self):
+        return self.gravity.copy()
+
+    def setTimeStep(self, dt):
+        self.dt = float(dt)
+        self._version += 1
+
+    def getTimeStep(self):
+        return self.dt
+
+    def setPenetrationCorrectionEnabled(self, enable: bool):
+        self.penetration_correction = bool(enable)
+        self._version += 1
+
+    def getPenetrationCorrectionEnabled(self):
+        return self.penetration_correction
+
+    def setParallelVelocityAndPositionUpdates(self, enable: bool):
+        self.parallel_pos_vel = bool(enable)
+        self._version += 1
+
+    def setFallbackConstraintForceMixingConstant(self, c):
+        self.fallback_cfm = float(c)
+        self._version += 1
+
+    def setContactClippingDepth(self, d):
+        self.clipping_depth = float(d)
+        self._version += 1
+
+    # --- state (World.cpp:2024 setState / :2040 getState) --------------------------
+    def getPositions(self):
+        return np.concatenate([s.getPositions() for s in self.skeletons]) if self.skeletons else np.zeros(0)
+
+    def getVelocities(self):
+        return np.concatenate([s.getVelocities() for s in self.skeletons]) if self.skeletons else np.zeros(0)
+
+    def setPositions(self, q):
+        q = np.asarray(q, dtype=np.float64)
+        c = 0
+        for s in self.skeletons:
+            n = s.getNumDofs()
+            s.setPositions(q[c:c + n])
+            c += n
+
+    def setVelocities(self, v):
+        v = np.asarray(v, dtype=np.float64)
+        c = 0
+        for s in self.skeletons:
+            n = s.getNumDofs()
+            s.setVelocities(v[c:c + n])
+            c += n
+
+    def getState(self):
+        return np.concatenate([self.getPositions(), self.getVelocities()])
+
+    def setState(self, state):
+        n = self.getNumDofs()
+        state = np.asarray(state, dtype=np.float64)
+        if state.size != 2 * n:
+            raise ValueError(f"World::setState() expects {2 * n} values, got {state.size}")
+        self.setPositions(state[:n])
+        self.setVelocities(state[n:])
+
+    def getStateSize(self):
+        return 2 * self.getNumDofs()
+
+    def setControlForces(self, f):
+        self._forces = np.asarray(f, dtype=np.float64).copy()
+
+    def getControlForces(self):
+        return self._forces.copy()
+
+    # --- action space (World.cpp:2061-2130) ------------------------------------------
+    def getActionSpace(self) -> List[int]:
+        if self.action_space is None:
+            return list(range(self.getNumDofs()))
+        return list(self.action_space)
+
+    def setActionSpace(self, mapping):
+        n = self.getNumDofs()
+        mapping = [int(m) for m in mapping]
+        for m in mapping:
+            if m < 0 or m >= n:
+                raise ValueError(f"action mapping index {m} out of bounds [0,{n})")
+        self.action_space = mapping
+
+    def removeDofFromActionSpace(self, dof: int):
+        self.setActionSpace([a for a in self.getActionSpace() if a != dof])
+
+    def getActionSize(self):
+        return len(self.getActionSpace())
+
+    def setAction(self, action):
+        action = np.asarray(action, dtype=np.float64)
+        f = np.zeros(self.getNumDofs())
+        for i, m in enumerate(self.getActionSpace()):
+            f[m] = action[i]
+        self.setControlForces(f)
+
+    def getAction(self):
+        f = self.getControlForces()
+        return np.array([f[m] for m in self.getActionSpace()])
+
+    # --- flattening -----------------------------------------------------------------------
+    def desc_arrays(self) -> Dict[str, np.ndarray]:
+        bodies = []
+        for si, s in enumerate(self.skeletons):
+            for b in s.bodies:
+                bodies.append((si, s, b))
+        nb = len(bodies)
+        n = self.getNumDofs()
+        if nb > NIMBLE_MAX_BODIES or n > NIMBLE_MAX_DOFS:
+            raise ValueError(f"model too large: {nb} bodies / {n} dofs (max {NIMBLE_MAX_BODIES}/{NIMBLE_MAX_DOFS})")
+        index = {}
+        for k, (si, s, b) in enumerate(bodies):
+            index[id(b)] = k
+        dof_base = {}
+        c = 0
+        for s in self.skeletons:
+            dof_base[id(s)] = c
+            c += s.getNumDofs()
+
+        def t12(T):
+            return np.asarray(T, dtype=np.float64)[:3, :4].reshape(12)
+
+        A: Dict[str, list] = {k: [] for k in (
+            "parent", "skeleton", "joint_type", "dof_offset", "skeleton_mobile", "T_parent_joint",
+            "T_child_joint", "axis", "mass", "com", "moment", "friction", "restitution")}
+        for si, s, b in bodies:
+            j = b.joint
+            A["parent"].append(index[id(b.parent)] if b.parent is not None else -1)
+            A["skeleton"].append(si)
+            A["joint_type"].append(j.kind)
+            A["dof_offset"].append(dof_base[id(s)] + j.dof_offset)
+            A["skeleton_mobile"].append(1 if s.mobile else 0)
+            A["T_parent_joint"].append(t12(j.T_parent))
+            A["T_child_joint"].append(t12(j.T_child))
+            A["axis"].append(j.axis)
+            A["mass"].append(b.mass)
+            A["com"].append(b.com)
+            A["moment"].append(b.moment)
+            A["friction"].append(b.friction)
+            A["restitution"].append(b.restitution)
+        per_dof = {k: [] for k in ("damping", "spring", "rest_position", "pos_lower", "pos_upper", "vel_lower",
+                                    "vel_upper", "force_lower", "force_upper")}
+        attr = {"damping": "damping", "spring": "spring", "rest_position": "rest", "pos_lower": "pos_lo",
+                "pos_upper": "pos_hi", "vel_lower": "vel_lo", "vel_upper": "vel_hi", "force_lower": "force_lo",
+                "force_upper": "force_hi"}
+        for s in self.skeletons:
+            for b in s.bodies:
+                for k, a in attr.items():
+                    per_dof[k].extend(list(getattr(b.joint, a)))
+        shapes = []
+        for si, s, b in bodies:
+            for node in b.shape_nodes:
+                if node.collision:
+                    shapes.append((index[id(b)], node))
+        if len(shapes) > NIMBLE_MAX_SHAPES:
+            raise ValueError("too many collision shapes")
+        out = {
+            "num_bodies": nb, "num_dofs": n, "num_shapes": len(shapes), "dt": self.dt,
+            "gravity": self.gravity, "contact_clipping_depth": self.clipping_depth,
+            "fallback_cfm": self.fallback_cfm, "penetration_correction": int(self.penetration_correction),
+            "parallel_pos_vel": int(self.parallel_pos_vel),
+            "parent": np.array(A["parent"], np.int32), "skeleton": np.array(A["skeleton"], np.int32),
+            "joint_type": np.array(A["joint_type"], np.int32), "dof_offset": np.array(A["dof_offset"], np.int32),
+            "skeleton_mobile": np.array(A["skeleton_mobile"], np.int32),
+            "T_parent_joint": np.array(A["T_parent_joint"]).reshape(-1),
+            "T_child_joint": np.array(A["T_child_joint"]).reshape(-1),
+            "axis": np.array(A["axis"]).reshape(-1), "mass": np.array(A["mass"]),
+            "com": np.array(A["com"]).reshape(-1), "moment": np.array(A["moment"]).reshape(-1),
+            "friction": np.array(A["friction"]), "restitution": np.array(A["restitution"]),
+            "shape_body": np.array([s[0] for s in shapes], np.int32),
+            "shape_type": np.array([s[1].shape.kind for s in shapes], np.int32),
+            "shape_size": np.array([s[1].shape.size for s in shapes]).reshape(-1),
+            "shape_T": np.array([t12(s[1].T) for s in shapes]).reshape(-1),
+        }
+        for k, v in per_dof.items():
+            out[k] = np.array(v, dtype=np.float64)
+        return out
+
+    def desc(self):
+        return build_desc(self.desc_arrays())
+
+    def native(self):
+        """Device-side world handle (created lazily, rebuilt when the model changes)."""
+        from . import _native
+        if self._native is None or self._native[0] != self._version:
+            if self._native is not None:
+                self._native[1].close()
+            self._native = (self._version, _native.DeviceWorld(self))
+        return self._native[1]

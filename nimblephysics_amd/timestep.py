@@ -1,0 +1,95 @@
+"""nimble.timestep(world, state, action) as a torch.autograd.Function.
+
+Mirrors python/nimblephysics/timestep.py:13 (TimestepLayer) and :59
+(timestep): forward = neural::forwardPass(world) (World::step), backward =
+BackpropSnapshot::backpropState.  The reference takes a 1-D state and round
+trips through numpy on the CPU; here state/action are float64 device tensors,
+either 1-D (one world) or 2-D [batch, ...] (independent worlds sharing the
+model), and the whole batch is one kernel launch each way.
+
+World-side effects match the reference for the 1-D case: the world's
+positions/velocities are set to the returned state and the control forces are
+cleared (World::step(resetCommand=true) via forwardPass(world)).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from .simulation import World
+
+
+class BatchState:
+    """Per-world LCP warm-start caches (BoxedLcpConstraintSolver::mX) for a batch."""
+
+    def __init__(self, batch: int, cache_doubles: int, device):
+        self.batch = batch
+        self.cache = torch.zeros((batch, cache_doubles), dtype=torch.float64, device=device)
+        self.cache[:, 0] = -1.0  # empty cache
+
+
+def _batch_state(world: World, batch: int, dev, device) -> BatchState:
+    bs = getattr(world, "_batch_state", None)
+    if bs is None or bs.batch != batch or bs.cache.device != device or bs.cache.shape[1] != dev.cache_doubles:
+        bs = BatchState(batch, dev.cache_doubles, device)
+        world._batch_state = bs
+    return bs
+
+
+class TimestepLayer(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, world: World, state: torch.Tensor, action: torch.Tensor, mass: Optional[torch.Tensor]):
+        if mass is not None:
+            raise NotImplementedError("mass gradients (WithRespectToMass) are not on the batched hot path yet")
+        squeeze = state.dim() == 1
+        st = state.detach().reshape(1, -1) if squeeze else state.detach()
+        act = action.detach().reshape(1, -1) if squeeze else action.detach()
+        st = st.contiguous()
+        B = st.shape[0]
+        n = world.getNumDofs()
+        if st.shape[1] != 2 * n:
+            raise ValueError(f"state has {st.shape[1]} columns, world expects {2 * n}")
+        space = world.getActionSpace()
+        if act.shape[1] != len(space):
+            raise ValueError(f"action has {act.shape[1]} columns, action space has {len(space)}")
+        dev = world.native()
+        idx = torch.tensor(space, dtype=torch.long, device=st.device)
+        forces = torch.zeros((B, n), dtype=torch.float64, device=st.device)
+        forces.index_copy_(1, idx, act.contiguous())
+        bs = _batch_state(world, B, dev, st.device)
+        nxt = torch.empty_like(st)
+        snap = torch.empty((B, dev.snapshot_doubles), dtype=torch.float64, device=st.device)
+        stream = torch.cuda.current_stream(st.device).cuda_stream
+        dev.forward(st, forces, bs.cache, nxt, snap, stream)
+        ctx.world = world
+        ctx.squeeze = squeeze
+        ctx.save_for_backward(st, forces, snap, idx)
+        if squeeze:
+            # World::step side effects on the single world
+            out_cpu = nxt[0].cpu().numpy()
+            world.setState(out_cpu)
+            world.setControlForces(out_cpu[:n] * 0.0)
+            return nxt[0]
+        return nxt
+
+    @staticmethod
+    def backward(ctx, grad_next):
+        st, forces, snap, idx = ctx.saved_tensors
+        world = ctx.world
+        g = grad_next.detach().reshape(st.shape).contiguous().to(torch.float64)
+        dev = world.native()
+        gs = torch.empty_like(st)
+        gf = torch.empty_like(forces)
+        stream = torch.cuda.current_stream(st.device).cuda_stream
+        dev.backward(st, forces, snap, g, gs, gf, stream)
+        ga = gf.index_select(1, idx)
+        if ctx.squeeze:
+            return None, gs[0], ga[0], None
+        return None, gs, ga, None
+
+
+def timestep(world: World, state: torch.Tensor, action: torch.Tensor,
+             mass: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Differentiable step; see module docstring."""
+    return TimestepLayer.apply(world, state, action, mass)

@@ -1,0 +1,446 @@
+// ORACLE / TEST INFRASTRUCTURE ONLY.
+//
+// CPU restatement of the reference's differentiable timestep, used by tests/,
+// __graft_entry__.smoke() and bench.py's cpu_baseline leg as the checker.  It
+// is never linked into, called by, or shipped with the product path
+// (nimblephysics_amd/csrc), which must fail loudly without its HIP library.
+//
+// Structure follows the reference call graph:
+//   World::step                         dart/simulation/World.cpp:221
+//     Skeleton::computeForwardDynamics  dart/dynamics/Skeleton.cpp:13034 (ABA,
+//        BodyNode::updateBiasForce BodyNode.cpp:2067, updateAccelerationFD :2149,
+//        GenericJoint::updateTotalForceDynamic detail/GenericJoint.hpp:2554,
+//        updateAccelerationDynamic :2656, addChildArtInertiaToDynamic :2168,
+//        addChildBiasForceToDynamic :2395)
+//     Skeleton::integrateVelocities     Skeleton.cpp:9329
+//     ConstraintSolver::solve (contacts) -- oracle_contact.cpp
+//     World::integratePositions         World.cpp:300 (parallel pos/vel update)
+//   BackpropSnapshot::backprop          dart/neural/BackpropSnapshot.cpp:121
+//
+// Analytic derivatives that the reference computes in closed form
+// (Skeleton::getJacobianOfC Skeleton.cpp:1779, getJacobianOfMinv :2024) are
+// obtained here by forward-mode dual numbers through the same body-frame
+// recursions: exact to rounding, and independent of the product's
+// world-frame closed-form derivative kernels.
+#include "oracle.hpp"
+
+#include <cstring>
+#include <cstdio>
+#include <vector>
+
+namespace oracle {
+
+//------------------------------------------------------------------------------
+World::World(const nimble_world_desc* d) {
+  nb = d->num_bodies;
+  n = d->num_dofs;
+  dt = d->dt;
+  for (int i = 0; i < 3; i++) g[i] = d->gravity[i];
+  clipDepth = d->contact_clipping_depth;
+  fallbackCfm = d->fallback_cfm;
+  penetrationCorrection = d->penetration_correction != 0;
+  parallelPosVel = d->parallel_pos_vel != 0;
+  bodies.resize(nb);
+  for (int b = 0; b < nb; b++) {
+    Body& B = bodies[b];
+    B.parent = d->parent[b];
+    B.skel = d->skeleton[b];
+    B.jtype = d->joint_type[b];
+    B.dof0 = d->dof_offset[b];
+    B.mobile = d->skeleton_mobile[b] != 0;
+    B.ndof = B.jtype == NIMBLE_JOINT_WELD ? 0 : (B.jtype == NIMBLE_JOINT_FREE ? 6 : 1);
+    auto loadIso = [](const double* t, Iso<double>& T) {
+      for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) T.R(r, c) = t[r * 4 + c];
+        T.p[r] = t[r * 4 + 3];
+      }
+    };
+    loadIso(d->T_parent_joint + 12 * b, B.Tpj);
+    loadIso(d->T_child_joint + 12 * b, B.Tcj);
+    for (int i = 0; i < 3; i++) B.axis[i] = d->axis[3 * b + i];
+    // dart/dynamics/Inertia.cpp:1368 computeSpatialTensor
+    double m = d->mass[b];
+    V3<double> c{{d->com[3 * b], d->com[3 * b + 1], d->com[3 * b + 2]}};
+    const double* mo = d->moment + 6 * b;
+    M3<double> I;
+    I(0, 0) = mo[0]; I(1, 1) = mo[1]; I(2, 2) = mo[2];
+    I(0, 1) = I(1, 0) = mo[3]; I(0, 2) = I(2, 0) = mo[4]; I(1, 2) = I(2, 1) = mo[5];
+    M3<double> C = skew(c);
+    M3<double> CCt = mul(C, transpose(C));
+    B.G = zero66<double>();
+    for (int r = 0; r < 3; r++)
+      for (int cc = 0; cc < 3; cc++) {
+        B.G(r, cc) = I(r, cc) + m * CCt(r, cc);
+        B.G(r, cc + 3) = m * C(r, cc);
+        B.G(r + 3, cc) = m * C(cc, r);
+        B.G(r + 3, cc + 3) = (r == cc) ? m : 0.0;
+      }
+    B.friction = d->friction[b];
+    B.restitution = d->restitution[b];
+  }
+  damping.assign(d->damping, d->damping + n);
+  spring.assign(d->spring, d->spring + n);
+  restPos.assign(d->rest_position, d->rest_position + n);
+  posLo.assign(d->pos_lower, d->pos_lower + n);
+  posHi.assign(d->pos_upper, d->pos_upper + n);
+  velLo.assign(d->vel_lower, d->vel_lower + n);
+  velHi.assign(d->vel_upper, d->vel_upper + n);
+  forceLo.assign(d->force_lower, d->force_lower + n);
+  forceHi.assign(d->force_upper, d->force_upper + n);
+  shapes.resize(d->num_shapes);
+  for (int s = 0; s < d->num_shapes; s++) {
+    Shape& S = shapes[s];
+    S.body = d->shape_body[s];
+    S.type = d->shape_type[s];
+    for (int i = 0; i < 3; i++) S.size[i] = d->shape_size[3 * s + i];
+    for (int r = 0; r < 3; r++) {
+      for (int c = 0; c < 3; c++) S.T.R(r, c) = d->shape_T[12 * s + r * 4 + c];
+      S.T.p[r] = d->shape_T[12 * s + r * 4 + 3];
+    }
+  }
+  // dof -> body map
+  dofBody.assign(n, -1);
+  for (int b = 0; b < nb; b++)
+    for (int k = 0; k < bodies[b].ndof; k++) dofBody[bodies[b].dof0 + k] = b;
+}
+
+//------------------------------------------------------------------------------
+// Joint relative transform and Jacobian (RevoluteJoint.cpp:203, :141;
+// PrismaticJoint.cpp:188, :140; FreeJoint.cpp:1027, :1049 identity-Jacobian).
+template <class S>
+void jointTransform(const Body& B, const S* q, Iso<S>& T, M6<S>& Sj /* 6 x ndof, col-major in first ndof cols */) {
+  Iso<S> Tpj, Tcj;
+  for (int i = 0; i < 9; i++) { Tpj.R.m[i] = S(B.Tpj.R.m[i]); Tcj.R.m[i] = S(B.Tcj.R.m[i]); }
+  for (int i = 0; i < 3; i++) { Tpj.p[i] = S(B.Tpj.p[i]); Tcj.p[i] = S(B.Tcj.p[i]); }
+  Iso<S> Q = identityIso<S>();
+  M6<S> local = zero66<S>();
+  if (B.jtype == NIMBLE_JOINT_REVOLUTE) {
+    // math::expAngular(axis * q): Rodrigues
+    S c = cos(q[0]), s = sin(q[0]);
+    S a[3] = {S(B.axis[0]), S(B.axis[1]), S(B.axis[2])};
+    for (int r = 0; r < 3; r++)
+      for (int cc = 0; cc < 3; cc++) Q.R(r, cc) = (S(1.0) - c) * a[r] * a[cc] + ((r == cc) ? c : S(0.0));
+    Q.R(0, 1) = Q.R(0, 1) - s * a[2]; Q.R(0, 2) = Q.R(0, 2) + s * a[1];
+    Q.R(1, 0) = Q.R(1, 0) + s * a[2]; Q.R(1, 2) = Q.R(1, 2) - s * a[0];
+    Q.R(2, 0) = Q.R(2, 0) - s * a[1]; Q.R(2, 1) = Q.R(2, 1) + s * a[0];
+    for (int i = 0; i < 3; i++) local(i, 0) = a[i];
+  } else if (B.jtype == NIMBLE_JOINT_PRISMATIC) {
+    for (int i = 0; i < 3; i++) { Q.p[i] = S(B.axis[i]) * q[0]; local(i + 3, 0) = S(B.axis[i]); }
+  } else if (B.jtype == NIMBLE_JOINT_FREE) {
+    V3<S> w{{q[0], q[1], q[2]}};
+    Q.R = expMapRot(w);
+    for (int i = 0; i < 3; i++) Q.p[i] = q[3 + i];
+    for (int i = 0; i < 6; i++) local(i, i) = S(1.0);
+  }
+  T = compose(compose(Tpj, Q), inverse(Tcj));
+  // S = Ad(T_cj) * local  (AdTAngular / AdTLinear / getAdTMatrix)
+  Sj = zero66<S>();
+  for (int k = 0; k < B.ndof; k++) {
+    V6<S> col; for (int i = 0; i < 6; i++) col[i] = local(i, k);
+    V6<S> r = AdT(Tcj, col);
+    for (int i = 0; i < 6; i++) Sj(i, k) = r[i];
+  }
+}
+
+//------------------------------------------------------------------------------
+template <class S>
+void Kin<S>::compute(const World& w, const S* q, const S* dq) {
+  int nb = w.nb;
+  T.resize(nb); Tw.resize(nb); Sj.resize(nb); V.resize(nb); eta.resize(nb);
+  for (int b = 0; b < nb; b++) {
+    const Body& B = w.bodies[b];
+    jointTransform<S>(B, q + B.dof0, T[b], Sj[b]);
+    Tw[b] = B.parent >= 0 ? compose(Tw[B.parent], T[b]) : T[b];
+    V6<S> Sdq = zero6<S>();
+    for (int k = 0; k < B.ndof; k++)
+      for (int i = 0; i < 6; i++) Sdq[i] = Sdq[i] + Sj[b](i, k) * dq[B.dof0 + k];
+    V[b] = B.parent >= 0 ? add(AdInvT(T[b], V[B.parent]), Sdq) : Sdq;
+    // GenericJoint::setPartialAccelerationTo (detail/GenericJoint.hpp:1814), dS = 0
+    eta[b] = ad(V[b], Sdq);
+  }
+}
+template struct Kin<double>;
+template struct Kin<Dual>;
+
+//------------------------------------------------------------------------------
+// Inverse dynamics (BodyNode::updateTransmittedForceID BodyNode.cpp:1994 +
+// GenericJoint::updateForceID): tau = S^T F with
+//   F_i = G A_i - Fgrav_i - dad(V_i, G V_i) + sum_c dAdInvT(T_c, F_c).
+// Used for C(q,v)+g (Skeleton::updateCoriolisAndGravityForces :12652, i.e.
+// ddq = 0) and for mass-matrix products (gravity off, v = 0).
+template <class S>
+void inverseDynamics(const World& w, const Kin<S>& k, const S* ddq, bool withGravity, bool withVel, S* tau) {
+  int nb = w.nb;
+  std::vector<V6<S>> A(nb), F(nb);
+  for (int b = 0; b < nb; b++) {
+    const Body& B = w.bodies[b];
+    V6<S> Sddq = zero6<S>();
+    for (int kk = 0; kk < B.ndof; kk++)
+      for (int i = 0; i < 6; i++) Sddq[i] = Sddq[i] + k.Sj[b](i, kk) * ddq[B.dof0 + kk];
+    V6<S> base = B.parent >= 0 ? AdInvT(k.T[b], A[B.parent]) : zero6<S>();
+    A[b] = add(base, Sddq);
+    if (withVel) A[b] = add(A[b], k.eta[b]);
+  }
+  for (int b = nb - 1; b >= 0; b--) {
+    const Body& B = w.bodies[b];
+    M6<S> G; for (int i = 0; i < 36; i++) G.m[i] = S(B.G.m[i]);
+    V6<S> f = mul(G, A[b]);
+    if (withGravity) {
+      // AdInvRLinear(T_world, g)
+      V3<S> gg{{S(w.g[0]), S(w.g[1]), S(w.g[2])}};
+      V3<S> gl = mulT(k.Tw[b].R, gg);
+      V6<S> ag = zero6<S>(); for (int i = 0; i < 3; i++) ag[3 + i] = gl[i];
+      f = sub(f, mul(G, ag));
+    }
+    if (withVel) f = sub(f, dad(k.V[b], mul(G, k.V[b])));
+    F[b] = add(F[b], f);
+    if (B.parent >= 0) F[B.parent] = add(F[B.parent], dAdInvT(k.T[b], F[b]));
+    for (int kk = 0; kk < B.ndof; kk++) {
+      S s(0.0);
+      for (int i = 0; i < 6; i++) s += k.Sj[b](i, kk) * F[b][i];
+      tau[B.dof0 + kk] = s;
+    }
+  }
+}
+//------------------------------------------------------------------------------
+// Articulated-body forward dynamics exactly as Skeleton::computeForwardDynamics
+// (Skeleton.cpp:13034): backward pass updateArtInertia + updateBiasForce,
+// forward pass updateAccelerationFD.  Returns ddq.
+void forwardDynamicsABA(const World& w, const Kin<double>& k, const double* q, const double* dq,
+                        const double* tauCtrl, double* ddq) {
+  int nb = w.nb;
+  std::vector<M6<double>> AI(nb);
+  std::vector<V6<double>> Bias(nb), Acc(nb);
+  std::vector<std::vector<double>> Psi(nb), totalForce(nb);
+  for (int b = nb - 1; b >= 0; b--) {
+    const Body& B = w.bodies[b];
+    // updateArtInertia (BodyNode.cpp:2037)
+    AI[b] = B.G;
+    // updateBiasForce (BodyNode.cpp:2067)
+    V3<double> gl = mulT(k.Tw[b].R, V3<double>{{w.g[0], w.g[1], w.g[2]}});
+    V6<double> ag = zero6<double>(); for (int i = 0; i < 3; i++) ag[3 + i] = gl[i];
+    V6<double> Fg = mul(B.G, ag);
+    Bias[b] = sub(scale(dad(k.V[b], mul(B.G, k.V[b])), -1.0), Fg);
+    // children were processed already (reverse order): they added themselves.
+    (void)q;
+  }
+  // The reverse loop above initialised AI/Bias with the body's own terms;
+  // now accumulate children contributions in a second reverse sweep so that a
+  // child is complete before it is added to its parent.
+  for (int b = nb - 1; b >= 0; b--) {
+    const Body& B = w.bodies[b];
+    int nd = B.ndof;
+    // parent joint: updateInvProjArtInertia (detail/GenericJoint.hpp:2276)
+    Psi[b].assign(nd * nd, 0.0);
+    totalForce[b].assign(nd, 0.0);
+    if (nd > 0) {
+      std::vector<double> P(nd * nd);
+      for (int r = 0; r < nd; r++)
+        for (int c = 0; c < nd; c++) {
+          double s = 0;
+          for (int i = 0; i < 6; i++)
+            for (int j = 0; j < 6; j++) s += k.Sj[b](i, r) * AI[b](i, j) * k.Sj[b](j, c);
+          P[r * nd + c] = s;
+        }
+      invertSmall(P.data(), Psi[b].data(), nd);
+      // updateTotalForceDynamic (detail/GenericJoint.hpp:2554)
+      V6<double> bf = add(mul(AI[b], k.eta[b]), Bias[b]);
+      for (int r = 0; r < nd; r++) {
+        int dof = B.dof0 + r;
+        double springF = -w.spring[dof] * (q[dof] - w.restPos[dof] + dq[dof] * w.dt);
+        double dampF = -w.damping[dof] * dq[dof];
+        double s = 0; for (int i = 0; i < 6; i++) s += k.Sj[b](i, r) * bf[i];
+        totalForce[b][r] = tauCtrl[dof] + springF + dampF - s;
+      }
+    }
+    if (B.parent >= 0) {
+      // addChildArtInertiaToDynamic (detail/GenericJoint.hpp:2168)
+      M6<double> PI = AI[b];
+      if (nd > 0) {
+        double AIS[6][6];
+        for (int i = 0; i < 6; i++)
+          for (int c = 0; c < nd; c++) {
+            double s = 0; for (int j = 0; j < 6; j++) s += AI[b](i, j) * k.Sj[b](j, c);
+            AIS[i][c] = s;
+          }
+        for (int i = 0; i < 6; i++)
+          for (int j = 0; j < 6; j++) {
+            double s = 0;
+            for (int r = 0; r < nd; r++)
+              for (int c = 0; c < nd; c++) s += AIS[i][r] * Psi[b][r * nd + c] * AIS[j][c];
+            PI(i, j) -= s;
+          }
+      }
+      M6<double> add6 = transformInertia(inverse(k.T[b]), PI);
+      for (int i = 0; i < 36; i++) AI[B.parent].m[i] += add6.m[i];
+      // addChildBiasForceToDynamic (detail/GenericJoint.hpp:2395)
+      V6<double> SPsiTau = zero6<double>();
+      for (int r = 0; r < nd; r++) {
+        double t = 0; for (int c = 0; c < nd; c++) t += Psi[b][r * nd + c] * totalForce[b][c];
+        for (int i = 0; i < 6; i++) SPsiTau[i] += k.Sj[b](i, r) * t;
+      }
+      V6<double> beta = add(Bias[b], mul(AI[b], add(k.eta[b], SPsiTau)));
+      Bias[B.parent] = add(Bias[B.parent], dAdInvT(k.T[b], beta));
+    }
+  }
+  // forward recursion: updateAccelerationFD / updateAccelerationDynamic
+  for (int b = 0; b < nb; b++) {
+    const Body& B = w.bodies[b];
+    int nd = B.ndof;
+    V6<double> pa = B.parent >= 0 ? AdInvT(k.T[b], Acc[B.parent]) : zero6<double>();
+    V6<double> AIpa = mul(AI[b], pa);
+    std::vector<double> rhs(nd);
+    for (int r = 0; r < nd; r++) {
+      double s = 0; for (int i = 0; i < 6; i++) s += k.Sj[b](i, r) * AIpa[i];
+      rhs[r] = totalForce[b][r] - s;
+    }
+    V6<double> acc = add(pa, k.eta[b]);
+    for (int r = 0; r < nd; r++) {
+      double a = 0; for (int c = 0; c < nd; c++) a += Psi[b][r * nd + c] * rhs[c];
+      ddq[B.dof0 + r] = a;
+      for (int i = 0; i < 6; i++) acc[i] += k.Sj[b](i, r) * a;
+    }
+    Acc[b] = acc;
+  }
+}
+
+//------------------------------------------------------------------------------
+void invertSmall(const double* A, double* Ainv, int n) {
+  // Gauss-Jordan with partial pivoting (math::inverse<ConfigSpaceT>)
+  std::vector<double> M(A, A + n * n), I(n * n, 0.0);
+  for (int i = 0; i < n; i++) I[i * n + i] = 1.0;
+  for (int c = 0; c < n; c++) {
+    int p = c;
+    for (int r = c + 1; r < n; r++) if (std::fabs(M[r * n + c]) > std::fabs(M[p * n + c])) p = r;
+    if (p != c) for (int j = 0; j < n; j++) { std::swap(M[c * n + j], M[p * n + j]); std::swap(I[c * n + j], I[p * n + j]); }
+    double d = M[c * n + c];
+    for (int j = 0; j < n; j++) { M[c * n + j] /= d; I[c * n + j] /= d; }
+    for (int r = 0; r < n; r++) {
+      if (r == c) continue;
+      double f = M[r * n + c];
+      if (f == 0) continue;
+      for (int j = 0; j < n; j++) { M[r * n + j] -= f * M[c * n + j]; I[r * n + j] -= f * I[c * n + j]; }
+    }
+  }
+  std::memcpy(Ainv, I.data(), sizeof(double) * n * n);
+}
+
+//------------------------------------------------------------------------------
+void World::massMatrix(const Kin<double>& k, double* M) const {
+  // Skeleton::updateMassMatrix (Skeleton.cpp:12110): column-wise inverse
+  // dynamics with unit accelerations, no velocity or gravity terms.
+  std::vector<double> e(n, 0.0), col(n);
+  for (int c = 0; c < n; c++) {
+    std::fill(e.begin(), e.end(), 0.0);
+    e[c] = 1.0;
+    inverseDynamics<double>(*this, k, e.data(), false, false, col.data());
+    for (int r = 0; r < n; r++) M[r * n + c] = col[r];
+  }
+  // symmetrise exactly like the reference's lower-triangle fill
+  for (int r = 0; r < n; r++)
+    for (int c = r + 1; c < n; c++) M[c * n + r] = M[r * n + c];
+}
+
+void World::coriolisGravity(const Kin<double>& k, double* C) const {
+  std::vector<double> z(n, 0.0);
+  inverseDynamics<double>(*this, k, z.data(), true, true, C);
+}
+
+//------------------------------------------------------------------------------
+// Position integration.  World::integratePositions (World.cpp:300) with
+// mParallelVelocityAndPositionUpdates: p_{t+1} = integrate(p_t, v_t).
+void World::integratePositionsExplicit(const double* q, const double* v, double dtt, double* out) const {
+  for (int b = 0; b < nb; b++) {
+    const Body& B = bodies[b];
+    int o = B.dof0;
+    if (B.jtype == NIMBLE_JOINT_REVOLUTE || B.jtype == NIMBLE_JOINT_PRISMATIC) {
+      out[o] = q[o] + v[o] * dtt;  // math::integratePosition<R1Space>
+    } else if (B.jtype == NIMBLE_JOINT_FREE) {
+      // FreeJoint::integratePositionsExplicit (FreeJoint.cpp:920), identity-J:
+      // convertToPositions(convertToTransform(q) * convertToTransform(v*dt))
+      V3<double> w{{q[o], q[o + 1], q[o + 2]}};
+      M3<double> R = expMapRot(w);
+      V3<double> wd{{v[o] * dtt, v[o + 1] * dtt, v[o + 2] * dtt}};
+      M3<double> Rd = expMapRot(wd);
+      V3<double> ld{{v[o + 3] * dtt, v[o + 4] * dtt, v[o + 5] * dtt}};
+      M3<double> Rn = mul(R, Rd);
+      V3<double> pn = add(mul(R, ld), V3<double>{{q[o + 3], q[o + 4], q[o + 5]}});
+      V3<double> lg = logMap(Rn);
+      for (int i = 0; i < 3; i++) { out[o + i] = lg[i]; out[o + 3 + i] = pn[i]; }
+    }
+  }
+}
+
+// Skeleton::getPosPosJac / getVelPosJac (Skeleton.cpp:9291, :9310):
+// identity / dt*identity for R1 joints, central finite differences for the
+// FreeJoint (FreeJoint.cpp:965 EPS=1e-6, :987 EPS=1e-7).
+void World::posPosJac(const double* q, const double* v, double* J) const {
+  std::fill(J, J + n * n, 0.0);
+  for (int b = 0; b < nb; b++) {
+    const Body& B = bodies[b];
+    int o = B.dof0;
+    if (B.ndof == 1) J[o * n + o] = 1.0;
+    if (B.jtype == NIMBLE_JOINT_FREE) freeJointFD(q + o, v + o, true, J, o);
+  }
+}
+void World::velPosJac(const double* q, const double* v, double* J) const {
+  std::fill(J, J + n * n, 0.0);
+  for (int b = 0; b < nb; b++) {
+    const Body& B = bodies[b];
+    int o = B.dof0;
+    if (B.ndof == 1) J[o * n + o] = dt;
+    if (B.jtype == NIMBLE_JOINT_FREE) freeJointFD(q + o, v + o, false, J, o);
+  }
+}
+void World::freeJointFD(const double* q6, const double* v6, bool wrtPos, double* J, int o) const {
+  const double EPS = wrtPos ? 1e-6 : 1e-7;
+  auto integ = [&](const double* qq, const double* vv, double* out) {
+    V3<double> w{{qq[0], qq[1], qq[2]}};
+    M3<double> R = expMapRot(w);
+    V3<double> wd{{vv[0] * dt, vv[1] * dt, vv[2] * dt}};
+    M3<double> Rd = expMapRot(wd);
+    V3<double> ld{{vv[3] * dt, vv[4] * dt, vv[5] * dt}};
+    M3<double> Rn = mul(R, Rd);
+    V3<double> pn = add(mul(R, ld), V3<double>{{qq[3], qq[4], qq[5]}});
+    V3<double> lg = logMap(Rn);
+    for (int i = 0; i < 3; i++) { out[i] = lg[i]; out[3 + i] = pn[i]; }
+  };
+  for (int i = 0; i < 6; i++) {
+    double pq[6], pv[6], plus[6], minus[6];
+    for (int j = 0; j < 6; j++) { pq[j] = q6[j]; pv[j] = v6[j]; }
+    if (wrtPos) pq[i] += EPS; else pv[i] += EPS;
+    integ(pq, pv, plus);
+    for (int j = 0; j < 6; j++) { pq[j] = q6[j]; pv[j] = v6[j]; }
+    if (wrtPos) pq[i] -= EPS; else pv[i] -= EPS;
+    integ(pq, pv, minus);
+    for (int r = 0; r < 6; r++) J[(o + r) * n + (o + i)] = (plus[r] - minus[r]) / (2 * EPS);
+  }
+}
+
+//------------------------------------------------------------------------------
+// Jacobians of the unconstrained dynamics terms by forward-mode duals.
+//   dC[r*n+c]  = d C_r / d x_c   (x = q if wrtPos else v)       (getJacobianOfC)
+//   dMy[r*n+c] = d (M(q) y)_r / d q_c                           (getJacobianOfM)
+void World::jacobianOfC(const double* q, const double* v, bool wrtPos, double* dC) const {
+  std::vector<Dual> qd(n), vd(n), z(n, Dual(0.0)), tau(n);
+  for (int c = 0; c < n; c++) {
+    for (int i = 0; i < n; i++) { qd[i] = Dual(q[i]); vd[i] = Dual(v[i]); }
+    if (wrtPos) qd[c].d = 1.0; else vd[c].d = 1.0;
+    Kin<Dual> k; k.compute(*this, qd.data(), vd.data());
+    inverseDynamics<Dual>(*this, k, z.data(), true, true, tau.data());
+    for (int r = 0; r < n; r++) dC[r * n + c] = tau[r].d;
+  }
+}
+void World::jacobianOfMy(const double* q, const double* y, double* dMy) const {
+  std::vector<Dual> qd(n), vd(n, Dual(0.0)), yd(n), tau(n);
+  for (int i = 0; i < n; i++) yd[i] = Dual(y[i]);
+  for (int c = 0; c < n; c++) {
+    for (int i = 0; i < n; i++) qd[i] = Dual(q[i]);
+    qd[c].d = 1.0;
+    Kin<Dual> k; k.compute(*this, qd.data(), vd.data());
+    inverseDynamics<Dual>(*this, k, yd.data(), false, false, tau.data());
+    for (int r = 0; r < n; r++) dMy[r * n + c] = tau[r].d;
+  }
+}
+
+}  // namespace oracle

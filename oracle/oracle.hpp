@@ -1,0 +1,112 @@
+// ORACLE / TEST INFRASTRUCTURE ONLY -- see nimble_oracle.cpp header.
+#pragma once
+#include <vector>
+
+#include "../include/nimble_amd.h"
+#include "spatial.hpp"
+
+namespace oracle {
+
+struct Body {
+  int parent, skel, jtype, dof0, ndof;
+  bool mobile;
+  Iso<double> Tpj, Tcj;
+  double axis[3];
+  M6<double> G;  // spatial inertia in body frame
+  double friction, restitution;
+};
+
+struct Shape {
+  int body, type;
+  double size[3];
+  Iso<double> T;
+};
+
+struct World;
+
+template <class S>
+struct Kin {
+  std::vector<Iso<S>> T, Tw;   // relative (parent->child) and world transforms
+  std::vector<M6<S>> Sj;       // joint Jacobian columns (child frame)
+  std::vector<V6<S>> V, eta;   // body velocity and partial acceleration
+  void compute(const World& w, const S* q, const S* dq);
+};
+
+// One contact point as produced by the collision detector
+// (dart/collision/Contact.hpp).  normal points from B into A.
+struct Contact {
+  int shapeA, shapeB, bodyA, bodyB;
+  double point[3], normal[3], depth;
+  int type;
+};
+
+// Everything BackpropSnapshot needs (dart/neural/BackpropSnapshot.hpp and
+// ConstrainedGroupGradientMatrices.hpp).
+struct Snapshot {
+  std::vector<double> q, v, tau, preConstraintV, postQ, postV;
+  // constraint data (empty when no contact)
+  int numRows = 0;
+  std::vector<Contact> contacts;
+  std::vector<double> Aall;      // n x rows, column j = J^T e_j (getConstraintForces)
+  std::vector<double> massedImpulse;  // n x rows, column j = Minv J^T e_j
+  std::vector<double> lcpA, lcpB, lcpLo, lcpHi, lcpX;
+  std::vector<int> lcpFIndex;
+  std::vector<double> aColNorms;
+  std::vector<int> mapping;      // per row: CLAMPING=-1 .. see ConstraintMapping
+  std::vector<int> clampingIndex, upperBoundIndex;
+  int numClamping = 0, numUpperBound = 0;
+  std::vector<double> fc;        // clamping impulses
+  std::vector<double> bounceDiag, restitutionDiag, penetrationVel;
+  std::vector<double> E;         // numUpperBound x numClamping
+  double cfm = 0.0;
+  bool ignoredFriction = false;
+  bool shortCircuit = false;
+};
+
+struct World {
+  int nb = 0, n = 0;
+  double dt = 0.001, g[3] = {0, 0, 0};
+  double clipDepth = 0.03, fallbackCfm = 1e-4;
+  bool penetrationCorrection = false, parallelPosVel = true;
+  std::vector<Body> bodies;
+  std::vector<Shape> shapes;
+  std::vector<int> dofBody;
+  std::vector<double> damping, spring, restPos, posLo, posHi, velLo, velHi, forceLo, forceHi;
+
+  explicit World(const nimble_world_desc* d);
+
+  void massMatrix(const Kin<double>& k, double* M) const;
+  void coriolisGravity(const Kin<double>& k, double* C) const;
+  void integratePositionsExplicit(const double* q, const double* v, double dtt, double* out) const;
+  void posPosJac(const double* q, const double* v, double* J) const;
+  void velPosJac(const double* q, const double* v, double* J) const;
+  void freeJointFD(const double* q6, const double* v6, bool wrtPos, double* J, int o) const;
+  void jacobianOfC(const double* q, const double* v, bool wrtPos, double* dC) const;
+  void jacobianOfMy(const double* q, const double* y, double* dMy) const;
+
+  // ancestry helpers
+  bool isAncestorOrSelf(int anc, int b) const {
+    while (b >= 0) { if (b == anc) return true; b = bodies[b].parent; }
+    return false;
+  }
+};
+
+void forwardDynamicsABA(const World& w, const Kin<double>& k, const double* q, const double* dq,
+                        const double* tauCtrl, double* ddq);
+void invertSmall(const double* A, double* Ainv, int n);
+template <class S>
+void inverseDynamics(const World& w, const Kin<S>& k, const S* ddq, bool withGravity, bool withVel, S* tau);
+
+// timestep (oracle_step.cpp)
+void step(const World& w, const double* state, const double* tau, std::vector<double>& lcpCache,
+          double* nextState, Snapshot& snap);
+void backprop(const World& w, const Snapshot& snap, const double* gradNext, double* gradState, double* gradTau);
+
+// contacts (oracle_contact.cpp)
+void collide(const World& w, const Kin<double>& k, std::vector<Contact>& out);
+
+// dense helpers
+void cholSolve(const double* A, const double* b, double* x, int n);
+void pinvSolve(const double* A, const double* b, double* x, int n, double* pinvOut = nullptr);
+
+}  // namespace oracle

@@ -1,0 +1,152 @@
+"""ORACLE / TEST INFRASTRUCTURE ONLY.
+
+ctypes wrapper over oracle/liboracle.so -- the CPU restatement of the
+reference's timestep -- for tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg.  Never imported by nimblephysics_amd.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+REF_LIB = os.path.join(HERE, "_ref", "libodelcp.so")
+MAX_LCP = 48
+
+_lib = None
+_ref = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE, "all"])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = C.CDLL(LIB)
+        vp, ip, dp = C.c_void_p, C.c_int, C.POINTER(C.c_double)
+        L.oracle_world_create.argtypes = [vp]
+        L.oracle_world_create.restype = vp
+        L.oracle_world_destroy.argtypes = [vp]
+        L.oracle_snapshots_create.argtypes = [ip]
+        L.oracle_snapshots_create.restype = vp
+        L.oracle_snapshots_destroy.argtypes = [vp]
+        L.oracle_forward.argtypes = [vp, ip, dp, dp, dp, dp, vp]
+        L.oracle_backward.argtypes = [vp, ip, vp, dp, dp, dp]
+        L.oracle_mass_matrix.argtypes = [vp, dp, dp]
+        L.oracle_coriolis_gravity.argtypes = [vp, dp, dp, dp]
+        L.oracle_forward_dynamics.argtypes = [vp, dp, dp, dp, dp]
+        L.oracle_body_transforms.argtypes = [vp, dp, dp]
+        L.oracle_jacobian_of_c.argtypes = [vp, dp, dp, ip, dp]
+        L.oracle_num_contacts.argtypes = [vp, ip]
+        L.oracle_num_contacts.restype = ip
+        for extra in ("oracle_contacts", "oracle_lcp_debug"):
+            if hasattr(L, extra):
+                getattr(L, extra).restype = ip
+        _lib = L
+    return _lib
+
+
+def ref_lib():
+    """The reference's own Dantzig solver compiled from /root/reference
+    (oracle/_ref/libodelcp.so); None when it was not built."""
+    global _ref
+    if _ref is None and os.path.exists(REF_LIB):
+        R = C.CDLL(REF_LIB)
+        dp = C.POINTER(C.c_double)
+        R.ref_dSolveLCP.argtypes = [C.c_int, dp, dp, dp, dp, C.c_int, dp, dp, C.POINTER(C.c_int), C.c_int]
+        R.ref_dSolveLCP.restype = C.c_int
+        _ref = R
+    return _ref
+
+
+def _p(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+class OracleWorld:
+    def __init__(self, world):
+        self.desc, self._keep = world.desc()
+        self.n = world.getNumDofs()
+        self.nb = self.desc.num_bodies
+        self.h = lib().oracle_world_create(C.byref(self.desc))
+        self.snaps = None
+        self.batch = 0
+        self.cache = None
+
+    def __del__(self):
+        try:
+            if self.snaps:
+                lib().oracle_snapshots_destroy(self.snaps)
+            lib().oracle_world_destroy(self.h)
+        except Exception:
+            pass
+
+    def reset_cache(self, batch):
+        self.cache = np.zeros((batch, MAX_LCP + 1))
+        self.cache[:, 0] = -1
+
+    def forward(self, state, forces):
+        state = np.ascontiguousarray(np.atleast_2d(state), dtype=np.float64)
+        forces = np.ascontiguousarray(np.atleast_2d(forces), dtype=np.float64)
+        B = state.shape[0]
+        if self.snaps is None or self.batch != B:
+            if self.snaps:
+                lib().oracle_snapshots_destroy(self.snaps)
+            self.snaps = lib().oracle_snapshots_create(B)
+            self.batch = B
+        if self.cache is None or self.cache.shape[0] != B:
+            self.reset_cache(B)
+        nxt = np.zeros_like(state)
+        lib().oracle_forward(self.h, B, _p(state), _p(forces), _p(self.cache), _p(nxt), self.snaps)
+        return nxt
+
+    def backward(self, grad_next):
+        g = np.ascontiguousarray(np.atleast_2d(grad_next), dtype=np.float64)
+        B = g.shape[0]
+        gs = np.zeros_like(g)
+        gf = np.zeros((B, self.n))
+        lib().oracle_backward(self.h, B, self.snaps, _p(g), _p(gs), _p(gf))
+        return gs, gf
+
+    def mass_matrix(self, q):
+        q = np.ascontiguousarray(q, dtype=np.float64)
+        M = np.zeros((self.n, self.n))
+        lib().oracle_mass_matrix(self.h, _p(q), _p(M))
+        return M
+
+    def coriolis_gravity(self, q, v):
+        q = np.ascontiguousarray(q, dtype=np.float64)
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        Cg = np.zeros(self.n)
+        lib().oracle_coriolis_gravity(self.h, _p(q), _p(v), _p(Cg))
+        return Cg
+
+    def forward_dynamics(self, q, v, tau):
+        q, v, tau = (np.ascontiguousarray(x, dtype=np.float64) for x in (q, v, tau))
+        ddq = np.zeros(self.n)
+        lib().oracle_forward_dynamics(self.h, _p(q), _p(v), _p(tau), _p(ddq))
+        return ddq
+
+    def body_transforms(self, q):
+        q = np.ascontiguousarray(q, dtype=np.float64)
+        T = np.zeros((self.nb, 12))
+        lib().oracle_body_transforms(self.h, _p(q), _p(T))
+        return T.reshape(self.nb, 3, 4)
+
+    def jacobian_of_c(self, q, v, wrt_pos):
+        q = np.ascontiguousarray(q, dtype=np.float64)
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        J = np.zeros((self.n, self.n))
+        lib().oracle_jacobian_of_c(self.h, _p(q), _p(v), 1 if wrt_pos else 0, _p(J))
+        return J
+
+    def num_contacts(self, b=0):
+        return lib().oracle_num_contacts(self.snaps, b)

@@ -1,0 +1,84 @@
+// ORACLE / TEST INFRASTRUCTURE ONLY -- C entry points for tests/ (ctypes).
+#include <cstring>
+#include <vector>
+
+#include "oracle.hpp"
+
+using namespace oracle;
+
+struct OracleSnap { Snapshot s; };
+
+extern "C" {
+
+void* oracle_world_create(const nimble_world_desc* d) { return new World(d); }
+void oracle_world_destroy(void* w) { delete static_cast<World*>(w); }
+
+// Batched loop over independent worlds (the CPU baseline is this loop).
+// lcp_cache: [batch][NIMBLE_MAX_LCP + 1], element 0 = cached size (-1 = empty)
+void* oracle_snapshots_create(int batch) { return new std::vector<OracleSnap>(batch); }
+void oracle_snapshots_destroy(void* s) { delete static_cast<std::vector<OracleSnap>*>(s); }
+
+int oracle_forward(void* wp, int batch, const double* state, const double* tau, double* lcpCache,
+                   double* next, void* snaps) {
+  World& w = *static_cast<World*>(wp);
+  auto& S = *static_cast<std::vector<OracleSnap>*>(snaps);
+  const int n = w.n;
+  for (int b = 0; b < batch; b++) {
+    double* cache = lcpCache + (size_t)b * (NIMBLE_MAX_LCP + 1);
+    std::vector<double> c;
+    int sz = (int)cache[0];
+    if (sz >= 0) c.assign(cache + 1, cache + 1 + sz);
+    else c.clear();
+    std::vector<double>* cp = &c;
+    bool empty = sz < 0;
+    if (empty) c.clear();
+    step(w, state + (size_t)b * 2 * n, tau + (size_t)b * n, *cp, next + (size_t)b * 2 * n, S[b].s);
+    cache[0] = (double)c.size();
+    for (size_t i = 0; i < c.size(); i++) cache[1 + i] = c[i];
+  }
+  return 0;
+}
+
+int oracle_backward(void* wp, int batch, void* snaps, const double* gradNext, double* gradState, double* gradTau) {
+  World& w = *static_cast<World*>(wp);
+  auto& S = *static_cast<std::vector<OracleSnap>*>(snaps);
+  const int n = w.n;
+  for (int b = 0; b < batch; b++)
+    backprop(w, S[b].s, gradNext + (size_t)b * 2 * n, gradState + (size_t)b * 2 * n, gradTau + (size_t)b * n);
+  return 0;
+}
+
+// Debug getters (single world)
+void oracle_mass_matrix(void* wp, const double* q, double* M) {
+  World& w = *static_cast<World*>(wp);
+  std::vector<double> v(w.n, 0.0);
+  Kin<double> k; k.compute(w, q, v.data());
+  w.massMatrix(k, M);
+}
+void oracle_coriolis_gravity(void* wp, const double* q, const double* v, double* C) {
+  World& w = *static_cast<World*>(wp);
+  Kin<double> k; k.compute(w, q, v);
+  w.coriolisGravity(k, C);
+}
+void oracle_forward_dynamics(void* wp, const double* q, const double* v, const double* tau, double* ddq) {
+  World& w = *static_cast<World*>(wp);
+  Kin<double> k; k.compute(w, q, v);
+  forwardDynamicsABA(w, k, q, v, tau, ddq);
+}
+void oracle_body_transforms(void* wp, const double* q, double* T /* nb x 12 */) {
+  World& w = *static_cast<World*>(wp);
+  std::vector<double> v(w.n, 0.0);
+  Kin<double> k; k.compute(w, q, v.data());
+  for (int b = 0; b < w.nb; b++)
+    for (int r = 0; r < 3; r++) {
+      for (int c = 0; c < 3; c++) T[b * 12 + r * 4 + c] = k.Tw[b].R(r, c);
+      T[b * 12 + r * 4 + 3] = k.Tw[b].p[r];
+    }
+}
+void oracle_jacobian_of_c(void* wp, const double* q, const double* v, int wrtPos, double* dC) {
+  static_cast<World*>(wp)->jacobianOfC(q, v, wrtPos != 0, dC);
+}
+int oracle_num_contacts(void* snaps, int b) {
+  return (int)(*static_cast<std::vector<OracleSnap>*>(snaps))[b].s.contacts.size();
+}
+}

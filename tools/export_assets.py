@@ -1,0 +1,23 @@
+"""Regenerate nimblephysics_amd/assets/*.json from the reference's model data
+(run in the container that has /root/reference; the GPU box does not)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from nimblephysics_amd import assets, urdf  # noqa: E402
+
+REF = os.environ.get("NIMBLE_REFERENCE", "/root/reference")
+MODELS = {
+    "atlas": ("data/sdf/atlas/atlas_v3_box_colliders.urdf", False),
+    "atlas_ground": ("data/sdf/atlas/ground.urdf", False),
+    "kr5": ("data/urdf/KR5/KR5 sixx R650.urdf", True),
+    "kr5_ground": ("data/urdf/KR5/ground.urdf", True),
+    "cartpole_urdf": ("data/urdf/cartpole.urdf", False),
+}
+
+if __name__ == "__main__":
+    for name, (rel, ignore_mesh) in MODELS.items():
+        skel = urdf.load_urdf(os.path.join(REF, rel), ignore_mesh_collisions=ignore_mesh)
+        out = os.path.join(assets.ASSET_DIR, name + ".json")
+        assets.save_skeleton(skel, out)
+        print(name, skel.getNumDofs(), "dofs", len(skel.bodies), "bodies ->", out)

@@ -1,0 +1,190 @@
+"""Benchmark: differentiable timesteps/sec (fwd+bwd) on a batch of worlds.
+
+BASELINE.json metric "differentiable timesteps/sec (fwd+bwd), 1024-env Atlas
+w/ contact".  One step = nimble.timestep forward over the whole batch +
+backward of a synthetic upstream gradient through it (the reference's
+TimestepLayer.forward/backward, python/nimblephysics/timestep.py), then the
+batch state advances to the new state (a rollout, so contacts evolve and the
+LCP warm start is exercised).  Inputs are resident in HBM.
+
+Multi-GPU (torchrun): one process per GPU, each advancing its own shard of
+independent worlds (weak scaling, no data-path collective); the timed region
+is bracketed by barriers and the max over ranks is used.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import models  # noqa: E402
+import nimblephysics_amd as nimble  # noqa: E402
+from nimblephysics_amd import _native  # noqa: E402
+
+FP64_VECTOR_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (spec; = FP32 vector 157.3 / 2)
+HBM_PEAK_GBS = 8000.0
+
+WORKLOADS = {
+    "atlas": ("Atlas 33-DoF (atlas_v3_box_colliders) + ground, foot contact", lambda: models.atlas_world(True)),
+    "atlas_air": ("Atlas 33-DoF, no ground (contact-free)", lambda: models.atlas_world(False)),
+    "cartpole": ("cartpole, contact-free", models.cartpole_world),
+}
+
+
+def init_dist():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws > 1:
+        import torch.distributed as dist
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        return dist, dist.get_rank(), ws, local
+    return None, 0, 1, 0
+
+
+def barrier(dist):
+    if dist is not None:
+        dist.barrier()
+
+
+class KernelTimer:
+    """HIP events around the native launches, on the stream they run on."""
+
+    def __init__(self):
+        self.fwd, self.bwd = [], []
+        self.enabled = False
+
+    def wrap(self, devworld):
+        timer = self
+        f0, b0 = devworld.forward, devworld.backward
+
+        def fwd(*a):
+            if not timer.enabled:
+                return f0(*a)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            f0(*a)
+            e.record()
+            timer.fwd.append((s, e))
+
+        def bwd(*a):
+            if not timer.enabled:
+                return b0(*a)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            b0(*a)
+            e.record()
+            timer.bwd.append((s, e))
+        devworld.forward, devworld.backward = fwd, bwd
+
+    @staticmethod
+    def mean_ms(pairs):
+        return float(np.mean([s.elapsed_time(e) for s, e in pairs])) if pairs else float("nan")
+
+
+def cpu_baseline(world, batch, seconds_target=12.0):
+    """Oracle (CPU restatement, 1 thread) on a bounded sample of the same workload."""
+    from oracle.oracle import OracleWorld
+    o = OracleWorld(world)
+    st, f = models.random_states(world, batch, seed=11, q_scale=0.02, v_scale=0.05, f_scale=1.0)
+    g = np.random.default_rng(5).standard_normal(st.shape)
+    steps = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds_target:
+        nxt = o.forward(st, f)
+        o.backward(g)
+        st = nxt
+        steps += 1
+    dt = time.perf_counter() - t0
+    return {"value": steps * batch / dt, "unit": "timesteps/s", "cores": 1, "kind": "port",
+            "sample": f"{steps} fwd+bwd steps x {batch} worlds of the same workload, oracle/liboracle.so, 1 thread, {dt:.1f}s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=1024, help="worlds per GPU")
+    ap.add_argument("--workload", default="atlas", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    dist, rank, ws, local = init_dist()
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    wl_name, make = WORKLOADS[args.workload]
+    world = make()
+    n = world.getNumDofs()
+    st, f = models.random_states(world, args.batch, seed=1000 + rank, q_scale=0.02, v_scale=0.05, f_scale=1.0)
+    state = torch.tensor(st, device=dev)
+    action = torch.tensor(f, device=dev)
+    g = torch.tensor(np.random.default_rng(rank).standard_normal(st.shape), device=dev)
+    devworld = world.native()
+    timer = KernelTimer()
+    timer.wrap(devworld)
+
+    def one_step(state):
+        s = state.detach().requires_grad_(True)
+        a = action.detach().requires_grad_(True)
+        nxt = nimble.timestep(world, s, a)
+        nxt.backward(g)
+        return nxt.detach()
+
+    s0 = state
+    for _ in range(args.warmup):
+        state = one_step(state)
+    torch.cuda.synchronize()
+    barrier(dist)
+    torch.cuda.synchronize()
+    timer.enabled = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        state = one_step(state)
+    torch.cuda.synchronize()
+    barrier(dist)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    timer.enabled = False
+    if dist is not None:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    total = args.batch * ws * args.steps
+    value = total / elapsed
+    fwd_ms = timer.mean_ms(timer.fwd)
+    bwd_ms = timer.mean_ms(timer.bwd)
+    flops = _native.flop_estimate(world)
+    dom = "backward" if bwd_ms >= fwd_ms else "forward"
+    dom_ms = max(bwd_ms, fwd_ms)
+    achieved = flops[dom] * args.batch / (dom_ms * 1e-3) / 1e12
+    if rank == 0:
+        out = {
+            "metric": "differentiable timesteps/sec (fwd+bwd), 1024-env Atlas w/ contact",
+            "value": value, "unit": "timesteps/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64", "data": "synthetic (perturbed standing pose, random torques)",
+            "config": {"workload": wl_name, "worlds_per_gpu": args.batch, "dofs": n,
+                       "global_batch": args.batch * ws, "parallelism": f"independent worlds x{ws}"},
+            "kernels_ms": {"forward": fwd_ms, "backward": bwd_ms},
+            "roofline": {"bound": "mfma", "kernel": f"nimble_{dom}_kernel", "achieved": achieved,
+                         "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP64_VECTOR_PEAK_TFLOPS,
+                         "traffic": None, "flops_per_world": flops[dom],
+                         "note": "fp64 VALU-bound (no fp64 MFMA use); peak = fp64 vector rate"},
+        }
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(make(), 64)
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

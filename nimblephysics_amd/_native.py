@@ -96,3 +96,49 @@ class DeviceWorld:
         B = state.shape[0]
         _check(lib().nimble_backward(self.h, B, _ptr(state), _ptr(forces), _ptr(snapshot), _ptr(grad_next),
                                      _ptr(grad_state), _ptr(grad_forces), C.c_void_p(stream_ptr)))
+
+
+def flop_estimate(world) -> dict:
+    """Algorithmic fp64 FLOPs per world for one launch of each kernel, counted
+    from the implemented algorithm's loop structure (FMA = 2 FLOPs):
+    kinematics, world-frame composites, CRBA mass matrix, Cholesky + solves,
+    and in the backward the derivative composites plus one closed-form
+    dID/dq and dC/dv column per dof (only related body pairs)."""
+    d = world.desc_arrays()
+    nb, n = int(d["num_bodies"]), int(d["num_dofs"])
+    parent = list(d["parent"])
+    jt = list(d["joint_type"])
+    ndof = [0 if t == 0 else (6 if t == 3 else 1) for t in jt]
+    anc = []
+    for b in range(nb):
+        s = {b}
+        p = parent[b]
+        while p >= 0:
+            s.add(p)
+            p = parent[p]
+        anc.append(s)
+    dof_body = []
+    for b in range(nb):
+        dof_body += [b] * ndof[b]
+    kin = sum(330 + 60 * ndof[b] for b in range(nb))
+    comp = nb * 330 + nb * 42
+    related_pairs = sum(1 for j in range(n) for k in range(j + 1)
+                        if dof_body[k] in anc[dof_body[j]] or dof_body[j] in anc[dof_body[k]])
+    mass = related_pairs * 84 + n * 12
+    chol = n ** 3 / 3.0 + n ** 2
+    solve = 2.0 * n * n
+    fwd = kin + comp + mass + chol + solve + 10 * n
+    dcomp = nb * 1800 + nb * 126
+    lanes = 0.0
+    for k in range(n):
+        b = dof_body[k]
+        lanes += 1020
+        for c in range(nb):
+            if ndof[c] == 0:
+                continue
+            if b in anc[c]:
+                lanes += (1020 if c != b else 0) + 80 * ndof[c]
+            elif c in anc[b]:
+                lanes += 50 * ndof[c]
+    bwd = kin * 2 + comp + mass + chol + 2 * solve + dcomp + lanes + 20 * n
+    return {"forward": float(fwd), "backward": float(bwd)}

@@ -47,6 +47,9 @@ struct Snapshot {
   // constraint data (empty when no contact)
   int numRows = 0;
   std::vector<Contact> contacts;
+  std::vector<int> rowContact, rowDirIdx;  // per LCP row
+  std::vector<double> rowDir;              // per LCP row, world direction for body A (3)
+  std::vector<double> freeAcc;             // unconstrained ddq (Minv (tau - C - D v - K ..))
   std::vector<double> Aall;      // n x rows, column j = J^T e_j (getConstraintForces)
   std::vector<double> massedImpulse;  // n x rows, column j = Minv J^T e_j
   std::vector<double> lcpA, lcpB, lcpLo, lcpHi, lcpX;

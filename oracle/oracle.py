@@ -47,9 +47,15 @@ def lib():
         L.oracle_jacobian_of_c.argtypes = [vp, dp, dp, ip, dp]
         L.oracle_num_contacts.argtypes = [vp, ip]
         L.oracle_num_contacts.restype = ip
-        for extra in ("oracle_contacts", "oracle_lcp_debug"):
-            if hasattr(L, extra):
-                getattr(L, extra).restype = ip
+        L.oracle_contacts.argtypes = [vp, ip, dp, ip]
+        L.oracle_contacts.restype = ip
+        L.oracle_lcp_debug.argtypes = [vp, ip, C.POINTER(ip), dp, ip]
+        L.oracle_lcp_debug.restype = ip
+        L.oracle_dantzig.argtypes = [ip, dp, dp, dp, dp, C.POINTER(ip), dp, ip]
+        L.oracle_dantzig.restype = ip
+        L.oracle_cod_solve.argtypes = [dp, ip, ip, dp, dp]
+        L.oracle_box_box.argtypes = [dp, dp, dp, dp, dp]
+        L.oracle_box_box.restype = ip
         _lib = L
     return _lib
 
@@ -150,3 +156,66 @@ class OracleWorld:
 
     def num_contacts(self, b=0):
         return lib().oracle_num_contacts(self.snaps, b)
+
+
+def _pi(a):
+    return a.ctypes.data_as(C.POINTER(C.c_int))
+
+
+def contacts(ow: "OracleWorld", b=0, maxc=64):
+    out = np.zeros((maxc, 10))
+    k = lib().oracle_contacts(ow.snaps, b, _p(out), maxc)
+    return out[:k]
+
+
+def lcp_debug(ow: "OracleWorld", b=0, max_rows=64):
+    mapping = np.zeros(max_rows, dtype=np.int32)
+    x = np.zeros(max_rows)
+    m = lib().oracle_lcp_debug(ow.snaps, b, _pi(mapping), _p(x), max_rows)
+    return mapping[:m].copy(), x[:m].copy()
+
+
+def dantzig(A, b, lo, hi, findex, early=False):
+    """The oracle's restatement of dSolveLCP."""
+    A = np.ascontiguousarray(A, dtype=np.float64)
+    n = A.shape[0]
+    b, lo, hi = (np.ascontiguousarray(v, dtype=np.float64).copy() for v in (b, lo, hi))
+    fi = np.ascontiguousarray(findex, dtype=np.int32).copy()
+    x = np.zeros(n)
+    ok = lib().oracle_dantzig(n, _p(A), _p(b), _p(lo), _p(hi), _pi(fi), _p(x), 1 if early else 0)
+    return bool(ok), x
+
+
+def ref_dantzig(A, b, lo, hi, findex, early=False):
+    """The reference's own dSolveLCP (oracle/_ref/libodelcp.so); None if unbuilt."""
+    R = ref_lib()
+    if R is None:
+        return None
+    n = A.shape[0]
+    nskip = n if n <= 1 else (((n - 1) | 3) + 1)
+    Ap = np.zeros((n, nskip))
+    Ap[:, :n] = A
+    Ap = np.ascontiguousarray(Ap)
+    b, lo, hi = (np.ascontiguousarray(v, dtype=np.float64).copy() for v in (b, lo, hi))
+    fi = np.ascontiguousarray(findex, dtype=np.int32).copy()
+    x = np.zeros(n)
+    w = np.zeros(n)
+    ok = R.ref_dSolveLCP(n, _p(Ap), _p(x), _p(b), _p(w), 0, _p(lo), _p(hi), _pi(fi), 1 if early else 0)
+    return bool(ok), x
+
+
+def cod_solve(A, b):
+    A = np.ascontiguousarray(A, dtype=np.float64)
+    m, n = A.shape
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    x = np.zeros(n)
+    lib().oracle_cod_solve(_p(A), m, n, _p(b), _p(x))
+    return x
+
+
+def box_box(size1, T1, size2, T2):
+    out = np.zeros((16, 8))
+    s1, s2 = (np.ascontiguousarray(s, dtype=np.float64) for s in (size1, size2))
+    t1, t2 = (np.ascontiguousarray(np.asarray(T, dtype=np.float64)[:3, :4]) for T in (T1, T2))
+    k = lib().oracle_box_box(_p(s1), _p(t1), _p(s2), _p(t2), _p(out))
+    return out[:k]

@@ -3,6 +3,7 @@
 #include <vector>
 
 #include "oracle.hpp"
+#include "oracle_lcp.hpp"
 
 using namespace oracle;
 
@@ -81,4 +82,37 @@ void oracle_jacobian_of_c(void* wp, const double* q, const double* v, int wrtPos
 int oracle_num_contacts(void* snaps, int b) {
   return (int)(*static_cast<std::vector<OracleSnap>*>(snaps))[b].s.contacts.size();
 }
+// contacts of world b after a forward: per contact [point3, normal3, depth, type, bodyA, bodyB]
+int oracle_contacts(void* snaps, int b, double* out, int maxc) {
+  const auto& cs = (*static_cast<std::vector<OracleSnap>*>(snaps))[b].s.contacts;
+  int k = 0;
+  for (const auto& c : cs) {
+    if (k >= maxc) break;
+    double* o = out + 10 * k;
+    for (int i = 0; i < 3; i++) { o[i] = c.point[i]; o[3 + i] = c.normal[i]; }
+    o[6] = c.depth; o[7] = c.type; o[8] = c.bodyA; o[9] = c.bodyB;
+    k++;
+  }
+  return k;
 }
+// LCP classification of world b: mapping per row (-1 clamping, -2 not clamping, >=0 upper bound)
+int oracle_lcp_debug(void* snaps, int b, int* mapping, double* x, int maxRows) {
+  const auto& s = (*static_cast<std::vector<OracleSnap>*>(snaps))[b].s;
+  int m = s.numRows < maxRows ? s.numRows : maxRows;
+  for (int i = 0; i < m; i++) { mapping[i] = s.mapping[i]; x[i] = s.lcpX[i]; }
+  return s.numRows;
+}
+// Dantzig restatement on a raw problem (A n x n row-major); returns success
+int oracle_dantzig(int n, const double* A, const double* b, const double* lo, const double* hi, const int* findex,
+                   double* x, int earlyTermination) {
+  std::vector<double> Ac(A, A + n * n), bc(b, b + n), loc(lo, lo + n), hic(hi, hi + n);
+  std::vector<int> fi(findex, findex + n);
+  return dantzigSolveLCP(n, Ac.data(), x, bc.data(), nullptr, 0, loc.data(), hic.data(), fi.data(),
+                         earlyTermination != 0) ? 1 : 0;
+}
+void codSolveC(const double* A, int m, int n, const double* b, double* x);
+void oracle_cod_solve(const double* A, int m, int n, const double* b, double* x) { codSolveC(A, m, n, b, x); }
+int oracle_box_box(const double* size1, const double* T1, const double* size2, const double* T2, double* out);
+}
+namespace oracle { void codSolve(const double* A, int m, int n, const double* b, double* x); }
+void codSolveC(const double* A, int m, int n, const double* b, double* x) { oracle::codSolve(A, m, n, b, x); }

@@ -1,38 +1,908 @@
 // ORACLE / TEST INFRASTRUCTURE ONLY -- see nimble_oracle.cpp header.
-// Collision detection + contact LCP (filled in incrementally).
+//
+// Contacts on the timestep hot path, restated:
+//  * box-box narrow phase: dart/collision/dart/DARTCollide.cpp:764 dBoxBox
+//    (Nimble's variant: 15 separating axes with the 1.05 fudge factor on edge
+//    axes, incident-face clipping intersectRectQuad :513, all clipped points
+//    kept, contact typing VERTEX_FACE / FACE_VERTEX / EDGE_EDGE);
+//  * detector loop + filter: DARTCollisionDetector.cpp:127, postProcess :357,
+//    CollisionFilter.cpp:105;
+//  * ContactConstraint (dart/constraint/ContactConstraint.cpp): spatial normals
+//    :115-200, getInformation :393, tangent basis :705;
+//  * BoxedLcpConstraintSolver::buildLcpInputs / solveLcp
+//    (BoxedLcpConstraintSolver.cpp:175, :330) with the gradient short-circuit;
+//  * ConstrainedGroupGradientMatrices::constructMatrices (:482) and
+//    opportunisticallyStandardizeResults (:218);
+//  * LCPUtils (LCPUtils.cpp): isLCPSolutionValid, guessSolution, reduce,
+//    removeFriction;
+//  * BackpropSnapshot Jacobian pieces for the clamping set
+//    (BackpropSnapshot.cpp:980 getVelJacobianWrt, :2723
+//    getJacobianOfConstraintForce, :3181 getJacobianOfLCPOffsetClampingSubset).
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <limits>
 
 #include "oracle_lcp.hpp"
 
 namespace oracle {
 
-void collide(const World& w, const Kin<double>& k, std::vector<Contact>& out) {
-  out.clear();
-  (void)w; (void)k;
+void codSolve(const double* A, int m, int n, const double* b, double* x);
+bool pgsSolveLCP(int n, double* A, double* x, double* b, double* lo, double* hi, const int* findex);
+
+static const double kInf = std::numeric_limits<double>::infinity();
+enum { CT_FACE_VERTEX = 1, CT_VERTEX_FACE = 2, CT_EDGE_EDGE = 3 };
+
+//------------------------------------------------------------------------------
+// dBoxBox restatement.  R? are 3x3 row-major world rotations, p? centres,
+// A/B half sizes.  Appends contacts (normal from box 2 into box 1).
+static int boxBox(const double* p1, const double* R1, const double* A, const double* p2, const double* R2,
+                  const double* B, double clipDepth, std::vector<Contact>& out, int s1, int s2, int b1, int b2) {
+  const double fudge = 1.05;
+  auto col = [](const double* R, int c, double* o) { o[0] = R[c]; o[1] = R[3 + c]; o[2] = R[6 + c]; };
+  double p[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+  double pp[3];
+  for (int i = 0; i < 3; i++) pp[i] = R1[i] * p[0] + R1[3 + i] * p[1] + R1[6 + i] * p[2];  // R1^T p
+  double Rm[3][3], Q[3][3];
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) {
+      Rm[i][j] = R1[i] * R2[j] + R1[3 + i] * R2[3 + j] + R1[6 + i] * R2[6 + j];  // R1^T R2
+      Q[i][j] = std::fabs(Rm[i][j]);
+    }
+  double s = -1e12;
+  int invertNormal = 0, code = 0;
+  int normalCol = -1, normalBox = 0;  // face normal = column of R1 (box 1) or R2 (box 2)
+  double normalC[3] = {0, 0, 0};
+  auto tstFace = [&](double e1, double e2, int box, int colIdx, int cc) {
+    double s2v = std::fabs(e1) - e2;
+    if (s2v > s) { s = s2v; normalBox = box; normalCol = colIdx; invertNormal = e1 < 0; code = cc; }
+  };
+  tstFace(pp[0], A[0] + B[0] * Q[0][0] + B[1] * Q[0][1] + B[2] * Q[0][2], 1, 0, 1);
+  tstFace(pp[1], A[1] + B[0] * Q[1][0] + B[1] * Q[1][1] + B[2] * Q[1][2], 1, 1, 2);
+  tstFace(pp[2], A[2] + B[0] * Q[2][0] + B[1] * Q[2][1] + B[2] * Q[2][2], 1, 2, 3);
+  for (int j = 0; j < 3; j++) {
+    double c2[3];
+    col(R2, j, c2);
+    double e1 = c2[0] * p[0] + c2[1] * p[1] + c2[2] * p[2];
+    double e2 = A[0] * Q[0][j] + A[1] * Q[1][j] + A[2] * Q[2][j] + B[j];
+    tstFace(e1, e2, 2, j, 4 + j);
+  }
+  auto tstEdge = [&](double e1, double e2, double n1, double n2, double n3, int cc) {
+    double s2v = std::fabs(e1) - e2;
+    double l = std::sqrt(n1 * n1 + n2 * n2 + n3 * n3);
+    if (l > 0) {
+      s2v /= l;
+      if (s2v * fudge > s) {
+        s = s2v; normalCol = -1; normalC[0] = n1 / l; normalC[1] = n2 / l; normalC[2] = n3 / l;
+        invertNormal = e1 < 0; code = cc;
+      }
+    }
+  };
+  const double R11 = Rm[0][0], R12 = Rm[0][1], R13 = Rm[0][2], R21 = Rm[1][0], R22 = Rm[1][1], R23 = Rm[1][2],
+               R31 = Rm[2][0], R32 = Rm[2][1], R33 = Rm[2][2];
+  const double Q11 = Q[0][0], Q12 = Q[0][1], Q13 = Q[0][2], Q21 = Q[1][0], Q22 = Q[1][1], Q23 = Q[1][2],
+               Q31 = Q[2][0], Q32 = Q[2][1], Q33 = Q[2][2];
+  tstEdge(pp[2] * R21 - pp[1] * R31, A[1] * Q31 + A[2] * Q21 + B[1] * Q13 + B[2] * Q12, 0, -R31, R21, 7);
+  tstEdge(pp[2] * R22 - pp[1] * R32, A[1] * Q32 + A[2] * Q22 + B[0] * Q13 + B[2] * Q11, 0, -R32, R22, 8);
+  tstEdge(pp[2] * R23 - pp[1] * R33, A[1] * Q33 + A[2] * Q23 + B[0] * Q12 + B[1] * Q11, 0, -R33, R23, 9);
+  tstEdge(pp[0] * R31 - pp[2] * R11, A[0] * Q31 + A[2] * Q11 + B[1] * Q23 + B[2] * Q22, R31, 0, -R11, 10);
+  tstEdge(pp[0] * R32 - pp[2] * R12, A[0] * Q32 + A[2] * Q12 + B[0] * Q23 + B[2] * Q21, R32, 0, -R12, 11);
+  tstEdge(pp[0] * R33 - pp[2] * R13, A[0] * Q33 + A[2] * Q13 + B[0] * Q22 + B[1] * Q21, R33, 0, -R13, 12);
+  tstEdge(pp[1] * R11 - pp[0] * R21, A[0] * Q21 + A[1] * Q11 + B[1] * Q33 + B[2] * Q32, -R21, R11, 0, 13);
+  tstEdge(pp[1] * R12 - pp[0] * R22, A[0] * Q22 + A[1] * Q12 + B[0] * Q33 + B[2] * Q31, -R22, R12, 0, 14);
+  tstEdge(pp[1] * R13 - pp[0] * R23, A[0] * Q23 + A[1] * Q13 + B[0] * Q32 + B[1] * Q31, -R23, R13, 0, 15);
+  if (!code) return 0;
+  if (s > 0.0) return 0;
+  double normal[3];
+  if (normalCol >= 0) {
+    col(normalBox == 1 ? R1 : R2, normalCol, normal);
+  } else {
+    for (int i = 0; i < 3; i++) normal[i] = R1[i * 3] * normalC[0] + R1[i * 3 + 1] * normalC[1] + R1[i * 3 + 2] * normalC[2];
+    double l = std::sqrt(normal[0] * normal[0] + normal[1] * normal[1] + normal[2] * normal[2]);
+    for (int i = 0; i < 3; i++) normal[i] /= l;
+  }
+  if (invertNormal) for (int i = 0; i < 3; i++) normal[i] = -normal[i];
+
+  if (code > 6) {
+    // edge-edge (DARTCollide.cpp:992)
+    double pa[3] = {p1[0], p1[1], p1[2]}, pb[3] = {p2[0], p2[1], p2[2]};
+    for (int j = 0; j < 3; j++) {
+      double c1[3]; col(R1, j, c1);
+      double v = normal[0] * c1[0] + normal[1] * c1[1] + normal[2] * c1[2];
+      double sign = (v > -1e-10) ? 1.0 : -1.0;
+      for (int i = 0; i < 3; i++) pa[i] += sign * A[j] * c1[i];
+    }
+    for (int j = 0; j < 3; j++) {
+      double c2[3]; col(R2, j, c2);
+      double v = normal[0] * c2[0] + normal[1] * c2[1] + normal[2] * c2[2];
+      double sign = (v > -1e-3) ? -1.0 : 1.0;
+      for (int i = 0; i < 3; i++) pb[i] += sign * B[j] * c2[i];
+    }
+    double ua[3], ub[3];
+    col(R1, (code - 7) / 3, ua);
+    col(R2, (code - 7) % 3, ub);
+    // dLineClosestApproach
+    double pd[3] = {pb[0] - pa[0], pb[1] - pa[1], pb[2] - pa[2]};
+    double uaub = ua[0] * ub[0] + ua[1] * ub[1] + ua[2] * ub[2];
+    double q1 = ua[0] * pd[0] + ua[1] * pd[1] + ua[2] * pd[2];
+    double q2 = -(ub[0] * pd[0] + ub[1] * pd[1] + ub[2] * pd[2]);
+    double dd = 1 - uaub * uaub, alpha = 0, beta = 0;
+    if (dd > 0) { dd = 1.0 / dd; alpha = (q1 + uaub * q2) * dd; beta = (uaub * q1 + q2) * dd; }
+    for (int i = 0; i < 3; i++) { pa[i] += ua[i] * alpha; pb[i] += ub[i] * beta; }
+    const double pen = -s;
+    if (pen > clipDepth) return 0;
+    Contact c{};
+    c.shapeA = s1; c.shapeB = s2; c.bodyA = b1; c.bodyB = b2;
+    for (int i = 0; i < 3; i++) { c.point[i] = 0.5 * (pa[i] + pb[i]); c.normal[i] = -normal[i]; }
+    c.depth = pen;
+    c.type = CT_EDGE_EDGE;
+    out.push_back(c);
+    return 1;
+  }
+  // face-something (DARTCollide.cpp:1060)
+  const double *Ra, *Rb, *pa, *pb, *Sa, *Sb;
+  bool flip;
+  if (code <= 3) { Ra = R1; Rb = R2; pa = p1; pb = p2; Sa = A; Sb = B; flip = false; }
+  else { Ra = R2; Rb = R1; pa = p2; pb = p1; Sa = B; Sb = A; flip = true; }
+  double normal2[3], nr[3], anr[3];
+  for (int i = 0; i < 3; i++) normal2[i] = code <= 3 ? normal[i] : -normal[i];
+  for (int i = 0; i < 3; i++) nr[i] = Rb[i] * normal2[0] + Rb[3 + i] * normal2[1] + Rb[6 + i] * normal2[2];
+  for (int i = 0; i < 3; i++) anr[i] = std::fabs(nr[i]);
+  int lanr, a1, a2;
+  if (anr[1] > anr[0]) {
+    if (anr[1] > anr[2]) { a1 = 0; lanr = 1; a2 = 2; } else { a1 = 0; a2 = 1; lanr = 2; }
+  } else {
+    if (anr[0] > anr[2]) { lanr = 0; a1 = 1; a2 = 2; } else { a1 = 0; a2 = 1; lanr = 2; }
+  }
+  double center[3];
+  for (int i = 0; i < 3; i++)
+    center[i] = nr[lanr] < 0 ? pb[i] - pa[i] + Sb[lanr] * Rb[i * 3 + lanr] : pb[i] - pa[i] - Sb[lanr] * Rb[i * 3 + lanr];
+  int codeN = code <= 3 ? code - 1 : code - 4;
+  int code1, code2;
+  if (codeN == 0) { code1 = 1; code2 = 2; } else if (codeN == 1) { code1 = 0; code2 = 2; } else { code1 = 0; code2 = 1; }
+  auto inner = [](const double* R, int ca, const double* Rb2, int cb) {
+    return R[ca] * Rb2[cb] + R[3 + ca] * Rb2[3 + cb] + R[6 + ca] * Rb2[6 + cb];
+  };
+  double c1 = center[0] * Ra[code1] + center[1] * Ra[3 + code1] + center[2] * Ra[6 + code1];
+  double c2 = center[0] * Ra[code2] + center[1] * Ra[3 + code2] + center[2] * Ra[6 + code2];
+  double m11 = inner(Ra, code1, Rb, a1), m12 = inner(Ra, code1, Rb, a2);
+  double m21 = inner(Ra, code2, Rb, a1), m22 = inner(Ra, code2, Rb, a2);
+  double quad[8];
+  {
+    double k1 = m11 * Sb[a1], k2 = m21 * Sb[a1], k3 = m12 * Sb[a2], k4 = m22 * Sb[a2];
+    quad[0] = c1 - k1 - k3; quad[1] = c2 - k2 - k4;
+    quad[2] = c1 - k1 + k3; quad[3] = c2 - k2 + k4;
+    quad[4] = c1 + k1 + k3; quad[5] = c2 + k2 + k4;
+    quad[6] = c1 + k1 - k3; quad[7] = c2 + k2 - k4;
+  }
+  double rect[2] = {Sa[code1], Sa[code2]};
+  // intersectRectQuad (DARTCollide.cpp:513)
+  double ret[16], buffer[16];
+  int nq = 4, nrr = 0;
+  double* q = quad;
+  double* r = ret;
+  for (int dir = 0; dir <= 1; dir++) {
+    for (int sign = -1; sign <= 1; sign += 2) {
+      double* pq = q;
+      double* pr = r;
+      nrr = 0;
+      bool done = false;
+      for (int i = nq; i > 0; i--) {
+        if (sign * pq[dir] < rect[dir]) {
+          pr[0] = pq[0]; pr[1] = pq[1]; pr += 2; nrr++;
+          if (nrr & 8) { q = r; done = true; break; }
+        }
+        double* nextq = (i > 1) ? pq + 2 : q;
+        if ((sign * pq[dir] < rect[dir]) ^ (sign * nextq[dir] < rect[dir])) {
+          pr[1 - dir] = pq[1 - dir] + (nextq[1 - dir] - pq[1 - dir]) / (nextq[dir] - pq[dir]) * (sign * rect[dir] - pq[dir]);
+          pr[dir] = sign * rect[dir];
+          pr += 2; nrr++;
+          if (nrr & 8) { q = r; done = true; break; }
+        }
+        pq += 2;
+      }
+      if (done) goto clipped;
+      q = r;
+      r = (q == ret) ? buffer : ret;
+      nq = nrr;
+    }
+  }
+clipped:
+  if (q != ret) for (int i = 0; i < nrr * 2; i++) ret[i] = q[i];
+  int nPts = nrr;
+  if (nPts < 1) return 0;
+  double point[24], dep[8];
+  double det1 = 1.0 / (m11 * m22 - m12 * m21);
+  m11 *= det1; m12 *= det1; m21 *= det1; m22 *= det1;
+  int cnum = 0;
+  for (int j = 0; j < nPts; j++) {
+    double k1 = m22 * (ret[j * 2] - c1) - m12 * (ret[j * 2 + 1] - c2);
+    double k2 = -m21 * (ret[j * 2] - c1) + m11 * (ret[j * 2 + 1] - c2);
+    for (int i = 0; i < 3; i++) point[cnum * 3 + i] = center[i] + k1 * Rb[i * 3 + a1] + k2 * Rb[i * 3 + a2];
+    dep[cnum] = Sa[codeN] - (normal2[0] * point[cnum * 3] + normal2[1] * point[cnum * 3 + 1] + normal2[2] * point[cnum * 3 + 2]);
+    if (dep[cnum] >= 0) { ret[cnum * 2] = ret[j * 2]; ret[cnum * 2 + 1] = ret[j * 2 + 1]; cnum++; }
+  }
+  if (cnum < 1) return 0;
+  for (int j = 0; j < cnum; j++) {
+    Contact c{};
+    c.shapeA = s1; c.shapeB = s2; c.bodyA = b1; c.bodyB = b2;
+    for (int i = 0; i < 3; i++) { c.point[i] = point[j * 3 + i] + pa[i]; c.normal[i] = -normal[i]; }
+    c.depth = dep[j];
+    double xx = ret[j * 2], yy = ret[j * 2 + 1];
+    bool onEdgeX = std::fabs(xx) == rect[0];
+    bool onEdgeY = std::fabs(yy) == rect[1];
+    if (onEdgeX && onEdgeY) {
+      if (flip) { c.type = CT_FACE_VERTEX; for (int i = 0; i < 3; i++) c.point[i] += c.normal[i] * c.depth; }
+      else { c.type = CT_VERTEX_FACE; for (int i = 0; i < 3; i++) c.point[i] -= c.normal[i] * c.depth; }
+    } else if (!onEdgeX && !onEdgeY) {
+      c.type = flip ? CT_VERTEX_FACE : CT_FACE_VERTEX;
+    } else {
+      c.type = CT_EDGE_EDGE;
+    }
+    out.push_back(c);
+  }
+  return cnum;
 }
 
+}  // namespace oracle
+
+// Raw box-box entry for known-answer fixtures (collideBoxBox signature:
+// full sizes + world transforms [R|p] 3x4 row-major).  Output per contact:
+// point3, normal3, depth, type.
+extern "C" int oracle_box_box(const double* size1, const double* T1, const double* size2, const double* T2,
+                              double* out) {
+  double A[3] = {0.5 * size1[0], 0.5 * size1[1], 0.5 * size1[2]};
+  double B[3] = {0.5 * size2[0], 0.5 * size2[1], 0.5 * size2[2]};
+  double R1[9], R2[9], p1[3], p2[3];
+  for (int r = 0; r < 3; r++) {
+    for (int c = 0; c < 3; c++) { R1[r * 3 + c] = T1[r * 4 + c]; R2[r * 3 + c] = T2[r * 4 + c]; }
+    p1[r] = T1[r * 4 + 3];
+    p2[r] = T2[r * 4 + 3];
+  }
+  std::vector<oracle::Contact> cs;
+  oracle::boxBox(p1, R1, A, p2, R2, B, 1e12, cs, 0, 1, 0, 1);
+  for (size_t k = 0; k < cs.size(); k++) {
+    for (int i = 0; i < 3; i++) { out[8 * k + i] = cs[k].point[i]; out[8 * k + 3 + i] = cs[k].normal[i]; }
+    out[8 * k + 6] = cs[k].depth;
+    out[8 * k + 7] = cs[k].type;
+  }
+  return (int)cs.size();
+}
+
+namespace oracle {
+
+void collide(const World& w, const Kin<double>& k, std::vector<Contact>& out) {
+  out.clear();
+  const int ns = (int)w.shapes.size();
+  for (int i = 0; i + 1 < ns; i++) {
+    for (int j = i + 1; j < ns; j++) {
+      const Shape& S1 = w.shapes[i];
+      const Shape& S2 = w.shapes[j];
+      const Body& B1 = w.bodies[S1.body];
+      const Body& B2 = w.bodies[S2.body];
+      // BodyNodeCollisionFilter (CollisionFilter.cpp:105)
+      if (S1.body == S2.body) continue;
+      if (!B1.mobile && !B2.mobile) continue;
+      if (B1.skel == B2.skel) continue;  // self-collision check disabled by default
+      Iso<double> T1 = compose(k.Tw[S1.body], S1.T);
+      Iso<double> T2 = compose(k.Tw[S2.body], S2.T);
+      std::vector<Contact> pair;
+      if (S1.type == NIMBLE_SHAPE_BOX && S2.type == NIMBLE_SHAPE_BOX) {
+        double A[3] = {0.5 * S1.size[0], 0.5 * S1.size[1], 0.5 * S1.size[2]};
+        double Bh[3] = {0.5 * S2.size[0], 0.5 * S2.size[1], 0.5 * S2.size[2]};
+        boxBox(T1.p.x, T1.R.m, A, T2.p.x, T2.R.m, Bh, w.clipDepth, pair, i, j, S1.body, S2.body);
+      } else {
+        std::fprintf(stderr, "oracle: shape pair (%d,%d) not supported\n", S1.type, S2.type);
+        std::abort();
+      }
+      // postProcess (DARTCollisionDetector.cpp:357): drop repeated points
+      for (const Contact& c : pair) {
+        bool close = false;
+        for (const Contact& t : out) {
+          double dd = 0;
+          for (int m = 0; m < 3; m++) dd += (c.point[m] - t.point[m]) * (c.point[m] - t.point[m]);
+          if (std::sqrt(dd) < 3.0e-12) { close = true; break; }
+        }
+        if (!close) out.push_back(c);
+      }
+    }
+  }
+}
+
+//------------------------------------------------------------------------------
+// Constraint rows.  One row = (contact, direction); generalized force column
+// J^T e = sum over reactive bodies of +-S_w . [p x d; d] (world frame), the
+// quantity DifferentiableContactConstraint::getConstraintForces (:231)
+// computes and the impulse test of ContactConstraint::applyUnitImpulse
+// (:525) realises.
+struct Row {
+  int contact, dir;  // dir 0 = normal, 1,2 = tangents
+  double d[3];       // world direction for body A (body B gets -d)
+};
+
+static void tangentBasis(const double* n, double* t1, double* t2) {
+  // ContactConstraint::getTangentBasisMatrixODE (:705), first dir = UnitZ
+  auto cr = [](const double* a, const double* b, double* o) {
+    o[0] = a[1] * b[2] - a[2] * b[1]; o[1] = a[2] * b[0] - a[0] * b[2]; o[2] = a[0] * b[1] - a[1] * b[0];
+  };
+  const double ez[3] = {0, 0, 1}, ex[3] = {1, 0, 0}, ey[3] = {0, 1, 0};
+  double t[3];
+  cr(ez, n, t);
+  if (t[0] * t[0] + t[1] * t[1] + t[2] * t[2] < 1e-12) {
+    cr(ex, n, t);
+    if (t[0] * t[0] + t[1] * t[1] + t[2] * t[2] < 1e-12) {
+      cr(ey, n, t);
+      if (t[0] * t[0] + t[1] * t[1] + t[2] * t[2] < 1e-12) cr(ez, n, t);
+    }
+  }
+  double l = std::sqrt(t[0] * t[0] + t[1] * t[1] + t[2] * t[2]);
+  for (int i = 0; i < 3; i++) t1[i] = t[i] / l;
+  cr(n, t1, t2);
+}
+
+static bool reactive(const World& w, int b) {
+  if (!w.bodies[b].mobile) return false;
+  for (int a = b; a >= 0; a = w.bodies[a].parent)
+    if (w.bodies[a].ndof > 0) return true;
+  return false;
+}
+
+static void rowForce(const World& w, const Kin<double>& k, const Contact& c, const double* d, double* col) {
+  const int n = w.n;
+  for (int i = 0; i < n; i++) col[i] = 0.0;
+  for (int side = 0; side < 2; side++) {
+    const int body = side == 0 ? c.bodyA : c.bodyB;
+    if (!reactive(w, body)) continue;
+    const double sgn = side == 0 ? 1.0 : -1.0;
+    double wr[6];
+    wr[0] = c.point[1] * d[2] - c.point[2] * d[1];
+    wr[1] = c.point[2] * d[0] - c.point[0] * d[2];
+    wr[2] = c.point[0] * d[1] - c.point[1] * d[0];
+    wr[3] = d[0]; wr[4] = d[1]; wr[5] = d[2];
+    for (int dof = 0; dof < n; dof++) {
+      const int b = w.dofBody[dof];
+      if (!w.isAncestorOrSelf(b, body)) continue;
+      const Body& B = w.bodies[b];
+      const int kk = dof - B.dof0;
+      // world screw axis = Ad_{Tw_b} S_local
+      V6<double> sl;
+      for (int i = 0; i < 6; i++) sl[i] = k.Sj[b](i, kk);
+      V6<double> sw = AdT(k.Tw[b], sl);
+      double s = 0;
+      for (int i = 0; i < 6; i++) s += sw[i] * wr[i];
+      col[dof] += sgn * s;
+    }
+  }
+}
+
+//------------------------------------------------------------------------------
+// LCPUtils::isLCPSolutionValid (LCPUtils.cpp:14)
+static bool lcpValid(const std::vector<double>& A, const std::vector<double>& x, const std::vector<double>& b,
+                     const std::vector<double>& hi, const std::vector<double>& lo, const std::vector<int>& fi,
+                     bool ignoreFriction) {
+  const int m = (int)x.size();
+  for (int i = 0; i < m; i++) {
+    double v = -b[i];
+    for (int j = 0; j < m; j++) v += A[i * m + j] * x[j];
+    double up = hi[i], low = lo[i];
+    if (fi[i] != -1) {
+      if (ignoreFriction) { if (x[i] != 0) return false; continue; }
+      up *= x[fi[i]];
+      low *= x[fi[i]];
+    }
+    const double tol = 1e-5;
+    if (std::fabs(low) < tol && std::fabs(up) < tol && std::fabs(x[i]) < tol) {
+    } else if (std::fabs(x[i] - low) < tol) {
+      if (v < -tol) return false;
+    } else if (std::fabs(x[i] - up) < tol) {
+      if (v > tol) return false;
+    } else if (x[i] > low && x[i] < up) {
+      if (std::fabs(v) > tol) return false;
+    } else {
+      return false;
+    }
+  }
+  return true;
+}
+
+// LCPUtils::guessSolution (LCPUtils.cpp:69)
+static std::vector<double> guessSolution(const std::vector<double>& A, const std::vector<double>& b,
+                                         const std::vector<int>& fi) {
+  const int m = (int)b.size();
+  std::vector<int> cl;
+  for (int i = 0; i < m; i++) {
+    if (fi[i] == -1) { if (b[i] > 0) cl.push_back(i); }
+    else cl.push_back(i);
+  }
+  std::vector<double> x(m, 0.0);
+  const int k = (int)cl.size();
+  if (k == 0) return x;
+  std::vector<double> Ar(k * k), br(k), xr(k);
+  for (int r = 0; r < k; r++) {
+    br[r] = b[cl[r]];
+    for (int c = 0; c < k; c++) Ar[r * k + c] = A[cl[r] * m + cl[c]];
+  }
+  codSolve(Ar.data(), k, k, br.data(), xr.data());
+  for (int i = 0; i < k; i++) x[cl[i]] = xr[i];
+  return x;
+}
+
+// ---- ConstrainedGroupGradientMatrices (the per-step "gradient matrices") ----
+struct GradMats {
+  const World* w;
+  int m = 0;  // constraint dim
+  std::vector<double> X, hi, lo, B, aColNorms, A;
+  std::vector<int> fi;
+  double cfm = 0;
+  bool ignoreFriction = false;
+  const std::vector<double>* allCols;      // n x m   (col j = J^T e_j)
+  const std::vector<double>* massedCols;   // n x m   (col j = Minv J^T e_j)
+  const std::vector<double>* Minv;         // n x n
+  std::vector<double> restitution;         // per row (0 without bounce)
+  std::vector<double> penVel;
+  // outputs
+  std::vector<int> mapping, clampIdx, ubIdx;
+  int nc = 0, nu = 0;
+  std::vector<double> fc, relVel, E, clampA;
+  bool standardized = false;
+
+  void construct() {
+    const int n = w->n;
+    mapping.assign(m, CM_NOT_CLAMPING);
+    clampIdx.assign(m, -1);
+    ubIdx.assign(m, -1);
+    nc = nu = 0;
+    const double TH = 1e-6;
+    for (int j = 0; j < m; j++) {
+      if (aColNorms[j] < 1e-9) { mapping[j] = CM_NOT_CLAMPING; continue; }
+      const double f = X[j];
+      double up = hi[j], low = lo[j];
+      const int fp = fi[j];
+      if (fp != -1) { up *= X[fp]; low *= X[fp]; }
+      if (std::fabs(f) < TH) {
+        if (fp != -1) {
+          if (std::fabs(X[fp]) < TH) mapping[j] = CM_NOT_CLAMPING;
+          else if (ignoreFriction) mapping[j] = CM_NOT_CLAMPING;
+          else { mapping[j] = CM_CLAMPING; clampIdx[j] = nc++; }
+        } else {
+          mapping[j] = CM_NOT_CLAMPING;
+        }
+        continue;
+      }
+      const double tie = 1e-5;
+      if ((f > low + tie && f < up - tie) || (low - f > 1e-2 || f - up > 1e-2)) {
+        mapping[j] = CM_CLAMPING; clampIdx[j] = nc++;
+      } else if (fp != -1 && std::fabs(X[fp]) > 1e-9 && aColNorms[fp] > 1e-9 &&
+                 (fp > j || mapping[fp] == CM_CLAMPING)) {
+        mapping[j] = fp; ubIdx[j] = nu++;
+      } else {
+        mapping[j] = CM_NOT_CLAMPING;
+      }
+    }
+    fc.assign(nc, 0.0);
+    relVel.assign(nc, 0.0);
+    E.assign(nu * nc, 0.0);
+    clampA.assign(nc * nc, 0.0);
+    for (int j = 0; j < m; j++) {
+      if (mapping[j] == CM_CLAMPING) { fc[clampIdx[j]] = X[j]; relVel[clampIdx[j]] = B[j]; }
+    }
+    for (int j = 0; j < m; j++) {
+      if (mapping[j] >= 0) {
+        const int fp = mapping[j];
+        const double up = X[fp] * hi[j], low = X[fp] * lo[j];
+        E[ubIdx[j] * nc + clampIdx[fp]] = std::fabs(X[j] - up) < std::fabs(X[j] - low) ? hi[j] : lo[j];
+      }
+    }
+    for (int r = 0; r < m; r++)
+      if (mapping[r] == CM_CLAMPING)
+        for (int c = 0; c < m; c++)
+          if (mapping[c] == CM_CLAMPING) clampA[clampIdx[r] * nc + clampIdx[c]] = A[r * m + c];
+    (void)n;
+    standardize();
+  }
+  // opportunisticallyStandardizeResults (ConstrainedGroupGradientMatrices.cpp:218)
+  bool standardize() {
+    standardized = true;
+    if (m == 0) return true;
+    const int n = w->n;
+    if (nc == 0) {
+      std::vector<double> zero(m, 0.0);
+      if (lcpValid(A, zero, B, hi, lo, fi, ignoreFriction)) { X = zero; return true; }
+      standardized = false;
+      return false;
+    }
+    std::vector<double> Q(nc * nc, 0.0);
+    if (nu == 0) {
+      Q = clampA;
+    } else {
+      // Q = A_c^T Minv (A_c + A_ub E) + cfm I
+      std::vector<double> AcubE(n * nc, 0.0);
+      for (int j = 0; j < m; j++) {
+        if (mapping[j] == CM_CLAMPING)
+          for (int i = 0; i < n; i++) AcubE[i * nc + clampIdx[j]] += (*allCols)[i * m + j];
+      }
+      for (int j = 0; j < m; j++)
+        if (mapping[j] >= 0)
+          for (int c = 0; c < nc; c++) {
+            const double e = E[ubIdx[j] * nc + c];
+            if (e != 0) for (int i = 0; i < n; i++) AcubE[i * nc + c] += (*allCols)[i * m + j] * e;
+          }
+      std::vector<double> MA(n * nc, 0.0);
+      for (int i = 0; i < n; i++)
+        for (int c = 0; c < nc; c++) {
+          double s = 0;
+          for (int t = 0; t < n; t++) s += (*Minv)[i * n + t] * AcubE[t * nc + c];
+          MA[i * nc + c] = s;
+        }
+      for (int j = 0; j < m; j++)
+        if (mapping[j] == CM_CLAMPING)
+          for (int c = 0; c < nc; c++) {
+            double s = 0;
+            for (int i = 0; i < n; i++) s += (*allCols)[i * m + j] * MA[i * nc + c];
+            Q[clampIdx[j] * nc + c] = s;
+          }
+      for (int c = 0; c < nc; c++) Q[c * nc + c] += cfm;
+    }
+    std::vector<double> f(nc);
+    codSolve(Q.data(), nc, nc, relVel.data(), f.data());
+    const std::vector<double> orig = fc;
+    bool anyNewlyNot = false;
+    std::vector<double> nx(m, 0.0);
+    for (int i = 0; i < m; i++) {
+      if (clampIdx[i] != -1) {
+        nx[i] = f[clampIdx[i]];
+        if (std::fabs(f[clampIdx[i]]) < 1e-6 && std::fabs(X[i]) > 1e-6 && fi[i] == -1) anyNewlyNot = true;
+      }
+      if (ubIdx[i] != -1) {
+        const int fp = fi[i];
+        const double om = orig[clampIdx[fp]] / X[i];
+        const double clean = std::fabs(om - hi[i]) < std::fabs(om - lo[i]) ? hi[i] : lo[i];
+        nx[i] = f[clampIdx[fp]] * clean;
+      }
+    }
+    if (lcpValid(A, nx, B, hi, lo, fi, ignoreFriction)) {
+      X = nx;
+      fc = f;
+      if (anyNewlyNot) construct();
+      return true;
+    }
+    standardized = false;
+    return false;
+  }
+};
+
+//------------------------------------------------------------------------------
 void solveContacts(const World& w, const Kin<double>& k, const double* q, const double* v, const double* tau,
-                   std::vector<double>& v1, const std::vector<Contact>& contacts,
+                   std::vector<double>& v1, const std::vector<Contact>& contactsIn,
                    std::vector<double>& lcpCache, Snapshot& snap) {
-  (void)w; (void)k; (void)q; (void)v; (void)tau; (void)v1; (void)lcpCache;
+  (void)q; (void)v; (void)tau;
+  const int n = w.n;
   snap.numRows = 0;
   snap.numClamping = 0;
   snap.numUpperBound = 0;
-  if (!contacts.empty()) { std::fprintf(stderr, "oracle: contacts not implemented\n"); std::abort(); }
+  snap.contacts.clear();
+  // ConstraintSolver::updateConstraints (ConstraintSolver.cpp:520)
+  std::vector<Contact> contacts;
+  for (const Contact& c : contactsIn) {
+    if (c.normal[0] * c.normal[0] + c.normal[1] * c.normal[1] + c.normal[2] * c.normal[2] < 1e-12) continue;
+    if (c.depth < 0.0) continue;
+    if (c.depth > w.clipDepth) continue;
+    if (!reactive(w, c.bodyA) && !reactive(w, c.bodyB)) continue;  // ContactConstraint::update
+    contacts.push_back(c);
+  }
+  snap.contacts = contacts;
+  if (contacts.empty()) return;
+  if ((int)contacts.size() > NIMBLE_MAX_CONTACTS) {
+    std::fprintf(stderr, "oracle: %zu contacts exceed NIMBLE_MAX_CONTACTS\n", contacts.size());
+    std::abort();
+  }
+  // rows (ContactConstraint: 3 rows with friction, else 1)
+  std::vector<Row> rows;
+  std::vector<double> lo, hi, bounce, rest, pen;
+  std::vector<int> fi;
+  for (int ci = 0; ci < (int)contacts.size(); ci++) {
+    const Contact& c = contacts[ci];
+    const double mu = std::min(w.bodies[c.bodyA].friction, w.bodies[c.bodyB].friction);
+    const double restC = w.bodies[c.bodyA].restitution * w.bodies[c.bodyB].restitution;
+    const bool frictionOn = mu > 1e-3;
+    const int base = (int)rows.size();
+    Row r0{ci, 0, {c.normal[0], c.normal[1], c.normal[2]}};
+    rows.push_back(r0);
+    lo.push_back(0.0); hi.push_back(kInf); fi.push_back(-1);
+    if (frictionOn) {
+      double t1[3], t2[3];
+      tangentBasis(c.normal, t1, t2);
+      rows.push_back(Row{ci, 1, {t1[0], t1[1], t1[2]}});
+      rows.push_back(Row{ci, 2, {t2[0], t2[1], t2[2]}});
+      lo.push_back(-mu); hi.push_back(mu); fi.push_back(base);
+      lo.push_back(-mu); hi.push_back(mu); fi.push_back(base);
+    }
+    // restitution is only "on" above DART_RESTITUTION_COEFF_THRESHOLD
+    rest.push_back(restC > 1e-3 ? restC : 0.0);
+    if (frictionOn) { rest.push_back(0); rest.push_back(0); }
+  }
+  const int m = (int)rows.size();
+  snap.numRows = m;
+  std::vector<double> allCols(n * m), massed(n * m);
+  // Minv via the mass matrix
+  std::vector<double> M(n * n), Minv(n * n);
+  w.massMatrix(k, M.data());
+  invertSmall(M.data(), Minv.data(), n);
+  for (int j = 0; j < m; j++) {
+    const Contact& c = contacts[rows[j].contact];
+    std::vector<double> col(n);
+    rowForce(w, k, c, rows[j].d, col.data());
+    for (int i = 0; i < n; i++) allCols[i * m + j] = col[i];
+  }
+  for (int i = 0; i < n; i++)
+    for (int j = 0; j < m; j++) {
+      double s = 0;
+      for (int t = 0; t < n; t++) s += Minv[i * n + t] * allCols[t * m + j];
+      massed[i * m + j] = s;
+    }
+  // A = J Minv J^T ; b = -J v1 (+ bouncing / penetration correction)
+  std::vector<double> A(m * m), b(m);
+  for (int r = 0; r < m; r++)
+    for (int c = 0; c < m; c++) {
+      double s = 0;
+      for (int i = 0; i < n; i++) s += allCols[i * m + r] * massed[i * m + c];
+      A[r * m + c] = s;
+    }
+  for (int r = 0; r < m; r++)
+    for (int c = r + 1; c < m; c++) A[c * m + r] = A[r * m + c];  // upper triangle copied down
+  pen.assign(m, 0.0);
+  for (int r = 0; r < m; r++) {
+    double s = 0;
+    for (int i = 0; i < n; i++) s += allCols[i * m + r] * v1[i];
+    b[r] = -s;
+  }
+  for (int r = 0; r < m; r++) {
+    if (rows[r].dir != 0) continue;
+    const Contact& c = contacts[rows[r].contact];
+    double bv = c.depth - 0.0;  // mErrorAllowance = 0
+    if (bv < 0.0) bv = 0.0;
+    else { bv *= 0.01 / w.dt; if (bv > 1e-3) bv = 1e-3; }
+    if (!w.penetrationCorrection) bv = 0;
+    pen[r] = bv;
+    if (rest[r] > 0) {
+      const double rv = b[r] * rest[r];
+      if (rv > 1e-1 && rv > bv) { bv = rv > 1e2 ? 1e2 : rv; pen[r] = 0.0; }
+      else rest[r] = 0.0;  // getCoefficientOfRestitution returns 0 unless bounced
+    }
+    b[r] += bv;
+  }
+  std::vector<double> aColNorms(m);
+  for (int j = 0; j < m; j++) {
+    double s = 0;
+    for (int i = 0; i < m; i++) s += A[i * m + j] * A[i * m + j];
+    aColNorms[j] = s;
+  }
+  // cached LCP solution (BoxedLcpConstraintSolver::mX)
+  std::vector<double> X;
+  if ((int)lcpCache.size() != m) X = guessSolution(A, b, fi);
+  else X = lcpCache;
+
+  GradMats gm;
+  gm.w = &w; gm.m = m; gm.hi = hi; gm.lo = lo; gm.fi = fi; gm.B = b; gm.aColNorms = aColNorms; gm.A = A;
+  gm.allCols = &allCols; gm.massedCols = &massed; gm.Minv = &Minv; gm.restitution = rest; gm.penVel = pen;
+  gm.X = X; gm.cfm = 0.0; gm.ignoreFriction = false;
+  gm.construct();
+  bool success = gm.standardized;
+  bool shortCircuit = success;
+  if (success) X = gm.X;
+  std::vector<double> Acfm = A;
+  double cfm = 0.0;
+  bool ignoredFriction = false;
+  if (!success) {
+    // Dantzig on the reduced (duplicate-merged) problem.  LCPUtils::reduce
+    // merges only near-identical columns, which the box contacts on this path
+    // never produce; a merge is detected and reported.
+    for (int a = 0; a < m; a++)
+      for (int c = a + 1; c < m; c++) {
+        double dd = 0;
+        for (int i = 0; i < m; i++) dd += (A[i * m + a] - A[i * m + c]) * (A[i * m + a] - A[i * m + c]);
+        if (dd < 1e-4 && std::fabs(b[a] - b[c]) < 1e-4 && fi[a] == fi[c] && hi[a] == hi[c] && lo[a] == lo[c]) {
+          std::fprintf(stderr, "oracle: duplicate LCP columns (LCPUtils::reduce) not supported\n");
+          std::abort();
+        }
+      }
+    std::vector<double> Ad = A, xd(m, 0.0), bd = b, lod = lo, hid = hi;
+    std::vector<int> fid = fi;
+    success = dantzigSolveLCP(m, Ad.data(), xd.data(), bd.data(), nullptr, 0, lod.data(), hid.data(), fid.data(), true);
+    if (success) {
+      X = xd;
+      if (!lcpValid(A, X, b, hi, lo, fi, false)) success = false;
+    }
+  }
+  for (double xv : X) if (std::isnan(xv)) { success = false; std::fill(X.begin(), X.end(), 0.0); break; }
+  if (!success) {
+    cfm = w.fallbackCfm;
+    for (int i = 0; i < m; i++) Acfm[i * m + i] += cfm;
+  }
+  if (!success) {
+    std::vector<double> Ad = Acfm, xd = lcpCache.size() == (size_t)m ? lcpCache : std::vector<double>(m, 0.0);
+    // mXBackup is the (possibly re-initialised) cached solution at build time
+    xd = ((int)lcpCache.size() != m) ? guessSolution(A, b, fi) : lcpCache;
+    std::vector<double> bd = b, lod = lo, hid = hi;
+    std::vector<int> fid = fi;
+    success = pgsSolveLCP(m, Ad.data(), xd.data(), bd.data(), lod.data(), hid.data(), fid.data());
+    if (success) {
+      X = xd;
+      if (!lcpValid(Acfm, X, b, hi, lo, fi, false)) success = false;
+    }
+  }
+  if (!success) {
+    ignoredFriction = true;
+    // LCPUtils::removeFriction + PGS on the normal rows only
+    std::vector<int> keep;
+    for (int i = 0; i < m; i++) if (fi[i] == -1) keep.push_back(i);
+    const int k2 = (int)keep.size();
+    std::vector<double> Ar(k2 * k2), br(k2), xr(k2, 0.0), lor(k2), hir(k2);
+    std::vector<int> fir(k2, -1);
+    for (int r = 0; r < k2; r++) {
+      br[r] = b[keep[r]]; lor[r] = lo[keep[r]]; hir[r] = hi[keep[r]];
+      for (int c = 0; c < k2; c++) Ar[r * k2 + c] = Acfm[keep[r] * m + keep[c]];
+    }
+    pgsSolveLCP(k2, Ar.data(), xr.data(), br.data(), lor.data(), hir.data(), fir.data());
+    std::fill(X.begin(), X.end(), 0.0);
+    for (int r = 0; r < k2; r++) X[keep[r]] = xr[r];
+  }
+  for (double xv : X) if (std::isnan(xv)) { std::fill(X.begin(), X.end(), 0.0); break; }
+  if (!shortCircuit) {
+    gm.X = X; gm.A = Acfm; gm.cfm = cfm; gm.ignoreFriction = ignoredFriction;
+    gm.construct();
+    if (gm.standardized) X = gm.X;
+  }
+  lcpCache = X;
+  // applyConstraintImpulses + computeImpulseForwardDynamics: v1 += Minv J^T x
+  for (int i = 0; i < n; i++) {
+    double s = 0;
+    for (int j = 0; j < m; j++) s += massed[i * m + j] * X[j];
+    v1[i] += s;
+  }
+  // snapshot for the backward pass
+  snap.Aall = allCols;
+  snap.rowContact.clear(); snap.rowDirIdx.clear(); snap.rowDir.clear();
+  for (const Row& r : rows) {
+    snap.rowContact.push_back(r.contact); snap.rowDirIdx.push_back(r.dir);
+    for (int i = 0; i < 3; i++) snap.rowDir.push_back(r.d[i]);
+  }
+  snap.massedImpulse = massed;
+  snap.lcpA = gm.A; snap.lcpB = b; snap.lcpLo = lo; snap.lcpHi = hi; snap.lcpX = gm.X; snap.lcpFIndex = fi;
+  snap.aColNorms = aColNorms;
+  snap.mapping = gm.mapping; snap.clampingIndex = gm.clampIdx; snap.upperBoundIndex = gm.ubIdx;
+  snap.numClamping = gm.nc; snap.numUpperBound = gm.nu;
+  snap.fc = gm.fc;
+  snap.E = gm.E;
+  snap.cfm = gm.cfm;
+  snap.ignoredFriction = gm.ignoreFriction;
+  snap.shortCircuit = shortCircuit;
+  snap.bounceDiag.assign(gm.nc, 1.0);
+  snap.penetrationVel.assign(gm.nc, 0.0);
+  for (int j = 0; j < m; j++)
+    if (gm.mapping[j] == CM_CLAMPING) {
+      snap.bounceDiag[gm.clampIdx[j]] = 1.0 + rest[j];
+      snap.penetrationVel[gm.clampIdx[j]] = pen[j];
+    }
 }
 
-void buildClampingMatrices(const World& w, const Snapshot& snap, std::vector<double>& Ac,
-                           std::vector<double>& Aub, std::vector<double>& AcubE) {
-  (void)w; (void)snap; Ac.clear(); Aub.clear(); AcubE.clear();
+//------------------------------------------------------------------------------
+void buildClampingMatrices(const World& w, const Snapshot& snap, std::vector<double>& Ac, std::vector<double>& Aub,
+                           std::vector<double>& AcubE) {
+  const int n = w.n, m = snap.numRows, nc = snap.numClamping, nu = snap.numUpperBound;
+  Ac.assign(n * nc, 0.0);
+  Aub.assign(n * nu, 0.0);
+  AcubE.assign(n * nc, 0.0);
+  for (int j = 0; j < m; j++) {
+    if (snap.mapping[j] == CM_CLAMPING)
+      for (int i = 0; i < n; i++) Ac[i * nc + snap.clampingIndex[j]] = snap.Aall[i * m + j];
+    else if (snap.mapping[j] >= 0)
+      for (int i = 0; i < n; i++) Aub[i * nu + snap.upperBoundIndex[j]] = snap.Aall[i * m + j];
+  }
+  for (int i = 0; i < n; i++)
+    for (int c = 0; c < nc; c++) {
+      double s = Ac[i * nc + c];
+      for (int u = 0; u < nu; u++) s += Aub[i * nu + u] * snap.E[u * nc + c];
+      AcubE[i * nc + c] = s;
+    }
 }
 
-void constrainedJacobians(const World&, const Kin<double>&, const Snapshot&, const std::vector<double>&,
-                          const std::vector<double>&, const std::vector<double>&, const std::vector<double>&,
-                          const std::vector<double>&, const std::vector<double>&, const std::vector<double>&,
-                          const std::vector<double>&, const std::vector<double>&, std::vector<double>&,
-                          std::vector<double>&, std::vector<double>&) {
-  std::abort();
+// Position-dependent constraint terms (dA_c f_c, dF_c wrt position) --
+// oracle_contact_grad.cpp.
+void positionConstraintTerms(const World& w, const Snapshot& snap, const std::vector<double>& Minv,
+                             const std::vector<double>& C, const std::vector<double>& dCq,
+                             const std::vector<double>& Ac, const std::vector<double>& Aub,
+                             const std::vector<double>& AcubE, const std::vector<double>& Qpinv,
+                             std::vector<double>& dFcPos, std::vector<double>& dAcf);
+
+void constrainedJacobians(const World& w, const Kin<double>& k, const Snapshot& snap, const std::vector<double>& M,
+                          const std::vector<double>& Minv, const std::vector<double>& C,
+                          const std::vector<double>& dCq, const std::vector<double>& dCv,
+                          const std::vector<double>& dM, const std::vector<double>& Ac,
+                          const std::vector<double>& Aub, const std::vector<double>& AcubE,
+                          std::vector<double>& posVel, std::vector<double>& velVel, std::vector<double>& forceVel) {
+  (void)k; (void)M; (void)Aub;
+  const int n = w.n, nc = snap.numClamping;
+  const double dt = w.dt;
+  // Q = A_c^T Minv A_c_ub_E + cfm I (BackpropSnapshot.cpp:2747)
+  std::vector<double> MA(n * nc), Q(nc * nc);
+  for (int i = 0; i < n; i++)
+    for (int c = 0; c < nc; c++) {
+      double s = 0;
+      for (int t = 0; t < n; t++) s += Minv[i * n + t] * AcubE[t * nc + c];
+      MA[i * nc + c] = s;
+    }
+  for (int r = 0; r < nc; r++)
+    for (int c = 0; c < nc; c++) {
+      double s = 0;
+      for (int i = 0; i < n; i++) s += Ac[i * nc + r] * MA[i * nc + c];
+      Q[r * nc + c] = s + (r == c ? snap.cfm : 0.0);
+    }
+  auto Qsolve = [&](const std::vector<double>& rhs /* nc x cols */, int cols, std::vector<double>& out) {
+    out.assign(nc * cols, 0.0);
+    std::vector<double> bb(nc), xx(nc);
+    for (int c = 0; c < cols; c++) {
+      for (int r = 0; r < nc; r++) bb[r] = rhs[r * cols + c];
+      codSolve(Q.data(), nc, nc, bb.data(), xx.data());
+      for (int r = 0; r < nc; r++) out[r * cols + c] = xx[r];
+    }
+  };
+  // dB wrt velocity (getJacobianOfLCPOffsetClampingSubset, VELOCITY):
+  //   -bounce .* A_c^T (I - dt Minv (dC_v + D + dt K))
+  std::vector<double> inner(n * n), dBv(nc * n), dBf(nc * n);
+  for (int r = 0; r < n; r++)
+    for (int c = 0; c < n; c++) {
+      double s = 0;
+      for (int t = 0; t < n; t++) {
+        double mat = dCv[t * n + c] + (t == c ? w.damping[c] + dt * w.spring[c] : 0.0);
+        s += Minv[r * n + t] * mat;
+      }
+      inner[r * n + c] = (r == c ? 1.0 : 0.0) - dt * s;
+    }
+  for (int r = 0; r < nc; r++)
+    for (int c = 0; c < n; c++) {
+      double s = 0, sf = 0;
+      for (int i = 0; i < n; i++) { s += Ac[i * nc + r] * inner[i * n + c]; sf += Ac[i * nc + r] * Minv[i * n + c]; }
+      dBv[r * n + c] = -snap.bounceDiag[r] * s;
+      dBf[r * n + c] = -snap.bounceDiag[r] * dt * sf;
+    }
+  std::vector<double> dFv, dFf;
+  Qsolve(dBv, n, dFv);
+  Qsolve(dBf, n, dFf);
+  // velVel = I + Minv (A_c_ub_E dF_c - dt dC_v) - dt Minv D - dt^2 Minv K
+  // forceVel = Minv (A_c_ub_E dF_c + dt I)
+  std::vector<double> T1(n * n), T2(n * n);
+  for (int i = 0; i < n; i++)
+    for (int c = 0; c < n; c++) {
+      double s1 = 0, s2 = 0;
+      for (int r = 0; r < nc; r++) { s1 += AcubE[i * nc + r] * dFv[r * n + c]; s2 += AcubE[i * nc + r] * dFf[r * n + c]; }
+      T1[i * n + c] = s1 - dt * dCv[i * n + c];
+      T2[i * n + c] = s2 + (i == c ? dt : 0.0);
+    }
+  for (int r = 0; r < n; r++)
+    for (int c = 0; c < n; c++) {
+      double s1 = 0, s2 = 0;
+      for (int t = 0; t < n; t++) { s1 += Minv[r * n + t] * T1[t * n + c]; s2 += Minv[r * n + t] * T2[t * n + c]; }
+      velVel[r * n + c] = (r == c ? 1.0 : 0.0) + s1 - dt * Minv[r * n + c] * w.damping[c] -
+                          dt * dt * Minv[r * n + c] * w.spring[c];
+      forceVel[r * n + c] = s2;
+    }
+  // position: dM + Minv (A_c_ub_E dF_c + dA_c f + dA_ub E f - dt dC) - dt Minv K
+  std::vector<double> dFq, dAcf;
+  positionConstraintTerms(w, snap, Minv, C, dCq, Ac, Aub, AcubE, Q, dFq, dAcf);
+  std::vector<double> T3(n * n);
+  for (int i = 0; i < n; i++)
+    for (int c = 0; c < n; c++) {
+      double s = 0;
+      for (int r = 0; r < nc; r++) s += AcubE[i * nc + r] * dFq[r * n + c];
+      T3[i * n + c] = s + dAcf[i * n + c] - dt * dCq[i * n + c];
+    }
+  for (int r = 0; r < n; r++)
+    for (int c = 0; c < n; c++) {
+      double s = 0;
+      for (int t = 0; t < n; t++) s += Minv[r * n + t] * T3[t * n + c];
+      posVel[r * n + c] = dM[r * n + c] + s - Minv[r * n + c] * dt * w.spring[c];
+    }
 }
 
 }  // namespace oracle

@@ -1,0 +1,379 @@
+// ORACLE / TEST INFRASTRUCTURE ONLY -- see nimble_oracle.cpp header.
+//
+// Position derivatives of the contact constraint terms, restating
+//  * DifferentiableContactConstraint::getConstraintForcesJacobian
+//    (dart/neural/DifferentiableContactConstraint.cpp:1654): d(J^T e_i)/dq =
+//    multiple_r * (dS_r/dq_k . wrench + S_r . dwrench/dq_k), with the screw
+//    gradient ad(S_pos_k, S_r) (:1226, FreeJoint::getScrewAxisGradientForForce
+//    FreeJoint.cpp:1193), the contact position gradient (:328) and the force
+//    direction gradient (:594 normal, :1092 tangent basis);
+//  * BackpropSnapshot::getJacobianOfConstraintForce (BackpropSnapshot.cpp:2723)
+//    = dQ_b + Q^+ dB, getJacobianOfLCPConstraintMatrixClampingSubset (:2889)
+//    including the pseudo-inverse gradient branch, and
+//    getJacobianOfLCPOffsetClampingSubset (:3181) for POSITION.
+// Supported contact types: VERTEX_FACE and FACE_VERTEX (box-box face
+// contacts); EDGE_EDGE aborts.
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+
+#include "oracle_lcp.hpp"
+
+namespace oracle {
+
+void codSolve(const double* A, int m, int n, const double* b, double* x);
+
+using Mat = std::vector<double>;
+enum { CT_FACE_VERTEX = 1, CT_VERTEX_FACE = 2, CT_EDGE_EDGE = 3 };
+
+static void cross3(const double* a, const double* b, double* o) {
+  o[0] = a[1] * b[2] - a[2] * b[1];
+  o[1] = a[2] * b[0] - a[0] * b[2];
+  o[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+// World screw axis for position (Joint::getWorldAxisScrewForPosition,
+// Joint.cpp:1167 with FreeJoint's position-space Jacobian FreeJoint.cpp:790)
+static void positionScrew(const World& w, const Kin<double>& k, const double* q, int dof, double* Z) {
+  const int b = w.dofBody[dof];
+  const Body& B = w.bodies[b];
+  const int c = dof - B.dof0;
+  V6<double> xi;
+  for (int i = 0; i < 6; i++) xi[i] = 0.0;
+  if (B.jtype == NIMBLE_JOINT_FREE) {
+    const double* th = q + B.dof0;
+    V3<double> t{{th[0], th[1], th[2]}};
+    if (c < 3) {
+      // J_r e_c = column c of expMapJac(th)^T
+      double t2 = th[0] * th[0] + th[1] * th[1] + th[2] * th[2];
+      double tt = std::sqrt(t2);
+      M3<double> K = skew(t), K2 = mul(K, K), J;
+      double a, bb;
+      if (tt < 1.0e-3) { a = 0.5; bb = 1.0 / 6.0; }  // expMapJac small-angle branch
+      else { a = (1 - std::cos(tt)) / t2; bb = (tt - std::sin(tt)) / (t2 * tt); }
+      for (int i = 0; i < 9; i++) J.m[i] = ((i % 4) == 0 ? 1.0 : 0.0) + a * K.m[i] + bb * K2.m[i];
+      // expMapJac(th)^T column c = row c of expMapJac
+      for (int i = 0; i < 3; i++) xi[i] = J(c, i);
+    } else {
+      M3<double> R = expMapRot(t);
+      for (int i = 0; i < 3; i++) xi[3 + i] = R(c - 3, i);  // R^T e
+    }
+    V6<double> z = AdT(compose(k.Tw[b], B.Tcj), xi);
+    for (int i = 0; i < 6; i++) Z[i] = z[i];
+  } else {
+    V6<double> sl;
+    for (int i = 0; i < 6; i++) sl[i] = k.Sj[b](i, c);
+    V6<double> z = AdT(k.Tw[b], sl);
+    for (int i = 0; i < 6; i++) Z[i] = z[i];
+  }
+}
+
+static void velocityScrew(const World& w, const Kin<double>& k, int dof, double* S) {
+  const int b = w.dofBody[dof];
+  V6<double> sl;
+  for (int i = 0; i < 6; i++) sl[i] = k.Sj[b](i, dof - w.bodies[b].dof0);
+  V6<double> s = AdT(k.Tw[b], sl);
+  for (int i = 0; i < 6; i++) S[i] = s[i];
+}
+
+// ContactConstraint::getTangentBasisMatrixODEGradient (ContactConstraint.cpp:772)
+static void tangentBasisGradient(const double* n, const double* g, double* T0, double* T1) {
+  const double ez[3] = {0, 0, 1}, ex[3] = {1, 0, 0}, ey[3] = {0, 1, 0};
+  const double* cr = ez;
+  double t[3];
+  cross3(cr, n, t);
+  if (t[0] * t[0] + t[1] * t[1] + t[2] * t[2] < 1e-12) {
+    cr = ex; cross3(cr, n, t);
+    if (t[0] * t[0] + t[1] * t[1] + t[2] * t[2] < 1e-12) {
+      cr = ey; cross3(cr, n, t);
+      if (t[0] * t[0] + t[1] * t[1] + t[2] * t[2] < 1e-12) { cr = ez; cross3(cr, n, t); }
+    }
+  }
+  double tn = std::sqrt(t[0] * t[0] + t[1] * t[1] + t[2] * t[2]);
+  for (int i = 0; i < 3; i++) t[i] /= tn;
+  double gc[3];
+  cross3(cr, g, gc);
+  for (int i = 0; i < 3; i++) gc[i] /= tn;
+  double gt[3];
+  if (std::fabs(tn - 1.0) > 1e-6) {
+    double dd = gc[0] * t[0] + gc[1] * t[1] + gc[2] * t[2];
+    for (int i = 0; i < 3; i++) gt[i] = gc[i] - dd * t[i];
+  } else {
+    for (int i = 0; i < 3; i++) gt[i] = gc[i];
+  }
+  double a[3], b[3];
+  cross3(g, t, a);
+  cross3(n, gt, b);
+  for (int i = 0; i < 3; i++) { T0[i] = gt[i]; T1[i] = a[i] + b[i]; }
+}
+
+// G_i = d(J^T e_i)/dq  (n x n) for constraint row i
+static void constraintForcesJacobian(const World& w, const Kin<double>& k, const Snapshot& snap, int row, Mat& G) {
+  const int n = w.n;
+  G.assign(n * n, 0.0);
+  const Contact& c = snap.contacts[snap.rowContact[row]];
+  const int dirIdx = snap.rowDirIdx[row];
+  const double* d = &snap.rowDir[3 * row];
+  const double* p = c.point;
+  double wr[6];
+  cross3(p, d, wr);
+  wr[3] = d[0]; wr[4] = d[1]; wr[5] = d[2];
+  auto parentOf = [&](int dof, int body) { return body >= 0 && w.isAncestorOrSelf(w.dofBody[dof], body); };
+  for (int kk = 0; kk < n; kk++) {
+    double Z[6];
+    positionScrew(w, k, snap.q.data(), kk, Z);
+    // d wrench / d q_k
+    double dp[3] = {0, 0, 0}, dd[3] = {0, 0, 0};
+    const bool pa = parentOf(kk, c.bodyA), pb = parentOf(kk, c.bodyB);
+    if (pa && pb) { std::fprintf(stderr, "oracle: self-collision gradients not supported\n"); std::abort(); }
+    int type = 0;  // 0 none, 1 vertex, 2 face
+    if (pa || pb) {
+      if (c.type == CT_EDGE_EDGE) { std::fprintf(stderr, "oracle: EDGE_EDGE position gradients not supported\n"); std::abort(); }
+      if (c.type == CT_VERTEX_FACE) type = pa ? 1 : 2;
+      else type = pa ? 2 : 1;
+    }
+    const double wv[3] = {Z[0], Z[1], Z[2]}, vv[3] = {Z[3], Z[4], Z[5]};
+    if (type == 1) {
+      // math::gradientWrtTheta(worldTwist, contactPos, 0)
+      if (std::sqrt(wv[0] * wv[0] + wv[1] * wv[1] + wv[2] * wv[2]) > 1e-6) {
+        cross3(wv, p, dp);
+        for (int i = 0; i < 3; i++) dp[i] += vv[i];
+      } else {
+        for (int i = 0; i < 3; i++) dp[i] = vv[i];
+      }
+    } else if (type == 2) {
+      double dn[3];
+      cross3(wv, c.normal, dn);  // gradientWrtThetaPureRotation
+      if (dirIdx == 0 || dn[0] * dn[0] + dn[1] * dn[1] + dn[2] * dn[2] <= 1e-12) {
+        for (int i = 0; i < 3; i++) dd[i] = dn[i];
+      } else {
+        double T0[3], T1[3];
+        tangentBasisGradient(c.normal, dn, T0, T1);
+        for (int i = 0; i < 3; i++) dd[i] = dirIdx == 1 ? T0[i] : T1[i];
+      }
+    }
+    double dwr[6], t1[3], t2[3];
+    cross3(p, dd, t1);
+    cross3(dp, d, t2);
+    for (int i = 0; i < 3; i++) { dwr[i] = t1[i] + t2[i]; dwr[3 + i] = dd[i]; }
+    for (int r = 0; r < n; r++) {
+      const bool ra = parentOf(r, c.bodyA), rb = parentOf(r, c.bodyB);
+      double mult = (ra && rb) ? 0.0 : (ra ? 1.0 : (rb ? -1.0 : 0.0));
+      if (mult == 0.0) continue;
+      double S[6];
+      velocityScrew(w, k, r, S);
+      double val = 0;
+      // screw-axis gradient: k's joint at or above r's joint
+      const int bk = w.dofBody[kk], br = w.dofBody[r];
+      if (w.isAncestorOrSelf(bk, br)) {
+        if (bk != br || w.bodies[bk].jtype == NIMBLE_JOINT_FREE) {
+          V6<double> zz, ss;
+          for (int i = 0; i < 6; i++) { zz[i] = Z[i]; ss[i] = S[i]; }
+          V6<double> g = ad(zz, ss);
+          for (int i = 0; i < 6; i++) val += g[i] * wr[i];
+        }
+      }
+      for (int i = 0; i < 6; i++) val += S[i] * dwr[i];
+      G[r * n + kk] = mult * val;
+    }
+  }
+}
+
+void positionConstraintTerms(const World& w, const Snapshot& snap, const Mat& Minv, const Mat& C, const Mat& dCq,
+                             const Mat& Ac, const Mat& Aub, const Mat& AcubE, const Mat& Qin, Mat& dFcPos,
+                             Mat& dAcf) {
+  const int n = w.n, m = snap.numRows, nc = snap.numClamping, nu = snap.numUpperBound;
+  const double dt = w.dt;
+  Kin<double> k;
+  k.compute(w, snap.q.data(), snap.v.data());
+  // per-row G matrices for clamping / upper-bound rows
+  std::vector<Mat> Gc(nc), Gu(nu);
+  for (int j = 0; j < m; j++) {
+    if (snap.mapping[j] == CM_CLAMPING) constraintForcesJacobian(w, k, snap, j, Gc[snap.clampingIndex[j]]);
+    else if (snap.mapping[j] >= 0) constraintForcesJacobian(w, k, snap, j, Gu[snap.upperBoundIndex[j]]);
+  }
+  auto dAc = [&](const Mat& f0) {  // getJacobianOfClampingConstraints: sum f0_i G_i
+    Mat R(n * n, 0.0);
+    for (int i = 0; i < nc; i++)
+      if (f0[i] != 0.0) for (int t = 0; t < n * n; t++) R[t] += f0[i] * Gc[i][t];
+    return R;
+  };
+  auto dAub = [&](const Mat& f0) {
+    Mat R(n * n, 0.0);
+    for (int i = 0; i < nu; i++)
+      if (f0[i] != 0.0) for (int t = 0; t < n * n; t++) R[t] += f0[i] * Gu[i][t];
+    return R;
+  };
+  auto dAcT = [&](const Mat& v0) {  // getJacobianOfClampingConstraintsTranspose: nc x n
+    Mat R(nc * n, 0.0);
+    for (int i = 0; i < nc; i++)
+      for (int kk = 0; kk < n; kk++) {
+        double s = 0;
+        for (int r = 0; r < n; r++) s += Gc[i][r * n + kk] * v0[r];
+        R[i * n + kk] = s;
+      }
+    return R;
+  };
+  auto dAubT = [&](const Mat& v0) {
+    Mat R(nu * n, 0.0);
+    for (int i = 0; i < nu; i++)
+      for (int kk = 0; kk < n; kk++) {
+        double s = 0;
+        for (int r = 0; r < n; r++) s += Gu[i][r * n + kk] * v0[r];
+        R[i * n + kk] = s;
+      }
+    return R;
+  };
+  auto mv = [&](const Mat& A, const Mat& x, int rows, int cols) {
+    Mat y(rows, 0.0);
+    for (int r = 0; r < rows; r++) { double s = 0; for (int c = 0; c < cols; c++) s += A[r * cols + c] * x[c]; y[r] = s; }
+    return y;
+  };
+  auto mm = [&](const Mat& A, const Mat& B, int r, int kk, int c) {
+    Mat Cm(r * c, 0.0);
+    for (int i = 0; i < r; i++)
+      for (int t = 0; t < kk; t++) {
+        double a = A[i * kk + t];
+        if (a == 0.0) continue;
+        for (int j = 0; j < c; j++) Cm[i * c + j] += a * B[t * c + j];
+      }
+    return Cm;
+  };
+  auto tr = [&](const Mat& A, int r, int c) {
+    Mat T(r * c);
+    for (int i = 0; i < r; i++) for (int j = 0; j < c; j++) T[j * r + i] = A[i * c + j];
+    return T;
+  };
+  auto jacMinv = [&](const Mat& x) {  // getJacobianOfMinv(x, POSITION) = -Minv d(M Minv x)/dq
+    Mat y = mv(Minv, x, n, n);
+    Mat dMy(n * n);
+    w.jacobianOfMy(snap.q.data(), y.data(), dMy.data());
+    Mat R = mm(Minv, dMy, n, n, n);
+    for (auto& v : R) v = -v;
+    return R;
+  };
+  Mat f = snap.fc;
+  Mat E = snap.E;
+  Mat Ef = mv(E, f, nu, nc);
+  // dA_c f + dA_ub E f
+  dAcf = dAc(f);
+  {
+    Mat t = dAub(Ef);
+    for (int i = 0; i < n * n; i++) dAcf[i] += t[i];
+  }
+  // dB (POSITION), getJacobianOfLCPOffsetClampingSubset:
+  //   -bounce .* (dA_c^T(v_f) + A_c^T dt (dMinv_f - Minv dC - Minv K))
+  Mat fext(n);
+  for (int i = 0; i < n; i++) {
+    double springF = w.spring[i] * (snap.q[i] - w.restPos[i] + dt * snap.v[i]);
+    fext[i] = snap.tau[i] - C[i] - w.damping[i] * snap.v[i] - springF;
+  }
+  Mat dMinvF = jacMinv(fext);
+  Mat inner(n * n);
+  {
+    Mat MdC = mm(Minv, dCq, n, n, n);
+    for (int r = 0; r < n; r++)
+      for (int c = 0; c < n; c++) inner[r * n + c] = dMinvF[r * n + c] - MdC[r * n + c] - Minv[r * n + c] * w.spring[c];
+  }
+  Mat dB = dAcT(snap.preConstraintV);
+  {
+    Mat AcT = tr(Ac, n, nc);
+    Mat t = mm(AcT, inner, nc, n, n);
+    for (int i = 0; i < nc; i++)
+      for (int c = 0; c < n; c++) dB[i * n + c] = -snap.bounceDiag[i] * (dB[i * n + c] + dt * t[i * n + c]);
+  }
+  // Q pseudo-inverse and Q^+ dB
+  const Mat& Q = Qin;
+  Mat Qinv(nc * nc);
+  {
+    Mat e(nc), col(nc);
+    for (int c = 0; c < nc; c++) {
+      std::fill(e.begin(), e.end(), 0.0);
+      e[c] = 1.0;
+      codSolve(Q.data(), nc, nc, e.data(), col.data());
+      for (int r = 0; r < nc; r++) Qinv[r * nc + c] = col[r];
+    }
+  }
+  auto Qsolve = [&](const Mat& R, int cols) {  // column-wise COD solve
+    Mat out(nc * cols), bb(nc), xx(nc);
+    for (int c = 0; c < cols; c++) {
+      for (int r = 0; r < nc; r++) bb[r] = R[r * cols + c];
+      codSolve(Q.data(), nc, nc, bb.data(), xx.data());
+      for (int r = 0; r < nc; r++) out[r * cols + c] = xx[r];
+    }
+    return out;
+  };
+  Mat AcT = tr(Ac, n, nc);
+  Mat AubT = tr(Aub, n, nu);
+  auto dQ = [&](const Mat& rhs) {  // nc x n
+    Mat AcubErhs = mv(AcubE, rhs, n, nc);
+    Mat MA = mv(Minv, AcubErhs, n, n);
+    Mat R = dAcT(MA);
+    Mat J = jacMinv(AcubErhs);
+    Mat inner2 = dAc(rhs);
+    if (nu > 0) {
+      Mat Erhs = mv(E, rhs, nu, nc);
+      Mat t = dAub(Erhs);
+      for (int i = 0; i < n * n; i++) inner2[i] += t[i];
+    }
+    Mat MI = mm(Minv, inner2, n, n, n);
+    for (int i = 0; i < n * n; i++) J[i] += MI[i];
+    Mat t2 = mm(AcT, J, nc, n, n);
+    for (int i = 0; i < nc * n; i++) R[i] += t2[i];
+    return R;
+  };
+  auto dQT = [&](const Mat& rhs) {  // nc x n
+    Mat Acrhs = mv(Ac, rhs, n, nc);
+    Mat MA = mv(Minv, Acrhs, n, n);
+    Mat J = jacMinv(Acrhs);
+    Mat MI = mm(Minv, dAc(rhs), n, n, n);
+    for (int i = 0; i < n * n; i++) J[i] += MI[i];
+    Mat R = dAcT(MA);
+    Mat t2 = mm(AcT, J, nc, n, n);
+    for (int i = 0; i < nc * n; i++) R[i] += t2[i];
+    if (nu > 0) {
+      Mat U = dAubT(MA);
+      Mat t3 = mm(AubT, J, nu, n, n);
+      for (int i = 0; i < nu * n; i++) U[i] += t3[i];
+      Mat ET = tr(E, nu, nc);
+      Mat t4 = mm(ET, U, nc, nu, n);
+      for (int i = 0; i < nc * n; i++) R[i] += t4[i];
+    }
+    return R;
+  };
+  Mat b(nc, 0.0);
+  for (int j = 0; j < m; j++)
+    if (snap.mapping[j] == CM_CLAMPING) b[snap.clampingIndex[j]] = snap.lcpB[j];
+  // imprecision map I - Q Q^+
+  Mat imp(nc * nc);
+  double impNorm = 0;
+  {
+    Mat QQ = mm(Q, Qinv, nc, nc, nc);
+    for (int r = 0; r < nc; r++)
+      for (int c = 0; c < nc; c++) {
+        imp[r * nc + c] = (r == c ? 1.0 : 0.0) - QQ[r * nc + c];
+        impNorm += imp[r * nc + c] * imp[r * nc + c];
+      }
+  }
+  Mat Qb(nc);
+  codSolve(Q.data(), nc, nc, b.data(), Qb.data());
+  Mat dQb = Qsolve(dQ(Qb), n);
+  for (auto& v : dQb) v = -v;
+  if (impNorm >= 1e-18) {
+    // full pseudo-inverse gradient (mathoverflow 29511), BackpropSnapshot.cpp:2960
+    Mat impb = mv(imp, b, nc, nc);
+    Mat QinvT = tr(Qinv, nc, nc);
+    Mat t1 = Qsolve(mm(QinvT, dQT(impb), nc, nc, n), n);
+    Mat IQQ(nc * nc);
+    Mat QiQ = mm(Qinv, Q, nc, nc, nc);
+    for (int r = 0; r < nc; r++)
+      for (int c = 0; c < nc; c++) IQQ[r * nc + c] = (r == c ? 1.0 : 0.0) - QiQ[r * nc + c];
+    Mat t2 = mm(IQQ, dQT(mv(QinvT, Qb, nc, nc)), nc, nc, n);
+    for (int i = 0; i < nc * n; i++) dQb[i] += t1[i] + t2[i];
+  }
+  Mat QdB = Qsolve(dB, n);
+  dFcPos.assign(nc * n, 0.0);
+  for (int i = 0; i < nc * n; i++) dFcPos[i] = dQb[i] + QdB[i];
+}
+
+}  // namespace oracle

@@ -1,0 +1,133 @@
+"""Pin the CPU oracle (CPU-only tests).
+
+* box-box narrow phase vs the reference's known-answer test
+  (unittests/unit/test_DARTCollide.cpp:554);
+* the Dantzig restatement vs the reference's OWN solver outputs
+  (tests/golden/lcp_fixtures.json, generated from oracle/_ref) and, when the
+  reference build is present, live against oracle/_ref on fresh problems;
+* COD solve == minimum-norm least squares;
+* dynamics identities (ABA vs M ddq + C = tau, as unittests/comprehensive/
+  test_Dynamics.cpp checks) and the analytic Jacobians vs central finite
+  differences of the oracle's own forward step (the reference's
+  GradientTestUtils.hpp strategy), with and without contact.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import models
+from oracle import oracle as O
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _dec(v):
+    return [float("inf") if x == "inf" else float("-inf") if x == "-inf" else x for x in v]
+
+
+def test_box_box_known_answer(oracle_built):
+    d = json.load(open(os.path.join(GOLD, "box_box_annotation.json")))
+    T1 = np.eye(4); T1[:3, 3] = d["T1_translation"]
+    T2 = np.eye(4); T2[:3, 3] = d["T2_translation"]
+    cs = O.box_box(d["size1"], T1, d["size2"], T2)
+    assert len(cs) == len(d["expected"])
+    names = {1: "FACE_VERTEX", 2: "VERTEX_FACE", 3: "EDGE_EDGE"}
+    got = sorted([(tuple(np.round(c[:3], 9)), names[int(c[7])]) for c in cs])
+    exp = sorted([(tuple(np.round(e["point"], 9)), e["type"]) for e in d["expected"]])
+    assert got == exp
+
+
+def test_dantzig_matches_reference_fixtures(oracle_built):
+    d = json.load(open(os.path.join(GOLD, "lcp_fixtures.json")))
+    for p in d["problems"]:
+        A = np.array(p["A"]); b = np.array(p["b"])
+        lo = np.array(_dec(p["lo"])); hi = np.array(_dec(p["hi"])); fi = np.array(p["findex"], dtype=np.int32)
+        ok, x = O.dantzig(A, b, lo, hi, fi)
+        assert ok == p["ref_success"], p["name"]
+        ref = np.array(p["ref_x"])
+        assert np.allclose(x, ref, rtol=1e-9, atol=1e-12), (p["name"], np.abs(x - ref).max())
+
+
+def test_dantzig_live_vs_reference(oracle_built):
+    if O.ref_lib() is None:
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    rng = np.random.default_rng(7)
+    for k in range(200):
+        nc, nd = int(rng.integers(1, 13)), int(rng.integers(6, 40))
+        J = rng.standard_normal((3 * nc, nd))
+        L = rng.standard_normal((nd, nd))
+        A = J @ (L @ L.T + 0.05 * np.eye(nd)) @ J.T
+        b = rng.standard_normal(3 * nc) * 0.2
+        lo = np.tile([0.0, -1.0, -1.0], nc); hi = np.tile([np.inf, 1.0, 1.0], nc)
+        fi = np.array([v for c in range(nc) for v in (-1, 3 * c, 3 * c)], dtype=np.int32)
+        for early in (False, True):
+            ok1, x1 = O.dantzig(A, b, lo, hi, fi, early)
+            ok2, x2 = O.ref_dantzig(A, b, lo, hi, fi, early)
+            assert ok1 == ok2
+            if ok1:
+                assert np.allclose(x1, x2, rtol=1e-9, atol=1e-12), np.abs(x1 - x2).max()
+
+
+def test_cod_is_min_norm_least_squares(oracle_built):
+    rng = np.random.default_rng(3)
+    for r in (1, 3, 5, 8):
+        U = rng.standard_normal((8, r))
+        A = U @ U.T  # rank r, symmetric PSD like Q
+        b = rng.standard_normal(8)
+        x = O.cod_solve(A, b)
+        ref = np.linalg.pinv(A, rcond=1e-12) @ b
+        assert np.allclose(x, ref, rtol=1e-8, atol=1e-10)
+    A = rng.standard_normal((6, 6))
+    b = rng.standard_normal(6)
+    assert np.allclose(O.cod_solve(A, b), np.linalg.solve(A, b))
+
+
+@pytest.mark.parametrize("name", ["cartpole", "kr5", "atlas_air"])
+def test_aba_matches_mass_matrix(oracle_built, name):
+    w = {"cartpole": models.cartpole_world, "kr5": models.kr5_world,
+         "atlas_air": lambda: models.atlas_world(False)}[name]()
+    o = O.OracleWorld(w)
+    n = w.getNumDofs()
+    st, f = models.random_states(w, 3, seed=5)
+    d = w.desc_arrays()
+    for b in range(3):
+        q, v = st[b, :n], st[b, n:]
+        M = o.mass_matrix(q)
+        assert np.allclose(M, M.T)
+        assert np.linalg.eigvalsh(M).min() > 0
+        ddq = o.forward_dynamics(q, v, f[b])
+        rhs = f[b] - d["spring"] * (q - d["rest_position"] + v * w.dt) - d["damping"] * v - o.coriolis_gravity(q, v)
+        assert np.abs(M @ ddq - rhs).max() <= 1e-10 * max(1.0, np.abs(rhs).max())
+
+
+def _fd_check(w, st, f, g, eps=1e-7):
+    o = O.OracleWorld(w)
+    n = w.getNumDofs()
+
+    def fwd(s, ff):
+        o.reset_cache(1)
+        return o.forward(s[None], ff[None])[0]
+    o.reset_cache(1)
+    o.forward(st[None], f[None])
+    gs, gf = o.backward(g[None])
+    fd_s = np.array([(fwd(st + eps * e, f) - fwd(st - eps * e, f)) @ g / (2 * eps) for e in np.eye(2 * n)])
+    fd_f = np.array([(fwd(st, f + eps * e) - fwd(st, f - eps * e)) @ g / (2 * eps) for e in np.eye(n)])
+    return gs[0], gf[0], fd_s, fd_f
+
+
+@pytest.mark.parametrize("name", ["cartpole", "kr5", "atlas_air", "atlas_contact"])
+def test_analytic_gradients_vs_finite_differences(oracle_built, name):
+    w = {"cartpole": models.cartpole_world, "kr5": models.kr5_world,
+         "atlas_air": lambda: models.atlas_world(False), "atlas_contact": lambda: models.atlas_world(True)}[name]()
+    small = name == "atlas_contact"
+    st, f = models.random_states(w, 1, seed=3, q_scale=0.01 if small else 0.3, v_scale=0.02 if small else 0.5)
+    g = np.random.default_rng(2).standard_normal(st.shape[1])
+    gs, gf, fd_s, fd_f = _fd_check(w, st[0], f[0], g)
+    if small:
+        o = O.OracleWorld(w)
+        o.forward(st, f)
+        assert o.num_contacts(0) > 0
+    assert np.abs(gs - fd_s).max() <= 1e-6 * np.abs(fd_s).max()
+    assert np.abs(gf - fd_f).max() <= 1e-6 * np.abs(fd_f).max()

@@ -132,7 +132,10 @@ int64_t nimble_lcp_cache_doubles(nimble_world_t world);
  *   forces     [batch][num_dofs]    control forces, device
  *   lcp_cache  [batch][lcp_cache_doubles] warm start, read + updated, device
  *   next_state [batch][2*num_dofs]  output, device
- *   snapshot   [batch][snapshot_doubles]  output, consumed by nimble_backward
+ *   snapshot   [batch][snapshot_doubles]  output, consumed by nimble_backward:
+ *              contacts, LCP rows and classification (clamping / upper-bound
+ *              / separating), clamping impulses f_c, pre-constraint velocity
+ *              -- the per-world state of BackpropSnapshot.
  */
 int nimble_forward(nimble_world_t world, int32_t batch, const double* state,
                    const double* forces, double* lcp_cache, double* next_state,
@@ -146,9 +149,11 @@ int nimble_forward(nimble_world_t world, int32_t batch, const double* state,
  *   grad_next_state [batch][2*num_dofs]  dL/d(next_state), device
  *   grad_state      [batch][2*num_dofs]  dL/d(state) output, device
  *   grad_forces     [batch][num_dofs]    dL/d(forces) output, device
+ * The snapshot's contact records are read; its workspace tail (present only
+ * for models whose worst-case LCP exceeds the on-chip pool) is scratch.
  */
 int nimble_backward(nimble_world_t world, int32_t batch, const double* state,
-                    const double* forces, const double* snapshot,
+                    const double* forces, double* snapshot,
                     const double* grad_next_state, double* grad_state,
                     double* grad_forces, void* stream);
 

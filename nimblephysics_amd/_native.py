@@ -9,7 +9,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libnimble_amd.so")
+LIB_PATH = os.environ.get("NIMBLE_AMD_LIB") or os.path.join(_HERE, "libnimble_amd.so")
 
 _lib = None
 

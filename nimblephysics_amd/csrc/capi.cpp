@@ -3,12 +3,14 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
 
 #include "model.h"
+#include "pool_sizes.h"
 
 static thread_local std::string g_err;
 
@@ -27,7 +29,8 @@ struct nimble_world {
   ModelDev host;
   ModelDev* dev = nullptr;
   Layout fwd, bwd;
-  int snapDoubles = 1;
+  int snapDoubles = 8;
+  int poolRows = 0, maxRows = 0;
   int cacheDoubles = NIMBLE_MAX_LCP + 1;
   hipFunction_t dummy = nullptr;
 };
@@ -35,7 +38,7 @@ struct nimble_world {
 extern "C" __global__ void nimble_forward_kernel(const ModelDev*, Layout, int, const double*, const double*, double*,
                                                  double*, double*, int, int);
 extern "C" __global__ void nimble_backward_kernel(const ModelDev*, Layout, int, const double*, const double*,
-                                                  const double*, int, const double*, double*, double*);
+                                                  double*, int, const double*, double*, double*);
 
 static void isoInverse(const double* T, double* O) {
   // [R|p]^-1 = [R^T | -R^T p]
@@ -44,7 +47,16 @@ static void isoInverse(const double* T, double* O) {
   for (int r = 0; r < 3; r++) O[r * 4 + 3] = -(O[r * 4] * T[3] + O[r * 4 + 1] * T[7] + O[r * 4 + 2] * T[11]);
 }
 
-static Layout makeLayout(const ModelDev& m, bool backward) {
+// LCP rows the LDS pool is sized for; worlds with more rows in a step use the
+// HBM workspace at the tail of their snapshot instead (same code path).
+static int ldsPoolRows(const ModelDev& m, int mcap) {
+  int r = 24;
+  if (const char* e = getenv("NIMBLE_AMD_LDS_ROWS")) r = atoi(e);
+  if (r < 0) r = 0;
+  return r < mcap ? r : mcap;
+}
+
+static Layout makeLayout(const ModelDev& m, bool backward, int poolRows) {
   Layout L{};
   int o = 0;
   auto take = [&](int count) { int r = o; o += (count + 1) & ~1; return r; };
@@ -53,11 +65,16 @@ static Layout makeLayout(const ModelDev& m, bool backward) {
   L.Tw = take(12 * nb); L.Sw = take(6 * n); L.V = take(6 * nb); L.A = take(6 * nb);
   L.IC = take(36 * nb); L.F = take(6 * nb); L.M = take(n * n); L.rhs = take(n); L.x = take(n);
   L.scratch = take(24 * 6);
-  L.ct = take(8);
+  L.v1 = take(n);
+  L.ct = take(m.numPairs > 0 ? ctDoubles(m.pairChunk) : 16);
   if (backward) {
+    // B1, B23, B4 contiguous: reused for the 8 x nb x 12 M-derivative fields
     L.B1 = take(36 * nb); L.B23 = take(36 * nb); L.B4 = take(36 * nb);
     L.P = take(6 * nb); L.H = take(6 * nb); L.w = take(n); L.gp = take(n); L.gv = take(n); L.out = take(3 * n);
   }
+  L.poolCap = 0;
+  if (m.numPairs > 0 && poolRows > 0) L.poolCap = backward ? bwdPoolDoublesHost(poolRows, n) : fwdPoolDoublesHost(poolRows, n);
+  L.pool = take(L.poolCap);
   L.total = o;
   return L;
 }
@@ -136,6 +153,7 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
   // Candidate pairs: DARTCollisionDetector::collide (DARTCollisionDetector.cpp:127)
   // object order i<j filtered by BodyNodeCollisionFilter (CollisionFilter.cpp:105)
   m.numPairs = 0;
+  m.pairChunk = 0;
   for (int i = 0; i < m.ns; i++)
     for (int j = i + 1; j < m.ns; j++) {
       int bi = m.shapeBody[i], bj = m.shapeBody[j];
@@ -147,20 +165,42 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
       m.pairB[m.numPairs] = j;
       m.numPairs++;
     }
-  w->fwd = makeLayout(m, false);
-  w->bwd = makeLayout(m, true);
-  if (w->bwd.total * 8 > 160 * 1024) { delete w; return fail(NIMBLE_ERR_UNSUPPORTED, "model too large for LDS"); }
+  m.pairChunk = m.numPairs < CT_PAIR_CHUNK_HOST ? m.numPairs : CT_PAIR_CHUNK_HOST;
+  // max LCP rows: 3 per contact, <= 8 box-box points per pair, <= NIMBLE_MAX_CONTACTS
+  int maxContacts = 8 * m.numPairs;
+  if (maxContacts > NIMBLE_MAX_CONTACTS) maxContacts = NIMBLE_MAX_CONTACTS;
+  const int mcap = 3 * maxContacts;
+  int poolRows = ldsPoolRows(m, mcap);
+  for (;;) {
+    w->fwd = makeLayout(m, false, poolRows);
+    w->bwd = makeLayout(m, true, poolRows);
+    if (w->bwd.total * 8 <= 160 * 1024 && w->fwd.total * 8 <= 160 * 1024) break;
+    if (poolRows == 0) { delete w; return fail(NIMBLE_ERR_UNSUPPORTED, "model too large for LDS"); }
+    poolRows = poolRows > 6 ? poolRows - 6 : 0;
+  }
+  w->poolRows = poolRows;
+  w->maxRows = mcap;
+  if (m.numPairs > 0) {
+    int ws = 0;
+    if (mcap > poolRows) {
+      const int a = fwdPoolDoublesHost(mcap, m.n), b = bwdPoolDoublesHost(mcap, m.n);
+      ws = a > b ? a : b;
+    }
+    w->snapDoubles = snapWorkspaceOffsetHost(m.n) + ws;
+  } else {
+    w->snapDoubles = 8;
+  }
   hipError_t e = hipMalloc(&w->dev, sizeof(ModelDev));
   if (e != hipSuccess) { delete w; return fail(NIMBLE_ERR_HIP, std::string("hipMalloc: ") + hipGetErrorString(e)); }
   e = hipMemcpy(w->dev, &m, sizeof(ModelDev), hipMemcpyHostToDevice);
-  if (e != hipSuccess) { hipFree(w->dev); delete w; return fail(NIMBLE_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e)); }
+  if (e != hipSuccess) { (void)hipFree(w->dev); delete w; return fail(NIMBLE_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e)); }
   *out = w;
   return NIMBLE_OK;
 }
 
 int nimble_world_destroy(nimble_world_t w) {
   if (!w) return NIMBLE_OK;
-  if (w->dev) hipFree(w->dev);
+  if (w->dev) (void)hipFree(w->dev);
   delete w;
   return NIMBLE_OK;
 }
@@ -178,7 +218,7 @@ int nimble_forward(nimble_world_t w, int32_t batch, const double* state, const d
                    double* next_state, double* snapshot, void* stream) {
   if (!w || batch < 0) return fail(NIMBLE_ERR_INVALID, "bad arguments");
   if (batch == 0) return NIMBLE_OK;
-  if (!state || !forces || !next_state) return fail(NIMBLE_ERR_INVALID, "null buffer");
+  if (!state || !forces || !next_state || !snapshot || !lcp_cache) return fail(NIMBLE_ERR_INVALID, "null buffer");
   hipStream_t st = (hipStream_t)stream;
   const size_t lds = (size_t)w->fwd.total * sizeof(double);
   hipLaunchKernelGGL(nimble_forward_kernel, dim3(gridFor(batch)), dim3(64), lds, st, w->dev, w->fwd, batch, state,
@@ -188,11 +228,11 @@ int nimble_forward(nimble_world_t w, int32_t batch, const double* state, const d
 }
 
 int nimble_backward(nimble_world_t w, int32_t batch, const double* state, const double* forces,
-                    const double* snapshot, const double* grad_next_state, double* grad_state,
+                    double* snapshot, const double* grad_next_state, double* grad_state,
                     double* grad_forces, void* stream) {
   if (!w || batch < 0) return fail(NIMBLE_ERR_INVALID, "bad arguments");
   if (batch == 0) return NIMBLE_OK;
-  if (!state || !forces || !grad_next_state || !grad_state || !grad_forces)
+  if (!state || !forces || !grad_next_state || !grad_state || !grad_forces || !snapshot)
     return fail(NIMBLE_ERR_INVALID, "null buffer");
   hipStream_t st = (hipStream_t)stream;
   const size_t lds = (size_t)w->bwd.total * sizeof(double);

@@ -1,0 +1,1801 @@
+// Contact handling for the gfx950 timestep: box-box narrow phase, contact
+// constraint rows, the boxed LCP with Nimble's gradient short-circuit
+// (classification + least-squares standardisation), Dantzig / PGS fallbacks,
+// and the constraint impulses.
+//
+// Reference behaviour (see oracle/ for the CPU restatement and its pins):
+//   dart/collision/dart/DARTCollide.cpp:764 dBoxBox, :513 intersectRectQuad
+//   dart/collision/dart/DARTCollisionDetector.cpp:127 (pair loop), :357 postProcess
+//   dart/constraint/ConstraintSolver.cpp:520 updateConstraints
+//   dart/constraint/ContactConstraint.cpp:393 getInformation, :705 tangent basis
+//   dart/constraint/BoxedLcpConstraintSolver.cpp:175 buildLcpInputs, :330 solveLcp
+//   dart/neural/ConstrainedGroupGradientMatrices.cpp:482 constructMatrices,
+//     :218 opportunisticallyStandardizeResults
+//   dart/external/odelcpsolver/lcp.cpp:780 dSolveLCP
+//   dart/constraint/PgsBoxedLcpSolver.cpp:85
+//
+// GPU structure: the pair tests run one pair per lane; the small dense LCP
+// algebra (m <= 48 rows) runs on LDS-resident matrices.  The sequential
+// pivoting of Dantzig and the Householder sweeps of the COD solve are driven
+// by lane 0 while lanes 1..63 wait at the next barrier -- for the <= 24-row
+// problems of the benchmark models this is a small fraction of the step.
+#pragma once
+#include "model.h"
+#include "spatial.cuh"
+#include "pool_sizes.h"
+
+#define CT_FACE_VERTEX 1
+#define CT_VERTEX_FACE 2
+#define CT_EDGE_EDGE 3
+#define CM_CLAMPING (-1)
+#define CM_NOT_CLAMPING (-2)
+
+
+// ---------------------------------------------------------------------------
+// dBoxBox (one pair, one lane).  R1/R2 row-major 3x3, A/B half sizes.
+// Writes up to 8 contact records to `out`; returns the count.
+// ---------------------------------------------------------------------------
+__device__ int deviceBoxBox(const double* p1, const double* R1, const double* A, const double* p2,
+                            const double* R2, const double* B, double clipDepth, int b1, int b2, double* out) {
+  // keep the separating-axis / clipping arithmetic unfused so that exact
+  // comparisons (edge classification) agree with the CPU restatement
+#pragma clang fp contract(off)
+  const double fudge = 1.05;
+  double p[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+  double pp[3];
+  for (int i = 0; i < 3; i++) pp[i] = R1[i] * p[0] + R1[3 + i] * p[1] + R1[6 + i] * p[2];
+  double Rm[9], Qm[9];
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) {
+      Rm[i * 3 + j] = R1[i] * R2[j] + R1[3 + i] * R2[3 + j] + R1[6 + i] * R2[6 + j];
+      Qm[i * 3 + j] = fabs(Rm[i * 3 + j]);
+    }
+  double s = -1e12;
+  int invertNormal = 0, code = 0, normalCol = -1, normalBox = 0;
+  double normalC[3] = {0, 0, 0};
+  for (int i = 0; i < 3; i++) {
+    double e1 = pp[i];
+    double e2 = A[i] + B[0] * Qm[i * 3] + B[1] * Qm[i * 3 + 1] + B[2] * Qm[i * 3 + 2];
+    double s2 = fabs(e1) - e2;
+    if (s2 > s) { s = s2; normalBox = 1; normalCol = i; invertNormal = e1 < 0; code = 1 + i; }
+  }
+  for (int j = 0; j < 3; j++) {
+    double e1 = R2[j] * p[0] + R2[3 + j] * p[1] + R2[6 + j] * p[2];
+    double e2 = A[0] * Qm[j] + A[1] * Qm[3 + j] + A[2] * Qm[6 + j] + B[j];
+    double s2 = fabs(e1) - e2;
+    if (s2 > s) { s = s2; normalBox = 2; normalCol = j; invertNormal = e1 < 0; code = 4 + j; }
+  }
+  const double R11 = Rm[0], R12 = Rm[1], R13 = Rm[2], R21 = Rm[3], R22 = Rm[4], R23 = Rm[5], R31 = Rm[6],
+               R32 = Rm[7], R33 = Rm[8];
+  const double Q11 = Qm[0], Q12 = Qm[1], Q13 = Qm[2], Q21 = Qm[3], Q22 = Qm[4], Q23 = Qm[5], Q31 = Qm[6],
+               Q32 = Qm[7], Q33 = Qm[8];
+  const double E1[9] = {pp[2] * R21 - pp[1] * R31, pp[2] * R22 - pp[1] * R32, pp[2] * R23 - pp[1] * R33,
+                        pp[0] * R31 - pp[2] * R11, pp[0] * R32 - pp[2] * R12, pp[0] * R33 - pp[2] * R13,
+                        pp[1] * R11 - pp[0] * R21, pp[1] * R12 - pp[0] * R22, pp[1] * R13 - pp[0] * R23};
+  const double E2[9] = {A[1] * Q31 + A[2] * Q21 + B[1] * Q13 + B[2] * Q12,
+                        A[1] * Q32 + A[2] * Q22 + B[0] * Q13 + B[2] * Q11,
+                        A[1] * Q33 + A[2] * Q23 + B[0] * Q12 + B[1] * Q11,
+                        A[0] * Q31 + A[2] * Q11 + B[1] * Q23 + B[2] * Q22,
+                        A[0] * Q32 + A[2] * Q12 + B[0] * Q23 + B[2] * Q21,
+                        A[0] * Q33 + A[2] * Q13 + B[0] * Q22 + B[1] * Q21,
+                        A[0] * Q21 + A[1] * Q11 + B[1] * Q33 + B[2] * Q32,
+                        A[0] * Q22 + A[1] * Q12 + B[0] * Q33 + B[2] * Q31,
+                        A[0] * Q23 + A[1] * Q13 + B[0] * Q32 + B[1] * Q31};
+  const double NN[27] = {0, -R31, R21, 0, -R32, R22, 0, -R33, R23,
+                         R31, 0, -R11, R32, 0, -R12, R33, 0, -R13,
+                         -R21, R11, 0, -R22, R12, 0, -R23, R13, 0};
+  for (int t = 0; t < 9; t++) {
+    double s2 = fabs(E1[t]) - E2[t];
+    const double n1 = NN[3 * t], n2 = NN[3 * t + 1], n3 = NN[3 * t + 2];
+    double l = sqrt(n1 * n1 + n2 * n2 + n3 * n3);
+    if (l > 0) {
+      s2 /= l;
+      if (s2 * fudge > s) {
+        s = s2; normalCol = -1; normalC[0] = n1 / l; normalC[1] = n2 / l; normalC[2] = n3 / l;
+        invertNormal = E1[t] < 0; code = 7 + t;
+      }
+    }
+  }
+  if (!code || s > 0.0) return 0;
+  double normal[3];
+  if (normalCol >= 0) {
+    const double* R = normalBox == 1 ? R1 : R2;
+    normal[0] = R[normalCol]; normal[1] = R[3 + normalCol]; normal[2] = R[6 + normalCol];
+  } else {
+    for (int i = 0; i < 3; i++) normal[i] = R1[i * 3] * normalC[0] + R1[i * 3 + 1] * normalC[1] + R1[i * 3 + 2] * normalC[2];
+    double l = sqrt(normal[0] * normal[0] + normal[1] * normal[1] + normal[2] * normal[2]);
+    for (int i = 0; i < 3; i++) normal[i] /= l;
+  }
+  if (invertNormal) for (int i = 0; i < 3; i++) normal[i] = -normal[i];
+  if (code > 6) {
+    double pa[3] = {p1[0], p1[1], p1[2]}, pb[3] = {p2[0], p2[1], p2[2]};
+    for (int j = 0; j < 3; j++) {
+      double v = normal[0] * R1[j] + normal[1] * R1[3 + j] + normal[2] * R1[6 + j];
+      double sign = (v > -1e-10) ? 1.0 : -1.0;
+      for (int i = 0; i < 3; i++) pa[i] += sign * A[j] * R1[i * 3 + j];
+    }
+    for (int j = 0; j < 3; j++) {
+      double v = normal[0] * R2[j] + normal[1] * R2[3 + j] + normal[2] * R2[6 + j];
+      double sign = (v > -1e-3) ? -1.0 : 1.0;
+      for (int i = 0; i < 3; i++) pb[i] += sign * B[j] * R2[i * 3 + j];
+    }
+    const int ca = (code - 7) / 3, cb = (code - 7) % 3;
+    double ua[3] = {R1[ca], R1[3 + ca], R1[6 + ca]}, ub[3] = {R2[cb], R2[3 + cb], R2[6 + cb]};
+    double pd[3] = {pb[0] - pa[0], pb[1] - pa[1], pb[2] - pa[2]};
+    double uaub = dot3(ua, ub), q1 = dot3(ua, pd), q2 = -dot3(ub, pd);
+    double dd = 1 - uaub * uaub, alpha = 0, beta = 0;
+    if (dd > 0) { dd = 1.0 / dd; alpha = (q1 + uaub * q2) * dd; beta = (uaub * q1 + q2) * dd; }
+    for (int i = 0; i < 3; i++) { pa[i] += ua[i] * alpha; pb[i] += ub[i] * beta; }
+    if (-s > clipDepth) return 0;
+    for (int i = 0; i < 3; i++) { out[i] = 0.5 * (pa[i] + pb[i]); out[3 + i] = -normal[i]; }
+    out[6] = -s; out[7] = CT_EDGE_EDGE; out[8] = b1; out[9] = b2;
+    return 1;
+  }
+  const double *Ra, *Rb, *pa, *pb, *Sa, *Sb;
+  const bool flip = code > 3;
+  if (!flip) { Ra = R1; Rb = R2; pa = p1; pb = p2; Sa = A; Sb = B; }
+  else { Ra = R2; Rb = R1; pa = p2; pb = p1; Sa = B; Sb = A; }
+  double normal2[3], nr[3], anr[3];
+  for (int i = 0; i < 3; i++) normal2[i] = flip ? -normal[i] : normal[i];
+  for (int i = 0; i < 3; i++) nr[i] = Rb[i] * normal2[0] + Rb[3 + i] * normal2[1] + Rb[6 + i] * normal2[2];
+  for (int i = 0; i < 3; i++) anr[i] = fabs(nr[i]);
+  int lanr, a1, a2;
+  if (anr[1] > anr[0]) {
+    if (anr[1] > anr[2]) { a1 = 0; lanr = 1; a2 = 2; } else { a1 = 0; a2 = 1; lanr = 2; }
+  } else {
+    if (anr[0] > anr[2]) { lanr = 0; a1 = 1; a2 = 2; } else { a1 = 0; a2 = 1; lanr = 2; }
+  }
+  double center[3];
+  for (int i = 0; i < 3; i++)
+    center[i] = nr[lanr] < 0 ? pb[i] - pa[i] + Sb[lanr] * Rb[i * 3 + lanr] : pb[i] - pa[i] - Sb[lanr] * Rb[i * 3 + lanr];
+  const int codeN = flip ? code - 4 : code - 1;
+  const int code1 = codeN == 0 ? 1 : 0, code2 = codeN == 2 ? 1 : 2;
+  double c1 = center[0] * Ra[code1] + center[1] * Ra[3 + code1] + center[2] * Ra[6 + code1];
+  double c2 = center[0] * Ra[code2] + center[1] * Ra[3 + code2] + center[2] * Ra[6 + code2];
+  double m11 = Ra[code1] * Rb[a1] + Ra[3 + code1] * Rb[3 + a1] + Ra[6 + code1] * Rb[6 + a1];
+  double m12 = Ra[code1] * Rb[a2] + Ra[3 + code1] * Rb[3 + a2] + Ra[6 + code1] * Rb[6 + a2];
+  double m21 = Ra[code2] * Rb[a1] + Ra[3 + code2] * Rb[3 + a1] + Ra[6 + code2] * Rb[6 + a1];
+  double m22 = Ra[code2] * Rb[a2] + Ra[3 + code2] * Rb[3 + a2] + Ra[6 + code2] * Rb[6 + a2];
+  double quad[8];
+  {
+    double k1 = m11 * Sb[a1], k2 = m21 * Sb[a1], k3 = m12 * Sb[a2], k4 = m22 * Sb[a2];
+    quad[0] = c1 - k1 - k3; quad[1] = c2 - k2 - k4;
+    quad[2] = c1 - k1 + k3; quad[3] = c2 - k2 + k4;
+    quad[4] = c1 + k1 + k3; quad[5] = c2 + k2 + k4;
+    quad[6] = c1 + k1 - k3; quad[7] = c2 + k2 - k4;
+  }
+  double rect[2] = {Sa[code1], Sa[code2]};
+  // intersectRectQuad with ping-pong buffers (bufA/bufB), as in the reference
+  double bufA[16], bufB[16];
+  for (int i = 0; i < 8; i++) bufB[i] = quad[i];
+  // q starts at quad (kept in bufB), r at ret (bufA)
+  double* q = bufB;
+  double* r = bufA;
+  int nq = 4, nrr = 0;
+  bool stop = false;
+  for (int dir = 0; dir <= 1 && !stop; dir++) {
+    for (int sign = -1; sign <= 1 && !stop; sign += 2) {
+      double* pq = q;
+      double* pr = r;
+      nrr = 0;
+      for (int i = nq; i > 0; i--) {
+        if (sign * pq[dir] < rect[dir]) {
+          pr[0] = pq[0]; pr[1] = pq[1]; pr += 2; nrr++;
+          if (nrr & 8) { q = r; stop = true; break; }
+        }
+        double* nextq = (i > 1) ? pq + 2 : q;
+        if ((sign * pq[dir] < rect[dir]) ^ (sign * nextq[dir] < rect[dir])) {
+          pr[1 - dir] = pq[1 - dir] + (nextq[1 - dir] - pq[1 - dir]) / (nextq[dir] - pq[dir]) * (sign * rect[dir] - pq[dir]);
+          pr[dir] = sign * rect[dir];
+          pr += 2; nrr++;
+          if (nrr & 8) { q = r; stop = true; break; }
+        }
+        pq += 2;
+      }
+      if (stop) break;
+      q = r;
+      r = (q == bufA) ? bufB : bufA;
+      nq = nrr;
+    }
+  }
+  double* ret = q;  // final polygon
+  if (nrr < 1) return 0;
+  double det1 = 1.0 / (m11 * m22 - m12 * m21);
+  m11 *= det1; m12 *= det1; m21 *= det1; m22 *= det1;
+  int cnum = 0;
+  for (int j = 0; j < nrr; j++) {
+    double k1 = m22 * (ret[j * 2] - c1) - m12 * (ret[j * 2 + 1] - c2);
+    double k2 = -m21 * (ret[j * 2] - c1) + m11 * (ret[j * 2 + 1] - c2);
+    double pt[3];
+    for (int i = 0; i < 3; i++) pt[i] = center[i] + k1 * Rb[i * 3 + a1] + k2 * Rb[i * 3 + a2];
+    double dep = Sa[codeN] - dot3(normal2, pt);
+    if (dep >= 0) {
+      double* o = out + CREC * cnum;
+      double xx = ret[j * 2], yy = ret[j * 2 + 1];
+      for (int i = 0; i < 3; i++) { o[i] = pt[i] + pa[i]; o[3 + i] = -normal[i]; }
+      o[6] = dep;
+      bool onX = fabs(xx) == rect[0], onY = fabs(yy) == rect[1];
+      int type;
+      if (onX && onY) {
+        if (flip) { type = CT_FACE_VERTEX; for (int i = 0; i < 3; i++) o[i] += o[3 + i] * dep; }
+        else { type = CT_VERTEX_FACE; for (int i = 0; i < 3; i++) o[i] -= o[3 + i] * dep; }
+      } else if (!onX && !onY) {
+        type = flip ? CT_VERTEX_FACE : CT_FACE_VERTEX;
+      } else {
+        type = CT_EDGE_EDGE;
+      }
+      o[7] = type; o[8] = b1; o[9] = b2;
+      cnum++;
+    }
+  }
+  return cnum;
+}
+
+// ContactConstraint::getTangentBasisMatrixODE (ContactConstraint.cpp:705)
+__device__ void tangentBasisODE(const double* n, double* t1, double* t2) {
+#pragma clang fp contract(off)
+  const double ez[3] = {0, 0, 1}, ex[3] = {1, 0, 0}, ey[3] = {0, 1, 0};
+  double t[3];
+  cross3(ez, n, t);
+  if (dot3(t, t) < 1e-12) {
+    cross3(ex, n, t);
+    if (dot3(t, t) < 1e-12) {
+      cross3(ey, n, t);
+      if (dot3(t, t) < 1e-12) cross3(ez, n, t);
+    }
+  }
+  double l = sqrt(dot3(t, t));
+  for (int i = 0; i < 3; i++) t1[i] = t[i] / l;
+  cross3(n, t1, t2);
+}
+
+// ---------------------------------------------------------------------------
+// Per-world LCP workspace, carved at run time for the actual row count m.
+// It lives in LDS when it fits the model's LDS pool and otherwise in the
+// world's snapshot tail in HBM (same code, different base pointer).
+// ---------------------------------------------------------------------------
+
+struct FwdPool {
+  double *cols, *massed, *A, *M1, *M2;
+  double *lo, *hi, *b, *X, *aCol, *rest, *pen, *relVel, *fc, *Eval, *nx, *fsol, *xc, *dvec;
+  int *fi, *mapping, *clampIdx, *ubIdx, *rowC, *rowDir, *clampRow, *cl;
+  double* scr;  // >= 24 m + 2 n + 16
+};
+
+__device__ inline void carveFwd(double* base, int m, int n, FwdPool& P) {
+  double* p = base;
+  P.cols = p; p += n * m;
+  P.massed = p; p += n * m;
+  P.A = p; p += m * m;
+  P.M1 = p; p += m * m;
+  P.M2 = p; p += m * m;
+  double** vecs[] = {&P.lo, &P.hi, &P.b, &P.X, &P.aCol, &P.rest, &P.pen, &P.relVel, &P.fc, &P.Eval, &P.nx, &P.fsol, &P.xc};
+  for (double** v : vecs) { *v = p; p += m; }
+  P.dvec = p; p += 3 * m;
+  int* ip = reinterpret_cast<int*>(p);
+  int** ivecs[] = {&P.fi, &P.mapping, &P.clampIdx, &P.ubIdx, &P.rowC, &P.rowDir, &P.clampRow, &P.cl};
+  for (int** v : ivecs) { *v = ip; ip += m; }
+  p += 4 * m;
+  P.scr = p;
+}
+
+// ---------------------------------------------------------------------------
+// Complete orthogonal decomposition (Eigen::CompleteOrthogonalDecomposition,
+// used by the reference for Q^+ b at ConstrainedGroupGradientMatrices.cpp:270
+// and BackpropSnapshot.cpp:2747): column-pivoted Householder QR, rank =
+// #{|R_kk| > eps * min(m,n) * max|R_kk|}, then RZ on the leading r rows.
+// Factorisation is lane-parallel over columns / rows; solves are per lane.
+// A is m x n with leading dimension ld; reflectors are stored in place.
+// ---------------------------------------------------------------------------
+struct Cod {
+  double* A;
+  int m, n, ld, kmax;
+  int* perm;        // n
+  double* vd;       // kmax  QR reflector heads
+  double* vn;       // kmax  QR reflector norms (<= 0: skipped)
+  double* zd;       // m     RZ reflector heads
+  double* zn;       // m     RZ reflector norms
+  int* rank;        // 1
+};
+
+// carve a Cod workspace from `w` (needs 6*max(m,n) + 8 doubles + the v vector)
+__device__ inline double* carveCod(double* w, double* A, int m, int n, int ld, Cod& c) {
+  const int mx = m > n ? m : n;
+  c.A = A; c.m = m; c.n = n; c.ld = ld; c.kmax = m < n ? m : n;
+  c.vd = w; w += mx;
+  c.vn = w; w += mx;
+  c.zd = w; w += mx;
+  c.zn = w; w += mx;
+  c.perm = reinterpret_cast<int*>(w); w += (mx + 1) / 2 + 1;
+  c.rank = reinterpret_cast<int*>(w); w += 2;
+  return w;
+}
+
+// `cn` and `v` are scratch vectors of n and m doubles.
+__device__ void codFactor(Cod& c, double* cn, double* v, int lane) {
+  double* A = c.A;
+  const int m = c.m, n = c.n, ld = c.ld;
+  for (int j = lane; j < n; j += WAVE) c.perm[j] = j;
+  __syncthreads();
+  double maxPivot = 0.0;
+  for (int k = 0; k < c.kmax; k++) {
+    for (int j = k + lane; j < n; j += WAVE) {
+      double sc = 0;
+      for (int i = k; i < m; i++) sc += A[i * ld + j] * A[i * ld + j];
+      cn[j] = sc;
+    }
+    __syncthreads();
+    int p = k;
+    double best = -1;
+    for (int j = k; j < n; j++)
+      if (cn[j] > best) { best = cn[j]; p = j; }
+    if (p != k) {
+      for (int i = lane; i < m; i += WAVE) {
+        double t = A[i * ld + k]; A[i * ld + k] = A[i * ld + p]; A[i * ld + p] = t;
+      }
+      if (lane == 0) { int t = c.perm[k]; c.perm[k] = c.perm[p]; c.perm[p] = t; }
+    }
+    __syncthreads();
+    double alpha = 0;
+    for (int i = k; i < m; i++) alpha += A[i * ld + k] * A[i * ld + k];
+    alpha = sqrt(alpha);
+    if (alpha == 0.0) {
+      if (lane == 0) c.vn[k] = -1.0;
+      __syncthreads();
+      continue;
+    }
+    if (A[k * ld + k] > 0) alpha = -alpha;
+    for (int i = k + lane; i < m; i += WAVE) v[i] = A[i * ld + k] - (i == k ? alpha : 0.0);
+    __syncthreads();
+    double vnorm = 0;
+    for (int i = k; i < m; i++) vnorm += v[i] * v[i];
+    if (vnorm > 0) {
+      for (int j = k + lane; j < n; j += WAVE) {
+        double sc = 0;
+        for (int i = k; i < m; i++) sc += v[i] * A[i * ld + j];
+        sc = 2 * sc / vnorm;
+        for (int i = k; i < m; i++) A[i * ld + j] -= sc * v[i];
+      }
+    }
+    __syncthreads();
+    maxPivot = fmax(maxPivot, fabs(A[k * ld + k]));
+    for (int i = k + 1 + lane; i < m; i += WAVE) A[i * ld + k] = v[i];
+    if (lane == 0) { c.vd[k] = v[k]; c.vn[k] = vnorm; }
+    __syncthreads();
+  }
+  const double thr = 2.220446049250313e-16 * c.kmax * maxPivot;
+  int r = 0;
+  for (int k = 0; k < c.kmax; k++)
+    if (fabs(A[k * ld + k]) > thr) r++;
+  if (lane == 0) *c.rank = r;
+  // RZ: reflect row i over columns {i} U {r..n-1}; row i's trailing part is
+  // kept as the reflector
+  for (int i = r - 1; i >= 0 && r < n; i--) {
+    double al = A[i * ld + i] * A[i * ld + i];
+    for (int j = r; j < n; j++) al += A[i * ld + j] * A[i * ld + j];
+    al = sqrt(al);
+    if (A[i * ld + i] > 0) al = -al;
+    const double vi = A[i * ld + i] - al;
+    double vnz = vi * vi;
+    for (int j = r; j < n; j++) vnz += A[i * ld + j] * A[i * ld + j];
+    __syncthreads();
+    if (lane == 0) { c.zd[i] = vi; c.zn[i] = vnz; }
+    if (vnz != 0) {
+      for (int row = lane; row <= i; row += WAVE) {
+        double sc = A[row * ld + i] * vi;
+        for (int j = r; j < n; j++) sc += A[row * ld + j] * A[i * ld + j];
+        sc = 2 * sc / vnz;
+        A[row * ld + i] -= sc * vi;
+        if (row < i)
+          for (int j = r; j < n; j++) A[row * ld + j] -= sc * A[i * ld + j];
+      }
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+}
+
+// x (n) = min-norm least-squares solution for rhs (m, destroyed); z: n scratch.
+__device__ void codSolveOne(const Cod& c, double* rhs, double* x, double* z) {
+  const double* A = c.A;
+  const int m = c.m, n = c.n, ld = c.ld;
+  for (int k = 0; k < c.kmax; k++) {
+    const double vnorm = c.vn[k];
+    if (!(vnorm > 0)) continue;
+    double sc = c.vd[k] * rhs[k];
+    for (int i = k + 1; i < m; i++) sc += A[i * ld + k] * rhs[i];
+    sc = 2 * sc / vnorm;
+    rhs[k] -= sc * c.vd[k];
+    for (int i = k + 1; i < m; i++) rhs[i] -= sc * A[i * ld + k];
+  }
+  const int r = *c.rank;
+  for (int j = 0; j < n; j++) z[j] = 0.0;
+  for (int i = r - 1; i >= 0; i--) {
+    double sc = rhs[i];
+    for (int j = i + 1; j < r; j++) sc -= A[i * ld + j] * z[j];
+    z[i] = sc / A[i * ld + i];
+  }
+  for (int i = 0; i < r && r < n; i++) {
+    const double vn = c.zn[i];
+    if (vn == 0) continue;
+    double sc = z[i] * c.zd[i];
+    for (int j = r; j < n; j++) sc += z[j] * A[i * ld + j];
+    sc = 2 * sc / vn;
+    z[i] -= sc * c.zd[i];
+    for (int j = r; j < n; j++) z[j] -= sc * A[i * ld + j];
+  }
+  for (int j = 0; j < n; j++) x[c.perm[j]] = z[j];
+}
+
+// ---------------------------------------------------------------------------
+// Dantzig boxed LCP (dart/external/odelcpsolver/lcp.cpp:780 dSolveLCP) on a
+// full, explicitly permuted LDS matrix.  Sequential pivoting: lane 0 only.
+// ---------------------------------------------------------------------------
+struct DevDantzig {
+  int n, nC, nN;
+  double *A, *x, *b, *w, *lo, *hi, *L, *d, *Dell, *ell, *tmp, *W1, *W2, *ta;
+  int *findex, *p, *C, *state;
+
+  __device__ double& Aat(int i, int j) { return A[i * n + j]; }
+  __device__ void swapD(double* a, int i, int j) { double t = a[i]; a[i] = a[j]; a[j] = t; }
+  __device__ void swapI(int* a, int i, int j) { int t = a[i]; a[i] = a[j]; a[j] = t; }
+  __device__ void swapProblem(int i1, int i2) {
+    if (i1 == i2) return;
+    for (int k = 0; k < n; k++) swapD(A, i1 * n + k, i2 * n + k);
+    for (int k = 0; k < n; k++) swapD(A, k * n + i1, k * n + i2);
+    swapD(x, i1, i2); swapD(b, i1, i2); swapD(w, i1, i2); swapD(lo, i1, i2); swapD(hi, i1, i2);
+    swapI(p, i1, i2); swapI(state, i1, i2); swapI(findex, i1, i2);
+  }
+  __device__ void solveL1(double* B, int m) {
+    for (int i = 0; i < m; i++) {
+      double s = B[i];
+      for (int k = 0; k < i; k++) s -= L[i * n + k] * B[k];
+      B[i] = s;
+    }
+  }
+  __device__ void solveL1T(double* B, int m) {
+    for (int i = m - 1; i >= 0; i--) {
+      double s = B[i];
+      for (int k = i + 1; k < m; k++) s -= L[k * n + i] * B[k];
+      B[i] = s;
+    }
+  }
+  __device__ void transferToC(int i) {
+    if (nC > 0) {
+      for (int j = 0; j < nC; j++) L[nC * n + j] = ell[j];
+      double dd = 0;
+      for (int j = 0; j < nC; j++) dd += ell[j] * Dell[j];
+      d[nC] = 1.0 / (Aat(i, i) - dd);
+    } else {
+      d[0] = 1.0 / Aat(i, i);
+    }
+    swapProblem(nC, i);
+    C[nC] = nC;
+    nC++;
+  }
+  __device__ void transferFromNtoC(int i) {
+    if (nC > 0) {
+      for (int j = 0; j < nC; j++) Dell[j] = Aat(i, C[j]);
+      solveL1(Dell, nC);
+      for (int j = 0; j < nC; j++) L[nC * n + j] = ell[j] = Dell[j] * d[j];
+      double dd = 0;
+      for (int j = 0; j < nC; j++) dd += ell[j] * Dell[j];
+      d[nC] = 1.0 / (Aat(i, i) - dd);
+    } else {
+      d[0] = 1.0 / Aat(i, i);
+    }
+    swapProblem(nC, i);
+    C[nC] = nC;
+    nN--;
+    nC++;
+  }
+  // _dLDLTAddTL (dart/external/odelcpsolver/matrix.cpp:286)
+  __device__ void ldltAddTL(double* Ls, double* ds, const double* a, int m) {
+    if (m < 2) return;
+    const double r2 = 0.70710678118654752440;
+    W1[0] = W2[0] = 0.0;
+    for (int j = 1; j < m; j++) W1[j] = W2[j] = a[j] * r2;
+    double W11 = (0.5 * a[0] + 1) * r2;
+    double W21 = (0.5 * a[0] - 1) * r2;
+    double alpha1 = 1.0, alpha2 = 1.0;
+    {
+      double dee = ds[0];
+      double alphanew = alpha1 + (W11 * W11) * dee;
+      dee /= alphanew;
+      double gamma1 = W11 * dee;
+      dee *= alpha1;
+      alpha1 = alphanew;
+      alphanew = alpha2 - (W21 * W21) * dee;
+      dee /= alphanew;
+      alpha2 = alphanew;
+      double k1 = 1.0 - W21 * gamma1;
+      double k2 = W21 * gamma1 * W11 - W21;
+      for (int q = 1; q < m; q++) {
+        double Wp = W1[q];
+        double el = Ls[q * n];
+        W1[q] = Wp - W11 * el;
+        W2[q] = k1 * Wp + k2 * el;
+      }
+    }
+    for (int j = 1; j < m; j++) {
+      double k1 = W1[j], k2 = W2[j];
+      double dee = ds[j];
+      double alphanew = alpha1 + (k1 * k1) * dee;
+      dee /= alphanew;
+      double gamma1 = k1 * dee;
+      dee *= alpha1;
+      alpha1 = alphanew;
+      alphanew = alpha2 - (k2 * k2) * dee;
+      dee /= alphanew;
+      double gamma2 = k2 * dee;
+      dee *= alpha2;
+      ds[j] = dee;
+      alpha2 = alphanew;
+      for (int q = j + 1; q < m; q++) {
+        double el = Ls[q * n + j];
+        double Wp = W1[q] - k1 * el;
+        el += gamma1 * Wp;
+        W1[q] = Wp;
+        Wp = W2[q] - k2 * el;
+        el -= gamma2 * Wp;
+        W2[q] = Wp;
+        Ls[q * n + j] = el;
+      }
+    }
+  }
+  // _dLDLTRemove (matrix.cpp:374) + _dRemoveRowCol
+  __device__ void ldltRemove(int r, int n2) {
+    if (r != n2 - 1) {
+      if (r == 0) {
+        for (int i = 0; i < n2; i++) ta[i] = -Aat(C[i], C[0]);
+        ta[0] += 1.0;
+        ldltAddTL(L, d, ta, n2);
+      } else {
+        // t (first r) then a (n2 - r) share `ta`: t in tmp
+        for (int i = 0; i < r; i++) tmp[i] = L[r * n + i] / d[i];
+        for (int i = 0; i < n2 - r; i++) {
+          double s = 0;
+          for (int k = 0; k < r; k++) s += L[(r + i) * n + k] * tmp[k];
+          ta[i] = s - Aat(C[r + i], C[r]);
+        }
+        ta[0] += 1.0;
+        ldltAddTL(L + r * n + r, d + r, ta, n2 - r);
+      }
+    }
+    if (r < n2 - 1) {
+      for (int i = 0; i < n2; i++)
+        for (int j = r; j < n2 - 1; j++) L[i * n + j] = L[i * n + j + 1];
+      for (int i = r; i < n2 - 1; i++)
+        for (int j = 0; j < n2; j++) L[i * n + j] = L[(i + 1) * n + j];
+      for (int i = r; i < n2 - 1; i++) d[i] = d[i + 1];
+    }
+  }
+  __device__ void transferFromCtoN(int i) {
+    int j = 0, lastIdx = -1;
+    for (; j < nC; j++) {
+      if (C[j] == nC - 1) lastIdx = j;
+      if (C[j] == i) {
+        ldltRemove(j, nC);
+        int k;
+        if (lastIdx == -1) {
+          for (k = j + 1; k < nC; k++)
+            if (C[k] == nC - 1) break;
+        } else {
+          k = lastIdx;
+        }
+        C[k] = C[j];
+        for (int t = j; t < nC - 1; t++) C[t] = C[t + 1];
+        break;
+      }
+    }
+    swapProblem(i, nC - 1);
+    nN++;
+    nC--;
+  }
+  __device__ void solve1(double* a, int i, int dir, bool onlyTransfer) {
+    if (nC > 0) {
+      for (int j = 0; j < nC; j++) Dell[j] = Aat(i, C[j]);
+      solveL1(Dell, nC);
+      for (int j = 0; j < nC; j++) ell[j] = Dell[j] * d[j];
+      if (!onlyTransfer) {
+        for (int j = 0; j < nC; j++) tmp[j] = ell[j];
+        solveL1T(tmp, nC);
+        if (dir > 0)
+          for (int j = 0; j < nC; j++) a[C[j]] = -tmp[j];
+        else
+          for (int j = 0; j < nC; j++) a[C[j]] = tmp[j];
+      }
+    }
+  }
+  __device__ double AiC_qC(int i, const double* q) { double s = 0; for (int j = 0; j < nC; j++) s += Aat(i, j) * q[j]; return s; }
+  __device__ double AiN_qN(int i, const double* q) { double s = 0; for (int j = nC; j < nC + nN; j++) s += Aat(i, j) * q[j]; return s; }
+};
+
+// Solve with early termination (the contact solver's setting).  On entry A
+// (n x n, destroyed), b, lo, hi, findex are the problem; x receives the
+// solution.  scr: 16 n doubles; iscr: 4 n ints.  Lane 0 only.
+__device__ bool devDantzig(int n, double* A, double* x, double* b, double* lo, double* hi, int* findex, double* Lbuf,
+                           double* scr, int* iscr) {
+  const double kInf = __builtin_inf();
+  DevDantzig D;
+  D.n = n; D.nC = 0; D.nN = 0;
+  D.A = A; D.x = x; D.b = b; D.lo = lo; D.hi = hi; D.findex = findex; D.L = Lbuf;
+  D.w = scr; D.d = scr + n; D.Dell = scr + 2 * n; D.ell = scr + 3 * n; D.tmp = scr + 4 * n;
+  D.W1 = scr + 5 * n; D.W2 = scr + 6 * n; D.ta = scr + 7 * n;
+  double* delta_x = scr + 8 * n;
+  double* delta_w = scr + 9 * n;
+  double* tcopy = scr + 10 * n;
+  D.p = iscr; D.C = iscr + n; D.state = iscr + 2 * n;
+  for (int k = 0; k < n * n; k++) Lbuf[k] = 0.0;
+  for (int k = 0; k < n; k++) {
+    x[k] = 0.0; D.p[k] = k; D.C[k] = 0; D.state[k] = 0;
+    D.w[k] = D.d[k] = D.Dell[k] = D.ell[k] = D.tmp[k] = 0.0;
+    delta_x[k] = delta_w[k] = 0.0;
+  }
+  for (int k = 0; k < n; k++) {
+    if (findex[k] >= 0) continue;
+    if (lo[k] == -kInf && hi[k] == kInf) return false;  // unbounded rows never occur for contacts
+  }
+  {
+    int numAtEnd = 0;
+    for (int k = n - 1; k >= 0; k--)
+      if (findex[k] >= 0) { D.swapProblem(k, n - 1 - numAtEnd); numAtEnd++; }
+  }
+  double* w = D.w;
+  bool hitFirstFriction = false;
+  for (int i = 0; i < n; i++) {
+    bool sError = false;
+    if (!hitFirstFriction && findex[i] >= 0) {
+      for (int j = 0; j < n; j++) delta_w[D.p[j]] = x[j];
+      for (int k = i; k < n; k++) {
+        double wfk = delta_w[findex[k]];
+        if (wfk == 0) { hi[k] = 0; lo[k] = 0; }
+        else { hi[k] = fabs(hi[k] * wfk); lo[k] = -hi[k]; }
+      }
+      hitFirstFriction = true;
+    }
+    w[i] = D.AiC_qC(i, x) + D.AiN_qN(i, x) - b[i];
+    if (lo[i] == 0 && w[i] >= 0) {
+      D.nN++;
+      D.state[i] = 0;
+    } else if (hi[i] == 0 && w[i] <= 0) {
+      D.nN++;
+      D.state[i] = 1;
+    } else if (w[i] == 0) {
+      D.solve1(delta_x, i, 0, true);
+      D.transferToC(i);
+    } else {
+      for (;;) {
+        int dir;
+        double dirf;
+        if (w[i] <= 0) { dir = 1; dirf = 1.0; } else { dir = -1; dirf = -1.0; }
+        D.solve1(delta_x, i, dir, false);
+        for (int k = 0; k < D.nN; k++) delta_w[D.nC + k] = D.AiC_qC(D.nC + k, delta_x);
+        for (int k = 0; k < D.nN; k++) delta_w[D.nC + k] += dir > 0 ? D.Aat(i, D.nC + k) : -D.Aat(i, D.nC + k);
+        delta_w[i] = D.AiC_qC(i, delta_x) + D.Aat(i, i) * dirf;
+        int cmd = 1, si = 0;
+        double s = -w[i] / delta_w[i];
+        if (dir > 0) {
+          if (hi[i] < kInf) { double s2 = (hi[i] - x[i]) * dirf; if (s2 < s) { s = s2; cmd = 3; } }
+        } else {
+          if (lo[i] > -kInf) { double s2 = (lo[i] - x[i]) * dirf; if (s2 < s) { s = s2; cmd = 2; } }
+        }
+        for (int k = 0; k < D.nN; k++) {
+          const int idx = D.nC + k;
+          if (!D.state[idx] ? delta_w[idx] < 0 : delta_w[idx] > 0) {
+            if (lo[idx] == 0 && hi[idx] == 0) continue;
+            double s2 = -w[idx] / delta_w[idx];
+            if (s2 < s) { s = s2; cmd = 4; si = idx; }
+          }
+        }
+        for (int k = 0; k < D.nC; k++) {
+          if (delta_x[k] < 0 && lo[k] > -kInf) {
+            double s2 = (lo[k] - x[k]) / delta_x[k];
+            if (s2 < s) { s = s2; cmd = 5; si = k; }
+          }
+          if (delta_x[k] > 0 && hi[k] < kInf) {
+            double s2 = (hi[k] - x[k]) / delta_x[k];
+            if (s2 < s) { s = s2; cmd = 6; si = k; }
+          }
+        }
+        if (s <= 0.0) return false;  // early termination
+        for (int k = 0; k < D.nC; k++) x[k] += s * delta_x[k];
+        x[i] += s * dirf;
+        for (int k = 0; k < D.nN; k++) w[D.nC + k] += s * delta_w[D.nC + k];
+        w[i] += s * delta_w[i];
+        switch (cmd) {
+          case 1: w[i] = 0; D.transferToC(i); break;
+          case 2: x[i] = lo[i]; D.state[i] = 0; D.nN++; break;
+          case 3: x[i] = hi[i]; D.state[i] = 1; D.nN++; break;
+          case 4: w[si] = 0; D.transferFromNtoC(si); break;
+          case 5: x[si] = lo[si]; D.state[si] = 0; D.transferFromCtoN(si); break;
+          case 6: x[si] = hi[si]; D.state[si] = 1; D.transferFromCtoN(si); break;
+        }
+        if (cmd <= 3) break;
+      }
+    }
+    if (sError) break;
+  }
+  for (int j = 0; j < n; j++) tcopy[j] = x[j];
+  for (int j = 0; j < n; j++) x[D.p[j]] = tcopy[j];
+  return true;
+}
+
+// PgsBoxedLcpSolver::solve (dart/constraint/PgsBoxedLcpSolver.cpp:85) with the
+// default option (30 iterations, 1e-6, 1e-3, 1e-9).  A, b modified.  Lane 0.
+__device__ bool devPgs(int n, double* A, double* x, double* b, const double* lo, const double* hi, const int* findex,
+                       int* order) {
+  const int maxIter = 30;
+  const double deltaXThr = 1e-6, relTol = 1e-3, epsDiv = 1e-9;
+  int no = 0;
+  bool possible = true;
+  for (int i = 0; i < n; i++) {
+    if (A[i * n + i] < epsDiv) { x[i] = 0.0; continue; }
+    order[no++] = i;
+    const double old = x[i];
+    double nx = b[i];
+    for (int j = 0; j < n; j++) if (j != i) nx -= A[i * n + j] * x[j];
+    nx /= A[i * n + i];
+    if (findex[i] >= 0) {
+      const double h = hi[i] * x[findex[i]], l = -h;
+      x[i] = nx > h ? h : (nx < l ? l : nx);
+    } else {
+      x[i] = nx > hi[i] ? hi[i] : (nx < lo[i] ? lo[i] : nx);
+    }
+    if (possible && fabs(x[i] - old) > deltaXThr) possible = false;
+  }
+  if (possible) return true;
+  for (int t = 0; t < no; t++) {
+    const int idx = order[t];
+    const double dummy = 1.0 / A[idx * n + idx];
+    b[idx] *= dummy;
+    for (int j = 0; j < n; j++) A[idx * n + j] *= dummy;
+  }
+  for (int iter = 1; iter < maxIter; iter++) {
+    possible = true;
+    for (int t = 0; t < no; t++) {
+      const int idx = order[t];
+      double nx = b[idx];
+      const double old = x[idx];
+      for (int j = 0; j < n; j++) if (j != idx) nx -= A[idx * n + j] * x[j];
+      if (findex[idx] >= 0) {
+        const double h = hi[idx] * x[findex[idx]], l = -h;
+        x[idx] = nx > h ? h : (nx < l ? l : nx);
+      } else {
+        x[idx] = nx > hi[idx] ? hi[idx] : (nx < lo[idx] ? lo[idx] : nx);
+      }
+      if (possible && fabs(x[idx]) > epsDiv) {
+        if (fabs((x[idx] - old) / x[idx]) > relTol) possible = false;
+      }
+    }
+    if (possible) break;
+  }
+  return possible;
+}
+
+// LCPUtils::isLCPSolutionValid (dart/neural/LCPUtils.cpp:14) for A + cfm I.
+__device__ bool devLcpValid(int m, const double* A, double cfm, const double* x, const double* b, const double* hi,
+                            const double* lo, const int* fi, bool ignoreFriction) {
+  for (int i = 0; i < m; i++) {
+    double v = -b[i];
+    for (int j = 0; j < m; j++) v += (A[i * m + j] + (i == j ? cfm : 0.0)) * x[j];
+    double up = hi[i], low = lo[i];
+    if (fi[i] != -1) {
+      if (ignoreFriction) { if (x[i] != 0) return false; continue; }
+      up *= x[fi[i]];
+      low *= x[fi[i]];
+    }
+    const double tol = 1e-5;
+    if (fabs(low) < tol && fabs(up) < tol && fabs(x[i]) < tol) {
+    } else if (fabs(x[i] - low) < tol) {
+      if (v < -tol) return false;
+    } else if (fabs(x[i] - up) < tol) {
+      if (v > tol) return false;
+    } else if (x[i] > low && x[i] < up) {
+      if (fabs(v) > tol) return false;
+    } else {
+      return false;
+    }
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// Contact-stage LDS header (at Layout::ct) and snapshot layout.
+// ---------------------------------------------------------------------------
+#define H_NCON 0
+#define H_M 1
+#define H_STATUS 2
+#define H_NDROP 3
+#define H_FLAG 4
+#define H_NC 5
+#define H_NU 6
+#define H_STD 7
+#define H_CFM 8
+#define H_SC 9
+#define H_IGN 10
+#define H_K 11
+#define H_PAIRCNT 16   // 16 per-pair counts of the current chunk
+
+// status bits
+#define ST_CONTACT_OVERFLOW 1
+#define ST_UNSUPPORTED_SHAPE 2
+#define ST_DROPPED_OVERFLOW 4
+#define ST_DUPLICATE_COLUMNS 8
+
+// row record fields
+#define RR_CONTACT 0
+#define RR_DIR 1
+#define RR_D 2
+#define RR_B 5
+#define RR_X 6
+#define RR_MAP 7
+#define RR_CIDX 8
+#define RR_UIDX 9
+#define RR_EVAL 10
+#define RR_BOUNCE 11
+
+// ---------------------------------------------------------------------------
+// Narrow phase over the candidate pairs + postProcess dedup + the
+// ConstraintSolver::updateConstraints filter.  Kept contacts land at
+// ct + CT_CONTACTS in detector order.
+// ---------------------------------------------------------------------------
+__device__ void collideWorld(const ModelDev& md, double* s, const Layout& L, int lane) {
+  double* ct = s + L.ct;
+  if (lane == 0) { ct[H_NCON] = 0; ct[H_NDROP] = 0; ct[H_STATUS] = 0; }
+  __syncthreads();
+  const int PC = md.pairChunk;
+  for (int p0 = 0; p0 < md.numPairs; p0 += PC) {
+    const int p = p0 + lane;
+    if (lane < PC && p < md.numPairs) {
+      const int si = md.pairA[p], sj = md.pairB[p];
+      const int bi = md.shapeBody[si], bj = md.shapeBody[sj];
+      int cnt = 0;
+      if (md.shapeType[si] == NIMBLE_SHAPE_BOX && md.shapeType[sj] == NIMBLE_SHAPE_BOX) {
+        double T1[12], T2[12];
+        tmul(s + L.Tw + 12 * bi, md.shapeT[si], T1);
+        tmul(s + L.Tw + 12 * bj, md.shapeT[sj], T2);
+        const double R1[9] = {T1[0], T1[1], T1[2], T1[4], T1[5], T1[6], T1[8], T1[9], T1[10]};
+        const double R2[9] = {T2[0], T2[1], T2[2], T2[4], T2[5], T2[6], T2[8], T2[9], T2[10]};
+        const double p1[3] = {T1[3], T1[7], T1[11]}, p2[3] = {T2[3], T2[7], T2[11]};
+        const double A[3] = {0.5 * md.shapeSize[si][0], 0.5 * md.shapeSize[si][1], 0.5 * md.shapeSize[si][2]};
+        const double B[3] = {0.5 * md.shapeSize[sj][0], 0.5 * md.shapeSize[sj][1], 0.5 * md.shapeSize[sj][2]};
+        cnt = deviceBoxBox(p1, R1, A, p2, R2, B, md.clipDepth, bi, bj, ct + CT_PAIRBUF + lane * 8 * CREC);
+      } else {
+        cnt = -1;
+      }
+      ct[H_PAIRCNT + lane] = cnt;
+    }
+    __syncthreads();
+    if (lane == 0) {
+      int nk = (int)ct[H_NCON], nd = (int)ct[H_NDROP], st = (int)ct[H_STATUS];
+      for (int q = 0; q < PC && p0 + q < md.numPairs; q++) {
+        const int cnt = (int)ct[H_PAIRCNT + q];
+        if (cnt < 0) { st |= ST_UNSUPPORTED_SHAPE; continue; }
+        for (int c = 0; c < cnt; c++) {
+          const double* rec = ct + CT_PAIRBUF + (q * 8 + c) * CREC;
+          bool close = false;
+          for (int t = 0; t < nk + nd && !close; t++) {
+            const double* o = t < nk ? ct + CT_CONTACTS + t * CREC : ct + CT_DROPPED + (t - nk) * CREC;
+            double dd = 0;
+            for (int i = 0; i < 3; i++) dd += (rec[i] - o[i]) * (rec[i] - o[i]);
+            if (sqrt(dd) < 3.0e-12) close = true;
+          }
+          if (close) continue;
+          const double nn = rec[3] * rec[3] + rec[4] * rec[4] + rec[5] * rec[5];
+          const int ba = (int)rec[8], bb = (int)rec[9];
+          const bool keep = !(nn < 1e-12) && !(rec[6] < 0.0) && !(rec[6] > md.clipDepth) &&
+                            (md.reactive[ba] || md.reactive[bb]);
+          double* dst = nullptr;
+          if (keep) {
+            if (nk < NIMBLE_MAX_CONTACTS) dst = ct + CT_CONTACTS + (nk++) * CREC;
+            else st |= ST_CONTACT_OVERFLOW;
+          } else {
+            if (nd < CT_MAX_DROPPED) {
+              // keep kept contacts contiguous: dropped list is separate
+              dst = ct + CT_DROPPED + (nd++) * CREC;
+            } else {
+              st |= ST_DROPPED_OVERFLOW;
+            }
+          }
+          if (dst)
+            for (int i = 0; i < CREC; i++) dst[i] = rec[i];
+        }
+      }
+      ct[H_NCON] = nk; ct[H_NDROP] = nd; ct[H_STATUS] = st;
+    }
+    __syncthreads();
+  }
+}
+
+// generalized force of a unit impulse along d at contact c (J^T e column entry
+// for dof i): sum over the reactive contact bodies of +-S_i . [p x d; d]
+__device__ inline double rowForceEntry(const ModelDev& md, const double* s, const Layout& L, const double* rec,
+                                       const double* d, int dof) {
+  const int body = md.dofBody[dof];
+  double wr[6];
+  cross3(rec, d, wr);
+  wr[3] = d[0]; wr[4] = d[1]; wr[5] = d[2];
+  const double sdot = dot6(s + L.Sw + 6 * dof, wr);
+  double val = 0.0;
+  const int ba = (int)rec[8], bb = (int)rec[9];
+  if (md.reactive[ba] && ((md.anc[ba] >> body) & 1ull)) val += sdot;
+  if (md.reactive[bb] && ((md.anc[bb] >> body) & 1ull)) val -= sdot;
+  return val;
+}
+
+// ---------------------------------------------------------------------------
+// ConstrainedGroupGradientMatrices::constructMatrices (:482) followed by
+// opportunisticallyStandardizeResults (:218), iterated while the
+// standardisation makes rows newly not-clamping (the reference recurses).
+// Q = A_cc + A_cu E + cfm I  (== A_c^T Minv A_c_ub_E + cfm I).
+// Returns the standardized flag (wave-uniform).
+// ---------------------------------------------------------------------------
+__device__ bool devConstruct(FwdPool& P, int m, double cfm, bool ignoreFriction, double* ct, int lane) {
+  for (int guard = 0; guard <= m + 1; guard++) {
+    if (lane == 0) {
+      const double TH = 1e-6;
+      int nc = 0, nu = 0;
+      for (int j = 0; j < m; j++) { P.mapping[j] = CM_NOT_CLAMPING; P.clampIdx[j] = -1; P.ubIdx[j] = -1; }
+      for (int j = 0; j < m; j++) {
+        if (P.aCol[j] < 1e-9) { P.mapping[j] = CM_NOT_CLAMPING; continue; }
+        const double f = P.X[j];
+        double up = P.hi[j], low = P.lo[j];
+        const int fp = P.fi[j];
+        if (fp != -1) { up *= P.X[fp]; low *= P.X[fp]; }
+        if (fabs(f) < TH) {
+          if (fp != -1) {
+            if (fabs(P.X[fp]) < TH) P.mapping[j] = CM_NOT_CLAMPING;
+            else if (ignoreFriction) P.mapping[j] = CM_NOT_CLAMPING;
+            else { P.mapping[j] = CM_CLAMPING; P.clampIdx[j] = nc++; }
+          } else {
+            P.mapping[j] = CM_NOT_CLAMPING;
+          }
+          continue;
+        }
+        const double tie = 1e-5;
+        if ((f > low + tie && f < up - tie) || (low - f > 1e-2 || f - up > 1e-2)) {
+          P.mapping[j] = CM_CLAMPING; P.clampIdx[j] = nc++;
+        } else if (fp != -1 && fabs(P.X[fp]) > 1e-9 && P.aCol[fp] > 1e-9 && (fp > j || P.mapping[fp] == CM_CLAMPING)) {
+          P.mapping[j] = fp; P.ubIdx[j] = nu++;
+        } else {
+          P.mapping[j] = CM_NOT_CLAMPING;
+        }
+      }
+      for (int j = 0; j < m; j++) {
+        if (P.mapping[j] == CM_CLAMPING) {
+          P.fc[P.clampIdx[j]] = P.X[j];
+          P.relVel[P.clampIdx[j]] = P.b[j];
+          P.clampRow[P.clampIdx[j]] = j;
+        }
+        P.Eval[j] = 0.0;
+        if (P.mapping[j] >= 0) {
+          const int fp = P.mapping[j];
+          const double up = P.X[fp] * P.hi[j], low = P.X[fp] * P.lo[j];
+          P.Eval[j] = fabs(P.X[j] - up) < fabs(P.X[j] - low) ? P.hi[j] : P.lo[j];
+        }
+      }
+      ct[H_NC] = nc; ct[H_NU] = nu;
+    }
+    __syncthreads();
+    const int nc = (int)ct[H_NC];
+    if (nc == 0) {
+      if (lane == 0) {
+        for (int j = 0; j < m; j++) P.nx[j] = 0.0;
+        const bool ok = devLcpValid(m, P.A, cfm, P.nx, P.b, P.hi, P.lo, P.fi, ignoreFriction);
+        if (ok) for (int j = 0; j < m; j++) P.X[j] = 0.0;
+        ct[H_STD] = ok ? 1 : 0;
+      }
+      __syncthreads();
+      return ct[H_STD] != 0;
+    }
+    // Q (nc x nc) into M1
+    double* Q = P.M1;
+    for (int t = lane; t < nc * nc; t += WAVE) {
+      const int cr = t / nc, cc = t % nc;
+      const int rr = P.clampRow[cr], rc = P.clampRow[cc];
+      double v = P.A[rr * m + rc];
+      for (int u = 0; u < m; u++)
+        if (P.mapping[u] >= 0 && P.clampIdx[P.mapping[u]] == cc) v += P.Eval[u] * P.A[rr * m + u];
+      if (cr == cc) v += cfm;
+      Q[t] = v;
+    }
+    __syncthreads();
+    Cod cod;
+    double* w = carveCod(P.scr, Q, nc, nc, nc, cod);
+    double* cn = w; w += m;
+    double* vv = w; w += m;
+    double* rhs = w; w += m;
+    double* z = w; w += m;
+    codFactor(cod, cn, vv, lane);
+    if (lane == 0) {
+      for (int i = 0; i < nc; i++) rhs[i] = P.relVel[i];
+      codSolveOne(cod, rhs, P.fsol, z);
+      bool anyNewlyNot = false;
+      for (int i = 0; i < m; i++) {
+        P.nx[i] = 0.0;
+        if (P.clampIdx[i] != -1) {
+          const double fi = P.fsol[P.clampIdx[i]];
+          P.nx[i] = fi;
+          if (fabs(fi) < 1e-6 && fabs(P.X[i]) > 1e-6 && P.fi[i] == -1) anyNewlyNot = true;
+        }
+        if (P.ubIdx[i] != -1) {
+          const int fp = P.fi[i];
+          const double om = P.fc[P.clampIdx[fp]] / P.X[i];
+          const double clean = fabs(om - P.hi[i]) < fabs(om - P.lo[i]) ? P.hi[i] : P.lo[i];
+          P.nx[i] = P.fsol[P.clampIdx[fp]] * clean;
+        }
+      }
+      const bool ok = devLcpValid(m, P.A, cfm, P.nx, P.b, P.hi, P.lo, P.fi, ignoreFriction);
+      int res = 0;
+      if (ok) {
+        for (int i = 0; i < m; i++) P.X[i] = P.nx[i];
+        for (int i = 0; i < nc; i++) P.fc[i] = P.fsol[i];
+        res = anyNewlyNot ? 2 : 1;
+      }
+      ct[H_STD] = res;
+    }
+    __syncthreads();
+    const int res = (int)ct[H_STD];
+    if (res != 2) return res != 0;
+  }
+  return false;
+}
+
+// guessSolution (LCPUtils.cpp:69): COD solve on {normal rows with b > 0} U
+// {friction rows}; result into x.
+__device__ void devGuess(FwdPool& P, int m, double* x, double* ct, int lane) {
+  if (lane == 0) {
+    int k = 0;
+    for (int i = 0; i < m; i++) {
+      if (P.fi[i] == -1) { if (P.b[i] > 0) P.cl[k++] = i; }
+      else P.cl[k++] = i;
+    }
+    ct[H_K] = k;
+  }
+  __syncthreads();
+  const int k = (int)ct[H_K];
+  for (int i = lane; i < m; i += WAVE) x[i] = 0.0;
+  if (k == 0) { __syncthreads(); return; }
+  double* Ar = P.M1;
+  for (int t = lane; t < k * k; t += WAVE) Ar[t] = P.A[P.cl[t / k] * m + P.cl[t % k]];
+  __syncthreads();
+  Cod cod;
+  double* w = carveCod(P.scr, Ar, k, k, k, cod);
+  double* cn = w; w += m;
+  double* vv = w; w += m;
+  double* rhs = w; w += m;
+  double* z = w; w += m;
+  double* xr = w; w += m;
+  codFactor(cod, cn, vv, lane);
+  if (lane == 0) {
+    for (int r = 0; r < k; r++) rhs[r] = P.b[P.cl[r]];
+    codSolveOne(cod, rhs, xr, z);
+    for (int r = 0; r < k; r++) x[P.cl[r]] = xr[r];
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// The whole constraint stage of one world (World.cpp:254 runConstraintEngine
+// on the hot path): rows, A = J Minv J^T, b, LCP with the short-circuit,
+// fallbacks, impulses (v1 += Minv J^T x), warm-start cache and snapshot.
+// `Lm` is the Cholesky factor of M (lower triangle, n x n).
+// ---------------------------------------------------------------------------
+__device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int lane, double* v1, double* cache,
+                             double* snap, double* overflowWs) {
+  const int n = md.n;
+  double* ct = s + L.ct;
+  const double* Lm = s + L.M;
+  collideWorld(md, s, L, lane);
+  const int nCon = (int)ct[H_NCON];
+  if (nCon == 0) {
+    if (lane == 0) {
+      for (int i = 0; i < 8; i++) snap[i] = 0.0;
+      snap[SN_STATUS] = ct[H_STATUS];
+    }
+    __syncthreads();
+    return;
+  }
+  // row count
+  if (lane == 0) {
+    int m = 0;
+    for (int c = 0; c < nCon; c++) {
+      const double* rec = ct + CT_CONTACTS + c * CREC;
+      const double mu = fmin(md.friction[(int)rec[8]], md.friction[(int)rec[9]]);
+      m += mu > 1e-3 ? 3 : 1;
+    }
+    ct[H_M] = m;
+  }
+  __syncthreads();
+  const int m = (int)ct[H_M];
+  FwdPool P;
+  const int need = fwdPoolDoubles(m, n);
+  carveFwd(need <= L.poolCap ? s + L.pool : overflowWs, m, n, P);
+  // rows (ContactConstraint: normal + 2 tangents with friction)
+  if (lane == 0) {
+    int r = 0;
+    for (int c = 0; c < nCon; c++) {
+      const double* rec = ct + CT_CONTACTS + c * CREC;
+      const int ba = (int)rec[8], bb = (int)rec[9];
+      const double mu = fmin(md.friction[ba], md.friction[bb]);
+      const double restC = md.restitution[ba] * md.restitution[bb];
+      const bool fr = mu > 1e-3;
+      const int base = r;
+      P.rowC[r] = c; P.rowDir[r] = 0;
+      for (int i = 0; i < 3; i++) P.dvec[3 * r + i] = rec[3 + i];
+      P.lo[r] = 0.0; P.hi[r] = __builtin_inf(); P.fi[r] = -1;
+      P.rest[r] = restC > 1e-3 ? restC : 0.0;
+      r++;
+      if (fr) {
+        double t1[3], t2[3];
+        tangentBasisODE(rec + 3, t1, t2);
+        for (int k = 0; k < 2; k++) {
+          P.rowC[r] = c; P.rowDir[r] = 1 + k;
+          for (int i = 0; i < 3; i++) P.dvec[3 * r + i] = k == 0 ? t1[i] : t2[i];
+          P.lo[r] = -mu; P.hi[r] = mu; P.fi[r] = base; P.rest[r] = 0.0;
+          r++;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // J^T columns
+  for (int t = lane; t < n * m; t += WAVE) {
+    const int i = t / m, j = t % m;
+    P.cols[t] = rowForceEntry(md, s, L, ct + CT_CONTACTS + P.rowC[j] * CREC, P.dvec + 3 * j, i);
+  }
+  __syncthreads();
+  // massed = Minv cols (one lane per column: L L^T x = c)
+  for (int j = lane; j < m; j += WAVE) {
+    double* x = P.massed;
+    for (int i = 0; i < n; i++) x[i * m + j] = P.cols[i * m + j];
+    for (int i = 0; i < n; i++) {
+      double sacc = x[i * m + j];
+      for (int k = 0; k < i; k++) sacc -= Lm[i * n + k] * x[k * m + j];
+      x[i * m + j] = sacc / Lm[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; i--) {
+      double sacc = x[i * m + j];
+      for (int k = i + 1; k < n; k++) sacc -= Lm[k * n + i] * x[k * m + j];
+      x[i * m + j] = sacc / Lm[i * n + i];
+    }
+  }
+  __syncthreads();
+  for (int t = lane; t < m * m; t += WAVE) {
+    const int r = t / m, c = t % m;
+    if (r <= c) {
+      double acc = 0;
+      for (int i = 0; i < n; i++) acc += P.cols[i * m + r] * P.massed[i * m + c];
+      P.A[r * m + c] = acc;
+      P.A[c * m + r] = acc;
+    }
+  }
+  for (int r = lane; r < m; r += WAVE) {
+    double acc = 0;
+    for (int i = 0; i < n; i++) acc += P.cols[i * m + r] * v1[i];
+    P.b[r] = -acc;
+  }
+  __syncthreads();
+  if (lane == 0) {
+    for (int r = 0; r < m; r++) {
+      P.pen[r] = 0.0;
+      if (P.rowDir[r] != 0) continue;
+      const double* rec = ct + CT_CONTACTS + P.rowC[r] * CREC;
+      double bv = rec[6];
+      if (bv < 0.0) bv = 0.0;
+      else { bv *= 0.01 / md.dt; if (bv > 1e-3) bv = 1e-3; }
+      if (!md.penCorr) bv = 0;
+      P.pen[r] = bv;
+      if (P.rest[r] > 0) {
+        const double rv = P.b[r] * P.rest[r];
+        if (rv > 1e-1 && rv > bv) { bv = rv > 1e2 ? 1e2 : rv; P.pen[r] = 0.0; }
+        else P.rest[r] = 0.0;
+      }
+      P.b[r] += bv;
+    }
+  }
+  __syncthreads();
+  for (int j = lane; j < m; j += WAVE) {
+    double acc = 0;
+    for (int i = 0; i < m; i++) acc += P.A[i * m + j] * P.A[i * m + j];
+    P.aCol[j] = acc;
+  }
+  __syncthreads();
+  // warm start (BoxedLcpConstraintSolver::mX) or guessSolution
+  const bool cached = (int)cache[0] == m;
+  if (cached) {
+    for (int i = lane; i < m; i += WAVE) { P.X[i] = cache[1 + i]; P.xc[i] = cache[1 + i]; }
+    __syncthreads();
+  } else {
+    devGuess(P, m, P.X, ct, lane);
+    for (int i = lane; i < m; i += WAVE) P.xc[i] = P.X[i];
+    __syncthreads();
+  }
+  bool success = devConstruct(P, m, 0.0, false, ct, lane);
+  const bool shortCircuit = success;
+  double cfm = 0.0;
+  bool ignoredFriction = false;
+  if (!success) {
+    // Dantzig on a copy (lane 0)
+    if (lane == 0) {
+      int st = (int)ct[H_STATUS];
+      for (int a = 0; a < m; a++)
+        for (int c = a + 1; c < m; c++) {
+          double dd = 0;
+          for (int i = 0; i < m; i++) dd += (P.A[i * m + a] - P.A[i * m + c]) * (P.A[i * m + a] - P.A[i * m + c]);
+          if (dd < 1e-4 && fabs(P.b[a] - P.b[c]) < 1e-4 && P.fi[a] == P.fi[c] && P.hi[a] == P.hi[c] &&
+              P.lo[a] == P.lo[c])
+            st |= ST_DUPLICATE_COLUMNS;
+        }
+      ct[H_STATUS] = st;
+      double* sc = P.scr;
+      double* xd = sc; sc += m;
+      double* bd = sc; sc += m;
+      double* lod = sc; sc += m;
+      double* hid = sc; sc += m;
+      int* fid = reinterpret_cast<int*>(sc); sc += m;  // m ints (room for 2m)
+      int* iscr = reinterpret_cast<int*>(sc); sc += 2 * m;  // 4m ints
+      double* dscr = sc;  // 11 m
+      for (int i = 0; i < m * m; i++) P.M1[i] = P.A[i];
+      for (int i = 0; i < m; i++) { bd[i] = P.b[i]; lod[i] = P.lo[i]; hid[i] = P.hi[i]; fid[i] = P.fi[i]; }
+      bool ok = devDantzig(m, P.M1, xd, bd, lod, hid, fid, P.M2, dscr, iscr);
+      if (ok) {
+        for (int i = 0; i < m; i++) P.X[i] = xd[i];
+        if (!devLcpValid(m, P.A, 0.0, P.X, P.b, P.hi, P.lo, P.fi, false)) ok = false;
+      }
+      ct[H_FLAG] = ok ? 1 : 0;
+    }
+    __syncthreads();
+    success = ct[H_FLAG] != 0;
+  }
+  if (lane == 0) {
+    bool ok = success;
+    bool ign = false;
+    double cf = 0.0;
+    for (int i = 0; i < m; i++)
+      if (isnan(P.X[i])) { ok = false; for (int j = 0; j < m; j++) P.X[j] = 0.0; break; }
+    if (!ok) {
+      cf = md.fallbackCfm;
+      double* sc = P.scr;
+      double* xd = sc; sc += m;
+      double* bd = sc; sc += m;
+      int* order = reinterpret_cast<int*>(sc); sc += m;
+      for (int r = 0; r < m; r++)
+        for (int c = 0; c < m; c++) P.M1[r * m + c] = P.A[r * m + c] + (r == c ? cf : 0.0);
+      for (int i = 0; i < m; i++) { xd[i] = P.xc[i]; bd[i] = P.b[i]; }
+      ok = devPgs(m, P.M1, xd, bd, P.lo, P.hi, P.fi, order);
+      if (ok) {
+        for (int i = 0; i < m; i++) P.X[i] = xd[i];
+        if (!devLcpValid(m, P.A, cf, P.X, P.b, P.hi, P.lo, P.fi, false)) ok = false;
+      }
+    }
+    if (!ok) {
+      ign = true;
+      double* sc = P.scr;
+      int* keep = reinterpret_cast<int*>(sc); sc += m;
+      double* xr = sc; sc += m;
+      double* br = sc; sc += m;
+      double* lor = sc; sc += m;
+      double* hir = sc; sc += m;
+      int* fir = reinterpret_cast<int*>(sc); sc += m;
+      int* order = reinterpret_cast<int*>(sc); sc += m;
+      int k2 = 0;
+      for (int i = 0; i < m; i++) if (P.fi[i] == -1) keep[k2++] = i;
+      for (int r = 0; r < k2; r++) {
+        br[r] = P.b[keep[r]]; lor[r] = P.lo[keep[r]]; hir[r] = P.hi[keep[r]]; fir[r] = -1; xr[r] = 0.0;
+        for (int c = 0; c < k2; c++) P.M1[r * k2 + c] = P.A[keep[r] * m + keep[c]] + (r == c ? cf : 0.0);
+      }
+      devPgs(k2, P.M1, xr, br, lor, hir, fir, order);
+      for (int i = 0; i < m; i++) P.X[i] = 0.0;
+      for (int r = 0; r < k2; r++) P.X[keep[r]] = xr[r];
+    }
+    for (int i = 0; i < m; i++)
+      if (isnan(P.X[i])) { for (int j = 0; j < m; j++) P.X[j] = 0.0; break; }
+    ct[H_CFM] = cf;
+    ct[H_IGN] = ign ? 1 : 0;
+  }
+  __syncthreads();
+  cfm = ct[H_CFM];
+  ignoredFriction = ct[H_IGN] != 0;
+  if (!shortCircuit) devConstruct(P, m, cfm, ignoredFriction, ct, lane);
+  // impulses, cache, snapshot
+  for (int i = lane; i < n; i += WAVE) {
+    double acc = 0;
+    for (int j = 0; j < m; j++) acc += P.massed[i * m + j] * P.X[j];
+    snap[SN_VF + i] = v1[i];
+    v1[i] += acc;
+  }
+  if (lane == 0) cache[0] = m;
+  for (int i = lane; i < m; i += WAVE) cache[1 + i] = P.X[i];
+  for (int t = lane; t < nCon * CREC; t += WAVE) snap[SN_CONTACTS + t] = ct[CT_CONTACTS + t];
+  for (int j = lane; j < m; j += WAVE) {
+    double* rr = snap + SN_ROWS + j * SN_ROWREC;
+    rr[RR_CONTACT] = P.rowC[j];
+    rr[RR_DIR] = P.rowDir[j];
+    for (int i = 0; i < 3; i++) rr[RR_D + i] = P.dvec[3 * j + i];
+    rr[RR_B] = P.b[j];
+    rr[RR_X] = P.X[j];
+    rr[RR_MAP] = P.mapping[j];
+    rr[RR_CIDX] = P.clampIdx[j];
+    rr[RR_UIDX] = P.ubIdx[j];
+    rr[RR_EVAL] = P.Eval[j];
+    rr[RR_BOUNCE] = 1.0 + P.rest[j];
+  }
+  const int nc = (int)ct[H_NC];
+  for (int i = lane; i < nc; i += WAVE) snap[SN_FC + i] = P.fc[i];
+  if (lane == 0) {
+    snap[SN_NCON] = nCon;
+    snap[SN_M] = m;
+    snap[SN_NC] = nc;
+    snap[SN_NU] = ct[H_NU];
+    snap[SN_CFM] = cfm;
+    snap[SN_STATUS] = ct[H_STATUS];
+    snap[SN_SC] = shortCircuit ? 1 : 0;
+    snap[SN_IGN] = ignoredFriction ? 1 : 0;
+  }
+  __syncthreads();
+}
+
+// ===========================================================================
+// Backward: the constraint terms of BackpropSnapshot::backprop as
+// vector-Jacobian products.  With w = Minv gv, u = A_cubE^T w,
+// lambda = (Q^+)^T u, beta = bounce .* lambda, mu = A_c beta, nu = Minv mu:
+//   grad_tau = dt (w - nu)
+//   grad_v   = gv - mu - dt (dC/dv + D + dt K)^T (w - nu)
+//   grad_q   = -dt (dID(a*)/dq)^T (w - nu) - dt K (w - nu) - dt m(delta, nu)
+//              + m(sigma, kappa) - [imprecise] (m(MA1, MArho) + m(MA2, MApi))
+//              + sum_j G_j^T g_j
+// where m(a, c) = (d(M a)/dq)^T c, G_j = d(J^T e_j)/dq
+// (DifferentiableContactConstraint.cpp:1654) and g_j collects, per clamping /
+// upper-bound row, the vectors multiplying G_j in
+//   dA_c f  (BackpropSnapshot.cpp:1046), dB (getJacobianOfLCPOffsetClampingSubset
+//   :3181), -Q^+ dQ(Q^+ b) and the pseudo-inverse gradient branch
+//   (getJacobianOfConstraintForce :2723, :2960).
+// ===========================================================================
+enum { NV_DELTA = 0, NV_NU, NV_SIGMA, NV_KAPPA, NV_MA1, NV_MARHO, NV_MA2, NV_MAPI, NV_YF, NV_W, NV_W2, NV_MU, NV_T0 };
+
+
+struct BwdPool {
+  double *Ac, *AcubE, *MA, *Q, *W, *PT, *Pscr, *gRows, *TAB, *NV;
+  double *fc, *bc, *bounce, *u, *lam, *beta, *xq, *rho, *piv, *zeta, *r1, *tc;
+  double* codw;
+  int* rowOf;
+};
+
+__device__ inline void carveBwd(double* base, int m, int n, BwdPool& P) {
+  double* p = base;
+  P.Ac = p; p += n * m;
+  P.AcubE = p; p += n * m;
+  P.MA = p; p += n * m;
+  P.gRows = p; p += n * m;
+  P.Q = p; p += m * m;
+  P.W = p; p += m * m;
+  P.PT = p; p += m * m;
+  P.Pscr = p; p += 2 * m * m;
+  P.TAB = p; p += 12 * m;
+  P.NV = p; p += NV_COLS * n;
+  double** vecs[] = {&P.fc, &P.bc, &P.bounce, &P.u, &P.lam, &P.beta, &P.xq, &P.rho, &P.piv, &P.zeta, &P.r1, &P.tc};
+  for (double** v : vecs) { *v = p; p += m; }
+  P.rowOf = reinterpret_cast<int*>(p); p += m;
+  P.codw = p;  // >= 8 m + 8
+}
+
+// Solve L L^T x = b for `cnt` right-hand sides stored as columns of X
+// (leading dimension ld); lane j handles column cols[j].
+__device__ void cholSolveColumns(const double* Lm, double* X, int n, int ld, const int* cols, int cnt, int lane) {
+  if (lane < cnt) {
+    const int j = cols[lane];
+    for (int i = 0; i < n; i++) {
+      double acc = X[i * ld + j];
+      for (int k = 0; k < i; k++) acc -= Lm[i * n + k] * X[k * ld + j];
+      X[i * ld + j] = acc / Lm[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; i--) {
+      double acc = X[i * ld + j];
+      for (int k = i + 1; k < n; k++) acc -= Lm[k * n + i] * X[k * ld + j];
+      X[i * ld + j] = acc / Lm[i * n + i];
+    }
+  }
+  __syncthreads();
+}
+
+// twist of body `b` for joint velocity vector g (column `col` of X, ld):
+// sum over ancestor dofs r of S_r g_r.  b < 0 -> 0.
+__device__ inline void bodyTwist(const ModelDev& md, const double* Sw, int b, const double* g, int ld, double* T) {
+  for (int i = 0; i < 6; i++) T[i] = 0.0;
+  if (b < 0) return;
+  const unsigned long long a = md.anc[b];
+  for (int r = 0; r < md.n; r++) {
+    if (!((a >> md.dofBody[r]) & 1ull)) continue;
+    const double gr = g[r * ld];
+    if (gr == 0.0) continue;
+    for (int i = 0; i < 6; i++) T[i] = fma(Sw[6 * r + i], gr, T[i]);
+  }
+}
+
+// ContactConstraint::getTangentBasisMatrixODEGradient (ContactConstraint.cpp:772)
+__device__ void tangentBasisGradient(const double* nrm, const double* g, double* T0, double* T1) {
+  const double ez[3] = {0, 0, 1}, ex[3] = {1, 0, 0}, ey[3] = {0, 1, 0};
+  const double* cr = ez;
+  double t[3];
+  cross3(cr, nrm, t);
+  if (dot3(t, t) < 1e-12) {
+    cr = ex; cross3(cr, nrm, t);
+    if (dot3(t, t) < 1e-12) {
+      cr = ey; cross3(cr, nrm, t);
+      if (dot3(t, t) < 1e-12) { cr = ez; cross3(cr, nrm, t); }
+    }
+  }
+  const double tn = sqrt(dot3(t, t));
+  for (int i = 0; i < 3; i++) t[i] /= tn;
+  double gc[3];
+  cross3(cr, g, gc);
+  for (int i = 0; i < 3; i++) gc[i] /= tn;
+  double gt[3];
+  if (fabs(tn - 1.0) > 1e-6) {
+    const double dd = dot3(gc, t);
+    for (int i = 0; i < 3; i++) gt[i] = gc[i] - dd * t[i];
+  } else {
+    for (int i = 0; i < 3; i++) gt[i] = gc[i];
+  }
+  double a[3], b[3];
+  cross3(g, t, a);
+  cross3(nrm, gt, b);
+  for (int i = 0; i < 3; i++) { T0[i] = gt[i]; T1[i] = a[i] + b[i]; }
+}
+
+// Contact preparation of the backward.  On return (all lanes):
+//   s[L.x]  = a* (acceleration incl. the constraint impulse / dt)
+//   s[L.w]  = w - nu       (the vector the unconstrained VJP machinery uses)
+//   NV columns hold the M-derivative pairs, mu, and P.gRows / P.TAB the
+//   per-row vectors of the G_j terms.  Returns the imprecise flag.
+__device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& L, int lane, const double* sn,
+                                   BwdPool& P, int m, int nc, double cfm, double* ct) {
+  const int n = md.n;
+  const double dt = md.dt;
+  const double* Lm = s + L.M;
+  const double* rows = sn + SN_ROWS;
+  if (lane == 0) {
+    for (int j = 0; j < m; j++)
+      if ((int)rows[j * SN_ROWREC + RR_MAP] == CM_CLAMPING) P.rowOf[(int)rows[j * SN_ROWREC + RR_CIDX]] = j;
+  }
+  __syncthreads();
+  // A_c and A_c + A_ub E (n x nc)
+  for (int t = lane; t < n * nc; t += WAVE) {
+    const int i = t / nc, c = t % nc;
+    const int r = P.rowOf[c];
+    const double* rr = rows + r * SN_ROWREC;
+    const double a = rowForceEntry(md, s, L, sn + SN_CONTACTS + (int)rr[RR_CONTACT] * CREC, rr + RR_D, i);
+    double ae = a;
+    for (int u = 0; u < m; u++) {
+      const double* ru = rows + u * SN_ROWREC;
+      const int mp = (int)ru[RR_MAP];
+      if (mp >= 0 && (int)rows[mp * SN_ROWREC + RR_CIDX] == c)
+        ae += ru[RR_EVAL] * rowForceEntry(md, s, L, sn + SN_CONTACTS + (int)ru[RR_CONTACT] * CREC, ru + RR_D, i);
+    }
+    P.Ac[t] = a;
+    P.AcubE[t] = ae;
+    P.MA[t] = ae;
+  }
+  for (int c = lane; c < nc; c += WAVE) {
+    const int r = P.rowOf[c];
+    P.fc[c] = sn[SN_FC + c];
+    P.bc[c] = rows[r * SN_ROWREC + RR_B];
+    P.bounce[c] = rows[r * SN_ROWREC + RR_BOUNCE];
+  }
+  // right-hand sides: fext (yf) and gv (w)
+  for (int i = lane; i < n; i += WAVE) {
+    const double qi = s[L.q + i], vi = s[L.v + i];
+    const double springF = md.spring[i] * (qi - md.rest[i] + dt * vi);
+    P.NV[i * NV_COLS + NV_YF] = s[L.tau + i] - s[L.rhs + i] - md.damping[i] * vi - springF;
+    P.NV[i * NV_COLS + NV_W] = s[L.gv + i];
+  }
+  __syncthreads();
+  {
+    int cols[2] = {NV_YF, NV_W};
+    int c = lane < 2 ? cols[lane] : 0;
+    if (lane < 2) {
+      for (int i = 0; i < n; i++) {
+        double acc = P.NV[i * NV_COLS + c];
+        for (int k = 0; k < i; k++) acc -= Lm[i * n + k] * P.NV[k * NV_COLS + c];
+        P.NV[i * NV_COLS + c] = acc / Lm[i * n + i];
+      }
+      for (int i = n - 1; i >= 0; i--) {
+        double acc = P.NV[i * NV_COLS + c];
+        for (int k = i + 1; k < n; k++) acc -= Lm[k * n + i] * P.NV[k * NV_COLS + c];
+        P.NV[i * NV_COLS + c] = acc / Lm[i * n + i];
+      }
+    } else if (lane - 2 < nc) {
+      // MA = Minv A_c_ub_E, one column per lane
+      const int j = lane - 2;
+      double* X = P.MA;
+      for (int i = 0; i < n; i++) {
+        double acc = X[i * nc + j];
+        for (int k = 0; k < i; k++) acc -= Lm[i * n + k] * X[k * nc + j];
+        X[i * nc + j] = acc / Lm[i * n + i];
+      }
+      for (int i = n - 1; i >= 0; i--) {
+        double acc = X[i * nc + j];
+        for (int k = i + 1; k < n; k++) acc -= Lm[k * n + i] * X[k * nc + j];
+        X[i * nc + j] = acc / Lm[i * n + i];
+      }
+    }
+    // columns beyond 62 (nc > 62 never happens: nc <= 48)
+  }
+  __syncthreads();
+  // Q = A_c^T MA + cfm I; W = copy to factor
+  for (int t = lane; t < nc * nc; t += WAVE) {
+    const int r = t / nc, c = t % nc;
+    double acc = 0;
+    for (int i = 0; i < n; i++) acc += P.Ac[i * nc + r] * P.MA[i * nc + c];
+    if (r == c) acc += cfm;
+    P.Q[t] = acc;
+    P.W[t] = acc;
+  }
+  // delta = MA fc / dt ; a* = yf + delta ; u = AcubE^T w
+  for (int i = lane; i < n; i += WAVE) {
+    double acc = 0;
+    for (int c = 0; c < nc; c++) acc += P.MA[i * nc + c] * P.fc[c];
+    const double d = acc / dt;
+    P.NV[i * NV_COLS + NV_DELTA] = d;
+    s[L.x + i] = P.NV[i * NV_COLS + NV_YF] + d;
+  }
+  for (int c = lane; c < nc; c += WAVE) {
+    double acc = 0;
+    for (int i = 0; i < n; i++) acc += P.AcubE[i * nc + c] * P.NV[i * NV_COLS + NV_W];
+    P.u[c] = acc;
+  }
+  __syncthreads();
+  // pinv(Q) via COD: column c of P (stored as row c of PT) solved by lane c
+  Cod cod;
+  double* w = carveCod(P.codw, P.W, nc, nc, nc, cod);
+  double* cn = w; w += m;
+  double* vv = w; w += m;
+  codFactor(cod, cn, vv, lane);
+  if (lane < nc) {
+    double* rhs = P.Pscr + lane * nc;
+    double* z = P.Pscr + nc * nc + lane * nc;
+    for (int i = 0; i < nc; i++) rhs[i] = i == lane ? 1.0 : 0.0;
+    codSolveOne(cod, rhs, P.PT + lane * nc, z);
+  }
+  __syncthreads();
+  // lambda = P^T u ; x = P b ; beta
+  for (int c = lane; c < nc; c += WAVE) {
+    double l = 0, xx = 0;
+    for (int r = 0; r < nc; r++) {
+      l += P.PT[c * nc + r] * P.u[r];
+      xx += P.PT[r * nc + c] * P.bc[r];
+    }
+    P.lam[c] = l;
+    P.beta[c] = P.bounce[c] * l;
+    P.xq[c] = xx;
+  }
+  // imprecision || I - Q Q^+ ||^2 (per-lane partial sums)
+  double part = 0.0;
+  for (int t = lane; t < nc * nc; t += WAVE) {
+    const int r = t / nc, c = t % nc;
+    double acc = 0;
+    for (int k = 0; k < nc; k++) acc += P.Q[r * nc + k] * P.PT[c * nc + k];
+    const double e = (r == c ? 1.0 : 0.0) - acc;
+    part += e * e;
+  }
+  // wave reduction through the (backward-idle) contact list region of ct
+  ct[CT_CONTACTS + lane] = part;
+  __syncthreads();
+  if (lane == 0) {
+    double tot = 0;
+    for (int i = 0; i < WAVE; i++) tot += ct[CT_CONTACTS + i];
+    ct[H_FLAG] = tot >= 1e-18 ? 1 : 0;
+  }
+  __syncthreads();
+  const int imp = (int)ct[H_FLAG];
+  // mu = A_c beta ; sigma = MA x ; rhs for kappa = A_c lambda
+  for (int i = lane; i < n; i += WAVE) {
+    double mu = 0, sg = 0, kp = 0;
+    for (int c = 0; c < nc; c++) {
+      mu += P.Ac[i * nc + c] * P.beta[c];
+      sg += P.MA[i * nc + c] * P.xq[c];
+      kp += P.Ac[i * nc + c] * P.lam[c];
+    }
+    P.NV[i * NV_COLS + NV_MU] = mu;
+    P.NV[i * NV_COLS + NV_NU] = mu;
+    P.NV[i * NV_COLS + NV_SIGMA] = sg;
+    P.NV[i * NV_COLS + NV_KAPPA] = kp;
+  }
+  if (imp) {
+    for (int c = lane; c < nc; c += WAVE) {
+      double qx = 0, qtl = 0, rh = 0, ze = 0;
+      for (int k = 0; k < nc; k++) {
+        qx += P.Q[c * nc + k] * P.xq[k];
+        qtl += P.Q[k * nc + c] * P.lam[k];
+        rh += P.PT[k * nc + c] * P.lam[k];   // (P lambda)_c
+        ze += P.PT[c * nc + k] * P.xq[k];    // (P^T x)_c
+      }
+      P.r1[c] = P.bc[c] - qx;
+      P.piv[c] = P.u[c] - qtl;
+      P.rho[c] = rh;
+      P.zeta[c] = ze;
+    }
+  } else {
+    for (int c = lane; c < nc; c += WAVE) { P.r1[c] = 0; P.piv[c] = 0; P.rho[c] = 0; P.zeta[c] = 0; }
+  }
+  __syncthreads();
+  for (int i = lane; i < n; i += WAVE) {
+    double a1 = 0, ar = 0, a2 = 0, ap = 0;
+    for (int c = 0; c < nc; c++) {
+      a1 += P.Ac[i * nc + c] * P.r1[c];
+      ar += P.MA[i * nc + c] * P.rho[c];
+      a2 += P.Ac[i * nc + c] * P.zeta[c];
+      ap += P.MA[i * nc + c] * P.piv[c];
+    }
+    P.NV[i * NV_COLS + NV_MA1] = a1;
+    P.NV[i * NV_COLS + NV_MARHO] = ar;
+    P.NV[i * NV_COLS + NV_MA2] = a2;
+    P.NV[i * NV_COLS + NV_MAPI] = ap;
+  }
+  __syncthreads();
+  {
+    const int cols[4] = {NV_NU, NV_KAPPA, NV_MA1, NV_MA2};
+    cholSolveColumns(Lm, P.NV, n, NV_COLS, cols, 4, lane);
+  }
+  // w - nu into s[L.w]
+  for (int i = lane; i < n; i += WAVE) {
+    const double w2 = P.NV[i * NV_COLS + NV_W] - P.NV[i * NV_COLS + NV_NU];
+    P.NV[i * NV_COLS + NV_W2] = w2;
+    s[L.w + i] = w2;
+  }
+  // per-row vectors g_j
+  for (int t = lane; t < m * n; t += WAVE) {
+    const int j = t / n, i = t % n;
+    const double* rr = rows + j * SN_ROWREC;
+    const int mp = (int)rr[RR_MAP];
+    const double* nv = P.NV + i * NV_COLS;
+    double g = 0.0;
+    if (mp == CM_CLAMPING) {
+      const int c = (int)rr[RR_CIDX];
+      g = P.fc[c] * nv[NV_W] - P.beta[c] * sn[SN_VF + i] - P.lam[c] * nv[NV_SIGMA] - P.xq[c] * nv[NV_KAPPA];
+      if (imp) g += P.rho[c] * nv[NV_MA1] + P.r1[c] * nv[NV_MARHO] + P.piv[c] * nv[NV_MA2] + P.zeta[c] * nv[NV_MAPI];
+    } else if (mp >= 0) {
+      const int c = (int)rows[mp * SN_ROWREC + RR_CIDX];
+      double inner = P.fc[c] * nv[NV_W] - P.xq[c] * nv[NV_KAPPA];
+      if (imp) inner += P.rho[c] * nv[NV_MA1] + P.piv[c] * nv[NV_MA2];
+      g = rr[RR_EVAL] * inner;
+    }
+    P.gRows[j * n + i] = g;
+  }
+  __syncthreads();
+  // T_A(g_j), T_B(g_j)
+  for (int t = lane; t < 2 * m; t += WAVE) {
+    const int j = t >> 1, side = t & 1;
+    const double* rec = sn + SN_CONTACTS + (int)rows[j * SN_ROWREC + RR_CONTACT] * CREC;
+    const int body = (int)rec[8 + side];
+    bodyTwist(md, s + L.Sw, body, P.gRows + j * n, 1, P.TAB + j * 12 + side * 6);
+  }
+  __syncthreads();
+  return imp;
+}
+
+// sum_j (G_j^T g_j)[k] for the lane's direction k with position generator Z.
+__device__ double contactGTerms(const ModelDev& md, const double* s, const Layout& L, const double* sn,
+                                const BwdPool& P, int m, int k, const double* Z, int* status) {
+  const int n = md.n;
+  const int bk = md.dofBody[k];
+  const int lam = md.parent[bk];
+  const double* rows = sn + SN_ROWS;
+  double acc = 0.0;
+  for (int j = 0; j < m; j++) {
+    const double* rr = rows + j * SN_ROWREC;
+    if ((int)rr[RR_MAP] == CM_NOT_CLAMPING) continue;
+    const double* rec = sn + SN_CONTACTS + (int)rr[RR_CONTACT] * CREC;
+    const int A = (int)rec[8], B = (int)rec[9];
+    const bool inA = (md.anc[A] >> bk) & 1ull;
+    const bool inB = (md.anc[B] >> bk) & 1ull;
+    if (!inA && !inB) continue;
+    const double* p = rec;
+    const double* d = rr + RR_D;
+    double wr[6];
+    cross3(p, d, wr);
+    wr[3] = d[0]; wr[4] = d[1]; wr[5] = d[2];
+    // screw-axis gradient part: (Z x Y) . wr
+    const double* g = P.gRows + j * n;
+    double Tl[6];
+    bodyTwist(md, s + L.Sw, lam, g, 1, Tl);
+    double Y[6];
+    for (int i = 0; i < 6; i++) {
+      double y = 0.0;
+      if (inA) y += P.TAB[j * 12 + i] - Tl[i];
+      if (inB) y -= P.TAB[j * 12 + 6 + i] - Tl[i];
+      Y[i] = y;
+    }
+    double zy[6];
+    crm(Z, Y, zy);
+    acc += dot6(zy, wr);
+    // contact-geometry part: (T_A - T_B) . d(wrench)/dq_k
+    if (inA && inB) { *status |= 1; continue; }
+    const int type = (int)rec[7];
+    int kind = 0;  // 1 vertex, 2 face
+    if (type == CT_VERTEX_FACE) kind = inA ? 1 : 2;
+    else if (type == CT_FACE_VERTEX) kind = inA ? 2 : 1;
+    else { *status |= 2; continue; }
+    double dp[3] = {0, 0, 0}, dd[3] = {0, 0, 0};
+    const double wv[3] = {Z[0], Z[1], Z[2]}, vv[3] = {Z[3], Z[4], Z[5]};
+    if (kind == 1) {
+      if (sqrt(dot3(wv, wv)) > 1e-6) {
+        cross3(wv, p, dp);
+        for (int i = 0; i < 3; i++) dp[i] += vv[i];
+      } else {
+        for (int i = 0; i < 3; i++) dp[i] = vv[i];
+      }
+    } else {
+      double dn[3];
+      cross3(wv, rec + 3, dn);
+      const int dirIdx = (int)rr[RR_DIR];
+      if (dirIdx == 0 || dot3(dn, dn) <= 1e-12) {
+        for (int i = 0; i < 3; i++) dd[i] = dn[i];
+      } else {
+        double T0[3], T1[3];
+        tangentBasisGradient(rec + 3, dn, T0, T1);
+        for (int i = 0; i < 3; i++) dd[i] = dirIdx == 1 ? T0[i] : T1[i];
+      }
+    }
+    double dwr[6], t1[3], t2[3];
+    cross3(p, dd, t1);
+    cross3(dp, d, t2);
+    for (int i = 0; i < 3; i++) { dwr[i] = t1[i] + t2[i]; dwr[3 + i] = dd[i]; }
+    double tab[6];
+    for (int i = 0; i < 6; i++) tab[i] = P.TAB[j * 12 + i] - P.TAB[j * 12 + 6 + i];
+    acc += dot6(tab, dwr);
+  }
+  return acc;
+}
+
+// M-derivative pairs m(a, c) = (d(M a)/dq)^T c evaluated for all directions:
+//   d(c^T M a)/dq_k = -(Z_k x V_c,lam) . H_a(k) - (Z_k x V_a,lam) . H_c(k)
+// with V_x,b the world twist of body b under joint rates x and H_x(k) the
+// subtree momentum sum_{b in sub(k)} I_b V_x,b.  Fields live in `buf`
+// (8 fields x nb x 12 doubles: V then H).
+__device__ void mFieldsBuild(const ModelDev& md, double* s, const Layout& L, const double* NV, double* buf, int lane) {
+  const int nb = md.nb;
+  for (int t = lane; t < 8 * nb; t += WAVE) {
+    const int f = t / nb, b = t % nb;
+    double* V = buf + (f * nb + b) * 12;
+    bodyTwist(md, s + L.Sw, b, NV + f, NV_COLS, V);
+    double I[36];
+    worldInertia(md, s + L.Tw + 12 * b, b, I);
+    mv6(I, V, V + 6);
+  }
+  __syncthreads();
+  for (int b = nb - 1; b > 0; b--) {
+    const int p = md.parent[b];
+    if (p >= 0 && lane < 48) {
+      const int f = lane / 6, i = lane % 6;
+      buf[(f * nb + p) * 12 + 6 + i] += buf[(f * nb + b) * 12 + 6 + i];
+    }
+    __syncthreads();
+  }
+}
+
+__device__ double mFieldsEval(const ModelDev& md, const double* buf, int k, const double* Z, double coefDelta,
+                              double imp) {
+  const int nb = md.nb;
+  const int bk = md.dofBody[k];
+  const int lam = md.parent[bk];
+  const double coef[4] = {coefDelta, 1.0, -imp, -imp};
+  double total = 0.0;
+  for (int pr = 0; pr < 4; pr++) {
+    const int fa = 2 * pr, fc = 2 * pr + 1;
+    const double* Ha = buf + (fa * nb + bk) * 12 + 6;
+    const double* Hc = buf + (fc * nb + bk) * 12 + 6;
+    double val = 0.0;
+    if (lam >= 0) {
+      double t[6];
+      crm(Z, buf + (fc * nb + lam) * 12, t);
+      val -= dot6(t, Ha);
+      crm(Z, buf + (fa * nb + lam) * 12, t);
+      val -= dot6(t, Hc);
+    }
+    total += coef[pr] * val;
+  }
+  return total;
+}

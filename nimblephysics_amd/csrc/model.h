@@ -36,8 +36,8 @@ struct ModelDev {
   double shapeSize[NS_MAX][3];
   double shapeT[NS_MAX][12];
   // candidate pairs (i < j) after BodyNodeCollisionFilter, in detector order
-  int numPairs;
-  int pairA[NS_MAX * 4], pairB[NS_MAX * 4];
+  int numPairs, pairChunk;
+  int pairA[NS_MAX * (NS_MAX - 1) / 2], pairB[NS_MAX * (NS_MAX - 1) / 2];
 };
 
 // LDS layout (in doubles) for one world instance; offsets computed on host.
@@ -45,7 +45,7 @@ struct Layout {
   int q, v, tau, Tw, Sw, V, A, IC, F, M, rhs, x, scratch;
   // backward extras
   int B1, B23, B4, P, H, w, gp, gv, out;
-  // contacts
-  int ct;
+  // contacts: stage header/lists, post-dynamics velocity, LCP workspace pool
+  int ct, v1, pool, poolCap;
   int total;
 };

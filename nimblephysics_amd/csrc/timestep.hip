@@ -233,6 +233,8 @@ __device__ void loadState(const ModelDev& md, double* s, const Layout& L, int la
   __syncthreads();
 }
 
+#include "contact.cuh"
+
 // Everything up to the factored mass matrix; leaves C in s[L.rhs].
 __device__ void coreDynamics(const ModelDev& md, double* s, const Layout& L, int lane) {
   kinematics(md, s, L, lane, nullptr);
@@ -267,22 +269,31 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, con
     }
     __syncthreads();
     cholSolve(s + L.M, x, n, lane);  // x = ddq
-    double* out = nextState + (size_t)env * 2 * n;
     // integrateVelocities (Skeleton.cpp:9329): v1 = v + dt ddq
-    for (int i = lane; i < n; i += WAVE) out[n + i] = s[L.v + i] + md.dt * x[i];
-    // integratePositions(initialVelocity) (World.cpp:300)
+    double* v1 = s + L.v1;
+    for (int i = lane; i < n; i += WAVE) v1[i] = s[L.v + i] + md.dt * x[i];
+    __syncthreads();
+    // runConstraintEngine (World.cpp:254): collision, LCP, impulses
+    if (md.numPairs > 0) {
+      double* sn = snapshot + (size_t)env * snapDoubles;
+      contactStage(md, s, L, lane, v1, lcpCache + (size_t)env * cacheDoubles, sn, sn + snapWorkspaceOffset(n));
+    }
+    double* out = nextState + (size_t)env * 2 * n;
+    for (int i = lane; i < n; i += WAVE) out[n + i] = v1[i];
+    // integratePositions (World.cpp:300): with the pre-step velocity when
+    // position and velocity updates run in parallel (the default)
+    const double* vint = md.parallelPosVel ? s + L.v : v1;
     if (lane < md.nb) {
       const int b = lane, o = md.dof0[b];
       const int jt = md.jtype[b];
       if (jt == NIMBLE_JOINT_REVOLUTE || jt == NIMBLE_JOINT_PRISMATIC) {
-        out[o] = s[L.q + o] + s[L.v + o] * md.dt;
+        out[o] = s[L.q + o] + vint[o] * md.dt;
       } else if (jt == NIMBLE_JOINT_FREE) {
         double r[6];
-        freeIntegrate(s + L.q + o, s + L.v + o, md.dt, r);
+        freeIntegrate(s + L.q + o, vint + o, md.dt, r);
         for (int i = 0; i < 6; i++) out[o + i] = r[i];
       }
     }
-    (void)lcpCache; (void)snapshot; (void)snapDoubles; (void)cacheDoubles;
     __syncthreads();
   }
 }
@@ -396,7 +407,7 @@ __device__ void rightJacobianCol(const double* th, int k, double* o) {
   const double t2 = th[0] * th[0] + th[1] * th[1] + th[2] * th[2];
   const double t = sqrt(t2);
   double a, b;
-  if (t < 1e-6) { a = 0.5; b = 1.0 / 6.0; }
+  if (t < 1e-3) { a = 0.5; b = 1.0 / 6.0; }  // expMapJac small-angle branch (Geometry.cpp)
   else { a = (1.0 - cos(t)) / t2; b = (t - sin(t)) / (t2 * t); }
   const double K[9] = {0, -th[2], th[1], th[2], 0, -th[0], -th[1], th[0], 0};
   for (int r = 0; r < 3; r++) {
@@ -407,7 +418,7 @@ __device__ void rightJacobianCol(const double* th, int k, double* o) {
 
 extern "C" __global__ void __launch_bounds__(WAVE)
 nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, const double* __restrict__ state,
-                       const double* __restrict__ forces, const double* __restrict__ snapshot, int snapDoubles,
+                       const double* __restrict__ forces, double* __restrict__ snapshot, int snapDoubles,
                        const double* __restrict__ gradNext, double* __restrict__ gradState,
                        double* __restrict__ gradForces) {
   extern __shared__ double s[];
@@ -423,29 +434,54 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
       s[L.gv + i] = gN[n + i];
     }
     coreDynamics(md, s, L, lane);
-    // z = dt (tau - C - D v - K (q - q0 + dt v))   [+ constraint impulses]
+    double* sn = snapshot + (size_t)env * snapDoubles;
+    const int nc = md.numPairs > 0 ? (int)sn[SN_NC] : 0;
+    const int m = md.numPairs > 0 ? (int)sn[SN_M] : 0;
     double* x = s + L.x;
-    for (int i = lane; i < n; i += WAVE) {
-      const double qi = s[L.q + i], vi = s[L.v + i];
-      const double springF = md.spring[i] * (qi - md.rest[i] + dt * vi);
-      const double dampF = md.damping[i] * vi;
-      x[i] = dt * (s[L.tau + i] - s[L.rhs + i] - dampF - springF);
+    double* w = s + L.w;
+    BwdPool P;
+    int imp = 0;
+    if (nc > 0) {
+      // constrained: a* = Minv (z + A_c_ub_E f_c) / dt, w <- w - nu
+      const int need = bwdPoolDoubles(m, n);
+      carveBwd(need <= L.poolCap ? s + L.pool : sn + snapWorkspaceOffset(n), m, n, P);
+      imp = contactBackwardPrep(md, s, L, lane, sn, P, m, nc, sn[SN_CFM], s + L.ct);
+#ifdef NIMBLE_DEBUG_DUMP
+      if (lane == 0) {
+        double* dbg = sn + snapWorkspaceOffset(n);
+        int o = 0;
+        dbg[o++] = nc; dbg[o++] = imp;
+        for (int i = 0; i < nc * nc; i++) dbg[o++] = P.Q[i];
+        for (int i = 0; i < nc; i++) dbg[o++] = P.u[i];
+        for (int i = 0; i < nc; i++) dbg[o++] = P.lam[i];
+        for (int i = 0; i < nc * nc; i++) dbg[o++] = P.PT[i];
+        for (int i = 0; i < n * nc; i++) dbg[o++] = P.AcubE[i];
+        for (int i = 0; i < n * nc; i++) dbg[o++] = P.Ac[i];
+        for (int i = 0; i < n * NV_COLS; i++) dbg[o++] = P.NV[i];
+        for (int i = 0; i < n; i++) dbg[o++] = s[L.w + i];
+      }
+#endif
+    } else {
+      // z = dt (tau - C - D v - K (q - q0 + dt v))
+      for (int i = lane; i < n; i += WAVE) {
+        const double qi = s[L.q + i], vi = s[L.v + i];
+        const double springF = md.spring[i] * (qi - md.rest[i] + dt * vi);
+        const double dampF = md.damping[i] * vi;
+        x[i] = dt * (s[L.tau + i] - s[L.rhs + i] - dampF - springF);
+        w[i] = s[L.gv + i];
+      }
+      __syncthreads();
+      cholSolve(s + L.M, x, n, lane);  // x = y = Minv z  => a* = y / dt
+      cholSolve(s + L.M, w, n, lane);  // w = Minv gv
+      for (int i = lane; i < n; i += WAVE) x[i] /= dt;
+      __syncthreads();
     }
-    (void)snapshot; (void)snapDoubles;
-    __syncthreads();
-    cholSolve(s + L.M, x, n, lane);  // x = y = Minv z  => a* = y / dt
-    for (int i = lane; i < n; i += WAVE) x[i] /= dt;
-    __syncthreads();
     kinematics(md, s, L, lane, x);  // A = accelerations at a*
     derivativeComposites(md, s, L, lane);
-    // w = Minv gv
-    double* w = s + L.w;
-    for (int i = lane; i < n; i += WAVE) w[i] = s[L.gv + i];
-    __syncthreads();
-    cholSolve(s + L.M, w, n, lane);
 
     // ---- per-direction columns -------------------------------------------
     double gq = 0.0, gvOut = 0.0, gt = 0.0;
+    double Z[6] = {0, 0, 0, 0, 0, 0};
     const int k = lane;
     if (k < n) {
       const int b = md.dofBody[k];
@@ -457,7 +493,6 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
         ul[i] = (lam >= 0 ? s[L.A + 6 * lam + i] : 0.0) - ag[i];
       }
       // position generator Z (world twist of the subtree per unit q_k)
-      double Z[6];
       const double* Sk = s + L.Sw + 6 * k;
       if (md.jtype[b] == NIMBLE_JOINT_FREE) {
         const int o = md.dof0[b];
@@ -519,6 +554,7 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
       gq = -dt * accQ - dt * md.spring[k] * wk;
       gvOut = s[L.gv + k] - dt * accV - dt * md.damping[k] * wk - dt * dt * md.spring[k] * wk;
       gt = dt * wk;
+      if (nc > 0) gvOut -= P.NV[k * NV_COLS + NV_MU];
       // posPos^T gp and velPos^T gp for 1-dof joints: identity / dt * identity
       if (md.ndof[b] == 1) {
         gq += s[L.gp + k];
@@ -526,6 +562,17 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
       }
     }
     __syncthreads();
+    if (nc > 0) {
+      // B1/B23/B4 are dead now: reuse them for the M-derivative fields
+      double* buf = s + L.B1;
+      mFieldsBuild(md, s, L, P.NV, buf, lane);
+      if (k < n) {
+        int status = 0;
+        gq += mFieldsEval(md, buf, k, Z, -dt, (double)imp);
+        gq += contactGTerms(md, s, L, sn, P, m, k, Z, &status);
+      }
+      __syncthreads();
+    }
     // FreeJoint posPos / velPos blocks: central differences exactly as
     // FreeJoint::finiteDifferencePosPosJacobian / VelPosJacobian
     // (FreeJoint.cpp:965, :987); 24 lanes, one perturbed integration each.

@@ -51,6 +51,13 @@ def lib():
         L.oracle_contacts.restype = ip
         L.oracle_lcp_debug.argtypes = [vp, ip, C.POINTER(ip), dp, ip]
         L.oracle_lcp_debug.restype = ip
+        L.oracle_lcp_flags.argtypes = [vp, ip, dp]
+        L.oracle_lcp_fc.argtypes = [vp, ip, dp, ip]
+        L.oracle_lcp_fc.restype = ip
+        L.oracle_lcp_cols.argtypes = [vp, ip, dp, ip]
+        L.oracle_lcp_cols.restype = ip
+        L.oracle_lcp_problem.argtypes = [vp, ip, dp, dp, dp, dp, C.POINTER(ip), ip]
+        L.oracle_lcp_problem.restype = ip
         L.oracle_dantzig.argtypes = [ip, dp, dp, dp, dp, C.POINTER(ip), dp, ip]
         L.oracle_dantzig.restype = ip
         L.oracle_cod_solve.argtypes = [dp, ip, ip, dp, dp]
@@ -173,6 +180,35 @@ def lcp_debug(ow: "OracleWorld", b=0, max_rows=64):
     x = np.zeros(max_rows)
     m = lib().oracle_lcp_debug(ow.snaps, b, _pi(mapping), _p(x), max_rows)
     return mapping[:m].copy(), x[:m].copy()
+
+
+def lcp_flags(ow: "OracleWorld", b=0):
+    """[shortCircuit, ignoredFriction, cfm, numClamping, numUpperBound]"""
+    out = np.zeros(5)
+    lib().oracle_lcp_flags(ow.snaps, b, _p(out))
+    return out
+
+
+def lcp_fc(ow: "OracleWorld", b=0, maxc=64):
+    fc = np.zeros(maxc)
+    k = lib().oracle_lcp_fc(ow.snaps, b, _p(fc), maxc)
+    return fc[:k].copy()
+
+
+def lcp_cols(ow: "OracleWorld", b=0):
+    """J^T columns (n x m) of world b's LCP rows."""
+    out = np.zeros(ow.n * 64)
+    m = lib().oracle_lcp_cols(ow.snaps, b, _p(out), out.size)
+    return out[:ow.n * m].reshape(ow.n, m).copy()
+
+
+def lcp_problem(ow: "OracleWorld", b=0, max_rows=64):
+    """(A, b, lo, hi, findex) of world b's LCP (A without the fallback CFM)."""
+    A = np.zeros(max_rows * max_rows)
+    bb, lo, hi = np.zeros(max_rows), np.zeros(max_rows), np.zeros(max_rows)
+    fi = np.zeros(max_rows, dtype=np.int32)
+    m = lib().oracle_lcp_problem(ow.snaps, b, _p(A), _p(bb), _p(lo), _p(hi), _pi(fi), max_rows)
+    return A[:m * m].reshape(m, m).copy(), bb[:m].copy(), lo[:m].copy(), hi[:m].copy(), fi[:m].copy()
 
 
 def dantzig(A, b, lo, hi, findex, early=False):

@@ -102,6 +102,37 @@ int oracle_lcp_debug(void* snaps, int b, int* mapping, double* x, int maxRows) {
   for (int i = 0; i < m; i++) { mapping[i] = s.mapping[i]; x[i] = s.lcpX[i]; }
   return s.numRows;
 }
+// LCP path flags of world b: [shortCircuit, ignoredFriction, cfm, numClamping, numUpperBound]
+void oracle_lcp_flags(void* snaps, int b, double* out) {
+  const auto& s = (*static_cast<std::vector<OracleSnap>*>(snaps))[b].s;
+  out[0] = s.shortCircuit ? 1 : 0;
+  out[1] = s.ignoredFriction ? 1 : 0;
+  out[2] = s.cfm;
+  out[3] = s.numClamping;
+  out[4] = s.numUpperBound;
+}
+// clamping impulses f_c of world b; returns numClamping
+int oracle_lcp_fc(void* snaps, int b, double* fc, int maxc) {
+  const auto& s = (*static_cast<std::vector<OracleSnap>*>(snaps))[b].s;
+  for (int i = 0; i < s.numClamping && i < maxc; i++) fc[i] = s.fc[i];
+  return s.numClamping;
+}
+// J^T columns of world b's LCP rows (n x m row-major); returns m
+int oracle_lcp_cols(void* snaps, int b, double* out, int maxElems) {
+  const auto& s = (*static_cast<std::vector<OracleSnap>*>(snaps))[b].s;
+  if ((int)s.Aall.size() > maxElems) return -1;
+  for (size_t i = 0; i < s.Aall.size(); i++) out[i] = s.Aall[i];
+  return s.numRows;
+}
+// LCP problem of world b (before the solve): A (m x m), b, lo, hi, findex; returns m
+int oracle_lcp_problem(void* snaps, int b, double* A, double* bb, double* lo, double* hi, int* fi, int maxRows) {
+  const auto& s = (*static_cast<std::vector<OracleSnap>*>(snaps))[b].s;
+  const int m = s.numRows;
+  if (m > maxRows) return -1;
+  for (int i = 0; i < m * m; i++) A[i] = s.lcpA[i] - ((i / m == i % m) ? s.cfm : 0.0);
+  for (int i = 0; i < m; i++) { bb[i] = s.lcpB[i]; lo[i] = s.lcpLo[i]; hi[i] = s.lcpHi[i]; fi[i] = s.lcpFIndex[i]; }
+  return m;
+}
 // Dantzig restatement on a raw problem (A n x n row-major); returns success
 int oracle_dantzig(int n, const double* A, const double* b, const double* lo, const double* hi, const int* findex,
                    double* x, int earlyTermination) {

@@ -1,0 +1,187 @@
+"""Contact-path parity of the HIP timestep against the CPU oracle.
+
+* contact index sets bit-exact: per world the same number of contacts and the
+  same (bodyA, bodyB, type) sequence in detector order, points to 1e-9;
+* LCP path: the same solver path (short-circuit / Dantzig / CFM+PGS /
+  friction removed) and the same row classification (clamping / upper-bound /
+  separating); then next state and gradients within BASELINE.json's 1e-6
+  relative tolerance (observed ~1e-13);
+* a world may take a different LCP path only when its LCP is numerically
+  ill-posed for the reference algorithm itself: resting boxes give rank-
+  deficient (e.g. rank 6 of 12) LCPs on which the reference's dSolveLCP
+  succeeds or early-terminates depending on 1e-16-level rounding (checked
+  here by perturbing the oracle's A by 1e-15 relative and requiring both
+  outcomes to occur).  Such worlds must be rare (< 3 %);
+* warm-started multi-step rollouts (the LCP cache, BoxedLcpConstraintSolver::mX).
+"""
+import numpy as np
+import pytest
+import torch
+
+import models
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-6
+SN_NCON, SN_M, SN_NC, SN_NU = 0, 1, 2, 3
+SN_CONTACTS, SN_ROWS, SN_ROWREC, RR_MAP = 16, 176, 12, 7
+
+
+def _rel(a, b):
+    return np.abs(a - b).max() / max(np.abs(b).max(), 1e-12)
+
+
+def _device_step(world, st, f, cache=None):
+    """One forward through the C-ABI with explicit buffers; returns
+    (next_state, snapshot, cache) as numpy plus the device buffers."""
+    dev = world.native()
+    d = torch.device("cuda:0")
+    B = st.shape[0]
+    ts = torch.tensor(st, device=d)
+    tf = torch.tensor(f, device=d)
+    if cache is None:
+        cache = torch.zeros((B, dev.cache_doubles), dtype=torch.float64, device=d)
+        cache[:, 0] = -1
+    nxt = torch.empty_like(ts)
+    snap = torch.zeros((B, dev.snapshot_doubles), dtype=torch.float64, device=d)
+    dev.forward(ts, tf, cache, nxt, snap, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return nxt, snap, cache, ts, tf
+
+
+def _device_backward(world, ts, tf, snap, g):
+    dev = world.native()
+    gs = torch.empty_like(ts)
+    gf = torch.empty_like(tf)
+    dev.backward(ts, tf, snap, torch.tensor(g, device=ts.device), gs, gf, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return gs.cpu().numpy(), gf.cpu().numpy()
+
+
+def _lcp_ambiguous(ow, b, trials=64):
+    """True when the oracle's Dantzig outcome on world b's LCP flips under
+    1e-15 relative symmetric perturbations of A."""
+    A, bb, lo, hi, fi = O.lcp_problem(ow, b)
+    rng = np.random.default_rng(b)
+    outs = set()
+    for _ in range(trials):
+        N = rng.standard_normal(A.shape)
+        ok, _x = O.dantzig(A * (1 + 1e-15 * (N + N.T) / 2), bb, lo, hi, fi, True)
+        outs.add(ok)
+        if len(outs) == 2:
+            return True
+    return False
+
+
+def _same_path(ow, sn, b):
+    fl = O.lcp_flags(ow, b)
+    gfl = np.array([sn[6], sn[7], sn[4], sn[2], sn[3]])
+    m = int(sn[SN_M])
+    mapping, _ = O.lcp_debug(ow, b)
+    gm = sn[SN_ROWS:SN_ROWS + SN_ROWREC * m].reshape(m, SN_ROWREC)[:, RR_MAP].astype(int)
+    return np.array_equal(fl, gfl) and np.array_equal(gm, mapping)
+
+
+def _check_contacts(ow, snap, B):
+    """Contact sets bit-exact for every world; returns the mask of worlds on
+    the same LCP path (the others are checked to be ill-posed)."""
+    same = np.ones(B, dtype=bool)
+    for b in range(B):
+        ref = O.contacts(ow, b)
+        sn = snap[b]
+        nc = int(sn[SN_NCON])
+        assert nc == len(ref), (b, nc, len(ref))
+        got = sn[SN_CONTACTS:SN_CONTACTS + 10 * nc].reshape(nc, 10)
+        # bit-exact identity of the contact set: bodies and types in order
+        assert np.array_equal(got[:, 7:10].astype(int), ref[:, 7:10].astype(int)), b
+        assert np.abs(got[:, :7] - ref[:, :7]).max(initial=0) < 1e-9, b
+        mapping, _ = O.lcp_debug(ow, b)
+        assert int(sn[SN_M]) == len(mapping), b
+        if not _same_path(ow, sn, b):
+            assert _lcp_ambiguous(ow, b), f"world {b}: LCP path differs on a well-posed problem"
+            same[b] = False
+    assert (~same).sum() <= max(1, int(0.03 * B)), (~same).sum()
+    return same
+
+
+def _parity(world, st, f, seed=11, check_grad=True):
+    ow = O.OracleWorld(world)
+    ref = ow.forward(st, f)
+    nxt, snap, cache, ts, tf = _device_step(world, st, f)
+    B = st.shape[0]
+    same = _check_contacts(ow, snap.cpu().numpy(), B)
+    n = world.getNumDofs()
+    got = nxt.cpu().numpy()[same]
+    ref = ref[same]
+    assert _rel(got[:, :n], ref[:, :n]) < RTOL
+    assert _rel(got[:, n:], ref[:, n:]) < RTOL
+    if check_grad:
+        g = np.random.default_rng(seed).standard_normal(st.shape)
+        rgs, rgf = ow.backward(g)
+        ggs, ggf = _device_backward(world, ts, tf, snap, g)
+        ggs, ggf, rgs, rgf = ggs[same], ggf[same], rgs[same], rgf[same]
+        assert _rel(ggs[:, :n], rgs[:, :n]) < RTOL, _rel(ggs[:, :n], rgs[:, :n])
+        assert _rel(ggs[:, n:], rgs[:, n:]) < RTOL, _rel(ggs[:, n:], rgs[:, n:])
+        assert _rel(ggf, rgf) < RTOL, _rel(ggf, rgf)
+    return ow, snap.cpu().numpy()
+
+
+@pytest.mark.parametrize("kind", ["rest", "slide", "tilt", "lift"])
+def test_box_contact_parity(kind):
+    world = models.box_world()
+    st, f = models.box_states(kind, 64, seed=5)
+    ow, snap = _parity(world, st, f)
+    ncon = snap[:, SN_NCON]
+    assert (ncon > 0).all()
+    if kind == "slide":
+        assert (snap[:, SN_NU] > 0).any()  # friction at the cone bound
+
+
+def test_atlas_contact_parity():
+    world = models.atlas_world(True)
+    st, f = models.random_states(world, 64, seed=3, q_scale=0.01, v_scale=0.02)
+    ow, snap = _parity(world, st, f)
+    assert (snap[:, SN_NCON] > 0).mean() > 0.5
+
+
+def test_atlas_rollout_warm_start():
+    """Five chained steps: the LCP cache written by each step seeds the next."""
+    world = models.atlas_world(True)
+    st, f = models.random_states(world, 32, seed=9, q_scale=0.01, v_scale=0.02)
+    ow = O.OracleWorld(world)
+    cache = None
+    cur = st
+    n = world.getNumDofs()
+    for k in range(5):
+        ref = ow.forward(cur, f)
+        nxt, snap, cache, ts, tf = _device_step(world, cur, f, cache)
+        got = nxt.cpu().numpy()
+        same = _check_contacts(ow, snap.cpu().numpy(), st.shape[0])
+        assert _rel(got[same], ref[same]) < RTOL, (k, _rel(got[same], ref[same]))
+        g = np.random.default_rng(k).standard_normal(st.shape)
+        rgs, rgf = ow.backward(g)
+        ggs, ggf = _device_backward(world, ts, tf, snap, g)
+        assert _rel(ggs[same], rgs[same]) < RTOL, (k, _rel(ggs[same], rgs[same]))
+        assert _rel(ggf[same], rgf[same]) < RTOL
+        cur = ref
+
+
+def test_timestep_layer_with_contact():
+    """The autograd.Function path (nimble.timestep) on the contact world."""
+    import nimblephysics_amd as nimble
+    world = models.atlas_world(True)
+    st, f = models.random_states(world, 16, seed=21, q_scale=0.01, v_scale=0.02)
+    ow = O.OracleWorld(world)
+    ref = ow.forward(st, f)
+    g = np.random.default_rng(4).standard_normal(st.shape)
+    rgs, rgf = ow.backward(g)
+    d = torch.device("cuda:0")
+    ts = torch.tensor(st, device=d, requires_grad=True)
+    tf = torch.tensor(f, device=d, requires_grad=True)
+    out = nimble.timestep(world, ts, tf)
+    out.backward(torch.tensor(g, device=d))
+    assert (O.lcp_flags(ow, 0) == O.lcp_flags(ow, 0)).all()
+    assert _rel(out.detach().cpu().numpy(), ref) < RTOL
+    assert _rel(ts.grad.cpu().numpy(), rgs) < RTOL
+    assert _rel(tf.grad.cpu().numpy(), rgf) < RTOL

@@ -89,6 +89,42 @@ class KernelTimer:
         return float(np.mean([s.elapsed_time(e) for s, e in pairs])) if pairs else float("nan")
 
 
+def contact_stats(world, state, action):
+    """One probe step through the C-ABI (outside the timed region): average
+    contacts, LCP rows and clamping rows per world of the workload."""
+    dev = world.native()
+    B = state.shape[0]
+    cache = torch.zeros((B, dev.cache_doubles), dtype=torch.float64, device=state.device)
+    cache[:, 0] = -1
+    nxt = torch.empty_like(state)
+    snap = torch.zeros((B, dev.snapshot_doubles), dtype=torch.float64, device=state.device)
+    n = world.getNumDofs()
+    forces = torch.zeros((B, n), dtype=torch.float64, device=state.device)
+    idx = torch.tensor(world.getActionSpace(), dtype=torch.long, device=state.device)
+    forces.index_copy_(1, idx, action)
+    dev.forward(state, forces, cache, nxt, snap, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    if dev.snapshot_doubles < 8:
+        return {"contacts": 0.0, "rows": 0.0, "clamping": 0.0, "worlds_in_contact": 0.0}
+    h = snap[:, :8].cpu().numpy() if dev.snapshot_doubles > 8 else np.zeros((B, 8))
+    return {"contacts": float(h[:, 0].mean()), "rows": float(h[:, 1].mean()), "clamping": float(h[:, 2].mean()),
+            "worlds_in_contact": float((h[:, 0] > 0).mean())}
+
+
+def pmc_traffic(kernel, batch):
+    """HBM bytes per launch of `kernel` from the committed PMC summary
+    (profiles/pmc_traffic.json: per-world FETCH_SIZE x2 (gfx950 correction)
+    + WRITE_SIZE, measured by tools/pmc_traffic.py); None when absent."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        return float(d[kernel]["bytes_per_world"]) * batch
+    except Exception:
+        return None
+
+
 def cpu_baseline(world, batch, seconds_target=12.0):
     """Oracle (CPU restatement, 1 thread) on a bounded sample of the same workload."""
     from oracle.oracle import OracleWorld
@@ -127,6 +163,7 @@ def main():
     state = torch.tensor(st, device=dev)
     action = torch.tensor(f, device=dev)
     g = torch.tensor(np.random.default_rng(rank).standard_normal(st.shape), device=dev)
+    cstats = contact_stats(world, state, action)
     devworld = world.native()
     timer = KernelTimer()
     timer.wrap(devworld)
@@ -161,7 +198,7 @@ def main():
     value = total / elapsed
     fwd_ms = timer.mean_ms(timer.fwd)
     bwd_ms = timer.mean_ms(timer.bwd)
-    flops = _native.flop_estimate(world)
+    flops = _native.flop_estimate(world, cstats["rows"], cstats["clamping"])
     dom = "backward" if bwd_ms >= fwd_ms else "forward"
     dom_ms = max(bwd_ms, fwd_ms)
     achieved = flops[dom] * args.batch / (dom_ms * 1e-3) / 1e12
@@ -172,11 +209,15 @@ def main():
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f64", "data": "synthetic (perturbed standing pose, random torques)",
             "config": {"workload": wl_name, "worlds_per_gpu": args.batch, "dofs": n,
-                       "global_batch": args.batch * ws, "parallelism": f"independent worlds x{ws}"},
+                       "global_batch": args.batch * ws, "parallelism": f"independent worlds x{ws}",
+                       "contacts_per_world": cstats["contacts"], "lcp_rows_per_world": cstats["rows"],
+                       "clamping_rows_per_world": cstats["clamping"],
+                       "worlds_in_contact": cstats["worlds_in_contact"]},
             "kernels_ms": {"forward": fwd_ms, "backward": bwd_ms},
             "roofline": {"bound": "mfma", "kernel": f"nimble_{dom}_kernel", "achieved": achieved,
                          "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP64_VECTOR_PEAK_TFLOPS,
-                         "traffic": None, "flops_per_world": flops[dom],
+                         "traffic": pmc_traffic(f"nimble_{dom}_kernel", args.batch),
+                         "flops_per_world": flops[dom],
                          "note": "fp64 VALU-bound (no fp64 MFMA use); peak = fp64 vector rate"},
         }
         if not args.no_cpu_baseline:

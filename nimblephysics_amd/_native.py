@@ -98,7 +98,28 @@ class DeviceWorld:
                                      _ptr(grad_state), _ptr(grad_forces), C.c_void_p(stream_ptr)))
 
 
-def flop_estimate(world) -> dict:
+def contact_flop_estimate(world, rows: float, clamping: float) -> dict:
+    """Algorithmic fp64 FLOPs per world of the contact stage for `rows` LCP
+    rows of which `clamping` clamp (averages over the batch): forward = J^T
+    columns, m Cholesky solves, A = J Minv J^T, b, the COD solves of the
+    guess + standardisation; backward = A_c / A_c_ub_E, nc solves, Q, pinv(Q)
+    by COD, the vector chain, the G_j^T g_j terms and the M-derivative
+    fields."""
+    d = world.desc_arrays()
+    nb, n = int(d["num_bodies"]), int(d["num_dofs"])
+    m, c = float(rows), float(clamping)
+    if m <= 0:
+        return {"forward": 0.0, "backward": 0.0}
+    cod = lambda k: 4.0 / 3.0 * k ** 3 + 4.0 * k * k  # noqa: E731
+    fwd = n * m * 14 + m * 2 * n * n + m * m * n + 2 * n * m + m * m * 2 + 2 * cod(m) + 2 * n * m
+    depth = 8.0  # ancestor dofs per contact body (Atlas foot chain incl. root: 12)
+    bwd = (2 * n * c * 14 * 2 + c * 2 * n * n + 2 * c * c * n + cod(c) + c * 4 * c * c + 2 * c * c * c
+           + 24 * n * c + 4 * 2 * n * n + m * n * 16 + n * m * (depth * 12 + 90)
+           + 8 * nb * (n * 12 + 100) + n * 8 * 30)
+    return {"forward": float(fwd), "backward": float(bwd)}
+
+
+def flop_estimate(world, rows: float = 0.0, clamping: float = 0.0) -> dict:
     """Algorithmic fp64 FLOPs per world for one launch of each kernel, counted
     from the implemented algorithm's loop structure (FMA = 2 FLOPs):
     kinematics, world-frame composites, CRBA mass matrix, Cholesky + solves,
@@ -141,4 +162,5 @@ def flop_estimate(world) -> dict:
             elif c in anc[b]:
                 lanes += 50 * ndof[c]
     bwd = kin * 2 + comp + mass + chol + 2 * solve + dcomp + lanes + 20 * n
-    return {"forward": float(fwd), "backward": float(bwd)}
+    c = contact_flop_estimate(world, rows, clamping)
+    return {"forward": float(fwd + c["forward"]), "backward": float(bwd + c["backward"])}

@@ -54,6 +54,42 @@ def barrier(dist):
         dist.barrier()
 
 
+def _sync(device):
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+
+
+def timed_loop(step, state, steps, warmup, dist, device):
+    """W untimed warmup steps, then EXACTLY `steps` timed steps bracketed by
+    barrier + device synchronize on both sides; returns (state, elapsed),
+    elapsed = max over ranks."""
+    for _ in range(warmup):
+        state = step(state)
+    _sync(device)
+    barrier(dist)
+    _sync(device)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        state = step(state)
+    _sync(device)
+    barrier(dist)
+    _sync(device)
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return state, elapsed
+
+
+def gather_grads(dist, grad, ws):
+    """north_star's RCCL all-gather of the per-world action gradients (the
+    one exchange step of a multi-GPU training loop); returns [ws*B, m]."""
+    out = torch.empty((ws * grad.shape[0],) + tuple(grad.shape[1:]), dtype=grad.dtype, device=grad.device)
+    dist.all_gather_into_tensor(out, grad.contiguous())
+    return out
+
+
 class KernelTimer:
     """HIP events around the native launches, on the stream they run on."""
 
@@ -151,6 +187,8 @@ def main():
     ap.add_argument("--batch", type=int, default=1024, help="worlds per GPU")
     ap.add_argument("--workload", default="atlas", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gather-grads", type=int, default=-1,
+                    help="all-gather action gradients each step (default: on when N > 1)")
     args = ap.parse_args()
 
     dist, rank, ws, local = init_dist()
@@ -168,32 +206,22 @@ def main():
     timer = KernelTimer()
     timer.wrap(devworld)
 
+    gather = (ws > 1) if args.gather_grads < 0 else bool(args.gather_grads)
+
     def one_step(state):
         s = state.detach().requires_grad_(True)
         a = action.detach().requires_grad_(True)
         nxt = nimble.timestep(world, s, a)
         nxt.backward(g)
+        if gather and dist is not None:
+            gather_grads(dist, a.grad, ws)
         return nxt.detach()
 
-    s0 = state
     for _ in range(args.warmup):
         state = one_step(state)
-    torch.cuda.synchronize()
-    barrier(dist)
-    torch.cuda.synchronize()
     timer.enabled = True
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        state = one_step(state)
-    torch.cuda.synchronize()
-    barrier(dist)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    state, elapsed = timed_loop(one_step, state, args.steps, 0, dist, dev)
     timer.enabled = False
-    if dist is not None:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
     total = args.batch * ws * args.steps
     value = total / elapsed
     fwd_ms = timer.mean_ms(timer.fwd)
@@ -209,7 +237,8 @@ def main():
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f64", "data": "synthetic (perturbed standing pose, random torques)",
             "config": {"workload": wl_name, "worlds_per_gpu": args.batch, "dofs": n,
-                       "global_batch": args.batch * ws, "parallelism": f"independent worlds x{ws}",
+                       "global_batch": args.batch * ws,
+                       "parallelism": f"independent worlds x{ws}" + (" + RCCL all-gather of action grads" if gather else ""),
                        "contacts_per_world": cstats["contacts"], "lcp_rows_per_world": cstats["rows"],
                        "clamping_rows_per_world": cstats["clamping"],
                        "worlds_in_contact": cstats["worlds_in_contact"]},

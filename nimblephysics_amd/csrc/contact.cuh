@@ -27,6 +27,17 @@
 #define CT_FACE_VERTEX 1
 #define CT_VERTEX_FACE 2
 #define CT_EDGE_EDGE 3
+#ifdef NIMBLE_STAGE_TIMING
+// debug builds: per-stage shader-clock stamps into the snapshot workspace
+#define STAMP(k)                                                                   \
+  do {                                                                             \
+    if (lane == 0 && g_stamp) g_stamp[k] = (double)__builtin_amdgcn_s_memtime(); \
+  } while (0)
+__device__ double* g_stamp_dummy;
+#else
+#define STAMP(k) do { } while (0)
+#endif
+
 #define CM_CLAMPING (-1)
 #define CM_NOT_CLAMPING (-2)
 
@@ -395,8 +406,9 @@ __device__ void codFactor(Cod& c, double* cn, double* v, int lane) {
   __syncthreads();
 }
 
-// x (n) = min-norm least-squares solution for rhs (m, destroyed); z: n scratch.
-__device__ void codSolveOne(const Cod& c, double* rhs, double* x, double* z) {
+// Per-lane solve on a codFactor()ed matrix (each lane its own rhs, e.g. the
+// columns of pinv(Q)): x (n) = min-norm least squares for rhs (m, destroyed).
+__device__ void codSolveLane(const Cod& c, double* rhs, double* x, double* z) {
   const double* A = c.A;
   const int m = c.m, n = c.n, ld = c.ld;
   for (int k = 0; k < c.kmax; k++) {
@@ -427,378 +439,7 @@ __device__ void codSolveOne(const Cod& c, double* rhs, double* x, double* z) {
   for (int j = 0; j < n; j++) x[c.perm[j]] = z[j];
 }
 
-// ---------------------------------------------------------------------------
-// Dantzig boxed LCP (dart/external/odelcpsolver/lcp.cpp:780 dSolveLCP) on a
-// full, explicitly permuted LDS matrix.  Sequential pivoting: lane 0 only.
-// ---------------------------------------------------------------------------
-struct DevDantzig {
-  int n, nC, nN;
-  double *A, *x, *b, *w, *lo, *hi, *L, *d, *Dell, *ell, *tmp, *W1, *W2, *ta;
-  int *findex, *p, *C, *state;
-
-  __device__ double& Aat(int i, int j) { return A[i * n + j]; }
-  __device__ void swapD(double* a, int i, int j) { double t = a[i]; a[i] = a[j]; a[j] = t; }
-  __device__ void swapI(int* a, int i, int j) { int t = a[i]; a[i] = a[j]; a[j] = t; }
-  __device__ void swapProblem(int i1, int i2) {
-    if (i1 == i2) return;
-    for (int k = 0; k < n; k++) swapD(A, i1 * n + k, i2 * n + k);
-    for (int k = 0; k < n; k++) swapD(A, k * n + i1, k * n + i2);
-    swapD(x, i1, i2); swapD(b, i1, i2); swapD(w, i1, i2); swapD(lo, i1, i2); swapD(hi, i1, i2);
-    swapI(p, i1, i2); swapI(state, i1, i2); swapI(findex, i1, i2);
-  }
-  __device__ void solveL1(double* B, int m) {
-    for (int i = 0; i < m; i++) {
-      double s = B[i];
-      for (int k = 0; k < i; k++) s -= L[i * n + k] * B[k];
-      B[i] = s;
-    }
-  }
-  __device__ void solveL1T(double* B, int m) {
-    for (int i = m - 1; i >= 0; i--) {
-      double s = B[i];
-      for (int k = i + 1; k < m; k++) s -= L[k * n + i] * B[k];
-      B[i] = s;
-    }
-  }
-  __device__ void transferToC(int i) {
-    if (nC > 0) {
-      for (int j = 0; j < nC; j++) L[nC * n + j] = ell[j];
-      double dd = 0;
-      for (int j = 0; j < nC; j++) dd += ell[j] * Dell[j];
-      d[nC] = 1.0 / (Aat(i, i) - dd);
-    } else {
-      d[0] = 1.0 / Aat(i, i);
-    }
-    swapProblem(nC, i);
-    C[nC] = nC;
-    nC++;
-  }
-  __device__ void transferFromNtoC(int i) {
-    if (nC > 0) {
-      for (int j = 0; j < nC; j++) Dell[j] = Aat(i, C[j]);
-      solveL1(Dell, nC);
-      for (int j = 0; j < nC; j++) L[nC * n + j] = ell[j] = Dell[j] * d[j];
-      double dd = 0;
-      for (int j = 0; j < nC; j++) dd += ell[j] * Dell[j];
-      d[nC] = 1.0 / (Aat(i, i) - dd);
-    } else {
-      d[0] = 1.0 / Aat(i, i);
-    }
-    swapProblem(nC, i);
-    C[nC] = nC;
-    nN--;
-    nC++;
-  }
-  // _dLDLTAddTL (dart/external/odelcpsolver/matrix.cpp:286)
-  __device__ void ldltAddTL(double* Ls, double* ds, const double* a, int m) {
-    if (m < 2) return;
-    const double r2 = 0.70710678118654752440;
-    W1[0] = W2[0] = 0.0;
-    for (int j = 1; j < m; j++) W1[j] = W2[j] = a[j] * r2;
-    double W11 = (0.5 * a[0] + 1) * r2;
-    double W21 = (0.5 * a[0] - 1) * r2;
-    double alpha1 = 1.0, alpha2 = 1.0;
-    {
-      double dee = ds[0];
-      double alphanew = alpha1 + (W11 * W11) * dee;
-      dee /= alphanew;
-      double gamma1 = W11 * dee;
-      dee *= alpha1;
-      alpha1 = alphanew;
-      alphanew = alpha2 - (W21 * W21) * dee;
-      dee /= alphanew;
-      alpha2 = alphanew;
-      double k1 = 1.0 - W21 * gamma1;
-      double k2 = W21 * gamma1 * W11 - W21;
-      for (int q = 1; q < m; q++) {
-        double Wp = W1[q];
-        double el = Ls[q * n];
-        W1[q] = Wp - W11 * el;
-        W2[q] = k1 * Wp + k2 * el;
-      }
-    }
-    for (int j = 1; j < m; j++) {
-      double k1 = W1[j], k2 = W2[j];
-      double dee = ds[j];
-      double alphanew = alpha1 + (k1 * k1) * dee;
-      dee /= alphanew;
-      double gamma1 = k1 * dee;
-      dee *= alpha1;
-      alpha1 = alphanew;
-      alphanew = alpha2 - (k2 * k2) * dee;
-      dee /= alphanew;
-      double gamma2 = k2 * dee;
-      dee *= alpha2;
-      ds[j] = dee;
-      alpha2 = alphanew;
-      for (int q = j + 1; q < m; q++) {
-        double el = Ls[q * n + j];
-        double Wp = W1[q] - k1 * el;
-        el += gamma1 * Wp;
-        W1[q] = Wp;
-        Wp = W2[q] - k2 * el;
-        el -= gamma2 * Wp;
-        W2[q] = Wp;
-        Ls[q * n + j] = el;
-      }
-    }
-  }
-  // _dLDLTRemove (matrix.cpp:374) + _dRemoveRowCol
-  __device__ void ldltRemove(int r, int n2) {
-    if (r != n2 - 1) {
-      if (r == 0) {
-        for (int i = 0; i < n2; i++) ta[i] = -Aat(C[i], C[0]);
-        ta[0] += 1.0;
-        ldltAddTL(L, d, ta, n2);
-      } else {
-        // t (first r) then a (n2 - r) share `ta`: t in tmp
-        for (int i = 0; i < r; i++) tmp[i] = L[r * n + i] / d[i];
-        for (int i = 0; i < n2 - r; i++) {
-          double s = 0;
-          for (int k = 0; k < r; k++) s += L[(r + i) * n + k] * tmp[k];
-          ta[i] = s - Aat(C[r + i], C[r]);
-        }
-        ta[0] += 1.0;
-        ldltAddTL(L + r * n + r, d + r, ta, n2 - r);
-      }
-    }
-    if (r < n2 - 1) {
-      for (int i = 0; i < n2; i++)
-        for (int j = r; j < n2 - 1; j++) L[i * n + j] = L[i * n + j + 1];
-      for (int i = r; i < n2 - 1; i++)
-        for (int j = 0; j < n2; j++) L[i * n + j] = L[(i + 1) * n + j];
-      for (int i = r; i < n2 - 1; i++) d[i] = d[i + 1];
-    }
-  }
-  __device__ void transferFromCtoN(int i) {
-    int j = 0, lastIdx = -1;
-    for (; j < nC; j++) {
-      if (C[j] == nC - 1) lastIdx = j;
-      if (C[j] == i) {
-        ldltRemove(j, nC);
-        int k;
-        if (lastIdx == -1) {
-          for (k = j + 1; k < nC; k++)
-            if (C[k] == nC - 1) break;
-        } else {
-          k = lastIdx;
-        }
-        C[k] = C[j];
-        for (int t = j; t < nC - 1; t++) C[t] = C[t + 1];
-        break;
-      }
-    }
-    swapProblem(i, nC - 1);
-    nN++;
-    nC--;
-  }
-  __device__ void solve1(double* a, int i, int dir, bool onlyTransfer) {
-    if (nC > 0) {
-      for (int j = 0; j < nC; j++) Dell[j] = Aat(i, C[j]);
-      solveL1(Dell, nC);
-      for (int j = 0; j < nC; j++) ell[j] = Dell[j] * d[j];
-      if (!onlyTransfer) {
-        for (int j = 0; j < nC; j++) tmp[j] = ell[j];
-        solveL1T(tmp, nC);
-        if (dir > 0)
-          for (int j = 0; j < nC; j++) a[C[j]] = -tmp[j];
-        else
-          for (int j = 0; j < nC; j++) a[C[j]] = tmp[j];
-      }
-    }
-  }
-  __device__ double AiC_qC(int i, const double* q) { double s = 0; for (int j = 0; j < nC; j++) s += Aat(i, j) * q[j]; return s; }
-  __device__ double AiN_qN(int i, const double* q) { double s = 0; for (int j = nC; j < nC + nN; j++) s += Aat(i, j) * q[j]; return s; }
-};
-
-// Solve with early termination (the contact solver's setting).  On entry A
-// (n x n, destroyed), b, lo, hi, findex are the problem; x receives the
-// solution.  scr: 16 n doubles; iscr: 4 n ints.  Lane 0 only.
-__device__ bool devDantzig(int n, double* A, double* x, double* b, double* lo, double* hi, int* findex, double* Lbuf,
-                           double* scr, int* iscr) {
-  const double kInf = __builtin_inf();
-  DevDantzig D;
-  D.n = n; D.nC = 0; D.nN = 0;
-  D.A = A; D.x = x; D.b = b; D.lo = lo; D.hi = hi; D.findex = findex; D.L = Lbuf;
-  D.w = scr; D.d = scr + n; D.Dell = scr + 2 * n; D.ell = scr + 3 * n; D.tmp = scr + 4 * n;
-  D.W1 = scr + 5 * n; D.W2 = scr + 6 * n; D.ta = scr + 7 * n;
-  double* delta_x = scr + 8 * n;
-  double* delta_w = scr + 9 * n;
-  double* tcopy = scr + 10 * n;
-  D.p = iscr; D.C = iscr + n; D.state = iscr + 2 * n;
-  for (int k = 0; k < n * n; k++) Lbuf[k] = 0.0;
-  for (int k = 0; k < n; k++) {
-    x[k] = 0.0; D.p[k] = k; D.C[k] = 0; D.state[k] = 0;
-    D.w[k] = D.d[k] = D.Dell[k] = D.ell[k] = D.tmp[k] = 0.0;
-    delta_x[k] = delta_w[k] = 0.0;
-  }
-  for (int k = 0; k < n; k++) {
-    if (findex[k] >= 0) continue;
-    if (lo[k] == -kInf && hi[k] == kInf) return false;  // unbounded rows never occur for contacts
-  }
-  {
-    int numAtEnd = 0;
-    for (int k = n - 1; k >= 0; k--)
-      if (findex[k] >= 0) { D.swapProblem(k, n - 1 - numAtEnd); numAtEnd++; }
-  }
-  double* w = D.w;
-  bool hitFirstFriction = false;
-  for (int i = 0; i < n; i++) {
-    bool sError = false;
-    if (!hitFirstFriction && findex[i] >= 0) {
-      for (int j = 0; j < n; j++) delta_w[D.p[j]] = x[j];
-      for (int k = i; k < n; k++) {
-        double wfk = delta_w[findex[k]];
-        if (wfk == 0) { hi[k] = 0; lo[k] = 0; }
-        else { hi[k] = fabs(hi[k] * wfk); lo[k] = -hi[k]; }
-      }
-      hitFirstFriction = true;
-    }
-    w[i] = D.AiC_qC(i, x) + D.AiN_qN(i, x) - b[i];
-    if (lo[i] == 0 && w[i] >= 0) {
-      D.nN++;
-      D.state[i] = 0;
-    } else if (hi[i] == 0 && w[i] <= 0) {
-      D.nN++;
-      D.state[i] = 1;
-    } else if (w[i] == 0) {
-      D.solve1(delta_x, i, 0, true);
-      D.transferToC(i);
-    } else {
-      for (;;) {
-        int dir;
-        double dirf;
-        if (w[i] <= 0) { dir = 1; dirf = 1.0; } else { dir = -1; dirf = -1.0; }
-        D.solve1(delta_x, i, dir, false);
-        for (int k = 0; k < D.nN; k++) delta_w[D.nC + k] = D.AiC_qC(D.nC + k, delta_x);
-        for (int k = 0; k < D.nN; k++) delta_w[D.nC + k] += dir > 0 ? D.Aat(i, D.nC + k) : -D.Aat(i, D.nC + k);
-        delta_w[i] = D.AiC_qC(i, delta_x) + D.Aat(i, i) * dirf;
-        int cmd = 1, si = 0;
-        double s = -w[i] / delta_w[i];
-        if (dir > 0) {
-          if (hi[i] < kInf) { double s2 = (hi[i] - x[i]) * dirf; if (s2 < s) { s = s2; cmd = 3; } }
-        } else {
-          if (lo[i] > -kInf) { double s2 = (lo[i] - x[i]) * dirf; if (s2 < s) { s = s2; cmd = 2; } }
-        }
-        for (int k = 0; k < D.nN; k++) {
-          const int idx = D.nC + k;
-          if (!D.state[idx] ? delta_w[idx] < 0 : delta_w[idx] > 0) {
-            if (lo[idx] == 0 && hi[idx] == 0) continue;
-            double s2 = -w[idx] / delta_w[idx];
-            if (s2 < s) { s = s2; cmd = 4; si = idx; }
-          }
-        }
-        for (int k = 0; k < D.nC; k++) {
-          if (delta_x[k] < 0 && lo[k] > -kInf) {
-            double s2 = (lo[k] - x[k]) / delta_x[k];
-            if (s2 < s) { s = s2; cmd = 5; si = k; }
-          }
-          if (delta_x[k] > 0 && hi[k] < kInf) {
-            double s2 = (hi[k] - x[k]) / delta_x[k];
-            if (s2 < s) { s = s2; cmd = 6; si = k; }
-          }
-        }
-        if (s <= 0.0) return false;  // early termination
-        for (int k = 0; k < D.nC; k++) x[k] += s * delta_x[k];
-        x[i] += s * dirf;
-        for (int k = 0; k < D.nN; k++) w[D.nC + k] += s * delta_w[D.nC + k];
-        w[i] += s * delta_w[i];
-        switch (cmd) {
-          case 1: w[i] = 0; D.transferToC(i); break;
-          case 2: x[i] = lo[i]; D.state[i] = 0; D.nN++; break;
-          case 3: x[i] = hi[i]; D.state[i] = 1; D.nN++; break;
-          case 4: w[si] = 0; D.transferFromNtoC(si); break;
-          case 5: x[si] = lo[si]; D.state[si] = 0; D.transferFromCtoN(si); break;
-          case 6: x[si] = hi[si]; D.state[si] = 1; D.transferFromCtoN(si); break;
-        }
-        if (cmd <= 3) break;
-      }
-    }
-    if (sError) break;
-  }
-  for (int j = 0; j < n; j++) tcopy[j] = x[j];
-  for (int j = 0; j < n; j++) x[D.p[j]] = tcopy[j];
-  return true;
-}
-
-// PgsBoxedLcpSolver::solve (dart/constraint/PgsBoxedLcpSolver.cpp:85) with the
-// default option (30 iterations, 1e-6, 1e-3, 1e-9).  A, b modified.  Lane 0.
-__device__ bool devPgs(int n, double* A, double* x, double* b, const double* lo, const double* hi, const int* findex,
-                       int* order) {
-  const int maxIter = 30;
-  const double deltaXThr = 1e-6, relTol = 1e-3, epsDiv = 1e-9;
-  int no = 0;
-  bool possible = true;
-  for (int i = 0; i < n; i++) {
-    if (A[i * n + i] < epsDiv) { x[i] = 0.0; continue; }
-    order[no++] = i;
-    const double old = x[i];
-    double nx = b[i];
-    for (int j = 0; j < n; j++) if (j != i) nx -= A[i * n + j] * x[j];
-    nx /= A[i * n + i];
-    if (findex[i] >= 0) {
-      const double h = hi[i] * x[findex[i]], l = -h;
-      x[i] = nx > h ? h : (nx < l ? l : nx);
-    } else {
-      x[i] = nx > hi[i] ? hi[i] : (nx < lo[i] ? lo[i] : nx);
-    }
-    if (possible && fabs(x[i] - old) > deltaXThr) possible = false;
-  }
-  if (possible) return true;
-  for (int t = 0; t < no; t++) {
-    const int idx = order[t];
-    const double dummy = 1.0 / A[idx * n + idx];
-    b[idx] *= dummy;
-    for (int j = 0; j < n; j++) A[idx * n + j] *= dummy;
-  }
-  for (int iter = 1; iter < maxIter; iter++) {
-    possible = true;
-    for (int t = 0; t < no; t++) {
-      const int idx = order[t];
-      double nx = b[idx];
-      const double old = x[idx];
-      for (int j = 0; j < n; j++) if (j != idx) nx -= A[idx * n + j] * x[j];
-      if (findex[idx] >= 0) {
-        const double h = hi[idx] * x[findex[idx]], l = -h;
-        x[idx] = nx > h ? h : (nx < l ? l : nx);
-      } else {
-        x[idx] = nx > hi[idx] ? hi[idx] : (nx < lo[idx] ? lo[idx] : nx);
-      }
-      if (possible && fabs(x[idx]) > epsDiv) {
-        if (fabs((x[idx] - old) / x[idx]) > relTol) possible = false;
-      }
-    }
-    if (possible) break;
-  }
-  return possible;
-}
-
-// LCPUtils::isLCPSolutionValid (dart/neural/LCPUtils.cpp:14) for A + cfm I.
-__device__ bool devLcpValid(int m, const double* A, double cfm, const double* x, const double* b, const double* hi,
-                            const double* lo, const int* fi, bool ignoreFriction) {
-  for (int i = 0; i < m; i++) {
-    double v = -b[i];
-    for (int j = 0; j < m; j++) v += (A[i * m + j] + (i == j ? cfm : 0.0)) * x[j];
-    double up = hi[i], low = lo[i];
-    if (fi[i] != -1) {
-      if (ignoreFriction) { if (x[i] != 0) return false; continue; }
-      up *= x[fi[i]];
-      low *= x[fi[i]];
-    }
-    const double tol = 1e-5;
-    if (fabs(low) < tol && fabs(up) < tol && fabs(x[i]) < tol) {
-    } else if (fabs(x[i] - low) < tol) {
-      if (v < -tol) return false;
-    } else if (fabs(x[i] - up) < tol) {
-      if (v > tol) return false;
-    } else if (x[i] > low && x[i] < up) {
-      if (fabs(v) > tol) return false;
-    } else {
-      return false;
-    }
-  }
-  return true;
-}
+#include "lcp_wave.cuh"
 
 // ---------------------------------------------------------------------------
 // Contact-stage LDS header (at Layout::ct) and snapshot layout.
@@ -979,15 +620,14 @@ __device__ bool devConstruct(FwdPool& P, int m, double cfm, bool ignoreFriction,
     }
     __syncthreads();
     const int nc = (int)ct[H_NC];
+    const double bR = lane < m ? P.b[lane] : 0.0, hiR = lane < m ? P.hi[lane] : 0.0;
+    const double loR = lane < m ? P.lo[lane] : 0.0;
+    const int fiR = lane < m ? P.fi[lane] : -1;
     if (nc == 0) {
-      if (lane == 0) {
-        for (int j = 0; j < m; j++) P.nx[j] = 0.0;
-        const bool ok = devLcpValid(m, P.A, cfm, P.nx, P.b, P.hi, P.lo, P.fi, ignoreFriction);
-        if (ok) for (int j = 0; j < m; j++) P.X[j] = 0.0;
-        ct[H_STD] = ok ? 1 : 0;
-      }
+      const bool ok = waveLcpValid(m, P.A, cfm, 0.0, bR, hiR, loR, fiR, ignoreFriction, lane);
+      if (ok && lane < m) P.X[lane] = 0.0;
       __syncthreads();
-      return ct[H_STD] != 0;
+      return ok;
     }
     // Q (nc x nc) into M1
     double* Q = P.M1;
@@ -1008,9 +648,13 @@ __device__ bool devConstruct(FwdPool& P, int m, double cfm, bool ignoreFriction,
     double* rhs = w; w += m;
     double* z = w; w += m;
     codFactor(cod, cn, vv, lane);
+    {
+      const double f = codSolveWave(cod, lane < nc ? P.relVel[lane] : 0.0, z, lane);
+      if (lane < nc) P.fsol[lane] = f;
+    }
+    (void)rhs;
+    __syncthreads();
     if (lane == 0) {
-      for (int i = 0; i < nc; i++) rhs[i] = P.relVel[i];
-      codSolveOne(cod, rhs, P.fsol, z);
       bool anyNewlyNot = false;
       for (int i = 0; i < m; i++) {
         P.nx[i] = 0.0;
@@ -1026,17 +670,16 @@ __device__ bool devConstruct(FwdPool& P, int m, double cfm, bool ignoreFriction,
           P.nx[i] = P.fsol[P.clampIdx[fp]] * clean;
         }
       }
-      const bool ok = devLcpValid(m, P.A, cfm, P.nx, P.b, P.hi, P.lo, P.fi, ignoreFriction);
-      int res = 0;
-      if (ok) {
-        for (int i = 0; i < m; i++) P.X[i] = P.nx[i];
-        for (int i = 0; i < nc; i++) P.fc[i] = P.fsol[i];
-        res = anyNewlyNot ? 2 : 1;
-      }
-      ct[H_STD] = res;
+      ct[H_FLAG] = anyNewlyNot ? 1 : 0;
     }
     __syncthreads();
-    const int res = (int)ct[H_STD];
+    const bool ok = waveLcpValid(m, P.A, cfm, lane < m ? P.nx[lane] : 0.0, bR, hiR, loR, fiR, ignoreFriction, lane);
+    const int res = ok ? ((int)ct[H_FLAG] ? 2 : 1) : 0;
+    if (ok) {
+      if (lane < m) P.X[lane] = P.nx[lane];
+      if (lane < nc) P.fc[lane] = P.fsol[lane];
+    }
+    __syncthreads();
     if (res != 2) return res != 0;
   }
   return false;
@@ -1068,11 +711,11 @@ __device__ void devGuess(FwdPool& P, int m, double* x, double* ct, int lane) {
   double* z = w; w += m;
   double* xr = w; w += m;
   codFactor(cod, cn, vv, lane);
-  if (lane == 0) {
-    for (int r = 0; r < k; r++) rhs[r] = P.b[P.cl[r]];
-    codSolveOne(cod, rhs, xr, z);
-    for (int r = 0; r < k; r++) x[P.cl[r]] = xr[r];
+  {
+    const double xr_ = codSolveWave(cod, lane < k ? P.b[P.cl[lane]] : 0.0, z, lane);
+    if (lane < k) x[P.cl[lane]] = xr_;
   }
+  (void)rhs; (void)xr;
   __syncthreads();
 }
 
@@ -1085,9 +728,14 @@ __device__ void devGuess(FwdPool& P, int m, double* x, double* ct, int lane) {
 __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int lane, double* v1, double* cache,
                              double* snap, double* overflowWs) {
   const int n = md.n;
+#ifdef NIMBLE_STAGE_TIMING
+  double* g_stamp = snap + snapWorkspaceOffset(n) + 1000;
+#endif
+  STAMP(0);
   double* ct = s + L.ct;
   const double* Lm = s + L.M;
   collideWorld(md, s, L, lane);
+  STAMP(1);
   const int nCon = (int)ct[H_NCON];
   if (nCon == 0) {
     if (lane == 0) {
@@ -1146,29 +794,32 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
     P.cols[t] = rowForceEntry(md, s, L, ct + CT_CONTACTS + P.rowC[j] * CREC, P.dvec + 3 * j, i);
   }
   __syncthreads();
-  // massed = Minv cols (one lane per column: L L^T x = c)
-  for (int j = lane; j < m; j += WAVE) {
-    double* x = P.massed;
-    for (int i = 0; i < n; i++) x[i * m + j] = P.cols[i * m + j];
-    for (int i = 0; i < n; i++) {
-      double sacc = x[i * m + j];
-      for (int k = 0; k < i; k++) sacc -= Lm[i * n + k] * x[k * m + j];
-      x[i * m + j] = sacc / Lm[i * n + i];
+  STAMP(2);
+  // Y = L^-1 J^T (row-parallel forward substitution; `massed` holds Y), so
+  // that A = J Minv J^T = Y^T Y and Minv J^T x = L^-T (Y x)
+  {
+    double* Y = P.massed;
+    for (int t = lane; t < n * m; t += WAVE) Y[t] = P.cols[t];
+    __syncthreads();
+    for (int k = 0; k < n; k++) {
+      const double inv = 1.0 / Lm[k * n + k];
+      for (int j = lane; j < m; j += WAVE) Y[k * m + j] *= inv;
+      __syncthreads();
+      const int cnt = (n - k - 1) * m;
+      for (int t = lane; t < cnt; t += WAVE) {
+        const int i = k + 1 + t / m, j = t % m;
+        Y[i * m + j] -= Lm[i * n + k] * Y[k * m + j];
+      }
+      __syncthreads();
     }
-    for (int i = n - 1; i >= 0; i--) {
-      double sacc = x[i * m + j];
-      for (int k = i + 1; k < n; k++) sacc -= Lm[k * n + i] * x[k * m + j];
-      x[i * m + j] = sacc / Lm[i * n + i];
-    }
-  }
-  __syncthreads();
-  for (int t = lane; t < m * m; t += WAVE) {
-    const int r = t / m, c = t % m;
-    if (r <= c) {
-      double acc = 0;
-      for (int i = 0; i < n; i++) acc += P.cols[i * m + r] * P.massed[i * m + c];
-      P.A[r * m + c] = acc;
-      P.A[c * m + r] = acc;
+    for (int t = lane; t < m * m; t += WAVE) {
+      const int r = t / m, c = t % m;
+      if (r <= c) {
+        double acc = 0;
+        for (int i = 0; i < n; i++) acc += Y[i * m + r] * Y[i * m + c];
+        P.A[r * m + c] = acc;
+        P.A[c * m + r] = acc;
+      }
     }
   }
   for (int r = lane; r < m; r += WAVE) {
@@ -1202,6 +853,7 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
     P.aCol[j] = acc;
   }
   __syncthreads();
+  STAMP(3);
   // warm start (BoxedLcpConstraintSolver::mX) or guessSolution
   const bool cached = (int)cache[0] == m;
   if (cached) {
@@ -1212,102 +864,123 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
     for (int i = lane; i < m; i += WAVE) P.xc[i] = P.X[i];
     __syncthreads();
   }
+  STAMP(4);
   bool success = devConstruct(P, m, 0.0, false, ct, lane);
+  STAMP(5);
   const bool shortCircuit = success;
   double cfm = 0.0;
   bool ignoredFriction = false;
+  const double bR = lane < m ? P.b[lane] : 0.0, hiR = lane < m ? P.hi[lane] : 0.0;
+  const double loR = lane < m ? P.lo[lane] : 0.0;
+  const int fiR = lane < m ? P.fi[lane] : -1;
   if (!success) {
-    // Dantzig on a copy (lane 0)
-    if (lane == 0) {
-      int st = (int)ct[H_STATUS];
-      for (int a = 0; a < m; a++)
-        for (int c = a + 1; c < m; c++) {
-          double dd = 0;
-          for (int i = 0; i < m; i++) dd += (P.A[i * m + a] - P.A[i * m + c]) * (P.A[i * m + a] - P.A[i * m + c]);
-          if (dd < 1e-4 && fabs(P.b[a] - P.b[c]) < 1e-4 && P.fi[a] == P.fi[c] && P.hi[a] == P.hi[c] &&
-              P.lo[a] == P.lo[c])
-            st |= ST_DUPLICATE_COLUMNS;
-        }
-      ct[H_STATUS] = st;
-      double* sc = P.scr;
-      double* xd = sc; sc += m;
-      double* bd = sc; sc += m;
-      double* lod = sc; sc += m;
-      double* hid = sc; sc += m;
-      int* fid = reinterpret_cast<int*>(sc); sc += m;  // m ints (room for 2m)
-      int* iscr = reinterpret_cast<int*>(sc); sc += 2 * m;  // 4m ints
-      double* dscr = sc;  // 11 m
-      for (int i = 0; i < m * m; i++) P.M1[i] = P.A[i];
-      for (int i = 0; i < m; i++) { bd[i] = P.b[i]; lod[i] = P.lo[i]; hid[i] = P.hi[i]; fid[i] = P.fi[i]; }
-      bool ok = devDantzig(m, P.M1, xd, bd, lod, hid, fid, P.M2, dscr, iscr);
-      if (ok) {
-        for (int i = 0; i < m; i++) P.X[i] = xd[i];
-        if (!devLcpValid(m, P.A, 0.0, P.X, P.b, P.hi, P.lo, P.fi, false)) ok = false;
+    // LCPUtils::reduce would merge near-duplicate columns; they do not occur
+    // for box contacts -- flag them in the status word if they ever do
+    {
+      bool dup = false;
+      for (int t = lane; t < m * m; t += WAVE) {
+        const int a = t / m, c = t % m;
+        if (c <= a) continue;
+        double dd = 0;
+        for (int i = 0; i < m; i++) dd += (P.A[i * m + a] - P.A[i * m + c]) * (P.A[i * m + a] - P.A[i * m + c]);
+        if (dd < 1e-4 && fabs(P.b[a] - P.b[c]) < 1e-4 && P.fi[a] == P.fi[c] && P.hi[a] == P.hi[c] && P.lo[a] == P.lo[c])
+          dup = true;
       }
-      ct[H_FLAG] = ok ? 1 : 0;
+      if (__ballot(dup) && lane == 0) ct[H_STATUS] = (double)((int)ct[H_STATUS] | ST_DUPLICATE_COLUMNS);
     }
+    for (int t = lane; t < m * m; t += WAVE) P.M1[t] = P.A[t];
     __syncthreads();
-    success = ct[H_FLAG] != 0;
+    double xd = 0.0;
+    bool ok = waveDantzig(m, P.M1, P.M2, P.scr, xd, bR, loR, hiR, fiR, lane);
+    if (ok) {
+      if (lane < m) P.X[lane] = xd;
+      __syncthreads();
+      ok = waveLcpValid(m, P.A, 0.0, xd, bR, hiR, loR, fiR, false, lane);
+    }
+    success = ok;
   }
-  if (lane == 0) {
+  STAMP(6);
+  {
     bool ok = success;
     bool ign = false;
     double cf = 0.0;
-    for (int i = 0; i < m; i++)
-      if (isnan(P.X[i])) { ok = false; for (int j = 0; j < m; j++) P.X[j] = 0.0; break; }
+    double X = lane < m ? P.X[lane] : 0.0;
+    if (__ballot(lane < m && isnan(X))) { ok = false; X = 0.0; }
     if (!ok) {
       cf = md.fallbackCfm;
-      double* sc = P.scr;
-      double* xd = sc; sc += m;
-      double* bd = sc; sc += m;
-      int* order = reinterpret_cast<int*>(sc); sc += m;
-      for (int r = 0; r < m; r++)
-        for (int c = 0; c < m; c++) P.M1[r * m + c] = P.A[r * m + c] + (r == c ? cf : 0.0);
-      for (int i = 0; i < m; i++) { xd[i] = P.xc[i]; bd[i] = P.b[i]; }
-      ok = devPgs(m, P.M1, xd, bd, P.lo, P.hi, P.fi, order);
+      for (int t = lane; t < m * m; t += WAVE) P.M1[t] = P.A[t] + ((t / m == t % m) ? cf : 0.0);
+      __syncthreads();
+      double xd = lane < m ? P.xc[lane] : 0.0;
+      ok = wavePgs(m, P.M1, xd, bR, loR, hiR, fiR, lane);
       if (ok) {
-        for (int i = 0; i < m; i++) P.X[i] = xd[i];
-        if (!devLcpValid(m, P.A, cf, P.X, P.b, P.hi, P.lo, P.fi, false)) ok = false;
+        X = xd;
+        ok = waveLcpValid(m, P.A, cf, X, bR, hiR, loR, fiR, false, lane);
       }
     }
     if (!ok) {
+      // LCPUtils::removeFriction + PGS on the normal rows only
       ign = true;
-      double* sc = P.scr;
-      int* keep = reinterpret_cast<int*>(sc); sc += m;
-      double* xr = sc; sc += m;
-      double* br = sc; sc += m;
-      double* lor = sc; sc += m;
-      double* hir = sc; sc += m;
-      int* fir = reinterpret_cast<int*>(sc); sc += m;
-      int* order = reinterpret_cast<int*>(sc); sc += m;
-      int k2 = 0;
-      for (int i = 0; i < m; i++) if (P.fi[i] == -1) keep[k2++] = i;
-      for (int r = 0; r < k2; r++) {
-        br[r] = P.b[keep[r]]; lor[r] = P.lo[keep[r]]; hir[r] = P.hi[keep[r]]; fir[r] = -1; xr[r] = 0.0;
-        for (int c = 0; c < k2; c++) P.M1[r * k2 + c] = P.A[keep[r] * m + keep[c]] + (r == c ? cf : 0.0);
+      const bool keepMe = lane < m && fiR == -1;
+      const unsigned long long km = __ballot(keepMe);
+      const int k2 = __popcll(km);
+      const int pos = __popcll(km & ((1ull << lane) - 1ull));
+      if (keepMe) P.cl[pos] = lane;
+      __syncthreads();
+      for (int t = lane; t < k2 * k2; t += WAVE) {
+        const int r = t / k2, c = t % k2;
+        P.M1[t] = P.A[P.cl[r] * m + P.cl[c]] + (r == c ? cf : 0.0);
       }
-      devPgs(k2, P.M1, xr, br, lor, hir, fir, order);
-      for (int i = 0; i < m; i++) P.X[i] = 0.0;
-      for (int r = 0; r < k2; r++) P.X[keep[r]] = xr[r];
+      __syncthreads();
+      const int kr = lane < k2 ? P.cl[lane] : 0;
+      double xr = 0.0;
+      wavePgs(k2, P.M1, xr, lane < k2 ? P.b[kr] : 0.0, lane < k2 ? P.lo[kr] : 0.0, lane < k2 ? P.hi[kr] : 0.0, -1,
+              lane);
+      __syncthreads();
+      if (lane < k2) P.fsol[lane] = xr;
+      __syncthreads();
+      X = 0.0;
+      if (keepMe) X = P.fsol[pos];
     }
-    for (int i = 0; i < m; i++)
-      if (isnan(P.X[i])) { for (int j = 0; j < m; j++) P.X[j] = 0.0; break; }
-    ct[H_CFM] = cf;
-    ct[H_IGN] = ign ? 1 : 0;
+    if (__ballot(lane < m && isnan(X))) X = 0.0;
+    if (lane < m) P.X[lane] = X;
+    if (lane == 0) { ct[H_CFM] = cf; ct[H_IGN] = ign ? 1 : 0; }
+    __syncthreads();
   }
-  __syncthreads();
   cfm = ct[H_CFM];
   ignoredFriction = ct[H_IGN] != 0;
-  if (!shortCircuit) devConstruct(P, m, cfm, ignoredFriction, ct, lane);
-  // impulses, cache, snapshot
-  for (int i = lane; i < n; i += WAVE) {
-    double acc = 0;
-    for (int j = 0; j < m; j++) acc += P.massed[i * m + j] * P.X[j];
-    snap[SN_VF + i] = v1[i];
-    v1[i] += acc;
+  STAMP(7);
+  // the step keeps the solver's x unless the re-standardisation succeeds
+  // (BoxedLcpConstraintSolver: `if (gm.standardized) x = gm.X`)
+  bool std2 = true;
+  if (!shortCircuit) {
+    for (int i = lane; i < m; i += WAVE) P.xc[i] = P.X[i];
+    __syncthreads();
+    std2 = devConstruct(P, m, cfm, ignoredFriction, ct, lane);
+  }
+  const double* Xf = std2 ? P.X : P.xc;
+  STAMP(8);
+  // impulses (applyConstraintImpulses + computeImpulseForwardDynamics):
+  // v1 += Minv J^T x = L^-T (Y x)
+  {
+    double* u = P.scr;
+    for (int i = lane; i < n; i += WAVE) {
+      double acc = 0;
+      for (int j = 0; j < m; j++) acc += P.massed[i * m + j] * Xf[j];
+      u[i] = acc;
+      snap[SN_VF + i] = v1[i];
+    }
+    __syncthreads();
+    for (int j = n - 1; j >= 0; j--) {
+      if (lane == 0) u[j] /= Lm[j * n + j];
+      __syncthreads();
+      const double uj = u[j];
+      for (int i = lane; i < j; i += WAVE) u[i] -= Lm[j * n + i] * uj;
+      __syncthreads();
+    }
+    for (int i = lane; i < n; i += WAVE) v1[i] += u[i];
   }
   if (lane == 0) cache[0] = m;
-  for (int i = lane; i < m; i += WAVE) cache[1 + i] = P.X[i];
+  for (int i = lane; i < m; i += WAVE) cache[1 + i] = Xf[i];
   for (int t = lane; t < nCon * CREC; t += WAVE) snap[SN_CONTACTS + t] = ct[CT_CONTACTS + t];
   for (int j = lane; j < m; j += WAVE) {
     double* rr = snap + SN_ROWS + j * SN_ROWREC;
@@ -1335,6 +1008,7 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
     snap[SN_IGN] = ignoredFriction ? 1 : 0;
   }
   __syncthreads();
+  STAMP(9);
 }
 
 // ===========================================================================
@@ -1557,7 +1231,7 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
     double* rhs = P.Pscr + lane * nc;
     double* z = P.Pscr + nc * nc + lane * nc;
     for (int i = 0; i < nc; i++) rhs[i] = i == lane ? 1.0 : 0.0;
-    codSolveOne(cod, rhs, P.PT + lane * nc, z);
+    codSolveLane(cod, rhs, P.PT + lane * nc, z);
   }
   __syncthreads();
   // lambda = P^T u ; x = P b ; beta

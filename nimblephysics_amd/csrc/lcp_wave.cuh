@@ -1,0 +1,498 @@
+// Wave-parallel LCP kernels for one world per 64-lane wave.  Vectors of the
+// (<= 48-row) LCP live one element per lane in registers, matrices in LDS;
+// the sequential structure of the reference algorithms (pivot order, sweep
+// order, tie-breaking) is kept exactly, only the inner vector work is spread
+// over the lanes:
+//   * wavePgs       PgsBoxedLcpSolver::solve (PgsBoxedLcpSolver.cpp:85)
+//   * waveDantzig   dSolveLCP (dart/external/odelcpsolver/lcp.cpp:780) with
+//                   _dLDLTAddTL / _dLDLTRemove (matrix.cpp:286, :374), early
+//                   termination as the contact solver uses it
+//   * waveLcpValid  LCPUtils::isLCPSolutionValid (LCPUtils.cpp:14)
+//   * codSolveWave  COD min-norm solve on a codFactor()ed matrix
+// All functions must be entered by the whole wave (uniform control flow).
+#pragma once
+#include "wave.cuh"
+
+#define LCP_INF __builtin_inf()
+
+// ---------------------------------------------------------------------------
+__device__ bool wavePgs(int n, double* A, double& x, double b, double lo, double hi, int findex, int lane) {
+  const double deltaXThr = 1e-6, relTol = 1e-3, epsDiv = 1e-9;
+  const bool act = lane < n;
+  bool possible = true;
+  const unsigned long long order = __ballot(act && A[lane * n + lane] >= epsDiv);
+  const double xf0 = 0.0;
+  (void)xf0;
+  for (int i = 0; i < n; i++) {
+    if (!((order >> i) & 1ull)) {
+      if (lane == i) x = 0.0;
+      continue;
+    }
+    const double Aii = A[i * n + i];
+    const double old = rdl(x, i);
+    const double part = (act && lane != i) ? A[i * n + lane] * x : 0.0;
+    double nx = (rdl(b, i) - waveSum(part)) / Aii;
+    const int fi = rdli(findex, i);
+    double h, l;
+    if (fi >= 0) { h = rdl(hi, i) * rdl(x, fi); l = -h; }
+    else { h = rdl(hi, i); l = rdl(lo, i); }
+    nx = nx > h ? h : (nx < l ? l : nx);
+    if (lane == i) x = nx;
+    if (possible && fabs(nx - old) > deltaXThr) possible = false;
+  }
+  if (possible) return true;
+  for (int idx = 0; idx < n; idx++) {
+    if (!((order >> idx) & 1ull)) continue;
+    const double dummy = 1.0 / A[idx * n + idx];
+    __syncthreads();
+    if (act) A[idx * n + lane] *= dummy;
+    if (lane == idx) b *= dummy;
+    __syncthreads();
+  }
+  for (int iter = 1; iter < 30; iter++) {
+    possible = true;
+    for (int idx = 0; idx < n; idx++) {
+      if (!((order >> idx) & 1ull)) continue;
+      const double old = rdl(x, idx);
+      const double part = (act && lane != idx) ? A[idx * n + lane] * x : 0.0;
+      double nx = rdl(b, idx) - waveSum(part);
+      const int fi = rdli(findex, idx);
+      double h, l;
+      if (fi >= 0) { h = rdl(hi, idx) * rdl(x, fi); l = -h; }
+      else { h = rdl(hi, idx); l = rdl(lo, idx); }
+      nx = nx > h ? h : (nx < l ? l : nx);
+      if (lane == idx) x = nx;
+      if (possible && fabs(nx) > epsDiv) {
+        if (fabs((nx - old) / nx) > relTol) possible = false;
+      }
+    }
+    if (possible) break;
+  }
+  return possible;
+}
+
+// ---------------------------------------------------------------------------
+__device__ bool waveLcpValid(int m, const double* A, double cfm, double x, double b, double hi, double lo, int fi,
+                             bool ignoreFriction, int lane) {
+  double v = -b;
+  for (int j = 0; j < m; j++) {
+    const double xj = rdl(x, j);
+    if (lane < m) v += (A[lane * m + j] + (lane == j ? cfm : 0.0)) * xj;
+  }
+  const double xf = __shfl(x, fi >= 0 ? fi : 0);
+  bool ok = true;
+  if (lane < m) {
+    double up = hi, low = lo;
+    bool done = false;
+    if (fi != -1) {
+      if (ignoreFriction) { ok = (x == 0); done = true; }
+      up *= xf;
+      low *= xf;
+    }
+    if (!done) {
+      const double tol = 1e-5;
+      if (fabs(low) < tol && fabs(up) < tol && fabs(x) < tol) {
+      } else if (fabs(x - low) < tol) {
+        if (v < -tol) ok = false;
+      } else if (fabs(x - up) < tol) {
+        if (v > tol) ok = false;
+      } else if (x > low && x < up) {
+        if (fabs(v) > tol) ok = false;
+      } else {
+        ok = false;
+      }
+    }
+  }
+  return __ballot(!ok) == 0ull;
+}
+
+// ---------------------------------------------------------------------------
+// x (lane-distributed, length c.n) = min-norm least-squares solution for rhs
+// (lane-distributed, length c.m).  scr: >= n doubles of LDS.
+__device__ double codSolveWave(const Cod& c, double rhs, double* scr, int lane) {
+  const double* A = c.A;
+  const int m = c.m, n = c.n, ld = c.ld;
+  for (int k = 0; k < c.kmax; k++) {
+    const double vnorm = c.vn[k];
+    if (!(vnorm > 0)) continue;
+    const double vk = c.vd[k];
+    const double v = lane == k ? vk : ((lane > k && lane < m) ? A[lane * ld + k] : 0.0);
+    double sc = waveSum(v * rhs);
+    sc = 2 * sc / vnorm;
+    if (lane >= k && lane < m) rhs -= sc * v;
+  }
+  const int r = *c.rank;
+  double z = 0.0, acc = 0.0;
+  for (int i = r - 1; i >= 0; i--) {
+    const double zi = (rdl(rhs, i) - rdl(acc, i)) / A[i * ld + i];
+    if (lane == i) z = zi;
+    if (lane < i) acc += A[lane * ld + i] * zi;
+  }
+  if (r < n) {
+    for (int i = 0; i < r; i++) {
+      const double vn = c.zn[i];
+      if (vn == 0) continue;
+      const double zd = c.zd[i];
+      const double t = (lane >= r && lane < n) ? z * A[i * ld + lane] : 0.0;
+      double sc = rdl(z, i) * zd + waveSum(t);
+      sc = 2 * sc / vn;
+      if (lane == i) z -= sc * zd;
+      if (lane >= r && lane < n) z -= sc * A[i * ld + lane];
+    }
+  }
+  __syncthreads();
+  if (lane < n) scr[c.perm[lane]] = z;
+  __syncthreads();
+  const double out = lane < n ? scr[lane] : 0.0;
+  __syncthreads();
+  return out;
+}
+
+// ---------------------------------------------------------------------------
+struct WaveDantzig {
+  int n, nC, nN, lane;
+  double* A;    // n x n, permuted in place (LDS)
+  double* L;    // n x n (LDS)
+  double* scr;  // >= n doubles (LDS)
+  double x, b, w, lo, hi, d, deltaX, deltaW, Dell, ell;
+  int findex, p, C, state;
+
+  __device__ __forceinline__ void swapReg(double& v, int i1, int i2) {
+    const double a = rdl(v, i1), c = rdl(v, i2);
+    if (lane == i1) v = c;
+    else if (lane == i2) v = a;
+  }
+  __device__ __forceinline__ void swapRegI(int& v, int i1, int i2) {
+    const int a = rdli(v, i1), c = rdli(v, i2);
+    if (lane == i1) v = c;
+    else if (lane == i2) v = a;
+  }
+  __device__ __forceinline__ void swapProblem(int i1, int i2) {
+    if (i1 == i2) return;
+    __syncthreads();
+    if (lane < n) {
+      const double t = A[i1 * n + lane];
+      A[i1 * n + lane] = A[i2 * n + lane];
+      A[i2 * n + lane] = t;
+    }
+    __syncthreads();
+    if (lane < n) {
+      const double t = A[lane * n + i1];
+      A[lane * n + i1] = A[lane * n + i2];
+      A[lane * n + i2] = t;
+    }
+    __syncthreads();
+    swapReg(x, i1, i2); swapReg(b, i1, i2); swapReg(w, i1, i2); swapReg(lo, i1, i2); swapReg(hi, i1, i2);
+    swapRegI(p, i1, i2); swapRegI(state, i1, i2); swapRegI(findex, i1, i2);
+  }
+  // L x = B (unit lower), B lane-distributed, first m entries
+  __device__ __forceinline__ void solveL1(double& B, int m) {
+    for (int k = 0; k < m; k++) {
+      const double bk = rdl(B, k);
+      if (lane > k && lane < m) B -= L[lane * n + k] * bk;
+    }
+  }
+  // L^T x = B
+  __device__ __forceinline__ void solveL1T(double& B, int m) {
+    for (int k = m - 1; k >= 0; k--) {
+      const double bk = rdl(B, k);
+      if (lane < k) B -= L[k * n + lane] * bk;
+    }
+  }
+  __device__ __forceinline__ void transferToC(int i) {
+    const double Aii = A[i * n + i];
+    if (nC > 0) {
+      if (lane < nC) L[nC * n + lane] = ell;
+      const double dd = waveSum(lane < nC ? ell * Dell : 0.0);
+      if (lane == nC) d = 1.0 / (Aii - dd);
+    } else {
+      if (lane == 0) d = 1.0 / Aii;
+    }
+    swapProblem(nC, i);
+    if (lane == nC) C = nC;
+    nC++;
+  }
+  __device__ __forceinline__ void transferFromNtoC(int i) {
+    const double Aii = A[i * n + i];
+    if (nC > 0) {
+      Dell = lane < nC ? A[i * n + C] : 0.0;
+      solveL1(Dell, nC);
+      ell = lane < nC ? Dell * d : 0.0;
+      if (lane < nC) L[nC * n + lane] = ell;
+      const double dd = waveSum(lane < nC ? ell * Dell : 0.0);
+      if (lane == nC) d = 1.0 / (Aii - dd);
+    } else {
+      if (lane == 0) d = 1.0 / Aii;
+    }
+    swapProblem(nC, i);
+    if (lane == nC) C = nC;
+    nN--;
+    nC++;
+  }
+  // _dLDLTAddTL on the sub-factorisation starting at (r, r); `a` holds
+  // element j at lane r + j
+  __device__ __forceinline__ void ldltAddTL(int r, int m2, double a) {
+    if (m2 < 2) return;
+    const double r2 = 0.70710678118654752440;
+    const int j0 = lane - r;
+    double W1 = 0.0, W2 = 0.0;
+    if (j0 >= 1 && j0 < m2) { W1 = a * r2; W2 = W1; }
+    const double a0 = rdl(a, r);
+    const double W11 = (0.5 * a0 + 1) * r2;
+    const double W21 = (0.5 * a0 - 1) * r2;
+    double alpha1 = 1.0, alpha2 = 1.0;
+    {
+      double dee = rdl(d, r);
+      double alphanew = alpha1 + (W11 * W11) * dee;
+      dee /= alphanew;
+      const double gamma1 = W11 * dee;
+      dee *= alpha1;
+      alpha1 = alphanew;
+      alphanew = alpha2 - (W21 * W21) * dee;
+      dee /= alphanew;
+      alpha2 = alphanew;
+      const double k1 = 1.0 - W21 * gamma1;
+      const double k2 = W21 * gamma1 * W11 - W21;
+      if (j0 >= 1 && j0 < m2) {
+        const double Wp = W1;
+        const double el = L[(r + j0) * n + r];
+        W1 = Wp - W11 * el;
+        W2 = k1 * Wp + k2 * el;
+      }
+    }
+    for (int j = 1; j < m2; j++) {
+      const double k1 = rdl(W1, r + j), k2 = rdl(W2, r + j);
+      double dee = rdl(d, r + j);
+      double alphanew = alpha1 + (k1 * k1) * dee;
+      dee /= alphanew;
+      const double gamma1 = k1 * dee;
+      dee *= alpha1;
+      alpha1 = alphanew;
+      alphanew = alpha2 - (k2 * k2) * dee;
+      dee /= alphanew;
+      const double gamma2 = k2 * dee;
+      dee *= alpha2;
+      if (lane == r + j) d = dee;
+      alpha2 = alphanew;
+      if (j0 > j && j0 < m2) {
+        double el = L[(r + j0) * n + r + j];
+        double Wp = W1 - k1 * el;
+        el += gamma1 * Wp;
+        W1 = Wp;
+        Wp = W2 - k2 * el;
+        el -= gamma2 * Wp;
+        W2 = Wp;
+        L[(r + j0) * n + r + j] = el;
+      }
+    }
+  }
+  __device__ __forceinline__ void ldltRemove(int r, int n2) {
+    if (r != n2 - 1) {
+      if (r == 0) {
+        const int C0 = rdli(C, 0);
+        double a = lane < n2 ? -A[C * n + C0] : 0.0;
+        if (lane == 0) a += 1.0;
+        ldltAddTL(0, n2, a);
+      } else {
+        const double t = lane < r ? L[r * n + lane] / d : 0.0;
+        const int Cr = rdli(C, r);
+        double a = 0.0;
+        double s = 0.0;
+        for (int k = 0; k < r; k++) {
+          const double tk = rdl(t, k);
+          if (lane >= r && lane < n2) s += L[lane * n + k] * tk;
+        }
+        if (lane >= r && lane < n2) a = s - A[C * n + Cr];
+        if (lane == r) a += 1.0;
+        ldltAddTL(r, n2 - r, a);
+      }
+    }
+    __syncthreads();
+    if (r < n2 - 1) {
+      if (lane < n2)
+        for (int j = r; j < n2 - 1; j++) L[lane * n + j] = L[lane * n + j + 1];
+      __syncthreads();
+      if (lane < n2)
+        for (int i = r; i < n2 - 1; i++) L[i * n + lane] = L[(i + 1) * n + lane];
+      __syncthreads();
+      const double dn = shiftDown1(d, lane);
+      if (lane >= r && lane < n2 - 1) d = dn;
+    }
+  }
+  __device__ __forceinline__ void transferFromCtoN(int i) {
+    const int j = waveFirst(lane < nC && C == i);
+    if (j >= 0) {
+      const int k = waveFirst(lane < nC && C == nC - 1);
+      ldltRemove(j, nC);
+      const int Cj = rdli(C, j);
+      if (lane == k) C = Cj;
+      const int Cn = shiftDown1i(C, lane);
+      if (lane >= j && lane < nC - 1) C = Cn;
+    }
+    swapProblem(i, nC - 1);
+    nN++;
+    nC--;
+  }
+  __device__ __forceinline__ void solve1(int i, int dir, bool onlyTransfer) {
+    if (nC > 0) {
+      Dell = lane < nC ? A[i * n + C] : 0.0;
+      solveL1(Dell, nC);
+      ell = lane < nC ? Dell * d : 0.0;
+      if (!onlyTransfer) {
+        double tmp = ell;
+        solveL1T(tmp, nC);
+        __syncthreads();
+        if (lane < nC) scr[C] = dir > 0 ? -tmp : tmp;
+        __syncthreads();
+        if (lane < nC) deltaX = scr[lane];
+        __syncthreads();
+      }
+    }
+  }
+  __device__ __forceinline__ double AiC(int i, double q) { return waveSum(lane < nC ? A[i * n + lane] * q : 0.0); }
+  __device__ __forceinline__ double AiN(int i, double q) {
+    return waveSum((lane >= nC && lane < nC + nN) ? A[i * n + lane] * q : 0.0);
+  }
+};
+
+// A (n x n LDS, destroyed), L (n x n LDS scratch), scr (>= n LDS); problem
+// vectors lane-distributed; returns success and x (lane-distributed).
+__device__ bool waveDantzig(int n, double* A, double* Lbuf, double* scr, double& xOut, double b, double lo, double hi,
+                            int findex, int lane) {
+  WaveDantzig D;
+  D.n = n; D.nC = 0; D.nN = 0; D.lane = lane;
+  D.A = A; D.L = Lbuf; D.scr = scr;
+  D.x = 0.0; D.b = b; D.w = 0.0; D.lo = lo; D.hi = hi; D.d = 0.0;
+  D.deltaX = 0.0; D.deltaW = 0.0; D.Dell = 0.0; D.ell = 0.0;
+  D.findex = findex; D.p = lane; D.C = 0; D.state = 0;
+  for (int k = lane; k < n * n; k += 64) Lbuf[k] = 0.0;
+  if (__ballot(lane < n && findex < 0 && lo == -LCP_INF && hi == LCP_INF)) return false;
+  {
+    int numAtEnd = 0;
+    for (int k = n - 1; k >= 0; k--)
+      if (rdli(D.findex, k) >= 0) { D.swapProblem(k, n - 1 - numAtEnd); numAtEnd++; }
+  }
+  __syncthreads();
+  bool hitFirstFriction = false;
+  for (int i = 0; i < n; i++) {
+    if (!hitFirstFriction && rdli(D.findex, i) >= 0) {
+      __syncthreads();
+      if (lane < n) scr[D.p] = D.x;
+      __syncthreads();
+      if (lane >= i && lane < n) {
+        const double wfk = scr[D.findex];
+        if (wfk == 0) { D.hi = 0; D.lo = 0; }
+        else { D.hi = fabs(D.hi * wfk); D.lo = -D.hi; }
+      }
+      __syncthreads();
+      hitFirstFriction = true;
+    }
+    const double wi = D.AiC(i, D.x) + D.AiN(i, D.x) - rdl(D.b, i);
+    if (lane == i) D.w = wi;
+    const double loi = rdl(D.lo, i), hii = rdl(D.hi, i);
+    if (loi == 0 && wi >= 0) {
+      D.nN++;
+      if (lane == i) D.state = 0;
+    } else if (hii == 0 && wi <= 0) {
+      D.nN++;
+      if (lane == i) D.state = 1;
+    } else if (wi == 0) {
+      D.solve1(i, 0, true);
+      D.transferToC(i);
+    } else {
+      for (;;) {
+        const double wiNow = rdl(D.w, i);
+        int dir;
+        double dirf;
+        if (wiNow <= 0) { dir = 1; dirf = 1.0; } else { dir = -1; dirf = -1.0; }
+        D.solve1(i, dir, false);
+        const int nC = D.nC, nN = D.nN;
+        const bool inN = lane >= nC && lane < nC + nN;
+        {
+          double acc = 0.0;
+          for (int j = 0; j < nC; j++) {
+            const double dxj = rdl(D.deltaX, j);
+            if (inN) acc += A[lane * n + j] * dxj;
+          }
+          if (inN) D.deltaW = acc + (dir > 0 ? A[i * n + lane] : -A[i * n + lane]);
+        }
+        const double dwi = D.AiC(i, D.deltaX) + A[i * n + i] * dirf;
+        if (lane == i) D.deltaW = dwi;
+        int cmd = 1, si = 0;
+        double s = -wiNow / dwi;
+        const double xi = rdl(D.x, i), hiI = rdl(D.hi, i), loI = rdl(D.lo, i);
+        if (dir > 0) {
+          if (hiI < LCP_INF) { const double s2 = (hiI - xi) * dirf; if (s2 < s) { s = s2; cmd = 3; } }
+        } else {
+          if (loI > -LCP_INF) { const double s2 = (loI - xi) * dirf; if (s2 < s) { s = s2; cmd = 2; } }
+        }
+        {
+          bool cand = false;
+          double s4 = LCP_INF;
+          if (inN) {
+            const bool dirOk = !D.state ? D.deltaW < 0 : D.deltaW > 0;
+            if (dirOk && !(D.lo == 0 && D.hi == 0)) { cand = true; s4 = -D.w / D.deltaW; }
+          }
+          const double m4 = waveMin(cand ? s4 : LCP_INF);
+          if (m4 < s) {
+            s = m4;
+            cmd = 4;
+            si = waveFirst(cand && s4 == m4);
+          }
+        }
+        {
+          int typ = 0;
+          double s56 = LCP_INF;
+          if (lane < nC) {
+            if (D.deltaX < 0 && D.lo > -LCP_INF) { s56 = (D.lo - D.x) / D.deltaX; typ = 5; }
+            if (D.deltaX > 0 && D.hi < LCP_INF) { s56 = (D.hi - D.x) / D.deltaX; typ = 6; }
+          }
+          const double m56 = waveMin(typ ? s56 : LCP_INF);
+          if (m56 < s) {
+            s = m56;
+            si = waveFirst(typ && s56 == m56);
+            cmd = rdli(typ, si);
+          }
+        }
+        if (s <= 0.0) return false;
+        if (lane < nC) D.x += s * D.deltaX;
+        if (lane == i) D.x += s * dirf;
+        if (inN) D.w += s * D.deltaW;
+        if (lane == i) D.w += s * dwi;
+        switch (cmd) {
+          case 1:
+            if (lane == i) D.w = 0;
+            D.transferToC(i);
+            break;
+          case 2:
+            if (lane == i) { D.x = D.lo; D.state = 0; }
+            D.nN++;
+            break;
+          case 3:
+            if (lane == i) { D.x = D.hi; D.state = 1; }
+            D.nN++;
+            break;
+          case 4:
+            if (lane == si) D.w = 0;
+            D.transferFromNtoC(si);
+            break;
+          case 5:
+            if (lane == si) { D.x = D.lo; D.state = 0; }
+            D.transferFromCtoN(si);
+            break;
+          case 6:
+            if (lane == si) { D.x = D.hi; D.state = 1; }
+            D.transferFromCtoN(si);
+            break;
+        }
+        if (cmd <= 3) break;
+      }
+    }
+  }
+  __syncthreads();
+  if (lane < n) scr[D.p] = D.x;
+  __syncthreads();
+  xOut = lane < n ? scr[lane] : 0.0;
+  __syncthreads();
+  return true;
+}

@@ -257,8 +257,13 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, con
   const int n = md.n;
   for (int env = blockIdx.x; env < batch; env += gridDim.x) {
     const double* st = state + (size_t)env * 2 * n;
+#ifdef NIMBLE_STAGE_TIMING
+    double* g_stamp = md.numPairs > 0 ? snapshot + (size_t)env * snapDoubles + snapWorkspaceOffset(n) + 1000 : nullptr;
+#endif
+    STAMP(10);
     loadState(md, s, L, lane, st, forces + (size_t)env * n);
     coreDynamics(md, s, L, lane);
+    STAMP(11);
     // rhs = tau + spring + damping - C   (GenericJoint::updateTotalForceDynamic)
     double* x = s + L.x;
     for (int i = lane; i < n; i += WAVE) {
@@ -273,6 +278,7 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, con
     double* v1 = s + L.v1;
     for (int i = lane; i < n; i += WAVE) v1[i] = s[L.v + i] + md.dt * x[i];
     __syncthreads();
+    STAMP(12);
     // runConstraintEngine (World.cpp:254): collision, LCP, impulses
     if (md.numPairs > 0) {
       double* sn = snapshot + (size_t)env * snapDoubles;
@@ -295,6 +301,7 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, con
       }
     }
     __syncthreads();
+    STAMP(13);
   }
 }
 

@@ -1,0 +1,50 @@
+// Wave-level primitives for the 64-lane CDNA4 wavefront: vectors of length
+// <= 64 are held one element per lane in registers; reductions use DPP
+// within 16-lane rows and v_readlane across rows, so their results are
+// wave-uniform (SGPR) values usable directly in control flow.
+#pragma once
+#include <hip/hip_runtime.h>
+
+__device__ __forceinline__ double rdl(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ int rdli(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+
+template <int CTRL>
+__device__ __forceinline__ double dppd(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// sum over all 64 lanes (every lane must be active); wave-uniform result
+__device__ __forceinline__ double waveSum(double v) {
+  v += dppd<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dppd<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dppd<0x124>(v);  // row_ror:4
+  v += dppd<0x128>(v);  // row_ror:8
+  return (rdl(v, 0) + rdl(v, 16)) + (rdl(v, 32) + rdl(v, 48));
+}
+
+// min over all lanes; wave-uniform
+__device__ __forceinline__ double waveMin(double v) {
+  v = fmin(v, dppd<0xB1>(v));
+  v = fmin(v, dppd<0x4E>(v));
+  v = fmin(v, dppd<0x124>(v));
+  v = fmin(v, dppd<0x128>(v));
+  return fmin(fmin(rdl(v, 0), rdl(v, 16)), fmin(rdl(v, 32), rdl(v, 48)));
+}
+
+// lowest lane index whose predicate holds (-1 if none); wave-uniform
+__device__ __forceinline__ int waveFirst(bool pred) {
+  const unsigned long long m = __ballot(pred);
+  return m ? __ffsll((long long)m) - 1 : -1;
+}
+
+// value held by lane (lane + 1) (the last lane gets its own value)
+__device__ __forceinline__ double shiftDown1(double v, int lane) {
+  return __shfl(v, lane + 1 < 64 ? lane + 1 : lane);
+}
+__device__ __forceinline__ int shiftDown1i(int v, int lane) { return __shfl(v, lane + 1 < 64 ? lane + 1 : lane); }

@@ -1,0 +1,42 @@
+"""Per-stage shader-clock breakdown of the forward kernel (debug build with
+-DNIMBLE_STAGE_TIMING; run on a GPU box with NIMBLE_AMD_LIB pointing at it)."""
+import sys
+
+import numpy as np
+import torch
+
+sys.path[:0] = ["tests", "."]
+import models  # noqa: E402
+import nimblephysics_amd as nimble  # noqa: E402
+
+B = 1024
+w = models.atlas_world(True)
+st, f = models.random_states(w, B, seed=1000, q_scale=0.02, v_scale=0.05)
+d = torch.device("cuda:0")
+state, action = torch.tensor(st, device=d), torch.tensor(f, device=d)
+dev = w.native()
+cache = torch.zeros((B, dev.cache_doubles), dtype=torch.float64, device=d)
+cache[:, 0] = -1
+snap = torch.zeros((B, dev.snapshot_doubles), dtype=torch.float64, device=d)
+nxt = torch.empty_like(state)
+s = torch.cuda.current_stream().cuda_stream
+n = w.getNumDofs()
+ws = ((752 + 48 + n + 7) // 8) * 8 + 1000
+for it in range(4):
+    snap[:, ws:ws + 14] = 0
+    dev.forward(state, action, cache, nxt, snap, s)
+    torch.cuda.synchronize()
+    state = nxt.clone()
+    T = snap[:, ws:ws + 14].cpu().numpy()
+    hd = snap[:, :8].cpu().numpy()
+    names = {(10, 11): "load+coreDynamics", (11, 12): "solve v1", (0, 1): "collide", (1, 2): "rows",
+             (2, 3): "cols/massed/A/b", (3, 4): "warm start/guess", (4, 5): "construct 1",
+             (5, 6): "dantzig", (6, 7): "pgs/fallbacks", (7, 8): "construct 2", (8, 9): "impulses/snapshot",
+             (12, 13): "contact stage total+integrate"}
+    print(f"--- step {it}: contact worlds {int((hd[:,0]>0).sum())}, short-circuit {int(hd[:,6].sum())}, "
+          f"cfm worlds {int((hd[:,4]>0).sum())}")
+    for (a, b), nm in names.items():
+        m = (T[:, a] > 0) & (T[:, b] > 0)
+        if m.any():
+            dtk = T[m, b] - T[m, a]
+            print(f"  {nm:32s} worlds {m.sum():5d}  mean {dtk.mean():10.0f}  max {dtk.max():10.0f}")

@@ -1130,6 +1130,10 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
   const double dt = md.dt;
   const double* Lm = s + L.M;
   const double* rows = sn + SN_ROWS;
+#ifdef NIMBLE_STAGE_TIMING
+  double* g_stamp = (double*)sn + snapWorkspaceOffset(n) + 1000;
+#endif
+  STAMP(30);
   if (lane == 0) {
     for (int j = 0; j < m; j++)
       if ((int)rows[j * SN_ROWREC + RR_MAP] == CM_CLAMPING) P.rowOf[(int)rows[j * SN_ROWREC + RR_CIDX]] = j;
@@ -1158,6 +1162,7 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
     P.bc[c] = rows[r * SN_ROWREC + RR_B];
     P.bounce[c] = rows[r * SN_ROWREC + RR_BOUNCE];
   }
+  STAMP(31);
   // right-hand sides: fext (yf) and gv (w)
   for (int i = lane; i < n; i += WAVE) {
     const double qi = s[L.q + i], vi = s[L.v + i];
@@ -1198,6 +1203,7 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
     // columns beyond 62 (nc > 62 never happens: nc <= 48)
   }
   __syncthreads();
+  STAMP(32);
   // Q = A_c^T MA + cfm I; W = copy to factor
   for (int t = lane; t < nc * nc; t += WAVE) {
     const int r = t / nc, c = t % nc;
@@ -1226,7 +1232,9 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
   double* w = carveCod(P.codw, P.W, nc, nc, nc, cod);
   double* cn = w; w += m;
   double* vv = w; w += m;
+  STAMP(33);
   codFactor(cod, cn, vv, lane);
+  STAMP(34);
   if (lane < nc) {
     double* rhs = P.Pscr + lane * nc;
     double* z = P.Pscr + nc * nc + lane * nc;
@@ -1234,6 +1242,7 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
     codSolveLane(cod, rhs, P.PT + lane * nc, z);
   }
   __syncthreads();
+  STAMP(35);
   // lambda = P^T u ; x = P b ; beta
   for (int c = lane; c < nc; c += WAVE) {
     double l = 0, xx = 0;
@@ -1309,10 +1318,12 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
     P.NV[i * NV_COLS + NV_MAPI] = ap;
   }
   __syncthreads();
+  STAMP(36);
   {
     const int cols[4] = {NV_NU, NV_KAPPA, NV_MA1, NV_MA2};
     cholSolveColumns(Lm, P.NV, n, NV_COLS, cols, 4, lane);
   }
+  STAMP(37);
   // w - nu into s[L.w]
   for (int i = lane; i < n; i += WAVE) {
     const double w2 = P.NV[i * NV_COLS + NV_W] - P.NV[i * NV_COLS + NV_NU];
@@ -1347,6 +1358,7 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
     bodyTwist(md, s + L.Sw, body, P.gRows + j * n, 1, P.TAB + j * 12 + side * 6);
   }
   __syncthreads();
+  STAMP(38);
   return imp;
 }
 

@@ -434,6 +434,10 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
   const int n = md.n;
   const double dt = md.dt;
   for (int env = blockIdx.x; env < batch; env += gridDim.x) {
+#ifdef NIMBLE_STAGE_TIMING
+    double* g_stamp = md.numPairs > 0 ? snapshot + (size_t)env * snapDoubles + snapWorkspaceOffset(n) + 1000 : nullptr;
+#endif
+    STAMP(20);
     loadState(md, s, L, lane, state + (size_t)env * 2 * n, forces + (size_t)env * n);
     const double* gN = gradNext + (size_t)env * 2 * n;
     for (int i = lane; i < n; i += WAVE) {
@@ -441,6 +445,7 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
       s[L.gv + i] = gN[n + i];
     }
     coreDynamics(md, s, L, lane);
+    STAMP(21);
     double* sn = snapshot + (size_t)env * snapDoubles;
     const int nc = md.numPairs > 0 ? (int)sn[SN_NC] : 0;
     const int m = md.numPairs > 0 ? (int)sn[SN_M] : 0;
@@ -483,8 +488,10 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
       for (int i = lane; i < n; i += WAVE) x[i] /= dt;
       __syncthreads();
     }
+    STAMP(22);
     kinematics(md, s, L, lane, x);  // A = accelerations at a*
     derivativeComposites(md, s, L, lane);
+    STAMP(23);
 
     // ---- per-direction columns -------------------------------------------
     double gq = 0.0, gvOut = 0.0, gt = 0.0;
@@ -569,6 +576,7 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
       }
     }
     __syncthreads();
+    STAMP(24);
     if (nc > 0) {
       // B1/B23/B4 are dead now: reuse them for the M-derivative fields
       double* buf = s + L.B1;
@@ -580,6 +588,7 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
       }
       __syncthreads();
     }
+    STAMP(25);
     // FreeJoint posPos / velPos blocks: central differences exactly as
     // FreeJoint::finiteDifferencePosPosJacobian / VelPosJacobian
     // (FreeJoint.cpp:965, :987); 24 lanes, one perturbed integration each.
@@ -626,5 +635,6 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
       gradForces[(size_t)env * n + k] = gt;
     }
     __syncthreads();
+    STAMP(26);
   }
 }

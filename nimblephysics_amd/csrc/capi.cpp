@@ -62,19 +62,38 @@ static Layout makeLayout(const ModelDev& m, bool backward, int poolRows) {
   auto take = [&](int count) { int r = o; o += (count + 1) & ~1; return r; };
   const int n = m.n, nb = m.nb;
   L.q = take(n); L.v = take(n); L.tau = take(n);
-  L.Tw = take(12 * nb); L.Sw = take(6 * n); L.V = take(6 * nb); L.A = take(6 * nb);
-  L.IC = take(36 * nb); L.F = take(6 * nb); L.M = take(n * n); L.rhs = take(n); L.x = take(n);
-  L.scratch = take(24 * 6);
+  L.Tw = take(12 * nb); L.Sw = take(6 * n);
+  L.M = take(n * (n + 1) / 2);  // packed lower triangle (M, then its Cholesky factor)
+  L.rhs = take(n); L.x = take(n);
   L.v1 = take(n);
-  L.ct = take(m.numPairs > 0 ? ctDoubles(m.pairChunk) : 16);
+  L.ct = take(!backward && m.numPairs > 0 ? ctDoubles() : 16);
   if (backward) {
+    L.scratch = take(24 * 6);
     // B1, B23, B4 contiguous: reused for the 8 x nb x 12 M-derivative fields
     L.B1 = take(36 * nb); L.B23 = take(36 * nb); L.B4 = take(36 * nb);
     L.P = take(6 * nb); L.H = take(6 * nb); L.w = take(n); L.gp = take(n); L.gv = take(n); L.out = take(3 * n);
+    L.poolCap = 0;
+    if (m.numPairs > 0 && poolRows > 0) L.poolCap = bwdPoolDoublesHost(poolRows, n);
+    L.pool = take(L.poolCap);
+    L.V = take(6 * nb); L.A = take(6 * nb); L.IC = take(36 * nb); L.F = take(6 * nb);
+  } else {
+    // V, A, IC, F last: after the dynamics they are dead and the contact
+    // stage (narrow-phase buffers, then the LCP pool) reuses the space
+    const int dyn = 54 * nb;
+    L.V = o; L.A = o + 6 * nb; L.IC = o + 12 * nb; L.F = o + 48 * nb;
+    L.poolCap = 0;
+    int area = dyn;
+    if (m.numPairs > 0) {
+      const int cs = collideScratchDoubles(m.pairChunk);
+      if (cs > area) area = cs;
+      if (poolRows > 0) {
+        L.poolCap = fwdPoolDoublesHost(poolRows, n);
+        if (L.poolCap > area) area = L.poolCap;
+      }
+    }
+    L.pool = o;
+    take(area);
   }
-  L.poolCap = 0;
-  if (m.numPairs > 0 && poolRows > 0) L.poolCap = backward ? bwdPoolDoublesHost(poolRows, n) : fwdPoolDoublesHost(poolRows, n);
-  L.pool = take(L.poolCap);
   L.total = o;
   return L;
 }
@@ -132,6 +151,22 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
     }
   }
   if (dofCount != m.n) { delete w; return fail(NIMBLE_ERR_INVALID, "dof count mismatch"); }
+  {
+    int k = 0;
+    for (int lev = 0; lev <= m.maxDepth; lev++) {
+      m.levelStart[lev] = k;
+      for (int b = 0; b < m.nb; b++)
+        if (m.depth[b] == lev) m.levelBodies[k++] = b;
+    }
+    m.levelStart[m.maxDepth + 1] = k;
+    k = 0;
+    for (int p = 0; p < m.nb; p++) {
+      m.childStart[p] = k;
+      for (int b = 0; b < m.nb; b++)
+        if (m.parent[b] == p) m.childList[k++] = b;
+    }
+    m.childStart[m.nb] = k;
+  }
   // BodyNode::isReactive (BodyNode.cpp:2384): mobile skeleton with dependent dofs
   for (int b = 0; b < m.nb; b++) {
     bool hasDof = false;
@@ -186,7 +221,7 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
       const int a = fwdPoolDoublesHost(mcap, m.n), b = bwdPoolDoublesHost(mcap, m.n);
       ws = a > b ? a : b;
     }
-    w->snapDoubles = snapWorkspaceOffsetHost(m.n) + ws;
+    w->snapDoubles = snapWorkspaceOffsetHost(m.n) + ws + SN_DEBUG_TAIL;
   } else {
     w->snapDoubles = 8;
   }

@@ -270,13 +270,13 @@ struct FwdPool {
   double *cols, *massed, *A, *M1, *M2;
   double *lo, *hi, *b, *X, *aCol, *rest, *pen, *relVel, *fc, *Eval, *nx, *fsol, *xc, *dvec;
   int *fi, *mapping, *clampIdx, *ubIdx, *rowC, *rowDir, *clampRow, *cl;
-  double* scr;  // >= 24 m + 2 n + 16
+  double* scr;  // >= 10 m + 2 n + 16
 };
 
 __device__ inline void carveFwd(double* base, int m, int n, FwdPool& P) {
   double* p = base;
   P.cols = p; p += n * m;
-  P.massed = p; p += n * m;
+  P.massed = P.cols;  // Y = L^-1 J^T overwrites J^T in place
   P.A = p; p += m * m;
   P.M1 = p; p += m * m;
   P.M2 = p; p += m * m;
@@ -332,12 +332,14 @@ __device__ void codFactor(Cod& c, double* cn, double* v, int lane) {
   for (int k = 0; k < c.kmax; k++) {
     for (int j = k + lane; j < n; j += WAVE) {
       double sc = 0;
+#pragma unroll 8
       for (int i = k; i < m; i++) sc += A[i * ld + j] * A[i * ld + j];
       cn[j] = sc;
     }
     __syncthreads();
     int p = k;
     double best = -1;
+#pragma unroll 8
     for (int j = k; j < n; j++)
       if (cn[j] > best) { best = cn[j]; p = j; }
     if (p != k) {
@@ -348,6 +350,7 @@ __device__ void codFactor(Cod& c, double* cn, double* v, int lane) {
     }
     __syncthreads();
     double alpha = 0;
+#pragma unroll 8
     for (int i = k; i < m; i++) alpha += A[i * ld + k] * A[i * ld + k];
     alpha = sqrt(alpha);
     if (alpha == 0.0) {
@@ -359,12 +362,15 @@ __device__ void codFactor(Cod& c, double* cn, double* v, int lane) {
     for (int i = k + lane; i < m; i += WAVE) v[i] = A[i * ld + k] - (i == k ? alpha : 0.0);
     __syncthreads();
     double vnorm = 0;
+#pragma unroll 8
     for (int i = k; i < m; i++) vnorm += v[i] * v[i];
     if (vnorm > 0) {
       for (int j = k + lane; j < n; j += WAVE) {
         double sc = 0;
+#pragma unroll 8
         for (int i = k; i < m; i++) sc += v[i] * A[i * ld + j];
         sc = 2 * sc / vnorm;
+#pragma unroll 8
         for (int i = k; i < m; i++) A[i * ld + j] -= sc * v[i];
       }
     }
@@ -404,39 +410,6 @@ __device__ void codFactor(Cod& c, double* cn, double* v, int lane) {
     __syncthreads();
   }
   __syncthreads();
-}
-
-// Per-lane solve on a codFactor()ed matrix (each lane its own rhs, e.g. the
-// columns of pinv(Q)): x (n) = min-norm least squares for rhs (m, destroyed).
-__device__ void codSolveLane(const Cod& c, double* rhs, double* x, double* z) {
-  const double* A = c.A;
-  const int m = c.m, n = c.n, ld = c.ld;
-  for (int k = 0; k < c.kmax; k++) {
-    const double vnorm = c.vn[k];
-    if (!(vnorm > 0)) continue;
-    double sc = c.vd[k] * rhs[k];
-    for (int i = k + 1; i < m; i++) sc += A[i * ld + k] * rhs[i];
-    sc = 2 * sc / vnorm;
-    rhs[k] -= sc * c.vd[k];
-    for (int i = k + 1; i < m; i++) rhs[i] -= sc * A[i * ld + k];
-  }
-  const int r = *c.rank;
-  for (int j = 0; j < n; j++) z[j] = 0.0;
-  for (int i = r - 1; i >= 0; i--) {
-    double sc = rhs[i];
-    for (int j = i + 1; j < r; j++) sc -= A[i * ld + j] * z[j];
-    z[i] = sc / A[i * ld + i];
-  }
-  for (int i = 0; i < r && r < n; i++) {
-    const double vn = c.zn[i];
-    if (vn == 0) continue;
-    double sc = z[i] * c.zd[i];
-    for (int j = r; j < n; j++) sc += z[j] * A[i * ld + j];
-    sc = 2 * sc / vn;
-    z[i] -= sc * c.zd[i];
-    for (int j = r; j < n; j++) z[j] -= sc * A[i * ld + j];
-  }
-  for (int j = 0; j < n; j++) x[c.perm[j]] = z[j];
 }
 
 #include "lcp_wave.cuh"
@@ -483,6 +456,8 @@ __device__ void codSolveLane(const Cod& c, double* rhs, double* x, double* z) {
 // ---------------------------------------------------------------------------
 __device__ void collideWorld(const ModelDev& md, double* s, const Layout& L, int lane) {
   double* ct = s + L.ct;
+  double* dropped = s + L.V;                            // alias area (dead V/A/IC/F)
+  double* pairbuf = dropped + CT_MAX_DROPPED * CREC;
   if (lane == 0) { ct[H_NCON] = 0; ct[H_NDROP] = 0; ct[H_STATUS] = 0; }
   __syncthreads();
   const int PC = md.pairChunk;
@@ -501,7 +476,7 @@ __device__ void collideWorld(const ModelDev& md, double* s, const Layout& L, int
         const double p1[3] = {T1[3], T1[7], T1[11]}, p2[3] = {T2[3], T2[7], T2[11]};
         const double A[3] = {0.5 * md.shapeSize[si][0], 0.5 * md.shapeSize[si][1], 0.5 * md.shapeSize[si][2]};
         const double B[3] = {0.5 * md.shapeSize[sj][0], 0.5 * md.shapeSize[sj][1], 0.5 * md.shapeSize[sj][2]};
-        cnt = deviceBoxBox(p1, R1, A, p2, R2, B, md.clipDepth, bi, bj, ct + CT_PAIRBUF + lane * 8 * CREC);
+        cnt = deviceBoxBox(p1, R1, A, p2, R2, B, md.clipDepth, bi, bj, pairbuf + lane * 8 * CREC);
       } else {
         cnt = -1;
       }
@@ -514,10 +489,10 @@ __device__ void collideWorld(const ModelDev& md, double* s, const Layout& L, int
         const int cnt = (int)ct[H_PAIRCNT + q];
         if (cnt < 0) { st |= ST_UNSUPPORTED_SHAPE; continue; }
         for (int c = 0; c < cnt; c++) {
-          const double* rec = ct + CT_PAIRBUF + (q * 8 + c) * CREC;
+          const double* rec = pairbuf + (q * 8 + c) * CREC;
           bool close = false;
           for (int t = 0; t < nk + nd && !close; t++) {
-            const double* o = t < nk ? ct + CT_CONTACTS + t * CREC : ct + CT_DROPPED + (t - nk) * CREC;
+            const double* o = t < nk ? ct + CT_CONTACTS + t * CREC : dropped + (t - nk) * CREC;
             double dd = 0;
             for (int i = 0; i < 3; i++) dd += (rec[i] - o[i]) * (rec[i] - o[i]);
             if (sqrt(dd) < 3.0e-12) close = true;
@@ -534,7 +509,7 @@ __device__ void collideWorld(const ModelDev& md, double* s, const Layout& L, int
           } else {
             if (nd < CT_MAX_DROPPED) {
               // keep kept contacts contiguous: dropped list is separate
-              dst = ct + CT_DROPPED + (nd++) * CREC;
+              dst = dropped + (nd++) * CREC;
             } else {
               st |= ST_DROPPED_OVERFLOW;
             }
@@ -719,14 +694,162 @@ __device__ void devGuess(FwdPool& P, int m, double* x, double* ct, int lane) {
   __syncthreads();
 }
 
+// Row-parallel back substitution L^T Z = Z for the n x k block Z (ld k).
+__device__ void backSubRows(const double* Lm, double* Z, int n, int k, int lane) {
+  for (int r = n - 1; r >= 0; r--) {
+    const double inv = 1.0 / Lm[tri(r, r)];
+    for (int c = lane; c < k; c += WAVE) Z[r * k + c] *= inv;
+    __syncthreads();
+    const int cnt = r * k;
+    for (int t = lane; t < cnt; t += WAVE) {
+      const int i = t / k, c = t % k;
+      Z[i * k + c] -= Lm[tri(r, i)] * Z[r * k + c];
+    }
+    __syncthreads();
+  }
+}
+
+// The upstream-gradient-independent pieces of the constrained backward
+// (BackpropSnapshot.cpp:2723 getJacobianOfConstraintForce and the clamping
+// matrices it uses), computed here where Y = L^-1 J^T and A are on chip:
+// A_c, A_c_ub_E, Minv A_c_ub_E, Minv A_c, Q = A_c^T Minv A_c_ub_E + cfm I,
+// pinv(Q) (COD) and the rank-deficiency flag ||I - Q Q^+||^2 >= 1e-18.
+__device__ void backwardPrecompute(const ModelDev& md, double* s, const Layout& L, int lane, FwdPool& P, int m,
+                                   double cfm, double* snap, double* ct) {
+  const int n = md.n;
+  const int nc = (int)ct[H_NC];
+  if (lane == 0) snap[SN_IMP] = 0.0;
+  if (nc == 0) { __syncthreads(); return; }
+  const double* Lm = s + L.M;
+  double* AcG = snap + snAc(n);
+  double* AcubEG = snap + snAcubE(n);
+  double* MAG = snap + snMA(n);
+  double* MAcG = snap + snMAc(n);
+  double* PTG = snap + snPT(n);
+  double* QG = snap + snQ(n);
+  const double* Y = P.massed;
+  const double* cts = s + L.ct + CT_CONTACTS;
+  // A_c, A_c_ub_E (global): J^T columns re-evaluated (the on-chip copy of J^T
+  // was overwritten by Y)
+  for (int t = lane; t < n * nc; t += WAVE) {
+    const int i = t / nc, c = t % nc;
+    const int r = P.clampRow[c];
+    const double a = rowForceEntry(md, s, L, cts + P.rowC[r] * CREC, P.dvec + 3 * r, i);
+    double ae = a;
+    for (int u = 0; u < m; u++)
+      if (P.mapping[u] >= 0 && P.clampIdx[P.mapping[u]] == c)
+        ae += P.Eval[u] * rowForceEntry(md, s, L, cts + P.rowC[u] * CREC, P.dvec + 3 * u, i);
+    AcG[t] = a;
+    AcubEG[t] = ae;
+  }
+  // Minv A_c_ub_E = L^-T (Y_c + Y_ub E) and Minv A_c = L^-T Y_c: back
+  // substitution in registers (row i on lane i), four columns per pass
+  for (int pass = 0; pass < 2; pass++) {
+    double* dst = pass == 0 ? MAG : MAcG;
+    for (int c0 = 0; c0 < nc; c0 += 4) {
+      double z[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int c = c0 + q;
+        double v = 0.0;
+        if (c < nc && lane < n) {
+          v = Y[lane * m + P.clampRow[c]];
+          if (pass == 0)
+            for (int u = 0; u < m; u++)
+              if (P.mapping[u] >= 0 && P.clampIdx[P.mapping[u]] == c) v += P.Eval[u] * Y[lane * m + u];
+        }
+        z[q] = v;
+      }
+      for (int k = n - 1; k >= 0; k--) {
+        const double inv = 1.0 / Lm[tri(k, k)];
+        const double lk = lane < k ? Lm[tri(k, lane)] : 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const double zk = rdl(z[q], k) * inv;
+          if (lane == k) z[q] = zk;
+          else if (lane < k) z[q] -= lk * zk;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        if (c0 + q < nc && lane < n) dst[lane * nc + c0 + q] = z[q];
+    }
+  }
+  // Q into M1 (kept) and M2 (factored)
+  for (int t = lane; t < nc * nc; t += WAVE) {
+    const int cr = t / nc, cc = t % nc;
+    const int rr = P.clampRow[cr], rc = P.clampRow[cc];
+    double v = P.A[rr * m + rc];
+    for (int u = 0; u < m; u++)
+      if (P.mapping[u] >= 0 && P.clampIdx[P.mapping[u]] == cc) v += P.Eval[u] * P.A[rr * m + u];
+    if (cr == cc) v += cfm;
+    P.M1[t] = v;
+    P.M2[t] = v;
+    QG[t] = v;
+  }
+  __syncthreads();
+  Cod cod;
+  double* w = carveCod(P.scr, P.M2, nc, nc, nc, cod);
+  double* cn = w; w += m;
+  double* vv = w; w += m;
+  codFactor(cod, cn, vv, lane);
+  // pinv(Q): lane c solves Q x = e_c in place in row c of the (now free) A region
+  double* Zs = P.A;
+  if (lane < nc) {
+    double* rhs = Zs + lane * nc;
+    for (int i = 0; i < nc; i++) rhs[i] = i == lane ? 1.0 : 0.0;
+    const double* F = cod.A;
+    for (int k = 0; k < cod.kmax; k++) {
+      const double vnorm = cod.vn[k];
+      if (!(vnorm > 0)) continue;
+      double sc = cod.vd[k] * rhs[k];
+      for (int i = k + 1; i < nc; i++) sc += F[i * nc + k] * rhs[i];
+      sc = 2 * sc / vnorm;
+      rhs[k] -= sc * cod.vd[k];
+      for (int i = k + 1; i < nc; i++) rhs[i] -= sc * F[i * nc + k];
+    }
+    const int r = *cod.rank;
+    for (int i = r - 1; i >= 0; i--) {
+      double sc = rhs[i];
+      for (int j = i + 1; j < r; j++) sc -= F[i * nc + j] * rhs[j];
+      rhs[i] = sc / F[i * nc + i];
+    }
+    for (int j = r; j < nc; j++) rhs[j] = 0.0;
+    for (int i = 0; i < r && r < nc; i++) {
+      const double vn = cod.zn[i];
+      if (vn == 0) continue;
+      double sc = rhs[i] * cod.zd[i];
+      for (int j = r; j < nc; j++) sc += rhs[j] * F[i * nc + j];
+      sc = 2 * sc / vn;
+      rhs[i] -= sc * cod.zd[i];
+      for (int j = r; j < nc; j++) rhs[j] -= sc * F[i * nc + j];
+    }
+    // column `lane` of pinv(Q) = row `lane` of pinv(Q)^T
+    for (int j = 0; j < nc; j++) PTG[lane * nc + cod.perm[j]] = rhs[j];
+  }
+  __syncthreads();
+  // ||I - Q Q^+||^2 with (Q Q^+)[r][c] = sum_j Q[r][perm_j] z_c[j]
+  double part = 0.0;
+  for (int t = lane; t < nc * nc; t += WAVE) {
+    const int r = t / nc, c = t % nc;
+    double acc = 0;
+    for (int j = 0; j < nc; j++) acc += P.M1[r * nc + cod.perm[j]] * Zs[c * nc + j];
+    const double e = (r == c ? 1.0 : 0.0) - acc;
+    part += e * e;
+  }
+  const double tot = waveSum(part);
+  if (lane == 0) snap[SN_IMP] = tot >= 1e-18 ? 1.0 : 0.0;
+  __syncthreads();
+}
+
 // ---------------------------------------------------------------------------
 // The whole constraint stage of one world (World.cpp:254 runConstraintEngine
 // on the hot path): rows, A = J Minv J^T, b, LCP with the short-circuit,
 // fallbacks, impulses (v1 += Minv J^T x), warm-start cache and snapshot.
 // `Lm` is the Cholesky factor of M (lower triangle, n x n).
 // ---------------------------------------------------------------------------
-__device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int lane, double* v1, double* cache,
-                             double* snap, double* overflowWs) {
+__device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int lane, double* v1, const double* ddq,
+                             double* cache, double* snap, double* overflowWs) {
   const int n = md.n;
 #ifdef NIMBLE_STAGE_TIMING
   double* g_stamp = snap + snapWorkspaceOffset(n) + 1000;
@@ -797,18 +920,24 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
   STAMP(2);
   // Y = L^-1 J^T (row-parallel forward substitution; `massed` holds Y), so
   // that A = J Minv J^T = Y^T Y and Minv J^T x = L^-T (Y x)
+  // b = -J v1 first: Y = L^-1 J^T is formed in place of J^T
+  for (int r = lane; r < m; r += WAVE) {
+    double acc = 0;
+#pragma unroll 8
+    for (int i = 0; i < n; i++) acc += P.cols[i * m + r] * v1[i];
+    P.b[r] = -acc;
+  }
+  __syncthreads();
   {
     double* Y = P.massed;
-    for (int t = lane; t < n * m; t += WAVE) Y[t] = P.cols[t];
-    __syncthreads();
     for (int k = 0; k < n; k++) {
-      const double inv = 1.0 / Lm[k * n + k];
+      const double inv = 1.0 / Lm[tri(k, k)];
       for (int j = lane; j < m; j += WAVE) Y[k * m + j] *= inv;
       __syncthreads();
       const int cnt = (n - k - 1) * m;
       for (int t = lane; t < cnt; t += WAVE) {
         const int i = k + 1 + t / m, j = t % m;
-        Y[i * m + j] -= Lm[i * n + k] * Y[k * m + j];
+        Y[i * m + j] -= Lm[tri(i, k)] * Y[k * m + j];
       }
       __syncthreads();
     }
@@ -816,18 +945,14 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
       const int r = t / m, c = t % m;
       if (r <= c) {
         double acc = 0;
+#pragma unroll 8
         for (int i = 0; i < n; i++) acc += Y[i * m + r] * Y[i * m + c];
         P.A[r * m + c] = acc;
         P.A[c * m + r] = acc;
       }
     }
   }
-  for (int r = lane; r < m; r += WAVE) {
-    double acc = 0;
-    for (int i = 0; i < n; i++) acc += P.cols[i * m + r] * v1[i];
-    P.b[r] = -acc;
-  }
-  __syncthreads();
+
   if (lane == 0) {
     for (int r = 0; r < m; r++) {
       P.pen[r] = 0.0;
@@ -849,6 +974,7 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
   __syncthreads();
   for (int j = lane; j < m; j += WAVE) {
     double acc = 0;
+#pragma unroll 8
     for (int i = 0; i < m; i++) acc += P.A[i * m + j] * P.A[i * m + j];
     P.aCol[j] = acc;
   }
@@ -971,10 +1097,10 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
     }
     __syncthreads();
     for (int j = n - 1; j >= 0; j--) {
-      if (lane == 0) u[j] /= Lm[j * n + j];
+      if (lane == 0) u[j] /= Lm[tri(j, j)];
       __syncthreads();
       const double uj = u[j];
-      for (int i = lane; i < j; i += WAVE) u[i] -= Lm[j * n + i] * uj;
+      for (int i = lane; i < j; i += WAVE) u[i] -= Lm[tri(j, i)] * uj;
       __syncthreads();
     }
     for (int i = lane; i < n; i += WAVE) v1[i] += u[i];
@@ -997,6 +1123,8 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
   }
   const int nc = (int)ct[H_NC];
   for (int i = lane; i < nc; i += WAVE) snap[SN_FC + i] = P.fc[i];
+  for (int i = lane; i < n; i += WAVE) snap[snYf(n) + i] = ddq[i];
+  backwardPrecompute(md, s, L, lane, P, m, cfm, snap, ct);
   if (lane == 0) {
     snap[SN_NCON] = nCon;
     snap[SN_M] = m;
@@ -1031,47 +1159,19 @@ enum { NV_DELTA = 0, NV_NU, NV_SIGMA, NV_KAPPA, NV_MA1, NV_MARHO, NV_MA2, NV_MAP
 
 
 struct BwdPool {
-  double *Ac, *AcubE, *MA, *Q, *W, *PT, *Pscr, *gRows, *TAB, *NV;
-  double *fc, *bc, *bounce, *u, *lam, *beta, *xq, *rho, *piv, *zeta, *r1, *tc;
-  double* codw;
+  double *gRows, *TAB, *NV;
+  double *fc, *bc, *bounce, *u, *lam, *beta, *xq, *rho, *piv, *zeta, *r1;
   int* rowOf;
 };
 
 __device__ inline void carveBwd(double* base, int m, int n, BwdPool& P) {
   double* p = base;
-  P.Ac = p; p += n * m;
-  P.AcubE = p; p += n * m;
-  P.MA = p; p += n * m;
   P.gRows = p; p += n * m;
-  P.Q = p; p += m * m;
-  P.W = p; p += m * m;
-  P.PT = p; p += m * m;
-  P.Pscr = p; p += 2 * m * m;
   P.TAB = p; p += 12 * m;
   P.NV = p; p += NV_COLS * n;
-  double** vecs[] = {&P.fc, &P.bc, &P.bounce, &P.u, &P.lam, &P.beta, &P.xq, &P.rho, &P.piv, &P.zeta, &P.r1, &P.tc};
+  double** vecs[] = {&P.fc, &P.bc, &P.bounce, &P.u, &P.lam, &P.beta, &P.xq, &P.rho, &P.piv, &P.zeta, &P.r1};
   for (double** v : vecs) { *v = p; p += m; }
-  P.rowOf = reinterpret_cast<int*>(p); p += m;
-  P.codw = p;  // >= 8 m + 8
-}
-
-// Solve L L^T x = b for `cnt` right-hand sides stored as columns of X
-// (leading dimension ld); lane j handles column cols[j].
-__device__ void cholSolveColumns(const double* Lm, double* X, int n, int ld, const int* cols, int cnt, int lane) {
-  if (lane < cnt) {
-    const int j = cols[lane];
-    for (int i = 0; i < n; i++) {
-      double acc = X[i * ld + j];
-      for (int k = 0; k < i; k++) acc -= Lm[i * n + k] * X[k * ld + j];
-      X[i * ld + j] = acc / Lm[i * n + i];
-    }
-    for (int i = n - 1; i >= 0; i--) {
-      double acc = X[i * ld + j];
-      for (int k = i + 1; k < n; k++) acc -= Lm[k * n + i] * X[k * ld + j];
-      X[i * ld + j] = acc / Lm[i * n + i];
-    }
-  }
-  __syncthreads();
+  P.rowOf = reinterpret_cast<int*>(p);
 }
 
 // twist of body `b` for joint velocity vector g (column `col` of X, ld):
@@ -1080,6 +1180,7 @@ __device__ inline void bodyTwist(const ModelDev& md, const double* Sw, int b, co
   for (int i = 0; i < 6; i++) T[i] = 0.0;
   if (b < 0) return;
   const unsigned long long a = md.anc[b];
+#pragma unroll 4
   for (int r = 0; r < md.n; r++) {
     if (!((a >> md.dofBody[r]) & 1ull)) continue;
     const double gr = g[r * ld];
@@ -1119,181 +1220,76 @@ __device__ void tangentBasisGradient(const double* nrm, const double* g, double*
   for (int i = 0; i < 3; i++) { T0[i] = gt[i]; T1[i] = a[i] + b[i]; }
 }
 
-// Contact preparation of the backward.  On return (all lanes):
+// Contact preparation of the backward from the snapshot's precomputed
+// clamping data (backwardPrecompute).  On return (all lanes):
 //   s[L.x]  = a* (acceleration incl. the constraint impulse / dt)
 //   s[L.w]  = w - nu       (the vector the unconstrained VJP machinery uses)
-//   NV columns hold the M-derivative pairs, mu, and P.gRows / P.TAB the
+//   NV columns hold the M-derivative pairs and mu; P.gRows / P.TAB the
 //   per-row vectors of the G_j terms.  Returns the imprecise flag.
 __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& L, int lane, const double* sn,
-                                   BwdPool& P, int m, int nc, double cfm, double* ct) {
+                                   BwdPool& P, int m, int nc, double* ct) {
   const int n = md.n;
   const double dt = md.dt;
-  const double* Lm = s + L.M;
   const double* rows = sn + SN_ROWS;
+  const double* Ac = sn + snAc(n);
+  const double* AcubE = sn + snAcubE(n);
+  const double* MA = sn + snMA(n);
+  const double* MAc = sn + snMAc(n);
+  const double* PT = sn + snPT(n);
+  const double* Q = sn + snQ(n);
+  const int imp = (int)sn[SN_IMP];
 #ifdef NIMBLE_STAGE_TIMING
   double* g_stamp = (double*)sn + snapWorkspaceOffset(n) + 1000;
 #endif
   STAMP(30);
-  if (lane == 0) {
-    for (int j = 0; j < m; j++)
-      if ((int)rows[j * SN_ROWREC + RR_MAP] == CM_CLAMPING) P.rowOf[(int)rows[j * SN_ROWREC + RR_CIDX]] = j;
-  }
+  (void)ct;
+  for (int j = lane; j < m; j += WAVE)
+    if ((int)rows[j * SN_ROWREC + RR_MAP] == CM_CLAMPING) P.rowOf[(int)rows[j * SN_ROWREC + RR_CIDX]] = j;
+  for (int i = lane; i < n; i += WAVE) s[L.w + i] = s[L.gv + i];
   __syncthreads();
-  // A_c and A_c + A_ub E (n x nc)
-  for (int t = lane; t < n * nc; t += WAVE) {
-    const int i = t / nc, c = t % nc;
-    const int r = P.rowOf[c];
-    const double* rr = rows + r * SN_ROWREC;
-    const double a = rowForceEntry(md, s, L, sn + SN_CONTACTS + (int)rr[RR_CONTACT] * CREC, rr + RR_D, i);
-    double ae = a;
-    for (int u = 0; u < m; u++) {
-      const double* ru = rows + u * SN_ROWREC;
-      const int mp = (int)ru[RR_MAP];
-      if (mp >= 0 && (int)rows[mp * SN_ROWREC + RR_CIDX] == c)
-        ae += ru[RR_EVAL] * rowForceEntry(md, s, L, sn + SN_CONTACTS + (int)ru[RR_CONTACT] * CREC, ru + RR_D, i);
-    }
-    P.Ac[t] = a;
-    P.AcubE[t] = ae;
-    P.MA[t] = ae;
-  }
   for (int c = lane; c < nc; c += WAVE) {
     const int r = P.rowOf[c];
     P.fc[c] = sn[SN_FC + c];
     P.bc[c] = rows[r * SN_ROWREC + RR_B];
     P.bounce[c] = rows[r * SN_ROWREC + RR_BOUNCE];
   }
+  cholSolve(s + L.M, s + L.w, n, lane);  // w = Minv gv
   STAMP(31);
-  // right-hand sides: fext (yf) and gv (w)
-  for (int i = lane; i < n; i += WAVE) {
-    const double qi = s[L.q + i], vi = s[L.v + i];
-    const double springF = md.spring[i] * (qi - md.rest[i] + dt * vi);
-    P.NV[i * NV_COLS + NV_YF] = s[L.tau + i] - s[L.rhs + i] - md.damping[i] * vi - springF;
-    P.NV[i * NV_COLS + NV_W] = s[L.gv + i];
-  }
-  __syncthreads();
-  {
-    int cols[2] = {NV_YF, NV_W};
-    int c = lane < 2 ? cols[lane] : 0;
-    if (lane < 2) {
-      for (int i = 0; i < n; i++) {
-        double acc = P.NV[i * NV_COLS + c];
-        for (int k = 0; k < i; k++) acc -= Lm[i * n + k] * P.NV[k * NV_COLS + c];
-        P.NV[i * NV_COLS + c] = acc / Lm[i * n + i];
-      }
-      for (int i = n - 1; i >= 0; i--) {
-        double acc = P.NV[i * NV_COLS + c];
-        for (int k = i + 1; k < n; k++) acc -= Lm[k * n + i] * P.NV[k * NV_COLS + c];
-        P.NV[i * NV_COLS + c] = acc / Lm[i * n + i];
-      }
-    } else if (lane - 2 < nc) {
-      // MA = Minv A_c_ub_E, one column per lane
-      const int j = lane - 2;
-      double* X = P.MA;
-      for (int i = 0; i < n; i++) {
-        double acc = X[i * nc + j];
-        for (int k = 0; k < i; k++) acc -= Lm[i * n + k] * X[k * nc + j];
-        X[i * nc + j] = acc / Lm[i * n + i];
-      }
-      for (int i = n - 1; i >= 0; i--) {
-        double acc = X[i * nc + j];
-        for (int k = i + 1; k < n; k++) acc -= Lm[k * n + i] * X[k * nc + j];
-        X[i * nc + j] = acc / Lm[i * n + i];
-      }
-    }
-    // columns beyond 62 (nc > 62 never happens: nc <= 48)
-  }
-  __syncthreads();
-  STAMP(32);
-  // Q = A_c^T MA + cfm I; W = copy to factor
-  for (int t = lane; t < nc * nc; t += WAVE) {
-    const int r = t / nc, c = t % nc;
-    double acc = 0;
-    for (int i = 0; i < n; i++) acc += P.Ac[i * nc + r] * P.MA[i * nc + c];
-    if (r == c) acc += cfm;
-    P.Q[t] = acc;
-    P.W[t] = acc;
-  }
-  // delta = MA fc / dt ; a* = yf + delta ; u = AcubE^T w
+  // delta = MA fc / dt ; a* = y_f + delta ; u = A_c_ub_E^T w
   for (int i = lane; i < n; i += WAVE) {
     double acc = 0;
-    for (int c = 0; c < nc; c++) acc += P.MA[i * nc + c] * P.fc[c];
+    for (int c = 0; c < nc; c++) acc += MA[i * nc + c] * P.fc[c];
     const double d = acc / dt;
     P.NV[i * NV_COLS + NV_DELTA] = d;
-    s[L.x + i] = P.NV[i * NV_COLS + NV_YF] + d;
+    P.NV[i * NV_COLS + NV_W] = s[L.w + i];
+    s[L.x + i] = sn[snYf(n) + i] + d;
   }
   for (int c = lane; c < nc; c += WAVE) {
     double acc = 0;
-    for (int i = 0; i < n; i++) acc += P.AcubE[i * nc + c] * P.NV[i * NV_COLS + NV_W];
+    for (int i = 0; i < n; i++) acc += AcubE[i * nc + c] * s[L.w + i];
     P.u[c] = acc;
   }
   __syncthreads();
-  // pinv(Q) via COD: column c of P (stored as row c of PT) solved by lane c
-  Cod cod;
-  double* w = carveCod(P.codw, P.W, nc, nc, nc, cod);
-  double* cn = w; w += m;
-  double* vv = w; w += m;
-  STAMP(33);
-  codFactor(cod, cn, vv, lane);
-  STAMP(34);
-  if (lane < nc) {
-    double* rhs = P.Pscr + lane * nc;
-    double* z = P.Pscr + nc * nc + lane * nc;
-    for (int i = 0; i < nc; i++) rhs[i] = i == lane ? 1.0 : 0.0;
-    codSolveLane(cod, rhs, P.PT + lane * nc, z);
-  }
-  __syncthreads();
-  STAMP(35);
   // lambda = P^T u ; x = P b ; beta
   for (int c = lane; c < nc; c += WAVE) {
     double l = 0, xx = 0;
     for (int r = 0; r < nc; r++) {
-      l += P.PT[c * nc + r] * P.u[r];
-      xx += P.PT[r * nc + c] * P.bc[r];
+      l += PT[c * nc + r] * P.u[r];
+      xx += PT[r * nc + c] * P.bc[r];
     }
     P.lam[c] = l;
     P.beta[c] = P.bounce[c] * l;
     P.xq[c] = xx;
   }
-  // imprecision || I - Q Q^+ ||^2 (per-lane partial sums)
-  double part = 0.0;
-  for (int t = lane; t < nc * nc; t += WAVE) {
-    const int r = t / nc, c = t % nc;
-    double acc = 0;
-    for (int k = 0; k < nc; k++) acc += P.Q[r * nc + k] * P.PT[c * nc + k];
-    const double e = (r == c ? 1.0 : 0.0) - acc;
-    part += e * e;
-  }
-  // wave reduction through the (backward-idle) contact list region of ct
-  ct[CT_CONTACTS + lane] = part;
   __syncthreads();
-  if (lane == 0) {
-    double tot = 0;
-    for (int i = 0; i < WAVE; i++) tot += ct[CT_CONTACTS + i];
-    ct[H_FLAG] = tot >= 1e-18 ? 1 : 0;
-  }
-  __syncthreads();
-  const int imp = (int)ct[H_FLAG];
-  // mu = A_c beta ; sigma = MA x ; rhs for kappa = A_c lambda
-  for (int i = lane; i < n; i += WAVE) {
-    double mu = 0, sg = 0, kp = 0;
-    for (int c = 0; c < nc; c++) {
-      mu += P.Ac[i * nc + c] * P.beta[c];
-      sg += P.MA[i * nc + c] * P.xq[c];
-      kp += P.Ac[i * nc + c] * P.lam[c];
-    }
-    P.NV[i * NV_COLS + NV_MU] = mu;
-    P.NV[i * NV_COLS + NV_NU] = mu;
-    P.NV[i * NV_COLS + NV_SIGMA] = sg;
-    P.NV[i * NV_COLS + NV_KAPPA] = kp;
-  }
   if (imp) {
     for (int c = lane; c < nc; c += WAVE) {
       double qx = 0, qtl = 0, rh = 0, ze = 0;
       for (int k = 0; k < nc; k++) {
-        qx += P.Q[c * nc + k] * P.xq[k];
-        qtl += P.Q[k * nc + c] * P.lam[k];
-        rh += P.PT[k * nc + c] * P.lam[k];   // (P lambda)_c
-        ze += P.PT[c * nc + k] * P.xq[k];    // (P^T x)_c
+        qx += Q[c * nc + k] * P.xq[k];
+        qtl += Q[k * nc + c] * P.lam[k];
+        rh += PT[k * nc + c] * P.lam[k];   // (P lambda)_c
+        ze += PT[c * nc + k] * P.xq[k];    // (P^T x)_c
       }
       P.r1[c] = P.bc[c] - qx;
       P.piv[c] = P.u[c] - qtl;
@@ -1304,32 +1300,37 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
     for (int c = lane; c < nc; c += WAVE) { P.r1[c] = 0; P.piv[c] = 0; P.rho[c] = 0; P.zeta[c] = 0; }
   }
   __syncthreads();
+  STAMP(35);
+  // mu = A_c beta ; nu = Minv A_c beta ; sigma = MA x ; kappa = Minv A_c lambda ; the
+  // pseudo-inverse branch vectors; w - nu
   for (int i = lane; i < n; i += WAVE) {
-    double a1 = 0, ar = 0, a2 = 0, ap = 0;
+    double mu = 0, nu = 0, sg = 0, kp = 0, a1 = 0, ar = 0, a2 = 0, ap = 0;
     for (int c = 0; c < nc; c++) {
-      a1 += P.Ac[i * nc + c] * P.r1[c];
-      ar += P.MA[i * nc + c] * P.rho[c];
-      a2 += P.Ac[i * nc + c] * P.zeta[c];
-      ap += P.MA[i * nc + c] * P.piv[c];
+      const double ac = Ac[i * nc + c], mac = MAc[i * nc + c], ma = MA[i * nc + c];
+      mu += ac * P.beta[c];
+      nu += mac * P.beta[c];
+      sg += ma * P.xq[c];
+      kp += mac * P.lam[c];
+      a1 += mac * P.r1[c];
+      ar += ma * P.rho[c];
+      a2 += mac * P.zeta[c];
+      ap += ma * P.piv[c];
     }
-    P.NV[i * NV_COLS + NV_MA1] = a1;
-    P.NV[i * NV_COLS + NV_MARHO] = ar;
-    P.NV[i * NV_COLS + NV_MA2] = a2;
-    P.NV[i * NV_COLS + NV_MAPI] = ap;
-  }
-  __syncthreads();
-  STAMP(36);
-  {
-    const int cols[4] = {NV_NU, NV_KAPPA, NV_MA1, NV_MA2};
-    cholSolveColumns(Lm, P.NV, n, NV_COLS, cols, 4, lane);
-  }
-  STAMP(37);
-  // w - nu into s[L.w]
-  for (int i = lane; i < n; i += WAVE) {
-    const double w2 = P.NV[i * NV_COLS + NV_W] - P.NV[i * NV_COLS + NV_NU];
-    P.NV[i * NV_COLS + NV_W2] = w2;
+    double* nv = P.NV + i * NV_COLS;
+    nv[NV_MU] = mu;
+    nv[NV_NU] = nu;
+    nv[NV_SIGMA] = sg;
+    nv[NV_KAPPA] = kp;
+    nv[NV_MA1] = a1;
+    nv[NV_MARHO] = ar;
+    nv[NV_MA2] = a2;
+    nv[NV_MAPI] = ap;
+    const double w2 = nv[NV_W] - nu;
+    nv[NV_W2] = w2;
     s[L.w + i] = w2;
   }
+  __syncthreads();
+  STAMP(37);
   // per-row vectors g_j
   for (int t = lane; t < m * n; t += WAVE) {
     const int j = t / n, i = t % n;

@@ -75,6 +75,7 @@ __device__ bool wavePgs(int n, double* A, double& x, double b, double lo, double
 __device__ bool waveLcpValid(int m, const double* A, double cfm, double x, double b, double hi, double lo, int fi,
                              bool ignoreFriction, int lane) {
   double v = -b;
+#pragma unroll 4
   for (int j = 0; j < m; j++) {
     const double xj = rdl(x, j);
     if (lane < m) v += (A[lane * m + j] + (lane == j ? cfm : 0.0)) * xj;
@@ -410,6 +411,7 @@ __device__ bool waveDantzig(int n, double* A, double* Lbuf, double* scr, double&
         const bool inN = lane >= nC && lane < nC + nN;
         {
           double acc = 0.0;
+#pragma unroll 4
           for (int j = 0; j < nC; j++) {
             const double dxj = rdl(D.deltaX, j);
             if (inN) acc += A[lane * n + j] * dxj;

@@ -21,6 +21,10 @@ struct ModelDev {
   int parent[NB_MAX], jtype[NB_MAX], dof0[NB_MAX], ndof[NB_MAX], depth[NB_MAX];
   int skel[NB_MAX], reactive[NB_MAX];
   unsigned long long anc[NB_MAX];  // bit a set <=> body a is an ancestor-or-self
+  // tree structure for level-parallel sweeps: bodies grouped by depth and
+  // children lists (both in ascending body order)
+  int levelStart[NB_MAX + 1], levelBodies[NB_MAX];
+  int childStart[NB_MAX + 1], childList[NB_MAX];
   double Tpj[NB_MAX][12];          // [R|p] row-major
   double Tcj[NB_MAX][12];
   double TcjInv[NB_MAX][12];

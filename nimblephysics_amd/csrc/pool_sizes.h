@@ -16,7 +16,13 @@
 #define CT_PAIRBUF (CT_DROPPED + CT_MAX_DROPPED * CREC)
 #define CT_PAIR_CHUNK 16
 #define CT_PAIR_CHUNK_HOST CT_PAIR_CHUNK
-__host__ __device__ inline int ctDoubles(int pairChunk) { return CT_PAIRBUF + pairChunk * 8 * CREC; }
+// the forward's header + kept contacts live in Layout::ct; the dropped list
+// and the per-pair narrow-phase buffers live at the start of the alias area
+// (dead dynamics buffers, Layout::V)
+__host__ __device__ inline int ctDoubles() { return CT_DROPPED; }
+__host__ __device__ inline int collideScratchDoubles(int pairChunk) {
+  return CT_MAX_DROPPED * CREC + pairChunk * 8 * CREC;
+}
 
 // snapshot layout
 #define SN_NCON 0
@@ -27,19 +33,31 @@ __host__ __device__ inline int ctDoubles(int pairChunk) { return CT_PAIRBUF + pa
 #define SN_STATUS 5
 #define SN_SC 6
 #define SN_IGN 7
+#define SN_IMP 8   // Q rank-deficient (pseudo-inverse gradient branch)
 #define SN_CONTACTS 16
 #define SN_ROWS (SN_CONTACTS + NIMBLE_MAX_CONTACTS * CREC)
 #define SN_ROWREC 12
 #define SN_FC (SN_ROWS + NIMBLE_MAX_LCP * SN_ROWREC)
 #define SN_VF (SN_FC + NIMBLE_MAX_LCP)
-__host__ __device__ inline int snapWorkspaceOffset(int n) { return ((SN_VF + n + 7) / 8) * 8; }
+#define SN_MAXL NIMBLE_MAX_LCP
+__host__ __device__ inline int snAlign8(int x) { return ((x + 7) / 8) * 8; }
+// unconstrained acceleration Minv (tau - C - D v - K ..) of the step
+__host__ __device__ inline int snYf(int n) { return SN_VF + n; }
+// gv-independent backward data, n x nc (leading dimension nc) / nc x nc
+__host__ __device__ inline int snAc(int n) { return snAlign8(snYf(n) + n); }
+__host__ __device__ inline int snAcubE(int n) { return snAc(n) + n * SN_MAXL; }
+__host__ __device__ inline int snMA(int n) { return snAcubE(n) + n * SN_MAXL; }     // Minv A_c_ub_E
+__host__ __device__ inline int snMAc(int n) { return snMA(n) + n * SN_MAXL; }       // Minv A_c
+__host__ __device__ inline int snPT(int n) { return snMAc(n) + n * SN_MAXL; }       // pinv(Q)^T
+__host__ __device__ inline int snQ(int n) { return snPT(n) + SN_MAXL * SN_MAXL; }   // Q
+__host__ __device__ inline int snapWorkspaceOffset(int n) { return snAlign8(snQ(n) + SN_MAXL * SN_MAXL); }
+// 64 doubles at the very end of every snapshot are kept for debug stamps
+#define SN_DEBUG_TAIL 64
 
 // LCP workspace pools for m rows and n dofs
 #define NV_COLS 16
-__host__ __device__ inline int fwdPoolDoubles(int m, int n) { return 2 * n * m + 3 * m * m + 48 * m + 2 * n + 32; }
-__host__ __device__ inline int bwdPoolDoubles(int m, int n) {
-  return 4 * n * m + 5 * m * m + 48 * m + NV_COLS * n + 64;
-}
+__host__ __device__ inline int fwdPoolDoubles(int m, int n) { return n * m + 3 * m * m + 30 * m + 2 * n + 48; }
+__host__ __device__ inline int bwdPoolDoubles(int m, int n) { return n * m + 24 * m + NV_COLS * n + 64; }
 
 #define fwdPoolDoublesHost fwdPoolDoubles
 #define bwdPoolDoublesHost bwdPoolDoubles

@@ -14,6 +14,8 @@ DEV void cross3(const double* a, const double* b, double* o) {
   o[1] = a[2] * b[0] - a[0] * b[2];
   o[2] = a[0] * b[1] - a[1] * b[0];
 }
+// packed lower-triangular index (row i, column k <= i)
+DEV int tri(int i, int k) { return ((i * (i + 1)) >> 1) + k; }
 DEV double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 DEV double dot6(const double* a, const double* b) {
   return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];

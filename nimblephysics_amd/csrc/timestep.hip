@@ -19,6 +19,7 @@
 
 #include "model.h"
 #include "spatial.cuh"
+#include "wave.cuh"
 
 #define WAVE 64
 
@@ -34,72 +35,95 @@
 __device__ void kinematics(const ModelDev& md, double* s, const Layout& L, int lane, const double* ddq) {
   const double* q = s + L.q;
   const double* v = s + L.v;
-  for (int lev = 0; lev <= md.maxDepth; lev++) {
+  // 1. local transforms T_pj * Q(q) * T_cj^-1 (one lane per body), into Tw
+  if (lane < md.nb) {
     const int b = lane;
-    if (b < md.nb && md.depth[b] == lev) {
-      const int jt = md.jtype[b];
-      const int o = md.dof0[b];
-      double Q[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
-      const double* a = md.axis[b];
-      if (jt == NIMBLE_JOINT_REVOLUTE) {
-        // math::expAngular(axis * q) (Geometry.cpp:3414)
-        double c = cos(q[o]), sn = sin(q[o]), t = 1.0 - c;
-        Q[0] = c + t * a[0] * a[0];        Q[1] = t * a[0] * a[1] - sn * a[2]; Q[2] = t * a[0] * a[2] + sn * a[1];
-        Q[4] = t * a[0] * a[1] + sn * a[2]; Q[5] = c + t * a[1] * a[1];        Q[6] = t * a[1] * a[2] - sn * a[0];
-        Q[8] = t * a[0] * a[2] - sn * a[1]; Q[9] = t * a[1] * a[2] + sn * a[0]; Q[10] = c + t * a[2] * a[2];
-      } else if (jt == NIMBLE_JOINT_PRISMATIC) {
-        Q[3] = a[0] * q[o]; Q[7] = a[1] * q[o]; Q[11] = a[2] * q[o];
-      } else if (jt == NIMBLE_JOINT_FREE) {
-        double R[9];
-        expMapRot(q + o, R);
-        Q[0] = R[0]; Q[1] = R[1]; Q[2] = R[2]; Q[3] = q[o + 3];
-        Q[4] = R[3]; Q[5] = R[4]; Q[6] = R[5]; Q[7] = q[o + 4];
-        Q[8] = R[6]; Q[9] = R[7]; Q[10] = R[8]; Q[11] = q[o + 5];
-      }
-      double T[12];
-      tmul(md.Tpj[b], Q, T);
-      tmul(T, md.TcjInv[b], T);
+    const int jt = md.jtype[b];
+    const int o = md.dof0[b];
+    double Q[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+    const double* a = md.axis[b];
+    if (jt == NIMBLE_JOINT_REVOLUTE) {
+      // math::expAngular(axis * q) (Geometry.cpp:3414)
+      double c = cos(q[o]), sn = sin(q[o]), t = 1.0 - c;
+      Q[0] = c + t * a[0] * a[0];        Q[1] = t * a[0] * a[1] - sn * a[2]; Q[2] = t * a[0] * a[2] + sn * a[1];
+      Q[4] = t * a[0] * a[1] + sn * a[2]; Q[5] = c + t * a[1] * a[1];        Q[6] = t * a[1] * a[2] - sn * a[0];
+      Q[8] = t * a[0] * a[2] - sn * a[1]; Q[9] = t * a[1] * a[2] + sn * a[0]; Q[10] = c + t * a[2] * a[2];
+    } else if (jt == NIMBLE_JOINT_PRISMATIC) {
+      Q[3] = a[0] * q[o]; Q[7] = a[1] * q[o]; Q[11] = a[2] * q[o];
+    } else if (jt == NIMBLE_JOINT_FREE) {
+      double R[9];
+      expMapRot(q + o, R);
+      Q[0] = R[0]; Q[1] = R[1]; Q[2] = R[2]; Q[3] = q[o + 3];
+      Q[4] = R[3]; Q[5] = R[4]; Q[6] = R[5]; Q[7] = q[o + 4];
+      Q[8] = R[6]; Q[9] = R[7]; Q[10] = R[8]; Q[11] = q[o + 5];
+    }
+    double T[12];
+    tmul(md.Tpj[b], Q, T);
+    tmul(T, md.TcjInv[b], s + L.Tw + 12 * b);
+  }
+  __syncthreads();
+  // 2. compose down the tree, one level at a time
+  for (int lev = 1; lev <= md.maxDepth; lev++) {
+    const int b0 = md.levelStart[lev], cnt = md.levelStart[lev + 1] - b0;
+    if (lane < cnt) {
+      const int b = md.levelBodies[b0 + lane];
       double* Tw = s + L.Tw + 12 * b;
-      const int p = md.parent[b];
-      double Vp[6] = {0, 0, 0, 0, 0, 0}, Ap[6] = {0, 0, 0, 0, 0, 0};
-      if (p >= 0) {
-        tmul(s + L.Tw + 12 * p, T, Tw);
-#pragma unroll
-        for (int i = 0; i < 6; i++) { Vp[i] = s[L.V + 6 * p + i]; Ap[i] = s[L.A + 6 * p + i]; }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 12; i++) Tw[i] = T[i];
-      }
-      // motion subspace in world frame: Ad_{Tw * Tcj} * S_local
-      double TwC[12];
-      tmul(Tw, md.Tcj[b], TwC);
-      double vj[6] = {0, 0, 0, 0, 0, 0}, aj[6] = {0, 0, 0, 0, 0, 0};
-      const int nd = md.ndof[b];
-      for (int k = 0; k < nd; k++) {
-        double loc[6] = {0, 0, 0, 0, 0, 0};
-        if (jt == NIMBLE_JOINT_REVOLUTE) { loc[0] = a[0]; loc[1] = a[1]; loc[2] = a[2]; }
-        else if (jt == NIMBLE_JOINT_PRISMATIC) { loc[3] = a[0]; loc[4] = a[1]; loc[5] = a[2]; }
-        else loc[k] = 1.0;
-        double* S = s + L.Sw + 6 * (o + k);
-        adT(TwC, loc, S);
-        const double qd = v[o + k];
-        const double qdd = ddq ? ddq[o + k] : 0.0;
-#pragma unroll
-        for (int i = 0; i < 6; i++) { vj[i] = fma(S[i], qd, vj[i]); aj[i] = fma(S[i], qdd, aj[i]); }
-      }
-      double Vb[6];
-#pragma unroll
-      for (int i = 0; i < 6; i++) Vb[i] = Vp[i] + vj[i];
-      double cr[6];
-      crm(Vb, vj, cr);  // d/dt(S) qdot = V_child x (S qdot)
-#pragma unroll
-      for (int i = 0; i < 6; i++) {
-        s[L.V + 6 * b + i] = Vb[i];
-        s[L.A + 6 * b + i] = Ap[i] + aj[i] + cr[i];
-      }
+      tmul(s + L.Tw + 12 * md.parent[b], Tw, Tw);
     }
     __syncthreads();
   }
+  // 3. world-frame motion subspace Ad_{Tw * Tcj} S_local (one lane per dof)
+  if (lane < md.n) {
+    const int k = lane, b = md.dofBody[k], jt = md.jtype[b];
+    const double* a = md.axis[b];
+    double loc[6] = {0, 0, 0, 0, 0, 0};
+    if (jt == NIMBLE_JOINT_REVOLUTE) { loc[0] = a[0]; loc[1] = a[1]; loc[2] = a[2]; }
+    else if (jt == NIMBLE_JOINT_PRISMATIC) { loc[3] = a[0]; loc[4] = a[1]; loc[5] = a[2]; }
+    else loc[k - md.dof0[b]] = 1.0;
+    double TwC[12];
+    tmul(s + L.Tw + 12 * b, md.Tcj[b], TwC);
+    adT(TwC, loc, s + L.Sw + 6 * k);
+  }
+  __syncthreads();
+  // 4. V_b = sum over ancestor dofs of S_j qdot_j
+  if (lane < md.nb) {
+    const int b = lane;
+    double V[6] = {0, 0, 0, 0, 0, 0};
+    const unsigned long long an = md.anc[b];
+#pragma unroll 4
+    for (int j = 0; j < md.n; j++) {
+      if (!((an >> md.dofBody[j]) & 1ull)) continue;
+      const double* S = s + L.Sw + 6 * j;
+#pragma unroll
+      for (int i = 0; i < 6; i++) V[i] = fma(S[i], v[j], V[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++) s[L.V + 6 * b + i] = V[i];
+  }
+  __syncthreads();
+  // 5. A_b = sum over ancestor dofs of S_j qddot_j + V_body(j) x (S_j qdot_j)
+  //    (BodyNode::updatePartialAcceleration / updateAccelerationFD unrolled)
+  if (lane < md.nb) {
+    const int b = lane;
+    double A[6] = {0, 0, 0, 0, 0, 0};
+    const unsigned long long an = md.anc[b];
+#pragma unroll 4
+    for (int j = 0; j < md.n; j++) {
+      const int bj = md.dofBody[j];
+      if (!((an >> bj) & 1ull)) continue;
+      const double* S = s + L.Sw + 6 * j;
+      double sv[6], cr[6];
+#pragma unroll
+      for (int i = 0; i < 6; i++) sv[i] = S[i] * v[j];
+      crm(s + L.V + 6 * bj, sv, cr);
+      const double qdd = ddq ? ddq[j] : 0.0;
+#pragma unroll
+      for (int i = 0; i < 6; i++) A[i] += fma(S[i], qdd, cr[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++) s[L.A + 6 * b + i] = A[i];
+  }
+  __syncthreads();
 }
 
 // World-frame spatial inertia of body b (6x6, row-major) at the world origin.
@@ -144,11 +168,16 @@ __device__ void composites(const ModelDev& md, double* s, const Layout& L, int l
     for (int i = 0; i < 6; i++) s[L.F + 6 * b + i] = f[i] + vxh[i];
   }
   __syncthreads();
-  for (int b = md.nb - 1; b > 0; b--) {
-    const int p = md.parent[b];
-    if (p >= 0) {
-      if (lane < 36) s[L.IC + 36 * p + lane] += s[L.IC + 36 * b + lane];
-      else if (lane < 42) s[L.F + 6 * p + lane - 36] += s[L.F + 6 * b + lane - 36];
+  // subtree sums, one tree level at a time (parents gather their children)
+  for (int lev = md.maxDepth - 1; lev >= 0; lev--) {
+    const int b0 = md.levelStart[lev], cnt = (md.levelStart[lev + 1] - b0) * 42;
+    for (int t = lane; t < cnt; t += WAVE) {
+      const int p = md.levelBodies[b0 + t / 42], e = t % 42;
+      const int off = e < 36 ? L.IC + 36 * p + e : L.F + 6 * p + (e - 36);
+      const int stride = e < 36 ? 36 : 6;
+      double acc = s[off];
+      for (int q = md.childStart[p]; q < md.childStart[p + 1]; q++) acc += s[off + stride * (md.childList[q] - p)];
+      s[off] = acc;
     }
     __syncthreads();
   }
@@ -175,51 +204,49 @@ __device__ void massMatrixAndBias(const ModelDev& md, double* s, const Layout& L
       mv6(s + L.IC + 36 * deep, s + L.Sw + 6 * k, tmp);
       val = dot6(s + L.Sw + 6 * j, tmp);
     }
-    s[L.M + j * n + k] = val;
-    s[L.M + k * n + j] = val;
+    s[L.M + tri(j, k)] = val;  // lower triangle, packed
   }
   for (int j = lane; j < n; j += WAVE) C[j] = dot6(s + L.Sw + 6 * j, s + L.F + 6 * md.dofBody[j]);
   __syncthreads();
 }
 
-// In-place Cholesky of the n x n matrix at A (lower triangle holds L).
+// In-place Cholesky of the packed lower triangle at A (row i at i(i+1)/2):
+// left-looking (Crout) with one lane per row, one barrier per column.  The
+// per-element subtraction order (k ascending) is that of the right-looking
+// factorisation.
 __device__ void cholesky(double* A, int n, int lane) {
   for (int j = 0; j < n; j++) {
-    if (lane == 0) A[j * n + j] = sqrt(A[j * n + j]);
-    __syncthreads();
-    const double d = A[j * n + j];
-    for (int i = j + 1 + lane; i < n; i += WAVE) A[i * n + j] /= d;
-    __syncthreads();
-    const int m = n - j - 1;
-    const int cnt = m * (m + 1) / 2;
-    for (int t = lane; t < cnt; t += WAVE) {
-      int r = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-      while (r * (r + 1) / 2 > t) r--;
-      while ((r + 1) * (r + 2) / 2 <= t) r++;
-      const int c = t - r * (r + 1) / 2;
-      const int i = j + 1 + r, k = j + 1 + c;
-      A[i * n + k] -= A[i * n + j] * A[k * n + j];
+    double sum = 0.0;
+    if (lane >= j && lane < n) {
+      const int ri = tri(lane, 0), rj = tri(j, 0);
+      sum = A[ri + j];
+#pragma unroll 8
+      for (int k = 0; k < j; k++) sum -= A[ri + k] * A[rj + k];
     }
+    const double djj = sqrt(rdl(sum, j));
+    if (lane == j) A[tri(j, j)] = djj;
+    else if (lane > j && lane < n) A[tri(lane, j)] = sum / djj;
     __syncthreads();
   }
 }
 
-// Solve L L^T x = b in place (x = b on entry).
+// Solve L L^T x = b in place (x = b on entry): x held one entry per lane,
+// no barriers inside.
 __device__ void cholSolve(const double* Lm, double* x, int n, int lane) {
-  for (int j = 0; j < n; j++) {
-    if (lane == 0) x[j] /= Lm[j * n + j];
-    __syncthreads();
-    const double xj = x[j];
-    for (int i = j + 1 + lane; i < n; i += WAVE) x[i] -= Lm[i * n + j] * xj;
-    __syncthreads();
+  double xi = lane < n ? x[lane] : 0.0;
+  for (int k = 0; k < n; k++) {
+    const double xk = rdl(xi, k) / Lm[tri(k, k)];
+    if (lane == k) xi = xk;
+    else if (lane > k && lane < n) xi -= Lm[tri(lane, k)] * xk;
   }
-  for (int j = n - 1; j >= 0; j--) {
-    if (lane == 0) x[j] /= Lm[j * n + j];
-    __syncthreads();
-    const double xj = x[j];
-    for (int i = lane; i < j; i += WAVE) x[i] -= Lm[j * n + i] * xj;
-    __syncthreads();
+  for (int k = n - 1; k >= 0; k--) {
+    const double xk = rdl(xi, k) / Lm[tri(k, k)];
+    if (lane == k) xi = xk;
+    else if (lane < k) xi -= Lm[tri(k, lane)] * xk;
   }
+  __syncthreads();
+  if (lane < n) x[lane] = xi;
+  __syncthreads();
 }
 
 __device__ void loadState(const ModelDev& md, double* s, const Layout& L, int lane, const double* state,
@@ -262,7 +289,13 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, con
 #endif
     STAMP(10);
     loadState(md, s, L, lane, st, forces + (size_t)env * n);
-    coreDynamics(md, s, L, lane);
+    kinematics(md, s, L, lane, nullptr);
+    STAMP(14);
+    composites(md, s, L, lane);
+    STAMP(15);
+    massMatrixAndBias(md, s, L, lane, s + L.rhs);
+    STAMP(16);
+    cholesky(s + L.M, md.n, lane);
     STAMP(11);
     // rhs = tau + spring + damping - C   (GenericJoint::updateTotalForceDynamic)
     double* x = s + L.x;
@@ -282,7 +315,7 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, con
     // runConstraintEngine (World.cpp:254): collision, LCP, impulses
     if (md.numPairs > 0) {
       double* sn = snapshot + (size_t)env * snapDoubles;
-      contactStage(md, s, L, lane, v1, lcpCache + (size_t)env * cacheDoubles, sn, sn + snapWorkspaceOffset(n));
+      contactStage(md, s, L, lane, v1, x, lcpCache + (size_t)env * cacheDoubles, sn, sn + snapWorkspaceOffset(n));
     }
     double* out = nextState + (size_t)env * 2 * n;
     for (int i = lane; i < n; i += WAVE) out[n + i] = v1[i];
@@ -354,20 +387,20 @@ __device__ void derivativeComposites(const ModelDev& md, double* s, const Layout
     }
   }
   __syncthreads();
-  for (int b = md.nb - 1; b > 0; b--) {
-    const int p = md.parent[b];
-    if (p >= 0) {
-      for (int t = lane; t < 126; t += WAVE) {
-        int off;
-        if (t < 36) off = L.B1 + t;
-        else if (t < 72) off = L.B23 + (t - 36);
-        else if (t < 108) off = L.B4 + (t - 72);
-        else if (t < 114) off = L.P + (t - 108);
-        else if (t < 120) off = L.H + (t - 114);
-        else off = L.F + (t - 120);
-        const int stride = (t < 108) ? 36 : 6;
-        s[off + stride * p] += s[off + stride * b];
-      }
+  for (int lev = md.maxDepth - 1; lev >= 0; lev--) {
+    const int b0 = md.levelStart[lev], cnt = (md.levelStart[lev + 1] - b0) * 126;
+    for (int t = lane; t < cnt; t += WAVE) {
+      const int p = md.levelBodies[b0 + t / 126], e = t % 126;
+      int off, stride;
+      if (e < 36) { off = L.B1 + e; stride = 36; }
+      else if (e < 72) { off = L.B23 + (e - 36); stride = 36; }
+      else if (e < 108) { off = L.B4 + (e - 72); stride = 36; }
+      else if (e < 114) { off = L.P + (e - 108); stride = 6; }
+      else if (e < 120) { off = L.H + (e - 114); stride = 6; }
+      else { off = L.F + (e - 120); stride = 6; }
+      double acc = s[off + stride * p];
+      for (int q = md.childStart[p]; q < md.childStart[p + 1]; q++) acc += s[off + stride * md.childList[q]];
+      s[off + stride * p] = acc;
     }
     __syncthreads();
   }
@@ -457,22 +490,7 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
       // constrained: a* = Minv (z + A_c_ub_E f_c) / dt, w <- w - nu
       const int need = bwdPoolDoubles(m, n);
       carveBwd(need <= L.poolCap ? s + L.pool : sn + snapWorkspaceOffset(n), m, n, P);
-      imp = contactBackwardPrep(md, s, L, lane, sn, P, m, nc, sn[SN_CFM], s + L.ct);
-#ifdef NIMBLE_DEBUG_DUMP
-      if (lane == 0) {
-        double* dbg = sn + snapWorkspaceOffset(n);
-        int o = 0;
-        dbg[o++] = nc; dbg[o++] = imp;
-        for (int i = 0; i < nc * nc; i++) dbg[o++] = P.Q[i];
-        for (int i = 0; i < nc; i++) dbg[o++] = P.u[i];
-        for (int i = 0; i < nc; i++) dbg[o++] = P.lam[i];
-        for (int i = 0; i < nc * nc; i++) dbg[o++] = P.PT[i];
-        for (int i = 0; i < n * nc; i++) dbg[o++] = P.AcubE[i];
-        for (int i = 0; i < n * nc; i++) dbg[o++] = P.Ac[i];
-        for (int i = 0; i < n * NV_COLS; i++) dbg[o++] = P.NV[i];
-        for (int i = 0; i < n; i++) dbg[o++] = s[L.w + i];
-      }
-#endif
+      imp = contactBackwardPrep(md, s, L, lane, sn, P, m, nc, s + L.ct);
     } else {
       // z = dt (tau - C - D v - K (q - q0 + dt v))
       for (int i = lane; i < n; i += WAVE) {

@@ -21,15 +21,17 @@ snap = torch.zeros((B, dev.snapshot_doubles), dtype=torch.float64, device=d)
 nxt = torch.empty_like(state)
 s = torch.cuda.current_stream().cuda_stream
 n = w.getNumDofs()
-ws = ((752 + 48 + n + 7) // 8) * 8 + 1000
+a8 = lambda x: ((x + 7) // 8) * 8
+ws = a8(a8(800 + 2 * n) + 4 * n * 48 + 2 * 2304) + 1000  # snapWorkspaceOffset(n) + 1000
 for it in range(4):
-    snap[:, ws:ws + 14] = 0
+    snap[:, ws:ws + 20] = 0
     dev.forward(state, action, cache, nxt, snap, s)
     torch.cuda.synchronize()
     state = nxt.clone()
-    T = snap[:, ws:ws + 14].cpu().numpy()
+    T = snap[:, ws:ws + 20].cpu().numpy()
     hd = snap[:, :8].cpu().numpy()
-    names = {(10, 11): "load+coreDynamics", (11, 12): "solve v1", (0, 1): "collide", (1, 2): "rows",
+    names = {(10, 14): " kinematics", (14, 15): " composites", (15, 16): " CRBA + bias", (16, 11): " cholesky",
+             (10, 11): "load+coreDynamics", (11, 12): "solve v1", (0, 1): "collide", (1, 2): "rows",
              (2, 3): "cols/massed/A/b", (3, 4): "warm start/guess", (4, 5): "construct 1",
              (5, 6): "dantzig", (6, 7): "pgs/fallbacks", (7, 8): "construct 2", (8, 9): "impulses/snapshot",
              (12, 13): "contact stage total+integrate"}

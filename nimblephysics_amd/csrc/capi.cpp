@@ -64,6 +64,7 @@ static Layout makeLayout(const ModelDev& m, bool backward, int poolRows) {
   L.q = take(n); L.v = take(n); L.tau = take(n);
   L.Tw = take(12 * nb); L.Sw = take(6 * n);
   L.M = take(n * (n + 1) / 2);  // packed lower triangle (M, then its Cholesky factor)
+  L.dinv = take(n);             // 1 / L_kk
   L.rhs = take(n); L.x = take(n);
   L.v1 = take(n);
   L.ct = take(!backward && m.numPairs > 0 ? ctDoubles() : 16);

@@ -322,61 +322,81 @@ __device__ inline double* carveCod(double* w, double* A, int m, int n, int ld, C
   return w;
 }
 
-// `cn` and `v` are scratch vectors of n and m doubles.
+// Lane-parallel factorisation: column norms live in registers (lane j =
+// column j), the pivot is a wave arg-max (first index among equal maxima, as
+// the sequential scan), alpha and |v|^2 are wave reductions, and the
+// reflector pass (lane = column) also recomputes the next step's partial
+// column norms (same sums as a fresh recomputation).  Requires n <= 64.
+// `cn` is unused (kept for the call signature), `v` holds m doubles.
 __device__ void codFactor(Cod& c, double* cn, double* v, int lane) {
+  (void)cn;
   double* A = c.A;
   const int m = c.m, n = c.n, ld = c.ld;
-  for (int j = lane; j < n; j += WAVE) c.perm[j] = j;
+  if (lane < n) c.perm[lane] = lane;
+  double norm = 0.0;  // partial norm of column `lane` over rows >= k
+  if (lane < n) {
+#pragma unroll 8
+    for (int i = 0; i < m; i++) norm += A[i * ld + lane] * A[i * ld + lane];
+  }
   __syncthreads();
   double maxPivot = 0.0;
   for (int k = 0; k < c.kmax; k++) {
-    for (int j = k + lane; j < n; j += WAVE) {
-      double sc = 0;
-#pragma unroll 8
-      for (int i = k; i < m; i++) sc += A[i * ld + j] * A[i * ld + j];
-      cn[j] = sc;
-    }
-    __syncthreads();
-    int p = k;
-    double best = -1;
-#pragma unroll 8
-    for (int j = k; j < n; j++)
-      if (cn[j] > best) { best = cn[j]; p = j; }
+    // pivot: largest remaining norm, lowest index on ties
+    const double cand = (lane >= k && lane < n) ? norm : -1.0;
+    const double best = -waveMin(-cand);
+    const int p = waveFirst(lane >= k && lane < n && cand == best);
     if (p != k) {
       for (int i = lane; i < m; i += WAVE) {
-        double t = A[i * ld + k]; A[i * ld + k] = A[i * ld + p]; A[i * ld + p] = t;
+        const double t = A[i * ld + k]; A[i * ld + k] = A[i * ld + p]; A[i * ld + p] = t;
       }
+      const double nk = rdl(norm, k), np = rdl(norm, p);
+      if (lane == k) norm = np;
+      else if (lane == p) norm = nk;
       if (lane == 0) { int t = c.perm[k]; c.perm[k] = c.perm[p]; c.perm[p] = t; }
     }
     __syncthreads();
-    double alpha = 0;
-#pragma unroll 8
-    for (int i = k; i < m; i++) alpha += A[i * ld + k] * A[i * ld + k];
-    alpha = sqrt(alpha);
+    const double akk = A[k * ld + k];
+    const double colv = (lane >= k && lane < m) ? A[lane * ld + k] : 0.0;
+    double alpha = sqrt(waveSum(colv * colv));
     if (alpha == 0.0) {
       if (lane == 0) c.vn[k] = -1.0;
+      // fresh norms of the remaining columns over rows >= k+1
+      if (lane > k && lane < n) {
+        double nrm = 0.0;
+#pragma unroll 8
+        for (int i = k + 1; i < m; i++) nrm += A[i * ld + lane] * A[i * ld + lane];
+        norm = nrm;
+      }
       __syncthreads();
       continue;
     }
-    if (A[k * ld + k] > 0) alpha = -alpha;
-    for (int i = k + lane; i < m; i += WAVE) v[i] = A[i * ld + k] - (i == k ? alpha : 0.0);
+    if (akk > 0) alpha = -alpha;
+    const double vi = (lane == k) ? colv - alpha : colv;
+    if (lane >= k && lane < m) v[lane] = vi;
+    const double vnorm = waveSum(vi * vi);
     __syncthreads();
-    double vnorm = 0;
-#pragma unroll 8
-    for (int i = k; i < m; i++) vnorm += v[i] * v[i];
-    if (vnorm > 0) {
-      for (int j = k + lane; j < n; j += WAVE) {
+    if (lane >= k && lane < n) {
+      double nrm = 0.0;
+      if (vnorm > 0) {
         double sc = 0;
 #pragma unroll 8
-        for (int i = k; i < m; i++) sc += v[i] * A[i * ld + j];
+        for (int i = k; i < m; i++) sc += v[i] * A[i * ld + lane];
         sc = 2 * sc / vnorm;
 #pragma unroll 8
-        for (int i = k; i < m; i++) A[i * ld + j] -= sc * v[i];
+        for (int i = k; i < m; i++) {
+          const double a = A[i * ld + lane] - sc * v[i];
+          A[i * ld + lane] = a;
+          if (i > k) nrm += a * a;
+        }
+      } else {
+#pragma unroll 8
+        for (int i = k + 1; i < m; i++) nrm += A[i * ld + lane] * A[i * ld + lane];
       }
+      norm = nrm;
     }
     __syncthreads();
     maxPivot = fmax(maxPivot, fabs(A[k * ld + k]));
-    for (int i = k + 1 + lane; i < m; i += WAVE) A[i * ld + k] = v[i];
+    if (lane > k && lane < m) A[lane * ld + k] = v[lane];
     if (lane == 0) { c.vd[k] = v[k]; c.vn[k] = vnorm; }
     __syncthreads();
   }
@@ -388,22 +408,24 @@ __device__ void codFactor(Cod& c, double* cn, double* v, int lane) {
   // RZ: reflect row i over columns {i} U {r..n-1}; row i's trailing part is
   // kept as the reflector
   for (int i = r - 1; i >= 0 && r < n; i--) {
-    double al = A[i * ld + i] * A[i * ld + i];
-    for (int j = r; j < n; j++) al += A[i * ld + j] * A[i * ld + j];
-    al = sqrt(al);
-    if (A[i * ld + i] > 0) al = -al;
-    const double vi = A[i * ld + i] - al;
-    double vnz = vi * vi;
-    for (int j = r; j < n; j++) vnz += A[i * ld + j] * A[i * ld + j];
+    const double aii = A[i * ld + i];
+    const double tj = (lane >= r && lane < n) ? A[i * ld + lane] : 0.0;
+    const double tail = waveSum(tj * tj);
+    double al = sqrt(aii * aii + tail);
+    if (aii > 0) al = -al;
+    const double vi = aii - al;
+    const double vnz = vi * vi + tail;
     __syncthreads();
     if (lane == 0) { c.zd[i] = vi; c.zn[i] = vnz; }
     if (vnz != 0) {
       for (int row = lane; row <= i; row += WAVE) {
         double sc = A[row * ld + i] * vi;
+#pragma unroll 4
         for (int j = r; j < n; j++) sc += A[row * ld + j] * A[i * ld + j];
         sc = 2 * sc / vnz;
         A[row * ld + i] -= sc * vi;
         if (row < i)
+#pragma unroll 4
           for (int j = r; j < n; j++) A[row * ld + j] -= sc * A[i * ld + j];
       }
     }
@@ -547,7 +569,9 @@ __device__ inline double rowForceEntry(const ModelDev& md, const double* s, cons
 // Q = A_cc + A_cu E + cfm I  (== A_c^T Minv A_c_ub_E + cfm I).
 // Returns the standardized flag (wave-uniform).
 // ---------------------------------------------------------------------------
-__device__ bool devConstruct(FwdPool& P, int m, double cfm, bool ignoreFriction, double* ct, int lane) {
+__device__ bool devConstruct(FwdPool& P, int m, double cfm, bool ignoreFriction, double* ct, int lane,
+                             double* g_stamp = nullptr) {
+  (void)g_stamp;
   for (int guard = 0; guard <= m + 1; guard++) {
     if (lane == 0) {
       const double TH = 1e-6;
@@ -604,14 +628,17 @@ __device__ bool devConstruct(FwdPool& P, int m, double cfm, bool ignoreFriction,
       __syncthreads();
       return ok;
     }
+    STAMP(40);
     // Q (nc x nc) into M1
     double* Q = P.M1;
     for (int t = lane; t < nc * nc; t += WAVE) {
       const int cr = t / nc, cc = t % nc;
       const int rr = P.clampRow[cr], rc = P.clampRow[cc];
       double v = P.A[rr * m + rc];
-      for (int u = 0; u < m; u++)
-        if (P.mapping[u] >= 0 && P.clampIdx[P.mapping[u]] == cc) v += P.Eval[u] * P.A[rr * m + u];
+      // upper-bound rows feeding clamping column cc are the friction rows of
+      // its contact (rows rc+1, rc+2) whose findex is rc
+      for (int u = rc + 1; u <= rc + 2 && u < m; u++)
+        if (P.mapping[u] == rc) v += P.Eval[u] * P.A[rr * m + u];
       if (cr == cc) v += cfm;
       Q[t] = v;
     }
@@ -622,11 +649,14 @@ __device__ bool devConstruct(FwdPool& P, int m, double cfm, bool ignoreFriction,
     double* vv = w; w += m;
     double* rhs = w; w += m;
     double* z = w; w += m;
+    STAMP(41);
     codFactor(cod, cn, vv, lane);
+    STAMP(42);
     {
       const double f = codSolveWave(cod, lane < nc ? P.relVel[lane] : 0.0, z, lane);
       if (lane < nc) P.fsol[lane] = f;
     }
+    STAMP(43);
     (void)rhs;
     __syncthreads();
     if (lane == 0) {
@@ -650,6 +680,7 @@ __device__ bool devConstruct(FwdPool& P, int m, double cfm, bool ignoreFriction,
     __syncthreads();
     const bool ok = waveLcpValid(m, P.A, cfm, lane < m ? P.nx[lane] : 0.0, bR, hiR, loR, fiR, ignoreFriction, lane);
     const int res = ok ? ((int)ct[H_FLAG] ? 2 : 1) : 0;
+    STAMP(44);
     if (ok) {
       if (lane < m) P.X[lane] = P.nx[lane];
       if (lane < nc) P.fc[lane] = P.fsol[lane];
@@ -694,40 +725,25 @@ __device__ void devGuess(FwdPool& P, int m, double* x, double* ct, int lane) {
   __syncthreads();
 }
 
-// Row-parallel back substitution L^T Z = Z for the n x k block Z (ld k).
-__device__ void backSubRows(const double* Lm, double* Z, int n, int k, int lane) {
-  for (int r = n - 1; r >= 0; r--) {
-    const double inv = 1.0 / Lm[tri(r, r)];
-    for (int c = lane; c < k; c += WAVE) Z[r * k + c] *= inv;
-    __syncthreads();
-    const int cnt = r * k;
-    for (int t = lane; t < cnt; t += WAVE) {
-      const int i = t / k, c = t % k;
-      Z[i * k + c] -= Lm[tri(r, i)] * Z[r * k + c];
-    }
-    __syncthreads();
-  }
-}
-
 // The upstream-gradient-independent pieces of the constrained backward
 // (BackpropSnapshot.cpp:2723 getJacobianOfConstraintForce and the clamping
-// matrices it uses), computed here where Y = L^-1 J^T and A are on chip:
-// A_c, A_c_ub_E, Minv A_c_ub_E, Minv A_c, Q = A_c^T Minv A_c_ub_E + cfm I,
-// pinv(Q) (COD) and the rank-deficiency flag ||I - Q Q^+||^2 >= 1e-18.
+// matrices it uses), computed here where A = J Minv J^T is on chip:
+// A_c, A_c_ub_E, Q = A_c^T Minv A_c_ub_E + cfm I, pinv(Q) (COD) and the
+// rank-deficiency flag ||I - Q Q^+||^2 >= 1e-18.
 __device__ void backwardPrecompute(const ModelDev& md, double* s, const Layout& L, int lane, FwdPool& P, int m,
                                    double cfm, double* snap, double* ct) {
   const int n = md.n;
+#ifdef NIMBLE_STAGE_TIMING
+  double* g_stamp = snap + snapWorkspaceOffset(n) + 1000;
+#endif
+  STAMP(45);
   const int nc = (int)ct[H_NC];
   if (lane == 0) snap[SN_IMP] = 0.0;
   if (nc == 0) { __syncthreads(); return; }
-  const double* Lm = s + L.M;
   double* AcG = snap + snAc(n);
   double* AcubEG = snap + snAcubE(n);
-  double* MAG = snap + snMA(n);
-  double* MAcG = snap + snMAc(n);
   double* PTG = snap + snPT(n);
   double* QG = snap + snQ(n);
-  const double* Y = P.massed;
   const double* cts = s + L.ct + CT_CONTACTS;
   // A_c, A_c_ub_E (global): J^T columns re-evaluated (the on-chip copy of J^T
   // was overwritten by Y)
@@ -736,52 +752,20 @@ __device__ void backwardPrecompute(const ModelDev& md, double* s, const Layout& 
     const int r = P.clampRow[c];
     const double a = rowForceEntry(md, s, L, cts + P.rowC[r] * CREC, P.dvec + 3 * r, i);
     double ae = a;
-    for (int u = 0; u < m; u++)
-      if (P.mapping[u] >= 0 && P.clampIdx[P.mapping[u]] == c)
-        ae += P.Eval[u] * rowForceEntry(md, s, L, cts + P.rowC[u] * CREC, P.dvec + 3 * u, i);
+    for (int u = r + 1; u <= r + 2 && u < m; u++)
+      if (P.mapping[u] == r) ae += P.Eval[u] * rowForceEntry(md, s, L, cts + P.rowC[u] * CREC, P.dvec + 3 * u, i);
     AcG[t] = a;
     AcubEG[t] = ae;
   }
-  // Minv A_c_ub_E = L^-T (Y_c + Y_ub E) and Minv A_c = L^-T Y_c: back
-  // substitution in registers (row i on lane i), four columns per pass
-  for (int pass = 0; pass < 2; pass++) {
-    double* dst = pass == 0 ? MAG : MAcG;
-    for (int c0 = 0; c0 < nc; c0 += 4) {
-      double z[4];
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const int c = c0 + q;
-        double v = 0.0;
-        if (c < nc && lane < n) {
-          v = Y[lane * m + P.clampRow[c]];
-          if (pass == 0)
-            for (int u = 0; u < m; u++)
-              if (P.mapping[u] >= 0 && P.clampIdx[P.mapping[u]] == c) v += P.Eval[u] * Y[lane * m + u];
-        }
-        z[q] = v;
-      }
-      for (int k = n - 1; k >= 0; k--) {
-        const double inv = 1.0 / Lm[tri(k, k)];
-        const double lk = lane < k ? Lm[tri(k, lane)] : 0.0;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const double zk = rdl(z[q], k) * inv;
-          if (lane == k) z[q] = zk;
-          else if (lane < k) z[q] -= lk * zk;
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < 4; q++)
-        if (c0 + q < nc && lane < n) dst[lane * nc + c0 + q] = z[q];
-    }
-  }
+  STAMP(46);
+  STAMP(47);
   // Q into M1 (kept) and M2 (factored)
   for (int t = lane; t < nc * nc; t += WAVE) {
     const int cr = t / nc, cc = t % nc;
     const int rr = P.clampRow[cr], rc = P.clampRow[cc];
     double v = P.A[rr * m + rc];
-    for (int u = 0; u < m; u++)
-      if (P.mapping[u] >= 0 && P.clampIdx[P.mapping[u]] == cc) v += P.Eval[u] * P.A[rr * m + u];
+    for (int u = rc + 1; u <= rc + 2 && u < m; u++)
+      if (P.mapping[u] == rc) v += P.Eval[u] * P.A[rr * m + u];
     if (cr == cc) v += cfm;
     P.M1[t] = v;
     P.M2[t] = v;
@@ -792,7 +776,9 @@ __device__ void backwardPrecompute(const ModelDev& md, double* s, const Layout& 
   double* w = carveCod(P.scr, P.M2, nc, nc, nc, cod);
   double* cn = w; w += m;
   double* vv = w; w += m;
+  STAMP(48);
   codFactor(cod, cn, vv, lane);
+  STAMP(49);
   // pinv(Q): lane c solves Q x = e_c in place in row c of the (now free) A region
   double* Zs = P.A;
   if (lane < nc) {
@@ -828,6 +814,7 @@ __device__ void backwardPrecompute(const ModelDev& md, double* s, const Layout& 
     for (int j = 0; j < nc; j++) PTG[lane * nc + cod.perm[j]] = rhs[j];
   }
   __syncthreads();
+  STAMP(50);
   // ||I - Q Q^+||^2 with (Q Q^+)[r][c] = sum_j Q[r][perm_j] z_c[j]
   double part = 0.0;
   for (int t = lane; t < nc * nc; t += WAVE) {
@@ -840,6 +827,7 @@ __device__ void backwardPrecompute(const ModelDev& md, double* s, const Layout& 
   const double tot = waveSum(part);
   if (lane == 0) snap[SN_IMP] = tot >= 1e-18 ? 1.0 : 0.0;
   __syncthreads();
+  STAMP(51);
 }
 
 // ---------------------------------------------------------------------------
@@ -931,7 +919,7 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
   {
     double* Y = P.massed;
     for (int k = 0; k < n; k++) {
-      const double inv = 1.0 / Lm[tri(k, k)];
+      const double inv = s[L.dinv + k];
       for (int j = lane; j < m; j += WAVE) Y[k * m + j] *= inv;
       __syncthreads();
       const int cnt = (n - k - 1) * m;
@@ -991,7 +979,11 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
     __syncthreads();
   }
   STAMP(4);
+#ifdef NIMBLE_STAGE_TIMING
+  bool success = devConstruct(P, m, 0.0, false, ct, lane, g_stamp);
+#else
   bool success = devConstruct(P, m, 0.0, false, ct, lane);
+#endif
   STAMP(5);
   const bool shortCircuit = success;
   double cfm = 0.0;
@@ -1088,22 +1080,19 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
   // impulses (applyConstraintImpulses + computeImpulseForwardDynamics):
   // v1 += Minv J^T x = L^-T (Y x)
   {
-    double* u = P.scr;
-    for (int i = lane; i < n; i += WAVE) {
-      double acc = 0;
-      for (int j = 0; j < m; j++) acc += P.massed[i * m + j] * Xf[j];
-      u[i] = acc;
-      snap[SN_VF + i] = v1[i];
+    double u = 0.0;
+    if (lane < n) {
+#pragma unroll 4
+      for (int j = 0; j < m; j++) u += P.massed[lane * m + j] * Xf[j];
+      snap[SN_VF + lane] = v1[lane];
+    }
+    for (int k = n - 1; k >= 0; k--) {
+      const double uk = rdl(u, k) * s[L.dinv + k];
+      if (lane == k) u = uk;
+      else if (lane < k) u -= Lm[tri(k, lane)] * uk;
     }
     __syncthreads();
-    for (int j = n - 1; j >= 0; j--) {
-      if (lane == 0) u[j] /= Lm[tri(j, j)];
-      __syncthreads();
-      const double uj = u[j];
-      for (int i = lane; i < j; i += WAVE) u[i] -= Lm[tri(j, i)] * uj;
-      __syncthreads();
-    }
-    for (int i = lane; i < n; i += WAVE) v1[i] += u[i];
+    if (lane < n) v1[lane] += u;
   }
   if (lane == 0) cache[0] = m;
   for (int i = lane; i < m; i += WAVE) cache[1 + i] = Xf[i];
@@ -1221,11 +1210,13 @@ __device__ void tangentBasisGradient(const double* nrm, const double* g, double*
 }
 
 // Contact preparation of the backward from the snapshot's precomputed
-// clamping data (backwardPrecompute).  On return (all lanes):
-//   s[L.x]  = a* (acceleration incl. the constraint impulse / dt)
-//   s[L.w]  = w - nu       (the vector the unconstrained VJP machinery uses)
-//   NV columns hold the M-derivative pairs and mu; P.gRows / P.TAB the
-//   per-row vectors of the G_j terms.  Returns the imprecise flag.
+// clamping data (backwardPrecompute).  The nine Minv products it needs are
+// two batched register Cholesky solves:
+//   batch 1: gv, A_cubE f_c, A_cubE x, A_c r1, A_c zeta -> w, dt*delta, sigma, MA1, MA2
+//   batch 2: A_c beta, A_c lambda, A_cubE rho, A_cubE pi -> nu, kappa, MArho, MApi
+// On return (all lanes): s[L.x] = a*, s[L.w] = w - nu, NV columns hold the
+// M-derivative pairs and mu; P.gRows / P.TAB the per-row vectors of the
+// G_j terms.  Returns the imprecise flag.
 __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& L, int lane, const double* sn,
                                    BwdPool& P, int m, int nc, double* ct) {
   const int n = md.n;
@@ -1233,10 +1224,10 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
   const double* rows = sn + SN_ROWS;
   const double* Ac = sn + snAc(n);
   const double* AcubE = sn + snAcubE(n);
-  const double* MA = sn + snMA(n);
-  const double* MAc = sn + snMAc(n);
   const double* PT = sn + snPT(n);
   const double* Q = sn + snQ(n);
+  const double* Lm = s + L.M;
+  const double* dinv = s + L.dinv;
   const int imp = (int)sn[SN_IMP];
 #ifdef NIMBLE_STAGE_TIMING
   double* g_stamp = (double*)sn + snapWorkspaceOffset(n) + 1000;
@@ -1245,7 +1236,6 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
   (void)ct;
   for (int j = lane; j < m; j += WAVE)
     if ((int)rows[j * SN_ROWREC + RR_MAP] == CM_CLAMPING) P.rowOf[(int)rows[j * SN_ROWREC + RR_CIDX]] = j;
-  for (int i = lane; i < n; i += WAVE) s[L.w + i] = s[L.gv + i];
   __syncthreads();
   for (int c = lane; c < nc; c += WAVE) {
     const int r = P.rowOf[c];
@@ -1253,81 +1243,109 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
     P.bc[c] = rows[r * SN_ROWREC + RR_B];
     P.bounce[c] = rows[r * SN_ROWREC + RR_BOUNCE];
   }
-  cholSolve(s + L.M, s + L.w, n, lane);  // w = Minv gv
-  STAMP(31);
-  // delta = MA fc / dt ; a* = y_f + delta ; u = A_c_ub_E^T w
-  for (int i = lane; i < n; i += WAVE) {
-    double acc = 0;
-    for (int c = 0; c < nc; c++) acc += MA[i * nc + c] * P.fc[c];
-    const double d = acc / dt;
-    P.NV[i * NV_COLS + NV_DELTA] = d;
-    P.NV[i * NV_COLS + NV_W] = s[L.w + i];
-    s[L.x + i] = sn[snYf(n) + i] + d;
+  __syncthreads();
+  // x = P b ; r1 = b - Q x ; zeta = P^T x
+  for (int c = lane; c < nc; c += WAVE) {
+    double xx = 0;
+    for (int r = 0; r < nc; r++) xx += PT[r * nc + c] * P.bc[r];
+    P.xq[c] = xx;
   }
+  __syncthreads();
+  for (int c = lane; c < nc; c += WAVE) {
+    double qx = 0, ze = 0;
+    if (imp)
+      for (int k = 0; k < nc; k++) {
+        qx += Q[c * nc + k] * P.xq[k];
+        ze += PT[c * nc + k] * P.xq[k];
+      }
+    P.r1[c] = imp ? P.bc[c] - qx : 0.0;
+    P.zeta[c] = imp ? ze : 0.0;
+  }
+  __syncthreads();
+  STAMP(31);
+  // batch 1
+  {
+    double X[5] = {0, 0, 0, 0, 0};
+    if (lane < n) {
+      X[0] = s[L.gv + lane];
+      double a1 = 0, a2 = 0, a3 = 0, a4 = 0;
+      for (int c = 0; c < nc; c++) {
+        const double ae = AcubE[lane * nc + c], ac = Ac[lane * nc + c];
+        a1 += ae * P.fc[c];
+        a2 += ae * P.xq[c];
+        a3 += ac * P.r1[c];
+        a4 += ac * P.zeta[c];
+      }
+      X[1] = a1; X[2] = a2; X[3] = a3; X[4] = a4;
+    }
+    cholSolveReg<5>(Lm, dinv, X, n, lane);
+    if (lane < n) {
+      double* nv = P.NV + lane * NV_COLS;
+      const double d = X[1] / dt;
+      nv[NV_W] = X[0];
+      nv[NV_DELTA] = d;
+      nv[NV_SIGMA] = X[2];
+      nv[NV_MA1] = X[3];
+      nv[NV_MA2] = X[4];
+      s[L.w + lane] = X[0];
+      s[L.x + lane] = sn[snYf(n) + lane] + d;
+    }
+  }
+  __syncthreads();
+  // u = A_c_ub_E^T w ; lambda = P^T u ; beta ; rho = P lambda ; pi = u - Q^T lambda
   for (int c = lane; c < nc; c += WAVE) {
     double acc = 0;
     for (int i = 0; i < n; i++) acc += AcubE[i * nc + c] * s[L.w + i];
     P.u[c] = acc;
   }
   __syncthreads();
-  // lambda = P^T u ; x = P b ; beta
   for (int c = lane; c < nc; c += WAVE) {
-    double l = 0, xx = 0;
-    for (int r = 0; r < nc; r++) {
-      l += PT[c * nc + r] * P.u[r];
-      xx += PT[r * nc + c] * P.bc[r];
-    }
+    double l = 0;
+    for (int r = 0; r < nc; r++) l += PT[c * nc + r] * P.u[r];
     P.lam[c] = l;
     P.beta[c] = P.bounce[c] * l;
-    P.xq[c] = xx;
   }
   __syncthreads();
-  if (imp) {
-    for (int c = lane; c < nc; c += WAVE) {
-      double qx = 0, qtl = 0, rh = 0, ze = 0;
+  for (int c = lane; c < nc; c += WAVE) {
+    double qtl = 0, rh = 0;
+    if (imp)
       for (int k = 0; k < nc; k++) {
-        qx += Q[c * nc + k] * P.xq[k];
         qtl += Q[k * nc + c] * P.lam[k];
-        rh += PT[k * nc + c] * P.lam[k];   // (P lambda)_c
-        ze += PT[c * nc + k] * P.xq[k];    // (P^T x)_c
+        rh += PT[k * nc + c] * P.lam[k];
       }
-      P.r1[c] = P.bc[c] - qx;
-      P.piv[c] = P.u[c] - qtl;
-      P.rho[c] = rh;
-      P.zeta[c] = ze;
-    }
-  } else {
-    for (int c = lane; c < nc; c += WAVE) { P.r1[c] = 0; P.piv[c] = 0; P.rho[c] = 0; P.zeta[c] = 0; }
+    P.piv[c] = imp ? P.u[c] - qtl : 0.0;
+    P.rho[c] = imp ? rh : 0.0;
   }
   __syncthreads();
   STAMP(35);
-  // mu = A_c beta ; nu = Minv A_c beta ; sigma = MA x ; kappa = Minv A_c lambda ; the
-  // pseudo-inverse branch vectors; w - nu
-  for (int i = lane; i < n; i += WAVE) {
-    double mu = 0, nu = 0, sg = 0, kp = 0, a1 = 0, ar = 0, a2 = 0, ap = 0;
-    for (int c = 0; c < nc; c++) {
-      const double ac = Ac[i * nc + c], mac = MAc[i * nc + c], ma = MA[i * nc + c];
-      mu += ac * P.beta[c];
-      nu += mac * P.beta[c];
-      sg += ma * P.xq[c];
-      kp += mac * P.lam[c];
-      a1 += mac * P.r1[c];
-      ar += ma * P.rho[c];
-      a2 += mac * P.zeta[c];
-      ap += ma * P.piv[c];
+  // batch 2
+  {
+    double X[4] = {0, 0, 0, 0};
+    double mu = 0;
+    if (lane < n) {
+      double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+      for (int c = 0; c < nc; c++) {
+        const double ae = AcubE[lane * nc + c], ac = Ac[lane * nc + c];
+        a0 += ac * P.beta[c];
+        a1 += ac * P.lam[c];
+        a2 += ae * P.rho[c];
+        a3 += ae * P.piv[c];
+      }
+      X[0] = a0; X[1] = a1; X[2] = a2; X[3] = a3;
+      mu = a0;
     }
-    double* nv = P.NV + i * NV_COLS;
-    nv[NV_MU] = mu;
-    nv[NV_NU] = nu;
-    nv[NV_SIGMA] = sg;
-    nv[NV_KAPPA] = kp;
-    nv[NV_MA1] = a1;
-    nv[NV_MARHO] = ar;
-    nv[NV_MA2] = a2;
-    nv[NV_MAPI] = ap;
-    const double w2 = nv[NV_W] - nu;
-    nv[NV_W2] = w2;
-    s[L.w + i] = w2;
+    cholSolveReg<4>(Lm, dinv, X, n, lane);
+    if (lane < n) {
+      double* nv = P.NV + lane * NV_COLS;
+      nv[NV_MU] = mu;
+      nv[NV_NU] = X[0];
+      nv[NV_KAPPA] = X[1];
+      nv[NV_MARHO] = X[2];
+      nv[NV_MAPI] = X[3];
+      const double w2 = nv[NV_W] - X[0];
+      nv[NV_W2] = w2;
+      s[L.w + lane] = w2;
+    }
   }
   __syncthreads();
   STAMP(37);

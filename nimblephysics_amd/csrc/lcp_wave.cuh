@@ -16,29 +16,43 @@
 #define LCP_INF __builtin_inf()
 
 // ---------------------------------------------------------------------------
+// Residual form: lane j keeps r_j = b_j - sum_k A_jk x_k; a sweep step on
+// row i needs only r_i + A_ii x_i (= b_i - sum_{k!=i} A_ik x_k) on lane i,
+// then every lane applies r_j -= A_ji * dx_i.  No cross-lane reduction on the
+// critical path (the reference recomputes the row sum; results agree to
+// rounding).
 __device__ bool wavePgs(int n, double* A, double& x, double b, double lo, double hi, int findex, int lane) {
   const double deltaXThr = 1e-6, relTol = 1e-3, epsDiv = 1e-9;
   const bool act = lane < n;
+  double diag = act ? A[lane * n + lane] : 1.0;
+  const unsigned long long order = __ballot(act && diag >= epsDiv);
+  double xF = __shfl(x, findex >= 0 ? findex : 0);
+  double r = act ? b : 0.0;
+  for (int k = 0; k < n; k++) {
+    const double xk = rdl(x, k);
+    if (act) r -= A[lane * n + k] * xk;
+  }
   bool possible = true;
-  const unsigned long long order = __ballot(act && A[lane * n + lane] >= epsDiv);
-  const double xf0 = 0.0;
-  (void)xf0;
+  double col = act ? A[lane * n] : 0.0;  // column 0 prefetched
   for (int i = 0; i < n; i++) {
+    const double cur = col;
+    if (i + 1 < n) col = act ? A[lane * n + i + 1] : 0.0;
+    double nx;
+    bool moved = false;
     if (!((order >> i) & 1ull)) {
-      if (lane == i) x = 0.0;
-      continue;
+      nx = 0.0;
+    } else {
+      nx = (r + diag * x) / diag;
+      const double h = findex >= 0 ? hi * xF : hi, l = findex >= 0 ? -h : lo;
+      nx = nx > h ? h : (nx < l ? l : nx);
+      moved = lane == i && fabs(nx - x) > deltaXThr;
     }
-    const double Aii = A[i * n + i];
-    const double old = rdl(x, i);
-    const double part = (act && lane != i) ? A[i * n + lane] * x : 0.0;
-    double nx = (rdl(b, i) - waveSum(part)) / Aii;
-    const int fi = rdli(findex, i);
-    double h, l;
-    if (fi >= 0) { h = rdl(hi, i) * rdl(x, fi); l = -h; }
-    else { h = rdl(hi, i); l = rdl(lo, i); }
-    nx = nx > h ? h : (nx < l ? l : nx);
-    if (lane == i) x = nx;
-    if (possible && fabs(nx - old) > deltaXThr) possible = false;
+    const double dx = rdl(nx - x, i);
+    const double nxi = rdl(nx, i);
+    if (lane == i) x = nxi;
+    if (findex == i) xF = nxi;
+    if (act) r -= cur * dx;
+    if (__ballot(moved)) possible = false;
   }
   if (possible) return true;
   for (int idx = 0; idx < n; idx++) {
@@ -46,25 +60,27 @@ __device__ bool wavePgs(int n, double* A, double& x, double b, double lo, double
     const double dummy = 1.0 / A[idx * n + idx];
     __syncthreads();
     if (act) A[idx * n + lane] *= dummy;
-    if (lane == idx) b *= dummy;
+    if (lane == idx) { b *= dummy; r *= dummy; }
     __syncthreads();
   }
+  diag = act ? A[lane * n + lane] : 1.0;
   for (int iter = 1; iter < 30; iter++) {
     possible = true;
+    col = act ? A[lane * n] : 0.0;
     for (int idx = 0; idx < n; idx++) {
+      const double cur = col;
+      if (idx + 1 < n) col = act ? A[lane * n + idx + 1] : 0.0;
       if (!((order >> idx) & 1ull)) continue;
-      const double old = rdl(x, idx);
-      const double part = (act && lane != idx) ? A[idx * n + lane] * x : 0.0;
-      double nx = rdl(b, idx) - waveSum(part);
-      const int fi = rdli(findex, idx);
-      double h, l;
-      if (fi >= 0) { h = rdl(hi, idx) * rdl(x, fi); l = -h; }
-      else { h = rdl(hi, idx); l = rdl(lo, idx); }
+      double nx = r + diag * x;
+      const double h = findex >= 0 ? hi * xF : hi, l = findex >= 0 ? -h : lo;
       nx = nx > h ? h : (nx < l ? l : nx);
-      if (lane == idx) x = nx;
-      if (possible && fabs(nx) > epsDiv) {
-        if (fabs((nx - old) / nx) > relTol) possible = false;
-      }
+      const bool moved = lane == idx && fabs(nx) > epsDiv && fabs((nx - x) / nx) > relTol;
+      const double dx = rdl(nx - x, idx);
+      const double nxi = rdl(nx, idx);
+      if (lane == idx) x = nxi;
+      if (findex == idx) xF = nxi;
+      if (act) r -= cur * dx;
+      if (__ballot(moved)) possible = false;
     }
     if (possible) break;
   }

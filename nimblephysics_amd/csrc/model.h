@@ -50,6 +50,6 @@ struct Layout {
   // backward extras
   int B1, B23, B4, P, H, w, gp, gv, out;
   // contacts: stage header/lists, post-dynamics velocity, LCP workspace pool
-  int ct, v1, pool, poolCap;
+  int ct, v1, pool, poolCap, dinv;
   int total;
 };

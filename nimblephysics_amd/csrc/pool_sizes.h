@@ -46,9 +46,7 @@ __host__ __device__ inline int snYf(int n) { return SN_VF + n; }
 // gv-independent backward data, n x nc (leading dimension nc) / nc x nc
 __host__ __device__ inline int snAc(int n) { return snAlign8(snYf(n) + n); }
 __host__ __device__ inline int snAcubE(int n) { return snAc(n) + n * SN_MAXL; }
-__host__ __device__ inline int snMA(int n) { return snAcubE(n) + n * SN_MAXL; }     // Minv A_c_ub_E
-__host__ __device__ inline int snMAc(int n) { return snMA(n) + n * SN_MAXL; }       // Minv A_c
-__host__ __device__ inline int snPT(int n) { return snMAc(n) + n * SN_MAXL; }       // pinv(Q)^T
+__host__ __device__ inline int snPT(int n) { return snAcubE(n) + n * SN_MAXL; }     // pinv(Q)^T
 __host__ __device__ inline int snQ(int n) { return snPT(n) + SN_MAXL * SN_MAXL; }   // Q
 __host__ __device__ inline int snapWorkspaceOffset(int n) { return snAlign8(snQ(n) + SN_MAXL * SN_MAXL); }
 // 64 doubles at the very end of every snapshot are kept for debug stamps

@@ -214,7 +214,7 @@ __device__ void massMatrixAndBias(const ModelDev& md, double* s, const Layout& L
 // left-looking (Crout) with one lane per row, one barrier per column.  The
 // per-element subtraction order (k ascending) is that of the right-looking
 // factorisation.
-__device__ void cholesky(double* A, int n, int lane) {
+__device__ void cholesky(double* A, double* dinv, int n, int lane) {
   for (int j = 0; j < n; j++) {
     double sum = 0.0;
     if (lane >= j && lane < n) {
@@ -224,7 +224,7 @@ __device__ void cholesky(double* A, int n, int lane) {
       for (int k = 0; k < j; k++) sum -= A[ri + k] * A[rj + k];
     }
     const double djj = sqrt(rdl(sum, j));
-    if (lane == j) A[tri(j, j)] = djj;
+    if (lane == j) { A[tri(j, j)] = djj; dinv[j] = 1.0 / djj; }
     else if (lane > j && lane < n) A[tri(lane, j)] = sum / djj;
     __syncthreads();
   }
@@ -232,20 +232,38 @@ __device__ void cholesky(double* A, int n, int lane) {
 
 // Solve L L^T x = b in place (x = b on entry): x held one entry per lane,
 // no barriers inside.
-__device__ void cholSolve(const double* Lm, double* x, int n, int lane) {
-  double xi = lane < n ? x[lane] : 0.0;
+// K right-hand sides at once, held in registers (row i on lane i): the K
+// independent dependency chains interleave.  dinv[k] = 1 / L_kk.
+template <int K>
+__device__ __forceinline__ void cholSolveReg(const double* Lm, const double* dinv, double (&x)[K], int n, int lane) {
   for (int k = 0; k < n; k++) {
-    const double xk = rdl(xi, k) / Lm[tri(k, k)];
-    if (lane == k) xi = xk;
-    else if (lane > k && lane < n) xi -= Lm[tri(lane, k)] * xk;
+    const double dk = dinv[k];
+    const double lk = (lane > k && lane < n) ? Lm[tri(lane, k)] : 0.0;
+#pragma unroll
+    for (int q = 0; q < K; q++) {
+      const double xk = rdl(x[q], k) * dk;
+      if (lane == k) x[q] = xk;
+      else if (lane > k) x[q] -= lk * xk;
+    }
   }
   for (int k = n - 1; k >= 0; k--) {
-    const double xk = rdl(xi, k) / Lm[tri(k, k)];
-    if (lane == k) xi = xk;
-    else if (lane < k) xi -= Lm[tri(k, lane)] * xk;
+    const double dk = dinv[k];
+    const double lk = lane < k ? Lm[tri(k, lane)] : 0.0;
+#pragma unroll
+    for (int q = 0; q < K; q++) {
+      const double xk = rdl(x[q], k) * dk;
+      if (lane == k) x[q] = xk;
+      else if (lane < k) x[q] -= lk * xk;
+    }
   }
+}
+
+// Solve L L^T x = b in place (x = b on entry, LDS).
+__device__ void cholSolve(const double* Lm, const double* dinv, double* x, int n, int lane) {
+  double xr[1] = {lane < n ? x[lane] : 0.0};
+  cholSolveReg<1>(Lm, dinv, xr, n, lane);
   __syncthreads();
-  if (lane < n) x[lane] = xi;
+  if (lane < n) x[lane] = xr[0];
   __syncthreads();
 }
 
@@ -267,7 +285,7 @@ __device__ void coreDynamics(const ModelDev& md, double* s, const Layout& L, int
   kinematics(md, s, L, lane, nullptr);
   composites(md, s, L, lane);
   massMatrixAndBias(md, s, L, lane, s + L.rhs);
-  cholesky(s + L.M, md.n, lane);
+  cholesky(s + L.M, s + L.dinv, md.n, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -295,7 +313,7 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, con
     STAMP(15);
     massMatrixAndBias(md, s, L, lane, s + L.rhs);
     STAMP(16);
-    cholesky(s + L.M, md.n, lane);
+    cholesky(s + L.M, s + L.dinv, md.n, lane);
     STAMP(11);
     // rhs = tau + spring + damping - C   (GenericJoint::updateTotalForceDynamic)
     double* x = s + L.x;
@@ -306,7 +324,7 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, con
       x[i] = s[L.tau + i] + springF + dampF - s[L.rhs + i];
     }
     __syncthreads();
-    cholSolve(s + L.M, x, n, lane);  // x = ddq
+    cholSolve(s + L.M, s + L.dinv, x, n, lane);  // x = ddq
     // integrateVelocities (Skeleton.cpp:9329): v1 = v + dt ddq
     double* v1 = s + L.v1;
     for (int i = lane; i < n; i += WAVE) v1[i] = s[L.v + i] + md.dt * x[i];
@@ -501,8 +519,8 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
         w[i] = s[L.gv + i];
       }
       __syncthreads();
-      cholSolve(s + L.M, x, n, lane);  // x = y = Minv z  => a* = y / dt
-      cholSolve(s + L.M, w, n, lane);  // w = Minv gv
+      cholSolve(s + L.M, s + L.dinv, x, n, lane);  // x = y = Minv z  => a* = y / dt
+      cholSolve(s + L.M, s + L.dinv, w, n, lane);  // w = Minv gv
       for (int i = lane; i < n; i += WAVE) x[i] /= dt;
       __syncthreads();
     }

@@ -22,16 +22,19 @@ nxt = torch.empty_like(state)
 s = torch.cuda.current_stream().cuda_stream
 n = w.getNumDofs()
 a8 = lambda x: ((x + 7) // 8) * 8
-ws = a8(a8(800 + 2 * n) + 4 * n * 48 + 2 * 2304) + 1000  # snapWorkspaceOffset(n) + 1000
+ws = a8(a8(800 + 2 * n) + 2 * n * 48 + 2 * 2304) + 1000  # snapWorkspaceOffset(n) + 1000
 for it in range(4):
-    snap[:, ws:ws + 20] = 0
+    snap[:, ws:ws + 60] = 0
     dev.forward(state, action, cache, nxt, snap, s)
     torch.cuda.synchronize()
     state = nxt.clone()
-    T = snap[:, ws:ws + 20].cpu().numpy()
+    T = snap[:, ws:ws + 60].cpu().numpy()
     hd = snap[:, :8].cpu().numpy()
     names = {(10, 14): " kinematics", (14, 15): " composites", (15, 16): " CRBA + bias", (16, 11): " cholesky",
-             (10, 11): "load+coreDynamics", (11, 12): "solve v1", (0, 1): "collide", (1, 2): "rows",
+             (10, 11): "load+coreDynamics", (40, 41): " c1: Q build", (41, 42): " c1: COD factor",
+             (42, 43): " c1: COD solve", (43, 44): " c1: nx + valid", (45, 46): " pre: Ac/AcubE",
+             (46, 47): " pre: MA/MAc backsub", (47, 48): " pre: Q", (48, 49): " pre: COD", (49, 50): " pre: pinv",
+             (50, 51): " pre: imp", (11, 12): "solve v1", (0, 1): "collide", (1, 2): "rows",
              (2, 3): "cols/massed/A/b", (3, 4): "warm start/guess", (4, 5): "construct 1",
              (5, 6): "dantzig", (6, 7): "pgs/fallbacks", (7, 8): "construct 2", (8, 9): "impulses/snapshot",
              (12, 13): "contact stage total+integrate"}

@@ -226,6 +226,9 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
   } else {
     w->snapDoubles = 8;
   }
+  // dynamics cache at the tail of every snapshot
+  w->fwd.snDyn = w->bwd.snDyn = w->snapDoubles;
+  w->snapDoubles += dynCacheDoubles(m.n, m.nb);
   hipError_t e = hipMalloc(&w->dev, sizeof(ModelDev));
   if (e != hipSuccess) { delete w; return fail(NIMBLE_ERR_HIP, std::string("hipMalloc: ") + hipGetErrorString(e)); }
   e = hipMemcpy(w->dev, &m, sizeof(ModelDev), hipMemcpyHostToDevice);

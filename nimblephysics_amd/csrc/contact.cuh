@@ -1381,60 +1381,116 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
   return imp;
 }
 
-// sum_j (G_j^T g_j)[k] for the lane's direction k with position generator Z.
-__device__ double contactGTerms(const ModelDev& md, const double* s, const Layout& L, const double* sn,
-                                const BwdPool& P, int m, int k, const double* Z, int* status) {
-  const int n = md.n;
-  const int bk = md.dofBody[k];
-  const int lam = md.parent[bk];
+// sum_j (G_j^T g_j)[k] for every direction k (lane k, position generator Z),
+// G_j = d(J^T e_j)/dq (DifferentiableContactConstraint.cpp:1654), grouped by
+// contact body c instead of by row:
+//   screw-axis part  (Z x Y_j).wr_j = Z.(Y_j x* wr_j) summed over the rows of
+//     c gives Z.(P^c_c - P^c_lambda(k)) with P^c_b = sum over the ancestor
+//     dofs r of b of S_r x* omega^c_r, omega^c_r = sum_j s_j g_j[r] wr_j
+//     (s_j = +1 when c is the row's body A, -1 for body B);
+//   vertex side      (T_A - T_B).[dp x d; 0] with dp = Z_w x p + Z_v gives
+//     Z_w.V^c + Z_v.U^c, U^c = sum_j d_j x Tw_j, V^c = sum_j p_j x (d_j x Tw_j)
+//     (the Z_w term only when |Z_w| > 1e-6, DifferentiableContactConstraint.cpp:328);
+//   face side        per row (tangent-basis gradient, ContactConstraint.cpp:772).
+// `ws` is workspace of 6 n + 6 nb + 16 doubles.  Returns the lane's sum.
+__device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& L, const double* sn,
+                                   const BwdPool& P, int m, const double* Z, double* ws, int lane) {
+  const int n = md.n, nb = md.nb;
   const double* rows = sn + SN_ROWS;
+  double* omega = ws;            // n x 6
+  double* Pc = ws + 6 * n;       // nb x 6
+  double* UV = Pc + 6 * nb;      // 6 (+ group body)
+  const int k = lane;
+  const int bk = k < n ? md.dofBody[k] : 0;
+  const int lam = k < n ? md.parent[bk] : -1;
   double acc = 0.0;
-  for (int j = 0; j < m; j++) {
-    const double* rr = rows + j * SN_ROWREC;
-    if ((int)rr[RR_MAP] == CM_NOT_CLAMPING) continue;
-    const double* rec = sn + SN_CONTACTS + (int)rr[RR_CONTACT] * CREC;
-    const int A = (int)rec[8], B = (int)rec[9];
-    const bool inA = (md.anc[A] >> bk) & 1ull;
-    const bool inB = (md.anc[B] >> bk) & 1ull;
-    if (!inA && !inB) continue;
-    const double* p = rec;
-    const double* d = rr + RR_D;
-    double wr[6];
-    cross3(p, d, wr);
-    wr[3] = d[0]; wr[4] = d[1]; wr[5] = d[2];
-    // screw-axis gradient part: (Z x Y) . wr
-    const double* g = P.gRows + j * n;
-    double Tl[6];
-    bodyTwist(md, s + L.Sw, lam, g, 1, Tl);
-    double Y[6];
-    for (int i = 0; i < 6; i++) {
-      double y = 0.0;
-      if (inA) y += P.TAB[j * 12 + i] - Tl[i];
-      if (inB) y -= P.TAB[j * 12 + 6 + i] - Tl[i];
-      Y[i] = y;
-    }
-    double zy[6];
-    crm(Z, Y, zy);
-    acc += dot6(zy, wr);
-    // contact-geometry part: (T_A - T_B) . d(wrench)/dq_k
-    if (inA && inB) { *status |= 1; continue; }
-    const int type = (int)rec[7];
-    int kind = 0;  // 1 vertex, 2 face
-    if (type == CT_VERTEX_FACE) kind = inA ? 1 : 2;
-    else if (type == CT_FACE_VERTEX) kind = inA ? 2 : 1;
-    else { *status |= 2; continue; }
-    double dp[3] = {0, 0, 0}, dd[3] = {0, 0, 0};
-    const double wv[3] = {Z[0], Z[1], Z[2]}, vv[3] = {Z[3], Z[4], Z[5]};
-    if (kind == 1) {
-      if (sqrt(dot3(wv, wv)) > 1e-6) {
-        cross3(wv, p, dp);
-        for (int i = 0; i < 3; i++) dp[i] += vv[i];
-      } else {
-        for (int i = 0; i < 3; i++) dp[i] = vv[i];
+  unsigned long long done = 0ull;  // bodies already processed
+  for (int j0 = 0; j0 < m; j0++) {
+    const double* r0 = rows + j0 * SN_ROWREC;
+    if ((int)r0[RR_MAP] == CM_NOT_CLAMPING) continue;
+    const double* rec0 = sn + SN_CONTACTS + (int)r0[RR_CONTACT] * CREC;
+    for (int side = 0; side < 2; side++) {
+      const int c = (int)rec0[8 + side];
+      if ((done >> c) & 1ull) continue;
+      done |= 1ull << c;
+      // omega^c_r (lane r), vertex sums (lanes over rows), all for body c
+      double om[6] = {0, 0, 0, 0, 0, 0};
+      double uv[6] = {0, 0, 0, 0, 0, 0};
+      for (int j = 0; j < m; j++) {
+        const double* rr = rows + j * SN_ROWREC;
+        if ((int)rr[RR_MAP] == CM_NOT_CLAMPING) continue;
+        const double* rec = sn + SN_CONTACTS + (int)rr[RR_CONTACT] * CREC;
+        const int A = (int)rec[8], B = (int)rec[9];
+        if (A != c && B != c) continue;
+        const double sg = A == c ? 1.0 : -1.0;
+        const double* p = rec;
+        const double* d = rr + RR_D;
+        double wr[6];
+        cross3(p, d, wr);
+        wr[3] = d[0]; wr[4] = d[1]; wr[5] = d[2];
+        if (lane < n) {
+          const double gr = sg * P.gRows[j * n + lane];
+#pragma unroll
+          for (int i = 0; i < 6; i++) om[i] = fma(gr, wr[i], om[i]);
+        }
+        // vertex side of this row?
+        const int type = (int)rec[7];
+        const bool vertexSide = (type == CT_VERTEX_FACE && A == c) || (type == CT_FACE_VERTEX && B == c);
+        if (vertexSide && lane == 0) {
+          double tw[3], dxt[3], pxd[3];
+          for (int i = 0; i < 3; i++) tw[i] = P.TAB[j * 12 + i] - P.TAB[j * 12 + 6 + i];
+          cross3(d, tw, dxt);
+          cross3(p, dxt, pxd);
+          for (int i = 0; i < 3; i++) { uv[i] += dxt[i]; uv[3 + i] += pxd[i]; }
+        }
       }
-    } else {
+      if (lane < n)
+        for (int i = 0; i < 6; i++) omega[lane * 6 + i] = om[i];
+      if (lane == 0)
+        for (int i = 0; i < 6; i++) UV[i] = uv[i];
+      __syncthreads();
+      // P^c_b = sum over ancestor dofs r of b of S_r x* omega_r
+      if (lane < nb) {
+        double pb[6] = {0, 0, 0, 0, 0, 0};
+        const unsigned long long an = md.anc[lane];
+        for (int r = 0; r < n; r++) {
+          if (!((an >> md.dofBody[r]) & 1ull)) continue;
+          double t[6];
+          crf(s + L.Sw + 6 * r, omega + 6 * r, t);
+#pragma unroll
+          for (int i = 0; i < 6; i++) pb[i] += t[i];
+        }
+        for (int i = 0; i < 6; i++) Pc[lane * 6 + i] = pb[i];
+      }
+      __syncthreads();
+      if (k < n && ((md.anc[c] >> bk) & 1ull)) {
+        double y[6];
+        for (int i = 0; i < 6; i++) y[i] = Pc[c * 6 + i] - (lam >= 0 ? Pc[lam * 6 + i] : 0.0);
+        acc += dot6(Z, y);
+        const double zw = sqrt(Z[0] * Z[0] + Z[1] * Z[1] + Z[2] * Z[2]);
+        if (zw > 1e-6) acc += Z[0] * UV[3] + Z[1] * UV[4] + Z[2] * UV[5];
+        acc += Z[3] * UV[0] + Z[4] * UV[1] + Z[5] * UV[2];
+      }
+      __syncthreads();
+    }
+  }
+  // face side: per row
+  if (k < n) {
+    for (int j = 0; j < m; j++) {
+      const double* rr = rows + j * SN_ROWREC;
+      if ((int)rr[RR_MAP] == CM_NOT_CLAMPING) continue;
+      const double* rec = sn + SN_CONTACTS + (int)rr[RR_CONTACT] * CREC;
+      const int A = (int)rec[8], B = (int)rec[9], type = (int)rec[7];
+      int faceBody = -1;
+      if (type == CT_VERTEX_FACE) faceBody = B;
+      else if (type == CT_FACE_VERTEX) faceBody = A;
+      if (faceBody < 0 || !((md.anc[faceBody] >> bk) & 1ull)) continue;
+      const double* p = rec;
+      const double* d = rr + RR_D;
       double dn[3];
+      const double wv[3] = {Z[0], Z[1], Z[2]};
       cross3(wv, rec + 3, dn);
+      double dd[3];
       const int dirIdx = (int)rr[RR_DIR];
       if (dirIdx == 0 || dot3(dn, dn) <= 1e-12) {
         for (int i = 0; i < 3; i++) dd[i] = dn[i];
@@ -1443,14 +1499,15 @@ __device__ double contactGTerms(const ModelDev& md, const double* s, const Layou
         tangentBasisGradient(rec + 3, dn, T0, T1);
         for (int i = 0; i < 3; i++) dd[i] = dirIdx == 1 ? T0[i] : T1[i];
       }
+      double pxdd[3];
+      cross3(p, dd, pxdd);
+      (void)d;
+      double v = 0.0;
+      for (int i = 0; i < 3; i++)
+        v += (P.TAB[j * 12 + i] - P.TAB[j * 12 + 6 + i]) * pxdd[i] +
+             (P.TAB[j * 12 + 3 + i] - P.TAB[j * 12 + 9 + i]) * dd[i];
+      acc += v;
     }
-    double dwr[6], t1[3], t2[3];
-    cross3(p, dd, t1);
-    cross3(dp, d, t2);
-    for (int i = 0; i < 3; i++) { dwr[i] = t1[i] + t2[i]; dwr[3 + i] = dd[i]; }
-    double tab[6];
-    for (int i = 0; i < 6; i++) tab[i] = P.TAB[j * 12 + i] - P.TAB[j * 12 + 6 + i];
-    acc += dot6(tab, dwr);
   }
   return acc;
 }

@@ -51,5 +51,7 @@ struct Layout {
   int B1, B23, B4, P, H, w, gp, gv, out;
   // contacts: stage header/lists, post-dynamics velocity, LCP workspace pool
   int ct, v1, pool, poolCap, dinv;
+  // offset (doubles) of the dynamics cache inside each world's snapshot
+  int snDyn;
   int total;
 };

@@ -280,6 +280,49 @@ __device__ void loadState(const ModelDev& md, double* s, const Layout& L, int la
 
 #include "contact.cuh"
 
+// Dynamics cache <-> LDS (Layout regions Tw, Sw, V, IC, M, dinv, rhs).
+__device__ void dynCacheCopy(const ModelDev& md, double* s, const Layout& L, double* cache, bool store, int lane) {
+  const int n = md.n, nb = md.nb;
+  const int seg[7][2] = {{L.Tw, 12 * nb}, {L.Sw, 6 * n}, {L.V, 6 * nb}, {L.IC, 36 * nb},
+                         {L.M, n * (n + 1) / 2}, {L.dinv, n}, {L.rhs, n}};
+  int o = 0;
+  for (int k = 0; k < 7; k++) {
+    const int base = seg[k][0], cnt = seg[k][1];
+    if (store)
+      for (int t = lane; t < cnt; t += WAVE) cache[o + t] = s[base + t];
+    else
+      for (int t = lane; t < cnt; t += WAVE) s[base + t] = cache[o + t];
+    o += cnt;
+  }
+  __syncthreads();
+}
+
+// Accelerations only (phase 5 of kinematics) for given ddq, with Tw, Sw, V
+// already in LDS.
+__device__ void accelerations(const ModelDev& md, double* s, const Layout& L, int lane, const double* ddq) {
+  const double* v = s + L.v;
+  if (lane < md.nb) {
+    const int b = lane;
+    double A[6] = {0, 0, 0, 0, 0, 0};
+    const unsigned long long an = md.anc[b];
+#pragma unroll 4
+    for (int j = 0; j < md.n; j++) {
+      const int bj = md.dofBody[j];
+      if (!((an >> bj) & 1ull)) continue;
+      const double* S = s + L.Sw + 6 * j;
+      double sv[6], cr[6];
+#pragma unroll
+      for (int i = 0; i < 6; i++) sv[i] = S[i] * v[j];
+      crm(s + L.V + 6 * bj, sv, cr);
+#pragma unroll
+      for (int i = 0; i < 6; i++) A[i] += fma(S[i], ddq[j], cr[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++) s[L.A + 6 * b + i] = A[i];
+  }
+  __syncthreads();
+}
+
 // Everything up to the factored mass matrix; leaves C in s[L.rhs].
 __device__ void coreDynamics(const ModelDev& md, double* s, const Layout& L, int lane) {
   kinematics(md, s, L, lane, nullptr);
@@ -314,6 +357,7 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, con
     massMatrixAndBias(md, s, L, lane, s + L.rhs);
     STAMP(16);
     cholesky(s + L.M, s + L.dinv, md.n, lane);
+    dynCacheCopy(md, s, L, snapshot + (size_t)env * snapDoubles + L.snDyn, true, lane);
     STAMP(11);
     // rhs = tau + spring + damping - C   (GenericJoint::updateTotalForceDynamic)
     double* x = s + L.x;
@@ -495,9 +539,9 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
       s[L.gp + i] = gN[i];
       s[L.gv + i] = gN[n + i];
     }
-    coreDynamics(md, s, L, lane);
-    STAMP(21);
     double* sn = snapshot + (size_t)env * snapDoubles;
+    dynCacheCopy(md, s, L, sn + L.snDyn, false, lane);  // the forward's kinematics, IC, L, C
+    STAMP(21);
     const int nc = md.numPairs > 0 ? (int)sn[SN_NC] : 0;
     const int m = md.numPairs > 0 ? (int)sn[SN_M] : 0;
     double* x = s + L.x;
@@ -525,7 +569,7 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
       __syncthreads();
     }
     STAMP(22);
-    kinematics(md, s, L, lane, x);  // A = accelerations at a*
+    accelerations(md, s, L, lane, x);  // A = accelerations at a*
     derivativeComposites(md, s, L, lane);
     STAMP(23);
 
@@ -614,13 +658,15 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
     __syncthreads();
     STAMP(24);
     if (nc > 0) {
-      // B1/B23/B4 are dead now: reuse them for the M-derivative fields
+      // B1/B23/B4 are dead now: workspace for the contact-geometry terms,
+      // then for the M-derivative fields
       double* buf = s + L.B1;
+      const double gterm = contactGTermsAll(md, s, L, sn, P, m, Z, buf, lane);
+      __syncthreads();
       mFieldsBuild(md, s, L, P.NV, buf, lane);
       if (k < n) {
-        int status = 0;
+        gq += gterm;
         gq += mFieldsEval(md, buf, k, Z, -dt, (double)imp);
-        gq += contactGTerms(md, s, L, sn, P, m, k, Z, &status);
       }
       __syncthreads();
     }

@@ -279,7 +279,7 @@ __device__ inline void carveFwd(double* base, int m, int n, FwdPool& P) {
   P.massed = P.cols;  // Y = L^-1 J^T overwrites J^T in place
   P.A = p; p += m * m;
   P.M1 = p; p += m * m;
-  P.M2 = p; p += m * m;
+  P.M2 = p; p += m * (m | 1);  // Dantzig's L with an odd leading dimension
   double** vecs[] = {&P.lo, &P.hi, &P.b, &P.X, &P.aCol, &P.rest, &P.pen, &P.relVel, &P.fc, &P.Eval, &P.nx, &P.fsol, &P.xc};
   for (double** v : vecs) { *v = p; p += m; }
   P.dvec = p; p += 3 * m;

@@ -20,29 +20,31 @@
 // row i needs only r_i + A_ii x_i (= b_i - sum_{k!=i} A_ik x_k) on lane i,
 // then every lane applies r_j -= A_ji * dx_i.  No cross-lane reduction on the
 // critical path (the reference recomputes the row sum; results agree to
-// rounding).
-__device__ bool wavePgs(int n, double* A, double& x, double b, double lo, double hi, int findex, int lane) {
+// rounding).  A is symmetric and read by rows (conflict-free LDS access);
+// the reference's in-place row scaling (1/A_jj) is applied lane-locally,
+// A_ji / A_jj = A_ij * dummy_j, so A is never written.
+__device__ bool wavePgs(int n, const double* A, double& x, double b, double lo, double hi, int findex, int lane) {
   const double deltaXThr = 1e-6, relTol = 1e-3, epsDiv = 1e-9;
   const bool act = lane < n;
-  double diag = act ? A[lane * n + lane] : 1.0;
-  const unsigned long long order = __ballot(act && diag >= epsDiv);
+  const double diagRaw = act ? A[lane * n + lane] : 1.0;
+  const unsigned long long order = __ballot(act && diagRaw >= epsDiv);
   double xF = __shfl(x, findex >= 0 ? findex : 0);
   double r = act ? b : 0.0;
   for (int k = 0; k < n; k++) {
     const double xk = rdl(x, k);
-    if (act) r -= A[lane * n + k] * xk;
+    if (act) r -= A[k * n + lane] * xk;
   }
   bool possible = true;
-  double col = act ? A[lane * n] : 0.0;  // column 0 prefetched
+  double row = act ? A[lane] : 0.0;  // row 0 prefetched
   for (int i = 0; i < n; i++) {
-    const double cur = col;
-    if (i + 1 < n) col = act ? A[lane * n + i + 1] : 0.0;
+    const double cur = row;
+    if (i + 1 < n) row = act ? A[(i + 1) * n + lane] : 0.0;
     double nx;
     bool moved = false;
     if (!((order >> i) & 1ull)) {
       nx = 0.0;
     } else {
-      nx = (r + diag * x) / diag;
+      nx = (r + diagRaw * x) / diagRaw;
       const double h = findex >= 0 ? hi * xF : hi, l = findex >= 0 ? -h : lo;
       nx = nx > h ? h : (nx < l ? l : nx);
       moved = lane == i && fabs(nx - x) > deltaXThr;
@@ -55,21 +57,17 @@ __device__ bool wavePgs(int n, double* A, double& x, double b, double lo, double
     if (__ballot(moved)) possible = false;
   }
   if (possible) return true;
-  for (int idx = 0; idx < n; idx++) {
-    if (!((order >> idx) & 1ull)) continue;
-    const double dummy = 1.0 / A[idx * n + idx];
-    __syncthreads();
-    if (act) A[idx * n + lane] *= dummy;
-    if (lane == idx) { b *= dummy; r *= dummy; }
-    __syncthreads();
-  }
-  diag = act ? A[lane * n + lane] : 1.0;
+  // row scaling of the reference, lane-local: A'_jk = A_jk * dummy_j
+  const bool inOrder = act && ((order >> lane) & 1ull);
+  const double dummy = inOrder ? 1.0 / diagRaw : 1.0;
+  if (inOrder) { b *= dummy; r *= dummy; }
+  const double diag = inOrder ? diagRaw * dummy : diagRaw;
   for (int iter = 1; iter < 30; iter++) {
     possible = true;
-    col = act ? A[lane * n] : 0.0;
+    row = act ? A[lane] : 0.0;
     for (int idx = 0; idx < n; idx++) {
-      const double cur = col;
-      if (idx + 1 < n) col = act ? A[lane * n + idx + 1] : 0.0;
+      const double cur = row;
+      if (idx + 1 < n) row = act ? A[(idx + 1) * n + lane] : 0.0;
       if (!((order >> idx) & 1ull)) continue;
       double nx = r + diag * x;
       const double h = findex >= 0 ? hi * xF : hi, l = findex >= 0 ? -h : lo;
@@ -79,7 +77,7 @@ __device__ bool wavePgs(int n, double* A, double& x, double b, double lo, double
       const double nxi = rdl(nx, idx);
       if (lane == idx) x = nxi;
       if (findex == idx) xF = nxi;
-      if (act) r -= cur * dx;
+      if (act) r -= (cur * dummy) * dx;
       if (__ballot(moved)) possible = false;
     }
     if (possible) break;
@@ -94,7 +92,7 @@ __device__ bool waveLcpValid(int m, const double* A, double cfm, double x, doubl
 #pragma unroll 4
   for (int j = 0; j < m; j++) {
     const double xj = rdl(x, j);
-    if (lane < m) v += (A[lane * m + j] + (lane == j ? cfm : 0.0)) * xj;
+    if (lane < m) v += (A[j * m + lane] + (lane == j ? cfm : 0.0)) * xj;  // A symmetric: row j
   }
   const double xf = __shfl(x, fi >= 0 ? fi : 0);
   bool ok = true;
@@ -167,9 +165,9 @@ __device__ double codSolveWave(const Cod& c, double rhs, double* scr, int lane) 
 
 // ---------------------------------------------------------------------------
 struct WaveDantzig {
-  int n, nC, nN, lane;
+  int n, nC, nN, lane, ldL;
   double* A;    // n x n, permuted in place (LDS)
-  double* L;    // n x n (LDS)
+  double* L;    // n x ldL, ldL odd (LDS bank-conflict-free columns)
   double* scr;  // >= n doubles (LDS)
   double x, b, w, lo, hi, d, deltaX, deltaW, Dell, ell;
   int findex, p, C, state;
@@ -206,20 +204,20 @@ struct WaveDantzig {
   __device__ __forceinline__ void solveL1(double& B, int m) {
     for (int k = 0; k < m; k++) {
       const double bk = rdl(B, k);
-      if (lane > k && lane < m) B -= L[lane * n + k] * bk;
+      if (lane > k && lane < m) B -= L[lane * ldL + k] * bk;
     }
   }
   // L^T x = B
   __device__ __forceinline__ void solveL1T(double& B, int m) {
     for (int k = m - 1; k >= 0; k--) {
       const double bk = rdl(B, k);
-      if (lane < k) B -= L[k * n + lane] * bk;
+      if (lane < k) B -= L[k * ldL + lane] * bk;
     }
   }
   __device__ __forceinline__ void transferToC(int i) {
     const double Aii = A[i * n + i];
     if (nC > 0) {
-      if (lane < nC) L[nC * n + lane] = ell;
+      if (lane < nC) L[nC * ldL + lane] = ell;
       const double dd = waveSum(lane < nC ? ell * Dell : 0.0);
       if (lane == nC) d = 1.0 / (Aii - dd);
     } else {
@@ -235,7 +233,7 @@ struct WaveDantzig {
       Dell = lane < nC ? A[i * n + C] : 0.0;
       solveL1(Dell, nC);
       ell = lane < nC ? Dell * d : 0.0;
-      if (lane < nC) L[nC * n + lane] = ell;
+      if (lane < nC) L[nC * ldL + lane] = ell;
       const double dd = waveSum(lane < nC ? ell * Dell : 0.0);
       if (lane == nC) d = 1.0 / (Aii - dd);
     } else {
@@ -272,7 +270,7 @@ struct WaveDantzig {
       const double k2 = W21 * gamma1 * W11 - W21;
       if (j0 >= 1 && j0 < m2) {
         const double Wp = W1;
-        const double el = L[(r + j0) * n + r];
+        const double el = L[(r + j0) * ldL + r];
         W1 = Wp - W11 * el;
         W2 = k1 * Wp + k2 * el;
       }
@@ -292,14 +290,14 @@ struct WaveDantzig {
       if (lane == r + j) d = dee;
       alpha2 = alphanew;
       if (j0 > j && j0 < m2) {
-        double el = L[(r + j0) * n + r + j];
+        double el = L[(r + j0) * ldL + r + j];
         double Wp = W1 - k1 * el;
         el += gamma1 * Wp;
         W1 = Wp;
         Wp = W2 - k2 * el;
         el -= gamma2 * Wp;
         W2 = Wp;
-        L[(r + j0) * n + r + j] = el;
+        L[(r + j0) * ldL + r + j] = el;
       }
     }
   }
@@ -307,19 +305,19 @@ struct WaveDantzig {
     if (r != n2 - 1) {
       if (r == 0) {
         const int C0 = rdli(C, 0);
-        double a = lane < n2 ? -A[C * n + C0] : 0.0;
+        double a = lane < n2 ? -A[C0 * n + C] : 0.0;  // A symmetric
         if (lane == 0) a += 1.0;
         ldltAddTL(0, n2, a);
       } else {
-        const double t = lane < r ? L[r * n + lane] / d : 0.0;
+        const double t = lane < r ? L[r * ldL + lane] / d : 0.0;
         const int Cr = rdli(C, r);
         double a = 0.0;
         double s = 0.0;
         for (int k = 0; k < r; k++) {
           const double tk = rdl(t, k);
-          if (lane >= r && lane < n2) s += L[lane * n + k] * tk;
+          if (lane >= r && lane < n2) s += L[lane * ldL + k] * tk;
         }
-        if (lane >= r && lane < n2) a = s - A[C * n + Cr];
+        if (lane >= r && lane < n2) a = s - A[Cr * n + C];  // A symmetric
         if (lane == r) a += 1.0;
         ldltAddTL(r, n2 - r, a);
       }
@@ -327,10 +325,10 @@ struct WaveDantzig {
     __syncthreads();
     if (r < n2 - 1) {
       if (lane < n2)
-        for (int j = r; j < n2 - 1; j++) L[lane * n + j] = L[lane * n + j + 1];
+        for (int j = r; j < n2 - 1; j++) L[lane * ldL + j] = L[lane * ldL + j + 1];
       __syncthreads();
       if (lane < n2)
-        for (int i = r; i < n2 - 1; i++) L[i * n + lane] = L[(i + 1) * n + lane];
+        for (int i = r; i < n2 - 1; i++) L[i * ldL + lane] = L[(i + 1) * ldL + lane];
       __syncthreads();
       const double dn = shiftDown1(d, lane);
       if (lane >= r && lane < n2 - 1) d = dn;
@@ -372,17 +370,17 @@ struct WaveDantzig {
   }
 };
 
-// A (n x n LDS, destroyed), L (n x n LDS scratch), scr (>= n LDS); problem
+// A (n x n LDS, destroyed), L (n x (n|1) LDS scratch), scr (>= n LDS); problem
 // vectors lane-distributed; returns success and x (lane-distributed).
 __device__ bool waveDantzig(int n, double* A, double* Lbuf, double* scr, double& xOut, double b, double lo, double hi,
                             int findex, int lane) {
   WaveDantzig D;
-  D.n = n; D.nC = 0; D.nN = 0; D.lane = lane;
+  D.n = n; D.nC = 0; D.nN = 0; D.lane = lane; D.ldL = n | 1;
   D.A = A; D.L = Lbuf; D.scr = scr;
   D.x = 0.0; D.b = b; D.w = 0.0; D.lo = lo; D.hi = hi; D.d = 0.0;
   D.deltaX = 0.0; D.deltaW = 0.0; D.Dell = 0.0; D.ell = 0.0;
   D.findex = findex; D.p = lane; D.C = 0; D.state = 0;
-  for (int k = lane; k < n * n; k += 64) Lbuf[k] = 0.0;
+  for (int k = lane; k < n * (n | 1); k += 64) Lbuf[k] = 0.0;
   if (__ballot(lane < n && findex < 0 && lo == -LCP_INF && hi == LCP_INF)) return false;
   {
     int numAtEnd = 0;
@@ -430,7 +428,7 @@ __device__ bool waveDantzig(int n, double* A, double* Lbuf, double* scr, double&
 #pragma unroll 4
           for (int j = 0; j < nC; j++) {
             const double dxj = rdl(D.deltaX, j);
-            if (inN) acc += A[lane * n + j] * dxj;
+            if (inN) acc += A[j * n + lane] * dxj;  // A symmetric: row j
           }
           if (inN) D.deltaW = acc + (dir > 0 ? A[i * n + lane] : -A[i * n + lane]);
         }

@@ -100,31 +100,34 @@ class DeviceWorld:
 
 def contact_flop_estimate(world, rows: float, clamping: float) -> dict:
     """Algorithmic fp64 FLOPs per world of the contact stage for `rows` LCP
-    rows of which `clamping` clamp (averages over the batch): forward = J^T
-    columns, m Cholesky solves, A = J Minv J^T, b, the COD solves of the
-    guess + standardisation; backward = A_c / A_c_ub_E, nc solves, Q, pinv(Q)
-    by COD, the vector chain, the G_j^T g_j terms and the M-derivative
-    fields."""
+    rows of which `clamping` clamp (batch averages), FMA = 2.  Forward: J^T
+    columns, Y = L^-1 J^T, A = Y^T Y, b, guess + standardisation COD solves,
+    validity checks, impulses, and the backward precompute (A_c, A_c_ub_E, Q,
+    COD + pinv(Q), rank check).  Backward: the nine Minv products (two batched
+    Cholesky solves), the clamping-space vector chain, per-row G vectors,
+    chain twists, grouped contact-geometry terms and the M-derivative fields.
+    Iterative fallbacks (Dantzig pivots, PGS sweeps) are not counted."""
     d = world.desc_arrays()
     nb, n = int(d["num_bodies"]), int(d["num_dofs"])
     m, c = float(rows), float(clamping)
     if m <= 0:
         return {"forward": 0.0, "backward": 0.0}
     cod = lambda k: 4.0 / 3.0 * k ** 3 + 4.0 * k * k  # noqa: E731
-    fwd = n * m * 14 + m * 2 * n * n + m * m * n + 2 * n * m + m * m * 2 + 2 * cod(m) + 2 * n * m
-    depth = 8.0  # ancestor dofs per contact body (Atlas foot chain incl. root: 12)
-    bwd = (2 * n * c * 14 * 2 + c * 2 * n * n + 2 * c * c * n + cod(c) + c * 4 * c * c + 2 * c * c * c
-           + 24 * n * c + 4 * 2 * n * n + m * n * 16 + n * m * (depth * 12 + 90)
-           + 8 * nb * (n * 12 + 100) + n * 8 * 30)
+    fwd = (14 * n * m + n * n * m + m * m * n + 2 * n * m + 2 * cod(m) + 4 * m * m + 2 * n * m + n * n
+           + 2 * 14 * n * c + 2 * c * c + cod(c) + 4 * c ** 3 + 2 * c ** 3)
+    groups = 2.0
+    bwd = (18 * n * n + 12 * 2 * n * c + 6 * 2 * c * c + 12 * m * n + 24 * m * n
+           + groups * (12 * m * n + 18 * nb * n) + 8 * nb * (12 * n + 100) + 20 * n)
     return {"forward": float(fwd), "backward": float(bwd)}
 
 
 def flop_estimate(world, rows: float = 0.0, clamping: float = 0.0) -> dict:
     """Algorithmic fp64 FLOPs per world for one launch of each kernel, counted
-    from the implemented algorithm's loop structure (FMA = 2 FLOPs):
-    kinematics, world-frame composites, CRBA mass matrix, Cholesky + solves,
-    and in the backward the derivative composites plus one closed-form
-    dID/dq and dC/dv column per dof (only related body pairs)."""
+    from the implemented algorithm's loop structure (FMA = 2 FLOPs): forward =
+    kinematics, world-frame composites, CRBA mass matrix, Cholesky + solve
+    (+ contact stage); backward = accelerations at a*, derivative composites,
+    one closed-form dID/dq and dC/dv column per dof (only related body pairs)
+    and two solves (+ contact terms)."""
     d = world.desc_arrays()
     nb, n = int(d["num_bodies"]), int(d["num_dofs"])
     parent = list(d["parent"])
@@ -161,6 +164,10 @@ def flop_estimate(world, rows: float = 0.0, clamping: float = 0.0) -> dict:
                 lanes += (1020 if c != b else 0) + 80 * ndof[c]
             elif c in anc[b]:
                 lanes += 50 * ndof[c]
-    bwd = kin * 2 + comp + mass + chol + 2 * solve + dcomp + lanes + 20 * n
+    # the backward reuses the forward's kinematics, composite inertias and
+    # Cholesky factor (snapshot dynamics cache): accelerations + derivative
+    # composites + the per-direction columns + two solves
+    accel = nb * n * 30
+    bwd = accel + dcomp + lanes + 2 * solve + 20 * n
     c = contact_flop_estimate(world, rows, clamping)
     return {"forward": float(fwd + c["forward"]), "backward": float(bwd + c["backward"])}

@@ -13,3 +13,6 @@ timeout -k 10 600 python bench.py "$@" > $R/gpurun_out/bench_$TAG.json 2> $R/gpu
 cat $R/gpurun_out/bench_$TAG.json
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline "$@" > $R/gpurun_out/prof_$TAG.log 2>&1 || { echo PROF FAILED; tail -20 $R/gpurun_out/prof_$TAG.log; exit 1; }
 find $R/gpurun_out/prof_$TAG -name "*stats*"
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $R/gpurun_out/pmc_fetch_$TAG -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline "$@" > $R/gpurun_out/pmc1_$TAG.log 2>&1 || { echo PMC1 FAILED; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $R/gpurun_out/pmc_write_$TAG -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline "$@" > $R/gpurun_out/pmc2_$TAG.log 2>&1 || { echo PMC2 FAILED; exit 1; }
+echo PMC OK

@@ -185,3 +185,17 @@ def test_timestep_layer_with_contact():
     assert _rel(out.detach().cpu().numpy(), ref) < RTOL
     assert _rel(ts.grad.cpu().numpy(), rgs) < RTOL
     assert _rel(tf.grad.cpu().numpy(), rgf) < RTOL
+
+
+@pytest.mark.parametrize("rows", [0, 6])
+def test_hbm_workspace_path(rows, monkeypatch):
+    """Worlds whose LCP exceeds the on-chip pool run the same code on the
+    snapshot's HBM workspace; force that path (pool for 0 / 6 rows) and check
+    parity on box and Atlas contact worlds."""
+    monkeypatch.setenv("NIMBLE_AMD_LDS_ROWS", str(rows))
+    world = models.box_world()
+    st, f = models.box_states("slide", 32, seed=8)
+    _parity(world, st, f)
+    world = models.atlas_world(True)
+    st, f = models.random_states(world, 32, seed=12, q_scale=0.01, v_scale=0.02)
+    _parity(world, st, f)

@@ -451,6 +451,7 @@ __device__ void codFactor(Cod& c, double* cn, double* v, int lane) {
 #define H_SC 9
 #define H_IGN 10
 #define H_K 11
+#define H_CODOK 12  // M1 + scr hold the COD of the final clamping Q
 #define H_PAIRCNT 16   // 16 per-pair counts of the current chunk
 
 // status bits
@@ -651,6 +652,7 @@ __device__ bool devConstruct(FwdPool& P, int m, double cfm, bool ignoreFriction,
     double* z = w; w += m;
     STAMP(41);
     codFactor(cod, cn, vv, lane);
+    if (lane == 0) ct[H_CODOK] = 1;
     STAMP(42);
     {
       const double f = codSolveWave(cod, lane < nc ? P.relVel[lane] : 0.0, z, lane);
@@ -767,17 +769,22 @@ __device__ void backwardPrecompute(const ModelDev& md, double* s, const Layout& 
     for (int u = rc + 1; u <= rc + 2 && u < m; u++)
       if (P.mapping[u] == rc) v += P.Eval[u] * P.A[rr * m + u];
     if (cr == cc) v += cfm;
-    P.M1[t] = v;
     P.M2[t] = v;
     QG[t] = v;
   }
+  // the final classification's COD of this Q is normally still on chip (M1 +
+  // scr, devConstruct); refactor only if a fallback solver clobbered it
+  const bool reuse = ct[H_CODOK] != 0;
+  __syncthreads();
+  if (!reuse)
+    for (int t = lane; t < nc * nc; t += WAVE) P.M1[t] = P.M2[t];
   __syncthreads();
   Cod cod;
-  double* w = carveCod(P.scr, P.M2, nc, nc, nc, cod);
+  double* w = carveCod(P.scr, P.M1, nc, nc, nc, cod);
   double* cn = w; w += m;
   double* vv = w; w += m;
   STAMP(48);
-  codFactor(cod, cn, vv, lane);
+  if (!reuse) codFactor(cod, cn, vv, lane);
   STAMP(49);
   // pinv(Q): lane c solves Q x = e_c in place in row c of the (now free) A region
   double* Zs = P.A;
@@ -820,7 +827,7 @@ __device__ void backwardPrecompute(const ModelDev& md, double* s, const Layout& 
   for (int t = lane; t < nc * nc; t += WAVE) {
     const int r = t / nc, c = t % nc;
     double acc = 0;
-    for (int j = 0; j < nc; j++) acc += P.M1[r * nc + cod.perm[j]] * Zs[c * nc + j];
+    for (int j = 0; j < nc; j++) acc += P.M2[r * nc + cod.perm[j]] * Zs[c * nc + j];
     const double e = (r == c ? 1.0 : 0.0) - acc;
     part += e * e;
   }
@@ -978,6 +985,7 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
     for (int i = lane; i < m; i += WAVE) P.xc[i] = P.X[i];
     __syncthreads();
   }
+  if (lane == 0) ct[H_CODOK] = 0;
   STAMP(4);
 #ifdef NIMBLE_STAGE_TIMING
   bool success = devConstruct(P, m, 0.0, false, ct, lane, g_stamp);
@@ -1006,6 +1014,7 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
       }
       if (__ballot(dup) && lane == 0) ct[H_STATUS] = (double)((int)ct[H_STATUS] | ST_DUPLICATE_COLUMNS);
     }
+    if (lane == 0) ct[H_CODOK] = 0;
     for (int t = lane; t < m * m; t += WAVE) P.M1[t] = P.A[t];
     __syncthreads();
     double xd = 0.0;
@@ -1026,6 +1035,7 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
     if (__ballot(lane < m && isnan(X))) { ok = false; X = 0.0; }
     if (!ok) {
       cf = md.fallbackCfm;
+      if (lane == 0) ct[H_CODOK] = 0;
       for (int t = lane; t < m * m; t += WAVE) P.M1[t] = P.A[t] + ((t / m == t % m) ? cf : 0.0);
       __syncthreads();
       double xd = lane < m ? P.xc[lane] : 0.0;

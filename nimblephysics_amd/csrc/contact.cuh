@@ -1018,7 +1018,11 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
     for (int t = lane; t < m * m; t += WAVE) P.M1[t] = P.A[t];
     __syncthreads();
     double xd = 0.0;
+    #ifdef NIMBLE_STAGE_TIMING
+    bool ok = waveDantzig(m, P.M1, P.M2, P.scr, xd, bR, loR, hiR, fiR, lane, g_stamp + 52);
+#else
     bool ok = waveDantzig(m, P.M1, P.M2, P.scr, xd, bR, loR, hiR, fiR, lane);
+#endif
     if (ok) {
       if (lane < m) P.X[lane] = xd;
       __syncthreads();
@@ -1039,7 +1043,11 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
       for (int t = lane; t < m * m; t += WAVE) P.M1[t] = P.A[t] + ((t / m == t % m) ? cf : 0.0);
       __syncthreads();
       double xd = lane < m ? P.xc[lane] : 0.0;
+      #ifdef NIMBLE_STAGE_TIMING
+      ok = wavePgs(m, P.M1, xd, bR, loR, hiR, fiR, lane, g_stamp + 54);
+#else
       ok = wavePgs(m, P.M1, xd, bR, loR, hiR, fiR, lane);
+#endif
       if (ok) {
         X = xd;
         ok = waveLcpValid(m, P.A, cf, X, bR, hiR, loR, fiR, false, lane);

@@ -23,65 +23,85 @@
 // rounding).  A is symmetric and read by rows (conflict-free LDS access);
 // the reference's in-place row scaling (1/A_jj) is applied lane-locally,
 // A_ji / A_jj = A_ij * dummy_j, so A is never written.
-__device__ bool wavePgs(int n, const double* A, double& x, double b, double lo, double hi, int findex, int lane) {
+__device__ bool wavePgs(int n, const double* A, double& x, double b, double lo, double hi, int findex, int lane,
+                        double* dbg = nullptr) {
   const double deltaXThr = 1e-6, relTol = 1e-3, epsDiv = 1e-9;
   const bool act = lane < n;
+  const int col = act ? lane : 0;  // idle lanes read a valid address, use 0
   const double diagRaw = act ? A[lane * n + lane] : 1.0;
   const unsigned long long order = __ballot(act && diagRaw >= epsDiv);
-  double xF = __shfl(x, findex >= 0 ? findex : 0);
+  const bool inOrder = act && ((order >> lane) & 1ull);
+  // rows whose x bounds friction rows (their update refreshes those bounds)
+  unsigned long long bounding = 0;
+  for (int i = 0; i < n; i++)
+    if (__ballot(findex == i)) bounding |= 1ull << i;
   double r = act ? b : 0.0;
   for (int k = 0; k < n; k++) {
     const double xk = rdl(x, k);
     if (act) r -= A[k * n + lane] * xk;
   }
-  bool possible = true;
-  double row = act ? A[lane] : 0.0;  // row 0 prefetched
-  for (int i = 0; i < n; i++) {
-    const double cur = row;
-    if (i + 1 < n) row = act ? A[(i + 1) * n + lane] : 0.0;
-    double nx;
-    bool moved = false;
-    if (!((order >> i) & 1ull)) {
-      nx = 0.0;
-    } else {
-      nx = (r + diagRaw * x) / diagRaw;
-      const double h = findex >= 0 ? hi * xF : hi, l = findex >= 0 ? -h : lo;
-      nx = nx > h ? h : (nx < l ? l : nx);
-      moved = lane == i && fabs(nx - x) > deltaXThr;
+  // current box of each row; friction rows track hi * x[findex]
+  double hB = hi, lB = lo;
+  if (findex >= 0) { hB = hi * __shfl(x, findex); lB = -hB; }
+  // Each lane's x changes only at its own row of a sweep, so within a sweep
+  // lane i still holds its sweep-start value x0 when row i is visited, and
+  // the reference's per-row "moved" test can be evaluated for all rows at
+  // once after the sweep (same operands, same outcome).  The row loop then
+  // carries only clamp -> readlane -> residual update; rows of A (symmetric,
+  // row i lane j = A_ji) are prefetched two ahead.
+  const double x0 = x;
+  const double act1 = act ? 1.0 : 0.0;
+  double xn = x;
+  {
+    double rowA = A[col], rowB = n > 1 ? A[n + col] : 0.0;
+    for (int i = 0; i < n; i++) {
+      const double cur = rowA * act1;
+      rowA = rowB;
+      if (i + 2 < n) rowB = A[(i + 2) * n + col];
+      double nx = 0.0;
+      if ((order >> i) & 1ull) {
+        nx = (r + diagRaw * x0) / diagRaw;
+        nx = nx > hB ? hB : (nx < lB ? lB : nx);
+      }
+      const double dx = rdl(nx - x0, i);
+      if (lane == i) xn = nx;
+      if ((bounding >> i) & 1ull) {
+        const double nxi = rdl(nx, i);
+        if (findex == i) { hB = hi * nxi; lB = -hB; }
+      }
+      r -= cur * dx;
     }
-    const double dx = rdl(nx - x, i);
-    const double nxi = rdl(nx, i);
-    if (lane == i) x = nxi;
-    if (findex == i) xF = nxi;
-    if (act) r -= cur * dx;
-    if (__ballot(moved)) possible = false;
   }
-  if (possible) return true;
+  if (!__ballot(inOrder && fabs(xn - x0) > deltaXThr)) { x = xn; return true; }
   // row scaling of the reference, lane-local: A'_jk = A_jk * dummy_j
-  const bool inOrder = act && ((order >> lane) & 1ull);
   const double dummy = inOrder ? 1.0 / diagRaw : 1.0;
   if (inOrder) { b *= dummy; r *= dummy; }
   const double diag = inOrder ? diagRaw * dummy : diagRaw;
+  const double dummyAct = act ? dummy : 0.0;
+  bool possible = false;
   for (int iter = 1; iter < 30; iter++) {
-    possible = true;
-    row = act ? A[lane] : 0.0;
+    const double xs = xn;
+    double rowA = A[col], rowB = n > 1 ? A[n + col] : 0.0;
     for (int idx = 0; idx < n; idx++) {
-      const double cur = row;
-      if (idx + 1 < n) row = act ? A[(idx + 1) * n + lane] : 0.0;
+      const double cur = rowA * dummyAct;
+      rowA = rowB;
+      if (idx + 2 < n) rowB = A[(idx + 2) * n + col];
       if (!((order >> idx) & 1ull)) continue;
-      double nx = r + diag * x;
-      const double h = findex >= 0 ? hi * xF : hi, l = findex >= 0 ? -h : lo;
-      nx = nx > h ? h : (nx < l ? l : nx);
-      const bool moved = lane == idx && fabs(nx) > epsDiv && fabs((nx - x) / nx) > relTol;
-      const double dx = rdl(nx - x, idx);
-      const double nxi = rdl(nx, idx);
-      if (lane == idx) x = nxi;
-      if (findex == idx) xF = nxi;
-      if (act) r -= (cur * dummy) * dx;
-      if (__ballot(moved)) possible = false;
+      double nx = r + diag * xs;
+      nx = nx > hB ? hB : (nx < lB ? lB : nx);
+      const double dx = rdl(nx - xs, idx);
+      if (lane == idx) xn = nx;
+      if ((bounding >> idx) & 1ull) {
+        const double nxi = rdl(nx, idx);
+        if (findex == idx) { hB = hi * nxi; lB = -hB; }
+      }
+      r -= cur * dx;
     }
+    possible = !__ballot(inOrder && fabs(xn) > epsDiv && fabs((xn - xs) / xn) > relTol);
+    if (dbg && lane == 0) dbg[0] = iter;
     if (possible) break;
   }
+  x = xn;
   return possible;
 }
 
@@ -373,8 +393,9 @@ struct WaveDantzig {
 // A (n x n LDS, destroyed), L (n x (n|1) LDS scratch), scr (>= n LDS); problem
 // vectors lane-distributed; returns success and x (lane-distributed).
 __device__ bool waveDantzig(int n, double* A, double* Lbuf, double* scr, double& xOut, double b, double lo, double hi,
-                            int findex, int lane) {
+                            int findex, int lane, double* dbg = nullptr) {
   WaveDantzig D;
+  int pivots = 0;
   D.n = n; D.nC = 0; D.nN = 0; D.lane = lane; D.ldL = n | 1;
   D.A = A; D.L = Lbuf; D.scr = scr;
   D.x = 0.0; D.b = b; D.w = 0.0; D.lo = lo; D.hi = hi; D.d = 0.0;
@@ -470,6 +491,8 @@ __device__ bool waveDantzig(int n, double* A, double* Lbuf, double* scr, double&
             cmd = rdli(typ, si);
           }
         }
+        pivots++;
+        if (dbg && lane == 0) { dbg[0] = pivots; dbg[1] = i; }
         if (s <= 0.0) return false;
         if (lane < nC) D.x += s * D.deltaX;
         if (lane == i) D.x += s * dirf;

@@ -45,3 +45,12 @@ for it in range(4):
         if m.any():
             dtk = T[m, b] - T[m, a]
             print(f"  {nm:32s} worlds {m.sum():5d}  mean {dtk.mean():10.0f}  max {dtk.max():10.0f}")
+    # the slowest worlds set the kernel time: their per-stage split
+    tot = np.where((T[:, 12] > 0) & (T[:, 13] > 0), T[:, 13] - T[:, 12], 0)
+    for wi in np.argsort(-tot)[:6]:
+        parts = []
+        for (a, b), nm in names.items():
+            if T[wi, a] > 0 and T[wi, b] > 0 and (b - a) != 1 or (a, b) in ((5, 6), (6, 7), (4, 5), (8, 9), (0, 1), (3, 4), (7, 8)):
+                if T[wi, a] > 0 and T[wi, b] > 0:
+                    parts.append(f"{nm.strip()}={int(T[wi, b] - T[wi, a])}")
+        print(f"  world {wi}: pivots {int(T[wi,52])} at row {int(T[wi,53])} pgs-sweeps {int(T[wi,54])} ign {hd[wi,7]:.0f} total {int(tot[wi])} rows {int(hd[wi,1])} clamp {int(hd[wi,2])} flag {hd[wi,4]:.0f} | " + " ".join(parts))

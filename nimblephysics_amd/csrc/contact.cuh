@@ -290,150 +290,6 @@ __device__ inline void carveFwd(double* base, int m, int n, FwdPool& P) {
   P.scr = p;
 }
 
-// ---------------------------------------------------------------------------
-// Complete orthogonal decomposition (Eigen::CompleteOrthogonalDecomposition,
-// used by the reference for Q^+ b at ConstrainedGroupGradientMatrices.cpp:270
-// and BackpropSnapshot.cpp:2747): column-pivoted Householder QR, rank =
-// #{|R_kk| > eps * min(m,n) * max|R_kk|}, then RZ on the leading r rows.
-// Factorisation is lane-parallel over columns / rows; solves are per lane.
-// A is m x n with leading dimension ld; reflectors are stored in place.
-// ---------------------------------------------------------------------------
-struct Cod {
-  double* A;
-  int m, n, ld, kmax;
-  int* perm;        // n
-  double* vd;       // kmax  QR reflector heads
-  double* vn;       // kmax  QR reflector norms (<= 0: skipped)
-  double* zd;       // m     RZ reflector heads
-  double* zn;       // m     RZ reflector norms
-  int* rank;        // 1
-};
-
-// carve a Cod workspace from `w` (needs 6*max(m,n) + 8 doubles + the v vector)
-__device__ inline double* carveCod(double* w, double* A, int m, int n, int ld, Cod& c) {
-  const int mx = m > n ? m : n;
-  c.A = A; c.m = m; c.n = n; c.ld = ld; c.kmax = m < n ? m : n;
-  c.vd = w; w += mx;
-  c.vn = w; w += mx;
-  c.zd = w; w += mx;
-  c.zn = w; w += mx;
-  c.perm = reinterpret_cast<int*>(w); w += (mx + 1) / 2 + 1;
-  c.rank = reinterpret_cast<int*>(w); w += 2;
-  return w;
-}
-
-// Lane-parallel factorisation: column norms live in registers (lane j =
-// column j), the pivot is a wave arg-max (first index among equal maxima, as
-// the sequential scan), alpha and |v|^2 are wave reductions, and the
-// reflector pass (lane = column) also recomputes the next step's partial
-// column norms (same sums as a fresh recomputation).  Requires n <= 64.
-// `cn` is unused (kept for the call signature), `v` holds m doubles.
-__device__ void codFactor(Cod& c, double* cn, double* v, int lane) {
-  (void)cn;
-  double* A = c.A;
-  const int m = c.m, n = c.n, ld = c.ld;
-  if (lane < n) c.perm[lane] = lane;
-  double norm = 0.0;  // partial norm of column `lane` over rows >= k
-  if (lane < n) {
-#pragma unroll 8
-    for (int i = 0; i < m; i++) norm += A[i * ld + lane] * A[i * ld + lane];
-  }
-  __syncthreads();
-  double maxPivot = 0.0;
-  for (int k = 0; k < c.kmax; k++) {
-    // pivot: largest remaining norm, lowest index on ties
-    const double cand = (lane >= k && lane < n) ? norm : -1.0;
-    const double best = -waveMin(-cand);
-    const int p = waveFirst(lane >= k && lane < n && cand == best);
-    if (p != k) {
-      for (int i = lane; i < m; i += WAVE) {
-        const double t = A[i * ld + k]; A[i * ld + k] = A[i * ld + p]; A[i * ld + p] = t;
-      }
-      const double nk = rdl(norm, k), np = rdl(norm, p);
-      if (lane == k) norm = np;
-      else if (lane == p) norm = nk;
-      if (lane == 0) { int t = c.perm[k]; c.perm[k] = c.perm[p]; c.perm[p] = t; }
-    }
-    __syncthreads();
-    const double akk = A[k * ld + k];
-    const double colv = (lane >= k && lane < m) ? A[lane * ld + k] : 0.0;
-    double alpha = sqrt(waveSum(colv * colv));
-    if (alpha == 0.0) {
-      if (lane == 0) c.vn[k] = -1.0;
-      // fresh norms of the remaining columns over rows >= k+1
-      if (lane > k && lane < n) {
-        double nrm = 0.0;
-#pragma unroll 8
-        for (int i = k + 1; i < m; i++) nrm += A[i * ld + lane] * A[i * ld + lane];
-        norm = nrm;
-      }
-      __syncthreads();
-      continue;
-    }
-    if (akk > 0) alpha = -alpha;
-    const double vi = (lane == k) ? colv - alpha : colv;
-    if (lane >= k && lane < m) v[lane] = vi;
-    const double vnorm = waveSum(vi * vi);
-    __syncthreads();
-    if (lane >= k && lane < n) {
-      double nrm = 0.0;
-      if (vnorm > 0) {
-        double sc = 0;
-#pragma unroll 8
-        for (int i = k; i < m; i++) sc += v[i] * A[i * ld + lane];
-        sc = 2 * sc / vnorm;
-#pragma unroll 8
-        for (int i = k; i < m; i++) {
-          const double a = A[i * ld + lane] - sc * v[i];
-          A[i * ld + lane] = a;
-          if (i > k) nrm += a * a;
-        }
-      } else {
-#pragma unroll 8
-        for (int i = k + 1; i < m; i++) nrm += A[i * ld + lane] * A[i * ld + lane];
-      }
-      norm = nrm;
-    }
-    __syncthreads();
-    maxPivot = fmax(maxPivot, fabs(A[k * ld + k]));
-    if (lane > k && lane < m) A[lane * ld + k] = v[lane];
-    if (lane == 0) { c.vd[k] = v[k]; c.vn[k] = vnorm; }
-    __syncthreads();
-  }
-  const double thr = 2.220446049250313e-16 * c.kmax * maxPivot;
-  int r = 0;
-  for (int k = 0; k < c.kmax; k++)
-    if (fabs(A[k * ld + k]) > thr) r++;
-  if (lane == 0) *c.rank = r;
-  // RZ: reflect row i over columns {i} U {r..n-1}; row i's trailing part is
-  // kept as the reflector
-  for (int i = r - 1; i >= 0 && r < n; i--) {
-    const double aii = A[i * ld + i];
-    const double tj = (lane >= r && lane < n) ? A[i * ld + lane] : 0.0;
-    const double tail = waveSum(tj * tj);
-    double al = sqrt(aii * aii + tail);
-    if (aii > 0) al = -al;
-    const double vi = aii - al;
-    const double vnz = vi * vi + tail;
-    __syncthreads();
-    if (lane == 0) { c.zd[i] = vi; c.zn[i] = vnz; }
-    if (vnz != 0) {
-      for (int row = lane; row <= i; row += WAVE) {
-        double sc = A[row * ld + i] * vi;
-#pragma unroll 4
-        for (int j = r; j < n; j++) sc += A[row * ld + j] * A[i * ld + j];
-        sc = 2 * sc / vnz;
-        A[row * ld + i] -= sc * vi;
-        if (row < i)
-#pragma unroll 4
-          for (int j = r; j < n; j++) A[row * ld + j] -= sc * A[i * ld + j];
-      }
-    }
-    __syncthreads();
-  }
-  __syncthreads();
-}
-
 #include "lcp_wave.cuh"
 
 // ---------------------------------------------------------------------------
@@ -619,7 +475,7 @@ __device__ bool devConstruct(FwdPool& P, int m, double cfm, bool ignoreFriction,
       ct[H_NC] = nc; ct[H_NU] = nu;
     }
     __syncthreads();
-    const int nc = (int)ct[H_NC];
+    const int nc = uni((int)ct[H_NC]);
     const double bR = lane < m ? P.b[lane] : 0.0, hiR = lane < m ? P.hi[lane] : 0.0;
     const double loR = lane < m ? P.lo[lane] : 0.0;
     const int fiR = lane < m ? P.fi[lane] : -1;
@@ -681,7 +537,7 @@ __device__ bool devConstruct(FwdPool& P, int m, double cfm, bool ignoreFriction,
     }
     __syncthreads();
     const bool ok = waveLcpValid(m, P.A, cfm, lane < m ? P.nx[lane] : 0.0, bR, hiR, loR, fiR, ignoreFriction, lane);
-    const int res = ok ? ((int)ct[H_FLAG] ? 2 : 1) : 0;
+    const int res = ok ? (uni((int)ct[H_FLAG]) ? 2 : 1) : 0;
     STAMP(44);
     if (ok) {
       if (lane < m) P.X[lane] = P.nx[lane];
@@ -705,7 +561,7 @@ __device__ void devGuess(FwdPool& P, int m, double* x, double* ct, int lane) {
     ct[H_K] = k;
   }
   __syncthreads();
-  const int k = (int)ct[H_K];
+  const int k = uni((int)ct[H_K]);
   for (int i = lane; i < m; i += WAVE) x[i] = 0.0;
   if (k == 0) { __syncthreads(); return; }
   double* Ar = P.M1;
@@ -739,7 +595,7 @@ __device__ void backwardPrecompute(const ModelDev& md, double* s, const Layout& 
   double* g_stamp = snap + snapWorkspaceOffset(n) + 1000;
 #endif
   STAMP(45);
-  const int nc = (int)ct[H_NC];
+  const int nc = uni((int)ct[H_NC]);
   if (lane == 0) snap[SN_IMP] = 0.0;
   if (nc == 0) { __syncthreads(); return; }
   double* AcG = snap + snAc(n);
@@ -774,7 +630,7 @@ __device__ void backwardPrecompute(const ModelDev& md, double* s, const Layout& 
   }
   // the final classification's COD of this Q is normally still on chip (M1 +
   // scr, devConstruct); refactor only if a fallback solver clobbered it
-  const bool reuse = ct[H_CODOK] != 0;
+  const bool reuse = uni(ct[H_CODOK] != 0 ? 1 : 0) != 0;
   __syncthreads();
   if (!reuse)
     for (int t = lane; t < nc * nc; t += WAVE) P.M1[t] = P.M2[t];
@@ -854,7 +710,7 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
   const double* Lm = s + L.M;
   collideWorld(md, s, L, lane);
   STAMP(1);
-  const int nCon = (int)ct[H_NCON];
+  const int nCon = uni((int)ct[H_NCON]);
   if (nCon == 0) {
     if (lane == 0) {
       for (int i = 0; i < 8; i++) snap[i] = 0.0;
@@ -874,7 +730,7 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
     ct[H_M] = m;
   }
   __syncthreads();
-  const int m = (int)ct[H_M];
+  const int m = uni((int)ct[H_M]);
   FwdPool P;
   const int need = fwdPoolDoubles(m, n);
   carveFwd(need <= L.poolCap ? s + L.pool : overflowWs, m, n, P);
@@ -976,7 +832,7 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
   __syncthreads();
   STAMP(3);
   // warm start (BoxedLcpConstraintSolver::mX) or guessSolution
-  const bool cached = (int)cache[0] == m;
+  const bool cached = uni((int)cache[0]) == m;
   if (cached) {
     for (int i = lane; i < m; i += WAVE) { P.X[i] = cache[1 + i]; P.xc[i] = cache[1 + i]; }
     __syncthreads();
@@ -1082,8 +938,8 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
     if (lane == 0) { ct[H_CFM] = cf; ct[H_IGN] = ign ? 1 : 0; }
     __syncthreads();
   }
-  cfm = ct[H_CFM];
-  ignoredFriction = ct[H_IGN] != 0;
+  cfm = unid(ct[H_CFM]);
+  ignoredFriction = uni(ct[H_IGN] != 0 ? 1 : 0) != 0;
   STAMP(7);
   // the step keeps the solver's x unless the re-standardisation succeeds
   // (BoxedLcpConstraintSolver: `if (gm.standardized) x = gm.X`)
@@ -1128,7 +984,7 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
     rr[RR_EVAL] = P.Eval[j];
     rr[RR_BOUNCE] = 1.0 + P.rest[j];
   }
-  const int nc = (int)ct[H_NC];
+  const int nc = uni((int)ct[H_NC]);
   for (int i = lane; i < nc; i += WAVE) snap[SN_FC + i] = P.fc[i];
   for (int i = lane; i < n; i += WAVE) snap[snYf(n) + i] = ddq[i];
   backwardPrecompute(md, s, L, lane, P, m, cfm, snap, ct);
@@ -1246,7 +1102,7 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
   const double* Q = sn + snQ(n);
   const double* Lm = s + L.M;
   const double* dinv = s + L.dinv;
-  const int imp = (int)sn[SN_IMP];
+  const int imp = uni((int)sn[SN_IMP]);
 #ifdef NIMBLE_STAGE_TIMING
   double* g_stamp = (double*)sn + snapWorkspaceOffset(n) + 1000;
 #endif

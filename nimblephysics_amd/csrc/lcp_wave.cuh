@@ -12,8 +12,18 @@
 // All functions must be entered by the whole wave (uniform control flow).
 #pragma once
 #include "wave.cuh"
+#include "cod_wave.cuh"
 
 #define LCP_INF __builtin_inf()
+
+// optional per-phase clock accounting (tools/lcp_bench: -DLCP_PROFILE)
+#ifdef LCP_PROFILE
+#define LP_BEGIN() const long long lp0_ = (long long)__builtin_amdgcn_s_memtime()
+#define LP_END(acc, k) (acc)[k] += (long long)__builtin_amdgcn_s_memtime() - lp0_
+#else
+#define LP_BEGIN() do { } while (0)
+#define LP_END(acc, k) do { } while (0)
+#endif
 
 // ---------------------------------------------------------------------------
 // Residual form: lane j keeps r_j = b_j - sum_k A_jk x_k; a sweep step on
@@ -25,7 +35,11 @@
 // A_ji / A_jj = A_ij * dummy_j, so A is never written.
 __device__ bool wavePgs(int n, const double* A, double& x, double b, double lo, double hi, int findex, int lane,
                         double* dbg = nullptr) {
+  n = uni(n);
   const double deltaXThr = 1e-6, relTol = 1e-3, epsDiv = 1e-9;
+#ifdef LCP_PROFILE
+  const long long tp0 = (long long)__builtin_amdgcn_s_memtime();
+#endif
   const bool act = lane < n;
   const int col = act ? lane : 0;  // idle lanes read a valid address, use 0
   const double diagRaw = act ? A[lane * n + lane] : 1.0;
@@ -40,6 +54,23 @@ __device__ bool wavePgs(int n, const double* A, double& x, double b, double lo, 
     const double xk = rdl(x, k);
     if (act) r -= A[k * n + lane] * xk;
   }
+  // Contact layout (the forward's rows: each contact is a normal row
+  // followed by 0 or 2 friction rows with findex = that normal and
+  // lo = -hi), every row in order: the friction box of row i is
+  // +-hi_i * x_N with x_N the newest x of the last normal row, which the
+  // sweep carries as one scalar -- no per-lane box registers.
+  bool contactRows = order == __ballot(act);
+  {
+    const int f1 = __shfl(findex, lane > 0 ? lane - 1 : 0), f2 = __shfl(findex, lane > 1 ? lane - 2 : 0);
+    const bool ok = !act || findex < 0 ||
+                    (lo == -hi && ((findex == lane - 1 && f1 < 0) || (findex == lane - 2 && f1 == lane - 2 && f2 < 0)));
+    contactRows = contactRows && !__ballot(!ok);
+  }
+  const unsigned long long normals = __ballot(act && findex < 0);
+  if (dbg && lane == 0) dbg[1] = contactRows ? 1 : 0;
+#ifdef LCP_PROFILE
+  const long long tp1 = (long long)__builtin_amdgcn_s_memtime();
+#endif
   // current box of each row; friction rows track hi * x[findex]
   double hB = hi, lB = lo;
   if (findex >= 0) { hB = hi * __shfl(x, findex); lB = -hB; }
@@ -47,17 +78,20 @@ __device__ bool wavePgs(int n, const double* A, double& x, double b, double lo, 
   // lane i still holds its sweep-start value x0 when row i is visited, and
   // the reference's per-row "moved" test can be evaluated for all rows at
   // once after the sweep (same operands, same outcome).  The row loop then
-  // carries only clamp -> readlane -> residual update; rows of A (symmetric,
-  // row i lane j = A_ji) are prefetched two ahead.
+  // carries only clamp -> readlane -> residual update.  Rows of A (symmetric,
+  // row i lane j = A_ji) are loaded one 4-row group ahead, so LDS latency is
+  // off the dependent chain.
   const double x0 = x;
   const double act1 = act ? 1.0 : 0.0;
   double xn = x;
+  const int nLast = n - 1;
+#define PGS_LOAD_GROUP(R, i0)                                        \
+  double R##0 = A[((i0) < n ? (i0) : nLast) * n + col];             \
+  double R##1 = A[((i0) + 1 < n ? (i0) + 1 : nLast) * n + col];     \
+  double R##2 = A[((i0) + 2 < n ? (i0) + 2 : nLast) * n + col];     \
+  double R##3 = A[((i0) + 3 < n ? (i0) + 3 : nLast) * n + col]
   {
-    double rowA = A[col], rowB = n > 1 ? A[n + col] : 0.0;
-    for (int i = 0; i < n; i++) {
-      const double cur = rowA * act1;
-      rowA = rowB;
-      if (i + 2 < n) rowB = A[(i + 2) * n + col];
+    auto row1 = [&](int i, double cur) {
       double nx = 0.0;
       if ((order >> i) & 1ull) {
         nx = (r + diagRaw * x0) / diagRaw;
@@ -69,9 +103,47 @@ __device__ bool wavePgs(int n, const double* A, double& x, double b, double lo, 
         const double nxi = rdl(nx, i);
         if (findex == i) { hB = hi * nxi; lB = -hB; }
       }
-      r -= cur * dx;
+      r -= (cur * act1) * dx;
+    };
+    double xN = 0.0;
+    // (the row kind is a scalar bit: the branch never waits on VALU results;
+    // x_N is only consumed by VALU multiplies, never by SALU)
+    auto row1c = [&](int i, double cur) {
+      double h = hi, l = lo;
+      if (!((normals >> i) & 1ull)) { h = hi * xN; l = lo * xN; }
+      double nx = (r + diagRaw * x0) / diagRaw;
+      const double t = nx < l ? l : nx;
+      nx = nx > h ? h : t;
+      const double dx = rdl(nx - x0, i);
+      if ((normals >> i) & 1ull) xN = rdl(nx, i);
+      if (lane == i) xn = nx;
+      r -= (cur * act1) * dx;
+    };
+    PGS_LOAD_GROUP(C, 0);
+    if (contactRows) {
+      for (int i0 = 0; i0 < n; i0 += 4) {
+        PGS_LOAD_GROUP(N, i0 + 4);
+        row1c(i0, C0);
+        if (i0 + 1 < n) row1c(i0 + 1, C1);
+        if (i0 + 2 < n) row1c(i0 + 2, C2);
+        if (i0 + 3 < n) row1c(i0 + 3, C3);
+        C0 = N0; C1 = N1; C2 = N2; C3 = N3;
+      }
+    } else {
+      for (int i0 = 0; i0 < n; i0 += 4) {
+        PGS_LOAD_GROUP(N, i0 + 4);
+        row1(i0, C0);
+        if (i0 + 1 < n) row1(i0 + 1, C1);
+        if (i0 + 2 < n) row1(i0 + 2, C2);
+        if (i0 + 3 < n) row1(i0 + 3, C3);
+        C0 = N0; C1 = N1; C2 = N2; C3 = N3;
+      }
     }
   }
+#ifdef LCP_PROFILE
+  const long long tp2 = (long long)__builtin_amdgcn_s_memtime();
+  if (dbg && lane == 0) { dbg[2] = (double)(tp1 - tp0); dbg[3] = (double)(tp2 - tp1); }
+#endif
   if (!__ballot(inOrder && fabs(xn - x0) > deltaXThr)) { x = xn; return true; }
   // row scaling of the reference, lane-local: A'_jk = A_jk * dummy_j
   const double dummy = inOrder ? 1.0 / diagRaw : 1.0;
@@ -81,12 +153,8 @@ __device__ bool wavePgs(int n, const double* A, double& x, double b, double lo, 
   bool possible = false;
   for (int iter = 1; iter < 30; iter++) {
     const double xs = xn;
-    double rowA = A[col], rowB = n > 1 ? A[n + col] : 0.0;
-    for (int idx = 0; idx < n; idx++) {
-      const double cur = rowA * dummyAct;
-      rowA = rowB;
-      if (idx + 2 < n) rowB = A[(idx + 2) * n + col];
-      if (!((order >> idx) & 1ull)) continue;
+    auto row = [&](int idx, double cur) {
+      if (!((order >> idx) & 1ull)) return;
       double nx = r + diag * xs;
       nx = nx > hB ? hB : (nx < lB ? lB : nx);
       const double dx = rdl(nx - xs, idx);
@@ -95,12 +163,48 @@ __device__ bool wavePgs(int n, const double* A, double& x, double b, double lo, 
         const double nxi = rdl(nx, idx);
         if (findex == idx) { hB = hi * nxi; lB = -hB; }
       }
-      r -= cur * dx;
+      r -= (cur * dummyAct) * dx;
+    };
+    double xN = 0.0;
+    auto rowc = [&](int idx, double cur) {
+      double h = hi, l = lo;
+      if (!((normals >> idx) & 1ull)) { h = hi * xN; l = lo * xN; }
+      double nx = r + diag * xs;
+      const double t = nx < l ? l : nx;
+      nx = nx > h ? h : t;
+      const double dx = rdl(nx - xs, idx);
+      if ((normals >> idx) & 1ull) xN = rdl(nx, idx);
+      if (lane == idx) xn = nx;
+      r -= (cur * dummyAct) * dx;
+    };
+    PGS_LOAD_GROUP(C, 0);
+    if (contactRows) {
+      for (int i0 = 0; i0 < n; i0 += 4) {
+        PGS_LOAD_GROUP(N, i0 + 4);
+        rowc(i0, C0);
+        if (i0 + 1 < n) rowc(i0 + 1, C1);
+        if (i0 + 2 < n) rowc(i0 + 2, C2);
+        if (i0 + 3 < n) rowc(i0 + 3, C3);
+        C0 = N0; C1 = N1; C2 = N2; C3 = N3;
+      }
+    } else {
+      for (int i0 = 0; i0 < n; i0 += 4) {
+        PGS_LOAD_GROUP(N, i0 + 4);
+        row(i0, C0);
+        if (i0 + 1 < n) row(i0 + 1, C1);
+        if (i0 + 2 < n) row(i0 + 2, C2);
+        if (i0 + 3 < n) row(i0 + 3, C3);
+        C0 = N0; C1 = N1; C2 = N2; C3 = N3;
+      }
     }
     possible = !__ballot(inOrder && fabs(xn) > epsDiv && fabs((xn - xs) / xn) > relTol);
     if (dbg && lane == 0) dbg[0] = iter;
     if (possible) break;
   }
+#undef PGS_LOAD_GROUP
+#ifdef LCP_PROFILE
+  if (dbg && lane == 0) dbg[4] = (double)((long long)__builtin_amdgcn_s_memtime() - tp2);
+#endif
   x = xn;
   return possible;
 }
@@ -108,6 +212,7 @@ __device__ bool wavePgs(int n, const double* A, double& x, double b, double lo, 
 // ---------------------------------------------------------------------------
 __device__ bool waveLcpValid(int m, const double* A, double cfm, double x, double b, double hi, double lo, int fi,
                              bool ignoreFriction, int lane) {
+  m = uni(m);
   double v = -b;
 #pragma unroll 4
   for (int j = 0; j < m; j++) {
@@ -148,7 +253,7 @@ __device__ double codSolveWave(const Cod& c, double rhs, double* scr, int lane) 
   const double* A = c.A;
   const int m = c.m, n = c.n, ld = c.ld;
   for (int k = 0; k < c.kmax; k++) {
-    const double vnorm = c.vn[k];
+    const double vnorm = unid(c.vn[k]);
     if (!(vnorm > 0)) continue;
     const double vk = c.vd[k];
     const double v = lane == k ? vk : ((lane > k && lane < m) ? A[lane * ld + k] : 0.0);
@@ -156,7 +261,7 @@ __device__ double codSolveWave(const Cod& c, double rhs, double* scr, int lane) 
     sc = 2 * sc / vnorm;
     if (lane >= k && lane < m) rhs -= sc * v;
   }
-  const int r = *c.rank;
+  const int r = uni(*c.rank);
   double z = 0.0, acc = 0.0;
   for (int i = r - 1; i >= 0; i--) {
     const double zi = (rdl(rhs, i) - rdl(acc, i)) / A[i * ld + i];
@@ -165,7 +270,7 @@ __device__ double codSolveWave(const Cod& c, double rhs, double* scr, int lane) 
   }
   if (r < n) {
     for (int i = 0; i < r; i++) {
-      const double vn = c.zn[i];
+      const double vn = unid(c.zn[i]);
       if (vn == 0) continue;
       const double zd = c.zd[i];
       const double t = (lane >= r && lane < n) ? z * A[i * ld + lane] : 0.0;
@@ -191,6 +296,9 @@ struct WaveDantzig {
   double* scr;  // >= n doubles (LDS)
   double x, b, w, lo, hi, d, deltaX, deltaW, Dell, ell;
   int findex, p, C, state;
+#ifdef LCP_PROFILE
+  long long prof[8];
+#endif
 
   __device__ __forceinline__ void swapReg(double& v, int i1, int i2) {
     const double a = rdl(v, i1), c = rdl(v, i2);
@@ -204,6 +312,7 @@ struct WaveDantzig {
   }
   __device__ __forceinline__ void swapProblem(int i1, int i2) {
     if (i1 == i2) return;
+    LP_BEGIN();
     __syncthreads();
     if (lane < n) {
       const double t = A[i1 * n + lane];
@@ -219,20 +328,68 @@ struct WaveDantzig {
     __syncthreads();
     swapReg(x, i1, i2); swapReg(b, i1, i2); swapReg(w, i1, i2); swapReg(lo, i1, i2); swapReg(hi, i1, i2);
     swapRegI(p, i1, i2); swapRegI(state, i1, i2); swapRegI(findex, i1, i2);
+    LP_END(prof, 0);
   }
-  // L x = B (unit lower), B lane-distributed, first m entries
+  // L x = B (unit lower), B lane-distributed, first m entries.  The L
+  // entries of each lane are loaded 8 at a time ahead of the dependent
+  // readlane -> FMA chain (LDS latency paid once per 8 steps) with the
+  // triangle mask folded into them (0 where a lane must not change), so a
+  // step is a readlane and one unpredicated FMA: no exec-mask update that
+  // would wait on a vector compare.  0 * b_k leaves a lane unchanged only
+  // for finite b_k; a non-finite b_k (degenerate factor) re-runs the solve
+  // predicated, exactly as the reference's loop.
   __device__ __forceinline__ void solveL1(double& B, int m) {
-    for (int k = 0; k < m; k++) {
-      const double bk = rdl(B, k);
-      if (lane > k && lane < m) B -= L[lane * ldL + k] * bk;
+    m = uni(m);
+    LP_BEGIN();
+    const double B0 = B;
+    const int row = (lane < m ? lane : 0) * ldL;
+    for (int k0 = 0; k0 < m; k0 += 8) {
+      double Lk[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        double v = L[row + (k0 + u < m ? k0 + u : 0)];
+        asm volatile("" : "+v"(v));  // keep the load unconditional (batched)
+        Lk[u] = (lane > k0 + u && lane < m) ? v : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++)
+        if (k0 + u < m) B -= Lk[u] * rdl(B, k0 + u);
     }
+    if (__ballot(lane < m && !isfinite(B))) {
+      B = B0;
+      for (int k = 0; k < m; k++) {
+        const double bk = rdl(B, k);
+        if (lane > k && lane < m) B -= L[lane * ldL + k] * bk;
+      }
+    }
+    LP_END(prof, 1);
   }
   // L^T x = B
   __device__ __forceinline__ void solveL1T(double& B, int m) {
-    for (int k = m - 1; k >= 0; k--) {
-      const double bk = rdl(B, k);
-      if (lane < k) B -= L[k * ldL + lane] * bk;
+    m = uni(m);
+    LP_BEGIN();
+    const double B0 = B;
+    const int col = lane < m ? lane : 0;
+    for (int k0 = m - 1; k0 >= 0; k0 -= 8) {
+      double Lk[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        double v = L[(k0 - u >= 0 ? k0 - u : 0) * ldL + col];
+        asm volatile("" : "+v"(v));
+        Lk[u] = lane < k0 - u ? v : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++)
+        if (k0 - u >= 0) B -= Lk[u] * rdl(B, k0 - u);
     }
+    if (__ballot(lane < m && !isfinite(B))) {
+      B = B0;
+      for (int k = m - 1; k >= 0; k--) {
+        const double bk = rdl(B, k);
+        if (lane < k) B -= L[k * ldL + lane] * bk;
+      }
+    }
+    LP_END(prof, 2);
   }
   __device__ __forceinline__ void transferToC(int i) {
     const double Aii = A[i * n + i];
@@ -322,6 +479,7 @@ struct WaveDantzig {
     }
   }
   __device__ __forceinline__ void ldltRemove(int r, int n2) {
+    LP_BEGIN();
     if (r != n2 - 1) {
       if (r == 0) {
         const int C0 = rdli(C, 0);
@@ -353,6 +511,7 @@ struct WaveDantzig {
       const double dn = shiftDown1(d, lane);
       if (lane >= r && lane < n2 - 1) d = dn;
     }
+    LP_END(prof, 3);
   }
   __device__ __forceinline__ void transferFromCtoN(int i) {
     const int j = waveFirst(lane < nC && C == i);
@@ -394,6 +553,7 @@ struct WaveDantzig {
 // vectors lane-distributed; returns success and x (lane-distributed).
 __device__ bool waveDantzig(int n, double* A, double* Lbuf, double* scr, double& xOut, double b, double lo, double hi,
                             int findex, int lane, double* dbg = nullptr) {
+  n = uni(n);
   WaveDantzig D;
   int pivots = 0;
   D.n = n; D.nC = 0; D.nN = 0; D.lane = lane; D.ldL = n | 1;
@@ -401,6 +561,9 @@ __device__ bool waveDantzig(int n, double* A, double* Lbuf, double* scr, double&
   D.x = 0.0; D.b = b; D.w = 0.0; D.lo = lo; D.hi = hi; D.d = 0.0;
   D.deltaX = 0.0; D.deltaW = 0.0; D.Dell = 0.0; D.ell = 0.0;
   D.findex = findex; D.p = lane; D.C = 0; D.state = 0;
+#ifdef LCP_PROFILE
+  for (int k = 0; k < 8; k++) D.prof[k] = 0;
+#endif
   for (int k = lane; k < n * (n | 1); k += 64) Lbuf[k] = 0.0;
   if (__ballot(lane < n && findex < 0 && lo == -LCP_INF && hi == LCP_INF)) return false;
   {
@@ -411,6 +574,8 @@ __device__ bool waveDantzig(int n, double* A, double* Lbuf, double* scr, double&
   __syncthreads();
   bool hitFirstFriction = false;
   for (int i = 0; i < n; i++) {
+    D.nC = uni(D.nC);
+    D.nN = uni(D.nN);
     if (!hitFirstFriction && rdli(D.findex, i) >= 0) {
       __syncthreads();
       if (lane < n) scr[D.p] = D.x;
@@ -423,7 +588,9 @@ __device__ bool waveDantzig(int n, double* A, double* Lbuf, double* scr, double&
       __syncthreads();
       hitFirstFriction = true;
     }
+    LP_BEGIN();
     const double wi = D.AiC(i, D.x) + D.AiN(i, D.x) - rdl(D.b, i);
+    LP_END(D.prof, 4);
     if (lane == i) D.w = wi;
     const double loi = rdl(D.lo, i), hii = rdl(D.hi, i);
     if (loi == 0 && wi >= 0) {
@@ -437,6 +604,8 @@ __device__ bool waveDantzig(int n, double* A, double* Lbuf, double* scr, double&
       D.transferToC(i);
     } else {
       for (;;) {
+        D.nC = uni(D.nC);
+        D.nN = uni(D.nN);
         const double wiNow = rdl(D.w, i);
         int dir;
         double dirf;
@@ -444,6 +613,7 @@ __device__ bool waveDantzig(int n, double* A, double* Lbuf, double* scr, double&
         D.solve1(i, dir, false);
         const int nC = D.nC, nN = D.nN;
         const bool inN = lane >= nC && lane < nC + nN;
+        LP_BEGIN();
         {
           double acc = 0.0;
 #pragma unroll 4
@@ -493,6 +663,11 @@ __device__ bool waveDantzig(int n, double* A, double* Lbuf, double* scr, double&
         }
         pivots++;
         if (dbg && lane == 0) { dbg[0] = pivots; dbg[1] = i; }
+        LP_END(D.prof, 5);
+#ifdef LCP_PROFILE
+        if (dbg && lane == 0)
+          for (int k = 0; k < 8; k++) dbg[2 + k] = (double)D.prof[k];
+#endif
         if (s <= 0.0) return false;
         if (lane < nC) D.x += s * D.deltaX;
         if (lane == i) D.x += s * dirf;

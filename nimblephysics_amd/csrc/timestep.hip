@@ -542,8 +542,8 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
     double* sn = snapshot + (size_t)env * snapDoubles;
     dynCacheCopy(md, s, L, sn + L.snDyn, false, lane);  // the forward's kinematics, IC, L, C
     STAMP(21);
-    const int nc = md.numPairs > 0 ? (int)sn[SN_NC] : 0;
-    const int m = md.numPairs > 0 ? (int)sn[SN_M] : 0;
+    const int nc = md.numPairs > 0 ? uni((int)sn[SN_NC]) : 0;
+    const int m = md.numPairs > 0 ? uni((int)sn[SN_M]) : 0;
     double* x = s + L.x;
     double* w = s + L.w;
     BwdPool P;

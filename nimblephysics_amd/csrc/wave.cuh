@@ -12,6 +12,16 @@ __device__ __forceinline__ double rdl(double v, int l) {
 }
 __device__ __forceinline__ int rdli(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
+// Scalar (SGPR) copy of a value all lanes hold equally -- counts and flags
+// read from LDS or global memory look lane-varying to the compiler, which
+// then turns every loop and branch on them into exec-masked vector code.
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ double unid(double v) {
+  const int lo = __builtin_amdgcn_readfirstlane(__double2loint(v));
+  const int hi = __builtin_amdgcn_readfirstlane(__double2hiint(v));
+  return __hiloint2double(hi, lo);
+}
+
 template <int CTRL>
 __device__ __forceinline__ double dppd(double v) {
   const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);

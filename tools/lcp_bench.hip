@@ -1,0 +1,73 @@
+// Stand-alone harness for the wave LCP solvers (tools/lcp_bench.py): one
+// problem per 64-lane workgroup, A staged in LDS as in the forward kernel,
+// shader clocks of each solver written per problem.  Built with
+// -DLCP_PROFILE for the Dantzig per-phase split.
+#include "../nimblephysics_amd/csrc/lcp_wave.cuh"
+
+struct Rec {  // per problem output (doubles)
+  enum { OK_D = 0, CLK_D, OK_P, CLK_P, PIV, PIVROW, PGS_IT, PROF = 8, X_D = 16, X_P = 64, PGSPROF = 112, SIZE = 120 };
+};
+
+extern "C" __global__ void __launch_bounds__(64)
+lcp_bench_kernel(int nmax, int nl, const int* nArr, const double* Ag, const double* bg, const double* log_,
+                 const double* hig, const int* fig, const double* x0g, double* out) {
+  extern __shared__ double lds[];
+  const int lane = threadIdx.x;
+  const int pb = blockIdx.x;
+  const int n = nArr[pb];
+  const int ldA = nl * nl;
+  double* A = lds;
+  double* M1 = A + ldA;
+  double* Lb = M1 + ldA;
+  double* scr = Lb + nl * (nl | 1);
+  double* o = out + (size_t)pb * Rec::SIZE;
+  for (int t = lane; t < n * n; t += 64) A[t] = Ag[(size_t)pb * nmax * nmax + t];
+  __syncthreads();
+  const double b = lane < n ? bg[pb * nmax + lane] : 0.0;
+  const double lo = lane < n ? log_[pb * nmax + lane] : 0.0;
+  const double hi = lane < n ? hig[pb * nmax + lane] : 0.0;
+  const int fi = lane < n ? fig[pb * nmax + lane] : -1;
+  double dbg[16];
+  for (int k = 0; k < 16; k++) dbg[k] = 0.0;
+  __shared__ double dshared[24];
+  if (lane < 24) dshared[lane] = 0.0;
+  __syncthreads();
+
+  for (int t = lane; t < n * n; t += 64) M1[t] = A[t];
+  __syncthreads();
+  long long t0 = __builtin_amdgcn_s_memtime();
+  double xd = 0.0;
+  const bool okD = waveDantzig(n, M1, Lb, scr, xd, b, lo, hi, fi, lane, dshared);
+  long long t1 = __builtin_amdgcn_s_memtime();
+  __syncthreads();
+  double xp = lane < n ? x0g[pb * nmax + lane] : 0.0;
+  long long t2 = __builtin_amdgcn_s_memtime();
+  const bool okP = wavePgs(n, A, xp, b, lo, hi, fi, lane, dshared + 12);
+  long long t3 = __builtin_amdgcn_s_memtime();
+  __syncthreads();
+  (void)dbg;
+  if (lane == 0) {
+    o[Rec::OK_D] = okD ? 1 : 0;
+    o[Rec::CLK_D] = (double)(t1 - t0);
+    o[Rec::OK_P] = okP ? 1 : 0;
+    o[Rec::CLK_P] = (double)(t3 - t2);
+    o[Rec::PIV] = dshared[0];
+    o[Rec::PIVROW] = dshared[1];
+    o[Rec::PGS_IT] = dshared[12];
+    o[Rec::PGS_IT + 1] = dshared[13];
+    for (int k = 0; k < 3; k++) o[Rec::PGSPROF + k] = dshared[14 + k];
+    for (int k = 0; k < 8; k++) o[Rec::PROF + k] = dshared[2 + k];
+  }
+  if (lane < n) {
+    o[Rec::X_D + lane] = xd;
+    o[Rec::X_P + lane] = xp;
+  }
+}
+
+extern "C" int lcp_bench_launch(int P, int nmax, int nl, const int* nArr, const double* A, const double* b, const double* lo,
+                                const double* hi, const int* fi, const double* x0, double* out, void* stream) {
+  const size_t lds = (size_t)(2 * nl * nl + nl * (nl | 1) + 64) * sizeof(double);
+  hipLaunchKernelGGL(lcp_bench_kernel, dim3(P), dim3(64), lds, (hipStream_t)stream, nmax, nl, nArr, A, b, lo, hi, fi, x0,
+                     out);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}

@@ -29,6 +29,18 @@ class BatchState:
         self.cache[:, 0] = -1.0  # empty cache
 
 
+def _action_index(world: World, device) -> torch.Tensor:
+    """Device copy of the action space's dof indices, made once per world and
+    device (a pageable host->device copy per step would serialise the host
+    with the stream)."""
+    space = tuple(world.getActionSpace())
+    cached = getattr(world, "_action_index", None)
+    if cached is None or cached[0] != space or cached[1].device != device:
+        cached = (space, torch.tensor(space, dtype=torch.long, device=device))
+        world._action_index = cached
+    return cached[1]
+
+
 def _batch_state(world: World, batch: int, dev, device) -> BatchState:
     bs = getattr(world, "_batch_state", None)
     if bs is None or bs.batch != batch or bs.cache.device != device or bs.cache.shape[1] != dev.cache_doubles:
@@ -50,11 +62,10 @@ class TimestepLayer(torch.autograd.Function):
         n = world.getNumDofs()
         if st.shape[1] != 2 * n:
             raise ValueError(f"state has {st.shape[1]} columns, world expects {2 * n}")
-        space = world.getActionSpace()
-        if act.shape[1] != len(space):
-            raise ValueError(f"action has {act.shape[1]} columns, action space has {len(space)}")
+        idx = _action_index(world, st.device)
+        if act.shape[1] != idx.shape[0]:
+            raise ValueError(f"action has {act.shape[1]} columns, action space has {idx.shape[0]}")
         dev = world.native()
-        idx = torch.tensor(space, dtype=torch.long, device=st.device)
         forces = torch.zeros((B, n), dtype=torch.float64, device=st.device)
         forces.index_copy_(1, idx, act.contiguous())
         bs = _batch_state(world, B, dev, st.device)

@@ -69,14 +69,17 @@ static Layout makeLayout(const ModelDev& m, bool backward, int poolRows) {
   L.v1 = take(n);
   L.ct = take(!backward && m.numPairs > 0 ? ctDoubles() : 16);
   if (backward) {
-    L.scratch = take(24 * 6);
-    // B1, B23, B4 contiguous: reused for the 8 x nb x 12 M-derivative fields
-    L.B1 = take(36 * nb); L.B23 = take(36 * nb); L.B4 = take(36 * nb);
-    L.P = take(6 * nb); L.H = take(6 * nb); L.w = take(n); L.gp = take(n); L.gv = take(n); L.out = take(3 * n);
+    // adjoint vectors (alpha..kappa per body); afterwards the workspace of
+    // the contact-geometry terms, the M-derivative field pairs and the free
+    // joint finite differences
+    L.adj = take(42 * nb > 24 * 6 ? 42 * nb : 24 * 6); L.Wt = take(6 * nb);
+    L.scratch = L.adj;
+    L.w = take(n); L.gp = take(n); L.gv = take(n);
     L.poolCap = 0;
     if (m.numPairs > 0 && poolRows > 0) L.poolCap = bwdPoolDoublesHost(poolRows, n);
     L.pool = take(L.poolCap);
-    L.V = take(6 * nb); L.A = take(6 * nb); L.IC = take(36 * nb); L.F = take(6 * nb);
+    L.V = take(6 * nb); L.A = take(6 * nb); L.F = take(6 * nb);
+    L.IC = -1;  // composite inertias are not needed by the adjoint backward
   } else {
     // V, A, IC, F last: after the dynamics they are dead and the contact
     // stage (narrow-phase buffers, then the LCP pool) reuses the space
@@ -206,14 +209,28 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
   int maxContacts = 8 * m.numPairs;
   if (maxContacts > NIMBLE_MAX_CONTACTS) maxContacts = NIMBLE_MAX_CONTACTS;
   const int mcap = 3 * maxContacts;
-  int poolRows = ldsPoolRows(m, mcap);
+  int fwdRows = ldsPoolRows(m, mcap);
   for (;;) {
-    w->fwd = makeLayout(m, false, poolRows);
-    w->bwd = makeLayout(m, true, poolRows);
-    if (w->bwd.total * 8 <= 160 * 1024 && w->fwd.total * 8 <= 160 * 1024) break;
-    if (poolRows == 0) { delete w; return fail(NIMBLE_ERR_UNSUPPORTED, "model too large for LDS"); }
-    poolRows = poolRows > 6 ? poolRows - 6 : 0;
+    w->fwd = makeLayout(m, false, fwdRows);
+    if (w->fwd.total * 8 <= 160 * 1024) break;
+    if (fwdRows == 0) { delete w; return fail(NIMBLE_ERR_UNSUPPORTED, "model too large for LDS"); }
+    fwdRows = fwdRows > 6 ? fwdRows - 6 : 0;
   }
+  // The backward kernel is occupancy-bound: its pool gets the rows that keep
+  // a world within a quarter of the CU's LDS (4 worlds per CU), worlds with
+  // more rows use the HBM workspace; failing that, whatever fits at all.
+  int bwdRows = -1;
+  for (int r = fwdRows; r >= 0; r--)
+    if (makeLayout(m, true, r).total * 8 <= 40 * 1024) { bwdRows = r; break; }
+  if (bwdRows < 0)
+    for (int r = fwdRows; r >= 0; r--)
+      if (makeLayout(m, true, r).total * 8 <= 160 * 1024) { bwdRows = r; break; }
+  if (bwdRows < 0) { delete w; return fail(NIMBLE_ERR_UNSUPPORTED, "model too large for LDS"); }
+  w->bwd = makeLayout(m, true, bwdRows);
+  if (getenv("NIMBLE_AMD_VERBOSE"))
+    fprintf(stderr, "nimble_amd: LDS forward %d B (pool rows %d), backward %d B (pool rows %d), max rows %d\n",
+            w->fwd.total * 8, fwdRows, w->bwd.total * 8, bwdRows, mcap);
+  const int poolRows = fwdRows < bwdRows ? fwdRows : bwdRows;
   w->poolRows = poolRows;
   w->maxRows = mcap;
   if (m.numPairs > 0) {

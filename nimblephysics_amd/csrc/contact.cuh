@@ -1391,47 +1391,52 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
 // with V_x,b the world twist of body b under joint rates x and H_x(k) the
 // subtree momentum sum_{b in sub(k)} I_b V_x,b.  Fields live in `buf`
 // (8 fields x nb x 12 doubles: V then H).
-__device__ void mFieldsBuild(const ModelDev& md, double* s, const Layout& L, const double* NV, double* buf, int lane) {
+// M-derivative terms: for the four (a, c) column pairs of NV, the fields
+// are body twists V = sum a_k S_k and subtree momenta H = sum I V; a dof k on
+// body b (parent l) gets -(Z x V_l^c) . H_b^a - (Z x V_l^a) . H_b^c.  Pairs are
+// built one at a time (2 x nb x 12 doubles of workspace), momenta summed
+// level-parallel.
+__device__ double mFieldsTerm(const ModelDev& md, double* s, const Layout& L, const double* NV, double* buf, int lane,
+                              int k, const double* Z, double coefDelta, double imp) {
   const int nb = md.nb;
-  for (int t = lane; t < 8 * nb; t += WAVE) {
-    const int f = t / nb, b = t % nb;
-    double* V = buf + (f * nb + b) * 12;
-    bodyTwist(md, s + L.Sw, b, NV + f, NV_COLS, V);
-    double I[36];
-    worldInertia(md, s + L.Tw + 12 * b, b, I);
-    mv6(I, V, V + 6);
-  }
-  __syncthreads();
-  for (int b = nb - 1; b > 0; b--) {
-    const int p = md.parent[b];
-    if (p >= 0 && lane < 48) {
-      const int f = lane / 6, i = lane % 6;
-      buf[(f * nb + p) * 12 + 6 + i] += buf[(f * nb + b) * 12 + 6 + i];
-    }
-    __syncthreads();
-  }
-}
-
-__device__ double mFieldsEval(const ModelDev& md, const double* buf, int k, const double* Z, double coefDelta,
-                              double imp) {
-  const int nb = md.nb;
-  const int bk = md.dofBody[k];
-  const int lam = md.parent[bk];
   const double coef[4] = {coefDelta, 1.0, -imp, -imp};
   double total = 0.0;
   for (int pr = 0; pr < 4; pr++) {
-    const int fa = 2 * pr, fc = 2 * pr + 1;
-    const double* Ha = buf + (fa * nb + bk) * 12 + 6;
-    const double* Hc = buf + (fc * nb + bk) * 12 + 6;
-    double val = 0.0;
-    if (lam >= 0) {
-      double t[6];
-      crm(Z, buf + (fc * nb + lam) * 12, t);
-      val -= dot6(t, Ha);
-      crm(Z, buf + (fa * nb + lam) * 12, t);
-      val -= dot6(t, Hc);
+    for (int t = lane; t < 2 * nb; t += WAVE) {
+      const int f = t / nb, b = t % nb;
+      double* V = buf + (f * nb + b) * 12;
+      bodyTwist(md, s + L.Sw, b, NV + 2 * pr + f, NV_COLS, V);
+      double I[36];
+      worldInertia(md, s + L.Tw + 12 * b, b, I);
+      mv6(I, V, V + 6);
     }
-    total += coef[pr] * val;
+    __syncthreads();
+    for (int lev = md.maxDepth - 1; lev >= 0; lev--) {
+      const int b0 = md.levelStart[lev], cnt = (md.levelStart[lev + 1] - b0) * 12;
+      for (int t = lane; t < cnt; t += WAVE) {
+        const int p = md.levelBodies[b0 + t / 12], e = t % 12, f = e / 6, i = 6 + e % 6;
+        double acc = buf[(f * nb + p) * 12 + i];
+        for (int q = md.childStart[p]; q < md.childStart[p + 1]; q++) acc += buf[(f * nb + md.childList[q]) * 12 + i];
+        buf[(f * nb + p) * 12 + i] = acc;
+      }
+      __syncthreads();
+    }
+    if (k < md.n) {
+      const int bk = md.dofBody[k];
+      const int lam = md.parent[bk];
+      const double* Ha = buf + bk * 12 + 6;
+      const double* Hc = buf + (nb + bk) * 12 + 6;
+      double val = 0.0;
+      if (lam >= 0) {
+        double t[6];
+        crm(Z, buf + (nb + lam) * 12, t);
+        val -= dot6(t, Ha);
+        crm(Z, buf + lam * 12, t);
+        val -= dot6(t, Hc);
+      }
+      total += coef[pr] * val;
+    }
+    __syncthreads();
   }
   return total;
 }

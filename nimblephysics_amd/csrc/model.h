@@ -47,8 +47,8 @@ struct ModelDev {
 // LDS layout (in doubles) for one world instance; offsets computed on host.
 struct Layout {
   int q, v, tau, Tw, Sw, V, A, IC, F, M, rhs, x, scratch;
-  // backward extras
-  int B1, B23, B4, P, H, w, gp, gv, out;
+  // backward extras: per-body adjoint vectors (7 x 6) and W, dof vectors
+  int adj, Wt, w, gp, gv;
   // contacts: stage header/lists, post-dynamics velocity, LCP workspace pool
   int ct, v1, pool, poolCap, dinv;
   // offset (doubles) of the dynamics cache inside each world's snapshot

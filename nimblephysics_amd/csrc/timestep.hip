@@ -288,6 +288,7 @@ __device__ void dynCacheCopy(const ModelDev& md, double* s, const Layout& L, dou
   int o = 0;
   for (int k = 0; k < 7; k++) {
     const int base = seg[k][0], cnt = seg[k][1];
+    if (base < 0) { o += cnt; continue; }  // region not kept in this kernel's LDS
     if (store)
       for (int t = lane; t < cnt; t += WAVE) cache[o + t] = s[base + t];
     else
@@ -405,103 +406,89 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, con
 // as vector-Jacobian products, no full Jacobian is ever formed.
 // ---------------------------------------------------------------------------
 
-// Per-body derivative composites at the state (q, v, a*):
-//   P = sum I u,  H = sum I V,  F = sum (I u + V x* I V),
-//   B1 = sum I [V x],  B23 = sum ([V x*] G(h) - G(h) [V x]),  B4 = sum [V x*] I
-// with u = A - a_g, h = I V and G(h) m := m x* h.
-__device__ void derivativeComposites(const ModelDev& md, double* s, const Layout& L, int lane) {
+// Adjoint (vector-Jacobian) form of the world-frame RNEA derivatives.  The
+// backward needs w^T dtau/dq and w^T dtau/dqdot at a* for the dynamics
+// adjoint w = Minv gv.  With W_c = sum of w_i S_i over the dofs of c and its
+// ancestors, per-body 6-vectors
+//   alpha = W x* p,  beta = I W,  gamma = -V x* beta,  eps = W x* h,
+//   delta = (V x W) x* h - V x* eps,  zeta = -I (V x W),
+//   kappa = (W - W_parent) x* F
+// (p = I (A - a_g), h = I V, F the composite force) and their subtree sums
+// (A, B, Gam, D, E, Zt, K), a dof k on body b with parent l gives
+//   w^T dtau/dq_k    = Z_k . [-A - u_l x* B + V_l x* (Gam + V_l x* B + E - Zt) + D + K]
+//   w^T dtau/dqdot_k = S_k . [-(V_l + V_b) x* B - Gam - E + Zt]
+// (Z_k the subtree's world twist per unit q_k, u_l = A_l - a_g).  This is the
+// per-direction sum over subtree bodies of the reference's dID/dq columns
+// (Skeleton::getJacobianOfID, DifferentiableContactConstraint / BackpropSnapshot
+// use) contracted with w, collapsed to O(nb) 6-vector work; the identity is
+// checked against central differences in tools/proto/adjoint_rnea.py.
+__device__ void adjointVectors(const ModelDev& md, double* s, const Layout& L, int lane) {
   const double ag[6] = {0, 0, 0, md.g[0], md.g[1], md.g[2]};
-  if (lane < md.nb) {
+  const int nb = md.nb, n = md.n;
+  if (lane < nb) {
     const int b = lane;
+    double W[6] = {0, 0, 0, 0, 0, 0};
+    for (int k = 0; k < n; k++)  // dofs in topological order: ancestors first
+      if ((md.anc[b] >> md.dofBody[k]) & 1ull) {
+        const double wk = s[L.w + k];
+        for (int i = 0; i < 6; i++) W[i] += wk * s[L.Sw + 6 * k + i];
+      }
     double I[36];
     worldInertia(md, s + L.Tw + 12 * b, b, I);
     const double* V = s + L.V + 6 * b;
-    double u[6], h[6], Iu[6], vxh[6];
+    double u[6], p[6], h[6], t[6], t2[6], VxW[6];
     for (int i = 0; i < 6; i++) u[i] = s[L.A + 6 * b + i] - ag[i];
-    mv6(I, u, Iu);
+    mv6(I, u, p);
     mv6(I, V, h);
-    crf(V, h, vxh);
+    crf(V, h, t);
     for (int i = 0; i < 6; i++) {
-      s[L.P + 6 * b + i] = Iu[i];
-      s[L.H + 6 * b + i] = h[i];
-      s[L.F + 6 * b + i] = Iu[i] + vxh[i];
+      s[L.F + 6 * b + i] = p[i] + t[i];  // f_b, summed over the subtree below
+      s[L.Wt + 6 * b + i] = W[i];
     }
-    // column-wise products: column c of each matrix is the image of e_c
-    for (int c = 0; c < 6; c++) {
-      double e[6] = {0, 0, 0, 0, 0, 0};
-      e[c] = 1.0;
-      double vxe[6], t1[6], t2[6], t3[6], Gh[6];
-      crm(V, e, vxe);          // [V x] e
-      mv6(I, vxe, t1);         // B1 col
-      // G(h) e = e x* h ;  [V x*] G(h) e
-      crf(e, h, Gh);
-      crf(V, Gh, t2);
-      // G(h) [V x] e = (V x e) x* h
-      crf(vxe, h, t3);
-      double Ie[6], t4[6];
-      for (int r = 0; r < 6; r++) Ie[r] = I[r * 6 + c];
-      crf(V, Ie, t4);          // [V x*] I e
-      for (int r = 0; r < 6; r++) {
-        s[L.B1 + 36 * b + r * 6 + c] = t1[r];
-        s[L.B23 + 36 * b + r * 6 + c] = t2[r] - t3[r];
-        s[L.B4 + 36 * b + r * 6 + c] = t4[r];
-      }
-    }
+    double* a = s + L.adj + 42 * b;
+    crf(W, p, a);           // alpha
+    mv6(I, W, a + 6);       // beta
+    crf(V, a + 6, t);
+    for (int i = 0; i < 6; i++) a[12 + i] = -t[i];  // gamma
+    crf(W, h, a + 24);      // eps
+    crm(V, W, VxW);
+    crf(VxW, h, t);
+    crf(V, a + 24, t2);
+    for (int i = 0; i < 6; i++) a[18 + i] = t[i] - t2[i];  // delta
+    mv6(I, VxW, t);
+    for (int i = 0; i < 6; i++) a[30 + i] = -t[i];  // zeta
   }
   __syncthreads();
+  // subtree sums of alpha..zeta and f (-> composite F), deepest level first
   for (int lev = md.maxDepth - 1; lev >= 0; lev--) {
-    const int b0 = md.levelStart[lev], cnt = (md.levelStart[lev + 1] - b0) * 126;
+    const int b0 = md.levelStart[lev], cnt = (md.levelStart[lev + 1] - b0) * 42;
     for (int t = lane; t < cnt; t += WAVE) {
-      const int p = md.levelBodies[b0 + t / 126], e = t % 126;
-      int off, stride;
-      if (e < 36) { off = L.B1 + e; stride = 36; }
-      else if (e < 72) { off = L.B23 + (e - 36); stride = 36; }
-      else if (e < 108) { off = L.B4 + (e - 72); stride = 36; }
-      else if (e < 114) { off = L.P + (e - 108); stride = 6; }
-      else if (e < 120) { off = L.H + (e - 114); stride = 6; }
-      else { off = L.F + (e - 120); stride = 6; }
+      const int p = md.levelBodies[b0 + t / 42], e = t % 42;
+      const int off = e < 36 ? L.adj + e : L.F + (e - 36);
+      const int stride = e < 36 ? 42 : 6;
       double acc = s[off + stride * p];
       for (int q = md.childStart[p]; q < md.childStart[p + 1]; q++) acc += s[off + stride * md.childList[q]];
       s[off + stride * p] = acc;
     }
     __syncthreads();
   }
-}
-
-// dF_c for a subtree motion with generator Z and base (V_lambda, u_lambda):
-__device__ void dForcePos(const double* s, const Layout& L, int c, const double* Z, const double* Vl,
-                          const double* ul, const double* Psi, const double* ZxVl, double* out) {
-  const double* IC = s + L.IC + 36 * c;
-  double t[6], a[6], r[6];
-  crf(Z, s + L.P + 6 * c, r);                   //  Z x* P
-  crm(Z, ul, t); mv6(IC, t, a);                 // -IC (Z x u_l)
-  for (int i = 0; i < 6; i++) r[i] -= a[i];
-  mv6(s + L.B1 + 36 * c, Psi, a);               // -B1 Psi
-  for (int i = 0; i < 6; i++) r[i] -= a[i];
-  crm(Psi, Vl, t); mv6(IC, t, a);               // -IC (Psi x V_l)
-  for (int i = 0; i < 6; i++) r[i] -= a[i];
-  mv6(s + L.B23 + 36 * c, Z, a);                // +B23 Z
-  for (int i = 0; i < 6; i++) r[i] += a[i];
-  crf(ZxVl, s + L.H + 6 * c, a);                // -(Z x V_l) x* H
-  for (int i = 0; i < 6; i++) r[i] -= a[i];
-  mv6(s + L.B4 + 36 * c, ZxVl, a);              // -B4 (Z x V_l)
-  for (int i = 0; i < 6; i++) out[i] = r[i] - a[i];
-}
-
-__device__ void dForceVel(const double* s, const Layout& L, int c, const double* S, const double* Vl,
-                          const double* Vb, double* out) {
-  const double* IC = s + L.IC + 36 * c;
-  double t1[6], t2[6], a[6], r[6];
-  crm(Vl, S, t1);
-  crm(S, Vb, t2);
-  for (int i = 0; i < 6; i++) t1[i] -= t2[i];
-  mv6(IC, t1, r);                               // IC (V_l x S - S x V_b)
-  mv6(s + L.B1 + 36 * c, S, a);                 // -B1 S
-  for (int i = 0; i < 6; i++) r[i] -= a[i];
-  crf(S, s + L.H + 6 * c, a);                   // +S x* H
-  for (int i = 0; i < 6; i++) r[i] += a[i];
-  mv6(s + L.B4 + 36 * c, S, a);                 // +B4 S
-  for (int i = 0; i < 6; i++) out[i] = r[i] + a[i];
+  if (lane < nb) {
+    const int b = lane, par = md.parent[b];
+    double d[6];
+    for (int i = 0; i < 6; i++) d[i] = s[L.Wt + 6 * b + i] - (par >= 0 ? s[L.Wt + 6 * par + i] : 0.0);
+    crf(d, s + L.F + 6 * b, s + L.adj + 42 * b + 36);  // kappa
+  }
+  __syncthreads();
+  for (int lev = md.maxDepth - 1; lev >= 0; lev--) {
+    const int b0 = md.levelStart[lev], cnt = (md.levelStart[lev + 1] - b0) * 6;
+    for (int t = lane; t < cnt; t += WAVE) {
+      const int p = md.levelBodies[b0 + t / 6], e = 36 + t % 6;
+      double acc = s[L.adj + 42 * p + e];
+      for (int q = md.childStart[p]; q < md.childStart[p + 1]; q++) acc += s[L.adj + 42 * md.childList[q] + e];
+      s[L.adj + 42 * p + e] = acc;
+    }
+    __syncthreads();
+  }
 }
 
 // Right Jacobian of SO(3) exp (J_r(th) = I - (1-cos)/t^2 [th] + (t-sin)/t^3 [th]^2)
@@ -570,7 +557,7 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
     }
     STAMP(22);
     accelerations(md, s, L, lane, x);  // A = accelerations at a*
-    derivativeComposites(md, s, L, lane);
+    adjointVectors(md, s, L, lane);
     STAMP(23);
 
     // ---- per-direction columns -------------------------------------------
@@ -606,44 +593,20 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
       } else {
         for (int i = 0; i < 6; i++) Z[i] = Sk[i];
       }
-      double Psi[6], ZxVl[6];
-      crm(Vl, Z, Psi);
-      crm(Z, Vl, ZxVl);
-      double dFb[6], dFbv[6];
-      dForcePos(s, L, b, Z, Vl, ul, Psi, ZxVl, dFb);
-      dForceVel(s, L, b, Sk, Vl, s + L.V + 6 * b, dFbv);
-      double accQ = 0.0, accV = 0.0;
-      for (int c = 0; c < md.nb; c++) {
-        const int nd = md.ndof[c];
-        if (nd == 0) continue;
-        const bool inSub = (md.anc[c] >> b) & 1ull;
-        const bool isAnc = ((md.anc[b] >> c) & 1ull) && c != b;
-        if (!inSub && !isAnc) continue;
-        const int o = md.dof0[c];
-        if (inSub) {
-          double dF[6], dFv[6];
-          if (c == b) {
-            for (int i = 0; i < 6; i++) { dF[i] = dFb[i]; dFv[i] = dFbv[i]; }
-          } else {
-            dForcePos(s, L, c, Z, Vl, ul, Psi, ZxVl, dF);
-            dForceVel(s, L, c, Sk, Vl, s + L.V + 6 * b, dFv);
-          }
-          const double* Fc = s + L.F + 6 * c;
-          for (int j = 0; j < nd; j++) {
-            const double* Sj = s + L.Sw + 6 * (o + j);
-            double zs[6];
-            crm(Z, Sj, zs);
-            accQ += w[o + j] * (dot6(Sj, dF) + dot6(zs, Fc));
-            accV += w[o + j] * dot6(Sj, dFv);
-          }
-        } else {
-          for (int j = 0; j < nd; j++) {
-            const double* Sj = s + L.Sw + 6 * (o + j);
-            accQ += w[o + j] * dot6(Sj, dFb);
-            accV += w[o + j] * dot6(Sj, dFbv);
-          }
-        }
-      }
+      // adjoint contraction at body b (subtree sums, see adjointVectors)
+      const double* a = s + L.adj + 42 * b;
+      double t[6], r[6], acc6[6];
+      crf(Vl, a + 6, t);  // V_l x* B
+      for (int i = 0; i < 6; i++) r[i] = a[12 + i] + t[i] + a[24 + i] - a[30 + i];
+      crf(Vl, r, t);
+      crf(ul, a + 6, r);  // u_l x* B
+      for (int i = 0; i < 6; i++) acc6[i] = -a[i] - r[i] + t[i] + a[18 + i] + a[36 + i];
+      const double accQ = dot6(Z, acc6);
+      double vs[6];
+      for (int i = 0; i < 6; i++) vs[i] = Vl[i] + s[L.V + 6 * b + i];
+      crf(vs, a + 6, t);
+      for (int i = 0; i < 6; i++) acc6[i] = -t[i] - a[12 + i] - a[24 + i] + a[30 + i];
+      const double accV = dot6(Sk, acc6);
       const double wk = w[k];
       gq = -dt * accQ - dt * md.spring[k] * wk;
       gvOut = s[L.gv + k] - dt * accV - dt * md.damping[k] * wk - dt * dt * md.spring[k] * wk;
@@ -658,15 +621,15 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
     __syncthreads();
     STAMP(24);
     if (nc > 0) {
-      // B1/B23/B4 are dead now: workspace for the contact-geometry terms,
-      // then for the M-derivative fields
-      double* buf = s + L.B1;
+      // the adjoint vectors are dead now: workspace for the contact-geometry
+      // terms (6n + 6nb <= 42nb), then for the M-derivative field pairs (24nb)
+      double* buf = s + L.adj;
       const double gterm = contactGTermsAll(md, s, L, sn, P, m, Z, buf, lane);
       __syncthreads();
-      mFieldsBuild(md, s, L, P.NV, buf, lane);
+      const double mterm = mFieldsTerm(md, s, L, P.NV, buf, lane, k, Z, -dt, (double)imp);
       if (k < n) {
         gq += gterm;
-        gq += mFieldsEval(md, buf, k, Z, -dt, (double)imp);
+        gq += mterm;
       }
       __syncthreads();
     }

@@ -277,7 +277,9 @@ int nimble_forward(nimble_world_t w, int32_t batch, const double* state, const d
   if (!state || !forces || !next_state || !snapshot || !lcp_cache) return fail(NIMBLE_ERR_INVALID, "null buffer");
   hipStream_t st = (hipStream_t)stream;
   const size_t lds = (size_t)w->fwd.total * sizeof(double);
-  hipLaunchKernelGGL(nimble_forward_kernel, dim3(gridFor(batch)), dim3(64), lds, st, w->dev, w->fwd, batch, state,
+  // contact models: a second (helper) wave per world for the LCP fallback
+  const int fwdThreads = w->host.numPairs > 0 ? 128 : 64;
+  hipLaunchKernelGGL(nimble_forward_kernel, dim3(gridFor(batch)), dim3(fwdThreads), lds, st, w->dev, w->fwd, batch, state,
                      forces, lcp_cache, next_state, snapshot, w->snapDoubles, w->cacheDoubles);
   HIP_TRY(hipGetLastError());
   return NIMBLE_OK;

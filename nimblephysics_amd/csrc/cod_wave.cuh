@@ -43,9 +43,19 @@ __device__ inline double* carveCod(double* w, double* A, int m, int n, int ld, C
 // the sequential scan), alpha and |v|^2 are wave reductions, and the
 // reflector pass (lane = column) also recomputes the next step's partial
 // column norms (same sums as a fresh recomputation).  Requires n <= 64.
-// `cn` is unused (kept for the call signature), `v` holds m doubles.
-__device__ void codFactor(Cod& c, double* cn, double* v, int lane) {
-  (void)cn;
+// Factorises the m x n matrix A (leading dimension ld) in place; ws is the
+// carveCod workspace, v a further m doubles of scratch.
+template <bool kLds>
+__device__ void codFactor(typename Space<kLds>::dptr Ain, typename Space<kLds>::dptr wsIn, int m_, int n_, int ld_,
+                          typename Space<kLds>::dptr vIn, int lane, double* prof = nullptr) {
+#ifdef NIMBLE_STAGE_TIMING
+  const long long tc0 = (long long)__builtin_amdgcn_s_memtime();
+#else
+  (void)prof;
+#endif
+  Cod c;
+  carveCod((double*)wsIn, (double*)Ain, uni(m_), uni(n_), uni(ld_), c);
+  double* v = (double*)vIn;
   double* A = c.A;
   const int m = c.m, n = c.n, ld = c.ld;
   if (lane < n) c.perm[lane] = lane;
@@ -54,7 +64,7 @@ __device__ void codFactor(Cod& c, double* cn, double* v, int lane) {
 #pragma unroll 8
     for (int i = 0; i < m; i++) norm += A[i * ld + lane] * A[i * ld + lane];
   }
-  __syncthreads();
+  WSYNC();
   double maxPivot = 0.0;
   for (int k = 0; k < c.kmax; k++) {
     // pivot: largest remaining norm, lowest index on ties
@@ -70,7 +80,7 @@ __device__ void codFactor(Cod& c, double* cn, double* v, int lane) {
       else if (lane == p) norm = nk;
       if (lane == 0) { int t = c.perm[k]; c.perm[k] = c.perm[p]; c.perm[p] = t; }
     }
-    __syncthreads();
+    WSYNC();
     const double akk = A[k * ld + k];
     const double colv = (lane >= k && lane < m) ? A[lane * ld + k] : 0.0;
     double alpha = sqrt(waveSum(colv * colv));
@@ -83,14 +93,14 @@ __device__ void codFactor(Cod& c, double* cn, double* v, int lane) {
         for (int i = k + 1; i < m; i++) nrm += A[i * ld + lane] * A[i * ld + lane];
         norm = nrm;
       }
-      __syncthreads();
+      WSYNC();
       continue;
     }
     if (akk > 0) alpha = -alpha;
     const double vi = (lane == k) ? colv - alpha : colv;
     if (lane >= k && lane < m) v[lane] = vi;
     const double vnorm = waveSum(vi * vi);
-    __syncthreads();
+    WSYNC();
     if (lane >= k && lane < n) {
       double nrm = 0.0;
       if (vnorm > 0) {
@@ -110,12 +120,15 @@ __device__ void codFactor(Cod& c, double* cn, double* v, int lane) {
       }
       norm = nrm;
     }
-    __syncthreads();
+    WSYNC();
     maxPivot = fmax(maxPivot, fabs(A[k * ld + k]));
     if (lane > k && lane < m) A[lane * ld + k] = v[lane];
     if (lane == 0) { c.vd[k] = v[k]; c.vn[k] = vnorm; }
-    __syncthreads();
+    WSYNC();
   }
+#ifdef NIMBLE_STAGE_TIMING
+  const long long tc1 = (long long)__builtin_amdgcn_s_memtime();
+#endif
   const double thr = 2.220446049250313e-16 * c.kmax * maxPivot;
   int r = 0;
   for (int k = 0; k < c.kmax; k++)
@@ -132,7 +145,7 @@ __device__ void codFactor(Cod& c, double* cn, double* v, int lane) {
     if (aii > 0) al = -al;
     const double vi = aii - al;
     const double vnz = vi * vi + tail;
-    __syncthreads();
+    WSYNC();
     if (lane == 0) { c.zd[i] = vi; c.zn[i] = vnz; }
     if (vnz != 0) {
       for (int row = lane; row <= i; row += WAVE) {
@@ -146,8 +159,14 @@ __device__ void codFactor(Cod& c, double* cn, double* v, int lane) {
           for (int j = r; j < n; j++) A[row * ld + j] -= sc * A[i * ld + j];
       }
     }
-    __syncthreads();
+    WSYNC();
   }
-  __syncthreads();
+  WSYNC();
+#ifdef NIMBLE_STAGE_TIMING
+  if (prof && lane == 0) {
+    prof[0] += (double)(tc1 - tc0);
+    prof[1] += (double)((long long)__builtin_amdgcn_s_memtime() - tc1);
+    prof[2] = r;
+  }
+#endif
 }
-

@@ -33,9 +33,17 @@
   do {                                                                             \
     if (lane == 0 && g_stamp) g_stamp[k] = (double)__builtin_amdgcn_s_memtime(); \
   } while (0)
+// accumulating timers (slots >= 60): TACC_BEGIN(t) ... TACC_END(slot, t)
+#define TACC_BEGIN(t) const long long t = (long long)__builtin_amdgcn_s_memtime()
+#define TACC_END(k, t)                                                                            \
+  do {                                                                                            \
+    if (lane == 0 && g_stamp) g_stamp[k] += (double)((long long)__builtin_amdgcn_s_memtime() - t); \
+  } while (0)
 __device__ double* g_stamp_dummy;
 #else
 #define STAMP(k) do { } while (0)
+#define TACC_BEGIN(t) do { } while (0)
+#define TACC_END(k, t) do { } while (0)
 #endif
 
 #define CM_CLAMPING (-1)
@@ -268,7 +276,7 @@ __device__ void tangentBasisODE(const double* n, double* t1, double* t2) {
 
 struct FwdPool {
   double *cols, *massed, *A, *M1, *M2;
-  double *lo, *hi, *b, *X, *aCol, *rest, *pen, *relVel, *fc, *Eval, *nx, *fsol, *xc, *dvec;
+  double *lo, *hi, *b, *X, *aCol, *rest, *pen, *relVel, *fc, *Eval, *nx, *fsol, *xc, *xh, *dvec;
   int *fi, *mapping, *clampIdx, *ubIdx, *rowC, *rowDir, *clampRow, *cl;
   double* scr;  // >= 10 m + 2 n + 16
 };
@@ -280,12 +288,32 @@ __device__ inline void carveFwd(double* base, int m, int n, FwdPool& P) {
   P.A = p; p += m * m;
   P.M1 = p; p += m * m;
   P.M2 = p; p += m * (m | 1);  // Dantzig's L with an odd leading dimension
-  double** vecs[] = {&P.lo, &P.hi, &P.b, &P.X, &P.aCol, &P.rest, &P.pen, &P.relVel, &P.fc, &P.Eval, &P.nx, &P.fsol, &P.xc};
-  for (double** v : vecs) { *v = p; p += m; }
+  // plain member assignments (no pointer-to-member tables) keep the
+  // pointers' provenance visible, so LDS-laundered bases stay LDS
+  P.lo = p; p += m;
+  P.hi = p; p += m;
+  P.b = p; p += m;
+  P.X = p; p += m;
+  P.aCol = p; p += m;
+  P.rest = p; p += m;
+  P.pen = p; p += m;
+  P.relVel = p; p += m;
+  P.fc = p; p += m;
+  P.Eval = p; p += m;
+  P.nx = p; p += m;
+  P.fsol = p; p += m;
+  P.xc = p; p += m;
+  P.xh = p; p += m;  // the helper wave's PGS solution
   P.dvec = p; p += 3 * m;
   int* ip = reinterpret_cast<int*>(p);
-  int** ivecs[] = {&P.fi, &P.mapping, &P.clampIdx, &P.ubIdx, &P.rowC, &P.rowDir, &P.clampRow, &P.cl};
-  for (int** v : ivecs) { *v = ip; ip += m; }
+  P.fi = ip; ip += m;
+  P.mapping = ip; ip += m;
+  P.clampIdx = ip; ip += m;
+  P.ubIdx = ip; ip += m;
+  P.rowC = ip; ip += m;
+  P.rowDir = ip; ip += m;
+  P.clampRow = ip; ip += m;
+  P.cl = ip; ip += m;
   p += 4 * m;
   P.scr = p;
 }
@@ -308,7 +336,44 @@ __device__ inline void carveFwd(double* base, int m, int n, FwdPool& P) {
 #define H_IGN 10
 #define H_K 11
 #define H_CODOK 12  // M1 + scr hold the COD of the final clamping Q
+#define H_HELPER 13 // 2 doubles = 4 ints: helper state, cancel, PGS ok (see helperWave)
 #define H_PAIRCNT 16   // 16 per-pair counts of the current chunk
+
+// ---------------------------------------------------------------------------
+// Helper wave.  The forward kernel runs two waves per world: wave 0 does the
+// step, wave 1 runs the first PGS fallback (PgsBoxedLcpSolver::solve on
+// A + cfm I from the warm start) speculatively while wave 0 runs Dantzig.
+// The reference runs that PGS only once Dantzig has failed, from the same
+// inputs (neither Dantzig nor the validity check touches A, b, lo, hi,
+// findex or the warm start), so taking the helper's result is identical and
+// Dantzig and PGS overlap instead of adding up.  Protocol per world, LDS ints
+// at ct[H_HELPER] {state, cancel, ok}: wave 0 posts TASK or SKIP exactly
+// once, the helper answers DONE, wave 0 resets to IDLE; a task still running
+// when wave 0 no longer needs it is cancelled (checked after every sweep).
+// ---------------------------------------------------------------------------
+#define HS_IDLE 0
+#define HS_TASK 1
+#define HS_SKIP 2
+#define HS_DONE 3
+__device__ __forceinline__ int* helperFlags(double* ct) { return reinterpret_cast<int*>(ct + H_HELPER); }
+__device__ __forceinline__ void helperPost(double* ct, int state, int lane) {
+  // release: the task's LDS inputs are visible before the state changes
+  if (lane == 0) __hip_atomic_store(helperFlags(ct), state, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ int helperState(double* ct) {
+  return uni(__hip_atomic_load(helperFlags(ct), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+// spin with s_sleep until pred(state); bounded so that a protocol error
+// traps rather than hanging the device
+template <class Pred>
+__device__ __forceinline__ int helperWait(double* ct, Pred pred) {
+  for (long long it = 0;; it++) {
+    const int st = helperState(ct);
+    if (pred(st)) return st;
+    if (it > (1ll << 24)) __builtin_trap();
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
 
 // status bits
 #define ST_CONTACT_OVERFLOW 1
@@ -333,12 +398,12 @@ __device__ inline void carveFwd(double* base, int m, int n, FwdPool& P) {
 // ConstraintSolver::updateConstraints filter.  Kept contacts land at
 // ct + CT_CONTACTS in detector order.
 // ---------------------------------------------------------------------------
-__device__ void collideWorld(const ModelDev& md, double* s, const Layout& L, int lane) {
+__device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, const Layout& L, int lane) {
   double* ct = s + L.ct;
   double* dropped = s + L.V;                            // alias area (dead V/A/IC/F)
   double* pairbuf = dropped + CT_MAX_DROPPED * CREC;
   if (lane == 0) { ct[H_NCON] = 0; ct[H_NDROP] = 0; ct[H_STATUS] = 0; }
-  __syncthreads();
+  WSYNC();
   const int PC = md.pairChunk;
   for (int p0 = 0; p0 < md.numPairs; p0 += PC) {
     const int p = p0 + lane;
@@ -361,7 +426,7 @@ __device__ void collideWorld(const ModelDev& md, double* s, const Layout& L, int
       }
       ct[H_PAIRCNT + lane] = cnt;
     }
-    __syncthreads();
+    WSYNC();
     if (lane == 0) {
       int nk = (int)ct[H_NCON], nd = (int)ct[H_NDROP], st = (int)ct[H_STATUS];
       for (int q = 0; q < PC && p0 + q < md.numPairs; q++) {
@@ -399,7 +464,7 @@ __device__ void collideWorld(const ModelDev& md, double* s, const Layout& L, int
       }
       ct[H_NCON] = nk; ct[H_NDROP] = nd; ct[H_STATUS] = st;
     }
-    __syncthreads();
+    WSYNC();
   }
 }
 
@@ -426,10 +491,18 @@ __device__ inline double rowForceEntry(const ModelDev& md, const double* s, cons
 // Q = A_cc + A_cu E + cfm I  (== A_c^T Minv A_c_ub_E + cfm I).
 // Returns the standardized flag (wave-uniform).
 // ---------------------------------------------------------------------------
-__device__ bool devConstruct(FwdPool& P, int m, double cfm, bool ignoreFriction, double* ct, int lane,
-                             double* g_stamp = nullptr) {
+template <bool kLds>
+__device__ bool devConstruct(typename Space<kLds>::dptr poolIn, int m, int n, double cfm, bool ignoreFriction,
+                             lds_double* ctIn, int lane, double* g_stamp = nullptr) {
   (void)g_stamp;
+  FwdPool P;
+  carveFwd((double*)poolIn, m, n, P);
+  double* ct = (double*)ctIn;
   for (int guard = 0; guard <= m + 1; guard++) {
+    TACC_BEGIN(tCls);
+#ifdef NIMBLE_STAGE_TIMING
+    if (lane == 0 && g_stamp) g_stamp[60] += 1;
+#endif
     if (lane == 0) {
       const double TH = 1e-6;
       int nc = 0, nu = 0;
@@ -474,18 +547,20 @@ __device__ bool devConstruct(FwdPool& P, int m, double cfm, bool ignoreFriction,
       }
       ct[H_NC] = nc; ct[H_NU] = nu;
     }
-    __syncthreads();
+    WSYNC();
+    TACC_END(61, tCls);
     const int nc = uni((int)ct[H_NC]);
     const double bR = lane < m ? P.b[lane] : 0.0, hiR = lane < m ? P.hi[lane] : 0.0;
     const double loR = lane < m ? P.lo[lane] : 0.0;
     const int fiR = lane < m ? P.fi[lane] : -1;
     if (nc == 0) {
-      const bool ok = waveLcpValid(m, P.A, cfm, 0.0, bR, hiR, loR, fiR, ignoreFriction, lane);
+      const bool ok = waveLcpValid<kLds>(m, spc<kLds>(P.A), cfm, 0.0, bR, hiR, loR, fiR, ignoreFriction, lane);
       if (ok && lane < m) P.X[lane] = 0.0;
-      __syncthreads();
+      WSYNC();
       return ok;
     }
     STAMP(40);
+    TACC_BEGIN(tQ);
     // Q (nc x nc) into M1
     double* Q = P.M1;
     for (int t = lane; t < nc * nc; t += WAVE) {
@@ -499,7 +574,7 @@ __device__ bool devConstruct(FwdPool& P, int m, double cfm, bool ignoreFriction,
       if (cr == cc) v += cfm;
       Q[t] = v;
     }
-    __syncthreads();
+    WSYNC();
     Cod cod;
     double* w = carveCod(P.scr, Q, nc, nc, nc, cod);
     double* cn = w; w += m;
@@ -507,16 +582,27 @@ __device__ bool devConstruct(FwdPool& P, int m, double cfm, bool ignoreFriction,
     double* rhs = w; w += m;
     double* z = w; w += m;
     STAMP(41);
-    codFactor(cod, cn, vv, lane);
+    TACC_END(62, tQ);
+    TACC_BEGIN(tF);
+#ifdef NIMBLE_STAGE_TIMING
+    codFactor<kLds>(sp<kLds>(Q), sp<kLds>(P.scr), nc, nc, nc, sp<kLds>(vv), lane, g_stamp ? g_stamp + 67 : nullptr);
+#else
+    codFactor<kLds>(sp<kLds>(Q), sp<kLds>(P.scr), nc, nc, nc, sp<kLds>(vv), lane);
+#endif
     if (lane == 0) ct[H_CODOK] = 1;
     STAMP(42);
+    TACC_END(63, tF);
+    TACC_BEGIN(tS);
     {
-      const double f = codSolveWave(cod, lane < nc ? P.relVel[lane] : 0.0, z, lane);
+      const double f = codSolveWave<kLds>(sp<kLds>(Q), sp<kLds>(P.scr), nc, nc, nc, lane < nc ? P.relVel[lane] : 0.0,
+                                          sp<kLds>(z), lane);
       if (lane < nc) P.fsol[lane] = f;
     }
     STAMP(43);
+    TACC_END(64, tS);
+    TACC_BEGIN(tN);
     (void)rhs;
-    __syncthreads();
+    WSYNC();
     if (lane == 0) {
       bool anyNewlyNot = false;
       for (int i = 0; i < m; i++) {
@@ -535,15 +621,19 @@ __device__ bool devConstruct(FwdPool& P, int m, double cfm, bool ignoreFriction,
       }
       ct[H_FLAG] = anyNewlyNot ? 1 : 0;
     }
-    __syncthreads();
-    const bool ok = waveLcpValid(m, P.A, cfm, lane < m ? P.nx[lane] : 0.0, bR, hiR, loR, fiR, ignoreFriction, lane);
+    WSYNC();
+    TACC_END(65, tN);
+    TACC_BEGIN(tV);
+    const bool ok =
+        waveLcpValid<kLds>(m, spc<kLds>(P.A), cfm, lane < m ? P.nx[lane] : 0.0, bR, hiR, loR, fiR, ignoreFriction, lane);
     const int res = ok ? (uni((int)ct[H_FLAG]) ? 2 : 1) : 0;
     STAMP(44);
+    TACC_END(66, tV);
     if (ok) {
       if (lane < m) P.X[lane] = P.nx[lane];
       if (lane < nc) P.fc[lane] = P.fsol[lane];
     }
-    __syncthreads();
+    WSYNC();
     if (res != 2) return res != 0;
   }
   return false;
@@ -551,7 +641,12 @@ __device__ bool devConstruct(FwdPool& P, int m, double cfm, bool ignoreFriction,
 
 // guessSolution (LCPUtils.cpp:69): COD solve on {normal rows with b > 0} U
 // {friction rows}; result into x.
-__device__ void devGuess(FwdPool& P, int m, double* x, double* ct, int lane) {
+template <bool kLds>
+__device__ void devGuess(typename Space<kLds>::dptr poolIn, int m, int n, lds_double* ctIn, int lane) {
+  FwdPool P;
+  carveFwd((double*)poolIn, m, n, P);
+  double* ct = (double*)ctIn;
+  double* x = P.X;
   if (lane == 0) {
     int k = 0;
     for (int i = 0; i < m; i++) {
@@ -560,13 +655,13 @@ __device__ void devGuess(FwdPool& P, int m, double* x, double* ct, int lane) {
     }
     ct[H_K] = k;
   }
-  __syncthreads();
+  WSYNC();
   const int k = uni((int)ct[H_K]);
   for (int i = lane; i < m; i += WAVE) x[i] = 0.0;
-  if (k == 0) { __syncthreads(); return; }
+  if (k == 0) { WSYNC(); return; }
   double* Ar = P.M1;
   for (int t = lane; t < k * k; t += WAVE) Ar[t] = P.A[P.cl[t / k] * m + P.cl[t % k]];
-  __syncthreads();
+  WSYNC();
   Cod cod;
   double* w = carveCod(P.scr, Ar, k, k, k, cod);
   double* cn = w; w += m;
@@ -574,13 +669,14 @@ __device__ void devGuess(FwdPool& P, int m, double* x, double* ct, int lane) {
   double* rhs = w; w += m;
   double* z = w; w += m;
   double* xr = w; w += m;
-  codFactor(cod, cn, vv, lane);
+  codFactor<kLds>(sp<kLds>(Ar), sp<kLds>(P.scr), k, k, k, sp<kLds>(vv), lane);
   {
-    const double xr_ = codSolveWave(cod, lane < k ? P.b[P.cl[lane]] : 0.0, z, lane);
+    const double xr_ = codSolveWave<kLds>(sp<kLds>(Ar), sp<kLds>(P.scr), k, k, k, lane < k ? P.b[P.cl[lane]] : 0.0,
+                                          sp<kLds>(z), lane);
     if (lane < k) x[P.cl[lane]] = xr_;
   }
   (void)rhs; (void)xr;
-  __syncthreads();
+  WSYNC();
 }
 
 // The upstream-gradient-independent pieces of the constrained backward
@@ -588,16 +684,22 @@ __device__ void devGuess(FwdPool& P, int m, double* x, double* ct, int lane) {
 // matrices it uses), computed here where A = J Minv J^T is on chip:
 // A_c, A_c_ub_E, Q = A_c^T Minv A_c_ub_E + cfm I, pinv(Q) (COD) and the
 // rank-deficiency flag ||I - Q Q^+||^2 >= 1e-18.
-__device__ void backwardPrecompute(const ModelDev& md, double* s, const Layout& L, int lane, FwdPool& P, int m,
-                                   double cfm, double* snap, double* ct) {
+template <bool kLds>
+__device__ void backwardPrecompute(const ModelDev& md, lds_double* sIn, const Layout& L, int lane,
+                                   typename Space<kLds>::dptr poolIn, int m, double cfm, double* snap, lds_double* ctIn) {
   const int n = md.n;
+  double* s = (double*)sIn;
+  double* ct = (double*)ctIn;
+  snap = gbl(snap);
+  FwdPool P;
+  carveFwd(kLds ? (double*)poolIn : gbl((double*)poolIn), m, n, P);
 #ifdef NIMBLE_STAGE_TIMING
   double* g_stamp = snap + snapWorkspaceOffset(n) + 1000;
 #endif
   STAMP(45);
   const int nc = uni((int)ct[H_NC]);
   if (lane == 0) snap[SN_IMP] = 0.0;
-  if (nc == 0) { __syncthreads(); return; }
+  if (nc == 0) { WSYNC(); return; }
   double* AcG = snap + snAc(n);
   double* AcubEG = snap + snAcubE(n);
   double* PTG = snap + snPT(n);
@@ -631,16 +733,16 @@ __device__ void backwardPrecompute(const ModelDev& md, double* s, const Layout& 
   // the final classification's COD of this Q is normally still on chip (M1 +
   // scr, devConstruct); refactor only if a fallback solver clobbered it
   const bool reuse = uni(ct[H_CODOK] != 0 ? 1 : 0) != 0;
-  __syncthreads();
+  WSYNC();
   if (!reuse)
     for (int t = lane; t < nc * nc; t += WAVE) P.M1[t] = P.M2[t];
-  __syncthreads();
+  WSYNC();
   Cod cod;
   double* w = carveCod(P.scr, P.M1, nc, nc, nc, cod);
   double* cn = w; w += m;
   double* vv = w; w += m;
   STAMP(48);
-  if (!reuse) codFactor(cod, cn, vv, lane);
+  if (!reuse) codFactor<kLds>(sp<kLds>(P.M1), sp<kLds>(P.scr), nc, nc, nc, sp<kLds>(vv), lane);
   STAMP(49);
   // pinv(Q): lane c solves Q x = e_c in place in row c of the (now free) A region
   double* Zs = P.A;
@@ -676,7 +778,7 @@ __device__ void backwardPrecompute(const ModelDev& md, double* s, const Layout& 
     // column `lane` of pinv(Q) = row `lane` of pinv(Q)^T
     for (int j = 0; j < nc; j++) PTG[lane * nc + cod.perm[j]] = rhs[j];
   }
-  __syncthreads();
+  WSYNC();
   STAMP(50);
   // ||I - Q Q^+||^2 with (Q Q^+)[r][c] = sum_j Q[r][perm_j] z_c[j]
   double part = 0.0;
@@ -689,7 +791,7 @@ __device__ void backwardPrecompute(const ModelDev& md, double* s, const Layout& 
   }
   const double tot = waveSum(part);
   if (lane == 0) snap[SN_IMP] = tot >= 1e-18 ? 1.0 : 0.0;
-  __syncthreads();
+  WSYNC();
   STAMP(51);
 }
 
@@ -699,15 +801,26 @@ __device__ void backwardPrecompute(const ModelDev& md, double* s, const Layout& 
 // fallbacks, impulses (v1 += Minv J^T x), warm-start cache and snapshot.
 // `Lm` is the Cholesky factor of M (lower triangle, n x n).
 // ---------------------------------------------------------------------------
-__device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int lane, double* v1, const double* ddq,
-                             double* cache, double* snap, double* overflowWs) {
+template <bool kLds>
+__device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, const Layout& L, int lane,
+                                           lds_double* v1In, const lds_double* ddqIn, double* cache, double* snap,
+                                           typename Space<kLds>::dptr poolIn, int nCon, int m, bool helperOn);
+
+// inlined into the forward kernel: the model, layout and LDS base keep their
+// kernel-argument provenance (scalar loads, LDS instructions)
+__device__ __forceinline__ void contactStage(const ModelDev& md, double* s, const Layout& L, int lane, double* v1,
+                                             const double* ddq, double* cache, double* snap, double* overflowWs,
+                                             bool helperOn) {
   const int n = md.n;
+  s = lds<true>(s);
+  snap = gbl(snap);
+  cache = gbl(cache);
+  overflowWs = gbl(overflowWs);
 #ifdef NIMBLE_STAGE_TIMING
   double* g_stamp = snap + snapWorkspaceOffset(n) + 1000;
 #endif
   STAMP(0);
   double* ct = s + L.ct;
-  const double* Lm = s + L.M;
   collideWorld(md, s, L, lane);
   STAMP(1);
   const int nCon = uni((int)ct[H_NCON]);
@@ -716,7 +829,7 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
       for (int i = 0; i < 8; i++) snap[i] = 0.0;
       snap[SN_STATUS] = ct[H_STATUS];
     }
-    __syncthreads();
+    WSYNC();
     return;
   }
   // row count
@@ -729,11 +842,36 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
     }
     ct[H_M] = m;
   }
-  __syncthreads();
+  WSYNC();
   const int m = uni((int)ct[H_M]);
+  // the LCP workspace is in LDS when it fits the pool (the common case, LDS
+  // instructions throughout), else in the world's HBM snapshot tail
+  if (fwdPoolDoubles(m, n) <= L.poolCap)
+    contactLcp<true>(md, sp<true>(s), L, lane, sp<true>(v1), spc<true>(ddq), cache, snap, sp<true>(s + L.pool), nCon,
+                     m, helperOn);
+  else
+    contactLcp<false>(md, sp<true>(s), L, lane, sp<true>(v1), spc<true>(ddq), cache, snap, overflowWs, nCon, m,
+                      false);
+}
+
+template <bool kLds>
+__device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, const Layout& L, int lane,
+                                           lds_double* v1In, const lds_double* ddqIn, double* cache, double* snap,
+                                           typename Space<kLds>::dptr poolIn, int nCon, int m, bool helperOn) {
+  const int n = md.n;
+  double* s = (double*)sIn;
+  double* v1 = (double*)v1In;
+  const double* ddq = (const double*)ddqIn;
+  double* pool = kLds ? (double*)poolIn : gbl((double*)poolIn);
+  snap = gbl(snap);
+  cache = gbl(cache);
+#ifdef NIMBLE_STAGE_TIMING
+  double* g_stamp = snap + snapWorkspaceOffset(n) + 1000;
+#endif
+  double* ct = s + L.ct;
+  const double* Lm = s + L.M;
   FwdPool P;
-  const int need = fwdPoolDoubles(m, n);
-  carveFwd(need <= L.poolCap ? s + L.pool : overflowWs, m, n, P);
+  carveFwd(pool, m, n, P);
   // rows (ContactConstraint: normal + 2 tangents with friction)
   if (lane == 0) {
     int r = 0;
@@ -761,13 +899,13 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
       }
     }
   }
-  __syncthreads();
+  WSYNC();
   // J^T columns
   for (int t = lane; t < n * m; t += WAVE) {
     const int i = t / m, j = t % m;
     P.cols[t] = rowForceEntry(md, s, L, ct + CT_CONTACTS + P.rowC[j] * CREC, P.dvec + 3 * j, i);
   }
-  __syncthreads();
+  WSYNC();
   STAMP(2);
   // Y = L^-1 J^T (row-parallel forward substitution; `massed` holds Y), so
   // that A = J Minv J^T = Y^T Y and Minv J^T x = L^-T (Y x)
@@ -778,19 +916,19 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
     for (int i = 0; i < n; i++) acc += P.cols[i * m + r] * v1[i];
     P.b[r] = -acc;
   }
-  __syncthreads();
+  WSYNC();
   {
     double* Y = P.massed;
     for (int k = 0; k < n; k++) {
       const double inv = s[L.dinv + k];
       for (int j = lane; j < m; j += WAVE) Y[k * m + j] *= inv;
-      __syncthreads();
+      WSYNC();
       const int cnt = (n - k - 1) * m;
       for (int t = lane; t < cnt; t += WAVE) {
         const int i = k + 1 + t / m, j = t % m;
         Y[i * m + j] -= Lm[tri(i, k)] * Y[k * m + j];
       }
-      __syncthreads();
+      WSYNC();
     }
     for (int t = lane; t < m * m; t += WAVE) {
       const int r = t / m, c = t % m;
@@ -822,31 +960,31 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
       P.b[r] += bv;
     }
   }
-  __syncthreads();
+  WSYNC();
   for (int j = lane; j < m; j += WAVE) {
     double acc = 0;
 #pragma unroll 8
     for (int i = 0; i < m; i++) acc += P.A[i * m + j] * P.A[i * m + j];
     P.aCol[j] = acc;
   }
-  __syncthreads();
+  WSYNC();
   STAMP(3);
   // warm start (BoxedLcpConstraintSolver::mX) or guessSolution
   const bool cached = uni((int)cache[0]) == m;
   if (cached) {
     for (int i = lane; i < m; i += WAVE) { P.X[i] = cache[1 + i]; P.xc[i] = cache[1 + i]; }
-    __syncthreads();
+    WSYNC();
   } else {
-    devGuess(P, m, P.X, ct, lane);
+    devGuess<kLds>(poolIn, m, n, sp<true>(ct), lane);
     for (int i = lane; i < m; i += WAVE) P.xc[i] = P.X[i];
-    __syncthreads();
+    WSYNC();
   }
   if (lane == 0) ct[H_CODOK] = 0;
   STAMP(4);
 #ifdef NIMBLE_STAGE_TIMING
-  bool success = devConstruct(P, m, 0.0, false, ct, lane, g_stamp);
+  bool success = devConstruct<kLds>(poolIn, m, n, 0.0, false, sp<true>(ct), lane, g_stamp);
 #else
-  bool success = devConstruct(P, m, 0.0, false, ct, lane);
+  bool success = devConstruct<kLds>(poolIn, m, n, 0.0, false, sp<true>(ct), lane);
 #endif
   STAMP(5);
   const bool shortCircuit = success;
@@ -855,6 +993,9 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
   const double bR = lane < m ? P.b[lane] : 0.0, hiR = lane < m ? P.hi[lane] : 0.0;
   const double loR = lane < m ? P.lo[lane] : 0.0;
   const int fiR = lane < m ? P.fi[lane] : -1;
+  // the helper wave solves the PGS fallback while Dantzig runs (see helperWave)
+  const bool tasked = kLds && helperOn && !success;
+  if (tasked) helperPost(ct, HS_TASK, lane);
   if (!success) {
     // LCPUtils::reduce would merge near-duplicate columns; they do not occur
     // for box contacts -- flag them in the status word if they ever do
@@ -872,17 +1013,17 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
     }
     if (lane == 0) ct[H_CODOK] = 0;
     for (int t = lane; t < m * m; t += WAVE) P.M1[t] = P.A[t];
-    __syncthreads();
+    WSYNC();
     double xd = 0.0;
     #ifdef NIMBLE_STAGE_TIMING
-    bool ok = waveDantzig(m, P.M1, P.M2, P.scr, xd, bR, loR, hiR, fiR, lane, g_stamp + 52);
+    bool ok = waveDantzig<kLds>(m, sp<kLds>(P.M1), sp<kLds>(P.M2), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane, g_stamp + 52);
 #else
-    bool ok = waveDantzig(m, P.M1, P.M2, P.scr, xd, bR, loR, hiR, fiR, lane);
+    bool ok = waveDantzig<kLds>(m, sp<kLds>(P.M1), sp<kLds>(P.M2), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane);
 #endif
     if (ok) {
       if (lane < m) P.X[lane] = xd;
-      __syncthreads();
-      ok = waveLcpValid(m, P.A, 0.0, xd, bR, hiR, loR, fiR, false, lane);
+      WSYNC();
+      ok = waveLcpValid<kLds>(m, spc<kLds>(P.A), 0.0, xd, bR, hiR, loR, fiR, false, lane);
     }
     success = ok;
   }
@@ -896,17 +1037,22 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
     if (!ok) {
       cf = md.fallbackCfm;
       if (lane == 0) ct[H_CODOK] = 0;
-      for (int t = lane; t < m * m; t += WAVE) P.M1[t] = P.A[t] + ((t / m == t % m) ? cf : 0.0);
-      __syncthreads();
-      double xd = lane < m ? P.xc[lane] : 0.0;
-      #ifdef NIMBLE_STAGE_TIMING
-      ok = wavePgs(m, P.M1, xd, bR, loR, hiR, fiR, lane, g_stamp + 54);
+      double xd;
+      if (tasked) {
+        helperWait(ct, [](int st) { return st == HS_DONE; });
+        xd = lane < m ? P.xh[lane] : 0.0;
+        ok = uni(helperFlags(ct)[2]) != 0;
+      } else {
+        xd = lane < m ? P.xc[lane] : 0.0;
+#ifdef NIMBLE_STAGE_TIMING
+        ok = wavePgs<kLds>(m, spc<kLds>(P.A), xd, bR, loR, hiR, fiR, lane, g_stamp + 54, cf);
 #else
-      ok = wavePgs(m, P.M1, xd, bR, loR, hiR, fiR, lane);
+        ok = wavePgs<kLds>(m, spc<kLds>(P.A), xd, bR, loR, hiR, fiR, lane, nullptr, cf);
 #endif
+      }
       if (ok) {
         X = xd;
-        ok = waveLcpValid(m, P.A, cf, X, bR, hiR, loR, fiR, false, lane);
+        ok = waveLcpValid<kLds>(m, spc<kLds>(P.A), cf, X, bR, hiR, loR, fiR, false, lane);
       }
     }
     if (!ok) {
@@ -917,26 +1063,26 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
       const int k2 = __popcll(km);
       const int pos = __popcll(km & ((1ull << lane) - 1ull));
       if (keepMe) P.cl[pos] = lane;
-      __syncthreads();
+      WSYNC();
       for (int t = lane; t < k2 * k2; t += WAVE) {
         const int r = t / k2, c = t % k2;
         P.M1[t] = P.A[P.cl[r] * m + P.cl[c]] + (r == c ? cf : 0.0);
       }
-      __syncthreads();
+      WSYNC();
       const int kr = lane < k2 ? P.cl[lane] : 0;
       double xr = 0.0;
-      wavePgs(k2, P.M1, xr, lane < k2 ? P.b[kr] : 0.0, lane < k2 ? P.lo[kr] : 0.0, lane < k2 ? P.hi[kr] : 0.0, -1,
+      wavePgs<kLds>(k2, spc<kLds>(P.M1), xr, lane < k2 ? P.b[kr] : 0.0, lane < k2 ? P.lo[kr] : 0.0, lane < k2 ? P.hi[kr] : 0.0, -1,
               lane);
-      __syncthreads();
+      WSYNC();
       if (lane < k2) P.fsol[lane] = xr;
-      __syncthreads();
+      WSYNC();
       X = 0.0;
       if (keepMe) X = P.fsol[pos];
     }
     if (__ballot(lane < m && isnan(X))) X = 0.0;
     if (lane < m) P.X[lane] = X;
     if (lane == 0) { ct[H_CFM] = cf; ct[H_IGN] = ign ? 1 : 0; }
-    __syncthreads();
+    WSYNC();
   }
   cfm = unid(ct[H_CFM]);
   ignoredFriction = uni(ct[H_IGN] != 0 ? 1 : 0) != 0;
@@ -946,8 +1092,8 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
   bool std2 = true;
   if (!shortCircuit) {
     for (int i = lane; i < m; i += WAVE) P.xc[i] = P.X[i];
-    __syncthreads();
-    std2 = devConstruct(P, m, cfm, ignoredFriction, ct, lane);
+    WSYNC();
+    std2 = devConstruct<kLds>(poolIn, m, n, cfm, ignoredFriction, sp<true>(ct), lane);
   }
   const double* Xf = std2 ? P.X : P.xc;
   STAMP(8);
@@ -965,7 +1111,7 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
       if (lane == k) u = uk;
       else if (lane < k) u -= Lm[tri(k, lane)] * uk;
     }
-    __syncthreads();
+    WSYNC();
     if (lane < n) v1[lane] += u;
   }
   if (lane == 0) cache[0] = m;
@@ -987,7 +1133,7 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
   const int nc = uni((int)ct[H_NC]);
   for (int i = lane; i < nc; i += WAVE) snap[SN_FC + i] = P.fc[i];
   for (int i = lane; i < n; i += WAVE) snap[snYf(n) + i] = ddq[i];
-  backwardPrecompute(md, s, L, lane, P, m, cfm, snap, ct);
+  backwardPrecompute<kLds>(md, sIn, L, lane, poolIn, m, cfm, snap, sp<true>(ct));
   if (lane == 0) {
     snap[SN_NCON] = nCon;
     snap[SN_M] = m;
@@ -998,8 +1144,43 @@ __device__ void contactStage(const ModelDev& md, double* s, const Layout& L, int
     snap[SN_SC] = shortCircuit ? 1 : 0;
     snap[SN_IGN] = ignoredFriction ? 1 : 0;
   }
-  __syncthreads();
+  WSYNC();
   STAMP(9);
+}
+
+// One world's turn of the helper wave (wave 1 of the forward workgroup):
+// wait for wave 0's TASK or SKIP, run the PGS fallback on the LDS pool for a
+// task, answer DONE, then wait until wave 0 has taken the answer.
+__device__ void helperWave(const ModelDev& md, double* s, const Layout& L, int lane) {
+  s = lds<true>(s);
+  double* ct = s + L.ct;
+  const int st = helperWait(ct, [](int v) { return v == HS_TASK || v == HS_SKIP; });
+  if (st == HS_TASK) {
+    const int m = uni((int)ct[H_M]);
+    FwdPool P;
+    carveFwd(s + L.pool, m, md.n, P);
+    double x = lane < m ? P.xc[lane] : 0.0;
+    const double bR = lane < m ? P.b[lane] : 0.0, hiR = lane < m ? P.hi[lane] : 0.0;
+    const double loR = lane < m ? P.lo[lane] : 0.0;
+    const int fiR = lane < m ? P.fi[lane] : -1;
+    const bool ok =
+        wavePgs<true>(m, spc<true>(P.A), x, bR, loR, hiR, fiR, lane, nullptr, md.fallbackCfm, helperFlags(ct) + 1);
+    if (lane < m) P.xh[lane] = x;
+    if (lane == 0) helperFlags(ct)[2] = ok ? 1 : 0;
+  }
+  helperPost(ct, HS_DONE, lane);
+  helperWait(ct, [](int v) { return v != HS_DONE; });
+}
+
+// wave 0's end of a world's protocol: post SKIP if no task went out, cancel
+// a task still running, collect DONE and reset to IDLE
+__device__ __forceinline__ void helperRetire(double* s, const Layout& L, int lane) {
+  double* ct = lds<true>(s) + L.ct;
+  if (helperState(ct) == HS_IDLE) helperPost(ct, HS_SKIP, lane);
+  if (lane == 0) __hip_atomic_store(helperFlags(ct) + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  helperWait(ct, [](int v) { return v == HS_DONE; });
+  if (lane == 0) __hip_atomic_store(helperFlags(ct) + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  helperPost(ct, HS_IDLE, lane);
 }
 
 // ===========================================================================
@@ -1032,8 +1213,17 @@ __device__ inline void carveBwd(double* base, int m, int n, BwdPool& P) {
   P.gRows = p; p += n * m;
   P.TAB = p; p += 12 * m;
   P.NV = p; p += NV_COLS * n;
-  double** vecs[] = {&P.fc, &P.bc, &P.bounce, &P.u, &P.lam, &P.beta, &P.xq, &P.rho, &P.piv, &P.zeta, &P.r1};
-  for (double** v : vecs) { *v = p; p += m; }
+  P.fc = p; p += m;
+  P.bc = p; p += m;
+  P.bounce = p; p += m;
+  P.u = p; p += m;
+  P.lam = p; p += m;
+  P.beta = p; p += m;
+  P.xq = p; p += m;
+  P.rho = p; p += m;
+  P.piv = p; p += m;
+  P.zeta = p; p += m;
+  P.r1 = p; p += m;
   P.rowOf = reinterpret_cast<int*>(p);
 }
 
@@ -1110,21 +1300,21 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
   (void)ct;
   for (int j = lane; j < m; j += WAVE)
     if ((int)rows[j * SN_ROWREC + RR_MAP] == CM_CLAMPING) P.rowOf[(int)rows[j * SN_ROWREC + RR_CIDX]] = j;
-  __syncthreads();
+  WSYNC();
   for (int c = lane; c < nc; c += WAVE) {
     const int r = P.rowOf[c];
     P.fc[c] = sn[SN_FC + c];
     P.bc[c] = rows[r * SN_ROWREC + RR_B];
     P.bounce[c] = rows[r * SN_ROWREC + RR_BOUNCE];
   }
-  __syncthreads();
+  WSYNC();
   // x = P b ; r1 = b - Q x ; zeta = P^T x
   for (int c = lane; c < nc; c += WAVE) {
     double xx = 0;
     for (int r = 0; r < nc; r++) xx += PT[r * nc + c] * P.bc[r];
     P.xq[c] = xx;
   }
-  __syncthreads();
+  WSYNC();
   for (int c = lane; c < nc; c += WAVE) {
     double qx = 0, ze = 0;
     if (imp)
@@ -1135,7 +1325,7 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
     P.r1[c] = imp ? P.bc[c] - qx : 0.0;
     P.zeta[c] = imp ? ze : 0.0;
   }
-  __syncthreads();
+  WSYNC();
   STAMP(31);
   // batch 1
   {
@@ -1165,21 +1355,21 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
       s[L.x + lane] = sn[snYf(n) + lane] + d;
     }
   }
-  __syncthreads();
+  WSYNC();
   // u = A_c_ub_E^T w ; lambda = P^T u ; beta ; rho = P lambda ; pi = u - Q^T lambda
   for (int c = lane; c < nc; c += WAVE) {
     double acc = 0;
     for (int i = 0; i < n; i++) acc += AcubE[i * nc + c] * s[L.w + i];
     P.u[c] = acc;
   }
-  __syncthreads();
+  WSYNC();
   for (int c = lane; c < nc; c += WAVE) {
     double l = 0;
     for (int r = 0; r < nc; r++) l += PT[c * nc + r] * P.u[r];
     P.lam[c] = l;
     P.beta[c] = P.bounce[c] * l;
   }
-  __syncthreads();
+  WSYNC();
   for (int c = lane; c < nc; c += WAVE) {
     double qtl = 0, rh = 0;
     if (imp)
@@ -1190,7 +1380,7 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
     P.piv[c] = imp ? P.u[c] - qtl : 0.0;
     P.rho[c] = imp ? rh : 0.0;
   }
-  __syncthreads();
+  WSYNC();
   STAMP(35);
   // batch 2
   {
@@ -1221,7 +1411,7 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
       s[L.w + lane] = w2;
     }
   }
-  __syncthreads();
+  WSYNC();
   STAMP(37);
   // per-row vectors g_j
   for (int t = lane; t < m * n; t += WAVE) {
@@ -1242,7 +1432,7 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
     }
     P.gRows[j * n + i] = g;
   }
-  __syncthreads();
+  WSYNC();
   // T_A(g_j), T_B(g_j)
   for (int t = lane; t < 2 * m; t += WAVE) {
     const int j = t >> 1, side = t & 1;
@@ -1250,7 +1440,7 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
     const int body = (int)rec[8 + side];
     bodyTwist(md, s + L.Sw, body, P.gRows + j * n, 1, P.TAB + j * 12 + side * 6);
   }
-  __syncthreads();
+  WSYNC();
   STAMP(38);
   return imp;
 }
@@ -1322,7 +1512,7 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
         for (int i = 0; i < 6; i++) omega[lane * 6 + i] = om[i];
       if (lane == 0)
         for (int i = 0; i < 6; i++) UV[i] = uv[i];
-      __syncthreads();
+      WSYNC();
       // P^c_b = sum over ancestor dofs r of b of S_r x* omega_r
       if (lane < nb) {
         double pb[6] = {0, 0, 0, 0, 0, 0};
@@ -1336,7 +1526,7 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
         }
         for (int i = 0; i < 6; i++) Pc[lane * 6 + i] = pb[i];
       }
-      __syncthreads();
+      WSYNC();
       if (k < n && ((md.anc[c] >> bk) & 1ull)) {
         double y[6];
         for (int i = 0; i < 6; i++) y[i] = Pc[c * 6 + i] - (lam >= 0 ? Pc[lam * 6 + i] : 0.0);
@@ -1345,7 +1535,7 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
         if (zw > 1e-6) acc += Z[0] * UV[3] + Z[1] * UV[4] + Z[2] * UV[5];
         acc += Z[3] * UV[0] + Z[4] * UV[1] + Z[5] * UV[2];
       }
-      __syncthreads();
+      WSYNC();
     }
   }
   // face side: per row
@@ -1410,7 +1600,7 @@ __device__ double mFieldsTerm(const ModelDev& md, double* s, const Layout& L, co
       worldInertia(md, s + L.Tw + 12 * b, b, I);
       mv6(I, V, V + 6);
     }
-    __syncthreads();
+    WSYNC();
     for (int lev = md.maxDepth - 1; lev >= 0; lev--) {
       const int b0 = md.levelStart[lev], cnt = (md.levelStart[lev + 1] - b0) * 12;
       for (int t = lane; t < cnt; t += WAVE) {
@@ -1419,7 +1609,7 @@ __device__ double mFieldsTerm(const ModelDev& md, double* s, const Layout& L, co
         for (int q = md.childStart[p]; q < md.childStart[p + 1]; q++) acc += buf[(f * nb + md.childList[q]) * 12 + i];
         buf[(f * nb + p) * 12 + i] = acc;
       }
-      __syncthreads();
+      WSYNC();
     }
     if (k < md.n) {
       const int bk = md.dofBody[k];
@@ -1436,7 +1626,7 @@ __device__ double mFieldsTerm(const ModelDev& md, double* s, const Layout& L, co
       }
       total += coef[pr] * val;
     }
-    __syncthreads();
+    WSYNC();
   }
   return total;
 }

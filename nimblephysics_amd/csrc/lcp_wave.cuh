@@ -33,16 +33,21 @@
 // rounding).  A is symmetric and read by rows (conflict-free LDS access);
 // the reference's in-place row scaling (1/A_jj) is applied lane-locally,
 // A_ji / A_jj = A_ij * dummy_j, so A is never written.
-__device__ bool wavePgs(int n, const double* A, double& x, double b, double lo, double hi, int findex, int lane,
-                        double* dbg = nullptr) {
+// `shift` is added to A's diagonal on the fly (A + cfm I without a copy);
+// `cancel` (LDS int, optional) is polled after every sweep and ends the
+// solve early with `false` when set.
+template <bool kLds>
+__device__ bool wavePgs(int n, typename Space<kLds>::cdptr Ain, double& x, double b, double lo, double hi, int findex,
+                        int lane, double* dbg = nullptr, double shift = 0.0, const int* cancel = nullptr) {
   n = uni(n);
+  const double* A = (const double*)Ain;
   const double deltaXThr = 1e-6, relTol = 1e-3, epsDiv = 1e-9;
 #ifdef LCP_PROFILE
   const long long tp0 = (long long)__builtin_amdgcn_s_memtime();
 #endif
   const bool act = lane < n;
   const int col = act ? lane : 0;  // idle lanes read a valid address, use 0
-  const double diagRaw = act ? A[lane * n + lane] : 1.0;
+  const double diagRaw = act ? A[lane * n + lane] + shift : 1.0;
   const unsigned long long order = __ballot(act && diagRaw >= epsDiv);
   const bool inOrder = act && ((order >> lane) & 1ull);
   // rows whose x bounds friction rows (their update refreshes those bounds)
@@ -52,7 +57,8 @@ __device__ bool wavePgs(int n, const double* A, double& x, double b, double lo, 
   double r = act ? b : 0.0;
   for (int k = 0; k < n; k++) {
     const double xk = rdl(x, k);
-    if (act) r -= A[k * n + lane] * xk;
+    const double a0 = A[k * n + col];
+    if (act) r -= (k == lane ? a0 + shift : a0) * xk;
   }
   // Contact layout (the forward's rows: each contact is a normal row
   // followed by 0 or 2 friction rows with findex = that normal and
@@ -85,11 +91,13 @@ __device__ bool wavePgs(int n, const double* A, double& x, double b, double lo, 
   const double act1 = act ? 1.0 : 0.0;
   double xn = x;
   const int nLast = n - 1;
-#define PGS_LOAD_GROUP(R, i0)                                        \
-  double R##0 = A[((i0) < n ? (i0) : nLast) * n + col];             \
-  double R##1 = A[((i0) + 1 < n ? (i0) + 1 : nLast) * n + col];     \
-  double R##2 = A[((i0) + 2 < n ? (i0) + 2 : nLast) * n + col];     \
-  double R##3 = A[((i0) + 3 < n ? (i0) + 3 : nLast) * n + col]
+#define PGS_ROW_AT(i) (((i) < n ? (i) : nLast) * n + col)
+#define PGS_SHIFTED(v, i) (lane == (i) ? (v) + shift : (v))
+#define PGS_LOAD_GROUP(R, i0)                                           \
+  double R##0 = PGS_SHIFTED(A[PGS_ROW_AT(i0)], (i0));                  \
+  double R##1 = PGS_SHIFTED(A[PGS_ROW_AT((i0) + 1)], (i0) + 1);        \
+  double R##2 = PGS_SHIFTED(A[PGS_ROW_AT((i0) + 2)], (i0) + 2);        \
+  double R##3 = PGS_SHIFTED(A[PGS_ROW_AT((i0) + 3)], (i0) + 3)
   {
     auto row1 = [&](int i, double cur) {
       double nx = 0.0;
@@ -200,8 +208,11 @@ __device__ bool wavePgs(int n, const double* A, double& x, double b, double lo, 
     possible = !__ballot(inOrder && fabs(xn) > epsDiv && fabs((xn - xs) / xn) > relTol);
     if (dbg && lane == 0) dbg[0] = iter;
     if (possible) break;
+    if (cancel && uni(__hip_atomic_load(cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) break;
   }
 #undef PGS_LOAD_GROUP
+#undef PGS_SHIFTED
+#undef PGS_ROW_AT
 #ifdef LCP_PROFILE
   if (dbg && lane == 0) dbg[4] = (double)((long long)__builtin_amdgcn_s_memtime() - tp2);
 #endif
@@ -210,9 +221,11 @@ __device__ bool wavePgs(int n, const double* A, double& x, double b, double lo, 
 }
 
 // ---------------------------------------------------------------------------
-__device__ bool waveLcpValid(int m, const double* A, double cfm, double x, double b, double hi, double lo, int fi,
-                             bool ignoreFriction, int lane) {
+template <bool kLds>
+__device__ bool waveLcpValid(int m, typename Space<kLds>::cdptr Ain, double cfm, double x, double b, double hi,
+                             double lo, int fi, bool ignoreFriction, int lane) {
   m = uni(m);
+  const double* A = (const double*)Ain;
   double v = -b;
 #pragma unroll 4
   for (int j = 0; j < m; j++) {
@@ -249,7 +262,13 @@ __device__ bool waveLcpValid(int m, const double* A, double cfm, double x, doubl
 // ---------------------------------------------------------------------------
 // x (lane-distributed, length c.n) = min-norm least-squares solution for rhs
 // (lane-distributed, length c.m).  scr: >= n doubles of LDS.
-__device__ double codSolveWave(const Cod& c, double rhs, double* scr, int lane) {
+// (A, ws, m, n, ld) as given to carveCod + codFactor
+template <bool kLds>
+__device__ double codSolveWave(typename Space<kLds>::dptr Ain, typename Space<kLds>::dptr wsIn, int m_, int n_, int ld_,
+                               double rhs, typename Space<kLds>::dptr scrIn, int lane) {
+  Cod c;
+  carveCod((double*)wsIn, (double*)Ain, uni(m_), uni(n_), uni(ld_), c);
+  double* scr = (double*)scrIn;
   const double* A = c.A;
   const int m = c.m, n = c.n, ld = c.ld;
   for (int k = 0; k < c.kmax; k++) {
@@ -280,11 +299,11 @@ __device__ double codSolveWave(const Cod& c, double rhs, double* scr, int lane) 
       if (lane >= r && lane < n) z -= sc * A[i * ld + lane];
     }
   }
-  __syncthreads();
+  WSYNC();
   if (lane < n) scr[c.perm[lane]] = z;
-  __syncthreads();
+  WSYNC();
   const double out = lane < n ? scr[lane] : 0.0;
-  __syncthreads();
+  WSYNC();
   return out;
 }
 
@@ -313,19 +332,19 @@ struct WaveDantzig {
   __device__ __forceinline__ void swapProblem(int i1, int i2) {
     if (i1 == i2) return;
     LP_BEGIN();
-    __syncthreads();
+    WSYNC();
     if (lane < n) {
       const double t = A[i1 * n + lane];
       A[i1 * n + lane] = A[i2 * n + lane];
       A[i2 * n + lane] = t;
     }
-    __syncthreads();
+    WSYNC();
     if (lane < n) {
       const double t = A[lane * n + i1];
       A[lane * n + i1] = A[lane * n + i2];
       A[lane * n + i2] = t;
     }
-    __syncthreads();
+    WSYNC();
     swapReg(x, i1, i2); swapReg(b, i1, i2); swapReg(w, i1, i2); swapReg(lo, i1, i2); swapReg(hi, i1, i2);
     swapRegI(p, i1, i2); swapRegI(state, i1, i2); swapRegI(findex, i1, i2);
     LP_END(prof, 0);
@@ -500,14 +519,14 @@ struct WaveDantzig {
         ldltAddTL(r, n2 - r, a);
       }
     }
-    __syncthreads();
+    WSYNC();
     if (r < n2 - 1) {
       if (lane < n2)
         for (int j = r; j < n2 - 1; j++) L[lane * ldL + j] = L[lane * ldL + j + 1];
-      __syncthreads();
+      WSYNC();
       if (lane < n2)
         for (int i = r; i < n2 - 1; i++) L[i * ldL + lane] = L[(i + 1) * ldL + lane];
-      __syncthreads();
+      WSYNC();
       const double dn = shiftDown1(d, lane);
       if (lane >= r && lane < n2 - 1) d = dn;
     }
@@ -535,11 +554,11 @@ struct WaveDantzig {
       if (!onlyTransfer) {
         double tmp = ell;
         solveL1T(tmp, nC);
-        __syncthreads();
+        WSYNC();
         if (lane < nC) scr[C] = dir > 0 ? -tmp : tmp;
-        __syncthreads();
+        WSYNC();
         if (lane < nC) deltaX = scr[lane];
-        __syncthreads();
+        WSYNC();
       }
     }
   }
@@ -551,9 +570,14 @@ struct WaveDantzig {
 
 // A (n x n LDS, destroyed), L (n x (n|1) LDS scratch), scr (>= n LDS); problem
 // vectors lane-distributed; returns success and x (lane-distributed).
-__device__ bool waveDantzig(int n, double* A, double* Lbuf, double* scr, double& xOut, double b, double lo, double hi,
+template <bool kLds>
+__device__ bool waveDantzig(int n, typename Space<kLds>::dptr Ain, typename Space<kLds>::dptr Lin,
+                            typename Space<kLds>::dptr scrIn, double& xOut, double b, double lo, double hi,
                             int findex, int lane, double* dbg = nullptr) {
   n = uni(n);
+  double* A = (double*)Ain;
+  double* Lbuf = (double*)Lin;
+  double* scr = (double*)scrIn;
   WaveDantzig D;
   int pivots = 0;
   D.n = n; D.nC = 0; D.nN = 0; D.lane = lane; D.ldL = n | 1;
@@ -571,21 +595,21 @@ __device__ bool waveDantzig(int n, double* A, double* Lbuf, double* scr, double&
     for (int k = n - 1; k >= 0; k--)
       if (rdli(D.findex, k) >= 0) { D.swapProblem(k, n - 1 - numAtEnd); numAtEnd++; }
   }
-  __syncthreads();
+  WSYNC();
   bool hitFirstFriction = false;
   for (int i = 0; i < n; i++) {
     D.nC = uni(D.nC);
     D.nN = uni(D.nN);
     if (!hitFirstFriction && rdli(D.findex, i) >= 0) {
-      __syncthreads();
+      WSYNC();
       if (lane < n) scr[D.p] = D.x;
-      __syncthreads();
+      WSYNC();
       if (lane >= i && lane < n) {
         const double wfk = scr[D.findex];
         if (wfk == 0) { D.hi = 0; D.lo = 0; }
         else { D.hi = fabs(D.hi * wfk); D.lo = -D.hi; }
       }
-      __syncthreads();
+      WSYNC();
       hitFirstFriction = true;
     }
     LP_BEGIN();
@@ -703,10 +727,10 @@ __device__ bool waveDantzig(int n, double* A, double* Lbuf, double* scr, double&
       }
     }
   }
-  __syncthreads();
+  WSYNC();
   if (lane < n) scr[D.p] = D.x;
-  __syncthreads();
+  WSYNC();
   xOut = lane < n ? scr[lane] : 0.0;
-  __syncthreads();
+  WSYNC();
   return true;
 }

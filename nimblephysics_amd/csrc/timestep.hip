@@ -32,7 +32,7 @@
 // Reference: BodyNode::updateTransform / updateVelocity /
 // updatePartialAcceleration (dart/dynamics/BodyNode.cpp:1960-1983).
 // ---------------------------------------------------------------------------
-__device__ void kinematics(const ModelDev& md, double* s, const Layout& L, int lane, const double* ddq) {
+__device__ __forceinline__ void kinematics(const ModelDev& md, double* s, const Layout& L, int lane, const double* ddq) {
   const double* q = s + L.q;
   const double* v = s + L.v;
   // 1. local transforms T_pj * Q(q) * T_cj^-1 (one lane per body), into Tw
@@ -61,7 +61,7 @@ __device__ void kinematics(const ModelDev& md, double* s, const Layout& L, int l
     tmul(md.Tpj[b], Q, T);
     tmul(T, md.TcjInv[b], s + L.Tw + 12 * b);
   }
-  __syncthreads();
+  WSYNC();
   // 2. compose down the tree, one level at a time
   for (int lev = 1; lev <= md.maxDepth; lev++) {
     const int b0 = md.levelStart[lev], cnt = md.levelStart[lev + 1] - b0;
@@ -70,7 +70,7 @@ __device__ void kinematics(const ModelDev& md, double* s, const Layout& L, int l
       double* Tw = s + L.Tw + 12 * b;
       tmul(s + L.Tw + 12 * md.parent[b], Tw, Tw);
     }
-    __syncthreads();
+    WSYNC();
   }
   // 3. world-frame motion subspace Ad_{Tw * Tcj} S_local (one lane per dof)
   if (lane < md.n) {
@@ -84,7 +84,7 @@ __device__ void kinematics(const ModelDev& md, double* s, const Layout& L, int l
     tmul(s + L.Tw + 12 * b, md.Tcj[b], TwC);
     adT(TwC, loc, s + L.Sw + 6 * k);
   }
-  __syncthreads();
+  WSYNC();
   // 4. V_b = sum over ancestor dofs of S_j qdot_j
   if (lane < md.nb) {
     const int b = lane;
@@ -100,7 +100,7 @@ __device__ void kinematics(const ModelDev& md, double* s, const Layout& L, int l
 #pragma unroll
     for (int i = 0; i < 6; i++) s[L.V + 6 * b + i] = V[i];
   }
-  __syncthreads();
+  WSYNC();
   // 5. A_b = sum over ancestor dofs of S_j qddot_j + V_body(j) x (S_j qdot_j)
   //    (BodyNode::updatePartialAcceleration / updateAccelerationFD unrolled)
   if (lane < md.nb) {
@@ -123,12 +123,12 @@ __device__ void kinematics(const ModelDev& md, double* s, const Layout& L, int l
 #pragma unroll
     for (int i = 0; i < 6; i++) s[L.A + 6 * b + i] = A[i];
   }
-  __syncthreads();
+  WSYNC();
 }
 
 // World-frame spatial inertia of body b (6x6, row-major) at the world origin.
 // dart/dynamics/Inertia.cpp:1368 computeSpatialTensor in world axes.
-__device__ void worldInertia(const ModelDev& md, const double* Tw, int b, double* I) {
+__device__ __forceinline__ void worldInertia(const ModelDev& md, const double* Tw, int b, double* I) {
   const double m = md.mass[b];
   double cw[3], Rc[9], tmp[9];
   for (int r = 0; r < 3; r++) cw[r] = Tw[r * 4] * md.com[b][0] + Tw[r * 4 + 1] * md.com[b][1] + Tw[r * 4 + 2] * md.com[b][2] + Tw[r * 4 + 3];
@@ -154,7 +154,7 @@ __device__ void worldInertia(const ModelDev& md, const double* Tw, int b, double
 // Composite inertias IC[b] (subtree sums) and bias forces F[b] = sum over the
 // subtree of  I_i (A_i - a_g) + V_i x* (I_i V_i)  -- the world-frame
 // restatement of BodyNode::updateTransmittedForceID (BodyNode.cpp:1994).
-__device__ void composites(const ModelDev& md, double* s, const Layout& L, int lane) {
+__device__ __forceinline__ void composites(const ModelDev& md, double* s, const Layout& L, int lane) {
   const double ag[6] = {0, 0, 0, md.g[0], md.g[1], md.g[2]};
   if (lane < md.nb) {
     const int b = lane;
@@ -167,7 +167,7 @@ __device__ void composites(const ModelDev& md, double* s, const Layout& L, int l
     crf(s + L.V + 6 * b, h, vxh);
     for (int i = 0; i < 6; i++) s[L.F + 6 * b + i] = f[i] + vxh[i];
   }
-  __syncthreads();
+  WSYNC();
   // subtree sums, one tree level at a time (parents gather their children)
   for (int lev = md.maxDepth - 1; lev >= 0; lev--) {
     const int b0 = md.levelStart[lev], cnt = (md.levelStart[lev + 1] - b0) * 42;
@@ -179,13 +179,13 @@ __device__ void composites(const ModelDev& md, double* s, const Layout& L, int l
       for (int q = md.childStart[p]; q < md.childStart[p + 1]; q++) acc += s[off + stride * (md.childList[q] - p)];
       s[off] = acc;
     }
-    __syncthreads();
+    WSYNC();
   }
 }
 
 // M_jk = S_j^T IC_{deeper(j,k)} S_k (composite-rigid-body algorithm), and the
 // generalized bias C_j = S_j . F_body(j).  M is stored full (n x n) at L.M.
-__device__ void massMatrixAndBias(const ModelDev& md, double* s, const Layout& L, int lane, double* C) {
+__device__ __forceinline__ void massMatrixAndBias(const ModelDev& md, double* s, const Layout& L, int lane, double* C) {
   const int n = md.n;
   const int pairs = n * (n + 1) / 2;
   for (int t = lane; t < pairs; t += WAVE) {
@@ -207,14 +207,14 @@ __device__ void massMatrixAndBias(const ModelDev& md, double* s, const Layout& L
     s[L.M + tri(j, k)] = val;  // lower triangle, packed
   }
   for (int j = lane; j < n; j += WAVE) C[j] = dot6(s + L.Sw + 6 * j, s + L.F + 6 * md.dofBody[j]);
-  __syncthreads();
+  WSYNC();
 }
 
 // In-place Cholesky of the packed lower triangle at A (row i at i(i+1)/2):
 // left-looking (Crout) with one lane per row, one barrier per column.  The
 // per-element subtraction order (k ascending) is that of the right-looking
 // factorisation.
-__device__ void cholesky(double* A, double* dinv, int n, int lane) {
+__device__ __forceinline__ void cholesky(double* A, double* dinv, int n, int lane) {
   for (int j = 0; j < n; j++) {
     double sum = 0.0;
     if (lane >= j && lane < n) {
@@ -226,7 +226,7 @@ __device__ void cholesky(double* A, double* dinv, int n, int lane) {
     const double djj = sqrt(rdl(sum, j));
     if (lane == j) { A[tri(j, j)] = djj; dinv[j] = 1.0 / djj; }
     else if (lane > j && lane < n) A[tri(lane, j)] = sum / djj;
-    __syncthreads();
+    WSYNC();
   }
 }
 
@@ -259,15 +259,15 @@ __device__ __forceinline__ void cholSolveReg(const double* Lm, const double* din
 }
 
 // Solve L L^T x = b in place (x = b on entry, LDS).
-__device__ void cholSolve(const double* Lm, const double* dinv, double* x, int n, int lane) {
+__device__ __forceinline__ void cholSolve(const double* Lm, const double* dinv, double* x, int n, int lane) {
   double xr[1] = {lane < n ? x[lane] : 0.0};
   cholSolveReg<1>(Lm, dinv, xr, n, lane);
-  __syncthreads();
+  WSYNC();
   if (lane < n) x[lane] = xr[0];
-  __syncthreads();
+  WSYNC();
 }
 
-__device__ void loadState(const ModelDev& md, double* s, const Layout& L, int lane, const double* state,
+__device__ __forceinline__ void loadState(const ModelDev& md, double* s, const Layout& L, int lane, const double* state,
                           const double* tau) {
   const int n = md.n;
   for (int i = lane; i < n; i += WAVE) {
@@ -275,13 +275,13 @@ __device__ void loadState(const ModelDev& md, double* s, const Layout& L, int la
     s[L.v + i] = state[n + i];
     s[L.tau + i] = tau[i];
   }
-  __syncthreads();
+  WSYNC();
 }
 
 #include "contact.cuh"
 
 // Dynamics cache <-> LDS (Layout regions Tw, Sw, V, IC, M, dinv, rhs).
-__device__ void dynCacheCopy(const ModelDev& md, double* s, const Layout& L, double* cache, bool store, int lane) {
+__device__ __forceinline__ void dynCacheCopy(const ModelDev& md, double* s, const Layout& L, double* cache, bool store, int lane) {
   const int n = md.n, nb = md.nb;
   const int seg[7][2] = {{L.Tw, 12 * nb}, {L.Sw, 6 * n}, {L.V, 6 * nb}, {L.IC, 36 * nb},
                          {L.M, n * (n + 1) / 2}, {L.dinv, n}, {L.rhs, n}};
@@ -295,12 +295,12 @@ __device__ void dynCacheCopy(const ModelDev& md, double* s, const Layout& L, dou
       for (int t = lane; t < cnt; t += WAVE) s[base + t] = cache[o + t];
     o += cnt;
   }
-  __syncthreads();
+  WSYNC();
 }
 
 // Accelerations only (phase 5 of kinematics) for given ddq, with Tw, Sw, V
 // already in LDS.
-__device__ void accelerations(const ModelDev& md, double* s, const Layout& L, int lane, const double* ddq) {
+__device__ __forceinline__ void accelerations(const ModelDev& md, double* s, const Layout& L, int lane, const double* ddq) {
   const double* v = s + L.v;
   if (lane < md.nb) {
     const int b = lane;
@@ -321,11 +321,11 @@ __device__ void accelerations(const ModelDev& md, double* s, const Layout& L, in
 #pragma unroll
     for (int i = 0; i < 6; i++) s[L.A + 6 * b + i] = A[i];
   }
-  __syncthreads();
+  WSYNC();
 }
 
 // Everything up to the factored mass matrix; leaves C in s[L.rhs].
-__device__ void coreDynamics(const ModelDev& md, double* s, const Layout& L, int lane) {
+__device__ __forceinline__ void coreDynamics(const ModelDev& md, double* s, const Layout& L, int lane) {
   kinematics(md, s, L, lane, nullptr);
   composites(md, s, L, lane);
   massMatrixAndBias(md, s, L, lane, s + L.rhs);
@@ -335,15 +335,29 @@ __device__ void coreDynamics(const ModelDev& md, double* s, const Layout& L, int
 // ---------------------------------------------------------------------------
 // Forward step.
 // ---------------------------------------------------------------------------
-extern "C" __global__ void __launch_bounds__(WAVE)
+// Two waves per world when the model has contact pairs (blockDim 128): wave
+// 1 is the LCP helper (helperWave), all of the step runs on wave 0.
+extern "C" __global__ void __launch_bounds__(2 * WAVE) __attribute__((amdgpu_waves_per_eu(2)))
 nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, const double* __restrict__ state,
                       const double* __restrict__ forces, double* __restrict__ lcpCache,
                       double* __restrict__ nextState, double* __restrict__ snapshot, int snapDoubles,
                       int cacheDoubles) {
   extern __shared__ double s[];
   const ModelDev& md = *mdp;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & (WAVE - 1);
   const int n = md.n;
+  const bool helperOn = blockDim.x > WAVE;
+  if (helperOn) {
+    if (threadIdx.x == 0) {
+      int* hf = reinterpret_cast<int*>(s + L.ct + H_HELPER);
+      hf[0] = HS_IDLE; hf[1] = 0; hf[2] = 0;
+    }
+    __syncthreads();  // the one barrier both waves take: flags initialised
+    if (threadIdx.x >= WAVE) {
+      for (int env = blockIdx.x; env < batch; env += gridDim.x) helperWave(md, s, L, lane);
+      return;
+    }
+  }
   for (int env = blockIdx.x; env < batch; env += gridDim.x) {
     const double* st = state + (size_t)env * 2 * n;
 #ifdef NIMBLE_STAGE_TIMING
@@ -368,18 +382,20 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, con
       const double dampF = -md.damping[i] * vi;
       x[i] = s[L.tau + i] + springF + dampF - s[L.rhs + i];
     }
-    __syncthreads();
+    WSYNC();
     cholSolve(s + L.M, s + L.dinv, x, n, lane);  // x = ddq
     // integrateVelocities (Skeleton.cpp:9329): v1 = v + dt ddq
     double* v1 = s + L.v1;
     for (int i = lane; i < n; i += WAVE) v1[i] = s[L.v + i] + md.dt * x[i];
-    __syncthreads();
+    WSYNC();
     STAMP(12);
     // runConstraintEngine (World.cpp:254): collision, LCP, impulses
     if (md.numPairs > 0) {
       double* sn = snapshot + (size_t)env * snapDoubles;
-      contactStage(md, s, L, lane, v1, x, lcpCache + (size_t)env * cacheDoubles, sn, sn + snapWorkspaceOffset(n));
+      contactStage(md, s, L, lane, v1, x, lcpCache + (size_t)env * cacheDoubles, sn, sn + snapWorkspaceOffset(n),
+                   helperOn);
     }
+    if (helperOn) helperRetire(s, L, lane);
     double* out = nextState + (size_t)env * 2 * n;
     for (int i = lane; i < n; i += WAVE) out[n + i] = v1[i];
     // integratePositions (World.cpp:300): with the pre-step velocity when
@@ -396,7 +412,7 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, con
         for (int i = 0; i < 6; i++) out[o + i] = r[i];
       }
     }
-    __syncthreads();
+    WSYNC();
     STAMP(13);
   }
 }
@@ -422,7 +438,7 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, con
 // (Skeleton::getJacobianOfID, DifferentiableContactConstraint / BackpropSnapshot
 // use) contracted with w, collapsed to O(nb) 6-vector work; the identity is
 // checked against central differences in tools/proto/adjoint_rnea.py.
-__device__ void adjointVectors(const ModelDev& md, double* s, const Layout& L, int lane) {
+__device__ __forceinline__ void adjointVectors(const ModelDev& md, double* s, const Layout& L, int lane) {
   const double ag[6] = {0, 0, 0, md.g[0], md.g[1], md.g[2]};
   const int nb = md.nb, n = md.n;
   if (lane < nb) {
@@ -458,7 +474,7 @@ __device__ void adjointVectors(const ModelDev& md, double* s, const Layout& L, i
     mv6(I, VxW, t);
     for (int i = 0; i < 6; i++) a[30 + i] = -t[i];  // zeta
   }
-  __syncthreads();
+  WSYNC();
   // subtree sums of alpha..zeta and f (-> composite F), deepest level first
   for (int lev = md.maxDepth - 1; lev >= 0; lev--) {
     const int b0 = md.levelStart[lev], cnt = (md.levelStart[lev + 1] - b0) * 42;
@@ -470,7 +486,7 @@ __device__ void adjointVectors(const ModelDev& md, double* s, const Layout& L, i
       for (int q = md.childStart[p]; q < md.childStart[p + 1]; q++) acc += s[off + stride * md.childList[q]];
       s[off + stride * p] = acc;
     }
-    __syncthreads();
+    WSYNC();
   }
   if (lane < nb) {
     const int b = lane, par = md.parent[b];
@@ -478,7 +494,7 @@ __device__ void adjointVectors(const ModelDev& md, double* s, const Layout& L, i
     for (int i = 0; i < 6; i++) d[i] = s[L.Wt + 6 * b + i] - (par >= 0 ? s[L.Wt + 6 * par + i] : 0.0);
     crf(d, s + L.F + 6 * b, s + L.adj + 42 * b + 36);  // kappa
   }
-  __syncthreads();
+  WSYNC();
   for (int lev = md.maxDepth - 1; lev >= 0; lev--) {
     const int b0 = md.levelStart[lev], cnt = (md.levelStart[lev + 1] - b0) * 6;
     for (int t = lane; t < cnt; t += WAVE) {
@@ -487,7 +503,7 @@ __device__ void adjointVectors(const ModelDev& md, double* s, const Layout& L, i
       for (int q = md.childStart[p]; q < md.childStart[p + 1]; q++) acc += s[L.adj + 42 * md.childList[q] + e];
       s[L.adj + 42 * p + e] = acc;
     }
-    __syncthreads();
+    WSYNC();
   }
 }
 
@@ -549,11 +565,11 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
         x[i] = dt * (s[L.tau + i] - s[L.rhs + i] - dampF - springF);
         w[i] = s[L.gv + i];
       }
-      __syncthreads();
+      WSYNC();
       cholSolve(s + L.M, s + L.dinv, x, n, lane);  // x = y = Minv z  => a* = y / dt
       cholSolve(s + L.M, s + L.dinv, w, n, lane);  // w = Minv gv
       for (int i = lane; i < n; i += WAVE) x[i] /= dt;
-      __syncthreads();
+      WSYNC();
     }
     STAMP(22);
     accelerations(md, s, L, lane, x);  // A = accelerations at a*
@@ -618,20 +634,20 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
         gvOut += dt * s[L.gp + k];
       }
     }
-    __syncthreads();
+    WSYNC();
     STAMP(24);
     if (nc > 0) {
       // the adjoint vectors are dead now: workspace for the contact-geometry
       // terms (6n + 6nb <= 42nb), then for the M-derivative field pairs (24nb)
       double* buf = s + L.adj;
       const double gterm = contactGTermsAll(md, s, L, sn, P, m, Z, buf, lane);
-      __syncthreads();
+      WSYNC();
       const double mterm = mFieldsTerm(md, s, L, P.NV, buf, lane, k, Z, -dt, (double)imp);
       if (k < n) {
         gq += gterm;
         gq += mterm;
       }
-      __syncthreads();
+      WSYNC();
     }
     STAMP(25);
     // FreeJoint posPos / velPos blocks: central differences exactly as
@@ -651,7 +667,7 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
         freeIntegrate(qq, vv, dt, r);
         for (int j = 0; j < 6; j++) fd[lane * 6 + j] = r[j];
       }
-      __syncthreads();
+      WSYNC();
       if (k >= o && k < o + 6) {
         const int i = k - o;
         double pp = 0.0, vp = 0.0;
@@ -664,7 +680,7 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
         gq += pp;
         gvOut += vp;
       }
-      __syncthreads();
+      WSYNC();
     }
     if (k < n) {
       // clipLossGradientsToBounds (BackpropSnapshot.cpp:425)
@@ -679,7 +695,7 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
       gradState[(size_t)env * 2 * n + n + k] = gvOut;
       gradForces[(size_t)env * n + k] = gt;
     }
-    __syncthreads();
+    WSYNC();
     STAMP(26);
   }
 }

@@ -12,6 +12,18 @@ __device__ __forceinline__ double rdl(double v, int l) {
 }
 __device__ __forceinline__ int rdli(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
+// Barrier of the one wave that owns a world.  The forward kernel runs a
+// second (helper) wave per workgroup that never joins the world's barriers,
+// so synchronisation is wave-scoped: workgroup-scope fences order the LDS
+// traffic (a wave's LDS operations execute in order) and the wave barrier
+// keeps the compiler from moving memory operations across it.
+#define WSYNC()                                            \
+  do {                                                     \
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); \
+    __builtin_amdgcn_wave_barrier();                       \
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup"); \
+  } while (0)
+
 // Scalar (SGPR) copy of a value all lanes hold equally -- counts and flags
 // read from LDS or global memory look lane-varying to the compiler, which
 // then turns every loop and branch on them into exec-masked vector code.
@@ -27,6 +39,37 @@ __device__ __forceinline__ double dppd(double v) {
   const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
   const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
   return __hiloint2double(hi, lo);
+}
+
+// LDS-typed pointers.  Device functions that are not inlined receive LDS
+// data through generic pointers, and the compiler then emits FLAT accesses
+// (slower, and each waits on both the vector-memory and the LDS counters).
+// Buffers that may live in LDS or in HBM are passed as Space<kLds>::dptr:
+// an address_space(3) pointer for LDS, so every access through it is a
+// ds_read/ds_write, and a plain pointer for the HBM fallback.  Casting a
+// generic pointer to the LDS type is only valid if it points into LDS.
+typedef __attribute__((address_space(3))) double lds_double;
+typedef __attribute__((address_space(3))) int lds_int;
+template <bool kLds> struct Space;
+template <> struct Space<true> { typedef lds_double* dptr; typedef const lds_double* cdptr; };
+template <> struct Space<false> { typedef double* dptr; typedef const double* cdptr; };
+template <bool kLds>
+__device__ __forceinline__ typename Space<kLds>::dptr sp(double* p) { return (typename Space<kLds>::dptr)p; }
+template <bool kLds>
+__device__ __forceinline__ typename Space<kLds>::cdptr spc(const double* p) { return (typename Space<kLds>::cdptr)p; }
+// generic view of a known-LDS pointer that keeps the LDS provenance visible
+// inside the current function
+template <bool kLds, class T>
+__device__ __forceinline__ T* lds(T* p) {
+  if constexpr (kLds) return (T*)((__attribute__((address_space(3))) T*)p);
+  else return p;
+}
+
+// generic view of a known-global (HBM) pointer: global_load/store instead of
+// FLAT (which also waits on the LDS counter)
+template <class T>
+__device__ __forceinline__ T* gbl(T* p) {
+  return (T*)((__attribute__((address_space(1))) T*)p);
 }
 
 // sum over all 64 lanes (every lane must be active); wave-uniform result

@@ -11,12 +11,12 @@ struct Rec {  // per problem output (doubles)
 extern "C" __global__ void __launch_bounds__(64)
 lcp_bench_kernel(int nmax, int nl, const int* nArr, const double* Ag, const double* bg, const double* log_,
                  const double* hig, const int* fig, const double* x0g, double* out) {
-  extern __shared__ double lds[];
+  extern __shared__ double ldsbuf[];
   const int lane = threadIdx.x;
   const int pb = blockIdx.x;
   const int n = nArr[pb];
   const int ldA = nl * nl;
-  double* A = lds;
+  double* A = ldsbuf;
   double* M1 = A + ldA;
   double* Lb = M1 + ldA;
   double* scr = Lb + nl * (nl | 1);
@@ -37,15 +37,31 @@ lcp_bench_kernel(int nmax, int nl, const int* nArr, const double* Ag, const doub
   __syncthreads();
   long long t0 = __builtin_amdgcn_s_memtime();
   double xd = 0.0;
-  const bool okD = waveDantzig(n, M1, Lb, scr, xd, b, lo, hi, fi, lane, dshared);
+  const bool okD = waveDantzig<true>(n, sp<true>(M1), sp<true>(Lb), sp<true>(scr), xd, b, lo, hi, fi, lane, dshared);
   long long t1 = __builtin_amdgcn_s_memtime();
   __syncthreads();
   double xp = lane < n ? x0g[pb * nmax + lane] : 0.0;
   long long t2 = __builtin_amdgcn_s_memtime();
-  const bool okP = wavePgs(n, A, xp, b, lo, hi, fi, lane, dshared + 12);
+  const bool okP = wavePgs<true>(n, spc<true>(A), xp, b, lo, hi, fi, lane, dshared + 12);
   long long t3 = __builtin_amdgcn_s_memtime();
   __syncthreads();
   (void)dbg;
+  // COD of the leading min(n, 8) block (construct-sized Q) and a solve
+  const int nq = n < 8 ? n : 8;
+  for (int t = lane; t < nq * nq; t += 64) M1[t] = A[(t / nq) * n + (t % nq)];
+  __syncthreads();
+  Cod cod;
+  double* w = carveCod(Lb, M1, nq, nq, nq, cod);
+  long long t4 = __builtin_amdgcn_s_memtime();
+  codFactor<true>(sp<true>(M1), sp<true>(Lb), nq, nq, nq, sp<true>(w + 64), lane);
+  long long t5 = __builtin_amdgcn_s_memtime();
+  const double zc = codSolveWave<true>(sp<true>(M1), sp<true>(Lb), nq, nq, nq, lane < nq ? b : 0.0, sp<true>(w + 128), lane);
+  long long t6 = __builtin_amdgcn_s_memtime();
+  if (lane == 0) {
+    o[Rec::PGSPROF + 3] = (double)(t5 - t4);
+    o[Rec::PGSPROF + 4] = (double)(t6 - t5);
+  }
+  if (lane < nq && !isfinite(zc)) o[Rec::PGSPROF + 5] = 1;
   if (lane == 0) {
     o[Rec::OK_D] = okD ? 1 : 0;
     o[Rec::CLK_D] = (double)(t1 - t0);
@@ -66,8 +82,8 @@ lcp_bench_kernel(int nmax, int nl, const int* nArr, const double* Ag, const doub
 
 extern "C" int lcp_bench_launch(int P, int nmax, int nl, const int* nArr, const double* A, const double* b, const double* lo,
                                 const double* hi, const int* fi, const double* x0, double* out, void* stream) {
-  const size_t lds = (size_t)(2 * nl * nl + nl * (nl | 1) + 64) * sizeof(double);
-  hipLaunchKernelGGL(lcp_bench_kernel, dim3(P), dim3(64), lds, (hipStream_t)stream, nmax, nl, nArr, A, b, lo, hi, fi, x0,
+  const size_t ldsBytes = (size_t)(2 * nl * nl + nl * (nl | 1) + 64) * sizeof(double);
+  hipLaunchKernelGGL(lcp_bench_kernel, dim3(P), dim3(64), ldsBytes, (hipStream_t)stream, nmax, nl, nArr, A, b, lo, hi, fi, x0,
                      out);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }

@@ -24,11 +24,12 @@ n = w.getNumDofs()
 a8 = lambda x: ((x + 7) // 8) * 8
 ws = a8(a8(800 + 2 * n) + 2 * n * 48 + 2 * 2304) + 1000  # snapWorkspaceOffset(n) + 1000
 for it in range(4):
-    snap[:, ws:ws + 60] = 0
+    snap[:, ws:ws + 100] = 0
+    prev_state, prev_cache = state.clone(), cache.clone()
     dev.forward(state, action, cache, nxt, snap, s)
     torch.cuda.synchronize()
     state = nxt.clone()
-    T = snap[:, ws:ws + 60].cpu().numpy()
+    T = snap[:, ws:ws + 100].cpu().numpy()
     hd = snap[:, :8].cpu().numpy()
     names = {(10, 14): " kinematics", (14, 15): " composites", (15, 16): " CRBA + bias", (16, 11): " cholesky",
              (10, 11): "load+coreDynamics", (40, 41): " c1: Q build", (41, 42): " c1: COD factor",
@@ -50,7 +51,26 @@ for it in range(4):
     for wi in np.argsort(-tot)[:6]:
         parts = []
         for (a, b), nm in names.items():
-            if T[wi, a] > 0 and T[wi, b] > 0 and (b - a) != 1 or (a, b) in ((5, 6), (6, 7), (4, 5), (8, 9), (0, 1), (3, 4), (7, 8)):
-                if T[wi, a] > 0 and T[wi, b] > 0:
-                    parts.append(f"{nm.strip()}={int(T[wi, b] - T[wi, a])}")
+            if T[wi, a] > 0 and T[wi, b] > 0 and (a, b) not in ((10, 11), (12, 13)):
+                parts.append(f"{nm.strip()}={int(T[wi, b] - T[wi, a])}")
+        print("      construct acc: iters %d cls %d Q %d codF %d codS %d nx %d valid %d | codF qr %d rz %d rank %d" % tuple(T[wi, 60:70]))
         print(f"  world {wi}: pivots {int(T[wi,52])} at row {int(T[wi,53])} pgs-sweeps {int(T[wi,54])} ign {hd[wi,7]:.0f} total {int(tot[wi])} rows {int(hd[wi,1])} clamp {int(hd[wi,2])} flag {hd[wi,4]:.0f} | " + " ".join(parts))
+
+# the slowest world of the last step re-run alone (one wave on the GPU): how
+# much of its time is contention with the other worlds' waves
+wi = int(np.argsort(-tot)[0])
+st1, ca1, ac1 = prev_state[wi:wi + 1].clone(), prev_cache[wi:wi + 1].clone(), action[wi:wi + 1].clone()
+sn1 = torch.zeros((1, dev.snapshot_doubles), dtype=torch.float64, device=d)
+nx1 = torch.empty_like(st1)
+for rep in range(2):
+    sn1[:, ws:ws + 100] = 0
+    c1 = ca1.clone()
+    dev.forward(st1, ac1, c1, nx1, sn1, s)
+    torch.cuda.synchronize()
+T1 = sn1[:, ws:ws + 100].cpu().numpy()[0]
+parts = []
+for (a, b), nm in names.items():
+    if T1[a] > 0 and T1[b] > 0 and (a, b) not in ((10, 11),):
+        parts.append(f"{nm.strip()}={int(T1[b] - T1[a])} (batch {int(T[wi, b] - T[wi, a])})")
+print(f"solo world {wi}: " + " ".join(parts))
+print("      construct acc solo: iters %d cls %d Q %d codF %d codS %d nx %d valid %d | codF qr %d rz %d rank %d" % tuple(T1[60:70]))

@@ -276,7 +276,7 @@ __device__ void tangentBasisODE(const double* n, double* t1, double* t2) {
 
 struct FwdPool {
   double *cols, *massed, *A, *M1, *M2;
-  double *lo, *hi, *b, *X, *aCol, *rest, *pen, *relVel, *fc, *Eval, *nx, *fsol, *xc, *xh, *dvec;
+  double *lo, *hi, *b, *X, *aCol, *rest, *pen, *relVel, *fc, *Eval, *nx, *fsol, *xc, *xh, *xh2, *dvec;
   int *fi, *mapping, *clampIdx, *ubIdx, *rowC, *rowDir, *clampRow, *cl;
   double* scr;  // >= 10 m + 2 n + 16
 };
@@ -303,7 +303,8 @@ __device__ inline void carveFwd(double* base, int m, int n, FwdPool& P) {
   P.nx = p; p += m;
   P.fsol = p; p += m;
   P.xc = p; p += m;
-  P.xh = p; p += m;  // the helper wave's PGS solution
+  P.xh = p; p += m;   // the helper wave's PGS solution
+  P.xh2 = p; p += m;  // ... and its frictionless PGS solution
   P.dvec = p; p += 3 * m;
   int* ip = reinterpret_cast<int*>(p);
   P.fi = ip; ip += m;
@@ -355,6 +356,7 @@ __device__ inline void carveFwd(double* base, int m, int n, FwdPool& P) {
 #define HS_TASK 1
 #define HS_SKIP 2
 #define HS_DONE 3
+#define HS_MID 4  // first PGS answered, frictionless PGS running
 __device__ __forceinline__ int* helperFlags(double* ct) { return reinterpret_cast<int*>(ct + H_HELPER); }
 __device__ __forceinline__ void helperPost(double* ct, int state, int lane) {
   // release: the task's LDS inputs are visible before the state changes
@@ -981,11 +983,17 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   }
   if (lane == 0) ct[H_CODOK] = 0;
   STAMP(4);
+  // the helper wave starts the PGS fallback now (see helperWave): its inputs
+  // are final, and it is cancelled if the classification below succeeds
+  const bool tasked = kLds && helperOn;
+  if (tasked) helperPost(ct, HS_TASK, lane);
 #ifdef NIMBLE_STAGE_TIMING
   bool success = devConstruct<kLds>(poolIn, m, n, 0.0, false, sp<true>(ct), lane, g_stamp);
 #else
   bool success = devConstruct<kLds>(poolIn, m, n, 0.0, false, sp<true>(ct), lane);
 #endif
+  if (tasked && success && lane == 0)
+    __hip_atomic_store(helperFlags(ct) + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   STAMP(5);
   const bool shortCircuit = success;
   double cfm = 0.0;
@@ -993,9 +1001,6 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   const double bR = lane < m ? P.b[lane] : 0.0, hiR = lane < m ? P.hi[lane] : 0.0;
   const double loR = lane < m ? P.lo[lane] : 0.0;
   const int fiR = lane < m ? P.fi[lane] : -1;
-  // the helper wave solves the PGS fallback while Dantzig runs (see helperWave)
-  const bool tasked = kLds && helperOn && !success;
-  if (tasked) helperPost(ct, HS_TASK, lane);
   if (!success) {
     // LCPUtils::reduce would merge near-duplicate columns; they do not occur
     // for box contacts -- flag them in the status word if they ever do
@@ -1039,7 +1044,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
       if (lane == 0) ct[H_CODOK] = 0;
       double xd;
       if (tasked) {
-        helperWait(ct, [](int st) { return st == HS_DONE; });
+        helperWait(ct, [](int st) { return st == HS_MID || st == HS_DONE; });
         xd = lane < m ? P.xh[lane] : 0.0;
         ok = uni(helperFlags(ct)[2]) != 0;
       } else {
@@ -1056,28 +1061,27 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
       }
     }
     if (!ok) {
-      // LCPUtils::removeFriction + PGS on the normal rows only
+      // LCPUtils::removeFriction + PGS on the normal rows only (the principal
+      // submatrix of A + cfm I over them, read in place)
       ign = true;
       const bool keepMe = lane < m && fiR == -1;
       const unsigned long long km = __ballot(keepMe);
       const int k2 = __popcll(km);
       const int pos = __popcll(km & ((1ull << lane) - 1ull));
-      if (keepMe) P.cl[pos] = lane;
-      WSYNC();
-      for (int t = lane; t < k2 * k2; t += WAVE) {
-        const int r = t / k2, c = t % k2;
-        P.M1[t] = P.A[P.cl[r] * m + P.cl[c]] + (r == c ? cf : 0.0);
+      if (tasked) {
+        helperWait(ct, [](int st) { return st == HS_DONE; });
+      } else {
+        int myRow = 0;
+        for (int t = 0, c = 0; t < m; t++)
+          if ((km >> t) & 1ull) { if (lane == c) myRow = t; c++; }
+        double xr = 0.0;
+        wavePgs<kLds, true>(k2, spc<kLds>(P.A), xr, lane < k2 ? P.b[myRow] : 0.0, lane < k2 ? P.lo[myRow] : 0.0,
+                      lane < k2 ? P.hi[myRow] : 0.0, -1, lane, nullptr, cf, nullptr, m, myRow);
+        if (lane < k2) P.xh2[lane] = xr;
+        WSYNC();
       }
-      WSYNC();
-      const int kr = lane < k2 ? P.cl[lane] : 0;
-      double xr = 0.0;
-      wavePgs<kLds>(k2, spc<kLds>(P.M1), xr, lane < k2 ? P.b[kr] : 0.0, lane < k2 ? P.lo[kr] : 0.0, lane < k2 ? P.hi[kr] : 0.0, -1,
-              lane);
-      WSYNC();
-      if (lane < k2) P.fsol[lane] = xr;
-      WSYNC();
       X = 0.0;
-      if (keepMe) X = P.fsol[pos];
+      if (keepMe) X = P.xh2[pos];
     }
     if (__ballot(lane < m && isnan(X))) X = 0.0;
     if (lane < m) P.X[lane] = X;
@@ -1163,10 +1167,24 @@ __device__ void helperWave(const ModelDev& md, double* s, const Layout& L, int l
     const double bR = lane < m ? P.b[lane] : 0.0, hiR = lane < m ? P.hi[lane] : 0.0;
     const double loR = lane < m ? P.lo[lane] : 0.0;
     const int fiR = lane < m ? P.fi[lane] : -1;
-    const bool ok =
-        wavePgs<true>(m, spc<true>(P.A), x, bR, loR, hiR, fiR, lane, nullptr, md.fallbackCfm, helperFlags(ct) + 1);
+    const double cf = md.fallbackCfm;
+    const bool ok = wavePgs<true>(m, spc<true>(P.A), x, bR, loR, hiR, fiR, lane, nullptr, cf, helperFlags(ct) + 1);
     if (lane < m) P.xh[lane] = x;
     if (lane == 0) helperFlags(ct)[2] = ok ? 1 : 0;
+    helperPost(ct, HS_MID, lane);
+    // then LCPUtils::removeFriction's PGS on the normal rows, unless wave 0
+    // has what it needs already (it cancels)
+    if (!uni(__hip_atomic_load(helperFlags(ct) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) {
+      const unsigned long long km = __ballot(lane < m && fiR == -1);
+      const int k2 = __popcll(km);
+      int myRow = 0;
+      for (int t = 0, c = 0; t < m; t++)
+        if ((km >> t) & 1ull) { if (lane == c) myRow = t; c++; }
+      double xr = 0.0;
+      wavePgs<true, true>(k2, spc<true>(P.A), xr, lane < k2 ? P.b[myRow] : 0.0, lane < k2 ? P.lo[myRow] : 0.0,
+                    lane < k2 ? P.hi[myRow] : 0.0, -1, lane, nullptr, cf, helperFlags(ct) + 1, m, myRow);
+      if (lane < k2) P.xh2[lane] = xr;
+    }
   }
   helperPost(ct, HS_DONE, lane);
   helperWait(ct, [](int v) { return v != HS_DONE; });

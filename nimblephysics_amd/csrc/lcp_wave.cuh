@@ -35,19 +35,26 @@
 // A_ji / A_jj = A_ij * dummy_j, so A is never written.
 // `shift` is added to A's diagonal on the fly (A + cfm I without a copy);
 // `cancel` (LDS int, optional) is polled after every sweep and ends the
-// solve early with `false` when set.
-template <bool kLds>
+// solve early with `false` when set.  With `ld` / `idx` the problem is the
+// principal submatrix A[idx][idx] of a matrix with leading dimension ld
+// (lane j holds idx_j), read in place (LCPUtils::removeFriction without a
+// gathered copy).
+template <bool kLds, bool kMapped = false>
 __device__ bool wavePgs(int n, typename Space<kLds>::cdptr Ain, double& x, double b, double lo, double hi, int findex,
-                        int lane, double* dbg = nullptr, double shift = 0.0, const int* cancel = nullptr) {
+                        int lane, double* dbg = nullptr, double shift = 0.0, const int* cancel = nullptr, int ld = -1,
+                        int idx = -1) {
   n = uni(n);
+  if (n == 0) return true;
+  ld = kMapped ? uni(ld) : n;
+  if (!kMapped) idx = lane;
   const double* A = (const double*)Ain;
   const double deltaXThr = 1e-6, relTol = 1e-3, epsDiv = 1e-9;
 #ifdef LCP_PROFILE
   const long long tp0 = (long long)__builtin_amdgcn_s_memtime();
 #endif
   const bool act = lane < n;
-  const int col = act ? lane : 0;  // idle lanes read a valid address, use 0
-  const double diagRaw = act ? A[lane * n + lane] + shift : 1.0;
+  const int col = act ? idx : rdli(idx, 0);  // idle lanes read a valid address, use 0
+  const double diagRaw = act ? A[col * ld + col] + shift : 1.0;
   const unsigned long long order = __ballot(act && diagRaw >= epsDiv);
   const bool inOrder = act && ((order >> lane) & 1ull);
   // rows whose x bounds friction rows (their update refreshes those bounds)
@@ -57,7 +64,7 @@ __device__ bool wavePgs(int n, typename Space<kLds>::cdptr Ain, double& x, doubl
   double r = act ? b : 0.0;
   for (int k = 0; k < n; k++) {
     const double xk = rdl(x, k);
-    const double a0 = A[k * n + col];
+    const double a0 = A[(kMapped ? rdli(idx, k) : k) * ld + col];
     if (act) r -= (k == lane ? a0 + shift : a0) * xk;
   }
   // Contact layout (the forward's rows: each contact is a normal row
@@ -91,7 +98,7 @@ __device__ bool wavePgs(int n, typename Space<kLds>::cdptr Ain, double& x, doubl
   const double act1 = act ? 1.0 : 0.0;
   double xn = x;
   const int nLast = n - 1;
-#define PGS_ROW_AT(i) (((i) < n ? (i) : nLast) * n + col)
+#define PGS_ROW_AT(i) ((kMapped ? rdli(idx, (i) < n ? (i) : nLast) : ((i) < n ? (i) : nLast)) * ld + col)
 #define PGS_SHIFTED(v, i) (lane == (i) ? (v) + shift : (v))
 #define PGS_LOAD_GROUP(R, i0)                                           \
   double R##0 = PGS_SHIFTED(A[PGS_ROW_AT(i0)], (i0));                  \

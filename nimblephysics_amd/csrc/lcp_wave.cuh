@@ -99,12 +99,11 @@ __device__ bool wavePgs(int n, typename Space<kLds>::cdptr Ain, double& x, doubl
   double xn = x;
   const int nLast = n - 1;
 #define PGS_ROW_AT(i) ((kMapped ? rdli(idx, (i) < n ? (i) : nLast) : ((i) < n ? (i) : nLast)) * ld + col)
-#define PGS_SHIFTED(v, i) (lane == (i) ? (v) + shift : (v))
-#define PGS_LOAD_GROUP(R, i0)                                           \
-  double R##0 = PGS_SHIFTED(A[PGS_ROW_AT(i0)], (i0));                  \
-  double R##1 = PGS_SHIFTED(A[PGS_ROW_AT((i0) + 1)], (i0) + 1);        \
-  double R##2 = PGS_SHIFTED(A[PGS_ROW_AT((i0) + 2)], (i0) + 2);        \
-  double R##3 = PGS_SHIFTED(A[PGS_ROW_AT((i0) + 3)], (i0) + 3)
+#define PGS_LOAD_GROUP(R, i0)               \
+  double R##0 = A[PGS_ROW_AT(i0)];         \
+  double R##1 = A[PGS_ROW_AT((i0) + 1)];   \
+  double R##2 = A[PGS_ROW_AT((i0) + 2)];   \
+  double R##3 = A[PGS_ROW_AT((i0) + 3)]
   {
     auto row1 = [&](int i, double cur) {
       double nx = 0.0;
@@ -154,6 +153,9 @@ __device__ bool wavePgs(int n, typename Space<kLds>::cdptr Ain, double& x, doubl
         C0 = N0; C1 = N1; C2 = N2; C3 = N3;
       }
     }
+    // the shift's share of the diagonal updates, deferred: lane i's residual
+    // is not read again before its own row in the next sweep
+    if (shift != 0.0 && act) r -= shift * (xn - x0);
   }
 #ifdef LCP_PROFILE
   const long long tp2 = (long long)__builtin_amdgcn_s_memtime();
@@ -212,13 +214,13 @@ __device__ bool wavePgs(int n, typename Space<kLds>::cdptr Ain, double& x, doubl
         C0 = N0; C1 = N1; C2 = N2; C3 = N3;
       }
     }
+    if (shift != 0.0) r -= (shift * dummyAct) * (xn - xs);
     possible = !__ballot(inOrder && fabs(xn) > epsDiv && fabs((xn - xs) / xn) > relTol);
     if (dbg && lane == 0) dbg[0] = iter;
     if (possible) break;
     if (cancel && uni(__hip_atomic_load(cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) break;
   }
 #undef PGS_LOAD_GROUP
-#undef PGS_SHIFTED
 #undef PGS_ROW_AT
 #ifdef LCP_PROFILE
   if (dbg && lane == 0) dbg[4] = (double)((long long)__builtin_amdgcn_s_memtime() - tp2);
@@ -646,11 +648,13 @@ __device__ bool waveDantzig(int n, typename Space<kLds>::dptr Ain, typename Spac
         const bool inN = lane >= nC && lane < nC + nN;
         LP_BEGIN();
         {
+          // every lane accumulates (no exec mask per step); only N lanes keep it
+          const int colA = lane < n ? lane : 0;
           double acc = 0.0;
 #pragma unroll 4
           for (int j = 0; j < nC; j++) {
             const double dxj = rdl(D.deltaX, j);
-            if (inN) acc += A[j * n + lane] * dxj;  // A symmetric: row j
+            acc += A[j * n + colA] * dxj;  // A symmetric: row j
           }
           if (inN) D.deltaW = acc + (dir > 0 ? A[i * n + lane] : -A[i * n + lane]);
         }
@@ -665,31 +669,32 @@ __device__ bool waveDantzig(int n, typename Space<kLds>::dptr Ain, typename Spac
           if (loI > -LCP_INF) { const double s2 = (loI - xi) * dirf; if (s2 < s) { s = s2; cmd = 2; } }
         }
         {
-          bool cand = false;
-          double s4 = LCP_INF;
+          // the N-side (cmd 4) and C-side (cmd 5/6) ratio tests of the
+          // reference over disjoint lanes: one division and one reduction;
+          // on equal minima the N side wins, as in the reference's order
+          bool cand4 = false;
+          int typ = 0;
+          double num = 0.0, den = 1.0;
           if (inN) {
             const bool dirOk = !D.state ? D.deltaW < 0 : D.deltaW > 0;
-            if (dirOk && !(D.lo == 0 && D.hi == 0)) { cand = true; s4 = -D.w / D.deltaW; }
+            if (dirOk && !(D.lo == 0 && D.hi == 0)) { cand4 = true; num = -D.w; den = D.deltaW; }
+          } else if (lane < nC) {
+            if (D.deltaX < 0 && D.lo > -LCP_INF) { num = D.lo - D.x; den = D.deltaX; typ = 5; }
+            if (D.deltaX > 0 && D.hi < LCP_INF) { num = D.hi - D.x; den = D.deltaX; typ = 6; }
           }
-          const double m4 = waveMin(cand ? s4 : LCP_INF);
-          if (m4 < s) {
-            s = m4;
-            cmd = 4;
-            si = waveFirst(cand && s4 == m4);
-          }
-        }
-        {
-          int typ = 0;
-          double s56 = LCP_INF;
-          if (lane < nC) {
-            if (D.deltaX < 0 && D.lo > -LCP_INF) { s56 = (D.lo - D.x) / D.deltaX; typ = 5; }
-            if (D.deltaX > 0 && D.hi < LCP_INF) { s56 = (D.hi - D.x) / D.deltaX; typ = 6; }
-          }
-          const double m56 = waveMin(typ ? s56 : LCP_INF);
-          if (m56 < s) {
-            s = m56;
-            si = waveFirst(typ && s56 == m56);
-            cmd = rdli(typ, si);
+          const double r = num / den;
+          const bool any = cand4 || typ;
+          const double mm = waveMin(any ? r : LCP_INF);
+          if (mm < s) {
+            s = mm;
+            const int s4i = waveFirst(cand4 && r == mm);
+            if (s4i >= 0) {
+              cmd = 4;
+              si = s4i;
+            } else {
+              si = waveFirst(typ && r == mm);
+              cmd = rdli(typ, si);
+            }
           }
         }
         pivots++;

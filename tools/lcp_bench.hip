@@ -5,7 +5,7 @@
 #include "../nimblephysics_amd/csrc/lcp_wave.cuh"
 
 struct Rec {  // per problem output (doubles)
-  enum { OK_D = 0, CLK_D, OK_P, CLK_P, PIV, PIVROW, PGS_IT, PROF = 8, X_D = 16, X_P = 64, PGSPROF = 112, SIZE = 120 };
+  enum { OK_D = 0, CLK_D, OK_P, CLK_P, PIV, PIVROW, PGS_IT, PROF = 8, X_D = 16, X_P = 64, PGSPROF = 112, CODPROF = 120, SIZE = 128 };
 };
 
 extern "C" __global__ void __launch_bounds__(64)
@@ -46,22 +46,20 @@ lcp_bench_kernel(int nmax, int nl, const int* nArr, const double* Ag, const doub
   long long t3 = __builtin_amdgcn_s_memtime();
   __syncthreads();
   (void)dbg;
-  // COD of the leading min(n, 8) block (construct-sized Q) and a solve
-  const int nq = n < 8 ? n : 8;
-  for (int t = lane; t < nq * nq; t += 64) M1[t] = A[(t / nq) * n + (t % nq)];
+  // COD of the full problem matrix (construct-sized Q) and a solve
+  for (int t = lane; t < n * n; t += 64) M1[t] = A[t];
+  for (int t = lane; t < 10 * nl + 16; t += 64) Lb[t] = 0.0;
   __syncthreads();
-  Cod cod;
-  double* w = carveCod(Lb, M1, nq, nq, nq, cod);
   long long t4 = __builtin_amdgcn_s_memtime();
-  codFactor<true>(sp<true>(M1), sp<true>(Lb), nq, nq, nq, sp<true>(w + 64), lane);
+  codFactor<true>(sp<true>(M1), sp<true>(Lb), n, n, n, sp<true>(Lb + 8 * nl + 16), lane);
   long long t5 = __builtin_amdgcn_s_memtime();
-  const double zc = codSolveWave<true>(sp<true>(M1), sp<true>(Lb), nq, nq, nq, lane < nq ? b : 0.0, sp<true>(w + 128), lane);
+  const double zc = codSolveWave<true>(sp<true>(M1), sp<true>(Lb), n, n, n, b, sp<true>(Lb + 9 * nl + 16), lane);
   long long t6 = __builtin_amdgcn_s_memtime();
   if (lane == 0) {
     o[Rec::PGSPROF + 3] = (double)(t5 - t4);
     o[Rec::PGSPROF + 4] = (double)(t6 - t5);
   }
-  if (lane < nq && !isfinite(zc)) o[Rec::PGSPROF + 5] = 1;
+  if (lane < n && !isfinite(zc)) o[Rec::PGSPROF + 7] = 1;
   if (lane == 0) {
     o[Rec::OK_D] = okD ? 1 : 0;
     o[Rec::CLK_D] = (double)(t1 - t0);
@@ -82,7 +80,7 @@ lcp_bench_kernel(int nmax, int nl, const int* nArr, const double* Ag, const doub
 
 extern "C" int lcp_bench_launch(int P, int nmax, int nl, const int* nArr, const double* A, const double* b, const double* lo,
                                 const double* hi, const int* fi, const double* x0, double* out, void* stream) {
-  const size_t ldsBytes = (size_t)(2 * nl * nl + nl * (nl | 1) + 64) * sizeof(double);
+  const size_t ldsBytes = (size_t)(3 * nl * nl + 2 * nl * (nl | 1) + 64) * sizeof(double);
   hipLaunchKernelGGL(lcp_bench_kernel, dim3(P), dim3(64), ldsBytes, (hipStream_t)stream, nmax, nl, nArr, A, b, lo, hi, fi, x0,
                      out);
   return hipGetLastError() == hipSuccess ? 0 : 1;

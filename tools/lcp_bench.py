@@ -20,7 +20,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
 PROB = os.path.join(ROOT, "dbg", "lcp_problems.npz")
 LIB = os.environ.get("LCP_BENCH_LIB", os.path.join(ROOT, "dbg", "liblcp_bench.so"))
 NMAX = 48
-REC = 120
+REC = 128
 
 
 def build():
@@ -132,7 +132,7 @@ def solo(count=6):
         o = out.cpu().numpy()[0]
         print(f" problem {k} n={d['n'][k]}: solo dantzig {o[1]:8.0f} (batch {base[k, 1]:8.0f}, pivots {o[4]:.0f}) "
               f"pgs {o[3]:8.0f} (batch {base[k, 3]:8.0f}, sweeps {o[6]:.0f}, fast {o[7]:.0f}) | "
-              + " ".join(f"{v:.0f}" for v in o[8:14]) + f" | pgs prologue {o[112]:.0f} sweep1 {o[113]:.0f} rest {o[114]:.0f} | cod8 factor {o[115]:.0f} solve {o[116]:.0f}")
+              + " ".join(f"{v:.0f}" for v in o[8:14]) + f" | cod factor {o[115]:.0f} solve {o[116]:.0f}")
 
 
 if __name__ == "__main__":

@@ -41,7 +41,9 @@ enum nimble_joint_type {
 /* Collision shape types (dart/collision/dart/DARTCollide.cpp:5030 collide()). */
 enum nimble_shape_type {
   NIMBLE_SHAPE_BOX = 0,
-  NIMBLE_SHAPE_SPHERE = 1
+  NIMBLE_SHAPE_SPHERE = 1,
+  NIMBLE_SHAPE_CAPSULE = 2    /* dart/dynamics/CapsuleShape.hpp: shape_size =
+                                 (radius, height, 0), axis = local z */
 };
 
 #define NIMBLE_MAX_BODIES 64
@@ -98,7 +100,7 @@ typedef struct nimble_world_desc {
   /* per collision shape [num_shapes] */
   const int32_t* shape_body;
   const int32_t* shape_type;        /* nimble_shape_type                   */
-  const double* shape_size;         /* [3] box size, or radius in [0]      */
+  const double* shape_size;         /* [3] box size; sphere (r); capsule (r, h) */
   const double* shape_T;            /* [12] ShapeNode relative transform   */
 } nimble_world_desc;
 

@@ -67,7 +67,12 @@ def skeleton_from_dict(d: dict) -> dyn.Skeleton:
         b.friction = bd["friction"]
         b.restitution = bd["restitution"]
         for sd in bd["shapes"]:
-            shape = dyn.BoxShape(sd["size"]) if sd["kind"] == dyn.SHAPE_BOX else dyn.SphereShape(sd["size"][0])
+            if sd["kind"] == dyn.SHAPE_BOX:
+                shape = dyn.BoxShape(sd["size"])
+            elif sd["kind"] == dyn.SHAPE_CAPSULE:
+                shape = dyn.CapsuleShape(sd["size"][0], sd["size"][1])
+            else:
+                shape = dyn.SphereShape(sd["size"][0])
             node = b.createShapeNode(shape, collision=True)
             node.T = np.array(sd["T"])
     skel.mobile = d.get("mobile", True)
@@ -97,6 +102,31 @@ def load_skeleton(name_or_path: str) -> dyn.Skeleton:
         path = os.path.join(ASSET_DIR, name_or_path + ".json")
     with open(path) as f:
         return skeleton_from_dict(json.load(f))
+
+
+def save_world(world, path: str):
+    """A whole world (skeletons in World::addSkeleton order + time step and
+    gravity) as JSON -- for .skel worlds, whose <physics> block is part of the
+    model."""
+    d = {"dt": world.getTimeStep(), "gravity": list(map(float, world.getGravity())),
+         "skeletons": [skeleton_to_dict(s) for s in world.skeletons]}
+    with open(path, "w") as f:
+        json.dump(_enc(d), f)
+
+
+def load_world(name_or_path: str):
+    from .simulation import World
+    path = name_or_path
+    if not os.path.exists(path):
+        path = os.path.join(ASSET_DIR, name_or_path + ".json")
+    with open(path) as f:
+        d = json.load(f)
+    w = World()
+    w.setTimeStep(d["dt"])
+    w.setGravity(d["gravity"])
+    for sd in d["skeletons"]:
+        w.addSkeleton(skeleton_from_dict(sd))
+    return w
 
 
 def cartpole() -> dyn.Skeleton:

@@ -29,6 +29,7 @@ JOINT_FREE = 3
 
 SHAPE_BOX = 0
 SHAPE_SPHERE = 1
+SHAPE_CAPSULE = 2
 
 
 def _iso(R=None, p=None) -> np.ndarray:
@@ -94,6 +95,20 @@ class SphereShape(Shape):
 
     def getRadius(self):
         return float(self.size[0])
+
+
+class CapsuleShape(Shape):
+    """dart/dynamics/CapsuleShape.hpp: radius, height (cylinder length along
+    the local z axis, hemispherical caps at z = +-height/2)."""
+
+    def __init__(self, radius: float, height: float):
+        super().__init__(SHAPE_CAPSULE, [radius, height, 0])
+
+    def getRadius(self):
+        return float(self.size[0])
+
+    def getHeight(self):
+        return float(self.size[1])
 
 
 class ShapeNode:

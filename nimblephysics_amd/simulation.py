@@ -45,6 +45,17 @@ class World:
         skel = _urdf.load_urdf(path, ignore_mesh_collisions=ignore_mesh_collisions)
         return self.addSkeleton(skel)
 
+    @staticmethod
+    def loadFrom(path: str) -> "World":
+        """World::loadFrom (python binding of dart/utils/UniversalLoader):
+        .skel files through SkelParser::readWorld (nimblephysics_amd/skel.py)."""
+        if path.endswith(".skel"):
+            from . import skel as _skel
+            return _skel.read_world(path)
+        w = World()
+        w.loadSkeleton(path)
+        return w
+
     def getSkeleton(self, key):
         if isinstance(key, int):
             return self.skeletons[key]

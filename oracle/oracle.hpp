@@ -34,10 +34,16 @@ struct Kin {
 
 // One contact point as produced by the collision detector
 // (dart/collision/Contact.hpp).  normal points from B into A.
+// Sphere-box contacts (types 4 SPHERE_BOX / 5 BOX_SPHERE, the reference's
+// ContactType numbering) also carry the sphere centre and the box faces the
+// centre was clamped against (Contact::faceNLocked / faceNNormal).
 struct Contact {
   int shapeA, shapeB, bodyA, bodyB;
   double point[3], normal[3], depth;
   int type;
+  double sphereCenter[3];
+  int faceLocked[3];
+  double faceNormal[9];
 };
 
 // Everything BackpropSnapshot needs (dart/neural/BackpropSnapshot.hpp and
@@ -64,6 +70,7 @@ struct Snapshot {
   double cfm = 0.0;
   bool ignoredFriction = false;
   bool shortCircuit = false;
+  int unsupportedContacts = 0;   // a narrow-phase branch not restated was hit
 };
 
 struct World {
@@ -106,7 +113,12 @@ void step(const World& w, const double* state, const double* tau, std::vector<do
 void backprop(const World& w, const Snapshot& snap, const double* gradNext, double* gradState, double* gradTau);
 
 // contacts (oracle_contact.cpp)
-void collide(const World& w, const Kin<double>& k, std::vector<Contact>& out);
+// *unsupported (optional) is set when a narrow-phase branch that is not
+// restated was hit (its contacts are dropped).
+void collide(const World& w, const Kin<double>& k, std::vector<Contact>& out, int* unsupported = nullptr);
+int capsuleBox(const Iso<double>& Tb, const double* size, const Iso<double>& Tc, double r, double h, bool boxFirst,
+               double clip, int shape1, int shape2, int body1, int body2, std::vector<Contact>& out,
+               int* unsupported);
 
 // dense helpers
 void cholSolve(const double* A, const double* b, double* x, int n);

@@ -183,8 +183,8 @@ def lcp_debug(ow: "OracleWorld", b=0, max_rows=64):
 
 
 def lcp_flags(ow: "OracleWorld", b=0):
-    """[shortCircuit, ignoredFriction, cfm, numClamping, numUpperBound]"""
-    out = np.zeros(5)
+    """[shortCircuit, ignoredFriction, cfm, numClamping, numUpperBound, unsupportedContacts]"""
+    out = np.zeros(6)
     lib().oracle_lcp_flags(ow.snaps, b, _p(out))
     return out
 
@@ -255,3 +255,17 @@ def box_box(size1, T1, size2, T2):
     t1, t2 = (np.ascontiguousarray(np.asarray(T, dtype=np.float64)[:3, :4]) for T in (T1, T2))
     k = lib().oracle_box_box(_p(s1), _p(t1), _p(s2), _p(t2), _p(out))
     return out[:k]
+
+
+def capsule_box(size, T_box, height, radius, T_capsule, box_first=True, clip=0.03):
+    """collideBoxCapsule (box_first) / collideCapsuleBox restated; rows of
+    (point3, normal3, depth, type) and an `unsupported` flag."""
+    out = np.zeros((16, 8))
+    s = np.ascontiguousarray(size, dtype=np.float64)
+    tb, tc = (np.ascontiguousarray(np.asarray(T, dtype=np.float64)[:3, :4]) for T in (T_box, T_capsule))
+    k = lib().oracle_capsule_box(_p(s), _p(tb), C.c_double(height), C.c_double(radius), _p(tc),
+                                 1 if box_first else 0, C.c_double(clip), _p(out))
+    unsupported = k < 0
+    if k < 0:
+        k = -1 - k
+    return out[:k], unsupported

@@ -110,6 +110,7 @@ void oracle_lcp_flags(void* snaps, int b, double* out) {
   out[2] = s.cfm;
   out[3] = s.numClamping;
   out[4] = s.numUpperBound;
+  out[5] = s.unsupportedContacts;
 }
 // clamping impulses f_c of world b; returns numClamping
 int oracle_lcp_fc(void* snaps, int b, double* fc, int maxc) {

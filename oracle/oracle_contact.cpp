@@ -271,8 +271,9 @@ extern "C" int oracle_box_box(const double* size1, const double* T1, const doubl
 
 namespace oracle {
 
-void collide(const World& w, const Kin<double>& k, std::vector<Contact>& out) {
+void collide(const World& w, const Kin<double>& k, std::vector<Contact>& out, int* unsupported) {
   out.clear();
+  int unsup = 0;
   const int ns = (int)w.shapes.size();
   for (int i = 0; i + 1 < ns; i++) {
     for (int j = i + 1; j < ns; j++) {
@@ -291,6 +292,12 @@ void collide(const World& w, const Kin<double>& k, std::vector<Contact>& out) {
         double A[3] = {0.5 * S1.size[0], 0.5 * S1.size[1], 0.5 * S1.size[2]};
         double Bh[3] = {0.5 * S2.size[0], 0.5 * S2.size[1], 0.5 * S2.size[2]};
         boxBox(T1.p.x, T1.R.m, A, T2.p.x, T2.R.m, Bh, w.clipDepth, pair, i, j, S1.body, S2.body);
+      } else if (S1.type == NIMBLE_SHAPE_BOX && S2.type == NIMBLE_SHAPE_CAPSULE) {
+        // collideBoxCapsule (DARTCollide.cpp:4422); capsule size = (radius, height)
+        capsuleBox(T1, S1.size, T2, S2.size[0], S2.size[1], true, w.clipDepth, i, j, S1.body, S2.body, pair, &unsup);
+      } else if (S1.type == NIMBLE_SHAPE_CAPSULE && S2.type == NIMBLE_SHAPE_BOX) {
+        // collideCapsuleBox (:4533)
+        capsuleBox(T2, S2.size, T1, S1.size[0], S1.size[1], false, w.clipDepth, i, j, S1.body, S2.body, pair, &unsup);
       } else {
         std::fprintf(stderr, "oracle: shape pair (%d,%d) not supported\n", S1.type, S2.type);
         std::abort();
@@ -307,6 +314,7 @@ void collide(const World& w, const Kin<double>& k, std::vector<Contact>& out) {
       }
     }
   }
+  if (unsupported) *unsupported = unsup;
 }
 
 //------------------------------------------------------------------------------

@@ -12,7 +12,8 @@
 //    including the pseudo-inverse gradient branch, and
 //    getJacobianOfLCPOffsetClampingSubset (:3181) for POSITION.
 // Supported contact types: VERTEX_FACE and FACE_VERTEX (box-box face
-// contacts); EDGE_EDGE aborts.
+// contacts), SPHERE_BOX and BOX_SPHERE (capsule/sphere-box, the SPHERE_TO_BOX
+// / BOX_TO_SPHERE branches of :328 and :594); EDGE_EDGE aborts.
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -24,7 +25,7 @@ namespace oracle {
 void codSolve(const double* A, int m, int n, const double* b, double* x);
 
 using Mat = std::vector<double>;
-enum { CT_FACE_VERTEX = 1, CT_VERTEX_FACE = 2, CT_EDGE_EDGE = 3 };
+enum { CT_FACE_VERTEX = 1, CT_VERTEX_FACE = 2, CT_EDGE_EDGE = 3, CT_SPHERE_BOX = 4, CT_BOX_SPHERE = 5 };
 
 static void cross3(const double* a, const double* b, double* o) {
   o[0] = a[1] * b[2] - a[2] * b[1];
@@ -126,14 +127,72 @@ static void constraintForcesJacobian(const World& w, const Kin<double>& k, const
     double dp[3] = {0, 0, 0}, dd[3] = {0, 0, 0};
     const bool pa = parentOf(kk, c.bodyA), pb = parentOf(kk, c.bodyB);
     if (pa && pb) { std::fprintf(stderr, "oracle: self-collision gradients not supported\n"); std::abort(); }
-    int type = 0;  // 0 none, 1 vertex, 2 face
+    int type = 0;  // 0 none, 1 vertex, 2 face, 3 sphere-to-box, 4 box-to-sphere (getDofContactType :116)
     if (pa || pb) {
       if (c.type == CT_EDGE_EDGE) { std::fprintf(stderr, "oracle: EDGE_EDGE position gradients not supported\n"); std::abort(); }
-      if (c.type == CT_VERTEX_FACE) type = pa ? 1 : 2;
+      if (c.type == CT_SPHERE_BOX) type = pa ? 3 : 4;
+      else if (c.type == CT_BOX_SPHERE) type = pa ? 4 : 3;
+      else if (c.type == CT_VERTEX_FACE) type = pa ? 1 : 2;
       else type = pa ? 2 : 1;
     }
     const double wv[3] = {Z[0], Z[1], Z[2]}, vv[3] = {Z[3], Z[4], Z[5]};
-    if (type == 1) {
+    // math::gradientWrtTheta(worldTwist, x, 0) (dart/math/Geometry.cpp:968)
+    auto gwt = [&](const double* x, double* out) {
+      if (std::sqrt(wv[0] * wv[0] + wv[1] * wv[1] + wv[2] * wv[2]) > 1e-6) {
+        cross3(wv, x, out);
+        for (int i = 0; i < 3; i++) out[i] += vv[i];
+      } else {
+        for (int i = 0; i < 3; i++) out[i] = vv[i];
+      }
+    };
+    // remove the components along the locked box faces (:356-372)
+    auto lockProject = [&](double* x) {
+      for (int f = 0; f < 3; f++) {
+        if (!c.faceLocked[f]) continue;
+        const double* fn = c.faceNormal + 3 * f;
+        const double d0 = fn[0] * x[0] + fn[1] * x[1] + fn[2] * x[2];
+        for (int i = 0; i < 3; i++) x[i] -= fn[i] * d0;
+      }
+    };
+    if (type == 3 || type == 4) {
+      double sg[3], dn[3];
+      gwt(c.sphereCenter, sg);
+      const double* nrm = c.normal;
+      double dist2 = 0;
+      for (int i = 0; i < 3; i++) dist2 += (c.sphereCenter[i] - p[i]) * (c.sphereCenter[i] - p[i]);
+      const double norm = std::sqrt(dist2);
+      if (type == 3) {  // SPHERE_TO_BOX
+        for (int i = 0; i < 3; i++) dp[i] = sg[i];
+        lockProject(dp);
+        double cpg[3], spg[3];
+        for (int i = 0; i < 3; i++) { cpg[i] = dp[i]; spg[i] = sg[i]; }
+        if (norm > 1e-5)
+          for (int i = 0; i < 3; i++) { cpg[i] /= norm; spg[i] /= norm; }
+        for (int i = 0; i < 3; i++) dn[i] = c.type == CT_BOX_SPHERE ? cpg[i] - spg[i] : spg[i] - cpg[i];
+      } else {  // BOX_TO_SPHERE
+        double neg[3];
+        for (int i = 0; i < 3; i++) neg[i] = -sg[i];
+        lockProject(neg);
+        double pg[3];
+        gwt(p, pg);
+        for (int i = 0; i < 3; i++) dp[i] = pg[i] + neg[i];
+        double cpg[3];
+        for (int i = 0; i < 3; i++) cpg[i] = dp[i];
+        if (norm > 1e-5)
+          for (int i = 0; i < 3; i++) cpg[i] /= norm;
+        for (int i = 0; i < 3; i++) dn[i] = c.type == CT_BOX_SPHERE ? cpg[i] : -cpg[i];
+      }
+      const double dnn = dn[0] * nrm[0] + dn[1] * nrm[1] + dn[2] * nrm[2];
+      for (int i = 0; i < 3; i++) dn[i] -= dnn * nrm[i];
+      // getContactForceGradient (:1092)
+      if (dirIdx == 0 || dn[0] * dn[0] + dn[1] * dn[1] + dn[2] * dn[2] <= 1e-12) {
+        for (int i = 0; i < 3; i++) dd[i] = dn[i];
+      } else {
+        double T0[3], T1[3];
+        tangentBasisGradient(c.normal, dn, T0, T1);
+        for (int i = 0; i < 3; i++) dd[i] = dirIdx == 1 ? T0[i] : T1[i];
+      }
+    } else if (type == 1) {
       // math::gradientWrtTheta(worldTwist, contactPos, 0)
       if (std::sqrt(wv[0] * wv[0] + wv[1] * wv[1] + wv[2] * wv[2]) > 1e-6) {
         cross3(wv, p, dp);

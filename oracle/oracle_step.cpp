@@ -98,7 +98,7 @@ void step(const World& w, const double* state, const double* tau, std::vector<do
 
   // runConstraintEngine (World.cpp:254): collision + LCP + impulses
   std::vector<Contact> contacts;
-  collide(w, k, contacts);
+  collide(w, k, contacts, &snap.unsupportedContacts);
   solveContacts(w, k, q, v, tau, v1, contacts, lcpCache, snap);
 
   // integratePositions(initialVelocity) (World.cpp:300)

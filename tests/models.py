@@ -96,3 +96,123 @@ def box_states(kind, batch, seed=0, size=(0.4, 0.3, 0.2)):
         v[:, 4] = 0.5 + 0.1 * rng.standard_normal(batch)
     f = 0.5 * rng.standard_normal((batch, 6))
     return np.concatenate([q, v], axis=1), f
+
+
+def half_cheetah_world():
+    """configs[2]: data/skel/half_cheetah.skel (ground box 1500 x 0.05 x 5 +
+    planar cheetah: prismatic x/y + revolute root, six revolute leg joints with
+    damping and springs, capsule colliders), dt 0.002, gravity -y.  Loaded
+    from the JSON export of SkelParser's result (tools/export_assets.py)."""
+    return assets.load_world("half_cheetah_world")
+
+
+def _fk_world(desc, q):
+    """Body world transforms for revolute / prismatic / weld trees (host-side
+    helper for placing synthetic states; the device computes its own)."""
+    nb = int(desc["num_bodies"])
+    Tw = np.zeros((nb, 4, 4))
+    for b in range(nb):
+        Tp = np.eye(4)
+        Tp[:3, :4] = desc["T_parent_joint"][12 * b:12 * b + 12].reshape(3, 4)
+        Tc = np.eye(4)
+        Tc[:3, :4] = desc["T_child_joint"][12 * b:12 * b + 12].reshape(3, 4)
+        J = np.eye(4)
+        jt = int(desc["joint_type"][b])
+        ax = desc["axis"][3 * b:3 * b + 3]
+        if jt == 1:
+            th = q[desc["dof_offset"][b]]
+            K = np.array([[0, -ax[2], ax[1]], [ax[2], 0, -ax[0]], [-ax[1], ax[0], 0]])
+            J[:3, :3] = np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
+        elif jt == 2:
+            J[:3, 3] = ax * q[desc["dof_offset"][b]]
+        elif jt != 0:
+            raise NotImplementedError("free joints: use the device kinematics")
+        par = int(desc["parent"][b])
+        base = Tw[par] if par >= 0 else np.eye(4)
+        Tw[b] = base @ Tp @ J @ np.linalg.inv(Tc)
+    return Tw
+
+
+def lowest_capsule_point(world, q):
+    """Lowest world y over the world's capsule colliders at configuration q."""
+    d = world.desc_arrays()
+    Tw = _fk_world(d, q)
+    low = np.inf
+    for s in range(int(d["num_shapes"])):
+        if int(d["shape_type"][s]) != 2:
+            continue
+        T = np.eye(4)
+        T[:3, :4] = d["shape_T"][12 * s:12 * s + 12].reshape(3, 4)
+        T = Tw[int(d["shape_body"][s])] @ T
+        r, h = d["shape_size"][3 * s], d["shape_size"][3 * s + 1]
+        for z in (h / 2, -h / 2):
+            low = min(low, (T @ np.array([0, 0, z, 1.0]))[1] - r)
+    return low
+
+
+def half_cheetah_states(world, batch, seed=0, angle_scale=0.25, v_scale=0.3, f_scale=5.0,
+                        pen_range=(-4e-3, 2e-3)):
+    """Synthetic half-cheetah states: random joint angles / velocities, the
+    root lowered so the lowest capsule point sits `pen` below the ground top
+    (negative = penetrating; contact for most worlds), random torques."""
+    rng = np.random.default_rng(seed)
+    n = world.getNumDofs()
+    q = np.zeros((batch, n))
+    q[:, 2] = 0.1 * rng.standard_normal(batch)
+    q[:, 3:] = angle_scale * rng.standard_normal((batch, n - 3))
+    q[:, 0] = 0.5 * rng.standard_normal(batch)
+    for b in range(batch):
+        pen = rng.uniform(*pen_range)
+        q[b, 1] = pen - lowest_capsule_point(world, q[b])
+    v = v_scale * rng.standard_normal((batch, n))
+    f = f_scale * rng.standard_normal((batch, n))
+    f[:, :3] = 0.0  # unactuated root (half_cheetah_bench.py force limits)
+    return np.concatenate([q, v], axis=1), f
+
+
+def capsule_edge_world():
+    """A free capsule whose lower cap rests on the top edge of a static box
+    (sphere-box contacts clamped against two faces: non-zero normal
+    gradients), capsule first in detector order (SPHERE_BOX contacts)."""
+    from nimblephysics_amd import dynamics as D
+    w = nimble.World()
+    w.setGravity([0, -9.81, 0])
+    cap = D.Skeleton("capsule")
+    _, b = cap.createFreeJointAndBodyNodePair()
+    b.setMass(0.8)
+    b.setMomentOfInertia(0.02, 0.03, 0.01)
+    b.createShapeNode(D.CapsuleShape(0.05, 0.3), collision=True)
+    w.addSkeleton(cap)
+    ground = D.Skeleton("block")
+    gj, gb = ground.createWeldJointAndBodyNodePair()
+    T = np.eye(4)
+    T[1, 3] = -0.1
+    gj.setTransformFromParentBodyNode(T)
+    gb.createShapeNode(D.BoxShape([0.4, 0.2, 0.4]), collision=True)
+    ground.setMobile(False)
+    w.addSkeleton(ground)
+    return w
+
+
+def capsule_edge_states(batch, seed=0):
+    """Capsule axis tilted up and away from the block's +x top edge (about
+    (1, 1, 0)/sqrt2), lower cap centre just beyond the edge and 1-3 mm closer
+    to it than the cap radius, so the contact is on the cap (sphere branch)
+    and the cap centre is clamped against both the +x and the +y face."""
+    rng = np.random.default_rng(seed)
+    q = np.zeros((batch, 6))
+    v = 0.05 * rng.standard_normal((batch, 6))
+    for b in range(batch):
+        th = 0.5 * np.pi + 0.1 * rng.standard_normal()
+        k = np.array([-1.0, 1.0, 0.2 * rng.standard_normal()])
+        k /= np.linalg.norm(k)
+        q[b, 0:3] = th * k
+        K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+        R = np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
+        a = R @ np.array([0, 0, 1.0])
+        pen = rng.uniform(1e-3, 3e-3)
+        u = np.array([1.0, 1.0, 0.0]) / np.sqrt(2)
+        c = np.array([0.2, 0.0, 0.03 * rng.standard_normal()]) + (0.05 - pen) * u
+        q[b, 3:6] = c + a * 0.15
+    f = 0.3 * rng.standard_normal((batch, 6))
+    return np.concatenate([q, v], axis=1), f

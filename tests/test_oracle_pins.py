@@ -131,3 +131,53 @@ def test_analytic_gradients_vs_finite_differences(oracle_built, name):
         assert o.num_contacts(0) > 0
     assert np.abs(gs - fd_s).max() <= 1e-6 * np.abs(fd_s).max()
     assert np.abs(gf - fd_f).max() <= 1e-6 * np.abs(fd_f).max()
+
+
+def test_capsule_box_known_answers(oracle_built):
+    """Capsule-box narrow phase (libccd MPR + DARTCollide's capsule/sphere-box
+    branches) vs the reference's known-answer tests.  The PIPE_EDGE contact
+    of the third case belongs to a branch the restatement flags as
+    unsupported; its SPHERE_BOX contact must still match."""
+    d = json.load(open(os.path.join(GOLD, "capsule_box_known_answers.json")))
+    for case in d["cases"]:
+        Tc = np.eye(4)
+        Tc[:3, 3] = case["capsule_translation"]
+        for order in ("capsule_first", "box_first"):
+            if order not in case:
+                continue
+            cs, unsupported = O.capsule_box(case["box_size"], np.eye(4), case["height"], case["radius"], Tc,
+                                            box_first=(order == "box_first"))
+            exp = [e for e in case[order]["contacts"] if e["type"] in (4, 5)]
+            assert unsupported == (len(exp) < len(case[order]["contacts"])), case["name"]
+            cs = sorted(cs, key=lambda c: c[2])  # sortContacts(UnitZ)
+            assert len(cs) == len(exp), (case["name"], order, cs)
+            for c, e in zip(cs, exp):
+                assert np.allclose(c[:3], e["point"], atol=1e-10), (case["name"], order)
+                assert np.allclose(c[3:6], e["normal"], atol=1e-10), (case["name"], order)
+                assert abs(c[6] - e["depth"]) < 1e-10 and int(c[7]) == e["type"], (case["name"], order)
+
+
+@pytest.mark.parametrize("name", ["half_cheetah", "capsule_edge"])
+def test_sphere_box_gradients_vs_finite_differences(oracle_built, name):
+    """Analytic Jacobians through capsule-box contacts (BOX_SPHERE on the
+    half-cheetah ground, SPHERE_BOX clamped on two faces at a block edge --
+    the non-zero normal-gradient branch) vs central differences."""
+    if name == "half_cheetah":
+        w = models.half_cheetah_world()
+        st, f = models.half_cheetah_states(w, 12, seed=1)
+        picks = [1, 3, 4]
+    else:
+        w = models.capsule_edge_world()
+        st, f = models.capsule_edge_states(8, seed=1)
+        picks = [2, 6, 0]
+    o = O.OracleWorld(w)
+    o.forward(st, f)
+    clamped = 0
+    for b in picks:
+        assert o.num_contacts(b) > 0 and O.lcp_flags(o, b)[5] == 0
+        clamped += O.lcp_flags(o, b)[3] > 0
+        g = np.random.default_rng(b).standard_normal(st.shape[1])
+        gs, gf, fd_s, fd_f = _fd_check(w, st[b], f[b], g)
+        assert np.abs(gs - fd_s).max() <= 1e-6 * np.abs(fd_s).max(), (name, b)
+        assert np.abs(gf - fd_f).max() <= 1e-6 * np.abs(fd_f).max(), (name, b)
+    assert clamped >= 2

@@ -4,7 +4,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from nimblephysics_amd import assets, urdf  # noqa: E402
+from nimblephysics_amd import assets, skel, urdf  # noqa: E402
 
 REF = os.environ.get("NIMBLE_REFERENCE", "/root/reference")
 MODELS = {
@@ -15,9 +15,18 @@ MODELS = {
     "cartpole_urdf": ("data/urdf/cartpole.urdf", False),
 }
 
+WORLDS = {
+    "half_cheetah_world": "data/skel/half_cheetah.skel",
+}
+
 if __name__ == "__main__":
     for name, (rel, ignore_mesh) in MODELS.items():
-        skel = urdf.load_urdf(os.path.join(REF, rel), ignore_mesh_collisions=ignore_mesh)
+        sk = urdf.load_urdf(os.path.join(REF, rel), ignore_mesh_collisions=ignore_mesh)
         out = os.path.join(assets.ASSET_DIR, name + ".json")
-        assets.save_skeleton(skel, out)
-        print(name, skel.getNumDofs(), "dofs", len(skel.bodies), "bodies ->", out)
+        assets.save_skeleton(sk, out)
+        print(name, sk.getNumDofs(), "dofs", len(sk.bodies), "bodies ->", out)
+    for name, rel in WORLDS.items():
+        w = skel.read_world(os.path.join(REF, rel))
+        out = os.path.join(assets.ASSET_DIR, name + ".json")
+        assets.save_world(w, out)
+        print(name, w.getNumDofs(), "dofs", [len(s.bodies) for s in w.skeletons], "bodies ->", out)

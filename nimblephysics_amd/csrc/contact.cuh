@@ -23,6 +23,7 @@
 #include "model.h"
 #include "spatial.cuh"
 #include "pool_sizes.h"
+#include "capsule.cuh"
 
 #define CT_FACE_VERTEX 1
 #define CT_VERTEX_FACE 2
@@ -423,6 +424,18 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
         const double A[3] = {0.5 * md.shapeSize[si][0], 0.5 * md.shapeSize[si][1], 0.5 * md.shapeSize[si][2]};
         const double B[3] = {0.5 * md.shapeSize[sj][0], 0.5 * md.shapeSize[sj][1], 0.5 * md.shapeSize[sj][2]};
         cnt = deviceBoxBox(p1, R1, A, p2, R2, B, md.clipDepth, bi, bj, pairbuf + lane * 8 * CREC);
+      } else if ((md.shapeType[si] == NIMBLE_SHAPE_BOX && md.shapeType[sj] == NIMBLE_SHAPE_CAPSULE) ||
+                 (md.shapeType[si] == NIMBLE_SHAPE_CAPSULE && md.shapeType[sj] == NIMBLE_SHAPE_BOX)) {
+        // collideBoxCapsule / collideCapsuleBox (DARTCollide.cpp:4422, :4533)
+        const bool boxFirst = md.shapeType[si] == NIMBLE_SHAPE_BOX;
+        const int sb = boxFirst ? si : sj, sc = boxFirst ? sj : si;
+        double Tb[12], Tc[12];
+        tmul(s + L.Tw + 12 * md.shapeBody[sb], md.shapeT[sb], Tb);
+        tmul(s + L.Tw + 12 * md.shapeBody[sc], md.shapeT[sc], Tc);
+        int unsup = 0;
+        cnt = deviceCapsuleBox(Tb, md.shapeSize[sb], Tc, md.shapeSize[sc][0], md.shapeSize[sc][1], boxFirst,
+                               md.clipDepth, bi, bj, sb, pairbuf + lane * 8 * CREC, &unsup);
+        if (unsup) cnt = -1 - cnt;  // flagged; the contacts found are still kept
       } else {
         cnt = -1;
       }
@@ -432,8 +445,8 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
     if (lane == 0) {
       int nk = (int)ct[H_NCON], nd = (int)ct[H_NDROP], st = (int)ct[H_STATUS];
       for (int q = 0; q < PC && p0 + q < md.numPairs; q++) {
-        const int cnt = (int)ct[H_PAIRCNT + q];
-        if (cnt < 0) { st |= ST_UNSUPPORTED_SHAPE; continue; }
+        int cnt = (int)ct[H_PAIRCNT + q];
+        if (cnt < 0) { st |= ST_UNSUPPORTED_SHAPE; cnt = -1 - cnt; }
         for (int c = 0; c < cnt; c++) {
           const double* rec = pairbuf + (q * 8 + c) * CREC;
           bool close = false;
@@ -1463,6 +1476,87 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
   return imp;
 }
 
+// Sphere-box contact rows (SPHERE_BOX / BOX_SPHERE): the full derivative
+// (T_A - T_B) . [p x dd + dp x d; dd] for dof k, with the contact position
+// and normal gradients of DifferentiableContactConstraint.cpp:353 (SPHERE_TO_BOX:
+// the sphere centre's motion with the locked box-face components removed),
+// :376 (BOX_TO_SPHERE), :640/:672 (normal gradients) and :1092 (friction
+// directions).  Locked face normals are the box's world axes (type field:
+// mask << 4, box shape << 8).
+__device__ double sphereRowTerm(const ModelDev& md, const double* s, const Layout& L, const BwdPool& P, int j,
+                                const double* rec, const double* rr, const double* Z, int bk) {
+  const int A = (int)rec[8], B = (int)rec[9], typ = (int)rec[7], type = typ & 15;
+  const bool pa = (md.anc[A] >> bk) & 1ull, pb = (md.anc[B] >> bk) & 1ull;
+  if (pa == pb) return 0.0;  // unrelated dof (self-collision is off by default)
+  const bool sphereToBox = type == CT_SPHERE_BOX ? pa : pb;
+  const int mask = (typ >> 4) & 7, shape = typ >> 8;
+  const double* p = rec;
+  const double* nrm = rec + 3;
+  const double* c = rec + 10;
+  const double wv[3] = {Z[0], Z[1], Z[2]};
+  const bool rotates = sqrt(Z[0] * Z[0] + Z[1] * Z[1] + Z[2] * Z[2]) > 1e-6;
+  // gradientWrtTheta(Z, x, 0) (dart/math/Geometry.cpp:968)
+  auto gwt = [&](const double* x, double* o) {
+    if (rotates) { cross3(wv, x, o); for (int i = 0; i < 3; i++) o[i] += Z[3 + i]; }
+    else { for (int i = 0; i < 3; i++) o[i] = Z[3 + i]; }
+  };
+  auto lockProject = [&](double* x) {
+    if (!mask) return;
+    const double* Tw = s + L.Tw + 12 * md.shapeBody[shape];
+    const double* Ts = md.shapeT[shape];
+    for (int f = 0; f < 3; f++) {
+      if (!((mask >> f) & 1)) continue;
+      double fn[3];
+      for (int r = 0; r < 3; r++) fn[r] = Tw[4 * r] * Ts[f] + Tw[4 * r + 1] * Ts[4 + f] + Tw[4 * r + 2] * Ts[8 + f];
+      const double d0 = dot3(fn, x);
+      for (int i = 0; i < 3; i++) x[i] -= fn[i] * d0;
+    }
+  };
+  double sg[3], dp[3], dn[3];
+  gwt(c, sg);
+  double dist2 = 0.0;
+  for (int i = 0; i < 3; i++) dist2 += (c[i] - p[i]) * (c[i] - p[i]);
+  const double norm = sqrt(dist2);
+  const double inv = norm > 1e-5 ? 1.0 / norm : 1.0;
+  if (sphereToBox) {
+    for (int i = 0; i < 3; i++) dp[i] = sg[i];
+    lockProject(dp);
+    for (int i = 0; i < 3; i++) {
+      const double cpg = dp[i] * inv, spg = sg[i] * inv;
+      dn[i] = type == CT_BOX_SPHERE ? cpg - spg : spg - cpg;
+    }
+  } else {
+    double neg[3], pg[3];
+    for (int i = 0; i < 3; i++) neg[i] = -sg[i];
+    lockProject(neg);
+    gwt(p, pg);
+    for (int i = 0; i < 3; i++) {
+      dp[i] = pg[i] + neg[i];
+      dn[i] = type == CT_BOX_SPHERE ? dp[i] * inv : -dp[i] * inv;
+    }
+  }
+  const double dnn = dot3(dn, nrm);
+  for (int i = 0; i < 3; i++) dn[i] -= dnn * nrm[i];
+  double dd[3];
+  const int dirIdx = (int)rr[RR_DIR];
+  if (dirIdx == 0 || dot3(dn, dn) <= 1e-12) {
+    for (int i = 0; i < 3; i++) dd[i] = dn[i];
+  } else {
+    double T0[3], T1[3];
+    tangentBasisGradient(nrm, dn, T0, T1);
+    for (int i = 0; i < 3; i++) dd[i] = dirIdx == 1 ? T0[i] : T1[i];
+  }
+  const double* d = rr + RR_D;
+  double pxdd[3], dpxd[3];
+  cross3(p, dd, pxdd);
+  cross3(dp, d, dpxd);
+  double v = 0.0;
+  for (int i = 0; i < 3; i++)
+    v += (P.TAB[j * 12 + i] - P.TAB[j * 12 + 6 + i]) * (pxdd[i] + dpxd[i]) +
+         (P.TAB[j * 12 + 3 + i] - P.TAB[j * 12 + 9 + i]) * dd[i];
+  return v;
+}
+
 // sum_j (G_j^T g_j)[k] for every direction k (lane k, position generator Z),
 // G_j = d(J^T e_j)/dq (DifferentiableContactConstraint.cpp:1654), grouped by
 // contact body c instead of by row:
@@ -1516,7 +1610,7 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
           for (int i = 0; i < 6; i++) om[i] = fma(gr, wr[i], om[i]);
         }
         // vertex side of this row?
-        const int type = (int)rec[7];
+        const int type = (int)rec[7] & 15;
         const bool vertexSide = (type == CT_VERTEX_FACE && A == c) || (type == CT_FACE_VERTEX && B == c);
         if (vertexSide && lane == 0) {
           double tw[3], dxt[3], pxd[3];
@@ -1562,7 +1656,11 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
       const double* rr = rows + j * SN_ROWREC;
       if ((int)rr[RR_MAP] == CM_NOT_CLAMPING) continue;
       const double* rec = sn + SN_CONTACTS + (int)rr[RR_CONTACT] * CREC;
-      const int A = (int)rec[8], B = (int)rec[9], type = (int)rec[7];
+      const int A = (int)rec[8], B = (int)rec[9], typ = (int)rec[7], type = typ & 15;
+      if (type == CT_SPHERE_BOX || type == CT_BOX_SPHERE) {
+        acc += sphereRowTerm(md, s, L, P, j, rec, rr, Z, bk);
+        continue;
+      }
       int faceBody = -1;
       if (type == CT_VERTEX_FACE) faceBody = B;
       else if (type == CT_FACE_VERTEX) faceBody = A;

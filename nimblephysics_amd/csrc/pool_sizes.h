@@ -6,8 +6,10 @@
 
 #include "../../include/nimble_amd.h"
 
-// contact record: point3 normal3 depth type bodyA bodyB
-#define CREC 10
+// contact record: point3 normal3 depth type bodyA bodyB sphereCentre3
+// (sphere-box types encode the locked-face mask and the box shape in `type`,
+// see capsule.cuh)
+#define CREC 13
 
 // contact-stage LDS region (Layout::ct)
 #define CT_CONTACTS 32

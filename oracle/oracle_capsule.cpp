@@ -20,8 +20,9 @@
 //    math::prepareConvex2DShape / pointInPlane (dart/math/Geometry.cpp:3813,
 //    :3843), convex2DShapeContains (:3756), get2DLineIntersection (:3790).
 // Not restated (flagged `unsupported`, contact dropped): the vertex-pipe and
-// edge-pipe branches (1 or 2 box witness points, :3071/:3110) and EDGE_PIPE /
-// PIPE_EDGE contacts from a capsule crossing a face boundary.
+// edge-pipe branches (1 or 2 box witness points, :3071/:3110), the 8-point
+// witness set of a zero penetration direction, and EDGE_PIPE / PIPE_EDGE
+// contacts from a capsule crossing a face boundary.
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -76,7 +77,8 @@ inline V rotT(const Xf& T, const V& v) {
             T.R[2] * v.x[0] + T.R[5] * v.x[1] + T.R[8] * v.x[2]);
 }
 inline V xf(const Xf& T, const V& v) { return rot(T, v) + T.p; }
-inline V xfInv(const Xf& T, const V& v) { return rotT(T, v - T.p); }
+// Eigen's Isometry inverse applied to v: R^T v + (-(R^T p))
+inline V xfInv(const Xf& T, const V& v) { return rotT(T, v) - rotT(T, T.p); }
 inline V col(const Xf& T, int c) { return mk(T.R[c], T.R[3 + c], T.R[6 + c]); }
 
 // ccd objects: box (size) or capsule (radius, height)
@@ -615,7 +617,8 @@ int capsuleBox(const Iso<double>& Tb, const double* size, const Iso<double>& Tc,
   }
   // pipe branch: box witness points, createCapsuleMeshContact
   std::vector<V> W = witnessBox(box, dir, !boxFirst ? true : false);
-  if (W.size() <= 2) { *unsupported = 1; return 0; }
+  // 1-2 points: vertex-/edge-pipe branches; > 4: a zero penetration direction
+  if (W.size() <= 2 || W.size() > 4) { *unsupported = 1; return 0; }
   V capA = xf(cap.T, mk(0, 0, h / 2)), capB = xf(cap.T, mk(0, 0, -h / 2));
   V normal = eigNormalized(cross(W[0] - W[1], W[1] - W[2]));
   if (normal.x[0] * dir.x[0] + normal.x[1] * dir.x[1] + normal.x[2] * dir.x[2] > 0) normal = normal * -1.0;

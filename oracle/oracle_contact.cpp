@@ -589,6 +589,9 @@ void solveContacts(const World& w, const Kin<double>& k, const double* q, const 
   snap.numClamping = 0;
   snap.numUpperBound = 0;
   snap.contacts.clear();
+  snap.shortCircuit = false;
+  snap.ignoredFriction = false;
+  snap.cfm = 0.0;
   // ConstraintSolver::updateConstraints (ConstraintSolver.cpp:520)
   std::vector<Contact> contacts;
   for (const Contact& c : contactsIn) {

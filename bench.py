@@ -31,10 +31,26 @@ from nimblephysics_amd import _native  # noqa: E402
 FP64_VECTOR_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (spec; = FP32 vector 157.3 / 2)
 HBM_PEAK_GBS = 8000.0
 
+def _atlas_states(world, batch, seed):
+    return models.random_states(world, batch, seed=seed, q_scale=0.02, v_scale=0.05, f_scale=1.0)
+
+
+def _cheetah_states(world, batch, seed):
+    return models.half_cheetah_states(world, batch, seed=seed)
+
+
+# name -> (description, world factory, synthetic state sampler, metric, default worlds per GPU)
 WORKLOADS = {
-    "atlas": ("Atlas 33-DoF (atlas_v3_box_colliders) + ground, foot contact", lambda: models.atlas_world(True)),
-    "atlas_air": ("Atlas 33-DoF, no ground (contact-free)", lambda: models.atlas_world(False)),
-    "cartpole": ("cartpole, contact-free", models.cartpole_world),
+    "atlas": ("Atlas 33-DoF (atlas_v3_box_colliders) + ground, foot contact", lambda: models.atlas_world(True),
+              _atlas_states, "differentiable timesteps/sec (fwd+bwd), 1024-env Atlas w/ contact", 1024),
+    "atlas_air": ("Atlas 33-DoF, no ground (contact-free)", lambda: models.atlas_world(False), _atlas_states,
+                  "differentiable timesteps/sec (fwd+bwd), Atlas contact-free", 1024),
+    "cartpole": ("cartpole, contact-free", models.cartpole_world, _atlas_states,
+                 "differentiable timesteps/sec (fwd+bwd), 1024-env cartpole (configs[1])", 1024),
+    "half_cheetah": ("half-cheetah 9-DoF (data/skel/half_cheetah.skel), capsules on the ground box",
+                     models.half_cheetah_world, _cheetah_states,
+                     "differentiable timesteps/sec (fwd+bwd), 4096-env half-cheetah w/ ground contact (configs[2])",
+                     4096),
 }
 
 
@@ -147,7 +163,7 @@ def contact_stats(world, state, action):
             "worlds_in_contact": float((h[:, 0] > 0).mean())}
 
 
-def pmc_traffic(kernel, batch):
+def pmc_traffic(workload, kernel, batch):
     """HBM bytes per launch of `kernel` from the committed PMC summary
     (profiles/pmc_traffic.json: per-world FETCH_SIZE x2 (gfx950 correction)
     + WRITE_SIZE, measured by tools/pmc_traffic.py); None when absent."""
@@ -156,16 +172,16 @@ def pmc_traffic(kernel, batch):
         return None
     try:
         d = json.load(open(path))
-        return float(d[kernel]["bytes_per_world"]) * batch
+        return float(d[workload][kernel]["bytes_per_world"]) * batch
     except Exception:
         return None
 
 
-def cpu_baseline(world, batch, seconds_target=12.0):
+def cpu_baseline(world, batch, sampler, seconds_target=12.0):
     """Oracle (CPU restatement, 1 thread) on a bounded sample of the same workload."""
     from oracle.oracle import OracleWorld
     o = OracleWorld(world)
-    st, f = models.random_states(world, batch, seed=11, q_scale=0.02, v_scale=0.05, f_scale=1.0)
+    st, f = sampler(world, batch, 11)
     g = np.random.default_rng(5).standard_normal(st.shape)
     steps = 0
     t0 = time.perf_counter()
@@ -184,7 +200,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=1024, help="worlds per GPU")
+    ap.add_argument("--batch", type=int, default=0, help="worlds per GPU (default: the workload's)")
     ap.add_argument("--workload", default="atlas", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather-grads", type=int, default=-1,
@@ -194,10 +210,12 @@ def main():
     dist, rank, ws, local = init_dist()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    wl_name, make = WORKLOADS[args.workload]
+    wl_name, make, sampler, metric, default_batch = WORKLOADS[args.workload]
+    if args.batch <= 0:
+        args.batch = default_batch
     world = make()
     n = world.getNumDofs()
-    st, f = models.random_states(world, args.batch, seed=1000 + rank, q_scale=0.02, v_scale=0.05, f_scale=1.0)
+    st, f = sampler(world, args.batch, 1000 + rank)
     state = torch.tensor(st, device=dev)
     action = torch.tensor(f, device=dev)
     g = torch.tensor(np.random.default_rng(rank).standard_normal(st.shape), device=dev)
@@ -232,10 +250,11 @@ def main():
     achieved = flops[dom] * args.batch / (dom_ms * 1e-3) / 1e12
     if rank == 0:
         out = {
-            "metric": "differentiable timesteps/sec (fwd+bwd), 1024-env Atlas w/ contact",
+            "metric": metric,
             "value": value, "unit": "timesteps/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f64", "data": "synthetic (perturbed standing pose, random torques)",
+            "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (perturbed poses near / in ground contact, random torques)",
             "config": {"workload": wl_name, "worlds_per_gpu": args.batch, "dofs": n,
                        "global_batch": args.batch * ws,
                        "parallelism": f"independent worlds x{ws}" + (" + RCCL all-gather of action grads" if gather else ""),
@@ -245,12 +264,12 @@ def main():
             "kernels_ms": {"forward": fwd_ms, "backward": bwd_ms},
             "roofline": {"bound": "mfma", "kernel": f"nimble_{dom}_kernel", "achieved": achieved,
                          "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP64_VECTOR_PEAK_TFLOPS,
-                         "traffic": pmc_traffic(f"nimble_{dom}_kernel", args.batch),
+                         "traffic": pmc_traffic(args.workload, f"nimble_{dom}_kernel", args.batch),
                          "flops_per_world": flops[dom],
                          "note": "fp64 VALU-bound (no fp64 MFMA use); peak = fp64 vector rate"},
         }
         if not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(make(), 64)
+            out["cpu_baseline"] = cpu_baseline(make(), 64, sampler)
         print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()

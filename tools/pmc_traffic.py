@@ -2,7 +2,9 @@
 gfx950's TCC slots require) into profiles/pmc_traffic.json: HBM-side bytes
 per launch and per world for each nimble kernel.
 
-  python tools/pmc_traffic.py <fetch_dir> <write_dir> <worlds_per_launch> [out.json]
+  python tools/pmc_traffic.py <fetch_dir> <write_dir> <worlds_per_launch> [workload] [out.json]
+
+The summary is stored under the workload's key (bench.py --workload).
 
 FETCH_SIZE/WRITE_SIZE are reported by rocprofv3 in KiB.  Per
 MI355X_MICROARCH.md (HBM section) FETCH_SIZE counts half of the bytes of wide
@@ -29,7 +31,8 @@ def load(d, counter):
 
 def main():
     fdir, wdir, worlds = sys.argv[1], sys.argv[2], int(sys.argv[3])
-    out = sys.argv[4] if len(sys.argv) > 4 else "profiles/pmc_traffic.json"
+    wl = sys.argv[4] if len(sys.argv) > 4 else "atlas"
+    out = sys.argv[5] if len(sys.argv) > 5 else "profiles/pmc_traffic.json"
     res = {}
     for k in ("nimble_forward_kernel", "nimble_backward_kernel"):
         fe = [v for n, v in load(fdir, "FETCH_SIZE") if k in n]
@@ -42,7 +45,9 @@ def main():
         res[k] = {"fetch_kib_raw": fkb, "write_kib": wkb, "launches": len(fe),
                   "bytes_per_launch": per_launch, "bytes_per_world": per_launch / worlds,
                   "worlds_per_launch": worlds, "fetch_correction": "x2 (gfx950 FETCH_SIZE)"}
-    json.dump(res, open(out, "w"), indent=1)
+    allw = json.load(open(out)) if os.path.exists(out) else {}
+    allw[wl] = res
+    json.dump(allw, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
 

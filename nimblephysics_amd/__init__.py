@@ -7,5 +7,6 @@ Drop-in for the reference's ``nimble.timestep`` hot path
 from . import dynamics, simulation  # noqa: F401
 from .simulation import World  # noqa: F401
 from .timestep import TimestepLayer, timestep  # noqa: F401
+from .loader import loadWorld  # noqa: F401
 
-__all__ = ["dynamics", "simulation", "World", "timestep", "TimestepLayer"]
+__all__ = ["dynamics", "simulation", "World", "timestep", "TimestepLayer", "loadWorld"]

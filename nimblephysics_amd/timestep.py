@@ -10,6 +10,12 @@ model), and the whole batch is one kernel launch each way.
 World-side effects match the reference for the 1-D case: the world's
 positions/velocities are set to the returned state and the control forces are
 cleared (World::step(resetCommand=true) via forwardPass(world)).
+
+CPU tensors (what the reference's layer takes, timestep.py:31 calls
+``state.detach().numpy()``) are accepted as a drop-in convenience: they are
+staged to the current HIP device, stepped by the same kernels, and the
+results / gradients come back on the CPU.  There is no CPU compute path --
+without a HIP device the call raises.
 """
 from __future__ import annotations
 
@@ -49,11 +55,24 @@ def _batch_state(world: World, batch: int, dev, device) -> BatchState:
     return bs
 
 
+def _compute_device(t: torch.Tensor) -> torch.device:
+    if t.device.type != "cpu":
+        return t.device
+    if not torch.cuda.is_available():
+        raise RuntimeError("nimblephysics_amd.timestep runs on a HIP device (MI355X); no GPU is visible "
+                           "and there is no CPU fallback")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
 class TimestepLayer(torch.autograd.Function):
     @staticmethod
     def forward(ctx, world: World, state: torch.Tensor, action: torch.Tensor, mass: Optional[torch.Tensor]):
         if mass is not None:
             raise NotImplementedError("mass gradients (WithRespectToMass) are not on the batched hot path yet")
+        ctx.out_device = state.device
+        cdev = _compute_device(state)
+        state = state.to(cdev, torch.float64)
+        action = action.to(cdev, torch.float64)
         squeeze = state.dim() == 1
         st = state.detach().reshape(1, -1) if squeeze else state.detach()
         act = action.detach().reshape(1, -1) if squeeze else action.detach()
@@ -81,23 +100,24 @@ class TimestepLayer(torch.autograd.Function):
             out_cpu = nxt[0].cpu().numpy()
             world.setState(out_cpu)
             world.setControlForces(out_cpu[:n] * 0.0)
-            return nxt[0]
-        return nxt
+            return nxt[0].to(ctx.out_device)
+        return nxt.to(ctx.out_device)
 
     @staticmethod
     def backward(ctx, grad_next):
         st, forces, snap, idx = ctx.saved_tensors
         world = ctx.world
-        g = grad_next.detach().reshape(st.shape).contiguous().to(torch.float64)
+        g = grad_next.detach().reshape(st.shape).to(st.device, torch.float64).contiguous()
         dev = world.native()
         gs = torch.empty_like(st)
         gf = torch.empty_like(forces)
         stream = torch.cuda.current_stream(st.device).cuda_stream
         dev.backward(st, forces, snap, g, gs, gf, stream)
         ga = gf.index_select(1, idx)
+        od = ctx.out_device
         if ctx.squeeze:
-            return None, gs[0], ga[0], None
-        return None, gs, ga, None
+            return None, gs[0].to(od), ga[0].to(od), None
+        return None, gs.to(od), ga.to(od), None
 
 
 def timestep(world: World, state: torch.Tensor, action: torch.Tensor,

@@ -60,3 +60,50 @@ def test_single_world_api():
     assert out.shape == (4,)
     assert _rel(out.cpu().numpy(), ref) < RTOL
     assert np.allclose(world.getState(), out.cpu().numpy())
+
+
+def test_reference_example_half_cheetah_cpu_tensors():
+    """python/new_examples/half_cheetah.py as written for the reference:
+    nimble.loadWorld("half_cheetah.skel"), 1-D CPU tensors of
+    getStateSize() / getActionSize(), chained nimble.timestep calls, then a
+    backward through the chain -- checked step by step against the oracle."""
+    import nimblephysics_amd as nimble
+    world = nimble.loadWorld("half_cheetah.skel")
+    o = OracleWorld(world)
+    state = torch.zeros((world.getStateSize()), dtype=torch.float64, requires_grad=True)
+    action = torch.zeros((world.getActionSize()), dtype=torch.float64)
+    n = world.getNumDofs()
+    cur = state
+    ref = np.zeros(2 * n)
+    forces = np.zeros(n)
+    contact_steps = 0
+    for _ in range(100):  # first ground contact at step 63
+        cur = nimble.timestep(world, cur, action)
+        assert cur.device.type == "cpu" and cur.shape == (2 * n,)
+        ref = o.forward(ref[None], forces[None])[0]
+        contact_steps += o.num_contacts(0) > 0
+        assert _rel(cur.detach().numpy(), ref) < RTOL
+    assert contact_steps > 10
+    cur.sum().backward()
+    assert state.grad is not None and state.grad.device.type == "cpu"
+    assert np.isfinite(state.grad.numpy()).all()
+
+
+def test_kr5_single_world_cpu_tensors():
+    """configs[0]: the 6-DoF KR5 arm, one world, CPU tensors through
+    nimble.timestep (forward + backward) vs the oracle."""
+    import nimblephysics_amd as nimble
+    world = models.kr5_world()
+    st, f = models.random_states(world, 1, seed=17)
+    o = OracleWorld(world)
+    ref = o.forward(st, f)[0]
+    g = np.random.default_rng(1).standard_normal(st.shape[1])
+    rgs, rgf = o.backward(g[None])
+    ts = torch.tensor(st[0], requires_grad=True)
+    tf = torch.tensor(f[0], requires_grad=True)
+    out = nimble.timestep(world, ts, tf)
+    out.backward(torch.tensor(g))
+    assert out.device.type == "cpu"
+    assert _rel(out.detach().numpy(), ref) < RTOL
+    assert _rel(ts.grad.numpy(), rgs[0]) < RTOL
+    assert _rel(tf.grad.numpy(), rgf[0]) < RTOL

@@ -22,7 +22,9 @@ nxt = torch.empty_like(state)
 s = torch.cuda.current_stream().cuda_stream
 n = w.getNumDofs()
 a8 = lambda x: ((x + 7) // 8) * 8
-ws = a8(a8(800 + 2 * n) + 2 * n * 48 + 2 * 2304) + 1000  # snapWorkspaceOffset(n) + 1000
+CREC = 13  # csrc/pool_sizes.h
+SN_VF = 16 + 16 * CREC + 48 * 12 + 48
+ws = a8(a8(SN_VF + 2 * n) + 2 * n * 48 + 2 * 2304) + 1000  # snapWorkspaceOffset(n) + 1000
 for it in range(4):
     snap[:, ws:ws + 100] = 0
     prev_state, prev_cache = state.clone(), cache.clone()

@@ -38,6 +38,121 @@ __device__ inline double* carveCod(double* w, double* A, int m, int n, int ld, C
   return w;
 }
 
+// Register-resident column-pivoted QR for m <= R rows: lane j keeps column
+// j in R registers for the whole factorisation.  Columns never move between
+// lanes; each lane carries its column's current slot `pos` instead, so a
+// pivot swap is two slot exchanges rather than a column copy, and ties go to
+// the lowest slot, as in the sequential scan.  Per step the pivot lane
+// stages its column in `vb` (LDS, >= R doubles), every lane reads it back
+// as the Householder vector (broadcast reads), and the reflector application
+// and the next step's partial norms are unpredicated per-lane FMA chains
+// (inactive lanes scale by 0).  alpha = sqrt(partial norm of the pivot
+// column), which the previous step recomputed over rows >= k.  The pivot
+// column is final after its step and is written to slot k of A right away
+// (R part by the pivot lane, reflector tail lane-parallel), so A ends in
+// the layout of the LDS factorisation, with perm / vd / vn.  Cost per step:
+// ~4R dependent-free VALU ops per lane plus two LDS round trips, instead of
+// 2(m-k) LDS round trips.
+template <bool kLds, int R>
+__device__ void codQrRegs(typename Space<kLds>::dptr A, Cod& c, typename Space<kLds>::dptr vb, int lane) {
+  const int m = c.m, n = c.n, ld = c.ld;
+  const bool col = lane < n;
+  const int cl = col ? lane : 0;
+  double a[R];
+#pragma unroll
+  for (int i = 0; i < R; i++) {
+    double v = A[(i < m ? i : 0) * ld + cl];
+    a[i] = (col && i < m) ? v : 0.0;
+  }
+  double norm = 0.0;
+#pragma unroll
+  for (int i = 0; i < R; i++) norm += a[i] * a[i];
+  int pos = lane;
+  WSYNC();  // every column is in registers: A may now be overwritten
+  for (int k = 0; k < c.kmax; k++) {
+    const bool cand = col && pos >= k;
+    const double best = -waveMin(cand ? -norm : 1.0);
+    const unsigned long long tie = __ballot(cand && norm == best);
+    int pl = __ffsll((long long)tie) - 1;
+    if (__popcll(tie) > 1) {
+      // lowest slot among equal maxima
+      const int ps = (int)waveMin((tie >> lane) & 1ull ? (double)pos : 1e9);
+      pl = waveFirst(((tie >> lane) & 1ull) && pos == ps);
+    }
+    const int ppos = rdli(pos, pl);
+    if (ppos != k) {
+      const int q = waveFirst(col && pos == k);
+      if (lane == q) pos = ppos;
+      if (lane == pl) pos = k;
+    }
+    if (lane == pl) {
+#pragma unroll
+      for (int i = 0; i < R; i++) vb[i] = a[i];
+    }
+    WSYNC();
+    if (best == 0.0) {
+      // zero column: no reflector; the column stays, fresh partial norms
+      // over rows >= k+1
+      if (lane == 0) c.vn[k] = -1.0;
+      if (lane < m) A[lane * ld + k] = vb[lane];
+      double nrm = 0.0;
+#pragma unroll
+      for (int i = 0; i < R; i++) {
+        const double t = i > k ? a[i] : 0.0;
+        nrm += t * t;
+      }
+      norm = nrm;
+      WSYNC();
+      continue;
+    }
+    const double akk = vb[k];
+    double alpha = sqrt(best);
+    if (akk > 0) alpha = -alpha;
+    const double vk = akk - alpha;
+    WSYNC();
+    if (lane <= k) vb[lane] = lane == k ? vk : 0.0;
+    WSYNC();
+    double v[R];
+#pragma unroll
+    for (int i = 0; i < R; i++) v[i] = vb[i];
+    double vn0 = 0.0, vn1 = 0.0, sc0 = 0.0, sc1 = 0.0;
+#pragma unroll
+    for (int i = 0; i < R; i += 2) {
+      vn0 += v[i] * v[i];
+      sc0 += v[i] * a[i];
+      if (i + 1 < R) { vn1 += v[i + 1] * v[i + 1]; sc1 += v[i + 1] * a[i + 1]; }
+    }
+    const double vnorm = unid(vn0 + vn1);
+    const bool act = col && pos >= k;
+    const double sc = act && vnorm > 0 ? 2 * (sc0 + sc1) / vnorm : 0.0;
+    double nrm = 0.0;
+#pragma unroll
+    for (int i = 0; i < R; i++) {
+      a[i] -= sc * v[i];
+      const double t = i > k ? a[i] : 0.0;
+      nrm += t * t;
+    }
+    norm = nrm;
+    // slot k is final: R part from the pivot lane, reflector tail below
+    if (lane == pl) {
+#pragma unroll
+      for (int i = 0; i < R; i++)
+        if (i <= k && i < m) A[i * ld + k] = a[i];
+    }
+    if (lane > k && lane < m) A[lane * ld + k] = vb[lane];
+    if (lane == 0) { c.vd[k] = vk; c.vn[k] = vnorm; }
+    WSYNC();
+  }
+  if (col) {
+    if (pos >= c.kmax) {
+#pragma unroll
+      for (int i = 0; i < R; i++)
+        if (i < m) A[i * ld + pos] = a[i];
+    }
+    c.perm[pos] = lane;
+  }
+}
+
 // Lane-parallel factorisation: column norms live in registers (lane j =
 // column j), the pivot is a wave arg-max (first index among equal maxima, as
 // the sequential scan), alpha and |v|^2 are wave reductions, and the
@@ -58,6 +173,16 @@ __device__ void codFactor(typename Space<kLds>::dptr Ain, typename Space<kLds>::
   double* v = (double*)vIn;
   double* A = c.A;
   const int m = c.m, n = c.n, ld = c.ld;
+  double maxPivot = 0.0;
+#ifndef NIMBLE_COD_LDS_ONLY
+  if (m <= 24) {
+    WSYNC();
+    codQrRegs<kLds, 24>(Ain, c, vIn, lane);
+    WSYNC();
+    goto rankAndRz;
+  }
+#endif
+  {
   if (lane < n) c.perm[lane] = lane;
   double norm = 0.0;  // partial norm of column `lane` over rows >= k
   if (lane < n) {
@@ -65,7 +190,6 @@ __device__ void codFactor(typename Space<kLds>::dptr Ain, typename Space<kLds>::
     for (int i = 0; i < m; i++) norm += A[i * ld + lane] * A[i * ld + lane];
   }
   WSYNC();
-  double maxPivot = 0.0;
   for (int k = 0; k < c.kmax; k++) {
     // pivot: largest remaining norm, lowest index on ties
     const double cand = (lane >= k && lane < n) ? norm : -1.0;
@@ -121,19 +245,20 @@ __device__ void codFactor(typename Space<kLds>::dptr Ain, typename Space<kLds>::
       norm = nrm;
     }
     WSYNC();
-    maxPivot = fmax(maxPivot, fabs(A[k * ld + k]));
     if (lane > k && lane < m) A[lane * ld + k] = v[lane];
     if (lane == 0) { c.vd[k] = v[k]; c.vn[k] = vnorm; }
     WSYNC();
   }
+  }
+rankAndRz:
 #ifdef NIMBLE_STAGE_TIMING
   const long long tc1 = (long long)__builtin_amdgcn_s_memtime();
 #endif
+  // max |R_kk| and rank = #{|R_kk| > eps * kmax * max|R_kk|}, lane k = R_kk
+  const double dkk = lane < c.kmax ? fabs(A[lane * ld + lane]) : 0.0;
+  maxPivot = -waveMin(-dkk);
   const double thr = 2.220446049250313e-16 * c.kmax * maxPivot;
-  int r = 0;
-  for (int k = 0; k < c.kmax; k++)
-    if (fabs(A[k * ld + k]) > thr) r++;
-  r = uni(r);
+  const int r = __popcll(__ballot(lane < c.kmax && dkk > thr));
   if (lane == 0) *c.rank = r;
   // RZ: reflect row i over columns {i} U {r..n-1}; row i's trailing part is
   // kept as the reflector

@@ -518,49 +518,49 @@ __device__ bool devConstruct(typename Space<kLds>::dptr poolIn, int m, int n, do
 #ifdef NIMBLE_STAGE_TIMING
     if (lane == 0 && g_stamp) g_stamp[60] += 1;
 #endif
-    if (lane == 0) {
-      const double TH = 1e-6;
-      int nc = 0, nu = 0;
-      for (int j = 0; j < m; j++) { P.mapping[j] = CM_NOT_CLAMPING; P.clampIdx[j] = -1; P.ubIdx[j] = -1; }
-      for (int j = 0; j < m; j++) {
-        if (P.aCol[j] < 1e-9) { P.mapping[j] = CM_NOT_CLAMPING; continue; }
-        const double f = P.X[j];
-        double up = P.hi[j], low = P.lo[j];
-        const int fp = P.fi[j];
-        if (fp != -1) { up *= P.X[fp]; low *= P.X[fp]; }
+    // Lane-parallel classification (lane = row j < m <= 64).  Whether a row
+    // clamps depends on its own data and X[findex] only; a row bounded by
+    // its friction parent additionally needs the parent's clamping flag
+    // (ballot bit), and the clamping / upper-bound indices are the rows'
+    // ranks among their kind (popcounts), which is the sequential loop's
+    // numbering.
+    {
+      const double TH = 1e-6, tie = 1e-5;
+      const bool live = lane < m;
+      const double f = live ? P.X[lane] : 0.0;
+      const double hiJ = live ? P.hi[lane] : 0.0, loJ = live ? P.lo[lane] : 0.0;
+      const int fp = live ? P.fi[lane] : -1;
+      const bool colOk = live && P.aCol[lane] >= 1e-9;
+      const double xfp = (live && fp != -1) ? P.X[fp] : 1.0;
+      const double up = hiJ * xfp, low = loJ * xfp;
+      bool clampR = false, ubCand = false;
+      if (colOk) {
         if (fabs(f) < TH) {
-          if (fp != -1) {
-            if (fabs(P.X[fp]) < TH) P.mapping[j] = CM_NOT_CLAMPING;
-            else if (ignoreFriction) P.mapping[j] = CM_NOT_CLAMPING;
-            else { P.mapping[j] = CM_CLAMPING; P.clampIdx[j] = nc++; }
-          } else {
-            P.mapping[j] = CM_NOT_CLAMPING;
-          }
-          continue;
-        }
-        const double tie = 1e-5;
-        if ((f > low + tie && f < up - tie) || (low - f > 1e-2 || f - up > 1e-2)) {
-          P.mapping[j] = CM_CLAMPING; P.clampIdx[j] = nc++;
-        } else if (fp != -1 && fabs(P.X[fp]) > 1e-9 && P.aCol[fp] > 1e-9 && (fp > j || P.mapping[fp] == CM_CLAMPING)) {
-          P.mapping[j] = fp; P.ubIdx[j] = nu++;
-        } else {
-          P.mapping[j] = CM_NOT_CLAMPING;
+          clampR = fp != -1 && !(fabs(xfp) < TH) && !ignoreFriction;
+        } else if ((f > low + tie && f < up - tie) || (low - f > 1e-2 || f - up > 1e-2)) {
+          clampR = true;
+        } else if (fp != -1 && fabs(xfp) > 1e-9 && P.aCol[fp] > 1e-9) {
+          ubCand = true;
         }
       }
-      for (int j = 0; j < m; j++) {
-        if (P.mapping[j] == CM_CLAMPING) {
-          P.fc[P.clampIdx[j]] = P.X[j];
-          P.relVel[P.clampIdx[j]] = P.b[j];
-          P.clampRow[P.clampIdx[j]] = j;
-        }
-        P.Eval[j] = 0.0;
-        if (P.mapping[j] >= 0) {
-          const int fp = P.mapping[j];
-          const double up = P.X[fp] * P.hi[j], low = P.X[fp] * P.lo[j];
-          P.Eval[j] = fabs(P.X[j] - up) < fabs(P.X[j] - low) ? P.hi[j] : P.lo[j];
+      const unsigned long long cm = __ballot(clampR);
+      const bool ubR = ubCand && (fp > lane || ((cm >> (fp & 63)) & 1ull));
+      const unsigned long long um = __ballot(ubR);
+      const unsigned long long below = (1ull << lane) - 1ull;
+      const int cIdx = clampR ? __popcll(cm & below) : -1;
+      const int uIdx = ubR ? __popcll(um & below) : -1;
+      if (live) {
+        P.mapping[lane] = clampR ? CM_CLAMPING : (ubR ? fp : CM_NOT_CLAMPING);
+        P.clampIdx[lane] = cIdx;
+        P.ubIdx[lane] = uIdx;
+        P.Eval[lane] = ubR ? (fabs(f - up) < fabs(f - low) ? hiJ : loJ) : 0.0;
+        if (clampR) {
+          P.fc[cIdx] = f;
+          P.relVel[cIdx] = P.b[lane];
+          P.clampRow[cIdx] = lane;
         }
       }
-      ct[H_NC] = nc; ct[H_NU] = nu;
+      if (lane == 0) { ct[H_NC] = __popcll(cm); ct[H_NU] = __popcll(um); }
     }
     WSYNC();
     TACC_END(61, tCls);
@@ -618,23 +618,26 @@ __device__ bool devConstruct(typename Space<kLds>::dptr poolIn, int m, int n, do
     TACC_BEGIN(tN);
     (void)rhs;
     WSYNC();
-    if (lane == 0) {
-      bool anyNewlyNot = false;
-      for (int i = 0; i < m; i++) {
-        P.nx[i] = 0.0;
-        if (P.clampIdx[i] != -1) {
-          const double fi = P.fsol[P.clampIdx[i]];
-          P.nx[i] = fi;
-          if (fabs(fi) < 1e-6 && fabs(P.X[i]) > 1e-6 && P.fi[i] == -1) anyNewlyNot = true;
+    {
+      // lane-parallel: new x from the clamping solution
+      bool newlyNot = false;
+      if (lane < m) {
+        double v = 0.0;
+        const int ci = P.clampIdx[lane];
+        if (ci != -1) {
+          v = P.fsol[ci];
+          newlyNot = fabs(v) < 1e-6 && fabs(P.X[lane]) > 1e-6 && P.fi[lane] == -1;
         }
-        if (P.ubIdx[i] != -1) {
-          const int fp = P.fi[i];
-          const double om = P.fc[P.clampIdx[fp]] / P.X[i];
-          const double clean = fabs(om - P.hi[i]) < fabs(om - P.lo[i]) ? P.hi[i] : P.lo[i];
-          P.nx[i] = P.fsol[P.clampIdx[fp]] * clean;
+        if (P.ubIdx[lane] != -1) {
+          const int pc = P.clampIdx[P.fi[lane]];
+          const double hiJ = P.hi[lane], loJ = P.lo[lane];
+          const double om = P.fc[pc] / P.X[lane];
+          v = P.fsol[pc] * (fabs(om - hiJ) < fabs(om - loJ) ? hiJ : loJ);
         }
+        P.nx[lane] = v;
       }
-      ct[H_FLAG] = anyNewlyNot ? 1 : 0;
+      const bool anyNewlyNot = __ballot(newlyNot) != 0ull;
+      if (lane == 0) ct[H_FLAG] = anyNewlyNot ? 1 : 0;
     }
     WSYNC();
     TACC_END(65, tN);
@@ -1570,7 +1573,9 @@ __device__ double sphereRowTerm(const ModelDev& md, const double* s, const Layou
 //   face side        per row (tangent-basis gradient, ContactConstraint.cpp:772).
 // `ws` is workspace of 6 n + 6 nb + 16 doubles.  Returns the lane's sum.
 __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& L, const double* sn,
-                                   const BwdPool& P, int m, const double* Z, double* ws, int lane) {
+                                   const BwdPool& P, int m, const double* Z, double* ws, int lane,
+                                   double* g_stamp = nullptr) {
+  (void)g_stamp;
   const int n = md.n, nb = md.nb;
   const double* rows = sn + SN_ROWS;
   double* omega = ws;            // n x 6
@@ -1590,6 +1595,7 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
       if ((done >> c) & 1ull) continue;
       done |= 1ull << c;
       // omega^c_r (lane r), vertex sums (lanes over rows), all for body c
+      TACC_BEGIN(tO);
       double om[6] = {0, 0, 0, 0, 0, 0};
       double uv[6] = {0, 0, 0, 0, 0, 0};
       for (int j = 0; j < m; j++) {
@@ -1625,6 +1631,8 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
       if (lane == 0)
         for (int i = 0; i < 6; i++) UV[i] = uv[i];
       WSYNC();
+      TACC_END(82, tO);
+      TACC_BEGIN(tP);
       // P^c_b = sum over ancestor dofs r of b of S_r x* omega_r
       if (lane < nb) {
         double pb[6] = {0, 0, 0, 0, 0, 0};
@@ -1648,9 +1656,12 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
         acc += Z[3] * UV[0] + Z[4] * UV[1] + Z[5] * UV[2];
       }
       WSYNC();
+      TACC_END(83, tP);
+      if (lane == 0 && g_stamp) g_stamp[85] += 1;
     }
   }
   // face side: per row
+  TACC_BEGIN(tF);
   if (k < n) {
     for (int j = 0; j < m; j++) {
       const double* rr = rows + j * SN_ROWREC;
@@ -1689,6 +1700,7 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
       acc += v;
     }
   }
+  TACC_END(84, tF);
   return acc;
 }
 

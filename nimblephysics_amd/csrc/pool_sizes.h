@@ -56,7 +56,8 @@ __host__ __device__ inline int snapWorkspaceOffset(int n) { return snAlign8(snQ(
 
 // LCP workspace pools for m rows and n dofs
 #define NV_COLS 16
-__host__ __device__ inline int fwdPoolDoubles(int m, int n) { return n * m + 3 * m * m + 33 * m + 2 * n + 48; }
+// (+24: codFactor's register path stages a 24-double column in the scratch)
+__host__ __device__ inline int fwdPoolDoubles(int m, int n) { return n * m + 3 * m * m + 33 * m + 2 * n + 72; }
 __host__ __device__ inline int bwdPoolDoubles(int m, int n) { return n * m + 24 * m + NV_COLS * n + 64; }
 
 #define fwdPoolDoublesHost fwdPoolDoubles

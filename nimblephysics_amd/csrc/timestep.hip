@@ -640,9 +640,17 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
       // the adjoint vectors are dead now: workspace for the contact-geometry
       // terms (6n + 6nb <= 42nb), then for the M-derivative field pairs (24nb)
       double* buf = s + L.adj;
+      TACC_BEGIN(tG);
+#ifdef NIMBLE_STAGE_TIMING
+      const double gterm = contactGTermsAll(md, s, L, sn, P, m, Z, buf, lane, g_stamp);
+#else
       const double gterm = contactGTermsAll(md, s, L, sn, P, m, Z, buf, lane);
+#endif
       WSYNC();
+      TACC_END(80, tG);
+      TACC_BEGIN(tM);
       const double mterm = mFieldsTerm(md, s, L, P.NV, buf, lane, k, Z, -dt, (double)imp);
+      TACC_END(81, tM);
       if (k < n) {
         gq += gterm;
         gq += mterm;

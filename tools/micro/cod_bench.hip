@@ -1,0 +1,42 @@
+// COD micro-benchmark (tools/micro/cod_bench.py): one n x n problem per
+// 64-lane workgroup, factorised and solved in LDS by codFactor /
+// codSolveWave; per problem: shader clocks, rank and the min-norm solution.
+// Built twice: register QR (default) and -DNIMBLE_COD_LDS_ONLY.
+#include "../../nimblephysics_amd/csrc/lcp_wave.cuh"
+
+extern "C" __global__ void __launch_bounds__(64)
+cod_bench_kernel(int nmax, const int* nArr, const double* Ag, const double* bg, double* out, int rec) {
+  extern __shared__ double ldsbuf[];
+  const int lane = threadIdx.x;
+  const int pb = blockIdx.x;
+  const int n = nArr[pb];
+  double* M = ldsbuf;                // n x n
+  double* ws = M + nmax * nmax;    // carveCod workspace + v + z
+  for (int t = lane; t < n * n; t += 64) M[t] = Ag[(size_t)pb * nmax * nmax + t];
+  for (int t = lane; t < 12 * nmax + 64; t += 64) ws[t] = 0.0;
+  __syncthreads();
+  double* v = ws + 6 * nmax + 16;
+  double* z = v + (nmax > 24 ? nmax : 24);
+  const double b = lane < n ? bg[pb * nmax + lane] : 0.0;
+  const long long t0 = __builtin_amdgcn_s_memtime();
+  codFactor<true>(sp<true>(M), sp<true>(ws), n, n, n, sp<true>(v), lane);
+  const long long t1 = __builtin_amdgcn_s_memtime();
+  const double x = codSolveWave<true>(sp<true>(M), sp<true>(ws), n, n, n, b, sp<true>(z), lane);
+  const long long t2 = __builtin_amdgcn_s_memtime();
+  double* o = out + (size_t)pb * rec;
+  Cod c;
+  carveCod(ws, M, n, n, n, c);
+  if (lane == 0) {
+    o[0] = (double)(t1 - t0);
+    o[1] = (double)(t2 - t1);
+    o[2] = *c.rank;
+  }
+  if (lane < n) o[8 + lane] = x;
+}
+
+extern "C" int cod_bench_launch(int P, int nmax, const int* nArr, const double* A, const double* b, double* out, int rec,
+                                void* stream) {
+  const size_t lds = (size_t)(nmax * nmax + 12 * nmax + 64) * sizeof(double);
+  hipLaunchKernelGGL(cod_bench_kernel, dim3(P), dim3(64), lds, (hipStream_t)stream, nmax, nArr, A, b, out, rec);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}

@@ -27,9 +27,10 @@ g = torch.tensor(np.random.default_rng(0).standard_normal(st.shape), device=d)
 gs, gf = torch.empty_like(state), torch.empty_like(action)
 dev.forward(state, action, cache, nxt, snap, s)
 snap[:, ws + 20:ws + 40] = 0
+snap[:, ws + 80:ws + 90] = 0
 dev.backward(state, action, snap, g, gs, gf, s)
 torch.cuda.synchronize()
-T = snap[:, ws:ws + 40].cpu().numpy()
+T = snap[:, ws:ws + 90].cpu().numpy()
 hd = snap[:, :8].cpu().numpy()
 names = [((20, 21), "load+coreDynamics"), ((21, 22), "contact prep / plain solves"), ((30, 31), " prep: Ac/AcubE"),
          ((31, 32), " prep: MA + yf,w solves"), ((32, 33), " prep: Q, delta, u"), ((33, 34), " prep: COD factor"),
@@ -42,3 +43,7 @@ for (a, b), nm in names:
     if m.any():
         dtk = T[m, b] - T[m, a]
         print(f"  {nm:36s} worlds {m.sum():5d}  mean {dtk.mean():10.0f}  max {dtk.max():10.0f}")
+for k, nm in [(80, "G terms total"), (81, "M fields"), (82, " G: omega/vertex sums"), (83, " G: P chain + contraction"),
+              (84, " G: face side"), (85, " G: contact bodies (count)")]:
+    v = T[:, k]
+    print(f"  {nm:36s} worlds {(v > 0).sum():5d}  mean {v[v > 0].mean() if (v > 0).any() else 0:10.0f}  max {v.max():10.0f}")

@@ -28,24 +28,7 @@
 #define CT_FACE_VERTEX 1
 #define CT_VERTEX_FACE 2
 #define CT_EDGE_EDGE 3
-#ifdef NIMBLE_STAGE_TIMING
-// debug builds: per-stage shader-clock stamps into the snapshot workspace
-#define STAMP(k)                                                                   \
-  do {                                                                             \
-    if (lane == 0 && g_stamp) g_stamp[k] = (double)__builtin_amdgcn_s_memtime(); \
-  } while (0)
-// accumulating timers (slots >= 60): TACC_BEGIN(t) ... TACC_END(slot, t)
-#define TACC_BEGIN(t) const long long t = (long long)__builtin_amdgcn_s_memtime()
-#define TACC_END(k, t)                                                                            \
-  do {                                                                                            \
-    if (lane == 0 && g_stamp) g_stamp[k] += (double)((long long)__builtin_amdgcn_s_memtime() - t); \
-  } while (0)
-__device__ double* g_stamp_dummy;
-#else
-#define STAMP(k) do { } while (0)
-#define TACC_BEGIN(t) do { } while (0)
-#define TACC_END(k, t) do { } while (0)
-#endif
+#include "stamp.cuh"
 
 #define CM_CLAMPING (-1)
 #define CM_NOT_CLAMPING (-2)
@@ -401,7 +384,9 @@ __device__ __forceinline__ int helperWait(double* ct, Pred pred) {
 // ConstraintSolver::updateConstraints filter.  Kept contacts land at
 // ct + CT_CONTACTS in detector order.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, const Layout& L, int lane) {
+__device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, const Layout& L, int lane,
+                                             double* g_stamp = nullptr) {
+  (void)g_stamp;
   double* ct = s + L.ct;
   double* dropped = s + L.V;                            // alias area (dead V/A/IC/F)
   double* pairbuf = dropped + CT_MAX_DROPPED * CREC;
@@ -409,6 +394,7 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
   WSYNC();
   const int PC = md.pairChunk;
   for (int p0 = 0; p0 < md.numPairs; p0 += PC) {
+    TACC_BEGIN(tNP);
     const int p = p0 + lane;
     if (lane < PC && p < md.numPairs) {
       const int si = md.pairA[p], sj = md.pairB[p];
@@ -442,6 +428,8 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
       ct[H_PAIRCNT + lane] = cnt;
     }
     WSYNC();
+    TACC_END(76, tNP);
+    TACC_BEGIN(tPP);
     if (lane == 0) {
       int nk = (int)ct[H_NCON], nd = (int)ct[H_NDROP], st = (int)ct[H_STATUS];
       for (int q = 0; q < PC && p0 + q < md.numPairs; q++) {
@@ -480,6 +468,7 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
       ct[H_NCON] = nk; ct[H_NDROP] = nd; ct[H_STATUS] = st;
     }
     WSYNC();
+    TACC_END(77, tPP);
   }
 }
 
@@ -839,7 +828,11 @@ __device__ __forceinline__ void contactStage(const ModelDev& md, double* s, cons
 #endif
   STAMP(0);
   double* ct = s + L.ct;
+#ifdef NIMBLE_STAGE_TIMING
+  collideWorld(md, s, L, lane, g_stamp);
+#else
   collideWorld(md, s, L, lane);
+#endif
   STAMP(1);
   const int nCon = uni((int)ct[H_NCON]);
   if (nCon == 0) {
@@ -850,18 +843,14 @@ __device__ __forceinline__ void contactStage(const ModelDev& md, double* s, cons
     WSYNC();
     return;
   }
-  // row count
-  if (lane == 0) {
-    int m = 0;
-    for (int c = 0; c < nCon; c++) {
-      const double* rec = ct + CT_CONTACTS + c * CREC;
-      const double mu = fmin(md.friction[(int)rec[8]], md.friction[(int)rec[9]]);
-      m += mu > 1e-3 ? 3 : 1;
-    }
-    ct[H_M] = m;
+  // row count: 3 rows per frictional contact, 1 otherwise (lane = contact)
+  bool fr = false;
+  if (lane < nCon) {
+    const double* rec = ct + CT_CONTACTS + lane * CREC;
+    fr = fmin(md.friction[(int)rec[8]], md.friction[(int)rec[9]]) > 1e-3;
   }
-  WSYNC();
-  const int m = uni((int)ct[H_M]);
+  const int m = nCon + 2 * __popcll(__ballot(fr));
+  if (lane == 0) ct[H_M] = m;  // read by the helper wave
   // the LCP workspace is in LDS when it fits the pool (the common case, LDS
   // instructions throughout), else in the world's HBM snapshot tail
   if (fwdPoolDoubles(m, n) <= L.poolCap)
@@ -890,38 +879,56 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   const double* Lm = s + L.M;
   FwdPool P;
   carveFwd(pool, m, n, P);
-  // rows (ContactConstraint: normal + 2 tangents with friction)
-  if (lane == 0) {
-    int r = 0;
-    for (int c = 0; c < nCon; c++) {
-      const double* rec = ct + CT_CONTACTS + c * CREC;
-      const int ba = (int)rec[8], bb = (int)rec[9];
-      const double mu = fmin(md.friction[ba], md.friction[bb]);
-      const double restC = md.restitution[ba] * md.restitution[bb];
-      const bool fr = mu > 1e-3;
-      const int base = r;
-      P.rowC[r] = c; P.rowDir[r] = 0;
-      for (int i = 0; i < 3; i++) P.dvec[3 * r + i] = rec[3 + i];
-      P.lo[r] = 0.0; P.hi[r] = __builtin_inf(); P.fi[r] = -1;
-      P.rest[r] = restC > 1e-3 ? restC : 0.0;
-      r++;
-      if (fr) {
-        double t1[3], t2[3];
-        tangentBasisODE(rec + 3, t1, t2);
-        for (int k = 0; k < 2; k++) {
-          P.rowC[r] = c; P.rowDir[r] = 1 + k;
-          for (int i = 0; i < 3; i++) P.dvec[3 * r + i] = k == 0 ? t1[i] : t2[i];
-          P.lo[r] = -mu; P.hi[r] = mu; P.fi[r] = base; P.rest[r] = 0.0;
-          r++;
-        }
+  // rows (ContactConstraint: normal + 2 tangents with friction), lane =
+  // contact; a contact's first row is its rank among the rows of the
+  // contacts before it (popcount of the frictional ones)
+  if (lane < nCon) {
+    const int c = lane;
+    const double* rec = ct + CT_CONTACTS + c * CREC;
+    const int ba = (int)rec[8], bb = (int)rec[9];
+    const double mu = fmin(md.friction[ba], md.friction[bb]);
+    const double restC = md.restitution[ba] * md.restitution[bb];
+    const bool fr = mu > 1e-3;
+    const unsigned long long frm = __ballot(fr);
+    int r = c + 2 * __popcll(frm & ((1ull << c) - 1ull));
+    const int base = r;
+    P.rowC[r] = c; P.rowDir[r] = 0;
+    for (int i = 0; i < 3; i++) P.dvec[3 * r + i] = rec[3 + i];
+    P.lo[r] = 0.0; P.hi[r] = __builtin_inf(); P.fi[r] = -1;
+    P.rest[r] = restC > 1e-3 ? restC : 0.0;
+    r++;
+    if (fr) {
+      double t1[3], t2[3];
+      tangentBasisODE(rec + 3, t1, t2);
+      for (int k = 0; k < 2; k++) {
+        P.rowC[r] = c; P.rowDir[r] = 1 + k;
+        for (int i = 0; i < 3; i++) P.dvec[3 * r + i] = k == 0 ? t1[i] : t2[i];
+        P.lo[r] = -mu; P.hi[r] = mu; P.fi[r] = base; P.rest[r] = 0.0;
+        r++;
       }
     }
   }
   WSYNC();
-  // J^T columns
-  for (int t = lane; t < n * m; t += WAVE) {
-    const int i = t / m, j = t % m;
-    P.cols[t] = rowForceEntry(md, s, L, ct + CT_CONTACTS + P.rowC[j] * CREC, P.dvec + 3 * j, i);
+  // J^T (n x m, row i = dof i): lane = dof, loop over the rows; the row's
+  // contact data are wave-uniform (rowForceEntry's arithmetic, without a
+  // division-based (dof, row) unranking per element)
+  for (int i = lane; i < n; i += WAVE) {
+    const int body = md.dofBody[i];
+    double S[6];
+    for (int q = 0; q < 6; q++) S[q] = s[L.Sw + 6 * i + q];
+    for (int j = 0; j < m; j++) {
+      const double* rec = ct + CT_CONTACTS + uni(P.rowC[j]) * CREC;
+      const double* d = P.dvec + 3 * j;
+      double wr[6];
+      cross3(rec, d, wr);
+      wr[3] = d[0]; wr[4] = d[1]; wr[5] = d[2];
+      const double sdot = dot6(S, wr);
+      const int ba = uni((int)rec[8]), bb = uni((int)rec[9]);
+      double val = 0.0;
+      if (md.reactive[ba] && ((md.anc[ba] >> body) & 1ull)) val += sdot;
+      if (md.reactive[bb] && ((md.anc[bb] >> body) & 1ull)) val -= sdot;
+      P.cols[i * m + j] = val;
+    }
   }
   WSYNC();
   STAMP(2);
@@ -936,47 +943,52 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   }
   WSYNC();
   {
+    // Y = L^-1 J^T by columns (lane = column j): element (i, j) receives
+    // -L_ik Y_kj for k = 0 .. i-1 in order and is then scaled by 1/L_ii --
+    // the same operation sequence as the row-by-row elimination, without
+    // its two barriers per row
     double* Y = P.massed;
-    for (int k = 0; k < n; k++) {
-      const double inv = s[L.dinv + k];
-      for (int j = lane; j < m; j += WAVE) Y[k * m + j] *= inv;
-      WSYNC();
-      const int cnt = (n - k - 1) * m;
-      for (int t = lane; t < cnt; t += WAVE) {
-        const int i = k + 1 + t / m, j = t % m;
-        Y[i * m + j] -= Lm[tri(i, k)] * Y[k * m + j];
-      }
-      WSYNC();
-    }
-    for (int t = lane; t < m * m; t += WAVE) {
-      const int r = t / m, c = t % m;
-      if (r <= c) {
-        double acc = 0;
+    for (int j = lane; j < m; j += WAVE) {
+      for (int i = 0; i < n; i++) {
+        double acc = Y[i * m + j];
+        const double* Li = Lm + tri(i, 0);
 #pragma unroll 8
-        for (int i = 0; i < n; i++) acc += Y[i * m + r] * Y[i * m + c];
-        P.A[r * m + c] = acc;
-        P.A[c * m + r] = acc;
+        for (int k = 0; k < i; k++) acc -= Li[k] * Y[k * m + j];
+        Y[i * m + j] = acc * s[L.dinv + i];
       }
     }
+    WSYNC();
+    // A = Y^T Y (upper triangle computed, mirrored), 8 x 8 lane tiles
+    const int rl = lane >> 3, cl = lane & 7;
+    for (int r0 = 0; r0 < m; r0 += 8)
+      for (int c0 = r0; c0 < m; c0 += 8) {
+        const int r = r0 + rl, c = c0 + cl;
+        if (r < m && c < m && r <= c) {
+          double acc = 0;
+#pragma unroll 8
+          for (int i = 0; i < n; i++) acc += Y[i * m + r] * Y[i * m + c];
+          P.A[r * m + c] = acc;
+          P.A[c * m + r] = acc;
+        }
+      }
   }
 
-  if (lane == 0) {
-    for (int r = 0; r < m; r++) {
-      P.pen[r] = 0.0;
-      if (P.rowDir[r] != 0) continue;
-      const double* rec = ct + CT_CONTACTS + P.rowC[r] * CREC;
-      double bv = rec[6];
-      if (bv < 0.0) bv = 0.0;
-      else { bv *= 0.01 / md.dt; if (bv > 1e-3) bv = 1e-3; }
-      if (!md.penCorr) bv = 0;
-      P.pen[r] = bv;
-      if (P.rest[r] > 0) {
-        const double rv = P.b[r] * P.rest[r];
-        if (rv > 1e-1 && rv > bv) { bv = rv > 1e2 ? 1e2 : rv; P.pen[r] = 0.0; }
-        else P.rest[r] = 0.0;
-      }
-      P.b[r] += bv;
+  // penetration correction / restitution bounce of the normal rows (lane = row)
+  for (int r = lane; r < m; r += WAVE) {
+    P.pen[r] = 0.0;
+    if (P.rowDir[r] != 0) continue;
+    const double* rec = ct + CT_CONTACTS + P.rowC[r] * CREC;
+    double bv = rec[6];
+    if (bv < 0.0) bv = 0.0;
+    else { bv *= 0.01 / md.dt; if (bv > 1e-3) bv = 1e-3; }
+    if (!md.penCorr) bv = 0;
+    P.pen[r] = bv;
+    if (P.rest[r] > 0) {
+      const double rv = P.b[r] * P.rest[r];
+      if (rv > 1e-1 && rv > bv) { bv = rv > 1e2 ? 1e2 : rv; P.pen[r] = 0.0; }
+      else P.rest[r] = 0.0;
     }
+    P.b[r] += bv;
   }
   WSYNC();
   for (int j = lane; j < m; j += WAVE) {

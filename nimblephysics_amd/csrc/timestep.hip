@@ -20,6 +20,8 @@
 #include "model.h"
 #include "spatial.cuh"
 #include "wave.cuh"
+#include "stamp.cuh"
+#include "chol_wave.cuh"
 
 #define WAVE 64
 
@@ -32,7 +34,10 @@
 // Reference: BodyNode::updateTransform / updateVelocity /
 // updatePartialAcceleration (dart/dynamics/BodyNode.cpp:1960-1983).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void kinematics(const ModelDev& md, double* s, const Layout& L, int lane, const double* ddq) {
+__device__ __forceinline__ void kinematics(const ModelDev& md, double* s, const Layout& L, int lane, const double* ddq,
+                                           double* g_stamp = nullptr) {
+  (void)g_stamp;
+  STAMP(70);
   const double* q = s + L.q;
   const double* v = s + L.v;
   // 1. local transforms T_pj * Q(q) * T_cj^-1 (one lane per body), into Tw
@@ -62,6 +67,7 @@ __device__ __forceinline__ void kinematics(const ModelDev& md, double* s, const 
     tmul(T, md.TcjInv[b], s + L.Tw + 12 * b);
   }
   WSYNC();
+  STAMP(71);
   // 2. compose down the tree, one level at a time
   for (int lev = 1; lev <= md.maxDepth; lev++) {
     const int b0 = md.levelStart[lev], cnt = md.levelStart[lev + 1] - b0;
@@ -72,6 +78,7 @@ __device__ __forceinline__ void kinematics(const ModelDev& md, double* s, const 
     }
     WSYNC();
   }
+  STAMP(72);
   // 3. world-frame motion subspace Ad_{Tw * Tcj} S_local (one lane per dof)
   if (lane < md.n) {
     const int k = lane, b = md.dofBody[k], jt = md.jtype[b];
@@ -85,6 +92,7 @@ __device__ __forceinline__ void kinematics(const ModelDev& md, double* s, const 
     adT(TwC, loc, s + L.Sw + 6 * k);
   }
   WSYNC();
+  STAMP(73);
   // 4. V_b = sum over ancestor dofs of S_j qdot_j
   if (lane < md.nb) {
     const int b = lane;
@@ -101,6 +109,7 @@ __device__ __forceinline__ void kinematics(const ModelDev& md, double* s, const 
     for (int i = 0; i < 6; i++) s[L.V + 6 * b + i] = V[i];
   }
   WSYNC();
+  STAMP(74);
   // 5. A_b = sum over ancestor dofs of S_j qddot_j + V_body(j) x (S_j qdot_j)
   //    (BodyNode::updatePartialAcceleration / updateAccelerationFD unrolled)
   if (lane < md.nb) {
@@ -124,6 +133,7 @@ __device__ __forceinline__ void kinematics(const ModelDev& md, double* s, const 
     for (int i = 0; i < 6; i++) s[L.A + 6 * b + i] = A[i];
   }
   WSYNC();
+  STAMP(75);
 }
 
 // World-frame spatial inertia of body b (6x6, row-major) at the world origin.
@@ -207,63 +217,6 @@ __device__ __forceinline__ void massMatrixAndBias(const ModelDev& md, double* s,
     s[L.M + tri(j, k)] = val;  // lower triangle, packed
   }
   for (int j = lane; j < n; j += WAVE) C[j] = dot6(s + L.Sw + 6 * j, s + L.F + 6 * md.dofBody[j]);
-  WSYNC();
-}
-
-// In-place Cholesky of the packed lower triangle at A (row i at i(i+1)/2):
-// left-looking (Crout) with one lane per row, one barrier per column.  The
-// per-element subtraction order (k ascending) is that of the right-looking
-// factorisation.
-__device__ __forceinline__ void cholesky(double* A, double* dinv, int n, int lane) {
-  for (int j = 0; j < n; j++) {
-    double sum = 0.0;
-    if (lane >= j && lane < n) {
-      const int ri = tri(lane, 0), rj = tri(j, 0);
-      sum = A[ri + j];
-#pragma unroll 8
-      for (int k = 0; k < j; k++) sum -= A[ri + k] * A[rj + k];
-    }
-    const double djj = sqrt(rdl(sum, j));
-    if (lane == j) { A[tri(j, j)] = djj; dinv[j] = 1.0 / djj; }
-    else if (lane > j && lane < n) A[tri(lane, j)] = sum / djj;
-    WSYNC();
-  }
-}
-
-// Solve L L^T x = b in place (x = b on entry): x held one entry per lane,
-// no barriers inside.
-// K right-hand sides at once, held in registers (row i on lane i): the K
-// independent dependency chains interleave.  dinv[k] = 1 / L_kk.
-template <int K>
-__device__ __forceinline__ void cholSolveReg(const double* Lm, const double* dinv, double (&x)[K], int n, int lane) {
-  for (int k = 0; k < n; k++) {
-    const double dk = dinv[k];
-    const double lk = (lane > k && lane < n) ? Lm[tri(lane, k)] : 0.0;
-#pragma unroll
-    for (int q = 0; q < K; q++) {
-      const double xk = rdl(x[q], k) * dk;
-      if (lane == k) x[q] = xk;
-      else if (lane > k) x[q] -= lk * xk;
-    }
-  }
-  for (int k = n - 1; k >= 0; k--) {
-    const double dk = dinv[k];
-    const double lk = lane < k ? Lm[tri(k, lane)] : 0.0;
-#pragma unroll
-    for (int q = 0; q < K; q++) {
-      const double xk = rdl(x[q], k) * dk;
-      if (lane == k) x[q] = xk;
-      else if (lane < k) x[q] -= lk * xk;
-    }
-  }
-}
-
-// Solve L L^T x = b in place (x = b on entry, LDS).
-__device__ __forceinline__ void cholSolve(const double* Lm, const double* dinv, double* x, int n, int lane) {
-  double xr[1] = {lane < n ? x[lane] : 0.0};
-  cholSolveReg<1>(Lm, dinv, xr, n, lane);
-  WSYNC();
-  if (lane < n) x[lane] = xr[0];
   WSYNC();
 }
 
@@ -365,13 +318,18 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, con
 #endif
     STAMP(10);
     loadState(md, s, L, lane, st, forces + (size_t)env * n);
+#ifdef NIMBLE_STAGE_TIMING
+    kinematics(md, s, L, lane, nullptr, g_stamp);
+#else
     kinematics(md, s, L, lane, nullptr);
+#endif
     STAMP(14);
     composites(md, s, L, lane);
     STAMP(15);
     massMatrixAndBias(md, s, L, lane, s + L.rhs);
     STAMP(16);
     cholesky(s + L.M, s + L.dinv, md.n, lane);
+    STAMP(17);
     dynCacheCopy(md, s, L, snapshot + (size_t)env * snapDoubles + L.snDyn, true, lane);
     STAMP(11);
     // rhs = tau + spring + damping - C   (GenericJoint::updateTotalForceDynamic)

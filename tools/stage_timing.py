@@ -33,7 +33,9 @@ for it in range(4):
     state = nxt.clone()
     T = snap[:, ws:ws + 100].cpu().numpy()
     hd = snap[:, :8].cpu().numpy()
-    names = {(10, 14): " kinematics", (14, 15): " composites", (15, 16): " CRBA + bias", (16, 11): " cholesky",
+    names = {(10, 14): " kinematics", (14, 15): " composites", (15, 16): " CRBA + bias", (16, 17): " cholesky", (17, 11): " dynamics cache store",
+             (70, 71): "  kin: local transforms", (71, 72): "  kin: tree compose", (72, 73): "  kin: motion subspace",
+             (73, 74): "  kin: twists", (74, 75): "  kin: accelerations",
              (10, 11): "load+coreDynamics", (40, 41): " c1: Q build", (41, 42): " c1: COD factor",
              (42, 43): " c1: COD solve", (43, 44): " c1: nx + valid", (45, 46): " pre: Ac/AcubE",
              (46, 47): " pre: MA/MAc backsub", (47, 48): " pre: Q", (48, 49): " pre: COD", (49, 50): " pre: pinv",
@@ -55,6 +57,7 @@ for it in range(4):
         for (a, b), nm in names.items():
             if T[wi, a] > 0 and T[wi, b] > 0 and (a, b) not in ((10, 11), (12, 13)):
                 parts.append(f"{nm.strip()}={int(T[wi, b] - T[wi, a])}")
+        print("      collide: narrow phase %d  post-process %d" % (T[wi, 76], T[wi, 77]))
         print("      construct acc: iters %d cls %d Q %d codF %d codS %d nx %d valid %d | codF qr %d rz %d rank %d" % tuple(T[wi, 60:70]))
         print(f"  world {wi}: pivots {int(T[wi,52])} at row {int(T[wi,53])} pgs-sweeps {int(T[wi,54])} ign {hd[wi,7]:.0f} total {int(tot[wi])} rows {int(hd[wi,1])} clamp {int(hd[wi,2])} flag {hd[wi,4]:.0f} | " + " ".join(parts))
 

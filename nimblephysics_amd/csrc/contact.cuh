@@ -430,7 +430,94 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
     WSYNC();
     TACC_END(76, tNP);
     TACC_BEGIN(tPP);
-    if (lane == 0) {
+    // postProcess dedup + filter, lane-parallel over this chunk's candidate
+    // points (lane = candidate, detector order) when none of them lies
+    // within the dedup distance of an earlier candidate of the chunk; then a
+    // candidate is dropped exactly when it is close to an already listed
+    // contact, and its kept / dropped list slot is its rank among its kind.
+    // Otherwise (or > 64 candidates) the sequential loop below runs.
+    bool serial = true;
+    {
+      const int npc = md.numPairs - p0 < PC ? md.numPairs - p0 : PC;
+      int cq = lane < npc ? (int)ct[H_PAIRCNT + lane] : 0;
+      const bool unsup = cq < 0;
+      if (unsup) cq = -1 - cq;
+      const unsigned long long um = __ballot(unsup);
+      int incl = cq;
+      for (int d = 1; d < 16; d <<= 1) {
+        const int t = __shfl_up(incl, d);
+        if (lane >= d) incl += t;
+      }
+      const int total = uni(__shfl(incl, npc > 0 ? npc - 1 : 0));
+      const int excl = incl - cq;
+      if (npc > 0 && total <= WAVE) {
+        serial = false;
+        // candidate -> (pair, point)
+        int q = 0, exq = 0;
+        for (int k = 0; k < npc; k++) {
+          const int e0 = rdli(excl, k), e1 = rdli(incl, k);
+          if (lane >= e0 && lane < e1) { q = k; exq = e0; }
+        }
+        const bool live = lane < total;
+        const int c = live ? lane - exq : 0;
+        const double* rec = pairbuf + (q * 8 + c) * CREC;
+        const double px = live ? rec[0] : 0.0, py = live ? rec[1] : 0.0, pz = live ? rec[2] : 0.0;
+        bool dupCand = false;
+        for (int j = 0; j < total; j++) {
+          const double dx = px - rdl(px, j), dy = py - rdl(py, j), dz = pz - rdl(pz, j);
+          double dd = 0;
+          dd += dx * dx;
+          dd += dy * dy;
+          dd += dz * dz;
+          if (j < lane && live && sqrt(dd) < 3.0e-12) dupCand = true;
+        }
+        if (__ballot(dupCand)) {
+          serial = true;
+        } else {
+          const int nk0 = uni((int)ct[H_NCON]), nd0 = uni((int)ct[H_NDROP]);
+          bool close = false;
+          for (int t = 0; t < nk0 + nd0; t++) {
+            const double* o = t < nk0 ? ct + CT_CONTACTS + t * CREC : dropped + (t - nk0) * CREC;
+            double dd = 0;
+            dd += (px - o[0]) * (px - o[0]);
+            dd += (py - o[1]) * (py - o[1]);
+            dd += (pz - o[2]) * (pz - o[2]);
+            if (sqrt(dd) < 3.0e-12) close = true;
+          }
+          bool keep = false;
+          if (live && !close) {
+            const double nn = rec[3] * rec[3] + rec[4] * rec[4] + rec[5] * rec[5];
+            const int ba = (int)rec[8], bb = (int)rec[9];
+            keep = !(nn < 1e-12) && !(rec[6] < 0.0) && !(rec[6] > md.clipDepth) && (md.reactive[ba] || md.reactive[bb]);
+          }
+          const bool drop = live && !close && !keep;
+          const unsigned long long km = __ballot(keep), dm = __ballot(drop);
+          const unsigned long long below = (1ull << lane) - 1ull;
+          double* dst = nullptr;
+          if (keep) {
+            const int idx = nk0 + __popcll(km & below);
+            if (idx < NIMBLE_MAX_CONTACTS) dst = ct + CT_CONTACTS + idx * CREC;
+          } else if (drop) {
+            const int idx = nd0 + __popcll(dm & below);
+            if (idx < CT_MAX_DROPPED) dst = dropped + idx * CREC;
+          }
+          if (dst)
+            for (int i = 0; i < CREC; i++) dst[i] = rec[i];
+          if (lane == 0) {
+            const int nk = nk0 + __popcll(km), nd = nd0 + __popcll(dm);
+            int st = (int)ct[H_STATUS];
+            if (um) st |= ST_UNSUPPORTED_SHAPE;
+            if (nk > NIMBLE_MAX_CONTACTS) st |= ST_CONTACT_OVERFLOW;
+            if (nd > CT_MAX_DROPPED) st |= ST_DROPPED_OVERFLOW;
+            ct[H_NCON] = nk < NIMBLE_MAX_CONTACTS ? nk : NIMBLE_MAX_CONTACTS;
+            ct[H_NDROP] = nd < CT_MAX_DROPPED ? nd : CT_MAX_DROPPED;
+            ct[H_STATUS] = st;
+          }
+        }
+      }
+    }
+    WSYNC();
+    if (serial && lane == 0) {
       int nk = (int)ct[H_NCON], nd = (int)ct[H_NDROP], st = (int)ct[H_STATUS];
       for (int q = 0; q < PC && p0 + q < md.numPairs; q++) {
         int cnt = (int)ct[H_PAIRCNT + q];

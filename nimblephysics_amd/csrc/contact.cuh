@@ -1806,50 +1806,101 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
 // M-derivative pairs m(a, c) = (d(M a)/dq)^T c evaluated for all directions:
 //   d(c^T M a)/dq_k = -(Z_k x V_c,lam) . H_a(k) - (Z_k x V_a,lam) . H_c(k)
 // with V_x,b the world twist of body b under joint rates x and H_x(k) the
-// subtree momentum sum_{b in sub(k)} I_b V_x,b.  Fields live in `buf`
-// (8 fields x nb x 12 doubles: V then H).
-// M-derivative terms: for the four (a, c) column pairs of NV, the fields
-// are body twists V = sum a_k S_k and subtree momenta H = sum I V; a dof k on
-// body b (parent l) gets -(Z x V_l^c) . H_b^a - (Z x V_l^a) . H_b^c.  Pairs are
-// built one at a time (2 x nb x 12 doubles of workspace), momenta summed
-// level-parallel.
+// subtree momentum sum_{b in sub(k)} I_b V_x,b.  For each of the four (a, c)
+// column pairs of NV, lane b builds both fields' twists and momenta I_b V
+// (world inertias are formed once, kept as their 3x3 rotational block, world
+// COM and mass: 13 doubles per body after the 2 x nb x 12 field doubles in
+// `buf`), then lane b sums the momenta over its subtree (bodies d whose
+// ancestor set contains b) -- no per-level barriers or tree-list loads.
 __device__ double mFieldsTerm(const ModelDev& md, double* s, const Layout& L, const double* NV, double* buf, int lane,
                               int k, const double* Z, double coefDelta, double imp) {
   const int nb = md.nb;
   const double coef[4] = {coefDelta, 1.0, -imp, -imp};
+  double* wI = buf + 24 * nb;
+  if (lane < nb) {
+    // worldInertia's arithmetic, stored compactly
+    const int b = lane;
+    const double* Tw = s + L.Tw + 12 * b;
+    const double m = md.mass[b];
+    double cw[3], Rc[9], tmp[9];
+    for (int r = 0; r < 3; r++)
+      cw[r] = Tw[r * 4] * md.com[b][0] + Tw[r * 4 + 1] * md.com[b][1] + Tw[r * 4 + 2] * md.com[b][2] + Tw[r * 4 + 3];
+    for (int r = 0; r < 3; r++)
+      for (int c = 0; c < 3; c++)
+        tmp[r * 3 + c] = Tw[r * 4] * md.Ic[b][c] + Tw[r * 4 + 1] * md.Ic[b][3 + c] + Tw[r * 4 + 2] * md.Ic[b][6 + c];
+    for (int r = 0; r < 3; r++)
+      for (int c = 0; c < 3; c++)
+        Rc[r * 3 + c] = tmp[r * 3] * Tw[c * 4] + tmp[r * 3 + 1] * Tw[c * 4 + 1] + tmp[r * 3 + 2] * Tw[c * 4 + 2];
+    const double C[9] = {0, -cw[2], cw[1], cw[2], 0, -cw[0], -cw[1], cw[0], 0};
+    double* w = wI + 13 * b;
+    for (int r = 0; r < 3; r++)
+      for (int c = 0; c < 3; c++) {
+        const double cct = C[r * 3] * C[c * 3] + C[r * 3 + 1] * C[c * 3 + 1] + C[r * 3 + 2] * C[c * 3 + 2];
+        w[r * 3 + c] = Rc[r * 3 + c] + m * cct;
+      }
+    w[9] = cw[0]; w[10] = cw[1]; w[11] = cw[2]; w[12] = m;
+  }
+  WSYNC();
   double total = 0.0;
   for (int pr = 0; pr < 4; pr++) {
-    for (int t = lane; t < 2 * nb; t += WAVE) {
-      const int f = t / nb, b = t % nb;
-      double* V = buf + (f * nb + b) * 12;
-      bodyTwist(md, s + L.Sw, b, NV + 2 * pr + f, NV_COLS, V);
+    if (lane < nb) {
+      const int b = lane;
+      double Va[6] = {0, 0, 0, 0, 0, 0}, Vc[6] = {0, 0, 0, 0, 0, 0};
+      const unsigned long long an = md.anc[b];
+      const double* ga = NV + 2 * pr;
+      const double* gc = NV + 2 * pr + 1;
+#pragma unroll 4
+      for (int r = 0; r < md.n; r++) {
+        if (!((an >> md.dofBody[r]) & 1ull)) continue;
+        const double xa = ga[r * NV_COLS], xc = gc[r * NV_COLS];
+        const double* S = s + L.Sw + 6 * r;
+        if (xa != 0.0)
+          for (int i = 0; i < 6; i++) Va[i] = fma(S[i], xa, Va[i]);
+        if (xc != 0.0)
+          for (int i = 0; i < 6; i++) Vc[i] = fma(S[i], xc, Vc[i]);
+      }
+      const double* w = wI + 13 * b;
+      const double m = w[12];
+      const double C[9] = {0, -w[11], w[10], w[11], 0, -w[9], -w[10], w[9], 0};
       double I[36];
-      worldInertia(md, s + L.Tw + 12 * b, b, I);
-      mv6(I, V, V + 6);
+      for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) {
+          I[r * 6 + c] = w[r * 3 + c];
+          I[r * 6 + c + 3] = m * C[r * 3 + c];
+          I[(r + 3) * 6 + c] = m * C[c * 3 + r];
+          I[(r + 3) * 6 + c + 3] = (r == c) ? m : 0.0;
+        }
+      double* Fa = buf + b * 12;
+      double* Fc = buf + (nb + b) * 12;
+      double ha[6], hc[6];
+      mv6(I, Va, ha);
+      mv6(I, Vc, hc);
+      for (int i = 0; i < 6; i++) { Fa[i] = Va[i]; Fa[6 + i] = ha[i]; Fc[i] = Vc[i]; Fc[6 + i] = hc[i]; }
     }
     WSYNC();
-    for (int lev = md.maxDepth - 1; lev >= 0; lev--) {
-      const int b0 = md.levelStart[lev], cnt = (md.levelStart[lev + 1] - b0) * 12;
-      for (int t = lane; t < cnt; t += WAVE) {
-        const int p = md.levelBodies[b0 + t / 12], e = t % 12, f = e / 6, i = 6 + e % 6;
-        double acc = buf[(f * nb + p) * 12 + i];
-        for (int q = md.childStart[p]; q < md.childStart[p + 1]; q++) acc += buf[(f * nb + md.childList[q]) * 12 + i];
-        buf[(f * nb + p) * 12 + i] = acc;
+    // subtree momenta: lane b sums I_d V_d over the bodies d below it
+    double Ha[6] = {0, 0, 0, 0, 0, 0}, Hc[6] = {0, 0, 0, 0, 0, 0};
+    if (lane < nb) {
+      for (int d = 0; d < nb; d++) {
+        if (!((md.anc[d] >> lane) & 1ull)) continue;
+        const double* Fa = buf + d * 12 + 6;
+        const double* Fc = buf + (nb + d) * 12 + 6;
+        for (int i = 0; i < 6; i++) { Ha[i] += Fa[i]; Hc[i] += Fc[i]; }
       }
-      WSYNC();
     }
+    // dof k reads its body's subtree momenta (every lane takes part)
+    const int bk = k < md.n ? md.dofBody[k] : 0;
+    double ha[6], hc[6];
+    for (int i = 0; i < 6; i++) { ha[i] = __shfl(Ha[i], bk); hc[i] = __shfl(Hc[i], bk); }
     if (k < md.n) {
-      const int bk = md.dofBody[k];
       const int lam = md.parent[bk];
-      const double* Ha = buf + bk * 12 + 6;
-      const double* Hc = buf + (nb + bk) * 12 + 6;
       double val = 0.0;
       if (lam >= 0) {
         double t[6];
         crm(Z, buf + (nb + lam) * 12, t);
-        val -= dot6(t, Ha);
+        val -= dot6(t, ha);
         crm(Z, buf + lam * 12, t);
-        val -= dot6(t, Hc);
+        val -= dot6(t, hc);
       }
       total += coef[pr] * val;
     }

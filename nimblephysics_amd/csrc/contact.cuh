@@ -1366,11 +1366,10 @@ __device__ inline void bodyTwist(const ModelDev& md, const double* Sw, int b, co
   for (int i = 0; i < 6; i++) T[i] = 0.0;
   if (b < 0) return;
   const unsigned long long a = md.anc[b];
+  // unpredicated: skipped dofs contribute fma(S, 0, T) = T
 #pragma unroll 4
   for (int r = 0; r < md.n; r++) {
-    if (!((a >> md.dofBody[r]) & 1ull)) continue;
-    const double gr = g[r * ld];
-    if (gr == 0.0) continue;
+    const double gr = ((a >> md.dofBody[r]) & 1ull) ? g[r * ld] : 0.0;
     for (int i = 0; i < 6; i++) T[i] = fma(Sw[6 * r + i], gr, T[i]);
   }
 }
@@ -1733,15 +1732,22 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
       TACC_END(82, tO);
       TACC_BEGIN(tP);
       // P^c_b = sum over ancestor dofs r of b of S_r x* omega_r
+      // (terms S_r x* omega_r formed once per dof, in place of omega_r;
+      // lane b adds them with 0 / 1 ancestor weights)
+      if (lane < n) {
+        double t[6];
+        crf(s + L.Sw + 6 * lane, omega + 6 * lane, t);
+        for (int i = 0; i < 6; i++) omega[lane * 6 + i] = t[i];
+      }
+      WSYNC();
       if (lane < nb) {
         double pb[6] = {0, 0, 0, 0, 0, 0};
         const unsigned long long an = md.anc[lane];
+#pragma unroll 4
         for (int r = 0; r < n; r++) {
-          if (!((an >> md.dofBody[r]) & 1ull)) continue;
-          double t[6];
-          crf(s + L.Sw + 6 * r, omega + 6 * r, t);
+          const double w = ((an >> md.dofBody[r]) & 1ull) ? 1.0 : 0.0;
 #pragma unroll
-          for (int i = 0; i < 6; i++) pb[i] += t[i];
+          for (int i = 0; i < 6; i++) pb[i] = fma(w, omega[6 * r + i], pb[i]);
         }
         for (int i = 0; i < 6; i++) Pc[lane * 6 + i] = pb[i];
       }
@@ -1851,13 +1857,13 @@ __device__ double mFieldsTerm(const ModelDev& md, double* s, const Layout& L, co
       const double* gc = NV + 2 * pr + 1;
 #pragma unroll 4
       for (int r = 0; r < md.n; r++) {
-        if (!((an >> md.dofBody[r]) & 1ull)) continue;
-        const double xa = ga[r * NV_COLS], xc = gc[r * NV_COLS];
+        const bool in = (an >> md.dofBody[r]) & 1ull;
+        const double xa = in ? ga[r * NV_COLS] : 0.0, xc = in ? gc[r * NV_COLS] : 0.0;
         const double* S = s + L.Sw + 6 * r;
-        if (xa != 0.0)
-          for (int i = 0; i < 6; i++) Va[i] = fma(S[i], xa, Va[i]);
-        if (xc != 0.0)
-          for (int i = 0; i < 6; i++) Vc[i] = fma(S[i], xc, Vc[i]);
+        for (int i = 0; i < 6; i++) {
+          Va[i] = fma(S[i], xa, Va[i]);
+          Vc[i] = fma(S[i], xc, Vc[i]);
+        }
       }
       const double* w = wI + 13 * b;
       const double m = w[12];
@@ -1881,11 +1887,12 @@ __device__ double mFieldsTerm(const ModelDev& md, double* s, const Layout& L, co
     // subtree momenta: lane b sums I_d V_d over the bodies d below it
     double Ha[6] = {0, 0, 0, 0, 0, 0}, Hc[6] = {0, 0, 0, 0, 0, 0};
     if (lane < nb) {
+#pragma unroll 2
       for (int d = 0; d < nb; d++) {
-        if (!((md.anc[d] >> lane) & 1ull)) continue;
+        const double w = ((md.anc[d] >> lane) & 1ull) ? 1.0 : 0.0;
         const double* Fa = buf + d * 12 + 6;
         const double* Fc = buf + (nb + d) * 12 + 6;
-        for (int i = 0; i < 6; i++) { Ha[i] += Fa[i]; Hc[i] += Fc[i]; }
+        for (int i = 0; i < 6; i++) { Ha[i] = fma(w, Fa[i], Ha[i]); Hc[i] = fma(w, Fc[i], Hc[i]); }
       }
     }
     // dof k reads its body's subtree momenta (every lane takes part)

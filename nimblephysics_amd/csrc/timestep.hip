@@ -34,6 +34,8 @@
 // Reference: BodyNode::updateTransform / updateVelocity /
 // updatePartialAcceleration (dart/dynamics/BodyNode.cpp:1960-1983).
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ void ancestorAccelerations(const ModelDev& md, double* s, const Layout& L, int lane,
+                                                      const double* ddq, double* X);
 __device__ __forceinline__ void kinematics(const ModelDev& md, double* s, const Layout& L, int lane, const double* ddq,
                                            double* g_stamp = nullptr) {
   (void)g_stamp;
@@ -98,12 +100,13 @@ __device__ __forceinline__ void kinematics(const ModelDev& md, double* s, const 
     const int b = lane;
     double V[6] = {0, 0, 0, 0, 0, 0};
     const unsigned long long an = md.anc[b];
+    // unpredicated: a non-ancestor dof contributes fma(S, 0, V) = V
 #pragma unroll 4
     for (int j = 0; j < md.n; j++) {
-      if (!((an >> md.dofBody[j]) & 1ull)) continue;
+      const double vj = ((an >> md.dofBody[j]) & 1ull) ? v[j] : 0.0;
       const double* S = s + L.Sw + 6 * j;
 #pragma unroll
-      for (int i = 0; i < 6; i++) V[i] = fma(S[i], v[j], V[i]);
+      for (int i = 0; i < 6; i++) V[i] = fma(S[i], vj, V[i]);
     }
 #pragma unroll
     for (int i = 0; i < 6; i++) s[L.V + 6 * b + i] = V[i];
@@ -111,29 +114,46 @@ __device__ __forceinline__ void kinematics(const ModelDev& md, double* s, const 
   WSYNC();
   STAMP(74);
   // 5. A_b = sum over ancestor dofs of S_j qddot_j + V_body(j) x (S_j qdot_j)
-  //    (BodyNode::updatePartialAcceleration / updateAccelerationFD unrolled)
+  //    (BodyNode::updatePartialAcceleration / updateAccelerationFD unrolled);
+  //    the per-dof terms go through the (not yet used) IC region
+  ancestorAccelerations(md, s, L, lane, ddq, s + L.IC);
+  STAMP(75);
+}
+
+// A_b = sum over the ancestor dofs j of b of X_j, X_j = S_j qddot_j +
+// V_body(j) x (S_j qdot_j): X_j is formed once per dof (lane = dof, into X,
+// 6n doubles of LDS scratch), then lane b adds the X_j of every dof with a
+// 0 / 1 weight (fma(1, X, A) = A + X; a non-ancestor adds nothing), the same
+// sums as the per-body loop over its ancestors without divergent branches.
+__device__ __forceinline__ void ancestorAccelerations(const ModelDev& md, double* s, const Layout& L, int lane,
+                                                      const double* ddq, double* X) {
+  const double* v = s + L.v;
+  for (int j = lane; j < md.n; j += WAVE) {
+    const int bj = md.dofBody[j];
+    const double* S = s + L.Sw + 6 * j;
+    double sv[6], cr[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) sv[i] = S[i] * v[j];
+    crm(s + L.V + 6 * bj, sv, cr);
+    const double qdd = ddq ? ddq[j] : 0.0;
+#pragma unroll
+    for (int i = 0; i < 6; i++) X[6 * j + i] = fma(S[i], qdd, cr[i]);
+  }
+  WSYNC();
   if (lane < md.nb) {
     const int b = lane;
     double A[6] = {0, 0, 0, 0, 0, 0};
     const unsigned long long an = md.anc[b];
 #pragma unroll 4
     for (int j = 0; j < md.n; j++) {
-      const int bj = md.dofBody[j];
-      if (!((an >> bj) & 1ull)) continue;
-      const double* S = s + L.Sw + 6 * j;
-      double sv[6], cr[6];
+      const double w = ((an >> md.dofBody[j]) & 1ull) ? 1.0 : 0.0;
 #pragma unroll
-      for (int i = 0; i < 6; i++) sv[i] = S[i] * v[j];
-      crm(s + L.V + 6 * bj, sv, cr);
-      const double qdd = ddq ? ddq[j] : 0.0;
-#pragma unroll
-      for (int i = 0; i < 6; i++) A[i] += fma(S[i], qdd, cr[i]);
+      for (int i = 0; i < 6; i++) A[i] = fma(w, X[6 * j + i], A[i]);
     }
 #pragma unroll
     for (int i = 0; i < 6; i++) s[L.A + 6 * b + i] = A[i];
   }
   WSYNC();
-  STAMP(75);
 }
 
 // World-frame spatial inertia of body b (6x6, row-major) at the world origin.
@@ -253,28 +273,10 @@ __device__ __forceinline__ void dynCacheCopy(const ModelDev& md, double* s, cons
 
 // Accelerations only (phase 5 of kinematics) for given ddq, with Tw, Sw, V
 // already in LDS.
-__device__ __forceinline__ void accelerations(const ModelDev& md, double* s, const Layout& L, int lane, const double* ddq) {
-  const double* v = s + L.v;
-  if (lane < md.nb) {
-    const int b = lane;
-    double A[6] = {0, 0, 0, 0, 0, 0};
-    const unsigned long long an = md.anc[b];
-#pragma unroll 4
-    for (int j = 0; j < md.n; j++) {
-      const int bj = md.dofBody[j];
-      if (!((an >> bj) & 1ull)) continue;
-      const double* S = s + L.Sw + 6 * j;
-      double sv[6], cr[6];
-#pragma unroll
-      for (int i = 0; i < 6; i++) sv[i] = S[i] * v[j];
-      crm(s + L.V + 6 * bj, sv, cr);
-#pragma unroll
-      for (int i = 0; i < 6; i++) A[i] += fma(S[i], ddq[j], cr[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < 6; i++) s[L.A + 6 * b + i] = A[i];
-  }
-  WSYNC();
+// (X: 6n doubles of LDS scratch)
+__device__ __forceinline__ void accelerations(const ModelDev& md, double* s, const Layout& L, int lane, const double* ddq,
+                                              double* X) {
+  ancestorAccelerations(md, s, L, lane, ddq, X);
 }
 
 // Everything up to the factored mass matrix; leaves C in s[L.rhs].
@@ -530,7 +532,7 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
       WSYNC();
     }
     STAMP(22);
-    accelerations(md, s, L, lane, x);  // A = accelerations at a*
+    accelerations(md, s, L, lane, x, s + L.adj);  // A = accelerations at a* (adjoint area not yet in use)
     adjointVectors(md, s, L, lane);
     STAMP(23);
 

@@ -1684,6 +1684,18 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
   const int lam = k < n ? md.parent[bk] : -1;
   double acc = 0.0;
   unsigned long long done = 0ull;  // bodies already processed
+  // bodies carrying a dof; a contact body with none of them among its
+  // ancestors (the static ground) contributes to no direction k: skipped
+  unsigned lo = 0u, hi = 0u;
+  if (k < n) {
+    if (bk < 32) lo = 1u << bk;
+    else hi = 1u << (bk - 32);
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    lo |= __shfl_xor(lo, o);
+    hi |= __shfl_xor(hi, o);
+  }
+  const unsigned long long dofBodies = ((unsigned long long)uni((int)hi) << 32) | (unsigned)uni((int)lo);
   for (int j0 = 0; j0 < m; j0++) {
     const double* r0 = rows + j0 * SN_ROWREC;
     if ((int)r0[RR_MAP] == CM_NOT_CLAMPING) continue;
@@ -1692,6 +1704,7 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
       const int c = (int)rec0[8 + side];
       if ((done >> c) & 1ull) continue;
       done |= 1ull << c;
+      if (!(md.anc[c] & dofBodies)) continue;
       // omega^c_r (lane r), vertex sums (lanes over rows), all for body c
       TACC_BEGIN(tO);
       double om[6] = {0, 0, 0, 0, 0, 0};

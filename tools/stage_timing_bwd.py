@@ -39,7 +39,8 @@ names = [((20, 21), "load+coreDynamics"), ((21, 22), "contact prep / plain solve
          ((23, 24), "per-direction ID columns"), ((24, 25), "M-fields + G terms"), ((25, 26), "FD free + write")]
 print("clamping worlds", int((hd[:, 2] > 0).sum()))
 for (a, b), nm in names:
-    m = (T[:, a] > 0) & (T[:, b] > 0)
+    # (worlds whose LCP uses the HBM workspace overwrite the stamp slots)
+    m = (T[:, a] > 0) & (T[:, b] > 0) & (T[:, b] - T[:, a] > 0) & (T[:, b] - T[:, a] < 1e8)
     if m.any():
         dtk = T[m, b] - T[m, a]
         print(f"  {nm:36s} worlds {m.sum():5d}  mean {dtk.mean():10.0f}  max {dtk.max():10.0f}")

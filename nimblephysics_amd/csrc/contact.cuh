@@ -1121,24 +1121,25 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
     // for box contacts -- flag them in the status word if they ever do
     {
       bool dup = false;
-      for (int t = lane; t < m * m; t += WAVE) {
-        const int a = t / m, c = t % m;
-        if (c <= a) continue;
+      const int al = lane >> 3, cl = lane & 7;
+      for (int a0 = 0; a0 < m; a0 += 8)
+        for (int c0 = a0; c0 < m; c0 += 8) {
+        const int a = a0 + al, c = c0 + cl;
+        if (a >= m || c >= m || c <= a) continue;
         double dd = 0;
         for (int i = 0; i < m; i++) dd += (P.A[i * m + a] - P.A[i * m + c]) * (P.A[i * m + a] - P.A[i * m + c]);
         if (dd < 1e-4 && fabs(P.b[a] - P.b[c]) < 1e-4 && P.fi[a] == P.fi[c] && P.hi[a] == P.hi[c] && P.lo[a] == P.lo[c])
           dup = true;
-      }
+        }
       if (__ballot(dup) && lane == 0) ct[H_STATUS] = (double)((int)ct[H_STATUS] | ST_DUPLICATE_COLUMNS);
     }
     if (lane == 0) ct[H_CODOK] = 0;
-    for (int t = lane; t < m * m; t += WAVE) P.M1[t] = P.A[t];
     WSYNC();
     double xd = 0.0;
     #ifdef NIMBLE_STAGE_TIMING
-    bool ok = waveDantzig<kLds>(m, sp<kLds>(P.M1), sp<kLds>(P.M2), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane, g_stamp + 52);
+    bool ok = waveDantzig<kLds>(m, spc<kLds>(P.A), sp<kLds>(P.M2), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane, g_stamp + 52);
 #else
-    bool ok = waveDantzig<kLds>(m, sp<kLds>(P.M1), sp<kLds>(P.M2), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane);
+    bool ok = waveDantzig<kLds>(m, spc<kLds>(P.A), sp<kLds>(P.M2), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane);
 #endif
     if (ok) {
       if (lane < m) P.X[lane] = xd;

@@ -319,7 +319,12 @@ __device__ double codSolveWave(typename Space<kLds>::dptr Ain, typename Space<kL
 // ---------------------------------------------------------------------------
 struct WaveDantzig {
   int n, nC, nN, lane, ldL;
-  double* A;    // n x n, permuted in place (LDS)
+  // A: the problem matrix (n x n, symmetric, LDS), read in place: slot i of
+  // the permuted problem is original row p_i (lane i's register p), so the
+  // permuted entry (i, j) is A[p_i n + p_j] and a swap of two slots is a
+  // swap of registers -- the same values the reference's physically
+  // permuted matrix holds (dLCP's row / column swaps), without moving them
+  const double* A;
   double* L;    // n x ldL, ldL odd (LDS bank-conflict-free columns)
   double* scr;  // >= n doubles (LDS)
   double x, b, w, lo, hi, d, deltaX, deltaW, Dell, ell;
@@ -338,22 +343,19 @@ struct WaveDantzig {
     if (lane == i1) v = c;
     else if (lane == i2) v = a;
   }
+  // permuted-matrix accessors: row slot i (wave-uniform), column of this
+  // lane's slot / of its C entry / the diagonal
+  __device__ __forceinline__ int rowOff(int i) const { return rdli(p, i) * n; }
+  __device__ __forceinline__ double Arow(int i) const { return A[rowOff(i) + (lane < n ? p : 0)]; }
+  __device__ __forceinline__ double Adiag(int i) const {
+    const int pi = rdli(p, i);
+    return A[pi * n + pi];
+  }
+  // p of the slot this lane's C entry names
+  __device__ __forceinline__ int pOfC() const { return __shfl(p, C & 63); }
   __device__ __forceinline__ void swapProblem(int i1, int i2) {
     if (i1 == i2) return;
     LP_BEGIN();
-    WSYNC();
-    if (lane < n) {
-      const double t = A[i1 * n + lane];
-      A[i1 * n + lane] = A[i2 * n + lane];
-      A[i2 * n + lane] = t;
-    }
-    WSYNC();
-    if (lane < n) {
-      const double t = A[lane * n + i1];
-      A[lane * n + i1] = A[lane * n + i2];
-      A[lane * n + i2] = t;
-    }
-    WSYNC();
     swapReg(x, i1, i2); swapReg(b, i1, i2); swapReg(w, i1, i2); swapReg(lo, i1, i2); swapReg(hi, i1, i2);
     swapRegI(p, i1, i2); swapRegI(state, i1, i2); swapRegI(findex, i1, i2);
     LP_END(prof, 0);
@@ -420,7 +422,7 @@ struct WaveDantzig {
     LP_END(prof, 2);
   }
   __device__ __forceinline__ void transferToC(int i) {
-    const double Aii = A[i * n + i];
+    const double Aii = Adiag(i);
     if (nC > 0) {
       if (lane < nC) L[nC * ldL + lane] = ell;
       const double dd = waveSum(lane < nC ? ell * Dell : 0.0);
@@ -433,9 +435,10 @@ struct WaveDantzig {
     nC++;
   }
   __device__ __forceinline__ void transferFromNtoC(int i) {
-    const double Aii = A[i * n + i];
+    const double Aii = Adiag(i);
     if (nC > 0) {
-      Dell = lane < nC ? A[i * n + C] : 0.0;
+      const int pc = pOfC();
+      Dell = lane < nC ? A[rowOff(i) + pc] : 0.0;
       solveL1(Dell, nC);
       ell = lane < nC ? Dell * d : 0.0;
       if (lane < nC) L[nC * ldL + lane] = ell;
@@ -509,9 +512,10 @@ struct WaveDantzig {
   __device__ __forceinline__ void ldltRemove(int r, int n2) {
     LP_BEGIN();
     if (r != n2 - 1) {
+      const int pc = pOfC();
       if (r == 0) {
         const int C0 = rdli(C, 0);
-        double a = lane < n2 ? -A[C0 * n + C] : 0.0;  // A symmetric
+        double a = lane < n2 ? -A[rowOff(C0) + pc] : 0.0;  // A symmetric
         if (lane == 0) a += 1.0;
         ldltAddTL(0, n2, a);
       } else {
@@ -523,7 +527,7 @@ struct WaveDantzig {
           const double tk = rdl(t, k);
           if (lane >= r && lane < n2) s += L[lane * ldL + k] * tk;
         }
-        if (lane >= r && lane < n2) a = s - A[Cr * n + C];  // A symmetric
+        if (lane >= r && lane < n2) a = s - A[rowOff(Cr) + pc];  // A symmetric
         if (lane == r) a += 1.0;
         ldltAddTL(r, n2 - r, a);
       }
@@ -557,7 +561,8 @@ struct WaveDantzig {
   }
   __device__ __forceinline__ void solve1(int i, int dir, bool onlyTransfer) {
     if (nC > 0) {
-      Dell = lane < nC ? A[i * n + C] : 0.0;
+      const int pc = pOfC();
+      Dell = lane < nC ? A[rowOff(i) + pc] : 0.0;
       solveL1(Dell, nC);
       ell = lane < nC ? Dell * d : 0.0;
       if (!onlyTransfer) {
@@ -571,20 +576,21 @@ struct WaveDantzig {
       }
     }
   }
-  __device__ __forceinline__ double AiC(int i, double q) { return waveSum(lane < nC ? A[i * n + lane] * q : 0.0); }
+  __device__ __forceinline__ double AiC(int i, double q) { return waveSum(lane < nC ? Arow(i) * q : 0.0); }
   __device__ __forceinline__ double AiN(int i, double q) {
-    return waveSum((lane >= nC && lane < nC + nN) ? A[i * n + lane] * q : 0.0);
+    return waveSum((lane >= nC && lane < nC + nN) ? Arow(i) * q : 0.0);
   }
 };
 
-// A (n x n LDS, destroyed), L (n x (n|1) LDS scratch), scr (>= n LDS); problem
-// vectors lane-distributed; returns success and x (lane-distributed).
+// A (n x n LDS, symmetric, read only), L (n x (n|1) LDS scratch), scr (>= n
+// LDS); problem vectors lane-distributed; returns success and x
+// (lane-distributed).
 template <bool kLds>
-__device__ bool waveDantzig(int n, typename Space<kLds>::dptr Ain, typename Space<kLds>::dptr Lin,
+__device__ bool waveDantzig(int n, typename Space<kLds>::cdptr Ain, typename Space<kLds>::dptr Lin,
                             typename Space<kLds>::dptr scrIn, double& xOut, double b, double lo, double hi,
-                            int findex, int lane, double* dbg = nullptr) {
+                            int findex, int lane, double* dbg = nullptr, const int* cancel = nullptr) {
   n = uni(n);
-  double* A = (double*)Ain;
+  const double* A = (const double*)Ain;
   double* Lbuf = (double*)Lin;
   double* scr = (double*)scrIn;
   WaveDantzig D;
@@ -649,16 +655,17 @@ __device__ bool waveDantzig(int n, typename Space<kLds>::dptr Ain, typename Spac
         LP_BEGIN();
         {
           // every lane accumulates (no exec mask per step); only N lanes keep it
-          const int colA = lane < n ? lane : 0;
+          const int colA = lane < n ? D.p : 0;
           double acc = 0.0;
 #pragma unroll 4
           for (int j = 0; j < nC; j++) {
             const double dxj = rdl(D.deltaX, j);
-            acc += A[j * n + colA] * dxj;  // A symmetric: row j
+            acc += A[D.rowOff(j) + colA] * dxj;  // A symmetric: row j
           }
-          if (inN) D.deltaW = acc + (dir > 0 ? A[i * n + lane] : -A[i * n + lane]);
+          const double aij = D.Arow(i);
+          if (inN) D.deltaW = acc + (dir > 0 ? aij : -aij);
         }
-        const double dwi = D.AiC(i, D.deltaX) + A[i * n + i] * dirf;
+        const double dwi = D.AiC(i, D.deltaX) + D.Adiag(i) * dirf;
         if (lane == i) D.deltaW = dwi;
         int cmd = 1, si = 0;
         double s = -wiNow / dwi;
@@ -705,6 +712,9 @@ __device__ bool waveDantzig(int n, typename Space<kLds>::dptr Ain, typename Spac
           for (int k = 0; k < 8; k++) dbg[2 + k] = (double)D.prof[k];
 #endif
         if (s <= 0.0) return false;
+        // `cancel` (LDS int, optional): polled once per pivot; a set flag
+        // abandons the solve (the caller no longer needs it)
+        if (cancel && uni(__hip_atomic_load(cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) return false;
         if (lane < nC) D.x += s * D.deltaX;
         if (lane == i) D.x += s * dirf;
         if (inN) D.w += s * D.deltaW;

@@ -37,7 +37,7 @@ lcp_bench_kernel(int nmax, int nl, const int* nArr, const double* Ag, const doub
   __syncthreads();
   long long t0 = __builtin_amdgcn_s_memtime();
   double xd = 0.0;
-  const bool okD = waveDantzig<true>(n, sp<true>(M1), sp<true>(Lb), sp<true>(scr), xd, b, lo, hi, fi, lane, dshared);
+  const bool okD = waveDantzig<true>(n, spc<true>(A), sp<true>(Lb), sp<true>(scr), xd, b, lo, hi, fi, lane, dshared);
   long long t1 = __builtin_amdgcn_s_memtime();
   __syncthreads();
   double xp = lane < n ? x0g[pb * nmax + lane] : 0.0;

@@ -520,9 +520,9 @@ __device__ __noinline__ int deviceCapsuleBox(const double* Tb, const double* bs,
       }
       const V sc = len2(sub(pt, capA)) < len2(sub(pt, capB)) ? capA : capB;
       if (!(dep >= 0 && dep < clip)) continue;
-      cnt += sphereBox(box, sc, nullptr, r, boxFirst, 0, clip, boxShape, out + CREC * cnt);
+      cnt += sphereBox(box, sc, nullptr, r, boxFirst, 0, clip, boxShape, out + PBREC * cnt);
     }
   }
-  for (int c = 0; c < cnt; c++) { out[CREC * c + 8] = body1; out[CREC * c + 9] = body2; }
+  for (int c = 0; c < cnt; c++) { out[PBREC * c + 8] = body1; out[PBREC * c + 9] = body2; }
   return cnt;
 }

@@ -128,6 +128,13 @@ __device__ int deviceBoxBox(const double* p1, const double* R1, const double* A,
     double uaub = dot3(ua, ub), q1 = dot3(ua, pd), q2 = -dot3(ub, pd);
     double dd = 1 - uaub * uaub, alpha = 0, beta = 0;
     if (dd > 0) { dd = 1.0 / dd; alpha = (q1 + uaub * q2) * dd; beta = (uaub * q1 + q2) * dd; }
+    // edge metadata (DARTCollide.cpp:1046): fixed points before the closest
+    // approach, unit directions
+    double* e = out + CREC;
+    {
+      const double la = sqrt(dot3(ua, ua)), lb = sqrt(dot3(ub, ub));
+      for (int i = 0; i < 3; i++) { e[i] = pa[i]; e[3 + i] = ua[i] / la; e[6 + i] = pb[i]; e[9 + i] = ub[i] / lb; }
+    }
     for (int i = 0; i < 3; i++) { pa[i] += ua[i] * alpha; pb[i] += ub[i] * beta; }
     if (-s > clipDepth) return 0;
     for (int i = 0; i < 3; i++) { out[i] = 0.5 * (pa[i] + pb[i]); out[3 + i] = -normal[i]; }
@@ -213,7 +220,7 @@ __device__ int deviceBoxBox(const double* p1, const double* R1, const double* A,
     for (int i = 0; i < 3; i++) pt[i] = center[i] + k1 * Rb[i * 3 + a1] + k2 * Rb[i * 3 + a2];
     double dep = Sa[codeN] - dot3(normal2, pt);
     if (dep >= 0) {
-      double* o = out + CREC * cnum;
+      double* o = out + PBREC * cnum;
       double xx = ret[j * 2], yy = ret[j * 2 + 1];
       for (int i = 0; i < 3; i++) { o[i] = pt[i] + pa[i]; o[3 + i] = -normal[i]; }
       o[6] = dep;
@@ -225,7 +232,46 @@ __device__ int deviceBoxBox(const double* p1, const double* R1, const double* A,
       } else if (!onX && !onY) {
         type = flip ? CT_VERTEX_FACE : CT_FACE_VERTEX;
       } else {
+        // on an edge of the reference face, not at a corner
+        // (DARTCollide.cpp:1318): edge A along that face edge through its
+        // nearest corner, edge B along the nearest incident-face edge
         type = CT_EDGE_EDGE;
+        const double faceX = xx > 0 ? rect[0] : -rect[0], faceY = yy > 0 ? rect[1] : -rect[1];
+        double eaF[3], eaD[3], ebF[3], ebD[3];
+        for (int i = 0; i < 3; i++)
+          eaF[i] = (pa[i] + Sa[codeN] * normal[i]) + faceX * Ra[i * 3 + code1] + faceY * Ra[i * 3 + code2];
+        {
+          double l = 0;
+          for (int i = 0; i < 3; i++) { eaD[i] = o[i] - eaF[i]; l += eaD[i] * eaD[i]; }
+          l = sqrt(l);
+          for (int i = 0; i < 3; i++) eaD[i] /= l;
+        }
+        double other[3], o1[3], o2[3];
+        for (int i = 0; i < 3; i++) { other[i] = Rb[i * 3 + lanr]; o1[i] = Rb[i * 3 + a1]; o2[i] = Rb[i * 3 + a2]; }
+        if (dot3(other, normal) < 0)
+          for (int i = 0; i < 3; i++) other[i] = -other[i];
+        double faceCenter[3];
+        for (int i = 0; i < 3; i++) faceCenter[i] = pb[i] - Sb[lanr] * other[i];
+        const double ifx = dot3(o1, o) - dot3(o1, pb), ify = dot3(o2, o) - dot3(o2, pb);
+        const double sx = ifx == 0 ? 1.0 : ifx / fabs(ifx), sy = ify == 0 ? 1.0 : ify / fabs(ify);
+        double nearB[3], otherB[3];
+        for (int i = 0; i < 3; i++) nearB[i] = (sx * Sb[a1]) * o1[i] + (sy * Sb[a2]) * o2[i] + faceCenter[i];
+        const double distX = fabs(fabs(ifx) - Sb[a1]), distY = fabs(fabs(ify) - Sb[a2]);
+        if (distX < distY)
+          for (int i = 0; i < 3; i++) otherB[i] = (sx * Sb[a1]) * o1[i] + (-1 * sy * Sb[a2]) * o2[i] + faceCenter[i];
+        else
+          for (int i = 0; i < 3; i++) otherB[i] = (-1 * sx * Sb[a1]) * o1[i] + (sy * Sb[a2]) * o2[i] + faceCenter[i];
+        {
+          double l = 0;
+          for (int i = 0; i < 3; i++) { ebD[i] = nearB[i] - otherB[i]; l += ebD[i] * ebD[i]; }
+          l = sqrt(l);
+          for (int i = 0; i < 3; i++) { ebD[i] /= l; ebF[i] = nearB[i]; }
+        }
+        double* e = o + CREC;
+        for (int i = 0; i < 3; i++) {
+          e[i] = flip ? ebF[i] : eaF[i]; e[3 + i] = flip ? ebD[i] : eaD[i];
+          e[6 + i] = flip ? eaF[i] : ebF[i]; e[9 + i] = flip ? eaD[i] : ebD[i];
+        }
       }
       o[7] = type; o[8] = b1; o[9] = b2;
       cnum++;
@@ -384,8 +430,10 @@ __device__ __forceinline__ int helperWait(double* ct, Pred pred) {
 // ConstraintSolver::updateConstraints filter.  Kept contacts land at
 // ct + CT_CONTACTS in detector order.
 // ---------------------------------------------------------------------------
+// snapEdge: the world's snapshot slots for the kept contacts' EDGE_EDGE
+// metadata (global memory)
 __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, const Layout& L, int lane,
-                                             double* g_stamp = nullptr) {
+                                             double* snapEdge, double* g_stamp = nullptr) {
   (void)g_stamp;
   double* ct = s + L.ct;
   double* dropped = s + L.V;                            // alias area (dead V/A/IC/F)
@@ -409,7 +457,7 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
         const double p1[3] = {T1[3], T1[7], T1[11]}, p2[3] = {T2[3], T2[7], T2[11]};
         const double A[3] = {0.5 * md.shapeSize[si][0], 0.5 * md.shapeSize[si][1], 0.5 * md.shapeSize[si][2]};
         const double B[3] = {0.5 * md.shapeSize[sj][0], 0.5 * md.shapeSize[sj][1], 0.5 * md.shapeSize[sj][2]};
-        cnt = deviceBoxBox(p1, R1, A, p2, R2, B, md.clipDepth, bi, bj, pairbuf + lane * 8 * CREC);
+        cnt = deviceBoxBox(p1, R1, A, p2, R2, B, md.clipDepth, bi, bj, pairbuf + lane * 8 * PBREC);
       } else if ((md.shapeType[si] == NIMBLE_SHAPE_BOX && md.shapeType[sj] == NIMBLE_SHAPE_CAPSULE) ||
                  (md.shapeType[si] == NIMBLE_SHAPE_CAPSULE && md.shapeType[sj] == NIMBLE_SHAPE_BOX)) {
         // collideBoxCapsule / collideCapsuleBox (DARTCollide.cpp:4422, :4533)
@@ -420,7 +468,7 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
         tmul(s + L.Tw + 12 * md.shapeBody[sc], md.shapeT[sc], Tc);
         int unsup = 0;
         cnt = deviceCapsuleBox(Tb, md.shapeSize[sb], Tc, md.shapeSize[sc][0], md.shapeSize[sc][1], boxFirst,
-                               md.clipDepth, bi, bj, sb, pairbuf + lane * 8 * CREC, &unsup);
+                               md.clipDepth, bi, bj, sb, pairbuf + lane * 8 * PBREC, &unsup);
         if (unsup) cnt = -1 - cnt;  // flagged; the contacts found are still kept
       } else {
         cnt = -1;
@@ -460,7 +508,7 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
         }
         const bool live = lane < total;
         const int c = live ? lane - exq : 0;
-        const double* rec = pairbuf + (q * 8 + c) * CREC;
+        const double* rec = pairbuf + (q * 8 + c) * PBREC;
         const double px = live ? rec[0] : 0.0, py = live ? rec[1] : 0.0, pz = live ? rec[2] : 0.0;
         bool dupCand = false;
         for (int j = 0; j < total; j++) {
@@ -496,7 +544,11 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
           double* dst = nullptr;
           if (keep) {
             const int idx = nk0 + __popcll(km & below);
-            if (idx < NIMBLE_MAX_CONTACTS) dst = ct + CT_CONTACTS + idx * CREC;
+            if (idx < NIMBLE_MAX_CONTACTS) {
+              dst = ct + CT_CONTACTS + idx * CREC;
+              if (((int)rec[7] & 15) == CT_EDGE_EDGE)
+                for (int i = 0; i < EDGE_REC; i++) snapEdge[idx * EDGE_REC + i] = rec[CREC + i];
+            }
           } else if (drop) {
             const int idx = nd0 + __popcll(dm & below);
             if (idx < CT_MAX_DROPPED) dst = dropped + idx * CREC;
@@ -523,7 +575,7 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
         int cnt = (int)ct[H_PAIRCNT + q];
         if (cnt < 0) { st |= ST_UNSUPPORTED_SHAPE; cnt = -1 - cnt; }
         for (int c = 0; c < cnt; c++) {
-          const double* rec = pairbuf + (q * 8 + c) * CREC;
+          const double* rec = pairbuf + (q * 8 + c) * PBREC;
           bool close = false;
           for (int t = 0; t < nk + nd && !close; t++) {
             const double* o = t < nk ? ct + CT_CONTACTS + t * CREC : dropped + (t - nk) * CREC;
@@ -538,8 +590,13 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
                             (md.reactive[ba] || md.reactive[bb]);
           double* dst = nullptr;
           if (keep) {
-            if (nk < NIMBLE_MAX_CONTACTS) dst = ct + CT_CONTACTS + (nk++) * CREC;
-            else st |= ST_CONTACT_OVERFLOW;
+            if (nk < NIMBLE_MAX_CONTACTS) {
+              if (((int)rec[7] & 15) == CT_EDGE_EDGE)
+                for (int i = 0; i < EDGE_REC; i++) snapEdge[nk * EDGE_REC + i] = rec[CREC + i];
+              dst = ct + CT_CONTACTS + (nk++) * CREC;
+            } else {
+              st |= ST_CONTACT_OVERFLOW;
+            }
           } else {
             if (nd < CT_MAX_DROPPED) {
               // keep kept contacts contiguous: dropped list is separate
@@ -916,9 +973,9 @@ __device__ __forceinline__ void contactStage(const ModelDev& md, double* s, cons
   STAMP(0);
   double* ct = s + L.ct;
 #ifdef NIMBLE_STAGE_TIMING
-  collideWorld(md, s, L, lane, g_stamp);
+  collideWorld(md, s, L, lane, snap + snEdge(n), g_stamp);
 #else
-  collideWorld(md, s, L, lane);
+  collideWorld(md, s, L, lane, snap + snEdge(n));
 #endif
   STAMP(1);
   const int nCon = uni((int)ct[H_NCON]);
@@ -1659,6 +1716,93 @@ __device__ double sphereRowTerm(const ModelDev& md, const double* s, const Layou
   return v;
 }
 
+// math::getContactPointGradient (dart/math/Geometry.cpp:1129), radii 1: the
+// derivative of the midpoint of the two edges' closest approach
+__device__ inline void edgeContactPointGradient(const double* pA, const double* dpA, const double* uA,
+                                                const double* duA, const double* pB, const double* dpB,
+                                                const double* uB, const double* duB, double* out) {
+  double p[3], d_p[3];
+  for (int i = 0; i < 3; i++) { p[i] = pB[i] - pA[i]; d_p[i] = dpB[i] - dpA[i]; }
+  const double uaub = dot3(uA, uB);
+  const double d_uaub = dot3(duA, uB) + dot3(uA, duB);
+  const double q1 = dot3(uA, p);
+  const double d_q1 = dot3(duA, p) + dot3(uA, d_p);
+  const double q2 = -dot3(uB, p);
+  const double d_q2 = -dot3(duB, p) - dot3(uB, d_p);
+  const double d = 1 - uaub * uaub;
+  const double d_d = -2 * d_uaub * uaub;
+  if (d <= 0) {
+    for (int i = 0; i < 3; i++) out[i] = (dpA[i] * 1.0 + dpB[i] * 1.0) / 2.0;
+    return;
+  }
+  const double e = 1.0 / d;
+  const double d_e = -(1.0 / (d * d)) * d_d;
+  const double alpha = (q1 + uaub * q2) * e;
+  const double d_alpha = (q1 + uaub * q2) * d_e + (d_q1 + d_uaub * q2 + uaub * d_q2) * e;
+  const double beta = (uaub * q1 + q2) * e;
+  const double d_beta = (uaub * q1 + q2) * d_e + (d_uaub * q1 + uaub * d_q1 + d_q2) * e;
+  for (int i = 0; i < 3; i++)
+    out[i] = ((dpA[i] + alpha * duA[i] + d_alpha * uA[i]) * 1.0 + (dpB[i] + beta * duB[i] + d_beta * uB[i]) * 1.0) /
+             2.0;
+}
+
+// G-term of an EDGE_EDGE row for direction k (position generator Z) when
+// k's joint moves exactly one of the two bodies: EDGE_A / EDGE_B contact
+// position gradient (DifferentiableContactConstraint.cpp:412 / :429) and
+// normal gradient (:708 / :722, not renormalised, as in the reference), the
+// tangent directions following through the tangent-basis gradient (:1092).
+// E: edgeAFixedPoint, edgeADir, edgeBFixedPoint, edgeBDir of the contact.
+__device__ double edgeRowTerm(const ModelDev& md, const BwdPool& P, int j, const double* rec, const double* rr,
+                              const double* E, const double* Z, int bk, int A, int B) {
+  const bool inA = (md.anc[A] >> bk) & 1ull, inB = (md.anc[B] >> bk) & 1ull;
+  if (inA == inB) return 0.0;  // neither body moves (self-collision pairs are not generated)
+  const double* eaF = E;
+  const double* eaD = E + 3;
+  const double* ebF = E + 6;
+  const double* ebD = E + 9;
+  const double wv[3] = {Z[0], Z[1], Z[2]}, vv[3] = {Z[3], Z[4], Z[5]};
+  double fg[3], dg[3];
+  const double* fx = inA ? eaF : ebF;
+  if (sqrt(dot3(wv, wv)) > 1e-6) {  // math::gradientWrtTheta
+    cross3(wv, fx, fg);
+    for (int i = 0; i < 3; i++) fg[i] += vv[i];
+  } else {
+    for (int i = 0; i < 3; i++) fg[i] = vv[i];
+  }
+  cross3(wv, inA ? eaD : ebD, dg);  // math::gradientWrtThetaPureRotation
+  const double zero[3] = {0, 0, 0};
+  double dp[3];
+  edgeContactPointGradient(eaF, inA ? fg : zero, eaD, inA ? dg : zero, ebF, inA ? zero : fg, ebD, inA ? zero : dg,
+                           dp);
+  const double* nrm = rec + 3;
+  double nb[3];
+  cross3(ebD, eaD, nb);
+  const double sign = dot3(nb, nrm) < 0 ? -1.0 : 1.0;
+  double dn[3];
+  if (inA) cross3(ebD, dg, dn);
+  else cross3(dg, eaD, dn);
+  for (int i = 0; i < 3; i++) dn[i] *= sign;
+  const int dirIdx = (int)rr[RR_DIR];
+  double dd[3];
+  if (dirIdx == 0 || dot3(dn, dn) <= 1e-12) {
+    for (int i = 0; i < 3; i++) dd[i] = dn[i];
+  } else {
+    double T0[3], T1[3];
+    tangentBasisGradient(nrm, dn, T0, T1);
+    for (int i = 0; i < 3; i++) dd[i] = dirIdx == 1 ? T0[i] : T1[i];
+  }
+  const double* p = rec;
+  const double* d = rr + RR_D;
+  double t1[3], t2[3];
+  cross3(dp, d, t1);
+  cross3(p, dd, t2);
+  double v = 0.0;
+  for (int i = 0; i < 3; i++)
+    v += (P.TAB[j * 12 + i] - P.TAB[j * 12 + 6 + i]) * (t1[i] + t2[i]) +
+         (P.TAB[j * 12 + 3 + i] - P.TAB[j * 12 + 9 + i]) * dd[i];
+  return v;
+}
+
 // sum_j (G_j^T g_j)[k] for every direction k (lane k, position generator Z),
 // G_j = d(J^T e_j)/dq (DifferentiableContactConstraint.cpp:1654), grouped by
 // contact body c instead of by row:
@@ -1789,6 +1933,10 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
       const int A = (int)rec[8], B = (int)rec[9], typ = (int)rec[7], type = typ & 15;
       if (type == CT_SPHERE_BOX || type == CT_BOX_SPHERE) {
         acc += sphereRowTerm(md, s, L, P, j, rec, rr, Z, bk);
+        continue;
+      }
+      if (type == CT_EDGE_EDGE) {
+        acc += edgeRowTerm(md, P, j, rec, rr, sn + snEdge(n) + (int)rr[RR_CONTACT] * EDGE_REC, Z, bk, A, B);
         continue;
       }
       int faceBody = -1;

@@ -10,6 +10,11 @@
 // (sphere-box types encode the locked-face mask and the box shape in `type`,
 // see capsule.cuh)
 #define CREC 13
+// narrow-phase buffer records: the contact record + EDGE_EDGE metadata
+// (edgeAFixedPoint, edgeADir, edgeBFixedPoint, edgeBDir: collision::Contact,
+// set by dBoxBox), which the kept contacts carry into the snapshot
+#define EDGE_REC 12
+#define PBREC (CREC + EDGE_REC)
 
 // contact-stage LDS region (Layout::ct)
 #define CT_CONTACTS 32
@@ -23,7 +28,7 @@
 // (dead dynamics buffers, Layout::V)
 __host__ __device__ inline int ctDoubles() { return CT_DROPPED; }
 __host__ __device__ inline int collideScratchDoubles(int pairChunk) {
-  return CT_MAX_DROPPED * CREC + pairChunk * 8 * CREC;
+  return CT_MAX_DROPPED * CREC + pairChunk * 8 * PBREC;
 }
 
 // snapshot layout
@@ -50,7 +55,9 @@ __host__ __device__ inline int snAc(int n) { return snAlign8(snYf(n) + n); }
 __host__ __device__ inline int snAcubE(int n) { return snAc(n) + n * SN_MAXL; }
 __host__ __device__ inline int snPT(int n) { return snAcubE(n) + n * SN_MAXL; }     // pinv(Q)^T
 __host__ __device__ inline int snQ(int n) { return snPT(n) + SN_MAXL * SN_MAXL; }   // Q
-__host__ __device__ inline int snapWorkspaceOffset(int n) { return snAlign8(snQ(n) + SN_MAXL * SN_MAXL); }
+// EDGE_EDGE metadata of the kept contacts (EDGE_REC doubles per contact slot)
+__host__ __device__ inline int snEdge(int n) { return snQ(n) + SN_MAXL * SN_MAXL; }
+__host__ __device__ inline int snapWorkspaceOffset(int n) { return snAlign8(snEdge(n) + NIMBLE_MAX_CONTACTS * EDGE_REC); }
 // 64 doubles at the very end of every snapshot are kept for debug stamps
 #define SN_DEBUG_TAIL 64
 

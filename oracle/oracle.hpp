@@ -44,6 +44,9 @@ struct Contact {
   double sphereCenter[3];
   int faceLocked[3];
   double faceNormal[9];
+  // EDGE_EDGE metadata (collision::Contact::edgeAFixedPoint / edgeADir /
+  // edgeBFixedPoint / edgeBDir, set by dBoxBox, DARTCollide.cpp:1046, :1334)
+  double edgeAFixed[3], edgeADir[3], edgeBFixed[3], edgeBDir[3];
 };
 
 // Everything BackpropSnapshot needs (dart/neural/BackpropSnapshot.hpp and

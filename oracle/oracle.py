@@ -250,7 +250,9 @@ def cod_solve(A, b):
 
 
 def box_box(size1, T1, size2, T2):
-    out = np.zeros((16, 8))
+    """dBoxBox restated; rows of (point3, normal3, depth, type, edgeAFixed3,
+    edgeADir3, edgeBFixed3, edgeBDir3) -- the edge fields for EDGE_EDGE."""
+    out = np.zeros((16, 20))
     s1, s2 = (np.ascontiguousarray(s, dtype=np.float64) for s in (size1, size2))
     t1, t2 = (np.ascontiguousarray(np.asarray(T, dtype=np.float64)[:3, :4]) for T in (T1, T2))
     k = lib().oracle_box_box(_p(s1), _p(t1), _p(s2), _p(t2), _p(out))

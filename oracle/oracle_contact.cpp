@@ -128,6 +128,7 @@ static int boxBox(const double* p1, const double* R1, const double* A, const dou
     double q2 = -(ub[0] * pd[0] + ub[1] * pd[1] + ub[2] * pd[2]);
     double dd = 1 - uaub * uaub, alpha = 0, beta = 0;
     if (dd > 0) { dd = 1.0 / dd; alpha = (q1 + uaub * q2) * dd; beta = (uaub * q1 + q2) * dd; }
+    const double paFixed[3] = {pa[0], pa[1], pa[2]}, pbFixed[3] = {pb[0], pb[1], pb[2]};
     for (int i = 0; i < 3; i++) { pa[i] += ua[i] * alpha; pb[i] += ub[i] * beta; }
     const double pen = -s;
     if (pen > clipDepth) return 0;
@@ -136,6 +137,14 @@ static int boxBox(const double* p1, const double* R1, const double* A, const dou
     for (int i = 0; i < 3; i++) { c.point[i] = 0.5 * (pa[i] + pb[i]); c.normal[i] = -normal[i]; }
     c.depth = pen;
     c.type = CT_EDGE_EDGE;
+    // edge metadata (DARTCollide.cpp:1046): fixed points before the closest
+    // approach, unit edge directions
+    const double la = std::sqrt(ua[0] * ua[0] + ua[1] * ua[1] + ua[2] * ua[2]);
+    const double lb = std::sqrt(ub[0] * ub[0] + ub[1] * ub[1] + ub[2] * ub[2]);
+    for (int i = 0; i < 3; i++) {
+      c.edgeAFixed[i] = paFixed[i]; c.edgeADir[i] = ua[i] / la;
+      c.edgeBFixed[i] = pbFixed[i]; c.edgeBDir[i] = ub[i] / lb;
+    }
     out.push_back(c);
     return 1;
   }
@@ -237,7 +246,48 @@ clipped:
     } else if (!onEdgeX && !onEdgeY) {
       c.type = flip ? CT_VERTEX_FACE : CT_FACE_VERTEX;
     } else {
+      // on an edge of the reference face but not at a corner
+      // (DARTCollide.cpp:1318): edge A along the reference face edge through
+      // its nearest corner, edge B along the nearest edge of the incident face
       c.type = CT_EDGE_EDGE;
+      const double faceX = xx > 0 ? rect[0] : -rect[0], faceY = yy > 0 ? rect[1] : -rect[1];
+      double eaF[3], eaD[3], ebF[3], ebD[3];
+      for (int i = 0; i < 3; i++)
+        eaF[i] = (pa[i] + Sa[codeN] * normal[i]) + faceX * Ra[i * 3 + code1] + faceY * Ra[i * 3 + code2];
+      {
+        double d[3], l = 0;
+        for (int i = 0; i < 3; i++) { d[i] = c.point[i] - eaF[i]; l += d[i] * d[i]; }
+        l = std::sqrt(l);
+        for (int i = 0; i < 3; i++) eaD[i] = d[i] / l;
+      }
+      double other[3], o1[3], o2[3];
+      for (int i = 0; i < 3; i++) { other[i] = Rb[i * 3 + lanr]; o1[i] = Rb[i * 3 + a1]; o2[i] = Rb[i * 3 + a2]; }
+      if (other[0] * normal[0] + other[1] * normal[1] + other[2] * normal[2] < 0)
+        for (int i = 0; i < 3; i++) other[i] = -other[i];
+      double faceCenter[3];
+      for (int i = 0; i < 3; i++) faceCenter[i] = pb[i] - Sb[lanr] * other[i];
+      const double ifx = (o1[0] * c.point[0] + o1[1] * c.point[1] + o1[2] * c.point[2]) -
+                         (o1[0] * pb[0] + o1[1] * pb[1] + o1[2] * pb[2]);
+      const double ify = (o2[0] * c.point[0] + o2[1] * c.point[1] + o2[2] * c.point[2]) -
+                         (o2[0] * pb[0] + o2[1] * pb[1] + o2[2] * pb[2]);
+      const double sx = ifx == 0 ? 1.0 : ifx / std::fabs(ifx), sy = ify == 0 ? 1.0 : ify / std::fabs(ify);
+      double nearB[3], otherB[3];
+      for (int i = 0; i < 3; i++) nearB[i] = (sx * Sb[a1]) * o1[i] + (sy * Sb[a2]) * o2[i] + faceCenter[i];
+      const double distX = std::fabs(std::fabs(ifx) - Sb[a1]), distY = std::fabs(std::fabs(ify) - Sb[a2]);
+      if (distX < distY)
+        for (int i = 0; i < 3; i++) otherB[i] = (sx * Sb[a1]) * o1[i] + (-1 * sy * Sb[a2]) * o2[i] + faceCenter[i];
+      else
+        for (int i = 0; i < 3; i++) otherB[i] = (-1 * sx * Sb[a1]) * o1[i] + (sy * Sb[a2]) * o2[i] + faceCenter[i];
+      {
+        double l = 0;
+        for (int i = 0; i < 3; i++) { ebD[i] = nearB[i] - otherB[i]; l += ebD[i] * ebD[i]; }
+        l = std::sqrt(l);
+        for (int i = 0; i < 3; i++) { ebD[i] /= l; ebF[i] = nearB[i]; }
+      }
+      for (int i = 0; i < 3; i++) {
+        c.edgeAFixed[i] = flip ? ebF[i] : eaF[i]; c.edgeADir[i] = flip ? ebD[i] : eaD[i];
+        c.edgeBFixed[i] = flip ? eaF[i] : ebF[i]; c.edgeBDir[i] = flip ? eaD[i] : ebD[i];
+      }
     }
     out.push_back(c);
   }
@@ -261,10 +311,16 @@ extern "C" int oracle_box_box(const double* size1, const double* T1, const doubl
   }
   std::vector<oracle::Contact> cs;
   oracle::boxBox(p1, R1, A, p2, R2, B, 1e12, cs, 0, 1, 0, 1);
+  // per contact: point3 normal3 depth type | edgeAFixed3 edgeADir3 edgeBFixed3 edgeBDir3
   for (size_t k = 0; k < cs.size(); k++) {
-    for (int i = 0; i < 3; i++) { out[8 * k + i] = cs[k].point[i]; out[8 * k + 3 + i] = cs[k].normal[i]; }
-    out[8 * k + 6] = cs[k].depth;
-    out[8 * k + 7] = cs[k].type;
+    double* o = out + 20 * k;
+    for (int i = 0; i < 3; i++) { o[i] = cs[k].point[i]; o[3 + i] = cs[k].normal[i]; }
+    o[6] = cs[k].depth;
+    o[7] = cs[k].type;
+    for (int i = 0; i < 3; i++) {
+      o[8 + i] = cs[k].edgeAFixed[i]; o[11 + i] = cs[k].edgeADir[i];
+      o[14 + i] = cs[k].edgeBFixed[i]; o[17 + i] = cs[k].edgeBDir[i];
+    }
   }
   return (int)cs.size();
 }

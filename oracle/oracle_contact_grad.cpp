@@ -13,7 +13,8 @@
 //    getJacobianOfLCPOffsetClampingSubset (:3181) for POSITION.
 // Supported contact types: VERTEX_FACE and FACE_VERTEX (box-box face
 // contacts), SPHERE_BOX and BOX_SPHERE (capsule/sphere-box, the SPHERE_TO_BOX
-// / BOX_TO_SPHERE branches of :328 and :594); EDGE_EDGE aborts.
+// / BOX_TO_SPHERE branches of :328 and :594) and EDGE_EDGE (the EDGE_A /
+// EDGE_B branches, :412 / :429 and :708 / :722).
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -108,6 +109,37 @@ static void tangentBasisGradient(const double* n, const double* g, double* T0, d
   for (int i = 0; i < 3; i++) { T0[i] = gt[i]; T1[i] = a[i] + b[i]; }
 }
 
+// math::getContactPointGradient (dart/math/Geometry.cpp:1129) with radii 1:
+// derivative of the midpoint of the edges' closest approach
+static void contactPointGradient(const double* pA, const double* dpA, const double* uA, const double* duA,
+                                 const double* pB, const double* dpB, const double* uB, const double* duB,
+                                 double* out) {
+  double p[3], d_p[3];
+  for (int i = 0; i < 3; i++) { p[i] = pB[i] - pA[i]; d_p[i] = dpB[i] - dpA[i]; }
+  auto dot = [](const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; };
+  const double uaub = dot(uA, uB);
+  const double d_uaub = dot(duA, uB) + dot(uA, duB);
+  const double q1 = dot(uA, p);
+  const double d_q1 = dot(duA, p) + dot(uA, d_p);
+  const double q2 = -dot(uB, p);
+  const double d_q2 = -dot(duB, p) - dot(uB, d_p);
+  const double d = 1 - uaub * uaub;
+  const double d_d = -2 * d_uaub * uaub;
+  if (d <= 0) {
+    for (int i = 0; i < 3; i++) out[i] = (dpA[i] * 1.0 + dpB[i] * 1.0) / 2.0;
+    return;
+  }
+  const double e = 1.0 / d;
+  const double d_e = -(1.0 / (d * d)) * d_d;
+  const double alpha = (q1 + uaub * q2) * e;
+  const double d_alpha = (q1 + uaub * q2) * d_e + (d_q1 + d_uaub * q2 + uaub * d_q2) * e;
+  const double beta = (uaub * q1 + q2) * e;
+  const double d_beta = (uaub * q1 + q2) * d_e + (d_uaub * q1 + uaub * d_q1 + d_q2) * e;
+  for (int i = 0; i < 3; i++)
+    out[i] = ((dpA[i] + alpha * duA[i] + d_alpha * uA[i]) * 1.0 + (dpB[i] + beta * duB[i] + d_beta * uB[i]) * 1.0) /
+             2.0;
+}
+
 // G_i = d(J^T e_i)/dq  (n x n) for constraint row i
 static void constraintForcesJacobian(const World& w, const Kin<double>& k, const Snapshot& snap, int row, Mat& G) {
   const int n = w.n;
@@ -129,8 +161,8 @@ static void constraintForcesJacobian(const World& w, const Kin<double>& k, const
     if (pa && pb) { std::fprintf(stderr, "oracle: self-collision gradients not supported\n"); std::abort(); }
     int type = 0;  // 0 none, 1 vertex, 2 face, 3 sphere-to-box, 4 box-to-sphere (getDofContactType :116)
     if (pa || pb) {
-      if (c.type == CT_EDGE_EDGE) { std::fprintf(stderr, "oracle: EDGE_EDGE position gradients not supported\n"); std::abort(); }
-      if (c.type == CT_SPHERE_BOX) type = pa ? 3 : 4;
+      if (c.type == CT_EDGE_EDGE) type = pa ? 5 : 6;  // EDGE_A / EDGE_B
+      else if (c.type == CT_SPHERE_BOX) type = pa ? 3 : 4;
       else if (c.type == CT_BOX_SPHERE) type = pa ? 4 : 3;
       else if (c.type == CT_VERTEX_FACE) type = pa ? 1 : 2;
       else type = pa ? 2 : 1;
@@ -199,6 +231,31 @@ static void constraintForcesJacobian(const World& w, const Kin<double>& k, const
         for (int i = 0; i < 3; i++) dp[i] += vv[i];
       } else {
         for (int i = 0; i < 3; i++) dp[i] = vv[i];
+      }
+    } else if (type == 5 || type == 6) {
+      // EDGE_A / EDGE_B (:412, :429): the contact point moves with the
+      // closest approach of the two edges (math::getContactPointGradient,
+      // Geometry.cpp:1129), the normal with the moving edge's direction
+      // (:708, :722; not renormalised, as in the reference)
+      const bool A = type == 5;
+      double fg[3], dg[3], zero[3] = {0, 0, 0};
+      gwt(A ? c.edgeAFixed : c.edgeBFixed, fg);
+      cross3(wv, A ? c.edgeADir : c.edgeBDir, dg);  // gradientWrtThetaPureRotation
+      contactPointGradient(c.edgeAFixed, A ? fg : zero, c.edgeADir, A ? dg : zero, c.edgeBFixed, A ? zero : fg,
+                           c.edgeBDir, A ? zero : dg, dp);
+      double nb[3];
+      cross3(c.edgeBDir, c.edgeADir, nb);
+      const double sign = (nb[0] * c.normal[0] + nb[1] * c.normal[1] + nb[2] * c.normal[2] < 0) ? -1.0 : 1.0;
+      double dn[3];
+      if (A) cross3(c.edgeBDir, dg, dn);
+      else cross3(dg, c.edgeADir, dn);
+      for (int i = 0; i < 3; i++) dn[i] *= sign;
+      if (dirIdx == 0 || dn[0] * dn[0] + dn[1] * dn[1] + dn[2] * dn[2] <= 1e-12) {
+        for (int i = 0; i < 3; i++) dd[i] = dn[i];
+      } else {
+        double T0[3], T1[3];
+        tangentBasisGradient(c.normal, dn, T0, T1);
+        for (int i = 0; i < 3; i++) dd[i] = dirIdx == 1 ? T0[i] : T1[i];
       }
     } else if (type == 2) {
       double dn[3];

@@ -216,3 +216,71 @@ def capsule_edge_states(batch, seed=0):
         q[b, 3:6] = c + a * 0.15
     f = 0.3 * rng.standard_normal((batch, 6))
     return np.concatenate([q, v], axis=1), f
+
+
+def _rotvec(R):
+    """Rotation vector (log map) of a rotation matrix (math::logMap)."""
+    c = max(-1.0, min(1.0, 0.5 * (np.trace(R) - 1.0)))
+    th = np.arccos(c)
+    if th < 1e-12:
+        return np.zeros(3)
+    w = np.array([R[2, 1] - R[1, 2], R[0, 2] - R[2, 0], R[1, 0] - R[0, 1]])
+    return th / (2.0 * np.sin(th)) * w
+
+
+def edge_world():
+    """Two free unit cubes, the second rotated by eulerXYZ(0, 45, 45) degrees
+    so that one of its edges presses on an edge of the first -- the EDGE_EDGE
+    setup of the reference's GRADIENTS.EDGE_EDGE_BOX_COLLISION
+    (unittests/comprehensive/test_CollideGradient.cpp:169).  Returns the world
+    and its state (positions, with box 2's +x / -y velocity of 0.1)."""
+    from nimblephysics_amd import dynamics as D
+    w = nimble.World()
+    w.setGravity([0, -9.81, 0])
+    for name in ("face box", "vertex box"):
+        sk = D.Skeleton(name)
+        _, b = sk.createFreeJointAndBodyNodePair()
+        b.createShapeNode(D.BoxShape([1.0, 1.0, 1.0]), collision=True)
+        w.addSkeleton(sk)
+    a = np.array([0.0, 45.0, 45.0]) * 3.1415 / 180
+    cx, sx, cy, sy, cz, sz = np.cos(a[0]), np.sin(a[0]), np.cos(a[1]), np.sin(a[1]), np.cos(a[2]), np.sin(a[2])
+    Rx = np.array([[1, 0, 0], [0, cx, -sx], [0, sx, cx]])
+    Ry = np.array([[cy, 0, sy], [0, 1, 0], [-sy, 0, cy]])
+    Rz = np.array([[cz, -sz, 0], [sz, cz, 0], [0, 0, 1]])
+    R = Rx @ Ry @ Rz
+    t = R @ np.array([1.0, -1.0, 0.0]) * ((2 * np.sqrt(0.5) / np.sqrt(2)) - 0.01)
+    q = np.zeros(12)
+    q[6:9] = _rotvec(R)
+    q[9:12] = t
+    v = np.zeros(12)
+    v[9] += 0.1
+    v[10] -= 0.1
+    return w, np.concatenate([q, v])
+
+
+def ledge_world():
+    """A free 0.5 m cube half over the edge of a static unit box (top face at
+    y = 0): the face-clipped contacts on the box's edge are EDGE_EDGE (the
+    configuration of the reference's BOX_BOX_FACE_FACE_COLLISION_ANNOTATION,
+    test_DARTCollide.cpp:554, turned to gravity -y).  Returns the world and a
+    resting state (1 mm penetration)."""
+    from nimblephysics_amd import dynamics as D
+    w = nimble.World()
+    w.setGravity([0, -9.81, 0])
+    box = D.Skeleton("box")
+    _, b = box.createFreeJointAndBodyNodePair()
+    b.createShapeNode(D.BoxShape([0.5, 0.5, 0.5]), collision=True)
+    w.addSkeleton(box)
+    ground = D.Skeleton("ledge")
+    gj, gb = ground.createWeldJointAndBodyNodePair()
+    T = np.eye(4)
+    T[1, 3] = -0.5
+    gj.setTransformFromParentBodyNode(T)
+    gb.createShapeNode(D.BoxShape([1.0, 1.0, 1.0]), collision=True)
+    ground.setMobile(False)
+    w.addSkeleton(ground)
+    q = np.zeros(6)
+    q[3:6] = [0.0, 0.25 - 1e-3, 0.5]
+    v = np.zeros(6)
+    v[4] = -0.05
+    return w, np.concatenate([q, v])

@@ -85,7 +85,7 @@ def _same_path(ow, sn, b):
     return np.array_equal(fl, gfl) and np.array_equal(gm, mapping)
 
 
-def _check_contacts(ow, snap, B):
+def _check_contacts(ow, snap, B, max_diverge=0.03):
     """Contact sets bit-exact for every world; returns the mask of worlds on
     the same LCP path (the others are checked to be ill-posed)."""
     same = np.ones(B, dtype=bool)
@@ -106,16 +106,16 @@ def _check_contacts(ow, snap, B):
         if not _same_path(ow, sn, b):
             assert _lcp_ambiguous(ow, b), f"world {b}: LCP path differs on a well-posed problem"
             same[b] = False
-    assert (~same).sum() <= max(1, int(0.03 * B)), (~same).sum()
+    assert (~same).sum() <= max(1, int(max_diverge * B)), (~same).sum()
     return same
 
 
-def _parity(world, st, f, seed=11, check_grad=True):
+def _parity(world, st, f, seed=11, check_grad=True, max_diverge=0.03):
     ow = O.OracleWorld(world)
     ref = ow.forward(st, f)
     nxt, snap, cache, ts, tf = _device_step(world, st, f)
     B = st.shape[0]
-    same = _check_contacts(ow, snap.cpu().numpy(), B)
+    same = _check_contacts(ow, snap.cpu().numpy(), B, max_diverge)
     n = world.getNumDofs()
     got = nxt.cpu().numpy()[same]
     ref = ref[same]
@@ -247,3 +247,34 @@ def test_hbm_workspace_path(rows, monkeypatch):
     world = models.atlas_world(True)
     st, f = models.random_states(world, 32, seed=12, q_scale=0.01, v_scale=0.02)
     _parity(world, st, f)
+
+
+@pytest.mark.parametrize("name", ["edge", "ledge"])
+def test_edge_edge_contact_parity(name):
+    """EDGE_EDGE contacts and their gradient terms: the reference's
+    GRADIENTS.EDGE_EDGE_BOX_COLLISION setup (box-box separating-axis edge
+    contact, box 2 driven into box 1) and a cube half over the edge of a
+    static box (face-clipped contacts on the edge, the configuration of
+    BOX_BOX_FACE_FACE_COLLISION_ANNOTATION); worlds perturbed around them."""
+    if name == "edge":
+        world, st0 = models.edge_world()
+        st0 = st0.copy()
+        st0[12 + 9], st0[12 + 10] = -0.3, 0.3
+    else:
+        world, st0 = models.ledge_world()
+    B = 16
+    rng = np.random.default_rng(21)
+    st = st0[None, :] + 1e-4 * rng.standard_normal((B, st0.shape[0]))
+    st[0] = st0
+    f = 0.1 * rng.standard_normal((B, world.getNumDofs()))
+    # the cube resting on the ledge has four contacts (12 rows, rank <= 6):
+    # an ill-posed LCP on which the reference's Dantzig itself flips outcome
+    # (each diverging world is checked to be such a case); the others must
+    # match on path, state and gradients
+    ow, snap = _parity(world, st, f, max_diverge=0.0 if name == "edge" else 0.25)
+    types = []
+    for b in range(B):
+        nc = int(snap[b, SN_NCON])
+        types += list((snap[b, SN_CONTACTS:SN_CONTACTS + CREC * nc].reshape(nc, CREC)[:, 7].astype(int) & 15))
+    assert 3 in types  # EDGE_EDGE present
+    assert (snap[:, SN_NC] > 0).any()  # and clamping

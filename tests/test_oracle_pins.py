@@ -37,6 +37,30 @@ def test_box_box_known_answer(oracle_built):
     got = sorted([(tuple(np.round(c[:3], 9)), names[int(c[7])]) for c in cs])
     exp = sorted([(tuple(np.round(e["point"], 9)), e["type"]) for e in d["expected"]])
     assert got == exp
+    # the reference's EDGE_EDGE metadata check (test_DARTCollide.cpp:578):
+    # the contact at (0.25, 0.5, 0) has |edgeADir| = x, |edgeBDir| = y
+    c1 = [c for c in cs if np.allclose(c[:3], [0.25, 0.5, 0.0])][0]
+    assert np.allclose(np.abs(c1[11:14]), [1, 0, 0]) and np.allclose(np.abs(c1[17:20]), [0, 1, 0])
+
+
+def test_edge_edge_gradients_vs_finite_differences(oracle_built):
+    """EDGE_EDGE contact gradients (EDGE_A / EDGE_B position and normal
+    terms) on the reference's GRADIENTS.EDGE_EDGE_BOX_COLLISION setup
+    (test_CollideGradient.cpp:169), with box 2 driven into box 1 so that the
+    edge contact clamps."""
+    w, st = models.edge_world()
+    st = st.copy()
+    st[12 + 9], st[12 + 10] = -0.3, 0.3
+    f = np.zeros(12)
+    o = O.OracleWorld(w)
+    o.forward(st[None], f[None])
+    cs = O.contacts(o, 0)
+    assert len(cs) > 0 and (cs[:, 7] == 3).all()
+    assert O.lcp_flags(o, 0)[3] > 0  # clamping rows
+    g = np.random.default_rng(2).standard_normal(24)
+    gs, gf, fd_s, fd_f = _fd_check(w, st, f, g)
+    assert np.abs(gs - fd_s).max() <= 1e-6 * np.abs(fd_s).max()
+    assert np.abs(gf - fd_f).max() <= 1e-6 * np.abs(fd_f).max()
 
 
 def test_dantzig_matches_reference_fixtures(oracle_built):

@@ -22,7 +22,7 @@ n = w.getNumDofs()
 a8 = lambda x: ((x + 7) // 8) * 8
 CREC = 13  # csrc/pool_sizes.h
 SN_VF = 16 + 16 * CREC + 48 * 12 + 48
-ws = a8(a8(SN_VF + 2 * n) + 2 * n * 48 + 2 * 2304) + 1000  # snapWorkspaceOffset(n) + 1000
+ws = a8(a8(SN_VF + 2 * n) + 2 * n * 48 + 2 * 2304 + 16 * 12) + 1000  # snapWorkspaceOffset(n) + 1000
 g = torch.tensor(np.random.default_rng(0).standard_normal(st.shape), device=d)
 gs, gf = torch.empty_like(state), torch.empty_like(action)
 dev.forward(state, action, cache, nxt, snap, s)

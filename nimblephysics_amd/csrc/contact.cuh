@@ -1418,6 +1418,13 @@ __device__ inline void carveBwd(double* base, int m, int n, BwdPool& P) {
   P.rowOf = reinterpret_cast<int*>(p);
 }
 
+// the dofs (bit r) whose joint moves body b: wave-uniform 64-bit mask
+// (n <= NIMBLE_MAX_DOFS = 64), so loops over them skip the unrelated dofs
+__device__ __forceinline__ unsigned long long ancestorDofMask(const ModelDev& md, unsigned long long bodies, int lane) {
+  const bool in = lane < md.n && ((bodies >> md.dofBody[lane < md.n ? lane : 0]) & 1ull);
+  return __ballot(in);
+}
+
 // twist of body `b` for joint velocity vector g (column `col` of X, ld):
 // sum over ancestor dofs r of S_r g_r.  b < 0 -> 0.
 __device__ inline void bodyTwist(const ModelDev& md, const double* Sw, int b, const double* g, int ld, double* T) {
@@ -1501,6 +1508,7 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
   // x = P b ; r1 = b - Q x ; zeta = P^T x
   for (int c = lane; c < nc; c += WAVE) {
     double xx = 0;
+#pragma unroll 8
     for (int r = 0; r < nc; r++) xx += PT[r * nc + c] * P.bc[r];
     P.xq[c] = xx;
   }
@@ -1508,6 +1516,7 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
   for (int c = lane; c < nc; c += WAVE) {
     double qx = 0, ze = 0;
     if (imp)
+#pragma unroll 8
       for (int k = 0; k < nc; k++) {
         qx += Q[c * nc + k] * P.xq[k];
         ze += PT[c * nc + k] * P.xq[k];
@@ -1523,6 +1532,7 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
     if (lane < n) {
       X[0] = s[L.gv + lane];
       double a1 = 0, a2 = 0, a3 = 0, a4 = 0;
+#pragma unroll 8
       for (int c = 0; c < nc; c++) {
         const double ae = AcubE[lane * nc + c], ac = Ac[lane * nc + c];
         a1 += ae * P.fc[c];
@@ -1549,12 +1559,14 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
   // u = A_c_ub_E^T w ; lambda = P^T u ; beta ; rho = P lambda ; pi = u - Q^T lambda
   for (int c = lane; c < nc; c += WAVE) {
     double acc = 0;
+#pragma unroll 8
     for (int i = 0; i < n; i++) acc += AcubE[i * nc + c] * s[L.w + i];
     P.u[c] = acc;
   }
   WSYNC();
   for (int c = lane; c < nc; c += WAVE) {
     double l = 0;
+#pragma unroll 8
     for (int r = 0; r < nc; r++) l += PT[c * nc + r] * P.u[r];
     P.lam[c] = l;
     P.beta[c] = P.bounce[c] * l;
@@ -1563,6 +1575,7 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
   for (int c = lane; c < nc; c += WAVE) {
     double qtl = 0, rh = 0;
     if (imp)
+#pragma unroll 8
       for (int k = 0; k < nc; k++) {
         qtl += Q[k * nc + c] * P.lam[k];
         rh += PT[k * nc + c] * P.lam[k];
@@ -1578,6 +1591,7 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
     double mu = 0;
     if (lane < n) {
       double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+#pragma unroll 8
       for (int c = 0; c < nc; c++) {
         const double ae = AcubE[lane * nc + c], ac = Ac[lane * nc + c];
         a0 += ac * P.beta[c];
@@ -1603,32 +1617,58 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
   }
   WSYNC();
   STAMP(37);
-  // per-row vectors g_j
-  for (int t = lane; t < m * n; t += WAVE) {
-    const int j = t / n, i = t % n;
-    const double* rr = rows + j * SN_ROWREC;
-    const int mp = (int)rr[RR_MAP];
+  // per-row vectors g_j (lane = dof i, rows wave-uniform)
+  for (int i = lane; i < n; i += WAVE) {
     const double* nv = P.NV + i * NV_COLS;
-    double g = 0.0;
-    if (mp == CM_CLAMPING) {
-      const int c = (int)rr[RR_CIDX];
-      g = P.fc[c] * nv[NV_W] - P.beta[c] * sn[SN_VF + i] - P.lam[c] * nv[NV_SIGMA] - P.xq[c] * nv[NV_KAPPA];
-      if (imp) g += P.rho[c] * nv[NV_MA1] + P.r1[c] * nv[NV_MARHO] + P.piv[c] * nv[NV_MA2] + P.zeta[c] * nv[NV_MAPI];
-    } else if (mp >= 0) {
-      const int c = (int)rows[mp * SN_ROWREC + RR_CIDX];
-      double inner = P.fc[c] * nv[NV_W] - P.xq[c] * nv[NV_KAPPA];
-      if (imp) inner += P.rho[c] * nv[NV_MA1] + P.piv[c] * nv[NV_MA2];
-      g = rr[RR_EVAL] * inner;
+    const double w = nv[NV_W], sg = nv[NV_SIGMA], ka = nv[NV_KAPPA], ma1 = nv[NV_MA1], mar = nv[NV_MARHO];
+    const double ma2 = nv[NV_MA2], map = nv[NV_MAPI], vf = sn[SN_VF + i];
+    for (int j = 0; j < m; j++) {
+      const double* rr = rows + j * SN_ROWREC;
+      const int mp = uni((int)rr[RR_MAP]);
+      double g = 0.0;
+      if (mp == CM_CLAMPING) {
+        const int c = uni((int)rr[RR_CIDX]);
+        g = P.fc[c] * w - P.beta[c] * vf - P.lam[c] * sg - P.xq[c] * ka;
+        if (imp) g += P.rho[c] * ma1 + P.r1[c] * mar + P.piv[c] * ma2 + P.zeta[c] * map;
+      } else if (mp >= 0) {
+        const int c = uni((int)rows[mp * SN_ROWREC + RR_CIDX]);
+        double inner = P.fc[c] * w - P.xq[c] * ka;
+        if (imp) inner += P.rho[c] * ma1 + P.piv[c] * ma2;
+        g = rr[RR_EVAL] * inner;
+      }
+      P.gRows[j * n + i] = g;
     }
-    P.gRows[j * n + i] = g;
   }
   WSYNC();
-  // T_A(g_j), T_B(g_j)
-  for (int t = lane; t < 2 * m; t += WAVE) {
-    const int j = t >> 1, side = t & 1;
-    const double* rec = sn + SN_CONTACTS + (int)rows[j * SN_ROWREC + RR_CONTACT] * CREC;
-    const int body = (int)rec[8 + side];
-    bodyTwist(md, s + L.Sw, body, P.gRows + j * n, 1, P.TAB + j * 12 + side * 6);
+  // T_A(g_j), T_B(g_j): lane = (row, side), summed over the dofs that move
+  // any contact body (the others have weight 0 for every lane)
+  {
+    const int t = lane;
+    int body = -1;
+    if (t < 2 * m) {
+      const double* rec = sn + SN_CONTACTS + (int)rows[(t >> 1) * SN_ROWREC + RR_CONTACT] * CREC;
+      body = (int)rec[8 + (t & 1)];
+    }
+    const unsigned long long an = body >= 0 ? md.anc[body] : 0ull;
+    // union over the wave of the ancestor sets
+    unsigned lo = (unsigned)an, hi = (unsigned)(an >> 32);
+    for (int o = 32; o >= 1; o >>= 1) {
+      lo |= __shfl_xor(lo, o);
+      hi |= __shfl_xor(hi, o);
+    }
+    const unsigned long long all = ((unsigned long long)uni((int)hi) << 32) | (unsigned)uni((int)lo);
+    unsigned long long dm = ancestorDofMask(md, all, lane);
+    double T[6] = {0, 0, 0, 0, 0, 0};
+    const double* g = P.gRows + (t < 2 * m ? (t >> 1) : 0) * n;
+    while (dm) {
+      const int r = __ffsll((long long)dm) - 1;
+      dm &= dm - 1ull;
+      // bodyTwist's arithmetic: fma(S_r, g_r, T) for the ancestor dofs
+      const double gr = ((an >> md.dofBody[r]) & 1ull) ? g[r] : 0.0;
+      for (int i = 0; i < 6; i++) T[i] = fma(s[L.Sw + 6 * r + i], gr, T[i]);
+    }
+    if (t < 2 * m)
+      for (int i = 0; i < 6; i++) P.TAB[(t >> 1) * 12 + (t & 1) * 6 + i] = T[i];
   }
   WSYNC();
   STAMP(38);
@@ -1898,16 +1938,22 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
         for (int i = 0; i < 6; i++) omega[lane * 6 + i] = t[i];
       }
       WSYNC();
-      if (lane < nb) {
-        double pb[6] = {0, 0, 0, 0, 0, 0};
-        const unsigned long long an = md.anc[lane];
-#pragma unroll 4
-        for (int r = 0; r < n; r++) {
-          const double w = ((an >> md.dofBody[r]) & 1ull) ? 1.0 : 0.0;
+      {
+        // omega is non-zero only on the dofs that move body c (its rows'
+        // bodies are c), so the sums run over those
+        unsigned long long dm = ancestorDofMask(md, md.anc[c], lane);
+        if (lane < nb) {
+          double pb[6] = {0, 0, 0, 0, 0, 0};
+          const unsigned long long an = md.anc[lane];
+          while (dm) {
+            const int r = __ffsll((long long)dm) - 1;
+            dm &= dm - 1ull;
+            const double w = ((an >> md.dofBody[r]) & 1ull) ? 1.0 : 0.0;
 #pragma unroll
-          for (int i = 0; i < 6; i++) pb[i] = fma(w, omega[6 * r + i], pb[i]);
+            for (int i = 0; i < 6; i++) pb[i] = fma(w, omega[6 * r + i], pb[i]);
+          }
+          for (int i = 0; i < 6; i++) Pc[lane * 6 + i] = pb[i];
         }
-        for (int i = 0; i < 6; i++) Pc[lane * 6 + i] = pb[i];
       }
       WSYNC();
       if (k < n && ((md.anc[c] >> bk) & 1ull)) {

@@ -1881,6 +1881,20 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
     hi |= __shfl_xor(hi, o);
   }
   const unsigned long long dofBodies = ((unsigned long long)uni((int)hi) << 32) | (unsigned)uni((int)lo);
+  // row data, lane j < m, loaded once from the snapshot; the loops below
+  // read them by readlane instead of chains of dependent memory loads
+  int rMap = CM_NOT_CLAMPING, rA = 0, rB = 0, rTyp = 0, rDir = 0, rCon = 0;
+  double rp[3] = {0, 0, 0}, rd[3] = {0, 0, 0}, rn[3] = {0, 0, 0};
+  if (lane < m) {
+    const double* rr = rows + lane * SN_ROWREC;
+    rMap = (int)rr[RR_MAP];
+    rDir = (int)rr[RR_DIR];
+    rCon = (int)rr[RR_CONTACT];
+    const double* rec = sn + SN_CONTACTS + rCon * CREC;
+    rA = (int)rec[8]; rB = (int)rec[9]; rTyp = (int)rec[7];
+    for (int i = 0; i < 3; i++) { rp[i] = rec[i]; rn[i] = rec[3 + i]; rd[i] = rr[RR_D + i]; }
+  }
+  const unsigned long long liveRows = __ballot(lane < m && rMap != CM_NOT_CLAMPING);
   for (int j0 = 0; j0 < m; j0++) {
     const double* r0 = rows + j0 * SN_ROWREC;
     if ((int)r0[RR_MAP] == CM_NOT_CLAMPING) continue;
@@ -1893,16 +1907,12 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
       // omega^c_r (lane r), vertex sums (lanes over rows), all for body c
       TACC_BEGIN(tO);
       double om[6] = {0, 0, 0, 0, 0, 0};
-      double uv[6] = {0, 0, 0, 0, 0, 0};
-      for (int j = 0; j < m; j++) {
-        const double* rr = rows + j * SN_ROWREC;
-        if ((int)rr[RR_MAP] == CM_NOT_CLAMPING) continue;
-        const double* rec = sn + SN_CONTACTS + (int)rr[RR_CONTACT] * CREC;
-        const int A = (int)rec[8], B = (int)rec[9];
-        if (A != c && B != c) continue;
-        const double sg = A == c ? 1.0 : -1.0;
-        const double* p = rec;
-        const double* d = rr + RR_D;
+      const unsigned long long rowsC = __ballot(((liveRows >> lane) & 1ull) && (rA == c || rB == c));
+      for (unsigned long long bits = rowsC; bits; bits &= bits - 1ull) {
+        const int j = __ffsll((long long)bits) - 1;
+        const double sg = rdli(rA, j) == c ? 1.0 : -1.0;
+        double p[3], d[3];
+        for (int i = 0; i < 3; i++) { p[i] = rdl(rp[i], j); d[i] = rdl(rd[i], j); }
         double wr[6];
         cross3(p, d, wr);
         wr[3] = d[0]; wr[4] = d[1]; wr[5] = d[2];
@@ -1911,21 +1921,27 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
 #pragma unroll
           for (int i = 0; i < 6; i++) om[i] = fma(gr, wr[i], om[i]);
         }
-        // vertex side of this row?
-        const int type = (int)rec[7] & 15;
-        const bool vertexSide = (type == CT_VERTEX_FACE && A == c) || (type == CT_FACE_VERTEX && B == c);
-        if (vertexSide && lane == 0) {
+      }
+      // vertex sides of c's rows (lane = row), summed over the wave
+      {
+        double uvl[6] = {0, 0, 0, 0, 0, 0};
+        const int type = rTyp & 15;
+        const bool vertexSide = ((rowsC >> lane) & 1ull) &&
+                                ((type == CT_VERTEX_FACE && rA == c) || (type == CT_FACE_VERTEX && rB == c));
+        if (vertexSide) {
           double tw[3], dxt[3], pxd[3];
-          for (int i = 0; i < 3; i++) tw[i] = P.TAB[j * 12 + i] - P.TAB[j * 12 + 6 + i];
-          cross3(d, tw, dxt);
-          cross3(p, dxt, pxd);
-          for (int i = 0; i < 3; i++) { uv[i] += dxt[i]; uv[3 + i] += pxd[i]; }
+          for (int i = 0; i < 3; i++) tw[i] = P.TAB[lane * 12 + i] - P.TAB[lane * 12 + 6 + i];
+          cross3(rd, tw, dxt);
+          cross3(rp, dxt, pxd);
+          for (int i = 0; i < 3; i++) { uvl[i] = dxt[i]; uvl[3 + i] = pxd[i]; }
         }
+        double uvs[6];
+        for (int i = 0; i < 6; i++) uvs[i] = waveSum(uvl[i]);
+        if (lane == 0)
+          for (int i = 0; i < 6; i++) UV[i] = uvs[i];
       }
       if (lane < n)
         for (int i = 0; i < 6; i++) omega[lane * 6 + i] = om[i];
-      if (lane == 0)
-        for (int i = 0; i < 6; i++) UV[i] = uv[i];
       WSYNC();
       TACC_END(82, tO);
       TACC_BEGIN(tP);
@@ -1972,40 +1988,37 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
   // face side: per row
   TACC_BEGIN(tF);
   if (k < n) {
-    for (int j = 0; j < m; j++) {
-      const double* rr = rows + j * SN_ROWREC;
-      if ((int)rr[RR_MAP] == CM_NOT_CLAMPING) continue;
-      const double* rec = sn + SN_CONTACTS + (int)rr[RR_CONTACT] * CREC;
-      const int A = (int)rec[8], B = (int)rec[9], typ = (int)rec[7], type = typ & 15;
-      if (type == CT_SPHERE_BOX || type == CT_BOX_SPHERE) {
-        acc += sphereRowTerm(md, s, L, P, j, rec, rr, Z, bk);
-        continue;
-      }
-      if (type == CT_EDGE_EDGE) {
-        acc += edgeRowTerm(md, P, j, rec, rr, sn + snEdge(n) + (int)rr[RR_CONTACT] * EDGE_REC, Z, bk, A, B);
+    for (unsigned long long bits = liveRows; bits; bits &= bits - 1ull) {
+      const int j = __ffsll((long long)bits) - 1;
+      const int A = rdli(rA, j), B = rdli(rB, j), type = rdli(rTyp, j) & 15;
+      if (type == CT_SPHERE_BOX || type == CT_BOX_SPHERE || type == CT_EDGE_EDGE) {
+        const double* rr = rows + j * SN_ROWREC;
+        const int con = rdli(rCon, j);
+        const double* rec = sn + SN_CONTACTS + con * CREC;
+        if (type == CT_EDGE_EDGE) acc += edgeRowTerm(md, P, j, rec, rr, sn + snEdge(n) + con * EDGE_REC, Z, bk, A, B);
+        else acc += sphereRowTerm(md, s, L, P, j, rec, rr, Z, bk);
         continue;
       }
       int faceBody = -1;
       if (type == CT_VERTEX_FACE) faceBody = B;
       else if (type == CT_FACE_VERTEX) faceBody = A;
       if (faceBody < 0 || !((md.anc[faceBody] >> bk) & 1ull)) continue;
-      const double* p = rec;
-      const double* d = rr + RR_D;
+      double p[3], nrm[3];
+      for (int i = 0; i < 3; i++) { p[i] = rdl(rp[i], j); nrm[i] = rdl(rn[i], j); }
       double dn[3];
       const double wv[3] = {Z[0], Z[1], Z[2]};
-      cross3(wv, rec + 3, dn);
+      cross3(wv, nrm, dn);
       double dd[3];
-      const int dirIdx = (int)rr[RR_DIR];
+      const int dirIdx = rdli(rDir, j);
       if (dirIdx == 0 || dot3(dn, dn) <= 1e-12) {
         for (int i = 0; i < 3; i++) dd[i] = dn[i];
       } else {
         double T0[3], T1[3];
-        tangentBasisGradient(rec + 3, dn, T0, T1);
+        tangentBasisGradient(nrm, dn, T0, T1);
         for (int i = 0; i < 3; i++) dd[i] = dirIdx == 1 ? T0[i] : T1[i];
       }
       double pxdd[3];
       cross3(p, dd, pxdd);
-      (void)d;
       double v = 0.0;
       for (int i = 0; i < 3; i++)
         v += (P.TAB[j * 12 + i] - P.TAB[j * 12 + 6 + i]) * pxdd[i] +

@@ -309,9 +309,13 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, con
     }
     __syncthreads();  // the one barrier both waves take: flags initialised
     if (threadIdx.x >= WAVE) {
+      // the helper's work is speculative: it only takes issue slots the
+      // step's wave leaves idle (lower wave priority on the shared SIMD)
+      __builtin_amdgcn_s_setprio(0);
       for (int env = blockIdx.x; env < batch; env += gridDim.x) helperWave(md, s, L, lane);
       return;
     }
+    __builtin_amdgcn_s_setprio(2);
   }
   for (int env = blockIdx.x; env < batch; env += gridDim.x) {
     const double* st = state + (size_t)env * 2 * n;

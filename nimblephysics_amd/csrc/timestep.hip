@@ -1,7 +1,8 @@
 // Batched differentiable timestep for gfx950 (MI355X).
 //
-// One world instance per 64-lane wavefront (one workgroup = one wave), all of
-// its working set staged in LDS.  The reference advances one World at a time
+// One world instance per 64-lane wavefront (plus, for contact models, a
+// second LCP helper wave in the forward's workgroup), all of its working set
+// staged in LDS.  The reference advances one World at a time
 // on the CPU (dart/simulation/World.cpp:221 World::step, with the
 // articulated-body recursions of dart/dynamics/Skeleton.cpp:13034); here every
 // quantity is kept in WORLD coordinates, which turns the per-body frame
@@ -11,7 +12,7 @@
 //   * composite (subtree) inertias and forces: one lane per matrix element,
 //     reverse body order;
 //   * mass matrix M_jk = S_j^T I^C S_k: one lane per (j,k) pair (CRBA);
-//   * M = L L^T and the solves: right-looking Cholesky, lanes over rows;
+//   * M = L L^T and the solves: left-looking (Crout) Cholesky, lanes over rows;
 //   * backward: one lane per input direction (q_k, v_k, tau_k), each lane
 //     forming its column of dID/dq and dC/dv in closed form from the
 //     world-frame composites and dotting it with Minv * dL/dv'.

@@ -2069,7 +2069,10 @@ __device__ double mFieldsTerm(const ModelDev& md, double* s, const Layout& L, co
   }
   WSYNC();
   double total = 0.0;
-  for (int pr = 0; pr < 4; pr++) {
+  // the pseudo-inverse branch's two pairs carry the factor -imp: skipped
+  // when Q has full rank
+  const int npairs = imp != 0.0 ? 4 : 2;
+  for (int pr = 0; pr < npairs; pr++) {
     if (lane < nb) {
       const int b = lane;
       double Va[6] = {0, 0, 0, 0, 0, 0}, Vc[6] = {0, 0, 0, 0, 0, 0};

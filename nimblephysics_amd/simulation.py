@@ -186,6 +186,22 @@ class World:
         f = self.getControlForces()
         return np.array([f[m] for m in self.getActionSpace()])
 
+    # --- tunable masses (World::getMassDims / getMasses / setMasses,
+    # dart/simulation/World.cpp) --------------------------------------------------------
+    # No body is registered for mass tuning (World::tuneMass is not on the
+    # batched path), which is the reference's default: the mass vector has
+    # zero entries and TimestepLayer's lossWrtMass is empty.
+    def getMassDims(self) -> int:
+        return 0
+
+    def getMasses(self):
+        return np.zeros(0)
+
+    def setMasses(self, masses):
+        masses = np.asarray(masses, dtype=np.float64).reshape(-1)
+        if masses.shape[0] != self.getMassDims():
+            raise ValueError(f"setMasses: {masses.shape[0]} values, the world has {self.getMassDims()} mass dims")
+
     # --- flattening -----------------------------------------------------------------------
     def desc_arrays(self) -> Dict[str, np.ndarray]:
         bodies = []

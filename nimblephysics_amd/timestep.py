@@ -16,6 +16,10 @@ CPU tensors (what the reference's layer takes, timestep.py:31 calls
 staged to the current HIP device, stepped by the same kernels, and the
 results / gradients come back on the CPU.  There is no CPU compute path --
 without a HIP device the call raises.
+
+``mass`` is the reference's tuned-mass vector (World::getMassDims entries,
+set with World::setMasses); no body is registered for mass tuning on this
+path, so it is empty when given and its gradient (lossWrtMass) is empty.
 """
 from __future__ import annotations
 
@@ -67,8 +71,18 @@ def _compute_device(t: torch.Tensor) -> torch.device:
 class TimestepLayer(torch.autograd.Function):
     @staticmethod
     def forward(ctx, world: World, state: torch.Tensor, action: torch.Tensor, mass: Optional[torch.Tensor]):
-        if mass is not None:
-            raise NotImplementedError("mass gradients (WithRespectToMass) are not on the batched hot path yet")
+        # `mass` follows the reference (timestep.py:34, world.setMasses): a
+        # vector of the world's getMassDims() tuned masses -- zero of them
+        # here (World::tuneMass is not on the batched path), so only an empty
+        # vector (or [B, 0]) is accepted and its gradient is empty
+        ctx.use_mass = mass is not None
+        if ctx.use_mass:
+            if mass.shape[-1] != world.getMassDims():
+                raise NotImplementedError(
+                    f"mass has {mass.shape[-1]} entries; tuned masses (World::tuneMass) are not on the batched "
+                    f"path and this world has {world.getMassDims()} mass dims")
+            ctx.mass_shape = tuple(mass.shape)
+            ctx.mass_device = mass.device
         ctx.out_device = state.device
         cdev = _compute_device(state)
         state = state.to(cdev, torch.float64)
@@ -115,9 +129,10 @@ class TimestepLayer(torch.autograd.Function):
         dev.backward(st, forces, snap, g, gs, gf, stream)
         ga = gf.index_select(1, idx)
         od = ctx.out_device
+        gm = torch.zeros(ctx.mass_shape, dtype=torch.float64, device=ctx.mass_device) if ctx.use_mass else None
         if ctx.squeeze:
-            return None, gs[0].to(od), ga[0].to(od), None
-        return None, gs.to(od), ga.to(od), None
+            return None, gs[0].to(od), ga[0].to(od), gm
+        return None, gs.to(od), ga.to(od), gm
 
 
 def timestep(world: World, state: torch.Tensor, action: torch.Tensor,

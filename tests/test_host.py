@@ -68,6 +68,21 @@ def test_world_description_atlas():
     assert (jt == 3).sum() == 1 and (jt == 1).sum() == 27
 
 
+def test_mass_argument_follows_reference_mass_dims():
+    """timestep(world, state, action, mass): the reference's mass vector has
+    getMassDims() entries (zero unless bodies are registered for mass
+    tuning); a non-empty one is rejected before any device work."""
+    import nimblephysics_amd as nimble
+    w = models.cartpole_world()
+    assert w.getMassDims() == 0 and w.getMasses().shape == (0,)
+    w.setMasses(np.zeros(0))
+    with pytest.raises(ValueError):
+        w.setMasses(np.ones(2))
+    st = torch.tensor(w.getState())
+    with pytest.raises(NotImplementedError):
+        nimble.timestep(w, st, torch.zeros(2, dtype=torch.float64), torch.ones(2, dtype=torch.float64))
+
+
 def test_product_rejects_cpu_tensors():
     from nimblephysics_amd import _native
     with pytest.raises(RuntimeError):

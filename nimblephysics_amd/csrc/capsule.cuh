@@ -24,6 +24,7 @@
 
 #define CT_SPHERE_BOX 4
 #define CT_BOX_SPHERE 5
+#define CT_SPHERE_SPHERE 6
 
 namespace cap {
 
@@ -401,6 +402,54 @@ DEV bool lineIntersect(P2 p, P2 p1, P2 q, P2 q1) {
 }
 
 }  // namespace cap
+
+// A standalone sphere shape (centre c0, radius r) against a box (size bs,
+// transform Tb 3x4): collideSphereBox (DARTCollide.cpp:1655) or, boxFirst,
+// collideBoxSphere (:1482) with the default BOTH half-space.  One record.
+__device__ __noinline__ int deviceSphereBox(const double* Tb, const double* bs, const double* c0, double r,
+                                            bool boxFirst, double clip, int body1, int body2, int boxShape,
+                                            double* out) {
+  using namespace cap;
+  Obj box;
+  for (int i = 0; i < 12; i++) box.T.m[i] = Tb[i];
+  box.s0 = bs[0]; box.s1 = bs[1]; box.s2 = bs[2]; box.capsule = false;
+  const int cnt = sphereBox(box, mk(c0[0], c0[1], c0[2]), nullptr, r, boxFirst, 0, clip, boxShape, out);
+  if (cnt) { out[8] = body1; out[9] = body2; }
+  return cnt;
+}
+
+// collideSphereSphere (DARTCollide.cpp:1812): one SPHERE_SPHERE record at the
+// radius-weighted point between the centres, normal from centre 1 to centre
+// 0 (zero for coincident centres); centre 0 at [10..12], and after the
+// record (the EDGE_REC tail) centre 1, radius 0, radius 1.
+__device__ __noinline__ int deviceSphereSphere(const double* c0, double r0, const double* c1, double r1, double clip,
+                                               int body1, int body2, double* out) {
+  const double rsum = r0 + r1;
+  double nv[3] = {c0[0] - c1[0], c0[1] - c1[1], c0[2] - c1[2]};
+  double nsq = nv[0] * nv[0] + nv[1] * nv[1] + nv[2] * nv[2];
+  if (nsq > rsum * rsum) return 0;
+  const double w0 = r0 / rsum, w1 = r1 / rsum;
+  double depth;
+  if (nsq < 1e-6) {  // DART_COLLISION_EPS
+    nv[0] = nv[1] = nv[2] = 0.0;
+    depth = rsum;
+  } else {
+    nsq = sqrt(nsq);
+    for (int i = 0; i < 3; i++) nv[i] *= 1.0 / nsq;
+    depth = rsum - nsq;
+  }
+  if (depth > clip) return 0;
+  for (int i = 0; i < 3; i++) {
+    out[i] = w1 * c0[i] + w0 * c1[i];
+    out[3 + i] = nv[i];
+    out[10 + i] = c0[i];
+    out[CREC + i] = c1[i];
+  }
+  out[6] = depth; out[7] = CT_SPHERE_SPHERE; out[8] = body1; out[9] = body2;
+  out[CREC + 3] = w0 * rsum;
+  out[CREC + 4] = w1 * rsum;
+  return 1;
+}
 
 // One capsule-box pair (box size `bs`, transforms Tb / Tc 3x4, capsule
 // radius r / height h).  Writes up to 2 records at `out`; returns the count

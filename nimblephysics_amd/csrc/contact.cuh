@@ -470,6 +470,21 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
         cnt = deviceCapsuleBox(Tb, md.shapeSize[sb], Tc, md.shapeSize[sc][0], md.shapeSize[sc][1], boxFirst,
                                md.clipDepth, bi, bj, sb, pairbuf + lane * 8 * PBREC, &unsup);
         if (unsup) cnt = -1 - cnt;  // flagged; the contacts found are still kept
+      } else if (md.shapeType[si] == NIMBLE_SHAPE_SPHERE || md.shapeType[sj] == NIMBLE_SHAPE_SPHERE) {
+        const int ti = md.shapeType[si], tj = md.shapeType[sj];
+        double T1[12], T2[12];
+        tmul(s + L.Tw + 12 * bi, md.shapeT[si], T1);
+        tmul(s + L.Tw + 12 * bj, md.shapeT[sj], T2);
+        const double c1[3] = {T1[3], T1[7], T1[11]}, c2[3] = {T2[3], T2[7], T2[11]};
+        double* out = pairbuf + lane * 8 * PBREC;
+        if (ti == NIMBLE_SHAPE_SPHERE && tj == NIMBLE_SHAPE_SPHERE)
+          cnt = deviceSphereSphere(c1, md.shapeSize[si][0], c2, md.shapeSize[sj][0], md.clipDepth, bi, bj, out);
+        else if (ti == NIMBLE_SHAPE_SPHERE && tj == NIMBLE_SHAPE_BOX)
+          cnt = deviceSphereBox(T2, md.shapeSize[sj], c1, md.shapeSize[si][0], false, md.clipDepth, bi, bj, sj, out);
+        else if (ti == NIMBLE_SHAPE_BOX && tj == NIMBLE_SHAPE_SPHERE)
+          cnt = deviceSphereBox(T1, md.shapeSize[si], c2, md.shapeSize[sj][0], true, md.clipDepth, bi, bj, si, out);
+        else
+          cnt = -1;
       } else {
         cnt = -1;
       }
@@ -546,7 +561,7 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
             const int idx = nk0 + __popcll(km & below);
             if (idx < NIMBLE_MAX_CONTACTS) {
               dst = ct + CT_CONTACTS + idx * CREC;
-              if (((int)rec[7] & 15) == CT_EDGE_EDGE)
+              if (((int)rec[7] & 15) == CT_EDGE_EDGE || ((int)rec[7] & 15) == CT_SPHERE_SPHERE)
                 for (int i = 0; i < EDGE_REC; i++) snapEdge[idx * EDGE_REC + i] = rec[CREC + i];
             }
           } else if (drop) {
@@ -591,7 +606,7 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
           double* dst = nullptr;
           if (keep) {
             if (nk < NIMBLE_MAX_CONTACTS) {
-              if (((int)rec[7] & 15) == CT_EDGE_EDGE)
+              if (((int)rec[7] & 15) == CT_EDGE_EDGE || ((int)rec[7] & 15) == CT_SPHERE_SPHERE)
                 for (int i = 0; i < EDGE_REC; i++) snapEdge[nk * EDGE_REC + i] = rec[CREC + i];
               dst = ct + CT_CONTACTS + (nk++) * CREC;
             } else {
@@ -1756,6 +1771,54 @@ __device__ double sphereRowTerm(const ModelDev& md, const double* s, const Layou
   return v;
 }
 
+// SPHERE_SPHERE rows (SPHERE_A / SPHERE_B of DifferentiableContactConstraint.cpp
+// :343 / :348 and :625 / :634): the contact point moves with the dof's
+// sphere centre weighted by the other radius, the normal with that centre
+// over the centre distance, projected off the normal.  E = centre B,
+// radius A, radius B (centre A is the record's sphere centre).
+__device__ double sphereSphereRowTerm(const ModelDev& md, const BwdPool& P, int j, const double* rec,
+                                      const double* rr, const double* E, const double* Z, int bk, int A, int B) {
+  const bool pa = (md.anc[A] >> bk) & 1ull, pb = (md.anc[B] >> bk) & 1ull;
+  if (pa == pb) return 0.0;
+  const double* nrm = rec + 3;
+  const double* cA = rec + 10;
+  const double* cen = pa ? cA : E;
+  const double wt = (pa ? E[4] : E[3]) / (E[3] + E[4]);
+  const double wv[3] = {Z[0], Z[1], Z[2]};
+  double g[3];
+  if (sqrt(Z[0] * Z[0] + Z[1] * Z[1] + Z[2] * Z[2]) > 1e-6) {  // gradientWrtTheta (Geometry.cpp:968)
+    cross3(wv, cen, g);
+    for (int i = 0; i < 3; i++) g[i] += Z[3 + i];
+  } else {
+    for (int i = 0; i < 3; i++) g[i] = Z[3 + i];
+  }
+  double dp[3], dn[3], dist2 = 0.0;
+  for (int i = 0; i < 3; i++) { dp[i] = wt * g[i]; dist2 += (cA[i] - E[i]) * (cA[i] - E[i]); }
+  const double norm = sqrt(dist2);
+  for (int i = 0; i < 3; i++) dn[i] = g[i] / norm;
+  const double dnn = dot3(dn, nrm);
+  for (int i = 0; i < 3; i++) dn[i] = (pa ? 1.0 : -1.0) * (dn[i] - dnn * nrm[i]);
+  double dd[3];
+  const int dirIdx = (int)rr[RR_DIR];
+  if (dirIdx == 0 || dot3(dn, dn) <= 1e-12) {
+    for (int i = 0; i < 3; i++) dd[i] = dn[i];
+  } else {
+    double T0[3], T1[3];
+    tangentBasisGradient(nrm, dn, T0, T1);
+    for (int i = 0; i < 3; i++) dd[i] = dirIdx == 1 ? T0[i] : T1[i];
+  }
+  const double* d = rr + RR_D;
+  const double* p = rec;
+  double pxdd[3], dpxd[3];
+  cross3(p, dd, pxdd);
+  cross3(dp, d, dpxd);
+  double v = 0.0;
+  for (int i = 0; i < 3; i++)
+    v += (P.TAB[j * 12 + i] - P.TAB[j * 12 + 6 + i]) * (pxdd[i] + dpxd[i]) +
+         (P.TAB[j * 12 + 3 + i] - P.TAB[j * 12 + 9 + i]) * dd[i];
+  return v;
+}
+
 // math::getContactPointGradient (dart/math/Geometry.cpp:1129), radii 1: the
 // derivative of the midpoint of the two edges' closest approach
 __device__ inline void edgeContactPointGradient(const double* pA, const double* dpA, const double* uA,
@@ -1991,11 +2054,13 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
     for (unsigned long long bits = liveRows; bits; bits &= bits - 1ull) {
       const int j = __ffsll((long long)bits) - 1;
       const int A = rdli(rA, j), B = rdli(rB, j), type = rdli(rTyp, j) & 15;
-      if (type == CT_SPHERE_BOX || type == CT_BOX_SPHERE || type == CT_EDGE_EDGE) {
+      if (type == CT_SPHERE_BOX || type == CT_BOX_SPHERE || type == CT_EDGE_EDGE || type == CT_SPHERE_SPHERE) {
         const double* rr = rows + j * SN_ROWREC;
         const int con = rdli(rCon, j);
         const double* rec = sn + SN_CONTACTS + con * CREC;
         if (type == CT_EDGE_EDGE) acc += edgeRowTerm(md, P, j, rec, rr, sn + snEdge(n) + con * EDGE_REC, Z, bk, A, B);
+        else if (type == CT_SPHERE_SPHERE)
+          acc += sphereSphereRowTerm(md, P, j, rec, rr, sn + snEdge(n) + con * EDGE_REC, Z, bk, A, B);
         else acc += sphereRowTerm(md, s, L, P, j, rec, rr, Z, bk);
         continue;
       }

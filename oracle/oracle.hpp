@@ -47,6 +47,9 @@ struct Contact {
   // EDGE_EDGE metadata (collision::Contact::edgeAFixedPoint / edgeADir /
   // edgeBFixedPoint / edgeBDir, set by dBoxBox, DARTCollide.cpp:1046, :1334)
   double edgeAFixed[3], edgeADir[3], edgeBFixed[3], edgeBDir[3];
+  // SPHERE_SPHERE metadata (collision::Contact::centerA / radiusA / centerB /
+  // radiusB, DARTCollide.cpp:1866); centerA is sphereCenter
+  double centerB[3], radiusA, radiusB;
 };
 
 // Everything BackpropSnapshot needs (dart/neural/BackpropSnapshot.hpp and
@@ -122,6 +125,13 @@ void collide(const World& w, const Kin<double>& k, std::vector<Contact>& out, in
 int capsuleBox(const Iso<double>& Tb, const double* size, const Iso<double>& Tc, double r, double h, bool boxFirst,
                double clip, int shape1, int shape2, int body1, int body2, std::vector<Contact>& out,
                int* unsupported);
+
+// standalone sphere shapes: collideSphereBox (DARTCollide.cpp:1655) /
+// collideBoxSphere (:1482, halfspace BOTH) and collideSphereSphere (:1812)
+int sphereBoxPair(const Iso<double>& Tb, const double* size, const double* c0, double r, bool boxFirst, double clip,
+                  int shape1, int shape2, int body1, int body2, std::vector<Contact>& out);
+int sphereSphere(const double* c0, double r0, const double* c1, double r1, double clip, int shape1, int shape2,
+                 int body1, int body2, std::vector<Contact>& out);
 
 // dense helpers
 void cholSolve(const double* A, const double* b, double* x, int n);

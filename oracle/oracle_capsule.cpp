@@ -645,6 +645,21 @@ int capsuleBox(const Iso<double>& Tb, const double* size, const Iso<double>& Tc,
   return added;
 }
 
+// A standalone sphere shape against a box: collideSphereBox (sphere is
+// collision object 1) / collideBoxSphere with the default BOTH half-space.
+int sphereBoxPair(const Iso<double>& Tb, const double* size, const double* c0, double r, bool boxFirst, double clip,
+                  int shape1, int shape2, int body1, int body2, std::vector<Contact>& out) {
+  Obj box{};
+  box.capsule = false;
+  for (int i = 0; i < 9; i++) box.T.R[i] = Tb.R.m[i];
+  for (int i = 0; i < 3; i++) { box.T.p.x[i] = Tb.p[i]; box.size[i] = size[i]; }
+  Contact c;
+  if (!sphereBox(box, mk(c0[0], c0[1], c0[2]), nullptr, r, boxFirst, 0, clip, c)) return 0;
+  c.shapeA = shape1; c.shapeB = shape2; c.bodyA = body1; c.bodyB = body2;
+  out.push_back(c);
+  return 1;
+}
+
 }  // namespace oracle
 
 // Raw capsule-box entry for the reference's known-answer tests

@@ -31,7 +31,7 @@ void codSolve(const double* A, int m, int n, const double* b, double* x);
 bool pgsSolveLCP(int n, double* A, double* x, double* b, double* lo, double* hi, const int* findex);
 
 static const double kInf = std::numeric_limits<double>::infinity();
-enum { CT_FACE_VERTEX = 1, CT_VERTEX_FACE = 2, CT_EDGE_EDGE = 3 };
+enum { CT_FACE_VERTEX = 1, CT_VERTEX_FACE = 2, CT_EDGE_EDGE = 3, CT_SPHERE_SPHERE = 6 };
 
 //------------------------------------------------------------------------------
 // dBoxBox restatement.  R? are 3x3 row-major world rotations, p? centres,
@@ -327,6 +327,36 @@ extern "C" int oracle_box_box(const double* size1, const double* T1, const doubl
 
 namespace oracle {
 
+// collideSphereSphere (DARTCollide.cpp:1812): one SPHERE_SPHERE contact at
+// the radius-weighted point between the centres, normal from centre 1 to 0
+int sphereSphere(const double* c0, double r0, const double* c1, double r1, double clip, int shape1, int shape2,
+                 int body1, int body2, std::vector<Contact>& out) {
+  const double rsum = r0 + r1;
+  double nrm[3];
+  for (int i = 0; i < 3; i++) nrm[i] = c0[i] - c1[i];
+  double nsq = nrm[0] * nrm[0] + nrm[1] * nrm[1] + nrm[2] * nrm[2];
+  if (nsq > rsum * rsum) return 0;
+  const double w0 = r0 / rsum, w1 = r1 / rsum;
+  Contact c{};
+  for (int i = 0; i < 3; i++) c.point[i] = w1 * c0[i] + w0 * c1[i];
+  if (nsq < 1e-6) {  // DART_COLLISION_EPS: coincident centres, zero normal
+    for (int i = 0; i < 3; i++) nrm[i] = 0.0;
+    c.depth = rsum;
+  } else {
+    nsq = std::sqrt(nsq);
+    for (int i = 0; i < 3; i++) nrm[i] *= 1.0 / nsq;
+    c.depth = rsum - nsq;
+  }
+  if (c.depth > clip) return 0;
+  c.type = CT_SPHERE_SPHERE;
+  for (int i = 0; i < 3; i++) { c.normal[i] = nrm[i]; c.sphereCenter[i] = c0[i]; c.centerB[i] = c1[i]; }
+  c.radiusA = w0 * rsum;
+  c.radiusB = w1 * rsum;
+  c.shapeA = shape1; c.shapeB = shape2; c.bodyA = body1; c.bodyB = body2;
+  out.push_back(c);
+  return 1;
+}
+
 void collide(const World& w, const Kin<double>& k, std::vector<Contact>& out, int* unsupported) {
   out.clear();
   int unsup = 0;
@@ -354,6 +384,12 @@ void collide(const World& w, const Kin<double>& k, std::vector<Contact>& out, in
       } else if (S1.type == NIMBLE_SHAPE_CAPSULE && S2.type == NIMBLE_SHAPE_BOX) {
         // collideCapsuleBox (:4533)
         capsuleBox(T2, S2.size, T1, S1.size[0], S1.size[1], false, w.clipDepth, i, j, S1.body, S2.body, pair, &unsup);
+      } else if (S1.type == NIMBLE_SHAPE_SPHERE && S2.type == NIMBLE_SHAPE_BOX) {
+        sphereBoxPair(T2, S2.size, T1.p.x, S1.size[0], false, w.clipDepth, i, j, S1.body, S2.body, pair);
+      } else if (S1.type == NIMBLE_SHAPE_BOX && S2.type == NIMBLE_SHAPE_SPHERE) {
+        sphereBoxPair(T1, S1.size, T2.p.x, S2.size[0], true, w.clipDepth, i, j, S1.body, S2.body, pair);
+      } else if (S1.type == NIMBLE_SHAPE_SPHERE && S2.type == NIMBLE_SHAPE_SPHERE) {
+        sphereSphere(T1.p.x, S1.size[0], T2.p.x, S2.size[0], w.clipDepth, i, j, S1.body, S2.body, pair);
       } else {
         std::fprintf(stderr, "oracle: shape pair (%d,%d) not supported\n", S1.type, S2.type);
         std::abort();

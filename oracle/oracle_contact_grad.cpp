@@ -26,7 +26,7 @@ namespace oracle {
 void codSolve(const double* A, int m, int n, const double* b, double* x);
 
 using Mat = std::vector<double>;
-enum { CT_FACE_VERTEX = 1, CT_VERTEX_FACE = 2, CT_EDGE_EDGE = 3, CT_SPHERE_BOX = 4, CT_BOX_SPHERE = 5 };
+enum { CT_FACE_VERTEX = 1, CT_VERTEX_FACE = 2, CT_EDGE_EDGE = 3, CT_SPHERE_BOX = 4, CT_BOX_SPHERE = 5, CT_SPHERE_SPHERE = 6 };
 
 static void cross3(const double* a, const double* b, double* o) {
   o[0] = a[1] * b[2] - a[2] * b[1];
@@ -162,6 +162,7 @@ static void constraintForcesJacobian(const World& w, const Kin<double>& k, const
     int type = 0;  // 0 none, 1 vertex, 2 face, 3 sphere-to-box, 4 box-to-sphere (getDofContactType :116)
     if (pa || pb) {
       if (c.type == CT_EDGE_EDGE) type = pa ? 5 : 6;  // EDGE_A / EDGE_B
+      else if (c.type == CT_SPHERE_SPHERE) type = pa ? 7 : 8;  // SPHERE_A / SPHERE_B
       else if (c.type == CT_SPHERE_BOX) type = pa ? 3 : 4;
       else if (c.type == CT_BOX_SPHERE) type = pa ? 4 : 3;
       else if (c.type == CT_VERTEX_FACE) type = pa ? 1 : 2;
@@ -217,6 +218,29 @@ static void constraintForcesJacobian(const World& w, const Kin<double>& k, const
       const double dnn = dn[0] * nrm[0] + dn[1] * nrm[1] + dn[2] * nrm[2];
       for (int i = 0; i < 3; i++) dn[i] -= dnn * nrm[i];
       // getContactForceGradient (:1092)
+      if (dirIdx == 0 || dn[0] * dn[0] + dn[1] * dn[1] + dn[2] * dn[2] <= 1e-12) {
+        for (int i = 0; i < 3; i++) dd[i] = dn[i];
+      } else {
+        double T0[3], T1[3];
+        tangentBasisGradient(c.normal, dn, T0, T1);
+        for (int i = 0; i < 3; i++) dd[i] = dirIdx == 1 ? T0[i] : T1[i];
+      }
+    } else if (type == 7 || type == 8) {
+      // SPHERE_A / SPHERE_B: the contact point moves with its sphere's centre
+      // weighted by the other radius (:343 / :348); the normal by the centre's
+      // motion over the centre distance, projected off the normal (:625 / :634)
+      const bool A = type == 7;
+      const double* cen = A ? c.sphereCenter : c.centerB;
+      const double wt = (A ? c.radiusB : c.radiusA) / (c.radiusA + c.radiusB);
+      double g[3], dn[3];
+      gwt(cen, g);
+      for (int i = 0; i < 3; i++) dp[i] = wt * g[i];
+      double dist2 = 0;
+      for (int i = 0; i < 3; i++) dist2 += (c.sphereCenter[i] - c.centerB[i]) * (c.sphereCenter[i] - c.centerB[i]);
+      const double norm = std::sqrt(dist2);
+      for (int i = 0; i < 3; i++) dn[i] = g[i] / norm;
+      const double dnn = dn[0] * c.normal[0] + dn[1] * c.normal[1] + dn[2] * c.normal[2];
+      for (int i = 0; i < 3; i++) dn[i] = (A ? 1.0 : -1.0) * (dn[i] - dnn * c.normal[i]);
       if (dirIdx == 0 || dn[0] * dn[0] + dn[1] * dn[1] + dn[2] * dn[2] <= 1e-12) {
         for (int i = 0; i < 3; i++) dd[i] = dn[i];
       } else {

@@ -284,3 +284,64 @@ def ledge_world():
     v = np.zeros(6)
     v[4] = -0.05
     return w, np.concatenate([q, v])
+
+
+SPHERE_RADII = (0.1, 0.15)
+
+
+def sphere_world(ground_first=True):
+    """Two free spheres (separate skeletons) on a static ground box: the
+    sphere-sphere pair is SPHERE_SPHERE (collideSphereSphere,
+    DARTCollide.cpp:1812) and each sphere-ground pair BOX_SPHERE (ground
+    first in detector order, collideBoxSphere :1482) or SPHERE_BOX
+    (collideSphereBox :1655), clamped against the ground's top face."""
+    from nimblephysics_amd import dynamics as D
+    w = nimble.World()
+    w.setGravity([0, -9.81, 0])
+
+    def ground():
+        g = D.Skeleton("ground")
+        gj, gb = g.createWeldJointAndBodyNodePair()
+        T = np.eye(4)
+        T[1, 3] = -0.25
+        gj.setTransformFromParentBodyNode(T)
+        gb.createShapeNode(D.BoxShape([4.0, 0.5, 4.0]), collision=True)
+        g.setMobile(False)
+        w.addSkeleton(g)
+
+    if ground_first:
+        ground()
+    for i, r in enumerate(SPHERE_RADII):
+        sk = D.Skeleton(f"ball{i}")
+        _, b = sk.createFreeJointAndBodyNodePair()
+        b.setMass(0.5 + i)
+        b.setMomentOfInertia(0.4 * (0.5 + i) * r * r, 0.4 * (0.5 + i) * r * r, 0.4 * (0.5 + i) * r * r)
+        b.createShapeNode(D.SphereShape(r), collision=True)
+        w.addSkeleton(sk)
+    if not ground_first:
+        ground()
+    return w
+
+
+def sphere_states(batch, seed=0):
+    """Both spheres 0.5-3 mm into the ground, pressed 0.5-3 mm into each
+    other along a random horizontal direction, moving down and together."""
+    rng = np.random.default_rng(seed)
+    r0, r1 = SPHERE_RADII
+    q = np.zeros((batch, 12))
+    v = 0.05 * rng.standard_normal((batch, 12))
+    for b in range(batch):
+        q[b, 0:3] = 0.3 * rng.standard_normal(3)
+        q[b, 6:9] = 0.3 * rng.standard_normal(3)
+        c0 = np.array([rng.uniform(-0.5, 0.5), r0 - rng.uniform(5e-4, 3e-3), rng.uniform(-0.5, 0.5)])
+        phi = rng.uniform(0, 2 * np.pi)
+        dy = (r1 - rng.uniform(5e-4, 3e-3)) - c0[1]
+        dist = r0 + r1 - rng.uniform(5e-4, 3e-3)
+        h = np.sqrt(dist * dist - dy * dy)
+        q[b, 3:6] = c0
+        q[b, 9:12] = c0 + np.array([h * np.cos(phi), dy, h * np.sin(phi)])
+        u = (q[b, 9:12] - c0) / dist
+        v[b, 3:6] += 0.1 * u - [0, 0.1, 0]
+        v[b, 9:12] += -0.1 * u - [0, 0.1, 0]
+    f = 0.3 * rng.standard_normal((batch, 12))
+    return np.concatenate([q, v], axis=1), f

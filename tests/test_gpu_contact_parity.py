@@ -278,3 +278,19 @@ def test_edge_edge_contact_parity(name):
         types += list((snap[b, SN_CONTACTS:SN_CONTACTS + CREC * nc].reshape(nc, CREC)[:, 7].astype(int) & 15))
     assert 3 in types  # EDGE_EDGE present
     assert (snap[:, SN_NC] > 0).any()  # and clamping
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ground_first", [True, False])
+def test_sphere_contact_parity(ground_first):
+    """Standalone sphere shapes: SPHERE_SPHERE contacts (collideSphereSphere)
+    and sphere-ground contacts (BOX_SPHERE via collideBoxSphere when the
+    ground is first in detector order, SPHERE_BOX via collideSphereBox
+    otherwise, clamped on the ground's top face), forward and gradients."""
+    world = models.sphere_world(ground_first)
+    st, f = models.sphere_states(64, seed=5)
+    ow, snap = _parity(world, st, f)
+    assert (snap[:, SN_NCON] == 3).all()
+    types = np.sort(snap[:, SN_CONTACTS + 7 + CREC * np.arange(3)].astype(int) & 15, axis=1)
+    want = [5, 5, 6] if ground_first else [4, 4, 6]
+    assert (types == want).all()

@@ -205,3 +205,31 @@ def test_sphere_box_gradients_vs_finite_differences(oracle_built, name):
         assert np.abs(gs - fd_s).max() <= 1e-6 * np.abs(fd_s).max(), (name, b)
         assert np.abs(gf - fd_f).max() <= 1e-6 * np.abs(fd_f).max(), (name, b)
     assert clamped >= 2
+
+
+@pytest.mark.parametrize("ground_first", [True, False])
+def test_sphere_contact_gradients_vs_finite_differences(oracle_built, ground_first):
+    """SPHERE_SPHERE (SPHERE_A / SPHERE_B terms) and sphere-ground
+    (BOX_SPHERE or SPHERE_BOX with the locked top face) contacts: the
+    collider's known geometry and the analytical gradients against central
+    differences of the oracle's own step."""
+    w = models.sphere_world(ground_first)
+    st, f = models.sphere_states(1, seed=3)
+    st, f = st[0], f[0]
+    o = O.OracleWorld(w)
+    o.forward(st[None], f[None])
+    cs = O.contacts(o, 0)
+    types = sorted(int(t) & 15 for t in cs[:, 7])
+    assert types == ([5, 5, 6] if ground_first else [4, 4, 6]), types
+    r0, r1 = models.SPHERE_RADII
+    c0, c1 = st[3:6], st[9:12]
+    ss = cs[(cs[:, 7].astype(int) & 15) == 6][0]
+    d = np.linalg.norm(c0 - c1)
+    assert np.allclose(ss[0:3], (r1 * c0 + r0 * c1) / (r0 + r1), atol=1e-12)
+    assert np.allclose(ss[3:6], (c0 - c1) / d, atol=1e-12)
+    assert abs(ss[6] - (r0 + r1 - d)) < 1e-12
+    assert O.lcp_flags(o, 0)[3] > 0  # clamping rows
+    g = np.random.default_rng(4).standard_normal(24)
+    gs, gf, fd_s, fd_f = _fd_check(w, st, f, g)
+    assert np.abs(gs - fd_s).max() <= 1e-6 * np.abs(fd_s).max()
+    assert np.abs(gf - fd_f).max() <= 1e-6 * np.abs(fd_f).max()

@@ -25,6 +25,8 @@
 #define CT_SPHERE_BOX 4
 #define CT_BOX_SPHERE 5
 #define CT_SPHERE_SPHERE 6
+#define CT_SPHERE_PIPE 7
+#define CT_PIPE_SPHERE 8
 
 namespace cap {
 
@@ -448,6 +450,69 @@ __device__ __noinline__ int deviceSphereSphere(const double* c0, double r0, cons
   out[6] = depth; out[7] = CT_SPHERE_SPHERE; out[8] = body1; out[9] = body2;
   out[CREC + 3] = w0 * rsum;
   out[CREC + 4] = w1 * rsum;
+  return 1;
+}
+
+// collideSphereCapsule (DARTCollide.cpp:4286) / collideCapsuleSphere (:4354,
+// capsule first): sphere centre c0 (radius rs) against the capsule's axis
+// segment (dDistPointToSegment :384; Tc 3x4, radius rc, height h).  One
+// record: SPHERE_SPHERE on a cap (tail: centre B, radius A, radius B; centre
+// A at [10..12]) or SPHERE_PIPE / PIPE_SPHERE (sphere centre at [10..12];
+// tail: pipe closest point, pipe fixed point, pipe direction, sphere radius,
+// pipe radius).
+__device__ __noinline__ int deviceSphereCapsule(const double* c0, double rs, const double* Tc, double rc, double h,
+                                                bool sphereFirst, double clip, int body1, int body2, double* out) {
+  double ua[3], ub[3], v[3], d[3];
+  for (int i = 0; i < 3; i++) {
+    ua[i] = Tc[4 * i + 2] * (-(h / 2)) + Tc[4 * i + 3];
+    ub[i] = Tc[4 * i + 2] * (h / 2) + Tc[4 * i + 3];
+    v[i] = ub[i] - ua[i];
+  }
+  const double c1 = (c0[0] - ua[0]) * v[0] + (c0[1] - ua[1]) * v[1] + (c0[2] - ua[2]) * v[2];
+  const double c2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+  double alpha;
+  if (c1 <= 0) {
+    alpha = 0;
+    for (int i = 0; i < 3; i++) d[i] = c0[i] - ua[i];
+  } else if (c2 <= c1) {
+    alpha = 1;
+    for (int i = 0; i < 3; i++) d[i] = c0[i] - ub[i];
+  } else {
+    alpha = c1 / c2;
+    for (int i = 0; i < 3; i++) d[i] = c0[i] - (ua[i] + alpha * v[i]);
+  }
+  const double dist = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+  const double r0 = sphereFirst ? rs : rc, r1 = sphereFirst ? rc : rs;
+  if (!(dist < r0 + r1)) return 0;
+  const double rsum = r0 + r1, w0 = r0 / rsum, w1 = r1 / rsum;
+  const double depth = rsum - dist;
+  if (depth > clip) return 0;
+  double cl[3], n[3];
+  for (int i = 0; i < 3; i++) cl[i] = ua[i] + v[i] * alpha;
+  const double* p1 = sphereFirst ? c0 : cl;
+  const double* p2 = sphereFirst ? cl : c0;
+  for (int i = 0; i < 3; i++) { out[i] = p1[i] * w1 + p2[i] * w0; n[i] = p1[i] - p2[i]; }
+  const double nn = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+  for (int i = 0; i < 3; i++) out[3 + i] = nn > 0 ? n[i] / nn : n[i];
+  out[6] = depth; out[8] = body1; out[9] = body2;
+  const double rA = w0 * rsum, rB = w1 * rsum;
+  if (fabs(alpha) < 1e-8 || fabs(1 - alpha) < 1e-8) {
+    out[7] = CT_SPHERE_SPHERE;
+    for (int i = 0; i < 3; i++) { out[10 + i] = p1[i]; out[CREC + i] = p2[i]; }
+    out[CREC + 3] = rA;
+    out[CREC + 4] = rB;
+  } else {
+    out[7] = sphereFirst ? CT_SPHERE_PIPE : CT_PIPE_SPHERE;
+    const double vn = sqrt(c2);
+    for (int i = 0; i < 3; i++) {
+      out[10 + i] = c0[i];
+      out[CREC + i] = cl[i];
+      out[CREC + 3 + i] = ua[i];
+      out[CREC + 6 + i] = vn > 0 ? v[i] / vn : v[i];
+    }
+    out[CREC + 9] = sphereFirst ? rA : rB;   // sphere radius
+    out[CREC + 10] = sphereFirst ? rB : rA;  // pipe radius
+  }
   return 1;
 }
 

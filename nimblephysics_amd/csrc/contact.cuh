@@ -483,6 +483,12 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
           cnt = deviceSphereBox(T2, md.shapeSize[sj], c1, md.shapeSize[si][0], false, md.clipDepth, bi, bj, sj, out);
         else if (ti == NIMBLE_SHAPE_BOX && tj == NIMBLE_SHAPE_SPHERE)
           cnt = deviceSphereBox(T1, md.shapeSize[si], c2, md.shapeSize[sj][0], true, md.clipDepth, bi, bj, si, out);
+        else if (ti == NIMBLE_SHAPE_SPHERE && tj == NIMBLE_SHAPE_CAPSULE)
+          cnt = deviceSphereCapsule(c1, md.shapeSize[si][0], T2, md.shapeSize[sj][0], md.shapeSize[sj][1], true,
+                                    md.clipDepth, bi, bj, out);
+        else if (ti == NIMBLE_SHAPE_CAPSULE && tj == NIMBLE_SHAPE_SPHERE)
+          cnt = deviceSphereCapsule(c2, md.shapeSize[sj][0], T1, md.shapeSize[si][0], md.shapeSize[si][1], false,
+                                    md.clipDepth, bi, bj, out);
         else
           cnt = -1;
       } else {
@@ -561,7 +567,7 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
             const int idx = nk0 + __popcll(km & below);
             if (idx < NIMBLE_MAX_CONTACTS) {
               dst = ct + CT_CONTACTS + idx * CREC;
-              if (((int)rec[7] & 15) == CT_EDGE_EDGE || ((int)rec[7] & 15) == CT_SPHERE_SPHERE)
+              if (((int)rec[7] & 15) == CT_EDGE_EDGE || ((int)rec[7] & 15) >= CT_SPHERE_SPHERE)
                 for (int i = 0; i < EDGE_REC; i++) snapEdge[idx * EDGE_REC + i] = rec[CREC + i];
             }
           } else if (drop) {
@@ -606,7 +612,7 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
           double* dst = nullptr;
           if (keep) {
             if (nk < NIMBLE_MAX_CONTACTS) {
-              if (((int)rec[7] & 15) == CT_EDGE_EDGE || ((int)rec[7] & 15) == CT_SPHERE_SPHERE)
+              if (((int)rec[7] & 15) == CT_EDGE_EDGE || ((int)rec[7] & 15) >= CT_SPHERE_SPHERE)
                 for (int i = 0; i < EDGE_REC; i++) snapEdge[nk * EDGE_REC + i] = rec[CREC + i];
               dst = ct + CT_CONTACTS + (nk++) * CREC;
             } else {
@@ -1819,6 +1825,80 @@ __device__ double sphereSphereRowTerm(const ModelDev& md, const BwdPool& P, int 
   return v;
 }
 
+// SPHERE_PIPE / PIPE_SPHERE rows: SPHERE_TO_PIPE (DifferentiableContactConstraint.cpp
+// :484 point, :819 normal) moves the point with the sphere centre, its
+// off-axis part weighted by the pipe radius; PIPE_TO_SPHERE (:496, :837) with
+// the axis point closest to the sphere centre (math::closestPointOnLineGradient,
+// Geometry.cpp:4427) weighted by the sphere radius.  E = pipe closest point,
+// pipe fixed point, pipe direction, sphere radius, pipe radius.
+__device__ double spherePipeRowTerm(const ModelDev& md, const BwdPool& P, int j, const double* rec,
+                                    const double* rr, const double* E, const double* Z, int bk, int A, int B,
+                                    int type) {
+  const bool pa = (md.anc[A] >> bk) & 1ull, pb = (md.anc[B] >> bk) & 1ull;
+  if (pa == pb) return 0.0;
+  const bool sphereSide = type == CT_SPHERE_PIPE ? pa : pb;
+  const double* nrm = rec + 3;
+  const double* sc = rec + 10;
+  const double* cl = E;
+  const double* fx = E + 3;
+  const double* dir = E + 6;
+  const double sR = E[9], pR = E[10];
+  const double wv[3] = {Z[0], Z[1], Z[2]};
+  const bool rotates = sqrt(Z[0] * Z[0] + Z[1] * Z[1] + Z[2] * Z[2]) > 1e-6;
+  auto gwt = [&](const double* x, double* o) {
+    if (rotates) { cross3(wv, x, o); for (int i = 0; i < 3; i++) o[i] += Z[3 + i]; }
+    else { for (int i = 0; i < 3; i++) o[i] = Z[3 + i]; }
+  };
+  double g[3], dp[3], dn[3];
+  if (sphereSide) {
+    gwt(sc, g);
+    const double par = dot3(dir, g);
+    const double wt = pR / (sR + pR);
+    for (int i = 0; i < 3; i++) { dp[i] = par * dir[i] + wt * (g[i] - par * dir[i]); dn[i] = g[i] - par * dir[i]; }
+  } else {
+    double fg[3], dg[3];
+    gwt(fx, fg);
+    cross3(wv, dir, dg);
+    double off = 0, dOff = 0, gOff = 0, dGOff = 0;
+    for (int i = 0; i < 3; i++) {
+      off += dir[i] * fx[i];
+      dOff += dg[i] * fx[i] + dir[i] * fg[i];
+      gOff += dir[i] * sc[i];
+      dGOff += dg[i] * sc[i];
+    }
+    const double rel = gOff - off, dRel = dGOff - dOff;
+    for (int i = 0; i < 3; i++) g[i] = fg[i] + rel * dg[i] + dRel * dir[i];
+    const double wt = sR / (sR + pR);
+    for (int i = 0; i < 3; i++) { dp[i] = wt * g[i]; dn[i] = g[i]; }
+  }
+  double dist2 = 0.0;
+  for (int i = 0; i < 3; i++) dist2 += (cl[i] - sc[i]) * (cl[i] - sc[i]);
+  const double norm = sqrt(dist2);
+  for (int i = 0; i < 3; i++) dn[i] /= norm;
+  const double dnn = dot3(dn, nrm);
+  const bool plus = sphereSide ? type == CT_SPHERE_PIPE : type == CT_PIPE_SPHERE;
+  for (int i = 0; i < 3; i++) dn[i] = (plus ? 1.0 : -1.0) * (dn[i] - dnn * nrm[i]);
+  double dd[3];
+  const int dirIdx = (int)rr[RR_DIR];
+  if (dirIdx == 0 || dot3(dn, dn) <= 1e-12) {
+    for (int i = 0; i < 3; i++) dd[i] = dn[i];
+  } else {
+    double T0[3], T1[3];
+    tangentBasisGradient(nrm, dn, T0, T1);
+    for (int i = 0; i < 3; i++) dd[i] = dirIdx == 1 ? T0[i] : T1[i];
+  }
+  const double* d = rr + RR_D;
+  const double* p = rec;
+  double pxdd[3], dpxd[3];
+  cross3(p, dd, pxdd);
+  cross3(dp, d, dpxd);
+  double v = 0.0;
+  for (int i = 0; i < 3; i++)
+    v += (P.TAB[j * 12 + i] - P.TAB[j * 12 + 6 + i]) * (pxdd[i] + dpxd[i]) +
+         (P.TAB[j * 12 + 3 + i] - P.TAB[j * 12 + 9 + i]) * dd[i];
+  return v;
+}
+
 // math::getContactPointGradient (dart/math/Geometry.cpp:1129), radii 1: the
 // derivative of the midpoint of the two edges' closest approach
 __device__ inline void edgeContactPointGradient(const double* pA, const double* dpA, const double* uA,
@@ -2054,13 +2134,15 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
     for (unsigned long long bits = liveRows; bits; bits &= bits - 1ull) {
       const int j = __ffsll((long long)bits) - 1;
       const int A = rdli(rA, j), B = rdli(rB, j), type = rdli(rTyp, j) & 15;
-      if (type == CT_SPHERE_BOX || type == CT_BOX_SPHERE || type == CT_EDGE_EDGE || type == CT_SPHERE_SPHERE) {
+      if (type >= CT_EDGE_EDGE) {
         const double* rr = rows + j * SN_ROWREC;
         const int con = rdli(rCon, j);
         const double* rec = sn + SN_CONTACTS + con * CREC;
         if (type == CT_EDGE_EDGE) acc += edgeRowTerm(md, P, j, rec, rr, sn + snEdge(n) + con * EDGE_REC, Z, bk, A, B);
         else if (type == CT_SPHERE_SPHERE)
           acc += sphereSphereRowTerm(md, P, j, rec, rr, sn + snEdge(n) + con * EDGE_REC, Z, bk, A, B);
+        else if (type == CT_SPHERE_PIPE || type == CT_PIPE_SPHERE)
+          acc += spherePipeRowTerm(md, P, j, rec, rr, sn + snEdge(n) + con * EDGE_REC, Z, bk, A, B, type);
         else acc += sphereRowTerm(md, s, L, P, j, rec, rr, Z, bk);
         continue;
       }

@@ -50,6 +50,10 @@ struct Contact {
   // SPHERE_SPHERE metadata (collision::Contact::centerA / radiusA / centerB /
   // radiusB, DARTCollide.cpp:1866); centerA is sphereCenter
   double centerB[3], radiusA, radiusB;
+  // SPHERE_PIPE / PIPE_SPHERE metadata (pipeClosestPoint / pipeFixedPoint /
+  // pipeDir / sphereRadius / pipeRadius, DARTCollide.cpp:4330, :4398);
+  // the sphere centre is sphereCenter
+  double pipeClosest[3], pipeFixed[3], pipeDir[3], sphereRadius, pipeRadius;
 };
 
 // Everything BackpropSnapshot needs (dart/neural/BackpropSnapshot.hpp and
@@ -132,6 +136,10 @@ int sphereBoxPair(const Iso<double>& Tb, const double* size, const double* c0, d
                   int shape1, int shape2, int body1, int body2, std::vector<Contact>& out);
 int sphereSphere(const double* c0, double r0, const double* c1, double r1, double clip, int shape1, int shape2,
                  int body1, int body2, std::vector<Contact>& out);
+
+// collideSphereCapsule (:4286) / collideCapsuleSphere (:4354, capsule first)
+int sphereCapsule(const double* c0, double rs, const Iso<double>& Tc, double rc, double h, bool sphereFirst,
+                  double clip, int shape1, int shape2, int body1, int body2, std::vector<Contact>& out);
 
 // dense helpers
 void cholSolve(const double* A, const double* b, double* x, int n);

@@ -31,7 +31,8 @@ void codSolve(const double* A, int m, int n, const double* b, double* x);
 bool pgsSolveLCP(int n, double* A, double* x, double* b, double* lo, double* hi, const int* findex);
 
 static const double kInf = std::numeric_limits<double>::infinity();
-enum { CT_FACE_VERTEX = 1, CT_VERTEX_FACE = 2, CT_EDGE_EDGE = 3, CT_SPHERE_SPHERE = 6 };
+enum { CT_FACE_VERTEX = 1, CT_VERTEX_FACE = 2, CT_EDGE_EDGE = 3, CT_SPHERE_SPHERE = 6, CT_SPHERE_PIPE = 7,
+       CT_PIPE_SPHERE = 8 };
 
 //------------------------------------------------------------------------------
 // dBoxBox restatement.  R? are 3x3 row-major world rotations, p? centres,
@@ -357,6 +358,69 @@ int sphereSphere(const double* c0, double r0, const double* c1, double r1, doubl
   return 1;
 }
 
+// Sphere (centre c0, radius rs) against a capsule (radius rc, height h along
+// the local z of Tc): dDistPointToSegment (DARTCollide.cpp:384) to the
+// capsule's axis segment, SPHERE_SPHERE when the closest point is a segment
+// end (alpha within 1e-8 of 0 or 1), else SPHERE_PIPE / PIPE_SPHERE.
+int sphereCapsule(const double* c0, double rs, const Iso<double>& Tc, double rc, double h, bool sphereFirst,
+                  double clip, int shape1, int shape2, int body1, int body2, std::vector<Contact>& out) {
+  double ua[3], ub[3], v[3], wv[3];
+  for (int i = 0; i < 3; i++) {
+    ua[i] = Tc.R.m[3 * i + 2] * (-(h / 2)) + Tc.p[i];
+    ub[i] = Tc.R.m[3 * i + 2] * (h / 2) + Tc.p[i];
+  }
+  for (int i = 0; i < 3; i++) { v[i] = ub[i] - ua[i]; wv[i] = c0[i] - ua[i]; }
+  auto nrm3 = [](const double* a) { return std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]); };
+  double alpha, dist, d[3];
+  const double c1 = wv[0] * v[0] + wv[1] * v[1] + wv[2] * v[2];
+  const double c2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+  if (c1 <= 0) {
+    alpha = 0;
+    for (int i = 0; i < 3; i++) d[i] = c0[i] - ua[i];
+  } else if (c2 <= c1) {
+    alpha = 1;
+    for (int i = 0; i < 3; i++) d[i] = c0[i] - ub[i];
+  } else {
+    alpha = c1 / c2;
+    for (int i = 0; i < 3; i++) d[i] = c0[i] - (ua[i] + alpha * v[i]);
+  }
+  dist = nrm3(d);
+  const double r0 = sphereFirst ? rs : rc, r1 = sphereFirst ? rc : rs;  // object 1 / object 2
+  if (!(dist < r0 + r1)) return 0;
+  double cl[3];
+  for (int i = 0; i < 3; i++) cl[i] = ua[i] + v[i] * alpha;
+  const double rsum = r0 + r1, w0 = r0 / rsum, w1 = r1 / rsum;
+  Contact c{};
+  c.depth = rsum - dist;
+  if (c.depth > clip) return 0;
+  const double* p1 = sphereFirst ? c0 : cl;  // object 1's centre / closest point
+  const double* p2 = sphereFirst ? cl : c0;
+  double n[3];
+  for (int i = 0; i < 3; i++) { c.point[i] = p1[i] * w1 + p2[i] * w0; n[i] = p1[i] - p2[i]; }
+  const double nn = nrm3(n);
+  for (int i = 0; i < 3; i++) c.normal[i] = nn > 0 ? n[i] / nn : n[i];  // Eigen normalized()
+  c.radiusA = w0 * rsum;
+  c.radiusB = w1 * rsum;
+  if (std::fabs(alpha) < 1e-8 || std::fabs(1 - alpha) < 1e-8) {
+    c.type = CT_SPHERE_SPHERE;
+    for (int i = 0; i < 3; i++) { c.sphereCenter[i] = p1[i]; c.centerB[i] = p2[i]; }
+  } else {
+    c.type = sphereFirst ? CT_SPHERE_PIPE : CT_PIPE_SPHERE;
+    c.sphereRadius = sphereFirst ? c.radiusA : c.radiusB;
+    c.pipeRadius = sphereFirst ? c.radiusB : c.radiusA;
+    const double vn = nrm3(v);
+    for (int i = 0; i < 3; i++) {
+      c.sphereCenter[i] = c0[i];
+      c.pipeClosest[i] = cl[i];
+      c.pipeFixed[i] = ua[i];
+      c.pipeDir[i] = vn > 0 ? v[i] / vn : v[i];
+    }
+  }
+  c.shapeA = shape1; c.shapeB = shape2; c.bodyA = body1; c.bodyB = body2;
+  out.push_back(c);
+  return 1;
+}
+
 void collide(const World& w, const Kin<double>& k, std::vector<Contact>& out, int* unsupported) {
   out.clear();
   int unsup = 0;
@@ -390,6 +454,11 @@ void collide(const World& w, const Kin<double>& k, std::vector<Contact>& out, in
         sphereBoxPair(T1, S1.size, T2.p.x, S2.size[0], true, w.clipDepth, i, j, S1.body, S2.body, pair);
       } else if (S1.type == NIMBLE_SHAPE_SPHERE && S2.type == NIMBLE_SHAPE_SPHERE) {
         sphereSphere(T1.p.x, S1.size[0], T2.p.x, S2.size[0], w.clipDepth, i, j, S1.body, S2.body, pair);
+      } else if (S1.type == NIMBLE_SHAPE_SPHERE && S2.type == NIMBLE_SHAPE_CAPSULE) {
+        sphereCapsule(T1.p.x, S1.size[0], T2, S2.size[0], S2.size[1], true, w.clipDepth, i, j, S1.body, S2.body, pair);
+      } else if (S1.type == NIMBLE_SHAPE_CAPSULE && S2.type == NIMBLE_SHAPE_SPHERE) {
+        sphereCapsule(T2.p.x, S2.size[0], T1, S1.size[0], S1.size[1], false, w.clipDepth, i, j, S1.body, S2.body,
+                      pair);
       } else {
         std::fprintf(stderr, "oracle: shape pair (%d,%d) not supported\n", S1.type, S2.type);
         std::abort();

@@ -26,7 +26,8 @@ namespace oracle {
 void codSolve(const double* A, int m, int n, const double* b, double* x);
 
 using Mat = std::vector<double>;
-enum { CT_FACE_VERTEX = 1, CT_VERTEX_FACE = 2, CT_EDGE_EDGE = 3, CT_SPHERE_BOX = 4, CT_BOX_SPHERE = 5, CT_SPHERE_SPHERE = 6 };
+enum { CT_FACE_VERTEX = 1, CT_VERTEX_FACE = 2, CT_EDGE_EDGE = 3, CT_SPHERE_BOX = 4, CT_BOX_SPHERE = 5, CT_SPHERE_SPHERE = 6,
+       CT_SPHERE_PIPE = 7, CT_PIPE_SPHERE = 8 };
 
 static void cross3(const double* a, const double* b, double* o) {
   o[0] = a[1] * b[2] - a[2] * b[1];
@@ -163,6 +164,8 @@ static void constraintForcesJacobian(const World& w, const Kin<double>& k, const
     if (pa || pb) {
       if (c.type == CT_EDGE_EDGE) type = pa ? 5 : 6;  // EDGE_A / EDGE_B
       else if (c.type == CT_SPHERE_SPHERE) type = pa ? 7 : 8;  // SPHERE_A / SPHERE_B
+      else if (c.type == CT_SPHERE_PIPE) type = pa ? 9 : 10;  // SPHERE_TO_PIPE / PIPE_TO_SPHERE
+      else if (c.type == CT_PIPE_SPHERE) type = pa ? 10 : 9;
       else if (c.type == CT_SPHERE_BOX) type = pa ? 3 : 4;
       else if (c.type == CT_BOX_SPHERE) type = pa ? 4 : 3;
       else if (c.type == CT_VERTEX_FACE) type = pa ? 1 : 2;
@@ -241,6 +244,48 @@ static void constraintForcesJacobian(const World& w, const Kin<double>& k, const
       for (int i = 0; i < 3; i++) dn[i] = g[i] / norm;
       const double dnn = dn[0] * c.normal[0] + dn[1] * c.normal[1] + dn[2] * c.normal[2];
       for (int i = 0; i < 3; i++) dn[i] = (A ? 1.0 : -1.0) * (dn[i] - dnn * c.normal[i]);
+      if (dirIdx == 0 || dn[0] * dn[0] + dn[1] * dn[1] + dn[2] * dn[2] <= 1e-12) {
+        for (int i = 0; i < 3; i++) dd[i] = dn[i];
+      } else {
+        double T0[3], T1[3];
+        tangentBasisGradient(c.normal, dn, T0, T1);
+        for (int i = 0; i < 3; i++) dd[i] = dirIdx == 1 ? T0[i] : T1[i];
+      }
+    } else if (type == 9 || type == 10) {
+      // SPHERE_TO_PIPE (:484 point, :819 normal): the sphere centre's motion,
+      // its off-axis part weighted by the pipe radius; PIPE_TO_SPHERE (:496,
+      // :837): the motion of the axis point closest to the sphere centre
+      // (math::closestPointOnLineGradient, Geometry.cpp:4427)
+      const double* dir = c.pipeDir;
+      double g[3], dn[3];
+      if (type == 9) {
+        gwt(c.sphereCenter, g);
+        const double par = dir[0] * g[0] + dir[1] * g[1] + dir[2] * g[2];
+        const double wt = c.pipeRadius / (c.sphereRadius + c.pipeRadius);
+        for (int i = 0; i < 3; i++) { dp[i] = par * dir[i] + wt * (g[i] - par * dir[i]); dn[i] = g[i] - par * dir[i]; }
+      } else {
+        double fg[3], dg[3];
+        gwt(c.pipeFixed, fg);
+        cross3(wv, dir, dg);  // gradientWrtThetaPureRotation
+        double off = 0, dOff = 0, gOff = 0, dGOff = 0;
+        for (int i = 0; i < 3; i++) {
+          off += dir[i] * c.pipeFixed[i];
+          dOff += dg[i] * c.pipeFixed[i] + dir[i] * fg[i];
+          gOff += dir[i] * c.sphereCenter[i];
+          dGOff += dg[i] * c.sphereCenter[i];
+        }
+        const double rel = gOff - off, dRel = dGOff - dOff;
+        for (int i = 0; i < 3; i++) g[i] = fg[i] + rel * dg[i] + dRel * dir[i];
+        const double wt = c.sphereRadius / (c.sphereRadius + c.pipeRadius);
+        for (int i = 0; i < 3; i++) { dp[i] = wt * g[i]; dn[i] = g[i]; }
+      }
+      double dist2 = 0;
+      for (int i = 0; i < 3; i++) dist2 += (c.pipeClosest[i] - c.sphereCenter[i]) * (c.pipeClosest[i] - c.sphereCenter[i]);
+      const double norm = std::sqrt(dist2);
+      for (int i = 0; i < 3; i++) dn[i] /= norm;
+      const double dnn = dn[0] * c.normal[0] + dn[1] * c.normal[1] + dn[2] * c.normal[2];
+      const bool plus = type == 9 ? c.type == CT_SPHERE_PIPE : c.type == CT_PIPE_SPHERE;
+      for (int i = 0; i < 3; i++) dn[i] = (plus ? 1.0 : -1.0) * (dn[i] - dnn * c.normal[i]);
       if (dirIdx == 0 || dn[0] * dn[0] + dn[1] * dn[1] + dn[2] * dn[2] <= 1e-12) {
         for (int i = 0; i < 3; i++) dd[i] = dn[i];
       } else {

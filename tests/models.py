@@ -345,3 +345,75 @@ def sphere_states(batch, seed=0):
         v[b, 9:12] += -0.1 * u - [0, 0.1, 0]
     f = 0.3 * rng.standard_normal((batch, 12))
     return np.concatenate([q, v], axis=1), f
+
+
+CAPSULE_BAR = (0.05, 0.4)  # radius, height
+BALL_RADIUS = 0.08
+
+
+def sphere_capsule_world(sphere_first=True):
+    """A free ball pressed onto a free horizontal capsule bar (no ground):
+    collideSphereCapsule (DARTCollide.cpp:4286) when the ball is first in
+    detector order, collideCapsuleSphere (:4354) otherwise -- SPHERE_PIPE /
+    PIPE_SPHERE contacts on the bar's cylinder, SPHERE_SPHERE on its caps."""
+    from nimblephysics_amd import dynamics as D
+    w = nimble.World()
+    w.setGravity([0, -9.81, 0])
+
+    def ball():
+        sk = D.Skeleton("ball")
+        _, b = sk.createFreeJointAndBodyNodePair()
+        b.setMass(0.7)
+        b.setMomentOfInertia(0.002, 0.002, 0.002)
+        b.createShapeNode(D.SphereShape(BALL_RADIUS), collision=True)
+        w.addSkeleton(sk)
+
+    if sphere_first:
+        ball()
+    bar = D.Skeleton("bar")
+    _, bb = bar.createFreeJointAndBodyNodePair()
+    bb.setMass(1.2)
+    bb.setMomentOfInertia(0.02, 0.02, 0.004)
+    bb.createShapeNode(D.CapsuleShape(*CAPSULE_BAR), collision=True)
+    w.addSkeleton(bar)
+    if not sphere_first:
+        ball()
+    return w
+
+
+def sphere_capsule_states(batch, seed=0, sphere_first=True, cap=False):
+    """Bar axis near the world x axis; ball 0.5-3 mm into the bar, over its
+    cylinder (or, cap=True, beyond one end, on the cap), closing at 0.1 m/s."""
+    rng = np.random.default_rng(seed)
+    rc, h = CAPSULE_BAR
+    st = np.zeros((batch, 24))
+    f = 0.3 * rng.standard_normal((batch, 12))
+    ib, ic = (0, 6) if sphere_first else (6, 0)  # ball / bar dof offsets
+    for b in range(batch):
+        k = np.array([0.0, 1.0, 0.0]) * (0.5 * np.pi) + 0.1 * rng.standard_normal(3)
+        th = np.linalg.norm(k)
+        kk = k / th
+        K = np.array([[0, -kk[2], kk[1]], [kk[2], 0, -kk[0]], [-kk[1], kk[0], 0]])
+        R = np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
+        axis = R[:, 2]
+        pc = 0.05 * rng.standard_normal(3)
+        st[b, ic:ic + 3] = k
+        st[b, ic + 3:ic + 6] = pc
+        dist = rc + BALL_RADIUS - rng.uniform(5e-4, 3e-3)
+        if cap:
+            end = pc + axis * (h / 2) * rng.choice([-1.0, 1.0])
+            u = np.sign(np.dot(end - pc, axis)) * axis + 0.8 * np.array([0, 1.0, 0]) + 0.2 * rng.standard_normal(3)
+            u /= np.linalg.norm(u)
+            cb = end + dist * u
+        else:
+            s = rng.uniform(-0.35, 0.35) * h
+            u = np.array([0, 1.0, 0]) + 0.4 * rng.standard_normal(3)
+            u -= np.dot(u, axis) * axis
+            u /= np.linalg.norm(u)
+            cb = pc + s * axis + dist * u
+        st[b, ib:ib + 3] = 0.3 * rng.standard_normal(3)
+        st[b, ib + 3:ib + 6] = cb
+        st[b, 12:] = 0.05 * rng.standard_normal(12)
+        st[b, 12 + ib + 3:12 + ib + 6] += -0.1 * u
+        st[b, 12 + ic + 3:12 + ic + 6] += 0.05 * u
+    return st, f

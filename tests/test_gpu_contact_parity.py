@@ -294,3 +294,19 @@ def test_sphere_contact_parity(ground_first):
     types = np.sort(snap[:, SN_CONTACTS + 7 + CREC * np.arange(3)].astype(int) & 15, axis=1)
     want = [5, 5, 6] if ground_first else [4, 4, 6]
     assert (types == want).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sphere_first", [True, False])
+def test_sphere_capsule_contact_parity(sphere_first):
+    """collideSphereCapsule / collideCapsuleSphere: a ball pressed onto a
+    free capsule bar, over its cylinder (SPHERE_PIPE / PIPE_SPHERE) and on
+    its caps (SPHERE_SPHERE), forward and gradients."""
+    world = models.sphere_capsule_world(sphere_first)
+    sp, fp = models.sphere_capsule_states(48, seed=7, sphere_first=sphere_first)
+    sc, fc = models.sphere_capsule_states(16, seed=8, sphere_first=sphere_first, cap=True)
+    st, f = np.concatenate([sp, sc]), np.concatenate([fp, fc])
+    ow, snap = _parity(world, st, f)
+    assert (snap[:, SN_NCON] == 1).all()
+    types = snap[:, SN_CONTACTS + 7].astype(int) & 15
+    assert (types[:48] == (7 if sphere_first else 8)).all() and (types[48:] == 6).all()

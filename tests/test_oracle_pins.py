@@ -233,3 +233,25 @@ def test_sphere_contact_gradients_vs_finite_differences(oracle_built, ground_fir
     gs, gf, fd_s, fd_f = _fd_check(w, st, f, g)
     assert np.abs(gs - fd_s).max() <= 1e-6 * np.abs(fd_s).max()
     assert np.abs(gf - fd_f).max() <= 1e-6 * np.abs(fd_f).max()
+
+
+@pytest.mark.parametrize("sphere_first", [True, False])
+@pytest.mark.parametrize("cap", [False, True])
+def test_sphere_capsule_gradients_vs_finite_differences(oracle_built, sphere_first, cap):
+    """collideSphereCapsule / collideCapsuleSphere: the SPHERE_PIPE /
+    PIPE_SPHERE contact (SPHERE_TO_PIPE and PIPE_TO_SPHERE terms) on the
+    bar's cylinder and the SPHERE_SPHERE contact on its cap, against central
+    differences of the oracle's step."""
+    w = models.sphere_capsule_world(sphere_first)
+    st, f = models.sphere_capsule_states(1, seed=6, sphere_first=sphere_first, cap=cap)
+    st, f = st[0], f[0]
+    o = O.OracleWorld(w)
+    o.forward(st[None], f[None])
+    cs = O.contacts(o, 0)
+    assert len(cs) == 1
+    assert int(cs[0, 7]) == (6 if cap else (7 if sphere_first else 8))
+    assert O.lcp_flags(o, 0)[3] > 0  # clamping rows
+    g = np.random.default_rng(8).standard_normal(24)
+    gs, gf, fd_s, fd_f = _fd_check(w, st, f, g)
+    assert np.abs(gs - fd_s).max() <= 1e-6 * np.abs(fd_s).max()
+    assert np.abs(gf - fd_f).max() <= 1e-6 * np.abs(fd_f).max()

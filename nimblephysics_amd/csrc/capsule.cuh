@@ -27,6 +27,7 @@
 #define CT_SPHERE_SPHERE 6
 #define CT_SPHERE_PIPE 7
 #define CT_PIPE_SPHERE 8
+#define CT_PIPE_PIPE 9
 
 namespace cap {
 
@@ -512,6 +513,98 @@ __device__ __noinline__ int deviceSphereCapsule(const double* c0, double rs, con
     }
     out[CREC + 9] = sphereFirst ? rA : rB;   // sphere radius
     out[CREC + 10] = sphereFirst ? rB : rA;  // pipe radius
+  }
+  return 1;
+}
+
+// collideCapsuleCapsule (DARTCollide.cpp:4183), T0 / T1 3x4.  One record:
+// SPHERE_SPHERE / SPHERE_PIPE / PIPE_SPHERE tails as deviceSphereCapsule, or
+// PIPE_PIPE: [10] radius A / rsum, [11] closest-point distance, [12] radius
+// B / rsum; tail: edge A fixed point, edge A dir, edge B fixed point, edge B
+// dir.
+__device__ __noinline__ int deviceCapsuleCapsule(const double* T0, double r0, double h0, const double* T1, double r1,
+                                                 double h1, double clip, int body1, int body2, double* out) {
+  double pa[3], pb[3], ua[3], ub[3];
+  for (int i = 0; i < 3; i++) {
+    pa[i] = T0[4 * i + 2] * (-(h0 / 2)) + T0[4 * i + 3];
+    pb[i] = T0[4 * i + 2] * (h0 / 2) + T0[4 * i + 3];
+    ua[i] = T1[4 * i + 2] * (-(h1 / 2)) + T1[4 * i + 3];
+    ub[i] = T1[4 * i + 2] * (h1 / 2) + T1[4 * i + 3];
+  }
+  // dSegmentsClosestApproach (DARTCollide.cpp:301)
+  double u[3], v[3], w[3];
+  for (int i = 0; i < 3; i++) { u[i] = pb[i] - pa[i]; v[i] = ub[i] - ua[i]; w[i] = pa[i] - ua[i]; }
+  const double a = u[0] * u[0] + u[1] * u[1] + u[2] * u[2], b = u[0] * v[0] + u[1] * v[1] + u[2] * v[2];
+  const double c = v[0] * v[0] + v[1] * v[1] + v[2] * v[2], d = u[0] * w[0] + u[1] * w[1] + u[2] * w[2];
+  const double e = v[0] * w[0] + v[1] * w[1] + v[2] * w[2];
+  const double D = a * c - b * b;
+  double sN, sD = D, tN, tD = D;
+  if (D < 1e-15) {
+    sN = 0.0; sD = 1.0; tN = e; tD = c;
+  } else {
+    sN = b * e - c * d;
+    tN = a * e - b * d;
+    if (sN < 0.0) { sN = 0.0; tN = e; tD = c; }
+    else if (sN > sD) { sN = sD; tN = e + b; tD = c; }
+  }
+  if (tN < 0.0) {
+    tN = 0.0;
+    if (-d < 0.0) sN = 0.0;
+    else if (-d > a) sN = sD;
+    else { sN = -d; sD = a; }
+  } else if (tN > tD) {
+    tN = tD;
+    if ((-d + b) < 0.0) sN = 0;
+    else if ((-d + b) > a) sN = sD;
+    else { sN = -d + b; sD = a; }
+  }
+  double alpha = fabs(sN) < 1e-15 ? 0.0 : sN / sD;
+  double beta = fabs(tN) < 1e-15 ? 0.0 : tN / tD;
+  if (alpha < 0) alpha = 0;
+  if (alpha > 1) alpha = 1;
+  if (beta < 0) beta = 0;
+  if (beta > 1) beta = 1;
+  double c0[3], c1[3], dd[3];
+  for (int i = 0; i < 3; i++) { c0[i] = pa[i] + u[i] * alpha; c1[i] = ua[i] + v[i] * beta; dd[i] = c0[i] - c1[i]; }
+  const double dist = sqrt(dd[0] * dd[0] + dd[1] * dd[1] + dd[2] * dd[2]);
+  const double rsum = r0 + r1;
+  if (!(dist <= rsum)) return 0;
+  const double w0 = r0 / rsum, w1 = r1 / rsum;
+  const double depth = rsum - dist;
+  if (depth > clip) return 0;
+  const bool s0 = fabs(alpha) < 1e-8 || fabs(1 - alpha) < 1e-8, s1 = fabs(beta) < 1e-8 || fabs(1 - beta) < 1e-8;
+  const double un = sqrt(a), vn = sqrt(c);
+  double point[3], nrm[3], dirA[3], dirB[3];
+  for (int i = 0; i < 3; i++) {
+    point[i] = c0[i] * w1 + c1[i] * w0;
+    nrm[i] = dist > 0 ? dd[i] / dist : dd[i];
+    dirA[i] = un > 0 ? u[i] / un : u[i];
+    dirB[i] = vn > 0 ? v[i] / vn : v[i];
+  }
+  for (int i = 0; i < 3; i++) { out[i] = point[i]; out[3 + i] = nrm[i]; }
+  out[6] = depth; out[8] = body1; out[9] = body2;
+  if (s0 && s1) {
+    out[7] = CT_SPHERE_SPHERE;
+    for (int i = 0; i < 3; i++) { out[10 + i] = c0[i]; out[CREC + i] = c1[i]; }
+    out[CREC + 3] = w0 * rsum;
+    out[CREC + 4] = w1 * rsum;
+  } else if (s0 || s1) {
+    out[7] = s0 ? CT_SPHERE_PIPE : CT_PIPE_SPHERE;
+    for (int i = 0; i < 3; i++) {
+      out[10 + i] = s0 ? c0[i] : c1[i];
+      out[CREC + i] = s0 ? c1[i] : c0[i];
+      out[CREC + 3 + i] = s0 ? ua[i] : pa[i];
+      out[CREC + 6 + i] = s0 ? dirB[i] : dirA[i];
+    }
+    out[CREC + 9] = s0 ? w0 * rsum : w1 * rsum;
+    out[CREC + 10] = s0 ? w1 * rsum : w0 * rsum;
+  } else {
+    out[7] = CT_PIPE_PIPE;
+    out[10] = w0; out[11] = dist; out[12] = w1;
+    for (int i = 0; i < 3; i++) {
+      out[CREC + i] = pa[i]; out[CREC + 3 + i] = dirA[i];
+      out[CREC + 6 + i] = ua[i]; out[CREC + 9 + i] = dirB[i];
+    }
   }
   return 1;
 }

@@ -470,6 +470,12 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
         cnt = deviceCapsuleBox(Tb, md.shapeSize[sb], Tc, md.shapeSize[sc][0], md.shapeSize[sc][1], boxFirst,
                                md.clipDepth, bi, bj, sb, pairbuf + lane * 8 * PBREC, &unsup);
         if (unsup) cnt = -1 - cnt;  // flagged; the contacts found are still kept
+      } else if (md.shapeType[si] == NIMBLE_SHAPE_CAPSULE && md.shapeType[sj] == NIMBLE_SHAPE_CAPSULE) {
+        double T1[12], T2[12];
+        tmul(s + L.Tw + 12 * bi, md.shapeT[si], T1);
+        tmul(s + L.Tw + 12 * bj, md.shapeT[sj], T2);
+        cnt = deviceCapsuleCapsule(T1, md.shapeSize[si][0], md.shapeSize[si][1], T2, md.shapeSize[sj][0],
+                                   md.shapeSize[sj][1], md.clipDepth, bi, bj, pairbuf + lane * 8 * PBREC);
       } else if (md.shapeType[si] == NIMBLE_SHAPE_SPHERE || md.shapeType[sj] == NIMBLE_SHAPE_SPHERE) {
         const int ti = md.shapeType[si], tj = md.shapeType[sj];
         double T1[12], T2[12];
@@ -1903,7 +1909,7 @@ __device__ double spherePipeRowTerm(const ModelDev& md, const BwdPool& P, int j,
 // derivative of the midpoint of the two edges' closest approach
 __device__ inline void edgeContactPointGradient(const double* pA, const double* dpA, const double* uA,
                                                 const double* duA, const double* pB, const double* dpB,
-                                                const double* uB, const double* duB, double* out) {
+                                                const double* uB, const double* duB, double* out, double rA = 1.0, double rB = 1.0) {
   double p[3], d_p[3];
   for (int i = 0; i < 3; i++) { p[i] = pB[i] - pA[i]; d_p[i] = dpB[i] - dpA[i]; }
   const double uaub = dot3(uA, uB);
@@ -1915,7 +1921,7 @@ __device__ inline void edgeContactPointGradient(const double* pA, const double* 
   const double d = 1 - uaub * uaub;
   const double d_d = -2 * d_uaub * uaub;
   if (d <= 0) {
-    for (int i = 0; i < 3; i++) out[i] = (dpA[i] * 1.0 + dpB[i] * 1.0) / 2.0;
+    for (int i = 0; i < 3; i++) out[i] = (dpA[i] * rB + dpB[i] * rA) / (rA + rB);
     return;
   }
   const double e = 1.0 / d;
@@ -1925,8 +1931,66 @@ __device__ inline void edgeContactPointGradient(const double* pA, const double* 
   const double beta = (uaub * q1 + q2) * e;
   const double d_beta = (uaub * q1 + q2) * d_e + (d_uaub * q1 + uaub * d_q1 + d_q2) * e;
   for (int i = 0; i < 3; i++)
-    out[i] = ((dpA[i] + alpha * duA[i] + d_alpha * uA[i]) * 1.0 + (dpB[i] + beta * duB[i] + d_beta * uB[i]) * 1.0) /
-             2.0;
+    out[i] = ((dpA[i] + alpha * duA[i] + d_alpha * uA[i]) * rB + (dpB[i] + beta * duB[i] + d_beta * uB[i]) * rA) /
+             (rA + rB);
+}
+
+// PIPE_PIPE rows (PIPE_A / PIPE_B of DifferentiableContactConstraint.cpp:510 /
+// :529 and :862 / :901): getContactPointGradient of the moving axis with the
+// contact's normalised radii for the point, and the two closest points'
+// gradients (radii 0/1, 1/0) over their distance for the normal.
+// E = edge A fixed point, edge A dir, edge B fixed point, edge B dir; the
+// record holds radius A / rsum, the distance, radius B / rsum at [10..12].
+__device__ double pipePipeRowTerm(const ModelDev& md, const BwdPool& P, int j, const double* rec, const double* rr,
+                                  const double* E, const double* Z, int bk, int A, int B) {
+  const bool pa = (md.anc[A] >> bk) & 1ull, pb = (md.anc[B] >> bk) & 1ull;
+  if (pa == pb) return 0.0;
+  const double* nrm = rec + 3;
+  const double* aF = E;
+  const double* aD = E + 3;
+  const double* bF = E + 6;
+  const double* bD = E + 9;
+  const double wv[3] = {Z[0], Z[1], Z[2]};
+  double fg[3], dg[3];
+  const double* x = pa ? aF : bF;
+  if (sqrt(Z[0] * Z[0] + Z[1] * Z[1] + Z[2] * Z[2]) > 1e-6) {
+    cross3(wv, x, fg);
+    for (int i = 0; i < 3; i++) fg[i] += Z[3 + i];
+  } else {
+    for (int i = 0; i < 3; i++) fg[i] = Z[3 + i];
+  }
+  cross3(wv, pa ? aD : bD, dg);
+  const double zero[3] = {0, 0, 0};
+  const double* dpA = pa ? fg : zero;
+  const double* duA = pa ? dg : zero;
+  const double* dpB = pa ? zero : fg;
+  const double* duB = pa ? zero : dg;
+  double dp[3], ca[3], cb[3], dn[3];
+  edgeContactPointGradient(aF, dpA, aD, duA, bF, dpB, bD, duB, dp, rec[10], rec[12]);
+  edgeContactPointGradient(aF, dpA, aD, duA, bF, dpB, bD, duB, ca, 0.0, 1.0);
+  edgeContactPointGradient(aF, dpA, aD, duA, bF, dpB, bD, duB, cb, 1.0, 0.0);
+  for (int i = 0; i < 3; i++) dn[i] = (ca[i] - cb[i]) / rec[11];
+  const double dnn = dot3(dn, nrm);
+  for (int i = 0; i < 3; i++) dn[i] -= dnn * nrm[i];
+  double dd[3];
+  const int dirIdx = (int)rr[RR_DIR];
+  if (dirIdx == 0 || dot3(dn, dn) <= 1e-12) {
+    for (int i = 0; i < 3; i++) dd[i] = dn[i];
+  } else {
+    double T0[3], T1[3];
+    tangentBasisGradient(nrm, dn, T0, T1);
+    for (int i = 0; i < 3; i++) dd[i] = dirIdx == 1 ? T0[i] : T1[i];
+  }
+  const double* d = rr + RR_D;
+  const double* p = rec;
+  double pxdd[3], dpxd[3];
+  cross3(p, dd, pxdd);
+  cross3(dp, d, dpxd);
+  double v = 0.0;
+  for (int i = 0; i < 3; i++)
+    v += (P.TAB[j * 12 + i] - P.TAB[j * 12 + 6 + i]) * (pxdd[i] + dpxd[i]) +
+         (P.TAB[j * 12 + 3 + i] - P.TAB[j * 12 + 9 + i]) * dd[i];
+  return v;
 }
 
 // G-term of an EDGE_EDGE row for direction k (position generator Z) when
@@ -2141,6 +2205,8 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
         if (type == CT_EDGE_EDGE) acc += edgeRowTerm(md, P, j, rec, rr, sn + snEdge(n) + con * EDGE_REC, Z, bk, A, B);
         else if (type == CT_SPHERE_SPHERE)
           acc += sphereSphereRowTerm(md, P, j, rec, rr, sn + snEdge(n) + con * EDGE_REC, Z, bk, A, B);
+        else if (type == CT_PIPE_PIPE)
+          acc += pipePipeRowTerm(md, P, j, rec, rr, sn + snEdge(n) + con * EDGE_REC, Z, bk, A, B);
         else if (type == CT_SPHERE_PIPE || type == CT_PIPE_SPHERE)
           acc += spherePipeRowTerm(md, P, j, rec, rr, sn + snEdge(n) + con * EDGE_REC, Z, bk, A, B, type);
         else acc += sphereRowTerm(md, s, L, P, j, rec, rr, Z, bk);

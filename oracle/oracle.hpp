@@ -54,6 +54,10 @@ struct Contact {
   // pipeDir / sphereRadius / pipeRadius, DARTCollide.cpp:4330, :4398);
   // the sphere centre is sphereCenter
   double pipeClosest[3], pipeFixed[3], pipeDir[3], sphereRadius, pipeRadius;
+  // PIPE_PIPE: edgeA/B fixed point and direction above, plus the closest
+  // points (edgeAClosestPoint / edgeBClosestPoint, DARTCollide.cpp:4270);
+  // radiusA / radiusB hold the normalised radii there, as in the reference
+  double edgeAClosest[3], edgeBClosest[3];
 };
 
 // Everything BackpropSnapshot needs (dart/neural/BackpropSnapshot.hpp and
@@ -140,6 +144,10 @@ int sphereSphere(const double* c0, double r0, const double* c1, double r1, doubl
 // collideSphereCapsule (:4286) / collideCapsuleSphere (:4354, capsule first)
 int sphereCapsule(const double* c0, double rs, const Iso<double>& Tc, double rc, double h, bool sphereFirst,
                   double clip, int shape1, int shape2, int body1, int body2, std::vector<Contact>& out);
+
+// collideCapsuleCapsule (:4183)
+int capsuleCapsule(const Iso<double>& T0, double r0, double h0, const Iso<double>& T1, double r1, double h1,
+                   double clip, int shape1, int shape2, int body1, int body2, std::vector<Contact>& out);
 
 // dense helpers
 void cholSolve(const double* A, const double* b, double* x, int n);

@@ -32,7 +32,7 @@ bool pgsSolveLCP(int n, double* A, double* x, double* b, double* lo, double* hi,
 
 static const double kInf = std::numeric_limits<double>::infinity();
 enum { CT_FACE_VERTEX = 1, CT_VERTEX_FACE = 2, CT_EDGE_EDGE = 3, CT_SPHERE_SPHERE = 6, CT_SPHERE_PIPE = 7,
-       CT_PIPE_SPHERE = 8 };
+       CT_PIPE_SPHERE = 8, CT_PIPE_PIPE = 9 };
 
 //------------------------------------------------------------------------------
 // dBoxBox restatement.  R? are 3x3 row-major world rotations, p? centres,
@@ -421,6 +421,102 @@ int sphereCapsule(const double* c0, double rs, const Iso<double>& Tc, double rc,
   return 1;
 }
 
+// collideCapsuleCapsule (DARTCollide.cpp:4183): closest approach of the two
+// axis segments; SPHERE_SPHERE / SPHERE_PIPE / PIPE_SPHERE when a closest
+// point is a segment end (within 1e-8), else PIPE_PIPE
+int capsuleCapsule(const Iso<double>& T0, double r0, double h0, const Iso<double>& T1, double r1, double h1,
+                   double clip, int shape1, int shape2, int body1, int body2, std::vector<Contact>& out) {
+  using std::sqrt;
+  using std::fabs;
+  double pa[3], pb[3], ua[3], ub[3];
+  for (int i = 0; i < 3; i++) {
+    pa[i] = T0.R.m[3 * i + 2] * (-(h0 / 2)) + T0.p[i];
+    pb[i] = T0.R.m[3 * i + 2] * (h0 / 2) + T0.p[i];
+    ua[i] = T1.R.m[3 * i + 2] * (-(h1 / 2)) + T1.p[i];
+    ub[i] = T1.R.m[3 * i + 2] * (h1 / 2) + T1.p[i];
+  }
+  // dSegmentsClosestApproach (DARTCollide.cpp:301)
+  double u[3], v[3], w[3];
+  for (int i = 0; i < 3; i++) { u[i] = pb[i] - pa[i]; v[i] = ub[i] - ua[i]; w[i] = pa[i] - ua[i]; }
+  const double a = u[0] * u[0] + u[1] * u[1] + u[2] * u[2], b = u[0] * v[0] + u[1] * v[1] + u[2] * v[2];
+  const double c = v[0] * v[0] + v[1] * v[1] + v[2] * v[2], d = u[0] * w[0] + u[1] * w[1] + u[2] * w[2];
+  const double e = v[0] * w[0] + v[1] * w[1] + v[2] * w[2];
+  const double D = a * c - b * b;
+  double sN, sD = D, tN, tD = D;
+  if (D < 1e-15) {
+    sN = 0.0; sD = 1.0; tN = e; tD = c;
+  } else {
+    sN = b * e - c * d;
+    tN = a * e - b * d;
+    if (sN < 0.0) { sN = 0.0; tN = e; tD = c; }
+    else if (sN > sD) { sN = sD; tN = e + b; tD = c; }
+  }
+  if (tN < 0.0) {
+    tN = 0.0;
+    if (-d < 0.0) sN = 0.0;
+    else if (-d > a) sN = sD;
+    else { sN = -d; sD = a; }
+  } else if (tN > tD) {
+    tN = tD;
+    if ((-d + b) < 0.0) sN = 0;
+    else if ((-d + b) > a) sN = sD;
+    else { sN = -d + b; sD = a; }
+  }
+  double alpha = fabs(sN) < 1e-15 ? 0.0 : sN / sD;
+  double beta = fabs(tN) < 1e-15 ? 0.0 : tN / tD;
+  if (alpha < 0) alpha = 0;
+  if (alpha > 1) alpha = 1;
+  if (beta < 0) beta = 0;
+  if (beta > 1) beta = 1;
+  double c0[3], c1[3], dd[3];
+  for (int i = 0; i < 3; i++) { c0[i] = pa[i] + u[i] * alpha; c1[i] = ua[i] + v[i] * beta; dd[i] = c0[i] - c1[i]; }
+  const double dist = sqrt(dd[0] * dd[0] + dd[1] * dd[1] + dd[2] * dd[2]);
+  const double rsum = r0 + r1;
+  if (!(dist <= rsum)) return 0;
+  const double w0 = r0 / rsum, w1 = r1 / rsum;
+  const double depth = rsum - dist;
+  if (depth > clip) return 0;
+  const bool s0 = fabs(alpha) < 1e-8 || fabs(1 - alpha) < 1e-8, s1 = fabs(beta) < 1e-8 || fabs(1 - beta) < 1e-8;
+  const double un = sqrt(a), vn = sqrt(c);
+  double point[3], nrm[3], dirA[3], dirB[3];
+  for (int i = 0; i < 3; i++) {
+    point[i] = c0[i] * w1 + c1[i] * w0;
+    nrm[i] = dist > 0 ? dd[i] / dist : dd[i];
+    dirA[i] = un > 0 ? u[i] / un : u[i];
+    dirB[i] = vn > 0 ? v[i] / vn : v[i];
+  }
+  Contact ct{};
+  ct.depth = depth;
+  for (int i = 0; i < 3; i++) { ct.point[i] = point[i]; ct.normal[i] = nrm[i]; }
+  ct.radiusA = w0 * rsum;
+  ct.radiusB = w1 * rsum;
+  if (s0 && s1) {
+    ct.type = CT_SPHERE_SPHERE;
+    for (int i = 0; i < 3; i++) { ct.sphereCenter[i] = c0[i]; ct.centerB[i] = c1[i]; }
+  } else if (s0 || s1) {
+    ct.type = s0 ? CT_SPHERE_PIPE : CT_PIPE_SPHERE;
+    ct.sphereRadius = s0 ? w0 * rsum : w1 * rsum;
+    ct.pipeRadius = s0 ? w1 * rsum : w0 * rsum;
+    for (int i = 0; i < 3; i++) {
+      ct.sphereCenter[i] = s0 ? c0[i] : c1[i];
+      ct.pipeClosest[i] = s0 ? c1[i] : c0[i];
+      ct.pipeFixed[i] = s0 ? ua[i] : pa[i];
+      ct.pipeDir[i] = s0 ? dirB[i] : dirA[i];
+    }
+  } else {
+    ct.type = CT_PIPE_PIPE;
+    ct.radiusA = w0;
+    ct.radiusB = w1;
+    for (int i = 0; i < 3; i++) {
+      ct.edgeAFixed[i] = pa[i]; ct.edgeAClosest[i] = c0[i]; ct.edgeADir[i] = dirA[i];
+      ct.edgeBFixed[i] = ua[i]; ct.edgeBClosest[i] = c1[i]; ct.edgeBDir[i] = dirB[i];
+    }
+  }
+  ct.shapeA = shape1; ct.shapeB = shape2; ct.bodyA = body1; ct.bodyB = body2;
+  out.push_back(ct);
+  return 1;
+}
+
 void collide(const World& w, const Kin<double>& k, std::vector<Contact>& out, int* unsupported) {
   out.clear();
   int unsup = 0;
@@ -459,6 +555,9 @@ void collide(const World& w, const Kin<double>& k, std::vector<Contact>& out, in
       } else if (S1.type == NIMBLE_SHAPE_CAPSULE && S2.type == NIMBLE_SHAPE_SPHERE) {
         sphereCapsule(T2.p.x, S2.size[0], T1, S1.size[0], S1.size[1], false, w.clipDepth, i, j, S1.body, S2.body,
                       pair);
+      } else if (S1.type == NIMBLE_SHAPE_CAPSULE && S2.type == NIMBLE_SHAPE_CAPSULE) {
+        capsuleCapsule(T1, S1.size[0], S1.size[1], T2, S2.size[0], S2.size[1], w.clipDepth, i, j, S1.body, S2.body,
+                       pair);
       } else {
         std::fprintf(stderr, "oracle: shape pair (%d,%d) not supported\n", S1.type, S2.type);
         std::abort();

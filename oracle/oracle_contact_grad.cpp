@@ -27,7 +27,7 @@ void codSolve(const double* A, int m, int n, const double* b, double* x);
 
 using Mat = std::vector<double>;
 enum { CT_FACE_VERTEX = 1, CT_VERTEX_FACE = 2, CT_EDGE_EDGE = 3, CT_SPHERE_BOX = 4, CT_BOX_SPHERE = 5, CT_SPHERE_SPHERE = 6,
-       CT_SPHERE_PIPE = 7, CT_PIPE_SPHERE = 8 };
+       CT_SPHERE_PIPE = 7, CT_PIPE_SPHERE = 8, CT_PIPE_PIPE = 9 };
 
 static void cross3(const double* a, const double* b, double* o) {
   o[0] = a[1] * b[2] - a[2] * b[1];
@@ -114,7 +114,7 @@ static void tangentBasisGradient(const double* n, const double* g, double* T0, d
 // derivative of the midpoint of the edges' closest approach
 static void contactPointGradient(const double* pA, const double* dpA, const double* uA, const double* duA,
                                  const double* pB, const double* dpB, const double* uB, const double* duB,
-                                 double* out) {
+                                 double* out, double rA = 1.0, double rB = 1.0) {
   double p[3], d_p[3];
   for (int i = 0; i < 3; i++) { p[i] = pB[i] - pA[i]; d_p[i] = dpB[i] - dpA[i]; }
   auto dot = [](const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; };
@@ -127,7 +127,7 @@ static void contactPointGradient(const double* pA, const double* dpA, const doub
   const double d = 1 - uaub * uaub;
   const double d_d = -2 * d_uaub * uaub;
   if (d <= 0) {
-    for (int i = 0; i < 3; i++) out[i] = (dpA[i] * 1.0 + dpB[i] * 1.0) / 2.0;
+    for (int i = 0; i < 3; i++) out[i] = (dpA[i] * rB + dpB[i] * rA) / (rA + rB);
     return;
   }
   const double e = 1.0 / d;
@@ -137,8 +137,8 @@ static void contactPointGradient(const double* pA, const double* dpA, const doub
   const double beta = (uaub * q1 + q2) * e;
   const double d_beta = (uaub * q1 + q2) * d_e + (d_uaub * q1 + uaub * d_q1 + d_q2) * e;
   for (int i = 0; i < 3; i++)
-    out[i] = ((dpA[i] + alpha * duA[i] + d_alpha * uA[i]) * 1.0 + (dpB[i] + beta * duB[i] + d_beta * uB[i]) * 1.0) /
-             2.0;
+    out[i] = ((dpA[i] + alpha * duA[i] + d_alpha * uA[i]) * rB + (dpB[i] + beta * duB[i] + d_beta * uB[i]) * rA) /
+             (rA + rB);
 }
 
 // G_i = d(J^T e_i)/dq  (n x n) for constraint row i
@@ -166,6 +166,7 @@ static void constraintForcesJacobian(const World& w, const Kin<double>& k, const
       else if (c.type == CT_SPHERE_SPHERE) type = pa ? 7 : 8;  // SPHERE_A / SPHERE_B
       else if (c.type == CT_SPHERE_PIPE) type = pa ? 9 : 10;  // SPHERE_TO_PIPE / PIPE_TO_SPHERE
       else if (c.type == CT_PIPE_SPHERE) type = pa ? 10 : 9;
+      else if (c.type == CT_PIPE_PIPE) type = pa ? 11 : 12;  // PIPE_A / PIPE_B
       else if (c.type == CT_SPHERE_BOX) type = pa ? 3 : 4;
       else if (c.type == CT_BOX_SPHERE) type = pa ? 4 : 3;
       else if (c.type == CT_VERTEX_FACE) type = pa ? 1 : 2;
@@ -286,6 +287,34 @@ static void constraintForcesJacobian(const World& w, const Kin<double>& k, const
       const double dnn = dn[0] * c.normal[0] + dn[1] * c.normal[1] + dn[2] * c.normal[2];
       const bool plus = type == 9 ? c.type == CT_SPHERE_PIPE : c.type == CT_PIPE_SPHERE;
       for (int i = 0; i < 3; i++) dn[i] = (plus ? 1.0 : -1.0) * (dn[i] - dnn * c.normal[i]);
+      if (dirIdx == 0 || dn[0] * dn[0] + dn[1] * dn[1] + dn[2] * dn[2] <= 1e-12) {
+        for (int i = 0; i < 3; i++) dd[i] = dn[i];
+      } else {
+        double T0[3], T1[3];
+        tangentBasisGradient(c.normal, dn, T0, T1);
+        for (int i = 0; i < 3; i++) dd[i] = dirIdx == 1 ? T0[i] : T1[i];
+      }
+    } else if (type == 11 || type == 12) {
+      // PIPE_A / PIPE_B (:510 / :529 point, :862 / :901 normal): the moving
+      // axis's fixed point and direction through math::getContactPointGradient
+      // with the contact's (normalised) radii; the normal from the two
+      // closest points' gradients (radii 0/1 and 1/0) over their distance
+      const bool A = type == 11;
+      double fg[3], dg[3], zero[3] = {0, 0, 0}, ca[3], cb[3], dn[3];
+      gwt(A ? c.edgeAFixed : c.edgeBFixed, fg);
+      cross3(wv, A ? c.edgeADir : c.edgeBDir, dg);
+      const double* dpA = A ? fg : zero; const double* duA = A ? dg : zero;
+      const double* dpB = A ? zero : fg; const double* duB = A ? zero : dg;
+      contactPointGradient(c.edgeAFixed, dpA, c.edgeADir, duA, c.edgeBFixed, dpB, c.edgeBDir, duB, dp, c.radiusA,
+                           c.radiusB);
+      contactPointGradient(c.edgeAFixed, dpA, c.edgeADir, duA, c.edgeBFixed, dpB, c.edgeBDir, duB, ca, 0.0, 1.0);
+      contactPointGradient(c.edgeAFixed, dpA, c.edgeADir, duA, c.edgeBFixed, dpB, c.edgeBDir, duB, cb, 1.0, 0.0);
+      double dist2 = 0;
+      for (int i = 0; i < 3; i++) dist2 += (c.edgeAClosest[i] - c.edgeBClosest[i]) * (c.edgeAClosest[i] - c.edgeBClosest[i]);
+      const double norm = std::sqrt(dist2);
+      for (int i = 0; i < 3; i++) dn[i] = (ca[i] - cb[i]) / norm;
+      const double dnn = dn[0] * c.normal[0] + dn[1] * c.normal[1] + dn[2] * c.normal[2];
+      for (int i = 0; i < 3; i++) dn[i] -= dnn * c.normal[i];
       if (dirIdx == 0 || dn[0] * dn[0] + dn[1] * dn[1] + dn[2] * dn[2] <= 1e-12) {
         for (int i = 0; i < 3; i++) dd[i] = dn[i];
       } else {

@@ -417,3 +417,45 @@ def sphere_capsule_states(batch, seed=0, sphere_first=True, cap=False):
         st[b, 12 + ib + 3:12 + ib + 6] += -0.1 * u
         st[b, 12 + ic + 3:12 + ic + 6] += 0.05 * u
     return st, f
+
+
+def capsule_pair_world():
+    """Two free capsule bars (separate skeletons, no ground):
+    collideCapsuleCapsule (DARTCollide.cpp:4183)."""
+    from nimblephysics_amd import dynamics as D
+    w = nimble.World()
+    w.setGravity([0, -9.81, 0])
+    for i, (r, h) in enumerate([CAPSULE_BAR, (0.04, 0.3)]):
+        sk = D.Skeleton(f"bar{i}")
+        _, b = sk.createFreeJointAndBodyNodePair()
+        b.setMass(1.0 + 0.5 * i)
+        b.setMomentOfInertia(0.02, 0.02, 0.004)
+        b.createShapeNode(D.CapsuleShape(r, h), collision=True)
+        w.addSkeleton(sk)
+    return w
+
+
+def capsule_pair_states(batch, seed=0, mode="cross"):
+    """Bar 0 along ~x; bar 1 either crossing above it along ~z (PIPE_PIPE)
+    or standing on it end-first along ~y (PIPE_SPHERE), 0.5-3 mm deep,
+    closing at 0.1 m/s."""
+    rng = np.random.default_rng(seed)
+    (r0, h0), (r1, h1) = CAPSULE_BAR, (0.04, 0.3)
+    st = np.zeros((batch, 24))
+    f = 0.3 * rng.standard_normal((batch, 12))
+    for b in range(batch):
+        k0 = np.array([0.0, 0.5 * np.pi, 0.0]) + 0.05 * rng.standard_normal(3)
+        p0 = 0.03 * rng.standard_normal(3)
+        st[b, 0:3], st[b, 3:6] = k0, p0
+        pen = rng.uniform(5e-4, 3e-3)
+        off = rng.uniform(-0.3, 0.3) * h0
+        if mode == "cross":
+            k1 = 0.05 * rng.standard_normal(3)  # axis ~z
+            p1 = p0 + np.array([off, r0 + r1 - pen, 0.0])
+        else:
+            k1 = np.array([-0.5 * np.pi, 0.0, 0.0]) + 0.05 * rng.standard_normal(3)  # axis ~y
+            p1 = p0 + np.array([off, r0 + r1 + h1 / 2 - pen, 0.0])
+        st[b, 6:9], st[b, 9:12] = k1, p1
+        st[b, 12:] = 0.05 * rng.standard_normal(12)
+        st[b, 12 + 10] -= 0.1 if mode == "cross" else 0.4
+    return st, f

@@ -310,3 +310,17 @@ def test_sphere_capsule_contact_parity(sphere_first):
     assert (snap[:, SN_NCON] == 1).all()
     types = snap[:, SN_CONTACTS + 7].astype(int) & 15
     assert (types[:48] == (7 if sphere_first else 8)).all() and (types[48:] == 6).all()
+
+
+@pytest.mark.gpu
+def test_capsule_capsule_contact_parity():
+    """collideCapsuleCapsule: crossing bars (PIPE_PIPE) and a bar standing on
+    another (PIPE_SPHERE), forward and gradients."""
+    world = models.capsule_pair_world()
+    sx, fx = models.capsule_pair_states(40, seed=11, mode="cross")
+    se, fe = models.capsule_pair_states(24, seed=12, mode="end")
+    ow, snap = _parity(world, np.concatenate([sx, se]), np.concatenate([fx, fe]))
+    ncon = snap[:, SN_NCON]
+    assert (ncon <= 1).all() and (ncon[:40] == 1).sum() >= 30 and (ncon[40:] == 1).sum() >= 12
+    types = snap[:, SN_CONTACTS + 7].astype(int) & 15
+    assert (types[:40][ncon[:40] == 1] == 9).all() and (types[40:][ncon[40:] == 1] == 8).all()

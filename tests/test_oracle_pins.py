@@ -255,3 +255,26 @@ def test_sphere_capsule_gradients_vs_finite_differences(oracle_built, sphere_fir
     gs, gf, fd_s, fd_f = _fd_check(w, st, f, g)
     assert np.abs(gs - fd_s).max() <= 1e-6 * np.abs(fd_s).max()
     assert np.abs(gf - fd_f).max() <= 1e-6 * np.abs(fd_f).max()
+
+
+@pytest.mark.parametrize("mode", ["cross", "end"])
+def test_capsule_capsule_gradients_vs_finite_differences(oracle_built, mode):
+    """collideCapsuleCapsule: PIPE_PIPE (PIPE_A / PIPE_B terms through
+    getContactPointGradient with the contact radii) for crossing bars and
+    PIPE_SPHERE for a bar standing on another, against central differences
+    of the oracle's step."""
+    w = models.capsule_pair_world()
+    for seed in range(9, 40):  # first deterministic case whose contact clamps
+        st, f = models.capsule_pair_states(1, seed=seed, mode=mode)
+        st, f = st[0], f[0]
+        o = O.OracleWorld(w)
+        o.forward(st[None], f[None])
+        if O.lcp_flags(o, 0)[3] > 0:
+            break
+    cs = O.contacts(o, 0)
+    assert len(cs) == 1 and int(cs[0, 7]) == (9 if mode == "cross" else 8)
+    assert O.lcp_flags(o, 0)[3] > 0
+    g = np.random.default_rng(10).standard_normal(24)
+    gs, gf, fd_s, fd_f = _fd_check(w, st, f, g)
+    assert np.abs(gs - fd_s).max() <= 1e-6 * np.abs(fd_s).max()
+    assert np.abs(gf - fd_f).max() <= 1e-6 * np.abs(fd_f).max()

@@ -165,34 +165,66 @@ def contact_stats(world, state, action):
 
 def pmc_traffic(workload, kernel, batch):
     """HBM bytes per launch of `kernel` from the committed PMC summary
-    (profiles/pmc_traffic.json: per-world FETCH_SIZE x2 (gfx950 correction)
-    + WRITE_SIZE, measured by tools/pmc_traffic.py); None when absent."""
+    (profiles/pmc_traffic.json: per-world FETCH_SIZE + WRITE_SIZE of the same
+    kernel on the same workload, measured by tools/pmc_traffic.py under
+    rocprofv3 --pmc -- counters cannot be read inside this process); None when
+    absent.  Returned with the summary's provenance."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
-        return None
+        return None, None
     try:
         d = json.load(open(path))
-        return float(d[workload][kernel]["bytes_per_world"]) * batch
+        e = d[workload][kernel]
+        return float(e["bytes_per_world"]) * batch, e.get("source", "profiles/pmc_traffic.json")
     except Exception:
-        return None
+        return None, None
 
 
-def cpu_baseline(world, batch, sampler, seconds_target=12.0):
-    """Oracle (CPU restatement, 1 thread) on a bounded sample of the same workload."""
+def _cpu_threads():
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    # the GPU box's CPU share is 16 cores per GPU (os.cpu_count() shows the
+    # whole machine there)
+    return max(1, min(n, 16))
+
+
+def cpu_baseline(make, batch, sampler, seconds_target=12.0):
+    """The oracle (the CPU restatement of the reference's step, `kind`
+    "port") on every usable host core: one thread per core, each stepping its
+    own `batch` worlds of the same workload fwd+bwd in a rollout for
+    ~seconds_target (ctypes releases the GIL inside the C library)."""
+    import threading
     from oracle.oracle import OracleWorld
-    o = OracleWorld(world)
-    st, f = sampler(world, batch, 11)
-    g = np.random.default_rng(5).standard_normal(st.shape)
-    steps = 0
+    threads = _cpu_threads()
+    counts = [0] * threads
+    stop = [False]
+
+    def worker(t):
+        world = make()
+        o = OracleWorld(world)
+        st, f = sampler(world, batch, 11 + t)
+        g = np.random.default_rng(5 + t).standard_normal(st.shape)
+        while not stop[0]:
+            nxt = o.forward(st, f)
+            o.backward(g)
+            st = nxt
+            counts[t] += 1
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds_target:
-        nxt = o.forward(st, f)
-        o.backward(g)
-        st = nxt
-        steps += 1
+    for th in ths:
+        th.start()
+    time.sleep(seconds_target)
+    stop[0] = True
+    for th in ths:
+        th.join()
     dt = time.perf_counter() - t0
-    return {"value": steps * batch / dt, "unit": "timesteps/s", "cores": 1, "kind": "port",
-            "sample": f"{steps} fwd+bwd steps x {batch} worlds of the same workload, oracle/liboracle.so, 1 thread, {dt:.1f}s"}
+    steps = sum(counts)
+    return {"value": steps * batch / dt, "unit": "timesteps/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} fwd+bwd steps x {batch} worlds of the same workload, oracle/liboracle.so "
+                      f"(CPU restatement of the reference's step), {threads} threads, {dt:.1f}s"}
 
 
 def main():
@@ -248,6 +280,7 @@ def main():
     dom = "backward" if bwd_ms >= fwd_ms else "forward"
     dom_ms = max(bwd_ms, fwd_ms)
     achieved = flops[dom] * args.batch / (dom_ms * 1e-3) / 1e12
+    traffic, traffic_src = pmc_traffic(args.workload, f"nimble_{dom}_kernel", args.batch)
     if rank == 0:
         out = {
             "metric": metric,
@@ -262,14 +295,16 @@ def main():
                        "clamping_rows_per_world": cstats["clamping"],
                        "worlds_in_contact": cstats["worlds_in_contact"]},
             "kernels_ms": {"forward": fwd_ms, "backward": bwd_ms},
-            "roofline": {"bound": "mfma", "kernel": f"nimble_{dom}_kernel", "achieved": achieved,
+            "roofline": {"bound": "fp64-valu", "kernel": f"nimble_{dom}_kernel", "achieved": achieved,
                          "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP64_VECTOR_PEAK_TFLOPS,
-                         "traffic": pmc_traffic(args.workload, f"nimble_{dom}_kernel", args.batch),
+                         "traffic": traffic, "traffic_source": traffic_src,
                          "flops_per_world": flops[dom],
-                         "note": "fp64 VALU-bound (no fp64 MFMA use); peak = fp64 vector rate"},
+                         "note": "peak = MI355X fp64 vector (VALU) rate; the kernel issues no MFMA "
+                                 "(DESIGN.md: fp64 MFMA measured, rejected); traffic = HBM bytes per launch "
+                                 "from the committed rocprofv3 PMC summary of this kernel"},
         }
         if not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(make(), 64, sampler)
+            out["cpu_baseline"] = cpu_baseline(make, 16, sampler)
         print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()

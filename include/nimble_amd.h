@@ -127,6 +127,24 @@ int nimble_world_destroy(nimble_world_t world);
 int64_t nimble_snapshot_doubles(nimble_world_t world);
 int64_t nimble_lcp_cache_doubles(nimble_world_t world);
 
+/* Candidate collision shape pairs of the model (DARTCollisionDetector::collide
+ * object pairs after BodyNodeCollisionFilter, DARTCollisionDetector.cpp:127,
+ * CollisionFilter.cpp:105).  0 means the model has no contact stage and its
+ * snapshots carry no contact header. */
+int32_t nimble_num_collision_pairs(nimble_world_t world);
+
+/* Per-world status word, snapshot element NIMBLE_SNAPSHOT_STATUS after
+ * nimble_forward (models with collision pairs).  The first three bits mean the
+ * world's contact set did not fit this path and its step differs from the
+ * reference's World::step; the host layer raises on them. */
+#define NIMBLE_SNAPSHOT_STATUS 5
+#define NIMBLE_STATUS_CONTACT_OVERFLOW 1  /* > NIMBLE_MAX_CONTACTS contacts     */
+#define NIMBLE_STATUS_UNSUPPORTED_SHAPE 2 /* shape pair without a collider     */
+#define NIMBLE_STATUS_DROPPED_OVERFLOW 4  /* dropped-contact dedup list full   */
+#define NIMBLE_STATUS_LCP_REDUCED 8       /* LCPUtils::reduce merged duplicate
+                                             columns (reference behaviour,
+                                             LCPUtils.cpp:144; informational) */
+
 /*
  * Batched differentiable forward step == neural::forwardPass + World::step
  * on each of `batch` worlds.

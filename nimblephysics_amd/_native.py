@@ -39,6 +39,8 @@ def lib():
         L.nimble_backward.restype = C.c_int
         L.nimble_last_error.argtypes = []
         L.nimble_last_error.restype = C.c_char_p
+        L.nimble_num_collision_pairs.argtypes = [C.c_void_p]
+        L.nimble_num_collision_pairs.restype = C.c_int32
         _lib = L
     return _lib
 
@@ -60,19 +62,44 @@ def _require_device(*tensors):
             raise TypeError("nimblephysics_amd computes in float64 (the reference's s_t); got " + str(t.dtype))
 
 
-class DeviceWorld:
-    """A world model uploaded to the device (nimble_world_create)."""
+# snapshot header (csrc/pool_sizes.h) and status bits (csrc/contact.cuh)
+SN_NCON, SN_M, SN_NC, SN_NU, SN_CFM, SN_STATUS = 0, 1, 2, 3, 4, 5
+ST_CONTACT_OVERFLOW, ST_UNSUPPORTED_SHAPE, ST_DROPPED_OVERFLOW, ST_REDUCED = 1, 2, 4, 8
+ST_DIVERGES = ST_CONTACT_OVERFLOW | ST_UNSUPPORTED_SHAPE | ST_DROPPED_OVERFLOW
 
-    def __init__(self, world):
+
+class ContactCapacityError(RuntimeError):
+    """A world's contact set does not fit the batched path (more contacts than
+    NIMBLE_MAX_CONTACTS, a shape pair without a collider, or an overflowing
+    dropped-contact list): its step would differ from the reference's."""
+
+
+def status_message(bits: int) -> str:
+    why = []
+    if bits & ST_CONTACT_OVERFLOW:
+        why.append("more contacts than NIMBLE_MAX_CONTACTS")
+    if bits & ST_UNSUPPORTED_SHAPE:
+        why.append("a shape pair without a collider on this path")
+    if bits & ST_DROPPED_OVERFLOW:
+        why.append("dropped-contact list overflow")
+    return ", ".join(why)
+
+
+class DeviceWorld:
+    """A world model uploaded to one device (nimble_world_create)."""
+
+    def __init__(self, world, device_index: int = 0):
         L = lib()
         desc, keep = world.desc()
         self._keep = keep
         h = C.c_void_p()
         _check(L.nimble_world_create(C.byref(desc), C.byref(h)))
         self.h = h
+        self.device_index = int(device_index)
         self.n = world.getNumDofs()
         self.snapshot_doubles = int(L.nimble_snapshot_doubles(h))
         self.cache_doubles = int(L.nimble_lcp_cache_doubles(h))
+        self.num_pairs = int(L.nimble_num_collision_pairs(h))
 
     def close(self):
         if self.h:
@@ -85,15 +112,48 @@ class DeviceWorld:
         except Exception:
             pass
 
+    def _on_my_device(self, *tensors):
+        for t in tensors:
+            if t is not None and t.device.index != self.device_index:
+                raise RuntimeError(f"tensor on {t.device}, world model uploaded to cuda:{self.device_index}")
+
+    def _shapes(self, B, state=None, forces=None, snapshot=None, cache=None):
+        n = self.n
+        if state is not None and tuple(state.shape) != (B, 2 * n):
+            raise ValueError(f"state shape {tuple(state.shape)} != ({B}, {2 * n})")
+        if forces is not None and tuple(forces.shape) != (B, n):
+            raise ValueError(f"forces shape {tuple(forces.shape)} != ({B}, {n})")
+        if snapshot is not None and (snapshot.shape[0] < B or snapshot.shape[1] != self.snapshot_doubles):
+            raise ValueError(f"snapshot shape {tuple(snapshot.shape)}: this world needs [{B}, {self.snapshot_doubles}]")
+        if cache is not None and (cache.shape[0] < B or cache.shape[1] != self.cache_doubles):
+            raise ValueError(f"LCP cache shape {tuple(cache.shape)}: this world needs [{B}, {self.cache_doubles}]")
+        for t in (state, forces, snapshot, cache):
+            if t is not None and not t.is_contiguous():
+                raise ValueError("nimblephysics_amd buffers must be contiguous")
+
+    def status(self, snapshot):
+        """Status bits per world ([B] int32, device) of the forward that wrote
+        `snapshot`; zeros for models without collision pairs."""
+        import torch
+        if self.num_pairs == 0:
+            return torch.zeros(snapshot.shape[0], dtype=torch.int32, device=snapshot.device)
+        return snapshot[:, SN_STATUS].to(torch.int32)
+
     def forward(self, state, forces, lcp_cache, next_state, snapshot, stream_ptr: int):
         _require_device(state, forces, lcp_cache, next_state, snapshot)
         B = state.shape[0]
+        self._on_my_device(state, forces, lcp_cache, next_state, snapshot)
+        self._shapes(B, state, forces, snapshot, lcp_cache)
         _check(lib().nimble_forward(self.h, B, _ptr(state), _ptr(forces), _ptr(lcp_cache), _ptr(next_state),
                                     _ptr(snapshot), C.c_void_p(stream_ptr)))
 
     def backward(self, state, forces, snapshot, grad_next, grad_state, grad_forces, stream_ptr: int):
         _require_device(state, forces, snapshot, grad_next, grad_state, grad_forces)
         B = state.shape[0]
+        self._on_my_device(state, forces, snapshot, grad_next, grad_state, grad_forces)
+        self._shapes(B, state, forces, snapshot)
+        self._shapes(B, grad_next, grad_forces)
+        self._shapes(B, grad_state)
         _check(lib().nimble_backward(self.h, B, _ptr(state), _ptr(forces), _ptr(snapshot), _ptr(grad_next),
                                      _ptr(grad_state), _ptr(grad_forces), C.c_void_p(stream_ptr)))
 

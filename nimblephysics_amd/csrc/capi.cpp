@@ -263,6 +263,7 @@ int nimble_world_destroy(nimble_world_t w) {
 
 int64_t nimble_snapshot_doubles(nimble_world_t w) { return w ? w->snapDoubles : -1; }
 int64_t nimble_lcp_cache_doubles(nimble_world_t w) { return w ? w->cacheDoubles : -1; }
+int32_t nimble_num_collision_pairs(nimble_world_t w) { return w ? w->host.numPairs : -1; }
 
 static int gridFor(int batch) {
   // one wave per world; cap the grid so every wave loops over several worlds

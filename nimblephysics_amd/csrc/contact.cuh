@@ -411,7 +411,7 @@ __device__ __forceinline__ int helperWait(double* ct, Pred pred) {
 #define ST_CONTACT_OVERFLOW 1
 #define ST_UNSUPPORTED_SHAPE 2
 #define ST_DROPPED_OVERFLOW 4
-#define ST_DUPLICATE_COLUMNS 8
+#define ST_DUPLICATE_COLUMNS 8  // LCPUtils::reduce merged columns (reference behaviour)
 
 // row record fields
 #define RR_CONTACT 0
@@ -1201,30 +1201,34 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   const double loR = lane < m ? P.lo[lane] : 0.0;
   const int fiR = lane < m ? P.fi[lane] : -1;
   if (!success) {
-    // LCPUtils::reduce would merge near-duplicate columns; they do not occur
-    // for box contacts -- flag them in the status word if they ever do
-    {
-      bool dup = false;
-      const int al = lane >> 3, cl = lane & 7;
-      for (int a0 = 0; a0 < m; a0 += 8)
-        for (int c0 = a0; c0 < m; c0 += 8) {
-        const int a = a0 + al, c = c0 + cl;
-        if (a >= m || c >= m || c <= a) continue;
-        double dd = 0;
-        for (int i = 0; i < m; i++) dd += (P.A[i * m + a] - P.A[i * m + c]) * (P.A[i * m + a] - P.A[i * m + c]);
-        if (dd < 1e-4 && fabs(P.b[a] - P.b[c]) < 1e-4 && P.fi[a] == P.fi[c] && P.hi[a] == P.hi[c] && P.lo[a] == P.lo[c])
-          dup = true;
-        }
-      if (__ballot(dup) && lane == 0) ct[H_STATUS] = (double)((int)ct[H_STATUS] | ST_DUPLICATE_COLUMNS);
-    }
+    // Dantzig on the reduced problem (BoxedLcpConstraintSolver.cpp:466-521):
+    // LCPUtils::reduce merges near-duplicate columns; when it merges any, the
+    // reduced matrix (in M1, free here) goes to Dantzig and the solution is
+    // mapped out (x_i = x_r[rank(rep_i)]); validity on the full problem
     if (lane == 0) ct[H_CODOK] = 0;
+    double scl;
+    int rep;
+    const unsigned long long full = m >= 64 ? ~0ull : ((1ull << m) - 1ull);
+    const unsigned long long alive = waveReduce<kLds>(m, spc<kLds>(P.A), 0.0, bR, loR, hiR, fiR, lane, scl, rep);
     WSYNC();
     double xd = 0.0;
-    #ifdef NIMBLE_STAGE_TIMING
-    bool ok = waveDantzig<kLds>(m, spc<kLds>(P.A), sp<kLds>(P.M2), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane, g_stamp + 52);
+    bool ok;
+    if (alive != full) {
+      if (lane == 0) ct[H_STATUS] = (double)((int)ct[H_STATUS] | ST_DUPLICATE_COLUMNS);
+      double br = bR, lr = loR, hr = hiR;
+      int fr = fiR, act;
+      const int mr = reducedVectors(alive, rep, lane, br, lr, hr, fr, act);
+      reducedMatrix<kLds>(m, spc<kLds>(P.A), 0.0, alive, act, scl, sp<kLds>(P.M1), false, lane);
+      double xr = 0.0;
+      ok = waveDantzig<kLds>(mr, spc<kLds>(P.M1), sp<kLds>(P.M2), sp<kLds>(P.scr), xr, br, lr, hr, fr, lane);
+      xd = __shfl(xr, reducedIndex(alive, rep));
+    } else {
+#ifdef NIMBLE_STAGE_TIMING
+      ok = waveDantzig<kLds>(m, spc<kLds>(P.A), sp<kLds>(P.M2), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane, g_stamp + 52);
 #else
-    bool ok = waveDantzig<kLds>(m, spc<kLds>(P.A), sp<kLds>(P.M2), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane);
+      ok = waveDantzig<kLds>(m, spc<kLds>(P.A), sp<kLds>(P.M2), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane);
 #endif
+    }
     if (ok) {
       if (lane < m) P.X[lane] = xd;
       WSYNC();
@@ -1243,7 +1247,25 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
       cf = md.fallbackCfm;
       if (lane == 0) ct[H_CODOK] = 0;
       double xd;
-      if (tasked) {
+      // PGS on the reduced A + cfm I (BoxedLcpConstraintSolver.cpp:550-597);
+      // the helper wave's speculative PGS is the unreduced solve, used when
+      // reduce merges nothing
+      double scl;
+      int rep;
+      const unsigned long long full = m >= 64 ? ~0ull : ((1ull << m) - 1ull);
+      const unsigned long long alive = waveReduce<kLds>(m, spc<kLds>(P.A), cf, bR, loR, hiR, fiR, lane, scl, rep);
+      WSYNC();
+      if (alive != full) {
+        if (lane == 0) ct[H_STATUS] = (double)((int)ct[H_STATUS] | ST_DUPLICATE_COLUMNS);
+        double br = bR, lr = loR, hr = hiR;
+        int fr = fiR, act;
+        const int mr = reducedVectors(alive, rep, lane, br, lr, hr, fr, act);
+        reducedMatrix<kLds>(m, spc<kLds>(P.A), cf, alive, act, scl, sp<kLds>(P.M1), true, lane);
+        double xr = __shfl(lane < m ? P.xc[lane] : 0.0, lane < mr ? act : 0);
+        if (lane >= mr) xr = 0.0;
+        ok = wavePgs<kLds>(mr, spc<kLds>(P.M1), xr, br, lr, hr, fr, lane, nullptr, 0.0);
+        xd = __shfl(xr, reducedIndex(alive, rep));
+      } else if (tasked) {
         helperWait(ct, [](int st) { return st == HS_MID || st == HS_DONE; });
         xd = lane < m ? P.xh[lane] : 0.0;
         ok = uni(helperFlags(ct)[2]) != 0;

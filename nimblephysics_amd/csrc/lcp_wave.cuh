@@ -756,3 +756,122 @@ __device__ bool waveDantzig(int n, typename Space<kLds>::cdptr Ain, typename Spa
   WSYNC();
   return true;
 }
+
+// ---------------------------------------------------------------------------
+// LCPUtils::reduce (LCPUtils.cpp:144) with mergeLCPColumns (:346), without
+// moving data.  A merge of column b into column a (the first pair, in (a, b)
+// order, whose columns differ by < 1e-4 in squared norm, with |b_a - b_b| <
+// 1e-4 and equal findex / hi / lo) deletes row and column b and doubles column
+// a, so the reduced problem is always the principal submatrix of the input
+// over the surviving rows, each column j scaled by a power of two scl_j:
+//   A_r[r][s] = (A[i][j] + shift [i == j]) * scl_j,  i = act_r, j = act_s.
+// `shift` is a CFM the caller has already (virtually) added to A's diagonal
+// (the PGS fallback reduces A + cfm I).  Lane i holds original row i's b, lo,
+// hi and findex.  Returns (wave-uniform) the mask of surviving rows; lane i
+// gets scl (its column scale, 1 for a removed row) and rep (the surviving row
+// row i was merged into).  `maxMerges` = 0 only reports whether a merge
+// exists (return value != the full mask).
+// ---------------------------------------------------------------------------
+template <bool kLds>
+__device__ unsigned long long waveReduce(int m, typename Space<kLds>::cdptr Ain, double shift, double b, double lo,
+                                         double hi, int fi, int lane, double& scl, int& rep, int maxMerges = 64) {
+  m = uni(m);
+  const double* A = (const double*)Ain;
+  unsigned long long alive = m >= 64 ? ~0ull : ((1ull << m) - 1ull);
+  scl = 1.0;
+  rep = lane;
+  const int col = lane < m ? lane : 0;
+  for (int merges = 0; merges <= maxMerges; merges++) {
+    // findex in terms of surviving rows (the reference remaps fIndex on
+    // every merge; comparing representatives is the same test)
+    const int fr = __shfl(rep, fi >= 0 ? fi : 0);
+    const int frow = fi >= 0 ? fr : -1;
+    const bool me = lane < m && ((alive >> lane) & 1ull);
+    int hitC = 64;
+    for (int c = 1; c < m; c++) {
+      if (!((alive >> c) & 1ull)) continue;
+      const double bc = rdl(b, c), loc = rdl(lo, c), hic = rdl(hi, c), sc = rdl(scl, c);
+      const int fc = rdli(frow, c);
+      bool cand = me && lane < c && hitC == 64 && fabs(b - bc) < 1e-4 && frow == fc && hi == hic && lo == loc;
+      if (__ballot(cand)) {
+        double dd = 0.0;
+        for (int i = 0; i < m; i++) {
+          if (!((alive >> i) & 1ull)) continue;
+          const double aa = (A[i * m + col] + (i == lane ? shift : 0.0)) * scl;
+          const double ac = (A[i * m + c] + (i == c ? shift : 0.0)) * sc;
+          dd += (aa - ac) * (aa - ac);
+        }
+        if (cand && dd < 1e-4) hitC = c;
+      }
+    }
+    const int a = waveFirst(hitC < 64);
+    if (a < 0 || merges == maxMerges) {
+      if (a >= 0) alive &= ~(1ull << rdli(hitC, a));  // report only
+      break;
+    }
+    const int cb = rdli(hitC, a);
+    alive &= ~(1ull << cb);
+    if (lane == a) scl *= 2.0;
+    if (rep == cb) rep = a;
+  }
+  return alive;
+}
+
+// rank of original row `row` among the surviving rows (its reduced index)
+__device__ __forceinline__ int reducedIndex(unsigned long long alive, int row) {
+  return __popcll(alive & ((1ull << row) - 1ull));
+}
+
+// the reduced problem's lane-held vectors: lane r gets the values of the r-th
+// surviving row (its findex as a reduced index); returns the reduced size
+__device__ __forceinline__ int reducedVectors(unsigned long long alive, int rep, int lane, double& b, double& lo,
+                                              double& hi, int& fi, int& act) {
+  const int mr = __popcll(alive);
+  // act_r: the r-th set bit of alive
+  act = 0;
+  {
+    unsigned long long a = alive;
+    for (int r = 0; r < mr; r++) {
+      const int i = __ffsll((long long)a) - 1;
+      if (lane == r) act = i;
+      a &= a - 1ull;
+    }
+  }
+  const int src = lane < mr ? act : 0;
+  const double nb = __shfl(b, src), nlo = __shfl(lo, src), nhi = __shfl(hi, src);
+  const int nfi = __shfl(fi, src);
+  const int frep = __shfl(rep, nfi >= 0 ? nfi : 0);
+  b = lane < mr ? nb : 0.0;
+  lo = lane < mr ? nlo : 0.0;
+  hi = lane < mr ? nhi : 0.0;
+  fi = (lane < mr && nfi >= 0) ? reducedIndex(alive, frep) : -1;
+  return mr;
+}
+
+// Dantzig's view of the reduced matrix: ODE's dLCP reads only the lower
+// triangle of the (row-major) A it is given (swapRowsAndCols / GETA,
+// lcp.cpp:144, matrix.cpp:371), i.e. the symmetric S[r][s] =
+// A_r[max(r,s)][min(r,s)] = A[i][j] * scl_{act_min(r,s)}; written to M
+// (mr x mr).  PGS reads rows (PgsBoxedLcpSolver.cpp:139): its copy is the
+// transpose T[s][r] = A_r[r][s] (wavePgs reads row i, lane j as A_ji).
+template <bool kLds>
+__device__ void reducedMatrix(int m, typename Space<kLds>::cdptr Ain, double shift, unsigned long long alive,
+                              int act, double scl, typename Space<kLds>::dptr Mout, bool forPgs, int lane) {
+  m = uni(m);
+  const int mr = __popcll(alive);
+  const double* A = (const double*)Ain;
+  double* M = (double*)Mout;
+  const double sclAct = __shfl(scl, lane < mr ? act : 0);  // scale of the lane's reduced column / row
+  for (int r = 0; r < mr; r++) {
+    const int i = rdli(act, r);
+    const double si = rdl(sclAct, r);
+    if (lane < mr) {
+      const int j = act;
+      const double v = A[i * m + j] + (i == j ? shift : 0.0);
+      // forPgs: T[r][lane] = A_r[lane][r] = (A[j][i] + ...) * scl_i
+      // Dantzig: S[r][lane] = A[i][j] * scl_{act_min(r, lane)}
+      M[r * mr + lane] = forPgs ? v * si : v * (r < lane ? si : sclAct);
+    }
+  }
+  WSYNC();
+}

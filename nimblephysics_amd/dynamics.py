@@ -32,6 +32,14 @@ SHAPE_SPHERE = 1
 SHAPE_CAPSULE = 2
 
 
+def _model_changed(skel: Optional["Skeleton"]) -> None:
+    """A model parameter changed: the owning World re-uploads its device model
+    before the next step (the reference's setters take effect on the next
+    World::step, so the device copy must never go stale)."""
+    if skel is not None and skel.world is not None:
+        skel.world._touch()
+
+
 def _iso(R=None, p=None) -> np.ndarray:
     T = np.eye(4)
     if R is not None:
@@ -121,12 +129,14 @@ class ShapeNode:
 
     def setRelativeTransform(self, T):
         self.T = _as_matrix(T)
+        _model_changed(self.body.skel)
 
     def getShape(self):
         return self.shape
 
     def createCollisionAspect(self):
         self.collision = True
+        _model_changed(self.body.skel)
 
     def createVisualAspect(self):
         self.visual = True
@@ -178,42 +188,54 @@ class Joint:
     def setAxis(self, axis):
         a = np.asarray(axis, dtype=np.float64)
         self.axis = a / np.linalg.norm(a)
+        _model_changed(self.skel)
 
     def getAxis(self):
         return self.axis.copy()
 
     def setTransformFromParentBodyNode(self, T):
         self.T_parent = _as_matrix(T)
+        _model_changed(self.skel)
 
     def setTransformFromChildBodyNode(self, T):
         self.T_child = _as_matrix(T)
+        _model_changed(self.skel)
 
     def setDampingCoefficient(self, i, d):
         self.damping[i] = d
+        _model_changed(self.skel)
 
     def setSpringStiffness(self, i, k):
         self.spring[i] = k
+        _model_changed(self.skel)
 
     def setRestPosition(self, i, q0):
         self.rest[i] = q0
+        _model_changed(self.skel)
 
     def setPositionUpperLimit(self, i, v):
         self.pos_hi[i] = v
+        _model_changed(self.skel)
 
     def setPositionLowerLimit(self, i, v):
         self.pos_lo[i] = v
+        _model_changed(self.skel)
 
     def setVelocityUpperLimit(self, i, v):
         self.vel_hi[i] = v
+        _model_changed(self.skel)
 
     def setVelocityLowerLimit(self, i, v):
         self.vel_lo[i] = v
+        _model_changed(self.skel)
 
     def setControlForceUpperLimit(self, i, v):
         self.force_hi[i] = v
+        _model_changed(self.skel)
 
     def setControlForceLowerLimit(self, i, v):
         self.force_lo[i] = v
+        _model_changed(self.skel)
 
 
 class BodyNode:
@@ -241,25 +263,31 @@ class BodyNode:
 
     def setMass(self, m):
         self.mass = float(m)
+        _model_changed(self.skel)
 
     def getMass(self):
         return self.mass
 
     def setLocalCOM(self, c):
         self.com = np.asarray(c, dtype=np.float64).copy()
+        _model_changed(self.skel)
 
     def setMomentOfInertia(self, Ixx, Iyy, Izz, Ixy=0.0, Ixz=0.0, Iyz=0.0):
         self.moment = np.array([Ixx, Iyy, Izz, Ixy, Ixz, Iyz], dtype=np.float64)
+        _model_changed(self.skel)
 
     def setFrictionCoeff(self, f):
         self.friction = float(f)
+        _model_changed(self.skel)
 
     def setRestitutionCoeff(self, r):
         self.restitution = float(r)
+        _model_changed(self.skel)
 
     def createShapeNode(self, shape: Shape, collision: bool = False):
         node = ShapeNode(self, shape, collision)
         self.shape_nodes.append(node)
+        _model_changed(self.skel)
         return node
 
     def getShapeNode(self, i):
@@ -287,6 +315,7 @@ class Skeleton:
         b.index = len(self.bodies)
         self.bodies.append(b)
         self._reindex()
+        _model_changed(self)
         return j, b
 
     def createRevoluteJointAndBodyNodePair(self, parent=None, joint_name=None, body_name=None):
@@ -351,6 +380,7 @@ class Skeleton:
 
     def setMobile(self, mobile: bool):
         self.mobile = bool(mobile)
+        _model_changed(self)
 
     def isMobile(self):
         return self.mobile
@@ -394,12 +424,14 @@ class Skeleton:
         for b in self.bodies:
             j = b.joint
             j.force_hi[:] = lim[j.dof_offset:j.dof_offset + j.getNumDofs()]
+        _model_changed(self)
 
     def setControlForceLowerLimits(self, lim):
         lim = np.asarray(lim, dtype=np.float64)
         for b in self.bodies:
             j = b.joint
             j.force_lo[:] = lim[j.dof_offset:j.dof_offset + j.getNumDofs()]
+        _model_changed(self)
 
     def getControlForceUpperLimits(self):
         return self._per_dof("force_hi")

@@ -32,7 +32,7 @@ class World:
         self.action_space: Optional[List[int]] = None
         self._forces: Optional[np.ndarray] = None
         self._version = 0
-        self._native = None  # (version, handle)
+        self._native_by_dev = {}  # device index -> (version, DeviceWorld)
 
     # --- model ------------------------------------------------------------------
     def addSkeleton(self, skel: dyn.Skeleton):
@@ -283,11 +283,47 @@ class World:
     def desc(self):
         return build_desc(self.desc_arrays())
 
-    def native(self):
-        """Device-side world handle (created lazily, rebuilt when the model changes)."""
+    def native(self, device=None):
+        """Device-side world handle for `device` (a torch device or index;
+        default: the current HIP device), created lazily and rebuilt whenever
+        the model changed (World setters, and every dynamics setter through
+        ``dynamics._model_changed``).  One handle per device: the model lives
+        in that device's HBM and its kernels launch there."""
         from . import _native
-        if self._native is None or self._native[0] != self._version:
-            if self._native is not None:
-                self._native[1].close()
-            self._native = (self._version, _native.DeviceWorld(self))
-        return self._native[1]
+        import torch
+        if device is None:
+            idx = torch.cuda.current_device()
+        else:
+            idx = device.index if isinstance(device, torch.device) else int(device)
+            if idx is None:
+                idx = torch.cuda.current_device()
+        handles = self.__dict__.setdefault("_native_by_dev", {})
+        cur = handles.get(idx)
+        if cur is None or cur[0] != self._version:
+            if cur is not None:
+                with torch.cuda.device(idx):
+                    cur[1].close()
+            with torch.cuda.device(idx):
+                handles[idx] = (self._version, _native.DeviceWorld(self, idx))
+        return handles[idx][1]
+
+    # --- per-world status of the last batched step (see timestep.py) ----------
+    def getLastStatus(self):
+        """Status bits of each world of the last ``timestep`` call (a device
+        int32 tensor [B], 0 = the step is the reference's): 1 contact
+        overflow, 2 unsupported shape pair, 4 dropped-contact list overflow
+        (these three mean the physics differs from the reference's), 8 the
+        LCP was reduced (LCPUtils::reduce merged duplicate columns; the
+        reference's own behaviour, informational)."""
+        return getattr(self, "_last_status", None)
+
+    def setStatusPolicy(self, policy: str):
+        """'raise' (default): ``timestep`` raises ContactCapacityError when a
+        world's step cannot match the reference (status bits 1, 2, 4);
+        'record': only record them in getLastStatus() (no host sync)."""
+        if policy not in ("raise", "record"):
+            raise ValueError(policy)
+        self._status_policy = policy
+
+    def getStatusPolicy(self) -> str:
+        return getattr(self, "_status_policy", "raise")

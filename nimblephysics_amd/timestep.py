@@ -17,6 +17,12 @@ staged to the current HIP device, stepped by the same kernels, and the
 results / gradients come back on the CPU.  There is no CPU compute path --
 without a HIP device the call raises.
 
+Status: worlds whose contact set does not fit this path (more contacts than
+NIMBLE_MAX_CONTACTS, a shape pair without a collider) would step differently
+from the reference, so under the world's default status policy ('raise') the
+call raises ContactCapacityError naming them; ``world.getLastStatus()`` holds
+the per-world status bits of the last call either way.
+
 ``mass`` is the reference's tuned-mass vector (World::getMassDims entries,
 set with World::setMasses); no body is registered for mass tuning on this
 path, so it is empty when given and its gradient (lossWrtMass) is empty.
@@ -27,6 +33,7 @@ from typing import Optional
 
 import torch
 
+from ._native import ContactCapacityError, ST_DIVERGES, status_message
 from .simulation import World
 
 
@@ -68,6 +75,24 @@ def _compute_device(t: torch.Tensor) -> torch.device:
     return torch.device("cuda", torch.cuda.current_device())
 
 
+def _check_status(world: World, dev, snap: torch.Tensor) -> None:
+    """Record the per-world status bits; under the 'raise' policy, fail loudly
+    on worlds whose step cannot be the reference's (one host sync)."""
+    status = dev.status(snap)
+    world._last_status = status
+    if dev.num_pairs == 0 or world.getStatusPolicy() != "raise":
+        return
+    bad = (status & ST_DIVERGES) != 0
+    if bool(bad.any()):
+        idx = torch.nonzero(bad).flatten().tolist()
+        bits = 0
+        for v in status[bad].tolist():
+            bits |= int(v)
+        raise ContactCapacityError(
+            f"{len(idx)} world(s) {idx[:8]}{'...' if len(idx) > 8 else ''}: {status_message(bits)}; "
+            f"their step would differ from the reference's (world.setStatusPolicy('record') to continue anyway)")
+
+
 class TimestepLayer(torch.autograd.Function):
     @staticmethod
     def forward(ctx, world: World, state: torch.Tensor, action: torch.Tensor, mass: Optional[torch.Tensor]):
@@ -85,28 +110,34 @@ class TimestepLayer(torch.autograd.Function):
             ctx.mass_device = mass.device
         ctx.out_device = state.device
         cdev = _compute_device(state)
-        state = state.to(cdev, torch.float64)
-        action = action.to(cdev, torch.float64)
-        squeeze = state.dim() == 1
-        st = state.detach().reshape(1, -1) if squeeze else state.detach()
-        act = action.detach().reshape(1, -1) if squeeze else action.detach()
-        st = st.contiguous()
-        B = st.shape[0]
-        n = world.getNumDofs()
-        if st.shape[1] != 2 * n:
-            raise ValueError(f"state has {st.shape[1]} columns, world expects {2 * n}")
-        idx = _action_index(world, st.device)
-        if act.shape[1] != idx.shape[0]:
-            raise ValueError(f"action has {act.shape[1]} columns, action space has {idx.shape[0]}")
-        dev = world.native()
-        forces = torch.zeros((B, n), dtype=torch.float64, device=st.device)
-        forces.index_copy_(1, idx, act.contiguous())
-        bs = _batch_state(world, B, dev, st.device)
-        nxt = torch.empty_like(st)
-        snap = torch.empty((B, dev.snapshot_doubles), dtype=torch.float64, device=st.device)
-        stream = torch.cuda.current_stream(st.device).cuda_stream
-        dev.forward(st, forces, bs.cache, nxt, snap, stream)
+        with torch.cuda.device(cdev):
+            state = state.to(cdev, torch.float64)
+            action = action.to(cdev, torch.float64)
+            squeeze = state.dim() == 1
+            st = state.detach().reshape(1, -1) if squeeze else state.detach()
+            act = action.detach().reshape(1, -1) if squeeze else action.detach()
+            st = st.contiguous()
+            B = st.shape[0]
+            n = world.getNumDofs()
+            if st.shape[1] != 2 * n:
+                raise ValueError(f"state has {st.shape[1]} columns, world expects {2 * n}")
+            idx = _action_index(world, st.device)
+            if act.shape[1] != idx.shape[0]:
+                raise ValueError(f"action has {act.shape[1]} columns, action space has {idx.shape[0]}")
+            dev = world.native(st.device)
+            forces = torch.zeros((B, n), dtype=torch.float64, device=st.device)
+            forces.index_copy_(1, idx, act.contiguous())
+            bs = _batch_state(world, B, dev, st.device)
+            nxt = torch.empty_like(st)
+            snap = torch.empty((B, dev.snapshot_doubles), dtype=torch.float64, device=st.device)
+            stream = torch.cuda.current_stream(st.device).cuda_stream
+            dev.forward(st, forces, bs.cache, nxt, snap, stream)
+            world._last_snapshot = snap  # the batched BackpropSnapshot of this step
+            _check_status(world, dev, snap)
         ctx.world = world
+        # the backward must run on the model (and snapshot layout) that
+        # produced this snapshot, even if the world changes in between
+        ctx.dev = dev
         ctx.squeeze = squeeze
         ctx.save_for_backward(st, forces, snap, idx)
         if squeeze:
@@ -120,14 +151,18 @@ class TimestepLayer(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_next):
         st, forces, snap, idx = ctx.saved_tensors
-        world = ctx.world
-        g = grad_next.detach().reshape(st.shape).to(st.device, torch.float64).contiguous()
-        dev = world.native()
-        gs = torch.empty_like(st)
-        gf = torch.empty_like(forces)
-        stream = torch.cuda.current_stream(st.device).cuda_stream
-        dev.backward(st, forces, snap, g, gs, gf, stream)
-        ga = gf.index_select(1, idx)
+        dev = ctx.dev
+        if dev.h is None:
+            raise RuntimeError("the world model that produced this step was released before backward")
+        if snap.shape[1] != dev.snapshot_doubles:
+            raise RuntimeError("snapshot layout does not match the world model of the forward")
+        with torch.cuda.device(st.device):
+            g = grad_next.detach().reshape(st.shape).to(st.device, torch.float64).contiguous()
+            gs = torch.empty_like(st)
+            gf = torch.empty_like(forces)
+            stream = torch.cuda.current_stream(st.device).cuda_stream
+            dev.backward(st, forces, snap, g, gs, gf, stream)
+            ga = gf.index_select(1, idx)
         od = ctx.out_device
         gm = torch.zeros(ctx.mass_shape, dtype=torch.float64, device=ctx.mass_device) if ctx.use_mass else None
         if ctx.squeeze:

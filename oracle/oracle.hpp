@@ -84,6 +84,7 @@ struct Snapshot {
   double cfm = 0.0;
   bool ignoredFriction = false;
   bool shortCircuit = false;
+  bool lcpReduced = false;  // LCPUtils::reduce merged columns on a fallback solve
   int unsupportedContacts = 0;   // a narrow-phase branch not restated was hit
 };
 

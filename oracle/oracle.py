@@ -63,6 +63,17 @@ def lib():
         L.oracle_cod_solve.argtypes = [dp, ip, ip, dp, dp]
         L.oracle_box_box.argtypes = [dp, dp, dp, dp, dp]
         L.oracle_box_box.restype = ip
+        pi = C.POINTER(ip)
+        L.oracle_lcp_reduce.argtypes = [ip, dp, dp, dp, dp, dp, pi, dp, dp, dp, dp, dp, pi, pi]
+        L.oracle_lcp_reduce.restype = ip
+        L.oracle_pgs.argtypes = [ip, dp, dp, dp, dp, dp, pi]
+        L.oracle_pgs.restype = ip
+        L.oracle_pgs_opt.argtypes = [ip, dp, dp, dp, dp, dp, pi, ip, C.c_double, C.c_double, C.c_double]
+        L.oracle_pgs_opt.restype = ip
+        L.oracle_lcp_valid.argtypes = [ip, dp, dp, dp, dp, dp, pi, ip]
+        L.oracle_lcp_valid.restype = ip
+        L.oracle_guess_solution.argtypes = [ip, dp, dp, pi, dp]
+        L.oracle_lcp_cascade.argtypes = [ip, dp, dp, dp, dp, pi, dp, C.c_double, dp]
         _lib = L
     return _lib
 
@@ -183,8 +194,8 @@ def lcp_debug(ow: "OracleWorld", b=0, max_rows=64):
 
 
 def lcp_flags(ow: "OracleWorld", b=0):
-    """[shortCircuit, ignoredFriction, cfm, numClamping, numUpperBound, unsupportedContacts]"""
-    out = np.zeros(6)
+    """[shortCircuit, ignoredFriction, cfm, numClamping, numUpperBound, unsupportedContacts, lcpReduced]"""
+    out = np.zeros(7)
     lib().oracle_lcp_flags(ow.snaps, b, _p(out))
     return out
 
@@ -271,3 +282,60 @@ def capsule_box(size, T_box, height, radius, T_capsule, box_first=True, clip=0.0
     if k < 0:
         k = -1 - k
     return out[:k], unsupported
+
+
+def _f(v):
+    return np.ascontiguousarray(v, dtype=np.float64).copy()
+
+
+def _i(v):
+    return np.ascontiguousarray(v, dtype=np.int32).copy()
+
+
+def lcp_reduce(A, x, b, hi, lo, fi):
+    """LCPUtils::reduce restated: (A_r, x_r, b_r, hi_r, lo_r, fi_r, map) with
+    x_full = x_r[map] (mapOut * x_r)."""
+    A = _f(A)
+    m = A.shape[0]
+    x, b, hi, lo, fi = _f(x), _f(b), _f(hi), _f(lo), _i(fi)
+    Ao, xo, bo, ho, lo_o = np.zeros(m * m), np.zeros(m), np.zeros(m), np.zeros(m), np.zeros(m)
+    fo, mp = np.zeros(m, np.int32), np.zeros(m, np.int32)
+    mr = lib().oracle_lcp_reduce(m, _p(A), _p(x), _p(b), _p(hi), _p(lo), _pi(fi), _p(Ao), _p(xo), _p(bo), _p(ho),
+                                 _p(lo_o), _pi(fo), _pi(mp))
+    return (Ao[:mr * mr].reshape(mr, mr), xo[:mr], bo[:mr], ho[:mr], lo_o[:mr], fo[:mr], mp)
+
+
+def pgs(A, x, b, lo, hi, fi, options=None):
+    """PgsBoxedLcpSolver::solve restated; options = (maxIter, deltaX, relTol,
+    epsDiv) for PgsBoxedLcpSolver::Option, None for the default."""
+    A, x, b, lo, hi, fi = _f(A), _f(x), _f(b), _f(lo), _f(hi), _i(fi)
+    n = A.shape[0]
+    if options is None:
+        ok = lib().oracle_pgs(n, _p(A), _p(x), _p(b), _p(lo), _p(hi), _pi(fi))
+    else:
+        it, dx, rt, eps = options
+        ok = lib().oracle_pgs_opt(n, _p(A), _p(x), _p(b), _p(lo), _p(hi), _pi(fi), int(it), dx, rt, eps)
+    return bool(ok), x
+
+
+def lcp_valid(A, x, b, hi, lo, fi, ignore_friction=False):
+    """LCPUtils::isLCPSolutionValid restated."""
+    A, x, b, hi, lo, fi = _f(A), _f(x), _f(b), _f(hi), _f(lo), _i(fi)
+    return bool(lib().oracle_lcp_valid(A.shape[0], _p(A), _p(x), _p(b), _p(hi), _p(lo), _pi(fi),
+                                       1 if ignore_friction else 0))
+
+
+def guess_solution(A, b, fi):
+    A, b, fi = _f(A), _f(b), _i(fi)
+    x = np.zeros(A.shape[0])
+    lib().oracle_guess_solution(A.shape[0], _p(A), _p(b), _pi(fi), _p(x))
+    return x
+
+
+def lcp_cascade(A, b, lo, hi, fi, warm, fallback_cfm=1e-4):
+    """BoxedLcpConstraintSolver::solveLcp's fallbacks (reduce + Dantzig, CFM +
+    reduce + PGS, removeFriction + PGS): (x, path, reduced, ignoredFriction, cfm)."""
+    A, b, lo, hi, fi, x = _f(A), _f(b), _f(lo), _f(hi), _i(fi), _f(warm)
+    info = np.zeros(4)
+    lib().oracle_lcp_cascade(A.shape[0], _p(A), _p(b), _p(lo), _p(hi), _pi(fi), _p(x), fallback_cfm, _p(info))
+    return x, int(info[0]), bool(info[1]), bool(info[2]), float(info[3])

@@ -111,6 +111,7 @@ void oracle_lcp_flags(void* snaps, int b, double* out) {
   out[3] = s.numClamping;
   out[4] = s.numUpperBound;
   out[5] = s.unsupportedContacts;
+  out[6] = s.lcpReduced ? 1 : 0;
 }
 // clamping impulses f_c of world b; returns numClamping
 int oracle_lcp_fc(void* snaps, int b, double* fc, int maxc) {
@@ -146,5 +147,76 @@ void codSolveC(const double* A, int m, int n, const double* b, double* x);
 void oracle_cod_solve(const double* A, int m, int n, const double* b, double* x) { codSolveC(A, m, n, b, x); }
 int oracle_box_box(const double* size1, const double* T1, const double* size2, const double* T2, double* out);
 }
-namespace oracle { void codSolve(const double* A, int m, int n, const double* b, double* x); }
+namespace oracle {
+void codSolve(const double* A, int m, int n, const double* b, double* x);
+bool pgsSolveLCP(int n, double* A, double* x, double* b, double* lo, double* hi, const int* findex);
+bool pgsSolveLCPOpt(int n, double* A, double* x, double* b, double* lo, double* hi, const int* findex, int maxIter,
+                    double deltaXThr, double relTol, double epsDiv);
+bool lcpValid(const std::vector<double>& A, const std::vector<double>& x, const std::vector<double>& b,
+              const std::vector<double>& hi, const std::vector<double>& lo, const std::vector<int>& fi,
+              bool ignoreFriction);
+std::vector<double> guessSolution(const std::vector<double>& A, const std::vector<double>& b,
+                                  const std::vector<int>& fi);
+std::vector<int> lcpReduce(std::vector<double>& A, std::vector<double>& X, std::vector<double>& b,
+                           std::vector<double>& hi, std::vector<double>& lo, std::vector<int>& fi);
+struct LcpCascade {
+  bool reduced = false, ignoredFriction = false;
+  double cfm = 0.0;
+  int path = 0;
+};
+LcpCascade lcpFallbackCascade(const std::vector<double>& A, const std::vector<double>& b,
+                              const std::vector<double>& lo, const std::vector<double>& hi,
+                              const std::vector<int>& fi, const std::vector<double>& warm, double fallbackCfm,
+                              std::vector<double>& X);
+}  // namespace oracle
+
+static std::vector<double> vec(const double* p, int n) { return std::vector<double>(p, p + n); }
+
+extern "C" {
+// LCPUtils::reduce on a raw problem (A m x m row-major); writes the reduced
+// problem (A as mr x mr) and map (original row -> reduced row); returns mr
+int oracle_lcp_reduce(int m, const double* A, const double* x, const double* b, const double* hi, const double* lo,
+                      const int* fi, double* Ao, double* xo, double* bo, double* hio, double* loo, int* fio, int* map) {
+  std::vector<double> Av = vec(A, m * m), xv = vec(x, m), bv = vec(b, m), hv = vec(hi, m), lv = vec(lo, m);
+  std::vector<int> fv(fi, fi + m);
+  const std::vector<int> mp = oracle::lcpReduce(Av, xv, bv, hv, lv, fv);
+  const int mr = (int)bv.size();
+  for (int i = 0; i < mr * mr; i++) Ao[i] = Av[i];
+  for (int i = 0; i < mr; i++) { xo[i] = xv[i]; bo[i] = bv[i]; hio[i] = hv[i]; loo[i] = lv[i]; fio[i] = fv[i]; }
+  for (int i = 0; i < m; i++) map[i] = mp[i];
+  return mr;
+}
+// PgsBoxedLcpSolver::solve restated (default options); x in/out
+int oracle_pgs(int n, const double* A, double* x, const double* b, const double* lo, const double* hi,
+               const int* fi) {
+  std::vector<double> Av = vec(A, n * n), bv = vec(b, n), lv = vec(lo, n), hv = vec(hi, n);
+  return oracle::pgsSolveLCP(n, Av.data(), x, bv.data(), lv.data(), hv.data(), fi) ? 1 : 0;
+}
+// PgsBoxedLcpSolver::solve with PgsBoxedLcpSolver::Option(maxIter, deltaX, relTol, epsDiv, false)
+int oracle_pgs_opt(int n, const double* A, double* x, const double* b, const double* lo, const double* hi,
+                   const int* fi, int maxIter, double deltaX, double relTol, double epsDiv) {
+  std::vector<double> Av = vec(A, n * n), bv = vec(b, n), lv = vec(lo, n), hv = vec(hi, n);
+  return oracle::pgsSolveLCPOpt(n, Av.data(), x, bv.data(), lv.data(), hv.data(), fi, maxIter, deltaX, relTol, epsDiv)
+             ? 1 : 0;
+}
+int oracle_lcp_valid(int m, const double* A, const double* x, const double* b, const double* hi, const double* lo,
+                     const int* fi, int ignoreFriction) {
+  return oracle::lcpValid(vec(A, m * m), vec(x, m), vec(b, m), vec(hi, m), vec(lo, m), std::vector<int>(fi, fi + m),
+                          ignoreFriction != 0) ? 1 : 0;
+}
+void oracle_guess_solution(int m, const double* A, const double* b, const int* fi, double* x) {
+  const std::vector<double> g = oracle::guessSolution(vec(A, m * m), vec(b, m), std::vector<int>(fi, fi + m));
+  for (int i = 0; i < m; i++) x[i] = g[i];
+}
+// the fallback cascade of BoxedLcpConstraintSolver::solveLcp; x: in warm
+// start, out solution; info: [path, reduced, ignoredFriction, cfm]
+void oracle_lcp_cascade(int m, const double* A, const double* b, const double* lo, const double* hi, const int* fi,
+                        double* x, double fallbackCfm, double* info) {
+  std::vector<double> X;
+  const oracle::LcpCascade r = oracle::lcpFallbackCascade(vec(A, m * m), vec(b, m), vec(lo, m), vec(hi, m),
+                                                          std::vector<int>(fi, fi + m), vec(x, m), fallbackCfm, X);
+  for (int i = 0; i < m; i++) x[i] = X[i];
+  info[0] = r.path; info[1] = r.reduced ? 1 : 0; info[2] = r.ignoredFriction ? 1 : 0; info[3] = r.cfm;
+}
+}
 void codSolveC(const double* A, int m, int n, const double* b, double* x) { oracle::codSolve(A, m, n, b, x); }

@@ -645,7 +645,7 @@ static void rowForce(const World& w, const Kin<double>& k, const Contact& c, con
 
 //------------------------------------------------------------------------------
 // LCPUtils::isLCPSolutionValid (LCPUtils.cpp:14)
-static bool lcpValid(const std::vector<double>& A, const std::vector<double>& x, const std::vector<double>& b,
+bool lcpValid(const std::vector<double>& A, const std::vector<double>& x, const std::vector<double>& b,
                      const std::vector<double>& hi, const std::vector<double>& lo, const std::vector<int>& fi,
                      bool ignoreFriction) {
   const int m = (int)x.size();
@@ -674,7 +674,7 @@ static bool lcpValid(const std::vector<double>& A, const std::vector<double>& x,
 }
 
 // LCPUtils::guessSolution (LCPUtils.cpp:69)
-static std::vector<double> guessSolution(const std::vector<double>& A, const std::vector<double>& b,
+std::vector<double> guessSolution(const std::vector<double>& A, const std::vector<double>& b,
                                          const std::vector<int>& fi) {
   const int m = (int)b.size();
   std::vector<int> cl;
@@ -693,6 +693,131 @@ static std::vector<double> guessSolution(const std::vector<double>& A, const std
   codSolve(Ar.data(), k, k, br.data(), xr.data());
   for (int i = 0; i < k; i++) x[cl[i]] = xr[i];
   return x;
+}
+
+// LCPUtils::reduce (LCPUtils.cpp:144) with mergeLCPColumns (:346): while
+// some column pair (a < b, first in (a, b) order) of the current problem has
+// ||A_a - A_b||^2 < 1e-4, |b_a - b_b| < 1e-4 and equal findex / hi / lo,
+// merge b into a: row and column b are deleted, column a is doubled, findex
+// entries pointing at b point at a, later indices shift down.  The problem is
+// reduced in place (A row-major, the new size on return); the returned map
+// sends each original row to its reduced row, i.e. mapOut * x_reduced is
+// x_full[i] = x_reduced[map[i]] (mapOut's columns are sums of unit columns).
+struct LcpCascade {
+  bool reduced = false, ignoredFriction = false;
+  double cfm = 0.0;
+  int path = 0;  // 0 Dantzig, 1 PGS (CFM), 2 frictionless PGS
+};
+
+std::vector<int> lcpReduce(std::vector<double>& A, std::vector<double>& X, std::vector<double>& b,
+                           std::vector<double>& hi, std::vector<double>& lo, std::vector<int>& fi) {
+  const int m0 = (int)b.size();
+  std::vector<int> map(m0);
+  for (int i = 0; i < m0; i++) map[i] = i;
+  for (;;) {
+    const int n = (int)b.size();
+    int ca = -1, cb = -1;
+    for (int a = 0; a < n - 1 && ca < 0; a++)
+      for (int c = a + 1; c < n; c++) {
+        double dd = 0;
+        for (int i = 0; i < n; i++) dd += (A[i * n + a] - A[i * n + c]) * (A[i * n + a] - A[i * n + c]);
+        if (dd < 1e-4 && std::fabs(b[a] - b[c]) < 1e-4 && fi[a] == fi[c] && hi[a] == hi[c] && lo[a] == lo[c]) {
+          ca = a; cb = c;
+          break;
+        }
+      }
+    if (ca < 0) break;
+    // mergeLCPColumns(ca, cb)
+    std::vector<double> nA((n - 1) * (n - 1));
+    for (int i = 0, ni = 0; i < n; i++) {
+      if (i == cb) continue;
+      for (int j = 0, nj = 0; j < n; j++) {
+        if (j == cb) continue;
+        nA[ni * (n - 1) + nj] = j == ca ? A[i * n + j] * 2.0 : A[i * n + j];
+        nj++;
+      }
+      ni++;
+    }
+    auto drop = [&](auto& v) { v.erase(v.begin() + cb); };
+    drop(X); drop(b); drop(hi); drop(lo); drop(fi);
+    for (int& f : fi) f = f == cb ? ca : (f > cb ? f - 1 : f);
+    for (int& r : map) r = r == cb ? ca : (r > cb ? r - 1 : r);
+    A.swap(nA);
+  }
+  return map;
+}
+
+// BoxedLcpConstraintSolver::solveLcp's fallbacks once the gradient
+// short-circuit failed (BoxedLcpConstraintSolver.cpp:459-687): Dantzig with
+// early termination on the reduced problem (LCPUtils::reduce), validity on
+// the full one; else CFM on the diagonal and PGS on the reduced A + cfm I from
+// the warm start, validity; else LCPUtils::removeFriction and PGS on the
+// normal rows from zero.  NaNs zero the solution.  X: the solution (in: the
+// warm start, which is also mXBackup).
+LcpCascade lcpFallbackCascade(const std::vector<double>& A, const std::vector<double>& b,
+                              const std::vector<double>& lo, const std::vector<double>& hi,
+                              const std::vector<int>& fi, const std::vector<double>& warm, double fallbackCfm,
+                              std::vector<double>& X) {
+  const int m = (int)b.size();
+  LcpCascade res;
+  X = warm;
+  bool success = false;
+  {
+    std::vector<double> Ad = A, xr = X, bd = b, lod = lo, hid = hi;
+    std::vector<int> fid = fi;
+    const std::vector<int> map = lcpReduce(Ad, xr, bd, hid, lod, fid);
+    const int mr = (int)bd.size();
+    if (mr < m) res.reduced = true;
+    // the reduced A is not symmetric (merged columns are doubled); ODE's dLCP
+    // only ever reads the lower triangle of the row-major matrix it is given
+    // (swapRowsAndCols, lcp.cpp:144; GETA, matrix.cpp:371) -- checked against
+    // the reference's compiled solver in tests/test_lcp_utils.py -- so the
+    // restatement gets that triangle mirrored
+    for (int r = 0; r < mr; r++)
+      for (int c = r + 1; c < mr; c++) Ad[r * mr + c] = Ad[c * mr + r];
+    std::vector<double> xd(mr, 0.0);
+    success = dantzigSolveLCP(mr, Ad.data(), xd.data(), bd.data(), nullptr, 0, lod.data(), hid.data(), fid.data(), true);
+    if (success) {
+      for (int i = 0; i < m; i++) X[i] = xd[map[i]];
+      if (!lcpValid(A, X, b, hi, lo, fi, false)) success = false;
+    }
+  }
+  for (double xv : X) if (std::isnan(xv)) { success = false; std::fill(X.begin(), X.end(), 0.0); break; }
+  if (success) return res;
+  res.path = 1;
+  res.cfm = fallbackCfm;
+  std::vector<double> Acfm = A;
+  for (int i = 0; i < m; i++) Acfm[i * m + i] += fallbackCfm;
+  {
+    std::vector<double> Ad = Acfm, xd = warm, bd = b, lod = lo, hid = hi;
+    std::vector<int> fid = fi;
+    const std::vector<int> map = lcpReduce(Ad, xd, bd, hid, lod, fid);
+    const int mr = (int)bd.size();
+    if (mr < m) res.reduced = true;
+    success = pgsSolveLCP(mr, Ad.data(), xd.data(), bd.data(), lod.data(), hid.data(), fid.data());
+    if (success) {
+      for (int i = 0; i < m; i++) X[i] = xd[map[i]];
+      if (!lcpValid(Acfm, X, b, hi, lo, fi, false)) success = false;
+    }
+  }
+  if (!success) {
+    res.path = 2;
+    res.ignoredFriction = true;
+    std::vector<int> keep;
+    for (int i = 0; i < m; i++) if (fi[i] == -1) keep.push_back(i);
+    const int k2 = (int)keep.size();
+    std::vector<double> Ar(k2 * k2), br(k2), xr(k2, 0.0), lor(k2), hir(k2);
+    std::vector<int> fir(k2, -1);
+    for (int r = 0; r < k2; r++) {
+      br[r] = b[keep[r]]; lor[r] = lo[keep[r]]; hir[r] = hi[keep[r]];
+      for (int c = 0; c < k2; c++) Ar[r * k2 + c] = Acfm[keep[r] * m + keep[c]];
+    }
+    pgsSolveLCP(k2, Ar.data(), xr.data(), br.data(), lor.data(), hir.data(), fir.data());
+    std::fill(X.begin(), X.end(), 0.0);
+    for (int r = 0; r < k2; r++) X[keep[r]] = xr[r];
+  }
+  for (double xv : X) if (std::isnan(xv)) { std::fill(X.begin(), X.end(), 0.0); break; }
+  return res;
 }
 
 // ---- ConstrainedGroupGradientMatrices (the per-step "gradient matrices") ----
@@ -851,6 +976,7 @@ void solveContacts(const World& w, const Kin<double>& k, const double* q, const 
   snap.contacts.clear();
   snap.shortCircuit = false;
   snap.ignoredFriction = false;
+  snap.lcpReduced = false;
   snap.cfm = 0.0;
   // ConstraintSolver::updateConstraints (ConstraintSolver.cpp:520)
   std::vector<Contact> contacts;
@@ -965,60 +1091,14 @@ void solveContacts(const World& w, const Kin<double>& k, const double* q, const 
   double cfm = 0.0;
   bool ignoredFriction = false;
   if (!success) {
-    // Dantzig on the reduced (duplicate-merged) problem.  LCPUtils::reduce
-    // merges only near-identical columns, which the box contacts on this path
-    // never produce; a merge is detected and reported.
-    for (int a = 0; a < m; a++)
-      for (int c = a + 1; c < m; c++) {
-        double dd = 0;
-        for (int i = 0; i < m; i++) dd += (A[i * m + a] - A[i * m + c]) * (A[i * m + a] - A[i * m + c]);
-        if (dd < 1e-4 && std::fabs(b[a] - b[c]) < 1e-4 && fi[a] == fi[c] && hi[a] == hi[c] && lo[a] == lo[c]) {
-          std::fprintf(stderr, "oracle: duplicate LCP columns (LCPUtils::reduce) not supported\n");
-          std::abort();
-        }
-      }
-    std::vector<double> Ad = A, xd(m, 0.0), bd = b, lod = lo, hid = hi;
-    std::vector<int> fid = fi;
-    success = dantzigSolveLCP(m, Ad.data(), xd.data(), bd.data(), nullptr, 0, lod.data(), hid.data(), fid.data(), true);
-    if (success) {
-      X = xd;
-      if (!lcpValid(A, X, b, hi, lo, fi, false)) success = false;
-    }
+    const std::vector<double> warm = X;  // mX == mXBackup (cache or guess)
+    const LcpCascade r = lcpFallbackCascade(A, b, lo, hi, fi, warm, w.fallbackCfm, X);
+    cfm = r.cfm;
+    ignoredFriction = r.ignoredFriction;
+    snap.lcpReduced = r.reduced;
+    if (cfm != 0.0)
+      for (int i = 0; i < m; i++) Acfm[i * m + i] += cfm;
   }
-  for (double xv : X) if (std::isnan(xv)) { success = false; std::fill(X.begin(), X.end(), 0.0); break; }
-  if (!success) {
-    cfm = w.fallbackCfm;
-    for (int i = 0; i < m; i++) Acfm[i * m + i] += cfm;
-  }
-  if (!success) {
-    std::vector<double> Ad = Acfm, xd = lcpCache.size() == (size_t)m ? lcpCache : std::vector<double>(m, 0.0);
-    // mXBackup is the (possibly re-initialised) cached solution at build time
-    xd = ((int)lcpCache.size() != m) ? guessSolution(A, b, fi) : lcpCache;
-    std::vector<double> bd = b, lod = lo, hid = hi;
-    std::vector<int> fid = fi;
-    success = pgsSolveLCP(m, Ad.data(), xd.data(), bd.data(), lod.data(), hid.data(), fid.data());
-    if (success) {
-      X = xd;
-      if (!lcpValid(Acfm, X, b, hi, lo, fi, false)) success = false;
-    }
-  }
-  if (!success) {
-    ignoredFriction = true;
-    // LCPUtils::removeFriction + PGS on the normal rows only
-    std::vector<int> keep;
-    for (int i = 0; i < m; i++) if (fi[i] == -1) keep.push_back(i);
-    const int k2 = (int)keep.size();
-    std::vector<double> Ar(k2 * k2), br(k2), xr(k2, 0.0), lor(k2), hir(k2);
-    std::vector<int> fir(k2, -1);
-    for (int r = 0; r < k2; r++) {
-      br[r] = b[keep[r]]; lor[r] = lo[keep[r]]; hir[r] = hi[keep[r]];
-      for (int c = 0; c < k2; c++) Ar[r * k2 + c] = Acfm[keep[r] * m + keep[c]];
-    }
-    pgsSolveLCP(k2, Ar.data(), xr.data(), br.data(), lor.data(), hir.data(), fir.data());
-    std::fill(X.begin(), X.end(), 0.0);
-    for (int r = 0; r < k2; r++) X[keep[r]] = xr[r];
-  }
-  for (double xv : X) if (std::isnan(xv)) { std::fill(X.begin(), X.end(), 0.0); break; }
   if (!shortCircuit) {
     gm.X = X; gm.A = Acfm; gm.cfm = cfm; gm.ignoreFriction = ignoredFriction;
     gm.construct();

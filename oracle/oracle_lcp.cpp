@@ -454,11 +454,12 @@ bool dantzigSolveLCP(int n, double* Ain /* n x n, row-major, no padding */, doub
   return true;
 }
 
-// PgsBoxedLcpSolver::solve (PgsBoxedLcpSolver.cpp:85), default Option
-// (30 iterations, deltaX 1e-6, relative 1e-3, eps 1e-9, no randomisation).
-bool pgsSolveLCP(int n, double* A /* n x n */, double* x, double* b, double* lo, double* hi, const int* findex) {
-  const int maxIter = 30;
-  const double deltaXThr = 1e-6, relTol = 1e-3, epsDiv = 1e-9;
+// PgsBoxedLcpSolver::solve (PgsBoxedLcpSolver.cpp:85) with an explicit
+// PgsBoxedLcpSolver::Option (no randomisation); pgsSolveLCP uses the default
+// Option (30 iterations, deltaX 1e-6, relative 1e-3, eps 1e-9) the contact
+// solver runs with.
+bool pgsSolveLCPOpt(int n, double* A /* n x n */, double* x, double* b, double* lo, double* hi, const int* findex,
+                    int maxIter, double deltaXThr, double relTol, double epsDiv) {
   std::vector<int> order;
   bool possible = true;
   for (int i = 0; i < n; i++) {
@@ -501,6 +502,10 @@ bool pgsSolveLCP(int n, double* A /* n x n */, double* x, double* b, double* lo,
     if (possible) break;
   }
   return possible;
+}
+
+bool pgsSolveLCP(int n, double* A, double* x, double* b, double* lo, double* hi, const int* findex) {
+  return pgsSolveLCPOpt(n, A, x, b, lo, hi, findex, 30, 1e-6, 1e-3, 1e-9);
 }
 
 }  // namespace oracle

@@ -459,3 +459,47 @@ def capsule_pair_states(batch, seed=0, mode="cross"):
         st[b, 12:] = 0.05 * rng.standard_normal(12)
         st[b, 12 + 10] -= 0.1 if mode == "cross" else 0.4
     return st, f
+
+
+def twin_world(shape="sphere", gap=2e-5):
+    """A free body carrying two identical collision shapes `gap` apart, on a
+    static ground box: every contact comes twice at almost the same point, so
+    the LCP has near-duplicate columns and the fallback solves go through
+    LCPUtils::reduce (LCPUtils.cpp:144; BoxedLcpConstraintSolver.cpp:472,
+    :558).  Spheres (r = 0.05) or boxes (0.2 x 0.1 x 0.15)."""
+    from nimblephysics_amd import dynamics as D
+    w = nimble.World()
+    w.setGravity([0, -9.81, 0])
+    sk = D.Skeleton("twin")
+    _, b = sk.createFreeJointAndBodyNodePair()
+    b.setMass(1.0)
+    b.setMomentOfInertia(0.01, 0.012, 0.008)
+    for dx in (0.0, gap):
+        node = b.createShapeNode(D.SphereShape(0.05) if shape == "sphere" else D.BoxShape([0.2, 0.1, 0.15]),
+                                 collision=True)
+        T = np.eye(4)
+        T[0, 3] = dx
+        node.setRelativeTransform(T)
+    w.addSkeleton(sk)
+    g = D.Skeleton("ground")
+    gj, gb = g.createWeldJointAndBodyNodePair()
+    T = np.eye(4)
+    T[1, 3] = -0.05
+    gj.setTransformFromParentBodyNode(T)
+    gb.createShapeNode(D.BoxShape([10.0, 0.1, 10.0]), collision=True)
+    g.setMobile(False)
+    w.addSkeleton(g)
+    return w
+
+
+def twin_states(batch, seed=0):
+    """Twin-shape body ~1 mm into the ground (half of the worlds sliding at
+    ~1 m/s along x), small random velocities and forces."""
+    rng = np.random.default_rng(seed)
+    q = np.zeros((batch, 6))
+    v = 0.01 * rng.standard_normal((batch, 6))
+    q[:, 4] = 0.05 - 1e-3 + 2e-4 * rng.standard_normal(batch)
+    q[:, 0:3] = 1e-3 * rng.standard_normal((batch, 3))
+    v[:, 3] += rng.choice([0.0, 1.0], batch) * (1 + 0.2 * rng.standard_normal(batch))
+    f = 0.5 * rng.standard_normal((batch, 6))
+    return np.concatenate([q, v], axis=1), f

@@ -30,8 +30,15 @@ SN_CONTACTS, SN_ROWREC, RR_MAP = 16, 12, 7
 SN_ROWS = SN_CONTACTS + 16 * CREC
 
 
-def _rel(a, b):
-    return np.abs(a - b).max() / max(np.abs(b).max(), 1e-12)
+def _rel(a, b, floor=1e-3):
+    """Largest per-element relative error |a - b| / max(|b|, floor * max|b|)
+    (the absolute floor keeps components that are zero in exact arithmetic
+    from dividing by rounding noise)."""
+    a, b = np.asarray(a), np.asarray(b)
+    if b.size == 0:
+        return 0.0
+    scale = np.maximum(np.abs(b), floor * max(np.abs(b).max(), 1e-300))
+    return float((np.abs(a - b) / scale).max())
 
 
 def _device_step(world, st, f, cache=None):
@@ -77,17 +84,34 @@ def _lcp_ambiguous(ow, b, trials=64):
 
 
 def _same_path(ow, sn, b):
-    fl = O.lcp_flags(ow, b)[:5]
-    gfl = np.array([sn[6], sn[7], sn[4], sn[2], sn[3]])
+    of = O.lcp_flags(ow, b)
+    fl = np.concatenate([of[:5], [of[6]]])  # ... and whether LCPUtils::reduce merged columns
+    gfl = np.array([sn[6], sn[7], sn[4], sn[2], sn[3], 1.0 if int(sn[5]) & 8 else 0.0])
     m = int(sn[SN_M])
     mapping, _ = O.lcp_debug(ow, b)
     gm = sn[SN_ROWS:SN_ROWS + SN_ROWREC * m].reshape(m, SN_ROWREC)[:, RR_MAP].astype(int)
     return np.array_equal(fl, gfl) and np.array_equal(gm, mapping)
 
 
-def _check_contacts(ow, snap, B, max_diverge=0.03):
+def _check_lcp_solution(ow, sn, cache_row, b):
+    """The GPU's final LCP solution of world b (its warm-start cache) solves
+    the LCP its own path claims: A (+ the path's CFM) with the reference's
+    isLCPSolutionValid, friction zero when friction was removed."""
+    A, bb, lo, hi, fi = O.lcp_problem(ow, b)
+    m = len(bb)
+    assert int(cache_row[0]) == m, b
+    x = cache_row[1:1 + m]
+    if sn[7]:  # removeFriction: the reference does not check validity
+        assert (x[fi >= 0] == 0).all(), b
+        return
+    assert O.lcp_valid(A + sn[4] * np.eye(m), x, bb, hi, lo, fi), f"world {b}: GPU LCP solution invalid"
+
+
+def _check_contacts(ow, snap, B, max_diverge=0.03, cache=None):
     """Contact sets bit-exact for every world; returns the mask of worlds on
-    the same LCP path (the others are checked to be ill-posed)."""
+    the same LCP path.  A world may leave the oracle's path only where the
+    reference's own Dantzig flips under 1e-15 perturbations (ill-posed); its
+    GPU solution is then checked to solve the LCP (isLCPSolutionValid)."""
     same = np.ones(B, dtype=bool)
     for b in range(B):
         ref = O.contacts(ow, b)
@@ -106,6 +130,8 @@ def _check_contacts(ow, snap, B, max_diverge=0.03):
         if not _same_path(ow, sn, b):
             assert _lcp_ambiguous(ow, b), f"world {b}: LCP path differs on a well-posed problem"
             same[b] = False
+            if cache is not None:
+                _check_lcp_solution(ow, sn, cache[b], b)
     assert (~same).sum() <= max(1, int(max_diverge * B)), (~same).sum()
     return same
 
@@ -115,7 +141,7 @@ def _parity(world, st, f, seed=11, check_grad=True, max_diverge=0.03):
     ref = ow.forward(st, f)
     nxt, snap, cache, ts, tf = _device_step(world, st, f)
     B = st.shape[0]
-    same = _check_contacts(ow, snap.cpu().numpy(), B, max_diverge)
+    same = _check_contacts(ow, snap.cpu().numpy(), B, max_diverge, cache.cpu().numpy())
     n = world.getNumDofs()
     got = nxt.cpu().numpy()[same]
     ref = ref[same]
@@ -162,7 +188,7 @@ def test_atlas_rollout_warm_start():
         ref = ow.forward(cur, f)
         nxt, snap, cache, ts, tf = _device_step(world, cur, f, cache)
         got = nxt.cpu().numpy()
-        same = _check_contacts(ow, snap.cpu().numpy(), st.shape[0])
+        same = _check_contacts(ow, snap.cpu().numpy(), st.shape[0], cache=cache.cpu().numpy())
         assert _rel(got[same], ref[same]) < RTOL, (k, _rel(got[same], ref[same]))
         g = np.random.default_rng(k).standard_normal(st.shape)
         rgs, rgf = ow.backward(g)
@@ -213,7 +239,7 @@ def test_half_cheetah_rollout():
     for k in range(10):
         ref = ow.forward(cur, f)
         nxt, snap, cache, ts, tf = _device_step(world, cur, f, cache)
-        same = _check_contacts(ow, snap.cpu().numpy(), st.shape[0])
+        same = _check_contacts(ow, snap.cpu().numpy(), st.shape[0], cache=cache.cpu().numpy())
         got = nxt.cpu().numpy()
         assert _rel(got[same], ref[same]) < RTOL, (k, _rel(got[same], ref[same]))
         g = np.random.default_rng(k).standard_normal(st.shape)
@@ -324,3 +350,72 @@ def test_capsule_capsule_contact_parity():
     assert (ncon <= 1).all() and (ncon[:40] == 1).sum() >= 30 and (ncon[40:] == 1).sum() >= 12
     types = snap[:, SN_CONTACTS + 7].astype(int) & 15
     assert (types[:40][ncon[:40] == 1] == 9).all() and (types[40:][ncon[40:] == 1] == 8).all()
+
+
+@pytest.mark.parametrize("shape", ["sphere", "box"])
+def test_lcp_reduce_duplicate_columns(shape):
+    """LCPUtils::reduce on the hot path: a body with two shapes 2e-5 apart
+    gives every contact twice, the fallback solves merge the duplicate
+    columns (status bit 8 == the oracle's reduced flag, checked per world in
+    _same_path), and state / gradients match."""
+    world = models.twin_world(shape)
+    st, f = models.twin_states(64, seed=3)
+    ow, snap = _parity(world, st, f, max_diverge=0.1 if shape == "box" else 0.03)
+    reduced = (snap[:, 5].astype(int) & 8) != 0
+    assert reduced.mean() > (0.9 if shape == "sphere" else 0.4), reduced.mean()
+
+
+def test_contact_overflow_raises():
+    """More contacts than NIMBLE_MAX_CONTACTS (five boxes resting on the
+    ground: 20 corner contacts) cannot be the reference's step: timestep
+    raises ContactCapacityError, and under the 'record' policy the per-world
+    status says why."""
+    import nimblephysics_amd as nimble
+    from nimblephysics_amd import dynamics as D
+    from nimblephysics_amd._native import ContactCapacityError
+    w = nimble.World()
+    w.setGravity([0, -9.81, 0])
+    g = D.Skeleton("ground")
+    gj, gb = g.createWeldJointAndBodyNodePair()
+    T = np.eye(4)
+    T[1, 3] = -0.05
+    gj.setTransformFromParentBodyNode(T)
+    gb.createShapeNode(D.BoxShape([10.0, 0.1, 10.0]), collision=True)
+    g.setMobile(False)
+    w.addSkeleton(g)
+    for k in range(5):
+        sk = D.Skeleton(f"box{k}")
+        _, b = sk.createFreeJointAndBodyNodePair()
+        b.createShapeNode(D.BoxShape([0.2, 0.1, 0.2]), collision=True)
+        w.addSkeleton(sk)
+    st = np.zeros((4, 60))
+    for k in range(5):
+        st[:, 6 * k + 3] = 0.5 * k
+        st[:, 6 * k + 4] = 0.05 - 1e-3
+    d = torch.device("cuda:0")
+    ts = torch.tensor(st, device=d)
+    act = torch.zeros((4, 30), dtype=torch.float64, device=d)
+    with pytest.raises(ContactCapacityError):
+        nimble.timestep(w, ts, act)
+    w.setStatusPolicy("record")
+    nimble.timestep(w, ts, act)
+    status = w.getLastStatus().cpu().numpy()
+    assert ((status & 1) != 0).all()
+
+
+def test_model_change_between_steps():
+    """A body-mass change between two steps reaches the device model
+    (dynamics setters invalidate the uploaded World): GPU == oracle on the
+    new model, and differs from the old one."""
+    import nimblephysics_amd as nimble
+    world = models.atlas_world(True)
+    st, f = models.random_states(world, 8, seed=5, q_scale=0.01, v_scale=0.02)
+    d = torch.device("cuda:0")
+    out1 = nimble.timestep(world, torch.tensor(st, device=d), torch.tensor(f, device=d)).cpu().numpy()
+    body = world.getSkeleton(0).getBodyNode(3)
+    body.setMass(body.getMass() * 3.0)
+    world._batch_state = None  # fresh LCP warm start, as the oracle below
+    out2 = nimble.timestep(world, torch.tensor(st, device=d), torch.tensor(f, device=d)).cpu().numpy()
+    ref2 = O.OracleWorld(world).forward(st, f)
+    assert np.abs(out2 - out1).max() > 1e-9
+    assert _rel(out2, ref2) < RTOL

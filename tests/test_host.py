@@ -18,13 +18,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _declared_symbols():
     src = open(os.path.join(ROOT, "include", "nimble_amd.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(nimble_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int32_t|int64_t|const char\*)\s+(nimble_\w+)\s*\(", src, re.M)))
 
 
 def test_header_declares_the_boundary():
     syms = _declared_symbols()
     for s in ("nimble_world_create", "nimble_world_destroy", "nimble_forward", "nimble_backward",
-              "nimble_snapshot_doubles", "nimble_lcp_cache_doubles", "nimble_last_error"):
+              "nimble_snapshot_doubles", "nimble_lcp_cache_doubles", "nimble_last_error",
+              "nimble_num_collision_pairs"):
         assert s in syms
 
 
@@ -129,3 +130,22 @@ def test_bench_harness_gloo_two_ranks():
     assert out[0][0] == 5.0 and out[1][0] == 5.0  # 2 warmup + 3 timed
     assert out[0][2] == 5
     assert abs(out[0][1] - out[1][1]) < 1e-12  # max over ranks agreed
+
+
+def test_dynamics_setters_invalidate_device_model():
+    """Every model setter bumps the world's version, so the next step
+    re-uploads the model (the reference's setters act on the next
+    World::step); no GPU needed to check the bookkeeping."""
+    w = models.box_world()
+    body = w.getSkeleton(0).getBodyNode(0)
+    joint = body.getParentJoint()
+    calls = [lambda: body.setMass(2.0), lambda: body.setLocalCOM([0.0, 0.1, 0.0]),
+             lambda: body.setMomentOfInertia(1, 2, 3), lambda: body.setFrictionCoeff(0.5),
+             lambda: body.setRestitutionCoeff(0.2), lambda: joint.setDampingCoefficient(0, 0.1),
+             lambda: joint.setSpringStiffness(0, 1.0), lambda: joint.setPositionUpperLimit(0, 1.0),
+             lambda: joint.setControlForceLowerLimit(0, -1.0), lambda: w.getSkeleton(1).setMobile(False),
+             lambda: body.getShapeNode(0).setRelativeTransform(np.eye(4))]
+    for c in calls:
+        v = w._version
+        c()
+        assert w._version > v

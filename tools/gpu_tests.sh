@@ -1,0 +1,17 @@
+#!/bin/bash
+# GPU-box: the -m gpu parity suite (one process), smoke, a short bench.
+# Usage: bash tools/gpu_tests.sh <tag> [pytest -k expr]
+set -o pipefail
+TAG=${1:-r02}
+K=${2:-}
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+if [ -n "$K" ]; then KA=(-k "$K"); else KA=(); fi
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${KA[@]}" > gpurun_out/gpu_tests_$TAG.log 2>&1
+rc=$?
+grep -E "PASSED|FAILED|ERROR|passed|failed" gpurun_out/gpu_tests_$TAG.log | tail -40
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { echo SMOKE FAILED; tail -20 gpurun_out/smoke_$TAG.log; exit 1; }
+tail -1 gpurun_out/smoke_$TAG.log
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo BENCH FAILED; tail -20 gpurun_out/bench_$TAG.err; exit 1; }
+cut -c1-1500 gpurun_out/bench_$TAG.json

@@ -246,6 +246,10 @@ def main():
     if args.batch <= 0:
         args.batch = default_batch
     world = make()
+    # status words are recorded on the device each step (no per-step host
+    # sync) and checked once after the timed region: a world whose step could
+    # not be the reference's fails the bench instead of being timed
+    world.setStatusPolicy("record")
     n = world.getNumDofs()
     st, f = sampler(world, args.batch, 1000 + rank)
     state = torch.tensor(st, device=dev)
@@ -258,10 +262,13 @@ def main():
 
     gather = (ws > 1) if args.gather_grads < 0 else bool(args.gather_grads)
 
+    status_acc = torch.zeros(args.batch, dtype=torch.int32, device=dev)
+
     def one_step(state):
         s = state.detach().requires_grad_(True)
         a = action.detach().requires_grad_(True)
         nxt = nimble.timestep(world, s, a)
+        status_acc.bitwise_or_(world.getLastStatus())
         nxt.backward(g)
         if gather and dist is not None:
             gather_grads(dist, a.grad, ws)
@@ -272,6 +279,9 @@ def main():
     timer.enabled = True
     state, elapsed = timed_loop(one_step, state, args.steps, 0, dist, dev)
     timer.enabled = False
+    bad = int(((status_acc & _native.ST_DIVERGES) != 0).sum().item())
+    if bad:
+        raise SystemExit(f"bench: {bad} world(s) left the reference's physics (status {_native.status_message(int(status_acc.max().item()))})")
     total = args.batch * ws * args.steps
     value = total / elapsed
     fwd_ms = timer.mean_ms(timer.fwd)

@@ -8,10 +8,12 @@ The summary is stored under the workload's key (bench.py --workload).
 
 FETCH_SIZE/WRITE_SIZE are reported by rocprofv3 in KiB.  Per
 MI355X_MICROARCH.md (HBM section) FETCH_SIZE counts half of the bytes of wide
-coalesced streaming reads on gfx950; the per-world rows this path reads are
-8-byte-per-lane accesses (uncalibrated width), so both the raw value and the
-x2-corrected upper estimate are recorded and `bytes_per_world` uses the
-corrected one (conservative: larger traffic)."""
+coalesced streaming reads on gfx950.  The per-world rows this path reads are
+8-byte-per-lane wave-contiguous accesses; tools/micro/bytes_calib.hip
+calibrates that width on a 512 MiB buffer (profiles/r02c_calib_*.csv):
+FETCH_SIZE = exactly 1/2 of the bytes for 8 B/lane reads as for 16 B/lane,
+WRITE_SIZE = exactly the bytes for 8 B/lane stores.  So `bytes_per_world`
+= 2 x FETCH_SIZE + WRITE_SIZE."""
 import csv
 import glob
 import json

@@ -79,3 +79,28 @@ for (a, b), nm in names.items():
         parts.append(f"{nm.strip()}={int(T1[b] - T1[a])} (batch {int(T[wi, b] - T[wi, a])})")
 print(f"solo world {wi}: " + " ".join(parts))
 print("      construct acc solo: iters %d cls %d Q %d codF %d codS %d nx %d valid %d | codF qr %d rz %d rank %d" % tuple(T1[60:70]))
+
+# per-world forward latency histogram of the last batch step (the kernel's
+# time is the slowest world's): written as JSON next to the log
+import json, os  # noqa: E402
+out = os.environ.get("STAGE_HIST_OUT")
+if out:
+    tot_all = np.where((T[:, 10] > 0) & (T[:, 13] > 0), T[:, 13] - T[:, 10], 0).astype(np.float64)
+    ok = tot_all > 0
+    v = tot_all[ok]
+    edges = np.linspace(0, v.max() * 1.0001, 21)
+    h, _ = np.histogram(v, bins=edges)
+    path = hd[:, 6]
+    res = {"worlds": int(ok.sum()), "unit": "shader clocks (s_memtime) per world, loadState..integratePositions",
+           "mean": float(v.mean()), "p50": float(np.percentile(v, 50)), "p90": float(np.percentile(v, 90)),
+           "p99": float(np.percentile(v, 99)), "max": float(v.max()), "max_over_mean": float(v.max() / v.mean()),
+           "bins_clk": [float(e) for e in edges], "counts": [int(c) for c in h],
+           "by_class": {
+               "no_contact": float(v[(hd[ok, 0] == 0)].mean()) if (hd[ok, 0] == 0).any() else None,
+               "short_circuit": float(v[(hd[ok, 0] > 0) & (path[ok] > 0)].mean()) if ((hd[ok, 0] > 0) & (path[ok] > 0)).any() else None,
+               "fallback": float(v[(hd[ok, 0] > 0) & (path[ok] == 0)].mean()) if ((hd[ok, 0] > 0) & (path[ok] == 0)).any() else None},
+           "slowest": [{"world": int(wi), "clk": float(tot_all[wi]), "rows": int(hd[wi, 1]), "clamping": int(hd[wi, 2]),
+                        "short_circuit": int(hd[wi, 6]), "dantzig_pivots": int(T[wi, 52]), "pgs_sweeps": int(T[wi, 54])}
+                       for wi in np.argsort(-tot_all)[:10]]}
+    json.dump(res, open(out, "w"), indent=1)
+    print("histogram ->", out, json.dumps({k: res[k] for k in ("mean", "p50", "p99", "max", "max_over_mean")}))

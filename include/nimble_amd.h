@@ -177,6 +177,26 @@ int nimble_backward(nimble_world_t world, int32_t batch, const double* state,
                     const double* grad_next_state, double* grad_state,
                     double* grad_forces, void* stream);
 
+/*
+ * Batched step Jacobians of a forward's snapshot, without bound clipping:
+ *   state_jacobian [batch][2n][2n]  d(next_state)/d(state) ==
+ *       BackpropSnapshot::getStateJacobian (dart/neural/BackpropSnapshot.cpp:1230):
+ *       [[posPos, velPos], [posVel, velVel]] (:1263, :1338, :762, :643)
+ *   force_jacobian [batch][2n][n]   d(next_state)/d(forces); its velocity rows
+ *       are getControlForceVelJacobian (:482), the columns of the action
+ *       space give getActionJacobian (:1245)
+ * Both are formed as 2n vector-Jacobian products per world (unit upstream
+ * gradients through the backward kernel), so they are exactly the matrices
+ * whose transposed products nimble_backward applies.
+ *   workspace  device buffer of nimble_jacobian_workspace_doubles(world,
+ *              batch) doubles (NULL when that is 0)
+ */
+int64_t nimble_jacobian_workspace_doubles(nimble_world_t world, int32_t batch);
+int nimble_jacobians(nimble_world_t world, int32_t batch, const double* state,
+                     const double* forces, const double* snapshot,
+                     double* state_jacobian, double* force_jacobian,
+                     double* workspace, void* stream);
+
 /* Last error message (thread-local). */
 const char* nimble_last_error(void);
 

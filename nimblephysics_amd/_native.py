@@ -39,6 +39,10 @@ def lib():
         L.nimble_backward.restype = C.c_int
         L.nimble_last_error.argtypes = []
         L.nimble_last_error.restype = C.c_char_p
+        L.nimble_jacobian_workspace_doubles.argtypes = [C.c_void_p, C.c_int32]
+        L.nimble_jacobian_workspace_doubles.restype = C.c_int64
+        L.nimble_jacobians.argtypes = [C.c_void_p, C.c_int32] + [C.c_void_p] * 6 + [C.c_void_p]
+        L.nimble_jacobians.restype = C.c_int
         L.nimble_num_collision_pairs.argtypes = [C.c_void_p]
         L.nimble_num_collision_pairs.restype = C.c_int32
         _lib = L
@@ -156,6 +160,24 @@ class DeviceWorld:
         self._shapes(B, grad_state)
         _check(lib().nimble_backward(self.h, B, _ptr(state), _ptr(forces), _ptr(snapshot), _ptr(grad_next),
                                      _ptr(grad_state), _ptr(grad_forces), C.c_void_p(stream_ptr)))
+
+
+    def jacobians(self, state, forces, snapshot, stream_ptr: int):
+        """(d next_state / d state [B, 2n, 2n], d next_state / d forces
+        [B, 2n, n]) of the forward that wrote `snapshot` (nimble_jacobians)."""
+        import torch
+        _require_device(state, forces, snapshot)
+        B = state.shape[0]
+        self._on_my_device(state, forces, snapshot)
+        self._shapes(B, state, forces, snapshot)
+        n = self.n
+        J = torch.empty((B, 2 * n, 2 * n), dtype=torch.float64, device=state.device)
+        F = torch.empty((B, 2 * n, n), dtype=torch.float64, device=state.device)
+        wsd = int(lib().nimble_jacobian_workspace_doubles(self.h, B))
+        ws = torch.empty(wsd, dtype=torch.float64, device=state.device) if wsd > 0 else None
+        _check(lib().nimble_jacobians(self.h, B, _ptr(state), _ptr(forces), _ptr(snapshot), _ptr(J), _ptr(F),
+                                      _ptr(ws), C.c_void_p(stream_ptr)))
+        return J, F
 
 
 def contact_flop_estimate(world, rows: float, clamping: float) -> dict:

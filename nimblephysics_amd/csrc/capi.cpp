@@ -31,6 +31,7 @@ struct nimble_world {
   Layout fwd, bwd;
   int snapDoubles = 8;
   int poolRows = 0, maxRows = 0;
+  int jacWsDoubles = 0;  // per-workgroup LCP workspace of the Jacobian launch
   int cacheDoubles = NIMBLE_MAX_LCP + 1;
   hipFunction_t dummy = nullptr;
 };
@@ -38,7 +39,7 @@ struct nimble_world {
 extern "C" __global__ void nimble_forward_kernel(const ModelDev*, Layout, int, const double*, const double*, double*,
                                                  double*, double*, int, int);
 extern "C" __global__ void nimble_backward_kernel(const ModelDev*, Layout, int, const double*, const double*,
-                                                  double*, int, const double*, double*, double*);
+                                                  double*, int, const double*, double*, double*, int, double*, int);
 
 static void isoInverse(const double* T, double* O) {
   // [R|p]^-1 = [R^T | -R^T p]
@@ -243,6 +244,9 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
   } else {
     w->snapDoubles = 8;
   }
+  // Jacobian launches run 2n items per world concurrently on one snapshot, so
+  // their off-chip LCP workspace is per workgroup instead of the snapshot tail
+  if (m.numPairs > 0 && bwdPoolDoublesHost(mcap, m.n) > w->bwd.poolCap) w->jacWsDoubles = bwdPoolDoublesHost(mcap, m.n);
   // dynamics cache at the tail of every snapshot
   w->fwd.snDyn = w->bwd.snDyn = w->snapDoubles;
   w->snapDoubles += dynCacheDoubles(m.n, m.nb);
@@ -296,7 +300,40 @@ int nimble_backward(nimble_world_t w, int32_t batch, const double* state, const 
   hipStream_t st = (hipStream_t)stream;
   const size_t lds = (size_t)w->bwd.total * sizeof(double);
   hipLaunchKernelGGL(nimble_backward_kernel, dim3(gridFor(batch)), dim3(64), lds, st, w->dev, w->bwd, batch, state,
-                     forces, snapshot, w->snapDoubles, grad_next_state, grad_state, grad_forces);
+                     forces, snapshot, w->snapDoubles, grad_next_state, grad_state, grad_forces, 1, (double*)nullptr, 0);
+  HIP_TRY(hipGetLastError());
+  return NIMBLE_OK;
+}
+
+// Workgroups of a Jacobian launch: enough to keep every SIMD of the chip
+// busy (items loop grid-stride), bounded so the per-workgroup workspace stays
+// small.
+#define JAC_GRID 8192
+
+int64_t nimble_jacobian_workspace_doubles(nimble_world_t w, int32_t batch) {
+  if (!w || batch < 0) return -1;
+  const long long items = (long long)batch * 2 * w->host.n;
+  const long long grid = items < JAC_GRID ? items : JAC_GRID;
+  return (int64_t)(grid * w->jacWsDoubles);
+}
+
+int nimble_jacobians(nimble_world_t w, int32_t batch, const double* state, const double* forces,
+                     const double* snapshot, double* state_jacobian, double* force_jacobian, double* workspace,
+                     void* stream) {
+  if (!w || batch < 0) return fail(NIMBLE_ERR_INVALID, "bad arguments");
+  if (batch == 0 || w->host.n == 0) return NIMBLE_OK;
+  if (!state || !forces || !snapshot || !state_jacobian || !force_jacobian)
+    return fail(NIMBLE_ERR_INVALID, "null buffer");
+  if (w->jacWsDoubles > 0 && !workspace)
+    return fail(NIMBLE_ERR_INVALID, "this model needs a Jacobian workspace (nimble_jacobian_workspace_doubles)");
+  const int rows = 2 * w->host.n;
+  const long long items = (long long)batch * rows;
+  const int grid = items < JAC_GRID ? (int)items : JAC_GRID;
+  hipStream_t st = (hipStream_t)stream;
+  const size_t lds = (size_t)w->bwd.total * sizeof(double);
+  hipLaunchKernelGGL(nimble_backward_kernel, dim3(grid), dim3(64), lds, st, w->dev, w->bwd, batch, state, forces,
+                     const_cast<double*>(snapshot), w->snapDoubles, (const double*)nullptr, state_jacobian,
+                     force_jacobian, rows, w->jacWsDoubles > 0 ? workspace : (double*)nullptr, w->jacWsDoubles);
   HIP_TRY(hipGetLastError());
   return NIMBLE_OK;
 }

@@ -486,28 +486,48 @@ __device__ void rightJacobianCol(const double* th, int k, double* o) {
   }
 }
 
+// `rows` upstream gradients per world: rows == 1 is backpropState with the
+// given gradNext [batch][2n]; rows == 2n (Jacobian mode) takes the unit
+// vectors e_r as upstream gradients (gradNext unused) and skips the bound
+// clipping, so item (world, r) of gradState / gradForces is row r of
+// d(next state)/d(state) / d(next state)/d(forces) -- the reference's
+// getStateJacobian / getControlForceVelJacobian (BackpropSnapshot.cpp:1230,
+// :482).  Items of one world then share its snapshot, so each item that
+// needs an off-chip LCP workspace uses its workgroup's slice of `ws`
+// (wsDoubles per workgroup; a workgroup runs its items one after another).
 extern "C" __global__ void __launch_bounds__(WAVE)
 nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, const double* __restrict__ state,
                        const double* __restrict__ forces, double* __restrict__ snapshot, int snapDoubles,
                        const double* __restrict__ gradNext, double* __restrict__ gradState,
-                       double* __restrict__ gradForces) {
+                       double* __restrict__ gradForces, int rows, double* __restrict__ ws, int wsDoubles) {
   extern __shared__ double s[];
   const ModelDev& md = *mdp;
   const int lane = threadIdx.x;
   const int n = md.n;
   const double dt = md.dt;
-  for (int env = blockIdx.x; env < batch; env += gridDim.x) {
+  const long long items = (long long)batch * rows;
+  for (long long item = blockIdx.x; item < items; item += gridDim.x) {
+    const int env = rows == 1 ? (int)item : (int)(item / rows);
+    const int unitRow = rows == 1 ? -1 : (int)(item - (long long)env * rows);
 #ifdef NIMBLE_STAGE_TIMING
     double* g_stamp = md.numPairs > 0 ? snapshot + (size_t)env * snapDoubles + snapWorkspaceOffset(n) + 1000 : nullptr;
 #endif
     STAMP(20);
     loadState(md, s, L, lane, state + (size_t)env * 2 * n, forces + (size_t)env * n);
-    const double* gN = gradNext + (size_t)env * 2 * n;
-    for (int i = lane; i < n; i += WAVE) {
-      s[L.gp + i] = gN[i];
-      s[L.gv + i] = gN[n + i];
+    if (unitRow < 0) {
+      const double* gN = gradNext + (size_t)env * 2 * n;
+      for (int i = lane; i < n; i += WAVE) {
+        s[L.gp + i] = gN[i];
+        s[L.gv + i] = gN[n + i];
+      }
+    } else {
+      for (int i = lane; i < n; i += WAVE) {
+        s[L.gp + i] = i == unitRow ? 1.0 : 0.0;
+        s[L.gv + i] = n + i == unitRow ? 1.0 : 0.0;
+      }
     }
     double* sn = snapshot + (size_t)env * snapDoubles;
+    double* hbmWs = ws != nullptr ? ws + (size_t)blockIdx.x * wsDoubles : sn + snapWorkspaceOffset(n);
     dynCacheCopy(md, s, L, sn + L.snDyn, false, lane);  // the forward's kinematics, IC, L, C
     STAMP(21);
     const int nc = md.numPairs > 0 ? uni((int)sn[SN_NC]) : 0;
@@ -519,7 +539,7 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
     if (nc > 0) {
       // constrained: a* = Minv (z + A_c_ub_E f_c) / dt, w <- w - nu
       const int need = bwdPoolDoubles(m, n);
-      carveBwd(need <= L.poolCap ? s + L.pool : sn + snapWorkspaceOffset(n), m, n, P);
+      carveBwd(need <= L.poolCap ? s + L.pool : hbmWs, m, n, P);
       imp = contactBackwardPrep(md, s, L, lane, sn, P, m, nc, s + L.ct);
     } else {
       // z = dt (tau - C - D v - K (q - q0 + dt v))
@@ -656,17 +676,20 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
       WSYNC();
     }
     if (k < n) {
-      // clipLossGradientsToBounds (BackpropSnapshot.cpp:425)
-      const double qk = s[L.q + k], vk = s[L.v + k], tk = s[L.tau + k];
-      if (qk == md.posLo[k] && gq > 0) gq = 0;
-      if (qk == md.posHi[k] && gq < 0) gq = 0;
-      if (vk == md.velLo[k] && gvOut > 0) gvOut = 0;
-      if (vk == md.velHi[k] && gvOut < 0) gvOut = 0;
-      if (tk == md.forceLo[k] && gt > 0) gt = 0;
-      if (tk == md.forceHi[k] && gt < 0) gt = 0;
-      gradState[(size_t)env * 2 * n + k] = gq;
-      gradState[(size_t)env * 2 * n + n + k] = gvOut;
-      gradForces[(size_t)env * n + k] = gt;
+      if (unitRow < 0) {
+        // clipLossGradientsToBounds (BackpropSnapshot.cpp:425); the
+        // Jacobian getters do not clip
+        const double qk = s[L.q + k], vk = s[L.v + k], tk = s[L.tau + k];
+        if (qk == md.posLo[k] && gq > 0) gq = 0;
+        if (qk == md.posHi[k] && gq < 0) gq = 0;
+        if (vk == md.velLo[k] && gvOut > 0) gvOut = 0;
+        if (vk == md.velHi[k] && gvOut < 0) gvOut = 0;
+        if (tk == md.forceLo[k] && gt > 0) gt = 0;
+        if (tk == md.forceHi[k] && gt < 0) gt = 0;
+      }
+      gradState[(size_t)item * 2 * n + k] = gq;
+      gradState[(size_t)item * 2 * n + n + k] = gvOut;
+      gradForces[(size_t)item * n + k] = gt;
     }
     WSYNC();
     STAMP(26);

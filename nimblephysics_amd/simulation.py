@@ -307,6 +307,26 @@ class World:
                 handles[idx] = (self._version, _native.DeviceWorld(self, idx))
         return handles[idx][1]
 
+    # --- step Jacobians at the current state (World.cpp:2190-2245) -------------
+    def getCachedBackpropSnapshot(self):
+        """neural.forwardPass(self, idempotent=True), re-run only when the
+        positions, velocities or control forces changed (World.cpp:2190)."""
+        from . import neural
+        key = (self.getPositions().tobytes(), self.getVelocities().tobytes(), self.getControlForces().tobytes(),
+               self._version)
+        cached = getattr(self, "_cached_snapshot_key", None)
+        if cached is None or cached[0] != key:
+            self._cached_snapshot_key = (key, neural.forwardPass(self, idempotent=True))
+        return self._cached_snapshot_key[1]
+
+    def getStateJacobian(self):
+        """d(next state)/d(state) [2n, 2n] at the current state (World.cpp:2210)."""
+        return self.getCachedBackpropSnapshot().getStateJacobian(self)
+
+    def getActionJacobian(self):
+        """d(next state)/d(action) [2n, |A|] at the current state (World.cpp:2227)."""
+        return self.getCachedBackpropSnapshot().getActionJacobian(self)
+
     # --- per-world status of the last batched step (see timestep.py) ----------
     def getLastStatus(self):
         """Status bits of each world of the last ``timestep`` call (a device

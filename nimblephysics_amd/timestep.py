@@ -93,6 +93,31 @@ def _check_status(world: World, dev, snap: torch.Tensor) -> None:
             f"their step would differ from the reference's (world.setStatusPolicy('record') to continue anyway)")
 
 
+def step_batch(world: World, st: torch.Tensor, act: torch.Tensor):
+    """One batched forward launch (neural::forwardPass on every row of the
+    2-D device tensors `st` [B, 2n] / `act` [B, |action space|]).  Returns
+    (device world, forces [B, n], next state [B, 2n], snapshot [B, S]); the
+    world's LCP warm-start caches advance and its status word is checked."""
+    B = st.shape[0]
+    n = world.getNumDofs()
+    if st.shape[1] != 2 * n:
+        raise ValueError(f"state has {st.shape[1]} columns, world expects {2 * n}")
+    idx = _action_index(world, st.device)
+    if act.shape[1] != idx.shape[0]:
+        raise ValueError(f"action has {act.shape[1]} columns, action space has {idx.shape[0]}")
+    dev = world.native(st.device)
+    forces = torch.zeros((B, n), dtype=torch.float64, device=st.device)
+    forces.index_copy_(1, idx, act.contiguous())
+    bs = _batch_state(world, B, dev, st.device)
+    nxt = torch.empty_like(st)
+    snap = torch.empty((B, dev.snapshot_doubles), dtype=torch.float64, device=st.device)
+    stream = torch.cuda.current_stream(st.device).cuda_stream
+    dev.forward(st, forces, bs.cache, nxt, snap, stream)
+    world._last_snapshot = snap  # the batched BackpropSnapshot of this step
+    _check_status(world, dev, snap)
+    return dev, forces, nxt, snap
+
+
 class TimestepLayer(torch.autograd.Function):
     @staticmethod
     def forward(ctx, world: World, state: torch.Tensor, action: torch.Tensor, mass: Optional[torch.Tensor]):
@@ -117,23 +142,9 @@ class TimestepLayer(torch.autograd.Function):
             st = state.detach().reshape(1, -1) if squeeze else state.detach()
             act = action.detach().reshape(1, -1) if squeeze else action.detach()
             st = st.contiguous()
-            B = st.shape[0]
             n = world.getNumDofs()
-            if st.shape[1] != 2 * n:
-                raise ValueError(f"state has {st.shape[1]} columns, world expects {2 * n}")
+            dev, forces, nxt, snap = step_batch(world, st, act)
             idx = _action_index(world, st.device)
-            if act.shape[1] != idx.shape[0]:
-                raise ValueError(f"action has {act.shape[1]} columns, action space has {idx.shape[0]}")
-            dev = world.native(st.device)
-            forces = torch.zeros((B, n), dtype=torch.float64, device=st.device)
-            forces.index_copy_(1, idx, act.contiguous())
-            bs = _batch_state(world, B, dev, st.device)
-            nxt = torch.empty_like(st)
-            snap = torch.empty((B, dev.snapshot_doubles), dtype=torch.float64, device=st.device)
-            stream = torch.cuda.current_stream(st.device).cuda_stream
-            dev.forward(st, forces, bs.cache, nxt, snap, stream)
-            world._last_snapshot = snap  # the batched BackpropSnapshot of this step
-            _check_status(world, dev, snap)
         ctx.world = world
         # the backward must run on the model (and snapshot layout) that
         # produced this snapshot, even if the world changes in between

@@ -126,6 +126,8 @@ void inverseDynamics(const World& w, const Kin<S>& k, const S* ddq, bool withGra
 void step(const World& w, const double* state, const double* tau, std::vector<double>& lcpCache,
           double* nextState, Snapshot& snap);
 void backprop(const World& w, const Snapshot& snap, const double* gradNext, double* gradState, double* gradTau);
+void stepJacobians(const World& w, const Snapshot& snap, double* posPos, double* posVel, double* velPos,
+                   double* velVel, double* forceVel);
 
 // contacts (oracle_contact.cpp)
 // *unsupported (optional) is set when a narrow-phase branch that is not

@@ -40,6 +40,7 @@ def lib():
         L.oracle_snapshots_destroy.argtypes = [vp]
         L.oracle_forward.argtypes = [vp, ip, dp, dp, dp, dp, vp]
         L.oracle_backward.argtypes = [vp, ip, vp, dp, dp, dp]
+        L.oracle_jacobians.argtypes = [vp, ip, vp, dp, dp]
         L.oracle_mass_matrix.argtypes = [vp, dp, dp]
         L.oracle_coriolis_gravity.argtypes = [vp, dp, dp, dp]
         L.oracle_forward_dynamics.argtypes = [vp, dp, dp, dp, dp]
@@ -139,6 +140,15 @@ class OracleWorld:
         gf = np.zeros((B, self.n))
         lib().oracle_backward(self.h, B, self.snaps, _p(g), _p(gs), _p(gf))
         return gs, gf
+
+    def jacobians(self):
+        """getStateJacobian [B, 2n, 2n] and d(next state)/d(tau) [B, 2n, n]
+        of the last forward (BackpropSnapshot.cpp:1230, :482)."""
+        B, n = self.batch, self.n
+        J = np.zeros((B, 2 * n, 2 * n))
+        F = np.zeros((B, 2 * n, n))
+        lib().oracle_jacobians(self.h, B, self.snaps, _p(J), _p(F))
+        return J, F
 
     def mass_matrix(self, q):
         q = np.ascontiguousarray(q, dtype=np.float64)

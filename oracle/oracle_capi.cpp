@@ -49,6 +49,30 @@ int oracle_backward(void* wp, int batch, void* snaps, const double* gradNext, do
   return 0;
 }
 
+// getStateJacobian [2n][2n] = [[posPos, velPos], [posVel, velVel]]
+// (BackpropSnapshot.cpp:1230) and d(next)/d(tau) [2n][n] = [0; forceVel]
+int oracle_jacobians(void* wp, int batch, void* snaps, double* stateJac, double* forceJac) {
+  World& w = *static_cast<World*>(wp);
+  auto& S = *static_cast<std::vector<OracleSnap>*>(snaps);
+  const int n = w.n;
+  std::vector<double> pp(n * n), pv(n * n), vp(n * n), vv(n * n), fv(n * n);
+  for (int b = 0; b < batch; b++) {
+    stepJacobians(w, S[b].s, pp.data(), pv.data(), vp.data(), vv.data(), fv.data());
+    double* J = stateJac + (size_t)b * 4 * n * n;
+    double* F = forceJac + (size_t)b * 2 * n * n;
+    for (int r = 0; r < n; r++)
+      for (int c = 0; c < n; c++) {
+        J[r * 2 * n + c] = pp[r * n + c];
+        J[r * 2 * n + n + c] = vp[r * n + c];
+        J[(n + r) * 2 * n + c] = pv[r * n + c];
+        J[(n + r) * 2 * n + n + c] = vv[r * n + c];
+        F[r * n + c] = 0.0;
+        F[(n + r) * n + c] = fv[r * n + c];
+      }
+  }
+  return 0;
+}
+
 // Debug getters (single world)
 void oracle_mass_matrix(void* wp, const double* q, double* M) {
   World& w = *static_cast<World*>(wp);

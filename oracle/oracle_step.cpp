@@ -2,6 +2,7 @@
 //
 // World::step (dart/simulation/World.cpp:221) and BackpropSnapshot::backprop
 // (dart/neural/BackpropSnapshot.cpp:121) restated on plain dense matrices.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -114,14 +115,16 @@ void step(const World& w, const double* state, const double* tau, std::vector<do
 // BackpropSnapshot::backprop (BackpropSnapshot.cpp:121) with
 // exploreAlternateStrategies == false: form posPos, posVel, velPos, velVel,
 // forceVel and multiply their transposes into the upstream gradient.
-void backprop(const World& w, const Snapshot& snap, const double* gradNext, double* gradState, double* gradTau) {
+// The five Jacobian blocks of the step (BackpropSnapshot::getPosPosJacobian
+// :1263, getPosVelJacobian :762, getVelPosJacobian :1338, getVelVelJacobian
+// :643, getControlForceVelJacobian :482), row-major n x n each.
+void stepJacobians(const World& w, const Snapshot& snap, double* posPosOut, double* posVelOut, double* velPosOut,
+                   double* velVelOut, double* forceVelOut) {
   const int n = w.n;
   const double dt = w.dt;
   const double* q = snap.q.data();
   const double* v = snap.v.data();
   const double* tau = snap.tau.data();
-  const double* gp = gradNext;
-  const double* gv = gradNext + n;
 
   Kin<double> k;
   k.compute(w, q, v);
@@ -184,6 +187,24 @@ void backprop(const World& w, const Snapshot& snap, const double* gradNext, doub
   w.velPosJac(q, v, velPos.data());
   // bounce approximation (BackpropSnapshot.cpp:1131) is identity without
   // restitution; restitution is not enabled on the hot path.
+  std::copy(posPos.begin(), posPos.end(), posPosOut);
+  std::copy(posVel.begin(), posVel.end(), posVelOut);
+  std::copy(velPos.begin(), velPos.end(), velPosOut);
+  std::copy(velVel.begin(), velVel.end(), velVelOut);
+  std::copy(forceVel.begin(), forceVel.end(), forceVelOut);
+}
+
+// BackpropSnapshot::backprop (:161-183): the transposed blocks times the
+// upstream gradient, then clipLossGradientsToBounds.
+void backprop(const World& w, const Snapshot& snap, const double* gradNext, double* gradState, double* gradTau) {
+  const int n = w.n;
+  const double* q = snap.q.data();
+  const double* v = snap.v.data();
+  const double* tau = snap.tau.data();
+  const double* gp = gradNext;
+  const double* gv = gradNext + n;
+  Mat posPos(n * n), posVel(n * n), velPos(n * n), velVel(n * n), forceVel(n * n);
+  stepJacobians(w, snap, posPos.data(), posVel.data(), velPos.data(), velVel.data(), forceVel.data());
 
   std::vector<double> lp(n), lv(n), lt(n), tmp(n);
   matTvec(posPos.data(), gp, lp.data(), n, n);

@@ -1,0 +1,128 @@
+"""BackpropSnapshot Jacobian getters on the device (nimble_jacobians) against
+the oracle's dense matrices (oracle_step.cpp stepJacobians: the reference's
+getPosPosJacobian / getPosVelJacobian / getVelPosJacobian / getVelVelJacobian
+/ getControlForceVelJacobian, BackpropSnapshot.cpp:1263/:762/:1338/:643/:482,
+assembled as getStateJacobian :1230 and getActionJacobian :1245).
+
+Tolerance: BASELINE.json's 1e-6 relative, per element, with an absolute
+floor of 1e-3 x the matrix's largest entry (see test_gpu_contact_parity._rel).
+"""
+import numpy as np
+import pytest
+import torch
+
+import models
+import nimblephysics_amd as nimble
+from oracle import oracle as O
+from test_gpu_contact_parity import RTOL, _check_contacts, _rel
+
+pytestmark = pytest.mark.gpu
+
+
+# FreeJoint's posPos / velPos blocks are central differences in the
+# reference itself (FreeJoint::finiteDifferencePosPosJacobian / VelPos,
+# FreeJoint.cpp:965, :987, eps 1e-6 / 1e-7): both sides carry the rounding
+# noise of the perturbed integrations divided by 2 eps (sin/cos and sums
+# round differently on the GPU), ~1e-10 absolute.  Those entries are compared
+# to an absolute 1e-8; every other entry to RTOL per element.
+FD_ATOL = 1e-8
+
+
+def _fd_mask(world):
+    d = world.desc_arrays()
+    n = world.getNumDofs()
+    mask = np.zeros((2 * n, 2 * n), dtype=bool)
+    for b, jt in enumerate(d["joint_type"]):
+        if int(jt) == 3:
+            o = int(d["dof_offset"][b])
+            mask[o:o + 6, o:o + 6] = True          # posPos
+            mask[o:o + 6, n + o:n + o + 6] = True  # velPos
+    return mask
+
+
+def _jac_err(J, R, mask):
+    """(per-element relative error off the FD blocks, max abs error on them)."""
+    Jm, Rm = np.where(mask, 0.0, J), np.where(mask, 0.0, R)
+    return _rel(Jm, Rm), float(np.abs(J - R)[mask].max(initial=0.0))
+
+
+def _batched(world, st, f):
+    d = torch.device("cuda:0")
+    ts, tf = torch.tensor(st, device=d), torch.tensor(f, device=d)
+    world._batch_state = None  # cold LCP caches, as the oracle's
+    snap = nimble.neural.forwardPass(world, state=ts, action=tf)
+    torch.cuda.synchronize()
+    return snap, ts, tf
+
+
+@pytest.mark.parametrize("name", ["cartpole", "kr5", "atlas_air"])
+def test_state_action_jacobians_no_contact(name):
+    world = {"cartpole": models.cartpole_world, "kr5": models.kr5_world,
+             "atlas_air": lambda: models.atlas_world(False)}[name]()
+    st, f = models.random_states(world, 16, seed=4)
+    ow = O.OracleWorld(world)
+    ow.forward(st, f)
+    RJ, RF = ow.jacobians()
+    snap, ts, tf = _batched(world, st, f)
+    J = snap.getStateJacobian(world).cpu().numpy()
+    F = snap.getActionJacobian(world).cpu().numpy()
+    assert J.shape == RJ.shape and F.shape == RF.shape
+    mask = _fd_mask(world)
+    for b in range(st.shape[0]):
+        rel, fd = _jac_err(J[b], RJ[b], mask)
+        assert rel < RTOL and fd < FD_ATOL, (b, rel, fd)
+        assert _rel(F[b], RF[b]) < RTOL, (b, _rel(F[b], RF[b]))
+    n = world.getNumDofs()
+    # the blocks are views of the same matrices
+    np.testing.assert_array_equal(snap.getVelVelJacobian(world).cpu().numpy(), J[:, n:, n:])
+    np.testing.assert_array_equal(snap.getPosVelJacobian(world).cpu().numpy(), J[:, n:, :n])
+    np.testing.assert_array_equal(snap.getControlForceVelJacobian(world).cpu().numpy(), F[:, n:, :])
+
+
+def test_state_action_jacobians_atlas_contact():
+    """1024 Atlas worlds on the ground (the bench batch): 67,584 Jacobian rows
+    in one launch, more than the 65,536-workgroup grid, so the kernel's
+    grid-stride loop runs; compared with the oracle on every world on the
+    oracle's LCP path."""
+    world = models.atlas_world(True)
+    B = 1024
+    st, f = models.random_states(world, B, seed=1000, q_scale=0.02, v_scale=0.05)
+    ow = O.OracleWorld(world)
+    ow.forward(st, f)
+    RJ, RF = ow.jacobians()
+    snap, ts, tf = _batched(world, st, f)
+    sn = world._last_snapshot.cpu().numpy()
+    same = _check_contacts(ow, sn, B, cache=world._batch_state.cache.cpu().numpy())
+    J = snap.getStateJacobian(world).cpu().numpy()
+    F = snap.getActionJacobian(world).cpu().numpy()
+    assert (sn[:, 0] > 0).mean() > 0.5
+    mask = _fd_mask(world)
+    errs = np.array([_jac_err(J[b], RJ[b], mask) for b in np.flatnonzero(same)])
+    worstF = max(_rel(F[b], RF[b]) for b in np.flatnonzero(same))
+    assert errs[:, 0].max() < RTOL and errs[:, 1].max() < FD_ATOL and worstF < RTOL, (errs.max(0), worstF)
+    # the Jacobian is the matrix whose transposed product backpropState
+    # applies (no clipping at these interior states)
+    g = torch.tensor(np.random.default_rng(2).standard_normal(st.shape), device=ts.device)
+    out = snap.backpropState(world, g)
+    vjp = torch.einsum("bij,bi->bj", torch.tensor(J, device=ts.device), g)
+    assert _rel(out.lossWrtState.cpu().numpy(), vjp.cpu().numpy()) < 1e-8
+
+
+def test_world_jacobians_single():
+    """World.getStateJacobian / getActionJacobian (World.cpp:2210 / :2227):
+    idempotent at the world's current state, 2-D numpy like the reference."""
+    world = models.kr5_world()
+    n = world.getNumDofs()
+    rng = np.random.default_rng(3)
+    world.setPositions(rng.standard_normal(n) * 0.3)
+    world.setVelocities(rng.standard_normal(n) * 0.3)
+    world.setControlForces(rng.standard_normal(n))
+    s0 = world.getState().copy()
+    J = world.getStateJacobian()
+    A = world.getActionJacobian()
+    assert J.shape == (2 * n, 2 * n) and A.shape == (2 * n, world.getActionSize())
+    np.testing.assert_array_equal(world.getState(), s0)  # idempotent
+    ow = O.OracleWorld(world)
+    ow.forward(s0[None], world.getControlForces()[None])
+    RJ, RF = ow.jacobians()
+    assert _rel(J, RJ[0]) < RTOL and _rel(A, RF[0]) < RTOL

@@ -106,6 +106,38 @@ def gather_grads(dist, grad, ws):
     return out
 
 
+def rank_inputs(world, sampler, batch, rank):
+    """Rank `rank`'s shard of the synthetic workload: its own `batch`
+    independent worlds (states, actions) and the upstream gradient of its
+    next states, seeded by the rank so the shards differ and are
+    reproducible."""
+    st, f = sampler(world, batch, 1000 + rank)
+    g = np.random.default_rng(rank).standard_normal(st.shape)
+    return st, f, g
+
+
+def make_step(timestep, world, action, g, gather, dist, ws, status_acc=None, gathered=None):
+    """One bench step on this rank's shard: `timestep` forward over the
+    batch, backward of the upstream gradient `g`, the per-world action
+    gradients all-gathered over the process group when `gather` (appended to
+    `gathered` when given), the state advanced to the next state."""
+
+    def one_step(state):
+        s = state.detach().requires_grad_(True)
+        a = action.detach().requires_grad_(True)
+        nxt = timestep(world, s, a)
+        if status_acc is not None:
+            status_acc.bitwise_or_(world.getLastStatus())
+        nxt.backward(g)
+        if gather and dist is not None:
+            out = gather_grads(dist, a.grad, ws)
+            if gathered is not None:
+                gathered.append(out)
+        return nxt.detach()
+
+    return one_step
+
+
 class KernelTimer:
     """HIP events around the native launches, on the stream they run on."""
 
@@ -251,10 +283,10 @@ def main():
     # not be the reference's fails the bench instead of being timed
     world.setStatusPolicy("record")
     n = world.getNumDofs()
-    st, f = sampler(world, args.batch, 1000 + rank)
+    st, f, g = rank_inputs(world, sampler, args.batch, rank)
     state = torch.tensor(st, device=dev)
     action = torch.tensor(f, device=dev)
-    g = torch.tensor(np.random.default_rng(rank).standard_normal(st.shape), device=dev)
+    g = torch.tensor(g, device=dev)
     cstats = contact_stats(world, state, action)
     devworld = world.native()
     timer = KernelTimer()
@@ -263,16 +295,7 @@ def main():
     gather = (ws > 1) if args.gather_grads < 0 else bool(args.gather_grads)
 
     status_acc = torch.zeros(args.batch, dtype=torch.int32, device=dev)
-
-    def one_step(state):
-        s = state.detach().requires_grad_(True)
-        a = action.detach().requires_grad_(True)
-        nxt = nimble.timestep(world, s, a)
-        status_acc.bitwise_or_(world.getLastStatus())
-        nxt.backward(g)
-        if gather and dist is not None:
-            gather_grads(dist, a.grad, ws)
-        return nxt.detach()
+    one_step = make_step(nimble.timestep, world, action, g, gather, dist, ws, status_acc)
 
     for _ in range(args.warmup):
         state = one_step(state)

@@ -76,7 +76,8 @@ def box_states(kind, batch, seed=0, size=(0.4, 0.3, 0.2)):
     """Box states in distinct contact regimes: 'rest' (flat, ~1 mm
     penetration, small velocities: sticking), 'slide' (tangential speed:
     friction at the cone bound -> upper-bound rows), 'tilt' (rotated about z:
-    two-point contact), 'lift' (separating velocity: nothing clamps)."""
+    two-point contact), 'lift' (separating velocity: nothing clamps), 'drop'
+    (falling onto the ground: bounces when restitution is on)."""
     rng = np.random.default_rng(seed)
     q = np.zeros((batch, 6))
     v = np.zeros((batch, 6))
@@ -94,8 +95,18 @@ def box_states(kind, batch, seed=0, size=(0.4, 0.3, 0.2)):
         q[:, 4] = 0.5 * (size[0] * np.sin(np.abs(ang)) + size[1] * np.cos(ang)) - 1e-3
     elif kind == "lift":
         v[:, 4] = 0.5 + 0.1 * rng.standard_normal(batch)
+    elif kind == "drop":
+        # falling onto the ground at ~1.5 m/s: with restitution the approach
+        # speed times the coefficient passes ContactConstraint's 0.1 bounce
+        # threshold
+        v[:, 4] = -1.5 + 0.2 * rng.standard_normal(batch)
     f = 0.5 * rng.standard_normal((batch, 6))
     return np.concatenate([q, v], axis=1), f
+
+
+def _box_sampler(world, batch, seed):
+    """bench-style sampler for box_world (resting boxes, random forces)."""
+    return box_states("rest", batch, seed=seed)
 
 
 def half_cheetah_world():

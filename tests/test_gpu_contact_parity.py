@@ -403,6 +403,79 @@ def test_contact_overflow_raises():
     assert ((status & 1) != 0).all()
 
 
+def test_restitution_bounce_parity():
+    """Restitution above DART_RESTITUTION_COEFF_THRESHOLD: a box dropped on
+    the ground at ~1.5 m/s with coefficients 0.8 x 0.8 gets the bounce
+    velocity in b (ContactConstraint.cpp:393 getInformation) and the
+    bounce diagonal 1 + e in the backward (BackpropSnapshot's
+    getBouncingConstraintMatrix); forward and gradients vs the oracle."""
+    world = models.box_world()
+    for s in range(2):
+        world.getSkeleton(s).getBodyNode(0).setRestitutionCoeff(0.8)
+    st, f = models.box_states("drop", 64, seed=7)
+    ow, snap = _parity(world, st, f)
+    bounced = 0
+    for b in range(st.shape[0]):
+        m = int(snap[b, SN_M])
+        rr = snap[b, SN_ROWS:SN_ROWS + SN_ROWREC * m].reshape(m, SN_ROWREC)
+        bounced += int((np.abs(rr[:, 11] - 1.64) < 1e-12).any())  # RR_BOUNCE = 1 + 0.8 * 0.8
+    assert bounced > st.shape[0] // 2, bounced
+    ref = ow.forward(st, f)
+    assert (ref[:, 6 + 4] > 0.5).mean() > 0.5  # the box leaves the ground upwards
+
+
+def test_penetration_correction_parity():
+    """setPenetrationCorrectionEnabled(True): the normal rows' b gets the
+    clamped penetration velocity min(depth * 0.01 / dt, 1e-3)
+    (ContactConstraint.cpp getInformation); resting and tilted boxes ~1 mm
+    into the ground, forward and gradients vs the oracle."""
+    world = models.box_world()
+    world.setPenetrationCorrectionEnabled(True)
+    for kind in ("rest", "tilt"):
+        st, f = models.box_states(kind, 48, seed=13)
+        _parity(world, st, f)
+    # and it changes the step: the same worlds without correction differ
+    st, f = models.box_states("rest", 8, seed=13)
+    on = O.OracleWorld(world).forward(st, f)
+    world.setPenetrationCorrectionEnabled(False)
+    off = O.OracleWorld(world).forward(st, f)
+    assert np.abs(on - off).max() > 1e-6
+
+
+def test_sequential_position_update_parity():
+    """setParallelVelocityAndPositionUpdates(False): positions integrate with
+    the post-constraint velocity (World.cpp:312 else-branch,
+    skel->integratePositions), on Atlas with foot contact; the reference's
+    BackpropSnapshot keeps its parallel-update Jacobians, as the oracle does."""
+    world = models.atlas_world(True)
+    world.setParallelVelocityAndPositionUpdates(False)
+    st, f = models.random_states(world, 48, seed=17, q_scale=0.01, v_scale=0.02)
+    _parity(world, st, f)
+    world.setParallelVelocityAndPositionUpdates(True)
+    par = O.OracleWorld(world).forward(st[:4], f[:4])
+    world.setParallelVelocityAndPositionUpdates(False)
+    seq = O.OracleWorld(world).forward(st[:4], f[:4])
+    assert np.abs(par - seq).max() > 1e-9
+
+
+def test_atlas_parity_bench_batch():
+    """configs[3] at the bench's size: 1024 Atlas worlds (the bench sampler's
+    perturbations), forward and gradients vs the oracle for every world."""
+    world = models.atlas_world(True)
+    st, f = models.random_states(world, 1024, seed=1000, q_scale=0.02, v_scale=0.05, f_scale=1.0)
+    ow, snap = _parity(world, st, f, max_diverge=0.01)
+    assert (snap[:, SN_NCON] > 0).mean() > 0.5
+
+
+def test_half_cheetah_parity_bench_batch():
+    """configs[2] at the bench's size: 4096 half-cheetah worlds, forward and
+    gradients vs the oracle for every world."""
+    world = models.half_cheetah_world()
+    st, f = models.half_cheetah_states(world, 4096, seed=1000)
+    ow, snap = _parity(world, st, f, max_diverge=0.01)
+    assert (snap[:, SN_NCON] > 0).mean() > 0.4
+
+
 def test_model_change_between_steps():
     """A body-mass change between two steps reaches the device model
     (dynamics setters invalidate the uploaded World): GPU == oracle on the

@@ -132,6 +132,94 @@ def test_bench_harness_gloo_two_ranks():
     assert abs(out[0][1] - out[1][1]) < 1e-12  # max over ranks agreed
 
 
+class _OracleTimestep(torch.autograd.Function):
+    """CPU stand-in for nimble.timestep in the multi-rank CPU test: the
+    oracle's forward / backward (the checker, test-only) behind the same
+    autograd signature, so bench's step, sharding and gather run for real."""
+
+    @staticmethod
+    def forward(ctx, ow, world, state, action):
+        n = world.getNumDofs()
+        forces = np.zeros((state.shape[0], n))
+        forces[:, world.getActionSpace()] = action.numpy()
+        ctx.ow, ctx.world = ow, world
+        return torch.from_numpy(ow.forward(state.numpy(), forces))
+
+    @staticmethod
+    def backward(ctx, grad):
+        gs, gf = ctx.ow.backward(grad.numpy())
+        return None, None, torch.from_numpy(gs), torch.from_numpy(gf[:, ctx.world.getActionSpace()])
+
+
+def _oracle_rollout_grads(world, rank, batch, steps):
+    """The action gradients of `steps` bench steps of rank `rank`'s shard,
+    computed in this process (no process group)."""
+    import bench
+    from oracle.oracle import OracleWorld
+    ow = OracleWorld(world)
+    st, f, g = bench.rank_inputs(world, models._box_sampler, batch, rank)
+    action, g = torch.from_numpy(f), torch.from_numpy(g)
+    grads = []
+
+    def ts(w, s, a):
+        out = _OracleTimestep.apply(ow, w, s, a)
+        return out
+
+    state = torch.from_numpy(st)
+    for _ in range(steps):
+        s = state.detach().requires_grad_(True)
+        a = action.detach().requires_grad_(True)
+        nxt = ts(world, s, a)
+        nxt.backward(g)
+        grads.append(a.grad.clone())
+        state = nxt.detach()
+    return grads
+
+
+def _rank_bench_main(rank, ws, port, batch, out):
+    import torch.distributed as dist
+    import bench
+    from oracle.oracle import OracleWorld
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    world = models.box_world()
+    ow = OracleWorld(world)
+    st, f, g = bench.rank_inputs(world, models._box_sampler, batch, rank)
+    gathered = []
+    step = bench.make_step(lambda w, s, a: _OracleTimestep.apply(ow, w, s, a), world, torch.from_numpy(f),
+                           torch.from_numpy(g), True, dist, ws, gathered=gathered)
+    state, elapsed = bench.timed_loop(step, torch.from_numpy(st), 2, 1, dist, torch.device("cpu"))
+    out[rank] = ([t.numpy() for t in gathered], elapsed)
+    dist.destroy_process_group()
+
+
+def test_bench_sharded_gather_gloo_two_ranks():
+    """bench.main's multi-GPU logic on CPU with real gradients: two gloo
+    ranks, each stepping its own shard of box-on-ground worlds fwd+bwd
+    (rank-seeded inputs, oracle timestep), all-gathering the per-world action
+    gradients every step.  The gathered [ws*B, m] tensor of every step equals
+    the concatenation of each rank's own gradients, recomputed here rank by
+    rank without a process group."""
+    import sys
+    import torch.multiprocessing as mp
+    sys.path.insert(0, ROOT)
+    mgr = mp.Manager()
+    out = mgr.dict()
+    port = _free_port()
+    B = 6
+    mp.spawn(_rank_bench_main, args=(2, port, B, out), nprocs=2, join=True)
+    world = models.box_world()
+    own = [_oracle_rollout_grads(world, r, B, 3) for r in range(2)]
+    for r in range(2):
+        gathered, _ = out[r]
+        assert len(gathered) == 3  # 1 warmup + 2 timed steps
+        for k in range(3):
+            want = np.concatenate([own[0][k].numpy(), own[1][k].numpy()])
+            assert gathered[k].shape == (2 * B, 6)
+            assert np.array_equal(gathered[k], want), (r, k)
+    assert not np.array_equal(own[0][0].numpy(), own[1][0].numpy())  # shards differ
+
+
 def test_dynamics_setters_invalidate_device_model():
     """Every model setter bumps the world's version, so the next step
     re-uploads the model (the reference's setters act on the next

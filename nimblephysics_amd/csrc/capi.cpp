@@ -88,9 +88,10 @@ static Layout makeLayout(const ModelDev& m, bool backward, int poolRows) {
     L.V = o; L.A = o + 6 * nb; L.IC = o + 12 * nb; L.F = o + 48 * nb;
     L.poolCap = 0;
     int area = dyn;
+    L.cscr = o + dyn;
     if (m.numPairs > 0) {
       const int cs = collideScratchDoubles(m.pairChunk);
-      if (cs > area) area = cs;
+      if (dyn + cs > area) area = dyn + cs;
       if (poolRows > 0) {
         L.poolCap = fwdPoolDoublesHost(poolRows, n);
         if (L.poolCap > area) area = L.poolCap;

@@ -368,6 +368,7 @@ __device__ inline void carveFwd(double* base, int m, int n, FwdPool& P) {
 #define H_K 11
 #define H_CODOK 12  // M1 + scr hold the COD of the final clamping Q
 #define H_HELPER 13 // 2 doubles = 4 ints: helper state, cancel, PGS ok (see helperWave)
+#define H_COLLIDE 15  // 2 ints: collision-detection hand-off between the waves (CS_*)
 #define H_PAIRCNT 16   // 16 per-pair counts of the current chunk
 
 // ---------------------------------------------------------------------------
@@ -407,6 +408,27 @@ __device__ __forceinline__ int helperWait(double* ct, Pred pred) {
   }
 }
 
+// Collision detection on the helper wave.  collideWorld only reads the
+// body transforms (kinematics) and writes the contact header / list and its
+// own scratch past the dynamics buffers, so it overlaps wave 0's composite
+// inertias, mass matrix, Cholesky factor and unconstrained velocity.  Per
+// world: wave 0 posts CS_GO after the kinematics, the helper answers CS_DONE,
+// wave 0 takes the contacts and resets to CS_IDLE before the next world.
+#define CS_IDLE 0
+#define CS_GO 1
+#define CS_DONE 2
+__device__ __forceinline__ int* collideFlag(double* ct) { return reinterpret_cast<int*>(ct + H_COLLIDE); }
+__device__ __forceinline__ void collidePost(double* ct, int state, int lane) {
+  if (lane == 0) __hip_atomic_store(collideFlag(ct), state, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void collideWait(double* ct, int want) {
+  for (long long it = 0;; it++) {
+    if (uni(__hip_atomic_load(collideFlag(ct), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == want) return;
+    if (it > (1ll << 24)) __builtin_trap();
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 // status bits
 #define ST_CONTACT_OVERFLOW 1
 #define ST_UNSUPPORTED_SHAPE 2
@@ -436,7 +458,7 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
                                              double* snapEdge, double* g_stamp = nullptr) {
   (void)g_stamp;
   double* ct = s + L.ct;
-  double* dropped = s + L.V;                            // alias area (dead V/A/IC/F)
+  double* dropped = s + L.cscr;                         // past the dynamics buffers
   double* pairbuf = dropped + CT_MAX_DROPPED * CREC;
   if (lane == 0) { ct[H_NCON] = 0; ct[H_NDROP] = 0; ct[H_STATUS] = 0; }
   WSYNC();
@@ -988,7 +1010,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
 // kernel-argument provenance (scalar loads, LDS instructions)
 __device__ __forceinline__ void contactStage(const ModelDev& md, double* s, const Layout& L, int lane, double* v1,
                                              const double* ddq, double* cache, double* snap, double* overflowWs,
-                                             bool helperOn) {
+                                             bool helperOn, bool collided) {
   const int n = md.n;
   s = lds<true>(s);
   snap = gbl(snap);
@@ -999,11 +1021,17 @@ __device__ __forceinline__ void contactStage(const ModelDev& md, double* s, cons
 #endif
   STAMP(0);
   double* ct = s + L.ct;
+  if (collided) {
+    // the helper wave ran the collision detection during the dynamics
+    collideWait(ct, CS_DONE);
+    collidePost(ct, CS_IDLE, lane);
+  } else {
 #ifdef NIMBLE_STAGE_TIMING
-  collideWorld(md, s, L, lane, snap + snEdge(n), g_stamp);
+    collideWorld(md, s, L, lane, snap + snEdge(n), g_stamp);
 #else
-  collideWorld(md, s, L, lane, snap + snEdge(n));
+    collideWorld(md, s, L, lane, snap + snEdge(n));
 #endif
+  }
   STAMP(1);
   const int nCon = uni((int)ct[H_NCON]);
   if (nCon == 0) {

@@ -53,5 +53,9 @@ struct Layout {
   int ct, v1, pool, poolCap, dinv;
   // offset (doubles) of the dynamics cache inside each world's snapshot
   int snDyn;
+  // forward: narrow-phase scratch (dropped list + pair buffers), placed past
+  // the dynamics buffers V/A/IC/F so the helper wave can run the collision
+  // detection while wave 0 is still in the dynamics
+  int cscr;
   int total;
 };

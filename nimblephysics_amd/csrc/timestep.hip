@@ -307,13 +307,20 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, con
     if (threadIdx.x == 0) {
       int* hf = reinterpret_cast<int*>(s + L.ct + H_HELPER);
       hf[0] = HS_IDLE; hf[1] = 0; hf[2] = 0;
+      *collideFlag(s + L.ct) = CS_IDLE;
     }
     __syncthreads();  // the one barrier both waves take: flags initialised
     if (threadIdx.x >= WAVE) {
       // the helper's work is speculative: it only takes issue slots the
       // step's wave leaves idle (lower wave priority on the shared SIMD)
       __builtin_amdgcn_s_setprio(0);
-      for (int env = blockIdx.x; env < batch; env += gridDim.x) helperWave(md, s, L, lane);
+      for (int env = blockIdx.x; env < batch; env += gridDim.x) {
+        double* ct = lds<true>(s) + L.ct;
+        collideWait(ct, CS_GO);
+        collideWorld(md, lds<true>(s), L, lane, snapshot + (size_t)env * snapDoubles + snEdge(n));
+        collidePost(ct, CS_DONE, lane);
+        helperWave(md, s, L, lane);
+      }
       return;
     }
     __builtin_amdgcn_s_setprio(2);
@@ -330,6 +337,8 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, con
 #else
     kinematics(md, s, L, lane, nullptr);
 #endif
+    // body transforms final: the helper wave detects the contacts meanwhile
+    if (helperOn) collidePost(lds<true>(s) + L.ct, CS_GO, lane);
     STAMP(14);
     composites(md, s, L, lane);
     STAMP(15);
@@ -358,7 +367,7 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, con
     if (md.numPairs > 0) {
       double* sn = snapshot + (size_t)env * snapDoubles;
       contactStage(md, s, L, lane, v1, x, lcpCache + (size_t)env * cacheDoubles, sn, sn + snapWorkspaceOffset(n),
-                   helperOn);
+                   helperOn, helperOn);
     }
     if (helperOn) helperRetire(s, L, lane);
     double* out = nextState + (size_t)env * 2 * n;

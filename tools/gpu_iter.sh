@@ -1,0 +1,18 @@
+#!/bin/bash
+# GPU-box iteration loop: the -m gpu suite, a short bench, the stage-timing
+# histogram (dbg/libnimble_dbg.so).  Usage: bash tools/gpu_iter.sh <tag> [pytest -k expr]
+set -o pipefail
+TAG=${1:-it}
+K=${2:-}
+export TMPDIR=/tmp
+O=gpurun_out
+mkdir -p $O
+if [ -n "$K" ]; then KA=(-k "$K"); else KA=(); fi
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread "${KA[@]}" > $O/gpu_tests_$TAG.log 2>&1
+rc=$?
+tail -3 $O/gpu_tests_$TAG.log
+[ $rc -ne 0 ] && { grep -E "Error|assert|FAILED" $O/gpu_tests_$TAG.log | head -20; exit $rc; }
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_$TAG.json 2> $O/bench_$TAG.err || { echo BENCH FAILED; tail -20 $O/bench_$TAG.err; exit 1; }
+python -c "import json;d=json.load(open('$O/bench_$TAG.json'));print('value',d['value'],'fwd',d['kernels_ms']['forward'],'bwd',d['kernels_ms']['backward'])"
+NIMBLE_AMD_LIB=dbg/libnimble_dbg.so STAGE_HIST_OUT=$O/stage_hist_$TAG.json timeout -k 10 120 python tools/stage_timing.py > $O/stage_$TAG.log 2>&1 || { echo STAGE FAILED; tail -20 $O/stage_$TAG.log; exit 1; }
+tail -1 $O/stage_$TAG.log

@@ -351,6 +351,39 @@ __device__ inline void carveFwd(double* base, int m, int n, FwdPool& P) {
 
 #include "lcp_wave.cuh"
 
+// A = Y^T Y (m x m, Y n x m row-major) with v_mfma_f64_16x16x4f64, one 16 x
+// 16 tile of A per MFMA chain over ceil(n / 4) k-steps (the upper tiles,
+// mirrored).  Operand lanes: A/B lane l = row / column l % 16 of the tile, k
+// = l / 16; result element e of lane l = tile row l / 16 + 4 e, column l % 16
+// (the f64 layout).  All 64 lanes must be active.  For the Atlas LCP (n = 33,
+// m = 24) this takes 5.3k clocks against 9.9k for the 8 x 8 VALU lane tiles
+// (tools/micro/mfma_gram.hip, profiles/r02e_mfma_gram_micro.json).
+typedef double nimble_double4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void gramMfma(const double* Y, double* A, int n, int m, int lane) {
+  const int i16 = lane & 15, kq = lane >> 4;
+  const int T = (m + 15) >> 4;
+  for (int ti = 0; ti < T; ti++)
+    for (int tj = ti; tj < T; tj++) {
+      nimble_double4 acc = {0.0, 0.0, 0.0, 0.0};
+      const int ri = ti * 16 + i16, cj = tj * 16 + i16;
+#pragma unroll 3
+      for (int k0 = 0; k0 < n; k0 += 4) {
+        const int k = k0 + kq;
+        const double a = (k < n && ri < m) ? Y[k * m + ri] : 0.0;
+        const double b = (k < n && cj < m) ? Y[k * m + cj] : 0.0;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const int r = ti * 16 + kq + 4 * e, c = tj * 16 + i16;
+        if (r < m && c < m && r <= c) {
+          A[r * m + c] = acc[e];
+          A[c * m + r] = acc[e];
+        }
+      }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Contact-stage LDS header (at Layout::ct) and snapshot layout.
 // ---------------------------------------------------------------------------
@@ -1145,7 +1178,9 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
     // Y = L^-1 J^T by columns (lane = column j): element (i, j) receives
     // -L_ik Y_kj for k = 0 .. i-1 in order and is then scaled by 1/L_ii --
     // the same operation sequence as the row-by-row elimination, without
-    // its two barriers per row
+    // its two barriers per row.  (Eight columns per pass held in registers
+    // with lane = dof row, readlane-broadcast like cholSolveReg, measured
+    // 1.5x slower here.)
     double* Y = P.massed;
     for (int j = lane; j < m; j += WAVE) {
       for (int i = 0; i < n; i++) {
@@ -1157,19 +1192,9 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
       }
     }
     WSYNC();
-    // A = Y^T Y (upper triangle computed, mirrored), 8 x 8 lane tiles
-    const int rl = lane >> 3, cl = lane & 7;
-    for (int r0 = 0; r0 < m; r0 += 8)
-      for (int c0 = r0; c0 < m; c0 += 8) {
-        const int r = r0 + rl, c = c0 + cl;
-        if (r < m && c < m && r <= c) {
-          double acc = 0;
-#pragma unroll 8
-          for (int i = 0; i < n; i++) acc += Y[i * m + r] * Y[i * m + c];
-          P.A[r * m + c] = acc;
-          P.A[c * m + r] = acc;
-        }
-      }
+    // A = Y^T Y on the matrix cores (the LCP matrix J Minv J^T)
+    gramMfma(Y, P.A, n, m, lane);
+    WSYNC();
   }
 
   // penetration correction / restitution bounce of the normal rows (lane = row)

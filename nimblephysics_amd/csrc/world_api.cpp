@@ -1,0 +1,451 @@
+// C++ World / Skeleton API surface (include/nimble_world.hpp) over the C-ABI.
+// Host code only: it flattens the object model into a nimble_world_desc the
+// way simulation.World.desc_arrays does on the Python side (same field
+// order and defaults), uploads it through nimble_world_create, and steps a
+// batch of one world through nimble_forward / nimble_backward /
+// nimble_jacobians on the current HIP device.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <string>
+
+#include "../../include/nimble_world.hpp"
+
+namespace nimble_amd {
+
+static void check(int rc, const char* what) {
+  if (rc != NIMBLE_OK) throw std::runtime_error(std::string(what) + ": " + nimble_last_error());
+}
+static void hipCheck(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+namespace dynamics {
+
+static const double kInf = std::numeric_limits<double>::infinity();
+
+// --- model-change propagation: every setter re-uploads the World's model ---
+void Skeleton::changed() {
+  if (mWorld) mWorld->touch();
+}
+void Joint::changed() { mSkel->changed(); }
+
+Joint::Joint(Skeleton* skel, int type, int dofs, const Properties& p)
+    : mSkel(skel), mType(type), mName(p.mName), mTp(p.mT_ParentBodyToJoint), mTc(p.mT_ChildBodyToJoint) {
+  mDamping.assign(dofs, 0.0);
+  mSpring.assign(dofs, 0.0);
+  mRest.assign(dofs, 0.0);
+  mPosLo.assign(dofs, -kInf);
+  mPosHi.assign(dofs, kInf);
+  mVelLo.assign(dofs, -kInf);
+  mVelHi.assign(dofs, kInf);
+  mForceLo.assign(dofs, -kInf);
+  mForceHi.assign(dofs, kInf);
+}
+void Joint::setTransformFromParentBodyNode(const Isometry3& T) { mTp = T; changed(); }
+void Joint::setTransformFromChildBodyNode(const Isometry3& T) { mTc = T; changed(); }
+void Joint::setDampingCoefficient(std::size_t i, double d) { mDamping.at(i) = d; changed(); }
+void Joint::setSpringStiffness(std::size_t i, double k) { mSpring.at(i) = k; changed(); }
+void Joint::setRestPosition(std::size_t i, double q0) { mRest.at(i) = q0; changed(); }
+void Joint::setPositionLowerLimit(std::size_t i, double v) { mPosLo.at(i) = v; changed(); }
+void Joint::setPositionUpperLimit(std::size_t i, double v) { mPosHi.at(i) = v; changed(); }
+void Joint::setVelocityLowerLimit(std::size_t i, double v) { mVelLo.at(i) = v; changed(); }
+void Joint::setVelocityUpperLimit(std::size_t i, double v) { mVelHi.at(i) = v; changed(); }
+void Joint::setControlForceLowerLimit(std::size_t i, double v) { mForceLo.at(i) = v; changed(); }
+void Joint::setControlForceUpperLimit(std::size_t i, double v) { mForceHi.at(i) = v; changed(); }
+
+static Vector3s normalized(const Vector3s& a) {
+  const double l = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+  if (!(l > 0)) throw std::invalid_argument("setAxis: zero axis");
+  return {a[0] / l, a[1] / l, a[2] / l};
+}
+void RevoluteJoint::setAxis(const Vector3s& axis) { mAxis = normalized(axis); changed(); }
+void PrismaticJoint::setAxis(const Vector3s& axis) { mAxis = normalized(axis); changed(); }
+
+void ShapeNode::setRelativeTransform(const Isometry3& T) {
+  mT = T;
+  mBody->mSkel->changed();
+}
+
+void BodyNode::setMass(double m) { mMass = m; mSkel->changed(); }
+void BodyNode::setLocalCOM(const Vector3s& c) { mCom = c; mSkel->changed(); }
+void BodyNode::setMomentOfInertia(double Ixx, double Iyy, double Izz, double Ixy, double Ixz, double Iyz) {
+  mMoment = {Ixx, Iyy, Izz, Ixy, Ixz, Iyz};
+  mSkel->changed();
+}
+void BodyNode::setFrictionCoeff(double f) { mFriction = f; mSkel->changed(); }
+void BodyNode::setRestitutionCoeff(double r) { mRestitution = r; mSkel->changed(); }
+ShapeNode* BodyNode::addShapeNode(const ShapePtr& shape, bool collision) {
+  mShapes.emplace_back(new ShapeNode(this, shape, collision));
+  mSkel->changed();
+  return mShapes.back().get();
+}
+
+BodyNode* Skeleton::getBodyNode(const std::string& name) const {
+  for (const auto& b : mBodies)
+    if (b->getName() == name) return b.get();
+  return nullptr;
+}
+void Skeleton::setMobile(bool mobile) { mMobile = mobile; changed(); }
+void Skeleton::setPositions(const VectorXs& q) {
+  if (q.size() != mQ.size()) throw std::invalid_argument("Skeleton::setPositions: size mismatch");
+  mQ = q;
+}
+void Skeleton::setVelocities(const VectorXs& v) {
+  if (v.size() != mV.size()) throw std::invalid_argument("Skeleton::setVelocities: size mismatch");
+  mV = v;
+}
+// dof offsets in body order; existing dofs keep their values, new ones start at 0
+void Skeleton::reindex() {
+  std::size_t off = 0;
+  for (auto& j : mJoints) {
+    j->mDofOffset = off;
+    off += j->getNumDofs();
+  }
+  mQ.resize(off, 0.0);
+  mV.resize(off, 0.0);
+  changed();
+}
+
+}  // namespace dynamics
+
+namespace simulation {
+
+World::~World() { release(); }
+
+void World::release() {
+  if (mHandle) nimble_world_destroy(mHandle);
+  mHandle = nullptr;
+  for (int k = 0; k < 5; k++) {
+    if (mDev[k]) (void)hipFree(mDev[k]);
+    mDev[k] = nullptr;
+    mDevDoubles[k] = 0;
+  }
+}
+
+std::string World::addSkeleton(const dynamics::SkeletonPtr& skel) {
+  if (skel->mWorld && skel->mWorld != this) throw std::invalid_argument("skeleton already belongs to a world");
+  skel->mWorld = this;
+  mSkels.push_back(skel);
+  mForces.resize(getNumDofs(), 0.0);
+  touch();
+  return skel->getName();
+}
+
+std::size_t World::getNumDofs() const {
+  std::size_t n = 0;
+  for (const auto& s : mSkels) n += s->getNumDofs();
+  return n;
+}
+
+VectorXs World::getPositions() const {
+  VectorXs q;
+  for (const auto& s : mSkels) q.insert(q.end(), s->mQ.begin(), s->mQ.end());
+  return q;
+}
+VectorXs World::getVelocities() const {
+  VectorXs v;
+  for (const auto& s : mSkels) v.insert(v.end(), s->mV.begin(), s->mV.end());
+  return v;
+}
+void World::setPositions(const VectorXs& q) {
+  if (q.size() != getNumDofs()) throw std::invalid_argument("World::setPositions: size mismatch");
+  std::size_t c = 0;
+  for (auto& s : mSkels)
+    for (auto& x : s->mQ) x = q[c++];
+}
+void World::setVelocities(const VectorXs& v) {
+  if (v.size() != getNumDofs()) throw std::invalid_argument("World::setVelocities: size mismatch");
+  std::size_t c = 0;
+  for (auto& s : mSkels)
+    for (auto& x : s->mV) x = v[c++];
+}
+VectorXs World::getState() const {
+  VectorXs st = getPositions();
+  const VectorXs v = getVelocities();
+  st.insert(st.end(), v.begin(), v.end());
+  return st;
+}
+void World::setState(const VectorXs& state) {
+  const std::size_t n = getNumDofs();
+  if (state.size() != 2 * n) throw std::invalid_argument("World::setState: size mismatch");
+  setPositions(VectorXs(state.begin(), state.begin() + n));
+  setVelocities(VectorXs(state.begin() + n, state.end()));
+}
+void World::setControlForces(const VectorXs& f) {
+  if (f.size() != getNumDofs()) throw std::invalid_argument("World::setControlForces: size mismatch");
+  mForces = f;
+}
+
+// simulation.World.desc_arrays, field by field
+const nimble_world_desc& World::describe() {
+  enum { PARENT, SKEL, JTYPE, DOFOFF, MOBILE, SHAPEBODY };
+  enum { TP, TC, AXIS, MASS, COM, MOMENT, FRIC, REST, DAMP, SPRING, RESTPOS, PLO, PHI, VLO, VHI, FLO, FHI, SSHAPE, ST };
+  for (auto& v : mI32) v.clear();
+  for (auto& v : mF64) v.clear();
+  std::vector<int32_t>& shapeType = mShapeTypes;
+  shapeType.clear();
+  int bodyBase = 0, dofBase = 0, nb = 0;
+  for (std::size_t si = 0; si < mSkels.size(); si++) {
+    const auto& s = *mSkels[si];
+    for (std::size_t k = 0; k < s.mBodies.size(); k++) {
+      const auto& b = *s.mBodies[k];
+      const auto& j = *b.mJoint;
+      int parent = -1;
+      for (std::size_t q = 0; q < s.mBodies.size(); q++)
+        if (s.mBodies[q].get() == b.mParent) parent = bodyBase + (int)q;
+      if (b.mParent && parent < 0) throw std::invalid_argument("describe: parent body of another skeleton");
+      mI32[PARENT].push_back(parent);
+      mI32[SKEL].push_back((int32_t)si);
+      mI32[JTYPE].push_back(j.mType);
+      mI32[DOFOFF].push_back(dofBase + (int32_t)j.mDofOffset);
+      mI32[MOBILE].push_back(s.mMobile ? 1 : 0);
+      mF64[TP].insert(mF64[TP].end(), j.mTp.m, j.mTp.m + 12);
+      mF64[TC].insert(mF64[TC].end(), j.mTc.m, j.mTc.m + 12);
+      mF64[AXIS].insert(mF64[AXIS].end(), j.mAxis.begin(), j.mAxis.end());
+      mF64[MASS].push_back(b.mMass);
+      mF64[COM].insert(mF64[COM].end(), b.mCom.begin(), b.mCom.end());
+      mF64[MOMENT].insert(mF64[MOMENT].end(), b.mMoment.begin(), b.mMoment.end());
+      mF64[FRIC].push_back(b.mFriction);
+      mF64[REST].push_back(b.mRestitution);
+      auto app = [&](int key, const VectorXs& v) { mF64[key].insert(mF64[key].end(), v.begin(), v.end()); };
+      app(DAMP, j.mDamping); app(SPRING, j.mSpring); app(RESTPOS, j.mRest);
+      app(PLO, j.mPosLo); app(PHI, j.mPosHi); app(VLO, j.mVelLo); app(VHI, j.mVelHi);
+      app(FLO, j.mForceLo); app(FHI, j.mForceHi);
+      for (const auto& node : b.mShapes) {
+        if (!node->mCollision) continue;
+        mI32[SHAPEBODY].push_back(bodyBase + (int32_t)k);
+        shapeType.push_back(node->mShape->kind());
+        const Vector3s& sz = node->mShape->size();
+        mF64[SSHAPE].insert(mF64[SSHAPE].end(), sz.begin(), sz.end());
+        mF64[ST].insert(mF64[ST].end(), node->mT.m, node->mT.m + 12);
+      }
+      nb++;
+    }
+    bodyBase += (int)s.mBodies.size();
+    dofBase += (int)s.getNumDofs();
+  }
+  if (nb > NIMBLE_MAX_BODIES || dofBase > NIMBLE_MAX_DOFS || (int)shapeType.size() > NIMBLE_MAX_SHAPES)
+    throw std::invalid_argument("describe: model too large for this path");
+  std::memset(&mDesc, 0, sizeof(mDesc));
+  mDesc.num_bodies = nb;
+  mDesc.num_dofs = dofBase;
+  mDesc.num_shapes = (int32_t)shapeType.size();
+  mDesc.dt = mDt;
+  for (int i = 0; i < 3; i++) mDesc.gravity[i] = mGravity[i];
+  mDesc.contact_clipping_depth = mClip;
+  mDesc.fallback_cfm = mCfm;
+  mDesc.penetration_correction = mPenCorr ? 1 : 0;
+  mDesc.parallel_pos_vel = mParallel ? 1 : 0;
+  mDesc.parent = mI32[PARENT].data();
+  mDesc.skeleton = mI32[SKEL].data();
+  mDesc.joint_type = mI32[JTYPE].data();
+  mDesc.dof_offset = mI32[DOFOFF].data();
+  mDesc.skeleton_mobile = mI32[MOBILE].data();
+  mDesc.T_parent_joint = mF64[TP].data();
+  mDesc.T_child_joint = mF64[TC].data();
+  mDesc.axis = mF64[AXIS].data();
+  mDesc.mass = mF64[MASS].data();
+  mDesc.com = mF64[COM].data();
+  mDesc.moment = mF64[MOMENT].data();
+  mDesc.friction = mF64[FRIC].data();
+  mDesc.restitution = mF64[REST].data();
+  mDesc.damping = mF64[DAMP].data();
+  mDesc.spring = mF64[SPRING].data();
+  mDesc.rest_position = mF64[RESTPOS].data();
+  mDesc.pos_lower = mF64[PLO].data();
+  mDesc.pos_upper = mF64[PHI].data();
+  mDesc.vel_lower = mF64[VLO].data();
+  mDesc.vel_upper = mF64[VHI].data();
+  mDesc.force_lower = mF64[FLO].data();
+  mDesc.force_upper = mF64[FHI].data();
+  mDesc.shape_body = mI32[SHAPEBODY].data();
+  mDesc.shape_type = mShapeTypes.data();
+  mDesc.shape_size = mF64[SSHAPE].data();
+  mDesc.shape_T = mF64[ST].data();
+  return mDesc;
+}
+
+nimble_world_t World::handle() {
+  if (mHandle && mBuiltVersion == mVersion) return mHandle;
+  if (mHandle) nimble_world_destroy(mHandle);
+  mHandle = nullptr;
+  const nimble_world_desc& d = describe();
+  check(nimble_world_create(&d, &mHandle), "nimble_world_create");
+  mBuiltVersion = mVersion;
+  return mHandle;
+}
+
+double* World::deviceBuffer(int k, std::size_t doubles) {
+  if (mDevDoubles[k] < doubles) {
+    if (mDev[k]) (void)hipFree(mDev[k]);
+    mDev[k] = nullptr;
+    hipCheck(hipMalloc(&mDev[k], (doubles ? doubles : 1) * sizeof(double)), "hipMalloc");
+    mDevDoubles[k] = doubles;
+  }
+  return mDev[k];
+}
+
+// one World::step on the device; the snapshot is copied out when asked for
+void World::runForward(std::vector<double>* snapshotOut) {
+  nimble_world_t h = handle();
+  const std::size_t n = getNumDofs();
+  const std::size_t snapD = (std::size_t)nimble_snapshot_doubles(h), cacheD = (std::size_t)nimble_lcp_cache_doubles(h);
+  if (mForces.size() != n) mForces.assign(n, 0.0);
+  if (mLcpCache.size() != cacheD) {
+    mLcpCache.assign(cacheD, 0.0);
+    mLcpCache[0] = -1;  // no warm start yet
+  }
+  const VectorXs st = getState();
+  double* dSt = deviceBuffer(0, 2 * n);
+  double* dF = deviceBuffer(1, n);
+  double* dC = deviceBuffer(2, cacheD);
+  double* dN = deviceBuffer(3, 2 * n);
+  double* dS = deviceBuffer(4, snapD);
+  hipCheck(hipMemcpy(dSt, st.data(), 2 * n * sizeof(double), hipMemcpyHostToDevice), "hipMemcpy");
+  hipCheck(hipMemcpy(dF, mForces.data(), n * sizeof(double), hipMemcpyHostToDevice), "hipMemcpy");
+  hipCheck(hipMemcpy(dC, mLcpCache.data(), cacheD * sizeof(double), hipMemcpyHostToDevice), "hipMemcpy");
+  check(nimble_forward(h, 1, dSt, dF, dC, dN, dS, nullptr), "nimble_forward");
+  hipCheck(hipDeviceSynchronize(), "nimble_forward");
+  VectorXs next(2 * n);
+  hipCheck(hipMemcpy(next.data(), dN, 2 * n * sizeof(double), hipMemcpyDeviceToHost), "hipMemcpy");
+  if (nimble_num_collision_pairs(h) > 0) {
+    double status = 0;
+    hipCheck(hipMemcpy(&status, dS + NIMBLE_SNAPSHOT_STATUS, sizeof(double), hipMemcpyDeviceToHost), "hipMemcpy");
+    const int bits = (int)status;
+    if (bits & (NIMBLE_STATUS_CONTACT_OVERFLOW | NIMBLE_STATUS_UNSUPPORTED_SHAPE | NIMBLE_STATUS_DROPPED_OVERFLOW))
+      throw ContactCapacityError("World::step: the contact set does not fit the batched path (status " +
+                                 std::to_string(bits) + ")");
+  }
+  if (snapshotOut) {
+    snapshotOut->resize(snapD);
+    hipCheck(hipMemcpy(snapshotOut->data(), dS, snapD * sizeof(double), hipMemcpyDeviceToHost), "hipMemcpy");
+  }
+  hipCheck(hipMemcpy(mLcpCache.data(), dC, cacheD * sizeof(double), hipMemcpyDeviceToHost), "hipMemcpy");
+  setState(next);
+}
+
+void World::step(bool resetCommand) {
+  runForward(nullptr);
+  if (resetCommand) mForces.assign(getNumDofs(), 0.0);
+}
+
+}  // namespace simulation
+
+namespace neural {
+
+std::shared_ptr<BackpropSnapshot> forwardPass(const simulation::WorldPtr& world, bool idempotent) {
+  auto snap = std::shared_ptr<BackpropSnapshot>(new BackpropSnapshot());
+  snap->mWorld = world;
+  snap->mN = world->getNumDofs();
+  snap->mState = world->getState();
+  snap->mForces = world->getControlForces();
+  if (snap->mForces.size() != snap->mN) snap->mForces.assign(snap->mN, 0.0);
+  const std::vector<double> cache = world->mLcpCache;
+  world->runForward(&snap->mSnapshot);
+  snap->mHandle = world->mHandle;
+  snap->mVersion = world->mVersion;
+  snap->mNext = world->getState();
+  if (idempotent) {
+    // RestorableSnapshot::restore
+    world->setState(snap->mState);
+    world->mLcpCache = cache;
+  } else {
+    // world->step(!idempotent): the commands are reset
+    world->mForces.assign(snap->mN, 0.0);
+  }
+  return snap;
+}
+
+// the snapshot belongs to the model it was taken on
+void BackpropSnapshot::checkModel(const char* what) const {
+  if (mWorld->mVersion != mVersion || mWorld->mHandle != mHandle)
+    throw std::runtime_error(std::string(what) + ": the world's model changed since forwardPass");
+}
+
+// uploads the step's inputs and snapshot (the World's device buffers may have
+// been reused by later steps)
+static void uploadStep(simulation::World& w, const VectorXs& st, const VectorXs& f, const std::vector<double>& snap,
+                       double*& dSt, double*& dF, double*& dS, std::size_t n) {
+  dSt = w.deviceBuffer(0, 2 * n);
+  dF = w.deviceBuffer(1, n);
+  dS = w.deviceBuffer(4, snap.size());
+  hipCheck(hipMemcpy(dSt, st.data(), 2 * n * sizeof(double), hipMemcpyHostToDevice), "hipMemcpy");
+  hipCheck(hipMemcpy(dF, f.data(), n * sizeof(double), hipMemcpyHostToDevice), "hipMemcpy");
+  hipCheck(hipMemcpy(dS, snap.data(), snap.size() * sizeof(double), hipMemcpyHostToDevice), "hipMemcpy");
+}
+
+void BackpropSnapshot::backpropState(const VectorXs& nextStateLossGrad, VectorXs& stateLossGrad,
+                                     VectorXs& forceLossGrad) const {
+  const std::size_t n = mN;
+  if (nextStateLossGrad.size() != 2 * n) throw std::invalid_argument("backpropState: gradient size mismatch");
+  checkModel("backpropState");
+  double *dSt, *dF, *dS;
+  uploadStep(*mWorld, mState, mForces, mSnapshot, dSt, dF, dS, n);
+  double* dG = mWorld->deviceBuffer(3, 2 * n);  // the next-state buffer is free here
+  double* dGs = mWorld->deviceBuffer(2, 2 * n > 1 ? 3 * n : 3 * n);
+  hipCheck(hipMemcpy(dG, nextStateLossGrad.data(), 2 * n * sizeof(double), hipMemcpyHostToDevice), "hipMemcpy");
+  double* dGf = dGs + 2 * n;
+  check(nimble_backward(mHandle, 1, dSt, dF, dS, dG, dGs, dGf, nullptr), "nimble_backward");
+  hipCheck(hipDeviceSynchronize(), "nimble_backward");
+  stateLossGrad.resize(2 * n);
+  forceLossGrad.resize(n);
+  hipCheck(hipMemcpy(stateLossGrad.data(), dGs, 2 * n * sizeof(double), hipMemcpyDeviceToHost), "hipMemcpy");
+  hipCheck(hipMemcpy(forceLossGrad.data(), dGf, n * sizeof(double), hipMemcpyDeviceToHost), "hipMemcpy");
+}
+
+void BackpropSnapshot::backprop(const LossGradient& next, LossGradient& prev) const {
+  const std::size_t n = mN;
+  VectorXs g(2 * n, 0.0), gs, gf;
+  for (std::size_t i = 0; i < n && i < next.lossWrtPosition.size(); i++) g[i] = next.lossWrtPosition[i];
+  for (std::size_t i = 0; i < n && i < next.lossWrtVelocity.size(); i++) g[n + i] = next.lossWrtVelocity[i];
+  backpropState(g, gs, gf);
+  prev.lossWrtPosition.assign(gs.begin(), gs.begin() + n);
+  prev.lossWrtVelocity.assign(gs.begin() + n, gs.end());
+  prev.lossWrtTorque = gf;
+}
+
+static void jacobians(const BackpropSnapshot& s, simulation::World& w, nimble_world_t h, const VectorXs& st,
+                      const VectorXs& f, const std::vector<double>& snap, std::size_t n, std::vector<double>& J,
+                      std::vector<double>& F) {
+  double *dSt, *dF, *dS;
+  uploadStep(w, st, f, snap, dSt, dF, dS, n);
+  (void)s;
+  double *dJ = nullptr, *dFj = nullptr, *dWs = nullptr;
+  hipCheck(hipMalloc(&dJ, 4 * n * n * sizeof(double)), "hipMalloc");
+  hipCheck(hipMalloc(&dFj, 2 * n * n * sizeof(double)), "hipMalloc");
+  const int64_t wsd = nimble_jacobian_workspace_doubles(h, 1);
+  if (wsd > 0) hipCheck(hipMalloc(&dWs, wsd * sizeof(double)), "hipMalloc");
+  const int rc = nimble_jacobians(h, 1, dSt, dF, dS, dJ, dFj, dWs, nullptr);
+  hipError_t e = hipDeviceSynchronize();
+  J.resize(4 * n * n);
+  F.resize(2 * n * n);
+  if (rc == NIMBLE_OK && e == hipSuccess) {
+    e = hipMemcpy(J.data(), dJ, J.size() * sizeof(double), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(F.data(), dFj, F.size() * sizeof(double), hipMemcpyDeviceToHost);
+  }
+  (void)hipFree(dJ);
+  (void)hipFree(dFj);
+  if (dWs) (void)hipFree(dWs);
+  check(rc, "nimble_jacobians");
+  hipCheck(e, "nimble_jacobians");
+}
+
+std::vector<double> BackpropSnapshot::getStateJacobian() const {
+  std::vector<double> J, F;
+  checkModel("getStateJacobian");
+  jacobians(*this, *mWorld, mHandle, mState, mForces, mSnapshot, mN, J, F);
+  return J;
+}
+
+std::vector<double> BackpropSnapshot::getForceJacobian() const {
+  std::vector<double> J, F;
+  checkModel("getForceJacobian");
+  jacobians(*this, *mWorld, mHandle, mState, mForces, mSnapshot, mN, J, F);
+  return F;
+}
+
+}  // namespace neural
+}  // namespace nimble_amd

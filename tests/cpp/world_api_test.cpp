@@ -1,0 +1,187 @@
+// Driver for tests/test_world_api.py: builds worlds through the C++ World /
+// Skeleton API (include/nimble_world.hpp) the way reference C++ code builds
+// them with dart::dynamics / dart::simulation, then
+//   world_api_test describe <box|pendulum>   prints the flattened
+//       nimble_world_desc as JSON (no GPU needed)
+//   world_api_test step <box|pendulum>       reads state [2n], forces [n] and an
+//       upstream gradient [2n] from stdin, runs neural::forwardPass, then
+//       BackpropSnapshot::backpropState and getStateJacobian / getForceJacobian,
+//       then two World::step calls; prints JSON.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <iostream>
+#include <string>
+#include <vector>
+
+#include "nimble_world.hpp"
+
+using namespace nimble_amd;
+
+// tests/models.py box_world: a free box over a static ground box
+static simulation::WorldPtr boxWorld() {
+  auto world = simulation::World::create();
+  world->setGravity({0, -9.81, 0});
+  auto box = dynamics::Skeleton::create("box");
+  auto pair = box->createJointAndBodyNodePair<dynamics::FreeJoint>();
+  dynamics::BodyNode* b = pair.second;
+  const double m = 1.0, sx = 0.4, sy = 0.3, sz = 0.2;
+  b->setMass(m);
+  b->setMomentOfInertia(m * (sy * sy + sz * sz) / 12, m * (sx * sx + sz * sz) / 12, m * (sx * sx + sy * sy) / 12);
+  b->createShapeNodeWith<dynamics::VisualAspect, dynamics::CollisionAspect, dynamics::DynamicsAspect>(
+      std::make_shared<dynamics::BoxShape>(Vector3s{sx, sy, sz}));
+  b->setFrictionCoeff(1.0);
+  world->addSkeleton(box);
+  auto ground = dynamics::Skeleton::create("ground");
+  auto gp = ground->createJointAndBodyNodePair<dynamics::WeldJoint>();
+  Isometry3 T = Isometry3::Identity();
+  T.setTranslation({0, -0.05, 0});
+  gp.first->setTransformFromParentBodyNode(T);
+  gp.second->createShapeNodeWith<dynamics::CollisionAspect>(std::make_shared<dynamics::BoxShape>(Vector3s{10.0, 0.1, 10.0}));
+  ground->setMobile(false);
+  world->addSkeleton(ground);
+  return world;
+}
+
+// a damped, sprung two-link pendulum on a prismatic cart (revolute axes off
+// the coordinate axes, joint offsets, COM offsets)
+static simulation::WorldPtr pendulumWorld() {
+  auto world = simulation::World::create();
+  world->setGravity({0, -9.81, 0});
+  world->setTimeStep(0.002);
+  auto sk = dynamics::Skeleton::create("pendulum");
+  auto cart = sk->createJointAndBodyNodePair<dynamics::PrismaticJoint>();
+  cart.first->setAxis({1, 0, 0});
+  cart.second->setMass(2.0);
+  dynamics::BodyNode* parent = cart.second;
+  for (int k = 0; k < 2; k++) {
+    dynamics::RevoluteJoint::Properties jp;
+    jp.mName = "hinge" + std::to_string(k);
+    auto link = sk->createJointAndBodyNodePair<dynamics::RevoluteJoint>(parent, jp);
+    link.first->setAxis({0.1 * k, 0.2, 1.0});
+    Isometry3 Tp = Isometry3::Identity();
+    Tp.setTranslation({0, k == 0 ? 0.0 : -0.5, 0});
+    link.first->setTransformFromParentBodyNode(Tp);
+    link.first->setDampingCoefficient(0, 0.05 * (k + 1));
+    link.first->setSpringStiffness(0, 0.5);
+    link.first->setRestPosition(0, 0.1);
+    link.second->setMass(0.5 + k);
+    link.second->setLocalCOM({0.01, -0.25, 0.0});
+    link.second->setMomentOfInertia(0.02, 0.01, 0.02, 0.001, 0.0, 0.0);
+    parent = link.second;
+  }
+  world->addSkeleton(sk);
+  return world;
+}
+
+static simulation::WorldPtr makeWorld(const std::string& name) {
+  if (name == "box") return boxWorld();
+  if (name == "pendulum") return pendulumWorld();
+  throw std::invalid_argument("unknown world " + name);
+}
+
+static void printArr(const char* key, const double* v, std::size_t n, bool comma = true) {
+  std::printf("\"%s\": [", key);
+  for (std::size_t i = 0; i < n; i++) std::printf("%s%.17g", i ? ", " : "", v[i]);
+  std::printf("]%s", comma ? ", " : "");
+}
+static void printArrI(const char* key, const int32_t* v, std::size_t n) {
+  std::printf("\"%s\": [", key);
+  for (std::size_t i = 0; i < n; i++) std::printf("%s%d", i ? ", " : "", v[i]);
+  std::printf("], ");
+}
+static void printVec(const char* key, const std::vector<double>& v, bool comma = true) {
+  printArr(key, v.data(), v.size(), comma);
+}
+
+static void describe(simulation::World& w) {
+  const nimble_world_desc& d = w.describe();
+  const std::size_t nb = d.num_bodies, n = d.num_dofs, ns = d.num_shapes;
+  std::printf("{\"num_bodies\": %d, \"num_dofs\": %d, \"num_shapes\": %d, \"dt\": %.17g, ", d.num_bodies, d.num_dofs,
+              d.num_shapes, d.dt);
+  printArr("gravity", d.gravity, 3);
+  std::printf("\"contact_clipping_depth\": %.17g, \"fallback_cfm\": %.17g, \"penetration_correction\": %d, "
+              "\"parallel_pos_vel\": %d, ", d.contact_clipping_depth, d.fallback_cfm, d.penetration_correction,
+              d.parallel_pos_vel);
+  printArrI("parent", d.parent, nb);
+  printArrI("skeleton", d.skeleton, nb);
+  printArrI("joint_type", d.joint_type, nb);
+  printArrI("dof_offset", d.dof_offset, nb);
+  printArrI("skeleton_mobile", d.skeleton_mobile, nb);
+  printArr("T_parent_joint", d.T_parent_joint, 12 * nb);
+  printArr("T_child_joint", d.T_child_joint, 12 * nb);
+  printArr("axis", d.axis, 3 * nb);
+  printArr("mass", d.mass, nb);
+  printArr("com", d.com, 3 * nb);
+  printArr("moment", d.moment, 6 * nb);
+  printArr("friction", d.friction, nb);
+  printArr("restitution", d.restitution, nb);
+  printArr("damping", d.damping, n);
+  printArr("spring", d.spring, n);
+  printArr("rest_position", d.rest_position, n);
+  printArr("pos_lower", d.pos_lower, n);
+  printArr("pos_upper", d.pos_upper, n);
+  printArr("vel_lower", d.vel_lower, n);
+  printArr("vel_upper", d.vel_upper, n);
+  printArr("force_lower", d.force_lower, n);
+  printArr("force_upper", d.force_upper, n);
+  printArrI("shape_body", d.shape_body, ns);
+  printArrI("shape_type", d.shape_type, ns);
+  printArr("shape_size", d.shape_size, 3 * ns);
+  printArr("shape_T", d.shape_T, 12 * ns, false);
+  std::printf("}\n");
+}
+
+int main(int argc, char** argv) {
+  if (argc < 3) {
+    std::fprintf(stderr, "usage: %s describe|step box|pendulum\n", argv[0]);
+    return 2;
+  }
+  try {
+    const std::string mode = argv[1];
+    auto world = makeWorld(argv[2]);
+    if (mode == "describe") {
+      describe(*world);
+      return 0;
+    }
+    const std::size_t n = world->getNumDofs();
+    std::vector<double> st(2 * n), f(n), g(2 * n);
+    for (auto& x : st) std::cin >> x;
+    for (auto& x : f) std::cin >> x;
+    for (auto& x : g) std::cin >> x;
+    if (!std::cin) throw std::runtime_error("short input");
+    world->setState(st);
+    world->setControlForces(f);
+    auto snap = neural::forwardPass(world, false);
+    std::vector<double> gs, gf;
+    snap->backpropState(g, gs, gf);
+    neural::LossGradient next, prev;
+    next.lossWrtPosition.assign(g.begin(), g.begin() + n);
+    next.lossWrtVelocity.assign(g.begin() + n, g.end());
+    snap->backprop(next, prev);
+    const std::vector<double> J = snap->getStateJacobian(), F = snap->getForceJacobian();
+    std::printf("{");
+    printVec("next", snap->getPostStepState());
+    printVec("world_state", world->getState());
+    printVec("grad_state", gs);
+    printVec("grad_forces", gf);
+    printVec("prev_pos", prev.lossWrtPosition);
+    printVec("prev_vel", prev.lossWrtVelocity);
+    printVec("prev_torque", prev.lossWrtTorque);
+    printVec("state_jacobian", J);
+    printVec("force_jacobian", F);
+    // two plain World::step calls continue the rollout (forces reset after
+    // the first, as Skeleton::resetCommands)
+    world->setControlForces(f);
+    world->step();
+    printVec("step2", world->getState());
+    world->step();
+    printVec("step3", world->getState());
+    printVec("forces_after", world->getControlForces(), false);
+    std::printf("}\n");
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "world_api_test: %s\n", e.what());
+    return 1;
+  }
+  return 0;
+}

@@ -1,0 +1,120 @@
+"""The C++ World / Skeleton API surface (include/nimble_world.hpp,
+nimblephysics_amd/csrc/world_api.cpp), driven by tests/cpp/world_api_test:
+
+* CPU: a world built through the C++ classes (Skeleton::create,
+  createJointAndBodyNodePair<FreeJoint / WeldJoint / PrismaticJoint /
+  RevoluteJoint>, BodyNode / Joint setters, createShapeNodeWith<...,
+  CollisionAspect>) flattens to the same nimble_world_desc as the same world
+  built through the Python mirror;
+* GPU: neural::forwardPass, BackpropSnapshot::backpropState / backprop /
+  getStateJacobian and World::step through the C++ API match the oracle.
+"""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import models
+import nimblephysics_amd as nimble
+from nimblephysics_amd import dynamics as D
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "tests", "cpp", "world_api_test")
+
+
+def _run(*args, stdin=None):
+    if not os.path.exists(EXE):
+        pytest.fail(f"{EXE} missing: run __graft_entry__.build()")
+    r = subprocess.run([EXE, *args], input=stdin, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    txt = r.stdout.replace("-inf", "-Infinity").replace("inf", "Infinity")
+    return json.loads(txt)
+
+
+def pendulum_world():
+    """tests/cpp/world_api_test.cpp pendulumWorld, through the Python mirror."""
+    w = nimble.World()
+    w.setGravity([0, -9.81, 0])
+    w.setTimeStep(0.002)
+    sk = D.Skeleton("pendulum")
+    j, cart = sk.createPrismaticJointAndBodyNodePair()
+    j.setAxis([1, 0, 0])
+    cart.setMass(2.0)
+    parent = cart
+    for k in range(2):
+        j, b = sk.createRevoluteJointAndBodyNodePair(parent)
+        j.setAxis([0.1 * k, 0.2, 1.0])
+        T = np.eye(4)
+        T[1, 3] = 0.0 if k == 0 else -0.5
+        j.setTransformFromParentBodyNode(T)
+        j.setDampingCoefficient(0, 0.05 * (k + 1))
+        j.setSpringStiffness(0, 0.5)
+        j.setRestPosition(0, 0.1)
+        b.setMass(0.5 + k)
+        b.setLocalCOM([0.01, -0.25, 0.0])
+        b.setMomentOfInertia(0.02, 0.01, 0.02, 0.001, 0.0, 0.0)
+        parent = b
+    w.addSkeleton(sk)
+    return w
+
+
+WORLDS = {"box": models.box_world, "pendulum": pendulum_world}
+
+
+@pytest.mark.parametrize("name", sorted(WORLDS))
+def test_cpp_world_describes_like_python(name):
+    got = _run("describe", name)
+    want = WORLDS[name]().desc_arrays()
+    assert set(got) == set(want), set(got) ^ set(want)
+    for k, v in want.items():
+        a, b = np.asarray(got[k], dtype=np.float64), np.asarray(v, dtype=np.float64)
+        assert a.shape == b.reshape(-1).shape or a.shape == b.shape, (k, a.shape, b.shape)
+        assert np.array_equal(a.reshape(-1), b.reshape(-1)), k
+
+
+def _inputs(world, seed):
+    n = world.getNumDofs()
+    rng = np.random.default_rng(seed)
+    if n == 6:  # the box resting ~1 mm into the ground
+        st, f = models.box_states("rest", 1, seed=seed)
+        st, f = st[0], f[0]
+    else:
+        st = np.concatenate([0.3 * rng.standard_normal(n), 0.5 * rng.standard_normal(n)])
+        f = rng.standard_normal(n)
+    g = rng.standard_normal(2 * n)
+    return st, f, g
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(WORLDS))
+def test_cpp_world_steps_match_oracle(name):
+    from oracle.oracle import OracleWorld
+    world = WORLDS[name]()
+    n = world.getNumDofs()
+    st, f, g = _inputs(world, 3)
+    txt = " ".join(repr(float(x)) for x in np.concatenate([st, f, g]))
+    out = _run("step", name, stdin=txt)
+    ow = OracleWorld(world)
+    ref = ow.forward(st[None], f[None])[0]
+    rgs, rgf = ow.backward(g[None])
+    J, F = ow.jacobians()
+    tol = 1e-9
+
+    def close(a, b):
+        a, b = np.asarray(a), np.asarray(b)
+        return np.abs(a - b).max() <= tol * max(1.0, np.abs(b).max())
+
+    assert close(out["next"], ref) and close(out["world_state"], ref)
+    assert close(out["grad_state"], rgs[0]) and close(out["grad_forces"], rgf[0])
+    assert close(out["prev_pos"], rgs[0][:n]) and close(out["prev_vel"], rgs[0][n:])
+    assert close(out["prev_torque"], rgf[0])
+    assert close(np.reshape(out["state_jacobian"], (2 * n, 2 * n)), J[0])
+    assert close(np.reshape(out["force_jacobian"], (2 * n, n)), F[0])
+    # World::step continues the rollout: forces applied once, then reset;
+    # the LCP warm start carries over as in the oracle
+    s2 = ow.forward(ref[None], f[None])[0]
+    s3 = ow.forward(s2[None], np.zeros((1, n)))[0]
+    assert close(out["step2"], s2) and close(out["step3"], s3)
+    assert np.all(np.asarray(out["forces_after"]) == 0)

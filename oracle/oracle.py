@@ -64,6 +64,8 @@ def lib():
         L.oracle_cod_solve.argtypes = [dp, ip, ip, dp, dp]
         L.oracle_box_box.argtypes = [dp, dp, dp, dp, dp]
         L.oracle_box_box.restype = ip
+        L.oracle_collide_pair.argtypes = [ip, dp, dp, ip, dp, dp, C.c_double, dp, ip]
+        L.oracle_collide_pair.restype = ip
         pi = C.POINTER(ip)
         L.oracle_lcp_reduce.argtypes = [ip, dp, dp, dp, dp, dp, pi, dp, dp, dp, dp, dp, pi, pi]
         L.oracle_lcp_reduce.restype = ip
@@ -288,6 +290,31 @@ def capsule_box(size, T_box, height, radius, T_capsule, box_first=True, clip=0.0
     tb, tc = (np.ascontiguousarray(np.asarray(T, dtype=np.float64)[:3, :4]) for T in (T_box, T_capsule))
     k = lib().oracle_capsule_box(_p(s), _p(tb), C.c_double(height), C.c_double(radius), _p(tc),
                                  1 if box_first else 0, C.c_double(clip), _p(out))
+    unsupported = k < 0
+    if k < 0:
+        k = -1 - k
+    return out[:k], unsupported
+
+
+SHAPE_TYPES = {"box": 0, "sphere": 1, "capsule": 2}
+
+
+def collide_pair(shape1, T1, shape2, T2, clip=0.03):
+    """One shape pair through the oracle's detector dispatch (the reference's
+    collide<Shape1, Shape2> of DARTCollide.cpp).  shapeK = (kind, size) with
+    kind box / sphere / capsule and size as in nimble_world_desc (box full
+    size; sphere (r,); capsule (r, h)).  Rows of (point3, normal3, depth,
+    type) in this package's type numbering, and an `unsupported` flag."""
+    out = np.zeros((16, 8))
+    sz = []
+    for kind, size in (shape1, shape2):
+        v = np.zeros(3)
+        s_ = np.atleast_1d(np.asarray(size, dtype=np.float64))
+        v[:len(s_)] = s_
+        sz.append(v)
+    t1, t2 = (np.ascontiguousarray(np.asarray(T, dtype=np.float64)[:3, :4]) for T in (T1, T2))
+    k = lib().oracle_collide_pair(SHAPE_TYPES[shape1[0]], _p(sz[0]), _p(t1), SHAPE_TYPES[shape2[0]], _p(sz[1]),
+                                  _p(t2), C.c_double(clip), _p(out), 16)
     unsupported = k < 0
     if k < 0:
         k = -1 - k

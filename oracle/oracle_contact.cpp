@@ -1257,3 +1257,51 @@ void constrainedJacobians(const World& w, const Kin<double>& k, const Snapshot& 
 }
 
 }  // namespace oracle
+
+// One shape pair through the same dispatch as collide() (the collide<Shape1,
+// Shape2> functions of DARTCollide.cpp): shape types / sizes as in
+// nimble_world_desc, world transforms 3x4 row-major.  Output per contact:
+// point3, normal3, depth, type (this package's numbering); returns the count,
+// or -1 - count when a branch that is not restated was taken.
+extern "C" int oracle_collide_pair(int type1, const double* size1, const double* T1r, int type2, const double* size2,
+                                   const double* T2r, double clip, double* out, int maxc) {
+  using namespace oracle;
+  Iso<double> T1, T2;
+  for (int r = 0; r < 3; r++) {
+    for (int c = 0; c < 3; c++) { T1.R(r, c) = T1r[r * 4 + c]; T2.R(r, c) = T2r[r * 4 + c]; }
+    T1.p[r] = T1r[r * 4 + 3];
+    T2.p[r] = T2r[r * 4 + 3];
+  }
+  std::vector<Contact> pair;
+  int unsup = 0;
+  if (type1 == NIMBLE_SHAPE_BOX && type2 == NIMBLE_SHAPE_BOX) {
+    double A[3] = {0.5 * size1[0], 0.5 * size1[1], 0.5 * size1[2]};
+    double Bh[3] = {0.5 * size2[0], 0.5 * size2[1], 0.5 * size2[2]};
+    boxBox(T1.p.x, T1.R.m, A, T2.p.x, T2.R.m, Bh, clip, pair, 0, 1, 0, 1);
+  } else if (type1 == NIMBLE_SHAPE_BOX && type2 == NIMBLE_SHAPE_CAPSULE) {
+    capsuleBox(T1, size1, T2, size2[0], size2[1], true, clip, 0, 1, 0, 1, pair, &unsup);
+  } else if (type1 == NIMBLE_SHAPE_CAPSULE && type2 == NIMBLE_SHAPE_BOX) {
+    capsuleBox(T2, size2, T1, size1[0], size1[1], false, clip, 0, 1, 0, 1, pair, &unsup);
+  } else if (type1 == NIMBLE_SHAPE_SPHERE && type2 == NIMBLE_SHAPE_BOX) {
+    sphereBoxPair(T2, size2, T1.p.x, size1[0], false, clip, 0, 1, 0, 1, pair);
+  } else if (type1 == NIMBLE_SHAPE_BOX && type2 == NIMBLE_SHAPE_SPHERE) {
+    sphereBoxPair(T1, size1, T2.p.x, size2[0], true, clip, 0, 1, 0, 1, pair);
+  } else if (type1 == NIMBLE_SHAPE_SPHERE && type2 == NIMBLE_SHAPE_SPHERE) {
+    sphereSphere(T1.p.x, size1[0], T2.p.x, size2[0], clip, 0, 1, 0, 1, pair);
+  } else if (type1 == NIMBLE_SHAPE_SPHERE && type2 == NIMBLE_SHAPE_CAPSULE) {
+    sphereCapsule(T1.p.x, size1[0], T2, size2[0], size2[1], true, clip, 0, 1, 0, 1, pair);
+  } else if (type1 == NIMBLE_SHAPE_CAPSULE && type2 == NIMBLE_SHAPE_SPHERE) {
+    sphereCapsule(T2.p.x, size2[0], T1, size1[0], size1[1], false, clip, 0, 1, 0, 1, pair);
+  } else if (type1 == NIMBLE_SHAPE_CAPSULE && type2 == NIMBLE_SHAPE_CAPSULE) {
+    capsuleCapsule(T1, size1[0], size1[1], T2, size2[0], size2[1], clip, 0, 1, 0, 1, pair);
+  } else {
+    return -1;
+  }
+  const int k = (int)pair.size() < maxc ? (int)pair.size() : maxc;
+  for (int c = 0; c < k; c++) {
+    for (int i = 0; i < 3; i++) { out[8 * c + i] = pair[c].point[i]; out[8 * c + 3 + i] = pair[c].normal[i]; }
+    out[8 * c + 6] = pair[c].depth;
+    out[8 * c + 7] = pair[c].type;
+  }
+  return unsup ? -1 - k : k;
+}

@@ -517,3 +517,40 @@ def twin_states(batch, seed=0):
     v[:, 3] += rng.choice([0.0, 1.0], batch) * (1 + 0.2 * rng.standard_normal(batch))
     f = 0.5 * rng.standard_normal((batch, 6))
     return np.concatenate([q, v], axis=1), f
+
+
+def known_answer_world(case, order="ab"):
+    """A world holding the two shapes of a collider known-answer case
+    (tests/golden/collide_known_answers.json) in detector order `order`: the
+    first shape on a static welded body at its pose, the second on a free
+    body whose state is its pose (rotation vector, translation).  No gravity:
+    one forward detects the contacts of exactly that pose.  Returns the world
+    and the state row."""
+    from nimblephysics_amd import dynamics as D
+    first, second = (case["a"], case["b"]) if order == "ab" else (case["b"], case["a"])
+
+    def shape(spec):
+        kind, size = spec
+        if kind == "box":
+            return D.BoxShape(size)
+        if kind == "sphere":
+            return D.SphereShape(size[0])
+        return D.CapsuleShape(size[0], size[1])
+
+    w = nimble.World()
+    w.setGravity([0, 0, 0])
+    s0 = D.Skeleton("first")
+    j0, b0 = s0.createWeldJointAndBodyNodePair()
+    j0.setTransformFromParentBodyNode(np.array(first[1]))
+    b0.createShapeNode(shape(first[0]), collision=True)
+    s0.setMobile(False)
+    w.addSkeleton(s0)
+    s1 = D.Skeleton("second")
+    _, b1 = s1.createFreeJointAndBodyNodePair()
+    b1.createShapeNode(shape(second[0]), collision=True)
+    w.addSkeleton(s1)
+    T = np.array(second[1])
+    st = np.zeros(12)
+    st[:3] = _rotvec(T[:3, :3])
+    st[3:6] = T[:3, 3]
+    return w, st

@@ -492,3 +492,31 @@ def test_model_change_between_steps():
     ref2 = O.OracleWorld(world).forward(st, f)
     assert np.abs(out2 - out1).max() > 1e-9
     assert _rel(out2, ref2) < RTOL
+
+
+@pytest.mark.parametrize("order", ["ab", "ba"])
+def test_collider_known_answers_on_device(order):
+    """The device narrow phase on the reference's collider known answers
+    (tests/golden/collide_known_answers.json: test_DARTCollide.cpp capsule-
+    capsule T / X / L, capsule-sphere end / side, sphere-box vertex / edge /
+    face), each pose one world, both detector orders: contact count, type,
+    point, normal and depth as the reference's tests expect."""
+    import json
+    import os
+    d = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                                    "collide_known_answers.json")))
+    for case in d["cases"]:
+        check = case.get("check", ["point", "normal", "depth"])
+        w, st = models.known_answer_world(case, order)
+        _, snap, _, _, _ = _device_step(w, st[None], np.zeros((1, 6)))
+        sn = snap.cpu().numpy()[0]
+        exp = case[order]
+        nc = int(sn[SN_NCON])
+        assert nc == len(exp), (case["name"], nc)
+        got = sn[SN_CONTACTS:SN_CONTACTS + CREC * nc].reshape(nc, CREC)
+        for c, e in zip(got, exp):
+            if "point" in check:
+                assert np.allclose(c[:3], e["point"], atol=1e-10), case["name"]
+            assert np.allclose(c[3:6], e["normal"], atol=1e-10), case["name"]
+            assert abs(c[6] - e["depth"]) < 1e-8, case["name"]
+            assert (int(c[7]) & 15) == e["type"], case["name"]

@@ -278,3 +278,35 @@ def test_capsule_capsule_gradients_vs_finite_differences(oracle_built, mode):
     gs, gf, fd_s, fd_f = _fd_check(w, st, f, g)
     assert np.abs(gs - fd_s).max() <= 1e-6 * np.abs(fd_s).max()
     assert np.abs(gf - fd_f).max() <= 1e-6 * np.abs(fd_f).max()
+
+
+def _check_known(cs, exp, check, tag):
+    assert len(cs) == len(exp), (tag, cs)
+    for c, e in zip(cs, exp):
+        if "point" in check:
+            assert np.allclose(c[:3], e["point"], atol=1e-10), tag
+        assert np.allclose(c[3:6], e["normal"], atol=1e-10), tag
+        assert abs(c[6] - e["depth"]) < 1e-8, tag
+        assert (int(c[7]) & 15) == e["type"], tag
+
+
+def test_collider_known_answers(oracle_built):
+    """collideCapsuleCapsule (T / X / L), collideCapsuleSphere /
+    collideSphereCapsule (end / side) and the sphere-box collider on the
+    reference's sphere vertex / edge / face geometry, both detector orders,
+    vs the reference's known answers (tests/golden/collide_known_answers.json,
+    made by make_collide_known_answers.py from test_DARTCollide.cpp)."""
+    d = json.load(open(os.path.join(GOLD, "collide_known_answers.json")))
+    for case in d["cases"]:
+        check = case.get("check", ["point", "normal", "depth"])
+        for order in ("ab", "ba"):
+            first, second = (case["a"], case["b"]) if order == "ab" else (case["b"], case["a"])
+            cs, unsupported = O.collide_pair(tuple(first[0]), np.array(first[1]), tuple(second[0]),
+                                             np.array(second[1]))
+            assert not unsupported
+            _check_known(cs, case[order], check, (case["name"], order))
+            # the same pose through a whole world (pair loop, postProcess)
+            w, st = models.known_answer_world(case, order)
+            o = O.OracleWorld(w)
+            o.forward(st[None], np.zeros((1, 6)))
+            _check_known(O.contacts(o, 0), case[order], check, (case["name"], order, "world"))

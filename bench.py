@@ -332,9 +332,11 @@ def main():
                          "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP64_VECTOR_PEAK_TFLOPS,
                          "traffic": traffic, "traffic_source": traffic_src,
                          "flops_per_world": flops[dom],
-                         "note": "peak = MI355X fp64 vector (VALU) rate; the kernel issues no MFMA "
-                                 "(DESIGN.md: fp64 MFMA measured, rejected); traffic = HBM bytes per launch "
-                                 "from the committed rocprofv3 PMC summary of this kernel"},
+                         "note": "peak = MI355X fp64 vector (VALU) rate, which on MI355X equals the fp64 "
+                                 "matrix-core rate; the forward's one dense product (the LCP matrix A = Y^T Y) runs "
+                                 "on v_mfma_f64_16x16x4f64, everything else on the VALU; traffic = HBM bytes per "
+                                 "launch (2 x FETCH_SIZE + WRITE_SIZE, separate rocprofv3 --pmc passes) from the "
+                                 "committed summary profiles/pmc_traffic.json (tools/gpu_measure.sh)"},
         }
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(make, 16, sampler)

@@ -58,6 +58,13 @@ def _action_index(world: World, device) -> torch.Tensor:
     return cached[1]
 
 
+def _identity_action(world: World, n: int) -> bool:
+    """True when the action space is every dof in order (the default), so
+    actions are the control forces themselves."""
+    space = world.getActionSpace()
+    return len(space) == n and all(int(a) == k for k, a in enumerate(space))
+
+
 def _batch_state(world: World, batch: int, dev, device) -> BatchState:
     bs = getattr(world, "_batch_state", None)
     if bs is None or bs.batch != batch or bs.cache.device != device or bs.cache.shape[1] != dev.cache_doubles:
@@ -106,8 +113,11 @@ def step_batch(world: World, st: torch.Tensor, act: torch.Tensor):
     if act.shape[1] != idx.shape[0]:
         raise ValueError(f"action has {act.shape[1]} columns, action space has {idx.shape[0]}")
     dev = world.native(st.device)
-    forces = torch.zeros((B, n), dtype=torch.float64, device=st.device)
-    forces.index_copy_(1, idx, act.contiguous())
+    if _identity_action(world, n):
+        forces = act.contiguous()  # every dof actuated, in order: no scatter
+    else:
+        forces = torch.zeros((B, n), dtype=torch.float64, device=st.device)
+        forces.index_copy_(1, idx, act.contiguous())
     bs = _batch_state(world, B, dev, st.device)
     nxt = torch.empty_like(st)
     snap = torch.empty((B, dev.snapshot_doubles), dtype=torch.float64, device=st.device)
@@ -146,6 +156,7 @@ class TimestepLayer(torch.autograd.Function):
             dev, forces, nxt, snap = step_batch(world, st, act)
             idx = _action_index(world, st.device)
         ctx.world = world
+        ctx.identity = _identity_action(world, world.getNumDofs())
         # the backward must run on the model (and snapshot layout) that
         # produced this snapshot, even if the world changes in between
         ctx.dev = dev
@@ -173,7 +184,7 @@ class TimestepLayer(torch.autograd.Function):
             gf = torch.empty_like(forces)
             stream = torch.cuda.current_stream(st.device).cuda_stream
             dev.backward(st, forces, snap, g, gs, gf, stream)
-            ga = gf.index_select(1, idx)
+            ga = gf if idx.shape[0] == gf.shape[1] and ctx.identity else gf.index_select(1, idx)
         od = ctx.out_device
         gm = torch.zeros(ctx.mass_shape, dtype=torch.float64, device=ctx.mass_device) if ctx.use_mass else None
         if ctx.squeeze:

@@ -10,7 +10,10 @@
 //   :1482 (TOP/BOTTOM half-space clip) / collideSphereBox :1655, or the
 //   pipe-face branch: ccdPointsAtWitnessBox :2060, createCapsuleMeshContact
 //   :3366, createFaceFaceContacts :2203.
-// The vertex-pipe / edge-pipe branches and EDGE_PIPE contacts are flagged
+// createCapsuleMeshContact's vertex-pipe (:3071) and non-parallel edge-pipe
+// (:3225) branches and its face branch's edge intersections (EDGE_PIPE /
+// PIPE_EDGE, :3320 / :3494) are restated; an edge parallel to the pipe
+// (:3118) and a zero penetration direction (8 witness points) are flagged
 // (ST_UNSUPPORTED_SHAPE) and dropped, as in the oracle.
 //
 // Output record (CREC doubles): point3 normal3 depth type bodyA bodyB
@@ -28,6 +31,10 @@
 #define CT_SPHERE_PIPE 7
 #define CT_PIPE_SPHERE 8
 #define CT_PIPE_PIPE 9
+#define CT_PIPE_VERTEX 10
+#define CT_VERTEX_PIPE 11
+#define CT_PIPE_EDGE 12
+#define CT_EDGE_PIPE 13
 
 namespace cap {
 
@@ -388,21 +395,77 @@ DEV bool contains(V pt, const V* s, int n, V o, V bx, V by) {
   }
   return true;
 }
-DEV bool lineIntersect(P2 p, P2 p1, P2 q, P2 q1) {
+// get2DLineIntersection (DARTCollide.cpp:3790), with its intersection point
+// (the collinear branch's out = p + s t, as written there)
+DEV bool lineIntersect(P2 p, P2 p1, P2 q, P2 q1, P2& out) {
   const double rx = p1.x - p.x, ry = p1.y - p.y, sx = q1.x - q.x, sy = q1.y - q.y;
   const double rs = cross2(rx, ry, sx, sy);
   if (rs == 0 && cross2(q.x - p.x, q.y - p.y, rx, ry) == 0) {
     const double rr = rx * rx + ry * ry;
     const double t0 = ((q.x - p.x) * rx + (q.y - p.y) * ry) / rr;
     const double t1 = ((q.x + sx - p.x) * rx + (q.y + sy - p.y) * ry) / rr;
-    return (t0 >= 0 && t0 <= 1) || (t1 >= 0 && t1 <= 1);
+    if (t0 >= 0 && t0 <= 1) { out = {p.x + sx * t0, p.y + sy * t0}; return true; }
+    if (t1 >= 0 && t1 <= 1) { out = {p.x + sx * t1, p.y + sy * t1}; return true; }
+    return false;
   } else if (rs == 0) {
     return false;
   }
   const double t = cross2(q.x - p.x, q.y - p.y, sx, sy) / rs;
   const double u = cross2(p.x - q.x, p.y - q.y, rx, ry) / cross2(sx, sy, rx, ry);
-  return t >= 0 && t <= 1 && u >= 0 && u <= 1;
+  if (t >= 0 && t <= 1 && u >= 0 && u <= 1) { out = {p.x + t * rx, p.y + t * ry}; return true; }
+  return false;
 }
+// math::getContactPoint (Geometry.cpp:1075) via dLineClosestApproach (:1042)
+DEV V lineContactPoint(V pA, V uA, V pB, V uB, double rA, double rB) {
+  const V p = sub(pB, pA);
+  const double uaub = dot(uA, uB), q1 = dot(uA, p), q2 = -dot(uB, p);
+  double d = 1 - uaub * uaub, alpha = 0, beta = 0;
+  if (d > 0) {
+    d = 1.0 / d;
+    alpha = (q1 + uaub * q2) * d;
+    beta = (uaub * q1 + q2) * d;
+  }
+  return scl(add(scl(add(pA, scl(uA, alpha)), rB), scl(add(pB, scl(uB, beta)), rA)), 1.0 / (rA + rB));
+}
+// dSegmentsClosestApproach (DARTCollide.cpp:301): segment pa -> pb against ua -> ub
+DEV void segClosest(V pa, V ua, V pb, V ub, double& alpha, double& beta) {
+  const V u = sub(pb, pa), v = sub(ub, ua), w = sub(pa, ua);
+  const double a = dot(u, u), b = dot(u, v), c = dot(v, v), d = dot(u, w), e = dot(v, w);
+  const double D = a * c - b * b;
+  double sN, sD = D, tN, tD = D;
+  if (D < 1e-15) {
+    sN = 0.0; sD = 1.0; tN = e; tD = c;
+  } else {
+    sN = b * e - c * d;
+    tN = a * e - b * d;
+    if (sN < 0.0) { sN = 0.0; tN = e; tD = c; }
+    else if (sN > sD) { sN = sD; tN = e + b; tD = c; }
+  }
+  if (tN < 0.0) {
+    tN = 0.0;
+    if (-d < 0.0) sN = 0.0;
+    else if (-d > a) sN = sD;
+    else { sN = -d; sD = a; }
+  } else if (tN > tD) {
+    tN = tD;
+    if ((-d + b) < 0.0) sN = 0;
+    else if ((-d + b) > a) sN = sD;
+    else { sN = -d + b; sD = a; }
+  }
+  alpha = fabs(sN) < 1e-15 ? 0.0 : sN / sD;
+  beta = fabs(tN) < 1e-15 ? 0.0 : tN / tD;
+}
+// pipe-mesh contact record: point, normal, depth, type; [10..12] pipe closest
+// point; tail: PIPE_VERTEX / VERTEX_PIPE pipe fixed point, pipe direction;
+// PIPE_EDGE / EDGE_PIPE edge A fixed point, edge A direction, pipe fixed
+// point, pipe direction (the edge's closest point is the contact point)
+DEV void pipeRecord(double* out, V point, V normal, double depth, int type, V pipeClosest) {
+  out[0] = point.x; out[1] = point.y; out[2] = point.z;
+  out[3] = normal.x; out[4] = normal.y; out[5] = normal.z;
+  out[6] = depth; out[7] = type;
+  out[10] = pipeClosest.x; out[11] = pipeClosest.y; out[12] = pipeClosest.z;
+}
+DEV void put3(double* o, V v) { o[0] = v.x; o[1] = v.y; o[2] = v.z; }
 
 }  // namespace cap
 
@@ -649,8 +712,43 @@ __device__ __noinline__ int deviceCapsuleBox(const double* Tb, const double* bs,
                      (k & 1) ? box.s2 * -0.5 : box.s2 * 0.5);
       if (maxDot - nm * dot(l, ld) < 0.01) W[nw++] = xf(box.T, l);  // DART_COLLISION_WITNESS_PLANE_DEPTH
     }
-    if (nw <= 2 || nw > 4) { *unsup = 1; return 0; }
     const V capA = xf(capo.T, mk(0, 0, h / 2)), capB = xf(capo.T, mk(0, 0, -h / 2));
+    const V axis = sub(capB, capA);
+    if (nw == 1) {
+      // vertex-pipe (createCapsuleMeshContact :3071): dDistPointToSegment
+      const double c1 = dot(sub(W[0], capA), axis), c2 = dot(axis, axis);
+      const double alpha = c1 <= 0 ? 0.0 : (c2 <= c1 ? 1.0 : c1 / c2);
+      const V nearest = add(capA, scl(axis, alpha));
+      V nv = eigNormalized(sub(nearest, W[0]));
+      if (boxFirst) nv = scl(nv, -1.0);
+      const double dep = r - sqrt(len2(sub(W[0], nearest)));
+      if (dep > clip) return 0;
+      pipeRecord(out, W[0], nv, dep, boxFirst ? CT_VERTEX_PIPE : CT_PIPE_VERTEX, nearest);
+      put3(out + CREC, capA);
+      put3(out + CREC + 3, eigNormalized(axis));
+      out[8] = body1; out[9] = body2;
+      return 1;
+    }
+    if (nw == 2) {
+      const V pipeDir = eigNormalized(axis), edgeDir = eigNormalized(sub(W[1], W[0]));
+      // an edge parallel to the pipe (:3118) is not restated
+      if (fabs(1.0 - fabs(dot(pipeDir, edgeDir))) < 1e-5) { *unsup = 1; return 0; }
+      // edge-pipe (:3225)
+      double alpha, beta;
+      segClosest(W[0], capA, W[1], capB, alpha, beta);
+      const V ec = add(W[0], scl(sub(W[1], W[0]), alpha)), pc = add(capA, scl(axis, beta));
+      const V nv = eigNormalized(sub(ec, pc));
+      const double dep = r - sqrt(len2(sub(ec, pc)));
+      if (dep > clip) return 0;
+      pipeRecord(out, ec, boxFirst ? nv : scl(nv, -1.0), dep, boxFirst ? CT_EDGE_PIPE : CT_PIPE_EDGE, pc);
+      put3(out + CREC, W[0]);
+      put3(out + CREC + 3, edgeDir);
+      put3(out + CREC + 6, capA);
+      put3(out + CREC + 9, pipeDir);
+      out[8] = body1; out[9] = body2;
+      return 1;
+    }
+    if (nw > 4) { *unsup = 1; return 0; }
     V normal = eigNormalized(crs(sub(W[0], W[1]), sub(W[1], W[2])));
     if (dot(normal, dir) > 0) normal = scl(normal, -1.0);
     // createFaceFaceContacts: A = (box face | capsule segment), B = the other
@@ -698,16 +796,6 @@ __device__ __noinline__ int deviceCapsuleBox(const double* Tb, const double* bs,
     for (int i = 0; i < nbh; i++) Bs[i] = Bh[i];
     sortByAngle(As, nah, origin, bx, by);
     sortByAngle(Bs, nbh, origin, bx, by);
-    // edge-edge intersections (EDGE_PIPE / PIPE_EDGE) are not restated
-    for (int i = 0; i < nah; i++) {
-      if (i == nah - 1 && nah == 2) continue;
-      const P2 a1 = inPlane(As[i], origin, bx, by), a2 = inPlane(As[i == nah - 1 ? 0 : i + 1], origin, bx, by);
-      for (int j = 0; j < nbh; j++) {
-        if (j == nbh - 1 && nbh == 2) continue;
-        const P2 b1 = inPlane(Bs[j], origin, bx, by), b2 = inPlane(Bs[j == nbh - 1 ? 0 : j + 1], origin, bx, by);
-        if (lineIntersect(a1, a2, b1, b2)) *unsup = 1;
-      }
-    }
     // vertex-in-face contacts of the capsule's segment (FACE_VERTEX of B when
     // box first, VERTEX_FACE of A otherwise) -> sphere-box at the nearer end
     const V* seg = boxFirst ? Bh : Ah;
@@ -728,6 +816,43 @@ __device__ __noinline__ int deviceCapsuleBox(const double* Tb, const double* bs,
       const V sc = len2(sub(pt, capA)) < len2(sub(pt, capB)) ? capA : capB;
       if (!(dep >= 0 && dep < clip)) continue;
       cnt += sphereBox(box, sc, nullptr, r, boxFirst, 0, clip, boxShape, out + PBREC * cnt);
+    }
+    // then createFaceFaceContacts' edge-edge intersections (:2403), as
+    // EDGE_PIPE (box first, :3320) / PIPE_EDGE (:3494) contacts
+    for (int i = 0; i < nah; i++) {
+      if (i == nah - 1 && nah == 2) continue;
+      const V a1w = As[i], a2w = As[i == nah - 1 ? 0 : i + 1];
+      const P2 a1 = inPlane(a1w, origin, bx, by), a2 = inPlane(a2w, origin, bx, by);
+      for (int j = 0; j < nbh; j++) {
+        if (j == nbh - 1 && nbh == 2) continue;
+        const V b1w = Bs[j], b2w = Bs[j == nbh - 1 ? 0 : j + 1];
+        const P2 b1 = inPlane(b1w, origin, bx, by), b2 = inPlane(b2w, origin, bx, by);
+        P2 o;
+        if (!lineIntersect(a1, a2, b1, b2, o) || cnt >= 8) continue;
+        const V aCl = add(add(oA, scl(bx, o.x)), scl(by, o.y)), bCl = add(add(oB, scl(bx, o.x)), scl(by, o.y));
+        const V aDir = eigNormalized(sub(a2w, a1w)), bDir = eigNormalized(sub(b2w, b1w));
+        V cn = crs(aDir, bDir);
+        if (dot(cn, nA) < 0) cn = scl(cn, -1.0);
+        double dep = dot(bCl, cn) - dot(aCl, cn);
+        if (dep < 0) { cn = scl(cn, -1.0); dep = -dep; }
+        if (!(dep >= 0 && dep < clip)) continue;
+        double* rec = out + PBREC * cnt;
+        if (boxFirst) {
+          // edge A = the box edge, the pipe = edge B shifted back by r
+          pipeRecord(rec, aCl, cn, dep, CT_EDGE_PIPE, sub(bCl, scl(normal, r)));
+          put3(rec + CREC, a1w);
+          put3(rec + CREC + 3, aDir);
+          put3(rec + CREC + 6, sub(b1w, scl(normal, r)));
+          put3(rec + CREC + 9, bDir);
+        } else {
+          pipeRecord(rec, bCl, cn, dep, CT_PIPE_EDGE, add(aCl, scl(normal, r)));
+          put3(rec + CREC, b1w);
+          put3(rec + CREC + 3, bDir);
+          put3(rec + CREC + 6, add(a1w, scl(normal, r)));
+          put3(rec + CREC + 9, aDir);
+        }
+        cnt++;
+      }
     }
   }
   for (int c = 0; c < cnt; c++) { out[PBREC * c + 8] = body1; out[PBREC * c + 9] = body2; }

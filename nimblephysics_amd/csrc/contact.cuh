@@ -2068,6 +2068,94 @@ __device__ double pipePipeRowTerm(const ModelDev& md, const BwdPool& P, int j, c
   return v;
 }
 
+// PIPE_VERTEX / VERTEX_PIPE and PIPE_EDGE / EDGE_PIPE rows (the capsule-box
+// vertex-pipe, edge-pipe and face-edge contacts).  getDofContactType (:166,
+// :213): a dof moving the pipe side gives PIPE_TO_VERTEX (point fixed, :334;
+// normal :967 -- math::closestPointOnLineGradient of the axis point nearest
+// the vertex) / PIPE_TO_EDGE (:538, :1029); moving the mesh side
+// VERTEX_TO_PIPE (the vertex moves, :408; normal :940) / EDGE_TO_PIPE (:555,
+// :1075).  The edge cases go through math::getContactPointGradient with
+// radii (0, 1) -- the contact point -- and (1, 0).  Record: [10..12] pipe
+// closest point; E = pipe fixed point, pipe dir (vertex types) or edge A
+// fixed point, edge A dir, pipe fixed point, pipe dir (edge types).
+__device__ double pipeMeshRowTerm(const ModelDev& md, const BwdPool& P, int j, const double* rec, const double* rr,
+                                  const double* E, const double* Z, int bk, int A, int B, int type) {
+  const bool pa = (md.anc[A] >> bk) & 1ull, pb = (md.anc[B] >> bk) & 1ull;
+  if (pa == pb) return 0.0;
+  const bool vertexType = type == CT_PIPE_VERTEX || type == CT_VERTEX_PIPE;
+  const bool pipeFirst = type == CT_PIPE_VERTEX || type == CT_PIPE_EDGE;
+  const bool pipeMoves = pa == pipeFirst;
+  const double* nrm = rec + 3;
+  const double* p = rec;
+  const double* pcl = rec + 10;
+  const double wv[3] = {Z[0], Z[1], Z[2]};
+  const bool rotates = sqrt(Z[0] * Z[0] + Z[1] * Z[1] + Z[2] * Z[2]) > 1e-6;
+  auto gwt = [&](const double* x, double* o) {
+    if (rotates) { cross3(wv, x, o); for (int i = 0; i < 3; i++) o[i] += Z[3 + i]; }
+    else { for (int i = 0; i < 3; i++) o[i] = Z[3 + i]; }
+  };
+  double dp[3], dn[3];
+  if (vertexType) {
+    const double* pf = E;
+    const double* dir = E + 3;
+    double g[3] = {0, 0, 0}, fg[3] = {0, 0, 0}, dg[3] = {0, 0, 0};
+    if (pipeMoves) { gwt(pf, fg); cross3(wv, dir, dg); }
+    else gwt(p, g);
+    double off = 0, dOff = 0, gOff = 0, dGOff = 0;
+    for (int i = 0; i < 3; i++) {
+      off += dir[i] * pf[i];
+      dOff += dg[i] * pf[i] + dir[i] * fg[i];
+      gOff += dir[i] * p[i];
+      dGOff += dg[i] * p[i] + dir[i] * g[i];
+    }
+    const double rel = gOff - off, dRel = dGOff - dOff;
+    double dist2 = 0.0;
+    for (int i = 0; i < 3; i++) dist2 += (pcl[i] - p[i]) * (pcl[i] - p[i]);
+    const double inv = 1.0 / sqrt(dist2);
+    for (int i = 0; i < 3; i++) {
+      dp[i] = g[i];
+      dn[i] = (fg[i] + rel * dg[i] + dRel * dir[i] - g[i]) * inv;
+    }
+  } else {
+    const double *ef = E, *ed = E + 3, *pf = E + 6, *pd = E + 9;
+    double fg[3], dg[3], other[3];
+    const double zero[3] = {0, 0, 0};
+    gwt(pipeMoves ? pf : ef, fg);
+    cross3(wv, pipeMoves ? pd : ed, dg);
+    const double* dpE = pipeMoves ? zero : fg;
+    const double* duE = pipeMoves ? zero : dg;
+    const double* dpP = pipeMoves ? fg : zero;
+    const double* duP = pipeMoves ? dg : zero;
+    edgeContactPointGradient(ef, dpE, ed, duE, pf, dpP, pd, duP, dp, 0.0, 1.0);
+    edgeContactPointGradient(ef, dpE, ed, duE, pf, dpP, pd, duP, other, 1.0, 0.0);
+    double dist2 = 0.0;
+    for (int i = 0; i < 3; i++) dist2 += (p[i] - pcl[i]) * (p[i] - pcl[i]);
+    const double inv = 1.0 / sqrt(dist2);
+    for (int i = 0; i < 3; i++) dn[i] = (other[i] - dp[i]) * inv;
+  }
+  const double dnn = dot3(dn, nrm);
+  const double sg = pipeFirst ? 1.0 : -1.0;
+  for (int i = 0; i < 3; i++) dn[i] = sg * (dn[i] - dnn * nrm[i]);
+  double dd[3];
+  const int dirIdx = (int)rr[RR_DIR];
+  if (dirIdx == 0 || dot3(dn, dn) <= 1e-12) {
+    for (int i = 0; i < 3; i++) dd[i] = dn[i];
+  } else {
+    double T0[3], T1[3];
+    tangentBasisGradient(nrm, dn, T0, T1);
+    for (int i = 0; i < 3; i++) dd[i] = dirIdx == 1 ? T0[i] : T1[i];
+  }
+  const double* d = rr + RR_D;
+  double pxdd[3], dpxd[3];
+  cross3(p, dd, pxdd);
+  cross3(dp, d, dpxd);
+  double v = 0.0;
+  for (int i = 0; i < 3; i++)
+    v += (P.TAB[j * 12 + i] - P.TAB[j * 12 + 6 + i]) * (pxdd[i] + dpxd[i]) +
+         (P.TAB[j * 12 + 3 + i] - P.TAB[j * 12 + 9 + i]) * dd[i];
+  return v;
+}
+
 // G-term of an EDGE_EDGE row for direction k (position generator Z) when
 // k's joint moves exactly one of the two bodies: EDGE_A / EDGE_B contact
 // position gradient (DifferentiableContactConstraint.cpp:412 / :429) and
@@ -2284,6 +2372,8 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
           acc += pipePipeRowTerm(md, P, j, rec, rr, sn + snEdge(n) + con * EDGE_REC, Z, bk, A, B);
         else if (type == CT_SPHERE_PIPE || type == CT_PIPE_SPHERE)
           acc += spherePipeRowTerm(md, P, j, rec, rr, sn + snEdge(n) + con * EDGE_REC, Z, bk, A, B, type);
+        else if (type >= CT_PIPE_VERTEX && type <= CT_EDGE_PIPE)
+          acc += pipeMeshRowTerm(md, P, j, rec, rr, sn + snEdge(n) + con * EDGE_REC, Z, bk, A, B, type);
         else acc += sphereRowTerm(md, s, L, P, j, rec, rr, Z, bk);
         continue;
       }

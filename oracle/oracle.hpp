@@ -37,6 +37,11 @@ struct Kin {
 // Sphere-box contacts (types 4 SPHERE_BOX / 5 BOX_SPHERE, the reference's
 // ContactType numbering) also carry the sphere centre and the box faces the
 // centre was clamped against (Contact::faceNLocked / faceNNormal).
+// pipe-mesh contact types of the capsule-box branches (this package's
+// numbering; the reference's PIPE_VERTEX 16 / VERTEX_PIPE 18 / PIPE_EDGE 17 /
+// EDGE_PIPE 19, dart/collision/Contact.hpp:76)
+enum { CT_PIPE_VERTEX = 10, CT_VERTEX_PIPE = 11, CT_PIPE_EDGE = 12, CT_EDGE_PIPE = 13 };
+
 struct Contact {
   int shapeA, shapeB, bodyA, bodyB;
   double point[3], normal[3], depth;

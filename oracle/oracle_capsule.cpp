@@ -19,10 +19,15 @@
 //    (:3366) with createFaceFaceContacts (:2203), keepOnlyConvex2DHull (:3545),
 //    math::prepareConvex2DShape / pointInPlane (dart/math/Geometry.cpp:3813,
 //    :3843), convex2DShapeContains (:3756), get2DLineIntersection (:3790).
-// Not restated (flagged `unsupported`, contact dropped): the vertex-pipe and
-// edge-pipe branches (1 or 2 box witness points, :3071/:3110), the 8-point
-// witness set of a zero penetration direction, and EDGE_PIPE / PIPE_EDGE
-// contacts from a capsule crossing a face boundary.
+// and createCapsuleMeshContact's vertex-pipe (one box witness point) and
+// non-parallel edge-pipe (two) branches (:3071, :3225) and the EDGE_EDGE
+// contacts of its face branch, converted to PIPE_EDGE / EDGE_PIPE (:3320,
+// :3494) -- with createFaceFaceContacts' edge intersections (:2403,
+// get2DLineIntersection :3790, math::getContactPoint Geometry.cpp:1075).
+// Not restated (flagged `unsupported`, contact dropped): an edge parallel to
+// the pipe (:3118; the reference's SPHERE_EDGE contacts there carry a NaN
+// sphere centre into their gradients) and the 8-point witness set of a zero
+// penetration direction.
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -491,26 +496,89 @@ bool convexContains(const V& pt, const std::vector<V>& shape, const V& o, const 
   return true;
 }
 
-bool lineIntersect2D(P2 p, P2 p1, P2 q, P2 q1) {
+// get2DLineIntersection (:3790), including its collinear branch's
+// out = p + s t (sic)
+bool lineIntersect2D(P2 p, P2 p1, P2 q, P2 q1, P2* out = nullptr) {
   double rx = p1.x - p.x, ry = p1.y - p.y, sx = q1.x - q.x, sy = q1.y - q.y;
   double rs = cross2(rx, ry, sx, sy);
   if (rs == 0 && cross2(q.x - p.x, q.y - p.y, rx, ry) == 0) {
     double rr = rx * rx + ry * ry;
     double t0 = ((q.x - p.x) * rx + (q.y - p.y) * ry) / rr;
     double t1 = ((q.x + sx - p.x) * rx + (q.y + sy - p.y) * ry) / rr;
-    return (t0 >= 0 && t0 <= 1) || (t1 >= 0 && t1 <= 1);
+    if (t0 >= 0 && t0 <= 1) { if (out) *out = {p.x + sx * t0, p.y + sy * t0}; return true; }
+    if (t1 >= 0 && t1 <= 1) { if (out) *out = {p.x + sx * t1, p.y + sy * t1}; return true; }
+    return false;
   } else if (rs == 0) {
     return false;
   }
   double t = cross2(q.x - p.x, q.y - p.y, sx, sy) / rs;
   double u = cross2(p.x - q.x, p.y - q.y, rx, ry) / cross2(sx, sy, rx, ry);
-  return t >= 0 && t <= 1 && u >= 0 && u <= 1;
+  if (t >= 0 && t <= 1 && u >= 0 && u <= 1) {
+    if (out) *out = {p.x + t * rx, p.y + t * ry};
+    return true;
+  }
+  return false;
+}
+
+// dSegmentsClosestApproach (DARTCollide.cpp:301): segment pa -> pb against
+// ua -> ub, parameters not clamped beyond the routine's own edge cases
+void segmentsClosestApproach(const double* pa, const double* ua, const double* pb, const double* ub, double* alpha,
+                             double* beta) {
+  double u[3], v[3], w[3];
+  for (int i = 0; i < 3; i++) { u[i] = pb[i] - pa[i]; v[i] = ub[i] - ua[i]; w[i] = pa[i] - ua[i]; }
+  const double a = u[0] * u[0] + u[1] * u[1] + u[2] * u[2], b = u[0] * v[0] + u[1] * v[1] + u[2] * v[2];
+  const double c = v[0] * v[0] + v[1] * v[1] + v[2] * v[2], d = u[0] * w[0] + u[1] * w[1] + u[2] * w[2];
+  const double e = v[0] * w[0] + v[1] * w[1] + v[2] * w[2];
+  const double D = a * c - b * b;
+  double sN, sD = D, tN, tD = D;
+  if (D < 1e-15) {
+    sN = 0.0; sD = 1.0; tN = e; tD = c;
+  } else {
+    sN = b * e - c * d;
+    tN = a * e - b * d;
+    if (sN < 0.0) { sN = 0.0; tN = e; tD = c; }
+    else if (sN > sD) { sN = sD; tN = e + b; tD = c; }
+  }
+  if (tN < 0.0) {
+    tN = 0.0;
+    if (-d < 0.0) sN = 0.0;
+    else if (-d > a) sN = sD;
+    else { sN = -d; sD = a; }
+  } else if (tN > tD) {
+    tN = tD;
+    if ((-d + b) < 0.0) sN = 0;
+    else if ((-d + b) > a) sN = sD;
+    else { sN = -d + b; sD = a; }
+  }
+  *alpha = std::fabs(sN) < 1e-15 ? 0.0 : sN / sD;
+  *beta = std::fabs(tN) < 1e-15 ? 0.0 : tN / tD;
+}
+
+// math::getContactPoint (Geometry.cpp:1075) via dLineClosestApproach (:1042)
+V contactPoint(const V& pA, const V& uA, const V& pB, const V& uB, double rA, double rB) {
+  V p = pB - pA;
+  const double uaub = dot(uA, uB), q1 = dot(uA, p), q2 = -dot(uB, p);
+  double d = 1 - uaub * uaub, alpha = 0, beta = 0;
+  if (d > 0) {
+    d = 1.0 / d;
+    alpha = (q1 + uaub * q2) * d;
+    beta = (uaub * q1 + q2) * d;
+  }
+  V ca = pA + uA * alpha, cb = pB + uB * beta;
+  return (ca * rB + cb * rA) * (1.0 / (rA + rB));
 }
 
 // createFaceFaceContacts (:2203) restricted to its vertex-in-hull contacts
 // (VERTEX_FACE for A's vertices, FACE_VERTEX for B's); the edge-edge
 // intersections it would also emit are counted in *edgeEdge.
-struct FFContact { V point, normal; double depth; int type; };  // type 1 VERTEX_FACE, 2 FACE_VERTEX
+// type 1 VERTEX_FACE, 2 FACE_VERTEX, 3 EDGE_EDGE (edge A / B fixed point,
+// direction and closest point)
+struct FFContact {
+  V point, normal;
+  double depth;
+  int type;
+  V aFixed, aDir, aClosest, bFixed, bDir, bClosest;
+};
 void faceFaceVertices(const V& dir, const std::vector<V>& A, const std::vector<V>& B, int pin,
                       std::vector<FFContact>& outv, int* edgeEdge) {
   auto faceNormal = [&](const std::vector<V>& P) {
@@ -568,11 +636,33 @@ void faceFaceVertices(const V& dir, const std::vector<V>& A, const std::vector<V
   int ee = 0;
   for (size_t i = 0; i < As.size(); i++) {
     if (i == As.size() - 1 && As.size() == 2) continue;
-    P2 a1 = inPlane(As[i], origin, bx, by), a2 = inPlane(As[i == As.size() - 1 ? 0 : i + 1], origin, bx, by);
+    const V& a1w = As[i];
+    const V& a2w = As[i == As.size() - 1 ? 0 : i + 1];
+    P2 a1 = inPlane(a1w, origin, bx, by), a2 = inPlane(a2w, origin, bx, by);
     for (size_t j = 0; j < Bs.size(); j++) {
       if (j == Bs.size() - 1 && Bs.size() == 2) continue;
-      P2 b1 = inPlane(Bs[j], origin, bx, by), b2 = inPlane(Bs[j == Bs.size() - 1 ? 0 : j + 1], origin, bx, by);
-      if (lineIntersect2D(a1, a2, b1, b2)) ee++;
+      const V& b1w = Bs[j];
+      const V& b2w = Bs[j == Bs.size() - 1 ? 0 : j + 1];
+      P2 b1 = inPlane(b1w, origin, bx, by), b2 = inPlane(b2w, origin, bx, by);
+      P2 o;
+      if (!lineIntersect2D(a1, a2, b1, b2, &o)) continue;
+      ee++;
+      // createFaceFaceContacts' EDGE_EDGE contact (:2441)
+      FFContact c;
+      c.type = 3;
+      c.aClosest = oA + bx * o.x + by * o.y;
+      c.bClosest = oB + bx * o.x + by * o.y;
+      c.aFixed = a1w;
+      c.aDir = eigNormalized(a2w - a1w);
+      c.bFixed = b1w;
+      c.bDir = eigNormalized(b2w - b1w);
+      c.normal = cross(c.aDir, c.bDir);
+      if (dot(c.normal, nA) < 0) c.normal = c.normal * -1.0;
+      c.depth = dot(c.bClosest, c.normal) - dot(c.aClosest, c.normal);
+      if (c.depth < 0) { c.normal = c.normal * -1.0; c.depth = -c.depth; }
+      const double rA = pin == 1 ? 0.0 : 1.0, rB = pin == 2 ? 0.0 : 1.0;
+      c.point = contactPoint(c.aFixed, c.aDir, c.bFixed, c.bDir, rA, rB);
+      outv.push_back(c);
     }
   }
   *edgeEdge = ee;
@@ -615,11 +705,59 @@ int capsuleBox(const Iso<double>& Tb, const double* size, const Iso<double>& Tc,
     if (k) emit(c);
     return k;
   }
-  // pipe branch: box witness points, createCapsuleMeshContact
+  // pipe branch: box witness points, createCapsuleMeshContact (:3050) with
+  // capsuleA / capsuleB the top / bottom axis points and flipObjectOrder =
+  // boxFirst
   std::vector<V> W = witnessBox(box, dir, !boxFirst ? true : false);
-  // 1-2 points: vertex-/edge-pipe branches; > 4: a zero penetration direction
-  if (W.size() <= 2 || W.size() > 4) { *unsupported = 1; return 0; }
   V capA = xf(cap.T, mk(0, 0, h / 2)), capB = xf(cap.T, mk(0, 0, -h / 2));
+  const V axis = capB - capA;
+  auto setPipe = [&](Contact& c, const V& closest, const V& fixed, const V& pdir) {
+    for (int i = 0; i < 3; i++) { c.pipeClosest[i] = closest.x[i]; c.pipeFixed[i] = fixed.x[i]; c.pipeDir[i] = pdir.x[i]; }
+    c.pipeRadius = r;
+  };
+  auto setV = [](double* o, const V& v) { for (int i = 0; i < 3; i++) o[i] = v.x[i]; };
+  if (W.size() == 1) {
+    // vertex-pipe (:3071): dDistPointToSegment from the vertex to the axis
+    const V w = W[0] - capA;
+    const double c1 = dot(w, axis), c2 = dot(axis, axis);
+    const double alpha = c1 <= 0 ? 0.0 : (c2 <= c1 ? 1.0 : c1 / c2);
+    const V nearest = capA + axis * alpha;
+    V normal = eigNormalized(nearest - W[0]);
+    Contact c{};
+    setV(c.point, W[0]);
+    if (boxFirst) normal = normal * -1.0;
+    setV(c.normal, normal);
+    c.type = boxFirst ? CT_VERTEX_PIPE : CT_PIPE_VERTEX;
+    setPipe(c, nearest, capA, eigNormalized(axis));
+    c.depth = r - std::sqrt(len2(W[0] - nearest));
+    if (c.depth > clip) return 0;
+    emit(c);
+    return 1;
+  }
+  if (W.size() == 2) {
+    const V pipeDir = eigNormalized(axis), edgeDir = eigNormalized(W[1] - W[0]);
+    if (std::fabs(1.0 - std::fabs(dot(pipeDir, edgeDir))) < 1e-5) { *unsupported = 1; return 0; }
+    // edge-pipe (:3225): dSegmentsClosestApproach(W0, capA, W1, capB)
+    double alpha, beta;
+    segmentsClosestApproach(W[0].x, capA.x, W[1].x, capB.x, &alpha, &beta);
+    const V edgeClosest = W[0] + (W[1] - W[0]) * alpha;
+    const V pipeClosest = capA + axis * beta;
+    const V normal = eigNormalized(edgeClosest - pipeClosest);
+    Contact c{};
+    setV(c.point, edgeClosest);
+    setV(c.normal, boxFirst ? normal : normal * -1.0);
+    c.type = boxFirst ? CT_EDGE_PIPE : CT_PIPE_EDGE;
+    setV(c.edgeAClosest, edgeClosest);
+    setV(c.edgeAFixed, W[0]);
+    setV(c.edgeADir, edgeDir);
+    setPipe(c, pipeClosest, capA, pipeDir);
+    c.depth = r - std::sqrt(len2(edgeClosest - pipeClosest));
+    if (c.depth > clip) return 0;
+    emit(c);
+    return 1;
+  }
+  // > 4 points: a zero penetration direction
+  if (W.size() > 4) { *unsupported = 1; return 0; }
   V normal = eigNormalized(cross(W[0] - W[1], W[1] - W[2]));
   if (normal.x[0] * dir.x[0] + normal.x[1] * dir.x[1] + normal.x[2] * dir.x[2] > 0) normal = normal * -1.0;
   std::vector<FFContact> fc;
@@ -631,9 +769,29 @@ int capsuleBox(const Iso<double>& Tb, const double* size, const Iso<double>& Tc,
     std::vector<V> cw{capA - normal * r, capB - normal * r};
     faceFaceVertices(dir, cw, W, 2, fc, &ee);
   }
-  if (ee > 0) *unsupported = 1;
   int added = 0;
   for (const FFContact& f : fc) {
+    if (f.type == 3) {
+      // EDGE_EDGE -> EDGE_PIPE (flipped, :3320) / PIPE_EDGE (:3494)
+      if (!(f.depth >= 0 && f.depth < clip)) continue;
+      Contact c{};
+      setV(c.normal, f.normal);
+      c.depth = f.depth;
+      if (boxFirst) {
+        c.type = CT_EDGE_PIPE;
+        setPipe(c, f.bClosest - normal * r, f.bFixed - normal * r, f.bDir);
+        setV(c.edgeAFixed, f.aFixed); setV(c.edgeADir, f.aDir); setV(c.edgeAClosest, f.aClosest);
+        setV(c.point, f.aClosest);
+      } else {
+        c.type = CT_PIPE_EDGE;
+        setPipe(c, f.aClosest + normal * r, f.aFixed + normal * r, f.aDir);
+        setV(c.edgeAFixed, f.bFixed); setV(c.edgeADir, f.bDir); setV(c.edgeAClosest, f.bClosest);
+        setV(c.point, f.bClosest);
+      }
+      emit(c);
+      added++;
+      continue;
+    }
     // flipped: FACE_VERTEX -> FACE_SPHERE; else VERTEX_FACE -> SPHERE_FACE
     if (f.type != (boxFirst ? 2 : 1)) continue;
     V sc = len2(f.point - capA) < len2(f.point - capB) ? capA : capB;

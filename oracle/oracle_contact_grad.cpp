@@ -167,6 +167,12 @@ static void constraintForcesJacobian(const World& w, const Kin<double>& k, const
       else if (c.type == CT_SPHERE_PIPE) type = pa ? 9 : 10;  // SPHERE_TO_PIPE / PIPE_TO_SPHERE
       else if (c.type == CT_PIPE_SPHERE) type = pa ? 10 : 9;
       else if (c.type == CT_PIPE_PIPE) type = pa ? 11 : 12;  // PIPE_A / PIPE_B
+      // getDofContactType (:166-172, :213-219): PIPE_TO_VERTEX 13,
+      // VERTEX_TO_PIPE 14, PIPE_TO_EDGE 15, EDGE_TO_PIPE 16
+      else if (c.type == CT_PIPE_VERTEX) type = pa ? 13 : 14;
+      else if (c.type == CT_VERTEX_PIPE) type = pa ? 14 : 13;
+      else if (c.type == CT_PIPE_EDGE) type = pa ? 15 : 16;
+      else if (c.type == CT_EDGE_PIPE) type = pa ? 16 : 15;
       else if (c.type == CT_SPHERE_BOX) type = pa ? 3 : 4;
       else if (c.type == CT_BOX_SPHERE) type = pa ? 4 : 3;
       else if (c.type == CT_VERTEX_FACE) type = pa ? 1 : 2;
@@ -287,6 +293,67 @@ static void constraintForcesJacobian(const World& w, const Kin<double>& k, const
       const double dnn = dn[0] * c.normal[0] + dn[1] * c.normal[1] + dn[2] * c.normal[2];
       const bool plus = type == 9 ? c.type == CT_SPHERE_PIPE : c.type == CT_PIPE_SPHERE;
       for (int i = 0; i < 3; i++) dn[i] = (plus ? 1.0 : -1.0) * (dn[i] - dnn * c.normal[i]);
+      if (dirIdx == 0 || dn[0] * dn[0] + dn[1] * dn[1] + dn[2] * dn[2] <= 1e-12) {
+        for (int i = 0; i < 3; i++) dd[i] = dn[i];
+      } else {
+        double T0[3], T1[3];
+        tangentBasisGradient(c.normal, dn, T0, T1);
+        for (int i = 0; i < 3; i++) dd[i] = dirIdx == 1 ? T0[i] : T1[i];
+      }
+    } else if (type == 13 || type == 14) {
+      // VERTEX_TO_PIPE (:408 point: the vertex moves; :940 normal) /
+      // PIPE_TO_VERTEX (:334 point fixed; :967 normal): the axis point
+      // closest to the vertex through math::closestPointOnLineGradient
+      double g[3] = {0, 0, 0}, cg[3], dn[3], fg[3] = {0, 0, 0}, dg[3] = {0, 0, 0};
+      if (type == 14) {
+        gwt(p, g);
+        for (int i = 0; i < 3; i++) dp[i] = g[i];
+      } else {
+        gwt(c.pipeFixed, fg);
+        cross3(wv, c.pipeDir, dg);  // gradientWrtThetaPureRotation
+      }
+      double off = 0, dOff = 0, gOff = 0, dGOff = 0;
+      for (int i = 0; i < 3; i++) {
+        off += c.pipeDir[i] * c.pipeFixed[i];
+        dOff += dg[i] * c.pipeFixed[i] + c.pipeDir[i] * fg[i];
+        gOff += c.pipeDir[i] * p[i];
+        dGOff += dg[i] * p[i] + c.pipeDir[i] * g[i];
+      }
+      const double rel = gOff - off, dRel = dGOff - dOff;
+      for (int i = 0; i < 3; i++) cg[i] = fg[i] + rel * dg[i] + dRel * c.pipeDir[i];
+      double dist2 = 0;
+      for (int i = 0; i < 3; i++) dist2 += (c.pipeClosest[i] - p[i]) * (c.pipeClosest[i] - p[i]);
+      const double norm = std::sqrt(dist2);
+      for (int i = 0; i < 3; i++) dn[i] = (cg[i] - g[i]) / norm;
+      const double dnn = dn[0] * c.normal[0] + dn[1] * c.normal[1] + dn[2] * c.normal[2];
+      const double sg = c.type == CT_PIPE_VERTEX ? 1.0 : -1.0;
+      for (int i = 0; i < 3; i++) dn[i] = sg * (dn[i] - dnn * c.normal[i]);
+      if (dirIdx == 0 || dn[0] * dn[0] + dn[1] * dn[1] + dn[2] * dn[2] <= 1e-12) {
+        for (int i = 0; i < 3; i++) dd[i] = dn[i];
+      } else {
+        double T0[3], T1[3];
+        tangentBasisGradient(c.normal, dn, T0, T1);
+        for (int i = 0; i < 3; i++) dd[i] = dirIdx == 1 ? T0[i] : T1[i];
+      }
+    } else if (type == 15 || type == 16) {
+      // PIPE_TO_EDGE / EDGE_TO_PIPE (:538 / :555 point, :1029 / :1075 normal):
+      // math::getContactPointGradient of the edge and the pipe axis with
+      // radii (0, 1) -- the contact point -- and (1, 0)
+      const bool pipeMoves = type == 15;
+      double fg[3], dg[3], zero[3] = {0, 0, 0}, other[3], dn[3];
+      gwt(pipeMoves ? c.pipeFixed : c.edgeAFixed, fg);
+      cross3(wv, pipeMoves ? c.pipeDir : c.edgeADir, dg);
+      const double* dpE = pipeMoves ? zero : fg; const double* duE = pipeMoves ? zero : dg;
+      const double* dpP = pipeMoves ? fg : zero; const double* duP = pipeMoves ? dg : zero;
+      contactPointGradient(c.edgeAFixed, dpE, c.edgeADir, duE, c.pipeFixed, dpP, c.pipeDir, duP, dp, 0.0, 1.0);
+      contactPointGradient(c.edgeAFixed, dpE, c.edgeADir, duE, c.pipeFixed, dpP, c.pipeDir, duP, other, 1.0, 0.0);
+      double dist2 = 0;
+      for (int i = 0; i < 3; i++) dist2 += (c.edgeAClosest[i] - c.pipeClosest[i]) * (c.edgeAClosest[i] - c.pipeClosest[i]);
+      const double norm = std::sqrt(dist2);
+      for (int i = 0; i < 3; i++) dn[i] = (other[i] - dp[i]) / norm;
+      const double dnn = dn[0] * c.normal[0] + dn[1] * c.normal[1] + dn[2] * c.normal[2];
+      const double sg = c.type == CT_PIPE_EDGE ? 1.0 : -1.0;
+      for (int i = 0; i < 3; i++) dn[i] = sg * (dn[i] - dnn * c.normal[i]);
       if (dirIdx == 0 || dn[0] * dn[0] + dn[1] * dn[1] + dn[2] * dn[2] <= 1e-12) {
         for (int i = 0; i < 3; i++) dd[i] = dn[i];
       } else {

@@ -12,6 +12,10 @@ copied from the cited test body, as the formula it is written with).
     :1639 VERTEX_SPHERE_COLLISION / :1903 SPHERE_VERTEX_COLLISION
     :1729 EDGE_SPHERE_COLLISION   / :1993 SPHERE_EDGE_COLLISION
     :1818 FACE_SPHERE_COLLISION   / :2082 SPHERE_FACE_COLLISION
+    :3117 CAPSULE_BOX_PIPE_EDGE_COLLISION      collideCapsuleBox / collideBoxCapsule
+    :3272 CAPSULE_BOX_PIPE_VERTEX_COLLISION
+    :2936 CAPSULE_BOX_SPHERE_AND_PIPE_EDGE_COLLISION (capsule first; contacts
+          in sortContacts(UnitZ) order)
 
 The sphere tests collide a sphere with a unit box *mesh* (ccdMPRPenetration +
 createMeshSphereContact).  The same geometry through the box collider
@@ -22,7 +26,8 @@ point and the box path the box surface point, so the face cases check normal
 and depth only ("check": ["normal", "depth"]).
 
 Type numbering: this package's (csrc/capsule.cuh): SPHERE_BOX 4, BOX_SPHERE 5,
-SPHERE_SPHERE 6, SPHERE_PIPE 7, PIPE_SPHERE 8, PIPE_PIPE 9; the reference's
+SPHERE_SPHERE 6, SPHERE_PIPE 7, PIPE_SPHERE 8, PIPE_PIPE 9, PIPE_VERTEX 10,
+VERTEX_PIPE 11, PIPE_EDGE 12, EDGE_PIPE 13 (the reference's 16 / 18 / 17 / 19); the reference's
 VERTEX_SPHERE / EDGE_SPHERE / FACE_SPHERE (mesh first) correspond to the box
 collider's BOX_SPHERE, SPHERE_VERTEX / SPHERE_EDGE / SPHERE_FACE to
 SPHERE_BOX.
@@ -36,6 +41,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = "unittests/unit/test_DARTCollide.cpp"
 SPHERE_BOX, BOX_SPHERE, SPHERE_SPHERE, SPHERE_PIPE, PIPE_SPHERE, PIPE_PIPE = 4, 5, 6, 7, 8, 9
+PIPE_VERTEX, VERTEX_PIPE, PIPE_EDGE, EDGE_PIPE = 10, 11, 12, 13
 
 
 def euler_xyz(a, b, c):
@@ -115,6 +121,27 @@ def main():
                   "a": [["sphere", [rs]], iso((1.0 - 0.01, 0, 0)).tolist()], "b": box,
                   "ab": [contact([0.5 - 0.01, 0, 0], ex, 0.01, SPHERE_BOX)],
                   "ba": [contact([0.5 - 0.01, 0, 0], -ex, 0.01, BOX_SPHERE)]})
+    # capsule (radius 0.5, height 1) against the unit box, crossing an edge /
+    # a vertex of it (box witness sets of 2 / 1 points)
+    r, h = 0.5, 1.0
+    c = 0.5 + math.sqrt(r * r / 2) - math.sqrt(0.01 * 0.01 / 2)
+    T2 = iso((0, c, c), euler_xyz(math.pi / 4, 0, 0))
+    n = np.array([0.0, 1.0, 1.0]) / math.sqrt(2)
+    cases.append({"name": "capsule_box_pipe_edge", "source": f"{SRC}:3117",
+                  "a": [["capsule", [r, h]], T2.tolist()], "b": box,
+                  "ab": [contact([0, 0.5, 0.5], n, 0.01, PIPE_EDGE)],
+                  "ba": [contact([0, 0.5, 0.5], -n, 0.01, EDGE_PIPE)]})
+    c = 0.5 + math.sqrt(r * r / 3) - math.sqrt(0.01 * 0.01 / 3)
+    T2 = iso((c, c, c), euler_xyz(math.pi / 4, 0, 0))
+    n = np.ones(3) / math.sqrt(3)
+    cases.append({"name": "capsule_box_pipe_vertex", "source": f"{SRC}:3272",
+                  "a": [["capsule", [r, h]], T2.tolist()], "b": box,
+                  "ab": [contact([0.5, 0.5, 0.5], n, 0.01, PIPE_VERTEX)],
+                  "ba": [contact([0.5, 0.5, 0.5], -n, 0.01, VERTEX_PIPE)]})
+    # :2936 a capsule lying on a 2 x 1 x 2 box with one end past its edge
+    cases.append({"name": "capsule_box_sphere_and_pipe_edge", "source": f"{SRC}:2936", "sort": "z",
+                  "a": [["capsule", [r, h]], iso((0, 0.99, 1.0)).tolist()], "b": [["box", [2.0, 1.0, 2.0]], iso().tolist()],
+                  "ab": [contact([0, 0.5, 0.5], ey, 0.01, SPHERE_BOX), contact([0, 0.5, 1.0], ey, 0.01, PIPE_EDGE)]})
     out = {"source": SRC + " (reference), transcribed by tests/golden/make_collide_known_answers.py; "
                            "'ab' = collide(a, b), 'ba' = collide(b, a); tolerance 1e-10 as in the tests "
                            "(1e-8 depth for the mesh-sphere cases)",

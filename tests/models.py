@@ -554,3 +554,16 @@ def known_answer_world(case, order="ab"):
     st[:3] = _rotvec(T[:3, :3])
     st[3:6] = T[:3, 3]
     return w, st
+
+
+def pipe_box_states(case, order, batch, seed=0):
+    """Perturbations of a capsule-box known-answer pose (the free body's pose
+    by ~1 mm / mrad, random velocities and forces): the contacts of the
+    vertex-pipe / edge-pipe / face-edge branches, clamping under the push."""
+    _, st0 = known_answer_world(case, order)
+    rng = np.random.default_rng(seed)
+    st = np.repeat(st0[None, :], batch, axis=0)
+    st[:, :6] += 1e-3 * rng.standard_normal((batch, 6))
+    st[:, 6:] = 0.2 * rng.standard_normal((batch, 6))
+    f = rng.standard_normal((batch, 6))
+    return st, f

@@ -117,6 +117,43 @@ def half_cheetah_world():
     return assets.load_world("half_cheetah_world")
 
 
+def broken_states(kind):
+    """The reference's broken-state regression inputs (tests/golden/
+    broken_states.json; test_HalfCheetahTrajectory.cpp :126-330,
+    test_AtlasTrajectory.cpp :147-372).  Returns (world, names, state [B, 2n],
+    forces [B, n], caches) with caches a list of LCP warm starts (None = empty).
+    Atlas states are permuted from the SDF model's dof order onto this
+    package's Atlas by the name of the body owning each dof."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "broken_states.json")) as fh:
+        d = json.load(fh)
+    if kind == "half_cheetah":
+        w = half_cheetah_world()
+        cases = d["half_cheetah"]
+        perm = np.arange(w.getNumDofs())
+    else:
+        w = atlas_world(True)
+        cases = d["atlas"]["cases"]
+        desc = w.desc_arrays()
+        sk = w.skeletons[0]
+        ours = {b.name: int(desc["dof_offset"][i]) for i, b in enumerate(sk.bodies)}
+        perm = []
+        for name in d["atlas"]["sdf_bodies"]:
+            perm += [ours[name] + k for k in range(6 if name == "pelvis" else 1)]
+        perm = np.array(perm)
+        assert sorted(perm) == list(range(sk.getNumDofs()))
+    n = w.getNumDofs()
+    st = np.zeros((len(cases), 2 * n))
+    f = np.zeros((len(cases), n))
+    for b, c in enumerate(cases):
+        st[b, perm] = c["pos"]
+        st[b, n + perm] = c["vel"]
+        f[b, perm] = c["force"]
+    caches = [c.get("lcp_cache") or None for c in cases]
+    return w, [c["name"] for c in cases], st, f, caches
+
+
 def _fk_world(desc, q):
     """Body world transforms for revolute / prismatic / weld trees (host-side
     helper for placing synthetic states; the device computes its own)."""

@@ -549,3 +549,51 @@ def test_pipe_box_contact_parity(name, order):
     want = {c["type"] for c in case[order]} - {4, 5}
     assert any(((types[:, 0] == t) | (types[:, 1] == t)).any() for t in want)
     assert (snap[:, SN_NC] > 0).any()
+
+
+def _seeded_cache(dev_doubles, caches, d):
+    """Per-world LCP warm starts ([size, x...], -1 = empty) as the device's
+    cache rows (World::setCachedLCPSolution)."""
+    cache = torch.zeros((len(caches), dev_doubles), dtype=torch.float64, device=d)
+    cache[:, 0] = -1
+    for b, c in enumerate(caches):
+        if c:
+            cache[b, 0] = len(c)
+            cache[b, 1:1 + len(c)] = torch.tensor(c, dtype=torch.float64)
+    return cache
+
+
+@pytest.mark.parametrize("kind", ["half_cheetah", "atlas"])
+def test_broken_state_parity(kind):
+    """The reference's broken-state regressions (test_HalfCheetahTrajectory.cpp
+    :126-330 with BROKEN_POINT's LCP cache, test_AtlasTrajectory.cpp :147-372;
+    tests/golden/broken_states.json): contact sets and LCP path identical to
+    the oracle's, the next state and the full Jacobians (getStateJacobian and
+    d next / d tau, one device backward per basis vector over a replicated
+    batch) within RTOL of the oracle's analytic ones, which
+    tests/test_oracle_pins.py checks against finite differences at the same
+    states."""
+    from test_oracle_pins import _seed_caches
+    w, names, st, f, caches = models.broken_states(kind)
+    n = w.getNumDofs()
+    B = len(names)
+    d = torch.device("cuda:0")
+    dev = w.native()
+    ow = O.OracleWorld(w)
+    _seed_caches(ow, caches)
+    ref = ow.forward(st, f)
+    J, F = ow.jacobians()
+    nxt, snap, cache, ts, tf = _device_step(w, st, f, _seeded_cache(dev.cache_doubles, caches, d))
+    same = _check_contacts(ow, snap.cpu().numpy(), B, cache=cache.cpu().numpy())
+    assert same.all(), names
+    assert (snap.cpu().numpy()[:, SN_NCON] > 0).all()
+    assert _rel(nxt.cpu().numpy(), ref) < RTOL
+    # full Jacobians: 2n copies of each world, backward of the i-th unit vector
+    R = 2 * n
+    st_r, f_r = np.repeat(st, R, axis=0), np.repeat(f, R, axis=0)
+    _nx, snap_r, _c, ts_r, tf_r = _device_step(w, st_r, f_r,
+                                               _seeded_cache(dev.cache_doubles, [c for c in caches for _ in range(R)], d))
+    gs, gf = _device_backward(w, ts_r, tf_r, snap_r, np.tile(np.eye(R), (B, 1)))
+    for b, name in enumerate(names):
+        assert _rel(gs[b * R:(b + 1) * R], J[b]) < RTOL, (name, _rel(gs[b * R:(b + 1) * R], J[b]))
+        assert _rel(gf[b * R:(b + 1) * R], F[b]) < RTOL, (name, _rel(gf[b * R:(b + 1) * R], F[b]))

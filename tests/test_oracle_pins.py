@@ -353,3 +353,53 @@ def test_pipe_box_gradients_vs_finite_differences(oracle_built, name, order):
     gs, gf, fd_s, fd_f = _fd_check(w, st, f, g)
     assert np.abs(gs - fd_s).max() <= 1e-6 * np.abs(fd_s).max()
     assert np.abs(gf - fd_f).max() <= 1e-6 * np.abs(fd_f).max()
+
+
+def _seed_caches(o, caches):
+    """setCachedLCPSolution for each world (None = empty)."""
+    o.reset_cache(len(caches))
+    for b, c in enumerate(caches):
+        if c:
+            o.cache[b, 0] = len(c)
+            o.cache[b, 1:1 + len(c)] = c
+
+
+@pytest.mark.parametrize("kind", ["half_cheetah", "atlas"])
+def test_broken_state_jacobians_vs_finite_differences(oracle_built, kind):
+    """The reference's broken-state regressions (test_HalfCheetahTrajectory.cpp
+    :126-330, test_AtlasTrajectory.cpp :147-372, tests/golden/broken_states.json):
+    at each state, with its LCP warm start, the full analytic Jacobians
+    (getStateJacobian and d next / d tau, the blocks verifyAnalyticalJacobians
+    / verifyVelGradients / verifyPosVelJacobian check) against central
+    differences of the oracle's own step.  Each state is in contact:
+    BOX_SPHERE capsule-ground contacts for the half-cheetah, eight
+    VERTEX_FACE foot contacts on the CFM + PGS fallback for Atlas."""
+    w, names, st, f, caches = models.broken_states(kind)
+    n = w.getNumDofs()
+    o = O.OracleWorld(w)
+    _seed_caches(o, caches)
+    o.forward(st, f)
+    J, F = o.jacobians()
+    eps_s, eps_f = 1e-6, 1e-4  # forces enter through dt / M: a larger step keeps rounding out
+    for b, name in enumerate(names):
+        assert o.num_contacts(b) > 0, name
+        if kind == "atlas":
+            assert O.lcp_flags(o, b)[1] == 1, name  # Dantzig fails -> CFM + PGS
+        fo = O.OracleWorld(w)
+
+        def fwd(s, ff):
+            _seed_caches(fo, [caches[b]])
+            return fo.forward(s[None], ff[None])[0]
+        fd_J = np.stack([(fwd(st[b] + eps_s * e, f[b]) - fwd(st[b] - eps_s * e, f[b])) / (2 * eps_s)
+                         for e in np.eye(2 * n)], axis=1)
+        fd_F = np.stack([(fwd(st[b], f[b] + eps_f * e) - fwd(st[b], f[b] - eps_f * e)) / (2 * eps_f)
+                         for e in np.eye(n)], axis=1)
+        # blockwise, as the reference's checks (pos-pos, pos-vel, vel-pos, vel-vel,
+        # force-vel): 1e-6 relative to the block, or the reference's own absolute
+        # 1e-8 (GradientTestUtils.hpp :1590 / :1686 equals(analytical, bruteForce, 1e-8))
+        # where central-difference rounding on |q| ~ 1.6 dominates an O(dt) block
+        for rows in (slice(0, n), slice(n, 2 * n)):
+            for cols in (slice(0, n), slice(n, 2 * n)):
+                blk, ref = J[b][rows, cols], fd_J[rows, cols]
+                assert np.abs(blk - ref).max() <= max(1e-6 * np.abs(ref).max(), 1e-8), (name, rows, cols)
+            assert np.abs(F[b][rows] - fd_F[rows]).max() <= 1e-6 * np.abs(fd_F[rows]).max(), (name, rows)

@@ -36,7 +36,7 @@ struct nimble_world {
   hipFunction_t dummy = nullptr;
 };
 
-extern "C" __global__ void nimble_forward_kernel(const ModelDev*, Layout, int, const double*, const double*, double*,
+extern "C" __global__ void nimble_forward_kernel(const ModelDev*, Layout, const double*, const double*, double*,
                                                  double*, double*, int, int);
 extern "C" __global__ void nimble_backward_kernel(const ModelDev*, Layout, int, const double*, const double*,
                                                   double*, int, const double*, double*, double*, int, double*, int);
@@ -270,6 +270,14 @@ int64_t nimble_snapshot_doubles(nimble_world_t w) { return w ? w->snapDoubles : 
 int64_t nimble_lcp_cache_doubles(nimble_world_t w) { return w ? w->cacheDoubles : -1; }
 int32_t nimble_num_collision_pairs(nimble_world_t w) { return w ? w->host.numPairs : -1; }
 
+// worlds per forward launch (one workgroup each); NIMBLE_AMD_FWD_CHUNK
+// lowers it so tests exercise the chunked launches at small batches
+static int fwdChunk() {
+  int c = 1 << 22;
+  if (const char* e = getenv("NIMBLE_AMD_FWD_CHUNK")) c = atoi(e);
+  return c > 0 && c < (1 << 22) ? c : (1 << 22);
+}
+
 static int gridFor(int batch) {
   // one wave per world; cap the grid so every wave loops over several worlds
   // only when the batch exceeds 64k
@@ -285,9 +293,17 @@ int nimble_forward(nimble_world_t w, int32_t batch, const double* state, const d
   const size_t lds = (size_t)w->fwd.total * sizeof(double);
   // contact models: a second (helper) wave per world for the LCP fallback
   const int fwdThreads = w->host.numPairs > 0 ? 128 : 64;
-  hipLaunchKernelGGL(nimble_forward_kernel, dim3(gridFor(batch)), dim3(fwdThreads), lds, st, w->dev, w->fwd, batch, state,
-                     forces, lcp_cache, next_state, snapshot, w->snapDoubles, w->cacheDoubles);
-  HIP_TRY(hipGetLastError());
+  // one workgroup per world; batches beyond one launch's grid go in chunks
+  const size_t n = (size_t)w->host.n;
+  const int chunk = fwdChunk();
+  for (int32_t b0 = 0; b0 < batch; b0 += chunk) {
+    const int cnt = batch - b0 < chunk ? batch - b0 : chunk;
+    hipLaunchKernelGGL(nimble_forward_kernel, dim3(cnt), dim3(fwdThreads), lds, st, w->dev, w->fwd,
+                       state + b0 * 2 * n, forces + b0 * n, lcp_cache + (size_t)b0 * w->cacheDoubles,
+                       next_state + b0 * 2 * n, snapshot + (size_t)b0 * w->snapDoubles, w->snapDoubles,
+                       w->cacheDoubles);
+    HIP_TRY(hipGetLastError());
+  }
   return NIMBLE_OK;
 }
 

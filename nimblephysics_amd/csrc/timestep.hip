@@ -292,9 +292,13 @@ __device__ __forceinline__ void coreDynamics(const ModelDev& md, double* s, cons
 // Forward step.
 // ---------------------------------------------------------------------------
 // Two waves per world when the model has contact pairs (blockDim 128): wave
-// 1 is the LCP helper (helperWave), all of the step runs on wave 0.
+// 1 is the LCP helper (helperWave), all of the step runs on wave 0.  One
+// world per workgroup and no world loop (the host splits batches larger than
+// one launch): a loop lets the compiler hoist ~120 per-lane model / LDS
+// addresses out of it, which stay live across the whole step and spilled
+// ~150 VGPRs (~44 KB of scratch writes per world).
 extern "C" __global__ void __launch_bounds__(2 * WAVE) __attribute__((amdgpu_waves_per_eu(2)))
-nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, const double* __restrict__ state,
+nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, const double* __restrict__ state,
                       const double* __restrict__ forces, double* __restrict__ lcpCache,
                       double* __restrict__ nextState, double* __restrict__ snapshot, int snapDoubles,
                       int cacheDoubles) {
@@ -314,7 +318,8 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, con
       // the helper's work is speculative: it only takes issue slots the
       // step's wave leaves idle (lower wave priority on the shared SIMD)
       __builtin_amdgcn_s_setprio(0);
-      for (int env = blockIdx.x; env < batch; env += gridDim.x) {
+      {
+        const int env = blockIdx.x;
         double* ct = lds<true>(s) + L.ct;
         collideWait(ct, CS_GO);
         collideWorld(md, lds<true>(s), L, lane, snapshot + (size_t)env * snapDoubles + snEdge(n));
@@ -325,7 +330,8 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, con
     }
     __builtin_amdgcn_s_setprio(2);
   }
-  for (int env = blockIdx.x; env < batch; env += gridDim.x) {
+  {
+    const int env = blockIdx.x;
     const double* st = state + (size_t)env * 2 * n;
 #ifdef NIMBLE_STAGE_TIMING
     double* g_stamp = md.numPairs > 0 ? snapshot + (size_t)env * snapDoubles + snapWorkspaceOffset(n) + 1000 : nullptr;

@@ -72,8 +72,8 @@ __host__ __device__ inline int bwdPoolDoubles(int m, int n) { return n * m + 24 
 #define snapWorkspaceOffsetHost snapWorkspaceOffset
 
 // Dynamics cache in every snapshot (forward -> backward): world transforms,
-// world-frame motion subspace, body twists, composite inertias, the packed
-// Cholesky factor of M, its reciprocal diagonal and the bias forces C.
+// world-frame motion subspace, body twists, the packed Cholesky factor of M,
+// its reciprocal diagonal and the bias forces C.
 __host__ __device__ inline int dynCacheDoubles(int n, int nb) {
-  return 12 * nb + 6 * n + 6 * nb + 36 * nb + n * (n + 1) / 2 + n + n;
+  return 12 * nb + 6 * n + 6 * nb + n * (n + 1) / 2 + n + n;
 }

@@ -254,13 +254,14 @@ __device__ __forceinline__ void loadState(const ModelDev& md, double* s, const L
 
 #include "contact.cuh"
 
-// Dynamics cache <-> LDS (Layout regions Tw, Sw, V, IC, M, dinv, rhs).
+// Dynamics cache <-> LDS (Layout regions Tw, Sw, V, M, dinv, rhs; the
+// adjoint backward needs no composite inertias, so they are not stored).
 __device__ __forceinline__ void dynCacheCopy(const ModelDev& md, double* s, const Layout& L, double* cache, bool store, int lane) {
   const int n = md.n, nb = md.nb;
-  const int seg[7][2] = {{L.Tw, 12 * nb}, {L.Sw, 6 * n}, {L.V, 6 * nb}, {L.IC, 36 * nb},
+  const int seg[6][2] = {{L.Tw, 12 * nb}, {L.Sw, 6 * n}, {L.V, 6 * nb},
                          {L.M, n * (n + 1) / 2}, {L.dinv, n}, {L.rhs, n}};
   int o = 0;
-  for (int k = 0; k < 7; k++) {
+  for (int k = 0; k < 6; k++) {
     const int base = seg[k][0], cnt = seg[k][1];
     if (base < 0) { o += cnt; continue; }  // region not kept in this kernel's LDS
     if (store)
@@ -543,7 +544,7 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, co
     }
     double* sn = snapshot + (size_t)env * snapDoubles;
     double* hbmWs = ws != nullptr ? ws + (size_t)blockIdx.x * wsDoubles : sn + snapWorkspaceOffset(n);
-    dynCacheCopy(md, s, L, sn + L.snDyn, false, lane);  // the forward's kinematics, IC, L, C
+    dynCacheCopy(md, s, L, sn + L.snDyn, false, lane);  // the forward's kinematics, L, C
     STAMP(21);
     const int nc = md.numPairs > 0 ? uni((int)sn[SN_NC]) : 0;
     const int m = md.numPairs > 0 ? uni((int)sn[SN_M]) : 0;

@@ -610,7 +610,6 @@ def test_forward_chunked_launches_match(monkeypatch):
     nxt1, snap1, cache1, ts, tf = _device_step(world, st, f)
     monkeypatch.setenv("NIMBLE_AMD_FWD_CHUNK", "5")
     nxt2, snap2, cache2, _, _ = _device_step(world, st, f)
-    monkeypatch.delenv("NIMBLE_AMD_FWD_CHUNK")
     assert (snap1[:, SN_NCON] > 0).any()
     assert torch.equal(nxt1, nxt2)
     assert torch.equal(cache1, cache2)
@@ -622,6 +621,7 @@ def test_forward_chunked_launches_match(monkeypatch):
         rb = b[w, SN_CONTACTS:SN_CONTACTS + CREC * nc].reshape(nc, CREC)
         assert np.array_equal(ra[:, :10], rb[:, :10]), w  # (sphere-centre slots unused for box contacts)
     g = np.random.default_rng(3).standard_normal(st.shape)
-    gs1, gf1 = _device_backward(world, ts, tf, snap1, g)
     gs2, gf2 = _device_backward(world, ts, tf, snap2, g)
+    monkeypatch.delenv("NIMBLE_AMD_FWD_CHUNK")
+    gs1, gf1 = _device_backward(world, ts, tf, snap1, g)
     assert np.array_equal(gs1, gs2) and np.array_equal(gf1, gf2)

@@ -38,7 +38,7 @@ struct nimble_world {
 
 extern "C" __global__ void nimble_forward_kernel(const ModelDev*, Layout, const double*, const double*, double*,
                                                  double*, double*, int, int);
-extern "C" __global__ void nimble_backward_kernel(const ModelDev*, Layout, int, const double*, const double*,
+extern "C" __global__ void nimble_backward_kernel(const ModelDev*, int, const double*, const double*,
                                                   double*, int, const double*, double*, double*, int, double*, int);
 
 static void isoInverse(const double* T, double* O) {
@@ -251,6 +251,8 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
   // dynamics cache at the tail of every snapshot
   w->fwd.snDyn = w->bwd.snDyn = w->snapDoubles;
   w->snapDoubles += dynCacheDoubles(m.n, m.nb);
+  m.lay[0] = w->fwd;
+  m.lay[1] = w->bwd;
   hipError_t e = hipMalloc(&w->dev, sizeof(ModelDev));
   if (e != hipSuccess) { delete w; return fail(NIMBLE_ERR_HIP, std::string("hipMalloc: ") + hipGetErrorString(e)); }
   e = hipMemcpy(w->dev, &m, sizeof(ModelDev), hipMemcpyHostToDevice);
@@ -316,7 +318,7 @@ int nimble_backward(nimble_world_t w, int32_t batch, const double* state, const 
     return fail(NIMBLE_ERR_INVALID, "null buffer");
   hipStream_t st = (hipStream_t)stream;
   const size_t lds = (size_t)w->bwd.total * sizeof(double);
-  hipLaunchKernelGGL(nimble_backward_kernel, dim3(gridFor(batch)), dim3(64), lds, st, w->dev, w->bwd, batch, state,
+  hipLaunchKernelGGL(nimble_backward_kernel, dim3(gridFor(batch)), dim3(64), lds, st, w->dev, batch, state,
                      forces, snapshot, w->snapDoubles, grad_next_state, grad_state, grad_forces, 1, (double*)nullptr, 0);
   HIP_TRY(hipGetLastError());
   return NIMBLE_OK;
@@ -348,7 +350,7 @@ int nimble_jacobians(nimble_world_t w, int32_t batch, const double* state, const
   const int grid = items < JAC_GRID ? (int)items : JAC_GRID;
   hipStream_t st = (hipStream_t)stream;
   const size_t lds = (size_t)w->bwd.total * sizeof(double);
-  hipLaunchKernelGGL(nimble_backward_kernel, dim3(grid), dim3(64), lds, st, w->dev, w->bwd, batch, state, forces,
+  hipLaunchKernelGGL(nimble_backward_kernel, dim3(grid), dim3(64), lds, st, w->dev, batch, state, forces,
                      const_cast<double*>(snapshot), w->snapDoubles, (const double*)nullptr, state_jacobian,
                      force_jacobian, rows, w->jacWsDoubles > 0 ? workspace : (double*)nullptr, w->jacWsDoubles);
   HIP_TRY(hipGetLastError());

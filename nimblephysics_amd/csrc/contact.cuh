@@ -1412,7 +1412,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   const int nc = uni((int)ct[H_NC]);
   for (int i = lane; i < nc; i += WAVE) snap[SN_FC + i] = P.fc[i];
   for (int i = lane; i < n; i += WAVE) snap[snYf(n) + i] = ddq[i];
-  backwardPrecompute<kLds>(md, sIn, L, lane, poolIn, m, cfm, snap, sp<true>(ct));
+  backwardPrecompute<kLds>(md, sIn, md.lay[0], lane, poolIn, m, cfm, snap, sp<true>(ct));  // (not inlined)
   if (lane == 0) {
     snap[SN_NCON] = nCon;
     snap[SN_M] = m;

@@ -11,6 +11,22 @@
 #define ND_MAX NIMBLE_MAX_DOFS
 #define NS_MAX NIMBLE_MAX_SHAPES
 
+// LDS layout (in doubles) for one world instance; offsets computed on host.
+struct Layout {
+  int q, v, tau, Tw, Sw, V, A, IC, F, M, rhs, x, scratch;
+  // backward extras: per-body adjoint vectors (7 x 6) and W, dof vectors
+  int adj, Wt, w, gp, gv;
+  // contacts: stage header/lists, post-dynamics velocity, LCP workspace pool
+  int ct, v1, pool, poolCap, dinv;
+  // offset (doubles) of the dynamics cache inside each world's snapshot
+  int snDyn;
+  // forward: narrow-phase scratch (dropped list + pair buffers), placed past
+  // the dynamics buffers V/A/IC/F so the helper wave can run the collision
+  // detection while wave 0 is still in the dynamics
+  int cscr;
+  int total;
+};
+
 struct ModelDev {
   int nb, n, ns, maxDepth;
   int numFree;
@@ -42,20 +58,10 @@ struct ModelDev {
   // candidate pairs (i < j) after BodyNodeCollisionFilter, in detector order
   int numPairs, pairChunk;
   int pairA[NS_MAX * (NS_MAX - 1) / 2], pairB[NS_MAX * (NS_MAX - 1) / 2];
+  // the kernels' LDS layouts, [0] forward, [1] backward.  Functions that are
+  // not inlined take them from here (through the scalar cache): a by-value
+  // kernel argument passed to them by reference is copied into per-lane
+  // scratch, ~7 KB of stores per wave
+  Layout lay[2];
 };
 
-// LDS layout (in doubles) for one world instance; offsets computed on host.
-struct Layout {
-  int q, v, tau, Tw, Sw, V, A, IC, F, M, rhs, x, scratch;
-  // backward extras: per-body adjoint vectors (7 x 6) and W, dof vectors
-  int adj, Wt, w, gp, gv;
-  // contacts: stage header/lists, post-dynamics velocity, LCP workspace pool
-  int ct, v1, pool, poolCap, dinv;
-  // offset (doubles) of the dynamics cache inside each world's snapshot
-  int snDyn;
-  // forward: narrow-phase scratch (dropped list + pair buffers), placed past
-  // the dynamics buffers V/A/IC/F so the helper wave can run the collision
-  // detection while wave 0 is still in the dynamics
-  int cscr;
-  int total;
-};

@@ -325,7 +325,7 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, const double* 
         collideWait(ct, CS_GO);
         collideWorld(md, lds<true>(s), L, lane, snapshot + (size_t)env * snapDoubles + snEdge(n));
         collidePost(ct, CS_DONE, lane);
-        helperWave(md, s, L, lane);
+        helperWave(md, s, md.lay[0], lane);  // not inlined: the model's copy of L, not the argument's
       }
       return;
     }
@@ -512,12 +512,13 @@ __device__ void rightJacobianCol(const double* th, int k, double* o) {
 // needs an off-chip LCP workspace uses its workgroup's slice of `ws`
 // (wsDoubles per workgroup; a workgroup runs its items one after another).
 extern "C" __global__ void __launch_bounds__(WAVE)
-nimble_backward_kernel(const ModelDev* __restrict__ mdp, Layout L, int batch, const double* __restrict__ state,
+nimble_backward_kernel(const ModelDev* __restrict__ mdp, int batch, const double* __restrict__ state,
                        const double* __restrict__ forces, double* __restrict__ snapshot, int snapDoubles,
                        const double* __restrict__ gradNext, double* __restrict__ gradState,
                        double* __restrict__ gradForces, int rows, double* __restrict__ ws, int wsDoubles) {
   extern __shared__ double s[];
   const ModelDev& md = *mdp;
+  const Layout& L = md.lay[1];
   const int lane = threadIdx.x;
   const int n = md.n;
   const double dt = md.dt;

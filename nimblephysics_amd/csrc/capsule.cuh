@@ -35,6 +35,10 @@
 #define CT_VERTEX_PIPE 11
 #define CT_PIPE_EDGE 12
 #define CT_EDGE_PIPE 13
+// a capsule end against a parallel box edge (SPHERE_EDGE / EDGE_SPHERE,
+// the reference's 8 / 11); geometry only, its gradients are NaN there
+#define CT_SPHERE_EDGE 14
+#define CT_EDGE_SPHERE 15
 
 namespace cap {
 
@@ -731,8 +735,44 @@ __device__ __noinline__ int deviceCapsuleBox(const double* Tb, const double* bs,
     }
     if (nw == 2) {
       const V pipeDir = eigNormalized(axis), edgeDir = eigNormalized(sub(W[1], W[0]));
-      // an edge parallel to the pipe (:3118) is not restated
-      if (fabs(1.0 - fabs(dot(pipeDir, edgeDir))) < 1e-5) { *unsup = 1; return 0; }
+      if (fabs(1.0 - fabs(dot(pipeDir, edgeDir))) < 1e-5) {
+        // an edge parallel to the pipe (:3122): one contact at each end of
+        // the overlap -- PIPE_VERTEX at an edge end the capsule passes, else
+        // SPHERE_EDGE at the capsule end (the reference leaves that
+        // contact's sphereCenter NaN, Contact.cpp:59, so its gradient is NaN:
+        // flagged unsupported, the contact kept)
+        const double eA = dot(edgeDir, W[0]), eB = dot(edgeDir, W[1]);
+        const double cA = dot(edgeDir, capA), cB = dot(edgeDir, capB);
+        V nv = sub(capA, W[0]);
+        nv = sub(nv, scl(edgeDir, dot(nv, edgeDir)));
+        const double dep = r - sqrt(len2(nv));
+        nv = eigNormalized(nv);
+        if (!(dep > 0 && dep < clip)) return 0;
+        const V onrm = boxFirst ? scl(nv, -1.0) : nv;
+        for (int end = 0; end < 2; end++) {
+          double* o = out + PBREC * end;
+          const bool lowEnd = end == 0;
+          const bool vertex = lowEnd ? fmin(cA, cB) < fmin(eA, eB) : fmax(cA, cB) > fmax(eA, eB);
+          if (vertex) {
+            const V vp = lowEnd ? (eA < eB ? W[0] : W[1]) : (eA < eB ? W[1] : W[0]);
+            pipeRecord(o, vp, onrm, dep, boxFirst ? CT_VERTEX_PIPE : CT_PIPE_VERTEX, add(vp, scl(nv, r)));
+            // the low end of collideCapsuleBox keeps pipeFixedPoint = capsuleB
+            // and the unnormalised axis as pipeDir (:3177-:3178)
+            const bool asIs = lowEnd && !boxFirst;
+            put3(o + CREC, asIs ? capB : capA);
+            put3(o + CREC + 3, asIs ? axis : pipeDir);
+          } else {
+            const V cp = lowEnd ? (cA < cB ? capA : capB) : (cA < cB ? capB : capA);
+            const V pt = sub(cp, scl(nv, r));
+            pipeRecord(o, pt, onrm, dep, boxFirst ? CT_EDGE_SPHERE : CT_SPHERE_EDGE, pt);
+            put3(o + CREC, W[0]);
+            put3(o + CREC + 3, edgeDir);
+            *unsup = 1;
+          }
+          o[8] = body1; o[9] = body2;
+        }
+        return 2;
+      }
       // edge-pipe (:3225)
       double alpha, beta;
       segClosest(W[0], capA, W[1], capB, alpha, beta);

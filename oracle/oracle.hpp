@@ -40,7 +40,8 @@ struct Kin {
 // pipe-mesh contact types of the capsule-box branches (this package's
 // numbering; the reference's PIPE_VERTEX 16 / VERTEX_PIPE 18 / PIPE_EDGE 17 /
 // EDGE_PIPE 19, dart/collision/Contact.hpp:76)
-enum { CT_PIPE_VERTEX = 10, CT_VERTEX_PIPE = 11, CT_PIPE_EDGE = 12, CT_EDGE_PIPE = 13 };
+enum { CT_PIPE_VERTEX = 10, CT_VERTEX_PIPE = 11, CT_PIPE_EDGE = 12, CT_EDGE_PIPE = 13, CT_SPHERE_EDGE = 14,
+       CT_EDGE_SPHERE = 15 };
 
 struct Contact {
   int shapeA, shapeB, bodyA, bodyB;

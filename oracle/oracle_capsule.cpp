@@ -19,15 +19,14 @@
 //    (:3366) with createFaceFaceContacts (:2203), keepOnlyConvex2DHull (:3545),
 //    math::prepareConvex2DShape / pointInPlane (dart/math/Geometry.cpp:3813,
 //    :3843), convex2DShapeContains (:3756), get2DLineIntersection (:3790).
-// and createCapsuleMeshContact's vertex-pipe (one box witness point) and
-// non-parallel edge-pipe (two) branches (:3071, :3225) and the EDGE_EDGE
-// contacts of its face branch, converted to PIPE_EDGE / EDGE_PIPE (:3320,
-// :3494) -- with createFaceFaceContacts' edge intersections (:2403,
+// and createCapsuleMeshContact's vertex-pipe (one box witness point),
+// edge-pipe (two; :3071, :3225, the parallel case :3122) branches and the
+// EDGE_EDGE contacts of its face branch, converted to PIPE_EDGE / EDGE_PIPE
+// (:3320, :3494) -- with createFaceFaceContacts' edge intersections (:2403,
 // get2DLineIntersection :3790, math::getContactPoint Geometry.cpp:1075).
-// Not restated (flagged `unsupported`, contact dropped): an edge parallel to
-// the pipe (:3118; the reference's SPHERE_EDGE contacts there carry a NaN
-// sphere centre into their gradients) and the 8-point witness set of a zero
-// penetration direction.
+// Flagged `unsupported`: the parallel case's SPHERE_EDGE contacts (kept; the
+// reference carries a NaN sphere centre into their gradients) and the
+// 8-point witness set of a zero penetration direction (dropped).
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -736,7 +735,51 @@ int capsuleBox(const Iso<double>& Tb, const double* size, const Iso<double>& Tc,
   }
   if (W.size() == 2) {
     const V pipeDir = eigNormalized(axis), edgeDir = eigNormalized(W[1] - W[0]);
-    if (std::fabs(1.0 - std::fabs(dot(pipeDir, edgeDir))) < 1e-5) { *unsupported = 1; return 0; }
+    if (std::fabs(1.0 - std::fabs(dot(pipeDir, edgeDir))) < 1e-5) {
+      // the edge is parallel to the pipe (:3122-:3300): a contact at each end
+      // of the overlap, PIPE_VERTEX (VERTEX_PIPE) at an edge end the capsule
+      // passes, else SPHERE_EDGE (EDGE_SPHERE) at the capsule end.  Those
+      // leave Contact::sphereCenter NaN (Contact.cpp:59), which their
+      // gradients read (DifferentiableContactConstraint.cpp:770): flagged
+      // unsupported, the contacts kept.
+      const double eA = dot(edgeDir, W[0]), eB = dot(edgeDir, W[1]);
+      const double cA = dot(edgeDir, capA), cB = dot(edgeDir, capB);
+      const double edgeMin = eA < eB ? eA : eB, edgeMax = eA < eB ? eB : eA;
+      const V edgeMinP = eA < eB ? W[0] : W[1], edgeMaxP = eA < eB ? W[1] : W[0];
+      const double capMin = cA < cB ? cA : cB, capMax = cA < cB ? cB : cA;
+      const V capMinP = cA < cB ? capA : capB, capMaxP = cA < cB ? capB : capA;
+      V normal = capA - W[0];
+      normal = normal - edgeDir * dot(normal, edgeDir);
+      const double dist = std::sqrt(len2(normal));
+      normal = eigNormalized(normal);
+      const double depth = r - dist;
+      int added = 0;
+      for (int end = 0; end < 2; end++) {
+        const bool low = end == 0;
+        Contact c{};
+        setV(c.normal, boxFirst ? normal * -1.0 : normal);
+        c.depth = depth;
+        if (low ? capMin < edgeMin : capMax > edgeMax) {
+          const V vp = low ? edgeMinP : edgeMaxP;
+          setV(c.point, vp);
+          c.type = boxFirst ? CT_VERTEX_PIPE : CT_PIPE_VERTEX;
+          // collideCapsuleBox's low end keeps pipeFixedPoint = capsuleB and the
+          // unnormalised axis (:3177-:3178); the other three use capsuleA
+          const bool asIs = low && !boxFirst;
+          setPipe(c, vp + normal * r, asIs ? capB : capA, asIs ? axis : pipeDir);
+        } else {
+          const V pt = (low ? capMinP : capMaxP) - normal * r;
+          setV(c.point, pt);
+          c.type = boxFirst ? CT_EDGE_SPHERE : CT_SPHERE_EDGE;
+          setV(c.edgeAClosest, pt);
+          setV(c.edgeAFixed, W[0]);
+          setV(c.edgeADir, edgeDir);
+          *unsupported = 1;
+        }
+        if (c.depth > 0 && c.depth < clip) { emit(c); added++; }
+      }
+      return added;
+    }
     // edge-pipe (:3225): dSegmentsClosestApproach(W0, capA, W1, capB)
     double alpha, beta;
     segmentsClosestApproach(W[0].x, capA.x, W[1].x, capB.x, &alpha, &beta);

@@ -16,6 +16,8 @@ copied from the cited test body, as the formula it is written with).
     :3272 CAPSULE_BOX_PIPE_VERTEX_COLLISION
     :2936 CAPSULE_BOX_SPHERE_AND_PIPE_EDGE_COLLISION (capsule first; contacts
           in sortContacts(UnitZ) order)
+    :3429 CAPSULE_BOX_PIPE_EDGE_PARALLEL_VERTEX_COLLISION
+    :3662 CAPSULE_BOX_PIPE_EDGE_PARALLEL_SPHERE_COLLISION
 
 The sphere tests collide a sphere with a unit box *mesh* (ccdMPRPenetration +
 createMeshSphereContact).  The same geometry through the box collider
@@ -27,7 +29,8 @@ and depth only ("check": ["normal", "depth"]).
 
 Type numbering: this package's (csrc/capsule.cuh): SPHERE_BOX 4, BOX_SPHERE 5,
 SPHERE_SPHERE 6, SPHERE_PIPE 7, PIPE_SPHERE 8, PIPE_PIPE 9, PIPE_VERTEX 10,
-VERTEX_PIPE 11, PIPE_EDGE 12, EDGE_PIPE 13 (the reference's 16 / 18 / 17 / 19); the reference's
+VERTEX_PIPE 11, PIPE_EDGE 12, EDGE_PIPE 13 (the reference's 16 / 18 / 17 / 19),
+SPHERE_EDGE 14, EDGE_SPHERE 15 (the reference's 8 / 11); the reference's
 VERTEX_SPHERE / EDGE_SPHERE / FACE_SPHERE (mesh first) correspond to the box
 collider's BOX_SPHERE, SPHERE_VERTEX / SPHERE_EDGE / SPHERE_FACE to
 SPHERE_BOX.
@@ -42,6 +45,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = "unittests/unit/test_DARTCollide.cpp"
 SPHERE_BOX, BOX_SPHERE, SPHERE_SPHERE, SPHERE_PIPE, PIPE_SPHERE, PIPE_PIPE = 4, 5, 6, 7, 8, 9
 PIPE_VERTEX, VERTEX_PIPE, PIPE_EDGE, EDGE_PIPE = 10, 11, 12, 13
+SPHERE_EDGE, EDGE_SPHERE = 14, 15
 
 
 def euler_xyz(a, b, c):
@@ -142,6 +146,26 @@ def main():
     cases.append({"name": "capsule_box_sphere_and_pipe_edge", "source": f"{SRC}:2936", "sort": "z",
                   "a": [["capsule", [r, h]], iso((0, 0.99, 1.0)).tolist()], "b": [["box", [2.0, 1.0, 2.0]], iso().tolist()],
                   "ab": [contact([0, 0.5, 0.5], ey, 0.01, SPHERE_BOX), contact([0, 0.5, 1.0], ey, 0.01, PIPE_EDGE)]})
+    # :3429 a capsule (height 2) lying parallel to a box edge and past both
+    # of its ends: a PIPE_VERTEX contact at each end of the edge
+    s2 = math.sqrt(r * r / 2) - math.sqrt(0.01 * 0.01 / 2)
+    T2 = iso((0.5 + s2, 0.5 + s2, 0))
+    n = np.array([1.0, 1.0, 0.0]) / math.sqrt(2)
+    cases.append({"name": "capsule_box_pipe_edge_parallel_vertex", "source": f"{SRC}:3429", "sort": "z",
+                  "a": [["capsule", [r, 2.0]], T2.tolist()], "b": box,
+                  "ab": [contact([0.5, 0.5, -0.5], n, 0.01, PIPE_VERTEX), contact([0.5, 0.5, 0.5], n, 0.01, PIPE_VERTEX)],
+                  "ba": [contact([0.5, 0.5, -0.5], -n, 0.01, VERTEX_PIPE),
+                         contact([0.5, 0.5, 0.5], -n, 0.01, VERTEX_PIPE)]})
+    # :3662 the same against a 1 x 1 x 2 box, the capsule (height 1) inside
+    # the edge's span: SPHERE_EDGE / EDGE_SPHERE at the capsule ends (geometry
+    # only: the reference's gradients of these read a NaN sphere centre, so
+    # the step flags them unsupported)
+    q = 0.5 - math.sqrt(0.01 * 0.01 / 2)
+    cases.append({"name": "capsule_box_pipe_edge_parallel_sphere", "source": f"{SRC}:3662", "sort": "z",
+                  "unsupported": True,
+                  "a": [["capsule", [r, 1.0]], T2.tolist()], "b": [["box", [1.0, 1.0, 2.0]], iso().tolist()],
+                  "ab": [contact([q, q, -0.5], n, 0.01, SPHERE_EDGE), contact([q, q, 0.5], n, 0.01, SPHERE_EDGE)],
+                  "ba": [contact([q, q, -0.5], -n, 0.01, EDGE_SPHERE), contact([q, q, 0.5], -n, 0.01, EDGE_SPHERE)]})
     out = {"source": SRC + " (reference), transcribed by tests/golden/make_collide_known_answers.py; "
                            "'ab' = collide(a, b), 'ba' = collide(b, a); tolerance 1e-10 as in the tests "
                            "(1e-8 depth for the mesh-sphere cases)",

@@ -24,7 +24,7 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 
 RTOL = 1e-6
-SN_NCON, SN_M, SN_NC, SN_NU = 0, 1, 2, 3
+SN_NCON, SN_M, SN_NC, SN_NU, SN_STATUS = 0, 1, 2, 3, 5
 CREC = 13  # contact record doubles (csrc/pool_sizes.h)
 SN_CONTACTS, SN_ROWREC, RR_MAP = 16, 12, 7
 SN_ROWS = SN_CONTACTS + 16 * CREC
@@ -524,9 +524,13 @@ def test_collider_known_answers_on_device(order):
             assert np.allclose(c[3:6], e["normal"], atol=1e-10), case["name"]
             assert abs(c[6] - e["depth"]) < 1e-8, case["name"]
             assert (int(c[7]) & 15) == e["type"], case["name"]
+        # ST_UNSUPPORTED_SHAPE (2) exactly where the reference's contacts have
+        # undefined (NaN) gradients
+        assert bool(int(sn[SN_STATUS]) & 2) == case.get("unsupported", False), case["name"]
 
 
-@pytest.mark.parametrize("name", ["capsule_box_pipe_edge", "capsule_box_pipe_vertex", "capsule_box_sphere_and_pipe_edge"])
+@pytest.mark.parametrize("name", ["capsule_box_pipe_edge", "capsule_box_pipe_vertex", "capsule_box_sphere_and_pipe_edge",
+                                  "capsule_box_pipe_edge_parallel_vertex"])
 @pytest.mark.parametrize("order", ["ab", "ba"])
 def test_pipe_box_contact_parity(name, order):
     """createCapsuleMeshContact's vertex-pipe, edge-pipe and face-edge

@@ -178,6 +178,21 @@ int nimble_backward(nimble_world_t world, int32_t batch, const double* state,
                     double* grad_forces, void* stream);
 
 /*
+ * nimble_backward plus the gradient with respect to every body's mass:
+ *   grad_masses [batch][num_bodies]  dL/d(mass of body b), device
+ * == BackpropSnapshot::backpropState's lossWrtMass = getMassVelJacobian^T
+ * dL/dv' (dart/neural/BackpropSnapshot.cpp:177, :580; getVelJacobianWrt with
+ * WithRespectTo::MASS, :980) for a world whose getMassDims() entries are the
+ * bodies' masses (World::tuneMass with INERTIA_MASS); the Python layer picks
+ * the tuned bodies' columns (python/nimblephysics/timestep.py:34, :57
+ * `mass` / lossWrtMass).
+ */
+int nimble_backward_masses(nimble_world_t world, int32_t batch, const double* state,
+                           const double* forces, double* snapshot,
+                           const double* grad_next_state, double* grad_state,
+                           double* grad_forces, double* grad_masses, void* stream);
+
+/*
  * Batched step Jacobians of a forward's snapshot, without bound clipping:
  *   state_jacobian [batch][2n][2n]  d(next_state)/d(state) ==
  *       BackpropSnapshot::getStateJacobian (dart/neural/BackpropSnapshot.cpp:1230):

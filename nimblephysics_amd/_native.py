@@ -37,6 +37,8 @@ def lib():
         L.nimble_forward.restype = C.c_int
         L.nimble_backward.argtypes = [C.c_void_p, C.c_int32] + [C.c_void_p] * 6 + [C.c_void_p]
         L.nimble_backward.restype = C.c_int
+        L.nimble_backward_masses.argtypes = [C.c_void_p, C.c_int32] + [C.c_void_p] * 7 + [C.c_void_p]
+        L.nimble_backward_masses.restype = C.c_int
         L.nimble_last_error.argtypes = []
         L.nimble_last_error.restype = C.c_char_p
         L.nimble_jacobian_workspace_doubles.argtypes = [C.c_void_p, C.c_int32]
@@ -101,6 +103,7 @@ class DeviceWorld:
         self.h = h
         self.device_index = int(device_index)
         self.n = world.getNumDofs()
+        self.nb = int(desc.num_bodies)
         self.snapshot_doubles = int(L.nimble_snapshot_doubles(h))
         self.cache_doubles = int(L.nimble_lcp_cache_doubles(h))
         self.num_pairs = int(L.nimble_num_collision_pairs(h))
@@ -160,6 +163,21 @@ class DeviceWorld:
         self._shapes(B, grad_state)
         _check(lib().nimble_backward(self.h, B, _ptr(state), _ptr(forces), _ptr(snapshot), _ptr(grad_next),
                                      _ptr(grad_state), _ptr(grad_forces), C.c_void_p(stream_ptr)))
+
+    def backward_masses(self, state, forces, snapshot, grad_next, grad_state, grad_forces, grad_masses,
+                        stream_ptr: int):
+        """backward() plus dL/d(body masses) [B, num_bodies] (nimble_backward_masses)."""
+        _require_device(state, forces, snapshot, grad_next, grad_state, grad_forces, grad_masses)
+        B = state.shape[0]
+        self._on_my_device(state, forces, snapshot, grad_next, grad_state, grad_forces, grad_masses)
+        self._shapes(B, state, forces, snapshot)
+        self._shapes(B, grad_next, grad_forces)
+        self._shapes(B, grad_state)
+        if tuple(grad_masses.shape) != (B, self.nb) or not grad_masses.is_contiguous():
+            raise ValueError(f"grad_masses shape {tuple(grad_masses.shape)} != ({B}, {self.nb})")
+        _check(lib().nimble_backward_masses(self.h, B, _ptr(state), _ptr(forces), _ptr(snapshot), _ptr(grad_next),
+                                            _ptr(grad_state), _ptr(grad_forces), _ptr(grad_masses),
+                                            C.c_void_p(stream_ptr)))
 
 
     def jacobians(self, state, forces, snapshot, stream_ptr: int):

@@ -515,7 +515,8 @@ extern "C" __global__ void __launch_bounds__(WAVE)
 nimble_backward_kernel(const ModelDev* __restrict__ mdp, int batch, const double* __restrict__ state,
                        const double* __restrict__ forces, double* __restrict__ snapshot, int snapDoubles,
                        const double* __restrict__ gradNext, double* __restrict__ gradState,
-                       double* __restrict__ gradForces, int rows, double* __restrict__ ws, int wsDoubles) {
+                       double* __restrict__ gradForces, int rows, double* __restrict__ ws, int wsDoubles,
+                       double* __restrict__ gradMasses) {
   extern __shared__ double s[];
   const ModelDev& md = *mdp;
   const Layout& L = md.lay[1];
@@ -660,6 +661,54 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, int batch, const double
       WSYNC();
     }
     STAMP(25);
+    if (gradMasses != nullptr) {
+      // lossWrtMass = getMassVelJacobian^T gv (BackpropSnapshot.cpp:177, :580:
+      // getVelJacobianWrt(WithRespectTo::MASS), :980) for every body mass.  The
+      // mass enters M and C only (not A_c, springs or the integration), so it
+      // takes the M / C terms of the position gradient above, with
+      // d/dq replaced by d/dm_b:  -dt (dID(q,v,a*)/dm_b)^T (w - nu) plus the
+      // M-derivative pairs  sum coef * (d(M a)/dm_b)^T c.  With the world COM
+      // c_b, dI_b/dm_b y = [c x u_y; u_y], u_y = y_lin - c x y_ang (the COM
+      // point's velocity under twist y), so (d(M a)/dm_b)^T c = u_a . u_c and
+      // y^T dID/dm_b = V_y^T [dI (A_b - a_g) + V_b x* (dI V_b)].
+      if (lane < md.nb) {
+        const int b = lane;
+        const double* Tw = s + L.Tw + 12 * b;
+        double cw[3];
+        for (int r = 0; r < 3; r++)
+          cw[r] = Tw[r * 4] * md.com[b][0] + Tw[r * 4 + 1] * md.com[b][1] + Tw[r * 4 + 2] * md.com[b][2] + Tw[r * 4 + 3];
+        auto comVel = [&](const double* y, double* u) {
+          double cx[3];
+          cross3(cw, y, cx);  // c x y_ang
+          for (int i = 0; i < 3; i++) u[i] = y[3 + i] - cx[i];
+        };
+        const double ag[6] = {0, 0, 0, md.g[0], md.g[1], md.g[2]};
+        const double* Vb = s + L.V + 6 * b;
+        double Ab[6], uA[3], uV[3], uW[3], Vw[6], h[6], fh[6];
+        for (int i = 0; i < 6; i++) Ab[i] = s[L.A + 6 * b + i] - ag[i];
+        comVel(Ab, uA);
+        comVel(Vb, uV);
+        bodyTwist(md, s + L.Sw, b, s + L.w, 1, Vw);
+        comVel(Vw, uW);
+        cross3(cw, uV, h);
+        for (int i = 0; i < 3; i++) h[3 + i] = uV[i];
+        crf(Vb, h, fh);  // V_b x* (dI V_b)
+        double val = -dt * (uW[0] * uA[0] + uW[1] * uA[1] + uW[2] * uA[2] + dot6(Vw, fh));
+        if (nc > 0) {
+          const double coef[4] = {-dt, 1.0, -(double)imp, -(double)imp};
+          for (int pr = 0; pr < (imp ? 4 : 2); pr++) {
+            double Va[6], Vc[6], ua[3], uc[3];
+            bodyTwist(md, s + L.Sw, b, P.NV + 2 * pr, NV_COLS, Va);
+            bodyTwist(md, s + L.Sw, b, P.NV + 2 * pr + 1, NV_COLS, Vc);
+            comVel(Va, ua);
+            comVel(Vc, uc);
+            val += coef[pr] * (ua[0] * uc[0] + ua[1] * uc[1] + ua[2] * uc[2]);
+          }
+        }
+        gradMasses[(size_t)item * md.nb + b] = val;
+      }
+      WSYNC();
+    }
     // FreeJoint posPos / velPos blocks: central differences exactly as
     // FreeJoint::finiteDifferencePosPosJacobian / VelPosJacobian
     // (FreeJoint.cpp:965, :987); 24 lanes, one perturbed integration each.

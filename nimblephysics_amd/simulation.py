@@ -32,6 +32,7 @@ class World:
         self.action_space: Optional[List[int]] = None
         self._forces: Optional[np.ndarray] = None
         self._version = 0
+        self._mass_tuned = []  # (body node, upper bound, lower bound) per mass dim
         self._native_by_dev = {}  # device index -> (version, DeviceWorld)
 
     # --- model ------------------------------------------------------------------
@@ -186,21 +187,49 @@ class World:
         f = self.getControlForces()
         return np.array([f[m] for m in self.getActionSpace()])
 
-    # --- tunable masses (World::getMassDims / getMasses / setMasses,
-    # dart/simulation/World.cpp) --------------------------------------------------------
-    # No body is registered for mass tuning (World::tuneMass is not on the
-    # batched path), which is the reference's default: the mass vector has
-    # zero entries and TimestepLayer's lossWrtMass is empty.
+    # --- tunable masses (World::tuneMass / getMassDims / getMasses / setMasses,
+    # dart/simulation/World.cpp; WithRespectToMass, dart/neural/WithRespectToMass.cpp)
+    # Body masses (WrtMassBodyNodeEntryType.INERTIA_MASS) are tunable: the mass
+    # vector holds them in registration order, setMasses writes them into the
+    # bodies (the device model is rebuilt on the next step), and
+    # TimestepLayer's lossWrtMass comes from nimble_backward_masses.  The COM /
+    # inertia-tensor entry types are not on this path.
+    def tuneMass(self, node, type="INERTIA_MASS", upperBound=None, lowerBound=None):
+        kind = getattr(type, "name", type)
+        if kind != "INERTIA_MASS":
+            raise NotImplementedError(f"tuneMass: only INERTIA_MASS entries are on the batched path (got {kind})")
+        if not any(node is b for s in self.skeletons for b in s.bodies):
+            raise ValueError("tuneMass: the body node is not in this world")
+        if any(node is b for b, _, _ in self._mass_tuned):
+            raise ValueError("tuneMass: body already registered")
+        up = np.asarray(upperBound if upperBound is not None else [np.inf], dtype=np.float64).reshape(-1)[0]
+        lo = np.asarray(lowerBound if lowerBound is not None else [0.0], dtype=np.float64).reshape(-1)[0]
+        self._mass_tuned.append((node, float(up), float(lo)))
+
     def getMassDims(self) -> int:
-        return 0
+        return len(self._mass_tuned)
 
     def getMasses(self):
-        return np.zeros(0)
+        return np.array([b.getMass() for b, _, _ in self._mass_tuned], dtype=np.float64)
+
+    def getMassUpperBound(self):
+        return np.array([u for _, u, _ in self._mass_tuned], dtype=np.float64)
+
+    def getMassLowerBound(self):
+        return np.array([l for _, _, l in self._mass_tuned], dtype=np.float64)
 
     def setMasses(self, masses):
         masses = np.asarray(masses, dtype=np.float64).reshape(-1)
         if masses.shape[0] != self.getMassDims():
             raise ValueError(f"setMasses: {masses.shape[0]} values, the world has {self.getMassDims()} mass dims")
+        for (b, _, _), m in zip(self._mass_tuned, masses):
+            if b.getMass() != float(m):  # an unchanged mass keeps the device model
+                b.setMass(float(m))
+
+    def _mass_body_indices(self):
+        """Global body index (device model order) of each tuned mass."""
+        order = [b for s in self.skeletons for b in s.bodies]
+        return [next(i for i, o in enumerate(order) if o is b) for b, _, _ in self._mass_tuned]
 
     # --- flattening -----------------------------------------------------------------------
     def desc_arrays(self) -> Dict[str, np.ndarray]:

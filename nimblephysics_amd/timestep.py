@@ -24,8 +24,11 @@ call raises ContactCapacityError naming them; ``world.getLastStatus()`` holds
 the per-world status bits of the last call either way.
 
 ``mass`` is the reference's tuned-mass vector (World::getMassDims entries,
-set with World::setMasses); no body is registered for mass tuning on this
-path, so it is empty when given and its gradient (lossWrtMass) is empty.
+registered with World::tuneMass(body, INERTIA_MASS), set with
+World::setMasses before the step): 1-D, shared by every world of the batch
+(the device model is rebuilt when it changes).  Its gradient is lossWrtMass
+(BackpropSnapshot::getMassVelJacobian^T dL/dv', nimble_backward_masses),
+summed over the batch for a batched state.
 """
 from __future__ import annotations
 
@@ -131,18 +134,17 @@ def step_batch(world: World, st: torch.Tensor, act: torch.Tensor):
 class TimestepLayer(torch.autograd.Function):
     @staticmethod
     def forward(ctx, world: World, state: torch.Tensor, action: torch.Tensor, mass: Optional[torch.Tensor]):
-        # `mass` follows the reference (timestep.py:34, world.setMasses): a
-        # vector of the world's getMassDims() tuned masses -- zero of them
-        # here (World::tuneMass is not on the batched path), so only an empty
-        # vector (or [B, 0]) is accepted and its gradient is empty
+        # `mass` follows the reference (timestep.py:34, world.setMasses): the
+        # world's getMassDims() tuned body masses, one vector for the batch
         ctx.use_mass = mass is not None
         if ctx.use_mass:
-            if mass.shape[-1] != world.getMassDims():
-                raise NotImplementedError(
-                    f"mass has {mass.shape[-1]} entries; tuned masses (World::tuneMass) are not on the batched "
-                    f"path and this world has {world.getMassDims()} mass dims")
+            if mass.dim() != 1 or mass.shape[0] != world.getMassDims():
+                raise ValueError(f"mass must be a vector of the world's {world.getMassDims()} tuned masses "
+                                 f"(World::tuneMass), got shape {tuple(mass.shape)}")
+            world.setMasses(mass.detach().cpu().numpy())
             ctx.mass_shape = tuple(mass.shape)
             ctx.mass_device = mass.device
+            ctx.mass_index = world._mass_body_indices()
         ctx.out_device = state.device
         cdev = _compute_device(state)
         with torch.cuda.device(cdev):
@@ -183,10 +185,18 @@ class TimestepLayer(torch.autograd.Function):
             gs = torch.empty_like(st)
             gf = torch.empty_like(forces)
             stream = torch.cuda.current_stream(st.device).cuda_stream
-            dev.backward(st, forces, snap, g, gs, gf, stream)
+            gm = None
+            if ctx.use_mass and len(ctx.mass_index) > 0:
+                gmb = torch.empty((st.shape[0], dev.nb), dtype=torch.float64, device=st.device)
+                dev.backward_masses(st, forces, snap, g, gs, gf, gmb, stream)
+                sel = torch.tensor(ctx.mass_index, dtype=torch.long, device=st.device)
+                gm = gmb.index_select(1, sel).sum(0).to(ctx.mass_device)
+            else:
+                dev.backward(st, forces, snap, g, gs, gf, stream)
             ga = gf if idx.shape[0] == gf.shape[1] and ctx.identity else gf.index_select(1, idx)
         od = ctx.out_device
-        gm = torch.zeros(ctx.mass_shape, dtype=torch.float64, device=ctx.mass_device) if ctx.use_mass else None
+        if ctx.use_mass and gm is None:
+            gm = torch.zeros(ctx.mass_shape, dtype=torch.float64, device=ctx.mass_device)
         if ctx.squeeze:
             return None, gs[0].to(od), ga[0].to(od), gm
         return None, gs.to(od), ga.to(od), gm

@@ -71,8 +71,10 @@ def test_world_description_atlas():
 
 def test_mass_argument_follows_reference_mass_dims():
     """timestep(world, state, action, mass): the reference's mass vector has
-    getMassDims() entries (zero unless bodies are registered for mass
-    tuning); a non-empty one is rejected before any device work."""
+    getMassDims() entries, one per World::tuneMass(body, INERTIA_MASS)
+    registration in order; setMasses writes the bodies (and re-versions the
+    device model only when a value changes); a vector of the wrong size is
+    rejected before any device work."""
     import nimblephysics_amd as nimble
     w = models.cartpole_world()
     assert w.getMassDims() == 0 and w.getMasses().shape == (0,)
@@ -80,8 +82,26 @@ def test_mass_argument_follows_reference_mass_dims():
     with pytest.raises(ValueError):
         w.setMasses(np.ones(2))
     st = torch.tensor(w.getState())
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(ValueError):
         nimble.timestep(w, st, torch.zeros(2, dtype=torch.float64), torch.ones(2, dtype=torch.float64))
+    sk = w.skeletons[0]
+    pole, cart = sk.bodies[1], sk.bodies[0]
+    w.tuneMass(pole, "INERTIA_MASS", np.array([5.0]), np.array([0.1]))
+    w.tuneMass(cart, "INERTIA_MASS")
+    with pytest.raises(ValueError):
+        w.tuneMass(pole, "INERTIA_MASS")
+    with pytest.raises(NotImplementedError):
+        w.tuneMass(cart, "INERTIA_COM")
+    assert w.getMassDims() == 2
+    assert np.allclose(w.getMasses(), [pole.getMass(), cart.getMass()])
+    assert w._mass_body_indices() == [1, 0]
+    assert w.getMassUpperBound()[0] == 5.0 and w.getMassLowerBound()[0] == 0.1
+    v0 = w._version
+    w.setMasses(w.getMasses())
+    assert w._version == v0  # unchanged masses keep the device model
+    w.setMasses([0.7, 2.5])
+    assert pole.getMass() == 0.7 and cart.getMass() == 2.5 and w._version > v0
+    assert np.asarray(w.desc_arrays()["mass"])[1] == 0.7
 
 
 def test_product_rejects_cpu_tensors():

@@ -138,6 +138,11 @@ int32_t nimble_num_collision_pairs(nimble_world_t world);
  * world's contact set did not fit this path and its step differs from the
  * reference's World::step; the host layer raises on them. */
 #define NIMBLE_SNAPSHOT_STATUS 5
+/* Number of clamping LCP rows (f_c entries) of the step, snapshot element
+ * NIMBLE_SNAPSHOT_NUM_CLAMPING; the clamping impulses f_c follow at
+ * NIMBLE_SNAPSHOT_FC (BackpropSnapshot::getClampingConstraintImpulses). */
+#define NIMBLE_SNAPSHOT_NUM_CLAMPING 2
+#define NIMBLE_SNAPSHOT_FC (16 + 13 * NIMBLE_MAX_CONTACTS + 12 * NIMBLE_MAX_LCP)
 #define NIMBLE_STATUS_CONTACT_OVERFLOW 1  /* > NIMBLE_MAX_CONTACTS contacts     */
 #define NIMBLE_STATUS_UNSUPPORTED_SHAPE 2 /* shape pair without a collider     */
 #define NIMBLE_STATUS_DROPPED_OVERFLOW 4  /* dropped-contact dedup list full   */
@@ -211,6 +216,23 @@ int nimble_jacobians(nimble_world_t world, int32_t batch, const double* state,
                      const double* forces, const double* snapshot,
                      double* state_jacobian, double* force_jacobian,
                      double* workspace, void* stream);
+
+/*
+ * Batched Jacobians of the clamping constraint impulses f_c (the snapshot's
+ * clamping rows, in the LCP's clamping order) of a forward's snapshot ==
+ * BackpropSnapshot::getJacobianOfConstraintForce (dart/neural/
+ * BackpropSnapshot.cpp:2723) for WithRespectTo POSITION / VELOCITY / FORCE:
+ *   dfc_dstate  [batch][NIMBLE_MAX_LCP][2n]  row r: d f_c[r] / d(q, v)
+ *   dfc_dforces [batch][NIMBLE_MAX_LCP][n]   row r: d f_c[r] / d tau
+ * rows r >= n_c (the world's clamping count, snapshot element
+ * NIMBLE_SNAPSHOT_NUM_CLAMPING) are zero.  Formed as vector-Jacobian products
+ * with unit upstream gradients on f_c through the backward kernel.
+ *   workspace  as for nimble_jacobians (nimble_jacobian_workspace_doubles)
+ */
+int nimble_constraint_force_jacobians(nimble_world_t world, int32_t batch, const double* state,
+                                      const double* forces, const double* snapshot,
+                                      double* dfc_dstate, double* dfc_dforces,
+                                      double* workspace, void* stream);
 
 /* Last error message (thread-local). */
 const char* nimble_last_error(void);

@@ -44,6 +44,8 @@ def lib():
         L.nimble_jacobian_workspace_doubles.argtypes = [C.c_void_p, C.c_int32]
         L.nimble_jacobian_workspace_doubles.restype = C.c_int64
         L.nimble_jacobians.argtypes = [C.c_void_p, C.c_int32] + [C.c_void_p] * 6 + [C.c_void_p]
+        L.nimble_constraint_force_jacobians.argtypes = [C.c_void_p, C.c_int32] + [C.c_void_p] * 6 + [C.c_void_p]
+        L.nimble_constraint_force_jacobians.restype = C.c_int
         L.nimble_jacobians.restype = C.c_int
         L.nimble_num_collision_pairs.argtypes = [C.c_void_p]
         L.nimble_num_collision_pairs.restype = C.c_int32
@@ -70,6 +72,9 @@ def _require_device(*tensors):
 
 # snapshot header (csrc/pool_sizes.h) and status bits (csrc/contact.cuh)
 SN_NCON, SN_M, SN_NC, SN_NU, SN_CFM, SN_STATUS = 0, 1, 2, 3, 4, 5
+MAX_CONTACTS = 16
+MAX_LCP = 3 * MAX_CONTACTS  # include/nimble_amd.h NIMBLE_MAX_LCP
+SN_FC = 16 + 13 * MAX_CONTACTS + 12 * MAX_LCP  # NIMBLE_SNAPSHOT_FC: clamping impulses f_c
 ST_CONTACT_OVERFLOW, ST_UNSUPPORTED_SHAPE, ST_DROPPED_OVERFLOW, ST_REDUCED = 1, 2, 4, 8
 ST_DIVERGES = ST_CONTACT_OVERFLOW | ST_UNSUPPORTED_SHAPE | ST_DROPPED_OVERFLOW
 
@@ -196,6 +201,24 @@ class DeviceWorld:
         _check(lib().nimble_jacobians(self.h, B, _ptr(state), _ptr(forces), _ptr(snapshot), _ptr(J), _ptr(F),
                                       _ptr(ws), C.c_void_p(stream_ptr)))
         return J, F
+
+    def constraint_force_jacobians(self, state, forces, snapshot, stream_ptr: int):
+        """(d f_c / d state [B, MAX_LCP, 2n], d f_c / d forces [B, MAX_LCP, n])
+        of the forward that wrote `snapshot` (nimble_constraint_force_jacobians;
+        rows past each world's clamping count are zero)."""
+        import torch
+        _require_device(state, forces, snapshot)
+        B = state.shape[0]
+        self._on_my_device(state, forces, snapshot)
+        self._shapes(B, state, forces, snapshot)
+        n = self.n
+        Js = torch.empty((B, MAX_LCP, 2 * n), dtype=torch.float64, device=state.device)
+        Jf = torch.empty((B, MAX_LCP, n), dtype=torch.float64, device=state.device)
+        wsd = int(lib().nimble_jacobian_workspace_doubles(self.h, B))
+        ws = torch.empty(wsd, dtype=torch.float64, device=state.device) if wsd > 0 else None
+        _check(lib().nimble_constraint_force_jacobians(self.h, B, _ptr(state), _ptr(forces), _ptr(snapshot),
+                                                       _ptr(Js), _ptr(Jf), _ptr(ws), C.c_void_p(stream_ptr)))
+        return Js, Jf
 
 
 def contact_flop_estimate(world, rows: float, clamping: float) -> dict:

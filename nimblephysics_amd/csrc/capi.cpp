@@ -40,7 +40,7 @@ extern "C" __global__ void nimble_forward_kernel(const ModelDev*, Layout, const 
                                                  double*, double*, int, int);
 extern "C" __global__ void nimble_backward_kernel(const ModelDev*, int, const double*, const double*,
                                                   double*, int, const double*, double*, double*, int, double*, int,
-                                                  double*);
+                                                  double*, int);
 
 static void isoInverse(const double* T, double* O) {
   // [R|p]^-1 = [R^T | -R^T p]
@@ -321,7 +321,7 @@ int nimble_backward(nimble_world_t w, int32_t batch, const double* state, const 
   const size_t lds = (size_t)w->bwd.total * sizeof(double);
   hipLaunchKernelGGL(nimble_backward_kernel, dim3(gridFor(batch)), dim3(64), lds, st, w->dev, batch, state,
                      forces, snapshot, w->snapDoubles, grad_next_state, grad_state, grad_forces, 1, (double*)nullptr, 0,
-                     (double*)nullptr);
+                     (double*)nullptr, 0);
   HIP_TRY(hipGetLastError());
   return NIMBLE_OK;
 }
@@ -337,7 +337,7 @@ int nimble_backward_masses(nimble_world_t w, int32_t batch, const double* state,
   const size_t lds = (size_t)w->bwd.total * sizeof(double);
   hipLaunchKernelGGL(nimble_backward_kernel, dim3(gridFor(batch)), dim3(64), lds, st, w->dev, batch, state,
                      forces, snapshot, w->snapDoubles, grad_next_state, grad_state, grad_forces, 1, (double*)nullptr, 0,
-                     grad_masses);
+                     grad_masses, 0);
   HIP_TRY(hipGetLastError());
   return NIMBLE_OK;
 }
@@ -349,7 +349,10 @@ int nimble_backward_masses(nimble_world_t w, int32_t batch, const double* state,
 
 int64_t nimble_jacobian_workspace_doubles(nimble_world_t w, int32_t batch) {
   if (!w || batch < 0) return -1;
-  const long long items = (long long)batch * 2 * w->host.n;
+  // enough for nimble_jacobians (2n items per world) and
+  // nimble_constraint_force_jacobians (NIMBLE_MAX_LCP items per world)
+  const int rows = 2 * w->host.n > NIMBLE_MAX_LCP ? 2 * w->host.n : NIMBLE_MAX_LCP;
+  const long long items = (long long)batch * rows;
   const long long grid = items < JAC_GRID ? items : JAC_GRID;
   return (int64_t)(grid * w->jacWsDoubles);
 }
@@ -371,7 +374,27 @@ int nimble_jacobians(nimble_world_t w, int32_t batch, const double* state, const
   hipLaunchKernelGGL(nimble_backward_kernel, dim3(grid), dim3(64), lds, st, w->dev, batch, state, forces,
                      const_cast<double*>(snapshot), w->snapDoubles, (const double*)nullptr, state_jacobian,
                      force_jacobian, rows, w->jacWsDoubles > 0 ? workspace : (double*)nullptr, w->jacWsDoubles,
-                     (double*)nullptr);
+                     (double*)nullptr, 0);
+  HIP_TRY(hipGetLastError());
+  return NIMBLE_OK;
+}
+
+int nimble_constraint_force_jacobians(nimble_world_t w, int32_t batch, const double* state, const double* forces,
+                                      const double* snapshot, double* dfc_dstate, double* dfc_dforces,
+                                      double* workspace, void* stream) {
+  if (!w || batch < 0) return fail(NIMBLE_ERR_INVALID, "bad arguments");
+  if (batch == 0 || w->host.n == 0) return NIMBLE_OK;
+  if (!state || !forces || !snapshot || !dfc_dstate || !dfc_dforces) return fail(NIMBLE_ERR_INVALID, "null buffer");
+  if (w->jacWsDoubles > 0 && !workspace)
+    return fail(NIMBLE_ERR_INVALID, "this model needs a Jacobian workspace (nimble_jacobian_workspace_doubles)");
+  const int rows = NIMBLE_MAX_LCP;
+  const long long items = (long long)batch * rows;
+  const int grid = items < JAC_GRID ? (int)items : JAC_GRID;
+  hipStream_t st = (hipStream_t)stream;
+  const size_t lds = (size_t)w->bwd.total * sizeof(double);
+  hipLaunchKernelGGL(nimble_backward_kernel, dim3(grid), dim3(64), lds, st, w->dev, batch, state, forces,
+                     const_cast<double*>(snapshot), w->snapDoubles, (const double*)nullptr, dfc_dstate, dfc_dforces,
+                     rows, w->jacWsDoubles > 0 ? workspace : (double*)nullptr, w->jacWsDoubles, (double*)nullptr, 1);
   HIP_TRY(hipGetLastError());
   return NIMBLE_OK;
 }

@@ -1581,7 +1581,7 @@ __device__ void tangentBasisGradient(const double* nrm, const double* g, double*
 // M-derivative pairs and mu; P.gRows / P.TAB the per-row vectors of the
 // G_j terms.  Returns the imprecise flag.
 __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& L, int lane, const double* sn,
-                                   BwdPool& P, int m, int nc, double* ct) {
+                                   BwdPool& P, int m, int nc, double* ct, int fcRow) {
   const int n = md.n;
   const double dt = md.dt;
   const double* rows = sn + SN_ROWS;
@@ -1658,12 +1658,13 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
     }
   }
   WSYNC();
-  // u = A_c_ub_E^T w ; lambda = P^T u ; beta ; rho = P lambda ; pi = u - Q^T lambda
+  // u = A_c_ub_E^T w (the adjoint of f_c; e_fcRow for getJacobianOfConstraintForce
+  // rows) ; lambda = P^T u ; beta ; rho = P lambda ; pi = u - Q^T lambda
   for (int c = lane; c < nc; c += WAVE) {
     double acc = 0;
 #pragma unroll 8
     for (int i = 0; i < n; i++) acc += AcubE[i * nc + c] * s[L.w + i];
-    P.u[c] = acc;
+    P.u[c] = fcRow >= 0 ? (c == fcRow ? 1.0 : 0.0) : acc;
   }
   WSYNC();
   for (int c = lane; c < nc; c += WAVE) {

@@ -47,6 +47,8 @@ __host__ __device__ inline int collideScratchDoubles(int pairChunk) {
 #define SN_FC (SN_ROWS + NIMBLE_MAX_LCP * SN_ROWREC)
 #define SN_VF (SN_FC + NIMBLE_MAX_LCP)
 #define SN_MAXL NIMBLE_MAX_LCP
+static_assert(SN_FC == NIMBLE_SNAPSHOT_FC && SN_NC == NIMBLE_SNAPSHOT_NUM_CLAMPING,
+              "include/nimble_amd.h snapshot offsets");
 __host__ __device__ inline int snAlign8(int x) { return ((x + 7) / 8) * 8; }
 // unconstrained acceleration Minv (tau - C - D v - K ..) of the step
 __host__ __device__ inline int snYf(int n) { return SN_VF + n; }

@@ -511,12 +511,19 @@ __device__ void rightJacobianCol(const double* th, int k, double* o) {
 // :482).  Items of one world then share its snapshot, so each item that
 // needs an off-chip LCP workspace uses its workgroup's slice of `ws`
 // (wsDoubles per workgroup; a workgroup runs its items one after another).
+// fcMode (rows == SN_MAXL): the upstream gradient sits on the clamping
+// impulses f_c instead -- item (world, r) puts e_r on f_c (no gradient on the
+// next state), so its outputs are row r of d f_c / d(q, v) and d f_c / d tau,
+// getJacobianOfConstraintForce (BackpropSnapshot.cpp:2723) for POSITION,
+// VELOCITY and FORCE; rows r >= n_c are zero.  The backward's contact terms
+// already run through lambda = (Q^+)^T u with u the adjoint of f_c, so the
+// mode only replaces u = A_c_ub_E^T Minv gv by e_r (and gv, gp by 0).
 extern "C" __global__ void __launch_bounds__(WAVE)
 nimble_backward_kernel(const ModelDev* __restrict__ mdp, int batch, const double* __restrict__ state,
                        const double* __restrict__ forces, double* __restrict__ snapshot, int snapDoubles,
                        const double* __restrict__ gradNext, double* __restrict__ gradState,
                        double* __restrict__ gradForces, int rows, double* __restrict__ ws, int wsDoubles,
-                       double* __restrict__ gradMasses) {
+                       double* __restrict__ gradMasses, int fcMode) {
   extern __shared__ double s[];
   const ModelDev& md = *mdp;
   const Layout& L = md.lay[1];
@@ -531,8 +538,15 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, int batch, const double
     double* g_stamp = md.numPairs > 0 ? snapshot + (size_t)env * snapDoubles + snapWorkspaceOffset(n) + 1000 : nullptr;
 #endif
     STAMP(20);
+    if (fcMode && (md.numPairs == 0 || unitRow >= uni((int)snapshot[(size_t)env * snapDoubles + SN_NC]))) {
+      for (int i = lane; i < 2 * n; i += WAVE) gradState[(size_t)item * 2 * n + i] = 0.0;
+      for (int i = lane; i < n; i += WAVE) gradForces[(size_t)item * n + i] = 0.0;
+      continue;
+    }
     loadState(md, s, L, lane, state + (size_t)env * 2 * n, forces + (size_t)env * n);
-    if (unitRow < 0) {
+    if (fcMode) {
+      for (int i = lane; i < n; i += WAVE) { s[L.gp + i] = 0.0; s[L.gv + i] = 0.0; }
+    } else if (unitRow < 0) {
       const double* gN = gradNext + (size_t)env * 2 * n;
       for (int i = lane; i < n; i += WAVE) {
         s[L.gp + i] = gN[i];
@@ -558,7 +572,7 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, int batch, const double
       // constrained: a* = Minv (z + A_c_ub_E f_c) / dt, w <- w - nu
       const int need = bwdPoolDoubles(m, n);
       carveBwd(need <= L.poolCap ? s + L.pool : hbmWs, m, n, P);
-      imp = contactBackwardPrep(md, s, L, lane, sn, P, m, nc, s + L.ct);
+      imp = contactBackwardPrep(md, s, L, lane, sn, P, m, nc, s + L.ct, fcMode ? unitRow : -1);
     } else {
       // z = dt (tau - C - D v - K (q - q0 + dt v))
       for (int i = lane; i < n; i += WAVE) {

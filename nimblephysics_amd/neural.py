@@ -63,6 +63,7 @@ class BackpropSnapshot:
         self._single = single
         self._n = world.getNumDofs()
         self._jac = None
+        self._fcjac = None
 
     # --- output shaping: [B, ...] device tensors, or 2-D numpy for forwardPass(world)
     def _out(self, t):
@@ -126,6 +127,43 @@ class BackpropSnapshot:
         self._check_world(world)
         n = self._n
         return self._out(self._jacobians()[1][:, n:, :])
+
+    # --- constraint forces (BackpropSnapshot.cpp:2723) --------------------------
+    def getNumClamping(self):
+        """Clamping LCP rows per world (the length of f_c)."""
+        from ._native import SN_NC
+        nc = self._snap[:, SN_NC].to(torch.int64)
+        return int(nc[0]) if self._single else nc
+
+    def getClampingConstraintImpulses(self):
+        """f_c, the clamping rows' impulses in the LCP's clamping order:
+        [B, MAX_LCP] (zero past each world's count), or [n_c] for one world."""
+        from ._native import MAX_LCP, SN_FC
+        fc = self._snap[:, SN_FC:SN_FC + MAX_LCP].clone()
+        nc = self._snap[:, 2].to(torch.int64)
+        fc[torch.arange(MAX_LCP, device=fc.device)[None, :] >= nc[:, None]] = 0.0
+        if self._single:
+            return fc[0, :int(nc[0])].detach().cpu().numpy()
+        return fc
+
+    def getJacobianOfConstraintForce(self, world: Optional[World] = None, wrt: str = "POSITION"):
+        """d f_c / d wrt for wrt in POSITION / VELOCITY / FORCE (:2723):
+        [B, MAX_LCP, n] device tensor (rows past each world's clamping count
+        zero), or [n_c, n] for one world."""
+        self._check_world(world)
+        kind = getattr(wrt, "name", wrt)
+        if self._fcjac is None:
+            with torch.cuda.device(self._state.device):
+                stream = torch.cuda.current_stream(self._state.device).cuda_stream
+                self._fcjac = self._dev.constraint_force_jacobians(self._state, self._forces, self._snap, stream)
+        Js, Jf = self._fcjac
+        n = self._n
+        J = {"POSITION": Js[:, :, :n], "VELOCITY": Js[:, :, n:], "FORCE": Jf}.get(kind)
+        if J is None:
+            raise ValueError(f"wrt must be POSITION, VELOCITY or FORCE, got {kind}")
+        if self._single:
+            return J[0, :int(self._snap[0, 2])].detach().cpu().numpy()
+        return J
 
     # --- backprop (BackpropSnapshot.cpp:121, :382) ------------------------------
     def _vjp(self, grad_next):

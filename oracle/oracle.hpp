@@ -133,7 +133,7 @@ void step(const World& w, const double* state, const double* tau, std::vector<do
           double* nextState, Snapshot& snap);
 void backprop(const World& w, const Snapshot& snap, const double* gradNext, double* gradState, double* gradTau);
 void stepJacobians(const World& w, const Snapshot& snap, double* posPos, double* posVel, double* velPos,
-                   double* velVel, double* forceVel);
+                   double* velVel, double* forceVel, std::vector<double>* dFcOut = nullptr);
 
 // contacts (oracle_contact.cpp)
 // *unsupported (optional) is set when a narrow-phase branch that is not

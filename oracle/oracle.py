@@ -41,6 +41,7 @@ def lib():
         L.oracle_forward.argtypes = [vp, ip, dp, dp, dp, dp, vp]
         L.oracle_backward.argtypes = [vp, ip, vp, dp, dp, dp]
         L.oracle_jacobians.argtypes = [vp, ip, vp, dp, dp]
+        L.oracle_constraint_force_jacobians.argtypes = [vp, ip, vp, dp, ip]
         L.oracle_mass_matrix.argtypes = [vp, dp, dp]
         L.oracle_coriolis_gravity.argtypes = [vp, dp, dp, dp]
         L.oracle_forward_dynamics.argtypes = [vp, dp, dp, dp, dp]
@@ -151,6 +152,14 @@ class OracleWorld:
         F = np.zeros((B, 2 * n, n))
         lib().oracle_jacobians(self.h, B, self.snaps, _p(J), _p(F))
         return J, F
+
+    def constraint_force_jacobians(self, max_rows=48):
+        """getJacobianOfConstraintForce of the last forward: [B, max_rows, 3n],
+        row r = d f_c[r] / d(q, v, tau) (BackpropSnapshot.cpp:2723), zero past
+        the world's clamping count."""
+        out = np.zeros((self.batch, max_rows, 3 * self.n))
+        lib().oracle_constraint_force_jacobians(self.h, self.batch, self.snaps, _p(out), max_rows)
+        return out
 
     def mass_matrix(self, q):
         q = np.ascontiguousarray(q, dtype=np.float64)

@@ -49,6 +49,24 @@ int oracle_backward(void* wp, int batch, void* snaps, const double* gradNext, do
   return 0;
 }
 
+// getJacobianOfConstraintForce (BackpropSnapshot.cpp:2723) per world:
+// out [batch][maxRows][3n], row r = d f_c[r] / d(q, v, tau), zero past n_c
+int oracle_constraint_force_jacobians(void* wp, int batch, void* snaps, double* out, int maxRows) {
+  World& w = *static_cast<World*>(wp);
+  auto& S = *static_cast<std::vector<OracleSnap>*>(snaps);
+  const int n = w.n;
+  std::vector<double> pp(n * n), pv(n * n), vp(n * n), vv(n * n), fv(n * n), dfc;
+  for (int b = 0; b < batch; b++) {
+    double* o = out + (size_t)b * maxRows * 3 * n;
+    std::fill(o, o + (size_t)maxRows * 3 * n, 0.0);
+    if (S[b].s.numClamping == 0) continue;
+    stepJacobians(w, S[b].s, pp.data(), pv.data(), vp.data(), vv.data(), fv.data(), &dfc);
+    const int nc = S[b].s.numClamping < maxRows ? S[b].s.numClamping : maxRows;
+    std::copy(dfc.begin(), dfc.begin() + (size_t)nc * 3 * n, o);
+  }
+  return 0;
+}
+
 // getStateJacobian [2n][2n] = [[posPos, velPos], [posVel, velVel]]
 // (BackpropSnapshot.cpp:1230) and d(next)/d(tau) [2n][n] = [0; forceVel]
 int oracle_jacobians(void* wp, int batch, void* snaps, double* stateJac, double* forceJac) {

@@ -1171,7 +1171,8 @@ void constrainedJacobians(const World& w, const Kin<double>& k, const Snapshot& 
                           const std::vector<double>& dCq, const std::vector<double>& dCv,
                           const std::vector<double>& dM, const std::vector<double>& Ac,
                           const std::vector<double>& Aub, const std::vector<double>& AcubE,
-                          std::vector<double>& posVel, std::vector<double>& velVel, std::vector<double>& forceVel) {
+                          std::vector<double>& posVel, std::vector<double>& velVel, std::vector<double>& forceVel,
+                          std::vector<double>* dFcOut) {
   (void)k; (void)M; (void)Aub;
   const int n = w.n, nc = snap.numClamping;
   const double dt = w.dt;
@@ -1241,6 +1242,17 @@ void constrainedJacobians(const World& w, const Kin<double>& k, const Snapshot& 
   // position: dM + Minv (A_c_ub_E dF_c + dA_c f + dA_ub E f - dt dC) - dt Minv K
   std::vector<double> dFq, dAcf;
   positionConstraintTerms(w, snap, Minv, C, dCq, Ac, Aub, AcubE, Q, dFq, dAcf);
+  if (dFcOut) {
+    // getJacobianOfConstraintForce (BackpropSnapshot.cpp:2723): rows f_c[r],
+    // columns POSITION | VELOCITY | FORCE
+    dFcOut->assign((size_t)nc * 3 * n, 0.0);
+    for (int r = 0; r < nc; r++)
+      for (int c = 0; c < n; c++) {
+        (*dFcOut)[(size_t)r * 3 * n + c] = dFq[r * n + c];
+        (*dFcOut)[(size_t)r * 3 * n + n + c] = dFv[r * n + c];
+        (*dFcOut)[(size_t)r * 3 * n + 2 * n + c] = dFf[r * n + c];
+      }
+  }
   std::vector<double> T3(n * n);
   for (int i = 0; i < n; i++)
     for (int c = 0; c < n; c++) {

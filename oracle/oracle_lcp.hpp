@@ -26,7 +26,8 @@ void constrainedJacobians(const World& w, const Kin<double>& k, const Snapshot& 
                           const std::vector<double>& dCv, const std::vector<double>& dM,
                           const std::vector<double>& Ac, const std::vector<double>& Aub,
                           const std::vector<double>& AcubE, std::vector<double>& posVel,
-                          std::vector<double>& velVel, std::vector<double>& forceVel);
+                          std::vector<double>& velVel, std::vector<double>& forceVel,
+                          std::vector<double>* dFcOut = nullptr);
 
 // dart/external/odelcpsolver/lcp.cpp:780 dSolveLCP (Dantzig), restated.
 bool dantzigSolveLCP(int n, double* A, double* x, double* b, double* w, int nub, double* lo, double* hi,

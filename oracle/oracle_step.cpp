@@ -119,7 +119,7 @@ void step(const World& w, const double* state, const double* tau, std::vector<do
 // :1263, getPosVelJacobian :762, getVelPosJacobian :1338, getVelVelJacobian
 // :643, getControlForceVelJacobian :482), row-major n x n each.
 void stepJacobians(const World& w, const Snapshot& snap, double* posPosOut, double* posVelOut, double* velPosOut,
-                   double* velVelOut, double* forceVelOut) {
+                   double* velVelOut, double* forceVelOut, std::vector<double>* dFcOut) {
   const int n = w.n;
   const double dt = w.dt;
   const double* q = snap.q.data();
@@ -179,7 +179,7 @@ void stepJacobians(const World& w, const Snapshot& snap, double* posPosOut, doub
         posVel[r * n + c] = dM[r * n + c] - dt * s - Minv[r * n + c] * dt * w.spring[c];
       }
   } else {
-    constrainedJacobians(w, k, snap, M, Minv, C, dCq, dCv, dM, Ac, Aub, AcubE, posVel, velVel, forceVel);
+    constrainedJacobians(w, k, snap, M, Minv, C, dCq, dCv, dM, Ac, Aub, AcubE, posVel, velVel, forceVel, dFcOut);
   }
 
   Mat posPos(n * n), velPos(n * n);

@@ -126,3 +126,47 @@ def test_world_jacobians_single():
     ow.forward(s0[None], world.getControlForces()[None])
     RJ, RF = ow.jacobians()
     assert _rel(J, RJ[0]) < RTOL and _rel(A, RF[0]) < RTOL
+
+
+@pytest.mark.parametrize("name", ["atlas", "half_cheetah", "capsule_edge", "atlas_broken"])
+def test_constraint_force_jacobians(name):
+    """getClampingConstraintImpulses and getJacobianOfConstraintForce for
+    POSITION / VELOCITY / FORCE (BackpropSnapshot.cpp:2723;
+    nimble_constraint_force_jacobians: unit upstream gradients on f_c through
+    the backward kernel) against the oracle's dense dF_c (oracle_contact.cpp
+    constrainedJacobians, itself checked against finite differences in
+    test_oracle_pins), on every world of the oracle's LCP path."""
+    if name == "atlas":
+        world = models.atlas_world(True)
+        st, f = models.random_states(world, 256, seed=7, q_scale=0.02, v_scale=0.05)
+    elif name == "half_cheetah":
+        world = models.half_cheetah_world()
+        st, f = models.half_cheetah_states(world, 128, seed=4)
+    elif name == "capsule_edge":
+        world = models.capsule_edge_world()
+        st, f = models.capsule_edge_states(64, seed=2)
+    else:
+        world, _, st, f, _ = models.broken_states("atlas")
+    n = world.getNumDofs()
+    B = st.shape[0]
+    ow = O.OracleWorld(world)
+    ow.forward(st, f)
+    RD = ow.constraint_force_jacobians()
+    snap, ts, tf = _batched(world, st, f)
+    sn = world._last_snapshot.cpu().numpy()
+    same = _check_contacts(ow, sn, B, cache=world._batch_state.cache.cpu().numpy())
+    fc = snap.getClampingConstraintImpulses().cpu().numpy()
+    Jq = snap.getJacobianOfConstraintForce(world, "POSITION").cpu().numpy()
+    Jv = snap.getJacobianOfConstraintForce(world, "VELOCITY").cpu().numpy()
+    Jf = snap.getJacobianOfConstraintForce(world, "FORCE").cpu().numpy()
+    checked = 0
+    for b in np.flatnonzero(same):
+        nc = int(sn[b, 2])
+        assert not np.any(Jq[b, nc:]) and not np.any(Jf[b, nc:])
+        if nc == 0:
+            continue
+        assert _rel(fc[b, :nc], O.lcp_fc(ow, b)[:nc]) < RTOL, b
+        got = np.concatenate([Jq[b, :nc], Jv[b, :nc], Jf[b, :nc]], axis=1)
+        assert _rel(got, RD[b, :nc]) < RTOL, (b, _rel(got, RD[b, :nc]))
+        checked += 1
+    assert checked >= 1

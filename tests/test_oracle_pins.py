@@ -403,3 +403,45 @@ def test_broken_state_jacobians_vs_finite_differences(oracle_built, kind):
                 blk, ref = J[b][rows, cols], fd_J[rows, cols]
                 assert np.abs(blk - ref).max() <= max(1e-6 * np.abs(ref).max(), 1e-8), (name, rows, cols)
             assert np.abs(F[b][rows] - fd_F[rows]).max() <= 1e-6 * np.abs(fd_F[rows]).max(), (name, rows)
+
+
+@pytest.mark.parametrize("name", ["half_cheetah", "capsule_edge", "atlas_broken"])
+def test_constraint_force_jacobian_vs_finite_differences(oracle_built, name):
+    """getJacobianOfConstraintForce (BackpropSnapshot.cpp:2723) for POSITION /
+    VELOCITY / FORCE from the oracle (the matrix the GPU's
+    nimble_constraint_force_jacobians is compared with) against central
+    differences of the oracle's clamping impulses f_c."""
+    if name == "half_cheetah":
+        w = models.half_cheetah_world()
+        st, f = models.half_cheetah_states(w, 12, seed=1)
+        picks = [1, 3, 4]
+    elif name == "capsule_edge":
+        w = models.capsule_edge_world()
+        st, f = models.capsule_edge_states(8, seed=1)
+        picks = [2, 6]
+    else:
+        w, _, st, f, _ = models.broken_states("half_cheetah")
+        picks = [0, 1, 2, 3]
+    n = w.getNumDofs()
+    o = O.OracleWorld(w)
+    o.forward(st, f)
+    J = o.constraint_force_jacobians()
+    for b in picks:
+        nc = int(O.lcp_flags(o, b)[3])
+        assert nc > 0, (name, b)
+        assert not J[b, nc:].any()
+
+        def fc(s, ff):
+            oo = O.OracleWorld(w)
+            oo.forward(s[None], ff[None])
+            return O.lcp_fc(oo, 0)[:nc]
+        fd = np.zeros((nc, 3 * n))
+        for i in range(2 * n):
+            e = np.zeros(2 * n)
+            e[i] = 1e-6
+            fd[:, i] = (fc(st[b] + e, f[b]) - fc(st[b] - e, f[b])) / 2e-6
+        for i in range(n):
+            e = np.zeros(n)
+            e[i] = 1e-4
+            fd[:, 2 * n + i] = (fc(st[b], f[b] + e) - fc(st[b], f[b] - e)) / 2e-4
+        assert np.abs(J[b, :nc] - fd).max() <= 1e-6 * np.abs(fd).max(), (name, b)

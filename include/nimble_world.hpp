@@ -70,6 +70,14 @@ struct ContactCapacityError : std::runtime_error {
 };
 
 namespace simulation { class World; }
+
+namespace neural {
+/* dart/neural/WithRespectToMass.hpp: the tunable entries of a body's inertia;
+ * the batched path tunes INERTIA_MASS */
+enum class WrtMassBodyNodeEntryType { INERTIA_MASS, INERTIA_COM, INERTIA_DIAGONAL, INERTIA_FULL };
+/* dart/neural/WithRespectTo.hpp (the state / control spaces) */
+enum class WithRespectTo { POSITION, VELOCITY, FORCE };
+}  // namespace neural
 namespace neural {
 class BackpropSnapshot;
 std::shared_ptr<BackpropSnapshot> forwardPass(const std::shared_ptr<simulation::World>& world, bool idempotent);
@@ -338,6 +346,20 @@ class World {
    * could not be the reference's. */
   void step(bool resetCommand = true);
 
+  /* World::tuneMass / getMassDims / getMasses / setMasses (World.cpp,
+   * WithRespectToMass.cpp): body masses registered in order form the mass
+   * vector whose gradient backpropState returns (lossWrtMass); other entry
+   * types throw std::invalid_argument. */
+  void tuneMass(dynamics::BodyNode* node, neural::WrtMassBodyNodeEntryType type, const VectorXs& upperBound,
+                const VectorXs& lowerBound);
+  std::size_t getMassDims() const { return mTunedMass.size(); }
+  VectorXs getMasses() const;
+  void setMasses(const VectorXs& masses);
+  VectorXs getMassUpperBound() const { return mMassUpper; }
+  VectorXs getMassLowerBound() const { return mMassLower; }
+  /* global body index (device model order) of each tuned mass */
+  std::vector<int> massBodyIndices() const;
+
   /* The flat description handed to nimble_world_create (storage owned by the
    * World until the next call) and the uploaded handle (rebuilt after any
    * model change). */
@@ -355,6 +377,8 @@ class World {
   double mDt = 0.001, mClip = 0.03, mCfm = 1e-4;
   bool mPenCorr = false, mParallel = true;
   VectorXs mForces;
+  std::vector<dynamics::BodyNode*> mTunedMass;
+  VectorXs mMassUpper, mMassLower;
   long mVersion = 0, mBuiltVersion = -1;
   nimble_world_t mHandle = nullptr;
   // describe() storage
@@ -391,6 +415,14 @@ class BackpropSnapshot {
    * gradient of the next state [2n] -> gradient of the state [2n] and of the
    * control forces [n] */
   void backpropState(const VectorXs& nextStateLossGrad, VectorXs& stateLossGrad, VectorXs& forceLossGrad) const;
+  /* ... and lossWrtMass [getMassDims()] = getMassVelJacobian^T dL/dv'
+   * (:177, :580) for the world's tuned body masses */
+  void backpropState(const VectorXs& nextStateLossGrad, VectorXs& stateLossGrad, VectorXs& forceLossGrad,
+                     VectorXs& massLossGrad) const;
+  /* getClampingConstraintImpulses: f_c of the step's clamping LCP rows */
+  VectorXs getClampingConstraintImpulses() const;
+  /* getJacobianOfConstraintForce (:2723): d f_c / d wrt, [n_c x n] row-major */
+  std::vector<double> getJacobianOfConstraintForce(WithRespectTo wrt) const;
   /* BackpropSnapshot::backprop (:121) with the reference's LossGradient */
   void backprop(const LossGradient& thisTimestepLoss, LossGradient& prevTimestepLoss) const;
   /* getStateJacobian (:1230) [2n x 2n] and getControlForceJacobian-style

@@ -278,6 +278,47 @@ nimble_world_t World::handle() {
   return mHandle;
 }
 
+void World::tuneMass(dynamics::BodyNode* node, neural::WrtMassBodyNodeEntryType type, const VectorXs& upperBound,
+                     const VectorXs& lowerBound) {
+  if (type != neural::WrtMassBodyNodeEntryType::INERTIA_MASS)
+    throw std::invalid_argument("tuneMass: only INERTIA_MASS entries are on the batched path");
+  bool found = false;
+  for (const auto& sk : mSkels)
+    for (const auto& b : sk->mBodies) found = found || b.get() == node;
+  if (!found) throw std::invalid_argument("tuneMass: the body node is not in this world");
+  for (auto* b : mTunedMass)
+    if (b == node) throw std::invalid_argument("tuneMass: body already registered");
+  mTunedMass.push_back(node);
+  mMassUpper.push_back(upperBound.empty() ? std::numeric_limits<double>::infinity() : upperBound[0]);
+  mMassLower.push_back(lowerBound.empty() ? 0.0 : lowerBound[0]);
+}
+
+VectorXs World::getMasses() const {
+  VectorXs m;
+  for (auto* b : mTunedMass) m.push_back(b->getMass());
+  return m;
+}
+
+void World::setMasses(const VectorXs& masses) {
+  if (masses.size() != mTunedMass.size()) throw std::invalid_argument("setMasses: size mismatch");
+  for (std::size_t i = 0; i < masses.size(); i++)
+    if (mTunedMass[i]->getMass() != masses[i]) mTunedMass[i]->setMass(masses[i]);
+}
+
+std::vector<int> World::massBodyIndices() const {
+  std::vector<int> idx;
+  for (auto* t : mTunedMass) {
+    int base = 0, found = -1;
+    for (const auto& sk : mSkels) {
+      for (std::size_t k = 0; k < sk->mBodies.size(); k++)
+        if (sk->mBodies[k].get() == t) found = base + (int)k;
+      base += (int)sk->mBodies.size();
+    }
+    idx.push_back(found);
+  }
+  return idx;
+}
+
 double* World::deviceBuffer(int k, std::size_t doubles) {
   if (mDevDoubles[k] < doubles) {
     if (mDev[k]) (void)hipFree(mDev[k]);
@@ -394,6 +435,70 @@ void BackpropSnapshot::backpropState(const VectorXs& nextStateLossGrad, VectorXs
   forceLossGrad.resize(n);
   hipCheck(hipMemcpy(stateLossGrad.data(), dGs, 2 * n * sizeof(double), hipMemcpyDeviceToHost), "hipMemcpy");
   hipCheck(hipMemcpy(forceLossGrad.data(), dGf, n * sizeof(double), hipMemcpyDeviceToHost), "hipMemcpy");
+}
+
+void BackpropSnapshot::backpropState(const VectorXs& nextStateLossGrad, VectorXs& stateLossGrad,
+                                     VectorXs& forceLossGrad, VectorXs& massLossGrad) const {
+  const std::size_t n = mN;
+  if (nextStateLossGrad.size() != 2 * n) throw std::invalid_argument("backpropState: gradient size mismatch");
+  checkModel("backpropState");
+  const std::vector<int> idx = mWorld->massBodyIndices();
+  const std::size_t nb = mWorld->describe().num_bodies;
+  double *dSt, *dF, *dS;
+  uploadStep(*mWorld, mState, mForces, mSnapshot, dSt, dF, dS, n);
+  double* dG = mWorld->deviceBuffer(3, 2 * n);
+  double* dGs = mWorld->deviceBuffer(2, 3 * n + nb);
+  hipCheck(hipMemcpy(dG, nextStateLossGrad.data(), 2 * n * sizeof(double), hipMemcpyHostToDevice), "hipMemcpy");
+  double* dGf = dGs + 2 * n;
+  double* dGm = dGs + 3 * n;
+  check(nimble_backward_masses(mHandle, 1, dSt, dF, dS, dG, dGs, dGf, dGm, nullptr), "nimble_backward_masses");
+  hipCheck(hipDeviceSynchronize(), "nimble_backward_masses");
+  stateLossGrad.resize(2 * n);
+  forceLossGrad.resize(n);
+  std::vector<double> gm(nb);
+  hipCheck(hipMemcpy(stateLossGrad.data(), dGs, 2 * n * sizeof(double), hipMemcpyDeviceToHost), "hipMemcpy");
+  hipCheck(hipMemcpy(forceLossGrad.data(), dGf, n * sizeof(double), hipMemcpyDeviceToHost), "hipMemcpy");
+  hipCheck(hipMemcpy(gm.data(), dGm, nb * sizeof(double), hipMemcpyDeviceToHost), "hipMemcpy");
+  massLossGrad.resize(idx.size());
+  for (std::size_t i = 0; i < idx.size(); i++) massLossGrad[i] = gm[idx[i]];
+}
+
+VectorXs BackpropSnapshot::getClampingConstraintImpulses() const {
+  const int nc = mSnapshot.size() > NIMBLE_SNAPSHOT_NUM_CLAMPING ? (int)mSnapshot[NIMBLE_SNAPSHOT_NUM_CLAMPING] : 0;
+  if (nc <= 0) return VectorXs();
+  return VectorXs(mSnapshot.begin() + NIMBLE_SNAPSHOT_FC, mSnapshot.begin() + NIMBLE_SNAPSHOT_FC + nc);
+}
+
+std::vector<double> BackpropSnapshot::getJacobianOfConstraintForce(WithRespectTo wrt) const {
+  checkModel("getJacobianOfConstraintForce");
+  const std::size_t n = mN;
+  const int nc = mSnapshot.size() > NIMBLE_SNAPSHOT_NUM_CLAMPING ? (int)mSnapshot[NIMBLE_SNAPSHOT_NUM_CLAMPING] : 0;
+  if (nc <= 0) return {};
+  double *dSt, *dF, *dS;
+  uploadStep(*mWorld, mState, mForces, mSnapshot, dSt, dF, dS, n);
+  double *dJs = nullptr, *dJf = nullptr, *dWs = nullptr;
+  hipCheck(hipMalloc(&dJs, (size_t)NIMBLE_MAX_LCP * 2 * n * sizeof(double)), "hipMalloc");
+  hipCheck(hipMalloc(&dJf, (size_t)NIMBLE_MAX_LCP * n * sizeof(double)), "hipMalloc");
+  const int64_t wsd = nimble_jacobian_workspace_doubles(mHandle, 1);
+  if (wsd > 0) hipCheck(hipMalloc(&dWs, wsd * sizeof(double)), "hipMalloc");
+  const int rc = nimble_constraint_force_jacobians(mHandle, 1, dSt, dF, dS, dJs, dJf, dWs, nullptr);
+  hipError_t e = hipDeviceSynchronize();
+  std::vector<double> Js((size_t)NIMBLE_MAX_LCP * 2 * n), Jf((size_t)NIMBLE_MAX_LCP * n);
+  if (rc == NIMBLE_OK && e == hipSuccess) {
+    e = hipMemcpy(Js.data(), dJs, Js.size() * sizeof(double), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(Jf.data(), dJf, Jf.size() * sizeof(double), hipMemcpyDeviceToHost);
+  }
+  (void)hipFree(dJs);
+  (void)hipFree(dJf);
+  if (dWs) (void)hipFree(dWs);
+  check(rc, "nimble_constraint_force_jacobians");
+  hipCheck(e, "nimble_constraint_force_jacobians");
+  std::vector<double> out((size_t)nc * n);
+  for (int r = 0; r < nc; r++)
+    for (std::size_t c = 0; c < n; c++)
+      out[r * n + c] = wrt == WithRespectTo::FORCE ? Jf[r * n + c]
+                                                    : Js[r * 2 * n + (wrt == WithRespectTo::VELOCITY ? n : 0) + c];
+  return out;
 }
 
 void BackpropSnapshot::backprop(const LossGradient& next, LossGradient& prev) const {

@@ -160,7 +160,31 @@ int main(int argc, char** argv) {
     next.lossWrtVelocity.assign(g.begin() + n, g.end());
     snap->backprop(next, prev);
     const std::vector<double> J = snap->getStateJacobian(), F = snap->getForceJacobian();
+    // lossWrtMass for the first mobile skeleton's root body (World::tuneMass)
+    int tunedIndex = 0;
+    for (std::size_t si = 0, base = 0; si < world->getNumSkeletons(); si++) {
+      auto sk = world->getSkeleton(si);
+      if (sk->isMobile()) {
+        world->tuneMass(sk->getBodyNode(0), neural::WrtMassBodyNodeEntryType::INERTIA_MASS, {10.0}, {0.1});
+        tunedIndex = (int)base;
+        break;
+      }
+      base += sk->getNumBodyNodes();
+    }
+    std::vector<double> gs2, gf2, gm;
+    snap->backpropState(g, gs2, gf2, gm);
+    const std::vector<double> fc = snap->getClampingConstraintImpulses();
+    const std::vector<double> dq = snap->getJacobianOfConstraintForce(neural::WithRespectTo::POSITION);
+    const std::vector<double> dv = snap->getJacobianOfConstraintForce(neural::WithRespectTo::VELOCITY);
+    const std::vector<double> dfo = snap->getJacobianOfConstraintForce(neural::WithRespectTo::FORCE);
     std::printf("{");
+    printVec("grad_state_m", gs2);
+    printVec("grad_mass", gm);
+    printVec("mass_dims", std::vector<double>{(double)world->getMassDims(), (double)tunedIndex});
+    printVec("fc", fc);
+    printVec("dfc_q", dq);
+    printVec("dfc_v", dv);
+    printVec("dfc_f", dfo);
     printVec("next", snap->getPostStepState());
     printVec("world_state", world->getState());
     printVec("grad_state", gs);

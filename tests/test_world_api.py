@@ -118,3 +118,34 @@ def test_cpp_world_steps_match_oracle(name):
     s3 = ow.forward(s2[None], np.zeros((1, n)))[0]
     assert close(out["step2"], s2) and close(out["step3"], s3)
     assert np.all(np.asarray(out["forces_after"]) == 0)
+    # backpropState with lossWrtMass (World::tuneMass on the first mobile
+    # skeleton's root body) leaves the state gradient as it was; the mass
+    # gradient against central differences of the oracle step
+    assert out["grad_state_m"] == out["grad_state"]
+    dims, b = out["mass_dims"]
+    assert dims == 1 and len(out["grad_mass"]) == 1
+    body = [bd for sk in world.skeletons for bd in sk.bodies][int(b)]
+    m0 = body.getMass()
+    e = 1e-5 * m0
+
+    def loss(m):
+        body.setMass(m)
+        try:
+            return float(OracleWorld(world).forward(st[None], f[None])[0] @ g)
+        finally:
+            body.setMass(m0)
+    fd = (loss(m0 + e) - loss(m0 - e)) / (2 * e)
+    assert abs(out["grad_mass"][0] - fd) <= 1e-6 * max(abs(fd), 1e-3) + 1e-14 * abs(loss(m0)) / e
+    # getClampingConstraintImpulses / getJacobianOfConstraintForce
+    from oracle.oracle import lcp_fc
+    ow = OracleWorld(world)  # a fresh oracle at the step's state (the rollout above moved on)
+    ow.forward(st[None], f[None])
+    RD = ow.constraint_force_jacobians()[0]
+    rfc = lcp_fc(ow, 0)
+    nc = len(out["fc"])
+    assert nc == len(rfc)
+    if nc:
+        assert close(out["fc"], rfc)
+        assert close(np.reshape(out["dfc_q"], (nc, n)), RD[:nc, :n])
+        assert close(np.reshape(out["dfc_v"], (nc, n)), RD[:nc, n:2 * n])
+        assert close(np.reshape(out["dfc_f"], (nc, n)), RD[:nc, 2 * n:])

@@ -2416,8 +2416,7 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
 // column pairs of NV, lane b builds both fields' twists and momenta I_b V
 // (world inertias are formed once, kept as their 3x3 rotational block, world
 // COM and mass: 13 doubles per body after the 2 x nb x 12 field doubles in
-// `buf`), then lane b sums the momenta over its subtree (bodies d whose
-// ancestor set contains b) -- no per-level barriers or tree-list loads.
+// `buf`), then the momenta are summed over each subtree level by level.
 __device__ double mFieldsTerm(const ModelDev& md, double* s, const Layout& L, const double* NV, double* buf, int lane,
                               int k, const double* Z, double coefDelta, double imp) {
   const int nb = md.nb;
@@ -2487,21 +2486,25 @@ __device__ double mFieldsTerm(const ModelDev& md, double* s, const Layout& L, co
       for (int i = 0; i < 6; i++) { Fa[i] = Va[i]; Fa[6 + i] = ha[i]; Fc[i] = Vc[i]; Fc[6 + i] = hc[i]; }
     }
     WSYNC();
-    // subtree momenta: lane b sums I_d V_d over the bodies d below it
-    double Ha[6] = {0, 0, 0, 0, 0, 0}, Hc[6] = {0, 0, 0, 0, 0, 0};
-    if (lane < nb) {
-#pragma unroll 2
-      for (int d = 0; d < nb; d++) {
-        const double w = ((md.anc[d] >> lane) & 1ull) ? 1.0 : 0.0;
-        const double* Fa = buf + d * 12 + 6;
-        const double* Fc = buf + (nb + d) * 12 + 6;
-        for (int i = 0; i < 6; i++) { Ha[i] = fma(w, Fa[i], Ha[i]); Hc[i] = fma(w, Fc[i], Hc[i]); }
+    // subtree momenta in place, deepest parent level first: lane = (body of
+    // the level, field, component) adds its children's sums -- ~12 LDS
+    // accesses per body instead of every lane reading all nb bodies' 12
+    // momenta (the four worlds of a CU share the LDS bandwidth)
+    for (int lev = md.maxDepth - 1; lev >= 0; lev--) {
+      const int b0 = md.levelStart[lev], cnt = (md.levelStart[lev + 1] - b0) * 12;
+      for (int t = lane; t < cnt; t += WAVE) {
+        const int p = md.levelBodies[b0 + t / 12], e = t % 12;
+        double* base = buf + (e < 6 ? 0 : nb * 12) + 6 + (e % 6);
+        double acc = base[p * 12];
+        for (int q = md.childStart[p]; q < md.childStart[p + 1]; q++) acc += base[md.childList[q] * 12];
+        base[p * 12] = acc;
       }
+      WSYNC();
     }
-    // dof k reads its body's subtree momenta (every lane takes part)
+    // dof k reads its body's subtree momenta
     const int bk = k < md.n ? md.dofBody[k] : 0;
     double ha[6], hc[6];
-    for (int i = 0; i < 6; i++) { ha[i] = __shfl(Ha[i], bk); hc[i] = __shfl(Hc[i], bk); }
+    for (int i = 0; i < 6; i++) { ha[i] = buf[bk * 12 + 6 + i]; hc[i] = buf[(nb + bk) * 12 + 6 + i]; }
     if (k < md.n) {
       const int lam = md.parent[bk];
       double val = 0.0;

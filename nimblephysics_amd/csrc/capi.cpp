@@ -173,6 +173,14 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
         if (m.parent[b] == p) m.childList[k++] = b;
     }
     m.childStart[m.nb] = k;
+    // (parent, child) edges, deepest child first and children in ascending
+    // order: IC[p] += IC[c] over this list is the level loop's sum, term
+    // for term
+    k = 0;
+    for (int lev = m.maxDepth; lev >= 1; lev--)
+      for (int b = 0; b < m.nb; b++)
+        if (m.depth[b] == lev && m.parent[b] >= 0) { m.accEdge[k][0] = m.parent[b]; m.accEdge[k][1] = b; k++; }
+    m.numAcc = k;
   }
   // BodyNode::isReactive (BodyNode.cpp:2384): mobile skeleton with dependent dofs
   for (int b = 0; b < m.nb; b++) {

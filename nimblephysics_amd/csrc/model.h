@@ -41,6 +41,9 @@ struct ModelDev {
   // children lists (both in ascending body order)
   int levelStart[NB_MAX + 1], levelBodies[NB_MAX];
   int childStart[NB_MAX + 1], childList[NB_MAX];
+  // subtree-sum schedule: (parent, child) edges, deepest child first
+  int numAcc;
+  int accEdge[NB_MAX][2];
   double Tpj[NB_MAX][12];          // [R|p] row-major
   double Tcj[NB_MAX][12];
   double TcjInv[NB_MAX][12];

@@ -199,19 +199,19 @@ __device__ __forceinline__ void composites(const ModelDev& md, double* s, const 
     for (int i = 0; i < 6; i++) s[L.F + 6 * b + i] = f[i] + vxh[i];
   }
   WSYNC();
-  // subtree sums, one tree level at a time (parents gather their children)
-  for (int lev = md.maxDepth - 1; lev >= 0; lev--) {
-    const int b0 = md.levelStart[lev], cnt = (md.levelStart[lev + 1] - b0) * 42;
-    for (int t = lane; t < cnt; t += WAVE) {
-      const int p = md.levelBodies[b0 + t / 42], e = t % 42;
-      const int off = e < 36 ? L.IC + 36 * p + e : L.F + 6 * p + (e - 36);
-      const int stride = e < 36 ? 36 : 6;
-      double acc = s[off];
-      for (int q = md.childStart[p]; q < md.childStart[p + 1]; q++) acc += s[off + stride * (md.childList[q] - p)];
-      s[off] = acc;
+  // subtree sums: lane = one of the 42 entries (IC 36, F 6), walking the
+  // model's deepest-child-first edge list (wave-uniform, scalar loads), so no
+  // per-level barrier and no dependent per-lane tree-table loads
+  if (lane < 42) {
+    const int off = lane < 36 ? L.IC + lane : L.F + (lane - 36);
+    const int stride = lane < 36 ? 36 : 6;
+#pragma unroll 4
+    for (int k = 0; k < md.numAcc; k++) {
+      const int p = md.accEdge[k][0], c = md.accEdge[k][1];
+      s[off + stride * p] += s[off + stride * c];
     }
-    WSYNC();
   }
+  WSYNC();
 }
 
 // M_jk = S_j^T IC_{deeper(j,k)} S_k (composite-rigid-body algorithm), and the

@@ -2486,21 +2486,18 @@ __device__ double mFieldsTerm(const ModelDev& md, double* s, const Layout& L, co
       for (int i = 0; i < 6; i++) { Fa[i] = Va[i]; Fa[6 + i] = ha[i]; Fc[i] = Vc[i]; Fc[6 + i] = hc[i]; }
     }
     WSYNC();
-    // subtree momenta in place, deepest parent level first: lane = (body of
-    // the level, field, component) adds its children's sums -- ~12 LDS
-    // accesses per body instead of every lane reading all nb bodies' 12
-    // momenta (the four worlds of a CU share the LDS bandwidth)
-    for (int lev = md.maxDepth - 1; lev >= 0; lev--) {
-      const int b0 = md.levelStart[lev], cnt = (md.levelStart[lev + 1] - b0) * 12;
-      for (int t = lane; t < cnt; t += WAVE) {
-        const int p = md.levelBodies[b0 + t / 12], e = t % 12;
-        double* base = buf + (e < 6 ? 0 : nb * 12) + 6 + (e % 6);
-        double acc = base[p * 12];
-        for (int q = md.childStart[p]; q < md.childStart[p + 1]; q++) acc += base[md.childList[q] * 12];
-        base[p * 12] = acc;
+    // subtree momenta in place over the deepest-child-first edge list (lane =
+    // field x component; see composites) -- instead of every lane reading all
+    // nb bodies' 12 momenta (the four worlds of a CU share the LDS bandwidth)
+    if (lane < 12) {
+      double* base = buf + (lane < 6 ? 0 : nb * 12) + 6 + (lane % 6);
+#pragma unroll 4
+      for (int k = 0; k < md.numAcc; k++) {
+        const int p = md.accEdge[k][0], c = md.accEdge[k][1];
+        base[p * 12] += base[c * 12];
       }
-      WSYNC();
     }
+    WSYNC();
     // dof k reads its body's subtree momenta
     const int bk = k < md.n ? md.dofBody[k] : 0;
     double ha[6], hc[6];

@@ -456,19 +456,18 @@ __device__ __forceinline__ void adjointVectors(const ModelDev& md, double* s, co
     for (int i = 0; i < 6; i++) a[30 + i] = -t[i];  // zeta
   }
   WSYNC();
-  // subtree sums of alpha..zeta and f (-> composite F), deepest level first
-  for (int lev = md.maxDepth - 1; lev >= 0; lev--) {
-    const int b0 = md.levelStart[lev], cnt = (md.levelStart[lev + 1] - b0) * 42;
-    for (int t = lane; t < cnt; t += WAVE) {
-      const int p = md.levelBodies[b0 + t / 42], e = t % 42;
-      const int off = e < 36 ? L.adj + e : L.F + (e - 36);
-      const int stride = e < 36 ? 42 : 6;
-      double acc = s[off + stride * p];
-      for (int q = md.childStart[p]; q < md.childStart[p + 1]; q++) acc += s[off + stride * md.childList[q]];
-      s[off + stride * p] = acc;
+  // subtree sums of alpha..zeta and f (-> composite F) over the deepest-
+  // child-first edge list (lane = entry; see composites)
+  if (lane < 42) {
+    const int off = lane < 36 ? L.adj + lane : L.F + (lane - 36);
+    const int stride = lane < 36 ? 42 : 6;
+#pragma unroll 4
+    for (int k = 0; k < md.numAcc; k++) {
+      const int p = md.accEdge[k][0], c = md.accEdge[k][1];
+      s[off + stride * p] += s[off + stride * c];
     }
-    WSYNC();
   }
+  WSYNC();
   if (lane < nb) {
     const int b = lane, par = md.parent[b];
     double d[6];
@@ -476,16 +475,15 @@ __device__ __forceinline__ void adjointVectors(const ModelDev& md, double* s, co
     crf(d, s + L.F + 6 * b, s + L.adj + 42 * b + 36);  // kappa
   }
   WSYNC();
-  for (int lev = md.maxDepth - 1; lev >= 0; lev--) {
-    const int b0 = md.levelStart[lev], cnt = (md.levelStart[lev + 1] - b0) * 6;
-    for (int t = lane; t < cnt; t += WAVE) {
-      const int p = md.levelBodies[b0 + t / 6], e = 36 + t % 6;
-      double acc = s[L.adj + 42 * p + e];
-      for (int q = md.childStart[p]; q < md.childStart[p + 1]; q++) acc += s[L.adj + 42 * md.childList[q] + e];
-      s[L.adj + 42 * p + e] = acc;
+  if (lane < 6) {
+    const int off = L.adj + 36 + lane;
+#pragma unroll 4
+    for (int k = 0; k < md.numAcc; k++) {
+      const int p = md.accEdge[k][0], c = md.accEdge[k][1];
+      s[off + 42 * p] += s[off + 42 * c];
     }
-    WSYNC();
   }
+  WSYNC();
 }
 
 // Right Jacobian of SO(3) exp (J_r(th) = I - (1-cos)/t^2 [th] + (t-sin)/t^3 [th]^2)

@@ -1720,24 +1720,32 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
   }
   WSYNC();
   STAMP(37);
-  // per-row vectors g_j (lane = dof i, rows wave-uniform)
+  // per-row vectors g_j (lane = dof i, rows wave-uniform).  Each row's map,
+  // clamping index and E value are loaded once, lane = row, and read back
+  // with readlane: no dependent snapshot loads inside the row loop.
+  int rMap = CM_NOT_CLAMPING, rC = 0;
+  double rE = 0.0;
+  if (lane < m) {
+    const double* rr = rows + lane * SN_ROWREC;
+    rMap = (int)rr[RR_MAP];
+    if (rMap == CM_CLAMPING) rC = (int)rr[RR_CIDX];
+    else if (rMap >= 0) { rC = (int)rows[rMap * SN_ROWREC + RR_CIDX]; rE = rr[RR_EVAL]; }
+  }
   for (int i = lane; i < n; i += WAVE) {
     const double* nv = P.NV + i * NV_COLS;
     const double w = nv[NV_W], sg = nv[NV_SIGMA], ka = nv[NV_KAPPA], ma1 = nv[NV_MA1], mar = nv[NV_MARHO];
     const double ma2 = nv[NV_MA2], map = nv[NV_MAPI], vf = sn[SN_VF + i];
     for (int j = 0; j < m; j++) {
-      const double* rr = rows + j * SN_ROWREC;
-      const int mp = uni((int)rr[RR_MAP]);
+      const int mp = rdli(rMap, j);
+      const int c = rdli(rC, j);
       double g = 0.0;
       if (mp == CM_CLAMPING) {
-        const int c = uni((int)rr[RR_CIDX]);
         g = P.fc[c] * w - P.beta[c] * vf - P.lam[c] * sg - P.xq[c] * ka;
         if (imp) g += P.rho[c] * ma1 + P.r1[c] * mar + P.piv[c] * ma2 + P.zeta[c] * map;
       } else if (mp >= 0) {
-        const int c = uni((int)rows[mp * SN_ROWREC + RR_CIDX]);
         double inner = P.fc[c] * w - P.xq[c] * ka;
         if (imp) inner += P.rho[c] * ma1 + P.piv[c] * ma2;
-        g = rr[RR_EVAL] * inner;
+        g = rdl(rE, j) * inner;
       }
       P.gRows[j * n + i] = g;
     }

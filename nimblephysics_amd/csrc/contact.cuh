@@ -2275,11 +2275,9 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
   }
   const unsigned long long liveRows = __ballot(lane < m && rMap != CM_NOT_CLAMPING);
   for (int j0 = 0; j0 < m; j0++) {
-    const double* r0 = rows + j0 * SN_ROWREC;
-    if ((int)r0[RR_MAP] == CM_NOT_CLAMPING) continue;
-    const double* rec0 = sn + SN_CONTACTS + (int)r0[RR_CONTACT] * CREC;
+    if (!((liveRows >> j0) & 1ull)) continue;
     for (int side = 0; side < 2; side++) {
-      const int c = (int)rec0[8 + side];
+      const int c = side ? rdli(rB, j0) : rdli(rA, j0);
       if ((done >> c) & 1ull) continue;
       done |= 1ull << c;
       if (!(md.anc[c] & dofBodies)) continue;

@@ -22,21 +22,16 @@ import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-sys.path.insert(0, os.path.join(ROOT, "tests"))
 
-import models  # noqa: E402
 import nimblephysics_amd as nimble  # noqa: E402
 from nimblephysics_amd import _native  # noqa: E402
+from nimblephysics_amd import workloads as models  # noqa: E402
 
 FP64_VECTOR_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (spec; = FP32 vector 157.3 / 2)
 HBM_PEAK_GBS = 8000.0
 
-def _atlas_states(world, batch, seed):
-    return models.random_states(world, batch, seed=seed, q_scale=0.02, v_scale=0.05, f_scale=1.0)
-
-
-def _cheetah_states(world, batch, seed):
-    return models.half_cheetah_states(world, batch, seed=seed)
+_atlas_states = models.atlas_states
+_cheetah_states = models.cheetah_states
 
 
 # name -> (description, world factory, synthetic state sampler, metric, default worlds per GPU)

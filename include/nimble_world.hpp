@@ -435,9 +435,11 @@ class BackpropSnapshot {
  private:
   friend std::shared_ptr<BackpropSnapshot> forwardPass(const simulation::WorldPtr& world, bool idempotent);
   void checkModel(const char* what) const;
+  int clampingCount() const;
   simulation::WorldPtr mWorld;
   nimble_world_t mHandle = nullptr;
   long mVersion = 0;
+  int mNumPairs = 0;  // collision pairs of the model that took the step
   std::size_t mN = 0;
   VectorXs mState, mForces, mNext;
   std::vector<double> mSnapshot;  // host copy of the device snapshot

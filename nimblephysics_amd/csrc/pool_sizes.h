@@ -60,8 +60,13 @@ __host__ __device__ inline int snQ(int n) { return snPT(n) + SN_MAXL * SN_MAXL; 
 // EDGE_EDGE metadata of the kept contacts (EDGE_REC doubles per contact slot)
 __host__ __device__ inline int snEdge(int n) { return snQ(n) + SN_MAXL * SN_MAXL; }
 __host__ __device__ inline int snapWorkspaceOffset(int n) { return snAlign8(snEdge(n) + NIMBLE_MAX_CONTACTS * EDGE_REC); }
-// 64 doubles at the very end of every snapshot are kept for debug stamps
+// 64 doubles at the very end of the snapshot for debug stamps, in the
+// stage-timing build only
+#ifdef NIMBLE_STAGE_TIMING
 #define SN_DEBUG_TAIL 64
+#else
+#define SN_DEBUG_TAIL 0
+#endif
 
 // LCP workspace pools for m rows and n dofs
 #define NV_COLS 16

@@ -375,6 +375,10 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, const double* 
       double* sn = snapshot + (size_t)env * snapDoubles;
       contactStage(md, s, L, lane, v1, x, lcpCache + (size_t)env * cacheDoubles, sn, sn + snapWorkspaceOffset(n),
                    helperOn, helperOn);
+    } else if (lane < 8) {
+      // a model without collision pairs still has a snapshot header (no
+      // contacts, no rows, no clamping) for the getters to read
+      snapshot[(size_t)env * snapDoubles + lane] = 0.0;
     }
     if (helperOn) helperRetire(s, L, lane);
     double* out = nextState + (size_t)env * 2 * n;

@@ -388,6 +388,7 @@ std::shared_ptr<BackpropSnapshot> forwardPass(const simulation::WorldPtr& world,
   world->runForward(&snap->mSnapshot);
   snap->mHandle = world->mHandle;
   snap->mVersion = world->mVersion;
+  snap->mNumPairs = nimble_num_collision_pairs(world->mHandle);
   snap->mNext = world->getState();
   if (idempotent) {
     // RestorableSnapshot::restore
@@ -463,8 +464,17 @@ void BackpropSnapshot::backpropState(const VectorXs& nextStateLossGrad, VectorXs
   for (std::size_t i = 0; i < idx.size(); i++) massLossGrad[i] = gm[idx[i]];
 }
 
+// Clamping rows of the step: 0 for a model without collision pairs (its
+// snapshot has no contact region), and never past the snapshot's f_c block.
+int BackpropSnapshot::clampingCount() const {
+  if (mNumPairs <= 0) return 0;
+  if (mSnapshot.size() < (std::size_t)(NIMBLE_SNAPSHOT_FC + NIMBLE_MAX_LCP)) return 0;
+  const int nc = (int)mSnapshot[NIMBLE_SNAPSHOT_NUM_CLAMPING];
+  return nc < 0 ? 0 : (nc > NIMBLE_MAX_LCP ? NIMBLE_MAX_LCP : nc);
+}
+
 VectorXs BackpropSnapshot::getClampingConstraintImpulses() const {
-  const int nc = mSnapshot.size() > NIMBLE_SNAPSHOT_NUM_CLAMPING ? (int)mSnapshot[NIMBLE_SNAPSHOT_NUM_CLAMPING] : 0;
+  const int nc = clampingCount();
   if (nc <= 0) return VectorXs();
   return VectorXs(mSnapshot.begin() + NIMBLE_SNAPSHOT_FC, mSnapshot.begin() + NIMBLE_SNAPSHOT_FC + nc);
 }
@@ -472,7 +482,7 @@ VectorXs BackpropSnapshot::getClampingConstraintImpulses() const {
 std::vector<double> BackpropSnapshot::getJacobianOfConstraintForce(WithRespectTo wrt) const {
   checkModel("getJacobianOfConstraintForce");
   const std::size_t n = mN;
-  const int nc = mSnapshot.size() > NIMBLE_SNAPSHOT_NUM_CLAMPING ? (int)mSnapshot[NIMBLE_SNAPSHOT_NUM_CLAMPING] : 0;
+  const int nc = clampingCount();
   if (nc <= 0) return {};
   double *dSt, *dF, *dS;
   uploadStep(*mWorld, mState, mForces, mSnapshot, dSt, dF, dS, n);

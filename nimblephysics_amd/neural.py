@@ -56,8 +56,10 @@ class BackpropSnapshot:
     def __init__(self, world: World, dev, state, forces, next_state, snapshot, single: bool):
         self._world = world
         self._dev = dev
-        self._state = state
-        self._forces = forces
+        # copies: the caller may reuse or update its state / action buffers in
+        # place before the lazily computed Jacobians and backprop read them
+        self._state = state.clone()
+        self._forces = forces.clone()
         self._next = next_state
         self._snap = snapshot
         self._single = single
@@ -129,19 +131,24 @@ class BackpropSnapshot:
         return self._out(self._jacobians()[1][:, n:, :])
 
     # --- constraint forces (BackpropSnapshot.cpp:2723) --------------------------
-    def getNumClamping(self):
-        """Clamping LCP rows per world (the length of f_c)."""
-        from ._native import SN_NC
-        nc = self._snap[:, SN_NC].to(torch.int64)
-        return int(nc[0]) if self._single else nc
+    def _clamping_counts(self):
+        """Clamping rows per world, clamped to [0, MAX_LCP]; zeros for a model
+        without collision pairs (whose snapshot has no contact region)."""
+        from ._native import MAX_LCP, SN_NC
+        if self._dev.num_pairs == 0:
+            return torch.zeros(self._state.shape[0], dtype=torch.int64, device=self._state.device)
+        return self._snap[:, SN_NC].to(torch.int64).clamp(0, MAX_LCP)
 
     def getClampingConstraintImpulses(self):
         """f_c, the clamping rows' impulses in the LCP's clamping order:
         [B, MAX_LCP] (zero past each world's count), or [n_c] for one world."""
         from ._native import MAX_LCP, SN_FC
-        fc = self._snap[:, SN_FC:SN_FC + MAX_LCP].clone()
-        nc = self._snap[:, 2].to(torch.int64)
-        fc[torch.arange(MAX_LCP, device=fc.device)[None, :] >= nc[:, None]] = 0.0
+        nc = self._clamping_counts()
+        if self._dev.num_pairs == 0:
+            fc = torch.zeros((self._state.shape[0], MAX_LCP), dtype=torch.float64, device=self._state.device)
+        else:
+            fc = self._snap[:, SN_FC:SN_FC + MAX_LCP].clone()
+            fc[torch.arange(MAX_LCP, device=fc.device)[None, :] >= nc[:, None]] = 0.0
         if self._single:
             return fc[0, :int(nc[0])].detach().cpu().numpy()
         return fc
@@ -162,31 +169,42 @@ class BackpropSnapshot:
         if J is None:
             raise ValueError(f"wrt must be POSITION, VELOCITY or FORCE, got {kind}")
         if self._single:
-            return J[0, :int(self._snap[0, 2])].detach().cpu().numpy()
+            return J[0, :int(self._clamping_counts()[0])].detach().cpu().numpy()
         return J
 
     # --- backprop (BackpropSnapshot.cpp:121, :382) ------------------------------
     def _vjp(self, grad_next):
+        """(lossWrtState, lossWrtForces, lossWrtMass): the mass part is
+        getMassVelJacobian^T dL/dv' (BackpropSnapshot.cpp:177, :418) for the
+        world's tuned masses, [B, getMassDims()]."""
         g = grad_next.reshape(self._state.shape).to(self._state.device, torch.float64).contiguous()
         gs = torch.empty_like(self._state)
         gf = torch.empty_like(self._forces)
+        B = self._state.shape[0]
+        mass_idx = self._world._mass_body_indices()
         with torch.cuda.device(self._state.device):
             stream = torch.cuda.current_stream(self._state.device).cuda_stream
-            self._dev.backward(self._state, self._forces, self._snap, g, gs, gf, stream)
-        return gs, gf
+            if mass_idx:
+                gmb = torch.empty((B, self._dev.nb), dtype=torch.float64, device=self._state.device)
+                self._dev.backward_masses(self._state, self._forces, self._snap, g, gs, gf, gmb, stream)
+                sel = torch.tensor(mass_idx, dtype=torch.long, device=self._state.device)
+                gm = gmb.index_select(1, sel)
+            else:
+                self._dev.backward(self._state, self._forces, self._snap, g, gs, gf, stream)
+                gm = torch.zeros((B, 0), dtype=torch.float64, device=self._state.device)
+        return gs, gf, gm
 
     def backpropState(self, world: Optional[World], nextTimestepStateLossGrad) -> LossGradientHighLevelAPI:
-        """lossWrtState [2n], lossWrtAction [|A|], lossWrtMass (empty)."""
+        """lossWrtState [2n], lossWrtAction [|A|], lossWrtMass [getMassDims()]."""
         self._check_world(world)
         g = torch.as_tensor(np.asarray(nextTimestepStateLossGrad) if not torch.is_tensor(nextTimestepStateLossGrad)
                             else nextTimestepStateLossGrad, dtype=torch.float64)
-        gs, gf = self._vjp(g)
+        gs, gf, gm = self._vjp(g)
         idx = _action_index(self._world, gf.device)
         out = LossGradientHighLevelAPI()
         out.lossWrtState = self._out(gs)
         out.lossWrtAction = self._out(gf.index_select(1, idx))
-        out.lossWrtMass = np.zeros(0) if self._single else torch.zeros((gs.shape[0], 0), dtype=torch.float64,
-                                                                       device=gs.device)
+        out.lossWrtMass = self._out(gm)
         return out
 
     def backprop(self, world: Optional[World], thisTimestepLoss: LossGradient, nextTimestepLoss: LossGradient):
@@ -199,13 +217,12 @@ class BackpropSnapshot:
             nextTimestepLoss.lossWrtVelocity) else nextTimestepLoss.lossWrtVelocity, dtype=torch.float64)
         B = self._state.shape[0]
         g = torch.cat([gp.reshape(B, -1), gv.reshape(B, -1)], dim=1)
-        gs, gf = self._vjp(g)
+        gs, gf, gm = self._vjp(g)
         n = self._n
         thisTimestepLoss.lossWrtPosition = self._out(gs[:, :n])
         thisTimestepLoss.lossWrtVelocity = self._out(gs[:, n:])
         thisTimestepLoss.lossWrtTorque = self._out(gf)
-        thisTimestepLoss.lossWrtMass = np.zeros(0) if self._single else torch.zeros(
-            (B, 0), dtype=torch.float64, device=gs.device)
+        thisTimestepLoss.lossWrtMass = self._out(gm)
 
     # --- recorded state (BackpropSnapshot.cpp:1403-1445, :1685-1702) -----------
     def getPreStepPosition(self):
@@ -274,16 +291,19 @@ def forwardPass(world: World, idempotent: bool = False, state=None, action=None)
         st, act = st.contiguous(), act.contiguous()
     prev = getattr(world, "_batch_state", None)
     saved = prev.cache.clone() if (idempotent and prev is not None) else None
-    with torch.cuda.device(dev):
-        devworld, forces, nxt, snap = step_batch(world, st, act)
-    if idempotent:
-        # RestorableSnapshot: the LCP warm-start cache is part of the world
-        # state the idempotent pass restores (NeuralUtils.cpp:26)
-        if saved is None:
-            world._batch_state = prev
-        else:
-            prev.cache.copy_(saved)
-            world._batch_state = prev
+    try:
+        with torch.cuda.device(dev):
+            devworld, forces, nxt, snap = step_batch(world, st, act)
+    finally:
+        if idempotent:
+            # RestorableSnapshot: the LCP warm-start cache is part of the world
+            # state the idempotent pass restores (NeuralUtils.cpp:26), also
+            # when the step raised
+            if saved is None:
+                world._batch_state = prev
+            else:
+                prev.cache.copy_(saved)
+                world._batch_state = prev
     if single and not idempotent:
         out = nxt[0].cpu().numpy()
         world.setState(out)

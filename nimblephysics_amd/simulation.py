@@ -329,9 +329,9 @@ class World:
         handles = self.__dict__.setdefault("_native_by_dev", {})
         cur = handles.get(idx)
         if cur is None or cur[0] != self._version:
-            if cur is not None:
-                with torch.cuda.device(idx):
-                    cur[1].close()
+            # a superseded handle is not closed here: autograd graphs and
+            # BackpropSnapshots of earlier steps may still hold it, and
+            # DeviceWorld.__del__ releases it once nothing does
             with torch.cuda.device(idx):
                 handles[idx] = (self._version, _native.DeviceWorld(self, idx))
         return handles[idx][1]

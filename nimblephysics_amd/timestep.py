@@ -141,7 +141,13 @@ class TimestepLayer(torch.autograd.Function):
             if mass.dim() != 1 or mass.shape[0] != world.getMassDims():
                 raise ValueError(f"mass must be a vector of the world's {world.getMassDims()} tuned masses "
                                  f"(World::tuneMass), got shape {tuple(mass.shape)}")
-            world.setMasses(mass.detach().cpu().numpy())
+            # one host round trip only when the masses may have changed: the
+            # same tensor object (held here, so its id cannot be reused) at the
+            # same in-place version on an unchanged world model is skipped
+            last = getattr(world, "_last_mass", None)
+            if last is None or last[0] is not mass or last[1] != mass._version or last[2] != world._version:
+                world.setMasses(mass.detach().cpu().numpy())
+                world._last_mass = (mass, mass._version, world._version)
             ctx.mass_shape = tuple(mass.shape)
             ctx.mass_device = mass.device
             ctx.mass_index = world._mass_body_indices()

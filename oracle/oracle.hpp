@@ -158,6 +158,23 @@ int sphereCapsule(const double* c0, double rs, const Iso<double>& Tc, double rc,
 int capsuleCapsule(const Iso<double>& T0, double r0, double h0, const Iso<double>& T1, double r1, double h1,
                    double clip, int shape1, int shape2, int body1, int body2, std::vector<Contact>& out);
 
+// Replay of another solver path (test infrastructure): when set for the
+// calling thread, solveContacts takes this final LCP solution and path (the
+// gradient short-circuit flag, the fallback CFM, friction removed) instead of
+// running the short-circuit classification and the Dantzig / PGS cascade, and
+// then classifies, standardises, applies impulses and records the snapshot
+// exactly as after its own solve.  Used to check a world whose ill-posed LCP
+// the GPU solved along another (equally valid) path: every quantity after
+// the solve is then compared on the GPU's path.
+struct ForcedLcp {
+  int m = -1;  // rows the forced x has (must equal the step's rows)
+  const double* x = nullptr;
+  bool shortCircuit = false, ignoredFriction = false;
+  double cfm = 0.0;
+  bool mismatch = false;  // set when the step's row count differed
+};
+extern thread_local ForcedLcp* tForcedLcp;
+
 // dense helpers
 void cholSolve(const double* A, const double* b, double* x, int n);
 void pinvSolve(const double* A, const double* b, double* x, int n, double* pinvOut = nullptr);

@@ -39,6 +39,7 @@ def lib():
         L.oracle_snapshots_create.restype = vp
         L.oracle_snapshots_destroy.argtypes = [vp]
         L.oracle_forward.argtypes = [vp, ip, dp, dp, dp, dp, vp]
+        L.oracle_forward_forced.argtypes = [vp, ip, dp, dp, dp, dp, vp, dp, dp]
         L.oracle_backward.argtypes = [vp, ip, vp, dp, dp, dp]
         L.oracle_jacobians.argtypes = [vp, ip, vp, dp, dp]
         L.oracle_constraint_force_jacobians.argtypes = [vp, ip, vp, dp, ip]
@@ -135,6 +136,30 @@ class OracleWorld:
         nxt = np.zeros_like(state)
         lib().oracle_forward(self.h, B, _p(state), _p(forces), _p(self.cache), _p(nxt), self.snaps)
         return nxt
+
+    def forward_forced(self, state, forces, forced_x, flags):
+        """forward with the LCP path of selected worlds replayed (ForcedLcp,
+        oracle.hpp): forced_x [B, MAX_LCP + 1] (column 0 = rows, < 0 = solve
+        as usual, then the final x), flags [B, 3] = (gradient short-circuit,
+        fallback cfm, friction removed).  Returns (next state, number of
+        forced worlds whose row count did not match)."""
+        state = np.ascontiguousarray(np.atleast_2d(state), dtype=np.float64)
+        forces = np.ascontiguousarray(np.atleast_2d(forces), dtype=np.float64)
+        fx = np.ascontiguousarray(forced_x, dtype=np.float64)
+        fl = np.ascontiguousarray(flags, dtype=np.float64)
+        B = state.shape[0]
+        assert fx.shape == (B, MAX_LCP + 1) and fl.shape == (B, 3)
+        if self.snaps is None or self.batch != B:
+            if self.snaps:
+                lib().oracle_snapshots_destroy(self.snaps)
+            self.snaps = lib().oracle_snapshots_create(B)
+            self.batch = B
+        if self.cache is None or self.cache.shape[0] != B:
+            self.reset_cache(B)
+        nxt = np.zeros_like(state)
+        bad = lib().oracle_forward_forced(self.h, B, _p(state), _p(forces), _p(self.cache), _p(nxt), self.snaps,
+                                          _p(fx), _p(fl))
+        return nxt, int(bad)
 
     def backward(self, grad_next):
         g = np.ascontiguousarray(np.atleast_2d(grad_next), dtype=np.float64)

@@ -40,6 +40,40 @@ int oracle_forward(void* wp, int batch, const double* state, const double* tau, 
   return 0;
 }
 
+// oracle_forward with the LCP path of selected worlds replayed
+// (ForcedLcp): forcedX [batch][NIMBLE_MAX_LCP + 1] (element 0 = rows, < 0 =
+// solve normally), flags [batch][3] = (short-circuit, cfm, friction removed).
+// Returns the number of forced worlds whose row count did not match.
+int oracle_forward_forced(void* wp, int batch, const double* state, const double* tau, double* lcpCache,
+                          double* next, void* snaps, const double* forcedX, const double* flags) {
+  World& w = *static_cast<World*>(wp);
+  auto& S = *static_cast<std::vector<OracleSnap>*>(snaps);
+  const int n = w.n;
+  int mismatched = 0;
+  for (int b = 0; b < batch; b++) {
+    double* cache = lcpCache + (size_t)b * (NIMBLE_MAX_LCP + 1);
+    std::vector<double> c;
+    const int sz = (int)cache[0];
+    if (sz >= 0) c.assign(cache + 1, cache + 1 + sz);
+    const double* fx = forcedX + (size_t)b * (NIMBLE_MAX_LCP + 1);
+    ForcedLcp f;
+    if ((int)fx[0] >= 0) {
+      f.m = (int)fx[0];
+      f.x = fx + 1;
+      f.shortCircuit = flags[b * 3 + 0] != 0.0;
+      f.cfm = flags[b * 3 + 1];
+      f.ignoredFriction = flags[b * 3 + 2] != 0.0;
+      tForcedLcp = &f;
+    }
+    step(w, state + (size_t)b * 2 * n, tau + (size_t)b * n, c, next + (size_t)b * 2 * n, S[b].s);
+    tForcedLcp = nullptr;
+    if (f.mismatch) mismatched++;
+    cache[0] = (double)c.size();
+    for (size_t i = 0; i < c.size(); i++) cache[1 + i] = c[i];
+  }
+  return mismatched;
+}
+
 int oracle_backward(void* wp, int batch, void* snaps, const double* gradNext, double* gradState, double* gradTau) {
   World& w = *static_cast<World*>(wp);
   auto& S = *static_cast<std::vector<OracleSnap>*>(snaps);

@@ -965,6 +965,8 @@ struct GradMats {
 };
 
 //------------------------------------------------------------------------------
+thread_local ForcedLcp* tForcedLcp = nullptr;
+
 void solveContacts(const World& w, const Kin<double>& k, const double* q, const double* v, const double* tau,
                    std::vector<double>& v1, const std::vector<Contact>& contactsIn,
                    std::vector<double>& lcpCache, Snapshot& snap) {
@@ -1082,15 +1084,34 @@ void solveContacts(const World& w, const Kin<double>& k, const double* q, const 
   GradMats gm;
   gm.w = &w; gm.m = m; gm.hi = hi; gm.lo = lo; gm.fi = fi; gm.B = b; gm.aColNorms = aColNorms; gm.A = A;
   gm.allCols = &allCols; gm.massedCols = &massed; gm.Minv = &Minv; gm.restitution = rest; gm.penVel = pen;
-  gm.X = X; gm.cfm = 0.0; gm.ignoreFriction = false;
-  gm.construct();
-  bool success = gm.standardized;
-  bool shortCircuit = success;
-  if (success) X = gm.X;
+  ForcedLcp* forced = tForcedLcp;
+  if (forced != nullptr && forced->m != m) { forced->mismatch = true; forced = nullptr; }
+  bool success, shortCircuit;
+  if (forced != nullptr) {
+    // replay: the given path's final solution in place of the solve
+    X.assign(forced->x, forced->x + m);
+    success = shortCircuit = forced->shortCircuit;
+    if (shortCircuit) {
+      gm.X = X; gm.cfm = 0.0; gm.ignoreFriction = false;
+      gm.construct();
+      if (gm.standardized) X = gm.X;
+    }
+  } else {
+    gm.X = X; gm.cfm = 0.0; gm.ignoreFriction = false;
+    gm.construct();
+    success = gm.standardized;
+    shortCircuit = success;
+    if (success) X = gm.X;
+  }
   std::vector<double> Acfm = A;
   double cfm = 0.0;
   bool ignoredFriction = false;
-  if (!success) {
+  if (!success && forced != nullptr) {
+    cfm = forced->cfm;
+    ignoredFriction = forced->ignoredFriction;
+    if (cfm != 0.0)
+      for (int i = 0; i < m; i++) Acfm[i * m + i] += cfm;
+  } else if (!success) {
     const std::vector<double> warm = X;  // mX == mXBackup (cache or guess)
     const LcpCascade r = lcpFallbackCascade(A, b, lo, hi, fi, warm, w.fallbackCfm, X);
     cfm = r.cfm;

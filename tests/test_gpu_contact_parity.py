@@ -30,7 +30,7 @@ SN_CONTACTS, SN_ROWREC, RR_MAP = 16, 12, 7
 SN_ROWS = SN_CONTACTS + 16 * CREC
 
 
-def _rel(a, b, floor=1e-3):
+def _rel(a, b, floor=1e-6):
     """Largest per-element relative error |a - b| / max(|b|, floor * max|b|)
     (the absolute floor keeps components that are zero in exact arithmetic
     from dividing by rounding noise)."""
@@ -212,7 +212,6 @@ def test_timestep_layer_with_contact():
     tf = torch.tensor(f, device=d, requires_grad=True)
     out = nimble.timestep(world, ts, tf)
     out.backward(torch.tensor(g, device=d))
-    assert (O.lcp_flags(ow, 0) == O.lcp_flags(ow, 0)).all()
     assert _rel(out.detach().cpu().numpy(), ref) < RTOL
     assert _rel(ts.grad.cpu().numpy(), rgs) < RTOL
     assert _rel(tf.grad.cpu().numpy(), rgf) < RTOL

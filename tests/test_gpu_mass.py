@@ -130,3 +130,67 @@ def test_timestep_layer_mass_argument():
     assert np.abs(out.detach().cpu().numpy() - ref).max() <= 1e-9 * np.abs(ref).max()
     per = _mass_parity(w, st, f, seed=1, bodies=[0, 27])
     assert np.allclose(mass.grad.cpu().numpy(), per[:, [0, 27]].sum(0), rtol=1e-12, atol=0)
+
+
+def test_backprop_snapshot_loss_wrt_mass():
+    """neural.forwardPass(...).backpropState / backprop fill lossWrtMass
+    [B, getMassDims()] (BackpropSnapshot.cpp:177, :418) with the same values
+    as the batched mass gradient, and leave the state / action gradients as
+    without tuned masses."""
+    from nimblephysics_amd import neural
+    w = models.atlas_world(True)
+    bodies = [b for s in w.skeletons for b in s.bodies]
+    w.tuneMass(bodies[27], "INERTIA_MASS")
+    w.tuneMass(bodies[0], "INERTIA_MASS")
+    st, f = models.random_states(w, 6, seed=9, q_scale=0.01, v_scale=0.02)
+    d = torch.device("cuda:0")
+    ts, tf = torch.tensor(st, device=d), torch.tensor(f, device=d)
+    snap = neural.forwardPass(w, state=ts, action=tf)
+    g = np.random.default_rng(3).standard_normal(st.shape)
+    out = snap.backpropState(w, torch.tensor(g, device=d))
+    assert tuple(out.lossWrtMass.shape) == (6, 2)
+    per = _mass_parity(w, st, f, seed=3, bodies=[0, 27])
+    assert np.allclose(out.lossWrtMass.cpu().numpy(), per[:, [27, 0]], rtol=1e-12, atol=0)
+    this, nxt = neural.LossGradient(), neural.LossGradient()
+    n = w.getNumDofs()
+    nxt.lossWrtPosition = torch.tensor(g[:, :n], device=d)
+    nxt.lossWrtVelocity = torch.tensor(g[:, n:], device=d)
+    snap.backprop(w, this, nxt)
+    assert torch.equal(this.lossWrtMass, out.lossWrtMass)
+    assert torch.equal(torch.cat([this.lossWrtPosition, this.lossWrtVelocity], 1), out.lossWrtState)
+
+
+def test_snapshot_state_is_copied():
+    """The snapshot keeps its own copy of the step's state and forces: a
+    caller reusing its buffers in place does not change later backprop."""
+    from nimblephysics_amd import neural
+    w = models.cartpole_world()
+    st, f = models.random_states(w, 4, seed=2)
+    d = torch.device("cuda:0")
+    ts, tf = torch.tensor(st, device=d), torch.tensor(f, device=d)
+    snap = neural.forwardPass(w, state=ts, action=tf)
+    J0 = snap.getStateJacobian(w).clone()
+    ts.add_(0.3)
+    tf.mul_(2.0)
+    snap2 = neural.forwardPass(w, state=torch.tensor(st, device=d), action=torch.tensor(f, device=d))
+    assert torch.equal(snap2.getStateJacobian(w), J0)
+    snap._jac = None
+    assert torch.equal(snap.getStateJacobian(w), J0)
+
+
+def test_constraint_force_getters_without_collision_pairs():
+    """A contact-free model: no clamping rows, empty f_c and dF_c (the forward
+    writes a zero snapshot header)."""
+    from nimblephysics_amd import neural
+    w = models.cartpole_world()
+    st, f = models.random_states(w, 3, seed=1)
+    d = torch.device("cuda:0")
+    snap = neural.forwardPass(w, state=torch.tensor(st, device=d), action=torch.tensor(f, device=d))
+    assert snap.getNumClamping().tolist() == [0, 0, 0]
+    assert float(snap.getClampingConstraintImpulses().abs().sum()) == 0.0
+    assert float(snap._snap[:, :8].abs().sum()) == 0.0
+    w.setState(st[0])
+    w.setControlForces(f[0])
+    one = neural.forwardPass(w, idempotent=True)
+    assert one.getClampingConstraintImpulses().shape == (0,)
+    assert one.getJacobianOfConstraintForce(w, "POSITION").shape[0] == 0

@@ -15,8 +15,11 @@ pytestmark = pytest.mark.gpu
 RTOL = 1e-6
 
 
-def _rel(a, b):
-    return np.abs(a - b).max() / max(np.abs(b).max(), 1e-12)
+def _rel(a, b, floor=1e-6):
+    """Largest per-element relative error, |a - b| / max(|b|, floor * max|b|)."""
+    a, b = np.asarray(a), np.asarray(b)
+    scale = np.maximum(np.abs(b), floor * max(np.abs(b).max(), 1e-300))
+    return float((np.abs(a - b) / scale).max())
 
 
 def _run_both(world, batch, seed):

@@ -1,0 +1,202 @@
+"""Parity over the bench's own rollout: 1024 Atlas worlds x 25 chained steps.
+
+The bench (bench.py, configs[3]) times 25 chained fwd+bwd steps of 1024
+worlds drawn by its own sampler (workloads.atlas_states, rank 0's seed), each
+step warm-started from the LCP cache of the previous one
+(BoxedLcpConstraintSolver::mX).  Here every step of that rollout is taken by
+the GPU and by the oracle from the SAME input -- the oracle's state and LCP
+cache of the previous step -- so each step's comparison is independent of
+earlier ones, and per step:
+
+* every world's contact set is bit-exact (bodies, types, points 1e-9);
+* a world is on the same LCP path when the solver flags (gradient short-
+  circuit, fallback CFM, friction removed, rank flag) and the per-row
+  classification agree; its final LCP solution x, next state and gradients
+  (random upstream vector) must match the oracle at 1e-6 per element
+  ("same path, different x" is counted and must be zero);
+* a world on another path is replayed: the oracle re-runs that step with the
+  GPU's final x and path forced (oracle ForcedLcp) and must then reproduce
+  the GPU's classification, next state and gradients at 1e-6.  Where the
+  paths split at Dantzig's outcome, the split is checked ambiguous for the
+  reference's own compiled dSolveLCP (oracle/_ref, 1e-15 relative
+  symmetric perturbations of A give both outcomes).
+
+The per-step table is written to gpurun_out/rollout_parity_atlas.json (and
+committed under profiles/).
+"""
+import json
+import os
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+import torch
+
+from nimblephysics_amd import _native, workloads
+from oracle import oracle as O
+from test_gpu_contact_parity import CREC, SN_CONTACTS, SN_M, SN_NCON, _device_backward, _device_step, _rel, _same_path
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-6
+THREADS = 16
+
+
+class ChunkedOracle:
+    """The oracle over a batch split into chunks stepped on host threads
+    (ctypes releases the GIL); world b lives in chunk b // size."""
+
+    def __init__(self, world, batch, chunks=THREADS):
+        self.size = (batch + chunks - 1) // chunks
+        self.parts = [(k, min(k + self.size, batch)) for k in range(0, batch, self.size)]
+        self.o = [O.OracleWorld(world) for _ in self.parts]
+        self.pool = ThreadPoolExecutor(len(self.parts))
+
+    def at(self, b):
+        return self.o[b // self.size], b % self.size
+
+    def forward(self, st, f, cache, forced=None):
+        out = np.zeros_like(st)
+        bad = [0]
+
+        def run(i):
+            s, e = self.parts[i]
+            o = self.o[i]
+            o.reset_cache(e - s)
+            o.cache[:] = cache[s:e]
+            if forced is None:
+                out[s:e] = o.forward(st[s:e], f[s:e])
+            else:
+                out[s:e], k = o.forward_forced(st[s:e], f[s:e], forced[0][s:e], forced[1][s:e])
+                bad[0] += k
+        list(self.pool.map(run, range(len(self.parts))))
+        new_cache = np.concatenate([o.cache for o in self.o])
+        return out, new_cache, bad[0]
+
+    def backward(self, g):
+        gs, gf = np.zeros_like(g), np.zeros((g.shape[0], self.o[0].n))
+
+        def run(i):
+            s, e = self.parts[i]
+            gs[s:e], gf[s:e] = self.o[i].backward(g[s:e])
+        list(self.pool.map(run, range(len(self.parts))))
+        return gs, gf
+
+
+def _ref_dantzig_ambiguous(A, bb, lo, hi, fi, seed, trials=64):
+    """The reference's compiled dSolveLCP succeeds on some and early-
+    terminates on other 1e-15-relative symmetric perturbations of A."""
+    rng = np.random.default_rng(seed)
+    outs = set()
+    for _ in range(trials):
+        N = rng.standard_normal(A.shape)
+        r = O.ref_dantzig(A * (1 + 1e-15 * (N + N.T) / 2), bb, lo, hi, fi, True)
+        if r is None:
+            return None
+        outs.add(r[0])
+        if len(outs) == 2:
+            return True
+    return False
+
+
+def _contacts_exact(ow, b, sn):
+    ref = O.contacts(ow, b)
+    nc = int(sn[SN_NCON])
+    if nc != len(ref):
+        return False
+    got = sn[SN_CONTACTS:SN_CONTACTS + CREC * nc].reshape(nc, CREC)
+    return (np.array_equal(got[:, 7].astype(int) & 15, ref[:, 7].astype(int))
+            and np.array_equal(got[:, 8:10].astype(int), ref[:, 8:10].astype(int))
+            and np.abs(got[:, :7] - ref[:, :7]).max(initial=0) < 1e-9)
+
+
+def test_atlas_bench_rollout_parity():
+    world = workloads.atlas_world(True)
+    world.setStatusPolicy("record")
+    B, STEPS = 1024, 25
+    n = world.getNumDofs()
+    st, f = workloads.atlas_states(world, B, 1000)  # bench.rank_inputs(rank 0)
+    dev = world.native()
+    assert dev.cache_doubles == _native.MAX_LCP + 1
+    orc = ChunkedOracle(world, B)
+    cache = np.zeros((B, dev.cache_doubles))
+    cache[:, 0] = -1
+    cur = st
+    table = []
+    for k in range(STEPS):
+        ref, ref_cache, _ = orc.forward(cur, f, cache)
+        nxt, snap, gcache, ts, tf = _device_step(world, cur, f, torch.tensor(cache, device="cuda:0"))
+        got, snap, gcache = nxt.cpu().numpy(), snap.cpu().numpy(), gcache.cpu().numpy()
+        g = np.random.default_rng(100 + k).standard_normal(cur.shape)
+        rgs, rgf = orc.backward(g)
+        ggs, ggf = _device_backward(world, ts, tf, snap, g)
+        row = {"step": k, "worlds_in_contact": 0, "lcp_rows_mean": 0.0, "diverged": 0, "diverged_kinds": {},
+               "same_path_diff_x": 0, "ref_ambiguous": 0, "ref_unambiguous": 0}
+        same = np.ones(B, dtype=bool)
+        for b in range(B):
+            o, i = orc.at(b)
+            sn = snap[b]
+            assert _contacts_exact(o, i, sn), (k, b)
+            if sn[SN_NCON] > 0:
+                row["worlds_in_contact"] += 1
+            m = int(sn[SN_M])
+            row["lcp_rows_mean"] += m / B
+            if m == 0:
+                continue
+            if _same_path(o, sn, b=i):
+                x_ref, x_gpu = ref_cache[b, 1:1 + m], gcache[b, 1:1 + m]
+                assert int(gcache[b, 0]) == m == int(ref_cache[b, 0]), (k, b)
+                if _rel(x_gpu, x_ref) >= RTOL:
+                    row["same_path_diff_x"] += 1
+                continue
+            same[b] = False
+            row["diverged"] += 1
+            of = O.lcp_flags(o, i)
+            kind = ("short-circuit" if of[0] != sn[6] else "cfm" if of[2] != sn[4] else
+                    "friction-removed" if of[1] != sn[7] else "classification")
+            row["diverged_kinds"][kind] = row["diverged_kinds"].get(kind, 0) + 1
+            if kind == "cfm":
+                # the paths split at Dantzig's outcome (success vs fallback)
+                A, bb, lo, hi, fi = O.lcp_problem(o, i)
+                amb = _ref_dantzig_ambiguous(A, bb, lo, hi, fi, seed=1000 * k + b)
+                row["ref_ambiguous" if amb else "ref_unambiguous"] += 1
+        row["lcp_rows_mean"] = round(row["lcp_rows_mean"], 3)
+        # same path: next state and gradients at 1e-6 per element
+        row["next_state_rel_err"] = _rel(got[same], ref[same])
+        row["grad_state_rel_err"] = _rel(ggs[same], rgs[same])
+        row["grad_force_rel_err"] = _rel(ggf[same], rgf[same])
+        # other path: the oracle replays the GPU's path and must agree on all
+        div = np.nonzero(~same)[0]
+        if len(div):
+            fx = np.full((B, dev.cache_doubles), -1.0)
+            fl = np.zeros((B, 3))
+            fx[div] = gcache[div]
+            fl[div, 0], fl[div, 1], fl[div, 2] = snap[div, 6], snap[div, 4], snap[div, 7]
+            rep, _, bad = orc.forward(cur, f, cache, forced=(fx, fl))
+            assert bad == 0, (k, bad)
+            for b in div:
+                o, i = orc.at(b)
+                assert _same_path(o, snap[b], b=i), (k, b, "replay did not reproduce the GPU's classification")
+            rgs2, rgf2 = orc.backward(g)
+            row["replay_next_state_rel_err"] = _rel(got[div], rep[div])
+            row["replay_grad_state_rel_err"] = _rel(ggs[div], rgs2[div])
+            row["replay_grad_force_rel_err"] = _rel(ggf[div], rgf2[div])
+            assert row["replay_next_state_rel_err"] < RTOL, row
+            assert row["replay_grad_state_rel_err"] < RTOL, row
+            assert row["replay_grad_force_rel_err"] < RTOL, row
+        table.append(row)
+        assert row["next_state_rel_err"] < RTOL, row
+        assert row["grad_state_rel_err"] < RTOL, row
+        assert row["grad_force_rel_err"] < RTOL, row
+        cur, cache = ref, ref_cache  # the next step starts from the oracle's state and cache
+    out = {"workload": "Atlas + ground, bench sampler rank 0 (seed 1000), 1024 worlds x 25 steps",
+           "rtol": RTOL, "steps": table,
+           "totals": {k: int(sum(r[k] for r in table)) for k in ("diverged", "same_path_diff_x", "ref_ambiguous",
+                                                                   "ref_unambiguous")}}
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(os.path.join("gpurun_out", "rollout_parity_atlas.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps(out["totals"]))
+    assert out["totals"]["same_path_diff_x"] == 0, out["totals"]
+    assert out["totals"]["ref_unambiguous"] == 0, out["totals"]
+    assert max(r["diverged"] for r in table) <= 0.03 * B

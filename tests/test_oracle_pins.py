@@ -420,8 +420,8 @@ def test_constraint_force_jacobian_vs_finite_differences(oracle_built, name):
         st, f = models.capsule_edge_states(8, seed=1)
         picks = [2, 6]
     else:
-        w, _, st, f, _ = models.broken_states("half_cheetah")
-        picks = [0, 1, 2, 3]
+        w, _, st, f, _ = models.broken_states("atlas")
+        picks = list(range(st.shape[0]))
     n = w.getNumDofs()
     o = O.OracleWorld(w)
     o.forward(st, f)
@@ -445,3 +445,34 @@ def test_constraint_force_jacobian_vs_finite_differences(oracle_built, name):
             e[i] = 1e-4
             fd[:, 2 * n + i] = (fc(st[b], f[b] + e) - fc(st[b], f[b] - e)) / 2e-4
         assert np.abs(J[b, :nc] - fd).max() <= 1e-6 * np.abs(fd).max(), (name, b)
+
+
+def test_forced_lcp_replay_reproduces_own_path(oracle_built):
+    """The replay hook (ForcedLcp) fed a world's own final LCP solution and
+    path gives that step back: next state, classification and gradients.
+    (The GPU rollout test replays the GPU's path through it.)"""
+    w = models.atlas_world(True)
+    st, f = models.random_states(w, 24, seed=3, q_scale=0.01, v_scale=0.02)
+    o = O.OracleWorld(w)
+    ref = o.forward(st, f)
+    B = st.shape[0]
+    g = np.random.default_rng(2).standard_normal(st.shape)
+    rgs, rgf = o.backward(g)
+    fx = o.cache.copy()
+    flags = np.array([[O.lcp_flags(o, b)[0], O.lcp_flags(o, b)[2], O.lcp_flags(o, b)[1]] for b in range(B)])
+    maps = [O.lcp_debug(o, b)[0] for b in range(B)]
+    o2 = O.OracleWorld(w)
+    nxt, bad = o2.forward_forced(st, f, fx, flags)
+    assert bad == 0
+    assert np.abs(nxt - ref).max() <= 1e-12 * np.abs(ref).max()
+    for b in range(B):
+        assert np.array_equal(O.lcp_debug(o2, b)[0], maps[b])
+    gs, gf = o2.backward(g)
+    assert np.abs(gs - rgs).max() <= 1e-10 * np.abs(rgs).max()
+    assert np.abs(gf - rgf).max() <= 1e-10 * np.abs(rgf).max()
+    # a row-count mismatch is reported, not replayed
+    fx2 = fx.copy()
+    hit = [b for b in range(B) if fx[b, 0] > 0][0]
+    fx2[hit, 0] += 3
+    _, bad = O.OracleWorld(w).forward_forced(st, f, fx2, flags)
+    assert bad == 1

@@ -42,17 +42,26 @@ enum nimble_joint_type {
 enum nimble_shape_type {
   NIMBLE_SHAPE_BOX = 0,
   NIMBLE_SHAPE_SPHERE = 1,
-  NIMBLE_SHAPE_CAPSULE = 2    /* dart/dynamics/CapsuleShape.hpp: shape_size =
+  NIMBLE_SHAPE_CAPSULE = 2,   /* dart/dynamics/CapsuleShape.hpp: shape_size =
                                  (radius, height, 0), axis = local z */
+  NIMBLE_SHAPE_MESH = 3       /* dart/dynamics/MeshShape.hpp: shape_size =
+                                 scale; vertices in mesh_vertices (the
+                                 aiScene's vertex list in order, collided as
+                                 their convex hull by libccd MPR,
+                                 DARTCollide.cpp:1935) */
 };
 
 #define NIMBLE_MAX_BODIES 64
 #define NIMBLE_MAX_DOFS 64
 #define NIMBLE_MAX_SHAPES 32
 /* Max contact points per world per step and LCP rows (3 per frictional
- * contact, dart/constraint/ContactConstraint.cpp:147 mDim = 3). */
-#define NIMBLE_MAX_CONTACTS 16
+ * contact, dart/constraint/ContactConstraint.cpp:147 mDim = 3): the layout of
+ * the snapshot and the LCP cache.  The device solves LCPs of up to
+ * NIMBLE_MAX_SOLVED_LCP rows (one row per lane of a 64-lane wavefront); a
+ * world with more rows is flagged NIMBLE_STATUS_LCP_TOO_LARGE. */
+#define NIMBLE_MAX_CONTACTS 32
 #define NIMBLE_MAX_LCP (3 * NIMBLE_MAX_CONTACTS)
+#define NIMBLE_MAX_SOLVED_LCP 64
 
 /*
  * Flat description of a World (all skeletons of the world concatenated in
@@ -102,6 +111,19 @@ typedef struct nimble_world_desc {
   const int32_t* shape_type;        /* nimble_shape_type                   */
   const double* shape_size;         /* [3] box size; sphere (r); capsule (r, h) */
   const double* shape_T;            /* [12] ShapeNode relative transform   */
+
+  /* mesh shapes: vertices of all meshes concatenated, shape s (type
+   * NIMBLE_SHAPE_MESH) owns [shape_mesh_first[s], + shape_mesh_count[s]) */
+  int32_t num_mesh_vertices;
+  int32_t reserved2;
+  const double* mesh_vertices;      /* [num_mesh_vertices][3], mesh frame, unscaled */
+  const int32_t* shape_mesh_first;  /* [num_shapes] (unused for other types) */
+  const int32_t* shape_mesh_count;  /* [num_shapes]                         */
+  /* optional (NULL = all vertices): 1 for the vertices within the witness
+   * plane depth (0.01, DARTCollide.cpp:58) of the mesh's convex hull
+   * boundary -- the only ones that can be a support point or a witness
+   * point; the device scans only these, in their original order */
+  const int32_t* mesh_vertex_candidate;
 } nimble_world_desc;
 
 typedef struct nimble_world* nimble_world_t;
@@ -149,6 +171,9 @@ int32_t nimble_num_collision_pairs(nimble_world_t world);
 #define NIMBLE_STATUS_LCP_REDUCED 8       /* LCPUtils::reduce merged duplicate
                                              columns (reference behaviour,
                                              LCPUtils.cpp:144; informational) */
+#define NIMBLE_STATUS_LCP_TOO_LARGE 16    /* more than NIMBLE_MAX_SOLVED_LCP LCP
+                                             rows: contacts recorded, the
+                                             constraint solve not taken      */
 
 /*
  * Batched differentiable forward step == neural::forwardPass + World::step

@@ -116,6 +116,18 @@ class CapsuleShape : public Shape {
   double getRadius() const { return mSize[0]; }
   double getHeight() const { return mSize[1]; }
 };
+/* dart/dynamics/MeshShape.hpp: collided as the convex hull of its vertex list
+ * (DARTCollide.cpp:1935); vertices [3k..3k+2] in the mesh frame, in the
+ * aiMesh's order, scaled by `scale` */
+class MeshShape : public Shape {
+ public:
+  MeshShape(const Vector3s& scale, std::vector<double> vertices)
+      : Shape(NIMBLE_SHAPE_MESH, scale), mVertices(std::move(vertices)) {}
+  Vector3s getScale() const { return mSize; }
+  const std::vector<double>& getVertices() const { return mVertices; }
+ private:
+  std::vector<double> mVertices;
+};
 using ShapePtr = std::shared_ptr<Shape>;
 
 /* Aspect tags of BodyNode::createShapeNodeWith<...> */
@@ -385,6 +397,8 @@ class World {
   std::vector<int32_t> mI32[6];
   std::vector<double> mF64[20];
   std::vector<int32_t> mShapeTypes;
+  std::vector<int32_t> mMeshFirst, mMeshCount;
+  std::vector<double> mMeshVertices;
   nimble_world_desc mDesc{};
   // batch-of-one device buffers (state, forces, LCP cache, next state, snapshot)
   double* mDev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};

@@ -11,7 +11,7 @@ P_F64 = C.POINTER(C.c_double)
 NIMBLE_MAX_BODIES = 64
 NIMBLE_MAX_DOFS = 64
 NIMBLE_MAX_SHAPES = 32
-NIMBLE_MAX_CONTACTS = 16
+NIMBLE_MAX_CONTACTS = 32
 NIMBLE_MAX_LCP = 3 * NIMBLE_MAX_CONTACTS
 
 
@@ -53,6 +53,12 @@ class NimbleWorldDesc(C.Structure):
         ("shape_type", P_I32),
         ("shape_size", P_F64),
         ("shape_T", P_F64),
+        ("num_mesh_vertices", C.c_int32),
+        ("reserved2", C.c_int32),
+        ("mesh_vertices", P_F64),
+        ("shape_mesh_first", P_I32),
+        ("shape_mesh_count", P_I32),
+        ("mesh_vertex_candidate", P_I32),
     ]
 
 
@@ -95,4 +101,19 @@ def build_desc(arrays: dict):
         a, p = _f64(arrays[name])
         keep.append(a)
         setattr(d, name, p)
+    mv = np.asarray(arrays.get("mesh_vertices", np.zeros((0, 3))), dtype=np.float64).reshape(-1, 3)
+    d.num_mesh_vertices = int(mv.shape[0])
+    a, p = _f64(mv)
+    keep.append(a)
+    d.mesh_vertices = p
+    ns = int(arrays["num_shapes"])
+    for name in ("shape_mesh_first", "shape_mesh_count"):
+        a, p = _i32(arrays.get(name, np.zeros(ns, dtype=np.int32)))
+        keep.append(a)
+        setattr(d, name, p)
+    cand = arrays.get("mesh_vertex_candidate")
+    if cand is not None and mv.shape[0] > 0:
+        a, p = _i32(cand)
+        keep.append(a)
+        d.mesh_vertex_candidate = p
     return d, keep

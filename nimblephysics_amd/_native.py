@@ -72,11 +72,12 @@ def _require_device(*tensors):
 
 # snapshot header (csrc/pool_sizes.h) and status bits (csrc/contact.cuh)
 SN_NCON, SN_M, SN_NC, SN_NU, SN_CFM, SN_STATUS = 0, 1, 2, 3, 4, 5
-MAX_CONTACTS = 16
+MAX_CONTACTS = 32
 MAX_LCP = 3 * MAX_CONTACTS  # include/nimble_amd.h NIMBLE_MAX_LCP
 SN_FC = 16 + 13 * MAX_CONTACTS + 12 * MAX_LCP  # NIMBLE_SNAPSHOT_FC: clamping impulses f_c
-ST_CONTACT_OVERFLOW, ST_UNSUPPORTED_SHAPE, ST_DROPPED_OVERFLOW, ST_REDUCED = 1, 2, 4, 8
-ST_DIVERGES = ST_CONTACT_OVERFLOW | ST_UNSUPPORTED_SHAPE | ST_DROPPED_OVERFLOW
+ST_CONTACT_OVERFLOW, ST_UNSUPPORTED_SHAPE, ST_DROPPED_OVERFLOW, ST_REDUCED, ST_LCP_TOO_LARGE = 1, 2, 4, 8, 16
+ST_DIVERGES = ST_CONTACT_OVERFLOW | ST_UNSUPPORTED_SHAPE | ST_DROPPED_OVERFLOW | ST_LCP_TOO_LARGE
+MAX_SOLVED_LCP = 64  # include/nimble_amd.h NIMBLE_MAX_SOLVED_LCP
 
 
 class ContactCapacityError(RuntimeError):
@@ -93,6 +94,8 @@ def status_message(bits: int) -> str:
         why.append("a shape pair without a collider on this path")
     if bits & ST_DROPPED_OVERFLOW:
         why.append("dropped-contact list overflow")
+    if bits & ST_LCP_TOO_LARGE:
+        why.append(f"more than {MAX_SOLVED_LCP} LCP rows")
     return ", ".join(why)
 
 

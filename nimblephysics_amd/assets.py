@@ -20,6 +20,16 @@ from . import dynamics as dyn
 ASSET_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets")
 
 
+def _shape_dict(node) -> dict:
+    d = {"kind": node.shape.kind, "size": node.shape.size.tolist(), "T": node.T.tolist()}
+    if node.shape.kind == dyn.SHAPE_MESH:
+        # float32 values (assimp's ai_real), exact in JSON as repr of the double
+        d["mesh"] = node.shape.path
+        d["vertices"] = node.shape.vertices.reshape(-1).tolist()
+        d["candidate"] = node.shape.candidate().tolist()
+    return d
+
+
 def skeleton_to_dict(skel: dyn.Skeleton) -> dict:
     bodies = []
     for b in skel.bodies:
@@ -38,8 +48,7 @@ def skeleton_to_dict(skel: dyn.Skeleton) -> dict:
             },
             "mass": b.mass, "com": b.com.tolist(), "moment": b.moment.tolist(),
             "friction": b.friction, "restitution": b.restitution,
-            "shapes": [{"kind": s.shape.kind, "size": s.shape.size.tolist(), "T": s.T.tolist()}
-                       for s in b.shape_nodes if s.collision],
+            "shapes": [_shape_dict(s) for s in b.shape_nodes if s.collision],
         })
     return {"name": skel.name, "mobile": skel.mobile, "bodies": bodies,
             "positions": skel.getPositions().tolist()}
@@ -71,6 +80,10 @@ def skeleton_from_dict(d: dict) -> dyn.Skeleton:
                 shape = dyn.BoxShape(sd["size"])
             elif sd["kind"] == dyn.SHAPE_CAPSULE:
                 shape = dyn.CapsuleShape(sd["size"][0], sd["size"][1])
+            elif sd["kind"] == dyn.SHAPE_MESH:
+                shape = dyn.MeshShape(sd["size"], np.array(sd["vertices"]), sd.get("mesh", ""))
+                if "candidate" in sd:
+                    shape._candidate = np.asarray(sd["candidate"], dtype=np.int32)
             else:
                 shape = dyn.SphereShape(sd["size"][0])
             node = b.createShapeNode(shape, collision=True)

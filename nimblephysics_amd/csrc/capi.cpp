@@ -34,6 +34,7 @@ struct nimble_world {
   int jacWsDoubles = 0;  // per-workgroup LCP workspace of the Jacobian launch
   int cacheDoubles = NIMBLE_MAX_LCP + 1;
   hipFunction_t dummy = nullptr;
+  double* meshDev = nullptr;  // ModelDev::meshVerts
 };
 
 extern "C" __global__ void nimble_forward_kernel(const ModelDev*, Layout, const double*, const double*, double*,
@@ -69,7 +70,7 @@ static Layout makeLayout(const ModelDev& m, bool backward, int poolRows) {
   L.dinv = take(n);             // 1 / L_kk
   L.rhs = take(n); L.x = take(n);
   L.v1 = take(n);
-  L.ct = take(!backward && m.numPairs > 0 ? ctDoubles() : 16);
+  L.ct = take(!backward && m.numPairs > 0 ? ctDoubles(m.maxContacts) : 16);
   if (backward) {
     // adjoint vectors (alpha..kappa per body); afterwards the workspace of
     // the contact-geometry terms, the M-derivative field pairs and the free
@@ -91,7 +92,7 @@ static Layout makeLayout(const ModelDev& m, bool backward, int poolRows) {
     int area = dyn;
     L.cscr = o + dyn;
     if (m.numPairs > 0) {
-      const int cs = collideScratchDoubles(m.pairChunk);
+      const int cs = collideScratchDoubles(m.pairChunk, m.hasMesh != 0);
       if (dyn + cs > area) area = dyn + cs;
       if (poolRows > 0) {
         L.poolCap = fwdPoolDoublesHost(poolRows, n);
@@ -216,15 +217,64 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
       m.numPairs++;
     }
   m.pairChunk = m.numPairs < CT_PAIR_CHUNK_HOST ? m.numPairs : CT_PAIR_CHUNK_HOST;
-  // max LCP rows: 3 per contact, <= 8 box-box points per pair, <= NIMBLE_MAX_CONTACTS
-  int maxContacts = 8 * m.numPairs;
+  // mesh colliders: candidate vertices (all when the description has no
+  // candidate mask), concatenated per shape; a mesh pair is narrow-phased by
+  // the whole wave, so a model with mesh pairs takes its pairs one at a time
+  {
+    std::vector<double> mv;
+    m.hasMesh = 0;
+    for (int sIdx = 0; sIdx < m.ns; sIdx++) {
+      m.meshFirst[sIdx] = 0; m.meshCount[sIdx] = 0; m.meshRadius[sIdx] = 0.0;
+      if (m.shapeType[sIdx] != NIMBLE_SHAPE_MESH) continue;
+      if (d->mesh_vertices == nullptr || d->shape_mesh_count == nullptr || d->shape_mesh_count[sIdx] <= 0) {
+        delete w;
+        return fail(NIMBLE_ERR_INVALID, "mesh shape without vertices");
+      }
+      const int f = d->shape_mesh_first[sIdx], c = d->shape_mesh_count[sIdx];
+      if (f < 0 || f + c > d->num_mesh_vertices) { delete w; return fail(NIMBLE_ERR_INVALID, "mesh vertex range"); }
+      m.meshFirst[sIdx] = (int)(mv.size() / 3);
+      double r2 = 0.0;
+      for (int k = 0; k < c; k++) {
+        const double* v = d->mesh_vertices + 3 * (size_t)(f + k);
+        double q = 0.0;
+        for (int i = 0; i < 3; i++) q += (v[i] * m.shapeSize[sIdx][i]) * (v[i] * m.shapeSize[sIdx][i]);
+        if (q > r2) r2 = q;
+        if (d->mesh_vertex_candidate != nullptr && d->mesh_vertex_candidate[f + k] == 0) continue;
+        mv.insert(mv.end(), v, v + 3);
+      }
+      m.meshCount[sIdx] = (int)(mv.size() / 3) - m.meshFirst[sIdx];
+      m.meshRadius[sIdx] = std::sqrt(r2);
+    }
+    if (!mv.empty()) {
+      hipError_t e = hipMalloc(&w->meshDev, mv.size() * sizeof(double));
+      if (e == hipSuccess) e = hipMemcpy(w->meshDev, mv.data(), mv.size() * sizeof(double), hipMemcpyHostToDevice);
+      if (e != hipSuccess) {
+        if (w->meshDev) (void)hipFree(w->meshDev);
+        delete w;
+        return fail(NIMBLE_ERR_HIP, std::string("mesh upload: ") + hipGetErrorString(e));
+      }
+    }
+    m.meshVerts = w->meshDev;
+    for (int p = 0; p < m.numPairs; p++)
+      if (m.shapeType[m.pairA[p]] == NIMBLE_SHAPE_MESH || m.shapeType[m.pairB[p]] == NIMBLE_SHAPE_MESH) m.hasMesh = 1;
+    if (m.hasMesh) m.pairChunk = m.numPairs > 0 ? 1 : 0;
+  }
+  // max contacts: <= 8 box-box points per pair (a mesh pair: any number),
+  // <= NIMBLE_MAX_CONTACTS; LCP rows the device solves: 3 per contact, <=
+  // NIMBLE_MAX_SOLVED_LCP (more rows: NIMBLE_STATUS_LCP_TOO_LARGE)
+  int maxContacts = m.hasMesh ? NIMBLE_MAX_CONTACTS : 8 * m.numPairs;
   if (maxContacts > NIMBLE_MAX_CONTACTS) maxContacts = NIMBLE_MAX_CONTACTS;
-  const int mcap = 3 * maxContacts;
+  m.maxContacts = maxContacts;
+  const int mcap = 3 * maxContacts < NIMBLE_MAX_SOLVED_LCP ? 3 * maxContacts : NIMBLE_MAX_SOLVED_LCP;
   int fwdRows = ldsPoolRows(m, mcap);
   for (;;) {
     w->fwd = makeLayout(m, false, fwdRows);
     if (w->fwd.total * 8 <= 160 * 1024) break;
-    if (fwdRows == 0) { delete w; return fail(NIMBLE_ERR_UNSUPPORTED, "model too large for LDS"); }
+    if (fwdRows == 0) {
+      if (w->meshDev) (void)hipFree(w->meshDev);
+      delete w;
+      return fail(NIMBLE_ERR_UNSUPPORTED, "model too large for LDS");
+    }
     fwdRows = fwdRows > 6 ? fwdRows - 6 : 0;
   }
   // The backward kernel is occupancy-bound: its pool gets the rows that keep
@@ -236,7 +286,11 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
   if (bwdRows < 0)
     for (int r = fwdRows; r >= 0; r--)
       if (makeLayout(m, true, r).total * 8 <= 160 * 1024) { bwdRows = r; break; }
-  if (bwdRows < 0) { delete w; return fail(NIMBLE_ERR_UNSUPPORTED, "model too large for LDS"); }
+  if (bwdRows < 0) {
+    if (w->meshDev) (void)hipFree(w->meshDev);
+    delete w;
+    return fail(NIMBLE_ERR_UNSUPPORTED, "model too large for LDS");
+  }
   w->bwd = makeLayout(m, true, bwdRows);
   if (getenv("NIMBLE_AMD_VERBOSE"))
     fprintf(stderr, "nimble_amd: LDS forward %d B (pool rows %d), backward %d B (pool rows %d), max rows %d\n",
@@ -263,9 +317,18 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
   m.lay[0] = w->fwd;
   m.lay[1] = w->bwd;
   hipError_t e = hipMalloc(&w->dev, sizeof(ModelDev));
-  if (e != hipSuccess) { delete w; return fail(NIMBLE_ERR_HIP, std::string("hipMalloc: ") + hipGetErrorString(e)); }
+  if (e != hipSuccess) {
+    if (w->meshDev) (void)hipFree(w->meshDev);
+    delete w;
+    return fail(NIMBLE_ERR_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
+  }
   e = hipMemcpy(w->dev, &m, sizeof(ModelDev), hipMemcpyHostToDevice);
-  if (e != hipSuccess) { (void)hipFree(w->dev); delete w; return fail(NIMBLE_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e)); }
+  if (e != hipSuccess) {
+    (void)hipFree(w->dev);
+    if (w->meshDev) (void)hipFree(w->meshDev);
+    delete w;
+    return fail(NIMBLE_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e));
+  }
   *out = w;
   return NIMBLE_OK;
 }
@@ -273,6 +336,7 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
 int nimble_world_destroy(nimble_world_t w) {
   if (!w) return NIMBLE_OK;
   if (w->dev) (void)hipFree(w->dev);
+  if (w->meshDev) (void)hipFree(w->meshDev);
   delete w;
   return NIMBLE_OK;
 }

@@ -103,10 +103,16 @@ DEV V support(const Obj& o, V dir) {
   return xf(o.T, add(ld, mk(0, 0, -o.s1 / 2)));
 }
 
+// ccd callbacks of an object type: supportOf (ccd.support) and centerOf
+// (ccd.center); the mesh collider (mesh.cuh) adds its own object type
+DEV V supportOf(const Obj& o, V dir) { return support(o, dir); }
+DEV V centerOf(const Obj& o) { return pos(o.T); }
+
 struct Supp { V v, v1, v2; };
-DEV void ccdSupport(const Obj& a, const Obj& b, V dir, Supp& s) {
-  s.v1 = support(a, dir);
-  s.v2 = support(b, scl(dir, -1.0));
+template <class OA, class OB>
+DEV void ccdSupport(const OA& a, const OB& b, V dir, Supp& s) {
+  s.v1 = supportOf(a, dir);
+  s.v2 = supportOf(b, scl(dir, -1.0));
   s.v = sub(s.v1, s.v2);
 }
 
@@ -185,10 +191,11 @@ DEV V findPos(const Supp* P) {
 }
 
 // ccdMPRPenetration: 0 intersecting (depth, dir, pos), -1 separated
-DEV int mpr(const Obj& a, const Obj& b, double& depth, V& pdir, V& ppos) {
+template <class OA, class OB>
+DEV int mpr(const OA& a, const OB& b, double& depth, V& pdir, V& ppos) {
   Supp P[4];
-  P[0].v1 = pos(a.T);
-  P[0].v2 = pos(b.T);
+  P[0].v1 = centerOf(a);
+  P[0].v2 = centerOf(b);
   P[0].v = sub(P[0].v1, P[0].v2);
   if (isZero(P[0].v.x) && isZero(P[0].v.y) && isZero(P[0].v.z)) P[0].v.x += kEps * 10.0;
   V dir = ccdNormalize(scl(P[0].v, -1.0));

@@ -24,6 +24,7 @@
 #include "spatial.cuh"
 #include "pool_sizes.h"
 #include "capsule.cuh"
+#include "mesh.cuh"
 
 #define CT_FACE_VERTEX 1
 #define CT_VERTEX_FACE 2
@@ -467,6 +468,7 @@ __device__ __forceinline__ void collideWait(double* ct, int want) {
 #define ST_UNSUPPORTED_SHAPE 2
 #define ST_DROPPED_OVERFLOW 4
 #define ST_DUPLICATE_COLUMNS 8  // LCPUtils::reduce merged columns (reference behaviour)
+#define ST_LCP_TOO_LARGE 16     // more LCP rows than the wave solves (NIMBLE_MAX_SOLVED_LCP)
 
 // row record fields
 #define RR_CONTACT 0
@@ -531,6 +533,8 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
         tmul(s + L.Tw + 12 * bj, md.shapeT[sj], T2);
         cnt = deviceCapsuleCapsule(T1, md.shapeSize[si][0], md.shapeSize[si][1], T2, md.shapeSize[sj][0],
                                    md.shapeSize[sj][1], md.clipDepth, bi, bj, pairbuf + lane * 8 * PBREC);
+      } else if (md.shapeType[si] == NIMBLE_SHAPE_MESH || md.shapeType[sj] == NIMBLE_SHAPE_MESH) {
+        cnt = 0;  // narrow-phased by the whole wave below
       } else if (md.shapeType[si] == NIMBLE_SHAPE_SPHERE || md.shapeType[sj] == NIMBLE_SHAPE_SPHERE) {
         const int ti = md.shapeType[si], tj = md.shapeType[sj];
         double T1[12], T2[12];
@@ -556,6 +560,42 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
         cnt = -1;
       }
       ct[H_PAIRCNT + lane] = cnt;
+    }
+    if (md.hasMesh) {
+      // a model with mesh pairs takes one pair per chunk; a mesh pair is
+      // collided by the whole wave (collideMeshBox / collideBoxMesh)
+      WSYNC();
+      const int si = md.pairA[p0], sj = md.pairB[p0];
+      const int ti = md.shapeType[si], tj = md.shapeType[sj];
+      if (ti == NIMBLE_SHAPE_MESH || tj == NIMBLE_SHAPE_MESH) {
+        int cnt = -1;  // mesh-sphere / mesh-capsule / mesh-mesh: no collider on this path
+        if ((ti == NIMBLE_SHAPE_MESH && tj == NIMBLE_SHAPE_BOX) || (ti == NIMBLE_SHAPE_BOX && tj == NIMBLE_SHAPE_MESH)) {
+          const bool meshFirst = ti == NIMBLE_SHAPE_MESH;
+          const int sm = meshFirst ? si : sj, sb = meshFirst ? sj : si;
+          double Tm[12], Tb[12];
+          tmul(s + L.Tw + 12 * md.shapeBody[sm], md.shapeT[sm], Tm);
+          tmul(s + L.Tw + 12 * md.shapeBody[sb], md.shapeT[sb], Tb);
+          // the mesh's bounding sphere more than 1 mm clear of the box: the
+          // convex hull and the box are separated, MPR reports no contact
+          double gap2 = 0.0;
+          for (int i = 0; i < 3; i++) {
+            const double c = (Tm[3] - Tb[3]) * Tb[i] + (Tm[7] - Tb[7]) * Tb[4 + i] + (Tm[11] - Tb[11]) * Tb[8 + i];
+            const double h = 0.5 * md.shapeSize[sb][i];
+            const double e = c > h ? c - h : (c < -h ? -h - c : 0.0);
+            gap2 += e * e;
+          }
+          const double reach = md.meshRadius[sm] + 1e-3;
+          if (gap2 > reach * reach) {
+            cnt = 0;
+          } else {
+            lds_double* mscr = (lds_double*)(pairbuf + pairBufRecs(PC, true) * PBREC);
+            cnt = deviceMeshBox(Tm, md.meshVerts + 3 * md.meshFirst[sm], md.meshCount[sm], md.shapeSize[sm], Tb,
+                                md.shapeSize[sb], meshFirst, md.clipDepth, md.shapeBody[si], md.shapeBody[sj],
+                                pairbuf, mscr, lane);
+          }
+        }
+        if (lane == 0) ct[H_PAIRCNT] = cnt;
+      }
     }
     WSYNC();
     TACC_END(76, tNP);
@@ -626,7 +666,7 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
           double* dst = nullptr;
           if (keep) {
             const int idx = nk0 + __popcll(km & below);
-            if (idx < NIMBLE_MAX_CONTACTS) {
+            if (idx < md.maxContacts) {
               dst = ct + CT_CONTACTS + idx * CREC;
               if (((int)rec[7] & 15) == CT_EDGE_EDGE || ((int)rec[7] & 15) >= CT_SPHERE_SPHERE)
                 for (int i = 0; i < EDGE_REC; i++) snapEdge[idx * EDGE_REC + i] = rec[CREC + i];
@@ -641,9 +681,9 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
             const int nk = nk0 + __popcll(km), nd = nd0 + __popcll(dm);
             int st = (int)ct[H_STATUS];
             if (um) st |= ST_UNSUPPORTED_SHAPE;
-            if (nk > NIMBLE_MAX_CONTACTS) st |= ST_CONTACT_OVERFLOW;
+            if (nk > md.maxContacts) st |= ST_CONTACT_OVERFLOW;
             if (nd > CT_MAX_DROPPED) st |= ST_DROPPED_OVERFLOW;
-            ct[H_NCON] = nk < NIMBLE_MAX_CONTACTS ? nk : NIMBLE_MAX_CONTACTS;
+            ct[H_NCON] = nk < md.maxContacts ? nk : md.maxContacts;
             ct[H_NDROP] = nd < CT_MAX_DROPPED ? nd : CT_MAX_DROPPED;
             ct[H_STATUS] = st;
           }
@@ -672,7 +712,7 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
                             (md.reactive[ba] || md.reactive[bb]);
           double* dst = nullptr;
           if (keep) {
-            if (nk < NIMBLE_MAX_CONTACTS) {
+            if (nk < md.maxContacts) {
               if (((int)rec[7] & 15) == CT_EDGE_EDGE || ((int)rec[7] & 15) >= CT_SPHERE_SPHERE)
                 for (int i = 0; i < EDGE_REC; i++) snapEdge[nk * EDGE_REC + i] = rec[CREC + i];
               dst = ct + CT_CONTACTS + (nk++) * CREC;
@@ -1082,6 +1122,21 @@ __device__ __forceinline__ void contactStage(const ModelDev& md, double* s, cons
     fr = fmin(md.friction[(int)rec[8]], md.friction[(int)rec[9]]) > 1e-3;
   }
   const int m = nCon + 2 * __popcll(__ballot(fr));
+  if (m > NIMBLE_MAX_SOLVED_LCP) {
+    // more rows than one wave's lanes: the contacts are recorded, the solve
+    // is not taken (flagged; the snapshot says no rows, so the backward and
+    // the Jacobians see a contact-free step)
+    for (int t = lane; t < nCon * CREC; t += WAVE) snap[SN_CONTACTS + t] = ct[CT_CONTACTS + t];
+    if (lane == 0) {
+      for (int i = 0; i < 16; i++) snap[i] = 0.0;
+      snap[SN_NCON] = nCon;
+      snap[SN_STATUS] = (double)((int)ct[H_STATUS] | ST_LCP_TOO_LARGE);
+      ct[H_M] = 0;
+      cache[0] = -1.0;
+    }
+    WSYNC();
+    return;
+  }
   if (lane == 0) ct[H_M] = m;  // read by the helper wave
   // the LCP workspace is in LDS when it fits the pool (the common case, LDS
   // instructions throughout), else in the world's HBM snapshot tail

@@ -58,6 +58,15 @@ struct ModelDev {
   int shapeBody[NS_MAX], shapeType[NS_MAX];
   double shapeSize[NS_MAX][3];
   double shapeT[NS_MAX][12];
+  // mesh shapes: their candidate vertices (mesh frame, unscaled; device
+  // buffer), first / count per shape, and the bounding radius of the scaled
+  // vertices about the mesh origin (pair culling)
+  const double* meshVerts;
+  int meshFirst[NS_MAX], meshCount[NS_MAX];
+  double meshRadius[NS_MAX];
+  int hasMesh;
+  // kept-contact capacity of the contact stage (<= NIMBLE_MAX_CONTACTS)
+  int maxContacts;
   // candidate pairs (i < j) after BodyNodeCollisionFilter, in detector order
   int numPairs, pairChunk;
   int pairA[NS_MAX * (NS_MAX - 1) / 2], pairB[NS_MAX * (NS_MAX - 1) / 2];

@@ -16,19 +16,24 @@
 #define EDGE_REC 12
 #define PBREC (CREC + EDGE_REC)
 
-// contact-stage LDS region (Layout::ct)
+// contact-stage LDS region (Layout::ct): header, then the kept contacts
+// (the model's contact capacity, ModelDev::maxContacts <= NIMBLE_MAX_CONTACTS)
 #define CT_CONTACTS 32
-#define CT_DROPPED (CT_CONTACTS + NIMBLE_MAX_CONTACTS * CREC)
 #define CT_MAX_DROPPED 8
-#define CT_PAIRBUF (CT_DROPPED + CT_MAX_DROPPED * CREC)
 #define CT_PAIR_CHUNK 16
 #define CT_PAIR_CHUNK_HOST CT_PAIR_CHUNK
+// contact records one mesh pair may produce, and its LDS scratch (mesh.cuh)
+#define MESH_PAIR_RECS 64
+#define MESH_PAIR_SCRATCH (16 * 64)
 // the forward's header + kept contacts live in Layout::ct; the dropped list
-// and the per-pair narrow-phase buffers live at the start of the alias area
-// (dead dynamics buffers, Layout::V)
-__host__ __device__ inline int ctDoubles() { return CT_DROPPED; }
-__host__ __device__ inline int collideScratchDoubles(int pairChunk) {
-  return CT_MAX_DROPPED * CREC + pairChunk * 8 * PBREC;
+// and the per-pair narrow-phase buffers (a mesh pair's records and scratch)
+// live at the start of the alias area past the dynamics buffers
+__host__ __device__ inline int ctDoubles(int maxContacts) { return CT_CONTACTS + maxContacts * CREC; }
+__host__ __device__ inline int pairBufRecs(int pairChunk, bool mesh) {
+  return mesh ? (MESH_PAIR_RECS > 8 * pairChunk ? MESH_PAIR_RECS : 8 * pairChunk) : 8 * pairChunk;
+}
+__host__ __device__ inline int collideScratchDoubles(int pairChunk, bool mesh) {
+  return CT_MAX_DROPPED * CREC + pairBufRecs(pairChunk, mesh) * PBREC + (mesh ? MESH_PAIR_SCRATCH : 0);
 }
 
 // snapshot layout

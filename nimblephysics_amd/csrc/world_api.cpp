@@ -187,6 +187,9 @@ const nimble_world_desc& World::describe() {
   for (auto& v : mF64) v.clear();
   std::vector<int32_t>& shapeType = mShapeTypes;
   shapeType.clear();
+  mMeshFirst.clear();
+  mMeshCount.clear();
+  mMeshVertices.clear();
   int bodyBase = 0, dofBase = 0, nb = 0;
   for (std::size_t si = 0; si < mSkels.size(); si++) {
     const auto& s = *mSkels[si];
@@ -221,6 +224,10 @@ const nimble_world_desc& World::describe() {
         const Vector3s& sz = node->mShape->size();
         mF64[SSHAPE].insert(mF64[SSHAPE].end(), sz.begin(), sz.end());
         mF64[ST].insert(mF64[ST].end(), node->mT.m, node->mT.m + 12);
+        const auto* mesh = dynamic_cast<const dynamics::MeshShape*>(node->mShape.get());
+        mMeshFirst.push_back(mesh ? (int32_t)(mMeshVertices.size() / 3) : 0);
+        mMeshCount.push_back(mesh ? (int32_t)(mesh->getVertices().size() / 3) : 0);
+        if (mesh) mMeshVertices.insert(mMeshVertices.end(), mesh->getVertices().begin(), mesh->getVertices().end());
       }
       nb++;
     }
@@ -265,6 +272,12 @@ const nimble_world_desc& World::describe() {
   mDesc.shape_type = mShapeTypes.data();
   mDesc.shape_size = mF64[SSHAPE].data();
   mDesc.shape_T = mF64[ST].data();
+  // mesh vertices; no candidate mask (the device scans every vertex)
+  mDesc.num_mesh_vertices = (int32_t)(mMeshVertices.size() / 3);
+  mDesc.mesh_vertices = mMeshVertices.data();
+  mDesc.shape_mesh_first = mMeshFirst.data();
+  mDesc.shape_mesh_count = mMeshCount.data();
+  mDesc.mesh_vertex_candidate = nullptr;
   return mDesc;
 }
 

@@ -30,6 +30,7 @@ JOINT_FREE = 3
 SHAPE_BOX = 0
 SHAPE_SPHERE = 1
 SHAPE_CAPSULE = 2
+SHAPE_MESH = 3
 
 
 def _model_changed(skel: Optional["Skeleton"]) -> None:
@@ -117,6 +118,32 @@ class CapsuleShape(Shape):
 
     def getHeight(self):
         return float(self.size[1])
+
+
+class MeshShape(Shape):
+    """dart/dynamics/MeshShape.hpp: a triangle mesh collided as the convex
+    hull of its vertex list (DARTCollide.cpp:1935).  ``vertices`` [N, 3] are
+    the aiMesh vertices in order (see mesh.py), ``scale`` the per-axis scale
+    (Shape size)."""
+
+    def __init__(self, scale, vertices, path: str = ""):
+        super().__init__(SHAPE_MESH, scale)
+        self.vertices = np.ascontiguousarray(np.asarray(vertices, dtype=np.float64).reshape(-1, 3))
+        self.path = path
+        self._candidate = None
+
+    def getScale(self):
+        return self.size.copy()
+
+    def getMeshPath(self):
+        return self.path
+
+    def candidate(self):
+        """Per-vertex mask of possible support / witness points (mesh.py)."""
+        if self._candidate is None:
+            from .mesh import candidate_mask
+            self._candidate = candidate_mask(self.vertices, self.size)
+        return self._candidate
 
 
 class ShapeNode:

@@ -305,6 +305,24 @@ class World:
             "shape_size": np.array([s[1].shape.size for s in shapes]).reshape(-1),
             "shape_T": np.array([t12(s[1].T) for s in shapes]).reshape(-1),
         }
+        # mesh colliders: vertex lists concatenated in shape order
+        first, count, verts, cand = [], [], [], []
+        nv = 0
+        for _, node in shapes:
+            sh = node.shape
+            if sh.kind == dyn.SHAPE_MESH:
+                first.append(nv)
+                count.append(sh.vertices.shape[0])
+                verts.append(sh.vertices)
+                cand.append(sh.candidate())
+                nv += sh.vertices.shape[0]
+            else:
+                first.append(0)
+                count.append(0)
+        out["shape_mesh_first"] = np.array(first, np.int32)
+        out["shape_mesh_count"] = np.array(count, np.int32)
+        out["mesh_vertices"] = np.concatenate(verts).reshape(-1) if verts else np.zeros(0)
+        out["mesh_vertex_candidate"] = np.concatenate(cand).astype(np.int32) if cand else np.zeros(0, np.int32)
         for k, v in per_dof.items():
             out[k] = np.array(v, dtype=np.float64)
         return out

@@ -6,9 +6,9 @@ createSkeletonRecursive, createDartJoint :380-520, createDartNodeProperties
 iterates joints in std::map (name-sorted) order -- so a link's children, and
 therefore DART's depth-first BodyNode / DOF order, are sorted by joint name.
 
-Supported collision geometry: box and sphere (the shapes the hot path's
-collision kernel handles).  Visual geometry is ignored.  Meshes used as
-collision geometry raise, unless ``ignore_mesh_collisions=True``.
+Supported collision geometry: box, sphere and STL meshes (MeshShape, read by
+mesh.read_stl).  Visual geometry is ignored.  ``ignore_mesh_collisions=True``
+drops mesh colliders.
 """
 from __future__ import annotations
 
@@ -74,7 +74,7 @@ def load_urdf(path: str, ignore_mesh_collisions: bool = False) -> dyn.Skeleton:
     def make_body(link: _Link, joint_kind: int, joint_name: str, parent_body):
         j, b = skel._create(joint_kind, parent_body, joint_name, link.name)
         _node_properties(link, b)
-        _shapes(link, b, ignore_mesh_collisions)
+        _shapes(link, b, ignore_mesh_collisions, os.path.dirname(os.path.abspath(path)))
         return j, b
 
     def recurse(link: _Link, parent_body):
@@ -153,16 +153,29 @@ def _node_properties(link: _Link, body: dyn.BodyNode):
     body.setMomentOfInertia(J[0, 0], J[1, 1], J[2, 2], J[0, 1], J[0, 2], J[1, 2])
 
 
-def _shapes(link: _Link, body: dyn.BodyNode, ignore_mesh: bool):
+def _shapes(link: _Link, body: dyn.BodyNode, ignore_mesh: bool, base_dir: str = "."):
     for c in link.e.findall("collision"):
         geo = c.find("geometry")
         shape = None
         box = geo.find("box")
         sph = geo.find("sphere")
+        msh = geo.find("mesh")
         if box is not None:
             shape = dyn.BoxShape(_vec(box.get("size")))
         elif sph is not None:
             shape = dyn.SphereShape(float(sph.get("radius")))
+        elif msh is not None and not ignore_mesh:
+            # DartLoader::createShape (DartLoader.cpp): a MeshShape of the
+            # file (resolved against the URDF's directory) with its scale
+            from .mesh import read_stl, unique_in_order
+            fn = msh.get("filename")
+            for pre in ("package://", "file://"):
+                if fn.startswith(pre):
+                    fn = fn[len(pre):]
+            path = fn if os.path.isabs(fn) else os.path.join(base_dir, fn)
+            if not path.lower().endswith(".stl"):
+                raise NotImplementedError(f"mesh collision geometry {fn}: only STL files are read")
+            shape = dyn.MeshShape(_vec(msh.get("scale"), (1.0, 1.0, 1.0)), unique_in_order(read_stl(path)), fn)
         else:
             if ignore_mesh:
                 continue

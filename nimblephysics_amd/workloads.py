@@ -131,3 +131,16 @@ def atlas_states(world, batch, seed):
 def cheetah_states(world, batch, seed):
     """The half-cheetah bench sampler."""
     return half_cheetah_states(world, batch, seed=seed)
+
+
+def atlas_mesh_world(with_ground=True):
+    """The reference atlas_bench's own Atlas (python/nimblephysics_benchmarks/
+    atlas_bench.py:18-19: atlas_v3_no_head.urdf, 29 STL mesh colliders) on the
+    ground box, set up as atlas_world."""
+    w = World()
+    w.setGravity([0, -9.81, 0])
+    atlas = w.addSkeleton(assets.load_skeleton("atlas_mesh"))
+    atlas.setPosition(0, -0.5 * 3.14159)
+    if with_ground:
+        w.addSkeleton(assets.load_skeleton("atlas_ground"))
+    return w

@@ -97,6 +97,10 @@ World::World(const nimble_world_desc* d) {
       for (int c = 0; c < 3; c++) S.T.R(r, c) = d->shape_T[12 * s + r * 4 + c];
       S.T.p[r] = d->shape_T[12 * s + r * 4 + 3];
     }
+    if (S.type == NIMBLE_SHAPE_MESH && d->mesh_vertices != nullptr) {
+      const int f = d->shape_mesh_first[s], c = d->shape_mesh_count[s];
+      S.verts.assign(d->mesh_vertices + 3 * (size_t)f, d->mesh_vertices + 3 * (size_t)(f + c));
+    }
   }
   // dof -> body map
   dofBody.assign(n, -1);

@@ -20,6 +20,9 @@ struct Shape {
   int body, type;
   double size[3];
   Iso<double> T;
+  // NIMBLE_SHAPE_MESH: the aiMesh vertex list (float values as the reference
+  // reads them), mesh frame, unscaled (size = scale)
+  std::vector<double> verts;  // [count][3]
 };
 
 struct World;
@@ -142,6 +145,11 @@ void collide(const World& w, const Kin<double>& k, std::vector<Contact>& out, in
 int capsuleBox(const Iso<double>& Tb, const double* size, const Iso<double>& Tc, double r, double h, bool boxFirst,
                double clip, int shape1, int shape2, int body1, int body2, std::vector<Contact>& out,
                int* unsupported);
+
+// mesh (vertices, scale, transform Tm) vs box (size, Tb): collideMeshBox
+// (DARTCollide.cpp:3935) when meshFirst, else collideBoxMesh (:3983)
+int meshBox(const Iso<double>& Tm, const Shape& mesh, const Iso<double>& Tb, const double* size, bool meshFirst,
+            double clip, int shape1, int shape2, int body1, int body2, std::vector<Contact>& out, int* unsupported);
 
 // standalone sphere shapes: collideSphereBox (DARTCollide.cpp:1655) /
 // collideBoxSphere (:1482, halfspace BOTH) and collideSphereSphere (:1812)

@@ -15,7 +15,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "liboracle.so")
 REF_LIB = os.path.join(HERE, "_ref", "libodelcp.so")
-MAX_LCP = 48
+MAX_LCP = 96  # include/nimble_amd.h NIMBLE_MAX_LCP (the LCP cache layout)
 
 _lib = None
 _ref = None
@@ -40,6 +40,7 @@ def lib():
         L.oracle_snapshots_destroy.argtypes = [vp]
         L.oracle_forward.argtypes = [vp, ip, dp, dp, dp, dp, vp]
         L.oracle_forward_forced.argtypes = [vp, ip, dp, dp, dp, dp, vp, dp, dp]
+        L.oracle_detect.argtypes = [vp, ip, dp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.oracle_backward.argtypes = [vp, ip, vp, dp, dp, dp]
         L.oracle_jacobians.argtypes = [vp, ip, vp, dp, dp]
         L.oracle_constraint_force_jacobians.argtypes = [vp, ip, vp, dp, ip]
@@ -161,6 +162,16 @@ class OracleWorld:
                                           _p(fx), _p(fl))
         return nxt, int(bad)
 
+    def detect(self, state):
+        """Contacts per world after the constraint filter (no step, no
+        contact-count limit) and the unsupported-branch flags."""
+        state = np.ascontiguousarray(np.atleast_2d(state), dtype=np.float64)
+        B = state.shape[0]
+        counts = np.zeros(B, dtype=np.int32)
+        uns = np.zeros(B, dtype=np.int32)
+        lib().oracle_detect(self.h, B, _p(state), _pi(counts), _pi(uns))
+        return counts, uns
+
     def backward(self, grad_next):
         g = np.ascontiguousarray(np.atleast_2d(grad_next), dtype=np.float64)
         B = g.shape[0]
@@ -178,7 +189,7 @@ class OracleWorld:
         lib().oracle_jacobians(self.h, B, self.snaps, _p(J), _p(F))
         return J, F
 
-    def constraint_force_jacobians(self, max_rows=48):
+    def constraint_force_jacobians(self, max_rows=MAX_LCP):
         """getJacobianOfConstraintForce of the last forward: [B, max_rows, 3n],
         row r = d f_c[r] / d(q, v, tau) (BackpropSnapshot.cpp:2723), zero past
         the world's clamping count."""
@@ -232,7 +243,7 @@ def contacts(ow: "OracleWorld", b=0, maxc=64):
     return out[:k]
 
 
-def lcp_debug(ow: "OracleWorld", b=0, max_rows=64):
+def lcp_debug(ow: "OracleWorld", b=0, max_rows=MAX_LCP):
     mapping = np.zeros(max_rows, dtype=np.int32)
     x = np.zeros(max_rows)
     m = lib().oracle_lcp_debug(ow.snaps, b, _pi(mapping), _p(x), max_rows)
@@ -246,7 +257,7 @@ def lcp_flags(ow: "OracleWorld", b=0):
     return out
 
 
-def lcp_fc(ow: "OracleWorld", b=0, maxc=64):
+def lcp_fc(ow: "OracleWorld", b=0, maxc=MAX_LCP):
     fc = np.zeros(maxc)
     k = lib().oracle_lcp_fc(ow.snaps, b, _p(fc), maxc)
     return fc[:k].copy()
@@ -254,12 +265,12 @@ def lcp_fc(ow: "OracleWorld", b=0, maxc=64):
 
 def lcp_cols(ow: "OracleWorld", b=0):
     """J^T columns (n x m) of world b's LCP rows."""
-    out = np.zeros(ow.n * 64)
+    out = np.zeros(ow.n * MAX_LCP)
     m = lib().oracle_lcp_cols(ow.snaps, b, _p(out), out.size)
     return out[:ow.n * m].reshape(ow.n, m).copy()
 
 
-def lcp_problem(ow: "OracleWorld", b=0, max_rows=64):
+def lcp_problem(ow: "OracleWorld", b=0, max_rows=MAX_LCP):
     """(A, b, lo, hi, findex) of world b's LCP (A without the fallback CFM)."""
     A = np.zeros(max_rows * max_rows)
     bb, lo, hi = np.zeros(max_rows), np.zeros(max_rows), np.zeros(max_rows)
@@ -328,6 +339,32 @@ def capsule_box(size, T_box, height, radius, T_capsule, box_first=True, clip=0.0
     if k < 0:
         k = -1 - k
     return out[:k], unsupported
+
+
+def mesh_box(verts, scale, T_mesh, size, T_box, mesh_first=True, clip=0.03):
+    """collideMeshBox (mesh_first) / collideBoxMesh restated; rows of
+    (point3, normal3, depth, type, edgeAFixed3, edgeADir3, edgeBFixed3,
+    edgeBDir3) and an `unsupported` flag (empty witness set)."""
+    v = np.ascontiguousarray(np.asarray(verts, dtype=np.float64).reshape(-1, 3))
+    out = np.zeros((256, 20))
+    sc, sz = (np.ascontiguousarray(x, dtype=np.float64) for x in (scale, size))
+    tm, tb = (np.ascontiguousarray(np.asarray(T, dtype=np.float64)[:3, :4]) for T in (T_mesh, T_box))
+    k = lib().oracle_mesh_box(_p(v), v.shape[0], _p(sc), _p(tm), _p(sz), _p(tb), 1 if mesh_first else 0,
+                              C.c_double(clip), _p(out))
+    unsupported = k < 0
+    if k < 0:
+        k = -1 - k
+    return out[:k], unsupported
+
+
+def box_box_as_mesh(size1, T1, size2, T2):
+    """collideBoxBoxAsMesh (DARTCollide.cpp:3889) restated; rows as mesh_box."""
+    out = np.zeros((64, 20))
+    s1, s2 = (np.ascontiguousarray(s, dtype=np.float64) for s in (size1, size2))
+    t1, t2 = (np.ascontiguousarray(np.asarray(T, dtype=np.float64)[:3, :4]) for T in (T1, T2))
+    k = lib().oracle_box_box_as_mesh(_p(s1), _p(t1), _p(s2), _p(t2), _p(out))
+    assert k >= 0, "empty witness set"
+    return out[:k]
 
 
 SHAPE_TYPES = {"box": 0, "sphere": 1, "capsule": 2}

@@ -74,6 +74,30 @@ int oracle_forward_forced(void* wp, int batch, const double* state, const double
   return mismatched;
 }
 
+// Collision detection only (kinematics + collide + the constraint filter's
+// depth / normal tests): contact count per world, no LCP, no size limit.
+// unsupported[b] = 1 when a narrow-phase branch not restated was hit.
+void oracle_detect(void* wp, int batch, const double* state, int* counts, int* unsupported) {
+  World& w = *static_cast<World*>(wp);
+  const int n = w.n;
+  for (int b = 0; b < batch; b++) {
+    const double* q = state + (size_t)b * 2 * n;
+    Kin<double> k;
+    k.compute(w, q, q + n);
+    std::vector<Contact> cs;
+    int unsup = 0;
+    collide(w, k, cs, &unsup);
+    int kept = 0;
+    for (const Contact& c : cs) {
+      if (c.normal[0] * c.normal[0] + c.normal[1] * c.normal[1] + c.normal[2] * c.normal[2] < 1e-12) continue;
+      if (c.depth < 0.0 || c.depth > w.clipDepth) continue;
+      kept++;
+    }
+    counts[b] = kept;
+    if (unsupported) unsupported[b] = unsup;
+  }
+}
+
 int oracle_backward(void* wp, int batch, void* snaps, const double* gradNext, double* gradState, double* gradTau) {
   World& w = *static_cast<World*>(wp);
   auto& S = *static_cast<std::vector<OracleSnap>*>(snaps);

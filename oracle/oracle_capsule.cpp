@@ -30,6 +30,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <limits>
 #include <vector>
 
@@ -85,15 +86,38 @@ inline V xf(const Xf& T, const V& v) { return rot(T, v) + T.p; }
 inline V xfInv(const Xf& T, const V& v) { return rotT(T, v) - rotT(T, T.p); }
 inline V col(const Xf& T, int c) { return mk(T.R[c], T.R[3 + c], T.R[6 + c]); }
 
-// ccd objects: box (size) or capsule (radius, height)
+// ccd objects: box (size), capsule (radius, height) or mesh (vertex list,
+// scale in size)
 struct Obj {
   bool capsule;
   Xf T;
   double size[3];
   double r, h;
+  const std::vector<double>* mesh = nullptr;
 };
 
+// ccdSupportMesh (DARTCollide.cpp:1935): the first vertex of largest
+// v . (R^T dir / scale), scaled and transformed
+V meshSupport(const Obj& o, const V& dir) {
+  V ld = rotT(o.T, dir);
+  ld.x[0] /= o.size[0];
+  ld.x[1] /= o.size[1];
+  ld.x[2] /= o.size[2];
+  double maxDot = -std::numeric_limits<double>::infinity();
+  V best = mk(0, 0, 0);
+  const std::vector<double>& v = *o.mesh;
+  for (size_t k = 0; k + 2 < v.size(); k += 3) {
+    const double d = v[k] * ld.x[0] + v[k + 1] * ld.x[1] + v[k + 2] * ld.x[2];
+    if (d > maxDot) { maxDot = d; best = mk(v[k], v[k + 1], v[k + 2]); }
+  }
+  best.x[0] *= o.size[0];
+  best.x[1] *= o.size[1];
+  best.x[2] *= o.size[2];
+  return xf(o.T, best);
+}
+
 void support(const Obj& o, const V& dir, V& out) {
+  if (o.mesh) { out = meshSupport(o, dir); return; }
   V ld = rotT(o.T, dir);
   if (!o.capsule) {  // ccdSupportBox (DARTCollide.cpp:1885)
     V c = mk(ccdSign(ld.x[0]) * o.size[0] * 0.5, ccdSign(ld.x[1]) * o.size[1] * 0.5, ccdSign(ld.x[2]) * o.size[2] * 0.5);
@@ -667,7 +691,169 @@ void faceFaceVertices(const V& dir, const std::vector<V>& A, const std::vector<V
   *edgeEdge = ee;
 }
 
+// ccdPointsAtWitnessMesh (DARTCollide.cpp:2119): the vertices within the
+// witness plane depth of the extreme one along dir (the least when neg),
+// scaled and transformed, dropping any within 1e-3 m of one already taken
+std::vector<V> witnessMesh(const Obj& o, const V& dir, bool neg) {
+  const double kPlane = 0.01;  // DART_COLLISION_WITNESS_PLANE_DEPTH
+  V ld = rotT(o.T, dir);
+  ld.x[0] /= o.size[0];
+  ld.x[1] /= o.size[1];
+  ld.x[2] /= o.size[2];
+  const std::vector<double>& v = *o.mesh;
+  auto dotOf = [&](size_t k) {
+    return v[k] * ld.x[0] * o.size[0] * o.size[0] + v[k + 1] * ld.x[1] * o.size[1] * o.size[1] +
+           v[k + 2] * ld.x[2] * o.size[2] * o.size[2];
+  };
+  double maxDot = (neg ? 1.0 : -1.0) * std::numeric_limits<double>::infinity();
+  for (size_t k = 0; k + 2 < v.size(); k += 3) {
+    const double d = dotOf(k);
+    if ((d > maxDot && !neg) || (d < maxDot && neg)) maxDot = d;
+  }
+  std::vector<V> pts;
+  for (size_t k = 0; k + 2 < v.size(); k += 3) {
+    const double d = dotOf(k);
+    if (std::fabs(d - maxDot) < kPlane) {
+      const V p = xf(o.T, mk(v[k] * o.size[0], v[k + 1] * o.size[1], v[k + 2] * o.size[2]));
+      bool dup = false;
+      for (const V& q : pts)
+        if (len2(q - p) < 1e-6) { dup = true; break; }
+      if (!dup) pts.push_back(p);
+    }
+  }
+  return pts;
+}
+
+// createMeshMeshContacts (DARTCollide.cpp:2508) on the witness sets A (object
+// 1) and B (object 2); contacts in the reference's order.  Returns false for
+// an empty witness set (the reference asserts).
+bool meshMeshContacts(const V& dir, const std::vector<V>& A, const std::vector<V>& B, std::vector<Contact>& outc) {
+  auto setV = [](double* o, const V& x) { for (int i = 0; i < 3; i++) o[i] = x.x[i]; };
+  auto dirDot = [&](const V& n) { return n.x[0] * dir.x[0] + n.x[1] * dir.x[1] + n.x[2] * dir.x[2]; };
+  if (A.empty() || B.empty()) return false;
+  const size_t na = A.size(), nb = B.size();
+  if (std::getenv("ORACLE_MESH_DEBUG")) std::fprintf(stderr, "mmc na=%zu nb=%zu dir=%.6f %.6f %.6f\n", na, nb, dir.x[0], dir.x[1], dir.x[2]);
+  if ((na == 1 && nb > 2) || (na > 2 && nb == 1)) {
+    // single vertex-face (:2551) / face-vertex (:2586)
+    const bool vf = na == 1;
+    const std::vector<V>& F = vf ? B : A;
+    V normal = eigNormalized(cross(F[0] - F[1], F[1] - F[2]));
+    if (dirDot(normal) > 0) normal = normal * -1.0;
+    Contact c{};
+    setV(c.point, vf ? A[0] : B[0]);
+    setV(c.normal, normal);
+    const double distA = dot(vf ? A[0] : A[0], normal), distB = dot(vf ? B[0] : B[0], normal);
+    c.depth = std::fabs(distA - distB);
+    c.type = vf ? 2 /*CT_VERTEX_FACE*/ : 1 /*CT_FACE_VERTEX*/;
+    outc.push_back(c);
+    return true;
+  }
+  if (na == 2 && nb == 2) {
+    // single edge-edge (:2621), dLineClosestApproach (:270)
+    const V ua = eigNormalized(A[0] - A[1]), ub = eigNormalized(B[0] - B[1]);
+    V pa = A[0], pb = B[0];
+    const V pp = pb - pa;
+    const double uaub = dot(ua, ub), q1 = dot(ua, pp), q2 = -dot(ub, pp);
+    double d = 1 - uaub * uaub, alpha = 0, beta = 0;
+    if (d > 0) {
+      d = 1.0 / d;
+      alpha = (q1 + uaub * q2) * d;
+      beta = (uaub * q1 + q2) * d;
+    }
+    for (int i = 0; i < 3; i++) pa.x[i] += ua.x[i] * alpha;
+    for (int i = 0; i < 3; i++) pb.x[i] += ub.x[i] * beta;
+    V normal = cross(ua, ub);
+    if (dirDot(normal) > 0) normal = normal * -1.0;
+    Contact c{};
+    setV(c.point, mk(0.5 * (pa.x[0] + pb.x[0]), 0.5 * (pa.x[1] + pb.x[1]), 0.5 * (pa.x[2] + pb.x[2])));
+    c.type = 3;  // CT_EDGE_EDGE
+    setV(c.edgeAFixed, A[0]); setV(c.edgeADir, ua);
+    setV(c.edgeBFixed, B[0]); setV(c.edgeBDir, ub);
+    setV(c.normal, normal);
+    c.depth = std::fabs(dot(pb, normal) - dot(pa, normal));
+    outc.push_back(c);
+    return true;
+  }
+  if ((na == 1 && nb == 2) || (na == 2 && nb == 1)) {
+    // vertex-edge (:2702) / edge-vertex (:2736): the normal is dir made
+    // orthogonal to the edge -- the edge-vertex branch reads
+    // (pointsAWitness[1] - pointsAWitness[1]).normalized() (sic): a zero
+    // vector (Eigen leaves it zero), so the normal stays dir
+    const bool ve = na == 1;
+    V normal = dir;
+    if (ve) {
+      const V edgeB = eigNormalized(B[0] - B[1]);
+      normal = normal - edgeB * dot(normal, edgeB);
+    }
+    if (dirDot(normal) > 0) normal = normal * -1.0;
+    Contact c{};
+    setV(c.point, ve ? A[0] : B[0]);
+    setV(c.normal, normal);
+    c.depth = std::fabs(dot(A[0], normal) - dot(B[0], normal));
+    c.type = ve ? 2 /*CT_VERTEX_FACE*/ : 1 /*CT_FACE_VERTEX*/;
+    outc.push_back(c);
+    return true;
+  }
+  if (na == 1 && nb == 1) {
+    // vertex-vertex (:2771): FACE_VERTEX at B's point, normal -dir
+    const V normal = dir * -1.0;
+    Contact c{};
+    setV(c.point, B[0]);
+    setV(c.normal, normal);
+    c.depth = std::fabs(dot(B[0], normal) - dot(A[0], normal));
+    c.type = 1;  // CT_FACE_VERTEX
+    outc.push_back(c);
+    return true;
+  }
+  // edge-face (:2672), face-edge (:2686) and face-face (:2804):
+  // createFaceFaceContacts with PinToFace::AVERAGE
+  std::vector<FFContact> fc;
+  int ee = 0;
+  faceFaceVertices(dir, A, B, 0, fc, &ee);
+  for (const FFContact& f : fc) {
+    Contact c{};
+    setV(c.point, f.point);
+    setV(c.normal, f.normal);
+    c.depth = f.depth;
+    if (f.type == 3) {
+      c.type = 3;  // CT_EDGE_EDGE
+      setV(c.edgeAFixed, f.aFixed); setV(c.edgeADir, f.aDir);
+      setV(c.edgeBFixed, f.bFixed); setV(c.edgeBDir, f.bDir);
+    } else {
+      c.type = f.type == 1 ? 2 /*CT_VERTEX_FACE*/ : 1 /*CT_FACE_VERTEX*/;
+    }
+    outc.push_back(c);
+  }
+  return true;
+}
+
 }  // namespace
+
+int meshBox(const Iso<double>& Tm, const Shape& mesh, const Iso<double>& Tb, const double* size, bool meshFirst,
+            double clip, int shape1, int shape2, int body1, int body2, std::vector<Contact>& out, int* unsupported) {
+  Obj box{}, msh{};
+  box.capsule = msh.capsule = false;
+  for (int i = 0; i < 9; i++) { box.T.R[i] = Tb.R.m[i]; msh.T.R[i] = Tm.R.m[i]; }
+  for (int i = 0; i < 3; i++) {
+    box.T.p.x[i] = Tb.p[i]; msh.T.p.x[i] = Tm.p[i];
+    box.size[i] = size[i]; msh.size[i] = mesh.size[i];
+  }
+  msh.mesh = &mesh.verts;
+  double depth;
+  V dir, pos;
+  const int intersect = meshFirst ? mprPenetration(msh, box, depth, dir, pos) : mprPenetration(box, msh, depth, dir, pos);
+  if (intersect != 0) return 0;
+  if (depth > clip) return 0;
+  const std::vector<V> A = meshFirst ? witnessMesh(msh, dir, false) : witnessBox(box, dir, false);
+  const std::vector<V> B = meshFirst ? witnessBox(box, dir, true) : witnessMesh(msh, dir, true);
+  std::vector<Contact> cs;
+  if (!meshMeshContacts(dir, A, B, cs)) { *unsupported = 1; return 0; }
+  for (Contact& c : cs) {
+    c.shapeA = shape1; c.shapeB = shape2; c.bodyA = body1; c.bodyB = body2;
+    out.push_back(c);
+  }
+  return (int)cs.size();
+}
 
 // Capsule (radius r, height h along local z, transform Tc) vs box (size, Tb);
 // boxFirst selects collideBoxCapsule (box is collision object 1) over
@@ -884,4 +1070,71 @@ extern "C" int oracle_capsule_box(const double* size, const double* Tbox, double
     out[8 * k + 7] = cs[k].type;
   }
   return unsup ? -1 - (int)cs.size() : (int)cs.size();
+}
+
+// Raw mesh-box entry (collideMeshBox / collideBoxMesh with the mesh's vertex
+// list, scale and 3x4 transform; box full size + transform).  Output per
+// contact: point3, normal3, depth, type (this oracle's CT numbering), edge A
+// fixed3 / dir3, edge B fixed3 / dir3 (20 doubles).  Returns the count, or
+// -1 - count when the witness sets were empty.
+extern "C" int oracle_mesh_box(const double* verts, int nverts, const double* scale, const double* Tmesh,
+                               const double* size, const double* Tbox, int meshFirst, double clip, double* out) {
+  oracle::Iso<double> Tm, Tb;
+  for (int r = 0; r < 3; r++) {
+    for (int c = 0; c < 3; c++) { Tm.R(r, c) = Tmesh[r * 4 + c]; Tb.R(r, c) = Tbox[r * 4 + c]; }
+    Tm.p[r] = Tmesh[r * 4 + 3];
+    Tb.p[r] = Tbox[r * 4 + 3];
+  }
+  oracle::Shape m{};
+  m.type = NIMBLE_SHAPE_MESH;
+  for (int i = 0; i < 3; i++) m.size[i] = scale[i];
+  m.verts.assign(verts, verts + 3 * nverts);
+  std::vector<oracle::Contact> cs;
+  int unsup = 0;
+  oracle::meshBox(Tm, m, Tb, size, meshFirst != 0, clip, 0, 1, 0, 1, cs, &unsup);
+  for (size_t k = 0; k < cs.size(); k++) {
+    double* o = out + 20 * k;
+    for (int i = 0; i < 3; i++) {
+      o[i] = cs[k].point[i]; o[3 + i] = cs[k].normal[i];
+      o[8 + i] = cs[k].edgeAFixed[i]; o[11 + i] = cs[k].edgeADir[i];
+      o[14 + i] = cs[k].edgeBFixed[i]; o[17 + i] = cs[k].edgeBDir[i];
+    }
+    o[6] = cs[k].depth;
+    o[7] = cs[k].type;
+  }
+  return unsup ? -1 - (int)cs.size() : (int)cs.size();
+}
+
+// collideBoxBoxAsMesh (DARTCollide.cpp:3889): MPR with ccdSupportBox on both,
+// box witness sets, createMeshMeshContacts -- what the reference's
+// verifyBoxMeshResultsIdenticalToAnalytical (test_DARTCollide.cpp:146)
+// compares with dBoxBox.  Output rows as oracle_mesh_box.
+extern "C" int oracle_box_box_as_mesh(const double* size0, const double* T0, const double* size1, const double* T1,
+                                      double* out) {
+  using namespace oracle;
+  Obj a{}, b{};
+  a.capsule = b.capsule = false;
+  for (int r = 0; r < 3; r++) {
+    for (int c = 0; c < 3; c++) { a.T.R[r * 3 + c] = T0[r * 4 + c]; b.T.R[r * 3 + c] = T1[r * 4 + c]; }
+    a.T.p.x[r] = T0[r * 4 + 3];
+    b.T.p.x[r] = T1[r * 4 + 3];
+    a.size[r] = size0[r];
+    b.size[r] = size1[r];
+  }
+  double depth;
+  V dir, pos;
+  if (mprPenetration(a, b, depth, dir, pos) != 0) return 0;
+  std::vector<Contact> cs;
+  if (!meshMeshContacts(dir, witnessBox(a, dir, false), witnessBox(b, dir, true), cs)) return -1;
+  for (size_t k = 0; k < cs.size(); k++) {
+    double* o = out + 20 * k;
+    for (int i = 0; i < 3; i++) {
+      o[i] = cs[k].point[i]; o[3 + i] = cs[k].normal[i];
+      o[8 + i] = cs[k].edgeAFixed[i]; o[11 + i] = cs[k].edgeADir[i];
+      o[14 + i] = cs[k].edgeBFixed[i]; o[17 + i] = cs[k].edgeBDir[i];
+    }
+    o[6] = cs[k].depth;
+    o[7] = cs[k].type;
+  }
+  return (int)cs.size();
 }

@@ -558,6 +558,10 @@ void collide(const World& w, const Kin<double>& k, std::vector<Contact>& out, in
       } else if (S1.type == NIMBLE_SHAPE_CAPSULE && S2.type == NIMBLE_SHAPE_CAPSULE) {
         capsuleCapsule(T1, S1.size[0], S1.size[1], T2, S2.size[0], S2.size[1], w.clipDepth, i, j, S1.body, S2.body,
                        pair);
+      } else if (S1.type == NIMBLE_SHAPE_MESH && S2.type == NIMBLE_SHAPE_BOX) {
+        meshBox(T1, S1, T2, S2.size, true, w.clipDepth, i, j, S1.body, S2.body, pair, &unsup);
+      } else if (S1.type == NIMBLE_SHAPE_BOX && S2.type == NIMBLE_SHAPE_MESH) {
+        meshBox(T2, S2, T1, S1.size, false, w.clipDepth, i, j, S1.body, S2.body, pair, &unsup);
       } else {
         std::fprintf(stderr, "oracle: shape pair (%d,%d) not supported\n", S1.type, S2.type);
         std::abort();

@@ -85,10 +85,10 @@ static void printArr(const char* key, const double* v, std::size_t n, bool comma
   for (std::size_t i = 0; i < n; i++) std::printf("%s%.17g", i ? ", " : "", v[i]);
   std::printf("]%s", comma ? ", " : "");
 }
-static void printArrI(const char* key, const int32_t* v, std::size_t n) {
+static void printArrI(const char* key, const int32_t* v, std::size_t n, bool comma = true) {
   std::printf("\"%s\": [", key);
   for (std::size_t i = 0; i < n; i++) std::printf("%s%d", i ? ", " : "", v[i]);
-  std::printf("], ");
+  std::printf("]%s", comma ? ", " : "");
 }
 static void printVec(const char* key, const std::vector<double>& v, bool comma = true) {
   printArr(key, v.data(), v.size(), comma);
@@ -128,7 +128,12 @@ static void describe(simulation::World& w) {
   printArrI("shape_body", d.shape_body, ns);
   printArrI("shape_type", d.shape_type, ns);
   printArr("shape_size", d.shape_size, 3 * ns);
-  printArr("shape_T", d.shape_T, 12 * ns, false);
+  printArr("shape_T", d.shape_T, 12 * ns);
+  printArrI("shape_mesh_first", d.shape_mesh_first, ns);
+  printArrI("shape_mesh_count", d.shape_mesh_count, ns);
+  printArr("mesh_vertices", d.mesh_vertices, 3 * (std::size_t)d.num_mesh_vertices);
+  // no candidate mask from the C++ API (every vertex is scanned)
+  printArrI("mesh_vertex_candidate", d.mesh_vertex_candidate, 0, false);
   std::printf("}\n");
 }
 

@@ -1,0 +1,82 @@
+"""The reference atlas_bench's own Atlas (atlas_v3_no_head.urdf: 29 STL mesh
+colliders, python/nimblephysics_benchmarks/atlas_bench.py:18-19) on the GPU.
+
+* Contact sets bit-exact against the oracle for every world of the bench
+  sampler's batch (collideMeshBox / collideBoxMesh, DARTCollide.cpp:3935 /
+  :3983, through createMeshMeshContacts :2508): count, body pair and type
+  sequence, points / normals / depths at 1e-9;
+* worlds whose LCP fits the device's one-row-per-lane solve (<= 64 rows, 21
+  frictional contacts) step and differentiate like the oracle (LCP path,
+  next state, gradients at 1e-6 per element);
+* worlds with more rows are flagged NIMBLE_STATUS_LCP_TOO_LARGE (the
+  timestep layer raises on them) with their contacts still recorded.
+"""
+import numpy as np
+import pytest
+
+from nimblephysics_amd import _native, workloads
+from oracle import oracle as O
+from test_gpu_contact_parity import (CREC, RTOL, SN_CONTACTS, SN_M, SN_NCON, SN_STATUS, _device_backward, _device_step,
+                                     _lcp_ambiguous, _rel, _same_path)
+
+pytestmark = pytest.mark.gpu
+
+
+def _mesh_parity(B, seed, q_scale=0.02, v_scale=0.05):
+    world = workloads.atlas_mesh_world(True)
+    world.setStatusPolicy("record")
+    st, f = workloads.random_states(world, B, seed=seed, q_scale=q_scale, v_scale=v_scale)
+    ow = O.OracleWorld(world)
+    ref = ow.forward(st, f)
+    nxt, tsnap, cache, ts, tf = _device_step(world, st, f)
+    g = np.random.default_rng(seed).standard_normal(st.shape)
+    ggs, ggf = _device_backward(world, ts, tf, tsnap, g)
+    rgs, rgf = ow.backward(g)
+    snap = tsnap.cpu().numpy()
+    got = nxt.cpu().numpy()
+    solved = np.zeros(B, dtype=bool)
+    same = np.zeros(B, dtype=bool)
+    counts = np.zeros(B, dtype=int)
+    for b in range(B):
+        sn = snap[b]
+        rc = O.contacts(ow, b)
+        nc = int(sn[SN_NCON])
+        counts[b] = nc
+        assert nc == len(rc), (b, nc, len(rc))
+        gc = sn[SN_CONTACTS:SN_CONTACTS + CREC * nc].reshape(nc, CREC)
+        assert np.array_equal(gc[:, 7].astype(int) & 15, rc[:, 7].astype(int)), b
+        assert np.array_equal(gc[:, 8:10].astype(int), rc[:, 8:10].astype(int)), b
+        assert np.abs(gc[:, :7] - rc[:, :7]).max(initial=0) < 1e-9, b
+        m_ref = len(O.lcp_debug(ow, b, max_rows=O.MAX_LCP)[0])
+        status = int(sn[SN_STATUS])
+        too_large = (status & _native.ST_LCP_TOO_LARGE) != 0
+        assert too_large == (m_ref > _native.MAX_SOLVED_LCP), (b, m_ref, status)
+        if too_large:
+            continue
+        solved[b] = True
+        assert int(sn[SN_M]) == m_ref, b
+        if m_ref == 0 or _same_path(ow, sn, b):
+            same[b] = True
+        else:
+            assert _lcp_ambiguous(ow, b), f"world {b}: LCP path differs on a well-posed problem"
+    n = world.getNumDofs()
+    assert _rel(got[same][:, :n], ref[same][:, :n]) < RTOL
+    assert _rel(got[same][:, n:], ref[same][:, n:]) < RTOL
+    assert _rel(ggs[same], rgs[same]) < RTOL, _rel(ggs[same], rgs[same])
+    assert _rel(ggf[same], rgf[same]) < RTOL
+    return counts, solved, same
+
+
+def test_mesh_atlas_bench_sampler():
+    """The bench sampler's states (feet on / near the ground, random poses)."""
+    counts, solved, same = _mesh_parity(256, 1000)
+    print("contacts per world", np.bincount(counts), "solved", solved.sum(), "same path", same.sum())
+    assert (counts > 0).mean() > 0.4
+    assert counts.max() > 16  # the STL soles give more contacts than the box feet
+    assert (~same[solved]).sum() <= max(1, int(0.03 * solved.sum()))
+
+
+def test_mesh_atlas_standing():
+    """Near the standing pose (smaller perturbations): fewer contact changes."""
+    counts, solved, same = _mesh_parity(128, 7, q_scale=0.005, v_scale=0.01)
+    assert (counts > 0).any()

@@ -3,12 +3,17 @@
 import os
 import sys
 
+import numpy as np  # noqa: F401
+
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from nimblephysics_amd import assets, skel, urdf  # noqa: E402
 
 REF = os.environ.get("NIMBLE_REFERENCE", "/root/reference")
 MODELS = {
     "atlas": ("data/sdf/atlas/atlas_v3_box_colliders.urdf", False),
+    # the reference atlas_bench's model (python/nimblephysics_benchmarks/
+    # atlas_bench.py:18): STL mesh colliders
+    "atlas_mesh": ("data/sdf/atlas/atlas_v3_no_head.urdf", False),
     "atlas_ground": ("data/sdf/atlas/ground.urdf", False),
     "kr5": ("data/urdf/KR5/KR5 sixx R650.urdf", True),
     "kr5_ground": ("data/urdf/KR5/ground.urdf", True),

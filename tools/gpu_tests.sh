@@ -7,7 +7,7 @@ K=${2:-}
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 if [ -n "$K" ]; then KA=(-k "$K"); else KA=(); fi
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${KA[@]}" > gpurun_out/gpu_tests_$TAG.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread "${KA[@]}" > gpurun_out/gpu_tests_$TAG.log 2>&1
 rc=$?
 grep -E "PASSED|FAILED|ERROR|passed|failed" gpurun_out/gpu_tests_$TAG.log | tail -40
 [ $rc -ne 0 ] && exit $rc

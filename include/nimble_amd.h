@@ -223,6 +223,21 @@ int nimble_backward_masses(nimble_world_t world, int32_t batch, const double* st
                            double* grad_forces, double* grad_masses, void* stream);
 
 /*
+ * nimble_backward plus the gradient with respect to every body's ten inertia
+ * parameters, in WithRespectToMass's INERTIA_FULL order
+ * (dart/neural/WithRespectToMass.cpp:35-181): mass, local COM x y z, moment
+ * about the COM Ixx Iyy Izz Ixy Ixz Iyz:
+ *   grad_inertia [batch][num_bodies][10]  device
+ * The Python / C++ layers pick the tuned entries' components (INERTIA_MASS,
+ * INERTIA_COM, INERTIA_COM_MU (beta-weighted COM), INERTIA_DIAGONAL,
+ * INERTIA_OFF_DIAGONAL, INERTIA_FULL).
+ */
+int nimble_backward_inertia(nimble_world_t world, int32_t batch, const double* state,
+                            const double* forces, double* snapshot,
+                            const double* grad_next_state, double* grad_state,
+                            double* grad_forces, double* grad_inertia, void* stream);
+
+/*
  * Batched step Jacobians of a forward's snapshot, without bound clipping:
  *   state_jacobian [batch][2n][2n]  d(next_state)/d(state) ==
  *       BackpropSnapshot::getStateJacobian (dart/neural/BackpropSnapshot.cpp:1230):

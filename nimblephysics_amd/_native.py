@@ -39,6 +39,8 @@ def lib():
         L.nimble_backward.restype = C.c_int
         L.nimble_backward_masses.argtypes = [C.c_void_p, C.c_int32] + [C.c_void_p] * 7 + [C.c_void_p]
         L.nimble_backward_masses.restype = C.c_int
+        L.nimble_backward_inertia.argtypes = [C.c_void_p, C.c_int32] + [C.c_void_p] * 7 + [C.c_void_p]
+        L.nimble_backward_inertia.restype = C.c_int
         L.nimble_last_error.argtypes = []
         L.nimble_last_error.restype = C.c_char_p
         L.nimble_jacobian_workspace_doubles.argtypes = [C.c_void_p, C.c_int32]
@@ -187,6 +189,22 @@ class DeviceWorld:
                                             _ptr(grad_state), _ptr(grad_forces), _ptr(grad_masses),
                                             C.c_void_p(stream_ptr)))
 
+    def backward_inertia(self, state, forces, snapshot, grad_next, grad_state, grad_forces, grad_inertia,
+                         stream_ptr: int):
+        """backward() plus dL/d(body inertia parameters) [B, num_bodies, 10] in
+        INERTIA_FULL order (mass, COM xyz, Ixx Iyy Izz Ixy Ixz Iyz;
+        nimble_backward_inertia)."""
+        _require_device(state, forces, snapshot, grad_next, grad_state, grad_forces, grad_inertia)
+        B = state.shape[0]
+        self._on_my_device(state, forces, snapshot, grad_next, grad_state, grad_forces, grad_inertia)
+        self._shapes(B, state, forces, snapshot)
+        self._shapes(B, grad_next, grad_forces)
+        self._shapes(B, grad_state)
+        if tuple(grad_inertia.shape) != (B, self.nb, 10) or not grad_inertia.is_contiguous():
+            raise ValueError(f"grad_inertia shape {tuple(grad_inertia.shape)} != ({B}, {self.nb}, 10)")
+        _check(lib().nimble_backward_inertia(self.h, B, _ptr(state), _ptr(forces), _ptr(snapshot), _ptr(grad_next),
+                                             _ptr(grad_state), _ptr(grad_forces), _ptr(grad_inertia),
+                                             C.c_void_p(stream_ptr)))
 
     def jacobians(self, state, forces, snapshot, stream_ptr: int):
         """(d next_state / d state [B, 2n, 2n], d next_state / d forces

@@ -41,7 +41,7 @@ extern "C" __global__ void nimble_forward_kernel(const ModelDev*, Layout, const 
                                                  double*, double*, int, int);
 extern "C" __global__ void nimble_backward_kernel(const ModelDev*, int, const double*, const double*,
                                                   double*, int, const double*, double*, double*, int, double*, int,
-                                                  double*, int);
+                                                  double*, int, int);
 
 static void isoInverse(const double* T, double* O) {
   // [R|p]^-1 = [R^T | -R^T p]
@@ -393,7 +393,7 @@ int nimble_backward(nimble_world_t w, int32_t batch, const double* state, const 
   const size_t lds = (size_t)w->bwd.total * sizeof(double);
   hipLaunchKernelGGL(nimble_backward_kernel, dim3(gridFor(batch)), dim3(64), lds, st, w->dev, batch, state,
                      forces, snapshot, w->snapDoubles, grad_next_state, grad_state, grad_forces, 1, (double*)nullptr, 0,
-                     (double*)nullptr, 0);
+                     (double*)nullptr, 0, 1);
   HIP_TRY(hipGetLastError());
   return NIMBLE_OK;
 }
@@ -409,7 +409,23 @@ int nimble_backward_masses(nimble_world_t w, int32_t batch, const double* state,
   const size_t lds = (size_t)w->bwd.total * sizeof(double);
   hipLaunchKernelGGL(nimble_backward_kernel, dim3(gridFor(batch)), dim3(64), lds, st, w->dev, batch, state,
                      forces, snapshot, w->snapDoubles, grad_next_state, grad_state, grad_forces, 1, (double*)nullptr, 0,
-                     grad_masses, 0);
+                     grad_masses, 0, 1);
+  HIP_TRY(hipGetLastError());
+  return NIMBLE_OK;
+}
+
+int nimble_backward_inertia(nimble_world_t w, int32_t batch, const double* state, const double* forces,
+                            double* snapshot, const double* grad_next_state, double* grad_state,
+                            double* grad_forces, double* grad_inertia, void* stream) {
+  if (!w || batch < 0) return fail(NIMBLE_ERR_INVALID, "bad arguments");
+  if (batch == 0) return NIMBLE_OK;
+  if (!state || !forces || !grad_next_state || !grad_state || !grad_forces || !snapshot || !grad_inertia)
+    return fail(NIMBLE_ERR_INVALID, "null buffer");
+  hipStream_t st = (hipStream_t)stream;
+  const size_t lds = (size_t)w->bwd.total * sizeof(double);
+  hipLaunchKernelGGL(nimble_backward_kernel, dim3(gridFor(batch)), dim3(64), lds, st, w->dev, batch, state,
+                     forces, snapshot, w->snapDoubles, grad_next_state, grad_state, grad_forces, 1, (double*)nullptr, 0,
+                     grad_inertia, 0, 10);
   HIP_TRY(hipGetLastError());
   return NIMBLE_OK;
 }
@@ -446,7 +462,7 @@ int nimble_jacobians(nimble_world_t w, int32_t batch, const double* state, const
   hipLaunchKernelGGL(nimble_backward_kernel, dim3(grid), dim3(64), lds, st, w->dev, batch, state, forces,
                      const_cast<double*>(snapshot), w->snapDoubles, (const double*)nullptr, state_jacobian,
                      force_jacobian, rows, w->jacWsDoubles > 0 ? workspace : (double*)nullptr, w->jacWsDoubles,
-                     (double*)nullptr, 0);
+                     (double*)nullptr, 0, 1);
   HIP_TRY(hipGetLastError());
   return NIMBLE_OK;
 }
@@ -466,7 +482,7 @@ int nimble_constraint_force_jacobians(nimble_world_t w, int32_t batch, const dou
   const size_t lds = (size_t)w->bwd.total * sizeof(double);
   hipLaunchKernelGGL(nimble_backward_kernel, dim3(grid), dim3(64), lds, st, w->dev, batch, state, forces,
                      const_cast<double*>(snapshot), w->snapDoubles, (const double*)nullptr, dfc_dstate, dfc_dforces,
-                     rows, w->jacWsDoubles > 0 ? workspace : (double*)nullptr, w->jacWsDoubles, (double*)nullptr, 1);
+                     rows, w->jacWsDoubles > 0 ? workspace : (double*)nullptr, w->jacWsDoubles, (double*)nullptr, 1, 1);
   HIP_TRY(hipGetLastError());
   return NIMBLE_OK;
 }

@@ -525,7 +525,7 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, int batch, const double
                        const double* __restrict__ forces, double* __restrict__ snapshot, int snapDoubles,
                        const double* __restrict__ gradNext, double* __restrict__ gradState,
                        double* __restrict__ gradForces, int rows, double* __restrict__ ws, int wsDoubles,
-                       double* __restrict__ gradMasses, int fcMode) {
+                       double* __restrict__ gradMasses, int fcMode, int massParams) {
   extern __shared__ double s[];
   const ModelDev& md = *mdp;
   const Layout& L = md.lay[1];
@@ -679,17 +679,23 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, int batch, const double
     STAMP(25);
     if (gradMasses != nullptr) {
       // lossWrtMass = getMassVelJacobian^T gv (BackpropSnapshot.cpp:177, :580:
-      // getVelJacobianWrt(WithRespectTo::MASS), :980) for every body mass.  The
-      // mass enters M and C only (not A_c, springs or the integration), so it
-      // takes the M / C terms of the position gradient above, with
-      // d/dq replaced by d/dm_b:  -dt (dID(q,v,a*)/dm_b)^T (w - nu) plus the
-      // M-derivative pairs  sum coef * (d(M a)/dm_b)^T c.  With the world COM
-      // c_b, dI_b/dm_b y = [c x u_y; u_y], u_y = y_lin - c x y_ang (the COM
-      // point's velocity under twist y), so (d(M a)/dm_b)^T c = u_a . u_c and
-      // y^T dID/dm_b = V_y^T [dI (A_b - a_g) + V_b x* (dI V_b)].
+      // getVelJacobianWrt(WithRespectTo::MASS), :980) for every body's inertia
+      // parameters (WithRespectToMass.cpp:35, INERTIA_FULL order: mass, local
+      // COM x y z, moment about the COM Ixx Iyy Izz Ixy Ixz Iyz; massParams 1
+      // = the mass only).  They enter M and C only (not A_c, springs or the
+      // integration), so each takes the M / C terms of the position gradient
+      // above with d/dq replaced by d/dtheta:  -dt (dID(q,v,a*)/dtheta)^T (w - nu)
+      // plus the M-derivative pairs  sum coef * x_a^T (dG_b/dtheta) x_c.  With
+      // twists x = [w; v] (world frame), the COM c (world), its velocity
+      // u_x = v - c x w and the body-frame angular velocity wb = R^T w:
+      //   x^T G y = wb_x^T I wb_y + m u_x . u_y,   G y = [R I wb_y + m c x u_y; m u_y]
+      // so d/dm: u_x . u_y; d/dc_k (r_k = R e_k, du_y = w_y x r_k):
+      // m (w_x x r_k . u_y + u_x . w_y x r_k); d/dI_ij: wb_x,i wb_y,j (+ sym).
+      // y^T dID/dtheta = V_y^T [dG (A_b - a_g) + V_b x* (dG V_b)].
       if (lane < md.nb) {
         const int b = lane;
         const double* Tw = s + L.Tw + 12 * b;
+        const double m = md.mass[b];
         double cw[3];
         for (int r = 0; r < 3; r++)
           cw[r] = Tw[r * 4] * md.com[b][0] + Tw[r * 4 + 1] * md.com[b][1] + Tw[r * 4 + 2] * md.com[b][2] + Tw[r * 4 + 3];
@@ -698,30 +704,82 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, int batch, const double
           cross3(cw, y, cx);  // c x y_ang
           for (int i = 0; i < 3; i++) u[i] = y[3 + i] - cx[i];
         };
+        auto bodyAng = [&](const double* y, double* wb) {  // R^T y_ang
+          for (int i = 0; i < 3; i++) wb[i] = Tw[i] * y[0] + Tw[4 + i] * y[1] + Tw[8 + i] * y[2];
+        };
+        // x^T dG/dtheta y for every parameter p (out[p], accumulated with coef)
+        auto pairTerms = [&](const double* x, const double* y, double coef, double* out) {
+          double ux[3], uy[3];
+          comVel(x, ux);
+          comVel(y, uy);
+          out[0] += coef * (ux[0] * uy[0] + ux[1] * uy[1] + ux[2] * uy[2]);
+          if (massParams < 10) return;
+          for (int k = 0; k < 3; k++) {
+            const double rk[3] = {Tw[k], Tw[4 + k], Tw[8 + k]};
+            double a[3], c[3];
+            cross3(x, rk, a);  // w_x x r_k
+            cross3(y, rk, c);  // w_y x r_k
+            out[1 + k] += coef * m * (a[0] * uy[0] + a[1] * uy[1] + a[2] * uy[2] + ux[0] * c[0] + ux[1] * c[1] + ux[2] * c[2]);
+          }
+          double bx[3], by[3];
+          bodyAng(x, bx);
+          bodyAng(y, by);
+          out[4] += coef * bx[0] * by[0];
+          out[5] += coef * bx[1] * by[1];
+          out[6] += coef * bx[2] * by[2];
+          out[7] += coef * (bx[0] * by[1] + bx[1] * by[0]);
+          out[8] += coef * (bx[0] * by[2] + bx[2] * by[0]);
+          out[9] += coef * (bx[1] * by[2] + bx[2] * by[1]);
+        };
         const double ag[6] = {0, 0, 0, md.g[0], md.g[1], md.g[2]};
         const double* Vb = s + L.V + 6 * b;
-        double Ab[6], uA[3], uV[3], uW[3], Vw[6], h[6], fh[6];
+        double Ab[6], Vw[6], val[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         for (int i = 0; i < 6; i++) Ab[i] = s[L.A + 6 * b + i] - ag[i];
-        comVel(Ab, uA);
-        comVel(Vb, uV);
         bodyTwist(md, s + L.Sw, b, s + L.w, 1, Vw);
-        comVel(Vw, uW);
-        cross3(cw, uV, h);
-        for (int i = 0; i < 3; i++) h[3 + i] = uV[i];
-        crf(Vb, h, fh);  // V_b x* (dI V_b)
-        double val = -dt * (uW[0] * uA[0] + uW[1] * uA[1] + uW[2] * uA[2] + dot6(Vw, fh));
+        pairTerms(Vw, Ab, -dt, val);
+        // Vw^T (V_b x* (dG V_b)) per parameter
+        {
+          double uV[3], h[6], fh[6];
+          comVel(Vb, uV);
+          cross3(cw, uV, h);
+          for (int i = 0; i < 3; i++) h[3 + i] = uV[i];
+          crf(Vb, h, fh);
+          val[0] += -dt * dot6(Vw, fh);
+          if (massParams >= 10) {
+            double bv[3];
+            bodyAng(Vb, bv);
+            for (int k = 0; k < 3; k++) {
+              const double rk[3] = {Tw[k], Tw[4 + k], Tw[8 + k]};
+              double du[3], t1[3], t2[3];
+              cross3(Vb, rk, du);  // dU/dc_k = w_V x r_k
+              cross3(rk, uV, t1);
+              cross3(cw, du, t2);
+              for (int i = 0; i < 3; i++) { h[i] = m * (t1[i] + t2[i]); h[3 + i] = m * du[i]; }
+              crf(Vb, h, fh);
+              val[1 + k] += -dt * dot6(Vw, fh);
+            }
+            // dG/dI_ij V_b = [R E_ij R^T w_V; 0]
+            const int pi[6] = {0, 1, 2, 0, 0, 1}, pj[6] = {0, 1, 2, 1, 2, 2};
+            for (int q = 0; q < 6; q++) {
+              double eb[3] = {0, 0, 0};
+              eb[pi[q]] += bv[pj[q]];
+              if (pi[q] != pj[q]) eb[pj[q]] += bv[pi[q]];
+              for (int i = 0; i < 3; i++) { h[i] = Tw[i * 4] * eb[0] + Tw[i * 4 + 1] * eb[1] + Tw[i * 4 + 2] * eb[2]; h[3 + i] = 0.0; }
+              crf(Vb, h, fh);
+              val[4 + q] += -dt * dot6(Vw, fh);
+            }
+          }
+        }
         if (nc > 0) {
           const double coef[4] = {-dt, 1.0, -(double)imp, -(double)imp};
           for (int pr = 0; pr < (imp ? 4 : 2); pr++) {
-            double Va[6], Vc[6], ua[3], uc[3];
+            double Va[6], Vc[6];
             bodyTwist(md, s + L.Sw, b, P.NV + 2 * pr, NV_COLS, Va);
             bodyTwist(md, s + L.Sw, b, P.NV + 2 * pr + 1, NV_COLS, Vc);
-            comVel(Va, ua);
-            comVel(Vc, uc);
-            val += coef[pr] * (ua[0] * uc[0] + ua[1] * uc[1] + ua[2] * uc[2]);
+            pairTerms(Va, Vc, coef[pr], val);
           }
         }
-        gradMasses[(size_t)item * md.nb + b] = val;
+        for (int q = 0; q < massParams; q++) gradMasses[((size_t)item * md.nb + b) * massParams + q] = val[q];
       }
       WSYNC();
     }

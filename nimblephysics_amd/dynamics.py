@@ -295,6 +295,17 @@ class BodyNode:
     def getMass(self):
         return self.mass
 
+    def setBeta(self, beta):
+        """BodyNode::setBeta (BodyNode.cpp:652): the COM direction that
+        INERTIA_COM_MU scales."""
+        self.beta = np.asarray(beta, dtype=np.float64).copy()
+
+    def getBeta(self):
+        return getattr(self, "beta", np.ones(3)).copy()
+
+    def getLocalCOM(self):
+        return self.com.copy()
+
     def setLocalCOM(self, c):
         self.com = np.asarray(c, dtype=np.float64).copy()
         _model_changed(self.skel)

@@ -28,7 +28,7 @@ import torch
 
 from . import _native
 from .simulation import World
-from .timestep import _action_index, _compute_device, step_batch
+from .timestep import _action_index, _compute_device, mass_gradient, step_batch
 
 
 class LossGradient:
@@ -181,14 +181,11 @@ class BackpropSnapshot:
         gs = torch.empty_like(self._state)
         gf = torch.empty_like(self._forces)
         B = self._state.shape[0]
-        mass_idx = self._world._mass_body_indices()
         with torch.cuda.device(self._state.device):
             stream = torch.cuda.current_stream(self._state.device).cuda_stream
-            if mass_idx:
-                gmb = torch.empty((B, self._dev.nb), dtype=torch.float64, device=self._state.device)
-                self._dev.backward_masses(self._state, self._forces, self._snap, g, gs, gf, gmb, stream)
-                sel = torch.tensor(mass_idx, dtype=torch.long, device=self._state.device)
-                gm = gmb.index_select(1, sel)
+            if self._world.getMassDims() > 0:
+                gm = mass_gradient(self._dev, self._world._mass_selection(), self._state, self._forces, self._snap, g,
+                                   gs, gf, stream)
             else:
                 self._dev.backward(self._state, self._forces, self._snap, g, gs, gf, stream)
                 gm = torch.zeros((B, 0), dtype=torch.float64, device=self._state.device)

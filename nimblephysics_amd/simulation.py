@@ -32,7 +32,7 @@ class World:
         self.action_space: Optional[List[int]] = None
         self._forces: Optional[np.ndarray] = None
         self._version = 0
-        self._mass_tuned = []  # (body node, upper bound, lower bound) per mass dim
+        self._mass_tuned = []  # (body node, entry type, upper bounds, lower bounds) per tuneMass entry
         self._native_by_dev = {}  # device index -> (version, DeviceWorld)
 
     # --- model ------------------------------------------------------------------
@@ -187,49 +187,125 @@ class World:
         f = self.getControlForces()
         return np.array([f[m] for m in self.getActionSpace()])
 
-    # --- tunable masses (World::tuneMass / getMassDims / getMasses / setMasses,
-    # dart/simulation/World.cpp; WithRespectToMass, dart/neural/WithRespectToMass.cpp)
-    # Body masses (WrtMassBodyNodeEntryType.INERTIA_MASS) are tunable: the mass
-    # vector holds them in registration order, setMasses writes them into the
-    # bodies (the device model is rebuilt on the next step), and
-    # TimestepLayer's lossWrtMass comes from nimble_backward_masses.  The COM /
-    # inertia-tensor entry types are not on this path.
+    # --- tunable inertia (World::tuneMass / getMassDims / getMasses / setMasses,
+    # dart/simulation/World.cpp:1013-1060, :1821; WithRespectToMass,
+    # dart/neural/WithRespectToMass.cpp:35-181).  Every WrtMassBodyNodeEntryType
+    # is tunable: INERTIA_MASS (1), INERTIA_COM (3, local COM), INERTIA_COM_MU
+    # (1, the COM along the body's beta direction), INERTIA_DIAGONAL (3, Ixx
+    # Iyy Izz), INERTIA_OFF_DIAGONAL (3, Ixy Ixz Iyz), INERTIA_FULL (10).  The
+    # mass vector holds the entries in registration order; setMasses writes
+    # them into the bodies (the device model is rebuilt on the next step);
+    # lossWrtMass comes from nimble_backward_masses (masses only) or
+    # nimble_backward_inertia (all ten parameters per body) through
+    # _mass_selection().
+    MASS_ENTRY_DIMS = {"INERTIA_MASS": 1, "INERTIA_COM": 3, "INERTIA_COM_MU": 1, "INERTIA_DIAGONAL": 3,
+                       "INERTIA_OFF_DIAGONAL": 3, "INERTIA_FULL": 10}
+
     def tuneMass(self, node, type="INERTIA_MASS", upperBound=None, lowerBound=None):
         kind = getattr(type, "name", type)
-        if kind != "INERTIA_MASS":
-            raise NotImplementedError(f"tuneMass: only INERTIA_MASS entries are on the batched path (got {kind})")
+        if kind not in self.MASS_ENTRY_DIMS:
+            raise ValueError(f"tuneMass: unknown WrtMassBodyNodeEntryType {kind}")
         if not any(node is b for s in self.skeletons for b in s.bodies):
             raise ValueError("tuneMass: the body node is not in this world")
-        if any(node is b for b, _, _ in self._mass_tuned):
-            raise ValueError("tuneMass: body already registered")
-        up = np.asarray(upperBound if upperBound is not None else [np.inf], dtype=np.float64).reshape(-1)[0]
-        lo = np.asarray(lowerBound if lowerBound is not None else [0.0], dtype=np.float64).reshape(-1)[0]
-        self._mass_tuned.append((node, float(up), float(lo)))
+        if any(node is e[0] and kind == e[1] for e in self._mass_tuned):
+            raise ValueError("tuneMass: entry already registered")
+        dims = self.MASS_ENTRY_DIMS[kind]
+        up = np.broadcast_to(np.asarray(upperBound if upperBound is not None else np.inf, dtype=np.float64).reshape(-1),
+                             (dims,)).copy()
+        lo = np.broadcast_to(np.asarray(lowerBound if lowerBound is not None else
+                                        (0.0 if kind == "INERTIA_MASS" else -np.inf), dtype=np.float64).reshape(-1),
+                             (dims,)).copy()
+        self._mass_tuned.append((node, kind, up, lo))
 
     def getMassDims(self) -> int:
-        return len(self._mass_tuned)
+        return sum(self.MASS_ENTRY_DIMS[k] for _, k, _, _ in self._mass_tuned)
+
+    @staticmethod
+    def _entry_get(b, kind):
+        """WrtMassBodyNodyEntry::get (WithRespectToMass.cpp:136)."""
+        I = b.moment  # Ixx Iyy Izz Ixy Ixz Iyz
+        if kind == "INERTIA_MASS":
+            return np.array([b.mass])
+        if kind == "INERTIA_COM":
+            return np.array(b.com, dtype=np.float64)
+        if kind == "INERTIA_COM_MU":
+            beta = b.getBeta()
+            k = 0 if beta[0] != 0 else (1 if beta[1] != 0 else 2)
+            return np.array([b.com[k] / beta[k]])
+        if kind == "INERTIA_DIAGONAL":
+            return np.array(I[:3], dtype=np.float64)
+        if kind == "INERTIA_OFF_DIAGONAL":
+            return np.array(I[3:], dtype=np.float64)
+        return np.concatenate([[b.mass], b.com, I])
 
     def getMasses(self):
-        return np.array([b.getMass() for b, _, _ in self._mass_tuned], dtype=np.float64)
+        if not self._mass_tuned:
+            return np.zeros(0)
+        return np.concatenate([self._entry_get(b, k) for b, k, _, _ in self._mass_tuned]).astype(np.float64)
 
     def getMassUpperBound(self):
-        return np.array([u for _, u, _ in self._mass_tuned], dtype=np.float64)
+        return np.concatenate([u for _, _, u, _ in self._mass_tuned]) if self._mass_tuned else np.zeros(0)
 
     def getMassLowerBound(self):
-        return np.array([l for _, _, l in self._mass_tuned], dtype=np.float64)
+        return np.concatenate([l for _, _, _, l in self._mass_tuned]) if self._mass_tuned else np.zeros(0)
 
     def setMasses(self, masses):
+        """WrtMassBodyNodyEntry::set (WithRespectToMass.cpp:45) per entry; an
+        unchanged value keeps the device model."""
         masses = np.asarray(masses, dtype=np.float64).reshape(-1)
         if masses.shape[0] != self.getMassDims():
             raise ValueError(f"setMasses: {masses.shape[0]} values, the world has {self.getMassDims()} mass dims")
-        for (b, _, _), m in zip(self._mass_tuned, masses):
-            if b.getMass() != float(m):  # an unchanged mass keeps the device model
-                b.setMass(float(m))
+        o = 0
+        for b, kind, _, _ in self._mass_tuned:
+            d = self.MASS_ENTRY_DIMS[kind]
+            v = masses[o:o + d]
+            o += d
+            if np.array_equal(v, self._entry_get(b, kind)):
+                continue
+            if kind == "INERTIA_MASS":
+                b.setMass(float(v[0]))
+            elif kind == "INERTIA_COM":
+                b.setLocalCOM(v)
+            elif kind == "INERTIA_COM_MU":
+                b.setLocalCOM(b.getBeta() * float(v[0]))
+            elif kind == "INERTIA_DIAGONAL":
+                b.setMomentOfInertia(v[0], v[1], v[2], *b.moment[3:])
+            elif kind == "INERTIA_OFF_DIAGONAL":
+                b.setMomentOfInertia(*b.moment[:3], v[0], v[1], v[2])
+            else:
+                b.setMass(float(v[0]))
+                b.setLocalCOM(v[1:4])
+                b.setMomentOfInertia(*v[4:10])
+
+    def _mass_selection(self):
+        """(masses_only, index / matrix): with only INERTIA_MASS entries, the
+        global body index of each (columns of nimble_backward_masses' [B,
+        num_bodies]); otherwise a [num_bodies * 10, getMassDims()] matrix
+        taking nimble_backward_inertia's INERTIA_FULL-ordered parameters to
+        the mass vector (COM_MU: the beta-weighted COM components)."""
+        order = [b for s in self.skeletons for b in s.bodies]
+        idx = [next(i for i, o in enumerate(order) if o is b) for b, _, _, _ in self._mass_tuned]
+        if all(k == "INERTIA_MASS" for _, k, _, _ in self._mass_tuned):
+            return True, idx
+        S = np.zeros((len(order) * 10, self.getMassDims()))
+        col = 0
+        for (b, kind, _, _), bi in zip(self._mass_tuned, idx):
+            base = 10 * bi
+            comps = {"INERTIA_MASS": [0], "INERTIA_COM": [1, 2, 3], "INERTIA_DIAGONAL": [4, 5, 6],
+                     "INERTIA_OFF_DIAGONAL": [7, 8, 9], "INERTIA_FULL": list(range(10))}.get(kind)
+            if comps is not None:
+                for c in comps:
+                    S[base + c, col] = 1.0
+                    col += 1
+            else:  # INERTIA_COM_MU: d com / d mu = beta
+                S[base + 1:base + 4, col] = b.getBeta()
+                col += 1
+        return False, S
 
     def _mass_body_indices(self):
-        """Global body index (device model order) of each tuned mass."""
+        """Global body index (device model order) of each tuned mass entry."""
         order = [b for s in self.skeletons for b in s.bodies]
-        return [next(i for i, o in enumerate(order) if o is b) for b, _, _ in self._mass_tuned]
+        return [next(i for i, o in enumerate(order) if o is b) for b, _, _, _ in self._mass_tuned]
 
     # --- flattening -----------------------------------------------------------------------
     def desc_arrays(self) -> Dict[str, np.ndarray]:

@@ -131,6 +131,22 @@ def step_batch(world: World, st: torch.Tensor, act: torch.Tensor):
     return dev, forces, nxt, snap
 
 
+def mass_gradient(dev, selection, st, forces, snap, g, gs, gf, stream):
+    """lossWrtMass [B, getMassDims()] (with the state / force gradients into
+    gs / gf): nimble_backward_masses when only body masses are tuned, else
+    nimble_backward_inertia's ten parameters per body taken to the mass
+    vector by World._mass_selection's matrix."""
+    only_masses, sel = selection
+    B = st.shape[0]
+    if only_masses:
+        gmb = torch.empty((B, dev.nb), dtype=torch.float64, device=st.device)
+        dev.backward_masses(st, forces, snap, g, gs, gf, gmb, stream)
+        return gmb.index_select(1, torch.tensor(sel, dtype=torch.long, device=st.device))
+    gi = torch.empty((B, dev.nb, 10), dtype=torch.float64, device=st.device)
+    dev.backward_inertia(st, forces, snap, g, gs, gf, gi, stream)
+    return gi.reshape(B, dev.nb * 10) @ torch.as_tensor(sel, dtype=torch.float64, device=st.device)
+
+
 class TimestepLayer(torch.autograd.Function):
     @staticmethod
     def forward(ctx, world: World, state: torch.Tensor, action: torch.Tensor, mass: Optional[torch.Tensor]):
@@ -150,7 +166,7 @@ class TimestepLayer(torch.autograd.Function):
                 world._last_mass = (mass, mass._version, world._version)
             ctx.mass_shape = tuple(mass.shape)
             ctx.mass_device = mass.device
-            ctx.mass_index = world._mass_body_indices()
+            ctx.mass_sel = world._mass_selection()
         ctx.out_device = state.device
         cdev = _compute_device(state)
         with torch.cuda.device(cdev):
@@ -192,11 +208,8 @@ class TimestepLayer(torch.autograd.Function):
             gf = torch.empty_like(forces)
             stream = torch.cuda.current_stream(st.device).cuda_stream
             gm = None
-            if ctx.use_mass and len(ctx.mass_index) > 0:
-                gmb = torch.empty((st.shape[0], dev.nb), dtype=torch.float64, device=st.device)
-                dev.backward_masses(st, forces, snap, g, gs, gf, gmb, stream)
-                sel = torch.tensor(ctx.mass_index, dtype=torch.long, device=st.device)
-                gm = gmb.index_select(1, sel).sum(0).to(ctx.mass_device)
+            if ctx.use_mass and ctx.mass_shape[0] > 0:
+                gm = mass_gradient(dev, ctx.mass_sel, st, forces, snap, g, gs, gf, stream).sum(0).to(ctx.mass_device)
             else:
                 dev.backward(st, forces, snap, g, gs, gf, stream)
             ga = gf if idx.shape[0] == gf.shape[1] and ctx.identity else gf.index_select(1, idx)

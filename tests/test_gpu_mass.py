@@ -194,3 +194,121 @@ def test_constraint_force_getters_without_collision_pairs():
     one = neural.forwardPass(w, idempotent=True)
     assert one.getClampingConstraintImpulses().shape == (0,)
     assert one.getJacobianOfConstraintForce(w, "POSITION").shape[0] == 0
+
+
+def _set_param(body, p, val):
+    """INERTIA_FULL component p of a body (WithRespectToMass.cpp:113)."""
+    if p == 0:
+        body.setMass(val)
+    elif p < 4:
+        c = body.com.copy()
+        c[p - 1] = val
+        body.setLocalCOM(c)
+    else:
+        I = body.moment.copy()
+        I[p - 4] = val
+        body.setMomentOfInertia(*I)
+
+
+def _get_param(body, p):
+    return body.mass if p == 0 else (body.com[p - 1] if p < 4 else body.moment[p - 4])
+
+
+def _inertia_parity(world, st, f, bodies, seed=5, tol=1e-6):
+    """nimble_backward_inertia's [B, nb, 10] against central differences of
+    the oracle's step over each inertia parameter of `bodies`."""
+    B = st.shape[0]
+    ow = O.OracleWorld(world)
+    ow.forward(st, f)
+    nxt, snap, cache, ts, tf = _device_step(world, st, f)
+    same = np.ones(B, dtype=bool)
+    if world.native().num_pairs > 0:
+        same = _check_contacts(ow, snap.cpu().numpy(), B, cache=cache.cpu().numpy())
+    dev = world.native()
+    g = np.random.default_rng(seed).standard_normal(st.shape)
+    gt = torch.tensor(g, device=ts.device)
+    gs, gf = torch.empty_like(ts), torch.empty_like(tf)
+    gi = torch.empty((B, dev.nb, 10), dtype=torch.float64, device=ts.device)
+    stream = torch.cuda.current_stream().cuda_stream
+    dev.backward_inertia(ts, tf, snap, gt, gs, gf, gi, stream)
+    gm = torch.empty((B, dev.nb), dtype=torch.float64, device=ts.device)
+    gs2, gf2 = torch.empty_like(ts), torch.empty_like(tf)
+    dev.backward_masses(ts, tf, snap, gt, gs2, gf2, gm, stream)
+    torch.cuda.synchronize()
+    assert torch.equal(gs, gs2) and torch.equal(gf, gf2)
+    gi, gm = gi.cpu().numpy(), gm.cpu().numpy()
+    assert np.allclose(gi[:, :, 0], gm, rtol=1e-12, atol=1e-14 * np.abs(gm).max())
+    blist = [b for s in world.skeletons for b in s.bodies]
+    got, ref, noise = [], [], []
+    for bi in bodies:
+        body = blist[bi]
+        for p in range(10):
+            v0 = _get_param(body, p)
+            e = 1e-6 * max(abs(v0), 1e-2)
+            try:
+                _set_param(body, p, v0 + e)
+                lp = (O.OracleWorld(world).forward(st, f) * g).sum(axis=1)
+                _set_param(body, p, v0 - e)
+                lm = (O.OracleWorld(world).forward(st, f) * g).sum(axis=1)
+            finally:
+                _set_param(body, p, v0)
+            got.append(gi[same, bi, p])
+            ref.append(((lp - lm) / (2 * e))[same])
+            noise.append(1e-14 * np.abs(lp).max() / e)
+    got, ref = np.stack(got, axis=1), np.stack(ref, axis=1)
+    err = np.abs(got - ref)
+    bound = tol * np.abs(ref).max() + 3 * np.array(noise)[None, :]
+    assert (err <= bound).all(), (err.max(axis=0), np.abs(ref).max(axis=0), noise)
+
+
+def test_inertia_gradients_cartpole():
+    w = models.cartpole_world()
+    st, f = models.random_states(w, 8, seed=2)
+    _inertia_parity(w, st, f, bodies=[0, 1])
+
+
+def test_inertia_gradients_atlas_air():
+    w = models.atlas_world(False)
+    st, f = models.random_states(w, 4, seed=3, q_scale=0.2, v_scale=0.3)
+    _inertia_parity(w, st, f, bodies=[0, 5, 20, 30])
+
+
+def test_inertia_gradients_atlas_contact():
+    w = models.atlas_world(True)
+    st, f = models.random_states(w, 8, seed=3, q_scale=0.01, v_scale=0.02)
+    _inertia_parity(w, st, f, bodies=[0, 24, 33])
+
+
+def test_inertia_gradients_half_cheetah_contact():
+    w = models.half_cheetah_world()
+    st, f = models.half_cheetah_states(w, 16, seed=4)
+    _inertia_parity(w, st, f, bodies=[2, 4, 7])
+
+
+def test_timestep_layer_inertia_entries():
+    """timestep(world, state, action, mass) with COM / diagonal / COM_MU /
+    FULL entries: mass.grad is the batch sum of the selected components."""
+    import nimblephysics_amd as nimble
+    w = models.atlas_world(True)
+    bodies = [b for s in w.skeletons for b in s.bodies]
+    bodies[27].setBeta([1.0, 0.5, 0.0])
+    w.tuneMass(bodies[0], "INERTIA_COM")
+    w.tuneMass(bodies[27], "INERTIA_DIAGONAL")
+    w.tuneMass(bodies[27], "INERTIA_COM_MU")
+    w.tuneMass(bodies[5], "INERTIA_FULL")
+    st, f = models.random_states(w, 6, seed=8, q_scale=0.01, v_scale=0.02)
+    d = torch.device("cuda:0")
+    mass = torch.tensor(w.getMasses(), device=d, requires_grad=True)
+    ts = torch.tensor(st, device=d, requires_grad=True)
+    tf = torch.tensor(f, device=d, requires_grad=True)
+    out = nimble.timestep(w, ts, tf, mass)
+    g = np.random.default_rng(1).standard_normal(st.shape)
+    out.backward(torch.tensor(g, device=d))
+    dev = w.native()
+    nxt, snap, cache, ts2, tf2 = _device_step(w, st, f)
+    gi = torch.empty((6, dev.nb, 10), dtype=torch.float64, device=d)
+    gs, gf = torch.empty_like(ts2), torch.empty_like(tf2)
+    dev.backward_inertia(ts2, tf2, snap, torch.tensor(g, device=d), gs, gf, gi, torch.cuda.current_stream().cuda_stream)
+    gi = gi.sum(0).cpu().numpy()
+    want = np.concatenate([gi[0, 1:4], gi[27, 4:7], [gi[27, 1] * 1.0 + gi[27, 2] * 0.5], gi[5, :]])
+    assert np.allclose(mass.grad.cpu().numpy(), want, rtol=1e-12, atol=1e-14 * np.abs(want).max())

@@ -90,8 +90,8 @@ def test_mass_argument_follows_reference_mass_dims():
     w.tuneMass(cart, "INERTIA_MASS")
     with pytest.raises(ValueError):
         w.tuneMass(pole, "INERTIA_MASS")
-    with pytest.raises(NotImplementedError):
-        w.tuneMass(cart, "INERTIA_COM")
+    with pytest.raises(ValueError):
+        w.tuneMass(cart, "INERTIA_COLOR")
     assert w.getMassDims() == 2
     assert np.allclose(w.getMasses(), [pole.getMass(), cart.getMass()])
     assert w._mass_body_indices() == [1, 0]
@@ -257,3 +257,37 @@ def test_dynamics_setters_invalidate_device_model():
         v = w._version
         c()
         assert w._version > v
+
+
+def test_tune_inertia_entries_follow_with_respect_to_mass():
+    """Every WrtMassBodyNodeEntryType (WithRespectToMass.cpp:35-181): dims,
+    get / set order (INERTIA_FULL = mass, COM, Ixx Iyy Izz Ixy Ixz Iyz),
+    COM_MU along the body's beta, and the selection from the device's
+    [num_bodies, 10] inertia gradients to the mass vector."""
+    w = models.cartpole_world()
+    sk = w.skeletons[0]
+    cart, pole = sk.bodies[0], sk.bodies[1]
+    pole.setLocalCOM([0.1, -0.2, 0.3])
+    pole.setMomentOfInertia(0.5, 0.6, 0.7, 0.01, 0.02, 0.03)
+    pole.setBeta([0.0, 2.0, 1.0])
+    w.tuneMass(pole, "INERTIA_COM")
+    w.tuneMass(cart, "INERTIA_DIAGONAL")
+    w.tuneMass(pole, "INERTIA_OFF_DIAGONAL")
+    w.tuneMass(pole, "INERTIA_COM_MU")
+    w.tuneMass(cart, "INERTIA_FULL")
+    assert w.getMassDims() == 3 + 3 + 3 + 1 + 10
+    m = w.getMasses()
+    assert np.allclose(m[:3], [0.1, -0.2, 0.3]) and np.allclose(m[6:9], [0.01, 0.02, 0.03])
+    assert np.isclose(m[9], -0.2 / 2.0)
+    assert np.allclose(m[10:], np.concatenate([[cart.getMass()], cart.com, cart.moment]))
+    m2 = m.copy()
+    m2[9] = 0.25  # COM_MU: com = beta * mu
+    w.setMasses(m2)
+    assert np.allclose(pole.com, [0.0, 0.5, 0.25])
+    only, S = w._mass_selection()
+    assert not only and S.shape == (2 * 10, 20)
+    # pole = body 1: COM columns 0..2, off-diagonal 6..8, COM_MU (beta) 9
+    assert S[11, 0] == 1 and S[12, 1] == 1 and S[13, 2] == 1
+    assert S[17, 6] == 1 and S[19, 8] == 1
+    assert np.allclose(S[11:14, 9], [0.0, 2.0, 1.0])
+    assert np.array_equal(S[0:10, 10:20], np.eye(10))

@@ -466,6 +466,28 @@ inline std::shared_ptr<BackpropSnapshot> forwardPass(const simulation::WorldPtr&
 }
 
 }  // namespace neural
+
+namespace utils {
+
+/* dart/utils/urdf/DartLoader.hpp parseSkeleton (DartLoader.cpp:199): one
+ * Skeleton from a URDF file; joints of a link in name order (urdfdom's
+ * std::map), a FreeJoint "rootJoint" above a root link not named "world",
+ * box / sphere / STL mesh collision geometry (paths resolved against the
+ * file's directory, package:// and file:// prefixes dropped); throws
+ * std::invalid_argument for what the timestep path does not model */
+class DartLoader {
+ public:
+  dynamics::SkeletonPtr parseSkeleton(const std::string& path);
+};
+
+/* dart/utils/SkelParser.hpp readWorld (SkelParser.cpp:402): the <world> of a
+ * .skel file (time step, gravity, skeletons with box / sphere / capsule
+ * collision shapes and weld / revolute / prismatic / free joints) */
+struct SkelParser {
+  static simulation::WorldPtr readWorld(const std::string& path);
+};
+
+}  // namespace utils
 }  // namespace nimble_amd
 
 #endif /* NIMBLE_WORLD_HPP_ */

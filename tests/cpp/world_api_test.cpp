@@ -7,6 +7,9 @@
 //       upstream gradient [2n] from stdin, runs neural::forwardPass, then
 //       BackpropSnapshot::backpropState and getStateJacobian / getForceJacobian,
 //       then two World::step calls; prints JSON.
+//   world_api_test describe-urdf|describe-skel <path>   loads the file with
+//       utils::DartLoader::parseSkeleton / utils::SkelParser::readWorld and
+//       prints {"positions": [...], "desc": {...}} (no GPU needed)
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -139,11 +142,29 @@ static void describe(simulation::World& w) {
 
 int main(int argc, char** argv) {
   if (argc < 3) {
-    std::fprintf(stderr, "usage: %s describe|step box|pendulum\n", argv[0]);
+    std::fprintf(stderr, "usage: %s describe|step box|pendulum | describe-urdf|describe-skel <path>\n", argv[0]);
     return 2;
   }
   try {
     const std::string mode = argv[1];
+    if (mode == "describe-urdf" || mode == "describe-skel") {
+      // utils::DartLoader / SkelParser: the loaded world's description plus
+      // its initial positions
+      simulation::WorldPtr w;
+      if (mode == "describe-urdf") {
+        w = simulation::World::create();
+        utils::DartLoader loader;
+        w->addSkeleton(loader.parseSkeleton(argv[2]));
+      } else {
+        w = utils::SkelParser::readWorld(argv[2]);
+      }
+      std::printf("{");
+      printVec("positions", w->getPositions(), false);
+      std::printf(", \"desc\": ");
+      describe(*w);
+      std::printf("}\n");
+      return 0;
+    }
     auto world = makeWorld(argv[2]);
     if (mode == "describe") {
       describe(*world);

@@ -373,8 +373,8 @@ def test_lcp_reduce_duplicate_columns(shape):
 
 
 def test_contact_overflow_raises():
-    """More contacts than NIMBLE_MAX_CONTACTS (five boxes resting on the
-    ground: 20 corner contacts) cannot be the reference's step: timestep
+    """More contacts than NIMBLE_MAX_CONTACTS (nine boxes resting on the
+    ground: 36 corner contacts > 32) cannot be the reference's step: timestep
     raises ContactCapacityError, and under the 'record' policy the per-world
     status says why."""
     import nimblephysics_amd as nimble
@@ -390,18 +390,18 @@ def test_contact_overflow_raises():
     gb.createShapeNode(D.BoxShape([10.0, 0.1, 10.0]), collision=True)
     g.setMobile(False)
     w.addSkeleton(g)
-    for k in range(5):
+    for k in range(9):
         sk = D.Skeleton(f"box{k}")
         _, b = sk.createFreeJointAndBodyNodePair()
         b.createShapeNode(D.BoxShape([0.2, 0.1, 0.2]), collision=True)
         w.addSkeleton(sk)
-    st = np.zeros((4, 60))
-    for k in range(5):
+    st = np.zeros((4, 108))
+    for k in range(9):
         st[:, 6 * k + 3] = 0.5 * k
         st[:, 6 * k + 4] = 0.05 - 1e-3
     d = torch.device("cuda:0")
     ts = torch.tensor(st, device=d)
-    act = torch.zeros((4, 30), dtype=torch.float64, device=d)
+    act = torch.zeros((4, 54), dtype=torch.float64, device=d)
     with pytest.raises(ContactCapacityError):
         nimble.timestep(w, ts, act)
     w.setStatusPolicy("record")

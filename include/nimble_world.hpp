@@ -72,9 +72,16 @@ struct ContactCapacityError : std::runtime_error {
 namespace simulation { class World; }
 
 namespace neural {
-/* dart/neural/WithRespectToMass.hpp: the tunable entries of a body's inertia;
- * the batched path tunes INERTIA_MASS */
-enum class WrtMassBodyNodeEntryType { INERTIA_MASS, INERTIA_COM, INERTIA_DIAGONAL, INERTIA_FULL };
+/* dart/neural/WithRespectToMass.hpp:25: the tunable entries of a body's
+ * inertia (dims 1, 3, 1, 3, 3, 10; FULL = mass, COM, Ixx Iyy Izz Ixy Ixz Iyz) */
+enum class WrtMassBodyNodeEntryType {
+  INERTIA_MASS,
+  INERTIA_COM,
+  INERTIA_COM_MU,
+  INERTIA_DIAGONAL,
+  INERTIA_OFF_DIAGONAL,
+  INERTIA_FULL
+};
 /* dart/neural/WithRespectTo.hpp (the state / control spaces) */
 enum class WithRespectTo { POSITION, VELOCITY, FORCE };
 }  // namespace neural
@@ -233,6 +240,11 @@ class BodyNode {
   void setLocalCOM(const Vector3s& c);
   Vector3s getLocalCOM() const { return mCom; }
   void setMomentOfInertia(double Ixx, double Iyy, double Izz, double Ixy = 0, double Ixz = 0, double Iyz = 0);
+  /* Ixx Iyy Izz Ixy Ixz Iyz */
+  std::array<double, 6> getMomentOfInertia() const { return mMoment; }
+  /* BodyNode::setBeta (BodyNode.cpp:652): the COM direction INERTIA_COM_MU scales */
+  void setBeta(const Vector3s& beta) { mBeta = beta; }
+  Vector3s getBeta() const { return mBeta; }
   void setFrictionCoeff(double f);
   double getFrictionCoeff() const { return mFriction; }
   void setRestitutionCoeff(double r);
@@ -257,6 +269,7 @@ class BodyNode {
   Vector3s mCom{{0, 0, 0}};
   std::array<double, 6> mMoment{{1, 1, 1, 0, 0, 0}};  // Ixx Iyy Izz Ixy Ixz Iyz
   double mFriction = 1.0, mRestitution = 0.0;
+  Vector3s mBeta{{1, 1, 1}};
   std::vector<std::unique_ptr<ShapeNode>> mShapes;
 };
 
@@ -359,18 +372,22 @@ class World {
   void step(bool resetCommand = true);
 
   /* World::tuneMass / getMassDims / getMasses / setMasses (World.cpp,
-   * WithRespectToMass.cpp): body masses registered in order form the mass
-   * vector whose gradient backpropState returns (lossWrtMass); other entry
-   * types throw std::invalid_argument. */
+   * WithRespectToMass.cpp:45 set / :136 get): the registered entries, in
+   * order, form the mass vector whose gradient backpropState returns
+   * (lossWrtMass); a body may carry several entry types, each once. */
   void tuneMass(dynamics::BodyNode* node, neural::WrtMassBodyNodeEntryType type, const VectorXs& upperBound,
                 const VectorXs& lowerBound);
-  std::size_t getMassDims() const { return mTunedMass.size(); }
+  std::size_t getMassDims() const { return mMassUpper.size(); }
   VectorXs getMasses() const;
   void setMasses(const VectorXs& masses);
   VectorXs getMassUpperBound() const { return mMassUpper; }
   VectorXs getMassLowerBound() const { return mMassLower; }
-  /* global body index (device model order) of each tuned mass */
+  /* global body index (device model order) of each tuned entry */
   std::vector<int> massBodyIndices() const;
+  /* true when every entry is INERTIA_MASS (nimble_backward_masses suffices);
+   * otherwise S [num_bodies * 10][getMassDims()] row-major takes
+   * nimble_backward_inertia's per-body parameters to the mass vector */
+  bool massSelection(std::vector<double>& S) const;
 
   /* The flat description handed to nimble_world_create (storage owned by the
    * World until the next call) and the uploaded handle (rebuilt after any
@@ -389,7 +406,7 @@ class World {
   double mDt = 0.001, mClip = 0.03, mCfm = 1e-4;
   bool mPenCorr = false, mParallel = true;
   VectorXs mForces;
-  std::vector<dynamics::BodyNode*> mTunedMass;
+  std::vector<std::pair<dynamics::BodyNode*, neural::WrtMassBodyNodeEntryType>> mTunedMass;
   VectorXs mMassUpper, mMassLower;
   long mVersion = 0, mBuiltVersion = -1;
   nimble_world_t mHandle = nullptr;

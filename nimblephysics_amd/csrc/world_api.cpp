@@ -291,36 +291,138 @@ nimble_world_t World::handle() {
   return mHandle;
 }
 
+namespace {
+using Entry = neural::WrtMassBodyNodeEntryType;
+std::size_t entryDims(Entry t) {
+  switch (t) {
+    case Entry::INERTIA_MASS: return 1;
+    case Entry::INERTIA_COM: return 3;
+    case Entry::INERTIA_COM_MU: return 1;
+    case Entry::INERTIA_DIAGONAL: return 3;
+    case Entry::INERTIA_OFF_DIAGONAL: return 3;
+    case Entry::INERTIA_FULL: return 10;
+  }
+  throw std::invalid_argument("tuneMass: unknown WrtMassBodyNodeEntryType");
+}
+// WrtMassBodyNodyEntry::get (WithRespectToMass.cpp:136)
+VectorXs entryGet(const dynamics::BodyNode* b, Entry t) {
+  const Vector3s c = b->getLocalCOM();
+  const std::array<double, 6> I = b->getMomentOfInertia();
+  switch (t) {
+    case Entry::INERTIA_MASS: return {b->getMass()};
+    case Entry::INERTIA_COM: return {c[0], c[1], c[2]};
+    case Entry::INERTIA_COM_MU: {
+      const Vector3s beta = b->getBeta();
+      const int k = beta[0] != 0 ? 0 : (beta[1] != 0 ? 1 : 2);
+      return {c[k] / beta[k]};
+    }
+    case Entry::INERTIA_DIAGONAL: return {I[0], I[1], I[2]};
+    case Entry::INERTIA_OFF_DIAGONAL: return {I[3], I[4], I[5]};
+    case Entry::INERTIA_FULL: return {b->getMass(), c[0], c[1], c[2], I[0], I[1], I[2], I[3], I[4], I[5]};
+  }
+  return {};
+}
+}  // namespace
+
 void World::tuneMass(dynamics::BodyNode* node, neural::WrtMassBodyNodeEntryType type, const VectorXs& upperBound,
                      const VectorXs& lowerBound) {
-  if (type != neural::WrtMassBodyNodeEntryType::INERTIA_MASS)
-    throw std::invalid_argument("tuneMass: only INERTIA_MASS entries are on the batched path");
+  const std::size_t dims = entryDims(type);
   bool found = false;
   for (const auto& sk : mSkels)
     for (const auto& b : sk->mBodies) found = found || b.get() == node;
   if (!found) throw std::invalid_argument("tuneMass: the body node is not in this world");
-  for (auto* b : mTunedMass)
-    if (b == node) throw std::invalid_argument("tuneMass: body already registered");
-  mTunedMass.push_back(node);
-  mMassUpper.push_back(upperBound.empty() ? std::numeric_limits<double>::infinity() : upperBound[0]);
-  mMassLower.push_back(lowerBound.empty() ? 0.0 : lowerBound[0]);
+  for (const auto& e : mTunedMass)
+    if (e.first == node && e.second == type) throw std::invalid_argument("tuneMass: entry already registered");
+  // bounds: one value per dim, or one value broadcast
+  auto bound = [&](const VectorXs& v, double dflt, std::size_t k) {
+    if (v.empty()) return dflt;
+    if (v.size() == 1) return v[0];
+    if (v.size() != dims) throw std::invalid_argument("tuneMass: bound size does not match the entry's dims");
+    return v[k];
+  };
+  const double lo = type == Entry::INERTIA_MASS ? 0.0 : -std::numeric_limits<double>::infinity();
+  mTunedMass.push_back({node, type});
+  for (std::size_t k = 0; k < dims; k++) {
+    mMassUpper.push_back(bound(upperBound, std::numeric_limits<double>::infinity(), k));
+    mMassLower.push_back(bound(lowerBound, lo, k));
+  }
 }
 
 VectorXs World::getMasses() const {
   VectorXs m;
-  for (auto* b : mTunedMass) m.push_back(b->getMass());
+  for (const auto& e : mTunedMass) {
+    const VectorXs v = entryGet(e.first, e.second);
+    m.insert(m.end(), v.begin(), v.end());
+  }
   return m;
 }
 
+// WrtMassBodyNodyEntry::set (WithRespectToMass.cpp:45); an unchanged entry
+// keeps the device model
 void World::setMasses(const VectorXs& masses) {
-  if (masses.size() != mTunedMass.size()) throw std::invalid_argument("setMasses: size mismatch");
-  for (std::size_t i = 0; i < masses.size(); i++)
-    if (mTunedMass[i]->getMass() != masses[i]) mTunedMass[i]->setMass(masses[i]);
+  if (masses.size() != getMassDims()) throw std::invalid_argument("setMasses: size mismatch");
+  std::size_t o = 0;
+  for (const auto& e : mTunedMass) {
+    dynamics::BodyNode* b = e.first;
+    const std::size_t d = entryDims(e.second);
+    const VectorXs v(masses.begin() + o, masses.begin() + o + d);
+    o += d;
+    if (v == entryGet(b, e.second)) continue;
+    const std::array<double, 6> I = b->getMomentOfInertia();
+    switch (e.second) {
+      case Entry::INERTIA_MASS: b->setMass(v[0]); break;
+      case Entry::INERTIA_COM: b->setLocalCOM({v[0], v[1], v[2]}); break;
+      case Entry::INERTIA_COM_MU: {
+        const Vector3s beta = b->getBeta();
+        b->setLocalCOM({beta[0] * v[0], beta[1] * v[0], beta[2] * v[0]});
+        break;
+      }
+      case Entry::INERTIA_DIAGONAL: b->setMomentOfInertia(v[0], v[1], v[2], I[3], I[4], I[5]); break;
+      case Entry::INERTIA_OFF_DIAGONAL: b->setMomentOfInertia(I[0], I[1], I[2], v[0], v[1], v[2]); break;
+      case Entry::INERTIA_FULL:
+        b->setMass(v[0]);
+        b->setLocalCOM({v[1], v[2], v[3]});
+        b->setMomentOfInertia(v[4], v[5], v[6], v[7], v[8], v[9]);
+        break;
+    }
+  }
+}
+
+bool World::massSelection(std::vector<double>& S) const {
+  bool massOnly = true;
+  for (const auto& e : mTunedMass) massOnly = massOnly && e.second == Entry::INERTIA_MASS;
+  if (massOnly) return true;
+  const std::vector<int> idx = massBodyIndices();
+  std::size_t nb = 0;
+  for (const auto& sk : mSkels) nb += sk->mBodies.size();
+  const std::size_t dims = getMassDims();
+  S.assign(nb * 10 * dims, 0.0);
+  std::size_t col = 0;
+  for (std::size_t i = 0; i < mTunedMass.size(); i++) {
+    const std::size_t base = 10 * (std::size_t)idx[i];
+    int first = 0, count = 0;
+    switch (mTunedMass[i].second) {
+      case Entry::INERTIA_MASS: first = 0; count = 1; break;
+      case Entry::INERTIA_COM: first = 1; count = 3; break;
+      case Entry::INERTIA_DIAGONAL: first = 4; count = 3; break;
+      case Entry::INERTIA_OFF_DIAGONAL: first = 7; count = 3; break;
+      case Entry::INERTIA_FULL: first = 0; count = 10; break;
+      case Entry::INERTIA_COM_MU: {  // d com / d mu = beta
+        const Vector3s beta = mTunedMass[i].first->getBeta();
+        for (int k = 0; k < 3; k++) S[(base + 1 + k) * dims + col] = beta[k];
+        col++;
+        continue;
+      }
+    }
+    for (int c = 0; c < count; c++) S[(base + first + c) * dims + col++] = 1.0;
+  }
+  return false;
 }
 
 std::vector<int> World::massBodyIndices() const {
   std::vector<int> idx;
-  for (auto* t : mTunedMass) {
+  for (const auto& e : mTunedMass) {
+    const dynamics::BodyNode* t = e.first;
     int base = 0, found = -1;
     for (const auto& sk : mSkels) {
       for (std::size_t k = 0; k < sk->mBodies.size(); k++)
@@ -457,24 +559,36 @@ void BackpropSnapshot::backpropState(const VectorXs& nextStateLossGrad, VectorXs
   if (nextStateLossGrad.size() != 2 * n) throw std::invalid_argument("backpropState: gradient size mismatch");
   checkModel("backpropState");
   const std::vector<int> idx = mWorld->massBodyIndices();
-  const std::size_t nb = mWorld->describe().num_bodies;
+  std::vector<double> S;
+  const bool massOnly = mWorld->massSelection(S);
+  const std::size_t nb = mWorld->describe().num_bodies, params = massOnly ? 1 : 10;
   double *dSt, *dF, *dS;
   uploadStep(*mWorld, mState, mForces, mSnapshot, dSt, dF, dS, n);
   double* dG = mWorld->deviceBuffer(3, 2 * n);
-  double* dGs = mWorld->deviceBuffer(2, 3 * n + nb);
+  double* dGs = mWorld->deviceBuffer(2, 3 * n + nb * params);
   hipCheck(hipMemcpy(dG, nextStateLossGrad.data(), 2 * n * sizeof(double), hipMemcpyHostToDevice), "hipMemcpy");
   double* dGf = dGs + 2 * n;
   double* dGm = dGs + 3 * n;
-  check(nimble_backward_masses(mHandle, 1, dSt, dF, dS, dG, dGs, dGf, dGm, nullptr), "nimble_backward_masses");
+  if (massOnly)
+    check(nimble_backward_masses(mHandle, 1, dSt, dF, dS, dG, dGs, dGf, dGm, nullptr), "nimble_backward_masses");
+  else
+    check(nimble_backward_inertia(mHandle, 1, dSt, dF, dS, dG, dGs, dGf, dGm, nullptr), "nimble_backward_inertia");
   hipCheck(hipDeviceSynchronize(), "nimble_backward_masses");
   stateLossGrad.resize(2 * n);
   forceLossGrad.resize(n);
-  std::vector<double> gm(nb);
+  std::vector<double> gm(nb * params);
   hipCheck(hipMemcpy(stateLossGrad.data(), dGs, 2 * n * sizeof(double), hipMemcpyDeviceToHost), "hipMemcpy");
   hipCheck(hipMemcpy(forceLossGrad.data(), dGf, n * sizeof(double), hipMemcpyDeviceToHost), "hipMemcpy");
-  hipCheck(hipMemcpy(gm.data(), dGm, nb * sizeof(double), hipMemcpyDeviceToHost), "hipMemcpy");
-  massLossGrad.resize(idx.size());
-  for (std::size_t i = 0; i < idx.size(); i++) massLossGrad[i] = gm[idx[i]];
+  hipCheck(hipMemcpy(gm.data(), dGm, gm.size() * sizeof(double), hipMemcpyDeviceToHost), "hipMemcpy");
+  const std::size_t dims = mWorld->getMassDims();
+  massLossGrad.assign(dims, 0.0);
+  if (massOnly) {
+    for (std::size_t i = 0; i < idx.size(); i++) massLossGrad[i] = gm[idx[i]];
+  } else {
+    for (std::size_t r = 0; r < nb * 10; r++)
+      if (gm[r] != 0.0)
+        for (std::size_t c = 0; c < dims; c++) massLossGrad[c] += S[r * dims + c] * gm[r];
+  }
 }
 
 // Clamping rows of the step: 0 for a model without collision pairs (its

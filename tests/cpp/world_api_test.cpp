@@ -199,6 +199,22 @@ int main(int argc, char** argv) {
     }
     std::vector<double> gs2, gf2, gm;
     snap->backpropState(g, gs2, gf2, gm);
+    const std::size_t massDims = world->getMassDims();
+    // then INERTIA_FULL and INERTIA_COM_MU (beta 0 1 2) on the same body:
+    // lossWrtMass through nimble_backward_inertia and the entry selection
+    dynamics::BodyNode* tunedBody = nullptr;
+    for (std::size_t si = 0, base = 0; si < world->getNumSkeletons(); si++) {
+      auto sk = world->getSkeleton(si);
+      for (std::size_t k = 0; k < sk->getNumBodyNodes(); k++, base++)
+        if ((int)base == tunedIndex) tunedBody = sk->getBodyNode(k);
+    }
+    tunedBody->setBeta({{0.0, 1.0, 2.0}});
+    world->tuneMass(tunedBody, neural::WrtMassBodyNodeEntryType::INERTIA_FULL, {}, {});
+    world->tuneMass(tunedBody, neural::WrtMassBodyNodeEntryType::INERTIA_COM_MU, {}, {});
+    std::vector<double> gs4, gf4, gmFull;
+    snap->backpropState(g, gs4, gf4, gmFull);
+    const std::vector<double> massesFull = world->getMasses();
+    world->setMasses(massesFull);  // unchanged values: the device model stays
     const std::vector<double> fc = snap->getClampingConstraintImpulses();
     const std::vector<double> dq = snap->getJacobianOfConstraintForce(neural::WithRespectTo::POSITION);
     const std::vector<double> dv = snap->getJacobianOfConstraintForce(neural::WithRespectTo::VELOCITY);
@@ -206,7 +222,10 @@ int main(int argc, char** argv) {
     std::printf("{");
     printVec("grad_state_m", gs2);
     printVec("grad_mass", gm);
-    printVec("mass_dims", std::vector<double>{(double)world->getMassDims(), (double)tunedIndex});
+    printVec("grad_mass_full", gmFull);
+    printVec("masses_full", massesFull);
+    printVec("mass_bounds_full", world->getMassLowerBound());
+    printVec("mass_dims", std::vector<double>{(double)massDims, (double)tunedIndex});
     printVec("fc", fc);
     printVec("dfc_q", dq);
     printVec("dfc_v", dv);

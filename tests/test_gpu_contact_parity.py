@@ -29,6 +29,13 @@ SN_NCON, SN_M, SN_NC, SN_NU, SN_STATUS = 0, 1, 2, 3, 5
 CREC = 13  # contact record doubles (csrc/pool_sizes.h)
 SN_CONTACTS, SN_ROWREC, RR_MAP = 16, 12, 7
 SN_ROWS = SN_CONTACTS + _native.MAX_CONTACTS * CREC
+# Gradient floor.  The reference's FreeJoint posPos / velPos blocks are central
+# differences (FreeJoint.cpp:965 eps 1e-6, :987 eps 1e-7), which the device
+# and the oracle both restate: rounding in the perturbed integration gives
+# ~eps_mach |q| / 1e-7 ~ 4e-9 absolute error per unit of upstream gradient in
+# either one, independently.  Gradient elements below 1e-4 of the batch's
+# largest are therefore compared absolutely, at 1e-10 of that largest.
+GRAD_FLOOR = 1e-4
 
 
 def _rel(a, b, floor=1e-5):
@@ -139,7 +146,7 @@ def _check_contacts(ow, snap, B, max_diverge=0.03, cache=None):
     return same
 
 
-def _parity(world, st, f, seed=11, check_grad=True, max_diverge=0.03, grad_floor=1e-5):
+def _parity(world, st, f, seed=11, check_grad=True, max_diverge=0.03, grad_floor=GRAD_FLOOR):
     ow = O.OracleWorld(world)
     ref = ow.forward(st, f)
     nxt, snap, cache, ts, tf = _device_step(world, st, f)
@@ -197,8 +204,8 @@ def test_atlas_rollout_warm_start():
         g = np.random.default_rng(k).standard_normal(st.shape)
         rgs, rgf = ow.backward(g)
         ggs, ggf = _device_backward(world, ts, tf, snap, g)
-        assert _rel(ggs[same], rgs[same]) < RTOL, (k, _rel(ggs[same], rgs[same]))
-        assert _rel(ggf[same], rgf[same]) < RTOL
+        assert _rel(ggs[same], rgs[same], GRAD_FLOOR) < RTOL, (k, _rel(ggs[same], rgs[same], GRAD_FLOOR))
+        assert _rel(ggf[same], rgf[same], GRAD_FLOOR) < RTOL
         cur = ref
 
 
@@ -248,8 +255,8 @@ def test_half_cheetah_rollout():
         g = np.random.default_rng(k).standard_normal(st.shape)
         rgs, rgf = ow.backward(g)
         ggs, ggf = _device_backward(world, ts, tf, snap, g)
-        assert _rel(ggs[same], rgs[same]) < RTOL, (k, _rel(ggs[same], rgs[same]))
-        assert _rel(ggf[same], rgf[same]) < RTOL
+        assert _rel(ggs[same], rgs[same], GRAD_FLOOR) < RTOL, (k, _rel(ggs[same], rgs[same], GRAD_FLOOR))
+        assert _rel(ggf[same], rgf[same], GRAD_FLOOR) < RTOL
         cur = ref
 
 
@@ -367,7 +374,7 @@ def test_lcp_reduce_duplicate_columns(shape):
     # numerically rank deficient by construction (columns 1e-10 m apart), so
     # rounding is amplified: elements below 1e-4 of the largest are compared
     # absolutely at 1e-10 of it (~2e-12 x max observed), the rest at 1e-6
-    ow, snap = _parity(world, st, f, max_diverge=0.1 if shape == "box" else 0.03, grad_floor=1e-4)
+    ow, snap = _parity(world, st, f, max_diverge=0.1 if shape == "box" else 0.03)
     reduced = (snap[:, 5].astype(int) & 8) != 0
     assert reduced.mean() > 0.4, reduced.mean()
 
@@ -391,17 +398,20 @@ def test_contact_overflow_raises():
     g.setMobile(False)
     w.addSkeleton(g)
     for k in range(9):
+        # vertical sliders (the model allows at most 8 free joints)
         sk = D.Skeleton(f"box{k}")
-        _, b = sk.createFreeJointAndBodyNodePair()
+        j, b = sk.createPrismaticJointAndBodyNodePair()
+        j.setAxis([0, 1, 0])
+        T = np.eye(4)
+        T[0, 3] = 0.5 * k
+        j.setTransformFromParentBodyNode(T)
         b.createShapeNode(D.BoxShape([0.2, 0.1, 0.2]), collision=True)
         w.addSkeleton(sk)
-    st = np.zeros((4, 108))
-    for k in range(9):
-        st[:, 6 * k + 3] = 0.5 * k
-        st[:, 6 * k + 4] = 0.05 - 1e-3
+    st = np.zeros((4, 18))
+    st[:, :9] = 0.05 - 1e-3
     d = torch.device("cuda:0")
     ts = torch.tensor(st, device=d)
-    act = torch.zeros((4, 54), dtype=torch.float64, device=d)
+    act = torch.zeros((4, 9), dtype=torch.float64, device=d)
     with pytest.raises(ContactCapacityError):
         nimble.timestep(w, ts, act)
     w.setStatusPolicy("record")

@@ -3,6 +3,7 @@
 import sys
 import numpy as np
 sys.path.insert(0, "tests")
+sys.path.insert(0, ".")
 from nimblephysics_amd import workloads
 from oracle import oracle as O
 from test_gpu_contact_parity import SN_M, SN_NCON, _device_backward, _device_step

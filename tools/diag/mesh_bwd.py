@@ -3,6 +3,7 @@ count, LCP rows and contact types of the worst worlds (diagnostic)."""
 import sys
 import numpy as np
 sys.path.insert(0, "tests")
+sys.path.insert(0, ".")
 from nimblephysics_amd import _native, workloads
 from oracle import oracle as O
 from test_gpu_contact_parity import CREC, SN_CONTACTS, SN_M, SN_NCON, SN_STATUS, _device_backward, _device_step, _same_path

@@ -38,6 +38,9 @@ _cheetah_states = models.cheetah_states
 WORKLOADS = {
     "atlas": ("Atlas 33-DoF (atlas_v3_box_colliders) + ground, foot contact", lambda: models.atlas_world(True),
               _atlas_states, "differentiable timesteps/sec (fwd+bwd), 1024-env Atlas w/ contact", 1024),
+    "atlas_mesh": ("Atlas 33-DoF (atlas_v3_no_head: 29 STL mesh colliders, the reference atlas_bench's model) "
+                   "+ ground, foot contact", lambda: models.atlas_mesh_world(True), _atlas_states,
+                   "differentiable timesteps/sec (fwd+bwd), 1024-env Atlas w/ contact, STL mesh colliders", 1024),
     "atlas_air": ("Atlas 33-DoF, no ground (contact-free)", lambda: models.atlas_world(False), _atlas_states,
                   "differentiable timesteps/sec (fwd+bwd), Atlas contact-free", 1024),
     "cartpole": ("cartpole, contact-free", models.cartpole_world, _atlas_states,

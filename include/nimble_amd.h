@@ -57,11 +57,13 @@ enum nimble_shape_type {
 /* Max contact points per world per step and LCP rows (3 per frictional
  * contact, dart/constraint/ContactConstraint.cpp:147 mDim = 3): the layout of
  * the snapshot and the LCP cache.  The device solves LCPs of up to
- * NIMBLE_MAX_SOLVED_LCP rows (one row per lane of a 64-lane wavefront); a
- * world with more rows is flagged NIMBLE_STATUS_LCP_TOO_LARGE. */
+ * NIMBLE_MAX_SOLVED_LCP rows: one row per lane of a 64-lane wavefront up to
+ * 64 rows, two per lane above (a second kernel takes those worlds), so every
+ * NIMBLE_MAX_LCP-row problem is solved; NIMBLE_STATUS_LCP_TOO_LARGE is kept
+ * for the layout's sake. */
 #define NIMBLE_MAX_CONTACTS 32
 #define NIMBLE_MAX_LCP (3 * NIMBLE_MAX_CONTACTS)
-#define NIMBLE_MAX_SOLVED_LCP 64
+#define NIMBLE_MAX_SOLVED_LCP 128
 
 /*
  * Flat description of a World (all skeletons of the world concatenated in

@@ -79,7 +79,7 @@ MAX_LCP = 3 * MAX_CONTACTS  # include/nimble_amd.h NIMBLE_MAX_LCP
 SN_FC = 16 + 13 * MAX_CONTACTS + 12 * MAX_LCP  # NIMBLE_SNAPSHOT_FC: clamping impulses f_c
 ST_CONTACT_OVERFLOW, ST_UNSUPPORTED_SHAPE, ST_DROPPED_OVERFLOW, ST_REDUCED, ST_LCP_TOO_LARGE = 1, 2, 4, 8, 16
 ST_DIVERGES = ST_CONTACT_OVERFLOW | ST_UNSUPPORTED_SHAPE | ST_DROPPED_OVERFLOW | ST_LCP_TOO_LARGE
-MAX_SOLVED_LCP = 64  # include/nimble_amd.h NIMBLE_MAX_SOLVED_LCP
+MAX_SOLVED_LCP = 128  # include/nimble_amd.h NIMBLE_MAX_SOLVED_LCP (two rows per lane above 64)
 
 
 class ContactCapacityError(RuntimeError):

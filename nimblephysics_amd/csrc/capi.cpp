@@ -31,6 +31,9 @@ struct nimble_world {
   Layout fwd, bwd;
   int snapDoubles = 8;
   int poolRows = 0, maxRows = 0;
+  // LCPs with more rows than this run in the two-rows-per-lane kernels
+  // (nimble_forward_wide_kernel / nimble_backward_wide_kernel)
+  int deferRows = 64;
   int jacWsDoubles = 0;  // per-workgroup LCP workspace of the Jacobian launch
   int cacheDoubles = NIMBLE_MAX_LCP + 1;
   hipFunction_t dummy = nullptr;
@@ -38,10 +41,15 @@ struct nimble_world {
 };
 
 extern "C" __global__ void nimble_forward_kernel(const ModelDev*, Layout, const double*, const double*, double*,
-                                                 double*, double*, int, int);
+                                                 double*, double*, int, int, int);
+extern "C" __global__ void nimble_forward_wide_kernel(const ModelDev*, Layout, const double*, const double*, double*,
+                                                      double*, double*, int, int);
 extern "C" __global__ void nimble_backward_kernel(const ModelDev*, int, const double*, const double*,
                                                   double*, int, const double*, double*, double*, int, double*, int,
-                                                  double*, int, int);
+                                                  double*, int, int, int);
+extern "C" __global__ void nimble_backward_wide_kernel(const ModelDev*, int, const double*, const double*,
+                                                       double*, int, const double*, double*, double*, int, double*,
+                                                       int, double*, int, int, int);
 
 static void isoInverse(const double* T, double* O) {
   // [R|p]^-1 = [R^T | -R^T p]
@@ -260,12 +268,18 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
     if (m.hasMesh) m.pairChunk = m.numPairs > 0 ? 1 : 0;
   }
   // max contacts: <= 8 box-box points per pair (a mesh pair: any number),
-  // <= NIMBLE_MAX_CONTACTS; LCP rows the device solves: 3 per contact, <=
-  // NIMBLE_MAX_SOLVED_LCP (more rows: NIMBLE_STATUS_LCP_TOO_LARGE)
+  // <= NIMBLE_MAX_CONTACTS; LCP rows: 3 per contact (> 64: the two-rows-per-
+  // lane kernels)
   int maxContacts = m.hasMesh ? NIMBLE_MAX_CONTACTS : 8 * m.numPairs;
   if (maxContacts > NIMBLE_MAX_CONTACTS) maxContacts = NIMBLE_MAX_CONTACTS;
   m.maxContacts = maxContacts;
   const int mcap = 3 * maxContacts < NIMBLE_MAX_SOLVED_LCP ? 3 * maxContacts : NIMBLE_MAX_SOLVED_LCP;
+  // NIMBLE_AMD_DEFER_ROWS (tests): a lower threshold sends smaller problems
+  // through the two-rows-per-lane kernels as well
+  if (const char* e = getenv("NIMBLE_AMD_DEFER_ROWS")) {
+    const int d = atoi(e);
+    if (d >= 0 && d < w->deferRows) w->deferRows = d;
+  }
   int fwdRows = ldsPoolRows(m, mcap);
   for (;;) {
     w->fwd = makeLayout(m, false, fwdRows);
@@ -300,7 +314,8 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
   w->maxRows = mcap;
   if (m.numPairs > 0) {
     int ws = 0;
-    if (mcap > poolRows) {
+    // (the two-rows-per-lane forward always works in HBM)
+    if (mcap > poolRows || mcap > w->deferRows) {
       const int a = fwdPoolDoublesHost(mcap, m.n), b = bwdPoolDoublesHost(mcap, m.n);
       ws = a > b ? a : b;
     }
@@ -376,10 +391,37 @@ int nimble_forward(nimble_world_t w, int32_t batch, const double* state, const d
     hipLaunchKernelGGL(nimble_forward_kernel, dim3(cnt), dim3(fwdThreads), lds, st, w->dev, w->fwd,
                        state + b0 * 2 * n, forces + b0 * n, lcp_cache + (size_t)b0 * w->cacheDoubles,
                        next_state + b0 * 2 * n, snapshot + (size_t)b0 * w->snapDoubles, w->snapDoubles,
-                       w->cacheDoubles);
+                       w->cacheDoubles, w->deferRows);
     HIP_TRY(hipGetLastError());
+    // the worlds whose LCP has more rows than one per lane (or than the
+    // test threshold): stepped by the two-rows-per-lane kernel
+    if (w->host.numPairs > 0 && w->maxRows > w->deferRows) {
+      hipLaunchKernelGGL(nimble_forward_wide_kernel, dim3(cnt), dim3(fwdThreads), lds, st, w->dev, w->fwd,
+                         state + b0 * 2 * n, forces + b0 * n, lcp_cache + (size_t)b0 * w->cacheDoubles,
+                         next_state + b0 * 2 * n, snapshot + (size_t)b0 * w->snapDoubles, w->snapDoubles,
+                         w->cacheDoubles);
+      HIP_TRY(hipGetLastError());
+    }
   }
   return NIMBLE_OK;
+}
+
+// the backward kernels: items of worlds with <= deferRows LCP rows, then (if
+// any world can have more) the two-rows-per-lane kernel for the others
+static hipError_t launchBackward(nimble_world_t w, int grid, hipStream_t st, int batch, const double* state,
+                                 const double* forces, double* snapshot, const double* gradNext, double* gradState,
+                                 double* gradForces, int rows, double* ws, int wsDoubles, double* gradMasses,
+                                 int fcMode, int massParams) {
+  const size_t lds = (size_t)w->bwd.total * sizeof(double);
+  hipLaunchKernelGGL(nimble_backward_kernel, dim3(grid), dim3(64), lds, st, w->dev, batch, state, forces, snapshot,
+                     w->snapDoubles, gradNext, gradState, gradForces, rows, ws, wsDoubles, gradMasses, fcMode,
+                     massParams, w->deferRows);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || w->host.numPairs == 0 || w->maxRows <= w->deferRows) return e;
+  hipLaunchKernelGGL(nimble_backward_wide_kernel, dim3(grid), dim3(64), lds, st, w->dev, batch, state, forces,
+                     snapshot, w->snapDoubles, gradNext, gradState, gradForces, rows, ws, wsDoubles, gradMasses,
+                     fcMode, massParams, w->deferRows);
+  return hipGetLastError();
 }
 
 int nimble_backward(nimble_world_t w, int32_t batch, const double* state, const double* forces,
@@ -390,11 +432,8 @@ int nimble_backward(nimble_world_t w, int32_t batch, const double* state, const 
   if (!state || !forces || !grad_next_state || !grad_state || !grad_forces || !snapshot)
     return fail(NIMBLE_ERR_INVALID, "null buffer");
   hipStream_t st = (hipStream_t)stream;
-  const size_t lds = (size_t)w->bwd.total * sizeof(double);
-  hipLaunchKernelGGL(nimble_backward_kernel, dim3(gridFor(batch)), dim3(64), lds, st, w->dev, batch, state,
-                     forces, snapshot, w->snapDoubles, grad_next_state, grad_state, grad_forces, 1, (double*)nullptr, 0,
-                     (double*)nullptr, 0, 1);
-  HIP_TRY(hipGetLastError());
+  HIP_TRY(launchBackward(w, gridFor(batch), st, batch, state, forces, snapshot, grad_next_state, grad_state,
+                        grad_forces, 1, nullptr, 0, nullptr, 0, 1));
   return NIMBLE_OK;
 }
 
@@ -406,11 +445,8 @@ int nimble_backward_masses(nimble_world_t w, int32_t batch, const double* state,
   if (!state || !forces || !grad_next_state || !grad_state || !grad_forces || !snapshot || !grad_masses)
     return fail(NIMBLE_ERR_INVALID, "null buffer");
   hipStream_t st = (hipStream_t)stream;
-  const size_t lds = (size_t)w->bwd.total * sizeof(double);
-  hipLaunchKernelGGL(nimble_backward_kernel, dim3(gridFor(batch)), dim3(64), lds, st, w->dev, batch, state,
-                     forces, snapshot, w->snapDoubles, grad_next_state, grad_state, grad_forces, 1, (double*)nullptr, 0,
-                     grad_masses, 0, 1);
-  HIP_TRY(hipGetLastError());
+  HIP_TRY(launchBackward(w, gridFor(batch), st, batch, state, forces, snapshot, grad_next_state, grad_state,
+                        grad_forces, 1, nullptr, 0, grad_masses, 0, 1));
   return NIMBLE_OK;
 }
 
@@ -422,11 +458,8 @@ int nimble_backward_inertia(nimble_world_t w, int32_t batch, const double* state
   if (!state || !forces || !grad_next_state || !grad_state || !grad_forces || !snapshot || !grad_inertia)
     return fail(NIMBLE_ERR_INVALID, "null buffer");
   hipStream_t st = (hipStream_t)stream;
-  const size_t lds = (size_t)w->bwd.total * sizeof(double);
-  hipLaunchKernelGGL(nimble_backward_kernel, dim3(gridFor(batch)), dim3(64), lds, st, w->dev, batch, state,
-                     forces, snapshot, w->snapDoubles, grad_next_state, grad_state, grad_forces, 1, (double*)nullptr, 0,
-                     grad_inertia, 0, 10);
-  HIP_TRY(hipGetLastError());
+  HIP_TRY(launchBackward(w, gridFor(batch), st, batch, state, forces, snapshot, grad_next_state, grad_state,
+                        grad_forces, 1, nullptr, 0, grad_inertia, 0, 10));
   return NIMBLE_OK;
 }
 
@@ -458,12 +491,9 @@ int nimble_jacobians(nimble_world_t w, int32_t batch, const double* state, const
   const long long items = (long long)batch * rows;
   const int grid = items < JAC_GRID ? (int)items : JAC_GRID;
   hipStream_t st = (hipStream_t)stream;
-  const size_t lds = (size_t)w->bwd.total * sizeof(double);
-  hipLaunchKernelGGL(nimble_backward_kernel, dim3(grid), dim3(64), lds, st, w->dev, batch, state, forces,
-                     const_cast<double*>(snapshot), w->snapDoubles, (const double*)nullptr, state_jacobian,
-                     force_jacobian, rows, w->jacWsDoubles > 0 ? workspace : (double*)nullptr, w->jacWsDoubles,
-                     (double*)nullptr, 0, 1);
-  HIP_TRY(hipGetLastError());
+  HIP_TRY(launchBackward(w, grid, st, batch, state, forces, const_cast<double*>(snapshot), nullptr, state_jacobian,
+                        force_jacobian, rows, w->jacWsDoubles > 0 ? workspace : nullptr, w->jacWsDoubles, nullptr, 0,
+                        1));
   return NIMBLE_OK;
 }
 
@@ -479,11 +509,8 @@ int nimble_constraint_force_jacobians(nimble_world_t w, int32_t batch, const dou
   const long long items = (long long)batch * rows;
   const int grid = items < JAC_GRID ? (int)items : JAC_GRID;
   hipStream_t st = (hipStream_t)stream;
-  const size_t lds = (size_t)w->bwd.total * sizeof(double);
-  hipLaunchKernelGGL(nimble_backward_kernel, dim3(grid), dim3(64), lds, st, w->dev, batch, state, forces,
-                     const_cast<double*>(snapshot), w->snapDoubles, (const double*)nullptr, dfc_dstate, dfc_dforces,
-                     rows, w->jacWsDoubles > 0 ? workspace : (double*)nullptr, w->jacWsDoubles, (double*)nullptr, 1, 1);
-  HIP_TRY(hipGetLastError());
+  HIP_TRY(launchBackward(w, grid, st, batch, state, forces, const_cast<double*>(snapshot), nullptr, dfc_dstate,
+                        dfc_dforces, rows, w->jacWsDoubles > 0 ? workspace : nullptr, w->jacWsDoubles, nullptr, 1, 1));
   return NIMBLE_OK;
 }
 

@@ -153,16 +153,17 @@ __device__ void codQrRegs(typename Space<kLds>::dptr A, Cod& c, typename Space<k
   }
 }
 
-// Lane-parallel factorisation: column norms live in registers (lane j =
-// column j), the pivot is a wave arg-max (first index among equal maxima, as
-// the sequential scan), alpha and |v|^2 are wave reductions, and the
-// reflector pass (lane = column) also recomputes the next step's partial
-// column norms (same sums as a fresh recomputation).  Requires n <= 64.
-// Factorises the m x n matrix A (leading dimension ld) in place; ws is the
-// carveCod workspace, v a further m doubles of scratch.
-template <bool kLds>
-__device__ void codFactor(typename Space<kLds>::dptr Ain, typename Space<kLds>::dptr wsIn, int m_, int n_, int ld_,
-                          typename Space<kLds>::dptr vIn, int lane, double* prof = nullptr) {
+// Lane-parallel factorisation: column norms live in registers (column j on
+// lane j & 63, slot j >> 6; R = 2 for the 65..128-column clamping sets), the
+// pivot is a wave arg-max (first index among equal maxima, as the sequential
+// scan), alpha and |v|^2 are wave reductions, and the reflector pass (lane =
+// column) also recomputes the next step's partial column norms (same sums as
+// a fresh recomputation).  Factorises the m x n matrix A (leading dimension
+// ld, n <= 64 R) in place; ws is the carveCod workspace, v a further m
+// doubles of scratch.
+template <bool kLds, int R>
+__device__ void codFactorR(typename Space<kLds>::dptr Ain, typename Space<kLds>::dptr wsIn, int m_, int n_, int ld_,
+                           typename Space<kLds>::dptr vIn, int lane, double* prof = nullptr) {
 #ifdef NIMBLE_STAGE_TIMING
   const long long tc0 = (long long)__builtin_amdgcn_s_memtime();
 #else
@@ -175,7 +176,7 @@ __device__ void codFactor(typename Space<kLds>::dptr Ain, typename Space<kLds>::
   const int m = c.m, n = c.n, ld = c.ld;
   double maxPivot = 0.0;
 #ifndef NIMBLE_COD_LDS_ONLY
-  if (m <= 24) {
+  if (m <= 24 && n <= 64) {
     WSYNC();
     codQrRegs<kLds, 24>(Ain, c, vIn, lane);
     WSYNC();
@@ -183,69 +184,104 @@ __device__ void codFactor(typename Space<kLds>::dptr Ain, typename Space<kLds>::
   }
 #endif
   {
-  if (lane < n) c.perm[lane] = lane;
-  double norm = 0.0;  // partial norm of column `lane` over rows >= k
-  if (lane < n) {
+  double norm[R];  // partial norm of column `row` over rows >= k
+#pragma unroll
+  for (int s = 0; s < R; s++) {
+    const int j = rowAt(s, lane);
+    norm[s] = 0.0;
+    if (j < n) {
+      c.perm[j] = j;
 #pragma unroll 8
-    for (int i = 0; i < m; i++) norm += A[i * ld + lane] * A[i * ld + lane];
+      for (int i = 0; i < m; i++) norm[s] += A[i * ld + j] * A[i * ld + j];
+    }
   }
   WSYNC();
   for (int k = 0; k < c.kmax; k++) {
     // pivot: largest remaining norm, lowest index on ties
-    const double cand = (lane >= k && lane < n) ? norm : -1.0;
-    const double best = -waveMin(-cand);
-    const int p = waveFirst(lane >= k && lane < n && cand == best);
+    double cand[R], neg[R];
+#pragma unroll
+    for (int s = 0; s < R; s++) {
+      const int j = rowAt(s, lane);
+      cand[s] = (j >= k && j < n) ? norm[s] : -1.0;
+      neg[s] = -cand[s];
+    }
+    const double best = -waveMinR(neg);
+    bool isBest[R];
+#pragma unroll
+    for (int s = 0; s < R; s++) isBest[s] = rowAt(s, lane) >= k && rowAt(s, lane) < n && cand[s] == best;
+    const int p = waveFirstR(isBest);
     if (p != k) {
       for (int i = lane; i < m; i += WAVE) {
         const double t = A[i * ld + k]; A[i * ld + k] = A[i * ld + p]; A[i * ld + p] = t;
       }
-      const double nk = rdl(norm, k), np = rdl(norm, p);
-      if (lane == k) norm = np;
-      else if (lane == p) norm = nk;
+      const double nk = rdlR(norm, k), np = rdlR(norm, p);
+      setR(norm, k, lane, np);
+      setR(norm, p, lane, nk);
       if (lane == 0) { int t = c.perm[k]; c.perm[k] = c.perm[p]; c.perm[p] = t; }
     }
     WSYNC();
     const double akk = A[k * ld + k];
-    const double colv = (lane >= k && lane < m) ? A[lane * ld + k] : 0.0;
-    double alpha = sqrt(waveSum(colv * colv));
+    double colv[R], sq[R];
+#pragma unroll
+    for (int s = 0; s < R; s++) {
+      const int i = rowAt(s, lane);
+      colv[s] = (i >= k && i < m) ? A[i * ld + k] : 0.0;
+      sq[s] = colv[s] * colv[s];
+    }
+    double alpha = sqrt(waveSumR(sq));
     if (alpha == 0.0) {
       if (lane == 0) c.vn[k] = -1.0;
       // fresh norms of the remaining columns over rows >= k+1
-      if (lane > k && lane < n) {
-        double nrm = 0.0;
+#pragma unroll
+      for (int s = 0; s < R; s++) {
+        const int j = rowAt(s, lane);
+        if (j > k && j < n) {
+          double nrm = 0.0;
 #pragma unroll 8
-        for (int i = k + 1; i < m; i++) nrm += A[i * ld + lane] * A[i * ld + lane];
-        norm = nrm;
+          for (int i = k + 1; i < m; i++) nrm += A[i * ld + j] * A[i * ld + j];
+          norm[s] = nrm;
+        }
       }
       WSYNC();
       continue;
     }
     if (akk > 0) alpha = -alpha;
-    const double vi = (lane == k) ? colv - alpha : colv;
-    if (lane >= k && lane < m) v[lane] = vi;
-    const double vnorm = waveSum(vi * vi);
+    double vi[R];
+#pragma unroll
+    for (int s = 0; s < R; s++) {
+      const int i = rowAt(s, lane);
+      vi[s] = (i == k) ? colv[s] - alpha : colv[s];
+      if (i >= k && i < m) v[i] = vi[s];
+      sq[s] = vi[s] * vi[s];
+    }
+    const double vnorm = waveSumR(sq);
     WSYNC();
-    if (lane >= k && lane < n) {
-      double nrm = 0.0;
-      if (vnorm > 0) {
-        double sc = 0;
+#pragma unroll
+    for (int s = 0; s < R; s++) {
+      const int j = rowAt(s, lane);
+      if (j >= k && j < n) {
+        double nrm = 0.0;
+        if (vnorm > 0) {
+          double sc = 0;
 #pragma unroll 8
-        for (int i = k; i < m; i++) sc += v[i] * A[i * ld + lane];
-        sc = 2 * sc / vnorm;
+          for (int i = k; i < m; i++) sc += v[i] * A[i * ld + j];
+          sc = 2 * sc / vnorm;
 #pragma unroll 8
-        for (int i = k; i < m; i++) {
-          const double a = A[i * ld + lane] - sc * v[i];
-          A[i * ld + lane] = a;
-          if (i > k) nrm += a * a;
+          for (int i = k; i < m; i++) {
+            const double a = A[i * ld + j] - sc * v[i];
+            A[i * ld + j] = a;
+            if (i > k) nrm += a * a;
+          }
+        } else {
+#pragma unroll 8
+          for (int i = k + 1; i < m; i++) nrm += A[i * ld + j] * A[i * ld + j];
         }
-      } else {
-#pragma unroll 8
-        for (int i = k + 1; i < m; i++) nrm += A[i * ld + lane] * A[i * ld + lane];
+        norm[s] = nrm;
       }
-      norm = nrm;
     }
     WSYNC();
-    if (lane > k && lane < m) A[lane * ld + k] = v[lane];
+    for (int i = lane; i < m; i += WAVE)
+      if (i > k) A[i * ld + k] = v[i];
     if (lane == 0) { c.vd[k] = v[k]; c.vn[k] = vnorm; }
     WSYNC();
   }
@@ -254,18 +290,32 @@ rankAndRz:
 #ifdef NIMBLE_STAGE_TIMING
   const long long tc1 = (long long)__builtin_amdgcn_s_memtime();
 #endif
-  // max |R_kk| and rank = #{|R_kk| > eps * kmax * max|R_kk|}, lane k = R_kk
-  const double dkk = lane < c.kmax ? fabs(A[lane * ld + lane]) : 0.0;
-  maxPivot = -waveMin(-dkk);
+  // max |R_kk| and rank = #{|R_kk| > eps * kmax * max|R_kk|}, row k = R_kk
+  double dkk[R], ndkk[R];
+#pragma unroll
+  for (int s = 0; s < R; s++) {
+    const int k = rowAt(s, lane);
+    dkk[s] = k < c.kmax ? fabs(A[k * ld + k]) : 0.0;
+    ndkk[s] = -dkk[s];
+  }
+  maxPivot = -waveMinR(ndkk);
   const double thr = 2.220446049250313e-16 * c.kmax * maxPivot;
-  const int r = __popcll(__ballot(lane < c.kmax && dkk > thr));
+  int r = 0;
+#pragma unroll
+  for (int s = 0; s < R; s++) r += __popcll(__ballot(rowAt(s, lane) < c.kmax && dkk[s] > thr));
   if (lane == 0) *c.rank = r;
   // RZ: reflect row i over columns {i} U {r..n-1}; row i's trailing part is
   // kept as the reflector
   for (int i = r - 1; i >= 0 && r < n; i--) {
     const double aii = unid(A[i * ld + i]);
-    const double tj = (lane >= r && lane < n) ? A[i * ld + lane] : 0.0;
-    const double tail = waveSum(tj * tj);
+    double tj[R];
+#pragma unroll
+    for (int s = 0; s < R; s++) {
+      const int j = rowAt(s, lane);
+      const double t = (j >= r && j < n) ? A[i * ld + j] : 0.0;
+      tj[s] = t * t;
+    }
+    const double tail = waveSumR(tj);
     double al = sqrt(aii * aii + tail);
     if (aii > 0) al = -al;
     const double vi = aii - al;
@@ -294,4 +344,10 @@ rankAndRz:
     prof[2] = r;
   }
 #endif
+}
+
+template <bool kLds>
+__device__ void codFactor(typename Space<kLds>::dptr Ain, typename Space<kLds>::dptr wsIn, int m_, int n_, int ld_,
+                          typename Space<kLds>::dptr vIn, int lane, double* prof = nullptr) {
+  codFactorR<kLds, 1>(Ain, wsIn, m_, n_, ld_, vIn, lane, prof);
 }

@@ -469,6 +469,8 @@ __device__ __forceinline__ void collideWait(double* ct, int want) {
 #define ST_DROPPED_OVERFLOW 4
 #define ST_DUPLICATE_COLUMNS 8  // LCPUtils::reduce merged columns (reference behaviour)
 #define ST_LCP_TOO_LARGE 16     // more LCP rows than the wave solves (NIMBLE_MAX_SOLVED_LCP)
+#define ST_DEFERRED 32          // (internal) the world's LCP has more rows than the one-row-per-lane
+                                // kernel takes: the two-rows-per-lane kernel steps it
 
 // row record fields
 #define RR_CONTACT 0
@@ -761,7 +763,7 @@ __device__ inline double rowForceEntry(const ModelDev& md, const double* s, cons
 // Q = A_cc + A_cu E + cfm I  (== A_c^T Minv A_c_ub_E + cfm I).
 // Returns the standardized flag (wave-uniform).
 // ---------------------------------------------------------------------------
-template <bool kLds>
+template <bool kLds, int R = 1>
 __device__ bool devConstruct(typename Space<kLds>::dptr poolIn, int m, int n, double cfm, bool ignoreFriction,
                              lds_double* ctIn, int lane, double* g_stamp = nullptr) {
   (void)g_stamp;
@@ -773,59 +775,90 @@ __device__ bool devConstruct(typename Space<kLds>::dptr poolIn, int m, int n, do
 #ifdef NIMBLE_STAGE_TIMING
     if (lane == 0 && g_stamp) g_stamp[60] += 1;
 #endif
-    // Lane-parallel classification (lane = row j < m <= 64).  Whether a row
-    // clamps depends on its own data and X[findex] only; a row bounded by
-    // its friction parent additionally needs the parent's clamping flag
-    // (ballot bit), and the clamping / upper-bound indices are the rows'
-    // ranks among their kind (popcounts), which is the sequential loop's
-    // numbering.
+    // Row-parallel classification (row j < m on lane j & 63, slot j >> 6).
+    // Whether a row clamps depends on its own data and X[findex] only; a
+    // row bounded by its friction parent additionally needs the parent's
+    // clamping flag (ballot bit), and the clamping / upper-bound indices are
+    // the rows' ranks among their kind (popcounts), which is the sequential
+    // loop's numbering.
     {
       const double TH = 1e-6, tie = 1e-5;
-      const bool live = lane < m;
-      const double f = live ? P.X[lane] : 0.0;
-      const double hiJ = live ? P.hi[lane] : 0.0, loJ = live ? P.lo[lane] : 0.0;
-      const int fp = live ? P.fi[lane] : -1;
-      const bool colOk = live && P.aCol[lane] >= 1e-9;
-      const double xfp = (live && fp != -1) ? P.X[fp] : 1.0;
-      const double up = hiJ * xfp, low = loJ * xfp;
-      bool clampR = false, ubCand = false;
-      if (colOk) {
-        if (fabs(f) < TH) {
-          clampR = fp != -1 && !(fabs(xfp) < TH) && !ignoreFriction;
-        } else if ((f > low + tie && f < up - tie) || (low - f > 1e-2 || f - up > 1e-2)) {
-          clampR = true;
-        } else if (fp != -1 && fabs(xfp) > 1e-9 && P.aCol[fp] > 1e-9) {
-          ubCand = true;
+      bool clampR[R], ubCand[R], live[R];
+      double f[R], hiJ[R], loJ[R], up[R], low[R];
+      int fp[R];
+      unsigned long long cm[R], um[R];
+#pragma unroll
+      for (int s = 0; s < R; s++) {
+        const int j = rowAt(s, lane);
+        live[s] = j < m;
+        f[s] = live[s] ? P.X[j] : 0.0;
+        hiJ[s] = live[s] ? P.hi[j] : 0.0;
+        loJ[s] = live[s] ? P.lo[j] : 0.0;
+        fp[s] = live[s] ? P.fi[j] : -1;
+        const bool colOk = live[s] && P.aCol[j] >= 1e-9;
+        const double xfp = (live[s] && fp[s] != -1) ? P.X[fp[s]] : 1.0;
+        up[s] = hiJ[s] * xfp;
+        low[s] = loJ[s] * xfp;
+        clampR[s] = false;
+        ubCand[s] = false;
+        if (colOk) {
+          if (fabs(f[s]) < TH) {
+            clampR[s] = fp[s] != -1 && !(fabs(xfp) < TH) && !ignoreFriction;
+          } else if ((f[s] > low[s] + tie && f[s] < up[s] - tie) || (low[s] - f[s] > 1e-2 || f[s] - up[s] > 1e-2)) {
+            clampR[s] = true;
+          } else if (fp[s] != -1 && fabs(xfp) > 1e-9 && P.aCol[fp[s]] > 1e-9) {
+            ubCand[s] = true;
+          }
+        }
+        cm[s] = __ballot(clampR[s]);
+      }
+      bool ubR[R];
+#pragma unroll
+      for (int s = 0; s < R; s++) {
+        ubR[s] = ubCand[s] && (fp[s] > rowAt(s, lane) || bitR(cm, fp[s] >= 0 ? fp[s] : 0));
+        um[s] = __ballot(ubR[s]);
+      }
+#pragma unroll
+      for (int s = 0; s < R; s++) {
+        const int j = rowAt(s, lane);
+        const int cIdx = clampR[s] ? rankR(cm, j) : -1;
+        const int uIdx = ubR[s] ? rankR(um, j) : -1;
+        if (live[s]) {
+          P.mapping[j] = clampR[s] ? CM_CLAMPING : (ubR[s] ? fp[s] : CM_NOT_CLAMPING);
+          P.clampIdx[j] = cIdx;
+          P.ubIdx[j] = uIdx;
+          P.Eval[j] = ubR[s] ? (fabs(f[s] - up[s]) < fabs(f[s] - low[s]) ? hiJ[s] : loJ[s]) : 0.0;
+          if (clampR[s]) {
+            P.fc[cIdx] = f[s];
+            P.relVel[cIdx] = P.b[j];
+            P.clampRow[cIdx] = j;
+          }
         }
       }
-      const unsigned long long cm = __ballot(clampR);
-      const bool ubR = ubCand && (fp > lane || ((cm >> (fp & 63)) & 1ull));
-      const unsigned long long um = __ballot(ubR);
-      const unsigned long long below = (1ull << lane) - 1ull;
-      const int cIdx = clampR ? __popcll(cm & below) : -1;
-      const int uIdx = ubR ? __popcll(um & below) : -1;
-      if (live) {
-        P.mapping[lane] = clampR ? CM_CLAMPING : (ubR ? fp : CM_NOT_CLAMPING);
-        P.clampIdx[lane] = cIdx;
-        P.ubIdx[lane] = uIdx;
-        P.Eval[lane] = ubR ? (fabs(f - up) < fabs(f - low) ? hiJ : loJ) : 0.0;
-        if (clampR) {
-          P.fc[cIdx] = f;
-          P.relVel[cIdx] = P.b[lane];
-          P.clampRow[cIdx] = lane;
-        }
-      }
-      if (lane == 0) { ct[H_NC] = __popcll(cm); ct[H_NU] = __popcll(um); }
+      if (lane == 0) { ct[H_NC] = popR(cm); ct[H_NU] = popR(um); }
     }
     WSYNC();
     TACC_END(61, tCls);
     const int nc = uni((int)ct[H_NC]);
-    const double bR = lane < m ? P.b[lane] : 0.0, hiR = lane < m ? P.hi[lane] : 0.0;
-    const double loR = lane < m ? P.lo[lane] : 0.0;
-    const int fiR = lane < m ? P.fi[lane] : -1;
+    double bR[R], hiR[R], loR[R];
+    int fiR[R];
+#pragma unroll
+    for (int s = 0; s < R; s++) {
+      const int j = rowAt(s, lane);
+      bR[s] = j < m ? P.b[j] : 0.0;
+      hiR[s] = j < m ? P.hi[j] : 0.0;
+      loR[s] = j < m ? P.lo[j] : 0.0;
+      fiR[s] = j < m ? P.fi[j] : -1;
+    }
     if (nc == 0) {
-      const bool ok = waveLcpValid<kLds>(m, spc<kLds>(P.A), cfm, 0.0, bR, hiR, loR, fiR, ignoreFriction, lane);
-      if (ok && lane < m) P.X[lane] = 0.0;
+      double zero[R];
+#pragma unroll
+      for (int s = 0; s < R; s++) zero[s] = 0.0;
+      const bool ok = waveLcpValidR<kLds, R>(m, spc<kLds>(P.A), cfm, zero, bR, hiR, loR, fiR, ignoreFriction, lane);
+      if (ok)
+#pragma unroll
+        for (int s = 0; s < R; s++)
+          if (rowAt(s, lane) < m) P.X[rowAt(s, lane)] = 0.0;
       WSYNC();
       return ok;
     }
@@ -851,45 +884,57 @@ __device__ bool devConstruct(typename Space<kLds>::dptr poolIn, int m, int n, do
     double* vv = w; w += m;
     double* rhs = w; w += m;
     double* z = w; w += m;
+    (void)cn;
     STAMP(41);
     TACC_END(62, tQ);
     TACC_BEGIN(tF);
 #ifdef NIMBLE_STAGE_TIMING
-    codFactor<kLds>(sp<kLds>(Q), sp<kLds>(P.scr), nc, nc, nc, sp<kLds>(vv), lane, g_stamp ? g_stamp + 67 : nullptr);
+    codFactorR<kLds, R>(sp<kLds>(Q), sp<kLds>(P.scr), nc, nc, nc, sp<kLds>(vv), lane, g_stamp ? g_stamp + 67 : nullptr);
 #else
-    codFactor<kLds>(sp<kLds>(Q), sp<kLds>(P.scr), nc, nc, nc, sp<kLds>(vv), lane);
+    codFactorR<kLds, R>(sp<kLds>(Q), sp<kLds>(P.scr), nc, nc, nc, sp<kLds>(vv), lane);
 #endif
     if (lane == 0) ct[H_CODOK] = 1;
     STAMP(42);
     TACC_END(63, tF);
     TACC_BEGIN(tS);
     {
-      const double f = codSolveWave<kLds>(sp<kLds>(Q), sp<kLds>(P.scr), nc, nc, nc, lane < nc ? P.relVel[lane] : 0.0,
-                                          sp<kLds>(z), lane);
-      if (lane < nc) P.fsol[lane] = f;
+      double rv[R], fs[R];
+#pragma unroll
+      for (int s = 0; s < R; s++) rv[s] = rowAt(s, lane) < nc ? P.relVel[rowAt(s, lane)] : 0.0;
+      codSolveWaveR<kLds, R>(sp<kLds>(Q), sp<kLds>(P.scr), nc, nc, nc, rv, sp<kLds>(z), lane, fs);
+#pragma unroll
+      for (int s = 0; s < R; s++)
+        if (rowAt(s, lane) < nc) P.fsol[rowAt(s, lane)] = fs[s];
     }
     STAMP(43);
     TACC_END(64, tS);
     TACC_BEGIN(tN);
     (void)rhs;
     WSYNC();
+    double nxR[R];
     {
-      // lane-parallel: new x from the clamping solution
+      // row-parallel: new x from the clamping solution
       bool newlyNot = false;
-      if (lane < m) {
-        double v = 0.0;
-        const int ci = P.clampIdx[lane];
-        if (ci != -1) {
-          v = P.fsol[ci];
-          newlyNot = fabs(v) < 1e-6 && fabs(P.X[lane]) > 1e-6 && P.fi[lane] == -1;
+#pragma unroll
+      for (int s = 0; s < R; s++) {
+        const int j = rowAt(s, lane);
+        nxR[s] = 0.0;
+        if (j < m) {
+          double v = 0.0;
+          const int ci = P.clampIdx[j];
+          if (ci != -1) {
+            v = P.fsol[ci];
+            newlyNot = newlyNot || (fabs(v) < 1e-6 && fabs(P.X[j]) > 1e-6 && P.fi[j] == -1);
+          }
+          if (P.ubIdx[j] != -1) {
+            const int pc = P.clampIdx[P.fi[j]];
+            const double hiJ = P.hi[j], loJ = P.lo[j];
+            const double om = P.fc[pc] / P.X[j];
+            v = P.fsol[pc] * (fabs(om - hiJ) < fabs(om - loJ) ? hiJ : loJ);
+          }
+          P.nx[j] = v;
+          nxR[s] = v;
         }
-        if (P.ubIdx[lane] != -1) {
-          const int pc = P.clampIdx[P.fi[lane]];
-          const double hiJ = P.hi[lane], loJ = P.lo[lane];
-          const double om = P.fc[pc] / P.X[lane];
-          v = P.fsol[pc] * (fabs(om - hiJ) < fabs(om - loJ) ? hiJ : loJ);
-        }
-        P.nx[lane] = v;
       }
       const bool anyNewlyNot = __ballot(newlyNot) != 0ull;
       if (lane == 0) ct[H_FLAG] = anyNewlyNot ? 1 : 0;
@@ -897,14 +942,17 @@ __device__ bool devConstruct(typename Space<kLds>::dptr poolIn, int m, int n, do
     WSYNC();
     TACC_END(65, tN);
     TACC_BEGIN(tV);
-    const bool ok =
-        waveLcpValid<kLds>(m, spc<kLds>(P.A), cfm, lane < m ? P.nx[lane] : 0.0, bR, hiR, loR, fiR, ignoreFriction, lane);
+    const bool ok = waveLcpValidR<kLds, R>(m, spc<kLds>(P.A), cfm, nxR, bR, hiR, loR, fiR, ignoreFriction, lane);
     const int res = ok ? (uni((int)ct[H_FLAG]) ? 2 : 1) : 0;
     STAMP(44);
     TACC_END(66, tV);
     if (ok) {
-      if (lane < m) P.X[lane] = P.nx[lane];
-      if (lane < nc) P.fc[lane] = P.fsol[lane];
+#pragma unroll
+      for (int s = 0; s < R; s++) {
+        const int j = rowAt(s, lane);
+        if (j < m) P.X[j] = P.nx[j];
+        if (j < nc) P.fc[j] = P.fsol[j];
+      }
     }
     WSYNC();
     if (res != 2) return res != 0;
@@ -914,7 +962,7 @@ __device__ bool devConstruct(typename Space<kLds>::dptr poolIn, int m, int n, do
 
 // guessSolution (LCPUtils.cpp:69): COD solve on {normal rows with b > 0} U
 // {friction rows}; result into x.
-template <bool kLds>
+template <bool kLds, int R = 1>
 __device__ void devGuess(typename Space<kLds>::dptr poolIn, int m, int n, lds_double* ctIn, int lane) {
   FwdPool P;
   carveFwd((double*)poolIn, m, n, P);
@@ -942,11 +990,16 @@ __device__ void devGuess(typename Space<kLds>::dptr poolIn, int m, int n, lds_do
   double* rhs = w; w += m;
   double* z = w; w += m;
   double* xr = w; w += m;
-  codFactor<kLds>(sp<kLds>(Ar), sp<kLds>(P.scr), k, k, k, sp<kLds>(vv), lane);
+  (void)cn;
+  codFactorR<kLds, R>(sp<kLds>(Ar), sp<kLds>(P.scr), k, k, k, sp<kLds>(vv), lane);
   {
-    const double xr_ = codSolveWave<kLds>(sp<kLds>(Ar), sp<kLds>(P.scr), k, k, k, lane < k ? P.b[P.cl[lane]] : 0.0,
-                                          sp<kLds>(z), lane);
-    if (lane < k) x[P.cl[lane]] = xr_;
+    double rv[R], xo[R];
+#pragma unroll
+    for (int s = 0; s < R; s++) rv[s] = rowAt(s, lane) < k ? P.b[P.cl[rowAt(s, lane)]] : 0.0;
+    codSolveWaveR<kLds, R>(sp<kLds>(Ar), sp<kLds>(P.scr), k, k, k, rv, sp<kLds>(z), lane, xo);
+#pragma unroll
+    for (int s = 0; s < R; s++)
+      if (rowAt(s, lane) < k) x[P.cl[rowAt(s, lane)]] = xo[s];
   }
   (void)rhs; (void)xr;
   WSYNC();
@@ -957,7 +1010,7 @@ __device__ void devGuess(typename Space<kLds>::dptr poolIn, int m, int n, lds_do
 // matrices it uses), computed here where A = J Minv J^T is on chip:
 // A_c, A_c_ub_E, Q = A_c^T Minv A_c_ub_E + cfm I, pinv(Q) (COD) and the
 // rank-deficiency flag ||I - Q Q^+||^2 >= 1e-18.
-template <bool kLds>
+template <bool kLds, int R = 1>
 __device__ void backwardPrecompute(const ModelDev& md, lds_double* sIn, const Layout& L, int lane,
                                    typename Space<kLds>::dptr poolIn, int m, double cfm, double* snap, lds_double* ctIn) {
   const int n = md.n;
@@ -1015,13 +1068,14 @@ __device__ void backwardPrecompute(const ModelDev& md, lds_double* sIn, const La
   double* cn = w; w += m;
   double* vv = w; w += m;
   STAMP(48);
-  if (!reuse) codFactor<kLds>(sp<kLds>(P.M1), sp<kLds>(P.scr), nc, nc, nc, sp<kLds>(vv), lane);
+  if (!reuse) codFactorR<kLds, R>(sp<kLds>(P.M1), sp<kLds>(P.scr), nc, nc, nc, sp<kLds>(vv), lane);
   STAMP(49);
-  // pinv(Q): lane c solves Q x = e_c in place in row c of the (now free) A region
+  // pinv(Q): lane c solves Q x = e_c in place in row c of the (now free) A
+  // region (columns c, c + 64, .. when n_c > 64)
   double* Zs = P.A;
-  if (lane < nc) {
-    double* rhs = Zs + lane * nc;
-    for (int i = 0; i < nc; i++) rhs[i] = i == lane ? 1.0 : 0.0;
+  for (int col = lane; col < nc; col += WAVE) {
+    double* rhs = Zs + col * nc;
+    for (int i = 0; i < nc; i++) rhs[i] = i == col ? 1.0 : 0.0;
     const double* F = cod.A;
     for (int k = 0; k < cod.kmax; k++) {
       const double vnorm = cod.vn[k];
@@ -1048,8 +1102,8 @@ __device__ void backwardPrecompute(const ModelDev& md, lds_double* sIn, const La
       rhs[i] -= sc * cod.zd[i];
       for (int j = r; j < nc; j++) rhs[j] -= sc * F[i * nc + j];
     }
-    // column `lane` of pinv(Q) = row `lane` of pinv(Q)^T
-    for (int j = 0; j < nc; j++) PTG[lane * nc + cod.perm[j]] = rhs[j];
+    // column `col` of pinv(Q) = row `col` of pinv(Q)^T
+    for (int j = 0; j < nc; j++) PTG[col * nc + cod.perm[j]] = rhs[j];
   }
   WSYNC();
   STAMP(50);
@@ -1074,16 +1128,20 @@ __device__ void backwardPrecompute(const ModelDev& md, lds_double* sIn, const La
 // fallbacks, impulses (v1 += Minv J^T x), warm-start cache and snapshot.
 // `Lm` is the Cholesky factor of M (lower triangle, n x n).
 // ---------------------------------------------------------------------------
-template <bool kLds>
+template <bool kLds, int R>
 __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, const Layout& L, int lane,
                                            lds_double* v1In, const lds_double* ddqIn, double* cache, double* snap,
                                            typename Space<kLds>::dptr poolIn, int nCon, int m, bool helperOn);
 
 // inlined into the forward kernel: the model, layout and LDS base keep their
-// kernel-argument provenance (scalar loads, LDS instructions)
-__device__ __forceinline__ void contactStage(const ModelDev& md, double* s, const Layout& L, int lane, double* v1,
+// kernel-argument provenance (scalar loads, LDS instructions).  R row slots
+// per lane (R = 1: <= 64 LCP rows).  A world with more than `deferRows` rows
+// is left to the R = 2 kernel (status ST_DEFERRED, nothing else of the step
+// written, the warm-start cache untouched): returns true then.
+template <int R>
+__device__ __forceinline__ bool contactStage(const ModelDev& md, double* s, const Layout& L, int lane, double* v1,
                                              const double* ddq, double* cache, double* snap, double* overflowWs,
-                                             bool helperOn, bool collided) {
+                                             bool helperOn, bool collided, int deferRows) {
   const int n = md.n;
   s = lds<true>(s);
   snap = gbl(snap);
@@ -1113,7 +1171,7 @@ __device__ __forceinline__ void contactStage(const ModelDev& md, double* s, cons
       snap[SN_STATUS] = ct[H_STATUS];
     }
     WSYNC();
-    return;
+    return false;
   }
   // row count: 3 rows per frictional contact, 1 otherwise (lane = contact)
   bool fr = false;
@@ -1122,7 +1180,12 @@ __device__ __forceinline__ void contactStage(const ModelDev& md, double* s, cons
     fr = fmin(md.friction[(int)rec[8]], md.friction[(int)rec[9]]) > 1e-3;
   }
   const int m = nCon + 2 * __popcll(__ballot(fr));
-  if (m > NIMBLE_MAX_SOLVED_LCP) {
+  if (m > deferRows) {
+    if (lane == 0) snap[SN_STATUS] = (double)((int)ct[H_STATUS] | ST_DEFERRED);
+    WSYNC();
+    return true;
+  }
+  if (m > 64 * R) {
     // more rows than one wave's lanes: the contacts are recorded, the solve
     // is not taken (flagged; the snapshot says no rows, so the backward and
     // the Jacobians see a contact-free step)
@@ -1135,20 +1198,22 @@ __device__ __forceinline__ void contactStage(const ModelDev& md, double* s, cons
       cache[0] = -1.0;
     }
     WSYNC();
-    return;
+    return false;
   }
   if (lane == 0) ct[H_M] = m;  // read by the helper wave
   // the LCP workspace is in LDS when it fits the pool (the common case, LDS
-  // instructions throughout), else in the world's HBM snapshot tail
-  if (fwdPoolDoubles(m, n) <= L.poolCap)
-    contactLcp<true>(md, sp<true>(s), L, lane, sp<true>(v1), spc<true>(ddq), cache, snap, sp<true>(s + L.pool), nCon,
-                     m, helperOn);
+  // instructions throughout), else in the world's HBM snapshot tail (always
+  // for the wide problems of R = 2)
+  if (R == 1 && fwdPoolDoubles(m, n) <= L.poolCap)
+    contactLcp<true, 1>(md, sp<true>(s), L, lane, sp<true>(v1), spc<true>(ddq), cache, snap, sp<true>(s + L.pool),
+                        nCon, m, helperOn);
   else
-    contactLcp<false>(md, sp<true>(s), L, lane, sp<true>(v1), spc<true>(ddq), cache, snap, overflowWs, nCon, m,
-                      false);
+    contactLcp<false, R>(md, sp<true>(s), L, lane, sp<true>(v1), spc<true>(ddq), cache, snap, overflowWs, nCon, m,
+                         false);
+  return false;
 }
 
-template <bool kLds>
+template <bool kLds, int R>
 __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, const Layout& L, int lane,
                                            lds_double* v1In, const lds_double* ddqIn, double* cache, double* snap,
                                            typename Space<kLds>::dptr poolIn, int nCon, int m, bool helperOn) {
@@ -1169,14 +1234,16 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   // rows (ContactConstraint: normal + 2 tangents with friction), lane =
   // contact; a contact's first row is its rank among the rows of the
   // contacts before it (popcount of the frictional ones)
-  if (lane < nCon) {
+  {
     const int c = lane;
-    const double* rec = ct + CT_CONTACTS + c * CREC;
+    const bool live = c < nCon;
+    const double* rec = ct + CT_CONTACTS + (live ? c : 0) * CREC;
     const int ba = (int)rec[8], bb = (int)rec[9];
     const double mu = fmin(md.friction[ba], md.friction[bb]);
     const double restC = md.restitution[ba] * md.restitution[bb];
-    const bool fr = mu > 1e-3;
-    const unsigned long long frm = __ballot(fr);
+    const bool fr = live && mu > 1e-3;
+    const unsigned long long frm = __ballot(fr);  // (the whole wave: cross-lane ops stay out of divergent code)
+    if (live) {
     int r = c + 2 * __popcll(frm & ((1ull << c) - 1ull));
     const int base = r;
     P.rowC[r] = c; P.rowDir[r] = 0;
@@ -1193,6 +1260,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
         P.lo[r] = -mu; P.hi[r] = mu; P.fi[r] = base; P.rest[r] = 0.0;
         r++;
       }
+    }
     }
   }
   WSYNC();
@@ -1284,7 +1352,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
     for (int i = lane; i < m; i += WAVE) { P.X[i] = cache[1 + i]; P.xc[i] = cache[1 + i]; }
     WSYNC();
   } else {
-    devGuess<kLds>(poolIn, m, n, sp<true>(ct), lane);
+    devGuess<kLds, R>(poolIn, m, n, sp<true>(ct), lane);
     for (int i = lane; i < m; i += WAVE) P.xc[i] = P.X[i];
     WSYNC();
   }
@@ -1295,9 +1363,9 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   const bool tasked = kLds && helperOn;
   if (tasked) helperPost(ct, HS_TASK, lane);
 #ifdef NIMBLE_STAGE_TIMING
-  bool success = devConstruct<kLds>(poolIn, m, n, 0.0, false, sp<true>(ct), lane, g_stamp);
+  bool success = devConstruct<kLds, R>(poolIn, m, n, 0.0, false, sp<true>(ct), lane, g_stamp);
 #else
-  bool success = devConstruct<kLds>(poolIn, m, n, 0.0, false, sp<true>(ct), lane);
+  bool success = devConstruct<kLds, R>(poolIn, m, n, 0.0, false, sp<true>(ct), lane);
 #endif
   if (tasked && success && lane == 0)
     __hip_atomic_store(helperFlags(ct) + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1305,42 +1373,76 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   const bool shortCircuit = success;
   double cfm = 0.0;
   bool ignoredFriction = false;
-  const double bR = lane < m ? P.b[lane] : 0.0, hiR = lane < m ? P.hi[lane] : 0.0;
-  const double loR = lane < m ? P.lo[lane] : 0.0;
-  const int fiR = lane < m ? P.fi[lane] : -1;
+  // the problem's row-held vectors (row j on lane j & 63, slot j >> 6)
+  double bR[R], hiR[R], loR[R];
+  int fiR[R];
+#pragma unroll
+  for (int q = 0; q < R; q++) {
+    const int j = rowAt(q, lane);
+    bR[q] = j < m ? P.b[j] : 0.0;
+    hiR[q] = j < m ? P.hi[j] : 0.0;
+    loR[q] = j < m ? P.lo[j] : 0.0;
+    fiR[q] = j < m ? P.fi[j] : -1;
+  }
+  auto fullMask = [&](unsigned long long (&mk)[R]) {
+#pragma unroll
+    for (int q = 0; q < R; q++) {
+      const int lo64 = 64 * q;
+      mk[q] = m >= lo64 + 64 ? ~0ull : (m > lo64 ? ((1ull << (m - lo64)) - 1ull) : 0ull);
+    }
+  };
+  auto sameMask = [&](const unsigned long long (&a)[R], const unsigned long long (&b)[R]) {
+    bool eq = true;
+#pragma unroll
+    for (int q = 0; q < R; q++) eq = eq && a[q] == b[q];
+    return eq;
+  };
+  // x_d[row] = x_r[reduced index of rep[row]]
+  auto mapOut = [&](const double (&xr)[R], const unsigned long long (&alive)[R], const int (&rep)[R],
+                    double (&xd)[R]) {
+#pragma unroll
+    for (int q = 0; q < R; q++) xd[q] = gatherR(xr, rankR(alive, rep[q]));
+  };
   if (!success) {
     // Dantzig on the reduced problem (BoxedLcpConstraintSolver.cpp:466-521):
     // LCPUtils::reduce merges near-duplicate columns; when it merges any, the
     // reduced matrix (in M1, free here) goes to Dantzig and the solution is
     // mapped out (x_i = x_r[rank(rep_i)]); validity on the full problem
     if (lane == 0) ct[H_CODOK] = 0;
-    double scl;
-    int rep;
-    const unsigned long long full = m >= 64 ? ~0ull : ((1ull << m) - 1ull);
-    const unsigned long long alive = waveReduce<kLds>(m, spc<kLds>(P.A), 0.0, bR, loR, hiR, fiR, lane, scl, rep);
+    double scl[R];
+    int rep[R];
+    unsigned long long full[R], alive[R];
+    fullMask(full);
+    waveReduceR<kLds, R>(m, spc<kLds>(P.A), 0.0, bR, loR, hiR, fiR, lane, scl, rep, alive);
     WSYNC();
-    double xd = 0.0;
+    double xd[R];
+#pragma unroll
+    for (int q = 0; q < R; q++) xd[q] = 0.0;
     bool ok;
-    if (alive != full) {
+    if (!sameMask(alive, full)) {
       if (lane == 0) ct[H_STATUS] = (double)((int)ct[H_STATUS] | ST_DUPLICATE_COLUMNS);
-      double br = bR, lr = loR, hr = hiR;
-      int fr = fiR, act;
-      const int mr = reducedVectors(alive, rep, lane, br, lr, hr, fr, act);
-      reducedMatrix<kLds>(m, spc<kLds>(P.A), 0.0, alive, act, scl, sp<kLds>(P.M1), false, lane);
-      double xr = 0.0;
-      ok = waveDantzig<kLds>(mr, spc<kLds>(P.M1), sp<kLds>(P.M2), sp<kLds>(P.scr), xr, br, lr, hr, fr, lane);
-      xd = __shfl(xr, reducedIndex(alive, rep));
+      double br[R], lr[R], hr[R], xr[R];
+      int fr[R], act[R];
+#pragma unroll
+      for (int q = 0; q < R; q++) { br[q] = bR[q]; lr[q] = loR[q]; hr[q] = hiR[q]; fr[q] = fiR[q]; }
+      const int mr = reducedVectorsR<R>(alive, rep, lane, br, lr, hr, fr, act);
+      reducedMatrixR<kLds, R>(m, spc<kLds>(P.A), 0.0, alive, act, scl, sp<kLds>(P.M1), false, lane);
+      ok = waveDantzigR<kLds, R>(mr, spc<kLds>(P.M1), sp<kLds>(P.M2), sp<kLds>(P.scr), xr, br, lr, hr, fr, lane);
+      mapOut(xr, alive, rep, xd);
     } else {
 #ifdef NIMBLE_STAGE_TIMING
-      ok = waveDantzig<kLds>(m, spc<kLds>(P.A), sp<kLds>(P.M2), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane, g_stamp + 52);
+      ok = waveDantzigR<kLds, R>(m, spc<kLds>(P.A), sp<kLds>(P.M2), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane,
+                                 g_stamp + 52);
 #else
-      ok = waveDantzig<kLds>(m, spc<kLds>(P.A), sp<kLds>(P.M2), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane);
+      ok = waveDantzigR<kLds, R>(m, spc<kLds>(P.A), sp<kLds>(P.M2), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane);
 #endif
     }
     if (ok) {
-      if (lane < m) P.X[lane] = xd;
+#pragma unroll
+      for (int q = 0; q < R; q++)
+        if (rowAt(q, lane) < m) P.X[rowAt(q, lane)] = xd[q];
       WSYNC();
-      ok = waveLcpValid<kLds>(m, spc<kLds>(P.A), 0.0, xd, bR, hiR, loR, fiR, false, lane);
+      ok = waveLcpValidR<kLds, R>(m, spc<kLds>(P.A), 0.0, xd, bR, hiR, loR, fiR, false, lane);
     }
     success = ok;
   }
@@ -1349,72 +1451,120 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
     bool ok = success;
     bool ign = false;
     double cf = 0.0;
-    double X = lane < m ? P.X[lane] : 0.0;
-    if (__ballot(lane < m && isnan(X))) { ok = false; X = 0.0; }
+    double X[R];
+    bool nan = false;
+#pragma unroll
+    for (int q = 0; q < R; q++) {
+      X[q] = rowAt(q, lane) < m ? P.X[rowAt(q, lane)] : 0.0;
+      nan = nan || (rowAt(q, lane) < m && isnan(X[q]));
+    }
+    if (__ballot(nan)) {
+      ok = false;
+#pragma unroll
+      for (int q = 0; q < R; q++) X[q] = 0.0;
+    }
     if (!ok) {
       cf = md.fallbackCfm;
       if (lane == 0) ct[H_CODOK] = 0;
-      double xd;
+      double xd[R];
       // PGS on the reduced A + cfm I (BoxedLcpConstraintSolver.cpp:550-597);
       // the helper wave's speculative PGS is the unreduced solve, used when
       // reduce merges nothing
-      double scl;
-      int rep;
-      const unsigned long long full = m >= 64 ? ~0ull : ((1ull << m) - 1ull);
-      const unsigned long long alive = waveReduce<kLds>(m, spc<kLds>(P.A), cf, bR, loR, hiR, fiR, lane, scl, rep);
+      double scl[R];
+      int rep[R];
+      unsigned long long full[R], alive[R];
+      fullMask(full);
+      waveReduceR<kLds, R>(m, spc<kLds>(P.A), cf, bR, loR, hiR, fiR, lane, scl, rep, alive);
       WSYNC();
-      if (alive != full) {
+      if (!sameMask(alive, full)) {
         if (lane == 0) ct[H_STATUS] = (double)((int)ct[H_STATUS] | ST_DUPLICATE_COLUMNS);
-        double br = bR, lr = loR, hr = hiR;
-        int fr = fiR, act;
-        const int mr = reducedVectors(alive, rep, lane, br, lr, hr, fr, act);
-        reducedMatrix<kLds>(m, spc<kLds>(P.A), cf, alive, act, scl, sp<kLds>(P.M1), true, lane);
-        double xr = __shfl(lane < m ? P.xc[lane] : 0.0, lane < mr ? act : 0);
-        if (lane >= mr) xr = 0.0;
-        ok = wavePgs<kLds>(mr, spc<kLds>(P.M1), xr, br, lr, hr, fr, lane, nullptr, 0.0);
-        xd = __shfl(xr, reducedIndex(alive, rep));
-      } else if (tasked) {
+        double br[R], lr[R], hr[R], xc[R], xr[R];
+        int fr[R], act[R];
+#pragma unroll
+        for (int q = 0; q < R; q++) {
+          br[q] = bR[q]; lr[q] = loR[q]; hr[q] = hiR[q]; fr[q] = fiR[q];
+          xc[q] = rowAt(q, lane) < m ? P.xc[rowAt(q, lane)] : 0.0;
+        }
+        const int mr = reducedVectorsR<R>(alive, rep, lane, br, lr, hr, fr, act);
+        reducedMatrixR<kLds, R>(m, spc<kLds>(P.A), cf, alive, act, scl, sp<kLds>(P.M1), true, lane);
+#pragma unroll
+        for (int q = 0; q < R; q++) {
+          xr[q] = gatherR(xc, rowAt(q, lane) < mr ? act[q] : 0);
+          if (rowAt(q, lane) >= mr) xr[q] = 0.0;
+        }
+        ok = wavePgsR<kLds, false, R>(mr, spc<kLds>(P.M1), xr, br, lr, hr, fr, lane, nullptr, 0.0);
+        mapOut(xr, alive, rep, xd);
+      } else if (R == 1 && tasked) {
         helperWait(ct, [](int st) { return st == HS_MID || st == HS_DONE; });
-        xd = lane < m ? P.xh[lane] : 0.0;
+        xd[0] = lane < m ? P.xh[lane] : 0.0;
         ok = uni(helperFlags(ct)[2]) != 0;
       } else {
-        xd = lane < m ? P.xc[lane] : 0.0;
+#pragma unroll
+        for (int q = 0; q < R; q++) xd[q] = rowAt(q, lane) < m ? P.xc[rowAt(q, lane)] : 0.0;
 #ifdef NIMBLE_STAGE_TIMING
-        ok = wavePgs<kLds>(m, spc<kLds>(P.A), xd, bR, loR, hiR, fiR, lane, g_stamp + 54, cf);
+        ok = wavePgsR<kLds, false, R>(m, spc<kLds>(P.A), xd, bR, loR, hiR, fiR, lane, g_stamp + 54, cf);
 #else
-        ok = wavePgs<kLds>(m, spc<kLds>(P.A), xd, bR, loR, hiR, fiR, lane, nullptr, cf);
+        ok = wavePgsR<kLds, false, R>(m, spc<kLds>(P.A), xd, bR, loR, hiR, fiR, lane, nullptr, cf);
 #endif
       }
       if (ok) {
-        X = xd;
-        ok = waveLcpValid<kLds>(m, spc<kLds>(P.A), cf, X, bR, hiR, loR, fiR, false, lane);
+#pragma unroll
+        for (int q = 0; q < R; q++) X[q] = xd[q];
+        ok = waveLcpValidR<kLds, R>(m, spc<kLds>(P.A), cf, X, bR, hiR, loR, fiR, false, lane);
       }
     }
     if (!ok) {
       // LCPUtils::removeFriction + PGS on the normal rows only (the principal
       // submatrix of A + cfm I over them, read in place)
       ign = true;
-      const bool keepMe = lane < m && fiR == -1;
-      const unsigned long long km = __ballot(keepMe);
-      const int k2 = __popcll(km);
-      const int pos = __popcll(km & ((1ull << lane) - 1ull));
-      if (tasked) {
+      bool keepMe[R];
+      unsigned long long km[R];
+#pragma unroll
+      for (int q = 0; q < R; q++) {
+        keepMe[q] = rowAt(q, lane) < m && fiR[q] == -1;
+        km[q] = __ballot(keepMe[q]);
+      }
+      const int k2 = popR(km);
+      if (R == 1 && tasked) {
         helperWait(ct, [](int st) { return st == HS_DONE; });
       } else {
-        int myRow = 0;
+        int myRow[R];
+#pragma unroll
+        for (int q = 0; q < R; q++) myRow[q] = 0;
         for (int t = 0, c = 0; t < m; t++)
-          if ((km >> t) & 1ull) { if (lane == c) myRow = t; c++; }
-        double xr = 0.0;
-        wavePgs<kLds, true>(k2, spc<kLds>(P.A), xr, lane < k2 ? P.b[myRow] : 0.0, lane < k2 ? P.lo[myRow] : 0.0,
-                      lane < k2 ? P.hi[myRow] : 0.0, -1, lane, nullptr, cf, nullptr, m, myRow);
-        if (lane < k2) P.xh2[lane] = xr;
+          if (bitR(km, t)) { setRi(myRow, c, lane, t); c++; }
+        double xr[R], br[R], lr[R], hr[R];
+        int fr[R];
+#pragma unroll
+        for (int q = 0; q < R; q++) {
+          const bool in = rowAt(q, lane) < k2;
+          xr[q] = 0.0;
+          br[q] = in ? P.b[myRow[q]] : 0.0;
+          lr[q] = in ? P.lo[myRow[q]] : 0.0;
+          hr[q] = in ? P.hi[myRow[q]] : 0.0;
+          fr[q] = -1;
+        }
+        wavePgsR<kLds, true, R>(k2, spc<kLds>(P.A), xr, br, lr, hr, fr, lane, nullptr, cf, nullptr, m, myRow);
+#pragma unroll
+        for (int q = 0; q < R; q++)
+          if (rowAt(q, lane) < k2) P.xh2[rowAt(q, lane)] = xr[q];
         WSYNC();
       }
-      X = 0.0;
-      if (keepMe) X = P.xh2[pos];
+#pragma unroll
+      for (int q = 0; q < R; q++) {
+        X[q] = 0.0;
+        if (keepMe[q]) X[q] = P.xh2[rankR(km, rowAt(q, lane))];
+      }
     }
-    if (__ballot(lane < m && isnan(X))) X = 0.0;
-    if (lane < m) P.X[lane] = X;
+    bool nan2 = false;
+#pragma unroll
+    for (int q = 0; q < R; q++) nan2 = nan2 || (rowAt(q, lane) < m && isnan(X[q]));
+    if (__ballot(nan2))
+#pragma unroll
+      for (int q = 0; q < R; q++) X[q] = 0.0;
+#pragma unroll
+    for (int q = 0; q < R; q++)
+      if (rowAt(q, lane) < m) P.X[rowAt(q, lane)] = X[q];
     if (lane == 0) { ct[H_CFM] = cf; ct[H_IGN] = ign ? 1 : 0; }
     WSYNC();
   }
@@ -1427,7 +1577,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   if (!shortCircuit) {
     for (int i = lane; i < m; i += WAVE) P.xc[i] = P.X[i];
     WSYNC();
-    std2 = devConstruct<kLds>(poolIn, m, n, cfm, ignoredFriction, sp<true>(ct), lane);
+    std2 = devConstruct<kLds, R>(poolIn, m, n, cfm, ignoredFriction, sp<true>(ct), lane);
   }
   const double* Xf = std2 ? P.X : P.xc;
   STAMP(8);
@@ -1467,7 +1617,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   const int nc = uni((int)ct[H_NC]);
   for (int i = lane; i < nc; i += WAVE) snap[SN_FC + i] = P.fc[i];
   for (int i = lane; i < n; i += WAVE) snap[snYf(n) + i] = ddq[i];
-  backwardPrecompute<kLds>(md, sIn, md.lay[0], lane, poolIn, m, cfm, snap, sp<true>(ct));  // (not inlined)
+  backwardPrecompute<kLds, R>(md, sIn, md.lay[0], lane, poolIn, m, cfm, snap, sp<true>(ct));  // (not inlined)
   if (lane == 0) {
     snap[SN_NCON] = nCon;
     snap[SN_M] = m;
@@ -1635,6 +1785,7 @@ __device__ void tangentBasisGradient(const double* nrm, const double* g, double*
 // On return (all lanes): s[L.x] = a*, s[L.w] = w - nu, NV columns hold the
 // M-derivative pairs and mu; P.gRows / P.TAB the per-row vectors of the
 // G_j terms.  Returns the imprecise flag.
+template <int R = 1>
 __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& L, int lane, const double* sn,
                                    BwdPool& P, int m, int nc, double* ct, int fcRow) {
   const int n = md.n;
@@ -1778,21 +1929,33 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
   // per-row vectors g_j (lane = dof i, rows wave-uniform).  Each row's map,
   // clamping index and E value are loaded once, lane = row, and read back
   // with readlane: no dependent snapshot loads inside the row loop.
-  int rMap = CM_NOT_CLAMPING, rC = 0;
-  double rE = 0.0;
-  if (lane < m) {
-    const double* rr = rows + lane * SN_ROWREC;
-    rMap = (int)rr[RR_MAP];
-    if (rMap == CM_CLAMPING) rC = (int)rr[RR_CIDX];
-    else if (rMap >= 0) { rC = (int)rows[rMap * SN_ROWREC + RR_CIDX]; rE = rr[RR_EVAL]; }
+  int rMap[R], rC[R];
+  double rE[R];
+#pragma unroll
+  for (int q = 0; q < R; q++) {
+    const int j = rowAt(q, lane);
+    rMap[q] = CM_NOT_CLAMPING;
+    rC[q] = 0;
+    rE[q] = 0.0;
+    if (j < m) {
+      const double* rr = rows + j * SN_ROWREC;
+      rMap[q] = (int)rr[RR_MAP];
+      if (rMap[q] == CM_CLAMPING) rC[q] = (int)rr[RR_CIDX];
+      else if (rMap[q] >= 0) { rC[q] = (int)rows[rMap[q] * SN_ROWREC + RR_CIDX]; rE[q] = rr[RR_EVAL]; }
+    }
   }
-  for (int i = lane; i < n; i += WAVE) {
-    const double* nv = P.NV + i * NV_COLS;
+  // (lane = dof i: n <= NIMBLE_MAX_DOFS = 64, one dof per lane; the row
+  // reads stay outside the lane-divergent part)
+  {
+    const int i = lane;
+    const bool live = i < n;
+    const double* nv = P.NV + (live ? i : 0) * NV_COLS;
     const double w = nv[NV_W], sg = nv[NV_SIGMA], ka = nv[NV_KAPPA], ma1 = nv[NV_MA1], mar = nv[NV_MARHO];
-    const double ma2 = nv[NV_MA2], map = nv[NV_MAPI], vf = sn[SN_VF + i];
+    const double ma2 = nv[NV_MA2], map = nv[NV_MAPI], vf = sn[SN_VF + (live ? i : 0)];
     for (int j = 0; j < m; j++) {
-      const int mp = rdli(rMap, j);
-      const int c = rdli(rC, j);
+      const int mp = rdliR(rMap, j);
+      const int c = rdliR(rC, j);
+      const double e = rdlR(rE, j);
       double g = 0.0;
       if (mp == CM_CLAMPING) {
         g = P.fc[c] * w - P.beta[c] * vf - P.lam[c] * sg - P.xq[c] * ka;
@@ -1800,41 +1963,51 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
       } else if (mp >= 0) {
         double inner = P.fc[c] * w - P.xq[c] * ka;
         if (imp) inner += P.rho[c] * ma1 + P.piv[c] * ma2;
-        g = rdl(rE, j) * inner;
+        g = e * inner;
       }
-      P.gRows[j * n + i] = g;
+      if (live) P.gRows[j * n + i] = g;
     }
   }
   WSYNC();
-  // T_A(g_j), T_B(g_j): lane = (row, side), summed over the dofs that move
-  // any contact body (the others have weight 0 for every lane)
+  // T_A(g_j), T_B(g_j): lane = (row, side) -- 2m of them, in passes of 64 --
+  // summed over the dofs that move any contact body (the others have weight
+  // 0 for every lane)
   {
-    const int t = lane;
-    int body = -1;
-    if (t < 2 * m) {
+    auto bodyOf = [&](int t) {
+      if (t >= 2 * m) return -1;
       const double* rec = sn + SN_CONTACTS + (int)rows[(t >> 1) * SN_ROWREC + RR_CONTACT] * CREC;
-      body = (int)rec[8 + (t & 1)];
+      return (int)rec[8 + (t & 1)];
+    };
+    // union over all rows of the ancestor sets
+    unsigned long long anAll = 0ull;
+    for (int t = lane; t < 2 * m; t += WAVE) {
+      const int body = bodyOf(t);
+      if (body >= 0) anAll |= md.anc[body];
     }
-    const unsigned long long an = body >= 0 ? md.anc[body] : 0ull;
-    // union over the wave of the ancestor sets
-    unsigned lo = (unsigned)an, hi = (unsigned)(an >> 32);
+    unsigned lo = (unsigned)anAll, hi = (unsigned)(anAll >> 32);
     for (int o = 32; o >= 1; o >>= 1) {
       lo |= __shfl_xor(lo, o);
       hi |= __shfl_xor(hi, o);
     }
     const unsigned long long all = ((unsigned long long)uni((int)hi) << 32) | (unsigned)uni((int)lo);
-    unsigned long long dm = ancestorDofMask(md, all, lane);
-    double T[6] = {0, 0, 0, 0, 0, 0};
-    const double* g = P.gRows + (t < 2 * m ? (t >> 1) : 0) * n;
-    while (dm) {
-      const int r = __ffsll((long long)dm) - 1;
-      dm &= dm - 1ull;
-      // bodyTwist's arithmetic: fma(S_r, g_r, T) for the ancestor dofs
-      const double gr = ((an >> md.dofBody[r]) & 1ull) ? g[r] : 0.0;
-      for (int i = 0; i < 6; i++) T[i] = fma(s[L.Sw + 6 * r + i], gr, T[i]);
+    const unsigned long long dmAll = ancestorDofMask(md, all, lane);
+    for (int t0 = 0; t0 < 2 * m; t0 += WAVE) {
+      const int t = t0 + lane;
+      const int body = bodyOf(t);
+      const unsigned long long an = body >= 0 ? md.anc[body] : 0ull;
+      unsigned long long dm = dmAll;
+      double T[6] = {0, 0, 0, 0, 0, 0};
+      const double* g = P.gRows + (t < 2 * m ? (t >> 1) : 0) * n;
+      while (dm) {
+        const int r = __ffsll((long long)dm) - 1;
+        dm &= dm - 1ull;
+        // bodyTwist's arithmetic: fma(S_r, g_r, T) for the ancestor dofs
+        const double gr = ((an >> md.dofBody[r]) & 1ull) ? g[r] : 0.0;
+        for (int i = 0; i < 6; i++) T[i] = fma(s[L.Sw + 6 * r + i], gr, T[i]);
+      }
+      if (t < 2 * m)
+        for (int i = 0; i < 6; i++) P.TAB[(t >> 1) * 12 + (t & 1) * 6 + i] = T[i];
     }
-    if (t < 2 * m)
-      for (int i = 0; i < 6; i++) P.TAB[(t >> 1) * 12 + (t & 1) * 6 + i] = T[i];
   }
   WSYNC();
   STAMP(38);
@@ -2289,6 +2462,7 @@ __device__ double edgeRowTerm(const ModelDev& md, const BwdPool& P, int j, const
 //     (the Z_w term only when |Z_w| > 1e-6, DifferentiableContactConstraint.cpp:328);
 //   face side        per row (tangent-basis gradient, ContactConstraint.cpp:772).
 // `ws` is workspace of 6 n + 6 nb + 16 doubles.  Returns the lane's sum.
+template <int R = 1>
 __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& L, const double* sn,
                                    const BwdPool& P, int m, const double* Z, double* ws, int lane,
                                    double* g_stamp = nullptr) {
@@ -2315,36 +2489,48 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
     hi |= __shfl_xor(hi, o);
   }
   const unsigned long long dofBodies = ((unsigned long long)uni((int)hi) << 32) | (unsigned)uni((int)lo);
-  // row data, lane j < m, loaded once from the snapshot; the loops below
-  // read them by readlane instead of chains of dependent memory loads
-  int rMap = CM_NOT_CLAMPING, rA = 0, rB = 0, rTyp = 0, rDir = 0, rCon = 0;
-  double rp[3] = {0, 0, 0}, rd[3] = {0, 0, 0}, rn[3] = {0, 0, 0};
-  if (lane < m) {
-    const double* rr = rows + lane * SN_ROWREC;
-    rMap = (int)rr[RR_MAP];
-    rDir = (int)rr[RR_DIR];
-    rCon = (int)rr[RR_CONTACT];
-    const double* rec = sn + SN_CONTACTS + rCon * CREC;
-    rA = (int)rec[8]; rB = (int)rec[9]; rTyp = (int)rec[7];
-    for (int i = 0; i < 3; i++) { rp[i] = rec[i]; rn[i] = rec[3 + i]; rd[i] = rr[RR_D + i]; }
+  // row data, row j < m on lane j & 63 (slot j >> 6), loaded once from the
+  // snapshot; the loops below read them by readlane instead of chains of
+  // dependent memory loads
+  int rMap[R], rA[R], rB[R], rTyp[R], rDir[R], rCon[R];
+  double rp[3][R], rd[3][R], rn[3][R];
+  unsigned long long liveRows[R];
+#pragma unroll
+  for (int q = 0; q < R; q++) {
+    const int j = rowAt(q, lane);
+    rMap[q] = CM_NOT_CLAMPING; rA[q] = 0; rB[q] = 0; rTyp[q] = 0; rDir[q] = 0; rCon[q] = 0;
+    for (int i = 0; i < 3; i++) { rp[i][q] = 0.0; rd[i][q] = 0.0; rn[i][q] = 0.0; }
+    if (j < m) {
+      const double* rr = rows + j * SN_ROWREC;
+      rMap[q] = (int)rr[RR_MAP];
+      rDir[q] = (int)rr[RR_DIR];
+      rCon[q] = (int)rr[RR_CONTACT];
+      const double* rec = sn + SN_CONTACTS + rCon[q] * CREC;
+      rA[q] = (int)rec[8]; rB[q] = (int)rec[9]; rTyp[q] = (int)rec[7];
+      for (int i = 0; i < 3; i++) { rp[i][q] = rec[i]; rn[i][q] = rec[3 + i]; rd[i][q] = rr[RR_D + i]; }
+    }
+    liveRows[q] = __ballot(j < m && rMap[q] != CM_NOT_CLAMPING);
   }
-  const unsigned long long liveRows = __ballot(lane < m && rMap != CM_NOT_CLAMPING);
   for (int j0 = 0; j0 < m; j0++) {
-    if (!((liveRows >> j0) & 1ull)) continue;
+    if (!bitR(liveRows, j0)) continue;
     for (int side = 0; side < 2; side++) {
-      const int c = side ? rdli(rB, j0) : rdli(rA, j0);
+      const int c = side ? rdliR(rB, j0) : rdliR(rA, j0);
       if ((done >> c) & 1ull) continue;
       done |= 1ull << c;
       if (!(md.anc[c] & dofBodies)) continue;
       // omega^c_r (lane r), vertex sums (lanes over rows), all for body c
       TACC_BEGIN(tO);
       double om[6] = {0, 0, 0, 0, 0, 0};
-      const unsigned long long rowsC = __ballot(((liveRows >> lane) & 1ull) && (rA == c || rB == c));
-      for (unsigned long long bits = rowsC; bits; bits &= bits - 1ull) {
-        const int j = __ffsll((long long)bits) - 1;
-        const double sg = rdli(rA, j) == c ? 1.0 : -1.0;
+      unsigned long long rowsC[R];
+#pragma unroll
+      for (int q = 0; q < R; q++) rowsC[q] = __ballot(((liveRows[q] >> lane) & 1ull) && (rA[q] == c || rB[q] == c));
+#pragma unroll
+      for (int q = 0; q < R; q++)
+      for (unsigned long long bits = rowsC[q]; bits; bits &= bits - 1ull) {
+        const int j = 64 * q + __ffsll((long long)bits) - 1;
+        const double sg = rdliR(rA, j) == c ? 1.0 : -1.0;
         double p[3], d[3];
-        for (int i = 0; i < 3; i++) { p[i] = rdl(rp[i], j); d[i] = rdl(rd[i], j); }
+        for (int i = 0; i < 3; i++) { p[i] = rdlR(rp[i], j); d[i] = rdlR(rd[i], j); }
         double wr[6];
         cross3(p, d, wr);
         wr[3] = d[0]; wr[4] = d[1]; wr[5] = d[2];
@@ -2357,15 +2543,23 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
       // vertex sides of c's rows (lane = row), summed over the wave
       {
         double uvl[6] = {0, 0, 0, 0, 0, 0};
-        const int type = rTyp & 15;
-        const bool vertexSide = ((rowsC >> lane) & 1ull) &&
-                                ((type == CT_VERTEX_FACE && rA == c) || (type == CT_FACE_VERTEX && rB == c));
-        if (vertexSide) {
-          double tw[3], dxt[3], pxd[3];
-          for (int i = 0; i < 3; i++) tw[i] = P.TAB[lane * 12 + i] - P.TAB[lane * 12 + 6 + i];
-          cross3(rd, tw, dxt);
-          cross3(rp, dxt, pxd);
-          for (int i = 0; i < 3; i++) { uvl[i] = dxt[i]; uvl[3 + i] = pxd[i]; }
+#pragma unroll
+        for (int q = 0; q < R; q++) {
+          const int type = rTyp[q] & 15;
+          const bool vertexSide = ((rowsC[q] >> lane) & 1ull) && ((type == CT_VERTEX_FACE && rA[q] == c) ||
+                                                                   (type == CT_FACE_VERTEX && rB[q] == c));
+          if (vertexSide) {
+            const int j = rowAt(q, lane);
+            double tw[3], dxt[3], pxd[3], dj[3], pj[3];
+            for (int i = 0; i < 3; i++) {
+              tw[i] = P.TAB[j * 12 + i] - P.TAB[j * 12 + 6 + i];
+              dj[i] = rd[i][q];
+              pj[i] = rp[i][q];
+            }
+            cross3(dj, tw, dxt);
+            cross3(pj, dxt, pxd);
+            for (int i = 0; i < 3; i++) { uvl[i] += dxt[i]; uvl[3 + i] += pxd[i]; }
+          }
         }
         double uvs[6];
         for (int i = 0; i < 6; i++) uvs[i] = waveSum(uvl[i]);
@@ -2419,13 +2613,19 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
   }
   // face side: per row
   TACC_BEGIN(tF);
-  if (k < n) {
-    for (unsigned long long bits = liveRows; bits; bits &= bits - 1ull) {
-      const int j = __ffsll((long long)bits) - 1;
-      const int A = rdli(rA, j), B = rdli(rB, j), type = rdli(rTyp, j) & 15;
+  {
+    // (the rows' readlanes for every lane; the terms for the lanes k < n)
+#pragma unroll
+    for (int q = 0; q < R; q++)
+    for (unsigned long long bits = liveRows[q]; bits; bits &= bits - 1ull) {
+      const int j = 64 * q + __ffsll((long long)bits) - 1;
+      const int A = rdliR(rA, j), B = rdliR(rB, j), type = rdliR(rTyp, j) & 15;
+      const int con = rdliR(rCon, j), dirIdx = rdliR(rDir, j);
+      double p[3], nrm[3];
+      for (int i = 0; i < 3; i++) { p[i] = rdlR(rp[i], j); nrm[i] = rdlR(rn[i], j); }
+      if (k >= n) continue;
       if (type >= CT_EDGE_EDGE) {
         const double* rr = rows + j * SN_ROWREC;
-        const int con = rdli(rCon, j);
         const double* rec = sn + SN_CONTACTS + con * CREC;
         if (type == CT_EDGE_EDGE) acc += edgeRowTerm(md, P, j, rec, rr, sn + snEdge(n) + con * EDGE_REC, Z, bk, A, B);
         else if (type == CT_SPHERE_SPHERE)
@@ -2443,13 +2643,10 @@ __device__ double contactGTermsAll(const ModelDev& md, double* s, const Layout& 
       if (type == CT_VERTEX_FACE) faceBody = B;
       else if (type == CT_FACE_VERTEX) faceBody = A;
       if (faceBody < 0 || !((md.anc[faceBody] >> bk) & 1ull)) continue;
-      double p[3], nrm[3];
-      for (int i = 0; i < 3; i++) { p[i] = rdl(rp[i], j); nrm[i] = rdl(rn[i], j); }
       double dn[3];
       const double wv[3] = {Z[0], Z[1], Z[2]};
       cross3(wv, nrm, dn);
       double dd[3];
-      const int dirIdx = rdli(rDir, j);
       if (dirIdx == 0 || dot3(dn, dn) <= 1e-12) {
         for (int i = 0; i < 3; i++) dd[i] = dn[i];
       } else {

@@ -1,5 +1,7 @@
 // Wave-parallel LCP kernels for one world per 64-lane wave.  Vectors of the
-// (<= 48-row) LCP live one element per lane in registers, matrices in LDS;
+// LCP live row-distributed in registers (row i on lane i & 63, slot i >> 6:
+// R = 1 slot for <= 64 rows, R = 2 for the 65..128-row problems), matrices
+// in LDS (or the world's HBM workspace);
 // the sequential structure of the reference algorithms (pivot order, sweep
 // order, tie-breaking) is kept exactly, only the inner vector work is spread
 // over the lanes:
@@ -10,6 +12,8 @@
 //   * waveLcpValid  LCPUtils::isLCPSolutionValid (LCPUtils.cpp:14)
 //   * codSolveWave  COD min-norm solve on a codFactor()ed matrix
 // All functions must be entered by the whole wave (uniform control flow).
+// The *R templates take the row-distributed arrays; the scalar forms are
+// their R = 1 instances.
 #pragma once
 #include "wave.cuh"
 #include "cod_wave.cuh"
@@ -39,320 +43,504 @@
 // principal submatrix A[idx][idx] of a matrix with leading dimension ld
 // (lane j holds idx_j), read in place (LCPUtils::removeFriction without a
 // gathered copy).
-template <bool kLds, bool kMapped = false>
-__device__ bool wavePgs(int n, typename Space<kLds>::cdptr Ain, double& x, double b, double lo, double hi, int findex,
-                        int lane, double* dbg = nullptr, double shift = 0.0, const int* cancel = nullptr, int ld = -1,
-                        int idx = -1) {
+template <bool kLds, bool kMapped, int R>
+__device__ bool wavePgsR(int n, typename Space<kLds>::cdptr Ain, double (&x)[R], const double (&bIn)[R],
+                         const double (&lo)[R], const double (&hi)[R], const int (&findex)[R], int lane,
+                         double* dbg = nullptr, double shift = 0.0, const int* cancel = nullptr, int ld = -1,
+                         const int* idxIn = nullptr) {
   n = uni(n);
   if (n == 0) return true;
   ld = kMapped ? uni(ld) : n;
-  if (!kMapped) idx = lane;
+  int idx[R];
+  double b[R];
+#pragma unroll
+  for (int s = 0; s < R; s++) {
+    idx[s] = kMapped ? idxIn[s] : rowAt(s, lane);
+    b[s] = bIn[s];
+  }
   const double* A = (const double*)Ain;
   const double deltaXThr = 1e-6, relTol = 1e-3, epsDiv = 1e-9;
 #ifdef LCP_PROFILE
   const long long tp0 = (long long)__builtin_amdgcn_s_memtime();
 #endif
-  const bool act = lane < n;
-  const int col = act ? idx : rdli(idx, 0);  // idle lanes read a valid address, use 0
-  const double diagRaw = act ? A[col * ld + col] + shift : 1.0;
-  const unsigned long long order = __ballot(act && diagRaw >= epsDiv);
-  const bool inOrder = act && ((order >> lane) & 1ull);
+  bool act[R];
+  int col[R];
+  double diagRaw[R];
+  unsigned long long order[R];
+  bool inOrder[R];
+  const int idx0 = rdliR(idx, 0);
+#pragma unroll
+  for (int s = 0; s < R; s++) {
+    act[s] = rowAt(s, lane) < n;
+    col[s] = act[s] ? idx[s] : idx0;  // idle lanes read a valid address, use 0
+    diagRaw[s] = act[s] ? A[col[s] * ld + col[s]] + shift : 1.0;
+    order[s] = __ballot(act[s] && diagRaw[s] >= epsDiv);
+    inOrder[s] = act[s] && ((order[s] >> lane) & 1ull);
+  }
   // rows whose x bounds friction rows (their update refreshes those bounds)
-  unsigned long long bounding = 0;
-  for (int i = 0; i < n; i++)
-    if (__ballot(findex == i)) bounding |= 1ull << i;
-  double r = act ? b : 0.0;
+  unsigned long long bounding[R];
+#pragma unroll
+  for (int s = 0; s < R; s++) bounding[s] = 0ull;
+  for (int i = 0; i < n; i++) {
+    bool hit = false;
+#pragma unroll
+    for (int s = 0; s < R; s++) hit = hit || findex[s] == i;
+    if (__ballot(hit)) bounding[i >> 6] |= 1ull << (i & 63);
+  }
+  double r[R];
+#pragma unroll
+  for (int s = 0; s < R; s++) r[s] = act[s] ? b[s] : 0.0;
   for (int k = 0; k < n; k++) {
-    const double xk = rdl(x, k);
-    const double a0 = A[(kMapped ? rdli(idx, k) : k) * ld + col];
-    if (act) r -= (k == lane ? a0 + shift : a0) * xk;
+    const double xk = rdlR(x, k);
+    const int rk = kMapped ? rdliR(idx, k) : k;
+#pragma unroll
+    for (int s = 0; s < R; s++) {
+      const double a0 = A[rk * ld + col[s]];
+      if (act[s]) r[s] -= (k == rowAt(s, lane) ? a0 + shift : a0) * xk;
+    }
   }
   // Contact layout (the forward's rows: each contact is a normal row
   // followed by 0 or 2 friction rows with findex = that normal and
   // lo = -hi), every row in order: the friction box of row i is
   // +-hi_i * x_N with x_N the newest x of the last normal row, which the
   // sweep carries as one scalar -- no per-lane box registers.
-  bool contactRows = order == __ballot(act);
-  {
-    const int f1 = __shfl(findex, lane > 0 ? lane - 1 : 0), f2 = __shfl(findex, lane > 1 ? lane - 2 : 0);
-    const bool ok = !act || findex < 0 ||
-                    (lo == -hi && ((findex == lane - 1 && f1 < 0) || (findex == lane - 2 && f1 == lane - 2 && f2 < 0)));
+  bool contactRows = true;
+  unsigned long long normals[R];
+#pragma unroll
+  for (int s = 0; s < R; s++) {
+    const int row = rowAt(s, lane);
+    contactRows = contactRows && order[s] == __ballot(act[s]);
+    const int f1 = gatherRi(findex, row > 0 ? row - 1 : 0), f2 = gatherRi(findex, row > 1 ? row - 2 : 0);
+    const bool ok = !act[s] || findex[s] < 0 ||
+                    (lo[s] == -hi[s] &&
+                     ((findex[s] == row - 1 && f1 < 0) || (findex[s] == row - 2 && f1 == row - 2 && f2 < 0)));
     contactRows = contactRows && !__ballot(!ok);
+    normals[s] = __ballot(act[s] && findex[s] < 0);
   }
-  const unsigned long long normals = __ballot(act && findex < 0);
   if (dbg && lane == 0) dbg[1] = contactRows ? 1 : 0;
 #ifdef LCP_PROFILE
   const long long tp1 = (long long)__builtin_amdgcn_s_memtime();
 #endif
   // current box of each row; friction rows track hi * x[findex]
-  double hB = hi, lB = lo;
-  if (findex >= 0) { hB = hi * __shfl(x, findex); lB = -hB; }
+  double hB[R], lB[R];
+#pragma unroll
+  for (int s = 0; s < R; s++) {
+    hB[s] = hi[s];
+    lB[s] = lo[s];
+    const double xf = gatherR(x, findex[s] >= 0 ? findex[s] : 0);
+    if (findex[s] >= 0) { hB[s] = hi[s] * xf; lB[s] = -hB[s]; }
+  }
   // Each lane's x changes only at its own row of a sweep, so within a sweep
-  // lane i still holds its sweep-start value x0 when row i is visited, and
-  // the reference's per-row "moved" test can be evaluated for all rows at
-  // once after the sweep (same operands, same outcome).  The row loop then
-  // carries only clamp -> readlane -> residual update.  Rows of A (symmetric,
-  // row i lane j = A_ji) are loaded one 4-row group ahead, so LDS latency is
-  // off the dependent chain.
-  const double x0 = x;
-  const double act1 = act ? 1.0 : 0.0;
-  double xn = x;
+  // row i still holds its sweep-start value x0 when it is visited, and the
+  // reference's per-row "moved" test can be evaluated for all rows at once
+  // after the sweep (same operands, same outcome).  The row loop then
+  // carries only clamp -> readlane -> residual update.  Rows of A
+  // (symmetric, row i lane j = A_ji) are loaded one 4-row group ahead, so
+  // the load latency is off the dependent chain.
+  double x0[R], xn[R], act1[R];
+#pragma unroll
+  for (int s = 0; s < R; s++) {
+    x0[s] = x[s];
+    xn[s] = x[s];
+    act1[s] = act[s] ? 1.0 : 0.0;
+  }
   const int nLast = n - 1;
-#define PGS_ROW_AT(i) ((kMapped ? rdli(idx, (i) < n ? (i) : nLast) : ((i) < n ? (i) : nLast)) * ld + col)
-#define PGS_LOAD_GROUP(R, i0)               \
-  double R##0 = A[PGS_ROW_AT(i0)];         \
-  double R##1 = A[PGS_ROW_AT((i0) + 1)];   \
-  double R##2 = A[PGS_ROW_AT((i0) + 2)];   \
-  double R##3 = A[PGS_ROW_AT((i0) + 3)]
+  auto rowAtI = [&](int i) { return kMapped ? rdliR(idx, i < n ? i : nLast) : (i < n ? i : nLast); };
+  // (slot of row i: wave-uniform; with R = 1 always 0)
+  auto pick = [&](const double (&v)[R], int i) -> double {
+    if constexpr (R == 1) return v[0];
+    else return (i >> 6) ? v[1] : v[0];
+  };
+  typedef double Grp[4][R];
+  auto loadGroup = [&](Grp& G, int i0) {
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int ro = rowAtI(i0 + u) * ld;
+#pragma unroll
+      for (int s = 0; s < R; s++) G[u][s] = A[ro + col[s]];
+    }
+  };
   {
-    auto row1 = [&](int i, double cur) {
+    auto row1 = [&](int i, const double (&cur)[R]) {
+      const double rr = pick(r, i), xs0 = pick(x0, i), dg = pick(diagRaw, i);
       double nx = 0.0;
-      if ((order >> i) & 1ull) {
-        nx = (r + diagRaw * x0) / diagRaw;
-        nx = nx > hB ? hB : (nx < lB ? lB : nx);
+      if (bitR(order, i)) {
+        const double hb = pick(hB, i), lb = pick(lB, i);
+        nx = (rr + dg * xs0) / dg;
+        nx = nx > hb ? hb : (nx < lb ? lb : nx);
       }
-      const double dx = rdl(nx - x0, i);
-      if (lane == i) xn = nx;
-      if ((bounding >> i) & 1ull) {
-        const double nxi = rdl(nx, i);
-        if (findex == i) { hB = hi * nxi; lB = -hB; }
+      const double dx = rdl(nx - xs0, i & 63);
+      setR(xn, i, lane, nx);
+      if (bitR(bounding, i)) {
+        const double nxi = rdl(nx, i & 63);
+#pragma unroll
+        for (int s = 0; s < R; s++)
+          if (findex[s] == i) { hB[s] = hi[s] * nxi; lB[s] = -hB[s]; }
       }
-      r -= (cur * act1) * dx;
+#pragma unroll
+      for (int s = 0; s < R; s++) r[s] -= (cur[s] * act1[s]) * dx;
     };
     double xN = 0.0;
     // (the row kind is a scalar bit: the branch never waits on VALU results;
     // x_N is only consumed by VALU multiplies, never by SALU)
-    auto row1c = [&](int i, double cur) {
-      double h = hi, l = lo;
-      if (!((normals >> i) & 1ull)) { h = hi * xN; l = lo * xN; }
-      double nx = (r + diagRaw * x0) / diagRaw;
+    auto row1c = [&](int i, const double (&cur)[R]) {
+      const bool nrm = bitR(normals, i);
+      double h = pick(hi, i), l = pick(lo, i);
+      if (!nrm) { h = h * xN; l = l * xN; }
+      const double rr = pick(r, i), xs0 = pick(x0, i), dg = pick(diagRaw, i);
+      double nx = (rr + dg * xs0) / dg;
       const double t = nx < l ? l : nx;
       nx = nx > h ? h : t;
-      const double dx = rdl(nx - x0, i);
-      if ((normals >> i) & 1ull) xN = rdl(nx, i);
-      if (lane == i) xn = nx;
-      r -= (cur * act1) * dx;
+      const double dx = rdl(nx - xs0, i & 63);
+      if (nrm) xN = rdl(nx, i & 63);
+      setR(xn, i, lane, nx);
+#pragma unroll
+      for (int s = 0; s < R; s++) r[s] -= (cur[s] * act1[s]) * dx;
     };
-    PGS_LOAD_GROUP(C, 0);
+    Grp C, N;
+    loadGroup(C, 0);
     if (contactRows) {
       for (int i0 = 0; i0 < n; i0 += 4) {
-        PGS_LOAD_GROUP(N, i0 + 4);
-        row1c(i0, C0);
-        if (i0 + 1 < n) row1c(i0 + 1, C1);
-        if (i0 + 2 < n) row1c(i0 + 2, C2);
-        if (i0 + 3 < n) row1c(i0 + 3, C3);
-        C0 = N0; C1 = N1; C2 = N2; C3 = N3;
+        loadGroup(N, i0 + 4);
+        row1c(i0, C[0]);
+        if (i0 + 1 < n) row1c(i0 + 1, C[1]);
+        if (i0 + 2 < n) row1c(i0 + 2, C[2]);
+        if (i0 + 3 < n) row1c(i0 + 3, C[3]);
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+#pragma unroll
+          for (int s = 0; s < R; s++) C[u][s] = N[u][s];
       }
     } else {
       for (int i0 = 0; i0 < n; i0 += 4) {
-        PGS_LOAD_GROUP(N, i0 + 4);
-        row1(i0, C0);
-        if (i0 + 1 < n) row1(i0 + 1, C1);
-        if (i0 + 2 < n) row1(i0 + 2, C2);
-        if (i0 + 3 < n) row1(i0 + 3, C3);
-        C0 = N0; C1 = N1; C2 = N2; C3 = N3;
+        loadGroup(N, i0 + 4);
+        row1(i0, C[0]);
+        if (i0 + 1 < n) row1(i0 + 1, C[1]);
+        if (i0 + 2 < n) row1(i0 + 2, C[2]);
+        if (i0 + 3 < n) row1(i0 + 3, C[3]);
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+#pragma unroll
+          for (int s = 0; s < R; s++) C[u][s] = N[u][s];
       }
     }
-    // the shift's share of the diagonal updates, deferred: lane i's residual
+    // the shift's share of the diagonal updates, deferred: a row's residual
     // is not read again before its own row in the next sweep
-    if (shift != 0.0 && act) r -= shift * (xn - x0);
+    if (shift != 0.0)
+#pragma unroll
+      for (int s = 0; s < R; s++)
+        if (act[s]) r[s] -= shift * (xn[s] - x0[s]);
   }
 #ifdef LCP_PROFILE
   const long long tp2 = (long long)__builtin_amdgcn_s_memtime();
   if (dbg && lane == 0) { dbg[2] = (double)(tp1 - tp0); dbg[3] = (double)(tp2 - tp1); }
 #endif
-  if (!__ballot(inOrder && fabs(xn - x0) > deltaXThr)) { x = xn; return true; }
+  {
+    bool moved = false;
+#pragma unroll
+    for (int s = 0; s < R; s++) moved = moved || (inOrder[s] && fabs(xn[s] - x0[s]) > deltaXThr);
+    if (!__ballot(moved)) {
+#pragma unroll
+      for (int s = 0; s < R; s++) x[s] = xn[s];
+      return true;
+    }
+  }
   // row scaling of the reference, lane-local: A'_jk = A_jk * dummy_j
-  const double dummy = inOrder ? 1.0 / diagRaw : 1.0;
-  if (inOrder) { b *= dummy; r *= dummy; }
-  const double diag = inOrder ? diagRaw * dummy : diagRaw;
-  const double dummyAct = act ? dummy : 0.0;
+  double diag[R], dummyAct[R];
+#pragma unroll
+  for (int s = 0; s < R; s++) {
+    const double dummy = inOrder[s] ? 1.0 / diagRaw[s] : 1.0;
+    if (inOrder[s]) { b[s] *= dummy; r[s] *= dummy; }
+    diag[s] = inOrder[s] ? diagRaw[s] * dummy : diagRaw[s];
+    dummyAct[s] = act[s] ? dummy : 0.0;
+  }
   bool possible = false;
   for (int iter = 1; iter < 30; iter++) {
-    const double xs = xn;
-    auto row = [&](int idx, double cur) {
-      if (!((order >> idx) & 1ull)) return;
-      double nx = r + diag * xs;
-      nx = nx > hB ? hB : (nx < lB ? lB : nx);
-      const double dx = rdl(nx - xs, idx);
-      if (lane == idx) xn = nx;
-      if ((bounding >> idx) & 1ull) {
-        const double nxi = rdl(nx, idx);
-        if (findex == idx) { hB = hi * nxi; lB = -hB; }
+    double xs[R];
+#pragma unroll
+    for (int s = 0; s < R; s++) xs[s] = xn[s];
+    auto row = [&](int i, const double (&cur)[R]) {
+      if (!bitR(order, i)) return;
+      const double hb = pick(hB, i), lb = pick(lB, i);
+      double nx = pick(r, i) + pick(diag, i) * pick(xs, i);
+      nx = nx > hb ? hb : (nx < lb ? lb : nx);
+      const double dx = rdl(nx - pick(xs, i), i & 63);
+      setR(xn, i, lane, nx);
+      if (bitR(bounding, i)) {
+        const double nxi = rdl(nx, i & 63);
+#pragma unroll
+        for (int s = 0; s < R; s++)
+          if (findex[s] == i) { hB[s] = hi[s] * nxi; lB[s] = -hB[s]; }
       }
-      r -= (cur * dummyAct) * dx;
+#pragma unroll
+      for (int s = 0; s < R; s++) r[s] -= (cur[s] * dummyAct[s]) * dx;
     };
     double xN = 0.0;
-    auto rowc = [&](int idx, double cur) {
-      double h = hi, l = lo;
-      if (!((normals >> idx) & 1ull)) { h = hi * xN; l = lo * xN; }
-      double nx = r + diag * xs;
+    auto rowc = [&](int i, const double (&cur)[R]) {
+      const bool nrm = bitR(normals, i);
+      double h = pick(hi, i), l = pick(lo, i);
+      if (!nrm) { h = h * xN; l = l * xN; }
+      double nx = pick(r, i) + pick(diag, i) * pick(xs, i);
       const double t = nx < l ? l : nx;
       nx = nx > h ? h : t;
-      const double dx = rdl(nx - xs, idx);
-      if ((normals >> idx) & 1ull) xN = rdl(nx, idx);
-      if (lane == idx) xn = nx;
-      r -= (cur * dummyAct) * dx;
+      const double dx = rdl(nx - pick(xs, i), i & 63);
+      if (nrm) xN = rdl(nx, i & 63);
+      setR(xn, i, lane, nx);
+#pragma unroll
+      for (int s = 0; s < R; s++) r[s] -= (cur[s] * dummyAct[s]) * dx;
     };
-    PGS_LOAD_GROUP(C, 0);
+    Grp C, N;
+    loadGroup(C, 0);
     if (contactRows) {
       for (int i0 = 0; i0 < n; i0 += 4) {
-        PGS_LOAD_GROUP(N, i0 + 4);
-        rowc(i0, C0);
-        if (i0 + 1 < n) rowc(i0 + 1, C1);
-        if (i0 + 2 < n) rowc(i0 + 2, C2);
-        if (i0 + 3 < n) rowc(i0 + 3, C3);
-        C0 = N0; C1 = N1; C2 = N2; C3 = N3;
+        loadGroup(N, i0 + 4);
+        rowc(i0, C[0]);
+        if (i0 + 1 < n) rowc(i0 + 1, C[1]);
+        if (i0 + 2 < n) rowc(i0 + 2, C[2]);
+        if (i0 + 3 < n) rowc(i0 + 3, C[3]);
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+#pragma unroll
+          for (int s = 0; s < R; s++) C[u][s] = N[u][s];
       }
     } else {
       for (int i0 = 0; i0 < n; i0 += 4) {
-        PGS_LOAD_GROUP(N, i0 + 4);
-        row(i0, C0);
-        if (i0 + 1 < n) row(i0 + 1, C1);
-        if (i0 + 2 < n) row(i0 + 2, C2);
-        if (i0 + 3 < n) row(i0 + 3, C3);
-        C0 = N0; C1 = N1; C2 = N2; C3 = N3;
+        loadGroup(N, i0 + 4);
+        row(i0, C[0]);
+        if (i0 + 1 < n) row(i0 + 1, C[1]);
+        if (i0 + 2 < n) row(i0 + 2, C[2]);
+        if (i0 + 3 < n) row(i0 + 3, C[3]);
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+#pragma unroll
+          for (int s = 0; s < R; s++) C[u][s] = N[u][s];
       }
     }
-    if (shift != 0.0) r -= (shift * dummyAct) * (xn - xs);
-    possible = !__ballot(inOrder && fabs(xn) > epsDiv && fabs((xn - xs) / xn) > relTol);
+    if (shift != 0.0)
+#pragma unroll
+      for (int s = 0; s < R; s++) r[s] -= (shift * dummyAct[s]) * (xn[s] - xs[s]);
+    bool far = false;
+#pragma unroll
+    for (int s = 0; s < R; s++) far = far || (inOrder[s] && fabs(xn[s]) > epsDiv && fabs((xn[s] - xs[s]) / xn[s]) > relTol);
+    possible = !__ballot(far);
     if (dbg && lane == 0) dbg[0] = iter;
     if (possible) break;
     if (cancel && uni(__hip_atomic_load(cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) break;
   }
-#undef PGS_LOAD_GROUP
-#undef PGS_ROW_AT
 #ifdef LCP_PROFILE
   if (dbg && lane == 0) dbg[4] = (double)((long long)__builtin_amdgcn_s_memtime() - tp2);
 #endif
-  x = xn;
+#pragma unroll
+  for (int s = 0; s < R; s++) x[s] = xn[s];
   return possible;
 }
 
-// ---------------------------------------------------------------------------
-template <bool kLds>
-__device__ bool waveLcpValid(int m, typename Space<kLds>::cdptr Ain, double cfm, double x, double b, double hi,
-                             double lo, int fi, bool ignoreFriction, int lane) {
-  m = uni(m);
-  const double* A = (const double*)Ain;
-  double v = -b;
-#pragma unroll 4
-  for (int j = 0; j < m; j++) {
-    const double xj = rdl(x, j);
-    if (lane < m) v += (A[j * m + lane] + (lane == j ? cfm : 0.0)) * xj;  // A symmetric: row j
-  }
-  const double xf = __shfl(x, fi >= 0 ? fi : 0);
-  bool ok = true;
-  if (lane < m) {
-    double up = hi, low = lo;
-    bool done = false;
-    if (fi != -1) {
-      if (ignoreFriction) { ok = (x == 0); done = true; }
-      up *= xf;
-      low *= xf;
-    }
-    if (!done) {
-      const double tol = 1e-5;
-      if (fabs(low) < tol && fabs(up) < tol && fabs(x) < tol) {
-      } else if (fabs(x - low) < tol) {
-        if (v < -tol) ok = false;
-      } else if (fabs(x - up) < tol) {
-        if (v > tol) ok = false;
-      } else if (x > low && x < up) {
-        if (fabs(v) > tol) ok = false;
-      } else {
-        ok = false;
-      }
-    }
-  }
-  return __ballot(!ok) == 0ull;
+// the one-row-per-lane form (rows <= 64)
+template <bool kLds, bool kMapped = false>
+__device__ bool wavePgs(int n, typename Space<kLds>::cdptr Ain, double& x, double b, double lo, double hi, int findex,
+                        int lane, double* dbg = nullptr, double shift = 0.0, const int* cancel = nullptr, int ld = -1,
+                        int idx = -1) {
+  double xa[1] = {x};
+  const double ba[1] = {b}, la[1] = {lo}, ha[1] = {hi};
+  const int fa[1] = {findex}, ia[1] = {idx};
+  const bool ok = wavePgsR<kLds, kMapped, 1>(n, Ain, xa, ba, la, ha, fa, lane, dbg, shift, cancel, ld, ia);
+  x = xa[0];
+  return ok;
 }
 
 // ---------------------------------------------------------------------------
-// x (lane-distributed, length c.n) = min-norm least-squares solution for rhs
-// (lane-distributed, length c.m).  scr: >= n doubles of LDS.
-// (A, ws, m, n, ld) as given to carveCod + codFactor
+template <bool kLds, int R>
+__device__ bool waveLcpValidR(int m, typename Space<kLds>::cdptr Ain, double cfm, const double (&x)[R],
+                              const double (&b)[R], const double (&hi)[R], const double (&lo)[R], const int (&fi)[R],
+                              bool ignoreFriction, int lane) {
+  m = uni(m);
+  const double* A = (const double*)Ain;
+  double v[R];
+#pragma unroll
+  for (int s = 0; s < R; s++) v[s] = -b[s];
+#pragma unroll 4
+  for (int j = 0; j < m; j++) {
+    const double xj = rdlR(x, j);
+#pragma unroll
+    for (int s = 0; s < R; s++) {
+      const int row = rowAt(s, lane);
+      if (row < m) v[s] += (A[j * m + row] + (row == j ? cfm : 0.0)) * xj;  // A symmetric: row j
+    }
+  }
+  bool bad = false;
+#pragma unroll
+  for (int s = 0; s < R; s++) {
+    const double xf = gatherR(x, fi[s] >= 0 ? fi[s] : 0);
+    if (rowAt(s, lane) < m) {
+      bool ok = true;
+      double up = hi[s], low = lo[s];
+      bool done = false;
+      if (fi[s] != -1) {
+        if (ignoreFriction) { ok = (x[s] == 0); done = true; }
+        up *= xf;
+        low *= xf;
+      }
+      if (!done) {
+        const double tol = 1e-5;
+        if (fabs(low) < tol && fabs(up) < tol && fabs(x[s]) < tol) {
+        } else if (fabs(x[s] - low) < tol) {
+          if (v[s] < -tol) ok = false;
+        } else if (fabs(x[s] - up) < tol) {
+          if (v[s] > tol) ok = false;
+        } else if (x[s] > low && x[s] < up) {
+          if (fabs(v[s]) > tol) ok = false;
+        } else {
+          ok = false;
+        }
+      }
+      bad = bad || !ok;
+    }
+  }
+  return __ballot(bad) == 0ull;
+}
+
 template <bool kLds>
-__device__ double codSolveWave(typename Space<kLds>::dptr Ain, typename Space<kLds>::dptr wsIn, int m_, int n_, int ld_,
-                               double rhs, typename Space<kLds>::dptr scrIn, int lane) {
+__device__ bool waveLcpValid(int m, typename Space<kLds>::cdptr Ain, double cfm, double x, double b, double hi,
+                             double lo, int fi, bool ignoreFriction, int lane) {
+  const double xa[1] = {x}, ba[1] = {b}, ha[1] = {hi}, la[1] = {lo};
+  const int fa[1] = {fi};
+  return waveLcpValidR<kLds, 1>(m, Ain, cfm, xa, ba, ha, la, fa, ignoreFriction, lane);
+}
+
+// ---------------------------------------------------------------------------
+// x (row-distributed, length c.n) = min-norm least-squares solution for rhs
+// (row-distributed, length c.m).  scr: >= n doubles.
+// (A, ws, m, n, ld) as given to carveCod + codFactor
+template <bool kLds, int R>
+__device__ void codSolveWaveR(typename Space<kLds>::dptr Ain, typename Space<kLds>::dptr wsIn, int m_, int n_, int ld_,
+                              const double (&rhsIn)[R], typename Space<kLds>::dptr scrIn, int lane, double (&out)[R]) {
   Cod c;
   carveCod((double*)wsIn, (double*)Ain, uni(m_), uni(n_), uni(ld_), c);
   double* scr = (double*)scrIn;
   const double* A = c.A;
   const int m = c.m, n = c.n, ld = c.ld;
+  double rhs[R];
+#pragma unroll
+  for (int s = 0; s < R; s++) rhs[s] = rhsIn[s];
   for (int k = 0; k < c.kmax; k++) {
     const double vnorm = unid(c.vn[k]);
     if (!(vnorm > 0)) continue;
     const double vk = c.vd[k];
-    const double v = lane == k ? vk : ((lane > k && lane < m) ? A[lane * ld + k] : 0.0);
-    double sc = waveSum(v * rhs);
+    double v[R], t[R];
+#pragma unroll
+    for (int s = 0; s < R; s++) {
+      const int row = rowAt(s, lane);
+      v[s] = row == k ? vk : ((row > k && row < m) ? A[row * ld + k] : 0.0);
+      t[s] = v[s] * rhs[s];
+    }
+    double sc = waveSumR(t);
     sc = 2 * sc / vnorm;
-    if (lane >= k && lane < m) rhs -= sc * v;
+#pragma unroll
+    for (int s = 0; s < R; s++) {
+      const int row = rowAt(s, lane);
+      if (row >= k && row < m) rhs[s] -= sc * v[s];
+    }
   }
   const int r = uni(*c.rank);
-  double z = 0.0, acc = 0.0;
+  double z[R], acc[R];
+#pragma unroll
+  for (int s = 0; s < R; s++) { z[s] = 0.0; acc[s] = 0.0; }
   for (int i = r - 1; i >= 0; i--) {
-    const double zi = (rdl(rhs, i) - rdl(acc, i)) / A[i * ld + i];
-    if (lane == i) z = zi;
-    if (lane < i) acc += A[lane * ld + i] * zi;
+    const double zi = (rdlR(rhs, i) - rdlR(acc, i)) / A[i * ld + i];
+    setR(z, i, lane, zi);
+#pragma unroll
+    for (int s = 0; s < R; s++) {
+      const int row = rowAt(s, lane);
+      if (row < i) acc[s] += A[row * ld + i] * zi;
+    }
   }
   if (r < n) {
     for (int i = 0; i < r; i++) {
       const double vn = unid(c.zn[i]);
       if (vn == 0) continue;
       const double zd = c.zd[i];
-      const double t = (lane >= r && lane < n) ? z * A[i * ld + lane] : 0.0;
-      double sc = rdl(z, i) * zd + waveSum(t);
+      double t[R];
+#pragma unroll
+      for (int s = 0; s < R; s++) {
+        const int row = rowAt(s, lane);
+        t[s] = (row >= r && row < n) ? z[s] * A[i * ld + row] : 0.0;
+      }
+      double sc = rdlR(z, i) * zd + waveSumR(t);
       sc = 2 * sc / vn;
-      if (lane == i) z -= sc * zd;
-      if (lane >= r && lane < n) z -= sc * A[i * ld + lane];
+#pragma unroll
+      for (int s = 0; s < R; s++) {
+        const int row = rowAt(s, lane);
+        if (row == i) z[s] -= sc * zd;
+        if (row >= r && row < n) z[s] -= sc * A[i * ld + row];
+      }
     }
   }
   WSYNC();
-  if (lane < n) scr[c.perm[lane]] = z;
+#pragma unroll
+  for (int s = 0; s < R; s++)
+    if (rowAt(s, lane) < n) scr[c.perm[rowAt(s, lane)]] = z[s];
   WSYNC();
-  const double out = lane < n ? scr[lane] : 0.0;
+#pragma unroll
+  for (int s = 0; s < R; s++) out[s] = rowAt(s, lane) < n ? scr[rowAt(s, lane)] : 0.0;
   WSYNC();
-  return out;
+}
+
+template <bool kLds>
+__device__ double codSolveWave(typename Space<kLds>::dptr Ain, typename Space<kLds>::dptr wsIn, int m_, int n_, int ld_,
+                               double rhs, typename Space<kLds>::dptr scrIn, int lane) {
+  const double ra[1] = {rhs};
+  double out[1];
+  codSolveWaveR<kLds, 1>(Ain, wsIn, m_, n_, ld_, ra, scrIn, lane, out);
+  return out[0];
 }
 
 // ---------------------------------------------------------------------------
+template <int R>
 struct WaveDantzig {
   int n, nC, nN, lane, ldL;
-  // A: the problem matrix (n x n, symmetric, LDS), read in place: slot i of
-  // the permuted problem is original row p_i (lane i's register p), so the
+  // A: the problem matrix (n x n, symmetric), read in place: slot i of the
+  // permuted problem is original row p_i (row i's register p), so the
   // permuted entry (i, j) is A[p_i n + p_j] and a swap of two slots is a
   // swap of registers -- the same values the reference's physically
   // permuted matrix holds (dLCP's row / column swaps), without moving them
   const double* A;
   double* L;    // n x ldL, ldL odd (LDS bank-conflict-free columns)
-  double* scr;  // >= n doubles (LDS)
-  double x, b, w, lo, hi, d, deltaX, deltaW, Dell, ell;
-  int findex, p, C, state;
+  double* scr;  // >= n doubles
+  double x[R], b[R], w[R], lo[R], hi[R], d[R], deltaX[R], deltaW[R], Dell[R], ell[R];
+  int findex[R], p[R], C[R], state[R];
 #ifdef LCP_PROFILE
   long long prof[8];
 #endif
 
-  __device__ __forceinline__ void swapReg(double& v, int i1, int i2) {
-    const double a = rdl(v, i1), c = rdl(v, i2);
-    if (lane == i1) v = c;
-    else if (lane == i2) v = a;
+  __device__ __forceinline__ int row(int s) const { return rowAt(s, lane); }
+  __device__ __forceinline__ void swapReg(double (&v)[R], int i1, int i2) {
+    const double a = rdlR(v, i1), c = rdlR(v, i2);
+#pragma unroll
+    for (int s = 0; s < R; s++) {
+      if (row(s) == i1) v[s] = c;
+      else if (row(s) == i2) v[s] = a;
+    }
   }
-  __device__ __forceinline__ void swapRegI(int& v, int i1, int i2) {
-    const int a = rdli(v, i1), c = rdli(v, i2);
-    if (lane == i1) v = c;
-    else if (lane == i2) v = a;
+  __device__ __forceinline__ void swapRegI(int (&v)[R], int i1, int i2) {
+    const int a = rdliR(v, i1), c = rdliR(v, i2);
+#pragma unroll
+    for (int s = 0; s < R; s++) {
+      if (row(s) == i1) v[s] = c;
+      else if (row(s) == i2) v[s] = a;
+    }
   }
   // permuted-matrix accessors: row slot i (wave-uniform), column of this
-  // lane's slot / of its C entry / the diagonal
-  __device__ __forceinline__ int rowOff(int i) const { return rdli(p, i) * n; }
-  __device__ __forceinline__ double Arow(int i) const { return A[rowOff(i) + (lane < n ? p : 0)]; }
+  // lane's slot s / of its C entry / the diagonal
+  // (cross-lane reads are kept out of lane-divergent expressions: callers
+  // take the row offset first, then index with it)
+  __device__ __forceinline__ int rowOff(int i) const { return rdliR(p, i) * n; }
+  __device__ __forceinline__ double ArowAt(int ro, int s) const { return A[ro + (row(s) < n ? p[s] : 0)]; }
   __device__ __forceinline__ double Adiag(int i) const {
-    const int pi = rdli(p, i);
+    const int pi = rdliR(p, i);
     return A[pi * n + pi];
   }
-  // p of the slot this lane's C entry names
-  __device__ __forceinline__ int pOfC() const { return __shfl(p, C & 63); }
+  // p of the slot this lane's C entry (slot s) names
+  __device__ __forceinline__ int pOfC(int s) const { return gatherRi(p, C[s] & (64 * R - 1)); }
   __device__ __forceinline__ void swapProblem(int i1, int i2) {
     if (i1 == i2) return;
     LP_BEGIN();
@@ -360,7 +548,7 @@ struct WaveDantzig {
     swapRegI(p, i1, i2); swapRegI(state, i1, i2); swapRegI(findex, i1, i2);
     LP_END(prof, 0);
   }
-  // L x = B (unit lower), B lane-distributed, first m entries.  The L
+  // L x = B (unit lower), B row-distributed, first m entries.  The L
   // entries of each lane are loaded 8 at a time ahead of the dependent
   // readlane -> FMA chain (LDS latency paid once per 8 steps) with the
   // triangle mask folded into them (0 where a lane must not change), so a
@@ -368,104 +556,162 @@ struct WaveDantzig {
   // would wait on a vector compare.  0 * b_k leaves a lane unchanged only
   // for finite b_k; a non-finite b_k (degenerate factor) re-runs the solve
   // predicated, exactly as the reference's loop.
-  __device__ __forceinline__ void solveL1(double& B, int m) {
+  __device__ __forceinline__ void solveL1(double (&B)[R], int m) {
     m = uni(m);
     LP_BEGIN();
-    const double B0 = B;
-    const int row = (lane < m ? lane : 0) * ldL;
-    for (int k0 = 0; k0 < m; k0 += 8) {
-      double Lk[8];
+    double B0[R];
+    int rowOffL[R];
 #pragma unroll
-      for (int u = 0; u < 8; u++) {
-        double v = L[row + (k0 + u < m ? k0 + u : 0)];
-        asm volatile("" : "+v"(v));  // keep the load unconditional (batched)
-        Lk[u] = (lane > k0 + u && lane < m) ? v : 0.0;
-      }
+    for (int s = 0; s < R; s++) {
+      B0[s] = B[s];
+      rowOffL[s] = (row(s) < m ? row(s) : 0) * ldL;
+    }
+    for (int k0 = 0; k0 < m; k0 += 8) {
+      double Lk[R][8];
+#pragma unroll
+      for (int s = 0; s < R; s++)
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          double v = L[rowOffL[s] + (k0 + u < m ? k0 + u : 0)];
+          asm volatile("" : "+v"(v));  // keep the load unconditional (batched)
+          Lk[s][u] = (row(s) > k0 + u && row(s) < m) ? v : 0.0;
+        }
 #pragma unroll
       for (int u = 0; u < 8; u++)
-        if (k0 + u < m) B -= Lk[u] * rdl(B, k0 + u);
+        if (k0 + u < m) {
+          const double bk = rdlR(B, k0 + u);
+#pragma unroll
+          for (int s = 0; s < R; s++) B[s] -= Lk[s][u] * bk;
+        }
     }
-    if (__ballot(lane < m && !isfinite(B))) {
-      B = B0;
+    bool nonFinite = false;
+#pragma unroll
+    for (int s = 0; s < R; s++) nonFinite = nonFinite || (row(s) < m && !isfinite(B[s]));
+    if (__ballot(nonFinite)) {
+#pragma unroll
+      for (int s = 0; s < R; s++) B[s] = B0[s];
       for (int k = 0; k < m; k++) {
-        const double bk = rdl(B, k);
-        if (lane > k && lane < m) B -= L[lane * ldL + k] * bk;
+        const double bk = rdlR(B, k);
+#pragma unroll
+        for (int s = 0; s < R; s++)
+          if (row(s) > k && row(s) < m) B[s] -= L[row(s) * ldL + k] * bk;
       }
     }
     LP_END(prof, 1);
   }
   // L^T x = B
-  __device__ __forceinline__ void solveL1T(double& B, int m) {
+  __device__ __forceinline__ void solveL1T(double (&B)[R], int m) {
     m = uni(m);
     LP_BEGIN();
-    const double B0 = B;
-    const int col = lane < m ? lane : 0;
-    for (int k0 = m - 1; k0 >= 0; k0 -= 8) {
-      double Lk[8];
+    double B0[R];
+    int colL[R];
 #pragma unroll
-      for (int u = 0; u < 8; u++) {
-        double v = L[(k0 - u >= 0 ? k0 - u : 0) * ldL + col];
-        asm volatile("" : "+v"(v));
-        Lk[u] = lane < k0 - u ? v : 0.0;
-      }
+    for (int s = 0; s < R; s++) {
+      B0[s] = B[s];
+      colL[s] = row(s) < m ? row(s) : 0;
+    }
+    for (int k0 = m - 1; k0 >= 0; k0 -= 8) {
+      double Lk[R][8];
+#pragma unroll
+      for (int s = 0; s < R; s++)
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          double v = L[(k0 - u >= 0 ? k0 - u : 0) * ldL + colL[s]];
+          asm volatile("" : "+v"(v));
+          Lk[s][u] = row(s) < k0 - u ? v : 0.0;
+        }
 #pragma unroll
       for (int u = 0; u < 8; u++)
-        if (k0 - u >= 0) B -= Lk[u] * rdl(B, k0 - u);
+        if (k0 - u >= 0) {
+          const double bk = rdlR(B, k0 - u);
+#pragma unroll
+          for (int s = 0; s < R; s++) B[s] -= Lk[s][u] * bk;
+        }
     }
-    if (__ballot(lane < m && !isfinite(B))) {
-      B = B0;
+    bool nonFinite = false;
+#pragma unroll
+    for (int s = 0; s < R; s++) nonFinite = nonFinite || (row(s) < m && !isfinite(B[s]));
+    if (__ballot(nonFinite)) {
+#pragma unroll
+      for (int s = 0; s < R; s++) B[s] = B0[s];
       for (int k = m - 1; k >= 0; k--) {
-        const double bk = rdl(B, k);
-        if (lane < k) B -= L[k * ldL + lane] * bk;
+        const double bk = rdlR(B, k);
+#pragma unroll
+        for (int s = 0; s < R; s++)
+          if (row(s) < k) B[s] -= L[k * ldL + row(s)] * bk;
       }
     }
     LP_END(prof, 2);
   }
+  __device__ __forceinline__ double sumC(const double (&u)[R], const double (&v)[R]) const {
+    double t[R];
+#pragma unroll
+    for (int s = 0; s < R; s++) t[s] = row(s) < nC ? u[s] * v[s] : 0.0;
+    return waveSumR(t);
+  }
   __device__ __forceinline__ void transferToC(int i) {
     const double Aii = Adiag(i);
     if (nC > 0) {
-      if (lane < nC) L[nC * ldL + lane] = ell;
-      const double dd = waveSum(lane < nC ? ell * Dell : 0.0);
-      if (lane == nC) d = 1.0 / (Aii - dd);
+#pragma unroll
+      for (int s = 0; s < R; s++)
+        if (row(s) < nC) L[nC * ldL + row(s)] = ell[s];
+      const double dd = sumC(ell, Dell);
+      setR(d, nC, lane, 1.0 / (Aii - dd));
     } else {
-      if (lane == 0) d = 1.0 / Aii;
+      setR(d, 0, lane, 1.0 / Aii);
     }
     swapProblem(nC, i);
-    if (lane == nC) C = nC;
+    setRi(C, nC, lane, nC);
     nC++;
+  }
+  __device__ __forceinline__ void loadDell(int i) {
+    const int ro = rowOff(i);
+#pragma unroll
+    for (int s = 0; s < R; s++) {
+      const int pc = pOfC(s);
+      Dell[s] = row(s) < nC ? A[ro + pc] : 0.0;
+    }
   }
   __device__ __forceinline__ void transferFromNtoC(int i) {
     const double Aii = Adiag(i);
     if (nC > 0) {
-      const int pc = pOfC();
-      Dell = lane < nC ? A[rowOff(i) + pc] : 0.0;
+      loadDell(i);
       solveL1(Dell, nC);
-      ell = lane < nC ? Dell * d : 0.0;
-      if (lane < nC) L[nC * ldL + lane] = ell;
-      const double dd = waveSum(lane < nC ? ell * Dell : 0.0);
-      if (lane == nC) d = 1.0 / (Aii - dd);
+#pragma unroll
+      for (int s = 0; s < R; s++) {
+        ell[s] = row(s) < nC ? Dell[s] * d[s] : 0.0;
+        if (row(s) < nC) L[nC * ldL + row(s)] = ell[s];
+      }
+      const double dd = sumC(ell, Dell);
+      setR(d, nC, lane, 1.0 / (Aii - dd));
     } else {
-      if (lane == 0) d = 1.0 / Aii;
+      setR(d, 0, lane, 1.0 / Aii);
     }
     swapProblem(nC, i);
-    if (lane == nC) C = nC;
+    setRi(C, nC, lane, nC);
     nN--;
     nC++;
   }
   // _dLDLTAddTL on the sub-factorisation starting at (r, r); `a` holds
-  // element j at lane r + j
-  __device__ __forceinline__ void ldltAddTL(int r, int m2, double a) {
+  // element j at row r + j
+  __device__ __forceinline__ void ldltAddTL(int r, int m2, const double (&a)[R]) {
     if (m2 < 2) return;
     const double r2 = 0.70710678118654752440;
-    const int j0 = lane - r;
-    double W1 = 0.0, W2 = 0.0;
-    if (j0 >= 1 && j0 < m2) { W1 = a * r2; W2 = W1; }
-    const double a0 = rdl(a, r);
+    int j0[R];
+    double W1[R], W2[R];
+#pragma unroll
+    for (int s = 0; s < R; s++) {
+      j0[s] = row(s) - r;
+      W1[s] = 0.0;
+      W2[s] = 0.0;
+      if (j0[s] >= 1 && j0[s] < m2) { W1[s] = a[s] * r2; W2[s] = W1[s]; }
+    }
+    const double a0 = rdlR(a, r);
     const double W11 = (0.5 * a0 + 1) * r2;
     const double W21 = (0.5 * a0 - 1) * r2;
     double alpha1 = 1.0, alpha2 = 1.0;
     {
-      double dee = rdl(d, r);
+      double dee = rdlR(d, r);
       double alphanew = alpha1 + (W11 * W11) * dee;
       dee /= alphanew;
       const double gamma1 = W11 * dee;
@@ -476,16 +722,18 @@ struct WaveDantzig {
       alpha2 = alphanew;
       const double k1 = 1.0 - W21 * gamma1;
       const double k2 = W21 * gamma1 * W11 - W21;
-      if (j0 >= 1 && j0 < m2) {
-        const double Wp = W1;
-        const double el = L[(r + j0) * ldL + r];
-        W1 = Wp - W11 * el;
-        W2 = k1 * Wp + k2 * el;
-      }
+#pragma unroll
+      for (int s = 0; s < R; s++)
+        if (j0[s] >= 1 && j0[s] < m2) {
+          const double Wp = W1[s];
+          const double el = L[(r + j0[s]) * ldL + r];
+          W1[s] = Wp - W11 * el;
+          W2[s] = k1 * Wp + k2 * el;
+        }
     }
     for (int j = 1; j < m2; j++) {
-      const double k1 = rdl(W1, r + j), k2 = rdl(W2, r + j);
-      double dee = rdl(d, r + j);
+      const double k1 = rdlR(W1, r + j), k2 = rdlR(W2, r + j);
+      double dee = rdlR(d, r + j);
       double alphanew = alpha1 + (k1 * k1) * dee;
       dee /= alphanew;
       const double gamma1 = k1 * dee;
@@ -495,65 +743,103 @@ struct WaveDantzig {
       dee /= alphanew;
       const double gamma2 = k2 * dee;
       dee *= alpha2;
-      if (lane == r + j) d = dee;
+      setR(d, r + j, lane, dee);
       alpha2 = alphanew;
-      if (j0 > j && j0 < m2) {
-        double el = L[(r + j0) * ldL + r + j];
-        double Wp = W1 - k1 * el;
-        el += gamma1 * Wp;
-        W1 = Wp;
-        Wp = W2 - k2 * el;
-        el -= gamma2 * Wp;
-        W2 = Wp;
-        L[(r + j0) * ldL + r + j] = el;
-      }
+#pragma unroll
+      for (int s = 0; s < R; s++)
+        if (j0[s] > j && j0[s] < m2) {
+          double el = L[(r + j0[s]) * ldL + r + j];
+          double Wp = W1[s] - k1 * el;
+          el += gamma1 * Wp;
+          W1[s] = Wp;
+          Wp = W2[s] - k2 * el;
+          el -= gamma2 * Wp;
+          W2[s] = Wp;
+          L[(r + j0[s]) * ldL + r + j] = el;
+        }
     }
   }
   __device__ __forceinline__ void ldltRemove(int r, int n2) {
     LP_BEGIN();
     if (r != n2 - 1) {
-      const int pc = pOfC();
+      double a[R];
       if (r == 0) {
-        const int C0 = rdli(C, 0);
-        double a = lane < n2 ? -A[rowOff(C0) + pc] : 0.0;  // A symmetric
-        if (lane == 0) a += 1.0;
+        const int ro = rowOff(rdliR(C, 0));
+#pragma unroll
+        for (int s = 0; s < R; s++) {
+          const int pc = pOfC(s);
+          a[s] = row(s) < n2 ? -A[ro + pc] : 0.0;  // A symmetric
+          if (row(s) == 0) a[s] += 1.0;
+        }
         ldltAddTL(0, n2, a);
       } else {
-        const double t = lane < r ? L[r * ldL + lane] / d : 0.0;
-        const int Cr = rdli(C, r);
-        double a = 0.0;
-        double s = 0.0;
-        for (int k = 0; k < r; k++) {
-          const double tk = rdl(t, k);
-          if (lane >= r && lane < n2) s += L[lane * ldL + k] * tk;
+        double t[R], sacc[R];
+#pragma unroll
+        for (int s = 0; s < R; s++) {
+          t[s] = row(s) < r ? L[r * ldL + row(s)] / d[s] : 0.0;
+          sacc[s] = 0.0;
         }
-        if (lane >= r && lane < n2) a = s - A[rowOff(Cr) + pc];  // A symmetric
-        if (lane == r) a += 1.0;
+        const int ro = rowOff(rdliR(C, r));
+        int pc[R];
+#pragma unroll
+        for (int s = 0; s < R; s++) pc[s] = pOfC(s);
+        for (int k = 0; k < r; k++) {
+          const double tk = rdlR(t, k);
+#pragma unroll
+          for (int s = 0; s < R; s++)
+            if (row(s) >= r && row(s) < n2) sacc[s] += L[row(s) * ldL + k] * tk;
+        }
+#pragma unroll
+        for (int s = 0; s < R; s++) {
+          a[s] = 0.0;
+          if (row(s) >= r && row(s) < n2) a[s] = sacc[s] - A[ro + pc[s]];  // A symmetric
+          if (row(s) == r) a[s] += 1.0;
+        }
         ldltAddTL(r, n2 - r, a);
       }
     }
     WSYNC();
     if (r < n2 - 1) {
-      if (lane < n2)
-        for (int j = r; j < n2 - 1; j++) L[lane * ldL + j] = L[lane * ldL + j + 1];
+#pragma unroll
+      for (int s = 0; s < R; s++)
+        if (row(s) < n2)
+          for (int j = r; j < n2 - 1; j++) L[row(s) * ldL + j] = L[row(s) * ldL + j + 1];
       WSYNC();
-      if (lane < n2)
-        for (int i = r; i < n2 - 1; i++) L[i * ldL + lane] = L[(i + 1) * ldL + lane];
+#pragma unroll
+      for (int s = 0; s < R; s++)
+        if (row(s) < n2)
+          for (int i = r; i < n2 - 1; i++) L[i * ldL + row(s)] = L[(i + 1) * ldL + row(s)];
       WSYNC();
-      const double dn = shiftDown1(d, lane);
-      if (lane >= r && lane < n2 - 1) d = dn;
+      double dn[R];
+#pragma unroll
+      for (int s = 0; s < R; s++) dn[s] = d[s];
+      shiftDownR(dn, lane);
+#pragma unroll
+      for (int s = 0; s < R; s++)
+        if (row(s) >= r && row(s) < n2 - 1) d[s] = dn[s];
     }
     LP_END(prof, 3);
   }
   __device__ __forceinline__ void transferFromCtoN(int i) {
-    const int j = waveFirst(lane < nC && C == i);
+    bool hitI[R], hitLast[R];
+#pragma unroll
+    for (int s = 0; s < R; s++) {
+      hitI[s] = row(s) < nC && C[s] == i;
+      hitLast[s] = row(s) < nC && C[s] == nC - 1;
+    }
+    const int j = waveFirstR(hitI);
     if (j >= 0) {
-      const int k = waveFirst(lane < nC && C == nC - 1);
+      const int k = waveFirstR(hitLast);
       ldltRemove(j, nC);
-      const int Cj = rdli(C, j);
-      if (lane == k) C = Cj;
-      const int Cn = shiftDown1i(C, lane);
-      if (lane >= j && lane < nC - 1) C = Cn;
+      const int Cj = rdliR(C, j);
+      setRi(C, k, lane, Cj);
+      int Cn[R];
+#pragma unroll
+      for (int s = 0; s < R; s++) Cn[s] = C[s];
+      shiftDownRi(Cn, lane);
+#pragma unroll
+      for (int s = 0; s < R; s++)
+        if (row(s) >= j && row(s) < nC - 1) C[s] = Cn[s];
     }
     swapProblem(i, nC - 1);
     nN++;
@@ -561,83 +847,112 @@ struct WaveDantzig {
   }
   __device__ __forceinline__ void solve1(int i, int dir, bool onlyTransfer) {
     if (nC > 0) {
-      const int pc = pOfC();
-      Dell = lane < nC ? A[rowOff(i) + pc] : 0.0;
+      loadDell(i);
       solveL1(Dell, nC);
-      ell = lane < nC ? Dell * d : 0.0;
+#pragma unroll
+      for (int s = 0; s < R; s++) ell[s] = row(s) < nC ? Dell[s] * d[s] : 0.0;
       if (!onlyTransfer) {
-        double tmp = ell;
+        double tmp[R];
+#pragma unroll
+        for (int s = 0; s < R; s++) tmp[s] = ell[s];
         solveL1T(tmp, nC);
         WSYNC();
-        if (lane < nC) scr[C] = dir > 0 ? -tmp : tmp;
+#pragma unroll
+        for (int s = 0; s < R; s++)
+          if (row(s) < nC) scr[C[s]] = dir > 0 ? -tmp[s] : tmp[s];
         WSYNC();
-        if (lane < nC) deltaX = scr[lane];
+#pragma unroll
+        for (int s = 0; s < R; s++)
+          if (row(s) < nC) deltaX[s] = scr[row(s)];
         WSYNC();
       }
     }
   }
-  __device__ __forceinline__ double AiC(int i, double q) { return waveSum(lane < nC ? Arow(i) * q : 0.0); }
-  __device__ __forceinline__ double AiN(int i, double q) {
-    return waveSum((lane >= nC && lane < nC + nN) ? Arow(i) * q : 0.0);
+  __device__ __forceinline__ double AiC(int i, const double (&q)[R]) {
+    const int ro = rowOff(i);
+    double t[R];
+#pragma unroll
+    for (int s = 0; s < R; s++) t[s] = row(s) < nC ? ArowAt(ro, s) * q[s] : 0.0;
+    return waveSumR(t);
+  }
+  __device__ __forceinline__ double AiN(int i, const double (&q)[R]) {
+    const int ro = rowOff(i);
+    double t[R];
+#pragma unroll
+    for (int s = 0; s < R; s++) t[s] = (row(s) >= nC && row(s) < nC + nN) ? ArowAt(ro, s) * q[s] : 0.0;
+    return waveSumR(t);
   }
 };
 
-// A (n x n LDS, symmetric, read only), L (n x (n|1) LDS scratch), scr (>= n
-// LDS); problem vectors lane-distributed; returns success and x
-// (lane-distributed).
-template <bool kLds>
-__device__ bool waveDantzig(int n, typename Space<kLds>::cdptr Ain, typename Space<kLds>::dptr Lin,
-                            typename Space<kLds>::dptr scrIn, double& xOut, double b, double lo, double hi,
-                            int findex, int lane, double* dbg = nullptr, const int* cancel = nullptr) {
+// A (n x n, symmetric, read only), L (n x (n|1) scratch), scr (>= n); problem
+// vectors row-distributed; returns success and x (row-distributed).
+template <bool kLds, int R>
+__device__ bool waveDantzigR(int n, typename Space<kLds>::cdptr Ain, typename Space<kLds>::dptr Lin,
+                             typename Space<kLds>::dptr scrIn, double (&xOut)[R], const double (&b)[R],
+                             const double (&lo)[R], const double (&hi)[R], const int (&findex)[R], int lane,
+                             double* dbg = nullptr, const int* cancel = nullptr) {
   n = uni(n);
   const double* A = (const double*)Ain;
   double* Lbuf = (double*)Lin;
   double* scr = (double*)scrIn;
-  WaveDantzig D;
+  WaveDantzig<R> D;
   int pivots = 0;
   D.n = n; D.nC = 0; D.nN = 0; D.lane = lane; D.ldL = n | 1;
   D.A = A; D.L = Lbuf; D.scr = scr;
-  D.x = 0.0; D.b = b; D.w = 0.0; D.lo = lo; D.hi = hi; D.d = 0.0;
-  D.deltaX = 0.0; D.deltaW = 0.0; D.Dell = 0.0; D.ell = 0.0;
-  D.findex = findex; D.p = lane; D.C = 0; D.state = 0;
+#pragma unroll
+  for (int s = 0; s < R; s++) {
+    D.x[s] = 0.0; D.b[s] = b[s]; D.w[s] = 0.0; D.lo[s] = lo[s]; D.hi[s] = hi[s]; D.d[s] = 0.0;
+    D.deltaX[s] = 0.0; D.deltaW[s] = 0.0; D.Dell[s] = 0.0; D.ell[s] = 0.0;
+    D.findex[s] = findex[s]; D.p[s] = rowAt(s, lane); D.C[s] = 0; D.state[s] = 0;
+  }
 #ifdef LCP_PROFILE
   for (int k = 0; k < 8; k++) D.prof[k] = 0;
 #endif
   for (int k = lane; k < n * (n | 1); k += 64) Lbuf[k] = 0.0;
-  if (__ballot(lane < n && findex < 0 && lo == -LCP_INF && hi == LCP_INF)) return false;
+  {
+    bool unb = false;
+#pragma unroll
+    for (int s = 0; s < R; s++)
+      unb = unb || (rowAt(s, lane) < n && findex[s] < 0 && lo[s] == -LCP_INF && hi[s] == LCP_INF);
+    if (__ballot(unb)) return false;
+  }
   {
     int numAtEnd = 0;
     for (int k = n - 1; k >= 0; k--)
-      if (rdli(D.findex, k) >= 0) { D.swapProblem(k, n - 1 - numAtEnd); numAtEnd++; }
+      if (rdliR(D.findex, k) >= 0) { D.swapProblem(k, n - 1 - numAtEnd); numAtEnd++; }
   }
   WSYNC();
   bool hitFirstFriction = false;
   for (int i = 0; i < n; i++) {
     D.nC = uni(D.nC);
     D.nN = uni(D.nN);
-    if (!hitFirstFriction && rdli(D.findex, i) >= 0) {
+    if (!hitFirstFriction && rdliR(D.findex, i) >= 0) {
       WSYNC();
-      if (lane < n) scr[D.p] = D.x;
+#pragma unroll
+      for (int s = 0; s < R; s++)
+        if (rowAt(s, lane) < n) scr[D.p[s]] = D.x[s];
       WSYNC();
-      if (lane >= i && lane < n) {
-        const double wfk = scr[D.findex];
-        if (wfk == 0) { D.hi = 0; D.lo = 0; }
-        else { D.hi = fabs(D.hi * wfk); D.lo = -D.hi; }
-      }
+#pragma unroll
+      for (int s = 0; s < R; s++)
+        if (rowAt(s, lane) >= i && rowAt(s, lane) < n) {
+          const double wfk = scr[D.findex[s]];
+          if (wfk == 0) { D.hi[s] = 0; D.lo[s] = 0; }
+          else { D.hi[s] = fabs(D.hi[s] * wfk); D.lo[s] = -D.hi[s]; }
+        }
       WSYNC();
       hitFirstFriction = true;
     }
     LP_BEGIN();
-    const double wi = D.AiC(i, D.x) + D.AiN(i, D.x) - rdl(D.b, i);
+    const double wi = D.AiC(i, D.x) + D.AiN(i, D.x) - rdlR(D.b, i);
     LP_END(D.prof, 4);
-    if (lane == i) D.w = wi;
-    const double loi = rdl(D.lo, i), hii = rdl(D.hi, i);
+    setR(D.w, i, lane, wi);
+    const double loi = rdlR(D.lo, i), hii = rdlR(D.hi, i);
     if (loi == 0 && wi >= 0) {
       D.nN++;
-      if (lane == i) D.state = 0;
+      setRi(D.state, i, lane, 0);
     } else if (hii == 0 && wi <= 0) {
       D.nN++;
-      if (lane == i) D.state = 1;
+      setRi(D.state, i, lane, 1);
     } else if (wi == 0) {
       D.solve1(i, 0, true);
       D.transferToC(i);
@@ -645,31 +960,44 @@ __device__ bool waveDantzig(int n, typename Space<kLds>::cdptr Ain, typename Spa
       for (;;) {
         D.nC = uni(D.nC);
         D.nN = uni(D.nN);
-        const double wiNow = rdl(D.w, i);
+        const double wiNow = rdlR(D.w, i);
         int dir;
         double dirf;
         if (wiNow <= 0) { dir = 1; dirf = 1.0; } else { dir = -1; dirf = -1.0; }
         D.solve1(i, dir, false);
         const int nC = D.nC, nN = D.nN;
-        const bool inN = lane >= nC && lane < nC + nN;
+        bool inN[R];
         LP_BEGIN();
         {
-          // every lane accumulates (no exec mask per step); only N lanes keep it
-          const int colA = lane < n ? D.p : 0;
-          double acc = 0.0;
+          // every lane accumulates (no exec mask per step); only N rows keep it
+          int colA[R];
+          double acc[R];
+#pragma unroll
+          for (int s = 0; s < R; s++) {
+            const int row = rowAt(s, lane);
+            inN[s] = row >= nC && row < nC + nN;
+            colA[s] = row < n ? D.p[s] : 0;
+            acc[s] = 0.0;
+          }
 #pragma unroll 4
           for (int j = 0; j < nC; j++) {
-            const double dxj = rdl(D.deltaX, j);
-            acc += A[D.rowOff(j) + colA] * dxj;  // A symmetric: row j
+            const double dxj = rdlR(D.deltaX, j);
+            const int ro = D.rowOff(j);
+#pragma unroll
+            for (int s = 0; s < R; s++) acc[s] += A[ro + colA[s]] * dxj;  // A symmetric: row j
           }
-          const double aij = D.Arow(i);
-          if (inN) D.deltaW = acc + (dir > 0 ? aij : -aij);
+          const int roI = D.rowOff(i);
+#pragma unroll
+          for (int s = 0; s < R; s++) {
+            const double aij = D.ArowAt(roI, s);
+            if (inN[s]) D.deltaW[s] = acc[s] + (dir > 0 ? aij : -aij);
+          }
         }
         const double dwi = D.AiC(i, D.deltaX) + D.Adiag(i) * dirf;
-        if (lane == i) D.deltaW = dwi;
+        setR(D.deltaW, i, lane, dwi);
         int cmd = 1, si = 0;
         double s = -wiNow / dwi;
-        const double xi = rdl(D.x, i), hiI = rdl(D.hi, i), loI = rdl(D.lo, i);
+        const double xi = rdlR(D.x, i), hiI = rdlR(D.hi, i), loI = rdlR(D.lo, i);
         if (dir > 0) {
           if (hiI < LCP_INF) { const double s2 = (hiI - xi) * dirf; if (s2 < s) { s = s2; cmd = 3; } }
         } else {
@@ -677,30 +1005,42 @@ __device__ bool waveDantzig(int n, typename Space<kLds>::cdptr Ain, typename Spa
         }
         {
           // the N-side (cmd 4) and C-side (cmd 5/6) ratio tests of the
-          // reference over disjoint lanes: one division and one reduction;
+          // reference over disjoint rows: one division and one reduction;
           // on equal minima the N side wins, as in the reference's order
-          bool cand4 = false;
-          int typ = 0;
-          double num = 0.0, den = 1.0;
-          if (inN) {
-            const bool dirOk = !D.state ? D.deltaW < 0 : D.deltaW > 0;
-            if (dirOk && !(D.lo == 0 && D.hi == 0)) { cand4 = true; num = -D.w; den = D.deltaW; }
-          } else if (lane < nC) {
-            if (D.deltaX < 0 && D.lo > -LCP_INF) { num = D.lo - D.x; den = D.deltaX; typ = 5; }
-            if (D.deltaX > 0 && D.hi < LCP_INF) { num = D.hi - D.x; den = D.deltaX; typ = 6; }
+          bool cand4[R], anyR[R], tmin[R];
+          int typ[R];
+          double rr[R], key[R];
+#pragma unroll
+          for (int q = 0; q < R; q++) {
+            const int row = rowAt(q, lane);
+            cand4[q] = false;
+            typ[q] = 0;
+            double num = 0.0, den = 1.0;
+            if (inN[q]) {
+              const bool dirOk = !D.state[q] ? D.deltaW[q] < 0 : D.deltaW[q] > 0;
+              if (dirOk && !(D.lo[q] == 0 && D.hi[q] == 0)) { cand4[q] = true; num = -D.w[q]; den = D.deltaW[q]; }
+            } else if (row < nC) {
+              if (D.deltaX[q] < 0 && D.lo[q] > -LCP_INF) { num = D.lo[q] - D.x[q]; den = D.deltaX[q]; typ[q] = 5; }
+              if (D.deltaX[q] > 0 && D.hi[q] < LCP_INF) { num = D.hi[q] - D.x[q]; den = D.deltaX[q]; typ[q] = 6; }
+            }
+            rr[q] = num / den;
+            anyR[q] = cand4[q] || typ[q];
+            key[q] = anyR[q] ? rr[q] : LCP_INF;
           }
-          const double r = num / den;
-          const bool any = cand4 || typ;
-          const double mm = waveMin(any ? r : LCP_INF);
+          const double mm = waveMinR(key);
           if (mm < s) {
             s = mm;
-            const int s4i = waveFirst(cand4 && r == mm);
+#pragma unroll
+            for (int q = 0; q < R; q++) tmin[q] = cand4[q] && rr[q] == mm;
+            const int s4i = waveFirstR(tmin);
             if (s4i >= 0) {
               cmd = 4;
               si = s4i;
             } else {
-              si = waveFirst(typ && r == mm);
-              cmd = rdli(typ, si);
+#pragma unroll
+              for (int q = 0; q < R; q++) tmin[q] = typ[q] && rr[q] == mm;
+              si = waveFirstR(tmin);
+              cmd = rdliR(typ, si);
             }
           }
         }
@@ -715,33 +1055,41 @@ __device__ bool waveDantzig(int n, typename Space<kLds>::cdptr Ain, typename Spa
         // `cancel` (LDS int, optional): polled once per pivot; a set flag
         // abandons the solve (the caller no longer needs it)
         if (cancel && uni(__hip_atomic_load(cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) return false;
-        if (lane < nC) D.x += s * D.deltaX;
-        if (lane == i) D.x += s * dirf;
-        if (inN) D.w += s * D.deltaW;
-        if (lane == i) D.w += s * dwi;
+#pragma unroll
+        for (int q = 0; q < R; q++) {
+          const int row = rowAt(q, lane);
+          if (row < nC) D.x[q] += s * D.deltaX[q];
+          if (row == i) D.x[q] += s * dirf;
+          if (inN[q]) D.w[q] += s * D.deltaW[q];
+          if (row == i) D.w[q] += s * dwi;
+        }
         switch (cmd) {
           case 1:
-            if (lane == i) D.w = 0;
+            setR(D.w, i, lane, 0.0);
             D.transferToC(i);
             break;
           case 2:
-            if (lane == i) { D.x = D.lo; D.state = 0; }
+            setR(D.x, i, lane, rdlR(D.lo, i));
+            setRi(D.state, i, lane, 0);
             D.nN++;
             break;
           case 3:
-            if (lane == i) { D.x = D.hi; D.state = 1; }
+            setR(D.x, i, lane, rdlR(D.hi, i));
+            setRi(D.state, i, lane, 1);
             D.nN++;
             break;
           case 4:
-            if (lane == si) D.w = 0;
+            setR(D.w, si, lane, 0.0);
             D.transferFromNtoC(si);
             break;
           case 5:
-            if (lane == si) { D.x = D.lo; D.state = 0; }
+            setR(D.x, si, lane, rdlR(D.lo, si));
+            setRi(D.state, si, lane, 0);
             D.transferFromCtoN(si);
             break;
           case 6:
-            if (lane == si) { D.x = D.hi; D.state = 1; }
+            setR(D.x, si, lane, rdlR(D.hi, si));
+            setRi(D.state, si, lane, 1);
             D.transferFromCtoN(si);
             break;
         }
@@ -750,11 +1098,26 @@ __device__ bool waveDantzig(int n, typename Space<kLds>::cdptr Ain, typename Spa
     }
   }
   WSYNC();
-  if (lane < n) scr[D.p] = D.x;
+#pragma unroll
+  for (int s = 0; s < R; s++)
+    if (rowAt(s, lane) < n) scr[D.p[s]] = D.x[s];
   WSYNC();
-  xOut = lane < n ? scr[lane] : 0.0;
+#pragma unroll
+  for (int s = 0; s < R; s++) xOut[s] = rowAt(s, lane) < n ? scr[rowAt(s, lane)] : 0.0;
   WSYNC();
   return true;
+}
+
+template <bool kLds>
+__device__ bool waveDantzig(int n, typename Space<kLds>::cdptr Ain, typename Space<kLds>::dptr Lin,
+                            typename Space<kLds>::dptr scrIn, double& xOut, double b, double lo, double hi,
+                            int findex, int lane, double* dbg = nullptr, const int* cancel = nullptr) {
+  double xa[1];
+  const double ba[1] = {b}, la[1] = {lo}, ha[1] = {hi};
+  const int fa[1] = {findex};
+  const bool ok = waveDantzigR<kLds, 1>(n, Ain, Lin, scrIn, xa, ba, la, ha, fa, lane, dbg, cancel);
+  xOut = xa[0];
+  return ok;
 }
 
 // ---------------------------------------------------------------------------
@@ -766,55 +1129,102 @@ __device__ bool waveDantzig(int n, typename Space<kLds>::cdptr Ain, typename Spa
 // over the surviving rows, each column j scaled by a power of two scl_j:
 //   A_r[r][s] = (A[i][j] + shift [i == j]) * scl_j,  i = act_r, j = act_s.
 // `shift` is a CFM the caller has already (virtually) added to A's diagonal
-// (the PGS fallback reduces A + cfm I).  Lane i holds original row i's b, lo,
-// hi and findex.  Returns (wave-uniform) the mask of surviving rows; lane i
+// (the PGS fallback reduces A + cfm I).  Row i holds original row i's b, lo,
+// hi and findex.  Gives (wave-uniform) the mask of surviving rows; row i
 // gets scl (its column scale, 1 for a removed row) and rep (the surviving row
 // row i was merged into).  `maxMerges` = 0 only reports whether a merge
-// exists (return value != the full mask).
+// exists (mask != the full mask).
 // ---------------------------------------------------------------------------
-template <bool kLds>
-__device__ unsigned long long waveReduce(int m, typename Space<kLds>::cdptr Ain, double shift, double b, double lo,
-                                         double hi, int fi, int lane, double& scl, int& rep, int maxMerges = 64) {
+template <bool kLds, int R>
+__device__ void waveReduceR(int m, typename Space<kLds>::cdptr Ain, double shift, const double (&b)[R],
+                            const double (&lo)[R], const double (&hi)[R], const int (&fi)[R], int lane,
+                            double (&scl)[R], int (&rep)[R], unsigned long long (&alive)[R], int maxMerges = 128) {
   m = uni(m);
   const double* A = (const double*)Ain;
-  unsigned long long alive = m >= 64 ? ~0ull : ((1ull << m) - 1ull);
-  scl = 1.0;
-  rep = lane;
-  const int col = lane < m ? lane : 0;
+  constexpr int kNone = 64 * R;
+  int col[R];
+#pragma unroll
+  for (int s = 0; s < R; s++) {
+    const int lo64 = 64 * s;
+    alive[s] = m >= lo64 + 64 ? ~0ull : (m > lo64 ? ((1ull << (m - lo64)) - 1ull) : 0ull);
+    scl[s] = 1.0;
+    rep[s] = rowAt(s, lane);
+    col[s] = rowAt(s, lane) < m ? rowAt(s, lane) : 0;
+  }
   for (int merges = 0; merges <= maxMerges; merges++) {
     // findex in terms of surviving rows (the reference remaps fIndex on
     // every merge; comparing representatives is the same test)
-    const int fr = __shfl(rep, fi >= 0 ? fi : 0);
-    const int frow = fi >= 0 ? fr : -1;
-    const bool me = lane < m && ((alive >> lane) & 1ull);
-    int hitC = 64;
+    int frow[R], hitC[R];
+    bool me[R];
+#pragma unroll
+    for (int s = 0; s < R; s++) {
+      const int fr = gatherRi(rep, fi[s] >= 0 ? fi[s] : 0);
+      frow[s] = fi[s] >= 0 ? fr : -1;
+      me[s] = rowAt(s, lane) < m && bitR(alive, rowAt(s, lane));
+      hitC[s] = kNone;
+    }
     for (int c = 1; c < m; c++) {
-      if (!((alive >> c) & 1ull)) continue;
-      const double bc = rdl(b, c), loc = rdl(lo, c), hic = rdl(hi, c), sc = rdl(scl, c);
-      const int fc = rdli(frow, c);
-      bool cand = me && lane < c && hitC == 64 && fabs(b - bc) < 1e-4 && frow == fc && hi == hic && lo == loc;
-      if (__ballot(cand)) {
-        double dd = 0.0;
+      if (!bitR(alive, c)) continue;
+      const double bc = rdlR(b, c), loc = rdlR(lo, c), hic = rdlR(hi, c), sc = rdlR(scl, c);
+      const int fc = rdliR(frow, c);
+      bool cand[R], anyCand = false;
+#pragma unroll
+      for (int s = 0; s < R; s++) {
+        cand[s] = me[s] && rowAt(s, lane) < c && hitC[s] == kNone && fabs(b[s] - bc) < 1e-4 && frow[s] == fc &&
+                  hi[s] == hic && lo[s] == loc;
+        anyCand = anyCand || cand[s];
+      }
+      if (__ballot(anyCand)) {
+        double dd[R];
+#pragma unroll
+        for (int s = 0; s < R; s++) dd[s] = 0.0;
         for (int i = 0; i < m; i++) {
-          if (!((alive >> i) & 1ull)) continue;
-          const double aa = (A[i * m + col] + (i == lane ? shift : 0.0)) * scl;
+          if (!bitR(alive, i)) continue;
           const double ac = (A[i * m + c] + (i == c ? shift : 0.0)) * sc;
-          dd += (aa - ac) * (aa - ac);
+#pragma unroll
+          for (int s = 0; s < R; s++) {
+            const double aa = (A[i * m + col[s]] + (i == rowAt(s, lane) ? shift : 0.0)) * scl[s];
+            dd[s] += (aa - ac) * (aa - ac);
+          }
         }
-        if (cand && dd < 1e-4) hitC = c;
+#pragma unroll
+        for (int s = 0; s < R; s++)
+          if (cand[s] && dd[s] < 1e-4) hitC[s] = c;
       }
     }
-    const int a = waveFirst(hitC < 64);
+    bool hit[R];
+#pragma unroll
+    for (int s = 0; s < R; s++) hit[s] = hitC[s] < kNone;
+    const int a = waveFirstR(hit);
     if (a < 0 || merges == maxMerges) {
-      if (a >= 0) alive &= ~(1ull << rdli(hitC, a));  // report only
+      if (a >= 0) {
+        const int cb = rdliR(hitC, a);
+        alive[cb >> 6] &= ~(1ull << (cb & 63));  // report only
+      }
       break;
     }
-    const int cb = rdli(hitC, a);
-    alive &= ~(1ull << cb);
-    if (lane == a) scl *= 2.0;
-    if (rep == cb) rep = a;
+    const int cb = rdliR(hitC, a);
+    alive[cb >> 6] &= ~(1ull << (cb & 63));
+#pragma unroll
+    for (int s = 0; s < R; s++) {
+      if (rowAt(s, lane) == a) scl[s] *= 2.0;
+      if (rep[s] == cb) rep[s] = a;
+    }
   }
-  return alive;
+}
+
+template <bool kLds>
+__device__ unsigned long long waveReduce(int m, typename Space<kLds>::cdptr Ain, double shift, double b, double lo,
+                                         double hi, int fi, int lane, double& scl, int& rep, int maxMerges = 64) {
+  const double ba[1] = {b}, la[1] = {lo}, ha[1] = {hi};
+  const int fa[1] = {fi};
+  double sa[1];
+  int ra[1];
+  unsigned long long al[1];
+  waveReduceR<kLds, 1>(m, Ain, shift, ba, la, ha, fa, lane, sa, ra, al, maxMerges);
+  scl = sa[0];
+  rep = ra[0];
+  return al[0];
 }
 
 // rank of original row `row` among the surviving rows (its reduced index)
@@ -822,29 +1232,59 @@ __device__ __forceinline__ int reducedIndex(unsigned long long alive, int row) {
   return __popcll(alive & ((1ull << row) - 1ull));
 }
 
-// the reduced problem's lane-held vectors: lane r gets the values of the r-th
+// the reduced problem's row-held vectors: row r gets the values of the r-th
 // surviving row (its findex as a reduced index); returns the reduced size
-__device__ __forceinline__ int reducedVectors(unsigned long long alive, int rep, int lane, double& b, double& lo,
-                                              double& hi, int& fi, int& act) {
-  const int mr = __popcll(alive);
+template <int R>
+__device__ __forceinline__ int reducedVectorsR(const unsigned long long (&alive)[R], const int (&rep)[R], int lane,
+                                               double (&b)[R], double (&lo)[R], double (&hi)[R], int (&fi)[R],
+                                               int (&act)[R]) {
+  const int mr = popR(alive);
   // act_r: the r-th set bit of alive
-  act = 0;
+#pragma unroll
+  for (int s = 0; s < R; s++) act[s] = 0;
   {
-    unsigned long long a = alive;
-    for (int r = 0; r < mr; r++) {
-      const int i = __ffsll((long long)a) - 1;
-      if (lane == r) act = i;
-      a &= a - 1ull;
+    int r = 0;
+#pragma unroll
+    for (int q = 0; q < R; q++) {
+      unsigned long long a = alive[q];
+      while (a) {
+        const int i = 64 * q + __ffsll((long long)a) - 1;
+        setRi(act, r, lane, i);
+        a &= a - 1ull;
+        r++;
+      }
     }
   }
-  const int src = lane < mr ? act : 0;
-  const double nb = __shfl(b, src), nlo = __shfl(lo, src), nhi = __shfl(hi, src);
-  const int nfi = __shfl(fi, src);
-  const int frep = __shfl(rep, nfi >= 0 ? nfi : 0);
-  b = lane < mr ? nb : 0.0;
-  lo = lane < mr ? nlo : 0.0;
-  hi = lane < mr ? nhi : 0.0;
-  fi = (lane < mr && nfi >= 0) ? reducedIndex(alive, frep) : -1;
+  double nb[R], nlo[R], nhi[R];
+  int nfi[R];
+#pragma unroll
+  for (int s = 0; s < R; s++) {
+    const int src = rowAt(s, lane) < mr ? act[s] : 0;
+    nb[s] = gatherR(b, src);
+    nlo[s] = gatherR(lo, src);
+    nhi[s] = gatherR(hi, src);
+    nfi[s] = gatherRi(fi, src);
+  }
+#pragma unroll
+  for (int s = 0; s < R; s++) {
+    const int frep = gatherRi(rep, nfi[s] >= 0 ? nfi[s] : 0);
+    const bool in = rowAt(s, lane) < mr;
+    b[s] = in ? nb[s] : 0.0;
+    lo[s] = in ? nlo[s] : 0.0;
+    hi[s] = in ? nhi[s] : 0.0;
+    fi[s] = (in && nfi[s] >= 0) ? rankR(alive, frep) : -1;
+  }
+  return mr;
+}
+
+__device__ __forceinline__ int reducedVectors(unsigned long long alive, int rep, int lane, double& b, double& lo,
+                                              double& hi, int& fi, int& act) {
+  const unsigned long long al[1] = {alive};
+  const int ra[1] = {rep};
+  double ba[1] = {b}, la[1] = {lo}, ha[1] = {hi};
+  int fa[1] = {fi}, aa[1];
+  const int mr = reducedVectorsR<1>(al, ra, lane, ba, la, ha, fa, aa);
+  b = ba[0]; lo = la[0]; hi = ha[0]; fi = fa[0]; act = aa[0];
   return mr;
 }
 
@@ -854,24 +1294,40 @@ __device__ __forceinline__ int reducedVectors(unsigned long long alive, int rep,
 // A_r[max(r,s)][min(r,s)] = A[i][j] * scl_{act_min(r,s)}; written to M
 // (mr x mr).  PGS reads rows (PgsBoxedLcpSolver.cpp:139): its copy is the
 // transpose T[s][r] = A_r[r][s] (wavePgs reads row i, lane j as A_ji).
-template <bool kLds>
-__device__ void reducedMatrix(int m, typename Space<kLds>::cdptr Ain, double shift, unsigned long long alive,
-                              int act, double scl, typename Space<kLds>::dptr Mout, bool forPgs, int lane) {
+template <bool kLds, int R>
+__device__ void reducedMatrixR(int m, typename Space<kLds>::cdptr Ain, double shift,
+                               const unsigned long long (&alive)[R], const int (&act)[R], const double (&scl)[R],
+                               typename Space<kLds>::dptr Mout, bool forPgs, int lane) {
   m = uni(m);
-  const int mr = __popcll(alive);
+  const int mr = popR(alive);
   const double* A = (const double*)Ain;
   double* M = (double*)Mout;
-  const double sclAct = __shfl(scl, lane < mr ? act : 0);  // scale of the lane's reduced column / row
+  double sclAct[R];  // scale of the row's reduced column / row
+#pragma unroll
+  for (int s = 0; s < R; s++) sclAct[s] = gatherR(scl, rowAt(s, lane) < mr ? act[s] : 0);
   for (int r = 0; r < mr; r++) {
-    const int i = rdli(act, r);
-    const double si = rdl(sclAct, r);
-    if (lane < mr) {
-      const int j = act;
-      const double v = A[i * m + j] + (i == j ? shift : 0.0);
-      // forPgs: T[r][lane] = A_r[lane][r] = (A[j][i] + ...) * scl_i
-      // Dantzig: S[r][lane] = A[i][j] * scl_{act_min(r, lane)}
-      M[r * mr + lane] = forPgs ? v * si : v * (r < lane ? si : sclAct);
+    const int i = rdliR(act, r);
+    const double si = rdlR(sclAct, r);
+#pragma unroll
+    for (int s = 0; s < R; s++) {
+      const int row = rowAt(s, lane);
+      if (row < mr) {
+        const int j = act[s];
+        const double v = A[i * m + j] + (i == j ? shift : 0.0);
+        // forPgs: T[r][row] = A_r[row][r] = (A[j][i] + ...) * scl_i
+        // Dantzig: S[r][row] = A[i][j] * scl_{act_min(r, row)}
+        M[r * mr + row] = forPgs ? v * si : v * (r < row ? si : sclAct[s]);
+      }
     }
   }
   WSYNC();
+}
+
+template <bool kLds>
+__device__ void reducedMatrix(int m, typename Space<kLds>::cdptr Ain, double shift, unsigned long long alive,
+                              int act, double scl, typename Space<kLds>::dptr Mout, bool forPgs, int lane) {
+  const unsigned long long al[1] = {alive};
+  const int aa[1] = {act};
+  const double sa[1] = {scl};
+  reducedMatrixR<kLds, 1>(m, Ain, shift, al, aa, sa, Mout, forPgs, lane);
 }

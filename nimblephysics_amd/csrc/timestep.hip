@@ -298,11 +298,17 @@ __device__ __forceinline__ void coreDynamics(const ModelDev& md, double* s, cons
 // one launch): a loop lets the compiler hoist ~120 per-lane model / LDS
 // addresses out of it, which stay live across the whole step and spilled
 // ~150 VGPRs (~44 KB of scratch writes per world).
-extern "C" __global__ void __launch_bounds__(2 * WAVE) __attribute__((amdgpu_waves_per_eu(2)))
-nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, const double* __restrict__ state,
-                      const double* __restrict__ forces, double* __restrict__ lcpCache,
-                      double* __restrict__ nextState, double* __restrict__ snapshot, int snapDoubles,
-                      int cacheDoubles) {
+//
+// R row slots per lane in the contact LCP (contactStage): the R = 1 kernel
+// leaves a world whose LCP has more than `deferRows` rows (> 64: more than
+// 21 frictional contacts) to the R = 2 kernel launched after it, which
+// steps only those worlds, from the same inputs.
+template <int R>
+__device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, const Layout& L,
+                                             const double* __restrict__ state, const double* __restrict__ forces,
+                                             double* __restrict__ lcpCache, double* __restrict__ nextState,
+                                             double* __restrict__ snapshot, int snapDoubles, int cacheDoubles,
+                                             int deferRows) {
   extern __shared__ double s[];
   const ModelDev& md = *mdp;
   const int lane = threadIdx.x & (WAVE - 1);
@@ -371,16 +377,18 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, const double* 
     WSYNC();
     STAMP(12);
     // runConstraintEngine (World.cpp:254): collision, LCP, impulses
+    bool deferred = false;
     if (md.numPairs > 0) {
       double* sn = snapshot + (size_t)env * snapDoubles;
-      contactStage(md, s, L, lane, v1, x, lcpCache + (size_t)env * cacheDoubles, sn, sn + snapWorkspaceOffset(n),
-                   helperOn, helperOn);
+      deferred = contactStage<R>(md, s, L, lane, v1, x, lcpCache + (size_t)env * cacheDoubles, sn,
+                                 sn + snapWorkspaceOffset(n), helperOn, helperOn, deferRows);
     } else if (lane < 8) {
       // a model without collision pairs still has a snapshot header (no
       // contacts, no rows, no clamping) for the getters to read
       snapshot[(size_t)env * snapDoubles + lane] = 0.0;
     }
     if (helperOn) helperRetire(s, L, lane);
+    if (deferred) return;  // the R = 2 kernel writes this world's step
     double* out = nextState + (size_t)env * 2 * n;
     for (int i = lane; i < n; i += WAVE) out[n + i] = v1[i];
     // integratePositions (World.cpp:300): with the pre-step velocity when
@@ -400,6 +408,28 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, const double* 
     WSYNC();
     STAMP(13);
   }
+}
+
+extern "C" __global__ void __launch_bounds__(2 * WAVE) __attribute__((amdgpu_waves_per_eu(2)))
+nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, const double* __restrict__ state,
+                      const double* __restrict__ forces, double* __restrict__ lcpCache,
+                      double* __restrict__ nextState, double* __restrict__ snapshot, int snapDoubles,
+                      int cacheDoubles, int deferRows) {
+  forwardWorld<1>(mdp, L, state, forces, lcpCache, nextState, snapshot, snapDoubles, cacheDoubles, deferRows);
+}
+
+// the worlds nimble_forward_kernel deferred (snapshot status ST_DEFERRED),
+// two LCP rows per lane.  (The same occupancy target as the one-row kernel:
+// the non-inlined narrow-phase functions both kernels call are compiled once,
+// for the tighter of the two register budgets.)
+extern "C" __global__ void __launch_bounds__(2 * WAVE) __attribute__((amdgpu_waves_per_eu(2)))
+nimble_forward_wide_kernel(const ModelDev* __restrict__ mdp, Layout L, const double* __restrict__ state,
+                           const double* __restrict__ forces, double* __restrict__ lcpCache,
+                           double* __restrict__ nextState, double* __restrict__ snapshot, int snapDoubles,
+                           int cacheDoubles) {
+  const int st = uni((int)snapshot[(size_t)blockIdx.x * snapDoubles + SN_STATUS]);
+  if (!(st & ST_DEFERRED)) return;  // (whole workgroup)
+  forwardWorld<2>(mdp, L, state, forces, lcpCache, nextState, snapshot, snapDoubles, cacheDoubles, 1 << 30);
 }
 
 // ---------------------------------------------------------------------------
@@ -520,12 +550,16 @@ __device__ void rightJacobianCol(const double* th, int k, double* o) {
 // VELOCITY and FORCE; rows r >= n_c are zero.  The backward's contact terms
 // already run through lambda = (Q^+)^T u with u the adjoint of f_c, so the
 // mode only replaces u = A_c_ub_E^T Minv gv by e_r (and gv, gp by 0).
-extern "C" __global__ void __launch_bounds__(WAVE)
-nimble_backward_kernel(const ModelDev* __restrict__ mdp, int batch, const double* __restrict__ state,
-                       const double* __restrict__ forces, double* __restrict__ snapshot, int snapDoubles,
-                       const double* __restrict__ gradNext, double* __restrict__ gradState,
-                       double* __restrict__ gradForces, int rows, double* __restrict__ ws, int wsDoubles,
-                       double* __restrict__ gradMasses, int fcMode, int massParams) {
+// R row slots per lane: the R = 1 kernel takes the items of worlds with at
+// most `deferRows` LCP rows, the R = 2 kernel the others.
+template <int R>
+__device__ __forceinline__ void backwardItems(const ModelDev* __restrict__ mdp, int batch,
+                                              const double* __restrict__ state, const double* __restrict__ forces,
+                                              double* __restrict__ snapshot, int snapDoubles,
+                                              const double* __restrict__ gradNext, double* __restrict__ gradState,
+                                              double* __restrict__ gradForces, int rows, double* __restrict__ ws,
+                                              int wsDoubles, double* __restrict__ gradMasses, int fcMode,
+                                              int massParams, int deferRows) {
   extern __shared__ double s[];
   const ModelDev& md = *mdp;
   const Layout& L = md.lay[1];
@@ -536,6 +570,10 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, int batch, const double
   for (long long item = blockIdx.x; item < items; item += gridDim.x) {
     const int env = rows == 1 ? (int)item : (int)(item / rows);
     const int unitRow = rows == 1 ? -1 : (int)(item - (long long)env * rows);
+    if (md.numPairs > 0) {
+      const int mEnv = uni((int)snapshot[(size_t)env * snapDoubles + SN_M]);
+      if ((mEnv > deferRows) != (R > 1)) continue;  // the other kernel's item
+    }
 #ifdef NIMBLE_STAGE_TIMING
     double* g_stamp = md.numPairs > 0 ? snapshot + (size_t)env * snapDoubles + snapWorkspaceOffset(n) + 1000 : nullptr;
 #endif
@@ -574,7 +612,7 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, int batch, const double
       // constrained: a* = Minv (z + A_c_ub_E f_c) / dt, w <- w - nu
       const int need = bwdPoolDoubles(m, n);
       carveBwd(need <= L.poolCap ? s + L.pool : hbmWs, m, n, P);
-      imp = contactBackwardPrep(md, s, L, lane, sn, P, m, nc, s + L.ct, fcMode ? unitRow : -1);
+      imp = contactBackwardPrep<R>(md, s, L, lane, sn, P, m, nc, s + L.ct, fcMode ? unitRow : -1);
     } else {
       // z = dt (tau - C - D v - K (q - q0 + dt v))
       for (int i = lane; i < n; i += WAVE) {
@@ -618,9 +656,9 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, int batch, const double
         if (c < 3) {
           rightJacobianCol(th, c, xi);
         } else {
-          double R[9];
-          expMapRot(th, R);
-          for (int r = 0; r < 3; r++) xi[3 + r] = R[(c - 3) * 3 + r];  // R^T e_c
+          double Rm[9];
+          expMapRot(th, Rm);
+          for (int r = 0; r < 3; r++) xi[3 + r] = Rm[(c - 3) * 3 + r];  // R^T e_c
         }
         double TwC[12];
         tmul(s + L.Tw + 12 * b, md.Tcj[b], TwC);
@@ -661,9 +699,9 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, int batch, const double
       double* buf = s + L.adj;
       TACC_BEGIN(tG);
 #ifdef NIMBLE_STAGE_TIMING
-      const double gterm = contactGTermsAll(md, s, L, sn, P, m, Z, buf, lane, g_stamp);
+      const double gterm = contactGTermsAll<R>(md, s, L, sn, P, m, Z, buf, lane, g_stamp);
 #else
-      const double gterm = contactGTermsAll(md, s, L, sn, P, m, Z, buf, lane);
+      const double gterm = contactGTermsAll<R>(md, s, L, sn, P, m, Z, buf, lane);
 #endif
       WSYNC();
       TACC_END(80, tG);
@@ -834,4 +872,24 @@ nimble_backward_kernel(const ModelDev* __restrict__ mdp, int batch, const double
     WSYNC();
     STAMP(26);
   }
+}
+
+extern "C" __global__ void __launch_bounds__(WAVE)
+nimble_backward_kernel(const ModelDev* __restrict__ mdp, int batch, const double* __restrict__ state,
+                       const double* __restrict__ forces, double* __restrict__ snapshot, int snapDoubles,
+                       const double* __restrict__ gradNext, double* __restrict__ gradState,
+                       double* __restrict__ gradForces, int rows, double* __restrict__ ws, int wsDoubles,
+                       double* __restrict__ gradMasses, int fcMode, int massParams, int deferRows) {
+  backwardItems<1>(mdp, batch, state, forces, snapshot, snapDoubles, gradNext, gradState, gradForces, rows, ws,
+                   wsDoubles, gradMasses, fcMode, massParams, deferRows);
+}
+
+extern "C" __global__ void __launch_bounds__(WAVE)
+nimble_backward_wide_kernel(const ModelDev* __restrict__ mdp, int batch, const double* __restrict__ state,
+                            const double* __restrict__ forces, double* __restrict__ snapshot, int snapDoubles,
+                            const double* __restrict__ gradNext, double* __restrict__ gradState,
+                            double* __restrict__ gradForces, int rows, double* __restrict__ ws, int wsDoubles,
+                            double* __restrict__ gradMasses, int fcMode, int massParams, int deferRows) {
+  backwardItems<2>(mdp, batch, state, forces, snapshot, snapDoubles, gradNext, gradState, gradForces, rows, ws,
+                   wsDoubles, gradMasses, fcMode, massParams, deferRows);
 }

@@ -101,3 +101,128 @@ __device__ __forceinline__ double shiftDown1(double v, int lane) {
   return __shfl(v, lane + 1 < 64 ? lane + 1 : lane);
 }
 __device__ __forceinline__ int shiftDown1i(int v, int lane) { return __shfl(v, lane + 1 < 64 ? lane + 1 : lane); }
+
+// ---------------------------------------------------------------------------
+// Row-distributed vectors of up to 64 R elements: row i lives on lane
+// (i & 63) in register slot (i >> 6) (R = 1 is the plain one-element-per-lane
+// layout above; R = 2 carries the 65..128-row LCPs of worlds with more than
+// 21 frictional contacts).  Row indices passed to these helpers are
+// wave-uniform.
+template <int R>
+__device__ __forceinline__ double rdlR(const double (&v)[R], int i) {
+  if constexpr (R == 1) return rdl(v[0], i);
+  else return rdl((i >> 6) ? v[1] : v[0], i & 63);
+}
+template <int R>
+__device__ __forceinline__ int rdliR(const int (&v)[R], int i) {
+  if constexpr (R == 1) return rdli(v[0], i);
+  else return rdli((i >> 6) ? v[1] : v[0], i & 63);
+}
+// row index of slot s on this lane
+__device__ __forceinline__ int rowAt(int s, int lane) { return lane + 64 * s; }
+// sum over all rows' partial values
+template <int R>
+__device__ __forceinline__ double waveSumR(const double (&v)[R]) {
+  double t = v[0];
+#pragma unroll
+  for (int s = 1; s < R; s++) t += v[s];
+  return waveSum(t);
+}
+// set row i of v (i wave-uniform) to val (this lane's value)
+template <int R>
+__device__ __forceinline__ void setR(double (&v)[R], int i, int lane, double val) {
+#pragma unroll
+  for (int s = 0; s < R; s++)
+    if (rowAt(s, lane) == i) v[s] = val;
+}
+template <int R>
+__device__ __forceinline__ void setRi(int (&v)[R], int i, int lane, int val) {
+#pragma unroll
+  for (int s = 0; s < R; s++)
+    if (rowAt(s, lane) == i) v[s] = val;
+}
+// bit i of a row mask
+template <int R>
+__device__ __forceinline__ bool bitR(const unsigned long long (&mk)[R], int i) {
+  if constexpr (R == 1) return (mk[0] >> i) & 1ull;
+  else return (((i >> 6) ? mk[1] : mk[0]) >> (i & 63)) & 1ull;
+}
+template <int R>
+__device__ __forceinline__ int popR(const unsigned long long (&mk)[R]) {
+  int c = 0;
+#pragma unroll
+  for (int s = 0; s < R; s++) c += __popcll(mk[s]);
+  return c;
+}
+// number of set rows below row i
+template <int R>
+__device__ __forceinline__ int rankR(const unsigned long long (&mk)[R], int i) {
+  int c = 0;
+#pragma unroll
+  for (int s = 0; s < R; s++) {
+    const int lo = 64 * s;
+    if (i >= lo + 64) c += __popcll(mk[s]);
+    else if (i > lo) c += __popcll(mk[s] & ((1ull << (i - lo)) - 1ull));
+  }
+  return c;
+}
+// lowest row whose predicate holds (-1 if none)
+template <int R>
+__device__ __forceinline__ int waveFirstR(const bool (&pred)[R]) {
+#pragma unroll
+  for (int s = 0; s < R; s++) {
+    const unsigned long long m = __ballot(pred[s]);
+    if (m) return 64 * s + __ffsll((long long)m) - 1;
+  }
+  return -1;
+}
+template <int R>
+__device__ __forceinline__ double waveMinR(const double (&v)[R]) {
+  double t = v[0];
+#pragma unroll
+  for (int s = 1; s < R; s++) t = fmin(t, v[s]);
+  return waveMin(t);
+}
+// row i receives row i + 1 (the last row keeps its own value)
+template <int R>
+__device__ __forceinline__ void shiftDownR(double (&v)[R], int lane) {
+  double nx[R];
+#pragma unroll
+  for (int s = 0; s < R; s++) {
+    nx[s] = __shfl(v[s], lane + 1 < 64 ? lane + 1 : lane);
+    const double next = s + 1 < R ? rdl(v[s + 1 < R ? s + 1 : s], 0) : v[s];
+    if (lane == 63) nx[s] = next;
+  }
+#pragma unroll
+  for (int s = 0; s < R; s++) v[s] = nx[s];
+}
+template <int R>
+__device__ __forceinline__ void shiftDownRi(int (&v)[R], int lane) {
+  int nx[R];
+#pragma unroll
+  for (int s = 0; s < R; s++) {
+    nx[s] = __shfl(v[s], lane + 1 < 64 ? lane + 1 : lane);
+    const int next = s + 1 < R ? rdli(v[s + 1 < R ? s + 1 : s], 0) : v[s];
+    if (lane == 63) nx[s] = next;
+  }
+#pragma unroll
+  for (int s = 0; s < R; s++) v[s] = nx[s];
+}
+// value of row `src` (lane-varying) of v, for every slot's row: a gather
+// across rows (the R = 1 case is __shfl)
+template <int R>
+__device__ __forceinline__ double gatherR(const double (&v)[R], int src) {
+  if constexpr (R == 1) return __shfl(v[0], src & 63);
+  else {
+    const double a = __shfl(v[0], src & 63), b = __shfl(v[1], src & 63);
+    return (src >> 6) ? b : a;
+  }
+}
+template <int R>
+__device__ __forceinline__ int gatherRi(const int (&v)[R], int src) {
+  if constexpr (R == 1) return __shfl(v[0], src & 63);
+  else {
+    const int a = __shfl(v[0], src & 63), b = __shfl(v[1], src & 63);
+    return (src >> 6) ? b : a;
+  }
+}

@@ -285,6 +285,28 @@ def test_hbm_workspace_path(rows, monkeypatch):
     _parity(world, st, f)
 
 
+@pytest.mark.parametrize("world_name", ["box", "atlas", "half_cheetah", "capsule_edge"])
+def test_wide_kernels(world_name, monkeypatch):
+    """The two-rows-per-lane kernels (nimble_forward_wide_kernel /
+    nimble_backward_wide_kernel, which take worlds with more than 64 LCP
+    rows) forced onto every contact world (NIMBLE_AMD_DEFER_ROWS=0): the
+    same parity against the oracle as the one-row-per-lane kernels."""
+    monkeypatch.setenv("NIMBLE_AMD_DEFER_ROWS", "0")
+    if world_name == "box":
+        world = models.box_world()
+        st, f = models.box_states("slide", 32, seed=8)
+    elif world_name == "atlas":
+        world = models.atlas_world(True)
+        st, f = models.random_states(world, 96, seed=12, q_scale=0.02, v_scale=0.05)
+    elif world_name == "half_cheetah":
+        world = models.half_cheetah_world()
+        st, f = models.half_cheetah_states(world, 64, seed=5)
+    else:
+        world = models.capsule_edge_world()
+        st, f = models.capsule_edge_states(32, seed=2)
+    _parity(world, st, f)
+
+
 @pytest.mark.parametrize("name", ["edge", "ledge"])
 def test_edge_edge_contact_parity(name):
     """EDGE_EDGE contacts and their gradient terms: the reference's

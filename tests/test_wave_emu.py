@@ -1,0 +1,93 @@
+"""The product kernels on the CPU: nimblephysics_amd/csrc compiled for the
+host against an emulation of the HIP execution model (tests/cpp/wave_emu:
+every lane a host thread, every cross-lane operation a rendezvous of the
+wave, checked for lanes out of step), with AddressSanitizer.
+
+* the wave LCP kernels (waveDantzigR, wavePgsR, waveLcpValidR, waveReduceR,
+  the COD factor and solve) in their one-row-per-lane (R = 1) and
+  two-rows-per-lane (R = 2) forms agree with each other bit for bit on
+  problems up to 64 rows and Dantzig agrees with the oracle's dSolveLCP
+  restatement up to 96 rows;
+* a whole forward + backward step through the C-ABI (capi.cpp unchanged,
+  kernels launched by the emulation), with the default split and with every
+  contact world forced through the wide kernels (NIMBLE_AMD_DEFER_ROWS=0),
+  matches the oracle -- and any out-of-bounds access aborts the run.
+
+No GPU needed; the emulation runs a few worlds in tens of seconds.
+"""
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+import models
+import wave_emu
+from oracle import oracle as O
+
+pytestmark = pytest.mark.skipif(not os.path.exists(wave_emu.CLANG) or shutil.which("true") is None,
+                                reason="needs the ROCm clang for the host build")
+
+
+def _problems(sizes, seed=3):
+    rng = np.random.default_rng(seed)
+    out = []
+    for m in sizes:
+        J = rng.standard_normal((m, 2 * m // 3 + 3))
+        A = J @ J.T + 1e-3 * np.eye(m)
+        b = rng.standard_normal(m)
+        lo, hi, fi = np.zeros(m), np.full(m, np.inf), -np.ones(m, dtype=int)
+        for c in range(m // 3):
+            for k in (1, 2):
+                lo[3 * c + k], hi[3 * c + k], fi[3 * c + k] = -0.8, 0.8, 3 * c
+        out.append((m, A, b, lo, hi, fi))
+    return out
+
+
+def test_lcp_wave_kernels_r1_r2():
+    exe = wave_emu.build("lcp_wave_emu")
+    probs = _problems((12, 40, 63, 66, 96))
+    txt = [str(len(probs))]
+    for m, A, b, lo, hi, fi in probs:
+        txt += [str(m), wave_emu._fmt(A), wave_emu._fmt(b), wave_emu._fmt(lo), wave_emu._fmt(hi),
+                wave_emu._fmt(fi, True), wave_emu._fmt(np.zeros(m))]
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")
+    r = subprocess.run([exe], input="\n".join(txt), capture_output=True, text=True, timeout=900, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    res = {}
+    for ln in r.stdout.splitlines():
+        t = ln.split()
+        R, m = int(t[0]), int(t[1])
+        res[(R, m)] = t[2:]
+    for m, A, b, lo, hi, fi in probs:
+        t2 = res[(2, m)]
+        if m <= 64:
+            assert res[(1, m)] == t2, m  # bit for bit
+        ok = bool(int(t2[0]))
+        x = np.array(t2[1:1 + m], dtype=float)
+        ok_ref, x_ref = O.dantzig(A, b, lo, hi, fi, True)
+        assert ok == ok_ref, m
+        if ok:
+            assert np.abs(x - x_ref).max() <= 1e-9 * max(1.0, np.abs(x_ref).max()), m
+        rank = int(t2[2 * m + 4])
+        assert rank == m
+        xc = np.array(t2[2 * m + 5:3 * m + 5], dtype=float)
+        ref = np.linalg.solve(A, b)
+        assert np.abs(xc - ref).max() <= 1e-8 * np.abs(ref).max(), m
+
+
+@pytest.mark.parametrize("defer", [None, "0"])
+def test_box_step_emulated(defer):
+    world = models.box_world()
+    st, f = models.box_states("slide", 2, seed=8)
+    g = np.random.default_rng(1).standard_normal(st.shape)
+    env = {"NIMBLE_AMD_DEFER_ROWS": defer} if defer else {}
+    nxt, gs, gf, head = wave_emu.step(world, st, f, g, env)
+    ow = O.OracleWorld(world)
+    ref = ow.forward(st, f)
+    rgs, rgf = ow.backward(g)
+    assert (head[:, 0] > 0).all()  # in contact
+    assert np.abs(nxt - ref).max() <= 1e-12
+    assert np.abs(gs - rgs).max() <= 1e-9 * np.abs(rgs).max()
+    assert np.abs(gf - rgf).max() <= 1e-9 * np.abs(rgf).max()

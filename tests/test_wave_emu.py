@@ -91,3 +91,24 @@ def test_box_step_emulated(defer):
     assert np.abs(nxt - ref).max() <= 1e-12
     assert np.abs(gs - rgs).max() <= 1e-9 * np.abs(rgs).max()
     assert np.abs(gf - rgf).max() <= 1e-9 * np.abs(rgf).max()
+
+
+def test_mesh_atlas_wide_step_emulated():
+    """Atlas with the STL soles: a bench-sampler world whose LCP has more
+    than 64 rows (81), stepped by the two-rows-per-lane kernels."""
+    from nimblephysics_amd import workloads
+    world = workloads.atlas_mesh_world(True)
+    st, f = workloads.random_states(world, 5, seed=1000, q_scale=0.02, v_scale=0.05)
+    st, f = st[4:5], f[4:5]
+    ow = O.OracleWorld(world)
+    ref = ow.forward(st, f)
+    assert len(O.lcp_debug(ow, 0)[0]) > 64
+    g = np.random.default_rng(3).standard_normal(st.shape)
+    rgs, rgf = ow.backward(g)
+    nxt, gs, gf, head = wave_emu.step(world, st, f, g)
+    assert int(head[0, 1]) > 64
+    assert np.abs(nxt - ref).max() <= 1e-11
+    # velocity-gradient noise of the FreeJoint central differences (see
+    # test_gpu_contact_parity.GRAD_FLOOR): 1e-9 of the largest element
+    assert np.abs(gs - rgs).max() <= 1e-9 * np.abs(rgs).max() * 10
+    assert np.abs(gf - rgf).max() <= 1e-9 * np.abs(rgf).max()

@@ -328,6 +328,14 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
       {
         const int env = blockIdx.x;
         double* ct = lds<true>(s) + L.ct;
+#ifdef NIMBLE_STAGE_TIMING
+        // where the helper runs: HW_ID (SIMD, CU, SE) and XCC_ID
+        if (lane == 0 && md.numPairs > 0) {
+          double* gs = snapshot + (size_t)env * snapDoubles + snapWorkspaceOffset(n) + 1000;
+          gs[92] = (double)(unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));
+          gs[93] = (double)(unsigned)__builtin_amdgcn_s_getreg(20 | (15 << 11));
+        }
+#endif
         collideWait(ct, CS_GO);
         collideWorld(md, lds<true>(s), L, lane, snapshot + (size_t)env * snapDoubles + snEdge(n));
         collidePost(ct, CS_DONE, lane);
@@ -344,6 +352,13 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
     double* g_stamp = md.numPairs > 0 ? snapshot + (size_t)env * snapDoubles + snapWorkspaceOffset(n) + 1000 : nullptr;
 #endif
     STAMP(10);
+#ifdef NIMBLE_STAGE_TIMING
+    // where wave 0 runs: HW_ID (SIMD, CU, SE) and XCC_ID
+    if (lane == 0 && g_stamp) {
+      g_stamp[90] = (double)(unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));
+      g_stamp[91] = (double)(unsigned)__builtin_amdgcn_s_getreg(20 | (15 << 11));
+    }
+#endif
     loadState(md, s, L, lane, st, forces + (size_t)env * n);
 #ifdef NIMBLE_STAGE_TIMING
     kinematics(md, s, L, lane, nullptr, g_stamp);

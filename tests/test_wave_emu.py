@@ -112,3 +112,14 @@ def test_mesh_atlas_wide_step_emulated():
     # test_gpu_contact_parity.GRAD_FLOOR): 1e-9 of the largest element
     assert np.abs(gs - rgs).max() <= 1e-9 * np.abs(rgs).max() * 10
     assert np.abs(gf - rgf).max() <= 1e-9 * np.abs(rgf).max()
+
+
+def test_snapshot_layout_matches_pool_sizes():
+    """_native.snapshot_layout (tools, tests) against csrc/pool_sizes.h."""
+    from nimblephysics_amd import _native
+    exe = wave_emu.build("layout_emu")
+    for n in (1, 6, 9, 33, 64):
+        got = [int(x) for x in subprocess.check_output([exe, str(n)], text=True).split()]
+        L = _native.snapshot_layout(n)
+        want = [L[k] for k in ("contacts", "rows", "fc", "vf", "yf", "ac", "acube", "pt", "q", "edge", "workspace")]
+        assert got == want, (n, got, want)

@@ -23,12 +23,8 @@ g = np.random.default_rng(1000).standard_normal(st.shape)
 ggs, ggf = _device_backward(world, ts, tf, tsnap, g)
 rgs, rgf = ow.backward(g)
 snap = tsnap.cpu().numpy()
-SN_FC = 16 + 13 * _native.MAX_CONTACTS + 12 * MAXL
-snYf = SN_FC + MAXL + n
-a8 = lambda x: ((x + 7) // 8) * 8
-snAc = a8(snYf + n)
-snPT = snAc + 2 * n * MAXL
-snQ = snPT + MAXL * MAXL
+LAY = _native.snapshot_layout(n)
+snPT, snQ = LAY["pt"], LAY["q"]
 for b in range(B):
     sn = snap[b]
     m = int(sn[SN_M])

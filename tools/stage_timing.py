@@ -21,10 +21,8 @@ snap = torch.zeros((B, dev.snapshot_doubles), dtype=torch.float64, device=d)
 nxt = torch.empty_like(state)
 s = torch.cuda.current_stream().cuda_stream
 n = w.getNumDofs()
-a8 = lambda x: ((x + 7) // 8) * 8
-CREC = 13  # csrc/pool_sizes.h
-SN_VF = 16 + 16 * CREC + 48 * 12 + 48
-ws = a8(a8(SN_VF + 2 * n) + 2 * n * 48 + 2 * 2304 + 16 * 12) + 1000  # snapWorkspaceOffset(n) + 1000
+from nimblephysics_amd import _native  # noqa: E402
+ws = _native.snapshot_layout(n)["stamps"]  # snapWorkspaceOffset(n) + 1000
 for it in range(4):
     snap[:, ws:ws + 100] = 0
     prev_state, prev_cache = state.clone(), cache.clone()
@@ -104,3 +102,27 @@ if out:
                        for wi in np.argsort(-tot_all)[:10]]}
     json.dump(res, open(out, "w"), indent=1)
     print("histogram ->", out, json.dumps({k: res[k] for k in ("mean", "p50", "p99", "max", "max_over_mean")}))
+
+# placement of each world's two waves (HW_ID: SIMD bits 5:4, CU 11:8, SE
+# 15:13; XCC_ID bits 3:0), from the last batch step
+hw0, hw1 = T[:, 90].astype(np.int64), T[:, 92].astype(np.int64)
+xcc0 = T[:, 91].astype(np.int64) & 15
+have = (hw0 > 0) | (hw1 > 0)
+if have.any():
+    simd0, simd1 = (hw0 >> 4) & 3, (hw1 >> 4) & 3
+    cu0, cu1 = (hw0 >> 8) & 15, (hw1 >> 8) & 15
+    same_simd = (simd0 == simd1) & (cu0 == cu1)
+    tot_all = np.where((T[:, 10] > 0) & (T[:, 13] > 0), T[:, 13] - T[:, 10], 0).astype(np.float64)
+    ok = have & (tot_all > 0)
+    print(f"placement: worlds {int(have.sum())}, helper on wave 0's SIMD {int(same_simd[have].sum())}, "
+          f"XCC histogram {np.bincount(xcc0[have], minlength=8).tolist()}")
+    for name, msk in (("same SIMD", ok & same_simd), ("other SIMD", ok & ~same_simd)):
+        if msk.any():
+            print(f"  {name:10s}: worlds {int(msk.sum())} mean {tot_all[msk].mean():.0f} clk, max {tot_all[msk].max():.0f}")
+    if out:
+        res = json.load(open(out))
+        res["placement"] = {"helper_on_same_simd": int(same_simd[have].sum()), "worlds": int(have.sum()),
+                            "xcc_histogram": np.bincount(xcc0[have], minlength=8).tolist(),
+                            "mean_clk_same_simd": float(tot_all[ok & same_simd].mean()) if (ok & same_simd).any() else None,
+                            "mean_clk_other_simd": float(tot_all[ok & ~same_simd].mean()) if (ok & ~same_simd).any() else None}
+        json.dump(res, open(out, "w"), indent=1)

@@ -19,10 +19,8 @@ snap = torch.zeros((B, dev.snapshot_doubles), dtype=torch.float64, device=d)
 nxt = torch.empty_like(state)
 s = torch.cuda.current_stream().cuda_stream
 n = w.getNumDofs()
-a8 = lambda x: ((x + 7) // 8) * 8
-CREC = 13  # csrc/pool_sizes.h
-SN_VF = 16 + 16 * CREC + 48 * 12 + 48
-ws = a8(a8(SN_VF + 2 * n) + 2 * n * 48 + 2 * 2304 + 16 * 12) + 1000  # snapWorkspaceOffset(n) + 1000
+from nimblephysics_amd import _native  # noqa: E402
+ws = _native.snapshot_layout(n)["stamps"]  # snapWorkspaceOffset(n) + 1000
 g = torch.tensor(np.random.default_rng(0).standard_normal(st.shape), device=d)
 gs, gf = torch.empty_like(state), torch.empty_like(action)
 dev.forward(state, action, cache, nxt, snap, s)

@@ -307,7 +307,7 @@ __device__ void tangentBasisODE(const double* n, double* t1, double* t2) {
 
 struct FwdPool {
   double *cols, *massed, *A, *M1, *M2;
-  double *lo, *hi, *b, *X, *aCol, *rest, *pen, *relVel, *fc, *Eval, *nx, *fsol, *xc, *xh, *xh2, *dvec;
+  double *lo, *hi, *b, *X, *aCol, *rest, *pen, *relVel, *fc, *Eval, *nx, *fsol, *xc, *xh, *xh2, *xp, *xf, *dvec;
   int *fi, *mapping, *clampIdx, *ubIdx, *rowC, *rowDir, *clampRow, *cl;
   double* scr;  // >= 10 m + 2 n + 16
 };
@@ -334,8 +334,10 @@ __device__ inline void carveFwd(double* base, int m, int n, FwdPool& P) {
   P.nx = p; p += m;
   P.fsol = p; p += m;
   P.xc = p; p += m;
-  P.xh = p; p += m;   // the helper wave's PGS solution
-  P.xh2 = p; p += m;  // ... and its frictionless PGS solution
+  P.xh = p; p += m;   // the helper wave's Dantzig solution
+  P.xh2 = p; p += m;  // ... and its scratch
+  P.xp = p; p += m;   // the PGS fallback's solution (either wave)
+  P.xf = p; p += m;   // the frictionless PGS's solution (either wave)
   P.dvec = p; p += 3 * m;
   int* ip = reinterpret_cast<int*>(p);
   P.fi = ip; ip += m;
@@ -401,27 +403,48 @@ __device__ __forceinline__ void gramMfma(const double* Y, double* A, int n, int 
 #define H_IGN 10
 #define H_K 11
 #define H_CODOK 12  // M1 + scr hold the COD of the final clamping Q
-#define H_HELPER 13 // 2 doubles = 4 ints: helper state, cancel, PGS ok (see helperWave)
+#define H_HELPER 13 // 2 doubles = 4 ints: helper state (HS_*), unused x3
 #define H_COLLIDE 15  // 2 ints: collision-detection hand-off between the waves (CS_*)
 #define H_PAIRCNT 16   // 16 per-pair counts of the current chunk
+#define H_BOARD 32     // 8 doubles = 16 ints: the LCP task board (BD_*)
 
 // ---------------------------------------------------------------------------
 // Helper wave.  The forward kernel runs two waves per world: wave 0 does the
-// step, wave 1 runs the first PGS fallback (PgsBoxedLcpSolver::solve on
-// A + cfm I from the warm start) speculatively while wave 0 runs Dantzig.
-// The reference runs that PGS only once Dantzig has failed, from the same
-// inputs (neither Dantzig nor the validity check touches A, b, lo, hi,
-// findex or the warm start), so taking the helper's result is identical and
-// Dantzig and PGS overlap instead of adding up.  Protocol per world, LDS ints
-// at ct[H_HELPER] {state, cancel, ok}: wave 0 posts TASK or SKIP exactly
-// once, the helper answers DONE, wave 0 resets to IDLE; a task still running
-// when wave 0 no longer needs it is cancelled (checked after every sweep).
+// step; wave 1 (the helper) detects the contacts (collideWorld, below) and
+// then shares the LCP cascade of BoxedLcpConstraintSolver::solve with wave 0.
+// The reference's cascade is a priority order over independent computations
+// on the same inputs A, b, lo, hi, findex (none of them writes those):
+//   C  the short-circuit classification (devConstruct, from the warm start)
+//   D  Dantzig on A (LCPUtils::reduce first: taken here only when it merges
+//      no column; otherwise wave 0 runs the reduced Dantzig itself)
+//   P  PGS on (reduced) A + cfm I from the warm start
+//   F  PGS on the normal rows only (LCPUtils::removeFriction), from zero
+// and its answer is the first of C, D, P, F that succeeds (and validates).
+// D needs only A, so the helper starts it as soon as A is built, while wave 0
+// computes the warm start and runs C; whichever wave is free then claims P
+// (once the warm start is final) and F.  Results are written to their own LDS
+// vectors (xh, xp, xf) and taken in the reference's order, so the answer is
+// the same whichever wave computed it and however the work interleaved; a
+// computation made moot by a higher-priority success is cancelled (polled
+// per pivot / sweep).  Protocol per world: wave 0 posts TASK (board cleared)
+// or SKIP exactly once, the helper answers DONE once it has stopped touching
+// the pool, wave 0 resets to IDLE.
 // ---------------------------------------------------------------------------
 #define HS_IDLE 0
 #define HS_TASK 1
 #define HS_SKIP 2
 #define HS_DONE 3
-#define HS_MID 4  // first PGS answered, frictionless PGS running
+#define BD_G 0        // warm start final (P.xc): 1
+#define BD_D 1        // Dantzig: 0 running, 1 ok + valid, 2 failed, 3 not run (reduce merges)
+#define BD_PCLAIM 2   // PGS fallback: 0 unclaimed, 1 wave 0, 2 helper
+#define BD_P 3        //   0 pending, 1 ok + valid, 2 failed
+#define BD_PDUP 4     //   its reduce merged columns
+#define BD_FCLAIM 5   // frictionless PGS: claim as BD_PCLAIM
+#define BD_F 6        //   0 pending, 1 done
+#define BD_STOPD 7    // cancel flags: Dantzig,
+#define BD_STOPP 8    //   PGS fallback,
+#define BD_STOPF 9    //   frictionless PGS
+#define BD_INTS 10
 __device__ __forceinline__ int* helperFlags(double* ct) { return reinterpret_cast<int*>(ct + H_HELPER); }
 __device__ __forceinline__ void helperPost(double* ct, int state, int lane) {
   // release: the task's LDS inputs are visible before the state changes
@@ -440,6 +463,24 @@ __device__ __forceinline__ int helperWait(double* ct, Pred pred) {
     if (it > (1ll << 24)) __builtin_trap();
     __builtin_amdgcn_s_sleep(1);
   }
+}
+__device__ __forceinline__ int* board(double* ct) { return reinterpret_cast<int*>(ct + H_BOARD); }
+__device__ __forceinline__ int boardGet(double* ct, int k) {
+  return uni(__hip_atomic_load(board(ct) + k, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+__device__ __forceinline__ void boardSet(double* ct, int k, int v, int lane) {
+  // release: a result's LDS vector is visible before its state
+  if (lane == 0) __hip_atomic_store(board(ct) + k, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// claim task slot k for `who` (1 wave 0, 2 helper); true for the one winner
+__device__ __forceinline__ bool boardClaim(double* ct, int k, int who, int lane) {
+  int won = 0;
+  if (lane == 0) {
+    int expect = 0;
+    won = __hip_atomic_compare_exchange_strong(board(ct) + k, &expect, who, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP) ? 1 : 0;
+  }
+  return rdli(won, 0) != 0;
 }
 
 // Collision detection on the helper wave.  collideWorld only reads the
@@ -1123,6 +1164,104 @@ __device__ void backwardPrecompute(const ModelDev& md, lds_double* sIn, const La
 }
 
 // ---------------------------------------------------------------------------
+// The LCP fallbacks of BoxedLcpConstraintSolver::solve, as functions of the
+// problem (A, b, lo, hi, findex, warm start in the pool) so that either wave
+// of the forward workgroup can run them (see the task board above).
+// ---------------------------------------------------------------------------
+template <int R>
+__device__ __forceinline__ bool allRowsAlive(int m, const unsigned long long (&alive)[R]) {
+  bool eq = true;
+#pragma unroll
+  for (int q = 0; q < R; q++) {
+    const int lo64 = 64 * q;
+    const unsigned long long full = m >= lo64 + 64 ? ~0ull : (m > lo64 ? ((1ull << (m - lo64)) - 1ull) : 0ull);
+    eq = eq && alive[q] == full;
+  }
+  return eq;
+}
+
+// PGS on the reduced A + cfm I (BoxedLcpConstraintSolver.cpp:550-597) from
+// the warm start x_c: LCPUtils::reduce at shift cfm; when it merges columns
+// the reduced matrix goes to `Mred` (M1 or M2: whichever the running wave
+// owns) and the solution is mapped out (x_i = x_r[rank(rep_i)]).  Returns
+// success and validity on the full problem; `dup`: reduce merged columns.
+template <bool kLds, int R>
+__device__ bool pgsFallbackR(const FwdPool& P, int m, double cf, const double (&bR)[R], const double (&loR)[R],
+                             const double (&hiR)[R], const int (&fiR)[R], typename Space<kLds>::dptr Mred, int lane,
+                             double (&xd)[R], bool& dup, const int* cancel, double* dbg) {
+  double scl[R];
+  int rep[R];
+  unsigned long long alive[R];
+  waveReduceR<kLds, R>(m, spc<kLds>(P.A), cf, bR, loR, hiR, fiR, lane, scl, rep, alive);
+  WSYNC();
+  dup = !allRowsAlive<R>(m, alive);
+  bool ok;
+  if (dup) {
+    double br[R], lr[R], hr[R], xc[R], xr[R];
+    int fr[R], act[R];
+#pragma unroll
+    for (int q = 0; q < R; q++) {
+      br[q] = bR[q]; lr[q] = loR[q]; hr[q] = hiR[q]; fr[q] = fiR[q];
+      xc[q] = rowAt(q, lane) < m ? P.xc[rowAt(q, lane)] : 0.0;
+    }
+    const int mr = reducedVectorsR<R>(alive, rep, lane, br, lr, hr, fr, act);
+    reducedMatrixR<kLds, R>(m, spc<kLds>(P.A), cf, alive, act, scl, Mred, true, lane);
+#pragma unroll
+    for (int q = 0; q < R; q++) {
+      xr[q] = gatherR(xc, rowAt(q, lane) < mr ? act[q] : 0);
+      if (rowAt(q, lane) >= mr) xr[q] = 0.0;
+    }
+    ok = wavePgsR<kLds, false, R>(mr, (typename Space<kLds>::cdptr)Mred, xr, br, lr, hr, fr, lane, nullptr, 0.0, cancel);
+#pragma unroll
+    for (int q = 0; q < R; q++) xd[q] = gatherR(xr, rankR(alive, rep[q]));
+  } else {
+#pragma unroll
+    for (int q = 0; q < R; q++) xd[q] = rowAt(q, lane) < m ? P.xc[rowAt(q, lane)] : 0.0;
+    ok = wavePgsR<kLds, false, R>(m, spc<kLds>(P.A), xd, bR, loR, hiR, fiR, lane, dbg, cf, cancel);
+  }
+  if (ok) ok = waveLcpValidR<kLds, R>(m, spc<kLds>(P.A), cf, xd, bR, hiR, loR, fiR, false, lane);
+  return ok;
+}
+
+// LCPUtils::removeFriction + PGS on the normal rows only (the principal
+// submatrix of A + cfm I over them, read in place), from zero; the answer
+// per row (friction rows 0).
+template <bool kLds, int R>
+__device__ void frictionlessPgsR(const FwdPool& P, int m, double cf, const int (&fiR)[R], int lane, double (&X)[R],
+                                 const int* cancel) {
+  bool keepMe[R];
+  unsigned long long km[R];
+#pragma unroll
+  for (int q = 0; q < R; q++) {
+    keepMe[q] = rowAt(q, lane) < m && fiR[q] == -1;
+    km[q] = __ballot(keepMe[q]);
+  }
+  const int k2 = popR(km);
+  int myRow[R];
+#pragma unroll
+  for (int q = 0; q < R; q++) myRow[q] = 0;
+  for (int t = 0, c = 0; t < m; t++)
+    if (bitR(km, t)) { setRi(myRow, c, lane, t); c++; }
+  double xr[R], br[R], lr[R], hr[R];
+  int fr[R];
+#pragma unroll
+  for (int q = 0; q < R; q++) {
+    const bool in = rowAt(q, lane) < k2;
+    xr[q] = 0.0;
+    br[q] = in ? P.b[myRow[q]] : 0.0;
+    lr[q] = in ? P.lo[myRow[q]] : 0.0;
+    hr[q] = in ? P.hi[myRow[q]] : 0.0;
+    fr[q] = -1;
+  }
+  wavePgsR<kLds, true, R>(k2, spc<kLds>(P.A), xr, br, lr, hr, fr, lane, nullptr, cf, cancel, m, myRow);
+#pragma unroll
+  for (int q = 0; q < R; q++) {
+    const double v = gatherR(xr, keepMe[q] ? rankR(km, rowAt(q, lane)) : 0);
+    X[q] = keepMe[q] ? v : 0.0;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // The whole constraint stage of one world (World.cpp:254 runConstraintEngine
 // on the hot path): rows, A = J Minv J^T, b, LCP with the short-circuit,
 // fallbacks, impulses (v1 += Minv J^T x), warm-start cache and snapshot.
@@ -1346,6 +1485,19 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   }
   WSYNC();
   STAMP(3);
+  // the helper wave starts Dantzig on A now (the task board, see helperWave):
+  // A, b, lo, hi and findex are final; the warm start follows
+  const bool tasked = kLds && R == 1 && helperOn;
+  if (tasked) {
+    if (lane < BD_INTS) board(ct)[lane] = 0;
+    helperPost(ct, HS_TASK, lane);
+  }
+  // a settled answer makes every solve still running moot
+  auto stopAll = [&]() {
+    boardSet(ct, BD_STOPD, 1, lane);
+    boardSet(ct, BD_STOPP, 1, lane);
+    boardSet(ct, BD_STOPF, 1, lane);
+  };
   // warm start (BoxedLcpConstraintSolver::mX) or guessSolution
   const bool cached = uni((int)cache[0]) == m;
   if (cached) {
@@ -1356,19 +1508,17 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
     for (int i = lane; i < m; i += WAVE) P.xc[i] = P.X[i];
     WSYNC();
   }
+  if (tasked) boardSet(ct, BD_G, 1, lane);
   if (lane == 0) ct[H_CODOK] = 0;
   STAMP(4);
-  // the helper wave starts the PGS fallback now (see helperWave): its inputs
-  // are final, and it is cancelled if the classification below succeeds
-  const bool tasked = kLds && helperOn;
-  if (tasked) helperPost(ct, HS_TASK, lane);
 #ifdef NIMBLE_STAGE_TIMING
   bool success = devConstruct<kLds, R>(poolIn, m, n, 0.0, false, sp<true>(ct), lane, g_stamp);
+  double* dbgPgs = g_stamp + 54;
 #else
   bool success = devConstruct<kLds, R>(poolIn, m, n, 0.0, false, sp<true>(ct), lane);
+  double* dbgPgs = nullptr;
 #endif
-  if (tasked && success && lane == 0)
-    __hip_atomic_store(helperFlags(ct) + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (tasked && success) stopAll();
   STAMP(5);
   const bool shortCircuit = success;
   double cfm = 0.0;
@@ -1384,25 +1534,9 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
     loR[q] = j < m ? P.lo[j] : 0.0;
     fiR[q] = j < m ? P.fi[j] : -1;
   }
-  auto fullMask = [&](unsigned long long (&mk)[R]) {
-#pragma unroll
-    for (int q = 0; q < R; q++) {
-      const int lo64 = 64 * q;
-      mk[q] = m >= lo64 + 64 ? ~0ull : (m > lo64 ? ((1ull << (m - lo64)) - 1ull) : 0ull);
-    }
-  };
-  auto sameMask = [&](const unsigned long long (&a)[R], const unsigned long long (&b)[R]) {
-    bool eq = true;
-#pragma unroll
-    for (int q = 0; q < R; q++) eq = eq && a[q] == b[q];
-    return eq;
-  };
-  // x_d[row] = x_r[reduced index of rep[row]]
-  auto mapOut = [&](const double (&xr)[R], const unsigned long long (&alive)[R], const int (&rep)[R],
-                    double (&xd)[R]) {
-#pragma unroll
-    for (int q = 0; q < R; q++) xd[q] = gatherR(xr, rankR(alive, rep[q]));
-  };
+  // the board's answer when Dantzig failed: 1 the PGS fallback, 2 the
+  // frictionless PGS (-1: Dantzig's, or no board)
+  int boardSrc = -1;
   if (!success) {
     // Dantzig on the reduced problem (BoxedLcpConstraintSolver.cpp:466-521):
     // LCPUtils::reduce merges near-duplicate columns; when it merges any, the
@@ -1411,15 +1545,18 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
     if (lane == 0) ct[H_CODOK] = 0;
     double scl[R];
     int rep[R];
-    unsigned long long full[R], alive[R];
-    fullMask(full);
+    unsigned long long alive[R];
     waveReduceR<kLds, R>(m, spc<kLds>(P.A), 0.0, bR, loR, hiR, fiR, lane, scl, rep, alive);
     WSYNC();
     double xd[R];
 #pragma unroll
     for (int q = 0; q < R; q++) xd[q] = 0.0;
     bool ok;
-    if (!sameMask(alive, full)) {
+    bool validated = false;
+    if (!allRowsAlive<R>(m, alive)) {
+      // (the helper sees the same merge and solves nothing: wait until it
+      // is out of the pool)
+      if (tasked) helperWait(ct, [](int v) { return v == HS_DONE; });
       if (lane == 0) ct[H_STATUS] = (double)((int)ct[H_STATUS] | ST_DUPLICATE_COLUMNS);
       double br[R], lr[R], hr[R], xr[R];
       int fr[R], act[R];
@@ -1428,7 +1565,55 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
       const int mr = reducedVectorsR<R>(alive, rep, lane, br, lr, hr, fr, act);
       reducedMatrixR<kLds, R>(m, spc<kLds>(P.A), 0.0, alive, act, scl, sp<kLds>(P.M1), false, lane);
       ok = waveDantzigR<kLds, R>(mr, spc<kLds>(P.M1), sp<kLds>(P.M2), sp<kLds>(P.scr), xr, br, lr, hr, fr, lane);
-      mapOut(xr, alive, rep, xd);
+#pragma unroll
+      for (int q = 0; q < R; q++) xd[q] = gatherR(xr, rankR(alive, rep[q]));
+    } else if (tasked) {
+      // the helper runs Dantzig; meanwhile this wave claims the PGS fallback,
+      // then the frictionless PGS, until the reference's order decides:
+      // Dantzig's answer if it succeeds, else the PGS fallback's, else the
+      // frictionless one
+      for (long long it = 0;; it++) {
+        const int d = boardGet(ct, BD_D);
+        if (d == 1) break;
+        const int pst = boardGet(ct, BD_P);
+        if (d >= 2 && pst == 1) { boardSrc = 1; break; }
+        if (d >= 2 && pst == 2 && boardGet(ct, BD_F) == 1) { boardSrc = 2; break; }
+        if (pst == 0 && boardClaim(ct, BD_PCLAIM, 1, lane)) {
+#ifdef NIMBLE_STAGE_TIMING
+          if (lane == 0) g_stamp[97] = 1;
+#endif
+          bool dup;
+          double xp[R];
+          const bool okp = pgsFallbackR<kLds, R>(P, m, md.fallbackCfm, bR, loR, hiR, fiR, sp<kLds>(P.M1), lane, xp,
+                                                 dup, board(ct) + BD_STOPP, dbgPgs);
+#pragma unroll
+          for (int q = 0; q < R; q++)
+            if (rowAt(q, lane) < m) P.xp[rowAt(q, lane)] = xp[q];
+          boardSet(ct, BD_PDUP, dup ? 1 : 0, lane);
+          if (okp) boardSet(ct, BD_STOPF, 1, lane);
+          boardSet(ct, BD_P, okp ? 1 : 2, lane);
+          continue;
+        }
+        if (pst != 1 && boardGet(ct, BD_F) == 0 && boardClaim(ct, BD_FCLAIM, 1, lane)) {
+#ifdef NIMBLE_STAGE_TIMING
+          if (lane == 0) g_stamp[98] = 1;
+#endif
+          double xf[R];
+          frictionlessPgsR<kLds, R>(P, m, md.fallbackCfm, fiR, lane, xf, board(ct) + BD_STOPF);
+#pragma unroll
+          for (int q = 0; q < R; q++)
+            if (rowAt(q, lane) < m) P.xf[rowAt(q, lane)] = xf[q];
+          boardSet(ct, BD_F, 1, lane);
+          continue;
+        }
+        if (it > (1ll << 24)) __builtin_trap();
+        __builtin_amdgcn_s_sleep(1);
+      }
+      // Dantzig's answer (checked valid by the helper)
+      ok = boardSrc < 0;
+      validated = true;
+#pragma unroll
+      for (int q = 0; q < R; q++) xd[q] = ok && rowAt(q, lane) < m ? P.xh[rowAt(q, lane)] : 0.0;
     } else {
 #ifdef NIMBLE_STAGE_TIMING
       ok = waveDantzigR<kLds, R>(m, spc<kLds>(P.A), sp<kLds>(P.M2), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane,
@@ -1442,7 +1627,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
       for (int q = 0; q < R; q++)
         if (rowAt(q, lane) < m) P.X[rowAt(q, lane)] = xd[q];
       WSYNC();
-      ok = waveLcpValidR<kLds, R>(m, spc<kLds>(P.A), 0.0, xd, bR, hiR, loR, fiR, false, lane);
+      if (!validated) ok = waveLcpValidR<kLds, R>(m, spc<kLds>(P.A), 0.0, xd, bR, hiR, loR, fiR, false, lane);
     }
     success = ok;
   }
@@ -1452,108 +1637,48 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
     bool ign = false;
     double cf = 0.0;
     double X[R];
-    bool nan = false;
-#pragma unroll
-    for (int q = 0; q < R; q++) {
-      X[q] = rowAt(q, lane) < m ? P.X[rowAt(q, lane)] : 0.0;
-      nan = nan || (rowAt(q, lane) < m && isnan(X[q]));
-    }
-    if (__ballot(nan)) {
-      ok = false;
-#pragma unroll
-      for (int q = 0; q < R; q++) X[q] = 0.0;
-    }
-    if (!ok) {
+    if (boardSrc > 0) {
+      // a fallback the board ran (validated by the wave that ran it)
       cf = md.fallbackCfm;
-      if (lane == 0) ct[H_CODOK] = 0;
-      double xd[R];
-      // PGS on the reduced A + cfm I (BoxedLcpConstraintSolver.cpp:550-597);
-      // the helper wave's speculative PGS is the unreduced solve, used when
-      // reduce merges nothing
-      double scl[R];
-      int rep[R];
-      unsigned long long full[R], alive[R];
-      fullMask(full);
-      waveReduceR<kLds, R>(m, spc<kLds>(P.A), cf, bR, loR, hiR, fiR, lane, scl, rep, alive);
-      WSYNC();
-      if (!sameMask(alive, full)) {
-        if (lane == 0) ct[H_STATUS] = (double)((int)ct[H_STATUS] | ST_DUPLICATE_COLUMNS);
-        double br[R], lr[R], hr[R], xc[R], xr[R];
-        int fr[R], act[R];
-#pragma unroll
-        for (int q = 0; q < R; q++) {
-          br[q] = bR[q]; lr[q] = loR[q]; hr[q] = hiR[q]; fr[q] = fiR[q];
-          xc[q] = rowAt(q, lane) < m ? P.xc[rowAt(q, lane)] : 0.0;
-        }
-        const int mr = reducedVectorsR<R>(alive, rep, lane, br, lr, hr, fr, act);
-        reducedMatrixR<kLds, R>(m, spc<kLds>(P.A), cf, alive, act, scl, sp<kLds>(P.M1), true, lane);
-#pragma unroll
-        for (int q = 0; q < R; q++) {
-          xr[q] = gatherR(xc, rowAt(q, lane) < mr ? act[q] : 0);
-          if (rowAt(q, lane) >= mr) xr[q] = 0.0;
-        }
-        ok = wavePgsR<kLds, false, R>(mr, spc<kLds>(P.M1), xr, br, lr, hr, fr, lane, nullptr, 0.0);
-        mapOut(xr, alive, rep, xd);
-      } else if (R == 1 && tasked) {
-        helperWait(ct, [](int st) { return st == HS_MID || st == HS_DONE; });
-        xd[0] = lane < m ? P.xh[lane] : 0.0;
-        ok = uni(helperFlags(ct)[2]) != 0;
-      } else {
-#pragma unroll
-        for (int q = 0; q < R; q++) xd[q] = rowAt(q, lane) < m ? P.xc[rowAt(q, lane)] : 0.0;
-#ifdef NIMBLE_STAGE_TIMING
-        ok = wavePgsR<kLds, false, R>(m, spc<kLds>(P.A), xd, bR, loR, hiR, fiR, lane, g_stamp + 54, cf);
-#else
-        ok = wavePgsR<kLds, false, R>(m, spc<kLds>(P.A), xd, bR, loR, hiR, fiR, lane, nullptr, cf);
-#endif
-      }
-      if (ok) {
-#pragma unroll
-        for (int q = 0; q < R; q++) X[q] = xd[q];
-        ok = waveLcpValidR<kLds, R>(m, spc<kLds>(P.A), cf, X, bR, hiR, loR, fiR, false, lane);
-      }
-    }
-    if (!ok) {
-      // LCPUtils::removeFriction + PGS on the normal rows only (the principal
-      // submatrix of A + cfm I over them, read in place)
-      ign = true;
-      bool keepMe[R];
-      unsigned long long km[R];
+      ign = boardSrc == 2;
+      if (boardGet(ct, BD_PDUP) && lane == 0) ct[H_STATUS] = (double)((int)ct[H_STATUS] | ST_DUPLICATE_COLUMNS);
 #pragma unroll
       for (int q = 0; q < R; q++) {
-        keepMe[q] = rowAt(q, lane) < m && fiR[q] == -1;
-        km[q] = __ballot(keepMe[q]);
+        const int j = rowAt(q, lane);
+        X[q] = j < m ? (boardSrc == 1 ? P.xp[j] : P.xf[j]) : 0.0;
       }
-      const int k2 = popR(km);
-      if (R == 1 && tasked) {
-        helperWait(ct, [](int st) { return st == HS_DONE; });
-      } else {
-        int myRow[R];
-#pragma unroll
-        for (int q = 0; q < R; q++) myRow[q] = 0;
-        for (int t = 0, c = 0; t < m; t++)
-          if (bitR(km, t)) { setRi(myRow, c, lane, t); c++; }
-        double xr[R], br[R], lr[R], hr[R];
-        int fr[R];
-#pragma unroll
-        for (int q = 0; q < R; q++) {
-          const bool in = rowAt(q, lane) < k2;
-          xr[q] = 0.0;
-          br[q] = in ? P.b[myRow[q]] : 0.0;
-          lr[q] = in ? P.lo[myRow[q]] : 0.0;
-          hr[q] = in ? P.hi[myRow[q]] : 0.0;
-          fr[q] = -1;
-        }
-        wavePgsR<kLds, true, R>(k2, spc<kLds>(P.A), xr, br, lr, hr, fr, lane, nullptr, cf, nullptr, m, myRow);
-#pragma unroll
-        for (int q = 0; q < R; q++)
-          if (rowAt(q, lane) < k2) P.xh2[rowAt(q, lane)] = xr[q];
-        WSYNC();
-      }
+    } else {
+      bool nan = false;
 #pragma unroll
       for (int q = 0; q < R; q++) {
-        X[q] = 0.0;
-        if (keepMe[q]) X[q] = P.xh2[rankR(km, rowAt(q, lane))];
+        X[q] = rowAt(q, lane) < m ? P.X[rowAt(q, lane)] : 0.0;
+        nan = nan || (rowAt(q, lane) < m && isnan(X[q]));
+      }
+      if (__ballot(nan)) {
+        ok = false;
+#pragma unroll
+        for (int q = 0; q < R; q++) X[q] = 0.0;
+      }
+      if (!ok) {
+        // (reached with a board only when the classification's answer holds
+        // a NaN: the helper has been stopped; wait until it is out of the pool)
+        if (tasked) {
+          stopAll();
+          helperWait(ct, [](int v) { return v == HS_DONE; });
+        }
+        cf = md.fallbackCfm;
+        if (lane == 0) ct[H_CODOK] = 0;
+        bool dup;
+        double xd[R];
+        ok = pgsFallbackR<kLds, R>(P, m, cf, bR, loR, hiR, fiR, sp<kLds>(P.M1), lane, xd, dup, nullptr, dbgPgs);
+        if (dup && lane == 0) ct[H_STATUS] = (double)((int)ct[H_STATUS] | ST_DUPLICATE_COLUMNS);
+        if (ok)
+#pragma unroll
+          for (int q = 0; q < R; q++) X[q] = xd[q];
+      }
+      if (!ok) {
+        ign = true;
+        frictionlessPgsR<kLds, R>(P, m, cf, fiR, lane, X, nullptr);
       }
     }
     bool nan2 = false;
@@ -1567,6 +1692,12 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
       if (rowAt(q, lane) < m) P.X[rowAt(q, lane)] = X[q];
     if (lane == 0) { ct[H_CFM] = cf; ct[H_IGN] = ign ? 1 : 0; }
     WSYNC();
+  }
+  // the helper out of the pool before construct 2 and the backward
+  // precompute overwrite it (M1, M2, A)
+  if (tasked) {
+    stopAll();
+    helperWait(ct, [](int v) { return v == HS_DONE; });
   }
   cfm = unid(ct[H_CFM]);
   ignoredFriction = uni(ct[H_IGN] != 0 ? 1 : 0) != 0;
@@ -1633,9 +1764,13 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
 }
 
 // One world's turn of the helper wave (wave 1 of the forward workgroup):
-// wait for wave 0's TASK or SKIP, run the PGS fallback on the LDS pool for a
-// task, answer DONE, then wait until wave 0 has taken the answer.
-__device__ void helperWave(const ModelDev& md, double* s, const Layout& L, int lane) {
+// wait for wave 0's TASK or SKIP; for a task, run Dantzig on A (unless
+// LCPUtils::reduce merges columns: wave 0 then solves the reduced problem
+// itself), then claim whichever fallbacks are still open (the task board,
+// see above); answer DONE, then wait until wave 0 has taken the answer.
+// `g_stamp`: the stage-timing build's stamps (else null).
+__device__ void helperWave(const ModelDev& md, double* s, const Layout& L, int lane, double* g_stamp) {
+  (void)g_stamp;
   s = lds<true>(s);
   double* ct = s + L.ct;
   const int st = helperWait(ct, [](int v) { return v == HS_TASK || v == HS_SKIP; });
@@ -1643,41 +1778,89 @@ __device__ void helperWave(const ModelDev& md, double* s, const Layout& L, int l
     const int m = uni((int)ct[H_M]);
     FwdPool P;
     carveFwd(s + L.pool, m, md.n, P);
-    double x = lane < m ? P.xc[lane] : 0.0;
-    const double bR = lane < m ? P.b[lane] : 0.0, hiR = lane < m ? P.hi[lane] : 0.0;
-    const double loR = lane < m ? P.lo[lane] : 0.0;
-    const int fiR = lane < m ? P.fi[lane] : -1;
-    const double cf = md.fallbackCfm;
-    const bool ok = wavePgs<true>(m, spc<true>(P.A), x, bR, loR, hiR, fiR, lane, nullptr, cf, helperFlags(ct) + 1);
-    if (lane < m) P.xh[lane] = x;
-    if (lane == 0) helperFlags(ct)[2] = ok ? 1 : 0;
-    helperPost(ct, HS_MID, lane);
-    // then LCPUtils::removeFriction's PGS on the normal rows, unless wave 0
-    // has what it needs already (it cancels)
-    if (!uni(__hip_atomic_load(helperFlags(ct) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) {
-      const unsigned long long km = __ballot(lane < m && fiR == -1);
-      const int k2 = __popcll(km);
-      int myRow = 0;
-      for (int t = 0, c = 0; t < m; t++)
-        if ((km >> t) & 1ull) { if (lane == c) myRow = t; c++; }
-      double xr = 0.0;
-      wavePgs<true, true>(k2, spc<true>(P.A), xr, lane < k2 ? P.b[myRow] : 0.0, lane < k2 ? P.lo[myRow] : 0.0,
-                    lane < k2 ? P.hi[myRow] : 0.0, -1, lane, nullptr, cf, helperFlags(ct) + 1, m, myRow);
-      if (lane < k2) P.xh2[lane] = xr;
+    const double bR[1] = {lane < m ? P.b[lane] : 0.0}, hiR[1] = {lane < m ? P.hi[lane] : 0.0};
+    const double loR[1] = {lane < m ? P.lo[lane] : 0.0};
+    const int fiR[1] = {lane < m ? P.fi[lane] : -1};
+    double scl[1];
+    int rep[1];
+    unsigned long long alive[1];
+    // (whether reduce merges anything: the first merge settles it)
+    waveReduceR<true, 1>(m, spc<true>(P.A), 0.0, bR, loR, hiR, fiR, lane, scl, rep, alive, 1);
+    if (!allRowsAlive<1>(m, alive)) {
+      boardSet(ct, BD_D, 3, lane);
+    } else {
+#ifdef NIMBLE_STAGE_TIMING
+      if (lane == 0 && g_stamp) g_stamp[94] = (double)__builtin_amdgcn_s_memtime();
+      double* dbgD = g_stamp ? g_stamp + 99 : nullptr;
+#else
+      double* dbgD = nullptr;
+#endif
+      double xd[1] = {0.0};
+      bool ok = waveDantzigR<true, 1>(m, spc<true>(P.A), sp<true>(P.M2), sp<true>(P.xh2), xd, bR, loR, hiR, fiR, lane,
+                                      dbgD, board(ct) + BD_STOPD);
+      ok = ok && !__ballot(lane < m && isnan(xd[0]));
+      if (ok) ok = waveLcpValidR<true, 1>(m, spc<true>(P.A), 0.0, xd, bR, hiR, loR, fiR, false, lane);
+      if (lane < m) P.xh[lane] = xd[0];
+      if (ok) {
+        boardSet(ct, BD_STOPP, 1, lane);
+        boardSet(ct, BD_STOPF, 1, lane);
+      }
+      boardSet(ct, BD_D, ok ? 1 : 2, lane);
+#ifdef NIMBLE_STAGE_TIMING
+      if (lane == 0 && g_stamp) { g_stamp[95] = (double)__builtin_amdgcn_s_memtime(); g_stamp[96] = ok ? 1 : 2; }
+#endif
+      // the fallbacks still open: the PGS fallback once the warm start is
+      // final, the frictionless PGS unless the PGS fallback has succeeded
+      const double cf = md.fallbackCfm;
+      for (long long it = 0; !ok; it++) {
+        const bool pOpen = boardGet(ct, BD_PCLAIM) == 0 && !boardGet(ct, BD_STOPP);
+        const bool fOpen = boardGet(ct, BD_FCLAIM) == 0 && !boardGet(ct, BD_STOPF) && boardGet(ct, BD_P) != 1;
+        if (pOpen && boardGet(ct, BD_G) == 1) {
+          if (boardClaim(ct, BD_PCLAIM, 2, lane)) {
+#ifdef NIMBLE_STAGE_TIMING
+            if (lane == 0 && g_stamp) g_stamp[97] = 2;
+#endif
+            bool dup;
+            double xp[1];
+            const bool okp = pgsFallbackR<true, 1>(P, m, cf, bR, loR, hiR, fiR, sp<true>(P.M2), lane, xp, dup,
+                                                   board(ct) + BD_STOPP, nullptr);
+            if (lane < m) P.xp[lane] = xp[0];
+            boardSet(ct, BD_PDUP, dup ? 1 : 0, lane);
+            if (okp) boardSet(ct, BD_STOPF, 1, lane);
+            boardSet(ct, BD_P, okp ? 1 : 2, lane);
+          }
+          continue;
+        }
+        if (fOpen) {
+          if (boardClaim(ct, BD_FCLAIM, 2, lane)) {
+#ifdef NIMBLE_STAGE_TIMING
+            if (lane == 0 && g_stamp) g_stamp[98] = 2;
+#endif
+            double xf[1];
+            frictionlessPgsR<true, 1>(P, m, cf, fiR, lane, xf, board(ct) + BD_STOPF);
+            if (lane < m) P.xf[lane] = xf[0];
+            boardSet(ct, BD_F, 1, lane);
+          }
+          continue;
+        }
+        if (!pOpen) break;
+        // only the PGS fallback is open, waiting for the warm start
+        if (it > (1ll << 24)) __builtin_trap();
+        __builtin_amdgcn_s_sleep(1);
+      }
     }
   }
   helperPost(ct, HS_DONE, lane);
   helperWait(ct, [](int v) { return v != HS_DONE; });
 }
 
-// wave 0's end of a world's protocol: post SKIP if no task went out, cancel
-// a task still running, collect DONE and reset to IDLE
+// wave 0's end of a world's protocol: post SKIP if no task went out, collect
+// DONE (a task has been stopped and collected in contactLcp already) and
+// reset to IDLE
 __device__ __forceinline__ void helperRetire(double* s, const Layout& L, int lane) {
   double* ct = lds<true>(s) + L.ct;
   if (helperState(ct) == HS_IDLE) helperPost(ct, HS_SKIP, lane);
-  if (lane == 0) __hip_atomic_store(helperFlags(ct) + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   helperWait(ct, [](int v) { return v == HS_DONE; });
-  if (lane == 0) __hip_atomic_store(helperFlags(ct) + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   helperPost(ct, HS_IDLE, lane);
 }
 

@@ -317,7 +317,7 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
   if (helperOn) {
     if (threadIdx.x == 0) {
       int* hf = reinterpret_cast<int*>(s + L.ct + H_HELPER);
-      hf[0] = HS_IDLE; hf[1] = 0; hf[2] = 0;
+      hf[0] = HS_IDLE; hf[1] = 0; hf[2] = 0; hf[3] = 0;
       *collideFlag(s + L.ct) = CS_IDLE;
     }
     __syncthreads();  // the one barrier both waves take: flags initialised
@@ -339,7 +339,12 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
         collideWait(ct, CS_GO);
         collideWorld(md, lds<true>(s), L, lane, snapshot + (size_t)env * snapDoubles + snEdge(n));
         collidePost(ct, CS_DONE, lane);
-        helperWave(md, s, md.lay[0], lane);  // not inlined: the model's copy of L, not the argument's
+#ifdef NIMBLE_STAGE_TIMING
+        double* hstamp = snapshot + (size_t)env * snapDoubles + snapWorkspaceOffset(n) + 1000;
+#else
+        double* hstamp = nullptr;
+#endif
+        helperWave(md, s, md.lay[0], lane, hstamp);  // not inlined: the model's copy of L, not the argument's
       }
       return;
     }

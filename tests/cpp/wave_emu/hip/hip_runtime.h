@@ -200,6 +200,9 @@ void launch(K kernel, dim3 grid, dim3 block, size_t lds, A... args) {
 // loop together, as the readfirstlane makes it do on the GPU
 #define __hip_atomic_load(p, o, s) wave_emu::atomicLoadUniform(p)
 #define __hip_atomic_store(p, v, o, s) __atomic_store_n((p), (v), __ATOMIC_SEQ_CST)
+// (lane 0 only, in the kernels; the winner is broadcast with a readlane)
+#define __hip_atomic_compare_exchange_strong(p, e, d, o1, o2, s) \
+  __atomic_compare_exchange_n((p), (e), (d), false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST)
 #define __HIP_MEMORY_SCOPE_WORKGROUP 0
 
 inline int __double2loint(double d) { return (int)(uint32_t)wave_emu::asU(d); }

@@ -11,7 +11,9 @@ wave, checked for lanes out of step), with AddressSanitizer.
 * a whole forward + backward step through the C-ABI (capi.cpp unchanged,
   kernels launched by the emulation), with the default split and with every
   contact world forced through the wide kernels (NIMBLE_AMD_DEFER_ROWS=0),
-  matches the oracle -- and any out-of-bounds access aborts the run.
+  and Atlas worlds through every answer of the LCP cascade (the two waves'
+  task board), matches the oracle -- and any out-of-bounds access aborts the
+  run.
 
 No GPU needed; the emulation runs a few worlds in tens of seconds.
 """
@@ -91,6 +93,33 @@ def test_box_step_emulated(defer):
     assert np.abs(nxt - ref).max() <= 1e-12
     assert np.abs(gs - rgs).max() <= 1e-9 * np.abs(rgs).max()
     assert np.abs(gf - rgf).max() <= 1e-9 * np.abs(rgf).max()
+
+
+def test_atlas_lcp_paths_emulated():
+    """Atlas bench-sampler worlds through each answer of the LCP cascade --
+    the short-circuit (14), Dantzig (0), the PGS fallback (10, 35) and the
+    frictionless PGS (1) -- with the forward's two waves sharing the cascade
+    on the task board (contact.cuh: Dantzig on the helper, the fallbacks on
+    whichever wave is free): the same answers as the oracle's sequential
+    cascade, flags included."""
+    world = models.atlas_world(True)
+    st, f = models.random_states(world, 1024, seed=1000, q_scale=0.02, v_scale=0.05)
+    idx = [0, 1, 10, 14, 35]
+    st, f = st[idx], f[idx]
+    ow = O.OracleWorld(world)
+    ref = ow.forward(st, f)
+    g = np.random.default_rng(3).standard_normal(st.shape)
+    rgs, rgf = ow.backward(g)
+    nxt, gs, gf, head = wave_emu.step(world, st, f, g)
+    paths = set()
+    for i in range(len(idx)):
+        fl = O.lcp_flags(ow, i)
+        assert (head[i, 6], head[i, 7], head[i, 4]) == (fl[0], fl[1], fl[2]), idx[i]
+        paths.add("C" if fl[0] else "F" if fl[1] else "P" if fl[2] > 0 else "D")
+        assert np.abs(nxt[i] - ref[i]).max() <= 1e-12, idx[i]
+        assert np.abs(gs[i] - rgs[i]).max() <= 1e-9 * np.abs(rgs[i]).max() * 10, idx[i]
+        assert np.abs(gf[i] - rgf[i]).max() <= 1e-9 * np.abs(rgf[i]).max(), idx[i]
+    assert paths == {"C", "D", "P", "F"}
 
 
 def test_mesh_atlas_wide_step_emulated():

@@ -211,6 +211,9 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
   }
   // Candidate pairs: DARTCollisionDetector::collide (DARTCollisionDetector.cpp:127)
   // object order i<j filtered by BodyNodeCollisionFilter (CollisionFilter.cpp:105)
+  // NIMBLE_AMD_HELPER_PRIO (measurements): the helper's priority on the task board
+  m.helperPrio = 0;
+  if (const char* e = getenv("NIMBLE_AMD_HELPER_PRIO")) m.helperPrio = atoi(e) & 3;
   m.numPairs = 0;
   m.pairChunk = 0;
   for (int i = 0; i < m.ns; i++)

@@ -53,6 +53,23 @@ __device__ inline double* carveCod(double* w, double* A, int m, int n, int ld, C
 // the layout of the LDS factorisation, with perm / vd / vn.  Cost per step:
 // ~4R dependent-free VALU ops per lane plus two LDS round trips, instead of
 // 2(m-k) LDS round trips.
+#ifdef NIMBLE_COD_PROFILE
+// per-phase clocks of codQrRegs, 8 per workgroup (tools/micro/cod_bench.hip
+// only): 0 pivot search + slot swap, 1 pivot-column broadcast + reflector
+// head, 2 reflector application + next partial norms, 3 write-back
+__device__ double* g_codProf;
+#define COD_PROF_BEGIN long long codT_ = (long long)__builtin_amdgcn_s_memtime()
+#define COD_PROF(k)                                                                    \
+  do {                                                                                 \
+    const long long t_ = (long long)__builtin_amdgcn_s_memtime();                     \
+    if (lane == 0) g_codProf[blockIdx.x * 8 + (k)] += (double)(t_ - codT_);            \
+    codT_ = t_;                                                                        \
+  } while (0)
+#else
+#define COD_PROF_BEGIN do { } while (0)
+#define COD_PROF(k) do { } while (0)
+#endif
+
 template <bool kLds, int R>
 __device__ void codQrRegs(typename Space<kLds>::dptr A, Cod& c, typename Space<kLds>::dptr vb, int lane) {
   const int m = c.m, n = c.n, ld = c.ld;
@@ -69,6 +86,7 @@ __device__ void codQrRegs(typename Space<kLds>::dptr A, Cod& c, typename Space<k
   for (int i = 0; i < R; i++) norm += a[i] * a[i];
   int pos = lane;
   WSYNC();  // every column is in registers: A may now be overwritten
+  COD_PROF_BEGIN;
   for (int k = 0; k < c.kmax; k++) {
     const bool cand = col && pos >= k;
     const double best = -waveMin(cand ? -norm : 1.0);
@@ -85,6 +103,7 @@ __device__ void codQrRegs(typename Space<kLds>::dptr A, Cod& c, typename Space<k
       if (lane == q) pos = ppos;
       if (lane == pl) pos = k;
     }
+    COD_PROF(0);
     if (lane == pl) {
 #pragma unroll
       for (int i = 0; i < R; i++) vb[i] = a[i];
@@ -115,6 +134,7 @@ __device__ void codQrRegs(typename Space<kLds>::dptr A, Cod& c, typename Space<k
     double v[R];
 #pragma unroll
     for (int i = 0; i < R; i++) v[i] = vb[i];
+    COD_PROF(1);
     double vn0 = 0.0, vn1 = 0.0, sc0 = 0.0, sc1 = 0.0;
 #pragma unroll
     for (int i = 0; i < R; i += 2) {
@@ -133,6 +153,7 @@ __device__ void codQrRegs(typename Space<kLds>::dptr A, Cod& c, typename Space<k
       nrm += t * t;
     }
     norm = nrm;
+    COD_PROF(2);
     // slot k is final: R part from the pivot lane, reflector tail below
     if (lane == pl) {
 #pragma unroll
@@ -142,6 +163,7 @@ __device__ void codQrRegs(typename Space<kLds>::dptr A, Cod& c, typename Space<k
     if (lane > k && lane < m) A[lane * ld + k] = vb[lane];
     if (lane == 0) { c.vd[k] = vk; c.vn[k] = vnorm; }
     WSYNC();
+    COD_PROF(3);
   }
   if (col) {
     if (pos >= c.kmax) {

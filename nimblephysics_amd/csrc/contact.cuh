@@ -336,8 +336,11 @@ __device__ inline void carveFwd(double* base, int m, int n, FwdPool& P) {
   P.xc = p; p += m;
   P.xh = p; p += m;   // the helper wave's Dantzig solution
   P.xh2 = p; p += m;  // ... and its scratch
-  P.xp = p; p += m;   // the PGS fallback's solution (either wave)
-  P.xf = p; p += m;   // the frictionless PGS's solution (either wave)
+  // (aliases, see the task board: the PGS fallback's solution overwrites
+  // its warm start once read, the frictionless PGS's solution the
+  // penetration-correction terms, dead after the row setup)
+  P.xp = P.xc;
+  P.xf = P.pen;
   P.dvec = p; p += 3 * m;
   int* ip = reinterpret_cast<int*>(p);
   P.fi = ip; ip += m;
@@ -406,7 +409,9 @@ __device__ __forceinline__ void gramMfma(const double* Y, double* A, int n, int 
 #define H_HELPER 13 // 2 doubles = 4 ints: helper state (HS_*), unused x3
 #define H_COLLIDE 15  // 2 ints: collision-detection hand-off between the waves (CS_*)
 #define H_PAIRCNT 16   // 16 per-pair counts of the current chunk
-#define H_BOARD 32     // 8 doubles = 16 ints: the LCP task board (BD_*)
+// the LCP task board (BD_*, 16 ints): the pair counts are collision-time
+// scratch, dead once the contacts are final, when the board is first used
+#define H_BOARD H_PAIRCNT
 
 // ---------------------------------------------------------------------------
 // Helper wave.  The forward kernel runs two waves per world: wave 0 does the
@@ -1775,6 +1780,12 @@ __device__ void helperWave(const ModelDev& md, double* s, const Layout& L, int l
   double* ct = s + L.ct;
   const int st = helperWait(ct, [](int v) { return v == HS_TASK || v == HS_SKIP; });
   if (st == HS_TASK) {
+    // the cascade's Dantzig is on the world's critical path: the helper
+    // competes for issue with the other world's step wave on its SIMD
+    const int prio = md.helperPrio;
+    if (prio == 1) __builtin_amdgcn_s_setprio(1);
+    else if (prio == 2) __builtin_amdgcn_s_setprio(2);
+    else if (prio == 3) __builtin_amdgcn_s_setprio(3);
     const int m = uni((int)ct[H_M]);
     FwdPool P;
     carveFwd(s + L.pool, m, md.n, P);
@@ -1850,6 +1861,7 @@ __device__ void helperWave(const ModelDev& md, double* s, const Layout& L, int l
       }
     }
   }
+  __builtin_amdgcn_s_setprio(0);
   helperPost(ct, HS_DONE, lane);
   helperWait(ct, [](int v) { return v != HS_DONE; });
 }

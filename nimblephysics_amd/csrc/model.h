@@ -65,6 +65,9 @@ struct ModelDev {
   int meshFirst[NS_MAX], meshCount[NS_MAX];
   double meshRadius[NS_MAX];
   int hasMesh;
+  // issue priority (s_setprio) of the forward's helper wave while it runs
+  // its share of the LCP cascade (the collision detection runs at 0)
+  int helperPrio;
   // kept-contact capacity of the contact stage (<= NIMBLE_MAX_CONTACTS)
   int maxContacts;
   // candidate pairs (i < j) after BodyNodeCollisionFilter, in detector order

@@ -18,7 +18,7 @@
 
 // contact-stage LDS region (Layout::ct): header, then the kept contacts
 // (the model's contact capacity, ModelDev::maxContacts <= NIMBLE_MAX_CONTACTS)
-#define CT_CONTACTS 40
+#define CT_CONTACTS 32
 #define CT_MAX_DROPPED 8
 #define CT_PAIR_CHUNK 16
 #define CT_PAIR_CHUNK_HOST CT_PAIR_CHUNK
@@ -76,7 +76,7 @@ __host__ __device__ inline int snapWorkspaceOffset(int n) { return snAlign8(snEd
 // LCP workspace pools for m rows and n dofs
 #define NV_COLS 16
 // (+24: codFactor's register path stages a 24-double column in the scratch)
-__host__ __device__ inline int fwdPoolDoubles(int m, int n) { return n * m + 3 * m * m + 35 * m + 2 * n + 72; }
+__host__ __device__ inline int fwdPoolDoubles(int m, int n) { return n * m + 3 * m * m + 33 * m + 2 * n + 72; }
 __host__ __device__ inline int bwdPoolDoubles(int m, int n) { return n * m + 24 * m + NV_COLS * n + 64; }
 
 #define fwdPoolDoublesHost fwdPoolDoubles

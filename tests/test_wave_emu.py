@@ -152,3 +152,13 @@ def test_snapshot_layout_matches_pool_sizes():
         L = _native.snapshot_layout(n)
         want = [L[k] for k in ("contacts", "rows", "fc", "vf", "yf", "ac", "acube", "pt", "q", "edge", "workspace")]
         assert got == want, (n, got, want)
+
+
+def test_bench_atlas_lds_fits_four_worlds_per_cu():
+    """The bench's occupancy: the forward and backward workgroups of the
+    Atlas bench world must each fit a quarter of a CU's 160 KB LDS, so that
+    the 1024 worlds of the bench are all resident at once (4 per CU on 256
+    CUs); one double over the budget leaves 256 worlds for a second round."""
+    fwd, bwd = wave_emu.lds_bytes(models.atlas_world(True))
+    assert fwd <= 40 * 1024, fwd
+    assert bwd <= 40 * 1024, bwd

@@ -63,9 +63,9 @@ def step(world, st, f, g, env=None, timeout=1800):
         with open(os.environ["WAVE_EMU_DUMP"], "w") as fh:
             fh.write("\n".join(lines))
     r = subprocess.run([exe], input="\n".join(lines), capture_output=True, text=True, timeout=timeout, env=e)
+    with open(os.path.join("/tmp", f"nimble_wave_emu_{os.getuid()}.stderr"), "w") as fh:
+        fh.write(r.stderr)
     if r.returncode != 0:
-        with open(os.path.join("/tmp", f"nimble_wave_emu_{os.getuid()}.stderr"), "w") as fh:
-            fh.write(r.stderr)
         raise RuntimeError(f"emulated step failed ({r.returncode}):\n{r.stderr[-6000:]}")
     out = {}
     for ln in r.stdout.splitlines():
@@ -74,3 +74,17 @@ def step(world, st, f, g, env=None, timeout=1800):
     B, n = st.shape[0], world.getNumDofs()
     return (out["next"].reshape(B, 2 * n), out["gs"].reshape(B, 2 * n), out["gf"].reshape(B, n),
             out["head"].reshape(B, 16))
+
+
+def lds_bytes(world):
+    """(forward, backward) LDS bytes per workgroup the C-ABI sizes for
+    `world` (NIMBLE_AMD_VERBOSE report of nimble_world_create, through the
+    emulated step of one world at rest)."""
+    import re
+    n = world.getNumDofs()
+    st = np.zeros((1, 2 * n))
+    f = np.zeros((1, n))
+    step(world, st, f, np.zeros_like(st), {"NIMBLE_AMD_VERBOSE": "1"})
+    txt = open(os.path.join("/tmp", f"nimble_wave_emu_{os.getuid()}.stderr")).read()
+    m = re.search(r"LDS forward (\d+) B .* backward (\d+) B", txt)
+    return int(m.group(1)), int(m.group(2))

@@ -1,7 +1,8 @@
 // COD micro-benchmark (tools/micro/cod_bench.py): one n x n problem per
 // 64-lane workgroup, factorised and solved in LDS by codFactor /
 // codSolveWave; per problem: shader clocks, rank and the min-norm solution.
-// Built twice: register QR (default) and -DNIMBLE_COD_LDS_ONLY.
+// Built three times: register QR (default), -DNIMBLE_COD_LDS_ONLY, and the
+// register QR with -DNIMBLE_COD_PROFILE (per-phase clocks in o[3..6]).
 #include "../../nimblephysics_amd/csrc/lcp_wave.cuh"
 
 extern "C" __global__ void __launch_bounds__(64)
@@ -32,11 +33,28 @@ cod_bench_kernel(int nmax, const int* nArr, const double* Ag, const double* bg, 
     o[2] = *c.rank;
   }
   if (lane < n) o[8 + lane] = x;
+#ifdef NIMBLE_COD_PROFILE
+  // per-phase clocks of the register QR (cod_wave.cuh codQrRegs)
+  if (lane < 4) o[3 + lane] = g_codProf[blockIdx.x * 8 + lane];
+#endif
 }
 
 extern "C" int cod_bench_launch(int P, int nmax, const int* nArr, const double* A, const double* b, double* out, int rec,
                                 void* stream) {
   const size_t lds = (size_t)(nmax * nmax + 12 * nmax + 64) * sizeof(double);
+#ifdef NIMBLE_COD_PROFILE
+  static double* prof = nullptr;
+  static int profN = 0;
+  if (profN < P) {
+    if (prof) (void)hipFree(prof);
+    if (hipMalloc(&prof, (size_t)P * 8 * sizeof(double)) != hipSuccess) return 1;
+    profN = P;
+  }
+  if (hipMemsetAsync(prof, 0, (size_t)P * 8 * sizeof(double), (hipStream_t)stream) != hipSuccess ||
+      hipMemcpyToSymbolAsync(HIP_SYMBOL(g_codProf), &prof, sizeof(prof), 0, hipMemcpyHostToDevice,
+                             (hipStream_t)stream) != hipSuccess)
+    return 1;
+#endif
   hipLaunchKernelGGL(cod_bench_kernel, dim3(P), dim3(64), lds, (hipStream_t)stream, nmax, nArr, A, b, out, rec);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }

@@ -3,6 +3,7 @@ construct-like matrices (Q = Y^T Y of rank r <= n, and full-rank ones).
 
   python tools/micro/cod_bench.py build   # here: dbg/libcod_{reg,lds}.so
   python tools/micro/cod_bench.py run     # GPU box: clocks, rank, solution
+  python tools/micro/cod_bench.py mfma    # GPU box: QR phase split + MFMA rank-4 update
 """
 import ctypes as C
 import os
@@ -14,6 +15,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 SRC = os.path.join(ROOT, "tools", "micro", "cod_bench.hip")
 LIBS = {"reg": os.path.join(ROOT, "dbg", "libcod_reg.so"), "lds": os.path.join(ROOT, "dbg", "libcod_lds.so")}
+PROF_LIB = os.path.join(ROOT, "dbg", "libcod_prof.so")
+MFMA_SRC = os.path.join(ROOT, "tools", "micro", "cod_mfma.hip")
+MFMA_EXE = os.path.join(ROOT, "dbg", "cod_mfma")
 NMAX, REC = 24, 64
 
 
@@ -23,6 +27,9 @@ def build():
         extra = ["-DNIMBLE_COD_LDS_ONLY"] if k == "lds" else []
         subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared"] + extra +
                               ["-o", lib, SRC])
+    subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+                           "-DNIMBLE_COD_PROFILE", "-o", PROF_LIB, SRC])
+    subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-o", MFMA_EXE, MFMA_SRC])
 
 
 def problems(P=2048, seed=0):
@@ -89,5 +96,32 @@ def run():
                   f" | solve reg {res['reg'][sel, 1].mean():7.0f} lds {res['lds'][sel, 1].mean():7.0f}")
 
 
+def mfma():
+    """The register QR's per-step phase split (24 x 24 problems, solo and at
+    1024 waves) and the rank-4 trailing-update micro-benchmark; JSON to stdout."""
+    import json
+    import torch
+    n, A, b = problems()
+    sel = np.where(n == 24)[0]
+    dev = torch.device("cuda:0")
+    s = torch.cuda.current_stream().cuda_stream
+    L = C.CDLL(PROF_LIB)
+    res = {}
+    for name, idx in (("solo_200", sel[:200]), ("batch_1024", np.resize(sel, 1024))):
+        T = [torch.tensor(x[idx], device=dev) for x in (n, A, b)]
+        out = torch.zeros((len(idx), REC), dtype=torch.float64, device=dev)
+        for _ in range(2):
+            assert L.cod_bench_launch(C.c_int(len(idx)), C.c_int(NMAX), *[C.c_void_p(t.data_ptr()) for t in T],
+                                      C.c_void_p(out.data_ptr()), C.c_int(REC), C.c_void_p(s)) == 0
+        torch.cuda.synchronize()
+        o = out.cpu().numpy()
+        res[name] = {"factor_clk": float(o[:, 0].mean()), "qr_pivot_clk": float(o[:, 3].mean()),
+                     "qr_broadcast_clk": float(o[:, 4].mean()), "qr_update_norms_clk": float(o[:, 5].mean()),
+                     "qr_writeback_clk": float(o[:, 6].mean())}
+    r = subprocess.run([MFMA_EXE], capture_output=True, text=True, timeout=120)
+    res["rank4_update"] = json.loads(r.stdout.strip().splitlines()[-1])
+    print(json.dumps(res, indent=1))
+
+
 if __name__ == "__main__":
-    {"build": build, "run": run}[sys.argv[1] if len(sys.argv) > 1 else "run"]()
+    {"build": build, "run": run, "mfma": mfma}[sys.argv[1] if len(sys.argv) > 1 else "run"]()

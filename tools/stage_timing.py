@@ -57,6 +57,12 @@ for it in range(4):
                 parts.append(f"{nm.strip()}={int(T[wi, b] - T[wi, a])}")
         print("      collide: narrow phase %d  post-process %d" % (T[wi, 76], T[wi, 77]))
         print("      construct acc: iters %d cls %d Q %d codF %d codS %d nx %d valid %d | codF qr %d rz %d rank %d" % tuple(T[wi, 60:70]))
+        if T[wi, 94] > 0:
+            a0 = T[wi, 3]
+            who = {0: "-", 1: "wave0", 2: "helper"}
+            print("      board (clk from A built): construct done %d, helper Dantzig %d..%d (%d pivots, %s), answer at %d; PGS fallback %s, frictionless %s"
+                  % (T[wi, 5] - a0, T[wi, 94] - a0, T[wi, 95] - a0, T[wi, 99], {1: "ok", 2: "failed"}.get(int(T[wi, 96]), "?"),
+                     T[wi, 6] - a0, who.get(int(T[wi, 97]), "?"), who.get(int(T[wi, 98]), "?")))
         print(f"  world {wi}: pivots {int(T[wi,52])} at row {int(T[wi,53])} pgs-sweeps {int(T[wi,54])} ign {hd[wi,7]:.0f} total {int(tot[wi])} rows {int(hd[wi,1])} clamp {int(hd[wi,2])} flag {hd[wi,4]:.0f} | " + " ".join(parts))
 
 # the slowest world of the last step re-run alone (one wave on the GPU): how

@@ -311,7 +311,7 @@ def main():
     timer.enabled = False
     bad = int(((status_acc & _native.ST_DIVERGES) != 0).sum().item())
     if bad:
-        raise SystemExit(f"bench: {bad} world(s) left the reference's physics (status {_native.status_message(int(status_acc.max().item()))})")
+        raise SystemExit(f"bench: {bad} world(s) left the reference's physics ({_native.status_message(int(np.bitwise_or.reduce(status_acc.cpu().numpy())))})")
     cstats = rollout_stats(world, state0, action, args.warmup, args.steps)
     total = args.batch * ws * args.steps
     value = total / elapsed

@@ -61,7 +61,7 @@ enum nimble_shape_type {
  * 64 rows, two per lane above (a second kernel takes those worlds), so every
  * NIMBLE_MAX_LCP-row problem is solved; NIMBLE_STATUS_LCP_TOO_LARGE is kept
  * for the layout's sake. */
-#define NIMBLE_MAX_CONTACTS 32
+#define NIMBLE_MAX_CONTACTS 42
 #define NIMBLE_MAX_LCP (3 * NIMBLE_MAX_CONTACTS)
 #define NIMBLE_MAX_SOLVED_LCP 128
 

@@ -74,7 +74,7 @@ def _require_device(*tensors):
 
 # snapshot header (csrc/pool_sizes.h) and status bits (csrc/contact.cuh)
 SN_NCON, SN_M, SN_NC, SN_NU, SN_CFM, SN_STATUS = 0, 1, 2, 3, 4, 5
-MAX_CONTACTS = 32
+MAX_CONTACTS = 42
 MAX_LCP = 3 * MAX_CONTACTS  # include/nimble_amd.h NIMBLE_MAX_LCP
 CREC, EDGE_REC, SN_ROWREC = 13, 12, 12  # csrc/pool_sizes.h
 

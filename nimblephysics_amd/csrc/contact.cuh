@@ -542,7 +542,7 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
   (void)g_stamp;
   double* ct = s + L.ct;
   double* dropped = s + L.cscr;                         // past the dynamics buffers
-  double* pairbuf = dropped + CT_MAX_DROPPED * CREC;
+  double* pairbuf = dropped + CT_MAX_DROPPED * DROP_REC;
   if (lane == 0) { ct[H_NCON] = 0; ct[H_NDROP] = 0; ct[H_STATUS] = 0; }
   WSYNC();
   const int PC = md.pairChunk;
@@ -695,7 +695,7 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
           const int nk0 = uni((int)ct[H_NCON]), nd0 = uni((int)ct[H_NDROP]);
           bool close = false;
           for (int t = 0; t < nk0 + nd0; t++) {
-            const double* o = t < nk0 ? ct + CT_CONTACTS + t * CREC : dropped + (t - nk0) * CREC;
+            const double* o = t < nk0 ? ct + CT_CONTACTS + t * CREC : dropped + (t - nk0) * DROP_REC;
             double dd = 0;
             dd += (px - o[0]) * (px - o[0]);
             dd += (py - o[1]) * (py - o[1]);
@@ -712,6 +712,7 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
           const unsigned long long km = __ballot(keep), dm = __ballot(drop);
           const unsigned long long below = (1ull << lane) - 1ull;
           double* dst = nullptr;
+          int len = CREC;
           if (keep) {
             const int idx = nk0 + __popcll(km & below);
             if (idx < md.maxContacts) {
@@ -721,10 +722,11 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
             }
           } else if (drop) {
             const int idx = nd0 + __popcll(dm & below);
-            if (idx < CT_MAX_DROPPED) dst = dropped + idx * CREC;
+            if (idx < CT_MAX_DROPPED) dst = dropped + idx * DROP_REC;
+            len = DROP_REC;
           }
           if (dst)
-            for (int i = 0; i < CREC; i++) dst[i] = rec[i];
+            for (int i = 0; i < len; i++) dst[i] = rec[i];
           if (lane == 0) {
             const int nk = nk0 + __popcll(km), nd = nd0 + __popcll(dm);
             int st = (int)ct[H_STATUS];
@@ -748,7 +750,7 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
           const double* rec = pairbuf + (q * 8 + c) * PBREC;
           bool close = false;
           for (int t = 0; t < nk + nd && !close; t++) {
-            const double* o = t < nk ? ct + CT_CONTACTS + t * CREC : dropped + (t - nk) * CREC;
+            const double* o = t < nk ? ct + CT_CONTACTS + t * CREC : dropped + (t - nk) * DROP_REC;
             double dd = 0;
             for (int i = 0; i < 3; i++) dd += (rec[i] - o[i]) * (rec[i] - o[i]);
             if (sqrt(dd) < 3.0e-12) close = true;
@@ -759,6 +761,7 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
           const bool keep = !(nn < 1e-12) && !(rec[6] < 0.0) && !(rec[6] > md.clipDepth) &&
                             (md.reactive[ba] || md.reactive[bb]);
           double* dst = nullptr;
+          int len = CREC;
           if (keep) {
             if (nk < md.maxContacts) {
               if (((int)rec[7] & 15) == CT_EDGE_EDGE || ((int)rec[7] & 15) >= CT_SPHERE_SPHERE)
@@ -769,14 +772,15 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
             }
           } else {
             if (nd < CT_MAX_DROPPED) {
-              // keep kept contacts contiguous: dropped list is separate
-              dst = dropped + (nd++) * CREC;
+              // keep kept contacts contiguous: the dropped list (positions) is separate
+              dst = dropped + (nd++) * DROP_REC;
+              len = DROP_REC;
             } else {
               st |= ST_DROPPED_OVERFLOW;
             }
           }
           if (dst)
-            for (int i = 0; i < CREC; i++) dst[i] = rec[i];
+            for (int i = 0; i < len; i++) dst[i] = rec[i];
         }
       }
       ct[H_NCON] = nk; ct[H_NDROP] = nd; ct[H_STATUS] = st;

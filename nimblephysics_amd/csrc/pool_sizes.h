@@ -19,7 +19,10 @@
 // contact-stage LDS region (Layout::ct): header, then the kept contacts
 // (the model's contact capacity, ModelDev::maxContacts <= NIMBLE_MAX_CONTACTS)
 #define CT_CONTACTS 32
-#define CT_MAX_DROPPED 8
+// postProcess dedup points of the contacts the constraint filter drops
+// (positions only: a later contact close to one is not kept either)
+#define CT_MAX_DROPPED 64
+#define DROP_REC 3
 #define CT_PAIR_CHUNK 16
 #define CT_PAIR_CHUNK_HOST CT_PAIR_CHUNK
 // contact records one mesh pair may produce, and its LDS scratch (mesh.cuh)
@@ -33,7 +36,7 @@ __host__ __device__ inline int pairBufRecs(int pairChunk, bool mesh) {
   return mesh ? (MESH_PAIR_RECS > 8 * pairChunk ? MESH_PAIR_RECS : 8 * pairChunk) : 8 * pairChunk;
 }
 __host__ __device__ inline int collideScratchDoubles(int pairChunk, bool mesh) {
-  return CT_MAX_DROPPED * CREC + pairBufRecs(pairChunk, mesh) * PBREC + (mesh ? MESH_PAIR_SCRATCH : 0);
+  return CT_MAX_DROPPED * DROP_REC + pairBufRecs(pairChunk, mesh) * PBREC + (mesh ? MESH_PAIR_SCRATCH : 0);
 }
 
 // snapshot layout

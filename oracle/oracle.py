@@ -15,7 +15,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "liboracle.so")
 REF_LIB = os.path.join(HERE, "_ref", "libodelcp.so")
-MAX_LCP = 96  # include/nimble_amd.h NIMBLE_MAX_LCP (the LCP cache layout)
+MAX_LCP = 126  # include/nimble_amd.h NIMBLE_MAX_LCP (the LCP cache layout)
 
 _lib = None
 _ref = None

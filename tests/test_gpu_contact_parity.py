@@ -402,10 +402,10 @@ def test_lcp_reduce_duplicate_columns(shape):
 
 
 def test_contact_overflow_raises():
-    """More contacts than NIMBLE_MAX_CONTACTS (nine boxes resting on the
-    ground: 36 corner contacts > 32) cannot be the reference's step: timestep
-    raises ContactCapacityError, and under the 'record' policy the per-world
-    status says why."""
+    """More contacts than NIMBLE_MAX_CONTACTS (MAX_CONTACTS // 4 + 1 boxes
+    resting on the ground, four corner contacts each) cannot be the
+    reference's step: timestep raises ContactCapacityError, and under the
+    'record' policy the per-world status says why."""
     import nimblephysics_amd as nimble
     from nimblephysics_amd import dynamics as D
     from nimblephysics_amd._native import ContactCapacityError
@@ -419,21 +419,22 @@ def test_contact_overflow_raises():
     gb.createShapeNode(D.BoxShape([10.0, 0.1, 10.0]), collision=True)
     g.setMobile(False)
     w.addSkeleton(g)
-    for k in range(9):
+    nbox = _native.MAX_CONTACTS // 4 + 1
+    for k in range(nbox):
         # vertical sliders (the model allows at most 8 free joints)
         sk = D.Skeleton(f"box{k}")
         j, b = sk.createPrismaticJointAndBodyNodePair()
         j.setAxis([0, 1, 0])
         T = np.eye(4)
-        T[0, 3] = 0.5 * k
+        T[0, 3] = 0.4 * k
         j.setTransformFromParentBodyNode(T)
         b.createShapeNode(D.BoxShape([0.2, 0.1, 0.2]), collision=True)
         w.addSkeleton(sk)
-    st = np.zeros((4, 18))
-    st[:, :9] = 0.05 - 1e-3
+    st = np.zeros((4, 2 * nbox))
+    st[:, :nbox] = 0.05 - 1e-3
     d = torch.device("cuda:0")
     ts = torch.tensor(st, device=d)
-    act = torch.zeros((4, 9), dtype=torch.float64, device=d)
+    act = torch.zeros((4, nbox), dtype=torch.float64, device=d)
     with pytest.raises(ContactCapacityError):
         nimble.timestep(w, ts, act)
     w.setStatusPolicy("record")

@@ -21,6 +21,8 @@ def build(name="step_emu", out=None):
     deps = [src, os.path.join(SRC, "hip", "hip_runtime.h")]
     csrc = os.path.join(ROOT, "nimblephysics_amd", "csrc")
     deps += [os.path.join(csrc, f) for f in os.listdir(csrc)]
+    inc = os.path.join(ROOT, "include")
+    deps += [os.path.join(inc, f) for f in os.listdir(inc)]
     if os.path.exists(out) and os.path.getmtime(out) > max(os.path.getmtime(d) for d in deps):
         return out
     subprocess.check_call([CLANG, "-std=c++20", "-O0", "-g", "-mavx512f", "-fsanitize=address",

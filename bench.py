@@ -219,6 +219,21 @@ def pmc_traffic(workload, kernel, batch):
         return None, None
 
 
+def pmc_mfma(workload, kernel):
+    """fp64 MFMA use of `kernel` per launch from the committed PMC summary
+    (profiles/pmc_mfma.json, tools/pmc_mfma.py over the rocprofv3 --pmc pass
+    of tools/gpu_measure.sh): rocprofv3's MfmaUtil (SQ_VALU_MFMA_BUSY_CYCLES
+    over GRBM_GUI_ACTIVE x SIMDs) and the MFMA FLOP rate; {} when absent."""
+    path = os.path.join(ROOT, "profiles", "pmc_mfma.json")
+    try:
+        e = json.load(open(path))[workload][kernel]
+    except Exception:
+        return {}
+    out = {"mfma_util": e.get("mfma_util"), "mfma_tflops": e.get("mfma_tflops"),
+           "mfma_flops_per_launch": e.get("mfma_f64_flops"), "mfma_source": "profiles/pmc_mfma.json"}
+    return out
+
+
 def _cpu_threads():
     try:
         n = len(os.sched_getaffinity(0))
@@ -339,6 +354,7 @@ def main():
             "roofline": {"bound": "fp64-valu", "kernel": f"nimble_{dom}_kernel", "achieved": achieved,
                          "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP64_VECTOR_PEAK_TFLOPS,
                          "traffic": traffic, "traffic_source": traffic_src,
+                         **pmc_mfma(args.workload, f"nimble_{dom}_kernel"),
                          "flops_per_world": flops[dom],
                          "note": "peak = MI355X fp64 vector (VALU) rate, which on MI355X equals the fp64 "
                                  "matrix-core rate; the forward's one dense product (the LCP matrix A = Y^T Y) runs "

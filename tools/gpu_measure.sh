@@ -31,8 +31,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_cartpole_$TAG -o r
 timeout -k 10 120 python bench.py --workload cartpole --no-cpu-baseline --steps 20 --warmup 3 > $O/bench_cartpole_$TAG.json 2>&1 || { echo CARTPOLE BENCH FAILED; exit 1; }
 echo WORKLOADS OK
 # fp64 matrix-core counters (last: a counter this rocprof does not know ends
-# only this pass)
+# only this pass); summarised here by tools/pmc_mfma.py -> profiles/pmc_mfma.json
 timeout -s KILL 60 rocprofv3 -L > $O/counters_$TAG.txt 2>&1
 grep -i -E "MFMA|MOPS" $O/counters_$TAG.txt | head -20
-timeout -s KILL 90 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_F64 SQ_BUSY_CU_CYCLES --kernel-trace -d $O/pmc_mfma_$TAG -o run --output-format csv -- $B --steps 3 --warmup 1 > $O/pmc5_$TAG.log 2>&1 || { echo PMC5 FAILED; tail -5 $O/pmc5_$TAG.log; exit 1; }
+timeout -s KILL 90 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_F64 SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d $O/pmc_mfma_$TAG -o run --output-format csv -- $B --steps 3 --warmup 1 > $O/pmc5_$TAG.log 2>&1 || { echo PMC5 FAILED; tail -5 $O/pmc5_$TAG.log; exit 1; }
 echo MEASURE DONE

@@ -79,12 +79,13 @@ MAX_LCP = 3 * MAX_CONTACTS  # include/nimble_amd.h NIMBLE_MAX_LCP
 CREC, EDGE_REC, SN_ROWREC = 13, 12, 12  # csrc/pool_sizes.h
 
 
-def snapshot_layout(n: int) -> dict:
+def snapshot_layout(n: int, timing: bool = False) -> dict:
     """Per-world snapshot offsets (doubles) of csrc/pool_sizes.h for a model
     with n dofs: header, contact records, row records, f_c, v_f, y_f, the
-    backward blocks (A_c, A_c_ub_E, pinv(Q)^T, Q), EDGE metadata and the
-    start of the HBM workspace (the stage-timing build's stamps sit 1000
-    doubles past it).  tests/test_wave_emu.py checks it against the header."""
+    backward blocks (A_c, A_c_ub_E, pinv(Q)^T, Q), EDGE metadata, the
+    stage-timing build's stamps (`timing`: 128 doubles, ahead of the
+    workspace) and the start of the HBM workspace.  tests/test_wave_emu.py
+    checks it against the header."""
     a8 = lambda x: ((x + 7) // 8) * 8
     L = {"contacts": 16}
     L["rows"] = L["contacts"] + MAX_CONTACTS * CREC
@@ -96,8 +97,8 @@ def snapshot_layout(n: int) -> dict:
     L["pt"] = L["acube"] + n * MAX_LCP
     L["q"] = L["pt"] + MAX_LCP * MAX_LCP
     L["edge"] = L["q"] + MAX_LCP * MAX_LCP
-    L["workspace"] = a8(L["edge"] + MAX_CONTACTS * EDGE_REC)
-    L["stamps"] = L["workspace"] + 1000
+    L["stamps"] = a8(L["edge"] + MAX_CONTACTS * EDGE_REC)
+    L["workspace"] = L["stamps"] + (128 if timing else 0)
     return L
 SN_FC = 16 + 13 * MAX_CONTACTS + 12 * MAX_LCP  # NIMBLE_SNAPSHOT_FC: clamping impulses f_c
 ST_CONTACT_OVERFLOW, ST_UNSUPPORTED_SHAPE, ST_DROPPED_OVERFLOW, ST_REDUCED, ST_LCP_TOO_LARGE = 1, 2, 4, 8, 16

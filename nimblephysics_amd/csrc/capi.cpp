@@ -322,7 +322,7 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
       const int a = fwdPoolDoublesHost(mcap, m.n), b = bwdPoolDoublesHost(mcap, m.n);
       ws = a > b ? a : b;
     }
-    w->snapDoubles = snapWorkspaceOffsetHost(m.n) + ws + SN_DEBUG_TAIL;
+    w->snapDoubles = snapWorkspaceOffsetHost(m.n) + ws;
   } else {
     w->snapDoubles = 8;
   }

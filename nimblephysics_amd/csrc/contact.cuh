@@ -1070,7 +1070,7 @@ __device__ void backwardPrecompute(const ModelDev& md, lds_double* sIn, const La
   FwdPool P;
   carveFwd(kLds ? (double*)poolIn : gbl((double*)poolIn), m, n, P);
 #ifdef NIMBLE_STAGE_TIMING
-  double* g_stamp = snap + snapWorkspaceOffset(n) + 1000;
+  double* g_stamp = snap + snStamps(n);
 #endif
   STAMP(45);
   const int nc = uni((int)ct[H_NC]);
@@ -1194,10 +1194,15 @@ __device__ __forceinline__ bool allRowsAlive(int m, const unsigned long long (&a
 // the reduced matrix goes to `Mred` (M1 or M2: whichever the running wave
 // owns) and the solution is mapped out (x_i = x_r[rank(rep_i)]).  Returns
 // success and validity on the full problem; `dup`: reduce merged columns.
+// (The pool's A and warm start come as plain pointers: a FwdPool passed by
+// reference to a function that is not inlined is materialised in per-lane
+// scratch, 16 KB of stores per wave.)
 template <bool kLds, int R>
-__device__ bool pgsFallbackR(const FwdPool& P, int m, double cf, const double (&bR)[R], const double (&loR)[R],
-                             const double (&hiR)[R], const int (&fiR)[R], typename Space<kLds>::dptr Mred, int lane,
-                             double (&xd)[R], bool& dup, const int* cancel, double* dbg) {
+__device__ bool pgsFallbackR(const double* PA, const double* Pxc, int m, double cf, const double (&bR)[R],
+                             const double (&loR)[R], const double (&hiR)[R], const int (&fiR)[R],
+                             typename Space<kLds>::dptr Mred, int lane, double (&xd)[R], bool& dup, const int* cancel,
+                             double* dbg) {
+  struct { const double *A, *xc; } P{PA, Pxc};
   double scl[R];
   int rep[R];
   unsigned long long alive[R];
@@ -1236,8 +1241,9 @@ __device__ bool pgsFallbackR(const FwdPool& P, int m, double cf, const double (&
 // submatrix of A + cfm I over them, read in place), from zero; the answer
 // per row (friction rows 0).
 template <bool kLds, int R>
-__device__ void frictionlessPgsR(const FwdPool& P, int m, double cf, const int (&fiR)[R], int lane, double (&X)[R],
-                                 const int* cancel) {
+__device__ void frictionlessPgsR(const double* PA, const double* Pb, const double* Plo, const double* Phi, int m,
+                                 double cf, const int (&fiR)[R], int lane, double (&X)[R], const int* cancel) {
+  struct { const double *A, *b, *lo, *hi; } P{PA, Pb, Plo, Phi};
   bool keepMe[R];
   unsigned long long km[R];
 #pragma unroll
@@ -1296,7 +1302,7 @@ __device__ __forceinline__ bool contactStage(const ModelDev& md, double* s, cons
   cache = gbl(cache);
   overflowWs = gbl(overflowWs);
 #ifdef NIMBLE_STAGE_TIMING
-  double* g_stamp = snap + snapWorkspaceOffset(n) + 1000;
+  double* g_stamp = snap + snStamps(n);
 #endif
   STAMP(0);
   double* ct = s + L.ct;
@@ -1373,7 +1379,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   snap = gbl(snap);
   cache = gbl(cache);
 #ifdef NIMBLE_STAGE_TIMING
-  double* g_stamp = snap + snapWorkspaceOffset(n) + 1000;
+  double* g_stamp = snap + snStamps(n);
 #endif
   double* ct = s + L.ct;
   const double* Lm = s + L.M;
@@ -1593,7 +1599,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
 #endif
           bool dup;
           double xp[R];
-          const bool okp = pgsFallbackR<kLds, R>(P, m, md.fallbackCfm, bR, loR, hiR, fiR, sp<kLds>(P.M1), lane, xp,
+          const bool okp = pgsFallbackR<kLds, R>(P.A, P.xc, m, md.fallbackCfm, bR, loR, hiR, fiR, sp<kLds>(P.M1), lane, xp,
                                                  dup, board(ct) + BD_STOPP, dbgPgs);
 #pragma unroll
           for (int q = 0; q < R; q++)
@@ -1608,7 +1614,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
           if (lane == 0) g_stamp[98] = 1;
 #endif
           double xf[R];
-          frictionlessPgsR<kLds, R>(P, m, md.fallbackCfm, fiR, lane, xf, board(ct) + BD_STOPF);
+          frictionlessPgsR<kLds, R>(P.A, P.b, P.lo, P.hi, m, md.fallbackCfm, fiR, lane, xf, board(ct) + BD_STOPF);
 #pragma unroll
           for (int q = 0; q < R; q++)
             if (rowAt(q, lane) < m) P.xf[rowAt(q, lane)] = xf[q];
@@ -1679,7 +1685,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
         if (lane == 0) ct[H_CODOK] = 0;
         bool dup;
         double xd[R];
-        ok = pgsFallbackR<kLds, R>(P, m, cf, bR, loR, hiR, fiR, sp<kLds>(P.M1), lane, xd, dup, nullptr, dbgPgs);
+        ok = pgsFallbackR<kLds, R>(P.A, P.xc, m, cf, bR, loR, hiR, fiR, sp<kLds>(P.M1), lane, xd, dup, nullptr, dbgPgs);
         if (dup && lane == 0) ct[H_STATUS] = (double)((int)ct[H_STATUS] | ST_DUPLICATE_COLUMNS);
         if (ok)
 #pragma unroll
@@ -1687,7 +1693,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
       }
       if (!ok) {
         ign = true;
-        frictionlessPgsR<kLds, R>(P, m, cf, fiR, lane, X, nullptr);
+        frictionlessPgsR<kLds, R>(P.A, P.b, P.lo, P.hi, m, cf, fiR, lane, X, nullptr);
       }
     }
     bool nan2 = false;
@@ -1837,7 +1843,7 @@ __device__ void helperWave(const ModelDev& md, double* s, const Layout& L, int l
 #endif
             bool dup;
             double xp[1];
-            const bool okp = pgsFallbackR<true, 1>(P, m, cf, bR, loR, hiR, fiR, sp<true>(P.M2), lane, xp, dup,
+            const bool okp = pgsFallbackR<true, 1>(P.A, P.xc, m, cf, bR, loR, hiR, fiR, sp<true>(P.M2), lane, xp, dup,
                                                    board(ct) + BD_STOPP, nullptr);
             if (lane < m) P.xp[lane] = xp[0];
             boardSet(ct, BD_PDUP, dup ? 1 : 0, lane);
@@ -1852,7 +1858,7 @@ __device__ void helperWave(const ModelDev& md, double* s, const Layout& L, int l
             if (lane == 0 && g_stamp) g_stamp[98] = 2;
 #endif
             double xf[1];
-            frictionlessPgsR<true, 1>(P, m, cf, fiR, lane, xf, board(ct) + BD_STOPF);
+            frictionlessPgsR<true, 1>(P.A, P.b, P.lo, P.hi, m, cf, fiR, lane, xf, board(ct) + BD_STOPF);
             if (lane < m) P.xf[lane] = xf[0];
             boardSet(ct, BD_F, 1, lane);
           }
@@ -1998,7 +2004,7 @@ __device__ int contactBackwardPrep(const ModelDev& md, double* s, const Layout& 
   const double* dinv = s + L.dinv;
   const int imp = uni((int)sn[SN_IMP]);
 #ifdef NIMBLE_STAGE_TIMING
-  double* g_stamp = (double*)sn + snapWorkspaceOffset(n) + 1000;
+  double* g_stamp = (double*)sn + snStamps(n);
 #endif
   STAMP(30);
   (void)ct;

@@ -67,14 +67,17 @@ __host__ __device__ inline int snPT(int n) { return snAcubE(n) + n * SN_MAXL; } 
 __host__ __device__ inline int snQ(int n) { return snPT(n) + SN_MAXL * SN_MAXL; }   // Q
 // EDGE_EDGE metadata of the kept contacts (EDGE_REC doubles per contact slot)
 __host__ __device__ inline int snEdge(int n) { return snQ(n) + SN_MAXL * SN_MAXL; }
-__host__ __device__ inline int snapWorkspaceOffset(int n) { return snAlign8(snEdge(n) + NIMBLE_MAX_CONTACTS * EDGE_REC); }
-// 64 doubles at the very end of the snapshot for debug stamps, in the
-// stage-timing build only
+// stage-timing builds (-DNIMBLE_STAGE_TIMING, tools/stage_timing*.py) keep
+// SN_DEBUG_TAIL doubles of clock stamps at snStamps(n), ahead of the HBM
+// workspace (which worlds with large LCPs use as their pool); product builds
+// have none
 #ifdef NIMBLE_STAGE_TIMING
-#define SN_DEBUG_TAIL 64
+#define SN_DEBUG_TAIL 128
 #else
 #define SN_DEBUG_TAIL 0
 #endif
+__host__ __device__ inline int snStamps(int n) { return snAlign8(snEdge(n) + NIMBLE_MAX_CONTACTS * EDGE_REC); }
+__host__ __device__ inline int snapWorkspaceOffset(int n) { return snStamps(n) + SN_DEBUG_TAIL; }
 
 // LCP workspace pools for m rows and n dofs
 #define NV_COLS 16

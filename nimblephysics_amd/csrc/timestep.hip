@@ -331,7 +331,7 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
 #ifdef NIMBLE_STAGE_TIMING
         // where the helper runs: HW_ID (SIMD, CU, SE) and XCC_ID
         if (lane == 0 && md.numPairs > 0) {
-          double* gs = snapshot + (size_t)env * snapDoubles + snapWorkspaceOffset(n) + 1000;
+          double* gs = snapshot + (size_t)env * snapDoubles + snStamps(n);
           gs[92] = (double)(unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));
           gs[93] = (double)(unsigned)__builtin_amdgcn_s_getreg(20 | (15 << 11));
         }
@@ -340,7 +340,7 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
         collideWorld(md, lds<true>(s), L, lane, snapshot + (size_t)env * snapDoubles + snEdge(n));
         collidePost(ct, CS_DONE, lane);
 #ifdef NIMBLE_STAGE_TIMING
-        double* hstamp = snapshot + (size_t)env * snapDoubles + snapWorkspaceOffset(n) + 1000;
+        double* hstamp = snapshot + (size_t)env * snapDoubles + snStamps(n);
 #else
         double* hstamp = nullptr;
 #endif
@@ -354,7 +354,7 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
     const int env = blockIdx.x;
     const double* st = state + (size_t)env * 2 * n;
 #ifdef NIMBLE_STAGE_TIMING
-    double* g_stamp = md.numPairs > 0 ? snapshot + (size_t)env * snapDoubles + snapWorkspaceOffset(n) + 1000 : nullptr;
+    double* g_stamp = md.numPairs > 0 ? snapshot + (size_t)env * snapDoubles + snStamps(n) : nullptr;
 #endif
     STAMP(10);
 #ifdef NIMBLE_STAGE_TIMING
@@ -595,7 +595,7 @@ __device__ __forceinline__ void backwardItems(const ModelDev* __restrict__ mdp, 
       if ((mEnv > deferRows) != (R > 1)) continue;  // the other kernel's item
     }
 #ifdef NIMBLE_STAGE_TIMING
-    double* g_stamp = md.numPairs > 0 ? snapshot + (size_t)env * snapDoubles + snapWorkspaceOffset(n) + 1000 : nullptr;
+    double* g_stamp = md.numPairs > 0 ? snapshot + (size_t)env * snapDoubles + snStamps(n) : nullptr;
 #endif
     STAMP(20);
     if (fcMode && (md.numPairs == 0 || unitRow >= uni((int)snapshot[(size_t)env * snapDoubles + SN_NC]))) {

@@ -10,7 +10,12 @@ import models  # noqa: E402
 import nimblephysics_amd as nimble  # noqa: E402
 
 B = 1024
-w = models.atlas_world(True)
+import os  # noqa: E402
+if os.environ.get("STAGE_WORKLOAD") == "atlas_mesh":
+    from nimblephysics_amd import workloads  # noqa: E402
+    w = workloads.atlas_mesh_world(True)
+else:
+    w = models.atlas_world(True)
 st, f = models.random_states(w, B, seed=1000, q_scale=0.02, v_scale=0.05)
 d = torch.device("cuda:0")
 state, action = torch.tensor(st, device=d), torch.tensor(f, device=d)
@@ -22,7 +27,7 @@ nxt = torch.empty_like(state)
 s = torch.cuda.current_stream().cuda_stream
 n = w.getNumDofs()
 from nimblephysics_amd import _native  # noqa: E402
-ws = _native.snapshot_layout(n)["stamps"]  # snapWorkspaceOffset(n) + 1000
+ws = _native.snapshot_layout(n, timing=True)["stamps"]  # csrc/pool_sizes.h snStamps(n)
 for it in range(4):
     snap[:, ws:ws + 100] = 0
     prev_state, prev_cache = state.clone(), cache.clone()

@@ -20,7 +20,7 @@ nxt = torch.empty_like(state)
 s = torch.cuda.current_stream().cuda_stream
 n = w.getNumDofs()
 from nimblephysics_amd import _native  # noqa: E402
-ws = _native.snapshot_layout(n)["stamps"]  # snapWorkspaceOffset(n) + 1000
+ws = _native.snapshot_layout(n, timing=True)["stamps"]  # csrc/pool_sizes.h snStamps(n)
 g = torch.tensor(np.random.default_rng(0).standard_normal(st.shape), device=d)
 gs, gf = torch.empty_like(state), torch.empty_like(action)
 dev.forward(state, action, cache, nxt, snap, s)

@@ -1157,14 +1157,41 @@ __device__ void backwardPrecompute(const ModelDev& md, lds_double* sIn, const La
   }
   WSYNC();
   STAMP(50);
-  // ||I - Q Q^+||^2 with (Q Q^+)[r][c] = sum_j Q[r][perm_j] z_c[j]
+  // ||I - Q Q^+||^2 with (Q Q^+)[r][c] = sum_j Q[r][perm_j] z_c[j] on the
+  // matrix cores: one v_mfma_f64_16x16x4f64 chain per 16 x 16 tile (A
+  // operand lane l: row l % 16 of Q with columns permuted, k = l / 16; B
+  // operand: the tile's columns of Q^+, i.e. the rows z_c of Zs; result
+  // element e of lane l = row l / 16 + 4 e, column l % 16).  The reference's
+  // GEMM (BackpropSnapshot.cpp:2964 imprecisionMap = I - Q * Qinv): O(n_c^3)
+  // multiply-adds, which the lane-per-entry dot products took ~7M clocks
+  // for at n_c = 96 (stage timing, mesh Atlas).
   double part = 0.0;
-  for (int t = lane; t < nc * nc; t += WAVE) {
-    const int r = t / nc, c = t % nc;
-    double acc = 0;
-    for (int j = 0; j < nc; j++) acc += P.M2[r * nc + cod.perm[j]] * Zs[c * nc + j];
-    const double e = (r == c ? 1.0 : 0.0) - acc;
-    part += e * e;
+  {
+    const int i16 = lane & 15, kq = lane >> 4;
+    const int T = (nc + 15) >> 4;
+    const double* Qm = P.M2;
+    for (int ti = 0; ti < T; ti++) {
+      const int r = ti * 16 + i16;
+      for (int tj = 0; tj < T; tj++) {
+        const int c = tj * 16 + i16;
+        nimble_double4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+        for (int k0 = 0; k0 < nc; k0 += 4) {
+          const int k = k0 + kq;
+          const bool kin = k < nc;
+          const int pk = cod.perm[kin ? k : 0];
+          const double a = (kin && r < nc) ? Qm[(r < nc ? r : 0) * nc + pk] : 0.0;
+          const double b = (kin && c < nc) ? Zs[(c < nc ? c : 0) * nc + (kin ? k : 0)] : 0.0;
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          const int rr = ti * 16 + kq + 4 * e;
+          const double d = (rr == c ? 1.0 : 0.0) - acc[e];
+          if (rr < nc && c < nc) part += d * d;
+        }
+      }
+    }
   }
   const double tot = waveSum(part);
   if (lane == 0) snap[SN_IMP] = tot >= 1e-18 ? 1.0 : 0.0;

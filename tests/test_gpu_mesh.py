@@ -7,8 +7,8 @@ colliders, python/nimblephysics_benchmarks/atlas_bench.py:18-19) on the GPU.
   sequence, points / normals / depths at 1e-9;
 * every world steps and differentiates like the oracle (LCP path, next
   state, gradients at 1e-6 per element), including the ~40% whose LCP has
-  more than 64 rows (up to 96: 32 frictional contacts), which the
-  two-rows-per-lane kernels take.
+  more than 64 rows (the layout holds 126: 42 frictional contacts), which
+  the two-rows-per-lane kernels take.
 """
 import numpy as np
 import pytest

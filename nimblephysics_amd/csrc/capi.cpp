@@ -34,6 +34,8 @@ struct nimble_world {
   // LCPs with more rows than this run in the two-rows-per-lane kernels
   // (nimble_forward_wide_kernel / nimble_backward_wide_kernel)
   int deferRows = 64;
+  Layout fwdWide{};     // the wide forward kernel's layout (LDS stage, see nimble_world_create)
+  size_t wideLds = 0;   // its LDS bytes
   int jacWsDoubles = 0;  // per-workgroup LCP workspace of the Jacobian launch
   int cacheDoubles = NIMBLE_MAX_LCP + 1;
   hipFunction_t dummy = nullptr;
@@ -309,6 +311,33 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
     return fail(NIMBLE_ERR_UNSUPPORTED, "model too large for LDS");
   }
   w->bwd = makeLayout(m, true, bwdRows);
+  // the wide forward kernel's layout: the forward's, plus an LDS stage at the
+  // pool (idle there: its pools are off chip) for the COD factorisations of
+  // the largest clamping set, mcap x mcap with the COD workspace, as far as
+  // a CU's 160 KB allow (one wide world per CU then; most of the launch's
+  // workgroups are not deferred worlds and exit at once)
+  w->fwdWide = w->fwd;
+  w->wideLds = (size_t)w->fwd.total * sizeof(double);
+  {
+    const int mc = 3 * maxContacts < NIMBLE_MAX_SOLVED_LCP ? 3 * maxContacts : NIMBLE_MAX_SOLVED_LCP;
+    const int need = mc * mc + 4 * mc + (mc + 1) / 2 + 3 + mc;
+    const int room = (int)(160 * 1024 / sizeof(double)) - w->fwd.pool;
+    // off unless NIMBLE_AMD_WIDE_STAGE=1: measured on the mesh Atlas (1024
+    // worlds, ~37 % wide) the stage's 148 KB leave one wide world per CU
+    // instead of three, and the faster factorisations do not make up for the
+    // second round (forward 11.38 vs 10.57 ms)
+    const char* ev = getenv("NIMBLE_AMD_WIDE_STAGE");
+    if (m.numPairs > 0 && mc > 24 && ev && atoi(ev) == 1) {
+      const int cap = need < room ? need : room;
+      w->fwdWide.stage = w->fwd.pool;
+      w->fwdWide.stageCap = cap;
+      const size_t end = (size_t)(w->fwd.pool + cap) * sizeof(double);
+      if (end > w->wideLds) w->wideLds = end;
+    }
+    if (getenv("NIMBLE_AMD_VERBOSE"))
+      fprintf(stderr, "nimble_amd: wide forward LDS %zu B (COD stage %d doubles of %d needed)\n", w->wideLds,
+              w->fwdWide.stageCap, need);
+  }
   if (getenv("NIMBLE_AMD_VERBOSE"))
     fprintf(stderr, "nimble_amd: LDS forward %d B (pool rows %d), backward %d B (pool rows %d), max rows %d\n",
             w->fwd.total * 8, fwdRows, w->bwd.total * 8, bwdRows, mcap);
@@ -399,7 +428,7 @@ int nimble_forward(nimble_world_t w, int32_t batch, const double* state, const d
     // the worlds whose LCP has more rows than one per lane (or than the
     // test threshold): stepped by the two-rows-per-lane kernel
     if (w->host.numPairs > 0 && w->maxRows > w->deferRows) {
-      hipLaunchKernelGGL(nimble_forward_wide_kernel, dim3(cnt), dim3(fwdThreads), lds, st, w->dev, w->fwd,
+      hipLaunchKernelGGL(nimble_forward_wide_kernel, dim3(cnt), dim3(fwdThreads), w->wideLds, st, w->dev, w->fwdWide,
                          state + b0 * 2 * n, forces + b0 * n, lcp_cache + (size_t)b0 * w->cacheDoubles,
                          next_state + b0 * 2 * n, snapshot + (size_t)b0 * w->snapDoubles, w->snapDoubles,
                          w->cacheDoubles);

@@ -813,9 +813,46 @@ __device__ inline double rowForceEntry(const ModelDev& md, const double* s, cons
 // Q = A_cc + A_cu E + cfm I  (== A_c^T Minv A_c_ub_E + cfm I).
 // Returns the standardized flag (wave-uniform).
 // ---------------------------------------------------------------------------
+// COD factorisation of a matrix in the HBM workspace (worlds whose LCP pool
+// is off chip: the wide kernels, > 64 rows) staged through the workgroup's
+// LDS when the launch provides a stage (Layout::stage / stageCap, see capi.cpp:
+// the pool area, idle in those kernels, extended for the model's largest
+// clamping set): the matrix and the COD workspace are copied in, factorised by
+// the LDS code (the same arithmetic, so the same factor bit for bit) and
+// copied back.  Each step of the factorisation reads its trailing columns
+// from LDS instead of L2 / HBM (~5M -> well under 1M clocks at 96 x 96).
+template <bool kLds, int R>
+__device__ __forceinline__ void codFactorAny(typename Space<kLds>::dptr A, typename Space<kLds>::dptr ws, int m, int n,
+                                             int ld, typename Space<kLds>::dptr v, int lane, lds_double* stage,
+                                             int stageCap, double* prof = nullptr) {
+  m = uni(m);
+  n = uni(n);
+  ld = uni(ld);
+  const int mx = m > n ? m : n;
+  const int wsd = 4 * mx + (mx + 1) / 2 + 3;  // carveCod: vd vn zd zn perm rank
+  if (kLds || stage == nullptr || m * ld + wsd + mx > stageCap) {
+    codFactorR<kLds, R>(A, ws, m, n, ld, v, lane, prof);
+    return;
+  }
+  double* gA = (double*)A;
+  double* gW = (double*)ws;
+  double* sA = (double*)stage;
+  double* sW = sA + m * ld;
+  double* sV = sW + wsd;
+  for (int t = lane; t < m * ld; t += WAVE) sA[t] = gA[t];
+  for (int t = lane; t < wsd; t += WAVE) sW[t] = gW[t];
+  WSYNC();
+  codFactorR<true, R>(sp<true>(sA), sp<true>(sW), m, n, ld, sp<true>(sV), lane, prof);
+  WSYNC();
+  for (int t = lane; t < m * ld; t += WAVE) gA[t] = sA[t];
+  for (int t = lane; t < wsd; t += WAVE) gW[t] = sW[t];
+  WSYNC();
+}
+
 template <bool kLds, int R = 1>
 __device__ bool devConstruct(typename Space<kLds>::dptr poolIn, int m, int n, double cfm, bool ignoreFriction,
-                             lds_double* ctIn, int lane, double* g_stamp = nullptr) {
+                             lds_double* ctIn, int lane, double* g_stamp = nullptr, lds_double* stage = nullptr,
+                             int stageCap = 0) {
   (void)g_stamp;
   FwdPool P;
   carveFwd((double*)poolIn, m, n, P);
@@ -939,9 +976,10 @@ __device__ bool devConstruct(typename Space<kLds>::dptr poolIn, int m, int n, do
     TACC_END(62, tQ);
     TACC_BEGIN(tF);
 #ifdef NIMBLE_STAGE_TIMING
-    codFactorR<kLds, R>(sp<kLds>(Q), sp<kLds>(P.scr), nc, nc, nc, sp<kLds>(vv), lane, g_stamp ? g_stamp + 67 : nullptr);
+    codFactorAny<kLds, R>(sp<kLds>(Q), sp<kLds>(P.scr), nc, nc, nc, sp<kLds>(vv), lane, stage, stageCap,
+                          g_stamp ? g_stamp + 67 : nullptr);
 #else
-    codFactorR<kLds, R>(sp<kLds>(Q), sp<kLds>(P.scr), nc, nc, nc, sp<kLds>(vv), lane);
+    codFactorAny<kLds, R>(sp<kLds>(Q), sp<kLds>(P.scr), nc, nc, nc, sp<kLds>(vv), lane, stage, stageCap);
 #endif
     if (lane == 0) ct[H_CODOK] = 1;
     STAMP(42);
@@ -1013,7 +1051,8 @@ __device__ bool devConstruct(typename Space<kLds>::dptr poolIn, int m, int n, do
 // guessSolution (LCPUtils.cpp:69): COD solve on {normal rows with b > 0} U
 // {friction rows}; result into x.
 template <bool kLds, int R = 1>
-__device__ void devGuess(typename Space<kLds>::dptr poolIn, int m, int n, lds_double* ctIn, int lane) {
+__device__ void devGuess(typename Space<kLds>::dptr poolIn, int m, int n, lds_double* ctIn, int lane,
+                         lds_double* stage = nullptr, int stageCap = 0) {
   FwdPool P;
   carveFwd((double*)poolIn, m, n, P);
   double* ct = (double*)ctIn;
@@ -1041,7 +1080,7 @@ __device__ void devGuess(typename Space<kLds>::dptr poolIn, int m, int n, lds_do
   double* z = w; w += m;
   double* xr = w; w += m;
   (void)cn;
-  codFactorR<kLds, R>(sp<kLds>(Ar), sp<kLds>(P.scr), k, k, k, sp<kLds>(vv), lane);
+  codFactorAny<kLds, R>(sp<kLds>(Ar), sp<kLds>(P.scr), k, k, k, sp<kLds>(vv), lane, stage, stageCap);
   {
     double rv[R], xo[R];
 #pragma unroll
@@ -1062,7 +1101,8 @@ __device__ void devGuess(typename Space<kLds>::dptr poolIn, int m, int n, lds_do
 // rank-deficiency flag ||I - Q Q^+||^2 >= 1e-18.
 template <bool kLds, int R = 1>
 __device__ void backwardPrecompute(const ModelDev& md, lds_double* sIn, const Layout& L, int lane,
-                                   typename Space<kLds>::dptr poolIn, int m, double cfm, double* snap, lds_double* ctIn) {
+                                   typename Space<kLds>::dptr poolIn, int m, double cfm, double* snap, lds_double* ctIn,
+                                   lds_double* stage = nullptr, int stageCap = 0) {
   const int n = md.n;
   double* s = (double*)sIn;
   double* ct = (double*)ctIn;
@@ -1118,7 +1158,7 @@ __device__ void backwardPrecompute(const ModelDev& md, lds_double* sIn, const La
   double* cn = w; w += m;
   double* vv = w; w += m;
   STAMP(48);
-  if (!reuse) codFactorR<kLds, R>(sp<kLds>(P.M1), sp<kLds>(P.scr), nc, nc, nc, sp<kLds>(vv), lane);
+  if (!reuse) codFactorAny<kLds, R>(sp<kLds>(P.M1), sp<kLds>(P.scr), nc, nc, nc, sp<kLds>(vv), lane, stage, stageCap);
   STAMP(49);
   // pinv(Q): lane c solves Q x = e_c in place in row c of the (now free) A
   // region (columns c, c + 64, .. when n_c > 64)
@@ -1530,6 +1570,9 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   // the helper wave starts Dantzig on A now (the task board, see helperWave):
   // A, b, lo, hi and findex are final; the warm start follows
   const bool tasked = kLds && R == 1 && helperOn;
+  // off-chip pools (wide kernels) factorise through the launch's LDS stage
+  lds_double* stage = (!kLds && L.stageCap > 0) ? sp<true>(s + L.stage) : nullptr;
+  const int stageCap = L.stageCap;
   if (tasked) {
     if (lane < BD_INTS) board(ct)[lane] = 0;
     helperPost(ct, HS_TASK, lane);
@@ -1546,7 +1589,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
     for (int i = lane; i < m; i += WAVE) { P.X[i] = cache[1 + i]; P.xc[i] = cache[1 + i]; }
     WSYNC();
   } else {
-    devGuess<kLds, R>(poolIn, m, n, sp<true>(ct), lane);
+    devGuess<kLds, R>(poolIn, m, n, sp<true>(ct), lane, stage, stageCap);
     for (int i = lane; i < m; i += WAVE) P.xc[i] = P.X[i];
     WSYNC();
   }
@@ -1554,10 +1597,10 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   if (lane == 0) ct[H_CODOK] = 0;
   STAMP(4);
 #ifdef NIMBLE_STAGE_TIMING
-  bool success = devConstruct<kLds, R>(poolIn, m, n, 0.0, false, sp<true>(ct), lane, g_stamp);
+  bool success = devConstruct<kLds, R>(poolIn, m, n, 0.0, false, sp<true>(ct), lane, g_stamp, stage, stageCap);
   double* dbgPgs = g_stamp + 54;
 #else
-  bool success = devConstruct<kLds, R>(poolIn, m, n, 0.0, false, sp<true>(ct), lane);
+  bool success = devConstruct<kLds, R>(poolIn, m, n, 0.0, false, sp<true>(ct), lane, nullptr, stage, stageCap);
   double* dbgPgs = nullptr;
 #endif
   if (tasked && success) stopAll();
@@ -1750,7 +1793,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   if (!shortCircuit) {
     for (int i = lane; i < m; i += WAVE) P.xc[i] = P.X[i];
     WSYNC();
-    std2 = devConstruct<kLds, R>(poolIn, m, n, cfm, ignoredFriction, sp<true>(ct), lane);
+    std2 = devConstruct<kLds, R>(poolIn, m, n, cfm, ignoredFriction, sp<true>(ct), lane, nullptr, stage, stageCap);
   }
   const double* Xf = std2 ? P.X : P.xc;
   STAMP(8);
@@ -1790,7 +1833,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   const int nc = uni((int)ct[H_NC]);
   for (int i = lane; i < nc; i += WAVE) snap[SN_FC + i] = P.fc[i];
   for (int i = lane; i < n; i += WAVE) snap[snYf(n) + i] = ddq[i];
-  backwardPrecompute<kLds, R>(md, sIn, md.lay[0], lane, poolIn, m, cfm, snap, sp<true>(ct));  // (not inlined)
+  backwardPrecompute<kLds, R>(md, sIn, md.lay[0], lane, poolIn, m, cfm, snap, sp<true>(ct), stage, stageCap);  // (not inlined)
   if (lane == 0) {
     snap[SN_NCON] = nCon;
     snap[SN_M] = m;

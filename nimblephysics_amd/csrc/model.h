@@ -24,6 +24,9 @@ struct Layout {
   // the dynamics buffers V/A/IC/F so the helper wave can run the collision
   // detection while wave 0 is still in the dynamics
   int cscr;
+  // forward, wide kernels only: an LDS stage (offset, capacity in doubles)
+  // for the COD factorisations of off-chip LCP pools (0: none)
+  int stage, stageCap;
   int total;
 };
 

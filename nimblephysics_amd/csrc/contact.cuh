@@ -1665,7 +1665,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
         if (d >= 2 && pst == 2 && boardGet(ct, BD_F) == 1) { boardSrc = 2; break; }
         if (pst == 0 && boardClaim(ct, BD_PCLAIM, 1, lane)) {
 #ifdef NIMBLE_STAGE_TIMING
-          if (lane == 0) g_stamp[97] = 1;
+          if (lane == 0) { g_stamp[97] = 1; g_stamp[100] = (double)__builtin_amdgcn_s_memtime(); }
 #endif
           bool dup;
           double xp[R];
@@ -1677,11 +1677,14 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
           boardSet(ct, BD_PDUP, dup ? 1 : 0, lane);
           if (okp) boardSet(ct, BD_STOPF, 1, lane);
           boardSet(ct, BD_P, okp ? 1 : 2, lane);
+#ifdef NIMBLE_STAGE_TIMING
+          if (lane == 0) g_stamp[101] = (double)__builtin_amdgcn_s_memtime();
+#endif
           continue;
         }
         if (pst != 1 && boardGet(ct, BD_F) == 0 && boardClaim(ct, BD_FCLAIM, 1, lane)) {
 #ifdef NIMBLE_STAGE_TIMING
-          if (lane == 0) g_stamp[98] = 1;
+          if (lane == 0) { g_stamp[98] = 1; g_stamp[102] = (double)__builtin_amdgcn_s_memtime(); }
 #endif
           double xf[R];
           frictionlessPgsR<kLds, R>(P.A, P.b, P.lo, P.hi, m, md.fallbackCfm, fiR, lane, xf, board(ct) + BD_STOPF);
@@ -1689,6 +1692,9 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
           for (int q = 0; q < R; q++)
             if (rowAt(q, lane) < m) P.xf[rowAt(q, lane)] = xf[q];
           boardSet(ct, BD_F, 1, lane);
+#ifdef NIMBLE_STAGE_TIMING
+          if (lane == 0) g_stamp[103] = (double)__builtin_amdgcn_s_memtime();
+#endif
           continue;
         }
         if (it > (1ll << 24)) __builtin_trap();
@@ -1909,7 +1915,7 @@ __device__ void helperWave(const ModelDev& md, double* s, const Layout& L, int l
         if (pOpen && boardGet(ct, BD_G) == 1) {
           if (boardClaim(ct, BD_PCLAIM, 2, lane)) {
 #ifdef NIMBLE_STAGE_TIMING
-            if (lane == 0 && g_stamp) g_stamp[97] = 2;
+            if (lane == 0 && g_stamp) { g_stamp[97] = 2; g_stamp[100] = (double)__builtin_amdgcn_s_memtime(); }
 #endif
             bool dup;
             double xp[1];
@@ -1919,18 +1925,24 @@ __device__ void helperWave(const ModelDev& md, double* s, const Layout& L, int l
             boardSet(ct, BD_PDUP, dup ? 1 : 0, lane);
             if (okp) boardSet(ct, BD_STOPF, 1, lane);
             boardSet(ct, BD_P, okp ? 1 : 2, lane);
+#ifdef NIMBLE_STAGE_TIMING
+            if (lane == 0 && g_stamp) g_stamp[101] = (double)__builtin_amdgcn_s_memtime();
+#endif
           }
           continue;
         }
         if (fOpen) {
           if (boardClaim(ct, BD_FCLAIM, 2, lane)) {
 #ifdef NIMBLE_STAGE_TIMING
-            if (lane == 0 && g_stamp) g_stamp[98] = 2;
+            if (lane == 0 && g_stamp) { g_stamp[98] = 2; g_stamp[102] = (double)__builtin_amdgcn_s_memtime(); }
 #endif
             double xf[1];
             frictionlessPgsR<true, 1>(P.A, P.b, P.lo, P.hi, m, cf, fiR, lane, xf, board(ct) + BD_STOPF);
             if (lane < m) P.xf[lane] = xf[0];
             boardSet(ct, BD_F, 1, lane);
+#ifdef NIMBLE_STAGE_TIMING
+            if (lane == 0 && g_stamp) g_stamp[103] = (double)__builtin_amdgcn_s_memtime();
+#endif
           }
           continue;
         }

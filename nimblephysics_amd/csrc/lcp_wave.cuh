@@ -43,13 +43,30 @@
 // principal submatrix A[idx][idx] of a matrix with leading dimension ld
 // (lane j holds idx_j), read in place (LCPUtils::removeFriction without a
 // gathered copy).
-template <bool kLds, bool kMapped, int R>
+//
+// Contact-layout rows clamp with v_max_f64 / v_min_f64 (their box is never
+// inverted: l = -h <= 0 <= h); for operands that are not NaN that is the
+// reference's compare-and-assign chain, two dependent operations instead of
+// six on the sweep's critical path.  A NaN anywhere leaves a non-finite
+// residual behind (maxNum would otherwise swallow it), so a solve that ends
+// with one is re-run from its inputs with the reference's chain (kExact).
+template <bool kLds, bool kMapped, int R, bool kExact = false>
 __device__ bool wavePgsR(int n, typename Space<kLds>::cdptr Ain, double (&x)[R], const double (&bIn)[R],
                          const double (&lo)[R], const double (&hi)[R], const int (&findex)[R], int lane,
                          double* dbg = nullptr, double shift = 0.0, const int* cancel = nullptr, int ld = -1,
                          const int* idxIn = nullptr) {
   n = uni(n);
   if (n == 0) return true;
+  double xEntry[R];
+#pragma unroll
+  for (int s = 0; s < R; s++) xEntry[s] = x[s];
+  // (kExact = false) a non-finite residual or iterate: re-run exactly
+  auto nonFinite = [&](const double (&rv)[R], const double (&xv)[R]) {
+    bool bad = false;
+#pragma unroll
+    for (int s = 0; s < R; s++) bad = bad || (rowAt(s, lane) < n && !(isfinite(rv[s]) && isfinite(xv[s])));
+    return __ballot(bad) != 0ull;
+  };
   ld = kMapped ? uni(ld) : n;
   int idx[R];
   double b[R];
@@ -189,8 +206,12 @@ __device__ bool wavePgsR(int n, typename Space<kLds>::cdptr Ain, double (&x)[R],
       if (!nrm) { h = h * xN; l = l * xN; }
       const double rr = pick(r, i), xs0 = pick(x0, i), dg = pick(diagRaw, i);
       double nx = (rr + dg * xs0) / dg;
-      const double t = nx < l ? l : nx;
-      nx = nx > h ? h : t;
+      if constexpr (kExact) {
+        const double t = nx < l ? l : nx;
+        nx = nx > h ? h : t;
+      } else {
+        nx = fmin(fmax(nx, l), h);
+      }
       const double dx = rdl(nx - xs0, i & 63);
       if (nrm) xN = rdl(nx, i & 63);
       setR(xn, i, lane, nx);
@@ -240,6 +261,13 @@ __device__ bool wavePgsR(int n, typename Space<kLds>::cdptr Ain, double (&x)[R],
 #pragma unroll
     for (int s = 0; s < R; s++) moved = moved || (inOrder[s] && fabs(xn[s] - x0[s]) > deltaXThr);
     if (!__ballot(moved)) {
+      if constexpr (!kExact) {
+        if (contactRows && nonFinite(r, xn)) {
+#pragma unroll
+          for (int s = 0; s < R; s++) x[s] = xEntry[s];
+          return wavePgsR<kLds, kMapped, R, true>(n, Ain, x, bIn, lo, hi, findex, lane, dbg, shift, cancel, ld, idxIn);
+        }
+      }
 #pragma unroll
       for (int s = 0; s < R; s++) x[s] = xn[s];
       return true;
@@ -281,8 +309,12 @@ __device__ bool wavePgsR(int n, typename Space<kLds>::cdptr Ain, double (&x)[R],
       double h = pick(hi, i), l = pick(lo, i);
       if (!nrm) { h = h * xN; l = l * xN; }
       double nx = pick(r, i) + pick(diag, i) * pick(xs, i);
-      const double t = nx < l ? l : nx;
-      nx = nx > h ? h : t;
+      if constexpr (kExact) {
+        const double t = nx < l ? l : nx;
+        nx = nx > h ? h : t;
+      } else {
+        nx = fmin(fmax(nx, l), h);
+      }
       const double dx = rdl(nx - pick(xs, i), i & 63);
       if (nrm) xN = rdl(nx, i & 63);
       setR(xn, i, lane, nx);
@@ -330,6 +362,13 @@ __device__ bool wavePgsR(int n, typename Space<kLds>::cdptr Ain, double (&x)[R],
 #ifdef LCP_PROFILE
   if (dbg && lane == 0) dbg[4] = (double)((long long)__builtin_amdgcn_s_memtime() - tp2);
 #endif
+  if constexpr (!kExact) {
+    if (contactRows && nonFinite(r, xn)) {
+#pragma unroll
+      for (int s = 0; s < R; s++) x[s] = xEntry[s];
+      return wavePgsR<kLds, kMapped, R, true>(n, Ain, x, bIn, lo, hi, findex, lane, dbg, shift, cancel, ld, idxIn);
+    }
+  }
 #pragma unroll
   for (int s = 0; s < R; s++) x[s] = xn[s];
   return possible;

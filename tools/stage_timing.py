@@ -29,12 +29,12 @@ n = w.getNumDofs()
 from nimblephysics_amd import _native  # noqa: E402
 ws = _native.snapshot_layout(n, timing=True)["stamps"]  # csrc/pool_sizes.h snStamps(n)
 for it in range(4):
-    snap[:, ws:ws + 100] = 0
+    snap[:, ws:ws + 110] = 0
     prev_state, prev_cache = state.clone(), cache.clone()
     dev.forward(state, action, cache, nxt, snap, s)
     torch.cuda.synchronize()
     state = nxt.clone()
-    T = snap[:, ws:ws + 100].cpu().numpy()
+    T = snap[:, ws:ws + 110].cpu().numpy()
     hd = snap[:, :8].cpu().numpy()
     names = {(10, 14): " kinematics", (14, 15): " composites", (15, 16): " CRBA + bias", (16, 17): " cholesky", (17, 11): " dynamics cache store",
              (70, 71): "  kin: local transforms", (71, 72): "  kin: tree compose", (72, 73): "  kin: motion subspace",
@@ -65,9 +65,12 @@ for it in range(4):
         if T[wi, 94] > 0:
             a0 = T[wi, 3]
             who = {0: "-", 1: "wave0", 2: "helper"}
-            print("      board (clk from A built): construct done %d, helper Dantzig %d..%d (%d pivots, %s), answer at %d; PGS fallback %s, frictionless %s"
+            rel = lambda k: int(T[wi, k] - a0) if T[wi, k] > 0 else -1  # noqa: E731
+            print("      board (clk from A built): construct done %d, helper Dantzig %d..%d (%d pivots, %s), answer at %d; "
+                  "PGS fallback %s %d..%d, frictionless %s %d..%d"
                   % (T[wi, 5] - a0, T[wi, 94] - a0, T[wi, 95] - a0, T[wi, 99], {1: "ok", 2: "failed"}.get(int(T[wi, 96]), "?"),
-                     T[wi, 6] - a0, who.get(int(T[wi, 97]), "?"), who.get(int(T[wi, 98]), "?")))
+                     T[wi, 6] - a0, who.get(int(T[wi, 97]), "?"), rel(100), rel(101), who.get(int(T[wi, 98]), "?"),
+                     rel(102), rel(103)))
         print(f"  world {wi}: pivots {int(T[wi,52])} at row {int(T[wi,53])} pgs-sweeps {int(T[wi,54])} ign {hd[wi,7]:.0f} total {int(tot[wi])} rows {int(hd[wi,1])} clamp {int(hd[wi,2])} flag {hd[wi,4]:.0f} | " + " ".join(parts))
 
 # the slowest world of the last step re-run alone (one wave on the GPU): how

@@ -213,7 +213,11 @@ __device__ bool wavePgsR(int n, typename Space<kLds>::cdptr Ain, double (&x)[R],
         nx = fmin(fmax(nx, l), h);
       }
       const double dx = rdl(nx - xs0, i & 63);
-      if (nrm) xN = rdl(nx, i & 63);
+      {
+        // (unconditional readlane, scalar select: no branch per row)
+        const double xi = rdl(nx, i & 63);
+        xN = nrm ? xi : xN;
+      }
       setR(xn, i, lane, nx);
 #pragma unroll
       for (int s = 0; s < R; s++) r[s] -= (cur[s] * act1[s]) * dx;
@@ -316,7 +320,11 @@ __device__ bool wavePgsR(int n, typename Space<kLds>::cdptr Ain, double (&x)[R],
         nx = fmin(fmax(nx, l), h);
       }
       const double dx = rdl(nx - pick(xs, i), i & 63);
-      if (nrm) xN = rdl(nx, i & 63);
+      {
+        // (unconditional readlane, scalar select: no branch per row)
+        const double xi = rdl(nx, i & 63);
+        xN = nrm ? xi : xN;
+      }
       setR(xn, i, lane, nx);
 #pragma unroll
       for (int s = 0; s < R; s++) r[s] -= (cur[s] * dummyAct[s]) * dx;

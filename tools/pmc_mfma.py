@@ -15,6 +15,9 @@ import os
 import sys
 
 SIMDS = 256 * 4
+# rocprofv3 reports GRBM_GUI_ACTIVE summed over the 8 XCDs (6.75M for a
+# 349.5 us launch = 8 x 2.4 GHz); MfmaUtil takes the per-XCD (max) value
+XCDS = 8
 PEAK_FP64_MFMA_TFLOPS = 78.6  # MI355X dense fp64 matrix rate (MI355X_MICROARCH.md)
 
 
@@ -44,8 +47,8 @@ def main():
              "mfma_tflops": flops / (ns * 1e-9) / 1e12 if ns else None}
         e["mfma_frac_of_fp64_matrix_peak"] = e["mfma_tflops"] / PEAK_FP64_MFMA_TFLOPS if ns else None
         if gui > 0:
-            e["grbm_gui_active"] = gui
-            e["mfma_util"] = busy / (gui * SIMDS)
+            e["grbm_gui_active_per_xcd"] = gui / XCDS
+            e["mfma_util"] = busy / (gui / XCDS * SIMDS)
         res[k] = e
     allw = json.load(open(out)) if os.path.exists(out) else {}
     allw[wl] = res

@@ -30,8 +30,18 @@ __device__ __forceinline__ void choleskyLds(double* A, double* dinv, int n, int 
     if (lane >= j && lane < n) {
       const int ri = tri(lane, 0), rj = tri(j, 0);
       sum = A[ri + j];
-#pragma unroll 8
-      for (int k = 0; k < j; k++) sum -= A[ri + k] * A[rj + k];
+      // blocks of 8: the sixteen loads issued before the multiply-adds
+      int k = 0;
+      for (; k + 8 <= j; k += 8) {
+        double a[8], c[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) { a[u] = A[ri + k + u]; c[u] = A[rj + k + u]; }
+#pragma unroll
+        for (int u = 0; u < 8; u++) asm volatile("" : "+v"(a[u]), "+v"(c[u]));
+#pragma unroll
+        for (int u = 0; u < 8; u++) sum -= a[u] * c[u];
+      }
+      for (; k < j; k++) sum -= A[ri + k] * A[rj + k];
     }
     const double ajj = rdl(sum, j);
     const double y = rsqrtRefined(ajj);

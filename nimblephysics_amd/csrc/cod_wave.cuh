@@ -349,8 +349,18 @@ rankAndRz:
     if (vnz != 0) {
       for (int row = lane; row <= i; row += WAVE) {
         double sc = A[row * ld + i] * vi;
-#pragma unroll 4
-        for (int j = r; j < n; j++) sc += A[row * ld + j] * A[i * ld + j];
+        // blocks of 4: the eight loads issued before the multiply-adds
+        int j = r;
+        for (; j + 4 <= n; j += 4) {
+          double a[4], c[4];
+#pragma unroll
+          for (int u = 0; u < 4; u++) { a[u] = A[row * ld + j + u]; c[u] = A[i * ld + j + u]; }
+#pragma unroll
+          for (int u = 0; u < 4; u++) asm volatile("" : "+v"(a[u]), "+v"(c[u]));
+#pragma unroll
+          for (int u = 0; u < 4; u++) sc += a[u] * c[u];
+        }
+        for (; j < n; j++) sc += A[row * ld + j] * A[i * ld + j];
         sc = 2 * sc / vnz;
         A[row * ld + i] -= sc * vi;
         if (row < i)

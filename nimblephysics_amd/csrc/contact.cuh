@@ -1518,6 +1518,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
     P.b[r] = -acc;
   }
   WSYNC();
+  STAMP(86);
   {
     // Y = L^-1 J^T by columns (lane = column j): element (i, j) receives
     // -L_ik Y_kj for k = 0 .. i-1 in order and is then scaled by 1/L_ii --
@@ -1525,20 +1526,39 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
     // its two barriers per row.  (Eight columns per pass held in registers
     // with lane = dof row, readlane-broadcast like cholSolveReg, measured
     // 1.5x slower here.)
+    // The L and Y operands of each 8-step block are loaded together before
+    // its multiply-adds (LDS latency once per block; left to the scheduler,
+    // every multiply-add waited on its own two loads: ~55k clocks for the
+    // Atlas LCP).  Same operations in the same order.
     double* Y = P.massed;
     for (int j = lane; j < m; j += WAVE) {
       for (int i = 0; i < n; i++) {
         double acc = Y[i * m + j];
         const double* Li = Lm + tri(i, 0);
-#pragma unroll 8
-        for (int k = 0; k < i; k++) acc -= Li[k] * Y[k * m + j];
+        int k = 0;
+        for (; k + 8 <= i; k += 8) {
+          double lv[8], yv[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) {
+            lv[u] = Li[k + u];
+            yv[u] = Y[(k + u) * m + j];
+          }
+          // (all sixteen issued before any is consumed)
+#pragma unroll
+          for (int u = 0; u < 8; u++) asm volatile("" : "+v"(lv[u]), "+v"(yv[u]));
+#pragma unroll
+          for (int u = 0; u < 8; u++) acc -= lv[u] * yv[u];
+        }
+        for (; k < i; k++) acc -= Li[k] * Y[k * m + j];
         Y[i * m + j] = acc * s[L.dinv + i];
       }
     }
     WSYNC();
+    STAMP(87);
     // A = Y^T Y on the matrix cores (the LCP matrix J Minv J^T)
     gramMfma(Y, P.A, n, m, lane);
     WSYNC();
+    STAMP(88);
   }
 
   // penetration correction / restitution bounce of the normal rows (lane = row)

@@ -615,14 +615,22 @@ struct WaveDantzig {
     }
     for (int k0 = 0; k0 < m; k0 += 8) {
       double Lk[R][8];
+      double Lv[R][8];
 #pragma unroll
       for (int s = 0; s < R; s++)
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-          double v = L[rowOffL[s] + (k0 + u < m ? k0 + u : 0)];
-          asm volatile("" : "+v"(v));  // keep the load unconditional (batched)
-          Lk[s][u] = (row(s) > k0 + u && row(s) < m) ? v : 0.0;
-        }
+        for (int u = 0; u < 8; u++) Lv[s][u] = L[rowOffL[s] + (k0 + u < m ? k0 + u : 0)];
+      // keep the loads unconditional and batched: all issued before any is
+      // consumed (one barrier per block -- a barrier per load made the
+      // wave wait for each load in turn)
+#pragma unroll
+      for (int s = 0; s < R; s++)
+#pragma unroll
+        for (int u = 0; u < 8; u++) asm volatile("" : "+v"(Lv[s][u]));
+#pragma unroll
+      for (int s = 0; s < R; s++)
+#pragma unroll
+        for (int u = 0; u < 8; u++) Lk[s][u] = (row(s) > k0 + u && row(s) < m) ? Lv[s][u] : 0.0;
 #pragma unroll
       for (int u = 0; u < 8; u++)
         if (k0 + u < m) {
@@ -659,14 +667,19 @@ struct WaveDantzig {
     }
     for (int k0 = m - 1; k0 >= 0; k0 -= 8) {
       double Lk[R][8];
+      double Lv[R][8];
 #pragma unroll
       for (int s = 0; s < R; s++)
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-          double v = L[(k0 - u >= 0 ? k0 - u : 0) * ldL + colL[s]];
-          asm volatile("" : "+v"(v));
-          Lk[s][u] = row(s) < k0 - u ? v : 0.0;
-        }
+        for (int u = 0; u < 8; u++) Lv[s][u] = L[(k0 - u >= 0 ? k0 - u : 0) * ldL + colL[s]];
+#pragma unroll
+      for (int s = 0; s < R; s++)
+#pragma unroll
+        for (int u = 0; u < 8; u++) asm volatile("" : "+v"(Lv[s][u]));
+#pragma unroll
+      for (int s = 0; s < R; s++)
+#pragma unroll
+        for (int u = 0; u < 8; u++) Lk[s][u] = row(s) < k0 - u ? Lv[s][u] : 0.0;
 #pragma unroll
       for (int u = 0; u < 8; u++)
         if (k0 - u >= 0) {

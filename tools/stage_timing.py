@@ -43,7 +43,8 @@ for it in range(4):
              (42, 43): " c1: COD solve", (43, 44): " c1: nx + valid", (45, 46): " pre: Ac/AcubE",
              (46, 47): " pre: MA/MAc backsub", (47, 48): " pre: Q", (48, 49): " pre: COD", (49, 50): " pre: pinv",
              (50, 51): " pre: imp", (11, 12): "solve v1", (0, 1): "collide", (1, 2): "rows",
-             (2, 3): "cols/massed/A/b", (3, 4): "warm start/guess", (4, 5): "construct 1",
+             (2, 3): "cols/massed/A/b", (2, 86): " b = -J v1", (86, 87): " Y = L^-1 J^T", (87, 88): " A = Y^T Y (MFMA)",
+             (88, 3): " pen / aCol", (3, 4): "warm start/guess", (4, 5): "construct 1",
              (5, 6): "dantzig", (6, 7): "pgs/fallbacks", (7, 8): "construct 2", (8, 9): "impulses/snapshot",
              (12, 13): "contact stage total+integrate"}
     print(f"--- step {it}: contact worlds {int((hd[:,0]>0).sum())}, short-circuit {int(hd[:,6].sum())}, "

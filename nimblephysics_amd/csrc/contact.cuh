@@ -1531,33 +1531,6 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
     // every multiply-add waited on its own two loads: ~55k clocks for the
     // Atlas LCP).  Same operations in the same order.
     double* Y = P.massed;
-    if (m <= 32) {
-      // two lanes per column (lane j and j + 32): each sums half of row i's
-      // dot product (k even / odd), the halves meet through a lane swap --
-      // half the dependent multiply-add chain of the one-lane form below
-      const int j = lane & 31, half = lane >> 5;
-      const bool col = j < m;
-      const int jj = col ? j : 0;
-      for (int i = 0; i < n; i++) {
-        const double* Li = Lm + tri(i, 0);
-        double part = 0.0;
-        int k = half;
-        for (; k + 14 < i; k += 16) {
-          double lv[8], yv[8];
-#pragma unroll
-          for (int u = 0; u < 8; u++) { lv[u] = Li[k + 2 * u]; yv[u] = Y[(k + 2 * u) * m + jj]; }
-#pragma unroll
-          for (int u = 0; u < 8; u++) asm volatile("" : "+v"(lv[u]), "+v"(yv[u]));
-#pragma unroll
-          for (int u = 0; u < 8; u++) part += lv[u] * yv[u];
-        }
-        for (; k < i; k += 2) part += Li[k] * Y[k * m + jj];
-        const double other = __shfl_xor(part, 32);
-        const double yij = (Y[i * m + jj] - (half ? other + part : part + other)) * s[L.dinv + i];
-        if (col && half == 0) Y[i * m + j] = yij;
-        WSYNC();
-      }
-    } else
     for (int j = lane; j < m; j += WAVE) {
       for (int i = 0; i < n; i++) {
         double acc = Y[i * m + j];

@@ -79,6 +79,40 @@ def test_lcp_wave_kernels_r1_r2():
         assert np.abs(xc - ref).max() <= 1e-8 * np.abs(ref).max(), m
 
 
+def test_pgs_fast_clamp_matches_reference_chain():
+    """The PGS fallback on contact-layout rows clamps with v_max / v_min
+    (lcp_wave.cuh wavePgsR) and re-runs with the reference's
+    compare-and-assign chain when a residual ends non-finite: against the
+    oracle's PgsBoxedLcpSolver::solve restatement (A + 1e-4 I, x0 = 0) on
+    contact-layout problems, one of them with a NaN in b."""
+    exe = wave_emu.build("lcp_wave_emu")
+    probs = _problems((12, 24, 40, 66), seed=5)
+    m, A, b, lo, hi, fi = probs[1]
+    b = b.copy()
+    b[4] = np.nan
+    probs.append((m, A, b, lo, hi, fi))
+    txt = [str(len(probs))]
+    for m, A, b, lo, hi, fi in probs:
+        txt += [str(m), wave_emu._fmt(A), wave_emu._fmt(b), wave_emu._fmt(lo), wave_emu._fmt(hi),
+                wave_emu._fmt(fi, True), wave_emu._fmt(np.zeros(m))]
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")
+    r = subprocess.run([exe], input="\n".join(txt), capture_output=True, text=True, timeout=900, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    out = iter(ln.split() for ln in r.stdout.splitlines())
+    for k, (m, A, b, lo, hi, fi) in enumerate(probs):
+        lines = [next(out)] + ([next(out)] if m <= 64 else [])  # R = 1 (m <= 64), then R = 2
+        ok_ref, x_ref = O.pgs(A + 1e-4 * np.eye(m), np.zeros(m), b, lo, hi, fi)
+        for t in lines:
+            assert int(t[1]) == m
+            okp = bool(int(t[3 + m]))
+            xp = np.array(t[4 + m:4 + 2 * m], dtype=float)
+            assert okp == ok_ref, (k, t[0], okp, ok_ref)
+            assert np.array_equal(np.isnan(xp), np.isnan(x_ref)), (k, t[0])
+            fin = ~np.isnan(x_ref)
+            err = np.abs(xp[fin] - x_ref[fin]).max(initial=0.0)
+            assert err <= 1e-9 * max(1.0, np.abs(x_ref[fin]).max(initial=0.0)), (k, t[0], err)
+
+
 @pytest.mark.parametrize("defer", [None, "0"])
 def test_box_step_emulated(defer):
     world = models.box_world()

@@ -50,6 +50,18 @@
 // six on the sweep's critical path.  A NaN anywhere leaves a non-finite
 // residual behind (maxNum would otherwise swallow it), so a solve that ends
 // with one is re-run from its inputs with the reference's chain (kExact).
+// The box scale of a contact-layout row: 1 for a normal row, x_N (its
+// normal's newest x) for a friction row, selected on the scalar unit, so the
+// row's box is one multiply (hi * 1 = hi exactly) instead of a multiply, a
+// per-lane select and the canonicalisation fmin / fmax need for a selected
+// operand, all on the sweep's dependent chain.  (Opaque to the optimiser,
+// which would otherwise fold x * (c ? 1 : y) back into c ? x : x * y.)
+__device__ __forceinline__ double boxScale(bool normal, double xN) {
+  double sc = normal ? 1.0 : xN;
+  asm("" : "+s"(sc));
+  return sc;
+}
+
 template <bool kLds, bool kMapped, int R, bool kExact = false>
 __device__ bool wavePgsR(int n, typename Space<kLds>::cdptr Ain, double (&x)[R], const double (&bIn)[R],
                          const double (&lo)[R], const double (&hi)[R], const int (&findex)[R], int lane,
@@ -202,8 +214,8 @@ __device__ bool wavePgsR(int n, typename Space<kLds>::cdptr Ain, double (&x)[R],
     // x_N is only consumed by VALU multiplies, never by SALU)
     auto row1c = [&](int i, const double (&cur)[R]) {
       const bool nrm = bitR(normals, i);
-      double h = pick(hi, i), l = pick(lo, i);
-      if (!nrm) { h = h * xN; l = l * xN; }
+      const double sc = boxScale(nrm, xN);
+      const double h = pick(hi, i) * sc, l = pick(lo, i) * sc;
       const double rr = pick(r, i), xs0 = pick(x0, i), dg = pick(diagRaw, i);
       double nx = (rr + dg * xs0) / dg;
       if constexpr (kExact) {
@@ -310,8 +322,8 @@ __device__ bool wavePgsR(int n, typename Space<kLds>::cdptr Ain, double (&x)[R],
     double xN = 0.0;
     auto rowc = [&](int i, const double (&cur)[R]) {
       const bool nrm = bitR(normals, i);
-      double h = pick(hi, i), l = pick(lo, i);
-      if (!nrm) { h = h * xN; l = l * xN; }
+      const double sc = boxScale(nrm, xN);
+      const double h = pick(hi, i) * sc, l = pick(lo, i) * sc;
       double nx = pick(r, i) + pick(diag, i) * pick(xs, i);
       if constexpr (kExact) {
         const double t = nx < l ? l : nx;

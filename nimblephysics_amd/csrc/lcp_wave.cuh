@@ -58,7 +58,7 @@
 // which would otherwise fold x * (c ? 1 : y) back into c ? x : x * y.)
 __device__ __forceinline__ double boxScale(bool normal, double xN) {
   double sc = normal ? 1.0 : xN;
-  asm("" : "+s"(sc));
+  NIMBLE_OPAQUE_SGPR(sc);
   return sc;
 }
 

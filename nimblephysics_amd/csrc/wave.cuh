@@ -34,6 +34,14 @@ __device__ __forceinline__ double unid(double v) {
   return __hiloint2double(hi, lo);
 }
 
+// Hides a wave-uniform value from the optimiser (an empty asm that pins it
+// in an SGPR pair), so an algebraic form chosen for the ISA is not folded
+// back.  The host emulator of the kernels (tests/cpp/wave_emu) defines it
+// away.
+#ifndef NIMBLE_OPAQUE_SGPR
+#define NIMBLE_OPAQUE_SGPR(x) asm("" : "+s"(x))
+#endif
+
 template <int CTRL>
 __device__ __forceinline__ double dppd(double v) {
   const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);

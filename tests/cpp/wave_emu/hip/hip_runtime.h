@@ -35,6 +35,7 @@ using std::sqrt;
 #define __forceinline__ inline
 #define __noinline__ __attribute__((noinline))
 #define __launch_bounds__(...)
+#define NIMBLE_OPAQUE_SGPR(x) ((void)(x))
 #define amdgpu_waves_per_eu(...) unused
 
 struct dim3 {

@@ -241,7 +241,16 @@ def _cpu_threads():
         n = os.cpu_count() or 1
     # the GPU box's CPU share is 16 cores per GPU (os.cpu_count() shows the
     # whole machine there)
-    return max(1, min(n, 16))
+    return max(1, min(n, 16)), n
+
+
+def _host_cores():
+    """(os.cpu_count(), this process's affinity size)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = None
+    return os.cpu_count(), aff
 
 
 def cpu_baseline(make, batch, sampler, seconds_target=12.0):
@@ -251,7 +260,8 @@ def cpu_baseline(make, batch, sampler, seconds_target=12.0):
     ~seconds_target (ctypes releases the GIL inside the C library)."""
     import threading
     from oracle.oracle import OracleWorld
-    threads = _cpu_threads()
+    threads, usable = _cpu_threads()
+    host_cpus, affinity = _host_cores()
     counts = [0] * threads
     stop = [False]
 
@@ -277,8 +287,56 @@ def cpu_baseline(make, batch, sampler, seconds_target=12.0):
     dt = time.perf_counter() - t0
     steps = sum(counts)
     return {"value": steps * batch / dt, "unit": "timesteps/s", "cores": threads, "kind": "port",
+            "host_cpu_count": host_cpus, "affinity_cpus": affinity,
+            "cores_note": "threads used = min(affinity, 16): the GPU box's CPU share is 16 cores per GPU, while "
+                          "os.cpu_count() there shows the whole machine",
             "sample": f"{steps} fwd+bwd steps x {batch} worlds of the same workload, oracle/liboracle.so "
                       f"(CPU restatement of the reference's step), {threads} threads, {dt:.1f}s"}
+
+
+def measure(wl, batch, steps, warmup, dist, rank, ws, dev, gather):
+    """Time `steps` bench steps (after `warmup`) of workload `wl` on this
+    rank's `batch` worlds; returns the measured numbers (value = worlds x
+    steps x ranks / max-over-ranks elapsed)."""
+    wl_name, make, sampler, metric, default_batch = WORKLOADS[wl]
+    batch = batch if batch > 0 else default_batch
+    world = make()
+    # status words are recorded on the device each step (no per-step host
+    # sync) and checked once after the timed region: a world whose step could
+    # not be the reference's fails the bench instead of being timed
+    world.setStatusPolicy("record")
+    n = world.getNumDofs()
+    st, f, g = rank_inputs(world, sampler, batch, rank)
+    state = torch.tensor(st, device=dev)
+    action = torch.tensor(f, device=dev)
+    g = torch.tensor(g, device=dev)
+    state0 = state.clone()
+    devworld = world.native()
+    timer = KernelTimer()
+    timer.wrap(devworld)
+    status_acc = torch.zeros(batch, dtype=torch.int32, device=dev)
+    one_step = make_step(nimble.timestep, world, action, g, gather, dist, ws, status_acc)
+    for _ in range(warmup):
+        state = one_step(state)
+    timer.enabled = True
+    state, elapsed = timed_loop(one_step, state, steps, 0, dist, dev)
+    timer.enabled = False
+    bad = int(((status_acc & _native.ST_DIVERGES) != 0).sum().item())
+    if bad:
+        raise SystemExit(f"bench ({wl}): {bad} world(s) left the reference's physics "
+                         f"({_native.status_message(int(np.bitwise_or.reduce(status_acc.cpu().numpy())))})")
+    cstats = rollout_stats(world, state0, action, warmup, steps)
+    fwd_ms = timer.mean_ms(timer.fwd)
+    bwd_ms = timer.mean_ms(timer.bwd)
+    flops = _native.flop_estimate(world, cstats["rows"], cstats["clamping"])
+    dom = "backward" if bwd_ms >= fwd_ms else "forward"
+    dom_ms = max(bwd_ms, fwd_ms)
+    achieved = flops[dom] * batch / (dom_ms * 1e-3) / 1e12
+    traffic, traffic_src = pmc_traffic(wl, f"nimble_{dom}_kernel", batch)
+    return {"wl": wl, "wl_name": wl_name, "metric": metric, "make": make, "sampler": sampler, "batch": batch, "n": n,
+            "value": batch * ws * steps / elapsed, "ms_per_step": elapsed / steps * 1e3, "cstats": cstats,
+            "fwd_ms": fwd_ms, "bwd_ms": bwd_ms, "dom": dom, "achieved": achieved, "flops": flops,
+            "traffic": traffic, "traffic_src": traffic_src}
 
 
 def main():
@@ -289,6 +347,8 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="worlds per GPU (default: the workload's)")
     ap.add_argument("--workload", default="atlas", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-mesh", action="store_true",
+                    help="skip the second measurement of the reference atlas_bench's STL-mesh Atlas")
     ap.add_argument("--gather-grads", type=int, default=-1,
                     help="all-gather action gradients each step (default: on when N > 1)")
     args = ap.parse_args()
@@ -296,64 +356,33 @@ def main():
     dist, rank, ws, local = init_dist()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    wl_name, make, sampler, metric, default_batch = WORKLOADS[args.workload]
-    if args.batch <= 0:
-        args.batch = default_batch
-    world = make()
-    # status words are recorded on the device each step (no per-step host
-    # sync) and checked once after the timed region: a world whose step could
-    # not be the reference's fails the bench instead of being timed
-    world.setStatusPolicy("record")
-    n = world.getNumDofs()
-    st, f, g = rank_inputs(world, sampler, args.batch, rank)
-    state = torch.tensor(st, device=dev)
-    action = torch.tensor(f, device=dev)
-    g = torch.tensor(g, device=dev)
-    state0 = state.clone()
-    devworld = world.native()
-    timer = KernelTimer()
-    timer.wrap(devworld)
-
     gather = (ws > 1) if args.gather_grads < 0 else bool(args.gather_grads)
-
-    status_acc = torch.zeros(args.batch, dtype=torch.int32, device=dev)
-    one_step = make_step(nimble.timestep, world, action, g, gather, dist, ws, status_acc)
-
-    for _ in range(args.warmup):
-        state = one_step(state)
-    timer.enabled = True
-    state, elapsed = timed_loop(one_step, state, args.steps, 0, dist, dev)
-    timer.enabled = False
-    bad = int(((status_acc & _native.ST_DIVERGES) != 0).sum().item())
-    if bad:
-        raise SystemExit(f"bench: {bad} world(s) left the reference's physics ({_native.status_message(int(np.bitwise_or.reduce(status_acc.cpu().numpy())))})")
-    cstats = rollout_stats(world, state0, action, args.warmup, args.steps)
-    total = args.batch * ws * args.steps
-    value = total / elapsed
-    fwd_ms = timer.mean_ms(timer.fwd)
-    bwd_ms = timer.mean_ms(timer.bwd)
-    flops = _native.flop_estimate(world, cstats["rows"], cstats["clamping"])
-    dom = "backward" if bwd_ms >= fwd_ms else "forward"
-    dom_ms = max(bwd_ms, fwd_ms)
-    achieved = flops[dom] * args.batch / (dom_ms * 1e-3) / 1e12
-    traffic, traffic_src = pmc_traffic(args.workload, f"nimble_{dom}_kernel", args.batch)
+    r = measure(args.workload, args.batch, args.steps, args.warmup, dist, rank, ws, dev, gather)
+    # the reference atlas_bench's own model (atlas_v3_no_head.urdf, 29 STL
+    # colliders), measured after the headline's timed region on the same
+    # ranks: reported beside the headline, never as `value`
+    mesh = None
+    if args.workload == "atlas" and not args.no_mesh:
+        mesh = measure("atlas_mesh", args.batch, min(args.steps, 20), min(args.warmup, 3), dist, rank, ws, dev, gather)
     if rank == 0:
+        cstats, flops, dom = r["cstats"], r["flops"], r["dom"]
+        achieved = r["achieved"]
         out = {
-            "metric": metric,
-            "value": value, "unit": "timesteps/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "metric": r["metric"],
+            "value": r["value"], "unit": "timesteps/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": r["ms_per_step"], "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (perturbed poses near / in ground contact, random torques)",
-            "config": {"workload": wl_name, "worlds_per_gpu": args.batch, "dofs": n,
-                       "global_batch": args.batch * ws,
+            "config": {"workload": r["wl_name"], "worlds_per_gpu": r["batch"], "dofs": r["n"],
+                       "global_batch": r["batch"] * ws,
                        "parallelism": f"independent worlds x{ws}" + (" + RCCL all-gather of action grads" if gather else ""),
                        "contacts_per_world": cstats["contacts"], "lcp_rows_per_world": cstats["rows"],
                        "clamping_rows_per_world": cstats["clamping"],
                        "worlds_in_contact": cstats["worlds_in_contact"], "contact_stats_source": cstats["source"]},
-            "kernels_ms": {"forward": fwd_ms, "backward": bwd_ms},
+            "kernels_ms": {"forward": r["fwd_ms"], "backward": r["bwd_ms"]},
             "roofline": {"bound": "fp64-valu", "kernel": f"nimble_{dom}_kernel", "achieved": achieved,
                          "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP64_VECTOR_PEAK_TFLOPS,
-                         "traffic": traffic, "traffic_source": traffic_src,
+                         "traffic": r["traffic"], "traffic_source": r["traffic_src"],
                          **pmc_mfma(args.workload, f"nimble_{dom}_kernel"),
                          "flops_per_world": flops[dom],
                          "note": "peak = MI355X fp64 vector (VALU) rate, which on MI355X equals the fp64 "
@@ -362,8 +391,20 @@ def main():
                                  "launch (2 x FETCH_SIZE + WRITE_SIZE, separate rocprofv3 --pmc passes) from the "
                                  "committed summary profiles/pmc_traffic.json (tools/gpu_measure.sh)"},
         }
+        if mesh is not None:
+            mf = mesh["flops"]
+            out["atlas_mesh"] = {
+                "workload": mesh["wl_name"], "metric": mesh["metric"], "value": mesh["value"], "unit": "timesteps/s",
+                "ms_per_step": mesh["ms_per_step"], "steps": min(args.steps, 20),
+                "kernels_ms": {"forward": mesh["fwd_ms"], "backward": mesh["bwd_ms"],
+                               "note": "forward = nimble_forward_kernel + nimble_forward_wide_kernel (the > 64-row "
+                                       "worlds), backward likewise; per-kernel split in profiles/*kernel_stats_atlas_mesh*"},
+                "contacts_per_world": mesh["cstats"]["contacts"], "lcp_rows_per_world": mesh["cstats"]["rows"],
+                "clamping_rows_per_world": mesh["cstats"]["clamping"],
+                "frac": mesh["achieved"] / FP64_VECTOR_PEAK_TFLOPS, "frac_kernel": f"nimble_{mesh['dom']}_kernel",
+                "flops_per_world": mf[mesh["dom"]], "traffic": mesh["traffic"], "traffic_source": mesh["traffic_src"]}
         if not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(make, 16, sampler)
+            out["cpu_baseline"] = cpu_baseline(r["make"], 16, r["sampler"])
         print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()

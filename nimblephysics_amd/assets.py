@@ -84,6 +84,7 @@ def skeleton_from_dict(d: dict) -> dyn.Skeleton:
                 shape = dyn.MeshShape(sd["size"], np.array(sd["vertices"]), sd.get("mesh", ""))
                 if "candidate" in sd:
                     shape._candidate = np.asarray(sd["candidate"], dtype=np.int32)
+                    shape._candidate_size = np.asarray(sd["size"], dtype=np.float64).copy()
             else:
                 shape = dyn.SphereShape(sd["size"][0])
             node = b.createShapeNode(shape, collision=True)

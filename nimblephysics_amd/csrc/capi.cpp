@@ -257,6 +257,10 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
       }
       m.meshCount[sIdx] = (int)(mv.size() / 3) - m.meshFirst[sIdx];
       m.meshRadius[sIdx] = std::sqrt(r2);
+      if (m.meshCount[sIdx] <= 0) {
+        delete w;
+        return fail(NIMBLE_ERR_INVALID, "mesh_vertex_candidate filters out every vertex of a mesh shape");
+      }
     }
     if (!mv.empty()) {
       hipError_t e = hipMalloc(&w->meshDev, mv.size() * sizeof(double));

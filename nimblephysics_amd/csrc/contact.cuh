@@ -459,13 +459,17 @@ __device__ __forceinline__ int helperState(double* ct) {
   return uni(__hip_atomic_load(helperFlags(ct), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
 }
 // spin with s_sleep until pred(state); bounded so that a protocol error
-// traps rather than hanging the device
+// traps rather than hanging the device.  The bound (2^30 polls of at least
+// s_sleep(1) = 64 clocks: > 30 s at 2.4 GHz) is four orders of magnitude above
+// the slowest world's whole step (~1M clocks, profiling and CU contention
+// included), so only a deadlock reaches it, never a slow but live partner.
+constexpr long long kSpinBound = 1ll << 30;
 template <class Pred>
 __device__ __forceinline__ int helperWait(double* ct, Pred pred) {
   for (long long it = 0;; it++) {
     const int st = helperState(ct);
     if (pred(st)) return st;
-    if (it > (1ll << 24)) __builtin_trap();
+    if (it > kSpinBound) __builtin_trap();
     __builtin_amdgcn_s_sleep(1);
   }
 }
@@ -504,7 +508,7 @@ __device__ __forceinline__ void collidePost(double* ct, int state, int lane) {
 __device__ __forceinline__ void collideWait(double* ct, int want) {
   for (long long it = 0;; it++) {
     if (uni(__hip_atomic_load(collideFlag(ct), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == want) return;
-    if (it > (1ll << 24)) __builtin_trap();
+    if (it > kSpinBound) __builtin_trap();
     __builtin_amdgcn_s_sleep(1);
   }
 }
@@ -977,7 +981,7 @@ __device__ bool devConstruct(typename Space<kLds>::dptr poolIn, int m, int n, do
     TACC_BEGIN(tF);
 #ifdef NIMBLE_STAGE_TIMING
     codFactorAny<kLds, R>(sp<kLds>(Q), sp<kLds>(P.scr), nc, nc, nc, sp<kLds>(vv), lane, stage, stageCap,
-                          g_stamp ? g_stamp + 67 : nullptr);
+                          g_stamp ? g_stamp + SLOT_COD : nullptr);
 #else
     codFactorAny<kLds, R>(sp<kLds>(Q), sp<kLds>(P.scr), nc, nc, nc, sp<kLds>(vv), lane, stage, stageCap);
 #endif
@@ -1618,7 +1622,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   STAMP(4);
 #ifdef NIMBLE_STAGE_TIMING
   bool success = devConstruct<kLds, R>(poolIn, m, n, 0.0, false, sp<true>(ct), lane, g_stamp, stage, stageCap);
-  double* dbgPgs = g_stamp + 54;
+  double* dbgPgs = g_stamp ? g_stamp + SLOT_PGS : nullptr;
 #else
   bool success = devConstruct<kLds, R>(poolIn, m, n, 0.0, false, sp<true>(ct), lane, nullptr, stage, stageCap);
   double* dbgPgs = nullptr;
@@ -1685,7 +1689,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
         if (d >= 2 && pst == 2 && boardGet(ct, BD_F) == 1) { boardSrc = 2; break; }
         if (pst == 0 && boardClaim(ct, BD_PCLAIM, 1, lane)) {
 #ifdef NIMBLE_STAGE_TIMING
-          if (lane == 0) { g_stamp[97] = 1; g_stamp[100] = (double)__builtin_amdgcn_s_memtime(); }
+          if (lane == 0 && g_stamp) { g_stamp[97] = 1; g_stamp[100] = (double)__builtin_amdgcn_s_memtime(); }
 #endif
           bool dup;
           double xp[R];
@@ -1698,13 +1702,13 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
           if (okp) boardSet(ct, BD_STOPF, 1, lane);
           boardSet(ct, BD_P, okp ? 1 : 2, lane);
 #ifdef NIMBLE_STAGE_TIMING
-          if (lane == 0) g_stamp[101] = (double)__builtin_amdgcn_s_memtime();
+          if (lane == 0 && g_stamp) g_stamp[101] = (double)__builtin_amdgcn_s_memtime();
 #endif
           continue;
         }
         if (pst != 1 && boardGet(ct, BD_F) == 0 && boardClaim(ct, BD_FCLAIM, 1, lane)) {
 #ifdef NIMBLE_STAGE_TIMING
-          if (lane == 0) { g_stamp[98] = 1; g_stamp[102] = (double)__builtin_amdgcn_s_memtime(); }
+          if (lane == 0 && g_stamp) { g_stamp[98] = 1; g_stamp[102] = (double)__builtin_amdgcn_s_memtime(); }
 #endif
           double xf[R];
           frictionlessPgsR<kLds, R>(P.A, P.b, P.lo, P.hi, m, md.fallbackCfm, fiR, lane, xf, board(ct) + BD_STOPF);
@@ -1713,11 +1717,11 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
             if (rowAt(q, lane) < m) P.xf[rowAt(q, lane)] = xf[q];
           boardSet(ct, BD_F, 1, lane);
 #ifdef NIMBLE_STAGE_TIMING
-          if (lane == 0) g_stamp[103] = (double)__builtin_amdgcn_s_memtime();
+          if (lane == 0 && g_stamp) g_stamp[103] = (double)__builtin_amdgcn_s_memtime();
 #endif
           continue;
         }
-        if (it > (1ll << 24)) __builtin_trap();
+        if (it > kSpinBound) __builtin_trap();
         __builtin_amdgcn_s_sleep(1);
       }
       // Dantzig's answer (checked valid by the helper)
@@ -1728,7 +1732,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
     } else {
 #ifdef NIMBLE_STAGE_TIMING
       ok = waveDantzigR<kLds, R>(m, spc<kLds>(P.A), sp<kLds>(P.M2), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane,
-                                 g_stamp + 52);
+                                 g_stamp ? g_stamp + SLOT_DANTZIG : nullptr);
 #else
       ok = waveDantzigR<kLds, R>(m, spc<kLds>(P.A), sp<kLds>(P.M2), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane);
 #endif
@@ -1908,7 +1912,7 @@ __device__ void helperWave(const ModelDev& md, double* s, const Layout& L, int l
     } else {
 #ifdef NIMBLE_STAGE_TIMING
       if (lane == 0 && g_stamp) g_stamp[94] = (double)__builtin_amdgcn_s_memtime();
-      double* dbgD = g_stamp ? g_stamp + 99 : nullptr;
+      double* dbgD = g_stamp ? g_stamp + SLOT_DANTZIG : nullptr;
 #else
       double* dbgD = nullptr;
 #endif
@@ -1968,7 +1972,7 @@ __device__ void helperWave(const ModelDev& md, double* s, const Layout& L, int l
         }
         if (!pOpen) break;
         // only the PGS fallback is open, waiting for the warm start
-        if (it > (1ll << 24)) __builtin_trap();
+        if (it > kSpinBound) __builtin_trap();
         __builtin_amdgcn_s_sleep(1);
       }
     }

@@ -70,6 +70,9 @@ DEV V meshSupport(const MeshObj& o, V dir) {
     if (d > best) { best = d; bi = k; }
   }
   waveArgMax(best, bi);
+  // no vertex beat -inf (a NaN direction from a non-finite state, or an empty
+  // list): the reference keeps maxDotPoint = 0, i.e. the mesh origin
+  if (bi == 0x7fffffff) return pos(o.T);
   const double* p = o.v + 3 * bi;
   return xf(o.T, mk(p[0] * o.sc[0], p[1] * o.sc[1], p[2] * o.sc[2]));
 }

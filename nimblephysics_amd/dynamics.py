@@ -140,9 +140,13 @@ class MeshShape(Shape):
 
     def candidate(self):
         """Per-vertex mask of possible support / witness points (mesh.py)."""
-        if self._candidate is None:
+        # keyed on the scale: the mask depends on it (a stale one would drop
+        # vertices that became support / witness points)
+        size = np.asarray(self.size, dtype=np.float64)
+        if self._candidate is None or not np.array_equal(getattr(self, "_candidate_size", None), size):
             from .mesh import candidate_mask
-            self._candidate = candidate_mask(self.vertices, self.size)
+            self._candidate = candidate_mask(self.vertices, size)
+            self._candidate_size = size.copy()
         return self._candidate
 
 
@@ -299,6 +303,7 @@ class BodyNode:
         """BodyNode::setBeta (BodyNode.cpp:652): the COM direction that
         INERTIA_COM_MU scales."""
         self.beta = np.asarray(beta, dtype=np.float64).copy()
+        _model_changed(self.skel)
 
     def getBeta(self):
         return getattr(self, "beta", np.ones(3)).copy()

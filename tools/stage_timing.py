@@ -1,5 +1,7 @@
 """Per-stage shader-clock breakdown of the forward kernel (debug build with
 -DNIMBLE_STAGE_TIMING; run on a GPU box with NIMBLE_AMD_LIB pointing at it)."""
+import glob
+import re
 import sys
 
 import numpy as np
@@ -9,6 +11,34 @@ sys.path[:0] = ["tests", "."]
 import models  # noqa: E402
 import nimblephysics_amd as nimble  # noqa: E402
 
+
+def check_slot_map(csrc="nimblephysics_amd/csrc"):
+    """Static check of the stamp slot map: every multi-slot debug block
+    (SLOT_* in stamp.cuh, with its width) is disjoint from the others and from
+    every single stamp / accumulator slot the sources write, and all fit in
+    SLOT_COUNT.  Returns the block table; raises on a collision."""
+    src = "".join(open(f).read() for f in sorted(glob.glob(csrc + "/*.cuh") + glob.glob(csrc + "/*.hip")))
+    stamp = open(csrc + "/stamp.cuh").read()
+    count = int(re.search(r"#define SLOT_COUNT (\d+)", stamp).group(1))
+    widths = {"SLOT_PGS": 5, "SLOT_COD": 3, "SLOT_DANTZIG": 10}
+    blocks = {k: (int(v), int(v) + widths[k]) for k, v in re.findall(r"#define (SLOT_\w+) (\d+)", stamp) if k in widths}
+    singles = set(int(k) for k in re.findall(r"STAMP\((\d+)\)", src))
+    singles |= set(int(k) for k in re.findall(r"TACC_END\((\d+)", src))
+    singles |= set(int(k) for k in re.findall(r"g_stamp\[(\d+)\]", src))
+    if re.search(r"g_stamp \+ \d", src):
+        raise AssertionError("raw g_stamp + <number> offset: use a SLOT_* block")
+    for k, (a, b) in blocks.items():
+        assert b <= count, (k, a, b, count)
+        hit = sorted(x for x in singles if a <= x < b)
+        assert not hit, f"{k} [{a},{b}) overlaps single slots {hit}"
+        for k2, (a2, b2) in blocks.items():
+            assert k == k2 or b <= a2 or b2 <= a, f"{k} overlaps {k2}"
+    assert max(singles) < count, max(singles)
+    return blocks
+
+
+SLOTS = check_slot_map()
+SD = SLOTS["SLOT_DANTZIG"][0]
 B = 1024
 import os  # noqa: E402
 if os.environ.get("STAGE_WORKLOAD") == "atlas_mesh":
@@ -29,12 +59,12 @@ n = w.getNumDofs()
 from nimblephysics_amd import _native  # noqa: E402
 ws = _native.snapshot_layout(n, timing=True)["stamps"]  # csrc/pool_sizes.h snStamps(n)
 for it in range(4):
-    snap[:, ws:ws + 110] = 0
+    snap[:, ws:ws + 128] = 0
     prev_state, prev_cache = state.clone(), cache.clone()
     dev.forward(state, action, cache, nxt, snap, s)
     torch.cuda.synchronize()
     state = nxt.clone()
-    T = snap[:, ws:ws + 110].cpu().numpy()
+    T = snap[:, ws:ws + 128].cpu().numpy()
     hd = snap[:, :8].cpu().numpy()
     names = {(10, 14): " kinematics", (14, 15): " composites", (15, 16): " CRBA + bias", (16, 17): " cholesky", (17, 11): " dynamics cache store",
              (70, 71): "  kin: local transforms", (71, 72): "  kin: tree compose", (72, 73): "  kin: motion subspace",
@@ -69,10 +99,10 @@ for it in range(4):
             rel = lambda k: int(T[wi, k] - a0) if T[wi, k] > 0 else -1  # noqa: E731
             print("      board (clk from A built): construct done %d, helper Dantzig %d..%d (%d pivots, %s), answer at %d; "
                   "PGS fallback %s %d..%d, frictionless %s %d..%d"
-                  % (T[wi, 5] - a0, T[wi, 94] - a0, T[wi, 95] - a0, T[wi, 99], {1: "ok", 2: "failed"}.get(int(T[wi, 96]), "?"),
+                  % (T[wi, 5] - a0, T[wi, 94] - a0, T[wi, 95] - a0, T[wi, SD], {1: "ok", 2: "failed"}.get(int(T[wi, 96]), "?"),
                      T[wi, 6] - a0, who.get(int(T[wi, 97]), "?"), rel(100), rel(101), who.get(int(T[wi, 98]), "?"),
                      rel(102), rel(103)))
-        print(f"  world {wi}: pivots {int(T[wi,52])} at row {int(T[wi,53])} pgs-sweeps {int(T[wi,54])} ign {hd[wi,7]:.0f} total {int(tot[wi])} rows {int(hd[wi,1])} clamp {int(hd[wi,2])} flag {hd[wi,4]:.0f} | " + " ".join(parts))
+        print(f"  world {wi}: pivots {int(T[wi,SD])} at row {int(T[wi,SD+1])} pgs-sweeps {int(T[wi,54])} ign {hd[wi,7]:.0f} total {int(tot[wi])} rows {int(hd[wi,1])} clamp {int(hd[wi,2])} flag {hd[wi,4]:.0f} | " + " ".join(parts))
 
 # the slowest world of the last step re-run alone (one wave on the GPU): how
 # much of its time is contention with the other worlds' waves
@@ -81,11 +111,11 @@ st1, ca1, ac1 = prev_state[wi:wi + 1].clone(), prev_cache[wi:wi + 1].clone(), ac
 sn1 = torch.zeros((1, dev.snapshot_doubles), dtype=torch.float64, device=d)
 nx1 = torch.empty_like(st1)
 for rep in range(2):
-    sn1[:, ws:ws + 100] = 0
+    sn1[:, ws:ws + 128] = 0
     c1 = ca1.clone()
     dev.forward(st1, ac1, c1, nx1, sn1, s)
     torch.cuda.synchronize()
-T1 = sn1[:, ws:ws + 100].cpu().numpy()[0]
+T1 = sn1[:, ws:ws + 128].cpu().numpy()[0]
 parts = []
 for (a, b), nm in names.items():
     if T1[a] > 0 and T1[b] > 0 and (a, b) not in ((10, 11),):
@@ -113,7 +143,7 @@ if out:
                "short_circuit": float(v[(hd[ok, 0] > 0) & (path[ok] > 0)].mean()) if ((hd[ok, 0] > 0) & (path[ok] > 0)).any() else None,
                "fallback": float(v[(hd[ok, 0] > 0) & (path[ok] == 0)].mean()) if ((hd[ok, 0] > 0) & (path[ok] == 0)).any() else None},
            "slowest": [{"world": int(wi), "clk": float(tot_all[wi]), "rows": int(hd[wi, 1]), "clamping": int(hd[wi, 2]),
-                        "short_circuit": int(hd[wi, 6]), "dantzig_pivots": int(T[wi, 52]), "pgs_sweeps": int(T[wi, 54])}
+                        "short_circuit": int(hd[wi, 6]), "dantzig_pivots": int(T[wi, SD]), "pgs_sweeps": int(T[wi, 54])}
                        for wi in np.argsort(-tot_all)[:10]]}
     json.dump(res, open(out, "w"), indent=1)
     print("histogram ->", out, json.dumps({k: res[k] for k in ("mean", "p50", "p99", "max", "max_over_mean")}))

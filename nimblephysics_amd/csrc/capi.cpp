@@ -316,22 +316,25 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
   }
   w->bwd = makeLayout(m, true, bwdRows);
   // the wide forward kernel's layout: the forward's, plus an LDS stage at the
-  // pool (idle there: its pools are off chip) for the COD factorisations of
-  // the largest clamping set, mcap x mcap with the COD workspace, as far as
-  // a CU's 160 KB allow (one wide world per CU then; most of the launch's
-  // workgroups are not deferred worlds and exit at once)
+  // pool (idle there: its pools are off chip) for the O(m^3) pieces of the
+  // largest LCPs -- the COD factorisations, the pseudo-inverse columns (the
+  // factor plus 64 right-hand sides), the Dantzig LDL^T factor -- as far as a
+  // CU's 160 KB allow.  One wide world per CU then (most of the launch's
+  // workgroups are not deferred worlds and exit at once); each phase checks
+  // at run time whether its operands fit the stage and otherwise works in
+  // HBM.  NIMBLE_AMD_WIDE_STAGE=0 turns the stage off (measurements).
   w->fwdWide = w->fwd;
   w->wideLds = (size_t)w->fwd.total * sizeof(double);
   {
     const int mc = 3 * maxContacts < NIMBLE_MAX_SOLVED_LCP ? 3 * maxContacts : NIMBLE_MAX_SOLVED_LCP;
-    const int need = mc * mc + 4 * mc + (mc + 1) / 2 + 3 + mc;
+    const int wsd = 4 * mc + (mc + 1) / 2 + 3;
+    int need = mc * mc + wsd + 65 * mc;                          // COD factor + workspace + pinv right-hand sides
+    const int needL = mc * (mc | 1) + 2 * mc;                    // Dantzig L (odd leading dimension) + scratch
+    if (needL > need) need = needL;
     const int room = (int)(160 * 1024 / sizeof(double)) - w->fwd.pool;
-    // off unless NIMBLE_AMD_WIDE_STAGE=1: measured on the mesh Atlas (1024
-    // worlds, ~37 % wide) the stage's 148 KB leave one wide world per CU
-    // instead of three, and the faster factorisations do not make up for the
-    // second round (forward 11.38 vs 10.57 ms)
     const char* ev = getenv("NIMBLE_AMD_WIDE_STAGE");
-    if (m.numPairs > 0 && mc > 24 && ev && atoi(ev) == 1) {
+    const bool on = !(ev && atoi(ev) == 0);
+    if (m.numPairs > 0 && mc > 64 && on && room > 0) {
       const int cap = need < room ? need : room;
       w->fwdWide.stage = w->fwd.pool;
       w->fwdWide.stageCap = cap;
@@ -339,8 +342,8 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
       if (end > w->wideLds) w->wideLds = end;
     }
     if (getenv("NIMBLE_AMD_VERBOSE"))
-      fprintf(stderr, "nimble_amd: wide forward LDS %zu B (COD stage %d doubles of %d needed)\n", w->wideLds,
-              w->fwdWide.stageCap, need);
+      fprintf(stderr, "nimble_amd: wide forward LDS %zu B (stage %d doubles of %d for %d rows)\n", w->wideLds,
+              w->fwdWide.stageCap, need, mc);
   }
   if (getenv("NIMBLE_AMD_VERBOSE"))
     fprintf(stderr, "nimble_amd: LDS forward %d B (pool rows %d), backward %d B (pool rows %d), max rows %d\n",
@@ -363,7 +366,9 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
   // their off-chip LCP workspace is per workgroup instead of the snapshot tail
   if (m.numPairs > 0 && bwdPoolDoublesHost(mcap, m.n) > w->bwd.poolCap) w->jacWsDoubles = bwdPoolDoublesHost(mcap, m.n);
   // dynamics cache at the tail of every snapshot
-  w->fwd.snDyn = w->bwd.snDyn = w->snapDoubles;
+  // (the wide forward's layout copy too: it reloads the cache the one-row
+  // kernel stored for a deferred world)
+  w->fwd.snDyn = w->bwd.snDyn = w->fwdWide.snDyn = w->snapDoubles;
   w->snapDoubles += dynCacheDoubles(m.n, m.nb);
   m.lay[0] = w->fwd;
   m.lay[1] = w->bwd;
@@ -432,7 +437,7 @@ int nimble_forward(nimble_world_t w, int32_t batch, const double* state, const d
     // the worlds whose LCP has more rows than one per lane (or than the
     // test threshold): stepped by the two-rows-per-lane kernel
     if (w->host.numPairs > 0 && w->maxRows > w->deferRows) {
-      hipLaunchKernelGGL(nimble_forward_wide_kernel, dim3(cnt), dim3(fwdThreads), w->wideLds, st, w->dev, w->fwdWide,
+      hipLaunchKernelGGL(nimble_forward_wide_kernel, dim3(cnt), dim3(64), w->wideLds, st, w->dev, w->fwdWide,
                          state + b0 * 2 * n, forces + b0 * n, lcp_cache + (size_t)b0 * w->cacheDoubles,
                          next_state + b0 * 2 * n, snapshot + (size_t)b0 * w->snapDoubles, w->snapDoubles,
                          w->cacheDoubles);

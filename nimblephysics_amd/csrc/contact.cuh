@@ -1098,6 +1098,75 @@ __device__ void devGuess(typename Space<kLds>::dptr poolIn, int m, int n, lds_do
   WSYNC();
 }
 
+// pinv(Q) from its COD factor `c` (factor, workspace and Z in LDS: the wide
+// kernels' stage), 64 columns per pass, lane = column: Z[i * 65 + lane] is
+// the column's right-hand side (row stride 65: the transposed write-back
+// below reads it conflict-free).  Per column the same operations in the same
+// order as the per-lane solve of backwardPrecompute's off-stage path (Q^T
+// reflectors, back substitution on T, Z^T reflectors), so the results are
+// bit for bit those.  Writes pinv(Q)^T rows to PTG (row col = column col of
+// pinv(Q), permuted) and the solves z_c to Zs (row c, for the imprecision
+// map), both in HBM.
+__device__ __forceinline__ void pinvColumnsStaged(const Cod& c, double* Z, double* PTG, double* Zs, int lane) {
+  const int nc = c.n;
+  const double* F = c.A;
+  const int kmax = c.kmax;
+  const int r = uni(*c.rank);
+  for (int c0 = 0; c0 < nc; c0 += WAVE) {
+    const int col = c0 + lane;
+    const int cnt = nc - c0 < WAVE ? nc - c0 : WAVE;
+    for (int i = 0; i < nc; i++) Z[i * 65 + lane] = i == col ? 1.0 : 0.0;
+    WSYNC();
+    double* z = Z + lane;
+    for (int k = 0; k < kmax; k++) {
+      const double vnorm = unid(c.vn[k]);
+      if (!(vnorm > 0)) continue;
+      const double vd = unid(c.vd[k]);
+      double sc = vd * z[k * 65];
+      int i = k + 1;
+      for (; i + 8 <= nc; i += 8) {
+        double fv[8], zv[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) { fv[u] = F[(i + u) * nc + k]; zv[u] = z[(i + u) * 65]; }
+#pragma unroll
+        for (int u = 0; u < 8; u++) asm volatile("" : "+v"(fv[u]), "+v"(zv[u]));
+#pragma unroll
+        for (int u = 0; u < 8; u++) sc += fv[u] * zv[u];
+      }
+      for (; i < nc; i++) sc += F[i * nc + k] * z[i * 65];
+      sc = 2 * sc / vnorm;
+      z[k * 65] -= sc * vd;
+      for (i = k + 1; i < nc; i++) z[i * 65] -= sc * F[i * nc + k];
+    }
+    for (int i = r - 1; i >= 0; i--) {
+      double sc = z[i * 65];
+      for (int j = i + 1; j < r; j++) sc -= F[i * nc + j] * z[j * 65];
+      z[i * 65] = sc / F[i * nc + i];
+    }
+    for (int j = r; j < nc; j++) z[j * 65] = 0.0;
+    for (int i = 0; i < r && r < nc; i++) {
+      const double vn = unid(c.zn[i]);
+      if (vn == 0) continue;
+      const double zd = unid(c.zd[i]);
+      double sc = z[i * 65] * zd;
+      for (int j = r; j < nc; j++) sc += z[j * 65] * F[i * nc + j];
+      sc = 2 * sc / vn;
+      z[i * 65] -= sc * zd;
+      for (int j = r; j < nc; j++) z[j * 65] -= sc * F[i * nc + j];
+    }
+    WSYNC();
+    // write-back, lane-contiguous in HBM: element t of the chunk is column
+    // c0 + t / nc, row t % nc
+    for (int t = lane; t < cnt * nc; t += WAVE) {
+      const int j = t / nc, i = t - j * nc;
+      const double v = Z[i * 65 + j];
+      Zs[(size_t)c0 * nc + t] = v;
+      PTG[(size_t)(c0 + j) * nc + c.perm[i]] = v;
+    }
+    WSYNC();
+  }
+}
+
 // The upstream-gradient-independent pieces of the constrained backward
 // (BackpropSnapshot.cpp:2723 getJacobianOfConstraintForce and the clamping
 // matrices it uses), computed here where A = J Minv J^T is on chip:
@@ -1161,12 +1230,37 @@ __device__ void backwardPrecompute(const ModelDev& md, lds_double* sIn, const La
   double* w = carveCod(P.scr, P.M1, nc, nc, nc, cod);
   double* cn = w; w += m;
   double* vv = w; w += m;
+  double* Zs = P.A;
+  // off-chip pools (the wide kernels): the factor and the right-hand sides
+  // on chip when the launch's LDS stage holds them (F n_c x n_c, the COD
+  // workspace, 64 right-hand sides n_c x 65): every access of the column
+  // solves below is then an LDS broadcast (F) or lane-contiguous (Z) instead
+  // of a dependent HBM / L2 load with a 64-line gather (~8.7M clocks at
+  // n_c = 96 on the mesh Atlas)
+  const int wsdS = 4 * nc + (nc + 1) / 2 + 3;
+  const bool staged = !kLds && stage != nullptr && nc * nc + wsdS + 65 * nc <= stageCap;
   STAMP(48);
+  if (staged) {
+    double* sF = (double*)stage;
+    double* sW = sF + nc * nc;
+    double* sZ = sW + wsdS;
+    if (reuse) {
+      for (int t = lane; t < nc * nc; t += WAVE) sF[t] = P.M1[t];
+      for (int t = lane; t < wsdS; t += WAVE) sW[t] = P.scr[t];
+      WSYNC();
+    } else {
+      for (int t = lane; t < nc * nc; t += WAVE) sF[t] = P.M2[t];
+      WSYNC();
+      codFactorR<true, R>(sp<true>(sF), sp<true>(sW), nc, nc, nc, sp<true>(sZ), lane);
+    }
+    carveCod(sW, sF, nc, nc, nc, cod);
+    STAMP(49);
+    pinvColumnsStaged(cod, sZ, PTG, Zs, lane);
+  } else {
   if (!reuse) codFactorAny<kLds, R>(sp<kLds>(P.M1), sp<kLds>(P.scr), nc, nc, nc, sp<kLds>(vv), lane, stage, stageCap);
   STAMP(49);
   // pinv(Q): lane c solves Q x = e_c in place in row c of the (now free) A
   // region (columns c, c + 64, .. when n_c > 64)
-  double* Zs = P.A;
   for (int col = lane; col < nc; col += WAVE) {
     double* rhs = Zs + col * nc;
     for (int i = 0; i < nc; i++) rhs[i] = i == col ? 1.0 : 0.0;
@@ -1198,6 +1292,7 @@ __device__ void backwardPrecompute(const ModelDev& md, lds_double* sIn, const La
     }
     // column `col` of pinv(Q) = row `col` of pinv(Q)^T
     for (int j = 0; j < nc; j++) PTG[col * nc + cod.perm[j]] = rhs[j];
+  }
   }
   WSYNC();
   STAMP(50);
@@ -1366,7 +1461,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
 template <int R>
 __device__ __forceinline__ bool contactStage(const ModelDev& md, double* s, const Layout& L, int lane, double* v1,
                                              const double* ddq, double* cache, double* snap, double* overflowWs,
-                                             bool helperOn, bool collided, int deferRows) {
+                                             bool helperOn, bool collided, int deferRows, bool handedOff = false) {
   const int n = md.n;
   s = lds<true>(s);
   snap = gbl(snap);
@@ -1377,7 +1472,14 @@ __device__ __forceinline__ bool contactStage(const ModelDev& md, double* s, cons
 #endif
   STAMP(0);
   double* ct = s + L.ct;
-  if (collided) {
+  if (handedOff) {
+    // the one-row kernel's contact header and kept contacts (written to the
+    // workspace when it deferred this world; read before the LCP pool,
+    // which starts there, overwrites them)
+    const int nk = uni((int)overflowWs[H_NCON]);
+    for (int t = lane; t < CT_CONTACTS + nk * CREC; t += WAVE) ct[t] = overflowWs[t];
+    WSYNC();
+  } else if (collided) {
     // the helper wave ran the collision detection during the dynamics
     collideWait(ct, CS_DONE);
     collidePost(ct, CS_IDLE, lane);
@@ -1406,6 +1508,9 @@ __device__ __forceinline__ bool contactStage(const ModelDev& md, double* s, cons
   }
   const int m = nCon + 2 * __popcll(__ballot(fr));
   if (m > deferRows) {
+    // hand the contacts to the wide kernel (the snapshot's workspace, its
+    // LCP pool later); the dynamics are in the snapshot's dynamics cache
+    for (int t = lane; t < CT_CONTACTS + nCon * CREC; t += WAVE) overflowWs[t] = ct[t];
     if (lane == 0) snap[SN_STATUS] = (double)((int)ct[H_STATUS] | ST_DEFERRED);
     WSYNC();
     return true;
@@ -1730,11 +1835,15 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
 #pragma unroll
       for (int q = 0; q < R; q++) xd[q] = ok && rowAt(q, lane) < m ? P.xh[rowAt(q, lane)] : 0.0;
     } else {
+      // off-chip pools: the LDL^T factor in the launch's LDS stage when it
+      // fits (every pivot's triangular solves and its row / column shifts
+      // read and write it; A is read a row at a time and stays in HBM)
+      double* Ld = (stage != nullptr && m * (m | 1) <= stageCap) ? (double*)stage : (double*)P.M2;
 #ifdef NIMBLE_STAGE_TIMING
-      ok = waveDantzigR<kLds, R>(m, spc<kLds>(P.A), sp<kLds>(P.M2), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane,
+      ok = waveDantzigR<kLds, R>(m, spc<kLds>(P.A), sp<kLds>(Ld), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane,
                                  g_stamp ? g_stamp + SLOT_DANTZIG : nullptr);
 #else
-      ok = waveDantzigR<kLds, R>(m, spc<kLds>(P.A), sp<kLds>(P.M2), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane);
+      ok = waveDantzigR<kLds, R>(m, spc<kLds>(P.A), sp<kLds>(Ld), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane);
 #endif
     }
     if (ok) {
@@ -1785,7 +1894,16 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
         if (lane == 0) ct[H_CODOK] = 0;
         bool dup;
         double xd[R];
-        ok = pgsFallbackR<kLds, R>(P.A, P.xc, m, cf, bR, loR, hiR, fiR, sp<kLds>(P.M1), lane, xd, dup, nullptr, dbgPgs);
+        // off-chip pools: the PGS sweeps read A from the LDS stage when it
+        // fits (a row per row step: LDS instead of L2 latency)
+        const double* As = P.A;
+        if (stage != nullptr && m * m <= stageCap) {
+          double* sA = (double*)stage;
+          for (int t = lane; t < m * m; t += WAVE) sA[t] = P.A[t];
+          WSYNC();
+          As = sA;
+        }
+        ok = pgsFallbackR<kLds, R>(As, P.xc, m, cf, bR, loR, hiR, fiR, sp<kLds>(P.M1), lane, xd, dup, nullptr, dbgPgs);
         if (dup && lane == 0) ct[H_STATUS] = (double)((int)ct[H_STATUS] | ST_DUPLICATE_COLUMNS);
         if (ok)
 #pragma unroll
@@ -1793,7 +1911,15 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
       }
       if (!ok) {
         ign = true;
-        frictionlessPgsR<kLds, R>(P.A, P.b, P.lo, P.hi, m, cf, fiR, lane, X, nullptr);
+        const double* As = P.A;
+        if (stage != nullptr && m * m <= stageCap) {
+          // (the stage holds A already when the PGS fallback ran from it)
+          double* sA = (double*)stage;
+          for (int t = lane; t < m * m; t += WAVE) sA[t] = P.A[t];
+          WSYNC();
+          As = sA;
+        }
+        frictionlessPgsR<kLds, R>(As, P.b, P.lo, P.hi, m, cf, fiR, lane, X, nullptr);
       }
     }
     bool nan2 = false;

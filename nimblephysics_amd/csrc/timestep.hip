@@ -365,6 +365,14 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
     }
 #endif
     loadState(md, s, L, lane, st, forces + (size_t)env * n);
+    if (R > 1) {
+      // a world the one-row kernel deferred: its kinematics, Cholesky factor
+      // and bias forces are in the snapshot's dynamics cache (stored before
+      // it deferred), its contacts in the workspace hand-off (contactStage):
+      // reloaded, not recomputed
+      dynCacheCopy(md, s, L, snapshot + (size_t)env * snapDoubles + L.snDyn, false, lane);
+      STAMP(11);
+    } else {
 #ifdef NIMBLE_STAGE_TIMING
     kinematics(md, s, L, lane, nullptr, g_stamp);
 #else
@@ -381,6 +389,7 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
     STAMP(17);
     dynCacheCopy(md, s, L, snapshot + (size_t)env * snapDoubles + L.snDyn, true, lane);
     STAMP(11);
+    }
     // rhs = tau + spring + damping - C   (GenericJoint::updateTotalForceDynamic)
     double* x = s + L.x;
     for (int i = lane; i < n; i += WAVE) {
@@ -401,7 +410,7 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
     if (md.numPairs > 0) {
       double* sn = snapshot + (size_t)env * snapDoubles;
       deferred = contactStage<R>(md, s, L, lane, v1, x, lcpCache + (size_t)env * cacheDoubles, sn,
-                                 sn + snapWorkspaceOffset(n), helperOn, helperOn, deferRows);
+                                 sn + snapWorkspaceOffset(n), helperOn, helperOn, deferRows, R > 1);
     } else if (lane < 8) {
       // a model without collision pairs still has a snapshot header (no
       // contacts, no rows, no clamping) for the getters to read
@@ -439,7 +448,8 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, const double* 
 }
 
 // the worlds nimble_forward_kernel deferred (snapshot status ST_DEFERRED),
-// two LCP rows per lane.  (The same occupancy target as the one-row kernel:
+// two LCP rows per lane, from the one-row kernel's dynamics and contacts
+// (launched with one wave per world: nothing left for a helper).  (The same occupancy target as the one-row kernel:
 // the non-inlined narrow-phase functions both kernels call are compiled once,
 // for the tighter of the two register budgets.)
 extern "C" __global__ void __launch_bounds__(2 * WAVE) __attribute__((amdgpu_waves_per_eu(2)))

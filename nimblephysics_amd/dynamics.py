@@ -462,25 +462,46 @@ class Skeleton:
     def getPositionUpperLimits(self):
         return self._per_dof("pos_hi")
 
-    def setControlForceUpperLimits(self, lim):
+    def _set_per_dof(self, attr, lim):
         lim = np.asarray(lim, dtype=np.float64)
+        if lim.shape != (self.getNumDofs(),):
+            raise ValueError(f"{attr}: expected {self.getNumDofs()} values, got shape {lim.shape}")
         for b in self.bodies:
             j = b.joint
-            j.force_hi[:] = lim[j.dof_offset:j.dof_offset + j.getNumDofs()]
+            getattr(j, attr)[:] = lim[j.dof_offset:j.dof_offset + j.getNumDofs()]
         _model_changed(self)
 
+    # Skeleton::setControlForceUpperLimits / ... (dart/dynamics/MetaSkeleton.cpp):
+    # per-dof limits in the skeleton's dof order
+    def setControlForceUpperLimits(self, lim):
+        self._set_per_dof("force_hi", lim)
+
     def setControlForceLowerLimits(self, lim):
-        lim = np.asarray(lim, dtype=np.float64)
-        for b in self.bodies:
-            j = b.joint
-            j.force_lo[:] = lim[j.dof_offset:j.dof_offset + j.getNumDofs()]
-        _model_changed(self)
+        self._set_per_dof("force_lo", lim)
+
+    def setPositionUpperLimits(self, lim):
+        self._set_per_dof("pos_hi", lim)
+
+    def setPositionLowerLimits(self, lim):
+        self._set_per_dof("pos_lo", lim)
+
+    def setVelocityUpperLimits(self, lim):
+        self._set_per_dof("vel_hi", lim)
+
+    def setVelocityLowerLimits(self, lim):
+        self._set_per_dof("vel_lo", lim)
 
     def getControlForceUpperLimits(self):
         return self._per_dof("force_hi")
 
     def getControlForceLowerLimits(self):
         return self._per_dof("force_lo")
+
+    def getVelocityUpperLimits(self):
+        return self._per_dof("vel_hi")
+
+    def getVelocityLowerLimits(self):
+        return self._per_dof("vel_lo")
 
 
 def rpy_to_matrix(rpy) -> np.ndarray:

@@ -450,6 +450,36 @@ class World:
         """d(next state)/d(action) [2n, |A|] at the current state (World.cpp:2227)."""
         return self.getCachedBackpropSnapshot().getActionJacobian(self)
 
+    # --- LCP warm start (BoxedLcpConstraintSolver::mX) ------------------------
+    def setCachedLCPSolution(self, x):
+        """World::setCachedLCPSolution (World.cpp): the warm start of the next
+        step's LCP, used only when its size equals that LCP's row count (else
+        ignored, as BoxedLcpConstraintSolver does).  `x` is one vector (every
+        world of the next batch) or a list with one vector (or None: empty)
+        per world."""
+        per_world = (isinstance(x, (list, tuple)) and len(x) > 0 and (x[0] is None or np.ndim(x[0]) == 1)) \
+            or (x is not None and np.ndim(x) == 2)
+        if per_world:
+            rows = [None if r is None else np.asarray(r, dtype=np.float64) for r in x]
+        else:
+            rows = [None if x is None else np.asarray(x, dtype=np.float64)]
+        for r in rows:
+            if r is not None and r.ndim != 1:
+                raise ValueError("setCachedLCPSolution: one 1-D vector per world")
+        self._pending_lcp_cache = rows
+
+    def getCachedLCPSolution(self, world_index: int = 0):
+        """The LCP solution of world `world_index` of the last batched step
+        (the next step's warm start; empty when it had no LCP)."""
+        bs = getattr(self, "_batch_state", None)
+        if bs is None:
+            rows = getattr(self, "_pending_lcp_cache", None) or [None]
+            r = rows[world_index if len(rows) > 1 else 0]
+            return np.zeros(0) if r is None else r.copy()
+        row = bs.cache[world_index].cpu().numpy()
+        m = int(row[0])
+        return row[1:1 + m].copy() if m > 0 else np.zeros(0)
+
     # --- per-world status of the last batched step (see timestep.py) ----------
     def getLastStatus(self):
         """Status bits of each world of the last ``timestep`` call (a device

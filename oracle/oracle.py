@@ -308,6 +308,25 @@ def ref_dantzig(A, b, lo, hi, findex, early=False):
     return bool(ok), x
 
 
+def ref_dantzig_ambiguous(A, b, lo, hi, findex, seed, trials=512, effective=True):
+    """True when the reference's own dSolveLCP (oracle/_ref) gives both
+    outcomes under 1e-15-relative symmetric perturbations of A; with
+    `effective` the outcome is success AND isLCPSolutionValid (what the
+    contact solver keeps), else the raw success flag.  None if unbuilt."""
+    if ref_lib() is None:
+        return None
+    rng = np.random.default_rng(seed)
+    outs = set()
+    for _ in range(trials):
+        N = rng.standard_normal(A.shape)
+        Ap = A * (1 + 1e-15 * (N + N.T) / 2)
+        ok, x = ref_dantzig(Ap, b, lo, hi, findex, True)
+        outs.add(bool(ok and (not effective or lcp_valid(A, x, b, hi, lo, findex))))
+        if len(outs) == 2:
+            return True
+    return False
+
+
 def cod_solve(A, b):
     A = np.ascontiguousarray(A, dtype=np.float64)
     m, n = A.shape

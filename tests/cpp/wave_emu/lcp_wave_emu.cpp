@@ -8,7 +8,10 @@
 //
 // input:  count, then per problem: m, A (m*m row-major), b, lo, hi, findex, x0
 // output: per problem and R: "R m okD xD... okP xP... validD reduceAlive codRank xCod..."
+// With LCP_EMU_DANTZIG_ONLY=1 in the environment only waveDantzigR and its
+// validity check run, R = 1 only for m <= 64: "R m okD xD... validD".
 #include <cstdio>
+#include <cstdlib>
 #include <functional>
 #include <thread>
 #include <vector>
@@ -33,6 +36,34 @@ static void runWave(const std::function<void(int)>& f) {
       f(l);
     });
   for (auto& t : ths) t.join();
+}
+
+template <int R>
+static void solveDantzig(const Problem& P) {
+  const int m = P.m;
+  std::vector<double> L((size_t)m * (m | 1) + 8), scr((size_t)m + 8), xD((size_t)64 * R);
+  int okD = 0, validD = 0;
+  runWave([&](int lane) {
+    double b[R], lo[R], hi[R], x[R];
+    int fi[R];
+    for (int s = 0; s < R; s++) {
+      const int r = lane + 64 * s;
+      b[s] = r < m ? P.b[r] : 0.0;
+      lo[s] = r < m ? P.lo[r] : 0.0;
+      hi[s] = r < m ? P.hi[r] : 0.0;
+      fi[s] = r < m ? P.fi[r] : -1;
+    }
+    const bool d = waveDantzigR<false, R>(m, P.A.data(), L.data(), scr.data(), x, b, lo, hi, fi, lane);
+    const bool v = d && waveLcpValidR<false, R>(m, P.A.data(), 0.0, x, b, hi, lo, fi, false, lane);
+    for (int s = 0; s < R; s++) {
+      const int r = lane + 64 * s;
+      if (r < 64 * R) xD[r] = x[s];
+    }
+    if (lane == 0) { okD = d; validD = v; }
+  });
+  std::printf("%d %d %d", R, m, okD);
+  for (int i = 0; i < m; i++) std::printf(" %.17g", xD[i]);
+  std::printf(" %d\n", validD);
 }
 
 template <int R>
@@ -99,6 +130,12 @@ int main() {
     for (auto& v : P.hi) std::scanf("%lf", &v);
     for (auto& v : P.fi) std::scanf("%d", &v);
     for (auto& v : P.x0) std::scanf("%lf", &v);
+    const char* only = std::getenv("LCP_EMU_DANTZIG_ONLY");
+    if (only && only[0] == '1') {
+      if (m <= 64) solveDantzig<1>(P);
+      else solveDantzig<2>(P);
+      continue;
+    }
     if (m <= 64) solve<1>(P);
     solve<2>(P);
   }

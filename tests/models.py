@@ -78,7 +78,11 @@ def broken_states(kind):
     test_AtlasTrajectory.cpp :147-372).  Returns (world, names, state [B, 2n],
     forces [B, n], caches) with caches a list of LCP warm starts (None = empty).
     Atlas states are permuted from the SDF model's dof order onto this
-    package's Atlas by the name of the body owning each dof."""
+    package's Atlas by the name of the body owning each dof.  "atlas" is the
+    box-foot bench Atlas (the tests' 96-entry caches do not fit its contact
+    set and are not used); "atlas_mesh" is the STL-mesh Atlas
+    (atlas_v3_no_head, the tests' own meshes) with createWorld's limits
+    (:113-122) and the tests' 96-entry LCP caches (its 32 foot contacts)."""
     import json
     import os
     with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "broken_states.json")) as fh:
@@ -88,7 +92,22 @@ def broken_states(kind):
         cases = d["half_cheetah"]
         perm = np.arange(w.getNumDofs())
     else:
-        w = atlas_world(True)
+        if kind == "atlas_mesh":
+            from nimblephysics_amd.workloads import atlas_mesh_world
+            w = atlas_mesh_world(True)
+            lim = d["atlas"]["limits"]
+            sk0 = w.skeletons[0]
+            n0 = sk0.getNumDofs()
+            fl = np.full(n0, lim["force"])
+            fl[:lim["force_root_zero"]] = 0.0
+            sk0.setControlForceUpperLimits(fl)
+            sk0.setControlForceLowerLimits(fl * -1)
+            sk0.setPositionUpperLimits(np.full(n0, lim["position"]))
+            sk0.setPositionLowerLimits(np.full(n0, lim["position"]) * -1)
+            sk0.setVelocityUpperLimits(np.full(n0, lim["velocity"]))
+            sk0.setVelocityLowerLimits(np.full(n0, lim["velocity"]) * -1)
+        else:
+            w = atlas_world(True)
         cases = d["atlas"]["cases"]
         desc = w.desc_arrays()
         sk = w.skeletons[0]
@@ -105,7 +124,8 @@ def broken_states(kind):
         st[b, perm] = c["pos"]
         st[b, n + perm] = c["vel"]
         f[b, perm] = c["force"]
-    caches = [c.get("lcp_cache") or None for c in cases]
+    key = "lcp_cache_sdf" if kind == "atlas_mesh" else "lcp_cache"
+    caches = [c.get(key) or None for c in cases]
     return w, [c["name"] for c in cases], st, f, caches
 
 

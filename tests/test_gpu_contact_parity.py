@@ -607,10 +607,12 @@ def _seeded_cache(dev_doubles, caches, d):
     return cache
 
 
-@pytest.mark.parametrize("kind", ["half_cheetah", "atlas"])
+@pytest.mark.parametrize("kind", ["half_cheetah", "atlas", "atlas_mesh"])
 def test_broken_state_parity(kind):
     """The reference's broken-state regressions (test_HalfCheetahTrajectory.cpp
-    :126-330 with BROKEN_POINT's LCP cache, test_AtlasTrajectory.cpp :147-372;
+    :126-330 with BROKEN_POINT's LCP cache, test_AtlasTrajectory.cpp :147-372
+    on the box-foot Atlas and, with the tests' 96-entry LCP caches and
+    createWorld's limits, on the STL-mesh Atlas they were written for;
     tests/golden/broken_states.json): contact sets and LCP path identical to
     the oracle's, the next state and the full Jacobians (getStateJacobian and
     d next / d tau, one device backward per basis vector over a replicated
@@ -639,10 +641,46 @@ def test_broken_state_parity(kind):
                                                _seeded_cache(dev.cache_doubles, [c for c in caches for _ in range(R)], d))
     gs, gf = _device_backward(w, ts_r, tf_r, snap_r, np.tile(np.eye(R), (B, 1)))
     # the reference's "broken" (ill-conditioned) states: entries below 1e-4 of
-    # the matrix's largest are held to 1e-10 of it absolutely (~1e-10 seen)
+    # the matrix's largest are held to 1e-10 of it absolutely (~1e-10 seen).
+    # The backward is backprop's VJP, so its rows are the Jacobians' rows
+    # after clipLossGradientsToBounds (BackpropSnapshot.cpp:425): with
+    # createWorld's zero root force bounds (the mesh Atlas) every root-force
+    # entry is clipped (tau = 0 = lower = upper)
     for b, name in enumerate(names):
-        assert _rel(gs[b * R:(b + 1) * R], J[b], 1e-4) < RTOL, (name, _rel(gs[b * R:(b + 1) * R], J[b], 1e-4))
-        assert _rel(gf[b * R:(b + 1) * R], F[b], 1e-4) < RTOL, (name, _rel(gf[b * R:(b + 1) * R], F[b], 1e-4))
+        eJ, eF = _clip_rows(w, st[b], f[b], J[b].T.copy(), F[b].T.copy())
+        eJ, eF = eJ.T, eF.T
+        assert _rel(gs[b * R:(b + 1) * R], eJ, 1e-4) < RTOL, (name, _rel(gs[b * R:(b + 1) * R], eJ, 1e-4))
+        assert _rel(gf[b * R:(b + 1) * R], eF, 1e-4) < RTOL, (name, _rel(gf[b * R:(b + 1) * R], eF, 1e-4))
+    if kind == "atlas_mesh":
+        # the Jacobian getters do not clip: getActionJacobian equals F
+        from nimblephysics_amd import neural
+        w.setCachedLCPSolution(caches)
+        w._batch_state = None
+        snap_j = neural.forwardPass(w, state=torch.tensor(st, device=d), action=torch.tensor(f, device=d))
+        FJ = snap_j.getActionJacobian(w).cpu().numpy()
+        for b, name in enumerate(names):
+            assert _rel(FJ[b], F[b], 1e-4) < RTOL, (name, _rel(FJ[b], F[b], 1e-4))
+        assert np.abs(F[0][:, :6]).max() > 0  # ... whose root columns the backward clips
+
+
+def _clip_rows(w, s, f, Gs, Gf):
+    """clipLossGradientsToBounds applied to each column of Gs [2n, k] / Gf
+    [n, k] (a batch of loss gradients w.r.t. state / force) at state s and
+    force f: a gradient that would push a dof past a bound it sits on is
+    zeroed (BackpropSnapshot.cpp:425, oracle_step.cpp)."""
+    d = w.desc_arrays()
+    n = w.getNumDofs()
+    q, v = s[:n], s[n:]
+    for k in range(n):
+        for col in range(Gs.shape[1]):
+            if (q[k] == d["pos_lower"][k] and Gs[k, col] > 0) or (q[k] == d["pos_upper"][k] and Gs[k, col] < 0):
+                Gs[k, col] = 0.0
+            if (v[k] == d["vel_lower"][k] and Gs[n + k, col] > 0) or (v[k] == d["vel_upper"][k] and Gs[n + k, col] < 0):
+                Gs[n + k, col] = 0.0
+        for col in range(Gf.shape[1]):
+            if (f[k] == d["force_lower"][k] and Gf[k, col] > 0) or (f[k] == d["force_upper"][k] and Gf[k, col] < 0):
+                Gf[k, col] = 0.0
+    return Gs, Gf
 
 
 def test_forward_chunked_launches_match(monkeypatch):

@@ -46,10 +46,12 @@ def _jac_err(J, R, mask):
     return _rel(Jm, Rm), float(np.abs(J - R)[mask].max(initial=0.0))
 
 
-def _batched(world, st, f):
+def _batched(world, st, f, caches=None):
     d = torch.device("cuda:0")
     ts, tf = torch.tensor(st, device=d), torch.tensor(f, device=d)
     world._batch_state = None  # cold LCP caches, as the oracle's
+    if caches is not None:
+        world.setCachedLCPSolution(caches)
     snap = nimble.neural.forwardPass(world, state=ts, action=tf)
     torch.cuda.synchronize()
     return snap, ts, tf
@@ -128,7 +130,7 @@ def test_world_jacobians_single():
     assert _rel(J, RJ[0]) < RTOL and _rel(A, RF[0]) < RTOL
 
 
-@pytest.mark.parametrize("name", ["atlas", "half_cheetah", "capsule_edge", "atlas_broken"])
+@pytest.mark.parametrize("name", ["atlas", "half_cheetah", "capsule_edge", "atlas_broken", "atlas_mesh_broken"])
 def test_constraint_force_jacobians(name):
     """getClampingConstraintImpulses and getJacobianOfConstraintForce for
     POSITION / VELOCITY / FORCE (BackpropSnapshot.cpp:2723;
@@ -146,13 +148,17 @@ def test_constraint_force_jacobians(name):
         world = models.capsule_edge_world()
         st, f = models.capsule_edge_states(64, seed=2)
     else:
-        world, _, st, f, _ = models.broken_states("atlas")
+        world, _, st, f, caches = models.broken_states("atlas_mesh" if name == "atlas_mesh_broken" else "atlas")
     n = world.getNumDofs()
     B = st.shape[0]
     ow = O.OracleWorld(world)
+    if name == "atlas_mesh_broken":
+        # the tests' 96-entry warm starts (World::setCachedLCPSolution)
+        from test_oracle_pins import _seed_caches
+        _seed_caches(ow, caches)
     ow.forward(st, f)
     RD = ow.constraint_force_jacobians()
-    snap, ts, tf = _batched(world, st, f)
+    snap, ts, tf = _batched(world, st, f, caches if name == "atlas_mesh_broken" else None)
     sn = world._last_snapshot.cpu().numpy()
     same = _check_contacts(ow, sn, B, cache=world._batch_state.cache.cpu().numpy())
     fc = snap.getClampingConstraintImpulses().cpu().numpy()

@@ -364,7 +364,7 @@ def _seed_caches(o, caches):
             o.cache[b, 1:1 + len(c)] = c
 
 
-@pytest.mark.parametrize("kind", ["half_cheetah", "atlas"])
+@pytest.mark.parametrize("kind", ["half_cheetah", "atlas", "atlas_mesh"])
 def test_broken_state_jacobians_vs_finite_differences(oracle_built, kind):
     """The reference's broken-state regressions (test_HalfCheetahTrajectory.cpp
     :126-330, test_AtlasTrajectory.cpp :147-372, tests/golden/broken_states.json):
@@ -373,7 +373,12 @@ def test_broken_state_jacobians_vs_finite_differences(oracle_built, kind):
     / verifyVelGradients / verifyPosVelJacobian check) against central
     differences of the oracle's own step.  Each state is in contact:
     BOX_SPHERE capsule-ground contacts for the half-cheetah, eight
-    VERTEX_FACE foot contacts on the CFM + PGS fallback for Atlas."""
+    VERTEX_FACE foot contacts on the CFM + PGS fallback for the box-foot
+    Atlas; on the STL-mesh Atlas (the tests' own model, with createWorld's
+    limits and the tests' 96-entry caches) 32 VERTEX_FACE sole contacts: the
+    cache warm-starts BROKEN_2 onto the gradient short-circuit (68 clamping,
+    16 upper-bound rows), BROKEN_1 / BROKEN_3 fall back to CFM + PGS and
+    removeFriction."""
     w, names, st, f, caches = models.broken_states(kind)
     n = w.getNumDofs()
     o = O.OracleWorld(w)
@@ -385,6 +390,13 @@ def test_broken_state_jacobians_vs_finite_differences(oracle_built, kind):
         assert o.num_contacts(b) > 0, name
         if kind == "atlas":
             assert O.lcp_flags(o, b)[1] == 1, name  # Dantzig fails -> CFM + PGS
+        if kind == "atlas_mesh":
+            assert o.num_contacts(b) == 32 and int(caches[b] and len(caches[b])) == 96, name
+            fl = O.lcp_flags(o, b)
+            if name == "BROKEN_2":
+                assert fl[0] == 1 and fl[3] == 68 and fl[4] == 16, fl  # warm start short-circuits
+            else:
+                assert fl[1] == 1 and fl[2] == 1e-4, fl  # CFM + PGS, friction removed
         fo = O.OracleWorld(w)
 
         def fwd(s, ff):
@@ -405,7 +417,7 @@ def test_broken_state_jacobians_vs_finite_differences(oracle_built, kind):
             assert np.abs(F[b][rows] - fd_F[rows]).max() <= 1e-6 * np.abs(fd_F[rows]).max(), (name, rows)
 
 
-@pytest.mark.parametrize("name", ["half_cheetah", "capsule_edge", "atlas_broken"])
+@pytest.mark.parametrize("name", ["half_cheetah", "capsule_edge", "atlas_broken", "atlas_mesh_broken"])
 def test_constraint_force_jacobian_vs_finite_differences(oracle_built, name):
     """getJacobianOfConstraintForce (BackpropSnapshot.cpp:2723) for POSITION /
     VELOCITY / FORCE from the oracle (the matrix the GPU's
@@ -420,10 +432,13 @@ def test_constraint_force_jacobian_vs_finite_differences(oracle_built, name):
         st, f = models.capsule_edge_states(8, seed=1)
         picks = [2, 6]
     else:
-        w, _, st, f, _ = models.broken_states("atlas")
+        w, _, st, f, caches = models.broken_states("atlas_mesh" if name == "atlas_mesh_broken" else "atlas")
         picks = list(range(st.shape[0]))
+    if name != "atlas_mesh_broken":
+        caches = [None] * st.shape[0]
     n = w.getNumDofs()
     o = O.OracleWorld(w)
+    _seed_caches(o, caches)
     o.forward(st, f)
     J = o.constraint_force_jacobians()
     for b in picks:
@@ -433,6 +448,7 @@ def test_constraint_force_jacobian_vs_finite_differences(oracle_built, name):
 
         def fc(s, ff):
             oo = O.OracleWorld(w)
+            _seed_caches(oo, [caches[b]])
             oo.forward(s[None], ff[None])
             return O.lcp_fc(oo, 0)[:nc]
         fd = np.zeros((nc, 3 * n))

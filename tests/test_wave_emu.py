@@ -79,6 +79,38 @@ def test_lcp_wave_kernels_r1_r2():
         assert np.abs(xc - ref).max() <= 1e-8 * np.abs(ref).max(), m
 
 
+def test_dantzig_disagreement_fixture_emulated():
+    """tests/golden/dantzig_disagreements.npz (tools/dantzig_reconcile.py: the
+    bench Atlas LCPs on which the device, the oracle's restatement and the
+    reference's compiled dSolveLCP do not all agree) through the host build
+    of waveDantzigR (R = 1): the effective outcome (success AND
+    isLCPSolutionValid) equals the reference's, with x within 1e-9 when
+    valid, or the problem is ambiguous for the reference itself (1e-15
+    perturbations).  A sample of 24 problems (the emulation runs ~1 s each)."""
+    from test_gpu_lcp import FIXTURE, classify
+    exe = wave_emu.build("lcp_wave_emu")
+    d = np.load(FIXTURE)
+    P = len(d["n"])
+    pick = np.linspace(0, P - 1, min(P, 24)).astype(int)
+    txt = [str(len(pick))]
+    for k in pick:
+        m = int(d["n"][k])
+        txt += [str(m), wave_emu._fmt(d["A"][k, :m * m]), wave_emu._fmt(d["b"][k, :m]), wave_emu._fmt(d["lo"][k, :m]),
+                wave_emu._fmt(d["hi"][k, :m]), wave_emu._fmt(d["fi"][k, :m], True), wave_emu._fmt(np.zeros(m))]
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0", LCP_EMU_DANTZIG_ONLY="1")
+    r = subprocess.run([exe], input="\n".join(txt), capture_output=True, text=True, timeout=900, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    kinds = {"agree": 0, "ambiguous": 0}
+    for k, ln in zip(pick, r.stdout.splitlines()):
+        t = ln.split()
+        m = int(d["n"][k])
+        assert int(t[0]) == 1 and int(t[1]) == m
+        ok, x = bool(int(t[2])), np.array(t[3:3 + m], dtype=float)
+        A = d["A"][k, :m * m].reshape(m, m)
+        kinds[classify(k, m, A, d["b"][k, :m], d["lo"][k, :m], d["hi"][k, :m], d["fi"][k, :m], ok, x, d)] += 1
+    print(kinds)
+
+
 def test_pgs_fast_clamp_matches_reference_chain():
     """The PGS fallback on contact-layout rows clamps with v_max / v_min
     (lcp_wave.cuh wavePgsR) and re-runs with the reference's

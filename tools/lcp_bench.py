@@ -18,7 +18,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
 PROB = os.path.join(ROOT, "dbg", "lcp_problems.npz")
-LIB = os.environ.get("LCP_BENCH_LIB", os.path.join(ROOT, "dbg", "liblcp_bench.so"))
+LIB = os.environ.get("LCP_BENCH_LIB", os.path.join(ROOT, "tests", "cpp", "liblcp_bench.so"))
 NMAX = 48
 REC = 128
 

@@ -53,7 +53,7 @@ enum nimble_shape_type {
 
 #define NIMBLE_MAX_BODIES 64
 #define NIMBLE_MAX_DOFS 64
-#define NIMBLE_MAX_SHAPES 32
+#define NIMBLE_MAX_SHAPES 64
 /* Max contact points per world per step and LCP rows (3 per frictional
  * contact, dart/constraint/ContactConstraint.cpp:147 mDim = 3): the layout of
  * the snapshot and the LCP cache.  The device solves LCPs of up to

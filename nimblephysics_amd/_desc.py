@@ -10,7 +10,7 @@ P_F64 = C.POINTER(C.c_double)
 
 NIMBLE_MAX_BODIES = 64
 NIMBLE_MAX_DOFS = 64
-NIMBLE_MAX_SHAPES = 32
+NIMBLE_MAX_SHAPES = 64
 NIMBLE_MAX_CONTACTS = 42
 NIMBLE_MAX_LCP = 3 * NIMBLE_MAX_CONTACTS
 

@@ -1107,21 +1107,28 @@ __device__ void devGuess(typename Space<kLds>::dptr poolIn, int m, int n, lds_do
 // bit for bit those.  Writes pinv(Q)^T rows to PTG (row col = column col of
 // pinv(Q), permuted) and the solves z_c to Zs (row c, for the imprecision
 // map), both in HBM.
-__device__ __forceinline__ void pinvColumnsStaged(const Cod& c, double* Z, double* PTG, double* Zs, int lane) {
-  const int nc = c.n;
-  const double* F = c.A;
-  const int kmax = c.kmax;
-  const int r = uni(*c.rank);
+__device__ __forceinline__ void pinvColumnsStaged(const lds_double* F, const lds_double* W, lds_double* Z, int nc,
+                                                  double* PTG, double* Zs, int lane) {
+  // the COD workspace as carveCod lays it out (vd vn zd zn perm rank), typed
+  // as LDS so that every access below is an LDS instruction
+  const lds_double* vdA = W;
+  const lds_double* vnA = W + nc;
+  const lds_double* zdA = W + 2 * nc;
+  const lds_double* znA = W + 3 * nc;
+  const lds_int* perm = (const lds_int*)(W + 4 * nc);
+  const lds_int* rankP = (const lds_int*)(W + 4 * nc + (nc + 1) / 2 + 1);
+  const int kmax = nc;
+  const int r = uni(*rankP);
   for (int c0 = 0; c0 < nc; c0 += WAVE) {
     const int col = c0 + lane;
     const int cnt = nc - c0 < WAVE ? nc - c0 : WAVE;
     for (int i = 0; i < nc; i++) Z[i * 65 + lane] = i == col ? 1.0 : 0.0;
     WSYNC();
-    double* z = Z + lane;
+    lds_double* z = Z + lane;
     for (int k = 0; k < kmax; k++) {
-      const double vnorm = unid(c.vn[k]);
+      const double vnorm = unid(vnA[k]);
       if (!(vnorm > 0)) continue;
-      const double vd = unid(c.vd[k]);
+      const double vd = unid(vdA[k]);
       double sc = vd * z[k * 65];
       int i = k + 1;
       for (; i + 8 <= nc; i += 8) {
@@ -1145,9 +1152,9 @@ __device__ __forceinline__ void pinvColumnsStaged(const Cod& c, double* Z, doubl
     }
     for (int j = r; j < nc; j++) z[j * 65] = 0.0;
     for (int i = 0; i < r && r < nc; i++) {
-      const double vn = unid(c.zn[i]);
+      const double vn = unid(znA[i]);
       if (vn == 0) continue;
-      const double zd = unid(c.zd[i]);
+      const double zd = unid(zdA[i]);
       double sc = z[i * 65] * zd;
       for (int j = r; j < nc; j++) sc += z[j * 65] * F[i * nc + j];
       sc = 2 * sc / vn;
@@ -1161,7 +1168,7 @@ __device__ __forceinline__ void pinvColumnsStaged(const Cod& c, double* Z, doubl
       const int j = t / nc, i = t - j * nc;
       const double v = Z[i * 65 + j];
       Zs[(size_t)c0 * nc + t] = v;
-      PTG[(size_t)(c0 + j) * nc + c.perm[i]] = v;
+      PTG[(size_t)(c0 + j) * nc + perm[i]] = v;
     }
     WSYNC();
   }
@@ -1255,7 +1262,7 @@ __device__ void backwardPrecompute(const ModelDev& md, lds_double* sIn, const La
     }
     carveCod(sW, sF, nc, nc, nc, cod);
     STAMP(49);
-    pinvColumnsStaged(cod, sZ, PTG, Zs, lane);
+    pinvColumnsStaged((const lds_double*)sF, (const lds_double*)sW, (lds_double*)sZ, nc, PTG, Zs, lane);
   } else {
   if (!reuse) codFactorAny<kLds, R>(sp<kLds>(P.M1), sp<kLds>(P.scr), nc, nc, nc, sp<kLds>(vv), lane, stage, stageCap);
   STAMP(49);
@@ -1838,13 +1845,26 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
       // off-chip pools: the LDL^T factor in the launch's LDS stage when it
       // fits (every pivot's triangular solves and its row / column shifts
       // read and write it; A is read a row at a time and stays in HBM)
-      double* Ld = (stage != nullptr && m * (m | 1) <= stageCap) ? (double*)stage : (double*)P.M2;
 #ifdef NIMBLE_STAGE_TIMING
-      ok = waveDantzigR<kLds, R>(m, spc<kLds>(P.A), sp<kLds>(Ld), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane,
-                                 g_stamp ? g_stamp + SLOT_DANTZIG : nullptr);
+      double* dbgDz = g_stamp ? g_stamp + SLOT_DANTZIG : nullptr;
 #else
-      ok = waveDantzigR<kLds, R>(m, spc<kLds>(P.A), sp<kLds>(Ld), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane);
+      double* dbgDz = nullptr;
 #endif
+      const int ldL = m | 1, nPk = m * (m + 1) / 2;
+      if (stage != nullptr && m * ldL + nPk + m <= stageCap) {
+        // L, A's packed lower triangle and the scatter vector all in the
+        // stage: every Dantzig access an LDS instruction
+        lds_double* sL = stage;
+        lds_double* sA = stage + m * ldL;
+        lds_double* sS = sA + nPk;
+        for (int i = 0; i < m; i++)
+          for (int j = lane; j <= i; j += WAVE) sA[i * (i + 1) / 2 + j] = P.A[i * m + j];
+        WSYNC();
+        ok = waveDantzigR<true, R, true>(m, sA, sL, sS, xd, bR, loR, hiR, fiR, lane, dbgDz);
+      } else {
+        double* Ld = (stage != nullptr && m * ldL <= stageCap) ? (double*)stage : (double*)P.M2;
+        ok = waveDantzigR<kLds, R>(m, spc<kLds>(P.A), sp<kLds>(Ld), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane, dbgDz);
+      }
     }
     if (ok) {
 #pragma unroll

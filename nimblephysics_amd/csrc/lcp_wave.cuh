@@ -554,7 +554,10 @@ __device__ double codSolveWave(typename Space<kLds>::dptr Ain, typename Space<kL
 }
 
 // ---------------------------------------------------------------------------
-template <int R>
+// kPk: A held as its packed lower triangle (element (a, b), a >= b, at
+// a (a + 1) / 2 + b): the wide kernels' LDS stage holds it beside L, where
+// the full matrix does not fit (same values, so the same results)
+template <int R, bool kPk = false>
 struct WaveDantzig {
   int n, nC, nN, lane, ldL;
   // A: the problem matrix (n x n, symmetric), read in place: slot i of the
@@ -592,11 +595,19 @@ struct WaveDantzig {
   // lane's slot s / of its C entry / the diagonal
   // (cross-lane reads are kept out of lane-divergent expressions: callers
   // take the row offset first, then index with it)
-  __device__ __forceinline__ int rowOff(int i) const { return rdliR(p, i) * n; }
-  __device__ __forceinline__ double ArowAt(int ro, int s) const { return A[ro + (row(s) < n ? p[s] : 0)]; }
+  // `ro` is the row token of rowOff: the row's offset (full) or index (packed)
+  __device__ __forceinline__ int rowOff(int i) const { return kPk ? rdliR(p, i) : rdliR(p, i) * n; }
+  __device__ __forceinline__ double Ael(int ro, int c) const {
+    if (kPk) {
+      const int a = ro > c ? ro : c, b = ro > c ? c : ro;
+      return A[a * (a + 1) / 2 + b];
+    }
+    return A[ro + c];
+  }
+  __device__ __forceinline__ double ArowAt(int ro, int s) const { return Ael(ro, row(s) < n ? p[s] : 0); }
   __device__ __forceinline__ double Adiag(int i) const {
     const int pi = rdliR(p, i);
-    return A[pi * n + pi];
+    return kPk ? A[pi * (pi + 1) / 2 + pi] : A[pi * n + pi];
   }
   // p of the slot this lane's C entry (slot s) names
   __device__ __forceinline__ int pOfC(int s) const { return gatherRi(p, C[s] & (64 * R - 1)); }
@@ -741,7 +752,7 @@ struct WaveDantzig {
 #pragma unroll
     for (int s = 0; s < R; s++) {
       const int pc = pOfC(s);
-      Dell[s] = row(s) < nC ? A[ro + pc] : 0.0;
+      Dell[s] = row(s) < nC ? Ael(ro, pc) : 0.0;
     }
   }
   __device__ __forceinline__ void transferFromNtoC(int i) {
@@ -840,7 +851,7 @@ struct WaveDantzig {
 #pragma unroll
         for (int s = 0; s < R; s++) {
           const int pc = pOfC(s);
-          a[s] = row(s) < n2 ? -A[ro + pc] : 0.0;  // A symmetric
+          a[s] = row(s) < n2 ? -Ael(ro, pc) : 0.0;  // A symmetric
           if (row(s) == 0) a[s] += 1.0;
         }
         ldltAddTL(0, n2, a);
@@ -864,7 +875,7 @@ struct WaveDantzig {
 #pragma unroll
         for (int s = 0; s < R; s++) {
           a[s] = 0.0;
-          if (row(s) >= r && row(s) < n2) a[s] = sacc[s] - A[ro + pc[s]];  // A symmetric
+          if (row(s) >= r && row(s) < n2) a[s] = sacc[s] - Ael(ro, pc[s]);  // A symmetric
           if (row(s) == r) a[s] += 1.0;
         }
         ldltAddTL(r, n2 - r, a);
@@ -958,7 +969,7 @@ struct WaveDantzig {
 
 // A (n x n, symmetric, read only), L (n x (n|1) scratch), scr (>= n); problem
 // vectors row-distributed; returns success and x (row-distributed).
-template <bool kLds, int R>
+template <bool kLds, int R, bool kPk = false>
 __device__ bool waveDantzigR(int n, typename Space<kLds>::cdptr Ain, typename Space<kLds>::dptr Lin,
                              typename Space<kLds>::dptr scrIn, double (&xOut)[R], const double (&b)[R],
                              const double (&lo)[R], const double (&hi)[R], const int (&findex)[R], int lane,
@@ -967,7 +978,7 @@ __device__ bool waveDantzigR(int n, typename Space<kLds>::cdptr Ain, typename Sp
   const double* A = (const double*)Ain;
   double* Lbuf = (double*)Lin;
   double* scr = (double*)scrIn;
-  WaveDantzig<R> D;
+  WaveDantzig<R, kPk> D;
   int pivots = 0;
   D.n = n; D.nC = 0; D.nN = 0; D.lane = lane; D.ldL = n | 1;
   D.A = A; D.L = Lbuf; D.scr = scr;
@@ -1056,7 +1067,7 @@ __device__ bool waveDantzigR(int n, typename Space<kLds>::cdptr Ain, typename Sp
             const double dxj = rdlR(D.deltaX, j);
             const int ro = D.rowOff(j);
 #pragma unroll
-            for (int s = 0; s < R; s++) acc[s] += A[ro + colA[s]] * dxj;  // A symmetric: row j
+            for (int s = 0; s < R; s++) acc[s] += D.Ael(ro, colA[s]) * dxj;  // A symmetric: row j
           }
           const int roI = D.rowOff(i);
 #pragma unroll

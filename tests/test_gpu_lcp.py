@@ -7,9 +7,11 @@ over the bench Atlas' LCPs).
 What reaches the step is the effective outcome, dSolveLCP's success AND
 LCPUtils::isLCPSolutionValid (BoxedLcpConstraintSolver.cpp:466-521).  Per
 problem: the device's effective outcome equals the reference's, and then x
-agrees to 1e-9 where both are valid; or the reference itself gives both
-outcomes under 1e-15-relative perturbations of A (ambiguous: rank-deficient
-A, both feet flat).  Run through the stand-alone harness
+agrees to 1e-9 where both are valid, or both are solutions of a degenerate
+LCP (rank-deficient A, x_device - x_ref in its null space; the step's
+re-standardisation then maps either to the same x); or the reference itself
+gives both outcomes under 1e-15-relative perturbations of A (ambiguous:
+rank-deficient A, both feet flat).  Run through the stand-alone harness
 tests/cpp/liblcp_bench.so (tools/lcp_bench.hip: the product's lcp_wave.cuh,
 A in LDS as in the forward kernel).
 """
@@ -40,7 +42,12 @@ def classify(k, m, A, b, lo, hi, fi, ok, x, d):
         if eff:
             rx = d["ref_x"][k, :m]
             err = np.abs(x - rx).max() / max(1.0, np.abs(rx).max())
-            assert err <= 1e-9, (k, err)
+            if err > 1e-9:
+                # both valid yet apart: a rank-deficient A whose LCP has a set of
+                # solutions; the difference must lie in A's null space (same w)
+                res = np.abs(A @ (x - rx)).max() / max(1.0, np.abs(A).max() * np.abs(rx).max())
+                assert res <= 1e-12 and np.linalg.matrix_rank(A) < m, (k, err, res)
+                return "nonunique"
         return "agree"
     amb = int(d["ref_ambiguous"][k])
     if amb < 0 and O.ref_lib() is not None:
@@ -72,7 +79,7 @@ def test_dantzig_disagreements_on_device():
     assert rc == 0
     torch.cuda.synchronize()
     o = out.cpu().numpy()
-    kinds = {"agree": 0, "ambiguous": 0}
+    kinds = {"agree": 0, "ambiguous": 0, "nonunique": 0}
     for k in range(P):
         m = int(d["n"][k])
         A = d["A"][k, :m * m].reshape(m, m)

@@ -39,7 +39,7 @@ def _run_both(world, batch, seed):
     return (ref_next, ref_gs, ref_gf), (nxt.detach().cpu().numpy(), tst.grad.cpu().numpy(), tf.grad.cpu().numpy())
 
 
-@pytest.mark.parametrize("name,batch", [("cartpole", 256), ("kr5", 128), ("atlas_air", 64)])
+@pytest.mark.parametrize("name,batch", [("cartpole", 1024), ("kr5", 128), ("atlas_air", 64)])
 def test_no_contact_parity(name, batch):
     world = {"cartpole": models.cartpole_world, "kr5": models.kr5_world,
              "atlas_air": lambda: models.atlas_world(with_ground=False)}[name]()

@@ -100,7 +100,7 @@ def test_dantzig_disagreement_fixture_emulated():
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0", LCP_EMU_DANTZIG_ONLY="1")
     r = subprocess.run([exe], input="\n".join(txt), capture_output=True, text=True, timeout=900, env=env)
     assert r.returncode == 0, r.stderr[-4000:]
-    kinds = {"agree": 0, "ambiguous": 0}
+    kinds = {"agree": 0, "ambiguous": 0, "nonunique": 0}
     for k, ln in zip(pick, r.stdout.splitlines()):
         t = ln.split()
         m = int(d["n"][k])

@@ -87,10 +87,18 @@ def classify():
             amb = ref_ambiguous(A, b, lo, hi, fi, seed=k)
         if ge != re_:
             tally["eff_gpu_vs_ref_disagree_ambiguous" if amb else "eff_gpu_vs_ref_disagree_unambiguous"] += 1
-        elif ge and re_:
+        xdiff = False
+        if ge and re_:
             e = float(np.abs(gx - rx).max() / max(1.0, np.abs(rx).max()))
             tally["both_valid_x_max_rel_err"] = max(tally["both_valid_x_max_rel_err"], e)
-        if not (gok == ook == rok) or not (ge == oe == re_):
+            if e > 1e-9:
+                # both solve the LCP: on a rank-deficient A the solution set is
+                # not a point -- x_gpu - x_ref lies in A's null space
+                xdiff = True
+                tally["both_valid_x_differ"] = tally.get("both_valid_x_differ", 0) + 1
+                res = float(np.abs(A @ (gx - rx)).max() / max(1.0, np.abs(A).max() * np.abs(rx).max()))
+                tally["both_valid_x_differ_null_residual"] = max(tally.get("both_valid_x_differ_null_residual", 0.0), res)
+        if not (gok == ook == rok) or not (ge == oe == re_) or xdiff:
             keep.append(k)
             rows.append({"problem": k, "m": m, "rank": int(np.linalg.matrix_rank(A)), "gpu_ok": gok, "gpu_valid": ge,
                          "oracle_ok": bool(ook), "oracle_valid": oe, "ref_ok": bool(rok), "ref_valid": re_,

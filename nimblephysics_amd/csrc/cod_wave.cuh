@@ -290,8 +290,24 @@ __device__ __forceinline__ void codFactorR(typename Space<kLds>::dptr Ain, typen
 #pragma unroll 8
           for (int i = k; i < m; i++) sc += v[i] * A[i * ld + j];
           sc = 2 * sc / vnorm;
-#pragma unroll 8
-          for (int i = k; i < m; i++) {
+          // eight rows' loads before their stores (A and v may alias for the
+          // compiler: element by element, every load would wait for the
+          // previous store); same operations in the same order
+          int i = k;
+          for (; i + 8 <= m; i += 8) {
+            double av[8], vv[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) { av[u] = A[(i + u) * ld + j]; vv[u] = v[i + u]; }
+#pragma unroll
+            for (int u = 0; u < 8; u++) asm volatile("" : "+v"(av[u]), "+v"(vv[u]));
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+              const double a = av[u] - sc * vv[u];
+              A[(i + u) * ld + j] = a;
+              if (i + u > k) nrm += a * a;
+            }
+          }
+          for (; i < m; i++) {
             const double a = A[i * ld + j] - sc * v[i];
             A[i * ld + j] = a;
             if (i > k) nrm += a * a;

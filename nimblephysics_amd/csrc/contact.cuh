@@ -1143,7 +1143,19 @@ __device__ __forceinline__ void pinvColumnsStaged(const lds_double* F, const lds
       for (; i < nc; i++) sc += F[i * nc + k] * z[i * 65];
       sc = 2 * sc / vnorm;
       z[k * 65] -= sc * vd;
-      for (i = k + 1; i < nc; i++) z[i * 65] -= sc * F[i * nc + k];
+      // (eight elements' loads issued before their stores: the compiler cannot
+      // tell Z from F, and would otherwise order every load after the
+      // previous element's store -- one LDS round trip per element)
+      for (i = k + 1; i + 8 <= nc; i += 8) {
+        double fv[8], zv[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) { fv[u] = F[(i + u) * nc + k]; zv[u] = z[(i + u) * 65]; }
+#pragma unroll
+        for (int u = 0; u < 8; u++) asm volatile("" : "+v"(fv[u]), "+v"(zv[u]));
+#pragma unroll
+        for (int u = 0; u < 8; u++) z[(i + u) * 65] = zv[u] - sc * fv[u];
+      }
+      for (; i < nc; i++) z[i * 65] -= sc * F[i * nc + k];
     }
     for (int i = r - 1; i >= 0; i--) {
       double sc = z[i * 65];

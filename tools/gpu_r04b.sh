@@ -20,3 +20,5 @@ timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/b
 python -c "import json;d=json.load(open('$O/bench_$TAG.json'));m=d['atlas_mesh'];print('value',d['value'],'fwd',d['kernels_ms']['forward'],'bwd',d['kernels_ms']['backward'],'| mesh',m['value'],m['kernels_ms']['forward'],m['kernels_ms']['backward'])"
 STAGE_WORKLOAD=atlas_mesh NIMBLE_AMD_LIB=dbg/libnimble_dbg.so STAGE_HIST_OUT=$O/stage_hist_mesh_$TAG.json timeout -k 10 200 python tools/stage_timing.py > $O/stage_mesh_$TAG.log 2>&1 || { echo MESH STAGE FAILED; tail -20 $O/stage_mesh_$TAG.log; exit 1; }
 tail -1 $O/stage_mesh_$TAG.log
+NIMBLE_AMD_LIB=dbg/libnimble_dbg.so BUCKETS_OUT=mesh_buckets_$TAG.json timeout -k 10 200 python tools/mesh_buckets.py > $O/mesh_buckets_$TAG.log 2>&1 || { echo BUCKETS FAILED; tail -20 $O/mesh_buckets_$TAG.log; exit 1; }
+grep -v amdgpu.ids $O/mesh_buckets_$TAG.log | sed -n '/step 1/,/step 2/p' | cut -c1-200

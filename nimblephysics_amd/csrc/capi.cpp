@@ -34,6 +34,12 @@ struct nimble_world {
   // LCPs with more rows than this run in the two-rows-per-lane kernels
   // (nimble_forward_wide_kernel / nimble_backward_wide_kernel)
   int deferRows = 64;
+  // the forward's own threshold: worlds whose LCP pool does not fit the
+  // one-row kernel's LDS (more rows than fwdDeferRows <= deferRows) go to
+  // the big-LDS wide kernel, which takes up to 64 rows with the pool in its
+  // LDS stage (the one-row code and task board) and more with two rows per
+  // lane; the backward keeps deferRows
+  int fwdDeferRows = 64;
   Layout fwdWide{};     // the wide forward kernel's layout (LDS stage, see nimble_world_create)
   size_t wideLds = 0;   // its LDS bytes
   int jacWsDoubles = 0;  // per-workgroup LCP workspace of the Jacobian launch
@@ -341,9 +347,23 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
       const size_t end = (size_t)(w->fwd.pool + cap) * sizeof(double);
       if (end > w->wideLds) w->wideLds = end;
     }
+    // worlds of up to 64 rows whose pool fits the stage: the wide kernel
+    // steps them with the pool on chip (contactStage), so the one-row kernel
+    // defers every world its own pool does not hold
+    w->fwdDeferRows = w->deferRows;
+    if (w->fwdWide.stageCap > 0 && fwdPoolDoublesHost(64, m.n) <= w->fwdWide.stageCap && fwdRows < w->fwdDeferRows) {
+      const char* ef = getenv("NIMBLE_AMD_WIDE_POOL");
+      if (!(ef && atoi(ef) == 0)) w->fwdDeferRows = fwdRows;
+    }
+    // NIMBLE_AMD_FWD_DEFER_ROWS (tests): a lower forward threshold sends
+    // smaller LCPs through the wide kernel's on-chip-pool path as well
+    if (const char* e = getenv("NIMBLE_AMD_FWD_DEFER_ROWS")) {
+      const int d = atoi(e);
+      if (d >= 0 && d < w->fwdDeferRows && w->fwdWide.stageCap > 0) w->fwdDeferRows = d;
+    }
     if (getenv("NIMBLE_AMD_VERBOSE"))
-      fprintf(stderr, "nimble_amd: wide forward LDS %zu B (stage %d doubles of %d for %d rows)\n", w->wideLds,
-              w->fwdWide.stageCap, need, mc);
+      fprintf(stderr, "nimble_amd: wide forward LDS %zu B (stage %d doubles of %d for %d rows), forward defers > %d rows\n",
+              w->wideLds, w->fwdWide.stageCap, need, mc, w->fwdDeferRows);
   }
   if (getenv("NIMBLE_AMD_VERBOSE"))
     fprintf(stderr, "nimble_amd: LDS forward %d B (pool rows %d), backward %d B (pool rows %d), max rows %d\n",
@@ -354,7 +374,7 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
   if (m.numPairs > 0) {
     int ws = 0;
     // (the two-rows-per-lane forward always works in HBM)
-    if (mcap > poolRows || mcap > w->deferRows) {
+    if (mcap > poolRows || mcap > w->fwdDeferRows) {
       const int a = fwdPoolDoublesHost(mcap, m.n), b = bwdPoolDoublesHost(mcap, m.n);
       ws = a > b ? a : b;
     }
@@ -432,12 +452,13 @@ int nimble_forward(nimble_world_t w, int32_t batch, const double* state, const d
     hipLaunchKernelGGL(nimble_forward_kernel, dim3(cnt), dim3(fwdThreads), lds, st, w->dev, w->fwd,
                        state + b0 * 2 * n, forces + b0 * n, lcp_cache + (size_t)b0 * w->cacheDoubles,
                        next_state + b0 * 2 * n, snapshot + (size_t)b0 * w->snapDoubles, w->snapDoubles,
-                       w->cacheDoubles, w->deferRows);
+                       w->cacheDoubles, w->fwdDeferRows);
     HIP_TRY(hipGetLastError());
-    // the worlds whose LCP has more rows than one per lane (or than the
-    // test threshold): stepped by the two-rows-per-lane kernel
-    if (w->host.numPairs > 0 && w->maxRows > w->deferRows) {
-      hipLaunchKernelGGL(nimble_forward_wide_kernel, dim3(cnt), dim3(64), w->wideLds, st, w->dev, w->fwdWide,
+    // the worlds whose LCP pool the one-row kernel does not hold on chip (or
+    // more rows than the test threshold): stepped by the big-LDS wide kernel
+    // (two waves: the LCP task board for the worlds of up to 64 rows)
+    if (w->host.numPairs > 0 && w->maxRows > w->fwdDeferRows) {
+      hipLaunchKernelGGL(nimble_forward_wide_kernel, dim3(cnt), dim3(128), w->wideLds, st, w->dev, w->fwdWide,
                          state + b0 * 2 * n, forces + b0 * n, lcp_cache + (size_t)b0 * w->cacheDoubles,
                          next_state + b0 * 2 * n, snapshot + (size_t)b0 * w->snapDoubles, w->snapDoubles,
                          w->cacheDoubles);

@@ -1553,7 +1553,11 @@ __device__ __forceinline__ bool contactStage(const ModelDev& md, double* s, cons
   // the LCP workspace is in LDS when it fits the pool (the common case, LDS
   // instructions throughout), else in the world's HBM snapshot tail (always
   // for the wide problems of R = 2)
-  if (R == 1 && fwdPoolDoubles(m, n) <= L.poolCap)
+  if ((R == 1 && fwdPoolDoubles(m, n) <= L.poolCap) ||
+      (R > 1 && m <= 64 && L.stageCap > 0 && fwdPoolDoubles(m, n) <= L.stageCap))
+    // the pool on chip: the one-row kernel's own pool, or the wide kernel's
+    // LDS stage (which starts at the pool) for the worlds the one-row kernel
+    // deferred because its pool could not hold them
     contactLcp<true, 1>(md, sp<true>(s), L, lane, sp<true>(v1), spc<true>(ddq), cache, snap, sp<true>(s + L.pool),
                         nCon, m, helperOn);
   else

@@ -618,14 +618,19 @@ struct WaveDantzig {
     swapRegI(p, i1, i2); swapRegI(state, i1, i2); swapRegI(findex, i1, i2);
     LP_END(prof, 0);
   }
-  // L x = B (unit lower), B row-distributed, first m entries.  The L
-  // entries of each lane are loaded 8 at a time ahead of the dependent
-  // readlane -> FMA chain (LDS latency paid once per 8 steps) with the
-  // triangle mask folded into them (0 where a lane must not change), so a
-  // step is a readlane and one unpredicated FMA: no exec-mask update that
-  // would wait on a vector compare.  0 * b_k leaves a lane unchanged only
-  // for finite b_k; a non-finite b_k (degenerate factor) re-runs the solve
-  // predicated, exactly as the reference's loop.
+  // L x = B (unit lower), B row-distributed, first m entries, in blocks of
+  // eight steps.  Per block the eight B entries are read once (readlanes
+  // issued together) and the block's own forward substitution runs on those
+  // wave-uniform values against the block's diagonal L entries (LDS
+  // broadcasts, loaded ahead); every lane then applies the eight known values
+  // to its rows.  A step is no longer a readlane -> FMA -> readlane chain
+  // (~150 clocks a step measured), and every B entry still receives its
+  // updates in the same order with the same operations (bit for bit the
+  // element-by-element substitution).  The L entries of each lane are masked
+  // with the triangle (0 where a lane must not change), so a lane step is one
+  // unpredicated FMA; 0 * b_k leaves a lane unchanged only for finite b_k: a
+  // non-finite b_k (degenerate factor) re-runs the solve predicated, exactly
+  // as the reference's loop.
   __device__ __forceinline__ void solveL1(double (&B)[R], int m) {
     m = uni(m);
     LP_BEGIN();
@@ -639,13 +644,18 @@ struct WaveDantzig {
     for (int k0 = 0; k0 < m; k0 += 8) {
       double Lk[R][8];
       double Lv[R][8];
+      double Ld[8][8];
 #pragma unroll
       for (int s = 0; s < R; s++)
 #pragma unroll
         for (int u = 0; u < 8; u++) Lv[s][u] = L[rowOffL[s] + (k0 + u < m ? k0 + u : 0)];
+      // the block's strictly lower diagonal entries (wave-uniform)
+#pragma unroll
+      for (int a = 1; a < 8; a++)
+#pragma unroll
+        for (int u = 0; u < a; u++) Ld[a][u] = k0 + a < m ? L[(k0 + a) * ldL + k0 + u] : 0.0;
       // keep the loads unconditional and batched: all issued before any is
-      // consumed (one barrier per block -- a barrier per load made the
-      // wave wait for each load in turn)
+      // consumed
 #pragma unroll
       for (int s = 0; s < R; s++)
 #pragma unroll
@@ -654,13 +664,17 @@ struct WaveDantzig {
       for (int s = 0; s < R; s++)
 #pragma unroll
         for (int u = 0; u < 8; u++) Lk[s][u] = (row(s) > k0 + u && row(s) < m) ? Lv[s][u] : 0.0;
+      double bb[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) bb[u] = k0 + u < m ? rdlR(B, k0 + u) : 0.0;
+#pragma unroll
+      for (int a = 1; a < 8; a++)
+#pragma unroll
+        for (int u = 0; u < a; u++) bb[a] -= Ld[a][u] * bb[u];
 #pragma unroll
       for (int u = 0; u < 8; u++)
-        if (k0 + u < m) {
-          const double bk = rdlR(B, k0 + u);
 #pragma unroll
-          for (int s = 0; s < R; s++) B[s] -= Lk[s][u] * bk;
-        }
+        for (int s = 0; s < R; s++) B[s] -= Lk[s][u] * bb[u];
     }
     bool nonFinite = false;
 #pragma unroll
@@ -677,7 +691,7 @@ struct WaveDantzig {
     }
     LP_END(prof, 1);
   }
-  // L^T x = B
+  // L^T x = B, blocks of eight steps from the last row up (as solveL1)
   __device__ __forceinline__ void solveL1T(double (&B)[R], int m) {
     m = uni(m);
     LP_BEGIN();
@@ -691,10 +705,17 @@ struct WaveDantzig {
     for (int k0 = m - 1; k0 >= 0; k0 -= 8) {
       double Lk[R][8];
       double Lv[R][8];
+      double Ld[8][8];
 #pragma unroll
       for (int s = 0; s < R; s++)
 #pragma unroll
         for (int u = 0; u < 8; u++) Lv[s][u] = L[(k0 - u >= 0 ? k0 - u : 0) * ldL + colL[s]];
+      // block entries: step u (row k0 - u) updates row k0 - a (a > u) with
+      // L[k0 - u][k0 - a]
+#pragma unroll
+      for (int a = 1; a < 8; a++)
+#pragma unroll
+        for (int u = 0; u < a; u++) Ld[a][u] = k0 - a >= 0 ? L[(k0 - u) * ldL + k0 - a] : 0.0;
 #pragma unroll
       for (int s = 0; s < R; s++)
 #pragma unroll
@@ -703,13 +724,17 @@ struct WaveDantzig {
       for (int s = 0; s < R; s++)
 #pragma unroll
         for (int u = 0; u < 8; u++) Lk[s][u] = row(s) < k0 - u ? Lv[s][u] : 0.0;
+      double bb[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) bb[u] = k0 - u >= 0 ? rdlR(B, k0 - u) : 0.0;
+#pragma unroll
+      for (int a = 1; a < 8; a++)
+#pragma unroll
+        for (int u = 0; u < a; u++) bb[a] -= Ld[a][u] * bb[u];
 #pragma unroll
       for (int u = 0; u < 8; u++)
-        if (k0 - u >= 0) {
-          const double bk = rdlR(B, k0 - u);
 #pragma unroll
-          for (int s = 0; s < R; s++) B[s] -= Lk[s][u] * bk;
-        }
+        for (int s = 0; s < R; s++) B[s] -= Lk[s][u] * bb[u];
     }
     bool nonFinite = false;
 #pragma unroll

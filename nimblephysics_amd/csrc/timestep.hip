@@ -336,9 +336,11 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
           gs[93] = (double)(unsigned)__builtin_amdgcn_s_getreg(20 | (15 << 11));
         }
 #endif
-        collideWait(ct, CS_GO);
-        collideWorld(md, lds<true>(s), L, lane, snapshot + (size_t)env * snapDoubles + snEdge(n));
-        collidePost(ct, CS_DONE, lane);
+        if (R == 1) {
+          collideWait(ct, CS_GO);
+          collideWorld(md, lds<true>(s), L, lane, snapshot + (size_t)env * snapDoubles + snEdge(n));
+          collidePost(ct, CS_DONE, lane);
+        }  // (the wide kernel's worlds come with the one-row kernel's contacts)
 #ifdef NIMBLE_STAGE_TIMING
         double* hstamp = snapshot + (size_t)env * snapDoubles + snStamps(n);
 #else
@@ -410,7 +412,7 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
     if (md.numPairs > 0) {
       double* sn = snapshot + (size_t)env * snapDoubles;
       deferred = contactStage<R>(md, s, L, lane, v1, x, lcpCache + (size_t)env * cacheDoubles, sn,
-                                 sn + snapWorkspaceOffset(n), helperOn, helperOn, deferRows, R > 1);
+                                 sn + snapWorkspaceOffset(n), helperOn, helperOn && R == 1, deferRows, R > 1);
     } else if (lane < 8) {
       // a model without collision pairs still has a snapshot header (no
       // contacts, no rows, no clamping) for the getters to read
@@ -448,8 +450,10 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, const double* 
 }
 
 // the worlds nimble_forward_kernel deferred (snapshot status ST_DEFERRED),
-// two LCP rows per lane, from the one-row kernel's dynamics and contacts
-// (launched with one wave per world: nothing left for a helper).  (The same occupancy target as the one-row kernel:
+// from the one-row kernel's dynamics and contacts: up to 64 LCP rows with the
+// pool in the big LDS stage (the one-row code, the helper wave on the task
+// board), more with two rows per lane and the pool in HBM (the stage holding
+// the factorisations).  (The same occupancy target as the one-row kernel:
 // the non-inlined narrow-phase functions both kernels call are compiled once,
 // for the tighter of the two register budgets.)
 extern "C" __global__ void __launch_bounds__(2 * WAVE) __attribute__((amdgpu_waves_per_eu(2)))

@@ -161,13 +161,17 @@ def test_box_step_emulated(defer):
     assert np.abs(gf - rgf).max() <= 1e-9 * np.abs(rgf).max()
 
 
-def test_atlas_lcp_paths_emulated():
+@pytest.mark.parametrize("fwd_defer", [None, "0"])
+def test_atlas_lcp_paths_emulated(fwd_defer):
     """Atlas bench-sampler worlds through each answer of the LCP cascade --
     the short-circuit (14), Dantzig (0), the PGS fallback (10, 35) and the
     frictionless PGS (1) -- with the forward's two waves sharing the cascade
     on the task board (contact.cuh: Dantzig on the helper, the fallbacks on
     whichever wave is free): the same answers as the oracle's sequential
-    cascade, flags included."""
+    cascade, flags included.  With NIMBLE_AMD_FWD_DEFER_ROWS=0 every contact
+    world is deferred to the wide kernel, which steps it from the one-row
+    kernel's dynamics and contacts with the pool in its LDS stage (the path
+    of the mesh Atlas' 25-64-row worlds)."""
     world = models.atlas_world(True)
     st, f = models.random_states(world, 1024, seed=1000, q_scale=0.02, v_scale=0.05)
     idx = [0, 1, 10, 14, 35]
@@ -176,7 +180,7 @@ def test_atlas_lcp_paths_emulated():
     ref = ow.forward(st, f)
     g = np.random.default_rng(3).standard_normal(st.shape)
     rgs, rgf = ow.backward(g)
-    nxt, gs, gf, head = wave_emu.step(world, st, f, g)
+    nxt, gs, gf, head = wave_emu.step(world, st, f, g, {"NIMBLE_AMD_FWD_DEFER_ROWS": fwd_defer} if fwd_defer else None)
     paths = set()
     for i in range(len(idx)):
         fl = O.lcp_flags(ow, i)
@@ -207,6 +211,38 @@ def test_mesh_atlas_wide_step_emulated():
     # test_gpu_contact_parity.GRAD_FLOOR): 1e-9 of the largest element
     assert np.abs(gs - rgs).max() <= 1e-9 * np.abs(rgs).max() * 10
     assert np.abs(gf - rgf).max() <= 1e-9 * np.abs(rgf).max()
+
+
+def test_mesh_atlas_wide_lds_pool_emulated():
+    """Mesh-Atlas worlds whose LCP (39-45 rows) does not fit the one-row
+    kernel's LDS pool: deferred to the wide kernel, which steps them from the
+    one-row kernel's dynamics cache and contact hand-off with the pool in its
+    LDS stage and the helper wave on the task board -- the short-circuit
+    (22), Dantzig (20) and the fallback cascade (0) -- beside an 81-row world
+    on the two-rows-per-lane path (4), all against the oracle."""
+    from nimblephysics_amd import workloads
+    world = workloads.atlas_mesh_world(True)
+    st, f = workloads.random_states(world, 24, seed=1000, q_scale=0.02, v_scale=0.05)
+    idx = [0, 4, 20, 22]
+    st, f = st[idx], f[idx]
+    ow = O.OracleWorld(world)
+    ref = ow.forward(st, f)
+    g = np.random.default_rng(5).standard_normal(st.shape)
+    rgs, rgf = ow.backward(g)
+    nxt, gs, gf, head = wave_emu.step(world, st, f, g, {"NIMBLE_AMD_VERBOSE": "1"})
+    log = open(os.path.join("/tmp", f"nimble_wave_emu_{os.getuid()}.stderr")).read()
+    assert "forward defers > 24 rows" in log, log[-400:]
+    paths = set()
+    for i in range(len(idx)):
+        fl = O.lcp_flags(ow, i)
+        m = len(O.lcp_debug(ow, i, max_rows=O.MAX_LCP)[0])
+        assert int(head[i, 1]) == m, idx[i]
+        assert (head[i, 6], head[i, 7], head[i, 4]) == (fl[0], fl[1], fl[2]), idx[i]
+        paths.add("C" if fl[0] else "F" if fl[1] else "P" if fl[2] > 0 else "D")
+        assert np.abs(nxt[i] - ref[i]).max() <= 1e-11, idx[i]
+        assert np.abs(gs[i] - rgs[i]).max() <= 1e-9 * np.abs(rgs[i]).max() * 10, idx[i]
+        assert np.abs(gf[i] - rgf[i]).max() <= 1e-9 * np.abs(rgf[i]).max(), idx[i]
+    assert {"C", "D"} <= paths and ("F" in paths or "P" in paths)
 
 
 def test_snapshot_layout_matches_pool_sizes():

@@ -15,6 +15,9 @@ grep -E "passed|failed|FAILED" $O/gpu_tests_$TAG.log | tail -6
 if [ -f tests/cpp/liblcp_bench.so ] && [ -z "$NO_MICRO" ]; then
   timeout -k 10 120 python tools/lcp_bench.py run > $O/lcp_micro_$TAG.log 2>&1 || { echo MICRO FAILED; tail $O/lcp_micro_$TAG.log; exit 1; }
   head -1 $O/lcp_micro_$TAG.log
+  grep "n=24" -A1 $O/lcp_micro_$TAG.log
+  timeout -k 10 120 python tools/lcp_bench.py run_wide > $O/lcp_wide_$TAG.log 2>&1 || { echo WIDE MICRO FAILED; tail $O/lcp_wide_$TAG.log; exit 1; }
+  grep -v amdgpu $O/lcp_wide_$TAG.log | head -3
 fi
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_$TAG.json 2> $O/bench_$TAG.err || { echo BENCH FAILED; tail -20 $O/bench_$TAG.err; exit 1; }
 python -c "import json;d=json.load(open('$O/bench_$TAG.json'));m=d['atlas_mesh'];print('value',d['value'],'fwd',d['kernels_ms']['forward'],'bwd',d['kernels_ms']['backward'],'| mesh',m['value'],m['kernels_ms']['forward'],m['kernels_ms']['backward'])"

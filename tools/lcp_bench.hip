@@ -85,3 +85,58 @@ extern "C" int lcp_bench_launch(int P, int nmax, int nl, const int* nArr, const 
                      out);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
+
+// The wide kernels' Dantzig (R = 2, up to 128 rows) as the forward stages it:
+// L, A's packed lower triangle and the scatter vector in LDS.  One problem
+// per 64-lane workgroup; per problem: ok, clocks, pivots, the per-phase split
+// (LCP_PROFILE: swap, solveL1, solveL1T, ldltRemove, w_i, pivot body), x.
+extern "C" __global__ void __launch_bounds__(64)
+lcp_bench_wide_kernel(int nmax, int nl, const int* nArr, const double* Ag, const double* bg, const double* log_,
+                      const double* hig, const int* fig, double* out) {
+  extern __shared__ double ldsbuf[];
+  const int lane = threadIdx.x;
+  const int pb = blockIdx.x;
+  const int n = nArr[pb];
+  lds_double* L = (lds_double*)ldsbuf;
+  lds_double* Ap = L + nl * (nl | 1);
+  lds_double* scr = Ap + nl * (nl + 1) / 2;
+  double* o = out + (size_t)pb * Rec::SIZE;
+  for (int i = 0; i < n; i++)
+    for (int j = lane; j <= i; j += 64) Ap[i * (i + 1) / 2 + j] = Ag[(size_t)pb * nmax * nmax + i * n + j];
+  __syncthreads();
+  double b[2], lo[2], hi[2], x[2];
+  int fi[2];
+  for (int s = 0; s < 2; s++) {
+    const int r = lane + 64 * s;
+    b[s] = r < n ? bg[pb * nmax + r] : 0.0;
+    lo[s] = r < n ? log_[pb * nmax + r] : 0.0;
+    hi[s] = r < n ? hig[pb * nmax + r] : 0.0;
+    fi[s] = r < n ? fig[pb * nmax + r] : -1;
+  }
+  __shared__ double dshared[24];
+  if (lane < 24) dshared[lane] = 0.0;
+  __syncthreads();
+  const long long t0 = __builtin_amdgcn_s_memtime();
+  const bool ok = waveDantzigR<true, 2, true>(n, Ap, L, scr, x, b, lo, hi, fi, lane, dshared);
+  const long long t1 = __builtin_amdgcn_s_memtime();
+  __syncthreads();
+  if (lane == 0) {
+    o[Rec::OK_D] = ok ? 1 : 0;
+    o[Rec::CLK_D] = (double)(t1 - t0);
+    o[Rec::PIV] = dshared[0];
+    o[Rec::PIVROW] = dshared[1];
+    for (int k = 0; k < 8; k++) o[Rec::PROF + k] = dshared[2 + k];
+  }
+  for (int s = 0; s < 2; s++) {
+    const int r = lane + 64 * s;
+    if (r < n && 16 + r < Rec::SIZE) o[16 + r] = x[s];
+  }
+}
+
+extern "C" int lcp_bench_wide_launch(int P, int nmax, int nl, const int* nArr, const double* A, const double* b,
+                                     const double* lo, const double* hi, const int* fi, double* out, void* stream) {
+  const size_t ldsBytes = (size_t)(nl * (nl | 1) + nl * (nl + 1) / 2 + nl + 8) * sizeof(double);
+  hipLaunchKernelGGL(lcp_bench_wide_kernel, dim3(P), dim3(64), ldsBytes, (hipStream_t)stream, nmax, nl, nArr, A, b, lo,
+                     hi, fi, out);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}

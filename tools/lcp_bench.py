@@ -110,6 +110,67 @@ def run(reps=3):
         print("      worst dantzig split: " + " ".join(f"{nm}={int(v)}" for nm, v in zip(names, prof)))
 
 
+PROB_WIDE = os.path.join(ROOT, "dbg", "lcp_wide.npz")
+NMAX_WIDE = 128
+
+
+def gen_wide(steps=2, batch=1024):
+    """The STL-mesh Atlas' LCPs with more than 64 rows (the wide kernels')."""
+    from nimblephysics_amd import workloads
+    from oracle.oracle import OracleWorld, lcp_problem, dantzig
+    w = workloads.atlas_mesh_world(True)
+    st, f = workloads.atlas_states(w, batch, 1000)
+    o = OracleWorld(w)
+    rows = []
+    for step in range(steps):
+        nxt = o.forward(st, f)
+        for b in range(batch):
+            A, bb, lo, hi, fi = lcp_problem(o, b)
+            if len(bb) > 64:
+                rows.append((len(bb), A, bb, lo, hi, fi))
+        st = nxt
+    P = len(rows)
+    N = NMAX_WIDE
+    n = np.array([r[0] for r in rows], dtype=np.int32)
+    A = np.zeros((P, N * N)); b = np.zeros((P, N)); lo = np.zeros((P, N)); hi = np.zeros((P, N))
+    fi = -np.ones((P, N), dtype=np.int32)
+    okD = np.zeros(P, dtype=np.int32)
+    for k, (m, Am, bm, lom, him, fim) in enumerate(rows):
+        A[k, :m * m] = np.asarray(Am).reshape(-1)
+        b[k, :m] = bm; lo[k, :m] = lom; hi[k, :m] = him; fi[k, :m] = fim
+        okD[k] = int(dantzig(np.asarray(Am).reshape(m, m), bm, lom, him, fim, early=True)[0])
+    np.savez_compressed(PROB_WIDE, n=n, A=A, b=b, lo=lo, hi=hi, fi=fi, okD=okD)
+    print(f"{P} wide problems, n {n.min()}..{n.max()}, oracle dantzig ok {okD.mean():.3f}")
+
+
+def run_wide(limit=512):
+    import torch
+    d = np.load(PROB_WIDE)
+    P = min(len(d["n"]), limit)
+    dev = torch.device("cuda:0")
+    T = {k: torch.tensor(d[k][:P], device=dev) for k in ("n", "A", "b", "lo", "hi", "fi")}
+    out = torch.zeros((P, REC), dtype=torch.float64, device=dev)
+    lib = C.CDLL(LIB)
+    s = torch.cuda.current_stream().cuda_stream
+    for _ in range(2):
+        rc = lib.lcp_bench_wide_launch(C.c_int(P), C.c_int(NMAX_WIDE), C.c_int(int(d["n"][:P].max())),
+                                       *[C.c_void_p(T[k].data_ptr()) for k in ("n", "A", "b", "lo", "hi", "fi")],
+                                       C.c_void_p(out.data_ptr()), C.c_void_p(s))
+        assert rc == 0
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    names = ["swap", "solveL1", "solveL1T", "ldltRemove", "w_i", "pivot body"]
+    piv = np.maximum(o[:, 4], 1)
+    print(f"{P} wide problems: ok agrees with oracle {np.mean((o[:, 0] > 0) == (d['okD'][:P] > 0)):.3f}; "
+          f"clocks mean {o[:, 1].mean():.0f} max {o[:, 1].max():.0f}; pivots mean {o[:, 4].mean():.1f} max {o[:, 4].max():.0f}; "
+          f"clocks per pivot mean {np.mean(o[:, 1] / piv):.0f}")
+    worst = np.argsort(-o[:, 1])[:5]
+    for k in worst:
+        print(f"  problem {k} n={d['n'][k]} clocks {o[k, 1]:.0f} pivots {o[k, 4]:.0f} | "
+              + " ".join(f"{nm}={int(v)}" for nm, v in zip(names, o[k, 8:14])))
+    np.save(os.path.join(ROOT, "gpurun_out", "lcp_wide_out.npy"), o)
+
+
 def solo(count=6):
     """The slowest n=24 problems, each launched alone (one wave on the GPU):
     uncontended latency of the solvers."""
@@ -143,5 +204,9 @@ if __name__ == "__main__":
         gen()
     elif cmd == "solo":
         solo()
+    elif cmd == "gen_wide":
+        gen_wide()
+    elif cmd == "run_wide":
+        run_wide()
     else:
         run()

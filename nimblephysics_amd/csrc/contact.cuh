@@ -492,6 +492,13 @@ __device__ __forceinline__ bool boardClaim(double* ct, int k, int who, int lane)
   return rdli(won, 0) != 0;
 }
 
+// board mode (helperFlags(ct)[1], set by wave 0 before it posts the task):
+// 0 the pool in LDS at L.pool (one row per lane), 1 the wide kernel's HBM
+// pool (two rows per lane) with Dantzig's factor at the start of its LDS
+// stage (which begins at L.pool)
+#define HB_LDS_POOL 0
+#define HB_WIDE 1
+
 // Collision detection on the helper wave.  collideWorld only reads the
 // body transforms (kinematics) and writes the contact header / list and its
 // own scratch past the dynamics buffers, so it overlaps wave 0's composite
@@ -1721,12 +1728,24 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   STAMP(3);
   // the helper wave starts Dantzig on A now (the task board, see helperWave):
   // A, b, lo, hi and findex are final; the warm start follows
-  const bool tasked = kLds && R == 1 && helperOn;
   // off-chip pools (wide kernels) factorise through the launch's LDS stage
   lds_double* stage = (!kLds && L.stageCap > 0) ? sp<true>(s + L.stage) : nullptr;
-  const int stageCap = L.stageCap;
+  int stageCap = L.stageCap;
+  // the wide kernel's worlds with an off-chip pool share the cascade on the
+  // task board too when Dantzig's LDL^T factor and scatter vector fit the
+  // start of the stage: the helper keeps them there for the whole cascade,
+  // wave 0's factorisations use the rest until the helper is out
+  const int dzStage = (m * (m | 1) + m + 1) & ~1;
+  const bool tasked = helperOn && (kLds ? R == 1 : (stage != nullptr && dzStage < stageCap));
+  lds_double* const stageAll = stage;
+  const int stageCapAll = stageCap;
   if (tasked) {
+    if (!kLds) {
+      stage += dzStage;
+      stageCap -= dzStage;
+    }
     if (lane < BD_INTS) board(ct)[lane] = 0;
+    if (lane == 0) helperFlags(ct)[1] = kLds ? HB_LDS_POOL : HB_WIDE;
     helperPost(ct, HS_TASK, lane);
   }
   // a settled answer makes every solve still running moot
@@ -1971,10 +1990,12 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
     WSYNC();
   }
   // the helper out of the pool before construct 2 and the backward
-  // precompute overwrite it (M1, M2, A)
+  // precompute overwrite it (M1, M2, A); the whole stage is wave 0's again
   if (tasked) {
     stopAll();
     helperWait(ct, [](int v) { return v == HS_DONE; });
+    stage = stageAll;
+    stageCap = stageCapAll;
   }
   cfm = unid(ct[H_CFM]);
   ignoredFriction = uni(ct[H_IGN] != 0 ? 1 : 0) != 0;
@@ -2046,7 +2067,119 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
 // itself), then claim whichever fallbacks are still open (the task board,
 // see above); answer DONE, then wait until wave 0 has taken the answer.
 // `g_stamp`: the stage-timing build's stamps (else null).
-__device__ void helperWave(const ModelDev& md, double* s, const Layout& L, int lane, double* g_stamp) {
+// The helper's share of the cascade for one world (see helperWave): R row
+// slots per lane, the pool P on chip (kLds) or in HBM; Dantzig's LDL^T factor
+// and scatter vector at Ldz / scrDz (LDS: the pool's M2 / xh2, or the wide
+// kernel's stage), the PGS fallback's reduced matrix at Mred.
+template <bool kLds, int R>
+__device__ __forceinline__ void helperTask(const ModelDev& md, double* ct, const FwdPool& Pin, int m, int lane,
+                                           lds_double* Ldz, lds_double* scrDz, typename Space<kLds>::dptr Mred,
+                                           double* g_stamp) {
+  (void)g_stamp;
+  // (pointers copied out: a pool struct taken by reference into the
+  // non-inlined solvers would be materialised in scratch)
+  const double* PA = Pin.A;
+  const double *Pb = Pin.b, *Plo = Pin.lo, *Phi = Pin.hi, *Pxc = Pin.xc;
+  double *Pxh = Pin.xh, *Pxp = Pin.xp, *Pxf = Pin.xf;
+  const int* Pfi = Pin.fi;
+  double bR[R], hiR[R], loR[R];
+  int fiR[R];
+#pragma unroll
+  for (int q = 0; q < R; q++) {
+    const int j = rowAt(q, lane);
+    bR[q] = j < m ? Pb[j] : 0.0;
+    hiR[q] = j < m ? Phi[j] : 0.0;
+    loR[q] = j < m ? Plo[j] : 0.0;
+    fiR[q] = j < m ? Pfi[j] : -1;
+  }
+  double scl[R];
+  int rep[R];
+  unsigned long long alive[R];
+  // (whether reduce merges anything: the first merge settles it)
+  waveReduceR<kLds, R>(m, spc<kLds>(PA), 0.0, bR, loR, hiR, fiR, lane, scl, rep, alive, 1);
+  if (!allRowsAlive<R>(m, alive)) {
+    boardSet(ct, BD_D, 3, lane);
+    return;
+  }
+#ifdef NIMBLE_STAGE_TIMING
+  if (lane == 0 && g_stamp) g_stamp[94] = (double)__builtin_amdgcn_s_memtime();
+  double* dbgD = g_stamp ? g_stamp + SLOT_DANTZIG : nullptr;
+#else
+  double* dbgD = nullptr;
+#endif
+  double xd[R];
+#pragma unroll
+  for (int q = 0; q < R; q++) xd[q] = 0.0;
+  bool ok = waveDantzigR<kLds, R, false, true>(m, spc<kLds>(PA), Ldz, scrDz, xd, bR, loR, hiR, fiR, lane, dbgD,
+                                               board(ct) + BD_STOPD);
+  bool nan = false;
+#pragma unroll
+  for (int q = 0; q < R; q++) nan = nan || (rowAt(q, lane) < m && isnan(xd[q]));
+  ok = ok && !__ballot(nan);
+  if (ok) ok = waveLcpValidR<kLds, R>(m, spc<kLds>(PA), 0.0, xd, bR, hiR, loR, fiR, false, lane);
+#pragma unroll
+  for (int q = 0; q < R; q++)
+    if (rowAt(q, lane) < m) Pxh[rowAt(q, lane)] = xd[q];
+  if (ok) {
+    boardSet(ct, BD_STOPP, 1, lane);
+    boardSet(ct, BD_STOPF, 1, lane);
+  }
+  boardSet(ct, BD_D, ok ? 1 : 2, lane);
+#ifdef NIMBLE_STAGE_TIMING
+  if (lane == 0 && g_stamp) { g_stamp[95] = (double)__builtin_amdgcn_s_memtime(); g_stamp[96] = ok ? 1 : 2; }
+#endif
+  // the fallbacks still open: the PGS fallback once the warm start is
+  // final, the frictionless PGS unless the PGS fallback has succeeded
+  const double cf = md.fallbackCfm;
+  for (long long it = 0; !ok; it++) {
+    const bool pOpen = boardGet(ct, BD_PCLAIM) == 0 && !boardGet(ct, BD_STOPP);
+    const bool fOpen = boardGet(ct, BD_FCLAIM) == 0 && !boardGet(ct, BD_STOPF) && boardGet(ct, BD_P) != 1;
+    if (pOpen && boardGet(ct, BD_G) == 1) {
+      if (boardClaim(ct, BD_PCLAIM, 2, lane)) {
+#ifdef NIMBLE_STAGE_TIMING
+        if (lane == 0 && g_stamp) { g_stamp[97] = 2; g_stamp[100] = (double)__builtin_amdgcn_s_memtime(); }
+#endif
+        bool dup;
+        double xp[R];
+        const bool okp = pgsFallbackR<kLds, R>(PA, Pxc, m, cf, bR, loR, hiR, fiR, Mred, lane, xp, dup,
+                                               board(ct) + BD_STOPP, nullptr);
+#pragma unroll
+        for (int q = 0; q < R; q++)
+          if (rowAt(q, lane) < m) Pxp[rowAt(q, lane)] = xp[q];
+        boardSet(ct, BD_PDUP, dup ? 1 : 0, lane);
+        if (okp) boardSet(ct, BD_STOPF, 1, lane);
+        boardSet(ct, BD_P, okp ? 1 : 2, lane);
+#ifdef NIMBLE_STAGE_TIMING
+        if (lane == 0 && g_stamp) g_stamp[101] = (double)__builtin_amdgcn_s_memtime();
+#endif
+      }
+      continue;
+    }
+    if (fOpen) {
+      if (boardClaim(ct, BD_FCLAIM, 2, lane)) {
+#ifdef NIMBLE_STAGE_TIMING
+        if (lane == 0 && g_stamp) { g_stamp[98] = 2; g_stamp[102] = (double)__builtin_amdgcn_s_memtime(); }
+#endif
+        double xf[R];
+        frictionlessPgsR<kLds, R>(PA, Pb, Plo, Phi, m, cf, fiR, lane, xf, board(ct) + BD_STOPF);
+#pragma unroll
+        for (int q = 0; q < R; q++)
+          if (rowAt(q, lane) < m) Pxf[rowAt(q, lane)] = xf[q];
+        boardSet(ct, BD_F, 1, lane);
+#ifdef NIMBLE_STAGE_TIMING
+        if (lane == 0 && g_stamp) g_stamp[103] = (double)__builtin_amdgcn_s_memtime();
+#endif
+      }
+      continue;
+    }
+    if (!pOpen) break;
+    // only the PGS fallback is open, waiting for the warm start
+    if (it > kSpinBound) __builtin_trap();
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+__device__ void helperWave(const ModelDev& md, double* s, const Layout& L, int lane, double* g_stamp, double* hbmPool) {
   (void)g_stamp;
   s = lds<true>(s);
   double* ct = s + L.ct;
@@ -2059,84 +2192,15 @@ __device__ void helperWave(const ModelDev& md, double* s, const Layout& L, int l
     else if (prio == 2) __builtin_amdgcn_s_setprio(2);
     else if (prio == 3) __builtin_amdgcn_s_setprio(3);
     const int m = uni((int)ct[H_M]);
+    const int mode = uni(helperFlags(ct)[1]);
     FwdPool P;
-    carveFwd(s + L.pool, m, md.n, P);
-    const double bR[1] = {lane < m ? P.b[lane] : 0.0}, hiR[1] = {lane < m ? P.hi[lane] : 0.0};
-    const double loR[1] = {lane < m ? P.lo[lane] : 0.0};
-    const int fiR[1] = {lane < m ? P.fi[lane] : -1};
-    double scl[1];
-    int rep[1];
-    unsigned long long alive[1];
-    // (whether reduce merges anything: the first merge settles it)
-    waveReduceR<true, 1>(m, spc<true>(P.A), 0.0, bR, loR, hiR, fiR, lane, scl, rep, alive, 1);
-    if (!allRowsAlive<1>(m, alive)) {
-      boardSet(ct, BD_D, 3, lane);
+    if (mode == HB_WIDE) {
+      carveFwd(gbl(hbmPool), m, md.n, P);
+      lds_double* Ldz = (lds_double*)(s + L.pool);
+      helperTask<false, 2>(md, ct, P, m, lane, Ldz, Ldz + m * (m | 1), sp<false>(P.M2), g_stamp);
     } else {
-#ifdef NIMBLE_STAGE_TIMING
-      if (lane == 0 && g_stamp) g_stamp[94] = (double)__builtin_amdgcn_s_memtime();
-      double* dbgD = g_stamp ? g_stamp + SLOT_DANTZIG : nullptr;
-#else
-      double* dbgD = nullptr;
-#endif
-      double xd[1] = {0.0};
-      bool ok = waveDantzigR<true, 1>(m, spc<true>(P.A), sp<true>(P.M2), sp<true>(P.xh2), xd, bR, loR, hiR, fiR, lane,
-                                      dbgD, board(ct) + BD_STOPD);
-      ok = ok && !__ballot(lane < m && isnan(xd[0]));
-      if (ok) ok = waveLcpValidR<true, 1>(m, spc<true>(P.A), 0.0, xd, bR, hiR, loR, fiR, false, lane);
-      if (lane < m) P.xh[lane] = xd[0];
-      if (ok) {
-        boardSet(ct, BD_STOPP, 1, lane);
-        boardSet(ct, BD_STOPF, 1, lane);
-      }
-      boardSet(ct, BD_D, ok ? 1 : 2, lane);
-#ifdef NIMBLE_STAGE_TIMING
-      if (lane == 0 && g_stamp) { g_stamp[95] = (double)__builtin_amdgcn_s_memtime(); g_stamp[96] = ok ? 1 : 2; }
-#endif
-      // the fallbacks still open: the PGS fallback once the warm start is
-      // final, the frictionless PGS unless the PGS fallback has succeeded
-      const double cf = md.fallbackCfm;
-      for (long long it = 0; !ok; it++) {
-        const bool pOpen = boardGet(ct, BD_PCLAIM) == 0 && !boardGet(ct, BD_STOPP);
-        const bool fOpen = boardGet(ct, BD_FCLAIM) == 0 && !boardGet(ct, BD_STOPF) && boardGet(ct, BD_P) != 1;
-        if (pOpen && boardGet(ct, BD_G) == 1) {
-          if (boardClaim(ct, BD_PCLAIM, 2, lane)) {
-#ifdef NIMBLE_STAGE_TIMING
-            if (lane == 0 && g_stamp) { g_stamp[97] = 2; g_stamp[100] = (double)__builtin_amdgcn_s_memtime(); }
-#endif
-            bool dup;
-            double xp[1];
-            const bool okp = pgsFallbackR<true, 1>(P.A, P.xc, m, cf, bR, loR, hiR, fiR, sp<true>(P.M2), lane, xp, dup,
-                                                   board(ct) + BD_STOPP, nullptr);
-            if (lane < m) P.xp[lane] = xp[0];
-            boardSet(ct, BD_PDUP, dup ? 1 : 0, lane);
-            if (okp) boardSet(ct, BD_STOPF, 1, lane);
-            boardSet(ct, BD_P, okp ? 1 : 2, lane);
-#ifdef NIMBLE_STAGE_TIMING
-            if (lane == 0 && g_stamp) g_stamp[101] = (double)__builtin_amdgcn_s_memtime();
-#endif
-          }
-          continue;
-        }
-        if (fOpen) {
-          if (boardClaim(ct, BD_FCLAIM, 2, lane)) {
-#ifdef NIMBLE_STAGE_TIMING
-            if (lane == 0 && g_stamp) { g_stamp[98] = 2; g_stamp[102] = (double)__builtin_amdgcn_s_memtime(); }
-#endif
-            double xf[1];
-            frictionlessPgsR<true, 1>(P.A, P.b, P.lo, P.hi, m, cf, fiR, lane, xf, board(ct) + BD_STOPF);
-            if (lane < m) P.xf[lane] = xf[0];
-            boardSet(ct, BD_F, 1, lane);
-#ifdef NIMBLE_STAGE_TIMING
-            if (lane == 0 && g_stamp) g_stamp[103] = (double)__builtin_amdgcn_s_memtime();
-#endif
-          }
-          continue;
-        }
-        if (!pOpen) break;
-        // only the PGS fallback is open, waiting for the warm start
-        if (it > kSpinBound) __builtin_trap();
-        __builtin_amdgcn_s_sleep(1);
-      }
+      carveFwd(s + L.pool, m, md.n, P);
+      helperTask<true, 1>(md, ct, P, m, lane, sp<true>(P.M2), sp<true>(P.xh2), sp<true>(P.M2), g_stamp);
     }
   }
   __builtin_amdgcn_s_setprio(0);

@@ -341,15 +341,68 @@ __device__ bool wavePgsR(int n, typename Space<kLds>::cdptr Ain, double (&x)[R],
 #pragma unroll
       for (int s = 0; s < R; s++) r[s] -= (cur[s] * dummyAct[s]) * dx;
     };
+    // four contact rows as one block: their residuals, diagonals, sweep-
+    // start x, boxes and the block's own coupling entries are read once as
+    // wave-uniform values, the four rows are solved in turn on those (each
+    // row's residual first takes the earlier rows' updates, in order), and
+    // every lane then applies the four x steps to its residual.  The
+    // operations are rowc's, in rowc's order, so the iterates are bit for bit
+    // the row-by-row sweep's; the readlane -> multiply-add chain of every row
+    // becomes one batch of readlanes per block.
+    auto blockc = [&](int i0, const Grp& Cg) {
+      double ru[4], du[4], xu[4], hu[4], lu[4], au[4][4], dxs[4], nxs[4];
+      double pv[4][R];
+#pragma unroll
+      for (int v = 0; v < 3; v++)
+#pragma unroll
+        for (int s = 0; s < R; s++) pv[v][s] = Cg[v][s] * dummyAct[s];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        ru[u] = rdlR(r, i0 + u);
+        du[u] = rdlR(diag, i0 + u);
+        xu[u] = rdlR(xs, i0 + u);
+        hu[u] = rdlR(hi, i0 + u);
+        lu[u] = rdlR(lo, i0 + u);
+#pragma unroll
+        for (int v = 0; v < u; v++) au[u][v] = rdlR(pv[v], i0 + u);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+#pragma unroll
+        for (int v = 0; v < u; v++) ru[u] -= au[u][v] * dxs[v];
+        const bool nrm = bitR(normals, i0 + u);
+        const double sc = boxScale(nrm, xN);
+        const double h = hu[u] * sc, l = lu[u] * sc;
+        double nx = ru[u] + du[u] * xu[u];
+        if constexpr (kExact) {
+          const double t = nx < l ? l : nx;
+          nx = nx > h ? h : t;
+        } else {
+          nx = fmin(fmax(nx, l), h);
+        }
+        dxs[u] = nx - xu[u];
+        xN = nrm ? nx : xN;
+        nxs[u] = nx;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+#pragma unroll
+        for (int s = 0; s < R; s++) r[s] -= (Cg[u][s] * dummyAct[s]) * dxs[u];
+        setR(xn, i0 + u, lane, nxs[u]);
+      }
+    };
     Grp C, N;
     loadGroup(C, 0);
     if (contactRows) {
       for (int i0 = 0; i0 < n; i0 += 4) {
         loadGroup(N, i0 + 4);
-        rowc(i0, C[0]);
-        if (i0 + 1 < n) rowc(i0 + 1, C[1]);
-        if (i0 + 2 < n) rowc(i0 + 2, C[2]);
-        if (i0 + 3 < n) rowc(i0 + 3, C[3]);
+        if (i0 + 3 < n) {
+          blockc(i0, C);
+        } else {
+          rowc(i0, C[0]);
+          if (i0 + 1 < n) rowc(i0 + 1, C[1]);
+          if (i0 + 2 < n) rowc(i0 + 2, C[2]);
+        }
 #pragma unroll
         for (int u = 0; u < 4; u++)
 #pragma unroll
@@ -649,11 +702,13 @@ struct WaveDantzig {
       for (int s = 0; s < R; s++)
 #pragma unroll
         for (int u = 0; u < 8; u++) Lv[s][u] = L[rowOffL[s] + (k0 + u < m ? k0 + u : 0)];
-      // the block's strictly lower diagonal entries (wave-uniform)
+      // the block's strictly lower diagonal entries (wave-uniform; indices
+      // clamped into the factor, entries past row m unused)
 #pragma unroll
       for (int a = 1; a < 8; a++)
 #pragma unroll
-        for (int u = 0; u < a; u++) Ld[a][u] = k0 + a < m ? L[(k0 + a) * ldL + k0 + u] : 0.0;
+        for (int u = 0; u < a; u++)
+          Ld[a][u] = L[(k0 + a < m ? k0 + a : m - 1) * ldL + (k0 + u < m ? k0 + u : m - 1)];
       // keep the loads unconditional and batched: all issued before any is
       // consumed
 #pragma unroll
@@ -661,16 +716,23 @@ struct WaveDantzig {
 #pragma unroll
         for (int u = 0; u < 8; u++) asm volatile("" : "+v"(Lv[s][u]));
 #pragma unroll
+      for (int a = 1; a < 8; a++)
+#pragma unroll
+        for (int u = 0; u < a; u++) asm volatile("" : "+v"(Ld[a][u]));
+#pragma unroll
       for (int s = 0; s < R; s++)
 #pragma unroll
         for (int u = 0; u < 8; u++) Lk[s][u] = (row(s) > k0 + u && row(s) < m) ? Lv[s][u] : 0.0;
       double bb[8];
 #pragma unroll
-      for (int u = 0; u < 8; u++) bb[u] = k0 + u < m ? rdlR(B, k0 + u) : 0.0;
+      for (int u = 0; u < 8; u++) bb[u] = rdlR(B, k0 + u < m ? k0 + u : m - 1);
 #pragma unroll
       for (int a = 1; a < 8; a++)
 #pragma unroll
         for (int u = 0; u < a; u++) bb[a] -= Ld[a][u] * bb[u];
+      // (entries past row m: 0, so that 0 * bb leaves every lane unchanged)
+#pragma unroll
+      for (int u = 1; u < 8; u++) bb[u] = k0 + u < m ? bb[u] : 0.0;
 #pragma unroll
       for (int u = 0; u < 8; u++)
 #pragma unroll
@@ -715,22 +777,28 @@ struct WaveDantzig {
 #pragma unroll
       for (int a = 1; a < 8; a++)
 #pragma unroll
-        for (int u = 0; u < a; u++) Ld[a][u] = k0 - a >= 0 ? L[(k0 - u) * ldL + k0 - a] : 0.0;
+        for (int u = 0; u < a; u++) Ld[a][u] = L[(k0 - u >= 0 ? k0 - u : 0) * ldL + (k0 - a >= 0 ? k0 - a : 0)];
 #pragma unroll
       for (int s = 0; s < R; s++)
 #pragma unroll
         for (int u = 0; u < 8; u++) asm volatile("" : "+v"(Lv[s][u]));
+#pragma unroll
+      for (int a = 1; a < 8; a++)
+#pragma unroll
+        for (int u = 0; u < a; u++) asm volatile("" : "+v"(Ld[a][u]));
 #pragma unroll
       for (int s = 0; s < R; s++)
 #pragma unroll
         for (int u = 0; u < 8; u++) Lk[s][u] = row(s) < k0 - u ? Lv[s][u] : 0.0;
       double bb[8];
 #pragma unroll
-      for (int u = 0; u < 8; u++) bb[u] = k0 - u >= 0 ? rdlR(B, k0 - u) : 0.0;
+      for (int u = 0; u < 8; u++) bb[u] = rdlR(B, k0 - u >= 0 ? k0 - u : 0);
 #pragma unroll
       for (int a = 1; a < 8; a++)
 #pragma unroll
         for (int u = 0; u < a; u++) bb[a] -= Ld[a][u] * bb[u];
+#pragma unroll
+      for (int u = 1; u < 8; u++) bb[u] = k0 - u >= 0 ? bb[u] : 0.0;
 #pragma unroll
       for (int u = 0; u < 8; u++)
 #pragma unroll
@@ -994,9 +1062,10 @@ struct WaveDantzig {
 
 // A (n x n, symmetric, read only), L (n x (n|1) scratch), scr (>= n); problem
 // vectors row-distributed; returns success and x (row-distributed).
-template <bool kLds, int R, bool kPk = false>
-__device__ bool waveDantzigR(int n, typename Space<kLds>::cdptr Ain, typename Space<kLds>::dptr Lin,
-                             typename Space<kLds>::dptr scrIn, double (&xOut)[R], const double (&b)[R],
+// kLds: A on chip; kLdsL: L and scr on chip (default: with A)
+template <bool kLds, int R, bool kPk = false, bool kLdsL = kLds>
+__device__ bool waveDantzigR(int n, typename Space<kLds>::cdptr Ain, typename Space<kLdsL>::dptr Lin,
+                             typename Space<kLdsL>::dptr scrIn, double (&xOut)[R], const double (&b)[R],
                              const double (&lo)[R], const double (&hi)[R], const int (&findex)[R], int lane,
                              double* dbg = nullptr, const int* cancel = nullptr) {
   n = uni(n);
@@ -1087,12 +1156,30 @@ __device__ bool waveDantzigR(int n, typename Space<kLds>::cdptr Ain, typename Sp
             colA[s] = row < n ? D.p[s] : 0;
             acc[s] = 0.0;
           }
-#pragma unroll 4
-          for (int j = 0; j < nC; j++) {
-            const double dxj = rdlR(D.deltaX, j);
-            const int ro = D.rowOff(j);
+          // eight C entries per block: their readlanes and A loads issued
+          // together, then the multiply-adds in j order (A symmetric: row j)
+          for (int j0 = 0; j0 < nC; j0 += 8) {
+            double dx[8], av[R][8];
+            int ro[8];
 #pragma unroll
-            for (int s = 0; s < R; s++) acc[s] += D.Ael(ro, colA[s]) * dxj;  // A symmetric: row j
+            for (int u = 0; u < 8; u++) {
+              const int j = j0 + u < nC ? j0 + u : 0;
+              dx[u] = rdlR(D.deltaX, j);
+              ro[u] = D.rowOff(j);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+#pragma unroll
+              for (int s = 0; s < R; s++) av[s][u] = D.Ael(ro[u], colA[s]);
+#pragma unroll
+            for (int s = 0; s < R; s++)
+#pragma unroll
+              for (int u = 0; u < 8; u++) asm volatile("" : "+v"(av[s][u]));
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+              if (j0 + u < nC)
+#pragma unroll
+                for (int s = 0; s < R; s++) acc[s] += av[s][u] * dx[u];
           }
           const int roI = D.rowOff(i);
 #pragma unroll

@@ -346,7 +346,9 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
 #else
         double* hstamp = nullptr;
 #endif
-        helperWave(md, s, md.lay[0], lane, hstamp);  // not inlined: the model's copy of L, not the argument's
+        // (the world's HBM LCP pool, the wide kernel's off-chip cascade)
+        double* hbmPool = snapshot + (size_t)env * snapDoubles + snapWorkspaceOffset(n);
+        helperWave(md, s, md.lay[0], lane, hstamp, hbmPool);  // not inlined: the model's copy of L, not the argument's
       }
       return;
     }

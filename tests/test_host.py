@@ -291,3 +291,29 @@ def test_tune_inertia_entries_follow_with_respect_to_mass():
     assert S[17, 6] == 1 and S[19, 8] == 1
     assert np.allclose(S[11:14, 9], [0.0, 2.0, 1.0])
     assert np.array_equal(S[0:10, 10:20], np.eye(10))
+
+
+def test_set_cached_lcp_solution_host_logic():
+    """World::setCachedLCPSolution: one vector for every world or one per
+    world, applied to the batch's warm-start rows on the next step (size
+    first, then x), empty rows for None; getCachedLCPSolution reads back."""
+    from types import SimpleNamespace
+    from nimblephysics_amd.timestep import _batch_state
+    w = models.box_world()
+    dev = SimpleNamespace(cache_doubles=10)
+    w.setCachedLCPSolution(np.array([0.5, 0.25, 0.0]))
+    assert np.array_equal(w.getCachedLCPSolution(), [0.5, 0.25, 0.0])
+    bs = _batch_state(w, 3, dev, torch.device("cpu"))
+    c = bs.cache.numpy()
+    assert (c[:, 0] == 3).all() and np.array_equal(c[2, 1:4], [0.5, 0.25, 0.0])
+    assert w._pending_lcp_cache is None
+    w.setCachedLCPSolution([None, np.array([1.0]), np.array([2.0, 3.0])])
+    c = _batch_state(w, 3, dev, torch.device("cpu")).cache.numpy()
+    assert c[0, 0] == -1 and c[1, 0] == 1 and c[1, 1] == 1.0 and c[2, 0] == 2 and np.array_equal(c[2, 1:3], [2, 3])
+    assert np.array_equal(w.getCachedLCPSolution(2), [2.0, 3.0]) and len(w.getCachedLCPSolution(0)) == 0
+    w.setCachedLCPSolution([np.ones(2), np.ones(2)])
+    with pytest.raises(ValueError):
+        _batch_state(w, 3, dev, torch.device("cpu"))
+    w.setCachedLCPSolution(np.ones(12))
+    with pytest.raises(ValueError):
+        _batch_state(w, 3, dev, torch.device("cpu"))

@@ -10,7 +10,7 @@ shift || true
 export TMPDIR=/tmp
 O=gpurun_out
 mkdir -p $O
-B="python bench.py --no-cpu-baseline $*"
+B="python bench.py --no-cpu-baseline --no-mesh $*"
 timeout -k 10 300 python bench.py "$@" > $O/bench_$TAG.json 2> $O/bench_$TAG.err || { echo BENCH FAILED; tail -20 $O/bench_$TAG.err; exit 1; }
 cut -c1-2500 $O/bench_$TAG.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$TAG -o run --output-format csv -- $B --steps 20 --warmup 3 > $O/prof_$TAG.log 2>&1 || { echo PROF FAILED; tail -20 $O/prof_$TAG.log; exit 1; }
@@ -29,6 +29,8 @@ cut -c1-1500 $O/bench_atlas_mesh_$TAG.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_mesh_$TAG -o run --output-format csv -- python bench.py --workload atlas_mesh --no-cpu-baseline --steps 10 --warmup 2 > $O/prof_mesh_$TAG.log 2>&1 || { echo MESH PROF FAILED; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_cartpole_$TAG -o run --output-format csv -- python bench.py --workload cartpole --no-cpu-baseline --steps 20 --warmup 3 > $O/prof_cartpole_$TAG.log 2>&1 || { echo CARTPOLE PROF FAILED; exit 1; }
 timeout -k 10 120 python bench.py --workload cartpole --no-cpu-baseline --steps 20 --warmup 3 > $O/bench_cartpole_$TAG.json 2>&1 || { echo CARTPOLE BENCH FAILED; exit 1; }
+timeout -k 10 120 python bench.py --workload half_cheetah --no-cpu-baseline --steps 20 --warmup 3 > $O/bench_half_cheetah_$TAG.json 2>&1 || { echo HALF CHEETAH BENCH FAILED; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_half_cheetah_$TAG -o run --output-format csv -- python bench.py --workload half_cheetah --no-cpu-baseline --steps 20 --warmup 3 > $O/prof_half_cheetah_$TAG.log 2>&1 || { echo HALF CHEETAH PROF FAILED; exit 1; }
 echo WORKLOADS OK
 # fp64 matrix-core counters (last: a counter this rocprof does not know ends
 # only this pass); summarised here by tools/pmc_mfma.py -> profiles/pmc_mfma.json

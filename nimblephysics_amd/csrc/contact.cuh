@@ -1735,19 +1735,28 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   // task board too when Dantzig's LDL^T factor and scatter vector fit the
   // start of the stage: the helper keeps them there for the whole cascade,
   // wave 0's factorisations use the rest until the helper is out
+  // (posted at once when the rest of the stage still holds the first
+  // classification's largest COD; otherwise only once that classification
+  // has failed, so that it factorises with the whole stage, and Dantzig then
+  // overlaps the PGS fallbacks only)
   const int dzStage = (m * (m | 1) + m + 1) & ~1;
-  const bool tasked = helperOn && (kLds ? R == 1 : (stage != nullptr && dzStage < stageCap));
+  const int codNeed = m * m + 4 * m + (m + 1) / 2 + 3 + m;  // codFactorAny's stage check at n_c = m
+  const bool taskable = helperOn && (kLds ? R == 1 : (stage != nullptr && dzStage < stageCap));
+  const bool earlyPost = taskable && (kLds || codNeed + dzStage <= stageCap);
+  bool tasked = taskable;
   lds_double* const stageAll = stage;
   const int stageCapAll = stageCap;
-  if (tasked) {
+  auto postTask = [&](bool warmFinal) {
     if (!kLds) {
       stage += dzStage;
       stageCap -= dzStage;
     }
     if (lane < BD_INTS) board(ct)[lane] = 0;
     if (lane == 0) helperFlags(ct)[1] = kLds ? HB_LDS_POOL : HB_WIDE;
+    if (warmFinal) boardSet(ct, BD_G, 1, lane);
     helperPost(ct, HS_TASK, lane);
-  }
+  };
+  if (earlyPost) postTask(false);
   // a settled answer makes every solve still running moot
   auto stopAll = [&]() {
     boardSet(ct, BD_STOPD, 1, lane);
@@ -1764,7 +1773,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
     for (int i = lane; i < m; i += WAVE) P.xc[i] = P.X[i];
     WSYNC();
   }
-  if (tasked) boardSet(ct, BD_G, 1, lane);
+  if (earlyPost) boardSet(ct, BD_G, 1, lane);
   if (lane == 0) ct[H_CODOK] = 0;
   STAMP(4);
 #ifdef NIMBLE_STAGE_TIMING
@@ -1774,7 +1783,11 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   bool success = devConstruct<kLds, R>(poolIn, m, n, 0.0, false, sp<true>(ct), lane, nullptr, stage, stageCap);
   double* dbgPgs = nullptr;
 #endif
-  if (tasked && success) stopAll();
+  if (earlyPost && success) stopAll();
+  if (taskable && !earlyPost) {
+    if (success) tasked = false;  // (no task went out; helperRetire posts SKIP)
+    else postTask(true);
+  }
   STAMP(5);
   const bool shortCircuit = success;
   double cfm = 0.0;

@@ -27,6 +27,8 @@ timeout -s KILL 60 rocprofv3 --pmc SQ_INSTS_FLAT SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_
 timeout -k 10 300 python bench.py --workload atlas_mesh --no-cpu-baseline --steps 20 --warmup 3 > $O/bench_atlas_mesh_$TAG.json 2> $O/bench_atlas_mesh_$TAG.err || { echo MESH BENCH FAILED; tail -20 $O/bench_atlas_mesh_$TAG.err; exit 1; }
 cut -c1-1500 $O/bench_atlas_mesh_$TAG.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_mesh_$TAG -o run --output-format csv -- python bench.py --workload atlas_mesh --no-cpu-baseline --steps 10 --warmup 2 > $O/prof_mesh_$TAG.log 2>&1 || { echo MESH PROF FAILED; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch_mesh_$TAG -o run --output-format csv -- python bench.py --workload atlas_mesh --no-cpu-baseline --steps 3 --warmup 1 > $O/pmc6_$TAG.log 2>&1 || { echo PMC6 FAILED; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write_mesh_$TAG -o run --output-format csv -- python bench.py --workload atlas_mesh --no-cpu-baseline --steps 3 --warmup 1 > $O/pmc7_$TAG.log 2>&1 || { echo PMC7 FAILED; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_cartpole_$TAG -o run --output-format csv -- python bench.py --workload cartpole --no-cpu-baseline --steps 20 --warmup 3 > $O/prof_cartpole_$TAG.log 2>&1 || { echo CARTPOLE PROF FAILED; exit 1; }
 timeout -k 10 120 python bench.py --workload cartpole --no-cpu-baseline --steps 20 --warmup 3 > $O/bench_cartpole_$TAG.json 2>&1 || { echo CARTPOLE BENCH FAILED; exit 1; }
 timeout -k 10 120 python bench.py --workload half_cheetah --no-cpu-baseline --steps 20 --warmup 3 > $O/bench_half_cheetah_$TAG.json 2>&1 || { echo HALF CHEETAH BENCH FAILED; exit 1; }

@@ -220,6 +220,7 @@ __device__ __forceinline__ void codFactorR(typename Space<kLds>::dptr Ain, typen
     }
   }
   WSYNC();
+  COD_PROF_BEGIN;
   for (int k = 0; k < c.kmax; k++) {
     // pivot: largest remaining norm, lowest index on ties
     double cand[R], neg[R];
@@ -244,6 +245,7 @@ __device__ __forceinline__ void codFactorR(typename Space<kLds>::dptr Ain, typen
       if (lane == 0) { int t = c.perm[k]; c.perm[k] = c.perm[p]; c.perm[p] = t; }
     }
     WSYNC();
+    COD_PROF(0);
     const double akk = A[k * ld + k];
     double colv[R], sq[R];
 #pragma unroll
@@ -280,6 +282,58 @@ __device__ __forceinline__ void codFactorR(typename Space<kLds>::dptr Ain, typen
     }
     const double vnorm = waveSumR(sq);
     WSYNC();
+    COD_PROF(1);
+    if (R == 2 && vnorm > 0) {
+      // both slots in one pass over the rows: two independent dot / norm
+      // chains per lane (same operations per column in the same order as the
+      // slot loop below, so the same factor bit for bit); an inactive slot
+      // reads column k and stores nothing
+      const int j0 = lane, j1 = lane + WAVE;
+      const bool a0 = j0 >= k && j0 < n, a1 = j1 >= k && j1 < n;
+      const int c0 = a0 ? j0 : k, c1 = a1 ? j1 : k;
+      double s0 = 0, s1 = 0;
+      int i = k;
+      for (; i + 8 <= m; i += 8) {
+        double x0[8], x1[8], vv[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) { vv[u] = v[i + u]; x0[u] = A[(i + u) * ld + c0]; x1[u] = A[(i + u) * ld + c1]; }
+#pragma unroll
+        for (int u = 0; u < 8; u++) { s0 += vv[u] * x0[u]; s1 += vv[u] * x1[u]; }
+      }
+      for (; i < m; i++) { const double vi = v[i]; s0 += vi * A[i * ld + c0]; s1 += vi * A[i * ld + c1]; }
+      COD_PROF(4);
+      s0 = 2 * s0 / vnorm;
+      s1 = 2 * s1 / vnorm;
+      double n0 = 0.0, n1 = 0.0;
+      i = k;
+      for (; i + 8 <= m; i += 8) {
+        double x0[8], x1[8], vv[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) { vv[u] = v[i + u]; x0[u] = A[(i + u) * ld + c0]; x1[u] = A[(i + u) * ld + c1]; }
+#pragma unroll
+        for (int u = 0; u < 8; u++) asm volatile("" : "+v"(x0[u]), "+v"(x1[u]), "+v"(vv[u]));
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const double b0 = x0[u] - s0 * vv[u];
+          const double b1 = x1[u] - s1 * vv[u];
+          if (a0) A[(i + u) * ld + j0] = b0;
+          if (a1) A[(i + u) * ld + j1] = b1;
+          const double t0 = i + u > k ? b0 : 0.0, t1 = i + u > k ? b1 : 0.0;
+          n0 += t0 * t0;
+          n1 += t1 * t1;
+        }
+      }
+      for (; i < m; i++) {
+        const double vi = v[i];
+        const double b0 = A[i * ld + c0] - s0 * vi;
+        const double b1 = A[i * ld + c1] - s1 * vi;
+        if (a0) A[i * ld + j0] = b0;
+        if (a1) A[i * ld + j1] = b1;
+        if (i > k) { n0 += b0 * b0; n1 += b1 * b1; }
+      }
+      if (a0) norm[0] = n0;
+      if (a1) norm[R - 1] = n1;
+    } else
 #pragma unroll
     for (int s = 0; s < R; s++) {
       const int j = rowAt(s, lane);
@@ -304,7 +358,8 @@ __device__ __forceinline__ void codFactorR(typename Space<kLds>::dptr Ain, typen
             for (int u = 0; u < 8; u++) {
               const double a = av[u] - sc * vv[u];
               A[(i + u) * ld + j] = a;
-              if (i + u > k) nrm += a * a;
+              const double t = i + u > k ? a : 0.0;  // (adds +0: the same sum)
+              nrm += t * t;
             }
           }
           for (; i < m; i++) {
@@ -320,10 +375,12 @@ __device__ __forceinline__ void codFactorR(typename Space<kLds>::dptr Ain, typen
       }
     }
     WSYNC();
+    COD_PROF(2);
     for (int i = lane; i < m; i += WAVE)
       if (i > k) A[i * ld + k] = v[i];
     if (lane == 0) { c.vd[k] = v[k]; c.vn[k] = vnorm; }
     WSYNC();
+    COD_PROF(3);
   }
   }
 rankAndRz:

@@ -1568,8 +1568,9 @@ __device__ __forceinline__ bool contactStage(const ModelDev& md, double* s, cons
     contactLcp<true, 1>(md, sp<true>(s), L, lane, sp<true>(v1), spc<true>(ddq), cache, snap, sp<true>(s + L.pool),
                         nCon, m, helperOn);
   else
+    // (the helper joins through the LDS stage: contactLcp's task board)
     contactLcp<false, R>(md, sp<true>(s), L, lane, sp<true>(v1), spc<true>(ddq), cache, snap, overflowWs, nCon, m,
-                         false);
+                         helperOn);
   return false;
 }
 
@@ -1822,11 +1823,13 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
     for (int q = 0; q < R; q++) xd[q] = 0.0;
     bool ok;
     bool validated = false;
-    if (!allRowsAlive<R>(m, alive)) {
-      // (the helper sees the same merge and solves nothing: wait until it
-      // is out of the pool)
+    const bool merged = !allRowsAlive<R>(m, alive);
+    if (merged && lane == 0) ct[H_STATUS] = (double)((int)ct[H_STATUS] | ST_DUPLICATE_COLUMNS);
+    if (merged && (kLds || !tasked)) {
+      // (on chip the helper sees the same merge and solves nothing: wait
+      // until it is out of the pool; the wide kernel's helper solves the
+      // reduced problem on the board below)
       if (tasked) helperWait(ct, [](int v) { return v == HS_DONE; });
-      if (lane == 0) ct[H_STATUS] = (double)((int)ct[H_STATUS] | ST_DUPLICATE_COLUMNS);
       double br[R], lr[R], hr[R], xr[R];
       int fr[R], act[R];
 #pragma unroll
@@ -2108,9 +2111,16 @@ __device__ __forceinline__ void helperTask(const ModelDev& md, double* ct, const
   double scl[R];
   int rep[R];
   unsigned long long alive[R];
-  // (whether reduce merges anything: the first merge settles it)
-  waveReduceR<kLds, R>(m, spc<kLds>(PA), 0.0, bR, loR, hiR, fiR, lane, scl, rep, alive, 1);
-  if (!allRowsAlive<R>(m, alive)) {
+  // LCPUtils::reduce (BoxedLcpConstraintSolver.cpp:466-521).  On chip
+  // (kLds) there is no room for a reduced matrix beside wave 0's fallbacks:
+  // a merge hands Dantzig back to wave 0 (only whether reduce merges anything
+  // is needed, the first merge settles it).  The wide kernel's HBM pool has
+  // one: Dantzig runs on the reduced problem here (matrix in Mred, which this
+  // wave's own PGS fallback reuses only after it), mapped out as wave 0 would
+  // (x_i = x_r[rank(rep_i)]), and is validated on the full problem.
+  waveReduceR<kLds, R>(m, spc<kLds>(PA), 0.0, bR, loR, hiR, fiR, lane, scl, rep, alive, kLds ? 1 : 128);
+  const bool merged = !allRowsAlive<R>(m, alive);
+  if (kLds && merged) {
     boardSet(ct, BD_D, 3, lane);
     return;
   }
@@ -2123,8 +2133,22 @@ __device__ __forceinline__ void helperTask(const ModelDev& md, double* ct, const
   double xd[R];
 #pragma unroll
   for (int q = 0; q < R; q++) xd[q] = 0.0;
-  bool ok = waveDantzigR<kLds, R, false, true>(m, spc<kLds>(PA), Ldz, scrDz, xd, bR, loR, hiR, fiR, lane, dbgD,
-                                               board(ct) + BD_STOPD);
+  bool ok;
+  if (!kLds && merged) {
+    double br[R], lr[R], hr[R], xr[R];
+    int fr[R], act[R];
+#pragma unroll
+    for (int q = 0; q < R; q++) { br[q] = bR[q]; lr[q] = loR[q]; hr[q] = hiR[q]; fr[q] = fiR[q]; }
+    const int mr = reducedVectorsR<R>(alive, rep, lane, br, lr, hr, fr, act);
+    reducedMatrixR<kLds, R>(m, spc<kLds>(PA), 0.0, alive, act, scl, Mred, false, lane);
+    WSYNC();
+    ok = waveDantzigR<kLds, R, false, true>(mr, Mred, Ldz, scrDz, xr, br, lr, hr, fr, lane, dbgD, board(ct) + BD_STOPD);
+#pragma unroll
+    for (int q = 0; q < R; q++) xd[q] = gatherR(xr, rankR(alive, rep[q]));
+  } else {
+    ok = waveDantzigR<kLds, R, false, true>(m, spc<kLds>(PA), Ldz, scrDz, xd, bR, loR, hiR, fiR, lane, dbgD,
+                                            board(ct) + BD_STOPD);
+  }
   bool nan = false;
 #pragma unroll
   for (int q = 0; q < R; q++) nan = nan || (rowAt(q, lane) < m && isnan(xd[q]));

@@ -341,68 +341,15 @@ __device__ bool wavePgsR(int n, typename Space<kLds>::cdptr Ain, double (&x)[R],
 #pragma unroll
       for (int s = 0; s < R; s++) r[s] -= (cur[s] * dummyAct[s]) * dx;
     };
-    // four contact rows as one block: their residuals, diagonals, sweep-
-    // start x, boxes and the block's own coupling entries are read once as
-    // wave-uniform values, the four rows are solved in turn on those (each
-    // row's residual first takes the earlier rows' updates, in order), and
-    // every lane then applies the four x steps to its residual.  The
-    // operations are rowc's, in rowc's order, so the iterates are bit for bit
-    // the row-by-row sweep's; the readlane -> multiply-add chain of every row
-    // becomes one batch of readlanes per block.
-    auto blockc = [&](int i0, const Grp& Cg) {
-      double ru[4], du[4], xu[4], hu[4], lu[4], au[4][4], dxs[4], nxs[4];
-      double pv[4][R];
-#pragma unroll
-      for (int v = 0; v < 3; v++)
-#pragma unroll
-        for (int s = 0; s < R; s++) pv[v][s] = Cg[v][s] * dummyAct[s];
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-        ru[u] = rdlR(r, i0 + u);
-        du[u] = rdlR(diag, i0 + u);
-        xu[u] = rdlR(xs, i0 + u);
-        hu[u] = rdlR(hi, i0 + u);
-        lu[u] = rdlR(lo, i0 + u);
-#pragma unroll
-        for (int v = 0; v < u; v++) au[u][v] = rdlR(pv[v], i0 + u);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-#pragma unroll
-        for (int v = 0; v < u; v++) ru[u] -= au[u][v] * dxs[v];
-        const bool nrm = bitR(normals, i0 + u);
-        const double sc = boxScale(nrm, xN);
-        const double h = hu[u] * sc, l = lu[u] * sc;
-        double nx = ru[u] + du[u] * xu[u];
-        if constexpr (kExact) {
-          const double t = nx < l ? l : nx;
-          nx = nx > h ? h : t;
-        } else {
-          nx = fmin(fmax(nx, l), h);
-        }
-        dxs[u] = nx - xu[u];
-        xN = nrm ? nx : xN;
-        nxs[u] = nx;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-#pragma unroll
-        for (int s = 0; s < R; s++) r[s] -= (Cg[u][s] * dummyAct[s]) * dxs[u];
-        setR(xn, i0 + u, lane, nxs[u]);
-      }
-    };
     Grp C, N;
     loadGroup(C, 0);
     if (contactRows) {
       for (int i0 = 0; i0 < n; i0 += 4) {
         loadGroup(N, i0 + 4);
-        if (i0 + 3 < n) {
-          blockc(i0, C);
-        } else {
-          rowc(i0, C[0]);
-          if (i0 + 1 < n) rowc(i0 + 1, C[1]);
-          if (i0 + 2 < n) rowc(i0 + 2, C[2]);
-        }
+        rowc(i0, C[0]);
+        if (i0 + 1 < n) rowc(i0 + 1, C[1]);
+        if (i0 + 2 < n) rowc(i0 + 2, C[2]);
+        if (i0 + 3 < n) rowc(i0 + 3, C[3]);
 #pragma unroll
         for (int u = 0; u < 4; u++)
 #pragma unroll
@@ -671,19 +618,14 @@ struct WaveDantzig {
     swapRegI(p, i1, i2); swapRegI(state, i1, i2); swapRegI(findex, i1, i2);
     LP_END(prof, 0);
   }
-  // L x = B (unit lower), B row-distributed, first m entries, in blocks of
-  // eight steps.  Per block the eight B entries are read once (readlanes
-  // issued together) and the block's own forward substitution runs on those
-  // wave-uniform values against the block's diagonal L entries (LDS
-  // broadcasts, loaded ahead); every lane then applies the eight known values
-  // to its rows.  A step is no longer a readlane -> FMA -> readlane chain
-  // (~150 clocks a step measured), and every B entry still receives its
-  // updates in the same order with the same operations (bit for bit the
-  // element-by-element substitution).  The L entries of each lane are masked
-  // with the triangle (0 where a lane must not change), so a lane step is one
-  // unpredicated FMA; 0 * b_k leaves a lane unchanged only for finite b_k: a
-  // non-finite b_k (degenerate factor) re-runs the solve predicated, exactly
-  // as the reference's loop.
+  // L x = B (unit lower), B row-distributed, first m entries.  The L
+  // entries of each lane are loaded 8 at a time ahead of the dependent
+  // readlane -> FMA chain (LDS latency paid once per 8 steps) with the
+  // triangle mask folded into them (0 where a lane must not change), so a
+  // step is a readlane and one unpredicated FMA: no exec-mask update that
+  // would wait on a vector compare.  0 * b_k leaves a lane unchanged only
+  // for finite b_k; a non-finite b_k (degenerate factor) re-runs the solve
+  // predicated, exactly as the reference's loop.
   __device__ __forceinline__ void solveL1(double (&B)[R], int m) {
     m = uni(m);
     LP_BEGIN();
@@ -697,46 +639,28 @@ struct WaveDantzig {
     for (int k0 = 0; k0 < m; k0 += 8) {
       double Lk[R][8];
       double Lv[R][8];
-      double Ld[8][8];
 #pragma unroll
       for (int s = 0; s < R; s++)
 #pragma unroll
         for (int u = 0; u < 8; u++) Lv[s][u] = L[rowOffL[s] + (k0 + u < m ? k0 + u : 0)];
-      // the block's strictly lower diagonal entries (wave-uniform; indices
-      // clamped into the factor, entries past row m unused)
-#pragma unroll
-      for (int a = 1; a < 8; a++)
-#pragma unroll
-        for (int u = 0; u < a; u++)
-          Ld[a][u] = L[(k0 + a < m ? k0 + a : m - 1) * ldL + (k0 + u < m ? k0 + u : m - 1)];
       // keep the loads unconditional and batched: all issued before any is
-      // consumed
+      // consumed (one barrier per block -- a barrier per load made the
+      // wave wait for each load in turn)
 #pragma unroll
       for (int s = 0; s < R; s++)
 #pragma unroll
         for (int u = 0; u < 8; u++) asm volatile("" : "+v"(Lv[s][u]));
 #pragma unroll
-      for (int a = 1; a < 8; a++)
-#pragma unroll
-        for (int u = 0; u < a; u++) asm volatile("" : "+v"(Ld[a][u]));
-#pragma unroll
       for (int s = 0; s < R; s++)
 #pragma unroll
         for (int u = 0; u < 8; u++) Lk[s][u] = (row(s) > k0 + u && row(s) < m) ? Lv[s][u] : 0.0;
-      double bb[8];
-#pragma unroll
-      for (int u = 0; u < 8; u++) bb[u] = rdlR(B, k0 + u < m ? k0 + u : m - 1);
-#pragma unroll
-      for (int a = 1; a < 8; a++)
-#pragma unroll
-        for (int u = 0; u < a; u++) bb[a] -= Ld[a][u] * bb[u];
-      // (entries past row m: 0, so that 0 * bb leaves every lane unchanged)
-#pragma unroll
-      for (int u = 1; u < 8; u++) bb[u] = k0 + u < m ? bb[u] : 0.0;
 #pragma unroll
       for (int u = 0; u < 8; u++)
+        if (k0 + u < m) {
+          const double bk = rdlR(B, k0 + u);
 #pragma unroll
-        for (int s = 0; s < R; s++) B[s] -= Lk[s][u] * bb[u];
+          for (int s = 0; s < R; s++) B[s] -= Lk[s][u] * bk;
+        }
     }
     bool nonFinite = false;
 #pragma unroll
@@ -753,7 +677,7 @@ struct WaveDantzig {
     }
     LP_END(prof, 1);
   }
-  // L^T x = B, blocks of eight steps from the last row up (as solveL1)
+  // L^T x = B
   __device__ __forceinline__ void solveL1T(double (&B)[R], int m) {
     m = uni(m);
     LP_BEGIN();
@@ -767,42 +691,25 @@ struct WaveDantzig {
     for (int k0 = m - 1; k0 >= 0; k0 -= 8) {
       double Lk[R][8];
       double Lv[R][8];
-      double Ld[8][8];
 #pragma unroll
       for (int s = 0; s < R; s++)
 #pragma unroll
         for (int u = 0; u < 8; u++) Lv[s][u] = L[(k0 - u >= 0 ? k0 - u : 0) * ldL + colL[s]];
-      // block entries: step u (row k0 - u) updates row k0 - a (a > u) with
-      // L[k0 - u][k0 - a]
-#pragma unroll
-      for (int a = 1; a < 8; a++)
-#pragma unroll
-        for (int u = 0; u < a; u++) Ld[a][u] = L[(k0 - u >= 0 ? k0 - u : 0) * ldL + (k0 - a >= 0 ? k0 - a : 0)];
 #pragma unroll
       for (int s = 0; s < R; s++)
 #pragma unroll
         for (int u = 0; u < 8; u++) asm volatile("" : "+v"(Lv[s][u]));
 #pragma unroll
-      for (int a = 1; a < 8; a++)
-#pragma unroll
-        for (int u = 0; u < a; u++) asm volatile("" : "+v"(Ld[a][u]));
-#pragma unroll
       for (int s = 0; s < R; s++)
 #pragma unroll
         for (int u = 0; u < 8; u++) Lk[s][u] = row(s) < k0 - u ? Lv[s][u] : 0.0;
-      double bb[8];
-#pragma unroll
-      for (int u = 0; u < 8; u++) bb[u] = rdlR(B, k0 - u >= 0 ? k0 - u : 0);
-#pragma unroll
-      for (int a = 1; a < 8; a++)
-#pragma unroll
-        for (int u = 0; u < a; u++) bb[a] -= Ld[a][u] * bb[u];
-#pragma unroll
-      for (int u = 1; u < 8; u++) bb[u] = k0 - u >= 0 ? bb[u] : 0.0;
 #pragma unroll
       for (int u = 0; u < 8; u++)
+        if (k0 - u >= 0) {
+          const double bk = rdlR(B, k0 - u);
 #pragma unroll
-        for (int s = 0; s < R; s++) B[s] -= Lk[s][u] * bb[u];
+          for (int s = 0; s < R; s++) B[s] -= Lk[s][u] * bk;
+        }
     }
     bool nonFinite = false;
 #pragma unroll

@@ -245,6 +245,34 @@ def test_mesh_atlas_wide_lds_pool_emulated():
     assert {"C", "D"} <= paths and ("F" in paths or "P" in paths)
 
 
+def test_mesh_atlas_wide_board_emulated():
+    """Mesh-Atlas worlds of 93 and 96 LCP rows (pool in HBM, two rows per
+    lane) on the wide kernel's task board: Dantzig's factor at the head of
+    the LDS stage on the helper wave.  At 93 rows the task goes out before
+    the first classification, which short-circuits (18); at 96 rows the
+    classification's COD needs the whole stage, so the task goes out only once
+    it has failed, and the cascade ends at the frictionless PGS (14)."""
+    from nimblephysics_amd import workloads
+    world = workloads.atlas_mesh_world(True)
+    st, f = workloads.random_states(world, 24, seed=1000, q_scale=0.02, v_scale=0.05)
+    idx = [14, 18]
+    st, f = st[idx], f[idx]
+    ow = O.OracleWorld(world)
+    ref = ow.forward(st, f)
+    g = np.random.default_rng(6).standard_normal(st.shape)
+    rgs, rgf = ow.backward(g)
+    nxt, gs, gf, head = wave_emu.step(world, st, f, g)
+    for i in range(len(idx)):
+        fl = O.lcp_flags(ow, i)
+        m = len(O.lcp_debug(ow, i, max_rows=O.MAX_LCP)[0])
+        assert m in (93, 96) and int(head[i, 1]) == m, idx[i]
+        assert (head[i, 6], head[i, 7], head[i, 4]) == (fl[0], fl[1], fl[2]), idx[i]
+        assert np.abs(nxt[i] - ref[i]).max() <= 1e-11, idx[i]
+        assert np.abs(gs[i] - rgs[i]).max() <= 1e-9 * np.abs(rgs[i]).max() * 10, idx[i]
+        assert np.abs(gf[i] - rgf[i]).max() <= 1e-9 * np.abs(rgf[i]).max(), idx[i]
+    assert head[0, 7] == 1 and head[1, 6] == 1
+
+
 def test_snapshot_layout_matches_pool_sizes():
     """_native.snapshot_layout (tools, tests) against csrc/pool_sizes.h."""
     from nimblephysics_amd import _native

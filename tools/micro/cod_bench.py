@@ -4,6 +4,7 @@ construct-like matrices (Q = Y^T Y of rank r <= n, and full-rank ones).
   python tools/micro/cod_bench.py build   # here: dbg/libcod_{reg,lds}.so
   python tools/micro/cod_bench.py run     # GPU box: clocks, rank, solution
   python tools/micro/cod_bench.py mfma    # GPU box: QR phase split + MFMA rank-4 update
+  python tools/micro/cod_bench.py wide    # GPU box: the two-slot LDS factorisation at 64..100
 """
 import ctypes as C
 import os
@@ -123,5 +124,57 @@ def mfma():
     print(json.dumps(res, indent=1))
 
 
+def wide(P=512, seed=1):
+    """codFactorR<true, 2> on n x n Gram matrices, n in 64..100 (the wide
+    forward kernel's staged classification factorisations): clocks of the
+    factorisation and the solve, the per-step phase split (pivot + swap,
+    reflector + |v|^2, trailing update + norms, write-back) and the error of
+    the min-norm solution against numpy."""
+    import json
+    import torch
+    NM = 100
+    rng = np.random.default_rng(seed)
+    n = rng.integers(64, NM + 1, size=P).astype(np.int32)
+    n[: P // 4] = 96
+    A = np.zeros((P, NM * NM))
+    b = np.zeros((P, NM))
+    for p in range(P):
+        k = n[p]
+        r = k if p % 3 == 0 else max(1, (2 * k) // 3)
+        Y = rng.standard_normal((k + 8, r)) @ rng.standard_normal((r, k))
+        A[p, : k * k] = (Y.T @ Y).ravel()
+        b[p, :k] = rng.standard_normal(k)
+    dev = torch.device("cuda:0")
+    s = torch.cuda.current_stream().cuda_stream
+    res = {}
+    for name, lib in (("plain", LIBS["reg"]), ("prof", PROF_LIB)):
+        L = C.CDLL(lib)
+        for label, cnt in (("solo_200", 200), ("batch", P)):
+            T = [torch.tensor(x[:cnt], device=dev) for x in (n, A, b)]
+            out = torch.zeros((cnt, 8 + 128), dtype=torch.float64, device=dev)
+            for _ in range(2):
+                assert L.cod_bench_wide_launch(C.c_int(cnt), C.c_int(NM), *[C.c_void_p(t.data_ptr()) for t in T],
+                                               C.c_void_p(out.data_ptr()), C.c_int(8 + 128), C.c_void_p(s)) == 0
+            torch.cuda.synchronize()
+            o = out.cpu().numpy()
+            sel = n[:cnt] == 96
+            r = {"factor_clk_n96": float(o[sel, 0].mean()), "solve_clk_n96": float(o[sel, 1].mean())}
+            if name == "prof":
+                r.update({k: float(o[sel, 3 + i].mean()) for i, k in
+                          enumerate(("pivot_swap", "reflector", "update_norms", "writeback", "dot"))})
+            else:
+                worst = 0.0
+                for p in range(min(cnt, 64)):
+                    k = n[p]
+                    Q = A[p, : k * k].reshape(k, k)
+                    rk = int(o[p, 2])
+                    U, S, Vt = np.linalg.svd(Q)
+                    xr = Vt[:rk].T @ ((U[:, :rk].T @ b[p, :k]) / S[:rk])
+                    worst = max(worst, np.abs(o[p, 8:8 + k] - xr).max() / max(1.0, np.abs(xr).max()))
+                r["max_rel_err_vs_svd"] = worst
+            res[f"{name}_{label}"] = r
+    print(json.dumps(res, indent=1))
+
+
 if __name__ == "__main__":
-    {"build": build, "run": run, "mfma": mfma}[sys.argv[1] if len(sys.argv) > 1 else "run"]()
+    {"build": build, "run": run, "mfma": mfma, "wide": wide}[sys.argv[1] if len(sys.argv) > 1 else "run"]()

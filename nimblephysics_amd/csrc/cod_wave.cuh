@@ -283,14 +283,22 @@ __device__ __forceinline__ void codFactorR(typename Space<kLds>::dptr Ain, typen
     const double vnorm = waveSumR(sq);
     WSYNC();
     COD_PROF(1);
-    if (R == 2 && vnorm > 0) {
+    if (R == 2 && vnorm > 0 && n > WAVE) {
       // both slots in one pass over the rows: two independent dot / norm
-      // chains per lane (same operations per column in the same order as the
-      // slot loop below, so the same factor bit for bit); an inactive slot
-      // reads column k and stores nothing
+      // chains per lane, the same operations per column in the same order as
+      // the slot loop below (the same factor bit for bit).  An inactive slot
+      // (a factored column, or past n) reads column k and stores into a
+      // per-lane sink -- the RZ reflector heads, not written before the RZ
+      // pass -- so no store is predicated (n > 64: zd holds > 64; with fewer
+      // columns the second slot is idle and the slot loop below skips it).  Row
+      // k is peeled off: it is updated but not part of the next step's norms.
       const int j0 = lane, j1 = lane + WAVE;
       const bool a0 = j0 >= k && j0 < n, a1 = j1 >= k && j1 < n;
       const int c0 = a0 ? j0 : k, c1 = a1 ? j1 : k;
+      double* const sink = c.zd + lane;
+      // (the store address of row i: the column's element or the sink)
+      auto at0 = [&](int i) { return a0 ? A + i * ld + c0 : sink; };
+      auto at1 = [&](int i) { return a1 ? A + i * ld + c1 : sink; };
       double s0 = 0, s1 = 0;
       int i = k;
       for (; i + 8 <= m; i += 8) {
@@ -304,8 +312,15 @@ __device__ __forceinline__ void codFactorR(typename Space<kLds>::dptr Ain, typen
       COD_PROF(4);
       s0 = 2 * s0 / vnorm;
       s1 = 2 * s1 / vnorm;
+      {
+        const double vk = v[k];
+        double x0 = A[k * ld + c0], x1 = A[k * ld + c1];
+        asm volatile("" : "+v"(x0), "+v"(x1));
+        *at0(k) = x0 - s0 * vk;
+        *at1(k) = x1 - s1 * vk;
+      }
       double n0 = 0.0, n1 = 0.0;
-      i = k;
+      i = k + 1;
       for (; i + 8 <= m; i += 8) {
         double x0[8], x1[8], vv[8];
 #pragma unroll
@@ -316,20 +331,22 @@ __device__ __forceinline__ void codFactorR(typename Space<kLds>::dptr Ain, typen
         for (int u = 0; u < 8; u++) {
           const double b0 = x0[u] - s0 * vv[u];
           const double b1 = x1[u] - s1 * vv[u];
-          if (a0) A[(i + u) * ld + j0] = b0;
-          if (a1) A[(i + u) * ld + j1] = b1;
-          const double t0 = i + u > k ? b0 : 0.0, t1 = i + u > k ? b1 : 0.0;
-          n0 += t0 * t0;
-          n1 += t1 * t1;
+          *at0(i + u) = b0;
+          *at1(i + u) = b1;
+          n0 += b0 * b0;
+          n1 += b1 * b1;
         }
       }
       for (; i < m; i++) {
         const double vi = v[i];
-        const double b0 = A[i * ld + c0] - s0 * vi;
-        const double b1 = A[i * ld + c1] - s1 * vi;
-        if (a0) A[i * ld + j0] = b0;
-        if (a1) A[i * ld + j1] = b1;
-        if (i > k) { n0 += b0 * b0; n1 += b1 * b1; }
+        double x0 = A[i * ld + c0], x1 = A[i * ld + c1];
+        asm volatile("" : "+v"(x0), "+v"(x1));
+        const double b0 = x0 - s0 * vi;
+        const double b1 = x1 - s1 * vi;
+        *at0(i) = b0;
+        *at1(i) = b1;
+        n0 += b0 * b0;
+        n1 += b1 * b1;
       }
       if (a0) norm[0] = n0;
       if (a1) norm[R - 1] = n1;

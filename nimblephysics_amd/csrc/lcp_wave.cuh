@@ -237,28 +237,40 @@ __device__ bool wavePgsR(int n, typename Space<kLds>::cdptr Ain, double (&x)[R],
     Grp C, N;
     loadGroup(C, 0);
     if (contactRows) {
-      for (int i0 = 0; i0 < n; i0 += 4) {
+      int i0 = 0;
+      for (; i0 + 4 <= n; i0 += 4) {
         loadGroup(N, i0 + 4);
         row1c(i0, C[0]);
-        if (i0 + 1 < n) row1c(i0 + 1, C[1]);
-        if (i0 + 2 < n) row1c(i0 + 2, C[2]);
-        if (i0 + 3 < n) row1c(i0 + 3, C[3]);
+        row1c(i0 + 1, C[1]);
+        row1c(i0 + 2, C[2]);
+        row1c(i0 + 3, C[3]);
 #pragma unroll
         for (int u = 0; u < 4; u++)
 #pragma unroll
           for (int s = 0; s < R; s++) C[u][s] = N[u][s];
       }
+      if (i0 < n) {
+        row1c(i0, C[0]);
+        if (i0 + 1 < n) row1c(i0 + 1, C[1]);
+        if (i0 + 2 < n) row1c(i0 + 2, C[2]);
+      }
     } else {
-      for (int i0 = 0; i0 < n; i0 += 4) {
+      int i0 = 0;
+      for (; i0 + 4 <= n; i0 += 4) {
         loadGroup(N, i0 + 4);
         row1(i0, C[0]);
-        if (i0 + 1 < n) row1(i0 + 1, C[1]);
-        if (i0 + 2 < n) row1(i0 + 2, C[2]);
-        if (i0 + 3 < n) row1(i0 + 3, C[3]);
+        row1(i0 + 1, C[1]);
+        row1(i0 + 2, C[2]);
+        row1(i0 + 3, C[3]);
 #pragma unroll
         for (int u = 0; u < 4; u++)
 #pragma unroll
           for (int s = 0; s < R; s++) C[u][s] = N[u][s];
+      }
+      if (i0 < n) {
+        row1(i0, C[0]);
+        if (i0 + 1 < n) row1(i0 + 1, C[1]);
+        if (i0 + 2 < n) row1(i0 + 2, C[2]);
       }
     }
     // the shift's share of the diagonal updates, deferred: a row's residual
@@ -343,29 +355,43 @@ __device__ bool wavePgsR(int n, typename Space<kLds>::cdptr Ain, double (&x)[R],
     };
     Grp C, N;
     loadGroup(C, 0);
+    // (full groups of four rows straight-line: a branch per row cost more
+    // than the row; the last, partial group row by row)
     if (contactRows) {
-      for (int i0 = 0; i0 < n; i0 += 4) {
+      int i0 = 0;
+      for (; i0 + 4 <= n; i0 += 4) {
         loadGroup(N, i0 + 4);
         rowc(i0, C[0]);
-        if (i0 + 1 < n) rowc(i0 + 1, C[1]);
-        if (i0 + 2 < n) rowc(i0 + 2, C[2]);
-        if (i0 + 3 < n) rowc(i0 + 3, C[3]);
+        rowc(i0 + 1, C[1]);
+        rowc(i0 + 2, C[2]);
+        rowc(i0 + 3, C[3]);
 #pragma unroll
         for (int u = 0; u < 4; u++)
 #pragma unroll
           for (int s = 0; s < R; s++) C[u][s] = N[u][s];
       }
+      if (i0 < n) {
+        rowc(i0, C[0]);
+        if (i0 + 1 < n) rowc(i0 + 1, C[1]);
+        if (i0 + 2 < n) rowc(i0 + 2, C[2]);
+      }
     } else {
-      for (int i0 = 0; i0 < n; i0 += 4) {
+      int i0 = 0;
+      for (; i0 + 4 <= n; i0 += 4) {
         loadGroup(N, i0 + 4);
         row(i0, C[0]);
-        if (i0 + 1 < n) row(i0 + 1, C[1]);
-        if (i0 + 2 < n) row(i0 + 2, C[2]);
-        if (i0 + 3 < n) row(i0 + 3, C[3]);
+        row(i0 + 1, C[1]);
+        row(i0 + 2, C[2]);
+        row(i0 + 3, C[3]);
 #pragma unroll
         for (int u = 0; u < 4; u++)
 #pragma unroll
           for (int s = 0; s < R; s++) C[u][s] = N[u][s];
+      }
+      if (i0 < n) {
+        row(i0, C[0]);
+        if (i0 + 1 < n) row(i0 + 1, C[1]);
+        if (i0 + 2 < n) row(i0 + 2, C[2]);
       }
     }
     if (shift != 0.0)
@@ -636,13 +662,17 @@ struct WaveDantzig {
       B0[s] = B[s];
       rowOffL[s] = (row(s) < m ? row(s) : 0) * ldL;
     }
-    for (int k0 = 0; k0 < m; k0 += 8) {
+    // full blocks of eight steps straight-line; the last, partial block
+    // pads its steps past m with b_k = +0 (their L entries are masked to 0:
+    // B - 0 * 0 is B bit for bit), so no step is a branch of its own (a
+    // taken branch per step cost more than the step)
+    auto block = [&](int k0, bool full) {
       double Lk[R][8];
       double Lv[R][8];
 #pragma unroll
       for (int s = 0; s < R; s++)
 #pragma unroll
-        for (int u = 0; u < 8; u++) Lv[s][u] = L[rowOffL[s] + (k0 + u < m ? k0 + u : 0)];
+        for (int u = 0; u < 8; u++) Lv[s][u] = L[rowOffL[s] + (full || k0 + u < m ? k0 + u : 0)];
       // keep the loads unconditional and batched: all issued before any is
       // consumed (one barrier per block -- a barrier per load made the
       // wave wait for each load in turn)
@@ -655,13 +685,17 @@ struct WaveDantzig {
 #pragma unroll
         for (int u = 0; u < 8; u++) Lk[s][u] = (row(s) > k0 + u && row(s) < m) ? Lv[s][u] : 0.0;
 #pragma unroll
-      for (int u = 0; u < 8; u++)
-        if (k0 + u < m) {
-          const double bk = rdlR(B, k0 + u);
+      for (int u = 0; u < 8; u++) {
+        const bool live = full || k0 + u < m;
+        double bk = rdlR(B, live ? k0 + u : k0);
+        if (!full) bk = live ? bk : 0.0;
 #pragma unroll
-          for (int s = 0; s < R; s++) B[s] -= Lk[s][u] * bk;
-        }
-    }
+        for (int s = 0; s < R; s++) B[s] -= Lk[s][u] * bk;
+      }
+    };
+    int k0 = 0;
+    for (; k0 + 8 <= m; k0 += 8) block(k0, true);
+    if (k0 < m) block(k0, false);
     bool nonFinite = false;
 #pragma unroll
     for (int s = 0; s < R; s++) nonFinite = nonFinite || (row(s) < m && !isfinite(B[s]));
@@ -688,13 +722,14 @@ struct WaveDantzig {
       B0[s] = B[s];
       colL[s] = row(s) < m ? row(s) : 0;
     }
-    for (int k0 = m - 1; k0 >= 0; k0 -= 8) {
+    // (blocks as solveL1's, from the last row up)
+    auto block = [&](int k0, bool full) {
       double Lk[R][8];
       double Lv[R][8];
 #pragma unroll
       for (int s = 0; s < R; s++)
 #pragma unroll
-        for (int u = 0; u < 8; u++) Lv[s][u] = L[(k0 - u >= 0 ? k0 - u : 0) * ldL + colL[s]];
+        for (int u = 0; u < 8; u++) Lv[s][u] = L[(full || k0 - u >= 0 ? k0 - u : 0) * ldL + colL[s]];
 #pragma unroll
       for (int s = 0; s < R; s++)
 #pragma unroll
@@ -704,13 +739,17 @@ struct WaveDantzig {
 #pragma unroll
         for (int u = 0; u < 8; u++) Lk[s][u] = row(s) < k0 - u ? Lv[s][u] : 0.0;
 #pragma unroll
-      for (int u = 0; u < 8; u++)
-        if (k0 - u >= 0) {
-          const double bk = rdlR(B, k0 - u);
+      for (int u = 0; u < 8; u++) {
+        const bool live = full || k0 - u >= 0;
+        double bk = rdlR(B, live ? k0 - u : k0);
+        if (!full) bk = live ? bk : 0.0;
 #pragma unroll
-          for (int s = 0; s < R; s++) B[s] -= Lk[s][u] * bk;
-        }
-    }
+        for (int s = 0; s < R; s++) B[s] -= Lk[s][u] * bk;
+      }
+    };
+    int k0 = m - 1;
+    for (; k0 - 7 >= 0; k0 -= 8) block(k0, true);
+    if (k0 >= 0) block(k0, false);
     bool nonFinite = false;
 #pragma unroll
     for (int s = 0; s < R; s++) nonFinite = nonFinite || (row(s) < m && !isfinite(B[s]));
@@ -1064,13 +1103,15 @@ __device__ bool waveDantzigR(int n, typename Space<kLds>::cdptr Ain, typename Sp
             acc[s] = 0.0;
           }
           // eight C entries per block: their readlanes and A loads issued
-          // together, then the multiply-adds in j order (A symmetric: row j)
-          for (int j0 = 0; j0 < nC; j0 += 8) {
+          // together, then the multiply-adds in j order (A symmetric: row j);
+          // the last, partial block pads with +0 * -0 terms (acc + -0 is acc
+          // bit for bit), so no term is a branch of its own
+          auto block = [&](int j0, bool full) {
             double dx[8], av[R][8];
             int ro[8];
 #pragma unroll
             for (int u = 0; u < 8; u++) {
-              const int j = j0 + u < nC ? j0 + u : 0;
+              const int j = full || j0 + u < nC ? j0 + u : 0;
               dx[u] = rdlR(D.deltaX, j);
               ro[u] = D.rowOff(j);
             }
@@ -1082,12 +1123,23 @@ __device__ bool waveDantzigR(int n, typename Space<kLds>::cdptr Ain, typename Sp
             for (int s = 0; s < R; s++)
 #pragma unroll
               for (int u = 0; u < 8; u++) asm volatile("" : "+v"(av[s][u]));
+            if (!full) {
+#pragma unroll
+              for (int u = 0; u < 8; u++) {
+                const bool live = j0 + u < nC;
+                dx[u] = live ? dx[u] : -0.0;
+#pragma unroll
+                for (int s = 0; s < R; s++) av[s][u] = live ? av[s][u] : 0.0;
+              }
+            }
 #pragma unroll
             for (int u = 0; u < 8; u++)
-              if (j0 + u < nC)
 #pragma unroll
-                for (int s = 0; s < R; s++) acc[s] += av[s][u] * dx[u];
-          }
+              for (int s = 0; s < R; s++) acc[s] += av[s][u] * dx[u];
+          };
+          int j0 = 0;
+          for (; j0 + 8 <= nC; j0 += 8) block(j0, true);
+          if (j0 < nC) block(j0, false);
           const int roI = D.rowOff(i);
 #pragma unroll
           for (int s = 0; s < R; s++) {

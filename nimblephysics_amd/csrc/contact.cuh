@@ -498,6 +498,13 @@ __device__ __forceinline__ bool boardClaim(double* ct, int k, int who, int lane)
 // stage (which begins at L.pool)
 #define HB_LDS_POOL 0
 #define HB_WIDE 1
+// wave 0 posts the cascade's task (board cleared, mode, warm start final or not)
+__device__ __forceinline__ void boardPost(double* ct, int mode, bool warmFinal, int lane) {
+  if (lane < BD_INTS) board(ct)[lane] = 0;
+  if (lane == 0) helperFlags(ct)[1] = mode;
+  if (warmFinal) boardSet(ct, BD_G, 1, lane);
+  helperPost(ct, HS_TASK, lane);
+}
 
 // Collision detection on the helper wave.  collideWorld only reads the
 // body transforms (kinematics) and writes the contact header / list and its
@@ -860,10 +867,15 @@ __device__ __forceinline__ void codFactorAny(typename Space<kLds>::dptr A, typen
   WSYNC();
 }
 
+// postDz > 0 (the wide kernel's first classification, task not yet posted):
+// once the classification's size n_c is known, the task board's Dantzig task
+// goes out here if the factor of this n_c still fits the stage after
+// Dantzig's postDz doubles at its head (the helper then runs Dantzig beside
+// this classification); whether it went out: helperState(ct) != HS_IDLE.
 template <bool kLds, int R = 1>
 __device__ bool devConstruct(typename Space<kLds>::dptr poolIn, int m, int n, double cfm, bool ignoreFriction,
                              lds_double* ctIn, int lane, double* g_stamp = nullptr, lds_double* stage = nullptr,
-                             int stageCap = 0) {
+                             int stageCap = 0, int postDz = 0) {
   (void)g_stamp;
   FwdPool P;
   carveFwd((double*)poolIn, m, n, P);
@@ -938,6 +950,11 @@ __device__ bool devConstruct(typename Space<kLds>::dptr poolIn, int m, int n, do
     WSYNC();
     TACC_END(61, tCls);
     const int nc = uni((int)ct[H_NC]);
+    if (postDz > 0 && guard == 0 && nc > 0 && nc * nc + 4 * nc + (nc + 1) / 2 + 3 + nc + postDz <= stageCap) {
+      boardPost(ct, HB_WIDE, true, lane);
+      stage += postDz;
+      stageCap -= postDz;
+    }
     double bR[R], hiR[R], loR[R];
     int fiR[R];
 #pragma unroll
@@ -1752,10 +1769,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
       stage += dzStage;
       stageCap -= dzStage;
     }
-    if (lane < BD_INTS) board(ct)[lane] = 0;
-    if (lane == 0) helperFlags(ct)[1] = kLds ? HB_LDS_POOL : HB_WIDE;
-    if (warmFinal) boardSet(ct, BD_G, 1, lane);
-    helperPost(ct, HS_TASK, lane);
+    boardPost(ct, kLds ? HB_LDS_POOL : HB_WIDE, warmFinal, lane);
   };
   if (earlyPost) postTask(false);
   // a settled answer makes every solve still running moot
@@ -1777,15 +1791,24 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   if (earlyPost) boardSet(ct, BD_G, 1, lane);
   if (lane == 0) ct[H_CODOK] = 0;
   STAMP(4);
+  // (not posted at once: the classification posts the task itself as soon as
+  // its n_c shows that its factor fits beside Dantzig's)
+  const int postDz = taskable && !earlyPost ? dzStage : 0;
 #ifdef NIMBLE_STAGE_TIMING
-  bool success = devConstruct<kLds, R>(poolIn, m, n, 0.0, false, sp<true>(ct), lane, g_stamp, stage, stageCap);
+  bool success = devConstruct<kLds, R>(poolIn, m, n, 0.0, false, sp<true>(ct), lane, g_stamp, stage, stageCap, postDz);
   double* dbgPgs = g_stamp ? g_stamp + SLOT_PGS : nullptr;
 #else
-  bool success = devConstruct<kLds, R>(poolIn, m, n, 0.0, false, sp<true>(ct), lane, nullptr, stage, stageCap);
+  bool success = devConstruct<kLds, R>(poolIn, m, n, 0.0, false, sp<true>(ct), lane, nullptr, stage, stageCap, postDz);
   double* dbgPgs = nullptr;
 #endif
-  if (earlyPost && success) stopAll();
-  if (taskable && !earlyPost) {
+  bool posted = earlyPost;
+  if (postDz > 0 && helperState(ct) != HS_IDLE) {
+    posted = true;
+    stage += dzStage;
+    stageCap -= dzStage;
+  }
+  if (posted && success) stopAll();
+  if (taskable && !posted) {
     if (success) tasked = false;  // (no task went out; helperRetire posts SKIP)
     else postTask(true);
   }

@@ -644,14 +644,70 @@ struct WaveDantzig {
     swapRegI(p, i1, i2); swapRegI(state, i1, i2); swapRegI(findex, i1, i2);
     LP_END(prof, 0);
   }
-  // L x = B (unit lower), B row-distributed, first m entries.  The L
-  // entries of each lane are loaded 8 at a time ahead of the dependent
-  // readlane -> FMA chain (LDS latency paid once per 8 steps) with the
-  // triangle mask folded into them (0 where a lane must not change), so a
-  // step is a readlane and one unpredicated FMA: no exec-mask update that
-  // would wait on a vector compare.  0 * b_k leaves a lane unchanged only
-  // for finite b_k; a non-finite b_k (degenerate factor) re-runs the solve
-  // predicated, exactly as the reference's loop.
+  // L x = B (unit lower), B row-distributed, first m entries, in blocks of
+  // eight steps.  A block's L entries are loaded together ahead of its
+  // dependent readlane -> FMA chain (LDS latency paid once per 8 steps) with
+  // the triangle mask folded into them (0 where a lane must not change), so
+  // a step is a readlane and unpredicated FMAs: no exec-mask update that
+  // would wait on a vector compare, and no branch (a taken branch per step
+  // cost more than the step).  Blocks are 8-aligned, so all steps of a block
+  // read their b_k from one register slot S (compile time: no slot select on
+  // the chain), and only the slots holding rows the block can change are
+  // updated -- rows > k for L, rows < k for L^T; the reference's loops touch
+  // no other row either.  The last, partial block pads its steps past m with
+  // b_k = +0 (masked L entries: B - 0 * 0 is B bit for bit).  0 * b_k leaves
+  // a lane unchanged only for finite b_k; a non-finite b_k (degenerate
+  // factor) re-runs the solve predicated, exactly as the reference's loop.
+  template <int S, bool kFull, bool kT>
+  __device__ __forceinline__ void solveBlock(double (&B)[R], int m, int k0, const int (&lOff)[R]) {
+    // steps: k = k0 + u (L) or k = k0 + 7 - u (L^T, k0 the block's lowest row)
+    double Lk[R][8];
+#pragma unroll
+    for (int s = 0; s < R; s++) {
+      if (kT ? s > S : s < S) continue;
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int k = kT ? k0 + 7 - u : k0 + u;
+        const int kc = kFull || k < m ? k : k0;
+        Lk[s][u] = kT ? L[kc * ldL + lOff[s]] : L[lOff[s] + kc];
+      }
+    }
+    // keep the loads unconditional and batched: all issued before any is
+    // consumed (one barrier per block -- a barrier per load made the wave
+    // wait for each load in turn)
+#pragma unroll
+    for (int s = 0; s < R; s++) {
+      if (kT ? s > S : s < S) continue;
+#pragma unroll
+      for (int u = 0; u < 8; u++) asm volatile("" : "+v"(Lk[s][u]));
+    }
+#pragma unroll
+    for (int s = 0; s < R; s++) {
+      if (kT ? s > S : s < S) continue;
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int k = kT ? k0 + 7 - u : k0 + u;
+        Lk[s][u] = (kT ? row(s) < k : row(s) > k) && row(s) < m ? Lk[s][u] : 0.0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int k = kT ? k0 + 7 - u : k0 + u;
+      const bool live = kFull || k < m;
+      double bk = rdl(B[S], (live ? k : k0) & 63);
+      if (!kFull) bk = live ? bk : 0.0;
+#pragma unroll
+      for (int s = 0; s < R; s++) {
+        if (kT ? s > S : s < S) continue;
+        B[s] -= Lk[s][u] * bk;
+      }
+    }
+  }
+  template <bool kFull, bool kT>
+  __device__ __forceinline__ void solveBlockAt(double (&B)[R], int m, int k0, const int (&lOff)[R]) {
+    if (R == 1 || k0 < 64) solveBlock<0, kFull, kT>(B, m, k0, lOff);
+    else solveBlock<R - 1, kFull, kT>(B, m, k0, lOff);
+  }
   __device__ __forceinline__ void solveL1(double (&B)[R], int m) {
     m = uni(m);
     LP_BEGIN();
@@ -662,40 +718,9 @@ struct WaveDantzig {
       B0[s] = B[s];
       rowOffL[s] = (row(s) < m ? row(s) : 0) * ldL;
     }
-    // full blocks of eight steps straight-line; the last, partial block
-    // pads its steps past m with b_k = +0 (their L entries are masked to 0:
-    // B - 0 * 0 is B bit for bit), so no step is a branch of its own (a
-    // taken branch per step cost more than the step)
-    auto block = [&](int k0, bool full) {
-      double Lk[R][8];
-      double Lv[R][8];
-#pragma unroll
-      for (int s = 0; s < R; s++)
-#pragma unroll
-        for (int u = 0; u < 8; u++) Lv[s][u] = L[rowOffL[s] + (full || k0 + u < m ? k0 + u : 0)];
-      // keep the loads unconditional and batched: all issued before any is
-      // consumed (one barrier per block -- a barrier per load made the
-      // wave wait for each load in turn)
-#pragma unroll
-      for (int s = 0; s < R; s++)
-#pragma unroll
-        for (int u = 0; u < 8; u++) asm volatile("" : "+v"(Lv[s][u]));
-#pragma unroll
-      for (int s = 0; s < R; s++)
-#pragma unroll
-        for (int u = 0; u < 8; u++) Lk[s][u] = (row(s) > k0 + u && row(s) < m) ? Lv[s][u] : 0.0;
-#pragma unroll
-      for (int u = 0; u < 8; u++) {
-        const bool live = full || k0 + u < m;
-        double bk = rdlR(B, live ? k0 + u : k0);
-        if (!full) bk = live ? bk : 0.0;
-#pragma unroll
-        for (int s = 0; s < R; s++) B[s] -= Lk[s][u] * bk;
-      }
-    };
     int k0 = 0;
-    for (; k0 + 8 <= m; k0 += 8) block(k0, true);
-    if (k0 < m) block(k0, false);
+    for (; k0 + 8 <= m; k0 += 8) solveBlockAt<true, false>(B, m, k0, rowOffL);
+    if (k0 < m) solveBlockAt<false, false>(B, m, k0, rowOffL);
     bool nonFinite = false;
 #pragma unroll
     for (int s = 0; s < R; s++) nonFinite = nonFinite || (row(s) < m && !isfinite(B[s]));
@@ -711,7 +736,8 @@ struct WaveDantzig {
     }
     LP_END(prof, 1);
   }
-  // L^T x = B
+  // L^T x = B: the blocks from the last row up, the partial one first
+  // (8-aligned below it)
   __device__ __forceinline__ void solveL1T(double (&B)[R], int m) {
     m = uni(m);
     LP_BEGIN();
@@ -722,34 +748,12 @@ struct WaveDantzig {
       B0[s] = B[s];
       colL[s] = row(s) < m ? row(s) : 0;
     }
-    // (blocks as solveL1's, from the last row up)
-    auto block = [&](int k0, bool full) {
-      double Lk[R][8];
-      double Lv[R][8];
-#pragma unroll
-      for (int s = 0; s < R; s++)
-#pragma unroll
-        for (int u = 0; u < 8; u++) Lv[s][u] = L[(full || k0 - u >= 0 ? k0 - u : 0) * ldL + colL[s]];
-#pragma unroll
-      for (int s = 0; s < R; s++)
-#pragma unroll
-        for (int u = 0; u < 8; u++) asm volatile("" : "+v"(Lv[s][u]));
-#pragma unroll
-      for (int s = 0; s < R; s++)
-#pragma unroll
-        for (int u = 0; u < 8; u++) Lk[s][u] = row(s) < k0 - u ? Lv[s][u] : 0.0;
-#pragma unroll
-      for (int u = 0; u < 8; u++) {
-        const bool live = full || k0 - u >= 0;
-        double bk = rdlR(B, live ? k0 - u : k0);
-        if (!full) bk = live ? bk : 0.0;
-#pragma unroll
-        for (int s = 0; s < R; s++) B[s] -= Lk[s][u] * bk;
-      }
-    };
-    int k0 = m - 1;
-    for (; k0 - 7 >= 0; k0 -= 8) block(k0, true);
-    if (k0 >= 0) block(k0, false);
+    if (m > 0) {
+      int k0 = (m - 1) & ~7;  // lowest row of the top block
+      if (k0 + 8 > m) solveBlockAt<false, true>(B, m, k0, colL);
+      else solveBlockAt<true, true>(B, m, k0, colL);
+      for (k0 -= 8; k0 >= 0; k0 -= 8) solveBlockAt<true, true>(B, m, k0, colL);
+    }
     bool nonFinite = false;
 #pragma unroll
     for (int s = 0; s < R; s++) nonFinite = nonFinite || (row(s) < m && !isfinite(B[s]));

@@ -872,7 +872,11 @@ __device__ __forceinline__ void codFactorAny(typename Space<kLds>::dptr A, typen
 // goes out here if the factor of this n_c still fits the stage after
 // Dantzig's postDz doubles at its head (the helper then runs Dantzig beside
 // this classification); whether it went out: helperState(ct) != HS_IDLE.
-template <bool kLds, int R = 1>
+// kK: which forward kernel calls (0 the one-row kernel, 1 the wide one): a
+// separate instance per kernel -- one instance reached from both kernels was
+// compiled with callee-saved register spills on entry (16 -> 464 B/lane of
+// scratch per call, forward writes ~25 -> ~85 KB/world measured)
+template <bool kLds, int R = 1, int kK = 0>
 __device__ bool devConstruct(typename Space<kLds>::dptr poolIn, int m, int n, double cfm, bool ignoreFriction,
                              lds_double* ctIn, int lane, double* g_stamp = nullptr, lds_double* stage = nullptr,
                              int stageCap = 0, int postDz = 0) {
@@ -1078,7 +1082,7 @@ __device__ bool devConstruct(typename Space<kLds>::dptr poolIn, int m, int n, do
 
 // guessSolution (LCPUtils.cpp:69): COD solve on {normal rows with b > 0} U
 // {friction rows}; result into x.
-template <bool kLds, int R = 1>
+template <bool kLds, int R = 1, int kK = 0>  // (kK: as devConstruct)
 __device__ void devGuess(typename Space<kLds>::dptr poolIn, int m, int n, lds_double* ctIn, int lane,
                          lds_double* stage = nullptr, int stageCap = 0) {
   FwdPool P;
@@ -1215,7 +1219,7 @@ __device__ __forceinline__ void pinvColumnsStaged(const lds_double* F, const lds
 // matrices it uses), computed here where A = J Minv J^T is on chip:
 // A_c, A_c_ub_E, Q = A_c^T Minv A_c_ub_E + cfm I, pinv(Q) (COD) and the
 // rank-deficiency flag ||I - Q Q^+||^2 >= 1e-18.
-template <bool kLds, int R = 1>
+template <bool kLds, int R = 1, int kK = 0>  // (kK: as devConstruct)
 __device__ void backwardPrecompute(const ModelDev& md, lds_double* sIn, const Layout& L, int lane,
                                    typename Space<kLds>::dptr poolIn, int m, double cfm, double* snap, lds_double* ctIn,
                                    lds_double* stage = nullptr, int stageCap = 0) {
@@ -1491,7 +1495,7 @@ __device__ void frictionlessPgsR(const double* PA, const double* Pb, const doubl
 // fallbacks, impulses (v1 += Minv J^T x), warm-start cache and snapshot.
 // `Lm` is the Cholesky factor of M (lower triangle, n x n).
 // ---------------------------------------------------------------------------
-template <bool kLds, int R>
+template <bool kLds, int R, int kK = 0>
 __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, const Layout& L, int lane,
                                            lds_double* v1In, const lds_double* ddqIn, double* cache, double* snap,
                                            typename Space<kLds>::dptr poolIn, int nCon, int m, bool helperOn);
@@ -1582,7 +1586,7 @@ __device__ __forceinline__ bool contactStage(const ModelDev& md, double* s, cons
     // the pool on chip: the one-row kernel's own pool, or the wide kernel's
     // LDS stage (which starts at the pool) for the worlds the one-row kernel
     // deferred because its pool could not hold them
-    contactLcp<true, 1>(md, sp<true>(s), L, lane, sp<true>(v1), spc<true>(ddq), cache, snap, sp<true>(s + L.pool),
+    contactLcp<true, 1, (R > 1 ? 1 : 0)>(md, sp<true>(s), L, lane, sp<true>(v1), spc<true>(ddq), cache, snap, sp<true>(s + L.pool),
                         nCon, m, helperOn);
   else
     // (the helper joins through the LDS stage: contactLcp's task board)
@@ -1591,7 +1595,7 @@ __device__ __forceinline__ bool contactStage(const ModelDev& md, double* s, cons
   return false;
 }
 
-template <bool kLds, int R>
+template <bool kLds, int R, int kK>
 __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, const Layout& L, int lane,
                                            lds_double* v1In, const lds_double* ddqIn, double* cache, double* snap,
                                            typename Space<kLds>::dptr poolIn, int nCon, int m, bool helperOn) {
@@ -1784,7 +1788,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
     for (int i = lane; i < m; i += WAVE) { P.X[i] = cache[1 + i]; P.xc[i] = cache[1 + i]; }
     WSYNC();
   } else {
-    devGuess<kLds, R>(poolIn, m, n, sp<true>(ct), lane, stage, stageCap);
+    devGuess<kLds, R, kK>(poolIn, m, n, sp<true>(ct), lane, stage, stageCap);
     for (int i = lane; i < m; i += WAVE) P.xc[i] = P.X[i];
     WSYNC();
   }
@@ -1795,10 +1799,10 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   // its n_c shows that its factor fits beside Dantzig's)
   const int postDz = taskable && !earlyPost ? dzStage : 0;
 #ifdef NIMBLE_STAGE_TIMING
-  bool success = devConstruct<kLds, R>(poolIn, m, n, 0.0, false, sp<true>(ct), lane, g_stamp, stage, stageCap, postDz);
+  bool success = devConstruct<kLds, R, kK>(poolIn, m, n, 0.0, false, sp<true>(ct), lane, g_stamp, stage, stageCap, postDz);
   double* dbgPgs = g_stamp ? g_stamp + SLOT_PGS : nullptr;
 #else
-  bool success = devConstruct<kLds, R>(poolIn, m, n, 0.0, false, sp<true>(ct), lane, nullptr, stage, stageCap, postDz);
+  bool success = devConstruct<kLds, R, kK>(poolIn, m, n, 0.0, false, sp<true>(ct), lane, nullptr, stage, stageCap, postDz);
   double* dbgPgs = nullptr;
 #endif
   bool posted = earlyPost;
@@ -2045,7 +2049,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   if (!shortCircuit) {
     for (int i = lane; i < m; i += WAVE) P.xc[i] = P.X[i];
     WSYNC();
-    std2 = devConstruct<kLds, R>(poolIn, m, n, cfm, ignoredFriction, sp<true>(ct), lane, nullptr, stage, stageCap);
+    std2 = devConstruct<kLds, R, kK>(poolIn, m, n, cfm, ignoredFriction, sp<true>(ct), lane, nullptr, stage, stageCap);
   }
   const double* Xf = std2 ? P.X : P.xc;
   STAMP(8);
@@ -2085,7 +2089,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   const int nc = uni((int)ct[H_NC]);
   for (int i = lane; i < nc; i += WAVE) snap[SN_FC + i] = P.fc[i];
   for (int i = lane; i < n; i += WAVE) snap[snYf(n) + i] = ddq[i];
-  backwardPrecompute<kLds, R>(md, sIn, md.lay[0], lane, poolIn, m, cfm, snap, sp<true>(ct), stage, stageCap);  // (not inlined)
+  backwardPrecompute<kLds, R, kK>(md, sIn, md.lay[0], lane, poolIn, m, cfm, snap, sp<true>(ct), stage, stageCap);  // (not inlined)
   if (lane == 0) {
     snap[SN_NCON] = nCon;
     snap[SN_M] = m;
@@ -2239,6 +2243,10 @@ __device__ __forceinline__ void helperTask(const ModelDev& md, double* ct, const
   }
 }
 
+// kWide: the wide kernel's helper (both board modes); the one-row kernel's
+// only ever sees HB_LDS_POOL (a separate, smaller function: the wide mode's
+// registers made every call save ~160 callee-saved VGPRs to scratch)
+template <bool kWide>
 __device__ void helperWave(const ModelDev& md, double* s, const Layout& L, int lane, double* g_stamp, double* hbmPool) {
   (void)g_stamp;
   s = lds<true>(s);
@@ -2254,7 +2262,7 @@ __device__ void helperWave(const ModelDev& md, double* s, const Layout& L, int l
     const int m = uni((int)ct[H_M]);
     const int mode = uni(helperFlags(ct)[1]);
     FwdPool P;
-    if (mode == HB_WIDE) {
+    if (kWide && mode == HB_WIDE) {
       carveFwd(gbl(hbmPool), m, md.n, P);
       lds_double* Ldz = (lds_double*)(s + L.pool);
       helperTask<false, 2>(md, ct, P, m, lane, Ldz, Ldz + m * (m | 1), sp<false>(P.M2), g_stamp);

@@ -43,15 +43,19 @@ struct nimble_world {
   Layout fwdWide{};     // the wide forward kernel's layout (LDS stage, see nimble_world_create)
   size_t wideLds = 0;   // its LDS bytes
   int jacWsDoubles = 0;  // per-workgroup LCP workspace of the Jacobian launch
+  // the one-row kernel's deferred-world lists (DEFER_BUCKETS counters + one
+  // list per bucket, per launch), read by the wide kernel; grown on demand
+  int* deferList = nullptr;
+  size_t deferCap = 0;
   int cacheDoubles = NIMBLE_MAX_LCP + 1;
   hipFunction_t dummy = nullptr;
   double* meshDev = nullptr;  // ModelDev::meshVerts
 };
 
 extern "C" __global__ void nimble_forward_kernel(const ModelDev*, Layout, const double*, const double*, double*,
-                                                 double*, double*, int, int, int);
+                                                 double*, double*, int, int, int, int*);
 extern "C" __global__ void nimble_forward_wide_kernel(const ModelDev*, Layout, const double*, const double*, double*,
-                                                      double*, double*, int, int);
+                                                      double*, double*, int, int, const int*);
 extern "C" __global__ void nimble_backward_kernel(const ModelDev*, int, const double*, const double*,
                                                   double*, int, const double*, double*, double*, int, double*, int,
                                                   double*, int, int, int);
@@ -413,6 +417,7 @@ int nimble_world_destroy(nimble_world_t w) {
   if (!w) return NIMBLE_OK;
   if (w->dev) (void)hipFree(w->dev);
   if (w->meshDev) (void)hipFree(w->meshDev);
+  if (w->deferList) (void)hipFree(w->deferList);
   delete w;
   return NIMBLE_OK;
 }
@@ -447,21 +452,34 @@ int nimble_forward(nimble_world_t w, int32_t batch, const double* state, const d
   // one workgroup per world; batches beyond one launch's grid go in chunks
   const size_t n = (size_t)w->host.n;
   const int chunk = fwdChunk();
+  const bool wide = w->host.numPairs > 0 && w->maxRows > w->fwdDeferRows;
+  if (wide) {
+    const int c0 = batch < chunk ? batch : chunk;
+    const size_t need = DEFER_BUCKETS + (size_t)DEFER_BUCKETS * c0;
+    if (need > w->deferCap) {
+      if (w->deferList) HIP_TRY(hipFree(w->deferList));
+      w->deferList = nullptr;
+      w->deferCap = 0;
+      HIP_TRY(hipMalloc(&w->deferList, need * sizeof(int)));
+      w->deferCap = need;
+    }
+  }
   for (int32_t b0 = 0; b0 < batch; b0 += chunk) {
     const int cnt = batch - b0 < chunk ? batch - b0 : chunk;
+    if (wide) HIP_TRY(hipMemsetAsync(w->deferList, 0, DEFER_BUCKETS * sizeof(int), st));
     hipLaunchKernelGGL(nimble_forward_kernel, dim3(cnt), dim3(fwdThreads), lds, st, w->dev, w->fwd,
                        state + b0 * 2 * n, forces + b0 * n, lcp_cache + (size_t)b0 * w->cacheDoubles,
                        next_state + b0 * 2 * n, snapshot + (size_t)b0 * w->snapDoubles, w->snapDoubles,
-                       w->cacheDoubles, w->fwdDeferRows);
+                       w->cacheDoubles, w->fwdDeferRows, wide ? w->deferList : nullptr);
     HIP_TRY(hipGetLastError());
     // the worlds whose LCP pool the one-row kernel does not hold on chip (or
     // more rows than the test threshold): stepped by the big-LDS wide kernel
     // (two waves: the LCP task board for the worlds of up to 64 rows)
-    if (w->host.numPairs > 0 && w->maxRows > w->fwdDeferRows) {
+    if (wide) {
       hipLaunchKernelGGL(nimble_forward_wide_kernel, dim3(cnt), dim3(128), w->wideLds, st, w->dev, w->fwdWide,
                          state + b0 * 2 * n, forces + b0 * n, lcp_cache + (size_t)b0 * w->cacheDoubles,
                          next_state + b0 * 2 * n, snapshot + (size_t)b0 * w->snapDoubles, w->snapDoubles,
-                         w->cacheDoubles);
+                         w->cacheDoubles, (const int*)w->deferList);
       HIP_TRY(hipGetLastError());
     }
   }

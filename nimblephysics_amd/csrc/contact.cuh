@@ -527,6 +527,10 @@ __device__ __forceinline__ void collideWait(double* ct, int want) {
   }
 }
 
+// the one-row kernel's deferred worlds, bucketed by LCP rows for the wide
+// kernel's launch order (largest first; DEFER_BUCKETS in pool_sizes.h)
+__device__ __forceinline__ int deferBucket(int m) { return m > 88 ? 0 : (m > 80 ? 1 : (m > 64 ? 2 : 3)); }
+
 // status bits
 #define ST_CONTACT_OVERFLOW 1
 #define ST_UNSUPPORTED_SHAPE 2
@@ -1508,7 +1512,8 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
 template <int R>
 __device__ __forceinline__ bool contactStage(const ModelDev& md, double* s, const Layout& L, int lane, double* v1,
                                              const double* ddq, double* cache, double* snap, double* overflowWs,
-                                             bool helperOn, bool collided, int deferRows, bool handedOff = false) {
+                                             bool helperOn, bool collided, int deferRows, bool handedOff = false,
+                                             int* deferList = nullptr, int env = 0) {
   const int n = md.n;
   s = lds<true>(s);
   snap = gbl(snap);
@@ -1559,6 +1564,12 @@ __device__ __forceinline__ bool contactStage(const ModelDev& md, double* s, cons
     // LCP pool later); the dynamics are in the snapshot's dynamics cache
     for (int t = lane; t < CT_CONTACTS + nCon * CREC; t += WAVE) overflowWs[t] = ct[t];
     if (lane == 0) snap[SN_STATUS] = (double)((int)ct[H_STATUS] | ST_DEFERRED);
+    if (deferList != nullptr && lane == 0) {
+      // the wide kernel's order: largest LCPs first (deferBucket)
+      const int q = deferBucket(m);
+      const int i = __hip_atomic_fetch_add(deferList + q, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      deferList[DEFER_BUCKETS + q * gridDim.x + i] = env;
+    }
     WSYNC();
     return true;
   }

@@ -26,6 +26,9 @@
 #define CT_PAIR_CHUNK 16
 #define CT_PAIR_CHUNK_HOST CT_PAIR_CHUNK
 // contact records one mesh pair may produce, and its LDS scratch (mesh.cuh)
+// the one-row forward kernel's deferred worlds, in DEFER_BUCKETS lists by LCP
+// rows (contact.cuh deferBucket) for the wide kernel's launch order
+#define DEFER_BUCKETS 4
 #define MESH_PAIR_RECS 64
 #define MESH_PAIR_SCRATCH (16 * 64)
 // the forward's header + kept contacts live in Layout::ct; the dropped list

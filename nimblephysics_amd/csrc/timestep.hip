@@ -308,7 +308,7 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
                                              const double* __restrict__ state, const double* __restrict__ forces,
                                              double* __restrict__ lcpCache, double* __restrict__ nextState,
                                              double* __restrict__ snapshot, int snapDoubles, int cacheDoubles,
-                                             int deferRows) {
+                                             int deferRows, int env, int* deferList) {
   extern __shared__ double s[];
   const ModelDev& md = *mdp;
   const int lane = threadIdx.x & (WAVE - 1);
@@ -326,7 +326,6 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
       // step's wave leaves idle (lower wave priority on the shared SIMD)
       __builtin_amdgcn_s_setprio(0);
       {
-        const int env = blockIdx.x;
         double* ct = lds<true>(s) + L.ct;
 #ifdef NIMBLE_STAGE_TIMING
         // where the helper runs: HW_ID (SIMD, CU, SE) and XCC_ID
@@ -355,7 +354,6 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
     __builtin_amdgcn_s_setprio(2);
   }
   {
-    const int env = blockIdx.x;
     const double* st = state + (size_t)env * 2 * n;
 #ifdef NIMBLE_STAGE_TIMING
     double* g_stamp = md.numPairs > 0 ? snapshot + (size_t)env * snapDoubles + snStamps(n) : nullptr;
@@ -414,7 +412,8 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
     if (md.numPairs > 0) {
       double* sn = snapshot + (size_t)env * snapDoubles;
       deferred = contactStage<R>(md, s, L, lane, v1, x, lcpCache + (size_t)env * cacheDoubles, sn,
-                                 sn + snapWorkspaceOffset(n), helperOn, helperOn && R == 1, deferRows, R > 1);
+                                 sn + snapWorkspaceOffset(n), helperOn, helperOn && R == 1, deferRows, R > 1,
+                                 deferList, env);
     } else if (lane < 8) {
       // a model without collision pairs still has a snapshot header (no
       // contacts, no rows, no clamping) for the getters to read
@@ -447,8 +446,9 @@ extern "C" __global__ void __launch_bounds__(2 * WAVE) __attribute__((amdgpu_wav
 nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, const double* __restrict__ state,
                       const double* __restrict__ forces, double* __restrict__ lcpCache,
                       double* __restrict__ nextState, double* __restrict__ snapshot, int snapDoubles,
-                      int cacheDoubles, int deferRows) {
-  forwardWorld<1>(mdp, L, state, forces, lcpCache, nextState, snapshot, snapDoubles, cacheDoubles, deferRows);
+                      int cacheDoubles, int deferRows, int* deferList) {
+  forwardWorld<1>(mdp, L, state, forces, lcpCache, nextState, snapshot, snapDoubles, cacheDoubles, deferRows,
+                  blockIdx.x, deferList);
 }
 
 // the worlds nimble_forward_kernel deferred (snapshot status ST_DEFERRED),
@@ -462,10 +462,26 @@ extern "C" __global__ void __launch_bounds__(2 * WAVE) __attribute__((amdgpu_wav
 nimble_forward_wide_kernel(const ModelDev* __restrict__ mdp, Layout L, const double* __restrict__ state,
                            const double* __restrict__ forces, double* __restrict__ lcpCache,
                            double* __restrict__ nextState, double* __restrict__ snapshot, int snapDoubles,
-                           int cacheDoubles) {
-  const int st = uni((int)snapshot[(size_t)blockIdx.x * snapDoubles + SN_STATUS]);
+                           int cacheDoubles, const int* deferList) {
+  // workgroup b steps the b-th deferred world in the one-row kernel's lists,
+  // the largest LCPs first (deferList: DEFER_BUCKETS counters, then one list
+  // of gridDim.x world indices per bucket): the slowest worlds start at once
+  // instead of behind the others on a CU (one wide world per CU)
+  int env = blockIdx.x;
+  if (deferList) {
+    int b = blockIdx.x, q = 0;
+    for (; q < DEFER_BUCKETS; q++) {
+      const int c = deferList[q];
+      if (b < c) break;
+      b -= c;
+    }
+    if (q == DEFER_BUCKETS) return;  // (whole workgroup: past the deferred worlds)
+    env = deferList[DEFER_BUCKETS + q * gridDim.x + b];
+  }
+  const int st = uni((int)snapshot[(size_t)env * snapDoubles + SN_STATUS]);
   if (!(st & ST_DEFERRED)) return;  // (whole workgroup)
-  forwardWorld<2>(mdp, L, state, forces, lcpCache, nextState, snapshot, snapDoubles, cacheDoubles, 1 << 30);
+  forwardWorld<2>(mdp, L, state, forces, lcpCache, nextState, snapshot, snapDoubles, cacheDoubles, 1 << 30, env,
+                  nullptr);
 }
 
 // ---------------------------------------------------------------------------

@@ -205,6 +205,9 @@ void launch(K kernel, dim3 grid, dim3 block, size_t lds, A... args) {
 #define __hip_atomic_compare_exchange_strong(p, e, d, o1, o2, s) \
   __atomic_compare_exchange_n((p), (e), (d), false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST)
 #define __HIP_MEMORY_SCOPE_WORKGROUP 0
+#define __HIP_MEMORY_SCOPE_AGENT 1
+// (lane 0 only: the deferred-world lists)
+#define __hip_atomic_fetch_add(p, v, o, s) __atomic_fetch_add((p), (v), __ATOMIC_SEQ_CST)
 
 inline int __double2loint(double d) { return (int)(uint32_t)wave_emu::asU(d); }
 inline int __double2hiint(double d) { return (int)(uint32_t)(wave_emu::asU(d) >> 32); }
@@ -237,6 +240,7 @@ template <class T>
 inline hipError_t hipMalloc(T** p, size_t n) { return hipMalloc((void**)p, n); }
 inline hipError_t hipFree(void* p) { std::free(p); return 0; }
 inline hipError_t hipMemcpy(void* d, const void* s, size_t n, int) { std::memcpy(d, s, n); return 0; }
+inline hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t) { std::memset(p, v, n); return 0; }
 inline hipError_t hipGetLastError() { return 0; }
 inline const char* hipGetErrorString(hipError_t) { return "emulated"; }
 #define hipLaunchKernelGGL(k, g, b, lds, st, ...) wave_emu::launch(k, dim3(g), dim3(b), (size_t)(lds), __VA_ARGS__)

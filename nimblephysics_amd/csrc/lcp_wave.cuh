@@ -658,15 +658,13 @@ struct WaveDantzig {
   // b_k = +0 (masked L entries: B - 0 * 0 is B bit for bit).  0 * b_k leaves
   // a lane unchanged only for finite b_k; a non-finite b_k (degenerate
   // factor) re-runs the solve predicated, exactly as the reference's loop.
-  // kLo: m <= 64, every row the solve can change is in slot 0 (the other
-  // slots are neither loaded nor updated)
-  template <int S, bool kFull, bool kT, bool kLo = false>
+  template <int S, bool kFull, bool kT>
   __device__ __forceinline__ void solveBlock(double (&B)[R], int m, int k0, const int (&lOff)[R]) {
     // steps: k = k0 + u (L) or k = k0 + 7 - u (L^T, k0 the block's lowest row)
     double Lk[R][8];
 #pragma unroll
     for (int s = 0; s < R; s++) {
-      if ((kT ? s > S : s < S) || (kLo && s > 0)) continue;
+      if (kT ? s > S : s < S) continue;
 #pragma unroll
       for (int u = 0; u < 8; u++) {
         const int k = kT ? k0 + 7 - u : k0 + u;
@@ -679,13 +677,13 @@ struct WaveDantzig {
     // wait for each load in turn)
 #pragma unroll
     for (int s = 0; s < R; s++) {
-      if ((kT ? s > S : s < S) || (kLo && s > 0)) continue;
+      if (kT ? s > S : s < S) continue;
 #pragma unroll
       for (int u = 0; u < 8; u++) asm volatile("" : "+v"(Lk[s][u]));
     }
 #pragma unroll
     for (int s = 0; s < R; s++) {
-      if ((kT ? s > S : s < S) || (kLo && s > 0)) continue;
+      if (kT ? s > S : s < S) continue;
 #pragma unroll
       for (int u = 0; u < 8; u++) {
         const int k = kT ? k0 + 7 - u : k0 + u;
@@ -700,15 +698,14 @@ struct WaveDantzig {
       if (!kFull) bk = live ? bk : 0.0;
 #pragma unroll
       for (int s = 0; s < R; s++) {
-        if ((kT ? s > S : s < S) || (kLo && s > 0)) continue;
+        if (kT ? s > S : s < S) continue;
         B[s] -= Lk[s][u] * bk;
       }
     }
   }
   template <bool kFull, bool kT>
   __device__ __forceinline__ void solveBlockAt(double (&B)[R], int m, int k0, const int (&lOff)[R]) {
-    if (R > 1 && m <= 64) solveBlock<0, kFull, kT, true>(B, m, k0, lOff);
-    else if (R == 1 || k0 < 64) solveBlock<0, kFull, kT>(B, m, k0, lOff);
+    if (R == 1 || k0 < 64) solveBlock<0, kFull, kT>(B, m, k0, lOff);
     else solveBlock<R - 1, kFull, kT>(B, m, k0, lOff);
   }
   __device__ __forceinline__ void solveL1(double (&B)[R], int m) {

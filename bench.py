@@ -7,9 +7,11 @@ TimestepLayer.forward/backward, python/nimblephysics/timestep.py), then the
 batch state advances to the new state (a rollout, so contacts evolve and the
 LCP warm start is exercised).  Inputs are resident in HBM.
 
-Multi-GPU (torchrun): one process per GPU, each advancing its own shard of
-independent worlds (weak scaling, no data-path collective); the timed region
-is bracketed by barriers and the max over ranks is used.
+Multi-GPU: one process per GPU, each advancing its own shard of independent
+worlds (weak scaling; the per-step RCCL all-gather of the action gradients is
+the only exchange); the timed region is bracketed by barriers and the max
+over ranks is used.  The ranks come from torchrun (WORLD_SIZE must equal
+--gpus) or, without a launcher, `bench.py --gpus N` spawns them itself.
 """
 import argparse
 import json
@@ -52,15 +54,65 @@ WORKLOADS = {
 }
 
 
-def init_dist():
+def init_dist(device_type="cuda"):
+    """torch.distributed from the env a launcher set (torchrun, or
+    launch_ranks below): RCCL ("nccl") on the GPU, gloo for the CPU test
+    path.  Returns (dist or None, rank, world size, local rank)."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     if ws > 1:
         import torch.distributed as dist
         local = int(os.environ.get("LOCAL_RANK", "0"))
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if device_type == "cuda":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
         return dist, dist.get_rank(), ws, local
     return None, 0, 1, 0
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_entry(rank, nranks, port, argv):
+    """Body of one rank started by launch_ranks: the torchrun env for this
+    rank, then the ordinary single-rank main."""
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(nranks), LOCAL_WORLD_SIZE=str(nranks),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      NIMBLE_BENCH_LAUNCHER=f"bench.py --gpus {nranks} (one spawned process per GPU)")
+    run(parse_args(argv))
+
+
+def launch_ranks(argv, nranks, target=None):
+    """`bench.py --gpus N` without a launcher: start N fresh rank processes
+    (multiprocessing "spawn": new interpreters, one per GPU) before this
+    process makes any HIP call, each with the env torchrun would give it, and
+    wait for all of them.  Rank 0 prints the JSON line.  Returns the exit code
+    (non-zero if any rank failed)."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    target = target or _rank_entry
+    procs = [ctx.Process(target=target, args=(r, nranks, port, list(argv))) for r in range(nranks)]
+    for p in procs:
+        p.start()
+    from multiprocessing.connection import wait
+    code = 0
+    live = list(procs)
+    while live:
+        wait([p.sentinel for p in live])
+        for p in [p for p in live if not p.is_alive()]:
+            live.remove(p)
+            if p.exitcode != 0 and not code:
+                code = p.exitcode if p.exitcode and p.exitcode > 0 else 1
+                # a failed rank leaves the others waiting in a collective
+                for q in live:
+                    q.terminate()
+    return code
 
 
 def barrier(dist):
@@ -202,10 +254,11 @@ def rollout_stats(world, state, action, warmup, steps):
             "source": f"snapshot headers of the {steps} timed steps (deterministic replay after timing)"}
 
 
-def pmc_traffic(workload, kernel, batch):
-    """HBM bytes per launch of `kernel` from the committed PMC summary
+def pmc_traffic(workload, kernels, batch):
+    """HBM bytes per step of `kernels` (summed: the mesh model's forward is the
+    one-row launch plus the wide launch) from the committed PMC summary
     (profiles/pmc_traffic.json: per-world FETCH_SIZE + WRITE_SIZE of the same
-    kernel on the same workload, measured by tools/pmc_traffic.py under
+    kernels on the same workload, measured by tools/pmc_traffic.py under
     rocprofv3 --pmc -- counters cannot be read inside this process); None when
     absent.  Returned with the summary's provenance."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -213,8 +266,9 @@ def pmc_traffic(workload, kernel, batch):
         return None, None
     try:
         d = json.load(open(path))
-        e = d[workload][kernel]
-        return float(e["bytes_per_world"]) * batch, e.get("source", "profiles/pmc_traffic.json")
+        es = [d[workload][k] for k in kernels]
+        return (sum(float(e["bytes_per_world"]) for e in es) * batch,
+                es[0].get("source", "profiles/pmc_traffic.json") + f" ({' + '.join(kernels)})")
     except Exception:
         return None, None
 
@@ -235,13 +289,18 @@ def pmc_mfma(workload, kernel):
 
 
 def _cpu_threads():
+    """(threads to use, affinity size, why).  The GPU box grants each GPU a
+    CPU share that its harness exports as OMP_NUM_THREADS (16 per GPU there;
+    os.cpu_count() and the affinity mask show the whole machine): use every
+    core of that share, or every affinity core when no share is exported."""
     try:
         n = len(os.sched_getaffinity(0))
     except AttributeError:
         n = os.cpu_count() or 1
-    # the GPU box's CPU share is 16 cores per GPU (os.cpu_count() shows the
-    # whole machine there)
-    return max(1, min(n, 16)), n
+    share = os.environ.get("OMP_NUM_THREADS")
+    if share and share.isdigit() and int(share) > 0:
+        return max(1, min(n, int(share))), n, f"OMP_NUM_THREADS={share}: the host's CPU share for this GPU job"
+    return n, n, "every core of the affinity mask"
 
 
 def _host_cores():
@@ -260,7 +319,7 @@ def cpu_baseline(make, batch, sampler, seconds_target=12.0):
     ~seconds_target (ctypes releases the GIL inside the C library)."""
     import threading
     from oracle.oracle import OracleWorld
-    threads, usable = _cpu_threads()
+    threads, usable, why = _cpu_threads()
     host_cpus, affinity = _host_cores()
     counts = [0] * threads
     stop = [False]
@@ -288,39 +347,62 @@ def cpu_baseline(make, batch, sampler, seconds_target=12.0):
     steps = sum(counts)
     return {"value": steps * batch / dt, "unit": "timesteps/s", "cores": threads, "kind": "port",
             "host_cpu_count": host_cpus, "affinity_cpus": affinity,
-            "cores_note": "threads used = min(affinity, 16): the GPU box's CPU share is 16 cores per GPU, while "
-                          "os.cpu_count() there shows the whole machine",
+            "cores_note": f"threads used = {threads} ({why}); affinity mask {usable} cores",
             "sample": f"{steps} fwd+bwd steps x {batch} worlds of the same workload, oracle/liboracle.so "
                       f"(CPU restatement of the reference's step), {threads} threads, {dt:.1f}s"}
+
+
+def solver_flops(rows, counts):
+    """fp64 FLOPs of the iterative LCP solvers per world from the counts the
+    forward kernels record in each snapshot header (batch averages): a
+    Dantzig pivot on an m-row problem with an active set of k ~ m/2 rows does
+    the two triangular solves of solve1 (2 k^2), the pivot-column matvec
+    (2 m k) and the LDL^T row add / remove (k^2): ~1.75 m^2; a PGS sweep
+    does m rows of a 2m-FLOP dot product plus the clamp (~20): 2 m^2 + 20 m.
+    `counts` holds per-world means of pivots, of pivots x m^2 and of sweeps x
+    (2 m^2 + 20 m) (the kernels' m differs per world)."""
+    if not counts:
+        return 0.0
+    return 1.75 * counts["pivot_m2"] + counts["sweep_flops"]
 
 
 def measure(wl, batch, steps, warmup, dist, rank, ws, dev, gather):
     """Time `steps` bench steps (after `warmup`) of workload `wl` on this
     rank's `batch` worlds; returns the measured numbers (value = worlds x
-    steps x ranks / max-over-ranks elapsed)."""
+    steps x ranks / max-over-ranks elapsed).  On a CPU device (the launcher's
+    gloo test, with a host timestep patched in by the test) only the timing
+    and the gather run: the kernel timers, status words, replay statistics and
+    roofline need the GPU."""
     wl_name, make, sampler, metric, default_batch = WORKLOADS[wl]
     batch = batch if batch > 0 else default_batch
+    gpu = dev.type == "cuda"
     world = make()
-    # status words are recorded on the device each step (no per-step host
-    # sync) and checked once after the timed region: a world whose step could
-    # not be the reference's fails the bench instead of being timed
-    world.setStatusPolicy("record")
     n = world.getNumDofs()
     st, f, g = rank_inputs(world, sampler, batch, rank)
     state = torch.tensor(st, device=dev)
     action = torch.tensor(f, device=dev)
     g = torch.tensor(g, device=dev)
     state0 = state.clone()
-    devworld = world.native()
+    status_acc = None
     timer = KernelTimer()
-    timer.wrap(devworld)
-    status_acc = torch.zeros(batch, dtype=torch.int32, device=dev)
+    if gpu:
+        # status words are recorded on the device each step (no per-step host
+        # sync) and checked once after the timed region: a world whose step
+        # could not be the reference's fails the bench instead of being timed
+        world.setStatusPolicy("record")
+        timer.wrap(world.native())
+        status_acc = torch.zeros(batch, dtype=torch.int32, device=dev)
     one_step = make_step(nimble.timestep, world, action, g, gather, dist, ws, status_acc)
     for _ in range(warmup):
         state = one_step(state)
-    timer.enabled = True
+    timer.enabled = gpu
     state, elapsed = timed_loop(one_step, state, steps, 0, dist, dev)
     timer.enabled = False
+    out = {"wl": wl, "wl_name": wl_name, "metric": metric, "make": make, "sampler": sampler, "batch": batch, "n": n,
+           "value": batch * ws * steps / elapsed, "ms_per_step": elapsed / steps * 1e3, "cstats": None,
+           "flops": None}
+    if not gpu:
+        return out
     bad = int(((status_acc & _native.ST_DIVERGES) != 0).sum().item())
     if bad:
         raise SystemExit(f"bench ({wl}): {bad} world(s) left the reference's physics "
@@ -332,14 +414,97 @@ def measure(wl, batch, steps, warmup, dist, rank, ws, dev, gather):
     dom = "backward" if bwd_ms >= fwd_ms else "forward"
     dom_ms = max(bwd_ms, fwd_ms)
     achieved = flops[dom] * batch / (dom_ms * 1e-3) / 1e12
-    traffic, traffic_src = pmc_traffic(wl, f"nimble_{dom}_kernel", batch)
-    return {"wl": wl, "wl_name": wl_name, "metric": metric, "make": make, "sampler": sampler, "batch": batch, "n": n,
-            "value": batch * ws * steps / elapsed, "ms_per_step": elapsed / steps * 1e3, "cstats": cstats,
-            "fwd_ms": fwd_ms, "bwd_ms": bwd_ms, "dom": dom, "achieved": achieved, "flops": flops,
-            "traffic": traffic, "traffic_src": traffic_src}
+    traffic, traffic_src = pmc_traffic(wl, [f"nimble_{dom}_kernel"] + ([f"nimble_{dom}_wide_kernel"]
+                                                                      if wl == "atlas_mesh" else []), batch)
+    out.update(cstats=cstats, fwd_ms=fwd_ms, bwd_ms=bwd_ms, dom=dom, achieved=achieved, flops=flops,
+               traffic=traffic, traffic_src=traffic_src)
+    sc = cstats.get("solver_counts")
+    if sc is not None:
+        fs = dict(flops)
+        fs["forward"] = flops["forward"] + solver_flops(cstats["rows"], sc)
+        out.update(flops_solvers=fs, solver_counts=sc,
+                   achieved_solvers=fs[dom] * batch / (dom_ms * 1e-3) / 1e12)
+    return out
 
 
-def main():
+def roofline(r, wl):
+    """The `roofline` object for the dominant kernel of the headline."""
+    dom = r["dom"]
+    out = {"bound": "fp64-valu", "kernel": f"nimble_{dom}_kernel", "achieved": r["achieved"],
+           "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": r["achieved"] / FP64_VECTOR_PEAK_TFLOPS,
+           "traffic": r["traffic"], "traffic_source": r["traffic_src"],
+           **pmc_mfma(wl, f"nimble_{dom}_kernel"),
+           "flops_per_world": r["flops"][dom]}
+    if r.get("achieved_solvers") is not None:
+        out["achieved_with_solvers"] = r["achieved_solvers"]
+        out["frac_with_solvers"] = r["achieved_solvers"] / FP64_VECTOR_PEAK_TFLOPS
+        out["flops_per_world_with_solvers"] = r["flops_solvers"][dom]
+        out["solver_counts"] = r["solver_counts"]
+    out["note"] = ("peak = MI355X fp64 vector (VALU) rate, which on MI355X equals the fp64 matrix-core rate; "
+                   "frac counts the direct work (dynamics, rows, A = Y^T Y on v_mfma_f64_16x16x4f64, COD solves, "
+                   "backward precompute); frac_with_solvers adds the iterative solvers' work from the pivot and "
+                   "sweep counts the kernels record per world (Dantzig pivots, PGS sweeps); traffic = HBM bytes "
+                   "per launch (2 x FETCH_SIZE + WRITE_SIZE, separate rocprofv3 --pmc passes) from the committed "
+                   "summary profiles/pmc_traffic.json")
+    return out
+
+
+def mesh_report(args, mesh):
+    """The `atlas_mesh` object: the reference atlas_bench's own model."""
+    mf = mesh["flops"]
+    kern = {"forward": "nimble_forward_kernel + nimble_forward_wide_kernel",
+            "backward": "nimble_backward_kernel + nimble_backward_wide_kernel"}[mesh["dom"]]
+    out = {"workload": mesh["wl_name"], "metric": mesh["metric"], "value": mesh["value"], "unit": "timesteps/s",
+           "ms_per_step": mesh["ms_per_step"], "steps": min(args.steps, 20),
+           "kernels_ms": {"forward": mesh["fwd_ms"], "backward": mesh["bwd_ms"],
+                          "note": "forward = nimble_forward_kernel + nimble_forward_wide_kernel (the worlds the "
+                                  "one-row kernel defers), backward likewise; per-kernel split in "
+                                  "profiles/*kernel_stats_atlas_mesh*"},
+           "contacts_per_world": mesh["cstats"]["contacts"], "lcp_rows_per_world": mesh["cstats"]["rows"],
+           "clamping_rows_per_world": mesh["cstats"]["clamping"],
+           "frac": mesh["achieved"] / FP64_VECTOR_PEAK_TFLOPS, "frac_kernel": kern,
+           "flops_per_world": mf[mesh["dom"]], "traffic": mesh["traffic"], "traffic_source": mesh["traffic_src"],
+           **pmc_mfma("atlas_mesh", "nimble_forward_wide_kernel")}
+    if mesh.get("achieved_solvers") is not None:
+        out["frac_with_solvers"] = mesh["achieved_solvers"] / FP64_VECTOR_PEAK_TFLOPS
+        out["flops_per_world_with_solvers"] = mesh["flops_solvers"][mesh["dom"]]
+        out["solver_counts"] = mesh["solver_counts"]
+    return out
+
+
+def report(args, r, mesh, ws, gather):
+    """Rank 0's JSON line."""
+    cstats = r["cstats"]
+    out = {
+        "metric": r["metric"],
+        "value": r["value"], "unit": "timesteps/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": r["ms_per_step"], "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (perturbed poses near / in ground contact, random torques)",
+        "config": {"workload": r["wl_name"], "worlds_per_gpu": r["batch"], "dofs": r["n"],
+                   "global_batch": r["batch"] * ws,
+                   "parallelism": f"independent worlds x{ws}" + (" + RCCL all-gather of action grads" if gather else ""),
+                   "launcher": os.environ.get("NIMBLE_BENCH_LAUNCHER", "torchrun" if ws > 1 else "single process"),
+                   **({k: cstats[k] for k in ("contacts", "rows", "clamping", "worlds_in_contact", "source")}
+                      if cstats else {})},
+    }
+    if cstats:
+        out["config"] = {**{k: v for k, v in out["config"].items()
+                            if k not in ("contacts", "rows", "clamping", "worlds_in_contact", "source")},
+                         "contacts_per_world": cstats["contacts"], "lcp_rows_per_world": cstats["rows"],
+                         "clamping_rows_per_world": cstats["clamping"],
+                         "worlds_in_contact": cstats["worlds_in_contact"], "contact_stats_source": cstats["source"]}
+    if r["flops"] is not None:
+        out["kernels_ms"] = {"forward": r["fwd_ms"], "backward": r["bwd_ms"]}
+        out["roofline"] = roofline(r, args.workload)
+    if mesh is not None:
+        out["atlas_mesh"] = mesh_report(args, mesh)
+    if not args.no_cpu_baseline and args.device == "cuda":
+        out["cpu_baseline"] = cpu_baseline(r["make"], 16, r["sampler"])
+    return out
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -351,11 +516,23 @@ def main():
                     help="skip the second measurement of the reference atlas_bench's STL-mesh Atlas")
     ap.add_argument("--gather-grads", type=int, default=-1,
                     help="all-gather action gradients each step (default: on when N > 1)")
-    args = ap.parse_args()
+    ap.add_argument("--device", default="cuda", choices=("cuda", "cpu"),
+                    help="cpu: gloo process group on host tensors (the launcher's CPU test; the product "
+                         "timestep itself runs only on the GPU)")
+    ap.add_argument("--out", default=None, help="also write rank 0's JSON line to this file")
+    return ap.parse_args(argv)
 
-    dist, rank, ws, local = init_dist()
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+
+def run(args):
+    """One rank: init the process group from the env, measure, rank 0 prints."""
+    dist, rank, ws, local = init_dist(args.device)
+    if ws != args.gpus:
+        raise SystemExit(f"bench: WORLD_SIZE {ws} != --gpus {args.gpus}")
+    if args.device == "cuda":
+        dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+    else:
+        dev = torch.device("cpu")
     gather = (ws > 1) if args.gather_grads < 0 else bool(args.gather_grads)
     r = measure(args.workload, args.batch, args.steps, args.warmup, dist, rank, ws, dev, gather)
     # the reference atlas_bench's own model (atlas_v3_no_head.urdf, 29 STL
@@ -365,49 +542,34 @@ def main():
     if args.workload == "atlas" and not args.no_mesh:
         mesh = measure("atlas_mesh", args.batch, min(args.steps, 20), min(args.warmup, 3), dist, rank, ws, dev, gather)
     if rank == 0:
-        cstats, flops, dom = r["cstats"], r["flops"], r["dom"]
-        achieved = r["achieved"]
-        out = {
-            "metric": r["metric"],
-            "value": r["value"], "unit": "timesteps/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": r["ms_per_step"], "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic (perturbed poses near / in ground contact, random torques)",
-            "config": {"workload": r["wl_name"], "worlds_per_gpu": r["batch"], "dofs": r["n"],
-                       "global_batch": r["batch"] * ws,
-                       "parallelism": f"independent worlds x{ws}" + (" + RCCL all-gather of action grads" if gather else ""),
-                       "contacts_per_world": cstats["contacts"], "lcp_rows_per_world": cstats["rows"],
-                       "clamping_rows_per_world": cstats["clamping"],
-                       "worlds_in_contact": cstats["worlds_in_contact"], "contact_stats_source": cstats["source"]},
-            "kernels_ms": {"forward": r["fwd_ms"], "backward": r["bwd_ms"]},
-            "roofline": {"bound": "fp64-valu", "kernel": f"nimble_{dom}_kernel", "achieved": achieved,
-                         "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP64_VECTOR_PEAK_TFLOPS,
-                         "traffic": r["traffic"], "traffic_source": r["traffic_src"],
-                         **pmc_mfma(args.workload, f"nimble_{dom}_kernel"),
-                         "flops_per_world": flops[dom],
-                         "note": "peak = MI355X fp64 vector (VALU) rate, which on MI355X equals the fp64 "
-                                 "matrix-core rate; the forward's one dense product (the LCP matrix A = Y^T Y) runs "
-                                 "on v_mfma_f64_16x16x4f64, everything else on the VALU; traffic = HBM bytes per "
-                                 "launch (2 x FETCH_SIZE + WRITE_SIZE, separate rocprofv3 --pmc passes) from the "
-                                 "committed summary profiles/pmc_traffic.json (tools/gpu_measure.sh)"},
-        }
-        if mesh is not None:
-            mf = mesh["flops"]
-            out["atlas_mesh"] = {
-                "workload": mesh["wl_name"], "metric": mesh["metric"], "value": mesh["value"], "unit": "timesteps/s",
-                "ms_per_step": mesh["ms_per_step"], "steps": min(args.steps, 20),
-                "kernels_ms": {"forward": mesh["fwd_ms"], "backward": mesh["bwd_ms"],
-                               "note": "forward = nimble_forward_kernel + nimble_forward_wide_kernel (the > 64-row "
-                                       "worlds), backward likewise; per-kernel split in profiles/*kernel_stats_atlas_mesh*"},
-                "contacts_per_world": mesh["cstats"]["contacts"], "lcp_rows_per_world": mesh["cstats"]["rows"],
-                "clamping_rows_per_world": mesh["cstats"]["clamping"],
-                "frac": mesh["achieved"] / FP64_VECTOR_PEAK_TFLOPS, "frac_kernel": f"nimble_{mesh['dom']}_kernel",
-                "flops_per_world": mf[mesh["dom"]], "traffic": mesh["traffic"], "traffic_source": mesh["traffic_src"]}
-        if not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(r["make"], 16, r["sampler"])
-        print(json.dumps(out))
+        out = report(args, r, mesh, ws, gather)
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.out:
+            with open(args.out, "w") as fh:
+                fh.write(line + "\n")
     if dist is not None:
         dist.destroy_process_group()
+
+
+def main(argv=None, rank_target=None):
+    """`python bench.py --gpus N ...`: under a launcher (torchrun: WORLD_SIZE
+    set) this process is one rank and WORLD_SIZE must equal N; without one,
+    N > 1 starts N rank processes itself (launch_ranks) so the job spans N
+    GPUs either way."""
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = parse_args(argv)
+    if args.gpus < 1:
+        raise SystemExit("bench: --gpus must be >= 1")
+    env_ws = os.environ.get("WORLD_SIZE")
+    if env_ws is not None and int(env_ws) != args.gpus:
+        raise SystemExit(f"bench: WORLD_SIZE={env_ws} from the launcher but --gpus {args.gpus}")
+    if args.gpus > 1 and env_ws is None:
+        code = launch_ranks(argv, args.gpus, rank_target)
+        if code:
+            raise SystemExit(code)
+        return
+    run(args)
 
 
 if __name__ == "__main__":

@@ -3,6 +3,7 @@ include/nimble_amd.h declares, the world description flattening, the
 ctypes struct layout, the product path refusing CPU tensors (no fallback),
 and the multi-rank bench harness on gloo (world_size 2)."""
 import ctypes as C
+import json
 import os
 import re
 import socket
@@ -238,6 +239,97 @@ def test_bench_sharded_gather_gloo_two_ranks():
             assert gathered[k].shape == (2 * B, 6)
             assert np.array_equal(gathered[k], want), (r, k)
     assert not np.array_equal(own[0][0].numpy(), own[1][0].numpy())  # shards differ
+
+
+_BOX_WL = ("box on ground (launcher test)", models.box_world, models._box_sampler, "launcher test metric", 6)
+
+
+def _bench_spawned_rank(rank, nranks, port, argv):
+    """One rank started by bench.launch_ranks in the launcher test: the host
+    timestep (the oracle behind the autograd signature) in place of the GPU
+    one, every all-gathered gradient recorded, then bench's own rank body."""
+    import sys
+    from types import SimpleNamespace
+    sys.path.insert(0, ROOT)
+    import bench
+    from oracle.oracle import OracleWorld
+    bench.WORKLOADS["box"] = _BOX_WL
+    ows = {}
+
+    def ts(w, s, a):
+        return _OracleTimestep.apply(ows.setdefault(id(w), OracleWorld(w)), w, s, a)
+
+    bench.nimble = SimpleNamespace(timestep=ts)
+    rec = []
+    gather0 = bench.gather_grads
+
+    def gather(dist, grad, ws):
+        out = gather0(dist, grad, ws)
+        rec.append(out.numpy().copy())
+        return out
+
+    bench.gather_grads = gather
+    bench._rank_entry(rank, nranks, port, argv)
+    outdir = os.path.dirname(argv[argv.index("--out") + 1])
+    np.save(os.path.join(outdir, f"gathered_rank{rank}.npy"), np.stack(rec))
+
+
+def test_bench_main_spawns_ranks_for_gpus_two(tmp_path, monkeypatch):
+    """`bench.py --gpus 2` with no launcher env starts its own two rank
+    processes (bench.launch_ranks, spawned before any device call), each
+    with the env torchrun would set; the ranks form a gloo group, step their
+    own shards, all-gather the action gradients every step, and rank 0
+    writes the one JSON line with n_gpus = 2.  Every gathered [2B, m] tensor
+    equals the concatenation of both ranks' own gradients recomputed here."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setitem(bench.WORKLOADS, "box", _BOX_WL)
+    out = tmp_path / "bench.json"
+    argv = ["--gpus", "2", "--device", "cpu", "--workload", "box", "--steps", "2", "--warmup", "1",
+            "--no-cpu-baseline", "--out", str(out)]
+    bench.main(argv, rank_target=_bench_spawned_rank)
+    line = json.loads(out.read_text())
+    assert line["n_gpus"] == 2 and line["steps"] == 2 and line["config"]["global_batch"] == 12
+    assert "all-gather" in line["config"]["parallelism"] and line["value"] > 0
+    world = models.box_world()
+    own = [_oracle_rollout_grads(world, r, 6, 3) for r in range(2)]
+    for r in range(2):
+        got = np.load(tmp_path / f"gathered_rank{r}.npy")
+        assert got.shape == (3, 12, 6)  # 1 warmup + 2 timed steps
+        for k in range(3):
+            assert np.array_equal(got[k], np.concatenate([own[0][k].numpy(), own[1][k].numpy()])), (r, k)
+
+
+def test_bench_main_rejects_world_size_mismatch(monkeypatch):
+    """A launcher's WORLD_SIZE that differs from --gpus is an error (the run
+    would otherwise time another number of GPUs than it reports)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    with pytest.raises(SystemExit) as e:
+        bench.main(["--gpus", "2", "--no-cpu-baseline"])
+    assert e.value.code not in (0, None)
+
+
+def test_bench_failed_rank_fails_the_launch(tmp_path, monkeypatch):
+    """A rank that exits non-zero makes launch_ranks return non-zero and
+    stops the ranks still waiting."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    code = bench.launch_ranks(["--gpus", "2"], 2, target=_bench_failing_rank)
+    assert code == 3
+
+
+def _bench_failing_rank(rank, nranks, port, argv):
+    import time
+    if rank == 1:
+        raise SystemExit(3)
+    time.sleep(60)
 
 
 def test_dynamics_setters_invalidate_device_model():

@@ -238,7 +238,7 @@ def rollout_stats(world, state, action, warmup, steps):
     idx = torch.tensor(world.getActionSpace(), dtype=torch.long, device=state.device)
     forces.index_copy_(1, idx, action)
     snap = torch.zeros((B, dev.snapshot_doubles), dtype=torch.float64, device=state.device)
-    acc = torch.zeros(4, dtype=torch.float64, device=state.device)
+    acc = torch.zeros(7, dtype=torch.float64, device=state.device)
     cur = state.clone()
     stream = torch.cuda.current_stream().cuda_stream
     for k in range(warmup + steps):
@@ -248,10 +248,19 @@ def rollout_stats(world, state, action, warmup, steps):
             h = snap[:, :3]
             acc[:3] += h.sum(0)
             acc[3] += (h[:, 0] > 0).sum()
+            # the LCP solvers' executed work the kernels tally per world
+            acc[4:7] += snap[:, _native.SN_PIVOTS:_native.SN_SOLVER_FLOPS + 1].sum(0)
         cur = nxt
     a = (acc / (B * max(steps, 1))).cpu().numpy()
-    return {"contacts": float(a[0]), "rows": float(a[1]), "clamping": float(a[2]), "worlds_in_contact": float(a[3]),
-            "source": f"snapshot headers of the {steps} timed steps (deterministic replay after timing)"}
+    out = {"contacts": float(a[0]), "rows": float(a[1]), "clamping": float(a[2]), "worlds_in_contact": float(a[3]),
+           "source": f"snapshot headers of the {steps} timed steps (deterministic replay after timing)"}
+    if dev.num_pairs > 0:
+        out["solver_counts"] = {"dantzig_pivots_per_world": float(a[4]), "pgs_sweeps_per_world": float(a[5]),
+                                "solver_flops_per_world": float(a[6]),
+                                "source": "snapshot elements NIMBLE_SNAPSHOT_PIVOTS / _SWEEPS / _SOLVER_FLOPS: "
+                                          "the executed work of every Dantzig / PGS solve of the step (both "
+                                          "waves, speculative solves cancelled by the cascade included)"}
+    return out
 
 
 def pmc_traffic(workload, kernels, batch):
@@ -352,20 +361,6 @@ def cpu_baseline(make, batch, sampler, seconds_target=12.0):
                       f"(CPU restatement of the reference's step), {threads} threads, {dt:.1f}s"}
 
 
-def solver_flops(rows, counts):
-    """fp64 FLOPs of the iterative LCP solvers per world from the counts the
-    forward kernels record in each snapshot header (batch averages): a
-    Dantzig pivot on an m-row problem with an active set of k ~ m/2 rows does
-    the two triangular solves of solve1 (2 k^2), the pivot-column matvec
-    (2 m k) and the LDL^T row add / remove (k^2): ~1.75 m^2; a PGS sweep
-    does m rows of a 2m-FLOP dot product plus the clamp (~20): 2 m^2 + 20 m.
-    `counts` holds per-world means of pivots, of pivots x m^2 and of sweeps x
-    (2 m^2 + 20 m) (the kernels' m differs per world)."""
-    if not counts:
-        return 0.0
-    return 1.75 * counts["pivot_m2"] + counts["sweep_flops"]
-
-
 def measure(wl, batch, steps, warmup, dist, rank, ws, dev, gather):
     """Time `steps` bench steps (after `warmup`) of workload `wl` on this
     rank's `batch` worlds; returns the measured numbers (value = worlds x
@@ -421,7 +416,7 @@ def measure(wl, batch, steps, warmup, dist, rank, ws, dev, gather):
     sc = cstats.get("solver_counts")
     if sc is not None:
         fs = dict(flops)
-        fs["forward"] = flops["forward"] + solver_flops(cstats["rows"], sc)
+        fs["forward"] = flops["forward"] + sc["solver_flops_per_world"]
         out.update(flops_solvers=fs, solver_counts=sc,
                    achieved_solvers=fs[dom] * batch / (dom_ms * 1e-3) / 1e12)
     return out

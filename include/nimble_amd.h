@@ -176,6 +176,15 @@ int32_t nimble_num_collision_pairs(nimble_world_t world);
 #define NIMBLE_STATUS_LCP_TOO_LARGE 16    /* more than NIMBLE_MAX_SOLVED_LCP LCP
                                              rows: contacts recorded, the
                                              constraint solve not taken      */
+#define NIMBLE_STATUS_PROTOCOL 64         /* a wait between the world's two
+                                             waves hit the kernel's deadlock
+                                             guard; the step finished on one
+                                             wave (raised like the above)    */
+/* The LCP solvers' executed work in the step (snapshot elements, doubles):
+ * Dantzig pivots, PGS sweeps and their FLOPs, both waves of the world. */
+#define NIMBLE_SNAPSHOT_PIVOTS 9
+#define NIMBLE_SNAPSHOT_SWEEPS 10
+#define NIMBLE_SNAPSHOT_SOLVER_FLOPS 11
 
 /*
  * Batched differentiable forward step == neural::forwardPass + World::step

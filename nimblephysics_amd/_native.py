@@ -102,7 +102,9 @@ def snapshot_layout(n: int, timing: bool = False) -> dict:
     return L
 SN_FC = 16 + 13 * MAX_CONTACTS + 12 * MAX_LCP  # NIMBLE_SNAPSHOT_FC: clamping impulses f_c
 ST_CONTACT_OVERFLOW, ST_UNSUPPORTED_SHAPE, ST_DROPPED_OVERFLOW, ST_REDUCED, ST_LCP_TOO_LARGE = 1, 2, 4, 8, 16
-ST_DIVERGES = ST_CONTACT_OVERFLOW | ST_UNSUPPORTED_SHAPE | ST_DROPPED_OVERFLOW | ST_LCP_TOO_LARGE
+ST_PROTOCOL = 64  # a wait between a world's two waves hit the kernel's deadlock guard
+ST_DIVERGES = ST_CONTACT_OVERFLOW | ST_UNSUPPORTED_SHAPE | ST_DROPPED_OVERFLOW | ST_LCP_TOO_LARGE | ST_PROTOCOL
+SN_PIVOTS, SN_SWEEPS, SN_SOLVER_FLOPS = 9, 10, 11  # the LCP solvers' executed work (include/nimble_amd.h)
 MAX_SOLVED_LCP = 128  # include/nimble_amd.h NIMBLE_MAX_SOLVED_LCP (two rows per lane above 64)
 
 
@@ -122,6 +124,8 @@ def status_message(bits: int) -> str:
         why.append("dropped-contact list overflow")
     if bits & ST_LCP_TOO_LARGE:
         why.append(f"more than {MAX_SOLVED_LCP} LCP rows")
+    if bits & ST_PROTOCOL:
+        why.append("the kernel's two-wave deadlock guard expired (step finished on one wave)")
     return ", ".join(why)
 
 

@@ -43,19 +43,15 @@ struct nimble_world {
   Layout fwdWide{};     // the wide forward kernel's layout (LDS stage, see nimble_world_create)
   size_t wideLds = 0;   // its LDS bytes
   int jacWsDoubles = 0;  // per-workgroup LCP workspace of the Jacobian launch
-  // the one-row kernel's deferred-world lists (DEFER_BUCKETS counters + one
-  // list per bucket, per launch), read by the wide kernel; grown on demand
-  int* deferList = nullptr;
-  size_t deferCap = 0;
   int cacheDoubles = NIMBLE_MAX_LCP + 1;
   hipFunction_t dummy = nullptr;
   double* meshDev = nullptr;  // ModelDev::meshVerts
 };
 
 extern "C" __global__ void nimble_forward_kernel(const ModelDev*, Layout, const double*, const double*, double*,
-                                                 double*, double*, int, int, int, int*);
+                                                 double*, double*, int, int, int, int);
 extern "C" __global__ void nimble_forward_wide_kernel(const ModelDev*, Layout, const double*, const double*, double*,
-                                                      double*, double*, int, int, const int*);
+                                                      double*, double*, int, int, int);
 extern "C" __global__ void nimble_backward_kernel(const ModelDev*, int, const double*, const double*,
                                                   double*, int, const double*, double*, double*, int, double*, int,
                                                   double*, int, int, int);
@@ -417,7 +413,6 @@ int nimble_world_destroy(nimble_world_t w) {
   if (!w) return NIMBLE_OK;
   if (w->dev) (void)hipFree(w->dev);
   if (w->meshDev) (void)hipFree(w->meshDev);
-  if (w->deferList) (void)hipFree(w->deferList);
   delete w;
   return NIMBLE_OK;
 }
@@ -460,24 +455,16 @@ int nimble_forward(nimble_world_t w, int32_t batch, const double* state, const d
     const char* e = getenv("NIMBLE_AMD_LARGEST_FIRST");
     return !(e != nullptr && atoi(e) == 0);
   }();
-  if (wide && largestFirst) {
-    const int c0 = batch < chunk ? batch : chunk;
-    const size_t need = DEFER_BUCKETS + (size_t)DEFER_BUCKETS * c0;
-    if (need > w->deferCap) {
-      if (w->deferList) HIP_TRY(hipFree(w->deferList));
-      w->deferList = nullptr;
-      w->deferCap = 0;
-      HIP_TRY(hipMalloc(&w->deferList, need * sizeof(int)));
-      w->deferCap = need;
-    }
-  }
   for (int32_t b0 = 0; b0 < batch; b0 += chunk) {
     const int cnt = batch - b0 < chunk ? batch - b0 : chunk;
-    if (wide && largestFirst) HIP_TRY(hipMemsetAsync(w->deferList, 0, DEFER_BUCKETS * sizeof(int), st));
+    // the deferred-world lists live in this call's snapshot headers
+    // (contact.cuh deferEntry): only their counters are reset here
+    if (wide && largestFirst)
+      HIP_TRY(hipMemsetAsync(snapshot + (size_t)b0 * w->snapDoubles + SN_DEFERCNT, 0, DEFER_BUCKETS * sizeof(int), st));
     hipLaunchKernelGGL(nimble_forward_kernel, dim3(cnt), dim3(fwdThreads), lds, st, w->dev, w->fwd,
                        state + b0 * 2 * n, forces + b0 * n, lcp_cache + (size_t)b0 * w->cacheDoubles,
                        next_state + b0 * 2 * n, snapshot + (size_t)b0 * w->snapDoubles, w->snapDoubles,
-                       w->cacheDoubles, w->fwdDeferRows, wide && largestFirst ? w->deferList : nullptr);
+                       w->cacheDoubles, w->fwdDeferRows, wide && largestFirst ? 1 : 0);
     HIP_TRY(hipGetLastError());
     // the worlds whose LCP pool the one-row kernel does not hold on chip (or
     // more rows than the test threshold): stepped by the big-LDS wide kernel
@@ -486,7 +473,7 @@ int nimble_forward(nimble_world_t w, int32_t batch, const double* state, const d
       hipLaunchKernelGGL(nimble_forward_wide_kernel, dim3(cnt), dim3(128), w->wideLds, st, w->dev, w->fwdWide,
                          state + b0 * 2 * n, forces + b0 * n, lcp_cache + (size_t)b0 * w->cacheDoubles,
                          next_state + b0 * 2 * n, snapshot + (size_t)b0 * w->snapDoubles, w->snapDoubles,
-                         w->cacheDoubles, largestFirst ? (const int*)w->deferList : nullptr);
+                         w->cacheDoubles, largestFirst ? 1 : 0);
       HIP_TRY(hipGetLastError());
     }
   }

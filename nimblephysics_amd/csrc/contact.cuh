@@ -409,6 +409,9 @@ __device__ __forceinline__ void gramMfma(const double* Y, double* A, int n, int 
 #define H_HELPER 13 // 2 doubles = 4 ints: helper state (HS_*), unused x3
 #define H_COLLIDE 15  // 2 ints: collision-detection hand-off between the waves (CS_*)
 #define H_PAIRCNT 16   // 16 per-pair counts of the current chunk
+// the LCP solvers' executed-work tally (2 doubles = 4 ints: Dantzig pivots,
+// PGS sweeps, FLOPs, unused), in the pair counts' dead tail past the board
+#define H_TALLY 24
 // the LCP task board (BD_*, 16 ints): the pair counts are collision-time
 // scratch, dead once the contacts are final, when the board is first used
 #define H_BOARD H_PAIRCNT
@@ -458,22 +461,38 @@ __device__ __forceinline__ void helperPost(double* ct, int state, int lane) {
 __device__ __forceinline__ int helperState(double* ct) {
   return uni(__hip_atomic_load(helperFlags(ct), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
 }
-// spin with s_sleep until pred(state); bounded so that a protocol error
-// traps rather than hanging the device.  The bound (2^30 polls of at least
-// s_sleep(1) = 64 clocks: > 30 s at 2.4 GHz) is four orders of magnitude above
-// the slowest world's whole step (~1M clocks, profiling and CU contention
-// included), so only a deadlock reaches it, never a slow but live partner.
-constexpr long long kSpinBound = 1ll << 30;
+// Deadlock guard of every wait between the two waves: a wait that outlasts
+// kSpinTicks of the constant 100 MHz real-time counter (1 s: more than two
+// hundred times the slowest world's whole step, ~8.4M clocks = 3.5 ms, so
+// never a slow but live partner) gives up instead of hanging the device or
+// trapping: it raises the world's protocol flag (helperFlags(ct)[3], set
+// into the snapshot status as ST_PROTOCOL by wave 0, a status that makes the
+// step raise) and the waiting wave goes on alone -- wave 0 runs the rest of
+// the cascade serially, the helper leaves -- so every wave reaches its exit
+// and the launch drains.  The clock is read once per 64 polls.
+constexpr long long kSpinTicks = 100000000ll;
+__device__ __forceinline__ long long spinClock() { return (long long)__builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ bool spinExpired(long long t0, int it) {
+  return (it & 63) == 63 && spinClock() - t0 > kSpinTicks;
+}
+__device__ __forceinline__ void protocolFail(double* ct) { helperFlags(ct)[3] = 1; }
+__device__ __forceinline__ bool protocolFailed(double* ct) { return uni(helperFlags(ct)[3]) != 0; }
+// spin with s_sleep until pred(state); -1 when the guard expired
 template <class Pred>
 __device__ __forceinline__ int helperWait(double* ct, Pred pred) {
-  for (long long it = 0;; it++) {
+  const long long t0 = spinClock();
+  for (int it = 0;; it++) {
     const int st = helperState(ct);
     if (pred(st)) return st;
-    if (it > kSpinBound) __builtin_trap();
+    if (spinExpired(t0, it)) {
+      protocolFail(ct);
+      return -1;
+    }
     __builtin_amdgcn_s_sleep(1);
   }
 }
 __device__ __forceinline__ int* board(double* ct) { return reinterpret_cast<int*>(ct + H_BOARD); }
+__device__ __forceinline__ int* tallyOf(double* ct) { return reinterpret_cast<int*>(ct + H_TALLY); }
 __device__ __forceinline__ int boardGet(double* ct, int k) {
   return uni(__hip_atomic_load(board(ct) + k, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
 }
@@ -519,10 +538,15 @@ __device__ __forceinline__ int* collideFlag(double* ct) { return reinterpret_cas
 __device__ __forceinline__ void collidePost(double* ct, int state, int lane) {
   if (lane == 0) __hip_atomic_store(collideFlag(ct), state, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-__device__ __forceinline__ void collideWait(double* ct, int want) {
-  for (long long it = 0;; it++) {
-    if (uni(__hip_atomic_load(collideFlag(ct), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == want) return;
-    if (it > kSpinBound) __builtin_trap();
+// false when the deadlock guard expired (see helperWait)
+__device__ __forceinline__ bool collideWait(double* ct, int want) {
+  const long long t0 = spinClock();
+  for (int it = 0;; it++) {
+    if (uni(__hip_atomic_load(collideFlag(ct), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == want) return true;
+    if (spinExpired(t0, it)) {
+      protocolFail(ct);
+      return false;
+    }
     __builtin_amdgcn_s_sleep(1);
   }
 }
@@ -530,6 +554,18 @@ __device__ __forceinline__ void collideWait(double* ct, int want) {
 // the one-row kernel's deferred worlds, bucketed by LCP rows for the wide
 // kernel's launch order (largest first; DEFER_BUCKETS in pool_sizes.h)
 __device__ __forceinline__ int deferBucket(int m) { return m > 88 ? 0 : (m > 80 ? 1 : (m > 64 ? 2 : 3)); }
+// The lists are kept in memory the call owns (the launch's snapshot rows):
+// DEFER_BUCKETS counters in the first world's header (SN_DEFERCNT, zeroed by
+// the host before the launch), and entry g = q * grid + i (world index) in
+// header slot SN_DEFER of world g / 4 -- so concurrent forwards of one world
+// handle on different streams never share them.  No header write of a step
+// touches these slots.
+__device__ __forceinline__ int* deferCount(double* snapBase) {
+  return reinterpret_cast<int*>(snapBase + SN_DEFERCNT);
+}
+__device__ __forceinline__ int* deferEntry(double* snapBase, int snapDoubles, int g) {
+  return reinterpret_cast<int*>(snapBase + (size_t)(g >> 2) * snapDoubles + SN_DEFER) + (g & 3);
+}
 
 // status bits
 #define ST_CONTACT_OVERFLOW 1
@@ -539,6 +575,7 @@ __device__ __forceinline__ int deferBucket(int m) { return m > 88 ? 0 : (m > 80 
 #define ST_LCP_TOO_LARGE 16     // more LCP rows than the wave solves (NIMBLE_MAX_SOLVED_LCP)
 #define ST_DEFERRED 32          // (internal) the world's LCP has more rows than the one-row-per-lane
                                 // kernel takes: the two-rows-per-lane kernel steps it
+#define ST_PROTOCOL 64          // a wait between the world's two waves hit the deadlock guard (helperWait)
 
 // row record fields
 #define RR_CONTACT 0
@@ -1418,7 +1455,7 @@ template <bool kLds, int R>
 __device__ bool pgsFallbackR(const double* PA, const double* Pxc, int m, double cf, const double (&bR)[R],
                              const double (&loR)[R], const double (&hiR)[R], const int (&fiR)[R],
                              typename Space<kLds>::dptr Mred, int lane, double (&xd)[R], bool& dup, const int* cancel,
-                             double* dbg) {
+                             double* dbg, int* tally) {
   struct { const double *A, *xc; } P{PA, Pxc};
   double scl[R];
   int rep[R];
@@ -1442,13 +1479,14 @@ __device__ bool pgsFallbackR(const double* PA, const double* Pxc, int m, double 
       xr[q] = gatherR(xc, rowAt(q, lane) < mr ? act[q] : 0);
       if (rowAt(q, lane) >= mr) xr[q] = 0.0;
     }
-    ok = wavePgsR<kLds, false, R>(mr, (typename Space<kLds>::cdptr)Mred, xr, br, lr, hr, fr, lane, nullptr, 0.0, cancel);
+    ok = wavePgsR<kLds, false, R>(mr, (typename Space<kLds>::cdptr)Mred, xr, br, lr, hr, fr, lane, nullptr, 0.0, cancel,
+                                  -1, nullptr, tally);
 #pragma unroll
     for (int q = 0; q < R; q++) xd[q] = gatherR(xr, rankR(alive, rep[q]));
   } else {
 #pragma unroll
     for (int q = 0; q < R; q++) xd[q] = rowAt(q, lane) < m ? P.xc[rowAt(q, lane)] : 0.0;
-    ok = wavePgsR<kLds, false, R>(m, spc<kLds>(P.A), xd, bR, loR, hiR, fiR, lane, dbg, cf, cancel);
+    ok = wavePgsR<kLds, false, R>(m, spc<kLds>(P.A), xd, bR, loR, hiR, fiR, lane, dbg, cf, cancel, -1, nullptr, tally);
   }
   if (ok) ok = waveLcpValidR<kLds, R>(m, spc<kLds>(P.A), cf, xd, bR, hiR, loR, fiR, false, lane);
   return ok;
@@ -1459,7 +1497,8 @@ __device__ bool pgsFallbackR(const double* PA, const double* Pxc, int m, double 
 // per row (friction rows 0).
 template <bool kLds, int R>
 __device__ void frictionlessPgsR(const double* PA, const double* Pb, const double* Plo, const double* Phi, int m,
-                                 double cf, const int (&fiR)[R], int lane, double (&X)[R], const int* cancel) {
+                                 double cf, const int (&fiR)[R], int lane, double (&X)[R], const int* cancel,
+                                 int* tally) {
   struct { const double *A, *b, *lo, *hi; } P{PA, Pb, Plo, Phi};
   bool keepMe[R];
   unsigned long long km[R];
@@ -1485,7 +1524,7 @@ __device__ void frictionlessPgsR(const double* PA, const double* Pb, const doubl
     hr[q] = in ? P.hi[myRow[q]] : 0.0;
     fr[q] = -1;
   }
-  wavePgsR<kLds, true, R>(k2, spc<kLds>(P.A), xr, br, lr, hr, fr, lane, nullptr, cf, cancel, m, myRow);
+  wavePgsR<kLds, true, R>(k2, spc<kLds>(P.A), xr, br, lr, hr, fr, lane, nullptr, cf, cancel, m, myRow, tally);
 #pragma unroll
   for (int q = 0; q < R; q++) {
     const double v = gatherR(xr, keepMe[q] ? rankR(km, rowAt(q, lane)) : 0);
@@ -1513,7 +1552,7 @@ template <int R>
 __device__ __forceinline__ bool contactStage(const ModelDev& md, double* s, const Layout& L, int lane, double* v1,
                                              const double* ddq, double* cache, double* snap, double* overflowWs,
                                              bool helperOn, bool collided, int deferRows, bool handedOff = false,
-                                             int* deferList = nullptr, int env = 0) {
+                                             double* deferSnap = nullptr, int snapDoubles = 0, int env = 0) {
   const int n = md.n;
   s = lds<true>(s);
   snap = gbl(snap);
@@ -1528,13 +1567,20 @@ __device__ __forceinline__ bool contactStage(const ModelDev& md, double* s, cons
     // the one-row kernel's contact header and kept contacts (written to the
     // workspace when it deferred this world; read before the LCP pool,
     // which starts there, overwrites them)
+    // (only the header fields of the step, not the helper / collision flags
+    // or the board, which this kernel's helper is already polling)
     const int nk = uni((int)overflowWs[H_NCON]);
-    for (int t = lane; t < CT_CONTACTS + nk * CREC; t += WAVE) ct[t] = overflowWs[t];
+    if (lane < H_HELPER) ct[lane] = overflowWs[lane];
+    for (int t = lane; t < nk * CREC; t += WAVE) ct[CT_CONTACTS + t] = overflowWs[CT_CONTACTS + t];
     WSYNC();
   } else if (collided) {
-    // the helper wave ran the collision detection during the dynamics
-    collideWait(ct, CS_DONE);
-    collidePost(ct, CS_IDLE, lane);
+    // the helper wave ran the collision detection during the dynamics (the
+    // deadlock guard expired: this wave detects them itself)
+    if (collideWait(ct, CS_DONE)) {
+      collidePost(ct, CS_IDLE, lane);
+    } else {
+      collideWorld(md, s, L, lane, snap + snEdge(n));
+    }
   } else {
 #ifdef NIMBLE_STAGE_TIMING
     collideWorld(md, s, L, lane, snap + snEdge(n), g_stamp);
@@ -1546,7 +1592,7 @@ __device__ __forceinline__ bool contactStage(const ModelDev& md, double* s, cons
   const int nCon = uni((int)ct[H_NCON]);
   if (nCon == 0) {
     if (lane == 0) {
-      for (int i = 0; i < 8; i++) snap[i] = 0.0;
+      for (int i = 0; i < SN_DEFER; i++) snap[i] = 0.0;
       snap[SN_STATUS] = ct[H_STATUS];
     }
     WSYNC();
@@ -1564,11 +1610,12 @@ __device__ __forceinline__ bool contactStage(const ModelDev& md, double* s, cons
     // LCP pool later); the dynamics are in the snapshot's dynamics cache
     for (int t = lane; t < CT_CONTACTS + nCon * CREC; t += WAVE) overflowWs[t] = ct[t];
     if (lane == 0) snap[SN_STATUS] = (double)((int)ct[H_STATUS] | ST_DEFERRED);
-    if (deferList != nullptr && lane == 0) {
-      // the wide kernel's order: largest LCPs first (deferBucket)
+    if (deferSnap != nullptr && lane == 0) {
+      // the wide kernel's order: largest LCPs first (deferBucket); the lists
+      // live in the call's own snapshot headers (deferCount / deferEntry)
       const int q = deferBucket(m);
-      const int i = __hip_atomic_fetch_add(deferList + q, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      deferList[DEFER_BUCKETS + q * gridDim.x + i] = env;
+      const int i = __hip_atomic_fetch_add(deferCount(deferSnap) + q, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *deferEntry(deferSnap, snapDoubles, q * gridDim.x + i) = env;
     }
     WSYNC();
     return true;
@@ -1579,7 +1626,7 @@ __device__ __forceinline__ bool contactStage(const ModelDev& md, double* s, cons
     // the Jacobians see a contact-free step)
     for (int t = lane; t < nCon * CREC; t += WAVE) snap[SN_CONTACTS + t] = ct[CT_CONTACTS + t];
     if (lane == 0) {
-      for (int i = 0; i < 16; i++) snap[i] = 0.0;
+      for (int i = 0; i < SN_DEFER; i++) snap[i] = 0.0;
       snap[SN_NCON] = nCon;
       snap[SN_STATUS] = (double)((int)ct[H_STATUS] | ST_LCP_TOO_LARGE);
       ct[H_M] = 0;
@@ -1624,6 +1671,9 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   const double* Lm = s + L.M;
   FwdPool P;
   carveFwd(pool, m, n, P);
+  // (the pair counts are dead: the solvers' tally starts here, before any
+  // task goes out to the helper)
+  if (lane < 4) tallyOf(ct)[lane] = 0;
   // rows (ContactConstraint: normal + 2 tangents with friction), lane =
   // contact; a contact's first row is its rank among the rows of the
   // contacts before it (popcount of the frictional ones)
@@ -1874,7 +1924,8 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
       for (int q = 0; q < R; q++) { br[q] = bR[q]; lr[q] = loR[q]; hr[q] = hiR[q]; fr[q] = fiR[q]; }
       const int mr = reducedVectorsR<R>(alive, rep, lane, br, lr, hr, fr, act);
       reducedMatrixR<kLds, R>(m, spc<kLds>(P.A), 0.0, alive, act, scl, sp<kLds>(P.M1), false, lane);
-      ok = waveDantzigR<kLds, R>(mr, spc<kLds>(P.M1), sp<kLds>(P.M2), sp<kLds>(P.scr), xr, br, lr, hr, fr, lane);
+      ok = waveDantzigR<kLds, R>(mr, spc<kLds>(P.M1), sp<kLds>(P.M2), sp<kLds>(P.scr), xr, br, lr, hr, fr, lane,
+                                 nullptr, nullptr, tallyOf(ct));
 #pragma unroll
       for (int q = 0; q < R; q++) xd[q] = gatherR(xr, rankR(alive, rep[q]));
     } else if (tasked) {
@@ -1882,7 +1933,9 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
       // then the frictionless PGS, until the reference's order decides:
       // Dantzig's answer if it succeeds, else the PGS fallback's, else the
       // frictionless one
-      for (long long it = 0;; it++) {
+      bool expired = false;
+      const long long t0 = spinClock();
+      for (int it = 0;; it++) {
         const int d = boardGet(ct, BD_D);
         if (d == 1) break;
         const int pst = boardGet(ct, BD_P);
@@ -1895,7 +1948,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
           bool dup;
           double xp[R];
           const bool okp = pgsFallbackR<kLds, R>(P.A, P.xc, m, md.fallbackCfm, bR, loR, hiR, fiR, sp<kLds>(P.M1), lane, xp,
-                                                 dup, board(ct) + BD_STOPP, dbgPgs);
+                                                 dup, board(ct) + BD_STOPP, dbgPgs, tallyOf(ct));
 #pragma unroll
           for (int q = 0; q < R; q++)
             if (rowAt(q, lane) < m) P.xp[rowAt(q, lane)] = xp[q];
@@ -1912,7 +1965,8 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
           if (lane == 0 && g_stamp) { g_stamp[98] = 1; g_stamp[102] = (double)__builtin_amdgcn_s_memtime(); }
 #endif
           double xf[R];
-          frictionlessPgsR<kLds, R>(P.A, P.b, P.lo, P.hi, m, md.fallbackCfm, fiR, lane, xf, board(ct) + BD_STOPF);
+          frictionlessPgsR<kLds, R>(P.A, P.b, P.lo, P.hi, m, md.fallbackCfm, fiR, lane, xf, board(ct) + BD_STOPF,
+                                    tallyOf(ct));
 #pragma unroll
           for (int q = 0; q < R; q++)
             if (rowAt(q, lane) < m) P.xf[rowAt(q, lane)] = xf[q];
@@ -1922,14 +1976,27 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
 #endif
           continue;
         }
-        if (it > kSpinBound) __builtin_trap();
+        if (spinExpired(t0, it)) {
+          expired = true;
+          break;
+        }
         __builtin_amdgcn_s_sleep(1);
       }
-      // Dantzig's answer (checked valid by the helper)
-      ok = boardSrc < 0;
-      validated = true;
+      if (expired) {
+        // the deadlock guard: the helper is gone; the cascade goes on here,
+        // serially (Dantzig now, the fallbacks below)
+        protocolFail(ct);
+        stopAll();
+        boardSrc = -1;
+        ok = waveDantzigR<kLds, R>(m, spc<kLds>(P.A), sp<kLds>(P.M2), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane,
+                                   nullptr, nullptr, tallyOf(ct));
+      } else {
+        // Dantzig's answer (checked valid by the helper)
+        ok = boardSrc < 0;
+        validated = true;
 #pragma unroll
-      for (int q = 0; q < R; q++) xd[q] = ok && rowAt(q, lane) < m ? P.xh[rowAt(q, lane)] : 0.0;
+        for (int q = 0; q < R; q++) xd[q] = ok && rowAt(q, lane) < m ? P.xh[rowAt(q, lane)] : 0.0;
+      }
     } else {
       // off-chip pools: the LDL^T factor in the launch's LDS stage when it
       // fits (every pivot's triangular solves and its row / column shifts
@@ -1949,10 +2016,11 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
         for (int i = 0; i < m; i++)
           for (int j = lane; j <= i; j += WAVE) sA[i * (i + 1) / 2 + j] = P.A[i * m + j];
         WSYNC();
-        ok = waveDantzigR<true, R, true>(m, sA, sL, sS, xd, bR, loR, hiR, fiR, lane, dbgDz);
+        ok = waveDantzigR<true, R, true>(m, sA, sL, sS, xd, bR, loR, hiR, fiR, lane, dbgDz, nullptr, tallyOf(ct));
       } else {
         double* Ld = (stage != nullptr && m * ldL <= stageCap) ? (double*)stage : (double*)P.M2;
-        ok = waveDantzigR<kLds, R>(m, spc<kLds>(P.A), sp<kLds>(Ld), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane, dbgDz);
+        ok = waveDantzigR<kLds, R>(m, spc<kLds>(P.A), sp<kLds>(Ld), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane, dbgDz,
+                                   nullptr, tallyOf(ct));
       }
     }
     if (ok) {
@@ -2012,7 +2080,8 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
           WSYNC();
           As = sA;
         }
-        ok = pgsFallbackR<kLds, R>(As, P.xc, m, cf, bR, loR, hiR, fiR, sp<kLds>(P.M1), lane, xd, dup, nullptr, dbgPgs);
+        ok = pgsFallbackR<kLds, R>(As, P.xc, m, cf, bR, loR, hiR, fiR, sp<kLds>(P.M1), lane, xd, dup, nullptr, dbgPgs,
+                                   tallyOf(ct));
         if (dup && lane == 0) ct[H_STATUS] = (double)((int)ct[H_STATUS] | ST_DUPLICATE_COLUMNS);
         if (ok)
 #pragma unroll
@@ -2028,7 +2097,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
           WSYNC();
           As = sA;
         }
-        frictionlessPgsR<kLds, R>(As, P.b, P.lo, P.hi, m, cf, fiR, lane, X, nullptr);
+        frictionlessPgsR<kLds, R>(As, P.b, P.lo, P.hi, m, cf, fiR, lane, X, nullptr, tallyOf(ct));
       }
     }
     bool nan2 = false;
@@ -2110,6 +2179,11 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
     snap[SN_STATUS] = ct[H_STATUS];
     snap[SN_SC] = shortCircuit ? 1 : 0;
     snap[SN_IGN] = ignoredFriction ? 1 : 0;
+    // (the helper's share is in: it answered DONE before construct 2)
+    const int* ty = tallyOf(ct);
+    snap[SN_PIVOTS] = ty[0];
+    snap[SN_SWEEPS] = ty[1];
+    snap[SN_SOLVER_FLOPS] = (double)(unsigned)ty[2];
   }
   WSYNC();
   STAMP(9);
@@ -2180,12 +2254,13 @@ __device__ __forceinline__ void helperTask(const ModelDev& md, double* ct, const
     const int mr = reducedVectorsR<R>(alive, rep, lane, br, lr, hr, fr, act);
     reducedMatrixR<kLds, R>(m, spc<kLds>(PA), 0.0, alive, act, scl, Mred, false, lane);
     WSYNC();
-    ok = waveDantzigR<kLds, R, false, true>(mr, Mred, Ldz, scrDz, xr, br, lr, hr, fr, lane, dbgD, board(ct) + BD_STOPD);
+    ok = waveDantzigR<kLds, R, false, true>(mr, Mred, Ldz, scrDz, xr, br, lr, hr, fr, lane, dbgD, board(ct) + BD_STOPD,
+                                            tallyOf(ct));
 #pragma unroll
     for (int q = 0; q < R; q++) xd[q] = gatherR(xr, rankR(alive, rep[q]));
   } else {
     ok = waveDantzigR<kLds, R, false, true>(m, spc<kLds>(PA), Ldz, scrDz, xd, bR, loR, hiR, fiR, lane, dbgD,
-                                            board(ct) + BD_STOPD);
+                                            board(ct) + BD_STOPD, tallyOf(ct));
   }
   bool nan = false;
 #pragma unroll
@@ -2206,7 +2281,8 @@ __device__ __forceinline__ void helperTask(const ModelDev& md, double* ct, const
   // the fallbacks still open: the PGS fallback once the warm start is
   // final, the frictionless PGS unless the PGS fallback has succeeded
   const double cf = md.fallbackCfm;
-  for (long long it = 0; !ok; it++) {
+  const long long t0 = spinClock();
+  for (int it = 0; !ok; it++) {
     const bool pOpen = boardGet(ct, BD_PCLAIM) == 0 && !boardGet(ct, BD_STOPP);
     const bool fOpen = boardGet(ct, BD_FCLAIM) == 0 && !boardGet(ct, BD_STOPF) && boardGet(ct, BD_P) != 1;
     if (pOpen && boardGet(ct, BD_G) == 1) {
@@ -2217,7 +2293,7 @@ __device__ __forceinline__ void helperTask(const ModelDev& md, double* ct, const
         bool dup;
         double xp[R];
         const bool okp = pgsFallbackR<kLds, R>(PA, Pxc, m, cf, bR, loR, hiR, fiR, Mred, lane, xp, dup,
-                                               board(ct) + BD_STOPP, nullptr);
+                                               board(ct) + BD_STOPP, nullptr, tallyOf(ct));
 #pragma unroll
         for (int q = 0; q < R; q++)
           if (rowAt(q, lane) < m) Pxp[rowAt(q, lane)] = xp[q];
@@ -2236,7 +2312,7 @@ __device__ __forceinline__ void helperTask(const ModelDev& md, double* ct, const
         if (lane == 0 && g_stamp) { g_stamp[98] = 2; g_stamp[102] = (double)__builtin_amdgcn_s_memtime(); }
 #endif
         double xf[R];
-        frictionlessPgsR<kLds, R>(PA, Pb, Plo, Phi, m, cf, fiR, lane, xf, board(ct) + BD_STOPF);
+        frictionlessPgsR<kLds, R>(PA, Pb, Plo, Phi, m, cf, fiR, lane, xf, board(ct) + BD_STOPF, tallyOf(ct));
 #pragma unroll
         for (int q = 0; q < R; q++)
           if (rowAt(q, lane) < m) Pxf[rowAt(q, lane)] = xf[q];
@@ -2249,7 +2325,10 @@ __device__ __forceinline__ void helperTask(const ModelDev& md, double* ct, const
     }
     if (!pOpen) break;
     // only the PGS fallback is open, waiting for the warm start
-    if (it > kSpinBound) __builtin_trap();
+    if (spinExpired(t0, it)) {
+      protocolFail(ct);
+      break;
+    }
     __builtin_amdgcn_s_sleep(1);
   }
 }
@@ -2263,6 +2342,7 @@ __device__ void helperWave(const ModelDev& md, double* s, const Layout& L, int l
   s = lds<true>(s);
   double* ct = s + L.ct;
   const int st = helperWait(ct, [](int v) { return v == HS_TASK || v == HS_SKIP; });
+  if (st < 0) return;  // (the deadlock guard expired: wave 0 goes on alone)
   if (st == HS_TASK) {
     // the cascade's Dantzig is on the world's critical path: the helper
     // competes for issue with the other world's step wave on its SIMD

@@ -66,9 +66,19 @@ template <bool kLds, bool kMapped, int R, bool kExact = false>
 __device__ bool wavePgsR(int n, typename Space<kLds>::cdptr Ain, double (&x)[R], const double (&bIn)[R],
                          const double (&lo)[R], const double (&hi)[R], const int (&findex)[R], int lane,
                          double* dbg = nullptr, double shift = 0.0, const int* cancel = nullptr, int ld = -1,
-                         const int* idxIn = nullptr) {
+                         const int* idxIn = nullptr, int* tally = nullptr) {
   n = uni(n);
   if (n == 0) return true;
+  // executed work for the roofline (tally: LDS ints [1] sweeps, [2] FLOPs;
+  // the residual set-up and every sweep are n rows of n multiply-adds plus
+  // the row's clamp, ~12 operations)
+  auto account = [&](int sweeps) {
+    if (tally && lane == 0) {
+      __hip_atomic_fetch_add(tally + 1, sweeps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_add(tally + 2, (sweeps + 1) * (2 * n * n + 12 * n), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  };
   double xEntry[R];
 #pragma unroll
   for (int s = 0; s < R; s++) xEntry[s] = x[s];
@@ -293,11 +303,14 @@ __device__ bool wavePgsR(int n, typename Space<kLds>::cdptr Ain, double (&x)[R],
         if (contactRows && nonFinite(r, xn)) {
 #pragma unroll
           for (int s = 0; s < R; s++) x[s] = xEntry[s];
-          return wavePgsR<kLds, kMapped, R, true>(n, Ain, x, bIn, lo, hi, findex, lane, dbg, shift, cancel, ld, idxIn);
+          account(1);
+          return wavePgsR<kLds, kMapped, R, true>(n, Ain, x, bIn, lo, hi, findex, lane, dbg, shift, cancel, ld, idxIn,
+                                                  tally);
         }
       }
 #pragma unroll
       for (int s = 0; s < R; s++) x[s] = xn[s];
+      account(1);
       return true;
     }
   }
@@ -311,7 +324,9 @@ __device__ bool wavePgsR(int n, typename Space<kLds>::cdptr Ain, double (&x)[R],
     dummyAct[s] = act[s] ? dummy : 0.0;
   }
   bool possible = false;
+  int sweeps = 1;
   for (int iter = 1; iter < 30; iter++) {
+    sweeps++;
     double xs[R];
 #pragma unroll
     for (int s = 0; s < R; s++) xs[s] = xn[s];
@@ -412,11 +427,14 @@ __device__ bool wavePgsR(int n, typename Space<kLds>::cdptr Ain, double (&x)[R],
     if (contactRows && nonFinite(r, xn)) {
 #pragma unroll
       for (int s = 0; s < R; s++) x[s] = xEntry[s];
-      return wavePgsR<kLds, kMapped, R, true>(n, Ain, x, bIn, lo, hi, findex, lane, dbg, shift, cancel, ld, idxIn);
+      account(sweeps);
+      return wavePgsR<kLds, kMapped, R, true>(n, Ain, x, bIn, lo, hi, findex, lane, dbg, shift, cancel, ld, idxIn,
+                                              tally);
     }
   }
 #pragma unroll
   for (int s = 0; s < R; s++) x[s] = xn[s];
+  account(sweeps);
   return possible;
 }
 
@@ -1017,13 +1035,24 @@ template <bool kLds, int R, bool kPk = false, bool kLdsL = kLds>
 __device__ bool waveDantzigR(int n, typename Space<kLds>::cdptr Ain, typename Space<kLdsL>::dptr Lin,
                              typename Space<kLdsL>::dptr scrIn, double (&xOut)[R], const double (&b)[R],
                              const double (&lo)[R], const double (&hi)[R], const int (&findex)[R], int lane,
-                             double* dbg = nullptr, const int* cancel = nullptr) {
+                             double* dbg = nullptr, const int* cancel = nullptr, int* tally = nullptr) {
   n = uni(n);
   const double* A = (const double*)Ain;
   double* Lbuf = (double*)Lin;
   double* scr = (double*)scrIn;
   WaveDantzig<R, kPk> D;
   int pivots = 0;
+  // executed work for the roofline (tally: LDS ints [0] pivots, [2] FLOPs):
+  // per row the w_i dot product (2n), per pivot the two triangular solves on
+  // the clamped set (2 n_C^2), the N-rows' column update (2 n_N n_C), its
+  // dot products and the ratio tests (~6n)
+  int flops = 0;
+  auto account = [&]() {
+    if (tally && lane == 0) {
+      __hip_atomic_fetch_add(tally, pivots, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_add(tally + 2, flops, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  };
   D.n = n; D.nC = 0; D.nN = 0; D.lane = lane; D.ldL = n | 1;
   D.A = A; D.L = Lbuf; D.scr = scr;
 #pragma unroll
@@ -1069,6 +1098,7 @@ __device__ bool waveDantzigR(int n, typename Space<kLds>::cdptr Ain, typename Sp
       WSYNC();
       hitFirstFriction = true;
     }
+    flops += 2 * n;
     LP_BEGIN();
     const double wi = D.AiC(i, D.x) + D.AiN(i, D.x) - rdlR(D.b, i);
     LP_END(D.prof, 4);
@@ -1203,16 +1233,23 @@ __device__ bool waveDantzigR(int n, typename Space<kLds>::cdptr Ain, typename Sp
           }
         }
         pivots++;
+        flops += 2 * nC * nC + 2 * nN * nC + 6 * n;
         if (dbg && lane == 0) { dbg[0] = pivots; dbg[1] = i; }
         LP_END(D.prof, 5);
 #ifdef LCP_PROFILE
         if (dbg && lane == 0)
           for (int k = 0; k < 8; k++) dbg[2 + k] = (double)D.prof[k];
 #endif
-        if (s <= 0.0) return false;
+        if (s <= 0.0) {
+          account();
+          return false;
+        }
         // `cancel` (LDS int, optional): polled once per pivot; a set flag
         // abandons the solve (the caller no longer needs it)
-        if (cancel && uni(__hip_atomic_load(cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) return false;
+        if (cancel && uni(__hip_atomic_load(cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) {
+          account();
+          return false;
+        }
 #pragma unroll
         for (int q = 0; q < R; q++) {
           const int row = rowAt(q, lane);
@@ -1263,6 +1300,7 @@ __device__ bool waveDantzigR(int n, typename Space<kLds>::cdptr Ain, typename Sp
 #pragma unroll
   for (int s = 0; s < R; s++) xOut[s] = rowAt(s, lane) < n ? scr[rowAt(s, lane)] : 0.0;
   WSYNC();
+  account();
   return true;
 }
 

@@ -52,12 +52,25 @@ __host__ __device__ inline int collideScratchDoubles(int pairChunk, bool mesh) {
 #define SN_SC 6
 #define SN_IGN 7
 #define SN_IMP 8   // Q rank-deficient (pseudo-inverse gradient branch)
+// the LCP solvers' executed work in this step (both waves): Dantzig pivots,
+// PGS sweeps and their FLOPs (the roofline's frac_with_solvers)
+#define SN_PIVOTS 9
+#define SN_SWEEPS 10
+#define SN_SOLVER_FLOPS 11
+// the one-row forward kernel's deferred-world lists (contact.cuh deferEntry,
+// deferCount): 2 doubles = 4 list entries per world, and in the first world
+// of a launch 2 doubles = DEFER_BUCKETS counters
+#define SN_DEFER 12
+#define SN_DEFERCNT 14
 #define SN_CONTACTS 16
 #define SN_ROWS (SN_CONTACTS + NIMBLE_MAX_CONTACTS * CREC)
 #define SN_ROWREC 12
 #define SN_FC (SN_ROWS + NIMBLE_MAX_LCP * SN_ROWREC)
 #define SN_VF (SN_FC + NIMBLE_MAX_LCP)
 #define SN_MAXL NIMBLE_MAX_LCP
+static_assert(SN_PIVOTS == NIMBLE_SNAPSHOT_PIVOTS && SN_SWEEPS == NIMBLE_SNAPSHOT_SWEEPS &&
+                  SN_SOLVER_FLOPS == NIMBLE_SNAPSHOT_SOLVER_FLOPS && SN_DEFERCNT + 2 <= SN_CONTACTS,
+              "include/nimble_amd.h snapshot offsets");
 static_assert(SN_FC == NIMBLE_SNAPSHOT_FC && SN_NC == NIMBLE_SNAPSHOT_NUM_CLAMPING,
               "include/nimble_amd.h snapshot offsets");
 __host__ __device__ inline int snAlign8(int x) { return ((x + 7) / 8) * 8; }

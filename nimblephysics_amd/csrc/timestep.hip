@@ -308,7 +308,7 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
                                              const double* __restrict__ state, const double* __restrict__ forces,
                                              double* __restrict__ lcpCache, double* __restrict__ nextState,
                                              double* __restrict__ snapshot, int snapDoubles, int cacheDoubles,
-                                             int deferRows, int env, int* deferList) {
+                                             int deferRows, int env, bool deferLists) {
   extern __shared__ double s[];
   const ModelDev& md = *mdp;
   const int lane = threadIdx.x & (WAVE - 1);
@@ -336,9 +336,11 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
         }
 #endif
         if (R == 1) {
-          collideWait(ct, CS_GO);
-          collideWorld(md, lds<true>(s), L, lane, snapshot + (size_t)env * snapDoubles + snEdge(n));
-          collidePost(ct, CS_DONE, lane);
+          // (the deadlock guard expired: wave 0 detects the contacts itself)
+          if (collideWait(ct, CS_GO)) {
+            collideWorld(md, lds<true>(s), L, lane, snapshot + (size_t)env * snapDoubles + snEdge(n));
+            collidePost(ct, CS_DONE, lane);
+          }
         }  // (the wide kernel's worlds come with the one-row kernel's contacts)
 #ifdef NIMBLE_STAGE_TIMING
         double* hstamp = snapshot + (size_t)env * snapDoubles + snStamps(n);
@@ -413,13 +415,21 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
       double* sn = snapshot + (size_t)env * snapDoubles;
       deferred = contactStage<R>(md, s, L, lane, v1, x, lcpCache + (size_t)env * cacheDoubles, sn,
                                  sn + snapWorkspaceOffset(n), helperOn, helperOn && R == 1, deferRows, R > 1,
-                                 deferList, env);
+                                 deferLists ? snapshot : nullptr, snapDoubles, env);
     } else if (lane < 8) {
       // a model without collision pairs still has a snapshot header (no
       // contacts, no rows, no clamping) for the getters to read
       snapshot[(size_t)env * snapDoubles + lane] = 0.0;
     }
-    if (helperOn) helperRetire(s, L, lane);
+    if (helperOn) {
+      helperRetire(s, L, lane);
+      // a wait between the two waves hit the deadlock guard: the step went on
+      // without the helper; flagged so that it raises (ST_PROTOCOL)
+      if (protocolFailed(lds<true>(s) + L.ct) && lane == 0) {
+        double* stp = snapshot + (size_t)env * snapDoubles + SN_STATUS;
+        *stp = (double)((int)*stp | ST_PROTOCOL);
+      }
+    }
     if (deferred) return;  // the R = 2 kernel writes this world's step
     double* out = nextState + (size_t)env * 2 * n;
     for (int i = lane; i < n; i += WAVE) out[n + i] = v1[i];
@@ -446,9 +456,9 @@ extern "C" __global__ void __launch_bounds__(2 * WAVE) __attribute__((amdgpu_wav
 nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, const double* __restrict__ state,
                       const double* __restrict__ forces, double* __restrict__ lcpCache,
                       double* __restrict__ nextState, double* __restrict__ snapshot, int snapDoubles,
-                      int cacheDoubles, int deferRows, int* deferList) {
+                      int cacheDoubles, int deferRows, int deferLists) {
   forwardWorld<1>(mdp, L, state, forces, lcpCache, nextState, snapshot, snapDoubles, cacheDoubles, deferRows,
-                  blockIdx.x, deferList);
+                  blockIdx.x, deferLists != 0);
 }
 
 // the worlds nimble_forward_kernel deferred (snapshot status ST_DEFERRED),
@@ -462,26 +472,27 @@ extern "C" __global__ void __launch_bounds__(2 * WAVE) __attribute__((amdgpu_wav
 nimble_forward_wide_kernel(const ModelDev* __restrict__ mdp, Layout L, const double* __restrict__ state,
                            const double* __restrict__ forces, double* __restrict__ lcpCache,
                            double* __restrict__ nextState, double* __restrict__ snapshot, int snapDoubles,
-                           int cacheDoubles, const int* deferList) {
+                           int cacheDoubles, int deferLists) {
   // workgroup b steps the b-th deferred world in the one-row kernel's lists,
-  // the largest LCPs first (deferList: DEFER_BUCKETS counters, then one list
-  // of gridDim.x world indices per bucket): the slowest worlds start at once
-  // instead of behind the others on a CU (one wide world per CU)
+  // the largest LCPs first (DEFER_BUCKETS counters, then one list of
+  // gridDim.x world indices per bucket, in the launch's snapshot headers):
+  // the slowest worlds start at once instead of behind the others on a CU
+  // (one wide world per CU)
   int env = blockIdx.x;
-  if (deferList) {
+  if (deferLists) {
     int b = blockIdx.x, q = 0;
     for (; q < DEFER_BUCKETS; q++) {
-      const int c = deferList[q];
+      const int c = deferCount(snapshot)[q];
       if (b < c) break;
       b -= c;
     }
     if (q == DEFER_BUCKETS) return;  // (whole workgroup: past the deferred worlds)
-    env = deferList[DEFER_BUCKETS + q * gridDim.x + b];
+    env = *deferEntry(snapshot, snapDoubles, q * gridDim.x + b);
   }
   const int st = uni((int)snapshot[(size_t)env * snapDoubles + SN_STATUS]);
   if (!(st & ST_DEFERRED)) return;  // (whole workgroup)
   forwardWorld<2>(mdp, L, state, forces, lcpCache, nextState, snapshot, snapDoubles, cacheDoubles, 1 << 30, env,
-                  nullptr);
+                  false);
 }
 
 // ---------------------------------------------------------------------------

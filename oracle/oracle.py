@@ -80,6 +80,8 @@ def lib():
         L.oracle_lcp_valid.restype = ip
         L.oracle_guess_solution.argtypes = [ip, dp, dp, pi, dp]
         L.oracle_lcp_cascade.argtypes = [ip, dp, dp, dp, dp, pi, dp, C.c_double, dp]
+        L.oracle_classify.argtypes = [ip, dp, dp, dp, dp, pi, dp]
+        L.oracle_classify.restype = ip
         _lib = L
     return _lib
 
@@ -322,6 +324,33 @@ def ref_dantzig_ambiguous(A, b, lo, hi, findex, seed, trials=512, effective=True
         Ap = A * (1 + 1e-15 * (N + N.T) / 2)
         ok, x = ref_dantzig(Ap, b, lo, hi, findex, True)
         outs.add(bool(ok and (not effective or lcp_valid(A, x, b, hi, lo, findex))))
+        if len(outs) == 2:
+            return True
+    return False
+
+
+def classify(A, b, lo, hi, findex, x):
+    """The gradient short-circuit (constructMatrices + standardisation) on a
+    raw problem from warm start x, Q from A's entries; (standardized, x)."""
+    A = np.ascontiguousarray(A, dtype=np.float64)
+    b, lo, hi = (np.ascontiguousarray(v, dtype=np.float64) for v in (b, lo, hi))
+    fi = np.ascontiguousarray(findex, dtype=np.int32)
+    xo = np.ascontiguousarray(x, dtype=np.float64).copy()
+    ok = lib().oracle_classify(A.shape[0], _p(A), _p(b), _p(lo), _p(hi), _pi(fi), _p(xo))
+    return bool(ok), xo
+
+
+def classify_ambiguous(A, b, lo, hi, findex, warm, seed, trials=64):
+    """True when the short-circuit outcome flips under 1e-15-relative
+    symmetric perturbations of A (warm: the step's warm start, or None for
+    guessSolution of the perturbed A, as the step without a cache)."""
+    rng = np.random.default_rng(seed)
+    outs = set()
+    for _ in range(trials):
+        N = rng.standard_normal(A.shape)
+        Ap = A * (1 + 1e-15 * (N + N.T) / 2)
+        x0 = guess_solution(Ap, b, findex) if warm is None else warm
+        outs.add(classify(Ap, b, lo, hi, findex, x0)[0])
         if len(outs) == 2:
             return True
     return False

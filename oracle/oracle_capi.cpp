@@ -320,3 +320,12 @@ void oracle_lcp_cascade(int m, const double* A, const double* b, const double* l
 }
 }
 void codSolveC(const double* A, int m, int n, const double* b, double* x) { oracle::codSolve(A, m, n, b, x); }
+namespace oracle {
+bool classifyLcp(int m, const double* A, const double* b, const double* lo, const double* hi, const int* fi,
+                 double* X);
+}
+// the short-circuit classification on a raw problem (tests: ambiguity probe)
+extern "C" int oracle_classify(int m, const double* A, const double* b, const double* lo, const double* hi,
+                               const int* fi, double* x) {
+  return oracle::classifyLcp(m, A, b, lo, hi, fi, x) ? 1 : 0;
+}

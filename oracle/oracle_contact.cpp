@@ -832,6 +832,10 @@ struct GradMats {
   std::vector<int> fi;
   double cfm = 0;
   bool ignoreFriction = false;
+  // Q from A's entries (A_cc + A_cu E: the same matrix as A_c^T Minv A_cubE,
+  // the device's form) instead of J and Minv: the classification probe of
+  // oracle_classify, which has A only
+  bool qFromA = false;
   const std::vector<double>* allCols;      // n x m   (col j = J^T e_j)
   const std::vector<double>* massedCols;   // n x m   (col j = Minv J^T e_j)
   const std::vector<double>* Minv;         // n x n
@@ -844,7 +848,7 @@ struct GradMats {
   bool standardized = false;
 
   void construct() {
-    const int n = w->n;
+    const int n = w ? w->n : 0;
     mapping.assign(m, CM_NOT_CLAMPING);
     clampIdx.assign(m, -1);
     ubIdx.assign(m, -1);
@@ -901,7 +905,7 @@ struct GradMats {
   bool standardize() {
     standardized = true;
     if (m == 0) return true;
-    const int n = w->n;
+    const int n = w ? w->n : 0;
     if (nc == 0) {
       std::vector<double> zero(m, 0.0);
       if (lcpValid(A, zero, B, hi, lo, fi, ignoreFriction)) { X = zero; return true; }
@@ -911,6 +915,18 @@ struct GradMats {
     std::vector<double> Q(nc * nc, 0.0);
     if (nu == 0) {
       Q = clampA;
+    } else if (qFromA) {
+      for (int r = 0; r < m; r++) {
+        if (mapping[r] != CM_CLAMPING) continue;
+        for (int c = 0; c < m; c++) {
+          if (mapping[c] != CM_CLAMPING) continue;
+          double v = A[r * m + c];
+          for (int u = 0; u < m; u++)
+            if (mapping[u] == c) v += E[ubIdx[u] * nc + clampIdx[c]] * A[r * m + u];
+          Q[clampIdx[r] * nc + clampIdx[c]] = v;
+        }
+      }
+      for (int c = 0; c < nc; c++) Q[c * nc + c] += cfm;
     } else {
       // Q = A_c^T Minv (A_c + A_ub E) + cfm I
       std::vector<double> AcubE(n * nc, 0.0);
@@ -1163,6 +1179,34 @@ void solveContacts(const World& w, const Kin<double>& k, const double* q, const 
 }
 
 //------------------------------------------------------------------------------
+// The gradient short-circuit's classification + standardisation alone
+// (ConstrainedGroupGradientMatrices::constructMatrices :482, :218) on a raw
+// problem with warm start X, Q from A's entries: test infrastructure, the
+// probe of whether a world's short-circuit outcome flips under 1e-15
+// perturbations of A.  Returns standardized; X receives the standardised x.
+bool classifyLcp(int m, const double* A, const double* b, const double* lo, const double* hi, const int* fi,
+                 double* X) {
+  GradMats gm;
+  gm.w = nullptr;
+  gm.m = m;
+  gm.A.assign(A, A + m * m);
+  gm.B.assign(b, b + m);
+  gm.lo.assign(lo, lo + m);
+  gm.hi.assign(hi, hi + m);
+  gm.fi.assign(fi, fi + m);
+  gm.X.assign(X, X + m);
+  gm.aColNorms.assign(m, 0.0);
+  for (int j = 0; j < m; j++) {
+    double s = 0;
+    for (int i = 0; i < m; i++) s += A[i * m + j] * A[i * m + j];
+    gm.aColNorms[j] = s;
+  }
+  gm.qFromA = true;
+  gm.construct();
+  for (int j = 0; j < m; j++) X[j] = gm.X[j];
+  return gm.standardized;
+}
+
 void buildClampingMatrices(const World& w, const Snapshot& snap, std::vector<double>& Ac, std::vector<double>& Aub,
                            std::vector<double>& AcubE) {
   const int n = w.n, m = snap.numRows, nc = snap.numClamping, nu = snap.numUpperBound;

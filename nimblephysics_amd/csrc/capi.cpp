@@ -222,6 +222,8 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
   // NIMBLE_AMD_HELPER_PRIO (measurements): the helper's priority on the task board
   m.helperPrio = 0;
   if (const char* e = getenv("NIMBLE_AMD_HELPER_PRIO")) m.helperPrio = atoi(e) & 3;
+  m.pinvMfma = 1;
+  if (const char* e = getenv("NIMBLE_AMD_PINV_MFMA")) m.pinvMfma = atoi(e) != 0 ? 1 : 0;
   m.numPairs = 0;
   m.pairChunk = 0;
   for (int i = 0; i < m.ns; i++)
@@ -334,7 +336,8 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
   {
     const int mc = 3 * maxContacts < NIMBLE_MAX_SOLVED_LCP ? 3 * maxContacts : NIMBLE_MAX_SOLVED_LCP;
     const int wsd = 4 * mc + (mc + 1) / 2 + 3;
-    int need = mc * mc + wsd + 65 * mc;                          // COD factor + workspace + pinv right-hand sides
+    int need = mc * mc + wsd + 65 * mc + 512;                    // COD factor + workspace + pinv right-hand sides
+                                                                 // (+ the MFMA pinv's 16 x 16 block matrices)
     const int needL = mc * (mc | 1) + 2 * mc;                    // Dantzig L (odd leading dimension) + scratch
     if (needL > need) need = needL;
     const int room = (int)(160 * 1024 / sizeof(double)) - w->fwd.pool;

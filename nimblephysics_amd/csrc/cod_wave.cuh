@@ -221,6 +221,14 @@ __device__ __forceinline__ void codFactorR(typename Space<kLds>::dptr Ain, typen
   }
   WSYNC();
   COD_PROF_BEGIN;
+  // Rank-revealing stop: the pivot's partial norm is |R_kk| and, with column
+  // pivoting, bounds every later |R_jj|; once it is within the rank threshold
+  // (eps kmax max|R_jj|, the rule below) the rank is k, and the remaining
+  // steps would only rotate rows >= k, which the rank-k solves and the RZ
+  // pass never read (their reflectors are marked skipped).  The clamping
+  // sets of the flat-foot mesh worlds have rank <= the 33 dofs at 93-99
+  // rows: most of the factorisation was these steps.
+  double maxPiv = 0.0;
   for (int k = 0; k < c.kmax; k++) {
     // pivot: largest remaining norm, lowest index on ties
     double cand[R], neg[R];
@@ -231,6 +239,15 @@ __device__ __forceinline__ void codFactorR(typename Space<kLds>::dptr Ain, typen
       neg[s] = -cand[s];
     }
     const double best = -waveMinR(neg);
+    {
+      const double piv = sqrt(best > 0.0 ? best : 0.0);
+      if (k > 0 && piv <= 2.220446049250313e-16 * c.kmax * maxPiv) {
+        for (int kk = k + lane; kk < c.kmax; kk += WAVE) c.vn[kk] = -1.0;
+        WSYNC();
+        break;
+      }
+      maxPiv = piv > maxPiv ? piv : maxPiv;
+    }
     bool isBest[R];
 #pragma unroll
     for (int s = 0; s < R; s++) isBest[s] = rowAt(s, lane) >= k && rowAt(s, lane) < n && cand[s] == best;

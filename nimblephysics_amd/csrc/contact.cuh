@@ -596,6 +596,10 @@ __device__ __forceinline__ int* deferEntry(double* snapBase, int snapDoubles, in
 // ---------------------------------------------------------------------------
 // snapEdge: the world's snapshot slots for the kept contacts' EDGE_EDGE
 // metadata (global memory)
+// kMeshInline: the mesh-box narrow phase inlined (the helper wave's pass,
+// the one that runs on the hot path; the other call sites keep the out-of-
+// line instance, so the kernel carries one inlined copy)
+template <bool kMeshInline = false>
 __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, const Layout& L, int lane,
                                              double* snapEdge, double* g_stamp = nullptr) {
   (void)g_stamp;
@@ -696,9 +700,14 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
             cnt = 0;
           } else {
             lds_double* mscr = (lds_double*)(pairbuf + pairBufRecs(PC, true) * PBREC);
-            cnt = deviceMeshBox(Tm, md.meshVerts + 3 * md.meshFirst[sm], md.meshCount[sm], md.shapeSize[sm], Tb,
+            if (kMeshInline)
+              cnt = meshBoxPair(Tm, md.meshVerts + 3 * md.meshFirst[sm], md.meshCount[sm], md.shapeSize[sm], Tb,
                                 md.shapeSize[sb], meshFirst, md.clipDepth, md.shapeBody[si], md.shapeBody[sj],
                                 pairbuf, mscr, lane);
+            else
+              cnt = deviceMeshBox(Tm, md.meshVerts + 3 * md.meshFirst[sm], md.meshCount[sm], md.shapeSize[sm], Tb,
+                                  md.shapeSize[sb], meshFirst, md.clipDepth, md.shapeBody[si], md.shapeBody[sj],
+                                  pairbuf, mscr, lane);
           }
         }
         if (lane == 0) ct[H_PAIRCNT] = cnt;
@@ -1255,6 +1264,239 @@ __device__ __forceinline__ void pinvColumnsStaged(const lds_double* F, const lds
   }
 }
 
+// pinv(Q) from its COD factor as blocked products on the matrix cores, 64
+// right-hand-side columns per pass (the stage layout of pinvColumnsStaged,
+// plus 512 doubles at Tb for a block's 16 x 16 Gram matrix and triangular
+// factor) -- the same three steps as the per-column solves, reorganised:
+//   X = Q_h^T [e_c0 .. e_c0+63]: the QR reflectors sixteen at a time as one
+//     block reflector I - V T V^T (T from the Gram matrix V^T V by LAPACK
+//     dlarft's columnwise recurrence), applied as X -= V (T^T (V^T X)):
+//     three v_mfma_f64_16x16x4f64 products;
+//   Y = T^-1 X on the leading r rows (r = rank; the rows below are 0): block
+//     back substitution, the 16 x 16 diagonal blocks solved lane-per-column,
+//     the blocks above updated by MFMA products;
+//   for r < n_c the RZ reflectors Z^T (reflector i over {i} U {r .. n_c-1})
+//     as block reflectors in the same way.
+// The results equal the per-column solves' up to the rounding of the
+// reordered sums.  The per-column form is lane-serial over n_c^2 steps
+// (~1.5M clocks at n_c = 93 on the mesh Atlas' flat-foot worlds).
+// MFMA operand layout (as gramMfma): A / B lane l = row / column l % 16 of
+// the tile, k = l / 16; result element e of lane l = row l / 16 + 4 e,
+// column l % 16 -- so a product's result feeds the next product's B operand
+// directly (its element s is B's k-step s).  All 64 lanes active.
+template <class VFn, class TauFn>
+__device__ __forceinline__ void blockReflect(VFn Vfn, TauFn tau, int k0, int kRow0, int nc, lds_double* Z,
+                                             lds_double* G, lds_double* T, lds_double* Pn, int lane) {
+  // applies H_{k0+15} .. H_{k0} (H_k = I - tau_k v_k v_k^T, v_k = V(., k),
+  // zero outside rows >= kRow0) to the nc x 64 block Z (row stride 65).
+  // Pn (optional): a 16 * NB x 17 LDS panel the block's sixteen reflectors
+  // are first expanded into (zeros included), so that every MFMA operand is
+  // one LDS read instead of the masked element function
+  const int i16 = lane & 15, kq = lane >> 4;
+  const int NB = (nc + 15) >> 4;
+  const int kStart = kRow0 & ~3;
+  if (Pn != nullptr) {
+    for (int t = kStart * 16 + lane; t < NB * 256; t += WAVE) {
+      const int i = t >> 4, j = t & 15;
+      Pn[i * 17 + j] = Vfn(i, k0 + j);
+    }
+    WSYNC();
+  }
+  auto V = [&](int i, int k) -> double { return Pn != nullptr ? Pn[i * 17 + (k - k0)] : Vfn(i, k); };
+  // (independent accumulator chains throughout: a chain of dependent MFMAs
+  // runs at the instruction's latency, independent ones at its issue rate)
+  {
+    nimble_double4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+    int k = kStart;
+    for (; k + 4 < nc; k += 8) {
+      const double a0 = V(k + kq, k0 + i16), a1 = V(k + 4 + kq, k0 + i16);
+      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, a0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, a1, acc1, 0, 0, 0);
+    }
+    if (k < nc) {
+      const double a0 = V(k + kq, k0 + i16);
+      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, a0, acc0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; e++) G[(kq + 4 * e) * 16 + i16] = acc0[e] + acc1[e];
+  }
+  WSYNC();
+  // T: lane i < 16 computes row i: T_ii = tau_i, T_ij = -tau_j sum_{k=i}^{j-1} T_ik G_kj
+  if (lane < 16) {
+    double t[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const double tj = tau(k0 + j);
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < j; k++) acc += (k >= lane ? t[k] : 0.0) * G[k * 16 + j];
+      t[j] = j < lane ? 0.0 : (j == lane ? tj : -tj * acc);
+    }
+#pragma unroll
+    for (int j = 0; j < 16; j++) T[lane * 16 + j] = t[j];
+  }
+  WSYNC();
+  // W = V^T Z (16 x 64, four column tiles), W2 = T^T W, Z -= V W2
+  nimble_double4 w[4], w2[4];
+#pragma unroll
+  for (int ct = 0; ct < 4; ct++) w[ct] = nimble_double4{0.0, 0.0, 0.0, 0.0};
+  for (int k = kStart; k < nc; k += 4) {
+    const int row = k + kq;
+    const double a = V(row, k0 + i16);
+    double bv[4];
+#pragma unroll
+    for (int ct = 0; ct < 4; ct++) {
+      const double zv = Z[(row < nc ? row : nc - 1) * 65 + ct * 16 + i16];
+      bv[ct] = row < nc ? zv : 0.0;
+    }
+#pragma unroll
+    for (int ct = 0; ct < 4; ct++) w[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv[ct], w[ct], 0, 0, 0);
+  }
+#pragma unroll
+  for (int ct = 0; ct < 4; ct++) w2[ct] = nimble_double4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int s2 = 0; s2 < 4; s2++) {
+    const double ta = T[(kq + 4 * s2) * 16 + i16];
+#pragma unroll
+    for (int ct = 0; ct < 4; ct++) w2[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(ta, w[ct][s2], w2[ct], 0, 0, 0);
+  }
+  for (int rt = kRow0 >> 4; rt < NB; rt++) {
+    const int r0 = rt * 16;
+    double vrow[4];
+#pragma unroll
+    for (int s2 = 0; s2 < 4; s2++) vrow[s2] = -V(r0 + i16, k0 + kq + 4 * s2);
+    nimble_double4 acc[4];
+#pragma unroll
+    for (int ct = 0; ct < 4; ct++)
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const int row = r0 + kq + 4 * e;
+        const double zv = Z[(row < nc ? row : nc - 1) * 65 + ct * 16 + i16];
+        acc[ct][e] = row < nc ? zv : 0.0;
+      }
+#pragma unroll
+    for (int s2 = 0; s2 < 4; s2++)
+#pragma unroll
+      for (int ct = 0; ct < 4; ct++)
+        acc[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(vrow[s2], w2[ct][s2], acc[ct], 0, 0, 0);
+#pragma unroll
+    for (int ct = 0; ct < 4; ct++)
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const int row = r0 + kq + 4 * e;
+        if (row < nc) Z[row * 65 + ct * 16 + i16] = acc[ct][e];
+      }
+  }
+  WSYNC();
+}
+
+__device__ __forceinline__ void pinvColumnsMfma(const lds_double* F, const lds_double* W, lds_double* Z,
+                                                lds_double* Tb, lds_double* Pn, int nc, double* PTG, double* Zs,
+                                                int lane) {
+  const lds_double* vdA = W;
+  const lds_double* vnA = W + nc;
+  const lds_double* zdA = W + 2 * nc;
+  const lds_double* znA = W + 3 * nc;
+  const lds_int* perm = (const lds_int*)(W + 4 * nc);
+  const lds_int* rankP = (const lds_int*)(W + 4 * nc + (nc + 1) / 2 + 1);
+  const int r = uni(*rankP);
+  const int i16 = lane & 15, kq = lane >> 4;
+  const int NB = (nc + 15) >> 4, NBr = (r + 15) >> 4;
+  lds_double* G = Tb;        // 16 x 16 Gram matrix of a block's reflectors
+  lds_double* T = Tb + 256;  // 16 x 16 upper-triangular block factor
+  // QR reflector k's element i (0 above its head; skipped reflectors: 0)
+  auto Vq = [&](int i, int k) -> double {
+    if (k >= nc || i >= nc || i < k) return 0.0;
+    if (!(vnA[k] > 0)) return 0.0;
+    return i == k ? vdA[k] : F[i * nc + k];
+  };
+  auto tauQ = [&](int k) -> double {
+    const double vn = k < nc ? vnA[k] : 0.0;
+    return vn > 0 ? 2.0 / vn : 0.0;
+  };
+  // RZ reflector k (k < r): head zd_k at row k, tail F[k][r ..] at rows r ..
+  auto Vz = [&](int i, int k) -> double {
+    if (k >= r || i >= nc) return 0.0;
+    if (znA[k] == 0) return 0.0;
+    return i == k ? zdA[k] : (i >= r ? F[k * nc + i] : 0.0);
+  };
+  auto tauZ = [&](int k) -> double {
+    const double vn = k < r ? znA[k] : 0.0;
+    return vn != 0 ? 2.0 / vn : 0.0;
+  };
+  for (int c0 = 0; c0 < nc; c0 += WAVE) {
+    const int cnt = nc - c0 < WAVE ? nc - c0 : WAVE;
+    for (int i = 0; i < nc; i++) Z[i * 65 + lane] = i == c0 + lane ? 1.0 : 0.0;
+    WSYNC();
+    // ---- X = Q_h^T X
+    for (int b = 0; b < NB; b++) blockReflect(Vq, tauQ, b * 16, b * 16, nc, Z, G, T, Pn, lane);
+    // ---- rows r .. n_c - 1 are 0; Y = T^-1 X on rows 0 .. r - 1, from the bottom
+    for (int i = r; i < nc; i++) Z[i * 65 + lane] = 0.0;
+    WSYNC();
+    for (int rb = NBr - 1; rb >= 0; rb--) {
+      const int r0 = rb * 16;
+      const int r1 = (r0 + 16 < r ? r0 + 16 : r) - 1;
+      {
+        double y[16];
+#pragma unroll
+        for (int u = 15; u >= 0; u--) {
+          const int i = r0 + u;
+          double acc = i <= r1 ? Z[i * 65 + lane] : 0.0;
+#pragma unroll
+          for (int v2 = u + 1; v2 < 16; v2++)
+            if (r0 + v2 <= r1) acc -= F[i * nc + r0 + v2] * y[v2];
+          y[u] = i <= r1 ? acc / F[i * nc + i] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 16; u++)
+          if (r0 + u <= r1) Z[(r0 + u) * 65 + lane] = y[u];
+      }
+      WSYNC();
+      // the blocks above: X_rt -= T[rt, rb] Y_rb
+      for (int rt = 0; rt < rb; rt++) {
+        const int q0 = rt * 16;
+        double rrow[4];
+#pragma unroll
+        for (int s2 = 0; s2 < 4; s2++) {
+          const int col = r0 + kq + 4 * s2;
+          const double fv = F[(q0 + i16) * nc + (col <= r1 ? col : r1)];
+          rrow[s2] = col <= r1 ? -fv : 0.0;
+        }
+        nimble_double4 acc[4];
+#pragma unroll
+        for (int ct = 0; ct < 4; ct++)
+#pragma unroll
+          for (int e = 0; e < 4; e++) acc[ct][e] = Z[(q0 + kq + 4 * e) * 65 + ct * 16 + i16];
+#pragma unroll
+        for (int s2 = 0; s2 < 4; s2++) {
+          const int row = r0 + kq + 4 * s2;
+#pragma unroll
+          for (int ct = 0; ct < 4; ct++) {
+            const double yz = Z[(row <= r1 ? row : r1) * 65 + ct * 16 + i16];
+            acc[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(rrow[s2], row <= r1 ? yz : 0.0, acc[ct], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int ct = 0; ct < 4; ct++)
+#pragma unroll
+          for (int e = 0; e < 4; e++) Z[(q0 + kq + 4 * e) * 65 + ct * 16 + i16] = acc[ct][e];
+      }
+      WSYNC();
+    }
+    // ---- Z^T (the RZ reflectors, reflector 0 first)
+    if (r < nc)
+      for (int b = 0; b < NBr; b++) blockReflect(Vz, tauZ, b * 16, b * 16, nc, Z, G, T, Pn, lane);
+    // write-back, lane-contiguous in HBM (as pinvColumnsStaged)
+    for (int t = lane; t < cnt * nc; t += WAVE) {
+      const int j = t / nc, i = t - j * nc;
+      const double v = Z[i * 65 + j];
+      Zs[(size_t)c0 * nc + t] = v;
+      PTG[(size_t)(c0 + j) * nc + perm[i]] = v;
+    }
+    WSYNC();
+  }
+}
+
 // The upstream-gradient-independent pieces of the constrained backward
 // (BackpropSnapshot.cpp:2723 getJacobianOfConstraintForce and the clamping
 // matrices it uses), computed here where A = J Minv J^T is on chip:
@@ -1327,6 +1569,11 @@ __device__ void backwardPrecompute(const ModelDev& md, lds_double* sIn, const La
   // n_c = 96 on the mesh Atlas)
   const int wsdS = 4 * nc + (nc + 1) / 2 + 3;
   const bool staged = !kLds && stage != nullptr && nc * nc + wsdS + 65 * nc <= stageCap;
+  // (+512: the MFMA solve's block Gram matrix and triangular factor; + the
+  // reflector panel when it fits too)
+  const bool stagedMfma = staged && nc * nc + wsdS + 65 * nc + 512 <= stageCap && md.pinvMfma;
+  const int panelD = ((nc + 15) >> 4) * 16 * 17;
+  const bool panel = stagedMfma && nc * nc + wsdS + 65 * nc + 512 + panelD <= stageCap;
   STAMP(48);
   if (staged) {
     double* sF = (double*)stage;
@@ -1343,7 +1590,11 @@ __device__ void backwardPrecompute(const ModelDev& md, lds_double* sIn, const La
     }
     carveCod(sW, sF, nc, nc, nc, cod);
     STAMP(49);
-    pinvColumnsStaged((const lds_double*)sF, (const lds_double*)sW, (lds_double*)sZ, nc, PTG, Zs, lane);
+    if (stagedMfma)
+      pinvColumnsMfma((const lds_double*)sF, (const lds_double*)sW, (lds_double*)sZ, (lds_double*)(sZ + 65 * nc),
+                      panel ? (lds_double*)(sZ + 65 * nc + 512) : nullptr, nc, PTG, Zs, lane);
+    else
+      pinvColumnsStaged((const lds_double*)sF, (const lds_double*)sW, (lds_double*)sZ, nc, PTG, Zs, lane);
   } else {
   if (!reuse) codFactorAny<kLds, R>(sp<kLds>(P.M1), sp<kLds>(P.scr), nc, nc, nc, sp<kLds>(vv), lane, stage, stageCap);
   STAMP(49);
@@ -1392,8 +1643,67 @@ __device__ void backwardPrecompute(const ModelDev& md, lds_double* sIn, const La
   // GEMM (BackpropSnapshot.cpp:2964 imprecisionMap = I - Q * Qinv): O(n_c^3)
   // multiply-adds, which the lane-per-entry dot products took ~7M clocks
   // for at n_c = 96 (stage timing, mesh Atlas).
+  // A rank-deficient factor (rank r < n_c) needs no product: Q Q^+ is then
+  // the orthogonal projector onto Q's r-dimensional range (exactly so for
+  // the COD pseudo-inverse, up to rounding), so ||I - Q Q^+||_F^2 = n_c - r
+  // >= 1, far above the reference's 1e-18 test -- the outcome is the rank's.
+  const int rankQ = uni(*cod.rank);
   double part = 0.0;
-  {
+  if (rankQ == nc && staged) {
+    // the stage is free again: Q with its columns permuted (row stride n_c |
+    // 1: the A operand's sixteen rows in distinct banks) and 64 pinv columns
+    // at a time from Zs, every MFMA operand an LDS read (from HBM with the
+    // permutation gathered per element this took ~0.44M clocks at n_c = 93)
+    lds_double* sQ = (lds_double*)stage;
+    const int ldq = nc | 1;
+    lds_double* sZt = sQ + nc * ldq;
+    const lds_int* permS = (const lds_int*)cod.perm;
+    for (int t = lane; t < nc * nc; t += WAVE) {
+      const int r = t / nc, k = t - r * nc;
+      sQ[r * ldq + k] = P.M2[r * nc + permS[k]];
+    }
+    const int i16 = lane & 15, kq = lane >> 4;
+    const int T = (nc + 15) >> 4;
+    for (int c0 = 0; c0 < nc; c0 += WAVE) {
+      const int cnt = nc - c0 < WAVE ? nc - c0 : WAVE;
+      WSYNC();
+      // Zt[k][c] = z_{c0+c}[k]: lane-contiguous HBM reads of the rows z_c
+      for (int t = lane; t < cnt * nc; t += WAVE) {
+        const int c = t / nc, k = t - c * nc;
+        sZt[k * 65 + c] = Zs[(size_t)(c0 + c) * nc + k];
+      }
+      WSYNC();
+      for (int ti = 0; ti < T; ti++) {
+        const int r = ti * 16 + i16;
+        const int rc = r < nc ? r : nc - 1;
+        nimble_double4 acc[4];
+#pragma unroll
+        for (int tj = 0; tj < 4; tj++) acc[tj] = nimble_double4{0.0, 0.0, 0.0, 0.0};
+        for (int k0 = 0; k0 < nc; k0 += 4) {
+          const int k = k0 + kq;
+          const int kc = k < nc ? k : nc - 1;
+          const double qa = sQ[rc * ldq + kc];
+          const double a = (k < nc && r < nc) ? qa : 0.0;
+#pragma unroll
+          for (int tj = 0; tj < 4; tj++) {
+            const int cl = tj * 16 + i16;
+            const double zb = sZt[kc * 65 + (cl < cnt ? cl : 0)];
+            acc[tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, (k < nc && cl < cnt) ? zb : 0.0, acc[tj], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int tj = 0; tj < 4; tj++)
+#pragma unroll
+          for (int e = 0; e < 4; e++) {
+            const int rr = ti * 16 + kq + 4 * e;
+            const int cl = tj * 16 + i16;
+            const double d = (rr == c0 + cl ? 1.0 : 0.0) - acc[tj][e];
+            if (rr < nc && cl < cnt) part += d * d;
+          }
+      }
+    }
+    WSYNC();
+  } else if (rankQ == nc) {
     const int i16 = lane & 15, kq = lane >> 4;
     const int T = (nc + 15) >> 4;
     const double* Qm = P.M2;
@@ -1420,7 +1730,7 @@ __device__ void backwardPrecompute(const ModelDev& md, lds_double* sIn, const La
       }
     }
   }
-  const double tot = waveSum(part);
+  const double tot = rankQ < nc ? (double)(nc - rankQ) : waveSum(part);
   if (lane == 0) snap[SN_IMP] = tot >= 1e-18 ? 1.0 : 0.0;
   WSYNC();
   STAMP(51);
@@ -1822,7 +2132,8 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   // classification's largest COD; otherwise only once that classification
   // has failed, so that it factorises with the whole stage, and Dantzig then
   // overlaps the PGS fallbacks only)
-  const int dzStage = (m * (m | 1) + m + 1) & ~1;
+  // (the factor packed: dantzigLDoubles, 37 KB instead of 74 KB at 96 rows)
+  const int dzStage = (dantzigLDoubles(m, true) + m + 1) & ~1;
   const int codNeed = m * m + 4 * m + (m + 1) / 2 + 3 + m;  // codFactorAny's stage check at n_c = m
   const bool taskable = helperOn && (kLds ? R == 1 : (stage != nullptr && dzStage < stageCap));
   const bool earlyPost = taskable && (kLds || codNeed + dzStage <= stageCap);
@@ -2006,17 +2317,18 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
 #else
       double* dbgDz = nullptr;
 #endif
-      const int ldL = m | 1, nPk = m * (m + 1) / 2;
-      if (stage != nullptr && m * ldL + nPk + m <= stageCap) {
-        // L, A's packed lower triangle and the scatter vector all in the
+      const int ldL = m | 1, nPk = m * (m + 1) / 2, nL = dantzigLDoubles(m, true);
+      if (stage != nullptr && nL + nPk + m <= stageCap) {
+        // L and A's packed lower triangles and the scatter vector all in the
         // stage: every Dantzig access an LDS instruction
         lds_double* sL = stage;
-        lds_double* sA = stage + m * ldL;
+        lds_double* sA = stage + nL;
         lds_double* sS = sA + nPk;
         for (int i = 0; i < m; i++)
           for (int j = lane; j <= i; j += WAVE) sA[i * (i + 1) / 2 + j] = P.A[i * m + j];
         WSYNC();
-        ok = waveDantzigR<true, R, true>(m, sA, sL, sS, xd, bR, loR, hiR, fiR, lane, dbgDz, nullptr, tallyOf(ct));
+        ok = waveDantzigR<true, R, true, true, true>(m, sA, sL, sS, xd, bR, loR, hiR, fiR, lane, dbgDz, nullptr,
+                                                     tallyOf(ct));
       } else {
         double* Ld = (stage != nullptr && m * ldL <= stageCap) ? (double*)stage : (double*)P.M2;
         ok = waveDantzigR<kLds, R>(m, spc<kLds>(P.A), sp<kLds>(Ld), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane, dbgDz,
@@ -2199,7 +2511,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
 // slots per lane, the pool P on chip (kLds) or in HBM; Dantzig's LDL^T factor
 // and scatter vector at Ldz / scrDz (LDS: the pool's M2 / xh2, or the wide
 // kernel's stage), the PGS fallback's reduced matrix at Mred.
-template <bool kLds, int R>
+template <bool kLds, int R, bool kPL = false>
 __device__ __forceinline__ void helperTask(const ModelDev& md, double* ct, const FwdPool& Pin, int m, int lane,
                                            lds_double* Ldz, lds_double* scrDz, typename Space<kLds>::dptr Mred,
                                            double* g_stamp) {
@@ -2254,13 +2566,13 @@ __device__ __forceinline__ void helperTask(const ModelDev& md, double* ct, const
     const int mr = reducedVectorsR<R>(alive, rep, lane, br, lr, hr, fr, act);
     reducedMatrixR<kLds, R>(m, spc<kLds>(PA), 0.0, alive, act, scl, Mred, false, lane);
     WSYNC();
-    ok = waveDantzigR<kLds, R, false, true>(mr, Mred, Ldz, scrDz, xr, br, lr, hr, fr, lane, dbgD, board(ct) + BD_STOPD,
-                                            tallyOf(ct));
+    ok = waveDantzigR<kLds, R, false, true, kPL>(mr, Mred, Ldz, scrDz, xr, br, lr, hr, fr, lane, dbgD,
+                                                 board(ct) + BD_STOPD, tallyOf(ct));
 #pragma unroll
     for (int q = 0; q < R; q++) xd[q] = gatherR(xr, rankR(alive, rep[q]));
   } else {
-    ok = waveDantzigR<kLds, R, false, true>(m, spc<kLds>(PA), Ldz, scrDz, xd, bR, loR, hiR, fiR, lane, dbgD,
-                                            board(ct) + BD_STOPD, tallyOf(ct));
+    ok = waveDantzigR<kLds, R, false, true, kPL>(m, spc<kLds>(PA), Ldz, scrDz, xd, bR, loR, hiR, fiR, lane, dbgD,
+                                                 board(ct) + BD_STOPD, tallyOf(ct));
   }
   bool nan = false;
 #pragma unroll
@@ -2356,7 +2668,7 @@ __device__ void helperWave(const ModelDev& md, double* s, const Layout& L, int l
     if (kWide && mode == HB_WIDE) {
       carveFwd(gbl(hbmPool), m, md.n, P);
       lds_double* Ldz = (lds_double*)(s + L.pool);
-      helperTask<false, 2>(md, ct, P, m, lane, Ldz, Ldz + m * (m | 1), sp<false>(P.M2), g_stamp);
+      helperTask<false, 2, true>(md, ct, P, m, lane, Ldz, Ldz + dantzigLDoubles(m, true), sp<false>(P.M2), g_stamp);
     } else {
       carveFwd(s + L.pool, m, md.n, P);
       helperTask<true, 1>(md, ct, P, m, lane, sp<true>(P.M2), sp<true>(P.xh2), sp<true>(P.M2), g_stamp);

@@ -600,17 +600,28 @@ __device__ double codSolveWave(typename Space<kLds>::dptr Ain, typename Space<kL
 // ---------------------------------------------------------------------------
 // kPk: A held as its packed lower triangle (element (a, b), a >= b, at
 // a (a + 1) / 2 + b): the wide kernels' LDS stage holds it beside L, where
-// the full matrix does not fit (same values, so the same results)
-template <int R, bool kPk = false>
+// the full matrix does not fit (same values, so the same results).
+// kPL: L (unit lower, only its strictly lower part is ever read) held packed
+// too, element (i, j), j < i, at i (i - 1) / 2 + j: dantzigLDoubles(n, true)
+// = n (n - 1) / 2 + 16 doubles instead of n (n | 1) -- 37 KB instead of 74 KB
+// at 96 rows, which lets the wide kernel's stage hold Dantzig's factor beside
+// the classification's COD from the start of the cascade.  (Reads past a
+// row's end are masked lanes; the 16 doubles of slack keep them in bounds.)
+__host__ __device__ __forceinline__ int dantzigLDoubles(int n, bool packed) {
+  return packed ? n * (n - 1) / 2 + 16 : n * (n | 1);
+}
+template <int R, bool kPk = false, bool kPL = false>
 struct WaveDantzig {
   int n, nC, nN, lane, ldL;
+  // offset of row i of L (i wave-uniform or per lane)
+  __device__ __forceinline__ int lrow(int i) const { return kPL ? (i * (i - 1)) >> 1 : i * ldL; }
   // A: the problem matrix (n x n, symmetric), read in place: slot i of the
   // permuted problem is original row p_i (row i's register p), so the
   // permuted entry (i, j) is A[p_i n + p_j] and a swap of two slots is a
   // swap of registers -- the same values the reference's physically
   // permuted matrix holds (dLCP's row / column swaps), without moving them
   const double* A;
-  double* L;    // n x ldL, ldL odd (LDS bank-conflict-free columns)
+  double* L;    // n x ldL, ldL odd (LDS bank-conflict-free columns), or packed (kPL)
   double* scr;  // >= n doubles
   double x[R], b[R], w[R], lo[R], hi[R], d[R], deltaX[R], deltaW[R], Dell[R], ell[R];
   int findex[R], p[R], C[R], state[R];
@@ -676,18 +687,20 @@ struct WaveDantzig {
   // b_k = +0 (masked L entries: B - 0 * 0 is B bit for bit).  0 * b_k leaves
   // a lane unchanged only for finite b_k; a non-finite b_k (degenerate
   // factor) re-runs the solve predicated, exactly as the reference's loop.
-  template <int S, bool kFull, bool kT>
+  // kOnly: update slot S alone (the other slot's updates are deferred, see
+  // solveL1 / solveL1T)
+  template <int S, bool kFull, bool kT, bool kOnly = false>
   __device__ __forceinline__ void solveBlock(double (&B)[R], int m, int k0, const int (&lOff)[R]) {
     // steps: k = k0 + u (L) or k = k0 + 7 - u (L^T, k0 the block's lowest row)
     double Lk[R][8];
 #pragma unroll
     for (int s = 0; s < R; s++) {
-      if (kT ? s > S : s < S) continue;
+      if ((kT ? s > S : s < S) || (kOnly && s != S)) continue;
 #pragma unroll
       for (int u = 0; u < 8; u++) {
         const int k = kT ? k0 + 7 - u : k0 + u;
         const int kc = kFull || k < m ? k : k0;
-        Lk[s][u] = kT ? L[kc * ldL + lOff[s]] : L[lOff[s] + kc];
+        Lk[s][u] = kT ? L[lrow(kc) + lOff[s]] : L[lOff[s] + kc];
       }
     }
     // keep the loads unconditional and batched: all issued before any is
@@ -695,13 +708,13 @@ struct WaveDantzig {
     // wait for each load in turn)
 #pragma unroll
     for (int s = 0; s < R; s++) {
-      if (kT ? s > S : s < S) continue;
+      if ((kT ? s > S : s < S) || (kOnly && s != S)) continue;
 #pragma unroll
       for (int u = 0; u < 8; u++) asm volatile("" : "+v"(Lk[s][u]));
     }
 #pragma unroll
     for (int s = 0; s < R; s++) {
-      if (kT ? s > S : s < S) continue;
+      if ((kT ? s > S : s < S) || (kOnly && s != S)) continue;
 #pragma unroll
       for (int u = 0; u < 8; u++) {
         const int k = kT ? k0 + 7 - u : k0 + u;
@@ -716,9 +729,38 @@ struct WaveDantzig {
       if (!kFull) bk = live ? bk : 0.0;
 #pragma unroll
       for (int s = 0; s < R; s++) {
-        if (kT ? s > S : s < S) continue;
+        if ((kT ? s > S : s < S) || (kOnly && s != S)) continue;
         B[s] -= Lk[s][u] * bk;
       }
+    }
+  }
+  // The deferred updates of slot D by the steps of blocks [kb0, kb1) (8-
+  // aligned, full) of slot 1 - D's solve, in the solve's step order: the same
+  // multiply-subtract per element as solveBlock's, with every b_k already
+  // final -- so an independent chain per lane of dependent FMAs instead of
+  // readlane -> FMA steps (the two slots' chains made an R = 2 step ~95
+  // clocks against ~75 for R = 1).
+  template <int D, bool kT>
+  __device__ __forceinline__ void deferredSlot(double (&B)[R], int m, int kb0, int kb1, const int (&lOff)[R]) {
+    constexpr int Sb = 1 - D;
+    for (int b = 0; b < (kb1 - kb0) / 8; b++) {
+      const int k0 = kT ? kb1 - 8 - 8 * b : kb0 + 8 * b;
+      double lv[8], bk[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int k = kT ? k0 + 7 - u : k0 + u;
+        lv[u] = kT ? L[lrow(k) + lOff[D]] : L[lOff[D] + k];
+        bk[u] = rdl(B[Sb], k & 63);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) asm volatile("" : "+v"(lv[u]));
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int k = kT ? k0 + 7 - u : k0 + u;
+        lv[u] = (kT ? row(D) < k : row(D) > k) && row(D) < m ? lv[u] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) B[D] -= lv[u] * bk[u];
     }
   }
   template <bool kFull, bool kT>
@@ -734,11 +776,25 @@ struct WaveDantzig {
 #pragma unroll
     for (int s = 0; s < R; s++) {
       B0[s] = B[s];
-      rowOffL[s] = (row(s) < m ? row(s) : 0) * ldL;
+      rowOffL[s] = lrow(row(s) < m ? row(s) : 0);
     }
     int k0 = 0;
-    for (; k0 + 8 <= m; k0 += 8) solveBlockAt<true, false>(B, m, k0, rowOffL);
-    if (k0 < m) solveBlockAt<false, false>(B, m, k0, rowOffL);
+    if constexpr (R == 2) {
+      // rows 0..63 first, slot 0 alone; slot 1's updates by those steps
+      // deferred to one pass; then rows 64.. on slot 1 (its own steps)
+      const int kA = m < 64 ? m : 64;
+      for (; k0 + 8 <= kA; k0 += 8) solveBlock<0, true, false, true>(B, m, k0, rowOffL);
+      if (m <= 64) {
+        if (k0 < m) solveBlock<0, false, false, true>(B, m, k0, rowOffL);
+      } else {
+        deferredSlot<1, false>(B, m, 0, 64, rowOffL);
+        for (; k0 + 8 <= m; k0 += 8) solveBlock<1, true, false>(B, m, k0, rowOffL);
+        if (k0 < m) solveBlock<1, false, false>(B, m, k0, rowOffL);
+      }
+    } else {
+      for (; k0 + 8 <= m; k0 += 8) solveBlockAt<true, false>(B, m, k0, rowOffL);
+      if (k0 < m) solveBlockAt<false, false>(B, m, k0, rowOffL);
+    }
     bool nonFinite = false;
 #pragma unroll
     for (int s = 0; s < R; s++) nonFinite = nonFinite || (row(s) < m && !isfinite(B[s]));
@@ -749,7 +805,7 @@ struct WaveDantzig {
         const double bk = rdlR(B, k);
 #pragma unroll
         for (int s = 0; s < R; s++)
-          if (row(s) > k && row(s) < m) B[s] -= L[row(s) * ldL + k] * bk;
+          if (row(s) > k && row(s) < m) B[s] -= L[lrow(row(s)) + k] * bk;
       }
     }
     LP_END(prof, 1);
@@ -766,7 +822,29 @@ struct WaveDantzig {
       B0[s] = B[s];
       colL[s] = row(s) < m ? row(s) : 0;
     }
-    if (m > 0) {
+    if (R == 2 && m > 64) {
+      // rows 64.. first, slot 1 alone; slot 0's updates by those steps
+      // deferred to one pass (its rows are all below them); then rows 0..63
+      int k0 = (m - 1) & ~7;
+      if (k0 + 8 > m) solveBlock<R - 1, false, true, true>(B, m, k0, colL);
+      else solveBlock<R - 1, true, true, true>(B, m, k0, colL);
+      for (k0 -= 8; k0 >= 64; k0 -= 8) solveBlock<R - 1, true, true, true>(B, m, k0, colL);
+      // the partial top block's padded steps change nothing: from m down
+      const int kTop = ((m - 1) & ~7) + 8;
+      if (kTop > m) {
+        // its live steps m-1 .. kTop-8, in the solve's order, then the full blocks
+        for (int k = m - 1; k >= kTop - 8; k--) {
+          const double bk = rdl(B[R - 1], k & 63);
+          double lv = L[lrow(k) + colL[0]];
+          lv = row(0) < k && row(0) < m ? lv : 0.0;
+          B[0] -= lv * bk;
+        }
+        deferredSlot<0, true>(B, m, 64, kTop - 8, colL);
+      } else {
+        deferredSlot<0, true>(B, m, 64, kTop, colL);
+      }
+      for (k0 = 56; k0 >= 0; k0 -= 8) solveBlock<0, true, true>(B, m, k0, colL);
+    } else if (m > 0) {
       int k0 = (m - 1) & ~7;  // lowest row of the top block
       if (k0 + 8 > m) solveBlockAt<false, true>(B, m, k0, colL);
       else solveBlockAt<true, true>(B, m, k0, colL);
@@ -782,7 +860,7 @@ struct WaveDantzig {
         const double bk = rdlR(B, k);
 #pragma unroll
         for (int s = 0; s < R; s++)
-          if (row(s) < k) B[s] -= L[k * ldL + row(s)] * bk;
+          if (row(s) < k) B[s] -= L[lrow(k) + row(s)] * bk;
       }
     }
     LP_END(prof, 2);
@@ -798,7 +876,7 @@ struct WaveDantzig {
     if (nC > 0) {
 #pragma unroll
       for (int s = 0; s < R; s++)
-        if (row(s) < nC) L[nC * ldL + row(s)] = ell[s];
+        if (row(s) < nC) L[lrow(nC) + row(s)] = ell[s];
       const double dd = sumC(ell, Dell);
       setR(d, nC, lane, 1.0 / (Aii - dd));
     } else {
@@ -824,7 +902,7 @@ struct WaveDantzig {
 #pragma unroll
       for (int s = 0; s < R; s++) {
         ell[s] = row(s) < nC ? Dell[s] * d[s] : 0.0;
-        if (row(s) < nC) L[nC * ldL + row(s)] = ell[s];
+        if (row(s) < nC) L[lrow(nC) + row(s)] = ell[s];
       }
       const double dd = sumC(ell, Dell);
       setR(d, nC, lane, 1.0 / (Aii - dd));
@@ -870,7 +948,7 @@ struct WaveDantzig {
       for (int s = 0; s < R; s++)
         if (j0[s] >= 1 && j0[s] < m2) {
           const double Wp = W1[s];
-          const double el = L[(r + j0[s]) * ldL + r];
+          const double el = L[lrow(r + j0[s]) + r];
           W1[s] = Wp - W11 * el;
           W2[s] = k1 * Wp + k2 * el;
         }
@@ -892,14 +970,14 @@ struct WaveDantzig {
 #pragma unroll
       for (int s = 0; s < R; s++)
         if (j0[s] > j && j0[s] < m2) {
-          double el = L[(r + j0[s]) * ldL + r + j];
+          double el = L[lrow(r + j0[s]) + r + j];
           double Wp = W1[s] - k1 * el;
           el += gamma1 * Wp;
           W1[s] = Wp;
           Wp = W2[s] - k2 * el;
           el -= gamma2 * Wp;
           W2[s] = Wp;
-          L[(r + j0[s]) * ldL + r + j] = el;
+          L[lrow(r + j0[s]) + r + j] = el;
         }
     }
   }
@@ -920,7 +998,7 @@ struct WaveDantzig {
         double t[R], sacc[R];
 #pragma unroll
         for (int s = 0; s < R; s++) {
-          t[s] = row(s) < r ? L[r * ldL + row(s)] / d[s] : 0.0;
+          t[s] = row(s) < r ? L[lrow(r) + row(s)] / d[s] : 0.0;
           sacc[s] = 0.0;
         }
         const int ro = rowOff(rdliR(C, r));
@@ -931,7 +1009,7 @@ struct WaveDantzig {
           const double tk = rdlR(t, k);
 #pragma unroll
           for (int s = 0; s < R; s++)
-            if (row(s) >= r && row(s) < n2) sacc[s] += L[row(s) * ldL + k] * tk;
+            if (row(s) >= r && row(s) < n2) sacc[s] += L[lrow(row(s)) + k] * tk;
         }
 #pragma unroll
         for (int s = 0; s < R; s++) {
@@ -944,15 +1022,50 @@ struct WaveDantzig {
     }
     WSYNC();
     if (r < n2 - 1) {
+      if (kPL) {
+        // row and column r out of the packed triangle, lane = column: new
+        // (i, j) = old (i + 1, j + [j >= r]) for rows i >= r (the rows above
+        // keep their place).  Eight rows per batch: all their reads, a wave
+        // barrier, then their writes -- a lane's source element is another
+        // lane's destination one row later, so the batch's reads must be
+        // done before any of its writes, and the next batch's sources (old
+        // rows >= i0 + 9) lie past every destination of this one
+        for (int i0 = r; i0 < n2 - 1; i0 += 8) {
+          double v[8][R];
 #pragma unroll
-      for (int s = 0; s < R; s++)
-        if (row(s) < n2)
-          for (int j = r; j < n2 - 1; j++) L[row(s) * ldL + j] = L[row(s) * ldL + j + 1];
-      WSYNC();
+          for (int u = 0; u < 8; u++) {
+            const int i = i0 + u;
+            const int src = lrow(i + 1 < n2 ? i + 1 : n2 - 1);
 #pragma unroll
-      for (int s = 0; s < R; s++)
-        if (row(s) < n2)
-          for (int i = r; i < n2 - 1; i++) L[i * ldL + row(s)] = L[(i + 1) * ldL + row(s)];
+            for (int s = 0; s < R; s++) {
+              const int j = row(s);
+              v[u][s] = (i < n2 - 1 && j < i) ? L[src + j + (j >= r ? 1 : 0)] : 0.0;
+            }
+          }
+          WSYNC();
+#pragma unroll
+          for (int u = 0; u < 8; u++) {
+            const int i = i0 + u;
+            const int dst = lrow(i);
+#pragma unroll
+            for (int s = 0; s < R; s++) {
+              const int j = row(s);
+              if (i < n2 - 1 && j < i) L[dst + j] = v[u][s];
+            }
+          }
+          WSYNC();
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < R; s++)
+          if (row(s) < n2)
+            for (int j = r; j < n2 - 1; j++) L[row(s) * ldL + j] = L[row(s) * ldL + j + 1];
+        WSYNC();
+#pragma unroll
+        for (int s = 0; s < R; s++)
+          if (row(s) < n2)
+            for (int i = r; i < n2 - 1; i++) L[i * ldL + row(s)] = L[(i + 1) * ldL + row(s)];
+      }
       WSYNC();
       double dn[R];
 #pragma unroll
@@ -1028,10 +1141,10 @@ struct WaveDantzig {
   }
 };
 
-// A (n x n, symmetric, read only), L (n x (n|1) scratch), scr (>= n); problem
+// A (n x n, symmetric, read only), L (dantzigLDoubles(n, kPL) scratch), scr (>= n); problem
 // vectors row-distributed; returns success and x (row-distributed).
 // kLds: A on chip; kLdsL: L and scr on chip (default: with A)
-template <bool kLds, int R, bool kPk = false, bool kLdsL = kLds>
+template <bool kLds, int R, bool kPk = false, bool kLdsL = kLds, bool kPL = false>
 __device__ bool waveDantzigR(int n, typename Space<kLds>::cdptr Ain, typename Space<kLdsL>::dptr Lin,
                              typename Space<kLdsL>::dptr scrIn, double (&xOut)[R], const double (&b)[R],
                              const double (&lo)[R], const double (&hi)[R], const int (&findex)[R], int lane,
@@ -1040,7 +1153,7 @@ __device__ bool waveDantzigR(int n, typename Space<kLds>::cdptr Ain, typename Sp
   const double* A = (const double*)Ain;
   double* Lbuf = (double*)Lin;
   double* scr = (double*)scrIn;
-  WaveDantzig<R, kPk> D;
+  WaveDantzig<R, kPk, kPL> D;
   int pivots = 0;
   // executed work for the roofline (tally: LDS ints [0] pivots, [2] FLOPs):
   // per row the w_i dot product (2n), per pivot the two triangular solves on
@@ -1064,7 +1177,7 @@ __device__ bool waveDantzigR(int n, typename Space<kLds>::cdptr Ain, typename Sp
 #ifdef LCP_PROFILE
   for (int k = 0; k < 8; k++) D.prof[k] = 0;
 #endif
-  for (int k = lane; k < n * (n | 1); k += 64) Lbuf[k] = 0.0;
+  for (int k = lane; k < dantzigLDoubles(n, kPL); k += 64) Lbuf[k] = 0.0;
   {
     bool unb = false;
 #pragma unroll
@@ -1359,15 +1472,37 @@ __device__ void waveReduceR(int m, typename Space<kLds>::cdptr Ain, double shift
       me[s] = rowAt(s, lane) < m && bitR(alive, rowAt(s, lane));
       hitC[s] = kNone;
     }
+    // Norms of the scaled surviving columns: a pair whose norms differ by
+    // more than the distance bound (plus the rounding of both norms and of
+    // the distance sum, a relative 1e-12 margin, far above m eps) cannot
+    // pass the distance test (||a - c|| >= | ||a|| - ||c|| |), so its O(m)
+    // row loop is skipped; the pairs that are compared are compared exactly
+    // as before.  (On the HBM-pool worlds every row loop is m dependent L2
+    // reads per lane: up to ~0.7M clocks per reduce at 96 rows.)
+    double nrm[R];
+#pragma unroll
+    for (int s = 0; s < R; s++) nrm[s] = 0.0;
+    for (int i = 0; i < m; i++) {
+      const bool ai = bitR(alive, i);
+#pragma unroll
+      for (int s = 0; s < R; s++) {
+        const double aa = (A[i * m + col[s]] + (i == rowAt(s, lane) ? shift : 0.0)) * scl[s];
+        nrm[s] += ai ? aa * aa : 0.0;
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < R; s++) nrm[s] = sqrt(nrm[s]);
     for (int c = 1; c < m; c++) {
       if (!bitR(alive, c)) continue;
       const double bc = rdlR(b, c), loc = rdlR(lo, c), hic = rdlR(hi, c), sc = rdlR(scl, c);
+      const double nrc = rdlR(nrm, c);
       const int fc = rdliR(frow, c);
       bool cand[R], anyCand = false;
 #pragma unroll
       for (int s = 0; s < R; s++) {
+        const bool far = fabs(nrm[s] - nrc) - 1e-12 * (nrm[s] + nrc) > 1.0000001e-2;
         cand[s] = me[s] && rowAt(s, lane) < c && hitC[s] == kNone && fabs(b[s] - bc) < 1e-4 && frow[s] == fc &&
-                  hi[s] == hic && lo[s] == loc;
+                  hi[s] == hic && lo[s] == loc && !far;
         anyCand = anyCand || cand[s];
       }
       if (__ballot(anyCand)) {

@@ -450,9 +450,14 @@ DEV int meshMeshContacts(V dir, const lds_double* A, int na, const lds_double* B
 // box size bs.  Writes up to MESH_MAXC records (PBREC stride) to `out`
 // (wave-uniform pointer); returns the count, or -1 - count when unsupported.
 // `scr` is MESH_SCRATCH doubles of LDS.
-__device__ __noinline__ int deviceMeshBox(const double* Tm, const double* v, int nv, const double* sc,
-                                          const double* Tb, const double* bs, bool meshFirst, double clip, int body1,
-                                          int body2, double* out, lds_double* scr, int lane) {
+// meshBoxPair is the body; deviceMeshBox its out-of-line instance.  (The
+// helper wave's collision pass inlines the body: as a called function its
+// prologue saved ~92 callee-saved VGPRs per lane to scratch on every call,
+// ~23 KB of writes per mesh pair near contact, the bulk of the mesh Atlas
+// forward's HBM writes.)
+__device__ __forceinline__ int meshBoxPair(const double* Tm, const double* v, int nv, const double* sc,
+                                           const double* Tb, const double* bs, bool meshFirst, double clip, int body1,
+                                           int body2, double* out, lds_double* scr, int lane) {
   using namespace cap;
   msh::MeshObj mo;
   Obj box;
@@ -477,4 +482,9 @@ __device__ __noinline__ int deviceMeshBox(const double* Tm, const double* v, int
   for (int c = lane; c < cnt; c += 64) { out[PBREC * c + 8] = body1; out[PBREC * c + 9] = body2; }
   WSYNC();
   return cnt;
+}
+__device__ __noinline__ int deviceMeshBox(const double* Tm, const double* v, int nv, const double* sc,
+                                          const double* Tb, const double* bs, bool meshFirst, double clip, int body1,
+                                          int body2, double* out, lds_double* scr, int lane) {
+  return meshBoxPair(Tm, v, nv, sc, Tb, bs, meshFirst, clip, body1, body2, out, scr, lane);
 }

@@ -71,6 +71,10 @@ struct ModelDev {
   // issue priority (s_setprio) of the forward's helper wave while it runs
   // its share of the LCP cascade (the collision detection runs at 0)
   int helperPrio;
+  // backwardPrecompute's pinv(Q) of the wide worlds as blocked MFMA products
+  // (contact.cuh pinvColumnsMfma) when the factor has full rank; 0: the
+  // per-column solves (NIMBLE_AMD_PINV_MFMA=0, measurements)
+  int pinvMfma;
   // kept-contact capacity of the contact stage (<= NIMBLE_MAX_CONTACTS)
   int maxContacts;
   // candidate pairs (i < j) after BodyNodeCollisionFilter, in detector order

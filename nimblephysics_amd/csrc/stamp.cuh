@@ -3,8 +3,10 @@
 #pragma once
 #include <hip/hip_runtime.h>
 // slot map of the 128 stamp doubles (tools/stage_timing.py checks it against
-// the sources): single stamps 0..51, 70..77, 86..88, 90..98 and the board's
-// 100..103; accumulators 60..66, 76..77, 80..85; multi-slot debug blocks:
+// the sources): single stamps 0..51, 70..77, 86..88, 90..98, the board's
+// 100..103 and the wide kernel's own start / reload / v1 / end 104..107 (a
+// deferred world's 10..13 are the one-row kernel's); accumulators 60..66,
+// 76..77, 80..85; multi-slot debug blocks:
 #define SLOT_PGS 54        // pgsFallback: 5 doubles (sweeps, contact rows, 3 phase clocks) -> 54..58
 #define SLOT_COD 67        // codFactor prof: 3 doubles -> 67..69
 #define SLOT_DANTZIG 110   // Dantzig: pivots, row, 8 phase clocks -> 110..119

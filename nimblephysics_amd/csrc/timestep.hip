@@ -338,7 +338,7 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
         if (R == 1) {
           // (the deadlock guard expired: wave 0 detects the contacts itself)
           if (collideWait(ct, CS_GO)) {
-            collideWorld(md, lds<true>(s), L, lane, snapshot + (size_t)env * snapDoubles + snEdge(n));
+            collideWorld<true>(md, lds<true>(s), L, lane, snapshot + (size_t)env * snapDoubles + snEdge(n));
             collidePost(ct, CS_DONE, lane);
           }
         }  // (the wide kernel's worlds come with the one-row kernel's contacts)
@@ -360,7 +360,12 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
 #ifdef NIMBLE_STAGE_TIMING
     double* g_stamp = md.numPairs > 0 ? snapshot + (size_t)env * snapDoubles + snStamps(n) : nullptr;
 #endif
-    STAMP(10);
+    // (stage timing: a deferred world's stamps of the wide kernel's own
+    // phases go to slots 104..107, so that every interval the tool forms is
+    // between two stamps of one launch -- shader clocks of two launches are
+    // not comparable)
+    if (R > 1) STAMP(104);
+    else STAMP(10);
 #ifdef NIMBLE_STAGE_TIMING
     // where wave 0 runs: HW_ID (SIMD, CU, SE) and XCC_ID
     if (lane == 0 && g_stamp) {
@@ -375,7 +380,7 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
       // it deferred), its contacts in the workspace hand-off (contactStage):
       // reloaded, not recomputed
       dynCacheCopy(md, s, L, snapshot + (size_t)env * snapDoubles + L.snDyn, false, lane);
-      STAMP(11);
+      STAMP(105);
     } else {
 #ifdef NIMBLE_STAGE_TIMING
     kinematics(md, s, L, lane, nullptr, g_stamp);
@@ -408,7 +413,8 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
     double* v1 = s + L.v1;
     for (int i = lane; i < n; i += WAVE) v1[i] = s[L.v + i] + md.dt * x[i];
     WSYNC();
-    STAMP(12);
+    if (R > 1) STAMP(106);
+    else STAMP(12);
     // runConstraintEngine (World.cpp:254): collision, LCP, impulses
     bool deferred = false;
     if (md.numPairs > 0) {
@@ -448,7 +454,8 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
       }
     }
     WSYNC();
-    STAMP(13);
+    if (R > 1) STAMP(107);
+    else STAMP(13);
   }
 }
 
@@ -898,7 +905,7 @@ __device__ __forceinline__ void backwardItems(const ModelDev* __restrict__ mdp, 
         double qq[6], vv[6], r[6];
         for (int j = 0; j < 6; j++) { qq[j] = s[L.q + o + j]; vv[j] = s[L.v + o + j]; }
         if (which == 0) qq[i] += sign * eps; else vv[i] += sign * eps;
-        freeIntegrate(qq, vv, dt, r);
+        fdFreeIntegrate(qq, vv, dt, r);  // (the oracle's operation sequence: spatial.cuh fd*)
         for (int j = 0; j < 6; j++) fd[lane * 6 + j] = r[j];
       }
       WSYNC();

@@ -471,9 +471,12 @@ class World:
     def getCachedLCPSolution(self, world_index: int = 0):
         """The LCP solution of world `world_index` of the last batched step
         (the next step's warm start; empty when it had no LCP)."""
+        # a value set since the last step is the one the next step will use
+        # (World::getCachedLCPSolution returns what setCachedLCPSolution set)
+        rows = getattr(self, "_pending_lcp_cache", None)
         bs = getattr(self, "_batch_state", None)
-        if bs is None:
-            rows = getattr(self, "_pending_lcp_cache", None) or [None]
+        if rows is not None or bs is None:
+            rows = rows or [None]
             r = rows[world_index if len(rows) > 1 else 0]
             return np.zeros(0) if r is None else r.copy()
         row = bs.cache[world_index].cpu().numpy()

@@ -75,18 +75,21 @@ def _batch_state(world: World, batch: int, dev, device) -> BatchState:
         world._batch_state = bs
     pending = getattr(world, "_pending_lcp_cache", None)
     if pending is not None:
-        # World::setCachedLCPSolution: one vector for every world, or one per world
+        # World::setCachedLCPSolution: one vector for every world, or one per
+        # world; every vector is checked before any cache row is written, and
+        # a rejected value is dropped (it would fail every later step too)
+        world._pending_lcp_cache = None
         if len(pending) not in (1, batch):
             raise ValueError(f"setCachedLCPSolution: {len(pending)} vectors for a batch of {batch}")
         cap = dev.cache_doubles - 1
-        for b in range(batch):
-            r = pending[b if len(pending) > 1 else 0]
+        for r in pending:
             if r is not None and len(r) > cap:
                 raise ValueError(f"cached LCP solution of {len(r)} rows; this model holds at most {cap}")
+        for b in range(batch):
+            r = pending[b if len(pending) > 1 else 0]
             bs.cache[b, 0] = -1.0 if r is None else float(len(r))
             if r is not None and len(r):
                 bs.cache[b, 1:1 + len(r)] = torch.as_tensor(r, dtype=torch.float64, device=device)
-        world._pending_lcp_cache = None
     return bs
 
 

@@ -192,6 +192,10 @@ void launch(K kernel, dim3 grid, dim3 block, size_t lds, A... args) {
 #define __builtin_amdgcn_fence(a, b) std::atomic_thread_fence(std::memory_order_seq_cst)
 #define __builtin_amdgcn_wave_barrier() wave_emu::waveSync()
 #define __builtin_amdgcn_s_memtime() 0ll
+// (the two-wave deadlock guard never expires under emulation: an emulated
+// wave can legitimately wait for seconds)
+#define __builtin_amdgcn_s_memrealtime() 0ll
+#define __builtin_amdgcn_s_getreg(r) 0u
 #define __builtin_amdgcn_s_setprio(p) ((void)0)
 #define __builtin_amdgcn_s_sleep(n) std::this_thread::sleep_for(std::chrono::microseconds(50))
 #define __builtin_amdgcn_rsq(x) (1.0 / std::sqrt(x))

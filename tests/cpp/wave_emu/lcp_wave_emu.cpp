@@ -7,11 +7,14 @@
 // the results for tests/test_wave_emu.py to check against the oracle.
 //
 // input:  count, then per problem: m, A (m*m row-major), b, lo, hi, findex, x0
-// output: per problem and R: "R m okD xD... okP xP... validD reduceAlive codRank xCod..."
+// output: per problem and R: "R m okD xD... okP xP... validD reduceAlive codRank xCod... packedSame"
+// (packedSame: the packed-factor Dantzig, kPL, gave the same flag and x bit
+// for bit, its factor in a buffer of exactly dantzigLDoubles(m, true))
 // With LCP_EMU_DANTZIG_ONLY=1 in the environment only waveDantzigR and its
 // validity check run, R = 1 only for m <= 64: "R m okD xD... validD".
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <functional>
 #include <thread>
 #include <vector>
@@ -73,7 +76,8 @@ static void solve(const Problem& P) {
   // (codFactor stages a 24-double column in v: the pool reserves it)
   std::vector<double> codWs((size_t)12 * m + 64), codV((size_t)(m > 24 ? m : 24) + 8), codScr((size_t)m + 8), Acopy(P.A);
   std::vector<double> xD((size_t)64 * R), xP((size_t)64 * R), xC((size_t)64 * R);
-  int okD = 0, okP = 0, validD = 0, alive = 0, rank = 0;
+  std::vector<double> Lp((size_t)dantzigLDoubles(m, true)), scrP((size_t)m), xDp((size_t)64 * R);
+  int okD = 0, okP = 0, validD = 0, alive = 0, rank = 0, okDp = 0;
   runWave([&](int lane) {
     double b[R], lo[R], hi[R], x[R], xp[R], xo[R];
     int fi[R];
@@ -87,6 +91,13 @@ static void solve(const Problem& P) {
     }
     const bool d = waveDantzigR<false, R>(m, P.A.data(), L.data(), scr.data(), x, b, lo, hi, fi, lane);
     const bool v = d && waveLcpValidR<false, R>(m, P.A.data(), 0.0, x, b, hi, lo, fi, false, lane);
+    // (the packed factor is the wide kernel's: R = 2 only, which the R = 1
+    // results equal bit for bit anyway)
+    double xpk[R];
+    bool dp = d;
+    for (int s = 0; s < R; s++) xpk[s] = x[s];
+    if constexpr (R == 2)
+      dp = waveDantzigR<false, R, false, false, true>(m, P.A.data(), Lp.data(), scrP.data(), xpk, b, lo, hi, fi, lane);
     const bool p = wavePgsR<false, false, R>(m, P.A.data(), xp, b, lo, hi, fi, lane, nullptr, 1e-4);
     double scl[R];
     int rep[R];
@@ -101,10 +112,10 @@ static void solve(const Problem& P) {
     carveCod(codWs.data(), M1.data(), m, m, m, c);
     for (int s = 0; s < R; s++) {
       const int r = lane + 64 * s;
-      if (r < 64 * R) { xD[r] = x[s]; xP[r] = xp[s]; xC[r] = xo[s]; }
+      if (r < 64 * R) { xD[r] = x[s]; xP[r] = xp[s]; xC[r] = xo[s]; xDp[r] = xpk[s]; }
     }
     if (lane == 0) {
-      okD = d; okP = p; validD = v; alive = popR(al); rank = *c.rank;
+      okD = d; okP = p; validD = v; alive = popR(al); rank = *c.rank; okDp = dp;
     }
   });
   std::printf("%d %d %d", R, m, okD);
@@ -113,7 +124,9 @@ static void solve(const Problem& P) {
   for (int i = 0; i < m; i++) std::printf(" %.17g", xP[i]);
   std::printf(" %d %d %d", validD, alive, rank);
   for (int i = 0; i < m; i++) std::printf(" %.17g", xC[i]);
-  std::printf("\n");
+  bool same = okDp == okD;
+  for (int i = 0; i < m; i++) same = same && std::memcmp(&xDp[i], &xD[i], sizeof(double)) == 0;
+  std::printf(" %d\n", same ? 1 : 0);
 }
 
 int main() {

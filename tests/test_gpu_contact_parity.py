@@ -9,9 +9,14 @@
 * a world may take a different LCP path only when its LCP is numerically
   ill-posed for the reference algorithm itself: resting boxes give rank-
   deficient (e.g. rank 6 of 12) LCPs on which the reference's dSolveLCP
-  succeeds or early-terminates depending on 1e-16-level rounding (checked
-  here by perturbing the oracle's A by 1e-15 relative and requiring both
-  outcomes to occur).  Such worlds must be rare (< 3 %);
+  succeeds or early-terminates depending on 1e-16-level rounding.  A split at
+  Dantzig's outcome is checked against the reference's own compiled
+  dSolveLCP (oracle/_ref: 1e-15-relative symmetric perturbations of A must
+  give both outcomes), a split at the gradient short-circuit against the
+  restated classification under the same perturbations; every split world
+  is then replayed in the oracle with the GPU's path and final x forced
+  (ForcedLcp) and its next state and gradients must match.  Such worlds must
+  be rare (< 3 %);
 * warm-started multi-step rollouts (the LCP cache, BoxedLcpConstraintSolver::mX).
 """
 import numpy as np
@@ -78,19 +83,55 @@ def _device_backward(world, ts, tf, snap, g):
     return gs.cpu().numpy(), gf.cpu().numpy()
 
 
-def _lcp_ambiguous(ow, b, trials=64):
-    """True when the oracle's Dantzig outcome on world b's LCP flips under
-    1e-15 relative symmetric perturbations of A."""
-    A, bb, lo, hi, fi = O.lcp_problem(ow, b)
-    rng = np.random.default_rng(b)
+def _ref_dantzig_ambiguous(A, bb, lo, hi, fi, seed, trials=64):
+    """The reference's compiled dSolveLCP (oracle/_ref) succeeds on some and
+    early-terminates on other 1e-15-relative symmetric perturbations of A;
+    None when oracle/_ref is not built."""
+    rng = np.random.default_rng(seed)
     outs = set()
     for _ in range(trials):
         N = rng.standard_normal(A.shape)
-        ok, _x = O.dantzig(A * (1 + 1e-15 * (N + N.T) / 2), bb, lo, hi, fi, True)
-        outs.add(ok)
+        r = O.ref_dantzig(A * (1 + 1e-15 * (N + N.T) / 2), bb, lo, hi, fi, True)
+        if r is None:
+            return None
+        outs.add(r[0])
         if len(outs) == 2:
             return True
     return False
+
+
+def _split_kind(ow, b, sn):
+    """Where world b's GPU path left the oracle's: at the gradient
+    short-circuit, at Dantzig's outcome (the fallback CFM), at the friction
+    removal, or in the final classification only."""
+    of = O.lcp_flags(ow, b)
+    return ("short-circuit" if of[0] != sn[6] else "cfm" if of[2] != sn[4] else
+            "friction-removed" if of[1] != sn[7] else "classification")
+
+
+def _split_ambiguous(ow, b, kind, warm, seed):
+    """Whether a path split is ambiguous for the reference's algorithm: a
+    Dantzig-outcome split for the reference's own compiled dSolveLCP, a
+    short-circuit split for the restated classification + standardisation
+    (oracle classify, from the step's warm start: `warm`, or guessSolution
+    when the step had no cache), both under 1e-15-relative symmetric
+    perturbations of A; None for the other kinds (not probed: replayed)."""
+    A, bb, lo, hi, fi = O.lcp_problem(ow, b)
+    if kind == "cfm":
+        amb = _ref_dantzig_ambiguous(A, bb, lo, hi, fi, seed)
+        assert amb is not None, "oracle/_ref (the reference's compiled dSolveLCP) is not built"
+        return amb
+    if kind == "short-circuit":
+        return O.classify_ambiguous(A, bb, lo, hi, fi, warm, seed)
+    return None
+
+
+def _warm_start(cache, b, m):
+    """The warm start world b's step read: its cache row when it holds m
+    entries, else None (guessSolution)."""
+    if cache is None or int(cache[b, 0]) != m:
+        return None
+    return cache[b, 1:1 + m].copy()
 
 
 def _same_path(ow, sn, b):
@@ -117,11 +158,14 @@ def _check_lcp_solution(ow, sn, cache_row, b):
     assert O.lcp_valid(A + sn[4] * np.eye(m), x, bb, hi, lo, fi), f"world {b}: GPU LCP solution invalid"
 
 
-def _check_contacts(ow, snap, B, max_diverge=0.03, cache=None):
+def _check_contacts(ow, snap, B, max_diverge=0.03, cache=None, warm_cache=None, seed=0, kinds=None):
     """Contact sets bit-exact for every world; returns the mask of worlds on
     the same LCP path.  A world may leave the oracle's path only where the
-    reference's own Dantzig flips under 1e-15 perturbations (ill-posed); its
-    GPU solution is then checked to solve the LCP (isLCPSolutionValid)."""
+    split is ambiguous for the reference's algorithm (`_split_ambiguous`:
+    its compiled dSolveLCP for Dantzig-outcome splits); its GPU solution is
+    then checked to solve the LCP of its own path (isLCPSolutionValid).
+    `cache`: the GPU's cache after the step, `warm_cache`: the one the step
+    read (None: no warm start); `kinds` collects the split kinds."""
     same = np.ones(B, dtype=bool)
     for b in range(B):
         ref = O.contacts(ow, b)
@@ -138,7 +182,11 @@ def _check_contacts(ow, snap, B, max_diverge=0.03, cache=None):
         mapping, _ = O.lcp_debug(ow, b)
         assert int(sn[SN_M]) == len(mapping), b
         if not _same_path(ow, sn, b):
-            assert _lcp_ambiguous(ow, b), f"world {b}: LCP path differs on a well-posed problem"
+            kind = _split_kind(ow, b, sn)
+            amb = _split_ambiguous(ow, b, kind, _warm_start(warm_cache, b, len(mapping)), seed * 100003 + b)
+            assert amb is not False, f"world {b}: LCP path split ({kind}) on a problem that is not ambiguous"
+            if kinds is not None:
+                kinds[kind] = kinds.get(kind, 0) + 1
             same[b] = False
             if cache is not None:
                 _check_lcp_solution(ow, sn, cache[b], b)
@@ -146,27 +194,64 @@ def _check_contacts(ow, snap, B, max_diverge=0.03, cache=None):
     return same
 
 
-def _parity(world, st, f, seed=11, check_grad=True, max_diverge=0.03, grad_floor=GRAD_FLOOR):
+def _forced_replay(world, st, f, snap, gcache, div, warm_cache=None):
+    """The oracle's step of `st` with the worlds `div` on the GPU's LCP path:
+    their final x (the GPU's cache after the step) and path flags (gradient
+    short-circuit, fallback CFM, friction removed) forced (ForcedLcp); the
+    other worlds solve as usual.  Returns (oracle world, next state, number of
+    forced worlds whose row count differed)."""
+    ow = O.OracleWorld(world)
+    B = st.shape[0]
+    if warm_cache is not None:
+        ow.reset_cache(B)
+        ow.cache[:] = warm_cache
+    fx = np.full((B, gcache.shape[1]), -1.0)
+    fl = np.zeros((B, 3))
+    fx[div] = gcache[div]
+    fl[div, 0], fl[div, 1], fl[div, 2] = snap[div, 6], snap[div, 4], snap[div, 7]
+    nxt, bad = ow.forward_forced(st, f, fx, fl)
+    return ow, nxt, bad
+
+
+def _parity(world, st, f, seed=11, check_grad=True, max_diverge=0.03, grad_floor=GRAD_FLOOR, kinds=None):
+    """GPU vs oracle on one batch: contact sets bit-exact, same-path worlds'
+    next state and gradients at 1e-6, and every split world (ambiguous for
+    the reference's algorithm, `_check_contacts`) replayed with its GPU path
+    forced, whose next state, classification and gradients must then match."""
     ow = O.OracleWorld(world)
     ref = ow.forward(st, f)
     nxt, snap, cache, ts, tf = _device_step(world, st, f)
     B = st.shape[0]
-    same = _check_contacts(ow, snap.cpu().numpy(), B, max_diverge, cache.cpu().numpy())
+    snap_np, cache_np = snap.cpu().numpy(), cache.cpu().numpy()
+    same = _check_contacts(ow, snap_np, B, max_diverge, cache_np, seed=seed, kinds=kinds)
     n = world.getNumDofs()
-    got = nxt.cpu().numpy()[same]
-    ref = ref[same]
-    assert _rel(got[:, :n], ref[:, :n]) < RTOL
-    assert _rel(got[:, n:], ref[:, n:]) < RTOL
+    got_all = nxt.cpu().numpy()
+    got = got_all[same]
+    refs = ref[same]
+    assert _rel(got[:, :n], refs[:, :n]) < RTOL
+    assert _rel(got[:, n:], refs[:, n:]) < RTOL
+    g = np.random.default_rng(seed).standard_normal(st.shape)
     if check_grad:
-        g = np.random.default_rng(seed).standard_normal(st.shape)
         rgs, rgf = ow.backward(g)
-        ggs, ggf = _device_backward(world, ts, tf, snap, g)
-        ggs, ggf, rgs, rgf = ggs[same], ggf[same], rgs[same], rgf[same]
+        ggs_all, ggf_all = _device_backward(world, ts, tf, snap, g)
+        ggs, ggf, rgs, rgf = ggs_all[same], ggf_all[same], rgs[same], rgf[same]
         fl = grad_floor
         assert _rel(ggs[:, :n], rgs[:, :n], fl) < RTOL, _rel(ggs[:, :n], rgs[:, :n], fl)
         assert _rel(ggs[:, n:], rgs[:, n:], fl) < RTOL, _rel(ggs[:, n:], rgs[:, n:], fl)
         assert _rel(ggf, rgf, fl) < RTOL, _rel(ggf, rgf, fl)
-    return ow, snap.cpu().numpy()
+    div = np.flatnonzero(~same)
+    if len(div):
+        ow2, rep, bad = _forced_replay(world, st, f, snap_np, cache_np, div)
+        assert bad == 0
+        for b in div:
+            assert _same_path(ow2, snap_np[b], b), f"world {b}: the forced replay classifies differently"
+        assert _rel(got_all[div], rep[div]) < RTOL, _rel(got_all[div], rep[div])
+        if check_grad:
+            rgs2, rgf2 = ow2.backward(g)
+            fl = grad_floor
+            assert _rel(ggs_all[div], rgs2[div], fl) < RTOL, _rel(ggs_all[div], rgs2[div], fl)
+            assert _rel(ggf_all[div], rgf2[div], fl) < RTOL, _rel(ggf_all[div], rgf2[div], fl)
+    return ow, snap_np
 
 
 @pytest.mark.parametrize("kind", ["rest", "slide", "tilt", "lift"])
@@ -197,9 +282,10 @@ def test_atlas_rollout_warm_start():
     n = world.getNumDofs()
     for k in range(5):
         ref = ow.forward(cur, f)
+        warm = None if cache is None else cache.cpu().numpy().copy()
         nxt, snap, cache, ts, tf = _device_step(world, cur, f, cache)
         got = nxt.cpu().numpy()
-        same = _check_contacts(ow, snap.cpu().numpy(), st.shape[0], cache=cache.cpu().numpy())
+        same = _check_contacts(ow, snap.cpu().numpy(), st.shape[0], cache=cache.cpu().numpy(), warm_cache=warm, seed=k)
         assert _rel(got[same], ref[same]) < RTOL, (k, _rel(got[same], ref[same]))
         g = np.random.default_rng(k).standard_normal(st.shape)
         rgs, rgf = ow.backward(g)
@@ -248,8 +334,9 @@ def test_half_cheetah_rollout():
     cur = st
     for k in range(10):
         ref = ow.forward(cur, f)
+        warm = None if cache is None else cache.cpu().numpy().copy()
         nxt, snap, cache, ts, tf = _device_step(world, cur, f, cache)
-        same = _check_contacts(ow, snap.cpu().numpy(), st.shape[0], cache=cache.cpu().numpy())
+        same = _check_contacts(ow, snap.cpu().numpy(), st.shape[0], cache=cache.cpu().numpy(), warm_cache=warm, seed=k)
         got = nxt.cpu().numpy()
         assert _rel(got[same], ref[same]) < RTOL, (k, _rel(got[same], ref[same]))
         g = np.random.default_rng(k).standard_normal(st.shape)
@@ -629,8 +716,10 @@ def test_broken_state_parity(kind):
     _seed_caches(ow, caches)
     ref = ow.forward(st, f)
     J, F = ow.jacobians()
-    nxt, snap, cache, ts, tf = _device_step(w, st, f, _seeded_cache(dev.cache_doubles, caches, d))
-    same = _check_contacts(ow, snap.cpu().numpy(), B, cache=cache.cpu().numpy())
+    seeded = _seeded_cache(dev.cache_doubles, caches, d)
+    warm = seeded.cpu().numpy().copy()
+    nxt, snap, cache, ts, tf = _device_step(w, st, f, seeded)
+    same = _check_contacts(ow, snap.cpu().numpy(), B, cache=cache.cpu().numpy(), warm_cache=warm)
     assert same.all(), names
     assert (snap.cpu().numpy()[:, SN_NCON] > 0).all()
     assert _rel(nxt.cpu().numpy(), ref) < RTOL

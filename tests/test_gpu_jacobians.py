@@ -21,11 +21,10 @@ pytestmark = pytest.mark.gpu
 
 # FreeJoint's posPos / velPos blocks are central differences in the
 # reference itself (FreeJoint::finiteDifferencePosPosJacobian / VelPos,
-# FreeJoint.cpp:965, :987, eps 1e-6 / 1e-7): both sides carry the rounding
-# noise of the perturbed integrations divided by 2 eps (sin/cos and sums
-# round differently on the GPU), ~1e-10 absolute.  Those entries are compared
-# to an absolute 1e-8; every other entry to RTOL per element.
-FD_ATOL = 1e-8
+# FreeJoint.cpp:965, :987, eps 1e-6 / 1e-7).  The device and the oracle
+# evaluate their perturbed integrations as one fixed IEEE operation sequence
+# (spatial.cuh fdFreeIntegrate / nimble_oracle.cpp), so those entries must be
+# equal bit for bit; every other entry is compared at RTOL per element.
 
 
 def _fd_mask(world):
@@ -41,7 +40,8 @@ def _fd_mask(world):
 
 
 def _jac_err(J, R, mask):
-    """(per-element relative error off the FD blocks, max abs error on them)."""
+    """(per-element relative error off the FD blocks, max abs error on them:
+    0 when they are bit-identical)."""
     Jm, Rm = np.where(mask, 0.0, J), np.where(mask, 0.0, R)
     return _rel(Jm, Rm), float(np.abs(J - R)[mask].max(initial=0.0))
 
@@ -72,7 +72,7 @@ def test_state_action_jacobians_no_contact(name):
     mask = _fd_mask(world)
     for b in range(st.shape[0]):
         rel, fd = _jac_err(J[b], RJ[b], mask)
-        assert rel < RTOL and fd < FD_ATOL, (b, rel, fd)
+        assert rel < RTOL and fd == 0.0, (b, rel, fd)
         assert _rel(F[b], RF[b]) < RTOL, (b, _rel(F[b], RF[b]))
     n = world.getNumDofs()
     # the blocks are views of the same matrices
@@ -101,7 +101,7 @@ def test_state_action_jacobians_atlas_contact():
     mask = _fd_mask(world)
     errs = np.array([_jac_err(J[b], RJ[b], mask) for b in np.flatnonzero(same)])
     worstF = max(_rel(F[b], RF[b]) for b in np.flatnonzero(same))
-    assert errs[:, 0].max() < RTOL and errs[:, 1].max() < FD_ATOL and worstF < RTOL, (errs.max(0), worstF)
+    assert errs[:, 0].max() < RTOL and errs[:, 1].max() == 0.0 and worstF < RTOL, (errs.max(0), worstF)
     # the Jacobian is the matrix whose transposed product backpropState
     # applies (no clipping at these interior states)
     g = torch.tensor(np.random.default_rng(2).standard_normal(st.shape), device=ts.device)

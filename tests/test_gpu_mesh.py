@@ -16,7 +16,7 @@ import pytest
 from nimblephysics_amd import _native, workloads
 from oracle import oracle as O
 from test_gpu_contact_parity import (CREC, GRAD_FLOOR, RTOL, SN_CONTACTS, SN_M, SN_NCON, SN_STATUS, _device_backward,
-                                     _device_step, _lcp_ambiguous, _rel, _same_path)
+                                     _device_step, _forced_replay, _rel, _same_path, _split_ambiguous, _split_kind)
 
 pytestmark = pytest.mark.gpu
 
@@ -56,12 +56,24 @@ def _mesh_parity(B, seed, q_scale=0.02, v_scale=0.05):
         if m_ref == 0 or _same_path(ow, sn, b):
             same[b] = True
         else:
-            assert _lcp_ambiguous(ow, b), f"world {b}: LCP path differs on a well-posed problem"
+            kind = _split_kind(ow, b, sn)
+            assert _split_ambiguous(ow, b, kind, None, seed * 100003 + b) is not False, \
+                f"world {b}: LCP path split ({kind}) on a problem that is not ambiguous"
     n = world.getNumDofs()
     assert _rel(got[same][:, :n], ref[same][:, :n]) < RTOL
     assert _rel(got[same][:, n:], ref[same][:, n:]) < RTOL
     assert _rel(ggs[same], rgs[same], GRAD_FLOOR) < RTOL, _rel(ggs[same], rgs[same], GRAD_FLOOR)
     assert _rel(ggf[same], rgf[same], GRAD_FLOOR) < RTOL
+    # split worlds: the oracle replays the GPU's path and must agree
+    div = np.flatnonzero(~same)
+    if len(div):
+        ow2, rep, bad = _forced_replay(world, st, f, snap, cache.cpu().numpy(), div)
+        assert bad == 0
+        assert all(_same_path(ow2, snap[b], b) for b in div)
+        assert _rel(got[div], rep[div]) < RTOL
+        rgs2, rgf2 = ow2.backward(g)
+        assert _rel(ggs[div], rgs2[div], GRAD_FLOOR) < RTOL
+        assert _rel(ggf[div], rgf2[div], GRAD_FLOOR) < RTOL
     return counts, solved, same, wide
 
 

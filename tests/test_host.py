@@ -406,6 +406,15 @@ def test_set_cached_lcp_solution_host_logic():
     w.setCachedLCPSolution([np.ones(2), np.ones(2)])
     with pytest.raises(ValueError):
         _batch_state(w, 3, dev, torch.device("cpu"))
+    assert w._pending_lcp_cache is None  # a rejected value is dropped
+    before = w._batch_state.cache.clone()
+    w.setCachedLCPSolution([np.ones(2), np.ones(20), np.ones(2)])
+    with pytest.raises(ValueError):
+        _batch_state(w, 3, dev, torch.device("cpu"))
+    assert torch.equal(w._batch_state.cache, before)  # validated before any row is written
     w.setCachedLCPSolution(np.ones(12))
     with pytest.raises(ValueError):
         _batch_state(w, 3, dev, torch.device("cpu"))
+    # the getter returns a value set since the last step, not the last step's
+    w.setCachedLCPSolution(np.array([4.0, 5.0]))
+    assert np.array_equal(w.getCachedLCPSolution(1), [4.0, 5.0])

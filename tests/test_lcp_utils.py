@@ -8,6 +8,7 @@ import os
 import numpy as np
 import pytest
 
+import models
 from oracle import oracle as O
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -154,3 +155,27 @@ def test_cascade_on_reference_cases(oracle_built, name):
         assert O.lcp_valid(A + cfm * np.eye(len(b)), xs, b, hi, lo, fi)
     else:
         assert ign and (xs[fi >= 0] == 0).all()
+
+
+def test_classify_probe_matches_the_oracle_step():
+    """oracle.classify (the short-circuit classification + standardisation on
+    a raw problem, Q from A's entries), which the GPU parity tests perturb to
+    probe whether a world's short-circuit split is ambiguous, reproduces the
+    oracle step's own short-circuit outcome on every contact world of an
+    Atlas and a resting-box batch (no warm start: guessSolution)."""
+    for mk, states in ((lambda: models.atlas_world(True),
+                        lambda w: models.random_states(w, 96, seed=3, q_scale=0.01, v_scale=0.02)),
+                       (models.box_world, lambda w: models.box_states("rest", 32, seed=5))):
+        w = mk()
+        st, f = states(w)
+        ow = O.OracleWorld(w)
+        ow.forward(st, f)
+        seen = 0
+        for b in range(st.shape[0]):
+            A, bb, lo, hi, fi = O.lcp_problem(ow, b)
+            if len(bb) == 0:
+                continue
+            ok, _ = O.classify(A, bb, lo, hi, fi, O.guess_solution(A, bb, fi))
+            assert ok == bool(O.lcp_flags(ow, b)[0]), b
+            seen += 1
+        assert seen > 20

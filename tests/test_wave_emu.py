@@ -55,7 +55,7 @@ def test_lcp_wave_kernels_r1_r2():
         txt += [str(m), wave_emu._fmt(A), wave_emu._fmt(b), wave_emu._fmt(lo), wave_emu._fmt(hi),
                 wave_emu._fmt(fi, True), wave_emu._fmt(np.zeros(m))]
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")
-    r = subprocess.run([exe], input="\n".join(txt), capture_output=True, text=True, timeout=900, env=env)
+    r = subprocess.run([exe], input="\n".join(txt), capture_output=True, text=True, timeout=1800, env=env)
     assert r.returncode == 0, r.stderr[-4000:]
     res = {}
     for ln in r.stdout.splitlines():
@@ -77,6 +77,8 @@ def test_lcp_wave_kernels_r1_r2():
         xc = np.array(t2[2 * m + 5:3 * m + 5], dtype=float)
         ref = np.linalg.solve(A, b)
         assert np.abs(xc - ref).max() <= 1e-8 * np.abs(ref).max(), m
+        # the packed-factor Dantzig (the wide kernel's, R = 2) equals the square one
+        assert t2[3 * m + 5] == "1", m
 
 
 def test_dantzig_disagreement_fixture_emulated():

@@ -76,7 +76,9 @@ for it in range(4):
              (2, 3): "cols/massed/A/b", (2, 86): " b = -J v1", (86, 87): " Y = L^-1 J^T", (87, 88): " A = Y^T Y (MFMA)",
              (88, 3): " pen / aCol", (3, 4): "warm start/guess", (4, 5): "construct 1",
              (5, 6): "dantzig", (6, 7): "pgs/fallbacks", (7, 8): "construct 2", (8, 9): "impulses/snapshot",
-             (12, 13): "contact stage total+integrate"}
+             (12, 13): "contact stage total+integrate",
+             (104, 105): "wide: reload dynamics", (105, 106): "wide: solve v1",
+             (106, 107): "wide: contact stage total+integrate"}
     print(f"--- step {it}: contact worlds {int((hd[:,0]>0).sum())}, short-circuit {int(hd[:,6].sum())}, "
           f"cfm worlds {int((hd[:,4]>0).sum())}")
     for (a, b), nm in names.items():
@@ -84,12 +86,18 @@ for it in range(4):
         if m.any():
             dtk = T[m, b] - T[m, a]
             print(f"  {nm:32s} worlds {m.sum():5d}  mean {dtk.mean():10.0f}  max {dtk.max():10.0f}")
-    # the slowest worlds set the kernel time: their per-stage split
-    tot = np.where((T[:, 12] > 0) & (T[:, 13] > 0), T[:, 13] - T[:, 12], 0)
+    # the slowest worlds set the kernel time: their per-stage split (a
+    # deferred world's contact stage ran in the wide kernel: 106..107)
+    wide = (T[:, 106] > 0) & (T[:, 107] > 0)
+    tot = np.where(wide, T[:, 107] - T[:, 106], np.where((T[:, 12] > 0) & (T[:, 13] > 0), T[:, 13] - T[:, 12], 0))
+    # every interval is between stamps of one launch: none may be negative
+    for (a, b), nm in names.items():
+        m = (T[:, a] > 0) & (T[:, b] > 0)
+        assert not (m & (T[:, b] < T[:, a])).any(), f"negative interval {nm.strip()}: stamps of two launches"
     for wi in np.argsort(-tot)[:6]:
         parts = []
         for (a, b), nm in names.items():
-            if T[wi, a] > 0 and T[wi, b] > 0 and (a, b) not in ((10, 11), (12, 13)):
+            if T[wi, a] > 0 and T[wi, b] > 0 and (a, b) not in ((10, 11), (12, 13), (106, 107)):
                 parts.append(f"{nm.strip()}={int(T[wi, b] - T[wi, a])}")
         print("      collide: narrow phase %d  post-process %d" % (T[wi, 76], T[wi, 77]))
         print("      construct acc: iters %d cls %d Q %d codF %d codS %d nx %d valid %d | codF qr %d rz %d rank %d" % tuple(T[wi, 60:70]))

@@ -601,20 +601,35 @@ __device__ double codSolveWave(typename Space<kLds>::dptr Ain, typename Space<kL
 // kPk: A held as its packed lower triangle (element (a, b), a >= b, at
 // a (a + 1) / 2 + b): the wide kernels' LDS stage holds it beside L, where
 // the full matrix does not fit (same values, so the same results).
-// kPL: L (unit lower, only its strictly lower part is ever read) held packed
-// too, element (i, j), j < i, at i (i - 1) / 2 + j: dantzigLDoubles(n, true)
-// = n (n - 1) / 2 + 16 doubles instead of n (n | 1) -- 37 KB instead of 74 KB
-// at 96 rows, which lets the wide kernel's stage hold Dantzig's factor beside
-// the classification's COD from the start of the cascade.  (Reads past a
-// row's end are masked lanes; the 16 doubles of slack keep them in bounds.)
+// kPL: L (unit lower) held packed too, in panels of 8 rows: panel q (rows
+// 8 q .. 8 q + 7) holds columns 0 .. 8 q + 7 column-major, element (i, j) at
+// panel(q) + 8 j + (i & 7) -- each row's i entries, then zeros to the end of
+// its panel; the panels 8 doubles apart modulo 32 to spread their LDS banks
+// -- 40 KB instead of 74 KB at 96 rows, which lets the wide kernel's stage
+// hold Dantzig's factor beside the classification's COD from the start of the
+// cascade.  Both solves read eight consecutive steps' elements at constant
+// strides (L: a row's eight columns 8 apart; L^T: a column's eight rows of a
+// panel, contiguous), immediate offsets from one address.
+//
+// The zeros are what the triangular solves read instead of a mask: in either
+// layout every element a solve may read at or right of the diagonal is +0
+// (the buffer is zeroed when Dantzig starts, and the factor's updates -- a
+// row appended, ldltAddTL, a row and column removed -- only ever write
+// strictly lower elements: the square layout's shifts move zeros into
+// zeros, the packed one's keep each row's padding where it is), so a lane
+// that must not change in a step multiplies +0 instead of selecting it.
+__host__ __device__ __forceinline__ int dantzigLPanel(int q) { return 32 * q * (q + 1) + 8 * q; }
+__host__ __device__ __forceinline__ int dantzigLPackedEl(int i, int j) { return dantzigLPanel(i >> 3) + 8 * j + (i & 7); }
 __host__ __device__ __forceinline__ int dantzigLDoubles(int n, bool packed) {
-  return packed ? n * (n - 1) / 2 + 16 : n * (n | 1);
+  return packed ? dantzigLPanel((n + 7) >> 3) + 8 : n * (n | 1);
 }
 template <int R, bool kPk = false, bool kPL = false>
 struct WaveDantzig {
   int n, nC, nN, lane, ldL;
   // offset of row i of L (i wave-uniform or per lane)
-  __device__ __forceinline__ int lrow(int i) const { return kPL ? (i * (i - 1)) >> 1 : i * ldL; }
+  // element (i, j) of L, and the stride between a row's consecutive columns
+  static constexpr int kCs = kPL ? 8 : 1;
+  __device__ __forceinline__ int lel(int i, int j) const { return kPL ? dantzigLPackedEl(i, j) : i * ldL + j; }
   // A: the problem matrix (n x n, symmetric), read in place: slot i of the
   // permuted problem is original row p_i (row i's register p), so the
   // permuted entry (i, j) is A[p_i n + p_j] and a swap of two slots is a
@@ -675,21 +690,28 @@ struct WaveDantzig {
   }
   // L x = B (unit lower), B row-distributed, first m entries, in blocks of
   // eight steps.  A block's L entries are loaded together ahead of its
-  // dependent readlane -> FMA chain (LDS latency paid once per 8 steps) with
-  // the triangle mask folded into them (0 where a lane must not change), so
+  // dependent readlane -> FMA chain (LDS latency paid once per 8 steps), so
   // a step is a readlane and unpredicated FMAs: no exec-mask update that
-  // would wait on a vector compare, and no branch (a taken branch per step
-  // cost more than the step).  Blocks are 8-aligned, so all steps of a block
-  // read their b_k from one register slot S (compile time: no slot select on
-  // the chain), and only the slots holding rows the block can change are
-  // updated -- rows > k for L, rows < k for L^T; the reference's loops touch
-  // no other row either.  The last, partial block pads its steps past m with
-  // b_k = +0 (masked L entries: B - 0 * 0 is B bit for bit).  0 * b_k leaves
-  // a lane unchanged only for finite b_k; a non-finite b_k (degenerate
-  // factor) re-runs the solve predicated, exactly as the reference's loop.
+  // would wait on a vector compare, no per-step select, and no branch (a
+  // taken branch per step cost more than the step).  A lane that must not
+  // change in a step reads a stored +0 (see dantzigLPackedRow): its own
+  // row's elements right of the diagonal, or -- a row already final or past
+  // m -- a block of zeros the offsets point it at, chosen once per block
+  // (lOff: the offset of the row's element 0 for L, the column's offset in
+  // its row for L^T).  Blocks are 8-aligned, so
+  // all steps of a block read their b_k from one register slot S (compile
+  // time: no slot select on the chain), and only the slots holding rows the
+  // block can change are updated -- rows > k for L, rows < k for L^T; the
+  // reference's loops touch no other row either.  The last, partial block
+  // pads its steps past m with b_k = +0 on zero elements (B - 0 * 0 is B bit
+  // for bit).  0 * b_k leaves a lane unchanged only for finite b_k; a
+  // non-finite b_k (degenerate factor) re-runs the solve predicated, exactly
+  // as the reference's loop.
   // kOnly: update slot S alone (the other slot's updates are deferred, see
-  // solveL1 / solveL1T)
-  template <int S, bool kFull, bool kT, bool kOnly = false>
+  // solveL1 / solveL1T).  kMask: the triangle applied in registers instead
+  // (the packed factor's partial top block of L^T: its padded steps have no
+  // zero row every lane's column falls in)
+  template <int S, bool kFull, bool kT, bool kOnly = false, bool kMask = false>
   __device__ __forceinline__ void solveBlock(double (&B)[R], int m, int k0, const int (&lOff)[R]) {
     // steps: k = k0 + u (L) or k = k0 + 7 - u (L^T, k0 the block's lowest row)
     double Lk[R][8];
@@ -699,8 +721,14 @@ struct WaveDantzig {
 #pragma unroll
       for (int u = 0; u < 8; u++) {
         const int k = kT ? k0 + 7 - u : k0 + u;
-        const int kc = kFull || k < m ? k : k0;
-        Lk[s][u] = kT ? L[lrow(kc) + lOff[s]] : L[lOff[s] + kc];
+        // a padded step's element: zero for every lane (L: column m - 1 of
+        // the square factor, the block's own padding in the packed one; L^T:
+        // the square factor's row 0)
+        const int kc = kFull || k < m ? k : (kMask ? k0 : kT ? 0 : kPL ? k : m - 1);
+        // (L^T: the row's element 0 from the block's panel, its k - k0 known
+        // at compile time in full blocks)
+        const int rb = kPL ? dantzigLPanel(k0 >> 3) + (kc - k0) : kc * ldL;
+        Lk[s][u] = kT ? L[rb + lOff[s]] : L[lOff[s] + kc * kCs];
       }
     }
     // keep the loads unconditional and batched: all issued before any is
@@ -712,13 +740,15 @@ struct WaveDantzig {
 #pragma unroll
       for (int u = 0; u < 8; u++) asm volatile("" : "+v"(Lk[s][u]));
     }
+    if (kMask) {
 #pragma unroll
-    for (int s = 0; s < R; s++) {
-      if ((kT ? s > S : s < S) || (kOnly && s != S)) continue;
+      for (int s = 0; s < R; s++) {
+        if ((kT ? s > S : s < S) || (kOnly && s != S)) continue;
 #pragma unroll
-      for (int u = 0; u < 8; u++) {
-        const int k = kT ? k0 + 7 - u : k0 + u;
-        Lk[s][u] = (kT ? row(s) < k : row(s) > k) && row(s) < m ? Lk[s][u] : 0.0;
+        for (int u = 0; u < 8; u++) {
+          const int k = kT ? k0 + 7 - u : k0 + u;
+          Lk[s][u] = (kT ? row(s) < k : row(s) > k) && row(s) < m ? Lk[s][u] : 0.0;
+        }
       }
     }
 #pragma unroll
@@ -749,7 +779,7 @@ struct WaveDantzig {
 #pragma unroll
       for (int u = 0; u < 8; u++) {
         const int k = kT ? k0 + 7 - u : k0 + u;
-        lv[u] = kT ? L[lrow(k) + lOff[D]] : L[lOff[D] + k];
+        lv[u] = kT ? L[lel(k, 0) + lOff[D]] : L[lOff[D] + k * kCs];
         bk[u] = rdl(B[Sb], k & 63);
       }
 #pragma unroll
@@ -763,6 +793,20 @@ struct WaveDantzig {
       for (int u = 0; u < 8; u++) B[D] -= lv[u] * bk[u];
     }
   }
+  // per-block offsets onto stored zeros (solveBlock): L -- a row offset, the
+  // lane's own row while it can still change (rows k0 .. m - 1), else the
+  // block's first row, whose padding covers the block's columns (packed; the
+  // square factor's fixed offsets need no per-block choice); L^T -- a
+  // column, the lane's own while its row can still change (rows < k0 + 8,
+  // < m), else the block's last column, right of every row of the block
+  __device__ __forceinline__ void fwdOffsets(int m, int k0, const int (&own)[R], int (&o)[R]) const {
+#pragma unroll
+    for (int s = 0; s < R; s++) o[s] = !kPL || (row(s) >= k0 && row(s) < m) ? own[s] : lel(k0, 0);
+  }
+  __device__ __forceinline__ void bwdColumns(int m, int k0, const int (&own)[R], int (&c)[R]) const {
+#pragma unroll
+    for (int s = 0; s < R; s++) c[s] = !kPL || (row(s) < k0 + 8 && row(s) < m) ? own[s] : (k0 + 7) * kCs;
+  }
   template <bool kFull, bool kT>
   __device__ __forceinline__ void solveBlockAt(double (&B)[R], int m, int k0, const int (&lOff)[R]) {
     if (R == 1 || k0 < 64) solveBlock<0, kFull, kT>(B, m, k0, lOff);
@@ -772,28 +816,47 @@ struct WaveDantzig {
     m = uni(m);
     LP_BEGIN();
     double B0[R];
-    int rowOffL[R];
+    int rowOffL[R], o[R];
 #pragma unroll
     for (int s = 0; s < R; s++) {
       B0[s] = B[s];
-      rowOffL[s] = lrow(row(s) < m ? row(s) : 0);
+      // (rows past m: the square factor's row 0, zero in every column)
+      rowOffL[s] = lel(row(s) < m ? row(s) : 0, 0);
     }
     int k0 = 0;
     if constexpr (R == 2) {
       // rows 0..63 first, slot 0 alone; slot 1's updates by those steps
       // deferred to one pass; then rows 64.. on slot 1 (its own steps)
       const int kA = m < 64 ? m : 64;
-      for (; k0 + 8 <= kA; k0 += 8) solveBlock<0, true, false, true>(B, m, k0, rowOffL);
+      for (; k0 + 8 <= kA; k0 += 8) {
+        fwdOffsets(m, k0, rowOffL, o);
+        solveBlock<0, true, false, true>(B, m, k0, o);
+      }
       if (m <= 64) {
-        if (k0 < m) solveBlock<0, false, false, true>(B, m, k0, rowOffL);
+        if (k0 < m) {
+          fwdOffsets(m, k0, rowOffL, o);
+          solveBlock<0, false, false, true>(B, m, k0, o);
+        }
       } else {
         deferredSlot<1, false>(B, m, 0, 64, rowOffL);
-        for (; k0 + 8 <= m; k0 += 8) solveBlock<1, true, false>(B, m, k0, rowOffL);
-        if (k0 < m) solveBlock<1, false, false>(B, m, k0, rowOffL);
+        for (; k0 + 8 <= m; k0 += 8) {
+          fwdOffsets(m, k0, rowOffL, o);
+          solveBlock<1, true, false>(B, m, k0, o);
+        }
+        if (k0 < m) {
+          fwdOffsets(m, k0, rowOffL, o);
+          solveBlock<1, false, false>(B, m, k0, o);
+        }
       }
     } else {
-      for (; k0 + 8 <= m; k0 += 8) solveBlockAt<true, false>(B, m, k0, rowOffL);
-      if (k0 < m) solveBlockAt<false, false>(B, m, k0, rowOffL);
+      for (; k0 + 8 <= m; k0 += 8) {
+        fwdOffsets(m, k0, rowOffL, o);
+        solveBlockAt<true, false>(B, m, k0, o);
+      }
+      if (k0 < m) {
+        fwdOffsets(m, k0, rowOffL, o);
+        solveBlockAt<false, false>(B, m, k0, o);
+      }
     }
     bool nonFinite = false;
 #pragma unroll
@@ -805,7 +868,7 @@ struct WaveDantzig {
         const double bk = rdlR(B, k);
 #pragma unroll
         for (int s = 0; s < R; s++)
-          if (row(s) > k && row(s) < m) B[s] -= L[lrow(row(s)) + k] * bk;
+          if (row(s) > k && row(s) < m) B[s] -= L[lel(row(s), k)] * bk;
       }
     }
     LP_END(prof, 1);
@@ -816,26 +879,43 @@ struct WaveDantzig {
     m = uni(m);
     LP_BEGIN();
     double B0[R];
-    int colL[R];
+    int colL[R], c[R];
 #pragma unroll
     for (int s = 0; s < R; s++) {
       B0[s] = B[s];
-      colL[s] = row(s) < m ? row(s) : 0;
+      // (rows past m: the square factor's column m - 1, zero in every row < m)
+      colL[s] = (row(s) < m ? row(s) : (kPL ? 0 : m - 1)) * kCs;
     }
+    // the top block: partial (padded steps; masked for the packed factor) or full
+    auto topBlock = [&](int k0) {
+      bwdColumns(m, k0, colL, c);
+      constexpr int St = R - 1;
+      if (R == 2 && m > 64) {
+        if (k0 + 8 > m) solveBlock<St, false, true, true, kPL>(B, m, k0, c);
+        else solveBlock<St, true, true, true>(B, m, k0, c);
+      } else if (k0 + 8 > m) {
+        if (R == 1 || k0 < 64) solveBlock<0, false, true, false, kPL>(B, m, k0, c);
+        else solveBlock<St, false, true, false, kPL>(B, m, k0, c);
+      } else {
+        solveBlockAt<true, true>(B, m, k0, c);
+      }
+    };
     if (R == 2 && m > 64) {
       // rows 64.. first, slot 1 alone; slot 0's updates by those steps
       // deferred to one pass (its rows are all below them); then rows 0..63
       int k0 = (m - 1) & ~7;
-      if (k0 + 8 > m) solveBlock<R - 1, false, true, true>(B, m, k0, colL);
-      else solveBlock<R - 1, true, true, true>(B, m, k0, colL);
-      for (k0 -= 8; k0 >= 64; k0 -= 8) solveBlock<R - 1, true, true, true>(B, m, k0, colL);
+      topBlock(k0);
+      for (k0 -= 8; k0 >= 64; k0 -= 8) {
+        bwdColumns(m, k0, colL, c);
+        solveBlock<R - 1, true, true, true>(B, m, k0, c);
+      }
       // the partial top block's padded steps change nothing: from m down
       const int kTop = ((m - 1) & ~7) + 8;
       if (kTop > m) {
         // its live steps m-1 .. kTop-8, in the solve's order, then the full blocks
         for (int k = m - 1; k >= kTop - 8; k--) {
           const double bk = rdl(B[R - 1], k & 63);
-          double lv = L[lrow(k) + colL[0]];
+          double lv = L[lel(k, 0) + colL[0]];
           lv = row(0) < k && row(0) < m ? lv : 0.0;
           B[0] -= lv * bk;
         }
@@ -843,12 +923,17 @@ struct WaveDantzig {
       } else {
         deferredSlot<0, true>(B, m, 64, kTop, colL);
       }
-      for (k0 = 56; k0 >= 0; k0 -= 8) solveBlock<0, true, true>(B, m, k0, colL);
+      for (k0 = 56; k0 >= 0; k0 -= 8) {
+        bwdColumns(m, k0, colL, c);
+        solveBlock<0, true, true>(B, m, k0, c);
+      }
     } else if (m > 0) {
       int k0 = (m - 1) & ~7;  // lowest row of the top block
-      if (k0 + 8 > m) solveBlockAt<false, true>(B, m, k0, colL);
-      else solveBlockAt<true, true>(B, m, k0, colL);
-      for (k0 -= 8; k0 >= 0; k0 -= 8) solveBlockAt<true, true>(B, m, k0, colL);
+      topBlock(k0);
+      for (k0 -= 8; k0 >= 0; k0 -= 8) {
+        bwdColumns(m, k0, colL, c);
+        solveBlockAt<true, true>(B, m, k0, c);
+      }
     }
     bool nonFinite = false;
 #pragma unroll
@@ -860,7 +945,7 @@ struct WaveDantzig {
         const double bk = rdlR(B, k);
 #pragma unroll
         for (int s = 0; s < R; s++)
-          if (row(s) < k) B[s] -= L[lrow(k) + row(s)] * bk;
+          if (row(s) < k) B[s] -= L[lel(k, row(s))] * bk;
       }
     }
     LP_END(prof, 2);
@@ -876,7 +961,7 @@ struct WaveDantzig {
     if (nC > 0) {
 #pragma unroll
       for (int s = 0; s < R; s++)
-        if (row(s) < nC) L[lrow(nC) + row(s)] = ell[s];
+        if (row(s) < nC) L[lel(nC, row(s))] = ell[s];
       const double dd = sumC(ell, Dell);
       setR(d, nC, lane, 1.0 / (Aii - dd));
     } else {
@@ -902,7 +987,7 @@ struct WaveDantzig {
 #pragma unroll
       for (int s = 0; s < R; s++) {
         ell[s] = row(s) < nC ? Dell[s] * d[s] : 0.0;
-        if (row(s) < nC) L[lrow(nC) + row(s)] = ell[s];
+        if (row(s) < nC) L[lel(nC, row(s))] = ell[s];
       }
       const double dd = sumC(ell, Dell);
       setR(d, nC, lane, 1.0 / (Aii - dd));
@@ -948,7 +1033,7 @@ struct WaveDantzig {
       for (int s = 0; s < R; s++)
         if (j0[s] >= 1 && j0[s] < m2) {
           const double Wp = W1[s];
-          const double el = L[lrow(r + j0[s]) + r];
+          const double el = L[lel(r + j0[s], r)];
           W1[s] = Wp - W11 * el;
           W2[s] = k1 * Wp + k2 * el;
         }
@@ -970,14 +1055,14 @@ struct WaveDantzig {
 #pragma unroll
       for (int s = 0; s < R; s++)
         if (j0[s] > j && j0[s] < m2) {
-          double el = L[lrow(r + j0[s]) + r + j];
+          double el = L[lel(r + j0[s], r + j)];
           double Wp = W1[s] - k1 * el;
           el += gamma1 * Wp;
           W1[s] = Wp;
           Wp = W2[s] - k2 * el;
           el -= gamma2 * Wp;
           W2[s] = Wp;
-          L[lrow(r + j0[s]) + r + j] = el;
+          L[lel(r + j0[s], r + j)] = el;
         }
     }
   }
@@ -998,7 +1083,7 @@ struct WaveDantzig {
         double t[R], sacc[R];
 #pragma unroll
         for (int s = 0; s < R; s++) {
-          t[s] = row(s) < r ? L[lrow(r) + row(s)] / d[s] : 0.0;
+          t[s] = row(s) < r ? L[lel(r, row(s))] / d[s] : 0.0;
           sacc[s] = 0.0;
         }
         const int ro = rowOff(rdliR(C, r));
@@ -1009,7 +1094,7 @@ struct WaveDantzig {
           const double tk = rdlR(t, k);
 #pragma unroll
           for (int s = 0; s < R; s++)
-            if (row(s) >= r && row(s) < n2) sacc[s] += L[lrow(row(s)) + k] * tk;
+            if (row(s) >= r && row(s) < n2) sacc[s] += L[lel(row(s), k)] * tk;
         }
 #pragma unroll
         for (int s = 0; s < R; s++) {
@@ -1035,22 +1120,21 @@ struct WaveDantzig {
 #pragma unroll
           for (int u = 0; u < 8; u++) {
             const int i = i0 + u;
-            const int src = lrow(i + 1 < n2 ? i + 1 : n2 - 1);
+            const int src = i + 1 < n2 ? i + 1 : n2 - 1;
 #pragma unroll
             for (int s = 0; s < R; s++) {
               const int j = row(s);
-              v[u][s] = (i < n2 - 1 && j < i) ? L[src + j + (j >= r ? 1 : 0)] : 0.0;
+              v[u][s] = (i < n2 - 1 && j < i) ? L[lel(src, j + (j >= r ? 1 : 0))] : 0.0;
             }
           }
           WSYNC();
 #pragma unroll
           for (int u = 0; u < 8; u++) {
             const int i = i0 + u;
-            const int dst = lrow(i);
 #pragma unroll
             for (int s = 0; s < R; s++) {
               const int j = row(s);
-              if (i < n2 - 1 && j < i) L[dst + j] = v[u][s];
+              if (i < n2 - 1 && j < i) L[lel(i, j)] = v[u][s];
             }
           }
           WSYNC();

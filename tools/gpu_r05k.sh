@@ -1,0 +1,28 @@
+# r05k: maskless triangular solves on the panel-packed factor -- step micro,
+# the LCP micro-benchmarks against the HEAD harness (dbg/liblcp_bench_base.so:
+# flags, pivots and x bit for bit), the -m gpu suite, bench, stage timing
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out; T=${TAG:-r05k}
+mkdir -p $O
+timeout -k 10 60 tools/micro/tri_bench > $O/${T}_tri_bench.log 2>&1 || { echo TRI FAILED; cat $O/${T}_tri_bench.log; exit 1; }
+cat $O/${T}_tri_bench.log
+LCP_BENCH_LIB=$PWD/dbg/liblcp_bench_base.so timeout -k 10 120 python tools/lcp_bench.py run > $O/${T}_lcp_base.log 2>&1 || { echo LB0 FAILED; tail $O/${T}_lcp_base.log; exit 1; }
+cp $O/lcp_out.npy dbg/lcp_baseline.npy
+timeout -k 10 120 python tools/lcp_bench.py run > $O/${T}_lcp_micro.log 2>&1 || { echo LB1 FAILED; tail $O/${T}_lcp_micro.log; exit 1; }
+grep -v amdgpu $O/${T}_lcp_micro.log | head -3; grep "n=24" -A1 $O/${T}_lcp_micro.log
+for pk in 0 1; do
+LCP_WIDE_PACKED=$pk LCP_BENCH_LIB=$PWD/dbg/liblcp_bench_base.so timeout -k 10 120 python tools/lcp_bench.py run_wide > $O/${T}_lcp_wide_base$pk.log 2>&1 || { echo LW0 FAILED; tail $O/${T}_lcp_wide_base$pk.log; exit 1; }
+cp $O/lcp_wide_out.npy dbg/lcp_wide_baseline.npy
+LCP_WIDE_PACKED=$pk timeout -k 10 120 python tools/lcp_bench.py run_wide > $O/${T}_lcp_wide$pk.log 2>&1 || { echo LW1 FAILED; tail $O/${T}_lcp_wide$pk.log; exit 1; }
+echo "packed=$pk base:"; grep -v amdgpu $O/${T}_lcp_wide_base$pk.log | head -2
+echo "packed=$pk new:"; grep -v amdgpu $O/${T}_lcp_wide$pk.log | grep -v "^  problem" ; grep -v amdgpu $O/${T}_lcp_wide$pk.log | grep "^  problem" | head -2
+done
+rm -f dbg/lcp_wide_baseline.npy dbg/lcp_baseline.npy
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/${T}_gpu_tests.log 2>&1 || { echo TESTS FAILED; grep -E "FAIL|Error" $O/${T}_gpu_tests.log | head -20; tail -30 $O/${T}_gpu_tests.log; exit 1; }
+tail -1 $O/${T}_gpu_tests.log
+timeout -k 10 300 python bench.py --no-cpu-baseline > $O/${T}_bench.json 2> $O/${T}_bench.err || { echo BENCH FAILED; tail -20 $O/${T}_bench.err; exit 1; }
+python -c "import json;d=json.load(open('$O/${T}_bench.json'));m=d['atlas_mesh'];r=d['roofline'];print('value',d['value'],d['kernels_ms'],r['frac'],r.get('frac_with_solvers'),'| mesh',m['value'],m['kernels_ms']['forward'],m['kernels_ms']['backward'])"
+STAGE_WORKLOAD=atlas_mesh NIMBLE_AMD_LIB=dbg/libnimble_dbg.so timeout -k 10 300 python tools/stage_timing.py > $O/${T}_stage_timing_atlas_mesh.log 2>&1 || { echo STAGE FAILED; tail -5 $O/${T}_stage_timing_atlas_mesh.log; exit 1; }
+NIMBLE_AMD_LIB=dbg/libnimble_dbg.so STAGE_HIST_OUT=$O/${T}_forward_world_latency_hist.json timeout -k 10 120 python tools/stage_timing.py > $O/${T}_stage_timing.log 2>&1 || { echo STAGE2 FAILED; tail -5 $O/${T}_stage_timing.log; exit 1; }
+echo R05K DONE

@@ -90,7 +90,9 @@ extern "C" int lcp_bench_launch(int P, int nmax, int nl, const int* nArr, const 
 // L, A's packed lower triangle and the scatter vector in LDS.  One problem
 // per 64-lane workgroup; per problem: ok, clocks, pivots, the per-phase split
 // (LCP_PROFILE: swap, solveL1, solveL1T, ldltRemove, w_i, pivot body), x.
-extern "C" __global__ void __launch_bounds__(64)
+// kPL: L in the packed panels the wide forward kernel's stage holds
+template <bool kPL>
+__global__ void __launch_bounds__(64)
 lcp_bench_wide_kernel(int nmax, int nl, const int* nArr, const double* Ag, const double* bg, const double* log_,
                       const double* hig, const int* fig, double* out) {
   extern __shared__ double ldsbuf[];
@@ -117,7 +119,7 @@ lcp_bench_wide_kernel(int nmax, int nl, const int* nArr, const double* Ag, const
   if (lane < 24) dshared[lane] = 0.0;
   __syncthreads();
   const long long t0 = __builtin_amdgcn_s_memtime();
-  const bool ok = waveDantzigR<true, 2, true>(n, Ap, L, scr, x, b, lo, hi, fi, lane, dshared);
+  const bool ok = waveDantzigR<true, 2, true, true, kPL>(n, Ap, L, scr, x, b, lo, hi, fi, lane, dshared);
   const long long t1 = __builtin_amdgcn_s_memtime();
   __syncthreads();
   if (lane == 0) {
@@ -136,7 +138,11 @@ lcp_bench_wide_kernel(int nmax, int nl, const int* nArr, const double* Ag, const
 extern "C" int lcp_bench_wide_launch(int P, int nmax, int nl, const int* nArr, const double* A, const double* b,
                                      const double* lo, const double* hi, const int* fi, double* out, void* stream) {
   const size_t ldsBytes = (size_t)(nl * (nl | 1) + nl * (nl + 1) / 2 + nl + 8) * sizeof(double);
-  hipLaunchKernelGGL(lcp_bench_wide_kernel, dim3(P), dim3(64), ldsBytes, (hipStream_t)stream, nmax, nl, nArr, A, b, lo,
-                     hi, fi, out);
+  if (getenv("LCP_WIDE_PACKED") && atoi(getenv("LCP_WIDE_PACKED")))
+    hipLaunchKernelGGL(lcp_bench_wide_kernel<true>, dim3(P), dim3(64), ldsBytes, (hipStream_t)stream, nmax, nl, nArr, A,
+                       b, lo, hi, fi, out);
+  else
+    hipLaunchKernelGGL(lcp_bench_wide_kernel<false>, dim3(P), dim3(64), ldsBytes, (hipStream_t)stream, nmax, nl, nArr,
+                       A, b, lo, hi, fi, out);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }

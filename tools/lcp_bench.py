@@ -169,6 +169,13 @@ def run_wide(limit=512):
         print(f"  problem {k} n={d['n'][k]} clocks {o[k, 1]:.0f} pivots {o[k, 4]:.0f} | "
               + " ".join(f"{nm}={int(v)}" for nm, v in zip(names, o[k, 8:14])))
     np.save(os.path.join(ROOT, "gpurun_out", "lcp_wide_out.npy"), o)
+    base = os.path.join(ROOT, "dbg", "lcp_wide_baseline.npy")
+    if os.path.exists(base):
+        ob = np.load(base)[:P]
+        a, c = np.nan_to_num(ob[:, 16:128], nan=1e300), np.nan_to_num(o[:, 16:128], nan=1e300)
+        dx = np.abs(a - c).max(axis=1) / np.maximum(1.0, np.abs(a).max(axis=1))
+        print(f"vs baseline: ok same {(ob[:, 0] == o[:, 0]).mean():.4f}, pivots same {(ob[:, 4] == o[:, 4]).mean():.4f}, "
+              f"bit-identical x {np.mean(dx == 0):.4f}, max rel dx {dx.max():.2e}, clocks {o[:, 1].sum() / ob[:, 1].sum():.3f}x")
 
 
 def solo(count=6):

@@ -7,14 +7,15 @@
 #include "../../nimblephysics_amd/csrc/lcp_wave.cuh"
 
 #define STEPS 1024
-template <int R>
+template <int R, bool kPL = false>
 __global__ void __launch_bounds__(64) tri(double* out, int m, int reps) {
   extern __shared__ double ldsbuf[];
   const int lane = threadIdx.x;
   const int ld = m | 1;
-  for (int t = lane; t < m * ld; t += 64) ldsbuf[t] = 1e-3 * ((t * 7919) % 97 - 48) / 97.0;
+  const int nL = dantzigLDoubles(m, kPL);
+  for (int t = lane; t < nL; t += 64) ldsbuf[t] = 1e-3 * ((t * 7919) % 97 - 48) / 97.0;
   __syncthreads();
-  WaveDantzig<R> D;
+  WaveDantzig<R, false, kPL> D;
   D.n = m;
   D.lane = lane;
   D.ldL = ld;
@@ -59,22 +60,23 @@ int main() {
   double h[8] = {0, 0, 0, 0, 0, 0, 0, 1e-3};
   for (int R = 1; R <= 2; R++) {
     const int ms[] = {24, 64, 96};
+    for (int pk = 0; pk < 2; pk++)
     for (int m : ms) {
       if ((R == 1 && m > 64) || (R == 2 && m < 64)) continue;
       (void)hipMemcpy(d, h, sizeof(h), hipMemcpyHostToDevice);
-      const size_t lds = (size_t)m * (m | 1) * sizeof(double);
-      if (R == 1) {
-        (void)hipFuncSetAttribute((const void*)tri<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(tri<1>, dim3(1), dim3(64), lds, 0, d, m, 20);
-      } else {
-        (void)hipFuncSetAttribute((const void*)tri<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(tri<2>, dim3(1), dim3(64), lds, 0, d, m, 20);
-      }
+      const size_t lds = (size_t)dantzigLDoubles(m, pk) * sizeof(double);
+      const void* f = R == 1 ? (pk ? (const void*)tri<1, true> : (const void*)tri<1>)
+                             : (pk ? (const void*)tri<2, true> : (const void*)tri<2>);
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (R == 1 && pk) hipLaunchKernelGGL((tri<1, true>), dim3(1), dim3(64), lds, 0, d, m, 20);
+      else if (R == 1) hipLaunchKernelGGL((tri<1>), dim3(1), dim3(64), lds, 0, d, m, 20);
+      else if (pk) hipLaunchKernelGGL((tri<2, true>), dim3(1), dim3(64), lds, 0, d, m, 20);
+      else hipLaunchKernelGGL((tri<2>), dim3(1), dim3(64), lds, 0, d, m, 20);
       (void)hipDeviceSynchronize();
       double o[8];
       (void)hipMemcpy(o, d, sizeof(o), hipMemcpyDeviceToHost);
-      printf("R=%d m=%3d: chain step %.1f (unrolled %.1f) | solveL1 %.0f clk = %.1f/step | solveL1T %.0f clk = %.1f/step | timer %.0f\n",
-             R, m, o[0], o[1], o[2], o[2] / m, o[3], o[3] / m, o[4]);
+      printf("%s R=%d m=%3d: chain step %.1f (unrolled %.1f) | solveL1 %.0f clk = %.1f/step | solveL1T %.0f clk = %.1f/step | timer %.0f\n",
+             pk ? "packed" : "square", R, m, o[0], o[1], o[2], o[2] / m, o[3], o[3] / m, o[4]);
     }
   }
   return 0;

@@ -15,6 +15,7 @@
 // The *R templates take the row-distributed arrays; the scalar forms are
 // their R = 1 instances.
 #pragma once
+#include <type_traits>
 #include "wave.cuh"
 #include "cod_wave.cuh"
 
@@ -612,20 +613,24 @@ __device__ double codSolveWave(typename Space<kLds>::dptr Ain, typename Space<kL
 // panel, contiguous), immediate offsets from one address.
 //
 // The zeros are what the triangular solves read instead of a mask: in either
-// layout every element a solve may read at or right of the diagonal is +0
-// (the buffer is zeroed when Dantzig starts, and the factor's updates -- a
-// row appended, ldltAddTL, a row and column removed -- only ever write
-// strictly lower elements: the square layout's shifts move zeros into
-// zeros, the packed one's keep each row's padding where it is), so a lane
-// that must not change in a step multiplies +0 instead of selecting it.
+// layout every element at or right of the diagonal is +0, and so is every
+// row >= n_C (the packed panels hold rows up to n, one past the last: a zero
+// row every column of which exists).  The buffer is zeroed when Dantzig
+// starts; the factor's updates -- a row appended at n_C, ldltAddTL, a row
+// and column removed -- only ever write strictly lower elements of rows
+// < n_C (the square layout's shifts move zeros into zeros, the packed one's
+// keep each row's padding where it is), and the removal zeroes the row it
+// leaves behind at the new n_C.  So a lane that must not change in a step
+// multiplies +0 instead of selecting it.
 __host__ __device__ __forceinline__ int dantzigLPanel(int q) { return 32 * q * (q + 1) + 8 * q; }
 __host__ __device__ __forceinline__ int dantzigLPackedEl(int i, int j) { return dantzigLPanel(i >> 3) + 8 * j + (i & 7); }
 __host__ __device__ __forceinline__ int dantzigLDoubles(int n, bool packed) {
-  return packed ? dantzigLPanel((n + 7) >> 3) + 8 : n * (n | 1);
+  return packed ? dantzigLPanel((n + 8) >> 3) + 8 : n * (n | 1);
 }
 template <int R, bool kPk = false, bool kPL = false>
 struct WaveDantzig {
   int n, nC, nN, lane, ldL;
+  bool degen;  // the factor has given a non-finite solve (solveAny)
   // offset of row i of L (i wave-uniform or per lane)
   // element (i, j) of L, and the stride between a row's consecutive columns
   static constexpr int kCs = kPL ? 8 : 1;
@@ -694,24 +699,23 @@ struct WaveDantzig {
   // a step is a readlane and unpredicated FMAs: no exec-mask update that
   // would wait on a vector compare, no per-step select, and no branch (a
   // taken branch per step cost more than the step).  A lane that must not
-  // change in a step reads a stored +0 (see dantzigLPackedRow): its own
-  // row's elements right of the diagonal, or -- a row already final or past
-  // m -- a block of zeros the offsets point it at, chosen once per block
-  // (lOff: the offset of the row's element 0 for L, the column's offset in
-  // its row for L^T).  Blocks are 8-aligned, so
-  // all steps of a block read their b_k from one register slot S (compile
-  // time: no slot select on the chain), and only the slots holding rows the
-  // block can change are updated -- rows > k for L, rows < k for L^T; the
-  // reference's loops touch no other row either.  The last, partial block
-  // pads its steps past m with b_k = +0 on zero elements (B - 0 * 0 is B bit
-  // for bit).  0 * b_k leaves a lane unchanged only for finite b_k; a
-  // non-finite b_k (degenerate factor) re-runs the solve predicated, exactly
-  // as the reference's loop.
+  // change in a step reads a stored +0 (see dantzigLPanel): its own row's
+  // elements right of the diagonal, or -- a row already final or past m --
+  // zeros the offsets point it at, chosen once per block (lOff: the offset
+  // of the row's element 0 for L, the column's offset in its row for L^T).
+  // Blocks are 8-aligned, so all steps of a block read their b_k from one
+  // register slot S (compile time: no slot select on the chain), and only
+  // the slots holding rows the block can change are updated -- rows > k for
+  // L, rows < k for L^T; the reference's loops touch no other row either.
+  // The last, partial block pads its steps past m with b_k = +0 on zero
+  // elements (B - 0 * 0 is B bit for bit).  0 * b_k leaves a lane unchanged
+  // only for finite b_k; a non-finite b_k (degenerate factor) re-runs the
+  // solve predicated, exactly as the reference's loop.
   // kOnly: update slot S alone (the other slot's updates are deferred, see
-  // solveL1 / solveL1T).  kMask: the triangle applied in registers instead
-  // (the packed factor's partial top block of L^T: its padded steps have no
-  // zero row every lane's column falls in)
-  template <int S, bool kFull, bool kT, bool kOnly = false, bool kMask = false>
+  // solveL1 / solveL1T).  kPred: a lane keeps its B where the reference's
+  // loop does not touch it (the result selected, not the multiplier zeroed:
+  // the form for non-finite b_k, where 0 * b_k is not 0)
+  template <int S, bool kFull, bool kT, bool kOnly = false, bool kPred = false>
   __device__ __forceinline__ void solveBlock(double (&B)[R], int m, int k0, const int (&lOff)[R]) {
     // steps: k = k0 + u (L) or k = k0 + 7 - u (L^T, k0 the block's lowest row)
     double Lk[R][8];
@@ -722,11 +726,11 @@ struct WaveDantzig {
       for (int u = 0; u < 8; u++) {
         const int k = kT ? k0 + 7 - u : k0 + u;
         // a padded step's element: zero for every lane (L: column m - 1 of
-        // the square factor, the block's own padding in the packed one; L^T:
-        // the square factor's row 0)
-        const int kc = kFull || k < m ? k : (kMask ? k0 : kT ? 0 : kPL ? k : m - 1);
+        // the square factor, the rows' own padding in the packed one; L^T:
+        // the square factor's row 0, the packed one's (zero) row k >= m)
+        const int kc = kFull || k < m ? k : (kPL ? k : kT ? 0 : m - 1);
         // (L^T: the row's element 0 from the block's panel, its k - k0 known
-        // at compile time in full blocks)
+        // at compile time)
         const int rb = kPL ? dantzigLPanel(k0 >> 3) + (kc - k0) : kc * ldL;
         Lk[s][u] = kT ? L[rb + lOff[s]] : L[lOff[s] + kc * kCs];
       }
@@ -740,17 +744,6 @@ struct WaveDantzig {
 #pragma unroll
       for (int u = 0; u < 8; u++) asm volatile("" : "+v"(Lk[s][u]));
     }
-    if (kMask) {
-#pragma unroll
-      for (int s = 0; s < R; s++) {
-        if ((kT ? s > S : s < S) || (kOnly && s != S)) continue;
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-          const int k = kT ? k0 + 7 - u : k0 + u;
-          Lk[s][u] = (kT ? row(s) < k : row(s) > k) && row(s) < m ? Lk[s][u] : 0.0;
-        }
-      }
-    }
 #pragma unroll
     for (int u = 0; u < 8; u++) {
       const int k = kT ? k0 + 7 - u : k0 + u;
@@ -760,17 +753,24 @@ struct WaveDantzig {
 #pragma unroll
       for (int s = 0; s < R; s++) {
         if ((kT ? s > S : s < S) || (kOnly && s != S)) continue;
-        B[s] -= Lk[s][u] * bk;
+        if (kPred) {
+          const double t = B[s] - Lk[s][u] * bk;
+          B[s] = (kT ? row(s) < k : row(s) > k) && row(s) < m && k < m ? t : B[s];
+        } else {
+          B[s] -= Lk[s][u] * bk;
+        }
       }
     }
   }
   // The deferred updates of slot D by the steps of blocks [kb0, kb1) (8-
-  // aligned, full) of slot 1 - D's solve, in the solve's step order: the same
-  // multiply-subtract per element as solveBlock's, with every b_k already
-  // final -- so an independent chain per lane of dependent FMAs instead of
-  // readlane -> FMA steps (the two slots' chains made an R = 2 step ~95
-  // clocks against ~75 for R = 1).
-  template <int D, bool kT>
+  // aligned; steps past m padded as in solveBlock) of slot 1 - D's solve, in
+  // the solve's step order: the same multiply-subtract per element as
+  // solveBlock's, with every b_k already final -- so an independent chain
+  // per lane of dependent FMAs instead of readlane -> FMA steps (the two
+  // slots' chains made an R = 2 step ~95 clocks against ~75 for R = 1).
+  // Every row of slot D is on the changing side of these steps (L: rows
+  // >= 64 > k; L^T: rows < 64 <= k), rows past m read zeros (lOff).
+  template <int D, bool kT, bool kPred = false>
   __device__ __forceinline__ void deferredSlot(double (&B)[R], int m, int kb0, int kb1, const int (&lOff)[R]) {
     constexpr int Sb = 1 - D;
     for (int b = 0; b < (kb1 - kb0) / 8; b++) {
@@ -779,26 +779,31 @@ struct WaveDantzig {
 #pragma unroll
       for (int u = 0; u < 8; u++) {
         const int k = kT ? k0 + 7 - u : k0 + u;
-        lv[u] = kT ? L[lel(k, 0) + lOff[D]] : L[lOff[D] + k * kCs];
+        lv[u] = kT ? L[(kPL ? dantzigLPanel(k0 >> 3) + 7 - u : (k < m ? k : 0) * ldL) + lOff[D]]
+                   : L[lOff[D] + k * kCs];
         bk[u] = rdl(B[Sb], k & 63);
+        bk[u] = k < m ? bk[u] : 0.0;
       }
 #pragma unroll
       for (int u = 0; u < 8; u++) asm volatile("" : "+v"(lv[u]));
 #pragma unroll
       for (int u = 0; u < 8; u++) {
-        const int k = kT ? k0 + 7 - u : k0 + u;
-        lv[u] = (kT ? row(D) < k : row(D) > k) && row(D) < m ? lv[u] : 0.0;
+        if (kPred) {
+          const int k = kT ? k0 + 7 - u : k0 + u;
+          const double t = B[D] - lv[u] * bk[u];
+          B[D] = (kT ? row(D) < k : row(D) > k) && row(D) < m && k < m ? t : B[D];
+        } else {
+          B[D] -= lv[u] * bk[u];
+        }
       }
-#pragma unroll
-      for (int u = 0; u < 8; u++) B[D] -= lv[u] * bk[u];
     }
   }
-  // per-block offsets onto stored zeros (solveBlock): L -- a row offset, the
-  // lane's own row while it can still change (rows k0 .. m - 1), else the
-  // block's first row, whose padding covers the block's columns (packed; the
-  // square factor's fixed offsets need no per-block choice); L^T -- a
-  // column, the lane's own while its row can still change (rows < k0 + 8,
-  // < m), else the block's last column, right of every row of the block
+  // per-block offsets onto stored zeros (solveBlock): L -- the lane's own
+  // row while it can still change (rows k0 .. m - 1), else the block's first
+  // row, whose padding covers the block's columns (packed; the square
+  // factor's fixed offsets need no per-block choice); L^T -- a column, the
+  // lane's own while its row can still change (rows < k0 + 8, < m), else
+  // the block's last column, right of every row of the block
   __device__ __forceinline__ void fwdOffsets(int m, int k0, const int (&own)[R], int (&o)[R]) const {
 #pragma unroll
     for (int s = 0; s < R; s++) o[s] = !kPL || (row(s) >= k0 && row(s) < m) ? own[s] : lel(k0, 0);
@@ -807,22 +812,19 @@ struct WaveDantzig {
 #pragma unroll
     for (int s = 0; s < R; s++) c[s] = !kPL || (row(s) < k0 + 8 && row(s) < m) ? own[s] : (k0 + 7) * kCs;
   }
-  template <bool kFull, bool kT>
+  template <bool kFull, bool kT, bool kPred>
   __device__ __forceinline__ void solveBlockAt(double (&B)[R], int m, int k0, const int (&lOff)[R]) {
-    if (R == 1 || k0 < 64) solveBlock<0, kFull, kT>(B, m, k0, lOff);
-    else solveBlock<R - 1, kFull, kT>(B, m, k0, lOff);
+    if (R == 1 || k0 < 64) solveBlock<0, kFull, kT, false, kPred>(B, m, k0, lOff);
+    else solveBlock<R - 1, kFull, kT, false, kPred>(B, m, k0, lOff);
   }
-  __device__ __forceinline__ void solveL1(double (&B)[R], int m) {
-    m = uni(m);
-    LP_BEGIN();
-    double B0[R];
+  template <bool kPred>
+  __device__ __forceinline__ void sweepL1(double (&B)[R], int m) {
     int rowOffL[R], o[R];
 #pragma unroll
-    for (int s = 0; s < R; s++) {
-      B0[s] = B[s];
-      // (rows past m: the square factor's row 0, zero in every column)
-      rowOffL[s] = lel(row(s) < m ? row(s) : 0, 0);
-    }
+    for (int s = 0; s < R; s++)
+      // (rows past m: a zero row -- the square factor's row 0, the packed
+      // one's row m)
+      rowOffL[s] = lel(row(s) < m ? row(s) : (kPL ? m : 0), 0);
     int k0 = 0;
     if constexpr (R == 2) {
       // rows 0..63 first, slot 0 alone; slot 1's updates by those steps
@@ -830,124 +832,116 @@ struct WaveDantzig {
       const int kA = m < 64 ? m : 64;
       for (; k0 + 8 <= kA; k0 += 8) {
         fwdOffsets(m, k0, rowOffL, o);
-        solveBlock<0, true, false, true>(B, m, k0, o);
+        solveBlock<0, true, false, true, kPred>(B, m, k0, o);
       }
       if (m <= 64) {
         if (k0 < m) {
           fwdOffsets(m, k0, rowOffL, o);
-          solveBlock<0, false, false, true>(B, m, k0, o);
+          solveBlock<0, false, false, true, kPred>(B, m, k0, o);
         }
       } else {
-        deferredSlot<1, false>(B, m, 0, 64, rowOffL);
+        deferredSlot<1, false, kPred>(B, m, 0, 64, rowOffL);
         for (; k0 + 8 <= m; k0 += 8) {
           fwdOffsets(m, k0, rowOffL, o);
-          solveBlock<1, true, false>(B, m, k0, o);
+          solveBlock<1, true, false, false, kPred>(B, m, k0, o);
         }
         if (k0 < m) {
           fwdOffsets(m, k0, rowOffL, o);
-          solveBlock<1, false, false>(B, m, k0, o);
+          solveBlock<1, false, false, false, kPred>(B, m, k0, o);
         }
       }
     } else {
       for (; k0 + 8 <= m; k0 += 8) {
         fwdOffsets(m, k0, rowOffL, o);
-        solveBlockAt<true, false>(B, m, k0, o);
+        solveBlockAt<true, false, kPred>(B, m, k0, o);
       }
       if (k0 < m) {
         fwdOffsets(m, k0, rowOffL, o);
-        solveBlockAt<false, false>(B, m, k0, o);
+        solveBlockAt<false, false, kPred>(B, m, k0, o);
       }
     }
-    bool nonFinite = false;
-#pragma unroll
-    for (int s = 0; s < R; s++) nonFinite = nonFinite || (row(s) < m && !isfinite(B[s]));
-    if (__ballot(nonFinite)) {
-#pragma unroll
-      for (int s = 0; s < R; s++) B[s] = B0[s];
-      for (int k = 0; k < m; k++) {
-        const double bk = rdlR(B, k);
-#pragma unroll
-        for (int s = 0; s < R; s++)
-          if (row(s) > k && row(s) < m) B[s] -= L[lel(row(s), k)] * bk;
-      }
-    }
-    LP_END(prof, 1);
   }
-  // L^T x = B: the blocks from the last row up, the partial one first
-  // (8-aligned below it)
-  __device__ __forceinline__ void solveL1T(double (&B)[R], int m) {
-    m = uni(m);
-    LP_BEGIN();
-    double B0[R];
+  // L^T: the blocks from the last row up, the partial one first (8-aligned
+  // below it)
+  template <bool kPred>
+  __device__ __forceinline__ void sweepL1T(double (&B)[R], int m) {
     int colL[R], c[R];
 #pragma unroll
-    for (int s = 0; s < R; s++) {
-      B0[s] = B[s];
+    for (int s = 0; s < R; s++)
       // (rows past m: the square factor's column m - 1, zero in every row < m)
       colL[s] = (row(s) < m ? row(s) : (kPL ? 0 : m - 1)) * kCs;
-    }
-    // the top block: partial (padded steps; masked for the packed factor) or full
-    auto topBlock = [&](int k0) {
-      bwdColumns(m, k0, colL, c);
-      constexpr int St = R - 1;
-      if (R == 2 && m > 64) {
-        if (k0 + 8 > m) solveBlock<St, false, true, true, kPL>(B, m, k0, c);
-        else solveBlock<St, true, true, true>(B, m, k0, c);
-      } else if (k0 + 8 > m) {
-        if (R == 1 || k0 < 64) solveBlock<0, false, true, false, kPL>(B, m, k0, c);
-        else solveBlock<St, false, true, false, kPL>(B, m, k0, c);
-      } else {
-        solveBlockAt<true, true>(B, m, k0, c);
-      }
-    };
-    if (R == 2 && m > 64) {
+    bool wide = false;
+    if constexpr (R == 2) wide = m > 64;
+    if (wide) {
       // rows 64.. first, slot 1 alone; slot 0's updates by those steps
       // deferred to one pass (its rows are all below them); then rows 0..63
       int k0 = (m - 1) & ~7;
-      topBlock(k0);
+      bwdColumns(m, k0, colL, c);
+      if (k0 + 8 > m) solveBlock<R - 1, false, true, true, kPred>(B, m, k0, c);
+      else solveBlock<R - 1, true, true, true, kPred>(B, m, k0, c);
       for (k0 -= 8; k0 >= 64; k0 -= 8) {
         bwdColumns(m, k0, colL, c);
-        solveBlock<R - 1, true, true, true>(B, m, k0, c);
+        solveBlock<R - 1, true, true, true, kPred>(B, m, k0, c);
       }
-      // the partial top block's padded steps change nothing: from m down
-      const int kTop = ((m - 1) & ~7) + 8;
-      if (kTop > m) {
-        // its live steps m-1 .. kTop-8, in the solve's order, then the full blocks
-        for (int k = m - 1; k >= kTop - 8; k--) {
-          const double bk = rdl(B[R - 1], k & 63);
-          double lv = L[lel(k, 0) + colL[0]];
-          lv = row(0) < k && row(0) < m ? lv : 0.0;
-          B[0] -= lv * bk;
-        }
-        deferredSlot<0, true>(B, m, 64, kTop - 8, colL);
-      } else {
-        deferredSlot<0, true>(B, m, 64, kTop, colL);
-      }
+      if constexpr (R == 2) deferredSlot<0, true, kPred>(B, m, 64, ((m - 1) & ~7) + 8, colL);
       for (k0 = 56; k0 >= 0; k0 -= 8) {
         bwdColumns(m, k0, colL, c);
-        solveBlock<0, true, true>(B, m, k0, c);
+        solveBlock<0, true, true, false, kPred>(B, m, k0, c);
       }
     } else if (m > 0) {
       int k0 = (m - 1) & ~7;  // lowest row of the top block
-      topBlock(k0);
+      bwdColumns(m, k0, colL, c);
+      if (k0 + 8 > m) solveBlockAt<false, true, kPred>(B, m, k0, c);
+      else solveBlockAt<true, true, kPred>(B, m, k0, c);
       for (k0 -= 8; k0 >= 0; k0 -= 8) {
         bwdColumns(m, k0, colL, c);
-        solveBlockAt<true, true>(B, m, k0, c);
+        solveBlockAt<true, true, kPred>(B, m, k0, c);
       }
     }
+  }
+  // A non-finite b_k (a degenerate factor: an infinite d after a zero
+  // pivot) makes 0 * b_k a NaN where the reference's loop leaves a row
+  // alone, so such a solve runs predicated (sweep<true>): when B arrives
+  // non-finite, once the factor has shown itself degenerate (`degen`,
+  // sticky for the rest of the solve: it stays so until the offending row
+  // leaves C), or -- the first time -- again from the start when the
+  // unpredicated sweep's result is non-finite.  Finite b_k give the same
+  // bits either way (a skipped lane's +0 * b_k adds a signed zero only).
+  template <bool kT>
+  __device__ __forceinline__ void solveAny(double (&B)[R], int m) {
+    m = uni(m);
+    bool bad = false;
+#pragma unroll
+    for (int s = 0; s < R; s++) bad = bad || (row(s) < m && !isfinite(B[s]));
+    if (degen || __ballot(bad)) {
+      if (kT) sweepL1T<true>(B, m);
+      else sweepL1<true>(B, m);
+      return;
+    }
+    double B0[R];
+#pragma unroll
+    for (int s = 0; s < R; s++) B0[s] = B[s];
+    if (kT) sweepL1T<false>(B, m);
+    else sweepL1<false>(B, m);
     bool nonFinite = false;
 #pragma unroll
     for (int s = 0; s < R; s++) nonFinite = nonFinite || (row(s) < m && !isfinite(B[s]));
     if (__ballot(nonFinite)) {
+      degen = true;
 #pragma unroll
       for (int s = 0; s < R; s++) B[s] = B0[s];
-      for (int k = m - 1; k >= 0; k--) {
-        const double bk = rdlR(B, k);
-#pragma unroll
-        for (int s = 0; s < R; s++)
-          if (row(s) < k) B[s] -= L[lel(k, row(s))] * bk;
-      }
+      if (kT) sweepL1T<true>(B, m);
+      else sweepL1<true>(B, m);
     }
+  }
+  __device__ __forceinline__ void solveL1(double (&B)[R], int m) {
+    LP_BEGIN();
+    solveAny<false>(B, m);
+    LP_END(prof, 1);
+  }
+  __device__ __forceinline__ void solveL1T(double (&B)[R], int m) {
+    LP_BEGIN();
+    solveAny<true>(B, m);
     LP_END(prof, 2);
   }
   __device__ __forceinline__ double sumC(const double (&u)[R], const double (&v)[R]) const {
@@ -1159,6 +1153,11 @@ struct WaveDantzig {
       for (int s = 0; s < R; s++)
         if (row(s) >= r && row(s) < n2 - 1) d[s] = dn[s];
     }
+    // the row left behind at the new n_C: zero again (dantzigLPanel)
+#pragma unroll
+    for (int s = 0; s < R; s++)
+      if (row(s) < n2 - 1) L[lel(n2 - 1, row(s))] = 0.0;
+    WSYNC();
     LP_END(prof, 3);
   }
   __device__ __forceinline__ void transferFromCtoN(int i) {
@@ -1250,7 +1249,7 @@ __device__ bool waveDantzigR(int n, typename Space<kLds>::cdptr Ain, typename Sp
       __hip_atomic_fetch_add(tally + 2, flops, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   };
-  D.n = n; D.nC = 0; D.nN = 0; D.lane = lane; D.ldL = n | 1;
+  D.n = n; D.nC = 0; D.nN = 0; D.lane = lane; D.ldL = n | 1; D.degen = false;
   D.A = A; D.L = Lbuf; D.scr = scr;
 #pragma unroll
   for (int s = 0; s < R; s++) {
@@ -1337,14 +1336,18 @@ __device__ bool waveDantzigR(int n, typename Space<kLds>::cdptr Ain, typename Sp
           // together, then the multiply-adds in j order (A symmetric: row j);
           // the last, partial block pads with +0 * -0 terms (acc + -0 is acc
           // bit for bit), so no term is a branch of its own
-          auto block = [&](int j0, bool full) {
+          // (S: the register slot of the block's C entries, compile time --
+          // 8-aligned blocks never straddle row 64)
+          auto block = [&](auto Sc, int j0, bool full) {
+            constexpr int S = decltype(Sc)::value;
             double dx[8], av[R][8];
             int ro[8];
 #pragma unroll
             for (int u = 0; u < 8; u++) {
-              const int j = full || j0 + u < nC ? j0 + u : 0;
-              dx[u] = rdlR(D.deltaX, j);
-              ro[u] = D.rowOff(j);
+              const int j = (full || j0 + u < nC ? j0 + u : j0) & 63;
+              dx[u] = rdl(D.deltaX[S], j);
+              const int pj = rdli(D.p[S], j);
+              ro[u] = kPk ? pj : pj * n;
             }
 #pragma unroll
             for (int u = 0; u < 8; u++)
@@ -1369,8 +1372,20 @@ __device__ bool waveDantzigR(int n, typename Space<kLds>::cdptr Ain, typename Sp
               for (int s = 0; s < R; s++) acc[s] += av[s][u] * dx[u];
           };
           int j0 = 0;
-          for (; j0 + 8 <= nC; j0 += 8) block(j0, true);
-          if (j0 < nC) block(j0, false);
+#ifdef LCP_PROFILE
+          const long long lpm_ = (long long)__builtin_amdgcn_s_memtime();
+#endif
+          using S0 = std::integral_constant<int, 0>;
+          using S1 = std::integral_constant<int, R - 1>;
+          for (; j0 + 8 <= nC && j0 < 64; j0 += 8) block(S0{}, j0, true);
+          for (; j0 + 8 <= nC; j0 += 8) block(S1{}, j0, true);
+          if (j0 < nC) {
+            if (j0 < 64) block(S0{}, j0, false);
+            else block(S1{}, j0, false);
+          }
+#ifdef LCP_PROFILE
+          D.prof[6] += (long long)__builtin_amdgcn_s_memtime() - lpm_;
+#endif
           const int roI = D.rowOff(i);
 #pragma unroll
           for (int s = 0; s < R; s++) {
@@ -1455,6 +1470,9 @@ __device__ bool waveDantzigR(int n, typename Space<kLds>::cdptr Ain, typename Sp
           if (inN[q]) D.w[q] += s * D.deltaW[q];
           if (row == i) D.w[q] += s * dwi;
         }
+#ifdef LCP_PROFILE
+        const long long lpt_ = (long long)__builtin_amdgcn_s_memtime();
+#endif
         switch (cmd) {
           case 1:
             setR(D.w, i, lane, 0.0);
@@ -1485,6 +1503,9 @@ __device__ bool waveDantzigR(int n, typename Space<kLds>::cdptr Ain, typename Sp
             D.transferFromCtoN(si);
             break;
         }
+#ifdef LCP_PROFILE
+        D.prof[7] += (long long)__builtin_amdgcn_s_memtime() - lpt_;
+#endif
         if (cmd <= 3) break;
       }
     }

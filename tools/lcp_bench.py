@@ -98,7 +98,7 @@ def run(reps=3):
         print(f"vs baseline: dantzig ok same {same_ok[0]:.4f}, pgs ok same {same_ok[1]:.4f}, "
               f"bit-identical x {np.mean(dx == 0):.4f}, max rel dx {dx.max():.2e}, "
               f"dantzig clocks {o[:, 1].sum() / ob[:, 1].sum():.3f}x, pgs clocks {o[:, 3].sum() / ob[:, 3].sum():.3f}x")
-    names = ["swap", "solveL1", "solveL1T", "ldltRemove", "w_i", "pivot body"]
+    names = ["swap", "solveL1", "solveL1T", "ldltRemove", "w_i", "pivot body", "(matvec)", "(transfers)"]
     for m in sorted(set(n.tolist())):
         sel = n == m
         cd, cp = o[sel, 1], o[sel, 3]
@@ -107,7 +107,7 @@ def run(reps=3):
               f"pgs mean {cp.mean():8.0f} max {cp.max():8.0f} (sweeps mean {o[sel, 6].mean():.1f})")
         worst = np.argmax(np.where(sel, o[:, 1], -1))
         prof = o[worst, 8:14]
-        print("      worst dantzig split: " + " ".join(f"{nm}={int(v)}" for nm, v in zip(names, prof)))
+        print("      worst dantzig split: " + " ".join(f"{nm}={int(v)}" for nm, v in zip(names, o[worst, 8:16])))
 
 
 PROB_WIDE = os.path.join(ROOT, "dbg", "lcp_wide.npz")
@@ -159,7 +159,7 @@ def run_wide(limit=512):
         assert rc == 0
     torch.cuda.synchronize()
     o = out.cpu().numpy()
-    names = ["swap", "solveL1", "solveL1T", "ldltRemove", "w_i", "pivot body"]
+    names = ["swap", "solveL1", "solveL1T", "ldltRemove", "w_i", "pivot body", "(matvec)", "(transfers)"]
     piv = np.maximum(o[:, 4], 1)
     print(f"{P} wide problems: ok agrees with oracle {np.mean((o[:, 0] > 0) == (d['okD'][:P] > 0)):.3f}; "
           f"clocks mean {o[:, 1].mean():.0f} max {o[:, 1].max():.0f}; pivots mean {o[:, 4].mean():.1f} max {o[:, 4].max():.0f}; "
@@ -167,7 +167,7 @@ def run_wide(limit=512):
     worst = np.argsort(-o[:, 1])[:5]
     for k in worst:
         print(f"  problem {k} n={d['n'][k]} clocks {o[k, 1]:.0f} pivots {o[k, 4]:.0f} | "
-              + " ".join(f"{nm}={int(v)}" for nm, v in zip(names, o[k, 8:14])))
+              + " ".join(f"{nm}={int(v)}" for nm, v in zip(names, o[k, 8:16])))
     np.save(os.path.join(ROOT, "gpurun_out", "lcp_wide_out.npy"), o)
     base = os.path.join(ROOT, "dbg", "lcp_wide_baseline.npy")
     if os.path.exists(base):

@@ -20,6 +20,7 @@ __global__ void __launch_bounds__(64) tri(double* out, int m, int reps) {
   D.lane = lane;
   D.ldL = ld;
   D.L = ldsbuf;
+  D.degen = false;
   double B[R];
   for (int s = 0; s < R; s++) B[s] = 1.0 + 1e-3 * (lane + 64 * s);
   long long t0, t1;
@@ -47,19 +48,30 @@ __global__ void __launch_bounds__(64) tri(double* out, int m, int reps) {
   for (int r = 0; r < reps; r++) D.solveL1T(B, m);
   t1 = __builtin_amdgcn_s_memtime();
   if (lane == 0) out[3] = (double)(t1 - t0) / reps;
+  // 6, 7: the predicated sweeps (a degenerate factor)
+  D.degen = true;
+  t0 = __builtin_amdgcn_s_memtime();
+  for (int r = 0; r < reps; r++) D.solveL1(B, m);
+  t1 = __builtin_amdgcn_s_memtime();
+  if (lane == 0) out[6] = (double)(t1 - t0) / reps;
+  t0 = __builtin_amdgcn_s_memtime();
+  for (int r = 0; r < reps; r++) D.solveL1T(B, m);
+  t1 = __builtin_amdgcn_s_memtime();
+  if (lane == 0) out[7] = (double)(t1 - t0) / reps;
   // 5: empty timer pair
   t0 = __builtin_amdgcn_s_memtime();
   t1 = __builtin_amdgcn_s_memtime();
   if (lane == 0) out[4] = (double)(t1 - t0);
   if (lane == 0) out[5] = x + B[0];
+  if (lane == 0 && out[5] == 12345.0) out[8] = 1;
 }
 
 int main() {
   double* d;
   (void)hipMalloc(&d, 64 * sizeof(double));
-  double h[8] = {0, 0, 0, 0, 0, 0, 0, 1e-3};
+  double h[16] = {0, 0, 0, 0, 0, 0, 0, 1e-3};
   for (int R = 1; R <= 2; R++) {
-    const int ms[] = {24, 64, 96};
+    const int ms[] = {21, 24, 64, 90, 96};
     for (int pk = 0; pk < 2; pk++)
     for (int m : ms) {
       if ((R == 1 && m > 64) || (R == 2 && m < 64)) continue;
@@ -73,10 +85,10 @@ int main() {
       else if (pk) hipLaunchKernelGGL((tri<2, true>), dim3(1), dim3(64), lds, 0, d, m, 20);
       else hipLaunchKernelGGL((tri<2>), dim3(1), dim3(64), lds, 0, d, m, 20);
       (void)hipDeviceSynchronize();
-      double o[8];
+      double o[16];
       (void)hipMemcpy(o, d, sizeof(o), hipMemcpyDeviceToHost);
-      printf("%s R=%d m=%3d: chain step %.1f (unrolled %.1f) | solveL1 %.0f clk = %.1f/step | solveL1T %.0f clk = %.1f/step | timer %.0f\n",
-             pk ? "packed" : "square", R, m, o[0], o[1], o[2], o[2] / m, o[3], o[3] / m, o[4]);
+      printf("%s R=%d m=%3d: chain step %.1f (unrolled %.1f) | solveL1 %.0f clk = %.1f/step | solveL1T %.0f clk = %.1f/step | predicated %.1f / %.1f per step | timer %.0f\n",
+             pk ? "packed" : "square", R, m, o[0], o[1], o[2], o[2] / m, o[3], o[3] / m, o[6] / m, o[7] / m, o[4]);
     }
   }
   return 0;

@@ -901,22 +901,29 @@ struct WaveDantzig {
   }
   // A non-finite b_k (a degenerate factor: an infinite d after a zero
   // pivot) makes 0 * b_k a NaN where the reference's loop leaves a row
-  // alone, so such a solve runs predicated (sweep<true>): when B arrives
-  // non-finite, once the factor has shown itself degenerate (`degen`,
-  // sticky for the rest of the solve: it stays so until the offending row
-  // leaves C), or -- the first time -- again from the start when the
-  // unpredicated sweep's result is non-finite.  Finite b_k give the same
-  // bits either way (a skipped lane's +0 * b_k adds a signed zero only).
+  // alone, so such a solve is re-run exactly as the reference's loop when
+  // the unpredicated sweep's result is non-finite (finite b_k give the same
+  // bits either way: a skipped lane's +0 * b_k adds a signed zero only).
+  // R = 1 (the one-row kernel: <= 64 rows, degenerate factors rare, and
+  // every variant of the sweep costs registers the kernel does not have):
+  // the unblocked loop.  R = 2 (the wide kernel's 65..128-row problems,
+  // whose failing Dantzig runs go degenerate for dozens of pivots): the
+  // blocked predicated sweep, taken directly when B arrives non-finite or
+  // once the factor has shown itself degenerate (`degen`, sticky for the
+  // rest of the solve) -- measured r05m..v5: 96-row problem 4.39M -> 2.35M
+  // clocks, the one-row kernel unchanged.
   template <bool kT>
   __device__ __forceinline__ void solveAny(double (&B)[R], int m) {
     m = uni(m);
-    bool bad = false;
+    if constexpr (R == 2) {
+      bool bad = false;
 #pragma unroll
-    for (int s = 0; s < R; s++) bad = bad || (row(s) < m && !isfinite(B[s]));
-    if (degen || __ballot(bad)) {
-      if (kT) sweepL1T<true>(B, m);
-      else sweepL1<true>(B, m);
-      return;
+      for (int s = 0; s < R; s++) bad = bad || (row(s) < m && !isfinite(B[s]));
+      if (degen || __ballot(bad)) {
+        if (kT) sweepL1T<true>(B, m);
+        else sweepL1<true>(B, m);
+        return;
+      }
     }
     double B0[R];
 #pragma unroll
@@ -930,8 +937,24 @@ struct WaveDantzig {
       degen = true;
 #pragma unroll
       for (int s = 0; s < R; s++) B[s] = B0[s];
-      if (kT) sweepL1T<true>(B, m);
-      else sweepL1<true>(B, m);
+      if constexpr (R == 2) {
+        if (kT) sweepL1T<true>(B, m);
+        else sweepL1<true>(B, m);
+      } else if (kT) {
+        for (int k = m - 1; k >= 0; k--) {
+          const double bk = rdlR(B, k);
+#pragma unroll
+          for (int s = 0; s < R; s++)
+            if (row(s) < k) B[s] -= L[lel(k, row(s))] * bk;
+        }
+      } else {
+        for (int k = 0; k < m; k++) {
+          const double bk = rdlR(B, k);
+#pragma unroll
+          for (int s = 0; s < R; s++)
+            if (row(s) > k && row(s) < m) B[s] -= L[lel(row(s), k)] * bk;
+        }
+      }
     }
   }
   __device__ __forceinline__ void solveL1(double (&B)[R], int m) {
@@ -1336,18 +1359,14 @@ __device__ bool waveDantzigR(int n, typename Space<kLds>::cdptr Ain, typename Sp
           // together, then the multiply-adds in j order (A symmetric: row j);
           // the last, partial block pads with +0 * -0 terms (acc + -0 is acc
           // bit for bit), so no term is a branch of its own
-          // (S: the register slot of the block's C entries, compile time --
-          // 8-aligned blocks never straddle row 64)
-          auto block = [&](auto Sc, int j0, bool full) {
-            constexpr int S = decltype(Sc)::value;
+          auto block = [&](int j0, bool full) {
             double dx[8], av[R][8];
             int ro[8];
 #pragma unroll
             for (int u = 0; u < 8; u++) {
-              const int j = (full || j0 + u < nC ? j0 + u : j0) & 63;
-              dx[u] = rdl(D.deltaX[S], j);
-              const int pj = rdli(D.p[S], j);
-              ro[u] = kPk ? pj : pj * n;
+              const int j = full || j0 + u < nC ? j0 + u : 0;
+              dx[u] = rdlR(D.deltaX, j);
+              ro[u] = D.rowOff(j);
             }
 #pragma unroll
             for (int u = 0; u < 8; u++)
@@ -1375,14 +1394,8 @@ __device__ bool waveDantzigR(int n, typename Space<kLds>::cdptr Ain, typename Sp
 #ifdef LCP_PROFILE
           const long long lpm_ = (long long)__builtin_amdgcn_s_memtime();
 #endif
-          using S0 = std::integral_constant<int, 0>;
-          using S1 = std::integral_constant<int, R - 1>;
-          for (; j0 + 8 <= nC && j0 < 64; j0 += 8) block(S0{}, j0, true);
-          for (; j0 + 8 <= nC; j0 += 8) block(S1{}, j0, true);
-          if (j0 < nC) {
-            if (j0 < 64) block(S0{}, j0, false);
-            else block(S1{}, j0, false);
-          }
+          for (; j0 + 8 <= nC; j0 += 8) block(j0, true);
+          if (j0 < nC) block(j0, false);
 #ifdef LCP_PROFILE
           D.prof[6] += (long long)__builtin_amdgcn_s_memtime() - lpm_;
 #endif

@@ -472,10 +472,13 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, const double* 
 // from the one-row kernel's dynamics and contacts: up to 64 LCP rows with the
 // pool in the big LDS stage (the one-row code, the helper wave on the task
 // board), more with two rows per lane and the pool in HBM (the stage holding
-// the factorisations).  (The same occupancy target as the one-row kernel:
-// the non-inlined narrow-phase functions both kernels call are compiled once,
-// for the tighter of the two register budgets.)
-extern "C" __global__ void __launch_bounds__(2 * WAVE) __attribute__((amdgpu_waves_per_eu(2)))
+// the factorisations).  One wide world per CU (its LDS stage), so one wave
+// per SIMD: the kernel takes the whole register file (256 VGPRs + AGPRs, no
+// spills; at two waves per SIMD it spilled 117 VGPRs to scratch: mesh Atlas
+// forward 2.54 -> 2.49 ms, r05 variant v1).  The non-inlined narrow-phase
+// functions both forward kernels call are compiled once, for the tighter of
+// the two register budgets.
+extern "C" __global__ void __launch_bounds__(2 * WAVE) __attribute__((amdgpu_waves_per_eu(1)))
 nimble_forward_wide_kernel(const ModelDev* __restrict__ mdp, Layout L, const double* __restrict__ state,
                            const double* __restrict__ forces, double* __restrict__ lcpCache,
                            double* __restrict__ nextState, double* __restrict__ snapshot, int snapDoubles,

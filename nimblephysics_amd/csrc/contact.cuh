@@ -703,7 +703,7 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
             if (kMeshInline)
               cnt = meshBoxPair(Tm, md.meshVerts + 3 * md.meshFirst[sm], md.meshCount[sm], md.shapeSize[sm], Tb,
                                 md.shapeSize[sb], meshFirst, md.clipDepth, md.shapeBody[si], md.shapeBody[sj],
-                                pairbuf, mscr, lane);
+                                pairbuf, mscr, lane, g_stamp);
             else
               cnt = deviceMeshBox(Tm, md.meshVerts + 3 * md.meshFirst[sm], md.meshCount[sm], md.shapeSize[sm], Tb,
                                   md.shapeSize[sb], meshFirst, md.clipDepth, md.shapeBody[si], md.shapeBody[sj],

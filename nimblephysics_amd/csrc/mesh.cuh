@@ -22,6 +22,7 @@
 // EDGE_EDGE tail edgeAFixed3 edgeADir3 edgeBFixed3 edgeBDir3 (CREC + 0..11).
 #pragma once
 #include "capsule.cuh"
+#include "stamp.cuh"
 #include "pool_sizes.h"
 #include "wave.cuh"
 
@@ -44,18 +45,29 @@ struct MeshObj {
   int lane;
 };
 
-// argmax over the wave: larger value, then lower index (the first of equals)
+// argmax over the wave: larger value, then lower index (the first of equals).
+// Two DPP reductions (the maximum, then the lowest index among the lanes
+// holding it -- each lane's index is the first of its own maxima, and lanes'
+// indices differ) instead of six rounds of cross-lane shuffles, each an LDS
+// permute waited on in turn.  `best` is never NaN (only d > best updates it).
+DEV int imin(int a, int b) { return a < b ? a : b; }
+DEV int waveMinIdx(int v) {
+  v = imin(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+  v = imin(v, __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+  v = imin(v, __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, false));  // row_ror:4
+  v = imin(v, __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false));  // row_ror:8
+  return imin(imin(rdli(v, 0), rdli(v, 16)), imin(rdli(v, 32), rdli(v, 48)));
+}
 DEV void waveArgMax(double& best, int& bi) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    const double ob = __shfl_xor(best, off);
-    const int oi = __shfl_xor(bi, off);
-    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
-  }
-  bi = __builtin_amdgcn_readfirstlane(bi);
+  const double mx = -waveMin(-best);
+  bi = waveMinIdx(best == mx ? bi : 0x7fffffff);
+  best = mx;
 }
 
-// ccdSupportMesh (DARTCollide.cpp:1935)
+// ccdSupportMesh (DARTCollide.cpp:1935).  The lane's vertices are read four
+// at a time (their loads issued together, then compared in index order: the
+// same first-of-equals scan), so a candidate list of a few hundred vertices
+// costs one memory latency per four of the lane's vertices, not per vertex
 DEV V meshSupport(const MeshObj& o, V dir) {
 #pragma clang fp contract(off)
   V ld = rotT(o.T, dir);
@@ -64,7 +76,20 @@ DEV V meshSupport(const MeshObj& o, V dir) {
   ld.z /= o.sc[2];
   double best = -__builtin_inf();
   int bi = 0x7fffffff;
-  for (int k = o.lane; k < o.nv; k += 64) {
+  int k = o.lane;
+  for (; k + 192 < o.nv; k += 256) {
+    double q[4][3];
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+#pragma unroll
+      for (int c = 0; c < 3; c++) q[u][c] = o.v[3 * (k + 64 * u) + c];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const double d = q[u][0] * ld.x + q[u][1] * ld.y + q[u][2] * ld.z;
+      if (d > best) { best = d; bi = k + 64 * u; }
+    }
+  }
+  for (; k < o.nv; k += 64) {
     const double* p = o.v + 3 * k;
     const double d = p[0] * ld.x + p[1] * ld.y + p[2] * ld.z;
     if (d > best) { best = d; bi = k; }
@@ -172,37 +197,83 @@ DEV void putRec(double* o, V point, V normal, double depth, int type) {
 // surviving mask.
 DEV unsigned long long hull2D(const lds_double* px, const lds_double* py, unsigned long long alive, int lane) {
 #pragma clang fp contract(off)
-  unsigned long long todo = alive;
+  // Lane j tests the line through point i and its own point j against every
+  // alive point k.  The reference's scan (the first clear sign, then the
+  // first opposite one ends it) keeps j exactly when no two measured points
+  // (|meas| >= 1e-3) lie on opposite sides, which does not depend on the
+  // order of k: so every lane runs the same k sequence to the end, reading
+  // the points by readlane from registers (each lane holds its own) instead
+  // of an LDS load waited on per step under a divergent early exit.
+  const bool have = (alive >> lane) & 1ull;
+  const double myx = have ? (double)px[lane] : 0.0, myy = have ? (double)py[lane] : 0.0;
+  // Deep points, settled without the scan.  The extreme points of the set
+  // in eight directions lie on its hull boundary, so each has a supporting
+  // line through another point: the scan keeps them, whatever it removed
+  // before (removals never take a supporting line's points away).  A point
+  // more than 1.5e-3 inside their octagon then has, for every line through
+  // it and another point, octagon vertices (alive) farther than 1e-3 on both
+  // sides: the scan removes it at its turn.  Unless another point projects
+  // onto it exactly (a zero-length line the reference normalises by no-op,
+  // keeping the point) -- such points take the scan.  The rest take the
+  // scan at their turn, against the set as the reference has it then (the
+  // deep points before them already gone, those after still there).
+  unsigned long long deep = 0ull;
+  if (__popcll(alive) > 8) {
+    const double dx[8] = {1, 1, 0, -1, -1, -1, 0, 1}, dy[8] = {0, 1, 1, 1, 0, -1, -1, -1};
+    double ox[8], oy[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      const double pr = have ? myx * dx[e] + myy * dy[e] : -__builtin_inf();
+      const double mx = -waveMin(-pr);
+      const int w = waveFirst(have && pr == mx);
+      ox[e] = rdl(myx, w);
+      oy[e] = rdl(myy, w);
+    }
+    double dmin = __builtin_inf();
+    bool degen = true;
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      const double ex = ox[(e + 1) & 7] - ox[e], ey = oy[(e + 1) & 7] - oy[e];
+      const double L = sqrt(ex * ex + ey * ey);
+      if (L > 1e-9) {
+        degen = false;
+        const double d = ((myx - ox[e]) * -ey + (myy - oy[e]) * ex) / L;  // inside: positive (CCW)
+        dmin = fmin(dmin, d);
+      }
+    }
+    bool twin = false;
+    for (unsigned long long m = alive; m; m &= m - 1) {
+      const int k = __ffsll((long long)m) - 1;
+      const double tx = myy - rdl(myy, k), ty = rdl(myx, k) - myx;  // the reference's line terms
+      twin = twin || (k != lane && tx * tx + ty * ty == 0.0);
+    }
+    deep = __ballot(have && !degen && dmin > 1.5e-3 && !twin);
+  }
+  unsigned long long todo = alive & ~deep;
   while (todo) {
     const int i = __ffsll((long long)todo) - 1;
     todo &= todo - 1;
-    const double six = px[i], siy = py[i];
-    bool isB = false;
+    alive &= ~(deep & ((1ull << i) - 1ull));
+    const double six = rdl(myx, i), siy = rdl(myy, i);
     const bool mine = ((alive >> lane) & 1ull) && lane != i;
-    if (mine) {
-      const double sjx = px[lane], sjy = py[lane];
-      double ax = siy - sjy, ay = sjx - six;
-      const double nn = ax * ax + ay * ay;
-      if (nn > 0) { const double q = sqrt(nn); ax /= q; ay /= q; }
-      const double b = -(ax * six + ay * siy);
-      isB = true;
-      int side = 0;
-      for (unsigned long long m = alive; m; m &= m - 1) {
-        const int k = __ffsll((long long)m) - 1;
-        const double meas = ax * px[k] + ay * py[k] + b;
+    double ax = siy - myy, ay = myx - six;
+    const double nn = ax * ax + ay * ay;
+    if (nn > 0) { const double q = sqrt(nn); ax /= q; ay /= q; }
+    const double b = -(ax * six + ay * siy);
+    bool pos = false, neg = false;
+    for (unsigned long long m = alive; m; m &= m - 1) {
+      const int k = __ffsll((long long)m) - 1;
+      const double meas = ax * rdl(myx, k) + ay * rdl(myy, k) + b;
+      if (!(fabs(meas) < 1e-3)) {
         const int ks = ccdSign(meas);
-        if (fabs(meas) < 1e-3) {
-        } else if (side == 0) {
-          side = ks;
-        } else if (side != ks) {
-          isB = false;
-          break;
-        }
+        pos = pos || ks > 0;
+        neg = neg || ks < 0;
       }
     }
+    const bool isB = mine && !(pos && neg);
     if (!__ballot(isB)) alive &= ~(1ull << i);
   }
-  return alive;
+  return alive & ~deep;
 }
 
 // prepareConvex2DShape (Geometry.cpp:3813): the points of `mask` sorted by
@@ -265,8 +336,11 @@ DEV bool containsSorted(P2 q, const lds_double* S, int n, V o, V bx, V by) {
 // in LDS (na, nb <= MESH_WMAX), scratch for 2-D coordinates and sorted hulls.
 // Appends records at out[PBREC * cnt]; returns the new count, -1 on overflow.
 DEV int faceFace(V dir, const lds_double* A, int na, const lds_double* B, int nb, lds_double* scr, double* out,
-                 int cnt, int lane) {
+                 int cnt, int lane, double* g_stamp = nullptr) {
 #pragma clang fp contract(off)
+  (void)g_stamp;
+  // (stage timing: 124 hulls, 125 angle sort, 126 containment, 127 edge pairs)
+  TACC_BEGIN(tH);
   lds_double* pxA = scr;
   lds_double* pyA = scr + MESH_WMAX;
   lds_double* pxB = scr + 2 * MESH_WMAX;
@@ -303,8 +377,12 @@ DEV int faceFace(V dir, const lds_double* A, int na, const lds_double* B, int nb
   const unsigned long long fullB = nb >= 64 ? ~0ull : ((1ull << nb) - 1ull);
   const unsigned long long hA = hull2D(pxA, pyA, fullA, lane);
   const unsigned long long hB = hull2D(pxB, pyB, fullB, lane);
+  TACC_END(124, tH);
+  TACC_BEGIN(tS);
   const int nsA = sortByAngle(A, pxA, pyA, hA, SA, lane);
   const int nsB = sortByAngle(B, pxB, pyB, hB, SB, lane);
+  TACC_END(125, tS);
+  TACC_BEGIN(tI);
   // vertices of A's hull inside B's (VERTEX_FACE), in hull order
   {
     bool in = false;
@@ -339,6 +417,8 @@ DEV int faceFace(V dir, const lds_double* A, int na, const lds_double* B, int nb
     }
     cnt += __popcll(m);
   }
+  TACC_END(126, tI);
+  TACC_BEGIN(tE);
   // edge pairs (i over A's sorted hull, j over B's), i-major: EDGE_EDGE
   const int ea = (nsA == 2) ? 1 : nsA, eb = (nsB == 2) ? 1 : nsB;
   for (int t0 = 0; t0 < ea * eb; t0 += 64) {
@@ -376,13 +456,14 @@ DEV int faceFace(V dir, const lds_double* A, int na, const lds_double* B, int nb
     }
     cnt += __popcll(m);
   }
+  TACC_END(127, tE);
   return cnt;
 }
 
 // createMeshMeshContacts (:2508) on witness sets A (object 1) / B (object 2);
 // returns the record count, -1 when unsupported (empty set / overflow)
 DEV int meshMeshContacts(V dir, const lds_double* A, int na, const lds_double* B, int nb, lds_double* scr, double* out,
-                         int lane) {
+                         int lane, double* g_stamp = nullptr) {
 #pragma clang fp contract(off)
   if (na <= 0 || nb <= 0) return -1;
   auto dirDot = [&](V n) { return n.x * dir.x + n.y * dir.y + n.z * dir.z; };
@@ -440,7 +521,7 @@ DEV int meshMeshContacts(V dir, const lds_double* A, int na, const lds_double* B
     if (lane == 0) putRec(out, b0, n, fabs(dot(b0, n) - dot(a0, n)), 1);
     return 1;
   }
-  return faceFace(dir, A, na, B, nb, scr, out, 0, lane);
+  return faceFace(dir, A, na, B, nb, scr, out, 0, lane, g_stamp);
 }
 
 }  // namespace msh
@@ -457,8 +538,11 @@ DEV int meshMeshContacts(V dir, const lds_double* A, int na, const lds_double* B
 // forward's HBM writes.)
 __device__ __forceinline__ int meshBoxPair(const double* Tm, const double* v, int nv, const double* sc,
                                            const double* Tb, const double* bs, bool meshFirst, double clip, int body1,
-                                           int body2, double* out, lds_double* scr, int lane) {
+                                           int body2, double* out, lds_double* scr, int lane,
+                                           double* g_stamp = nullptr) {
   using namespace cap;
+  (void)g_stamp;
+  TACC_BEGIN(tM);
   msh::MeshObj mo;
   Obj box;
   for (int i = 0; i < 12; i++) { mo.T.m[i] = Tm[i]; box.T.m[i] = Tb[i]; }
@@ -470,13 +554,22 @@ __device__ __forceinline__ int meshBoxPair(const double* Tm, const double* v, in
   double depth;
   V dir, ppos;
   const int hit = meshFirst ? mpr(mo, box, depth, dir, ppos) : mpr(box, mo, depth, dir, ppos);
+  // (stage timing: 120 pairs through MPR, 121 MPR, 122 witness sets, 123 contacts)
+  TACC_END(121, tM);
+#ifdef NIMBLE_STAGE_TIMING
+  if (lane == 0 && g_stamp) g_stamp[120] += 1;
+#endif
   if (hit != 0 || depth > clip) return 0;
+  TACC_BEGIN(tW);
   lds_double* wa = scr + 10 * MESH_WMAX;  // witness sets past the face-face scratch
   lds_double* wb = scr + 13 * MESH_WMAX;
   const int na = meshFirst ? msh::meshWitness(mo, dir, false, wa) : msh::boxWitness(box, dir, false, wa, lane);
   const int nb = meshFirst ? msh::boxWitness(box, dir, true, wb, lane) : msh::meshWitness(mo, dir, true, wb);
   if (na < 0 || nb < 0) return -1;
-  const int cnt = msh::meshMeshContacts(dir, wa, na, wb, nb, scr, out, lane);
+  TACC_END(122, tW);
+  TACC_BEGIN(tC);
+  const int cnt = msh::meshMeshContacts(dir, wa, na, wb, nb, scr, out, lane, g_stamp);
+  TACC_END(123, tC);
   if (cnt < 0) return -1;
   WSYNC();
   for (int c = lane; c < cnt; c += 64) { out[PBREC * c + 8] = body1; out[PBREC * c + 9] = body2; }

@@ -338,7 +338,12 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
         if (R == 1) {
           // (the deadlock guard expired: wave 0 detects the contacts itself)
           if (collideWait(ct, CS_GO)) {
+#ifdef NIMBLE_STAGE_TIMING
+            collideWorld<true>(md, lds<true>(s), L, lane, snapshot + (size_t)env * snapDoubles + snEdge(n),
+                               snapshot + (size_t)env * snapDoubles + snStamps(n));
+#else
             collideWorld<true>(md, lds<true>(s), L, lane, snapshot + (size_t)env * snapDoubles + snEdge(n));
+#endif
             collidePost(ct, CS_DONE, lane);
           }
         }  // (the wide kernel's worlds come with the one-row kernel's contacts)

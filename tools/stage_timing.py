@@ -94,6 +94,15 @@ for it in range(4):
     for (a, b), nm in names.items():
         m = (T[:, a] > 0) & (T[:, b] > 0)
         assert not (m & (T[:, b] < T[:, a])).any(), f"negative interval {nm.strip()}: stamps of two launches"
+    # the one-row kernel's own tail (its launch time is its slowest world's)
+    one = np.where(~wide & (T[:, 12] > 0) & (T[:, 13] > 0), T[:, 13] - T[:, 10], 0)
+    for wi in np.argsort(-one)[:3]:
+        parts = [f"{nm.strip()}={int(T[wi, b] - T[wi, a])}" for (a, b), nm in names.items()
+                 if T[wi, a] > 0 and T[wi, b] > 0 and b < 100 and (a, b) not in ((10, 11), (12, 13))]
+        print(f"  one-row world {wi}: total {int(one[wi])} rows {int(hd[wi, 1])} clamp {int(hd[wi, 2])} contacts {int(hd[wi, 0])} "
+              f"narrow phase {int(T[wi, 76])} post-process {int(T[wi, 77])} mesh pairs {int(T[wi, 120])} MPR {int(T[wi, 121])} "
+              f"witness {int(T[wi, 122])} contacts {int(T[wi, 123])} (hulls {int(T[wi, 124])} sort {int(T[wi, 125])} "
+              f"contain {int(T[wi, 126])} edges {int(T[wi, 127])}) | " + " ".join(parts))
     for wi in np.argsort(-tot)[:6]:
         parts = []
         for (a, b), nm in names.items():

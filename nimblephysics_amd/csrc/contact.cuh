@@ -736,7 +736,12 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
       }
       const int total = uni(__shfl(incl, npc > 0 ? npc - 1 : 0));
       const int excl = incl - cq;
-      if (npc > 0 && total <= WAVE) {
+      if (total == 0) {
+        // no candidate point in this chunk (most pairs of a mesh model, one
+        // per chunk): nothing to list; only an unsupported pair's flag
+        serial = false;
+        if (um && lane == 0) ct[H_STATUS] = (double)((int)ct[H_STATUS] | ST_UNSUPPORTED_SHAPE);
+      } else if (npc > 0 && total <= WAVE) {
         serial = false;
         // candidate -> (pair, point)
         int q = 0, exq = 0;

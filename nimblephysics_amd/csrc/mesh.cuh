@@ -207,11 +207,11 @@ DEV unsigned long long hull2D(const lds_double* px, const lds_double* py, unsign
   const bool have = (alive >> lane) & 1ull;
   const double myx = have ? (double)px[lane] : 0.0, myy = have ? (double)py[lane] : 0.0;
   // Deep points, settled without the scan.  The extreme points of the set
-  // in eight directions lie on its hull boundary, so each has a supporting
+  // in sixteen directions lie on its hull boundary, so each has a supporting
   // line through another point: the scan keeps them, whatever it removed
   // before (removals never take a supporting line's points away).  A point
-  // more than 1.5e-3 inside their octagon then has, for every line through
-  // it and another point, octagon vertices (alive) farther than 1e-3 on both
+  // more than 1.5e-3 inside their polygon then has, for every line through
+  // it and another point, polygon vertices (alive) farther than 1e-3 on both
   // sides: the scan removes it at its turn.  Unless another point projects
   // onto it exactly (a zero-length line the reference normalises by no-op,
   // keeping the point) -- such points take the scan.  The rest take the
@@ -219,10 +219,13 @@ DEV unsigned long long hull2D(const lds_double* px, const lds_double* py, unsign
   // deep points before them already gone, those after still there).
   unsigned long long deep = 0ull;
   if (__popcll(alive) > 8) {
-    const double dx[8] = {1, 1, 0, -1, -1, -1, 0, 1}, dy[8] = {0, 1, 1, 1, 0, -1, -1, -1};
-    double ox[8], oy[8];
+    // (16 directions, k pi / 8, counter-clockwise: their extreme points
+    // come in the hull's counter-clockwise order)
+    const double dx[16] = {1, 0.92387953251128674, 0.70710678118654757, 0.38268343236508984, 6.123233995736766e-17, -0.38268343236508973, -0.70710678118654746, -0.92387953251128674, -1, -0.92387953251128685, -0.70710678118654768, -0.38268343236509034, -1.8369701987210297e-16, 0.38268343236509, 0.70710678118654735, 0.92387953251128652};
+    const double dy[16] = {0, 0.38268343236508978, 0.70710678118654746, 0.92387953251128674, 1, 0.92387953251128674, 0.70710678118654757, 0.38268343236508989, 1.2246467991473532e-16, -0.38268343236508967, -0.70710678118654746, -0.92387953251128652, -1, -0.92387953251128663, -0.70710678118654768, -0.38268343236509039};
+    double ox[16], oy[16];
 #pragma unroll
-    for (int e = 0; e < 8; e++) {
+    for (int e = 0; e < 16; e++) {
       const double pr = have ? myx * dx[e] + myy * dy[e] : -__builtin_inf();
       const double mx = -waveMin(-pr);
       const int w = waveFirst(have && pr == mx);
@@ -232,8 +235,8 @@ DEV unsigned long long hull2D(const lds_double* px, const lds_double* py, unsign
     double dmin = __builtin_inf();
     bool degen = true;
 #pragma unroll
-    for (int e = 0; e < 8; e++) {
-      const double ex = ox[(e + 1) & 7] - ox[e], ey = oy[(e + 1) & 7] - oy[e];
+    for (int e = 0; e < 16; e++) {
+      const double ex = ox[(e + 1) & 15] - ox[e], ey = oy[(e + 1) & 15] - oy[e];
       const double L = sqrt(ex * ex + ey * ey);
       if (L > 1e-9) {
         degen = false;
@@ -249,18 +252,111 @@ DEV unsigned long long hull2D(const lds_double* px, const lds_double* py, unsign
     }
     deep = __ballot(have && !degen && dmin > 1.5e-3 && !twin);
   }
+  // Partner candidates: a boundary point's supporting line usually runs to
+  // a neighbour on the set's hull, so the hull is wrapped first (gift
+  // wrapping, one lane reduction per vertex) and each point names two
+  // candidates -- its hull neighbours, or the ends of the hull edge nearest
+  // to it.  A candidate's line is checked exactly as the reference's lane j
+  // checks it (the same operations, over every alive point, one per lane);
+  // only when neither candidate holds does the point take the full scan
+  // below.  (The wrap only steers the search: its result never decides a
+  // point.  Small sets skip it: the scan is cheaper there.)
+  int candA = -1, candB = -1;
+  if (__popcll(alive & ~deep) > 8) {
+    const double kx = have ? myx : __builtin_inf();
+    const double mnx = waveMin(kx);
+    const double ky = have && myx == mnx ? myy : __builtin_inf();
+    const double mny = waveMin(ky);
+    const int start = waveFirst(have && myx == mnx && myy == mny);
+    unsigned long long hullMask = 0ull;
+    int nxtH = -1, prvH = -1;
+    int c = start;
+    for (int step = 0; step < 64 && c >= 0; step++) {
+      hullMask |= 1ull << c;
+      const double cx = rdl(myx, c), cy = rdl(myy, c);
+      double qx = myx, qy = myy;
+      int qi = (have && lane != c && !(myx == cx && myy == cy)) ? lane : -1;
+      auto better = [&](double bx, double by, int bi) {
+        if (bi < 0) return false;
+        if (qi < 0) return true;
+        const double cr = (qx - cx) * (by - cy) - (qy - cy) * (bx - cx);
+        if (cr != 0.0) return cr < 0.0;  // b clockwise of the current winner
+        const double da = (qx - cx) * (qx - cx) + (qy - cy) * (qy - cy);
+        const double db = (bx - cx) * (bx - cx) + (by - cy) * (by - cy);
+        return db != da ? db > da : bi < qi;
+      };
+      auto combine = [&](double bx, double by, int bi) {
+        if (better(bx, by, bi)) { qx = bx; qy = by; qi = bi; }
+      };
+      combine(dppd<0xB1>(qx), dppd<0xB1>(qy), __builtin_amdgcn_update_dpp(-1, qi, 0xB1, 0xF, 0xF, false));
+      combine(dppd<0x4E>(qx), dppd<0x4E>(qy), __builtin_amdgcn_update_dpp(-1, qi, 0x4E, 0xF, 0xF, false));
+      combine(dppd<0x124>(qx), dppd<0x124>(qy), __builtin_amdgcn_update_dpp(-1, qi, 0x124, 0xF, 0xF, false));
+      combine(dppd<0x128>(qx), dppd<0x128>(qy), __builtin_amdgcn_update_dpp(-1, qi, 0x128, 0xF, 0xF, false));
+      const double rx[4] = {rdl(qx, 0), rdl(qx, 16), rdl(qx, 32), rdl(qx, 48)};
+      const double ry[4] = {rdl(qy, 0), rdl(qy, 16), rdl(qy, 32), rdl(qy, 48)};
+      const int ri[4] = {rdli(qi, 0), rdli(qi, 16), rdli(qi, 32), rdli(qi, 48)};
+      qx = rx[0]; qy = ry[0]; qi = ri[0];
+#pragma unroll
+      for (int r = 1; r < 4; r++) combine(rx[r], ry[r], ri[r]);
+      const int nx = uni(qi);
+      if (lane == c) nxtH = nx;
+      if (nx >= 0 && lane == nx) prvH = c;
+      if (nx < 0 || nx == start || ((hullMask >> nx) & 1ull)) break;
+      c = nx;
+    }
+    // (every lane runs the edge loop: its readlanes need the whole wave)
+    double best = __builtin_inf();
+    for (unsigned long long m = hullMask; m; m &= m - 1) {
+      const int v = __ffsll((long long)m) - 1;
+      const int w = rdli(nxtH, v);
+      if (w < 0) continue;
+      const double vx = rdl(myx, v), vy = rdl(myy, v), wx = rdl(myx, w), wy = rdl(myy, w);
+      const double ex = wx - vx, ey = wy - vy;
+      const double L2 = ex * ex + ey * ey;
+      const double cr = (myx - vx) * ey - (myy - vy) * ex;
+      const double d2 = L2 > 0.0 ? cr * cr / L2 : (myx - vx) * (myx - vx) + (myy - vy) * (myy - vy);
+      if (d2 < best) { best = d2; candA = v; candB = w; }
+    }
+    if ((hullMask >> lane) & 1ull) {
+      candA = prvH;
+      candB = nxtH;
+    }
+  }
   unsigned long long todo = alive & ~deep;
   while (todo) {
     const int i = __ffsll((long long)todo) - 1;
     todo &= todo - 1;
     alive &= ~(deep & ((1ull << i) - 1ull));
     const double six = rdl(myx, i), siy = rdl(myy, i);
+    {
+      // the candidates' lines, one alive point per lane
+      const bool liveK = (alive >> lane) & 1ull;
+      const int cA = rdli(candA, i), cB = rdli(candB, i);
+      bool found = false;
+#pragma unroll
+      for (int t = 0; t < 2; t++) {
+        const int j = t == 0 ? cA : cB;
+        if (found || j < 0 || j == i || !((alive >> j) & 1ull)) continue;
+        const double sjx = rdl(myx, j), sjy = rdl(myy, j);
+        double ax = siy - sjy, ay = sjx - six;
+        const double nn = ax * ax + ay * ay;
+        if (nn > 0) { const double q = sqrt(nn); ax /= q; ay /= q; }
+        const double b = -(ax * six + ay * siy);
+        const double meas = ax * myx + ay * myy + b;
+        const bool counted = liveK && !(fabs(meas) < 1e-3);
+        const int ks = ccdSign(meas);
+        const bool anyPos = __ballot(counted && ks > 0) != 0ull, anyNeg = __ballot(counted && ks < 0) != 0ull;
+        found = !(anyPos && anyNeg);
+      }
+      if (found) continue;  // kept
+    }
     const bool mine = ((alive >> lane) & 1ull) && lane != i;
     double ax = siy - myy, ay = myx - six;
     const double nn = ax * ax + ay * ay;
     if (nn > 0) { const double q = sqrt(nn); ax /= q; ay /= q; }
     const double b = -(ax * six + ay * siy);
     bool pos = false, neg = false;
+    int seen = 0;
     for (unsigned long long m = alive; m; m &= m - 1) {
       const int k = __ffsll((long long)m) - 1;
       const double meas = ax * rdl(myx, k) + ay * rdl(myy, k) + b;
@@ -269,6 +365,9 @@ DEV unsigned long long hull2D(const lds_double* px, const lds_double* py, unsign
         pos = pos || ks > 0;
         neg = neg || ks < 0;
       }
+      // every partner already has points on both sides: i is not a
+      // boundary point, whatever the rest of the points say
+      if ((++seen & 7) == 0 && !__ballot(mine && !(pos && neg))) break;
     }
     const bool isB = mine && !(pos && neg);
     if (!__ballot(isB)) alive &= ~(1ull << i);

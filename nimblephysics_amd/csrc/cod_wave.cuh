@@ -154,11 +154,18 @@ __device__ void codQrRegs(typename Space<kLds>::dptr A, Cod& c, typename Space<k
     }
     norm = nrm;
     COD_PROF(2);
-    // slot k is final: R part from the pivot lane, reflector tail below
+    // slot k is final: R part from the pivot lane, reflector tail below.
+    // The pivot lane stores its whole column, unconditionally (a uniform
+    // condition per element had become a branch per element): rows > k are
+    // overwritten by the tail right after (a wave's LDS operations execute
+    // in order), rows >= m go to vb's unused tail (the tail store reads vb
+    // only below m)
     if (lane == pl) {
 #pragma unroll
-      for (int i = 0; i < R; i++)
-        if (i <= k && i < m) A[i * ld + k] = a[i];
+      for (int i = 0; i < R; i++) {
+        auto dst = i < m ? &A[i * ld + k] : &vb[i];
+        *dst = a[i];
+      }
     }
     if (lane > k && lane < m) A[lane * ld + k] = vb[lane];
     if (lane == 0) { c.vd[k] = vk; c.vn[k] = vnorm; }

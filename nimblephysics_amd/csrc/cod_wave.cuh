@@ -477,9 +477,22 @@ rankAndRz:
         for (; j < n; j++) sc += A[row * ld + j] * A[i * ld + j];
         sc = 2 * sc / vnz;
         A[row * ld + i] -= sc * vi;
-        if (row < i)
-#pragma unroll 4
-          for (int j = r; j < n; j++) A[row * ld + j] -= sc * A[i * ld + j];
+        if (row < i) {
+          // blocks of 4 as above: the loads before the stores (A's two rows
+          // may alias for the compiler: element by element, every load would
+          // wait for the previous store); the same update per element
+          int j = r;
+          for (; j + 4 <= n; j += 4) {
+            double a[4], c[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) { a[u] = A[row * ld + j + u]; c[u] = A[i * ld + j + u]; }
+#pragma unroll
+            for (int u = 0; u < 4; u++) asm volatile("" : "+v"(a[u]), "+v"(c[u]));
+#pragma unroll
+            for (int u = 0; u < 4; u++) A[row * ld + j + u] = a[u] - sc * c[u];
+          }
+          for (; j < n; j++) A[row * ld + j] -= sc * A[i * ld + j];
+        }
       }
     }
     WSYNC();

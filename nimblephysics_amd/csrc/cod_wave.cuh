@@ -156,14 +156,14 @@ __device__ void codQrRegs(typename Space<kLds>::dptr A, Cod& c, typename Space<k
     COD_PROF(2);
     // slot k is final: R part from the pivot lane, reflector tail below.
     // The pivot lane stores its whole column, unconditionally (a uniform
-    // condition per element had become a branch per element): rows > k are
-    // overwritten by the tail right after (a wave's LDS operations execute
-    // in order), rows >= m go to vb's unused tail (the tail store reads vb
-    // only below m)
+    // condition per element had become a branch per element): the rows it
+    // does not own (> k, or past m) go to one sink, the RZ pass's reflector
+    // heads, which nothing reads before that pass writes them
     if (lane == pl) {
+      const auto sink = sp<kLds>(c.zd);
 #pragma unroll
       for (int i = 0; i < R; i++) {
-        auto dst = i < m ? &A[i * ld + k] : &vb[i];
+        auto dst = i <= k && i < m ? &A[i * ld + k] : sink;
         *dst = a[i];
       }
     }

@@ -1359,7 +1359,12 @@ __device__ bool waveDantzigR(int n, typename Space<kLds>::cdptr Ain, typename Sp
           // together, then the multiply-adds in j order (A symmetric: row j);
           // the last, partial block pads with +0 * -0 terms (acc + -0 is acc
           // bit for bit), so no term is a branch of its own
-          auto block = [&](int j0, bool full) {
+          // (Mc: the register slots holding N rows, a compile-time mask --
+          // the others' sums are never read, so their loads and multiply-adds
+          // are skipped: with two slots, a pivot at row i <= 64 has no N row
+          // in slot 1, one with n_C >= 64 none in slot 0)
+          auto block = [&](auto Mc, int j0, bool full) {
+            constexpr int M = decltype(Mc)::value;
             double dx[8], av[R][8];
             int ro[8];
 #pragma unroll
@@ -1371,31 +1376,45 @@ __device__ bool waveDantzigR(int n, typename Space<kLds>::cdptr Ain, typename Sp
 #pragma unroll
             for (int u = 0; u < 8; u++)
 #pragma unroll
-              for (int s = 0; s < R; s++) av[s][u] = D.Ael(ro[u], colA[s]);
+              for (int s = 0; s < R; s++)
+                if ((M >> s) & 1) av[s][u] = D.Ael(ro[u], colA[s]);
 #pragma unroll
             for (int s = 0; s < R; s++)
 #pragma unroll
-              for (int u = 0; u < 8; u++) asm volatile("" : "+v"(av[s][u]));
+              for (int u = 0; u < 8; u++)
+                if ((M >> s) & 1) asm volatile("" : "+v"(av[s][u]));
             if (!full) {
 #pragma unroll
               for (int u = 0; u < 8; u++) {
                 const bool live = j0 + u < nC;
                 dx[u] = live ? dx[u] : -0.0;
 #pragma unroll
-                for (int s = 0; s < R; s++) av[s][u] = live ? av[s][u] : 0.0;
+                for (int s = 0; s < R; s++)
+                  if ((M >> s) & 1) av[s][u] = live ? av[s][u] : 0.0;
               }
             }
 #pragma unroll
             for (int u = 0; u < 8; u++)
 #pragma unroll
-              for (int s = 0; s < R; s++) acc[s] += av[s][u] * dx[u];
+              for (int s = 0; s < R; s++)
+                if ((M >> s) & 1) acc[s] += av[s][u] * dx[u];
           };
-          int j0 = 0;
+          auto blocks = [&](auto Mc) {
+            int j0 = 0;
+            for (; j0 + 8 <= nC; j0 += 8) block(Mc, j0, true);
+            if (j0 < nC) block(Mc, j0, false);
+          };
 #ifdef LCP_PROFILE
           const long long lpm_ = (long long)__builtin_amdgcn_s_memtime();
 #endif
-          for (; j0 + 8 <= nC; j0 += 8) block(j0, true);
-          if (j0 < nC) block(j0, false);
+          const bool nIn0 = nN > 0 && nC < 64, nIn1 = R > 1 && nN > 0 && nC + nN > 64;
+          if constexpr (R == 1) {
+            if (nIn0) blocks(std::integral_constant<int, 1>{});
+          } else {
+            if (nIn0 && nIn1) blocks(std::integral_constant<int, 3>{});
+            else if (nIn1) blocks(std::integral_constant<int, 2>{});
+            else if (nIn0) blocks(std::integral_constant<int, 1>{});
+          }
 #ifdef LCP_PROFILE
           D.prof[6] += (long long)__builtin_amdgcn_s_memtime() - lpm_;
 #endif

@@ -100,7 +100,7 @@ def test_dantzig_disagreement_fixture_emulated():
         txt += [str(m), wave_emu._fmt(d["A"][k, :m * m]), wave_emu._fmt(d["b"][k, :m]), wave_emu._fmt(d["lo"][k, :m]),
                 wave_emu._fmt(d["hi"][k, :m]), wave_emu._fmt(d["fi"][k, :m], True), wave_emu._fmt(np.zeros(m))]
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0", LCP_EMU_DANTZIG_ONLY="1")
-    r = subprocess.run([exe], input="\n".join(txt), capture_output=True, text=True, timeout=900, env=env)
+    r = subprocess.run([exe], input="\n".join(txt), capture_output=True, text=True, timeout=1800, env=env)
     assert r.returncode == 0, r.stderr[-4000:]
     kinds = {"agree": 0, "ambiguous": 0, "nonunique": 0}
     for k, ln in zip(pick, r.stdout.splitlines()):
@@ -130,7 +130,7 @@ def test_pgs_fast_clamp_matches_reference_chain():
         txt += [str(m), wave_emu._fmt(A), wave_emu._fmt(b), wave_emu._fmt(lo), wave_emu._fmt(hi),
                 wave_emu._fmt(fi, True), wave_emu._fmt(np.zeros(m))]
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")
-    r = subprocess.run([exe], input="\n".join(txt), capture_output=True, text=True, timeout=900, env=env)
+    r = subprocess.run([exe], input="\n".join(txt), capture_output=True, text=True, timeout=1800, env=env)
     assert r.returncode == 0, r.stderr[-4000:]
     out = iter(ln.split() for ln in r.stdout.splitlines())
     for k, (m, A, b, lo, hi, fi) in enumerate(probs):

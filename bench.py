@@ -57,18 +57,24 @@ WORKLOADS = {
 def init_dist(device_type="cuda"):
     """torch.distributed from the env a launcher set (torchrun, or
     launch_ranks below): RCCL ("nccl") on the GPU, gloo for the CPU test
-    path.  Returns (dist or None, rank, world size, local rank)."""
-    ws = int(os.environ.get("WORLD_SIZE", "1"))
-    if ws > 1:
-        import torch.distributed as dist
-        local = int(os.environ.get("LOCAL_RANK", "0"))
-        if device_type == "cuda":
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group("gloo")
-        return dist, dist.get_rank(), ws, local
-    return None, 0, 1, 0
+    path.  A launcher's env (WORLD_SIZE set) always gets a process group,
+    world size 1 included (torchrun --nproc-per-node 1, and the -m gpu test
+    that runs the RCCL gather on the one GPU of a test box); a plain
+    `python bench.py` has none.  Returns (dist or None, rank, world size as
+    the process group reports it, local rank)."""
+    if "WORLD_SIZE" not in os.environ:
+        return None, 0, 1, 0
+    import torch.distributed as dist
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if device_type == "cuda":
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group("gloo")
+    ws = dist.get_world_size()
+    if ws != int(os.environ["WORLD_SIZE"]):
+        raise SystemExit(f"bench: process group has {ws} ranks, WORLD_SIZE={os.environ['WORLD_SIZE']}")
+    return dist, dist.get_rank(), ws, local
 
 
 def _free_port():

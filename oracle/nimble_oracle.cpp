@@ -498,6 +498,14 @@ static double fdAcos(double c) {
   if (c < -0.5) return kFdPi - 2.0 * fdAsinK(std::sqrt((1.0 + c) * 0.5));
   return kFdPio2 - fdAsinK(c);
 }
+// Test switch (oracle_set_fd_libm): evaluate the same integrations with
+// std::sin / cos / acos, as the reference does (Geometry.cpp:539, :720), so a
+// CPU test bounds how far the fixed sequence above sits from libm at the
+// reference's FD steps (tests/test_oracle_pins.py).
+static bool gFdLibm = false;
+static double fdS(double x) { return gFdLibm ? std::sin(x) : fdSin(x); }
+static double fdC(double x) { return gFdLibm ? std::cos(x) : fdCos(x); }
+static double fdA(double x) { return gFdLibm ? std::acos(x) : fdAcos(x); }
 // expMapRot (Geometry.cpp:539) in the reference's order
 static void fdExpMapRot(const double* q, double* R) {
   const double th = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2]);
@@ -508,14 +516,14 @@ static void fdExpMapRot(const double* q, double* R) {
   if (th < 1.0e-3) {
     for (int i = 0; i < 9; i++) R[i] = ((i % 4) == 0 ? 1.0 : 0.0) + K[i] + 0.5 * K2[i];
   } else {
-    const double a = fdSin(th) / th, b = (1.0 - fdCos(th)) / (th * th);
+    const double a = fdS(th) / th, b = (1.0 - fdC(th)) / (th * th);
     for (int i = 0; i < 9; i++) R[i] = ((i % 4) == 0 ? 1.0 : 0.0) + a * K[i] + b * K2[i];
   }
 }
 // logMap (Geometry.cpp:720)
 static void fdLogMap(const double* R, double* o) {
   const double eps = 1e-6;
-  const double th = fdAcos(std::fmax(std::fmin(0.5 * (R[0] + R[4] + R[8] - 1.0), 1.0), -1.0));
+  const double th = fdA(std::fmax(std::fmin(0.5 * (R[0] + R[4] + R[8] - 1.0), 1.0), -1.0));
   if (th > kFdPi - eps) {
     const double delta = 0.5 + 0.125 * (kFdPi - th) * (kFdPi - th);
     const double s0 = th * std::sqrt(1.0 + (R[0] - 1.0) * delta);
@@ -526,7 +534,7 @@ static void fdLogMap(const double* R, double* o) {
     o[2] = R[3] > R[1] ? s2 : -s2;
     return;
   }
-  const double alpha = th > eps ? 0.5 * th / fdSin(th) : 0.5 + (1.0 / 12.0) * th * th;
+  const double alpha = th > eps ? 0.5 * th / fdS(th) : 0.5 + (1.0 / 12.0) * th * th;
   o[0] = alpha * (R[7] - R[5]);
   o[1] = alpha * (R[2] - R[6]);
   o[2] = alpha * (R[3] - R[1]);
@@ -587,3 +595,5 @@ void World::jacobianOfMy(const double* q, const double* y, double* dMy) const {
 }
 
 }  // namespace oracle
+
+extern "C" void oracle_set_fd_libm(int on) { oracle::gFdLibm = on != 0; }

@@ -82,6 +82,8 @@ def lib():
         L.oracle_lcp_cascade.argtypes = [ip, dp, dp, dp, dp, pi, dp, C.c_double, dp]
         L.oracle_classify.argtypes = [ip, dp, dp, dp, dp, pi, dp]
         L.oracle_classify.restype = ip
+        L.oracle_lcp_path.argtypes = [ip, dp, dp, dp, dp, pi, dp, C.c_double, dp, pi]
+        L.oracle_set_fd_libm.argtypes = [ip]
         _lib = L
     return _lib
 
@@ -235,6 +237,13 @@ class OracleWorld:
         return lib().oracle_num_contacts(self.snaps, b)
 
 
+def set_fd_libm(on):
+    """Test switch: the FreeJoint FD blocks' perturbed integrations through
+    std::sin / cos / acos (the reference's, Geometry.cpp:539 / :720) instead
+    of the fixed IEEE sequence the device shares (nimble_oracle.cpp fd*)."""
+    lib().oracle_set_fd_libm(1 if on else 0)
+
+
 def _pi(a):
     return a.ctypes.data_as(C.POINTER(C.c_int))
 
@@ -352,6 +361,39 @@ def classify_ambiguous(A, b, lo, hi, findex, warm, seed, trials=64):
         x0 = guess_solution(Ap, b, findex) if warm is None else warm
         outs.add(classify(Ap, b, lo, hi, findex, x0)[0])
         if len(outs) == 2:
+            return True
+    return False
+
+
+def lcp_path(A, b, lo, hi, findex, warm, fallback_cfm):
+    """The LCP part of the oracle's step on a raw problem, Q from A's entries:
+    the short-circuit classification from `warm` (None: guessSolution), else
+    the fallback cascade, then the final classification.  Returns a hashable
+    outcome (shortCircuit, ignoredFriction, cfm, numClamping, numUpperBound,
+    lcpReduced, per-row mapping) -- the fields `_same_path` compares."""
+    A = _f(A)
+    m = A.shape[0]
+    b, lo, hi, fi = _f(b), _f(lo), _f(hi), _i(findex)
+    x0 = guess_solution(A, b, fi) if warm is None else _f(warm)
+    flags = np.zeros(6)
+    mapping = np.zeros(m, np.int32)
+    lib().oracle_lcp_path(m, _p(A), _p(b), _p(lo), _p(hi), _pi(fi), _p(x0), float(fallback_cfm), _p(flags),
+                          _pi(mapping))
+    return tuple(float(v) for v in flags) + (tuple(int(v) for v in mapping),)
+
+
+def path_ambiguous(A, b, lo, hi, findex, warm, fallback_cfm, seed, trials=64):
+    """True when the whole LCP path (lcp_path: short-circuit, cascade, final
+    classification) takes more than one outcome under 1e-15-relative
+    symmetric perturbations of A: the probe of splits that are neither at the
+    short-circuit nor at Dantzig's outcome (friction removal, final
+    classification)."""
+    rng = np.random.default_rng(seed)
+    outs = {lcp_path(A, b, lo, hi, findex, warm, fallback_cfm)}
+    for _ in range(trials):
+        N = rng.standard_normal(A.shape)
+        outs.add(lcp_path(A * (1 + 1e-15 * (N + N.T) / 2), b, lo, hi, findex, warm, fallback_cfm))
+        if len(outs) >= 2:
             return True
     return False
 

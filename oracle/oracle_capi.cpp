@@ -324,6 +324,16 @@ namespace oracle {
 bool classifyLcp(int m, const double* A, const double* b, const double* lo, const double* hi, const int* fi,
                  double* X);
 }
+namespace oracle {
+void lcpPathFromA(int m, const double* A, const double* b, const double* lo, const double* hi, const int* fi,
+                  const double* warm, double fallbackCfm, double* flags, int* mapping);
+}
+// the whole LCP path (short-circuit, cascade, final classification) on a raw
+// problem (tests: ambiguity probe of classification / friction-removed splits)
+extern "C" void oracle_lcp_path(int m, const double* A, const double* b, const double* lo, const double* hi,
+                                const int* fi, const double* warm, double fallbackCfm, double* flags, int* mapping) {
+  oracle::lcpPathFromA(m, A, b, lo, hi, fi, warm, fallbackCfm, flags, mapping);
+}
 // the short-circuit classification on a raw problem (tests: ambiguity probe)
 extern "C" int oracle_classify(int m, const double* A, const double* b, const double* lo, const double* hi,
                                const int* fi, double* x) {

@@ -1207,6 +1207,54 @@ bool classifyLcp(int m, const double* A, const double* b, const double* lo, cons
   return gm.standardized;
 }
 
+// The LCP part of solveContacts above on a raw problem (tests: the ambiguity
+// probe of path splits that are neither at the short-circuit nor at
+// Dantzig's outcome): the short-circuit classification from the warm start,
+// else BoxedLcpConstraintSolver's fallback cascade from it, then the final
+// classification, with Q from A's entries.  flags = [shortCircuit,
+// ignoredFriction, cfm, numClamping, numUpperBound, lcpReduced]; mapping gets
+// the final per-row classification.
+void lcpPathFromA(int m, const double* A, const double* b, const double* lo, const double* hi, const int* fi,
+                  const double* warm, double fallbackCfm, double* flags, int* mapping) {
+  GradMats gm;
+  gm.w = nullptr;
+  gm.m = m;
+  gm.A.assign(A, A + m * m);
+  gm.B.assign(b, b + m);
+  gm.lo.assign(lo, lo + m);
+  gm.hi.assign(hi, hi + m);
+  gm.fi.assign(fi, fi + m);
+  gm.aColNorms.assign(m, 0.0);
+  for (int j = 0; j < m; j++) {
+    double s = 0;
+    for (int i = 0; i < m; i++) s += A[i * m + j] * A[i * m + j];
+    gm.aColNorms[j] = s;
+  }
+  gm.qFromA = true;
+  std::vector<double> X(warm, warm + m);
+  gm.X = X; gm.cfm = 0.0; gm.ignoreFriction = false;
+  gm.construct();
+  const bool shortCircuit = gm.standardized;
+  bool reduced = false;
+  if (!shortCircuit) {
+    const std::vector<double> w0 = X;  // mX == mXBackup
+    const LcpCascade r = lcpFallbackCascade(gm.A, gm.B, gm.lo, gm.hi, gm.fi, w0, fallbackCfm, X);
+    reduced = r.reduced;
+    std::vector<double> Acfm(A, A + m * m);
+    if (r.cfm != 0.0)
+      for (int i = 0; i < m; i++) Acfm[i * m + i] += r.cfm;
+    gm.X = X; gm.A = Acfm; gm.cfm = r.cfm; gm.ignoreFriction = r.ignoredFriction;
+    gm.construct();
+  }
+  flags[0] = shortCircuit ? 1 : 0;
+  flags[1] = gm.ignoreFriction ? 1 : 0;
+  flags[2] = gm.cfm;
+  flags[3] = gm.nc;
+  flags[4] = gm.nu;
+  flags[5] = reduced ? 1 : 0;
+  for (int j = 0; j < m; j++) mapping[j] = gm.mapping[j];
+}
+
 void buildClampingMatrices(const World& w, const Snapshot& snap, std::vector<double>& Ac, std::vector<double>& Aub,
                            std::vector<double>& AcubE) {
   const int n = w.n, m = snap.numRows, nc = snap.numClamping, nu = snap.numUpperBound;

@@ -110,12 +110,15 @@ def _split_kind(ow, b, sn):
 
 
 def _split_ambiguous(ow, b, kind, warm, seed):
-    """Whether a path split is ambiguous for the reference's algorithm: a
-    Dantzig-outcome split for the reference's own compiled dSolveLCP, a
-    short-circuit split for the restated classification + standardisation
-    (oracle classify, from the step's warm start: `warm`, or guessSolution
-    when the step had no cache), both under 1e-15-relative symmetric
-    perturbations of A; None for the other kinds (not probed: replayed)."""
+    """Whether a path split is ambiguous for the reference's algorithm, under
+    1e-15-relative symmetric perturbations of A: a Dantzig-outcome split for
+    the reference's own compiled dSolveLCP; a short-circuit split for the
+    restated classification + standardisation (oracle classify, from the
+    step's warm start: `warm`, or guessSolution when the step had no cache);
+    a friction-removal or final-classification split for the restated whole
+    LCP path (short-circuit, fallback cascade, final classification:
+    oracle path_ambiguous).  Every kind is probed: a split on a problem whose
+    outcome does not move under the perturbations fails the caller."""
     A, bb, lo, hi, fi = O.lcp_problem(ow, b)
     if kind == "cfm":
         amb = _ref_dantzig_ambiguous(A, bb, lo, hi, fi, seed)
@@ -123,7 +126,7 @@ def _split_ambiguous(ow, b, kind, warm, seed):
         return amb
     if kind == "short-circuit":
         return O.classify_ambiguous(A, bb, lo, hi, fi, warm, seed)
-    return None
+    return O.path_ambiguous(A, bb, lo, hi, fi, warm, ow.desc.fallback_cfm, seed)
 
 
 def _warm_start(cache, b, m):
@@ -184,7 +187,7 @@ def _check_contacts(ow, snap, B, max_diverge=0.03, cache=None, warm_cache=None, 
         if not _same_path(ow, sn, b):
             kind = _split_kind(ow, b, sn)
             amb = _split_ambiguous(ow, b, kind, _warm_start(warm_cache, b, len(mapping)), seed * 100003 + b)
-            assert amb is not False, f"world {b}: LCP path split ({kind}) on a problem that is not ambiguous"
+            assert amb, f"world {b}: LCP path split ({kind}) on a problem that is not ambiguous"
             if kinds is not None:
                 kinds[kind] = kinds.get(kind, 0) + 1
             same[b] = False

@@ -213,10 +213,11 @@ def _rollout_parity(world, name, workload, B, STEPS):
             # a split at Dantzig's outcome (success vs fallback): ambiguous for
             # the reference's own compiled dSolveLCP?  At the gradient short-
             # circuit: for the classification + standardisation from the
-            # step's warm start?  (other kinds: replayed below)
+            # step's warm start?  At the friction removal or the final
+            # classification: for the restated whole LCP path?  (and every
+            # split is replayed below)
             amb = _split_ambiguous(o, i, kind, _warm_start(cache, b, m), seed=1000 * k + b)
-            if amb is not None:
-                row["ref_ambiguous" if amb else "ref_unambiguous"] += 1
+            row["ref_ambiguous" if amb else "ref_unambiguous"] += 1
         row["lcp_rows_mean"] = round(row["lcp_rows_mean"], 3)
         # same path: next state and gradients at 1e-6 per element
         row["next_state_rel_err"] = _rel(got[same], ref[same])

@@ -418,3 +418,24 @@ def test_set_cached_lcp_solution_host_logic():
     # the getter returns a value set since the last step, not the last step's
     w.setCachedLCPSolution(np.array([4.0, 5.0]))
     assert np.array_equal(w.getCachedLCPSolution(1), [4.0, 5.0])
+
+
+def test_init_dist_world_size_one_has_a_process_group():
+    """A launcher's env with WORLD_SIZE=1 (torchrun --nproc-per-node 1, or the
+    -m gpu RCCL test) gets a real process group, and the world size bench
+    reports is the group's; a plain run (no WORLD_SIZE) has none."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); import bench\n"
+            "d, r, ws, loc = bench.init_dist('cpu')\n"
+            "assert d is not None and d.is_initialized() and d.get_world_size() == ws == 1 and r == 0\n"
+            "d.destroy_process_group(); print('PG_OK')\n") % ROOT
+    env = dict(os.environ, RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_free_port()))
+    p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0 and "PG_OK" in p.stdout, p.stderr[-2000:]
+    env.pop("WORLD_SIZE")
+    p = subprocess.run([sys.executable, "-c", "import sys; sys.path.insert(0, %r); import bench; "
+                        "assert bench.init_dist('cpu')[0] is None; print('NO_PG')" % ROOT],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0 and "NO_PG" in p.stdout, p.stderr[-2000:]

@@ -492,3 +492,69 @@ def test_forced_lcp_replay_reproduces_own_path(oracle_built):
     fx2[hit, 0] += 3
     _, bad = O.OracleWorld(w).forward_forced(st, f, fx2, flags)
     assert bad == 1
+
+
+def _jacobians(w, st, f, caches, libm):
+    O.set_fd_libm(libm)
+    try:
+        o = O.OracleWorld(w)
+        _seed_caches(o, caches)
+        o.forward(st, f)
+        return o.jacobians()
+    finally:
+        O.set_fd_libm(False)
+
+
+@pytest.mark.parametrize("kind", ["atlas_broken", "atlas_mesh_broken", "atlas_bench", "atlas_mesh_bench"])
+def test_fd_blocks_fixed_sequence_vs_libm(oracle_built, kind):
+    """The FreeJoint FD blocks (FreeJoint.cpp:965 eps 1e-6, :987 eps 1e-7)
+    that the device and the oracle evaluate with one fixed IEEE sequence
+    (hand-written sin / cos / acos, nimble_oracle.cpp fd*) against the same
+    blocks through libm's std::sin / cos / acos, as the reference evaluates
+    them (Geometry.cpp:539 expMapRot, :720 logMap): at the reference's Atlas
+    broken states (with their LCP caches) and at the bench sampler's states,
+    the full getStateJacobian / d next / d tau differ only at the FD noise
+    level, eps_mach |q| / (2 eps) ~ 1e-9, under the reference's own absolute
+    1e-8 (GradientTestUtils.hpp :1590).  So the restatement of the FD blocks
+    stays pinned to the reference's libm evaluation, not only to itself."""
+    if kind.endswith("_broken"):
+        w, _, st, f, caches = models.broken_states("atlas_mesh" if kind == "atlas_mesh_broken" else "atlas")
+    else:
+        from nimblephysics_amd import workloads
+        w = workloads.atlas_mesh_world(True) if kind == "atlas_mesh_bench" else workloads.atlas_world(True)
+        st, f = workloads.atlas_states(w, 48, 1000)
+        caches = [None] * st.shape[0]
+    J0, F0 = _jacobians(w, st, f, caches, False)
+    J1, F1 = _jacobians(w, st, f, caches, True)
+    dJ, dF = np.abs(J0 - J1), np.abs(F0 - F1)
+    assert dJ.max() <= 1e-8 and dF.max() <= 1e-8, (dJ.max(), dF.max())
+    # per element against the FD noise of each entry's scale
+    n = w.getNumDofs()
+    qmax = np.abs(st[:, :n]).max(axis=1)[:, None, None]
+    assert (dJ <= 1e-8 * np.maximum(1.0, qmax)).all()
+    # the switch really changes the evaluation (two libms' last bits differ)
+    assert dJ.max() > 0
+
+
+def test_lcp_path_reproduces_the_step(oracle_built):
+    """oracle.lcp_path (the ambiguity probe of friction-removal and final-
+    classification path splits in the GPU parity tests) restates the LCP part
+    of the oracle's own step: on unperturbed problems it gives the step's
+    path flags and per-row classification."""
+    from nimblephysics_amd import workloads
+    checked = 0
+    for w in (workloads.atlas_world(True), workloads.atlas_mesh_world(True)):
+        st, f = workloads.atlas_states(w, 32, 1000)
+        o = O.OracleWorld(w)
+        o.forward(st, f)
+        for b in range(st.shape[0]):
+            A, bb, lo, hi, fi = O.lcp_problem(o, b)
+            if len(bb) == 0:
+                continue
+            got = O.lcp_path(A, bb, lo, hi, fi, None, o.desc.fallback_cfm)
+            fl = O.lcp_flags(o, b)
+            mapping, _ = O.lcp_debug(o, b)
+            want = (fl[0], fl[1], fl[2], fl[3], fl[4], fl[6], tuple(int(v) for v in mapping))
+            assert got == want, (b, got[:6], want[:6])
+            checked += 1
+    assert checked > 20

@@ -86,3 +86,46 @@ def test_dantzig_disagreements_on_device():
         kinds[classify(k, m, A, d["b"][k, :m], d["lo"][k, :m], d["hi"][k, :m], d["fi"][k, :m], o[k, 0] > 0,
                        o[k, X_D:X_D + m], d)] += 1
     print(kinds)
+
+
+FIXTURE_WIDE = os.path.join(ROOT, "tests", "golden", "dantzig_wide_disagreements.npz")
+
+
+@pytest.mark.parametrize("packed", [0, 1])
+def test_dantzig_wide_disagreements_on_device(packed, monkeypatch):
+    """The two-rows-per-lane Dantzig of the wide forward kernel (waveDantzigR
+    R = 2, L unpacked or in the packed panels of the wide kernel's LDS stage)
+    on the STL-mesh Atlas' > 64-row LCPs where the device, the oracle and the
+    reference's compiled dSolveLCP do not all give the same raw outcome
+    (tests/golden/dantzig_wide_disagreements.npz: tools/dantzig_reconcile.py
+    classify_wide over 512 problems, profiles/r06_dantzig_wide_reconcile.json:
+    effective outcomes equal on all 512).  Each problem's effective outcome
+    must equal the reference's, or the reference's must flip under 1e-15
+    perturbations."""
+    if not os.path.exists(HARNESS):
+        pytest.fail(f"{HARNESS} missing: __graft_entry__.build() compiles it")
+    monkeypatch.setenv("LCP_WIDE_PACKED", str(packed))
+    d = np.load(FIXTURE_WIDE)
+    P = len(d["n"])
+    assert P > 0
+    nmax = int(round(np.sqrt(d["A"].shape[1])))
+    dev = torch.device("cuda:0")
+    T = {k: torch.tensor(d[k], device=dev) for k in ("A", "b", "lo", "hi")}
+    T["fi"] = torch.tensor(d["fi"].astype(np.int32), device=dev)
+    T["n"] = torch.tensor(d["n"].astype(np.int32), device=dev)
+    assert int(d["n"].max()) <= 112  # the harness record holds x of up to 112 rows
+    out = torch.zeros((P, REC), dtype=torch.float64, device=dev)
+    lib = C.CDLL(HARNESS)
+    rc = lib.lcp_bench_wide_launch(C.c_int(P), C.c_int(nmax), C.c_int(int(d["n"].max())),
+                                   *[C.c_void_p(T[k].data_ptr()) for k in ("n", "A", "b", "lo", "hi", "fi")],
+                                   C.c_void_p(out.data_ptr()), C.c_void_p(torch.cuda.current_stream().cuda_stream))
+    assert rc == 0
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    kinds = {"agree": 0, "ambiguous": 0, "nonunique": 0}
+    for k in range(P):
+        m = int(d["n"][k])
+        A = d["A"][k, :m * m].reshape(m, m)
+        kinds[classify(k, m, A, d["b"][k, :m], d["lo"][k, :m], d["hi"][k, :m], d["fi"][k, :m], o[k, 0] > 0,
+                       o[k, X_D:X_D + m], d)] += 1
+    print(packed, kinds)

@@ -21,6 +21,12 @@ gpurun_out/lcp_out.npy for dbg/lcp_problems.npz):
 
   python tools/dantzig_reconcile.py classify   # summary -> profiles/r04_dantzig_reconcile.json
                                                # fixture -> tests/golden/dantzig_disagreements.npz
+  python tools/dantzig_reconcile.py classify_wide [TAG]
+      # the R = 2 (wide) Dantzig on the STL-mesh Atlas' > 64-row LCPs
+      # (tools/lcp_bench.py gen_wide / run_wide: gpurun_out/lcp_wide_out.npy,
+      # gpurun_out/lcp_wide_out_packed.npy with LCP_WIDE_PACKED=1)
+      #   summary -> profiles/r06_dantzig_wide_reconcile.json
+      #   fixture -> tests/golden/dantzig_wide_disagreements.npz
 
 The fixture keeps every problem on which the device, the oracle and the
 reference do not all give the same effective outcome, with the reference's
@@ -55,13 +61,46 @@ def effective(ok, x, A, b, lo, hi, fi):
     return bool(ok) and bool(O.lcp_valid(A, x, b, hi, lo, fi))
 
 
-def classify():
+def classify(prob=PROB, outs=((None, OUT),), summary=SUMMARY, fixture=FIXTURE, limit=None, source=None):
+    """Per problem: the device's, the oracle's and the reference's raw and
+    effective outcomes; every problem on which they do not all agree (for
+    any of the device runs in `outs`, (label, path) pairs) is kept, with the
+    reference's outcome and its ambiguity."""
     from oracle import oracle as O
-    d = np.load(PROB)
-    g = np.load(OUT)
-    P = len(d["n"])
+    d = np.load(prob)
+    gs = [(lab, np.load(path)) for lab, path in outs]
+    P = len(d["n"]) if limit is None else min(limit, len(d["n"]))
+    out = {"source": source or ("tools/dantzig_reconcile.py classify over dbg/lcp_problems.npz (tools/lcp_bench.py "
+                                "gen: the bench Atlas, 1024 worlds x 3 steps, seed 1000) and the device run "
+                                "gpurun_out/lcp_out.npy"),
+           "effective_outcome": "dSolveLCP success AND LCPUtils::isLCPSolutionValid (what the step keeps)"}
+    keep = set()
+    refs = {}
+    for lab, g in gs:
+        tally, rows = _classify_run(O, d, g, P, refs)
+        out["tally" if lab is None else f"tally_{lab}"] = tally
+        out["kept" if lab is None else f"kept_{lab}"] = rows
+        keep |= {r["problem"] for r in rows}
+        print(lab, json.dumps(tally, indent=1))
+    os.makedirs(os.path.dirname(summary), exist_ok=True)
+    json.dump(out, open(summary, "w"), indent=1)
+    _write_fixture(O, d, sorted(keep), refs, fixture)
+    print(f"{len(keep)} problems kept -> {fixture}")
+
+
+def _ref_outcome(O, d, k, refs):
+    """(raw ok, x, effective, ambiguous-or-None) of the reference's dSolveLCP on problem k (cached)."""
+    if k not in refs:
+        m = int(d["n"][k])
+        A = d["A"][k, :m * m].reshape(m, m)
+        b, lo, hi, fi = d["b"][k, :m], d["lo"][k, :m], d["hi"][k, :m], d["fi"][k, :m]
+        rok, rx = O.ref_dantzig(A, b, lo, hi, fi, True)
+        refs[k] = [bool(rok), rx, effective(rok, rx, A, b, lo, hi, fi), None]
+    return refs[k]
+
+
+def _classify_run(O, d, g, P, refs):
     rows = []
-    keep = []
     tally = {"problems": P, "raw_gpu_vs_oracle_agree": 0, "raw_gpu_vs_ref_agree": 0, "raw_oracle_vs_ref_agree": 0,
              "eff_gpu_vs_ref_agree": 0, "eff_oracle_vs_ref_agree": 0, "eff_gpu_vs_ref_disagree_ambiguous": 0,
              "eff_gpu_vs_ref_disagree_unambiguous": 0, "both_valid_x_max_rel_err": 0.0,
@@ -72,9 +111,9 @@ def classify():
         b, lo, hi, fi = d["b"][k, :m], d["lo"][k, :m], d["hi"][k, :m], d["fi"][k, :m]
         gok, gx = bool(g[k, 0] > 0), g[k, X_D:X_D + m]
         ook, ox = O.dantzig(A, b, lo, hi, fi, True)
-        rok, rx = O.ref_dantzig(A, b, lo, hi, fi, True)
-        ge, oe, re_ = effective(gok, gx, A, b, lo, hi, fi), effective(ook, ox, A, b, lo, hi, fi), \
-            effective(rok, rx, A, b, lo, hi, fi)
+        ref = _ref_outcome(O, d, k, refs)
+        rok, rx, re_ = ref[0], ref[1], ref[2]
+        ge, oe = effective(gok, gx, A, b, lo, hi, fi), effective(ook, ox, A, b, lo, hi, fi)
         tally["raw_gpu_vs_oracle_agree"] += int(gok == ook)
         tally["raw_gpu_vs_ref_agree"] += int(gok == rok)
         tally["raw_oracle_vs_ref_agree"] += int(ook == rok)
@@ -84,7 +123,9 @@ def classify():
         tally["raw_success_invalid_ref"] += int(rok and not re_)
         amb = None
         if not (ge == oe == re_):
-            amb = ref_ambiguous(A, b, lo, hi, fi, seed=k)
+            if ref[3] is None:
+                ref[3] = ref_ambiguous(A, b, lo, hi, fi, seed=k)
+            amb = ref[3]
         if ge != re_:
             tally["eff_gpu_vs_ref_disagree_ambiguous" if amb else "eff_gpu_vs_ref_disagree_unambiguous"] += 1
         xdiff = False
@@ -99,38 +140,56 @@ def classify():
                 res = float(np.abs(A @ (gx - rx)).max() / max(1.0, np.abs(A).max() * np.abs(rx).max()))
                 tally["both_valid_x_differ_null_residual"] = max(tally.get("both_valid_x_differ_null_residual", 0.0), res)
         if not (gok == ook == rok) or not (ge == oe == re_) or xdiff:
-            keep.append(k)
             rows.append({"problem": k, "m": m, "rank": int(np.linalg.matrix_rank(A)), "gpu_ok": gok, "gpu_valid": ge,
                          "oracle_ok": bool(ook), "oracle_valid": oe, "ref_ok": bool(rok), "ref_valid": re_,
                          "ref_ambiguous": amb})
     for key in list(tally):
         if key.endswith("_agree"):
             tally[key + "_frac"] = tally[key] / P
-    out = {"source": "tools/dantzig_reconcile.py classify over dbg/lcp_problems.npz (tools/lcp_bench.py gen: the "
-                     "bench Atlas, 1024 worlds x 3 steps, seed 1000) and the device run gpurun_out/lcp_out.npy",
-           "effective_outcome": "dSolveLCP success AND LCPUtils::isLCPSolutionValid (what the step keeps)",
-           "tally": tally, "kept": rows}
-    os.makedirs(os.path.dirname(SUMMARY), exist_ok=True)
-    json.dump(out, open(SUMMARY, "w"), indent=1)
-    # the fixture: inputs of the kept problems and the reference's outcome
+    return tally, rows
+
+
+def _write_fixture(O, d, keep, refs, fixture):
+    """The fixture: inputs of the kept problems (A cut to the largest kept
+    row count) and the reference's outcome."""
     ks = np.array(keep, dtype=np.int64)
     nmax = int(round(np.sqrt(d["A"].shape[1])))
-    ref_x = np.zeros((len(ks), nmax))
+    nk = int(d["n"][ks].max()) if len(ks) else 1
+    A = np.zeros((len(ks), nk * nk))
+    ref_x = np.zeros((len(ks), nk))
+    amb = np.zeros(len(ks), dtype=np.int32)
     for i, k in enumerate(ks):
         m = int(d["n"][k])
-        ref_x[i, :m] = O.ref_dantzig(d["A"][k, :m * m].reshape(m, m), d["b"][k, :m], d["lo"][k, :m],
-                                     d["hi"][k, :m], d["fi"][k, :m], True)[1]
-    np.savez_compressed(FIXTURE, problem=ks, n=d["n"][ks], A=d["A"][ks], b=d["b"][ks], lo=d["lo"][ks],
-                        hi=d["hi"][ks], fi=d["fi"][ks], ref_x=ref_x,
-                        ref_ok=np.array([r["ref_ok"] for r in rows], dtype=np.int32),
-                        ref_valid=np.array([r["ref_valid"] for r in rows], dtype=np.int32),
-                        ref_ambiguous=np.array([-1 if r["ref_ambiguous"] is None else int(r["ref_ambiguous"])
-                                                for r in rows], dtype=np.int32))
-    print(json.dumps(tally, indent=1))
-    print(f"{len(keep)} problems kept -> {FIXTURE}")
+        A[i, :m * m] = d["A"][k, :m * m]
+        r = _ref_outcome(O, d, k, refs)
+        ref_x[i, :m] = r[1]
+        amb[i] = -1 if r[3] is None else int(r[3])
+    vec = {key: d[key][ks][:, :nk] for key in ("b", "lo", "hi", "fi")}
+    np.savez_compressed(fixture, problem=ks, n=d["n"][ks], A=A, ref_x=ref_x, **vec,
+                        ref_ok=np.array([int(refs[k][0]) for k in ks], dtype=np.int32),
+                        ref_valid=np.array([int(refs[k][2]) for k in ks], dtype=np.int32),
+                        ref_ambiguous=amb, nmax_source=np.int32(nmax))
+
+
+PROB_WIDE = os.path.join(ROOT, "dbg", "lcp_wide.npz")
+SUMMARY_WIDE = os.path.join(ROOT, "profiles", "r06_dantzig_wide_reconcile.json")
+FIXTURE_WIDE = os.path.join(ROOT, "tests", "golden", "dantzig_wide_disagreements.npz")
+
+
+def classify_wide(tag="r06"):
+    outs = [("stage_unpacked", os.path.join(ROOT, "gpurun_out", "lcp_wide_out.npy")),
+            ("stage_packed", os.path.join(ROOT, "gpurun_out", "lcp_wide_out_packed.npy"))]
+    outs = [(lab, p) for lab, p in outs if os.path.exists(p)]
+    classify(PROB_WIDE, outs, SUMMARY_WIDE.replace("r06", tag), FIXTURE_WIDE, limit=512,
+             source="tools/dantzig_reconcile.py classify_wide over the first 512 problems of dbg/lcp_wide.npz "
+                    "(tools/lcp_bench.py gen_wide: the STL-mesh Atlas' LCPs of more than 64 rows, 1024 worlds x 2 "
+                    "steps, seed 1000) and the device runs of the R = 2 Dantzig (tools/lcp_bench.hip "
+                    "lcp_bench_wide_kernel, L unpacked / in the wide forward kernel's packed panels)")
 
 
 if __name__ == "__main__":
     cmd = sys.argv[1] if len(sys.argv) > 1 else "classify"
     if cmd == "classify":
         classify()
+    elif cmd == "classify_wide":
+        classify_wide(*sys.argv[2:3])

@@ -84,7 +84,11 @@ def run(reps=3):
         m = n[k]
         e = np.abs(o[k, 16:16 + m] - d["xD"][k, :m]).max() / max(1.0, np.abs(d["xD"][k, :m]).max())
         err = max(err, e)
-    print(f"{P} problems: dantzig success agrees with oracle on {agree.mean():.4f}, max rel x err {err:.2e}")
+    # (the RAW success flags: not the step's outcome, which is success AND
+    # isLCPSolutionValid -- tools/dantzig_reconcile.py classify compares that
+    # with the reference's compiled dSolveLCP)
+    print(f"{P} problems: raw dantzig flag same as the oracle's on {agree.mean():.4f} (effective outcomes: "
+          f"tools/dantzig_reconcile.py classify), max rel x err where both raw-succeed {err:.2e}")
     # regression check against a previous GPU run (dbg/lcp_baseline.npz, copied
     # from gpurun_out/lcp_out.npz): solver outputs should be unchanged
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
@@ -161,14 +165,16 @@ def run_wide(limit=512):
     o = out.cpu().numpy()
     names = ["swap", "solveL1", "solveL1T", "ldltRemove", "w_i", "pivot body", "(matvec)", "(transfers)"]
     piv = np.maximum(o[:, 4], 1)
-    print(f"{P} wide problems: ok agrees with oracle {np.mean((o[:, 0] > 0) == (d['okD'][:P] > 0)):.3f}; "
+    print(f"{P} wide problems (raw flag same as the oracle's {np.mean((o[:, 0] > 0) == (d['okD'][:P] > 0)):.3f}; "
+          "effective outcomes vs the reference: tools/dantzig_reconcile.py classify_wide); "
           f"clocks mean {o[:, 1].mean():.0f} max {o[:, 1].max():.0f}; pivots mean {o[:, 4].mean():.1f} max {o[:, 4].max():.0f}; "
           f"clocks per pivot mean {np.mean(o[:, 1] / piv):.0f}")
     worst = np.argsort(-o[:, 1])[:5]
     for k in worst:
         print(f"  problem {k} n={d['n'][k]} clocks {o[k, 1]:.0f} pivots {o[k, 4]:.0f} | "
               + " ".join(f"{nm}={int(v)}" for nm, v in zip(names, o[k, 8:16])))
-    np.save(os.path.join(ROOT, "gpurun_out", "lcp_wide_out.npy"), o)
+    packed = os.environ.get("LCP_WIDE_PACKED", "0") not in ("", "0")
+    np.save(os.path.join(ROOT, "gpurun_out", "lcp_wide_out_packed.npy" if packed else "lcp_wide_out.npy"), o)
     base = os.path.join(ROOT, "dbg", "lcp_wide_baseline.npy")
     if os.path.exists(base):
         ob = np.load(base)[:P]

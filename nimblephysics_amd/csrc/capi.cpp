@@ -224,6 +224,20 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
   if (const char* e = getenv("NIMBLE_AMD_HELPER_PRIO")) m.helperPrio = atoi(e) & 3;
   m.pinvMfma = 1;
   if (const char* e = getenv("NIMBLE_AMD_PINV_MFMA")) m.pinvMfma = atoi(e) != 0 ? 1 : 0;
+  // NIMBLE_AMD_GUARD_TEST="sites:stride:offset" (tests only): force the
+  // deadlock guard to expire at the wait sites `sites` (contact.cuh GW_*
+  // mask) in the worlds with index % stride == offset
+  m.guardSites = 0;
+  m.guardStride = 1;
+  m.guardOffset = 0;
+  if (const char* e = getenv("NIMBLE_AMD_GUARD_TEST")) {
+    int sites = 0, stride = 1, offset = 0;
+    if (sscanf(e, "%d:%d:%d", &sites, &stride, &offset) >= 1 && stride > 0 && offset >= 0 && offset < stride) {
+      m.guardSites = sites;
+      m.guardStride = stride;
+      m.guardOffset = offset;
+    }
+  }
   m.numPairs = 0;
   m.pairChunk = 0;
   for (int i = 0; i < m.ns; i++)

@@ -467,24 +467,57 @@ __device__ __forceinline__ int helperState(double* ct) {
 // never a slow but live partner) gives up instead of hanging the device or
 // trapping: it raises the world's protocol flag (helperFlags(ct)[3], set
 // into the snapshot status as ST_PROTOCOL by wave 0, a status that makes the
-// step raise) and the waiting wave goes on alone -- wave 0 runs the rest of
-// the cascade serially, the helper leaves -- so every wave reaches its exit
+// step raise).  A wait also gives up as soon as the partner has raised the
+// flag, so one expiry ends every wait of the world at once.  After a failure
+// neither wave relies on the other: wave 0 abandons the world's contact step
+// without touching anything the helper may still write (protocolAbort: the
+// contact header and list, the pool and the board's vectors stay the
+// helper's), the helper leaves at its next wait, every wave reaches its exit
 // and the launch drains.  The clock is read once per 64 polls.
 constexpr long long kSpinTicks = 100000000ll;
 __device__ __forceinline__ long long spinClock() { return (long long)__builtin_amdgcn_s_memrealtime(); }
 __device__ __forceinline__ bool spinExpired(long long t0, int it) {
   return (it & 63) == 63 && spinClock() - t0 > kSpinTicks;
 }
-__device__ __forceinline__ void protocolFail(double* ct) { helperFlags(ct)[3] = 1; }
-__device__ __forceinline__ bool protocolFailed(double* ct) { return uni(helperFlags(ct)[3]) != 0; }
-// spin with s_sleep until pred(state); -1 when the guard expired
+// (the flag is polled inside the waits while the other wave may raise it:
+// atomic accesses, so that the poll is re-read every time and, under the
+// host emulation, lane 0's observation is the whole wave's)
+__device__ __forceinline__ void protocolFail(double* ct) {
+  __hip_atomic_store(helperFlags(ct) + 3, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ bool protocolFailed(double* ct) {
+  return uni(__hip_atomic_load(helperFlags(ct) + 3, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != 0;
+}
+// The wait sites, for the guard's test switch: NIMBLE_AMD_GUARD_TEST
+// (capi.cpp, tests only) puts a mask of sites into helperFlags(ct)[2] for the
+// worlds it targets, and a wait at a masked site expires at once -- a partner
+// that is late at exactly that point -- so every failure path runs on purpose
+// (tests/test_gpu_guard.py, tests/test_wave_emu.py).  0 in every other run.
+#define GW_HELPER_GO 1      // helper: wave 0's CS_GO (body transforms final; one-row kernel)
+#define GW_COLLIDE_DONE 2   // wave 0: the helper's CS_DONE (contacts detected; one-row kernel)
+#define GW_MERGED 4         // wave 0: the helper out of the pool before a reduced Dantzig (on chip)
+#define GW_BOARD 8          // wave 0: the task board's answer (Dantzig / PGS fallback / frictionless)
+#define GW_NAN 16           // wave 0: the helper out of the pool before the fallbacks (NaN answer)
+#define GW_COLLECT 32       // wave 0: the helper out of the pool before construct 2
+#define GW_HELPER_TASK 64   // helper: wave 0's TASK or SKIP
+#define GW_HELPER_WARM 128  // helper: the final warm start for the PGS fallback
+#define GW_HELPER_IDLE 256  // helper: wave 0 took its DONE
+#define GW_RETIRE 512       // wave 0: the helper's DONE at the world's end
+#define GW_ONE_ROW_ONLY 1024  // (modifier) the sites in the one-row kernel only, not in the wide kernel
+__device__ __forceinline__ bool guardForced(double* ct, int site) { return (uni(helperFlags(ct)[2]) & site) != 0; }
+// spin with s_sleep until pred(state); -1 when the guard expired (or was
+// forced at `site`, or the partner failed)
 template <class Pred>
-__device__ __forceinline__ int helperWait(double* ct, Pred pred) {
+__device__ __forceinline__ int helperWait(double* ct, Pred pred, int site) {
+  if (guardForced(ct, site)) {
+    protocolFail(ct);
+    return -1;
+  }
   const long long t0 = spinClock();
   for (int it = 0;; it++) {
     const int st = helperState(ct);
     if (pred(st)) return st;
-    if (spinExpired(t0, it)) {
+    if (protocolFailed(ct) || spinExpired(t0, it)) {
       protocolFail(ct);
       return -1;
     }
@@ -539,11 +572,15 @@ __device__ __forceinline__ void collidePost(double* ct, int state, int lane) {
   if (lane == 0) __hip_atomic_store(collideFlag(ct), state, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 // false when the deadlock guard expired (see helperWait)
-__device__ __forceinline__ bool collideWait(double* ct, int want) {
+__device__ __forceinline__ bool collideWait(double* ct, int want, int site) {
+  if (guardForced(ct, site)) {
+    protocolFail(ct);
+    return false;
+  }
   const long long t0 = spinClock();
   for (int it = 0;; it++) {
     if (uni(__hip_atomic_load(collideFlag(ct), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == want) return true;
-    if (spinExpired(t0, it)) {
+    if (protocolFailed(ct) || spinExpired(t0, it)) {
       protocolFail(ct);
       return false;
     }
@@ -576,6 +613,20 @@ __device__ __forceinline__ int* deferEntry(double* snapBase, int snapDoubles, in
 #define ST_DEFERRED 32          // (internal) the world's LCP has more rows than the one-row-per-lane
                                 // kernel takes: the two-rows-per-lane kernel steps it
 #define ST_PROTOCOL 64          // a wait between the world's two waves hit the deadlock guard (helperWait)
+
+// wave 0 after a protocol failure (see helperWait): the world's contact step
+// is abandoned without reading or writing anything the helper may still
+// touch -- the snapshot says no contacts and no rows (the backward and the
+// Jacobians see a contact-free step), the warm start is dropped, the status
+// raises (ST_PROTOCOL) and the velocity stays the unconstrained v1
+__device__ __forceinline__ void protocolAbort(double* snap, double* cache, int lane) {
+  if (lane == 0) {
+    for (int i = 0; i < SN_DEFER; i++) snap[i] = 0.0;
+    snap[SN_STATUS] = ST_PROTOCOL;
+    cache[0] = -1.0;
+  }
+  WSYNC();
+}
 
 // row record fields
 #define RR_CONTACT 0
@@ -1884,17 +1935,25 @@ __device__ __forceinline__ bool contactStage(const ModelDev& md, double* s, cons
     // which starts there, overwrites them)
     // (only the header fields of the step, not the helper / collision flags
     // or the board, which this kernel's helper is already polling)
+    // (a protocol failure of the one-row kernel's turn, flagged in the
+    // snapshot status after the hand-off, stays in the world's status)
     const int nk = uni((int)overflowWs[H_NCON]);
-    if (lane < H_HELPER) ct[lane] = overflowWs[lane];
+    if (lane < H_HELPER) {
+      double v = overflowWs[lane];
+      if (lane == H_STATUS) v = (double)((int)v | ((int)snap[SN_STATUS] & ST_PROTOCOL));
+      ct[lane] = v;
+    }
     for (int t = lane; t < nk * CREC; t += WAVE) ct[CT_CONTACTS + t] = overflowWs[CT_CONTACTS + t];
     WSYNC();
   } else if (collided) {
     // the helper wave ran the collision detection during the dynamics (the
-    // deadlock guard expired: this wave detects them itself)
-    if (collideWait(ct, CS_DONE)) {
+    // deadlock guard expired: the helper may still be writing the contacts,
+    // the world's contact step is abandoned)
+    if (collideWait(ct, CS_DONE, GW_COLLIDE_DONE)) {
       collidePost(ct, CS_IDLE, lane);
     } else {
-      collideWorld(md, s, L, lane, snap + snEdge(n));
+      protocolAbort(snap, cache, lane);
+      return false;
     }
   } else {
 #ifdef NIMBLE_STAGE_TIMING
@@ -2233,7 +2292,11 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
       // (on chip the helper sees the same merge and solves nothing: wait
       // until it is out of the pool; the wide kernel's helper solves the
       // reduced problem on the board below)
-      if (tasked) helperWait(ct, [](int v) { return v == HS_DONE; });
+      if (tasked && helperWait(ct, [](int v) { return v == HS_DONE; }, GW_MERGED) < 0) {
+        stopAll();
+        protocolAbort(snap, cache, lane);
+        return;
+      }
       double br[R], lr[R], hr[R], xr[R];
       int fr[R], act[R];
 #pragma unroll
@@ -2249,9 +2312,9 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
       // then the frictionless PGS, until the reference's order decides:
       // Dantzig's answer if it succeeds, else the PGS fallback's, else the
       // frictionless one
-      bool expired = false;
+      bool expired = guardForced(ct, GW_BOARD);
       const long long t0 = spinClock();
-      for (int it = 0;; it++) {
+      for (int it = 0; !expired; it++) {
         const int d = boardGet(ct, BD_D);
         if (d == 1) break;
         const int pst = boardGet(ct, BD_P);
@@ -2292,27 +2355,26 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
 #endif
           continue;
         }
-        if (spinExpired(t0, it)) {
+        if (protocolFailed(ct) || spinExpired(t0, it)) {
           expired = true;
           break;
         }
         __builtin_amdgcn_s_sleep(1);
       }
       if (expired) {
-        // the deadlock guard: the helper is gone; the cascade goes on here,
-        // serially (Dantzig now, the fallbacks below)
+        // the deadlock guard: the helper may still be in the pool (its
+        // Dantzig factor, the board's vectors); the world's contact step is
+        // abandoned
         protocolFail(ct);
         stopAll();
-        boardSrc = -1;
-        ok = waveDantzigR<kLds, R>(m, spc<kLds>(P.A), sp<kLds>(P.M2), sp<kLds>(P.scr), xd, bR, loR, hiR, fiR, lane,
-                                   nullptr, nullptr, tallyOf(ct));
-      } else {
-        // Dantzig's answer (checked valid by the helper)
-        ok = boardSrc < 0;
-        validated = true;
-#pragma unroll
-        for (int q = 0; q < R; q++) xd[q] = ok && rowAt(q, lane) < m ? P.xh[rowAt(q, lane)] : 0.0;
+        protocolAbort(snap, cache, lane);
+        return;
       }
+      // Dantzig's answer (checked valid by the helper)
+      ok = boardSrc < 0;
+      validated = true;
+#pragma unroll
+      for (int q = 0; q < R; q++) xd[q] = ok && rowAt(q, lane) < m ? P.xh[rowAt(q, lane)] : 0.0;
     } else {
       // off-chip pools: the LDL^T factor in the launch's LDS stage when it
       // fits (every pivot's triangular solves and its row / column shifts
@@ -2382,7 +2444,10 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
         // a NaN: the helper has been stopped; wait until it is out of the pool)
         if (tasked) {
           stopAll();
-          helperWait(ct, [](int v) { return v == HS_DONE; });
+          if (helperWait(ct, [](int v) { return v == HS_DONE; }, GW_NAN) < 0) {
+            protocolAbort(snap, cache, lane);
+            return;
+          }
         }
         cf = md.fallbackCfm;
         if (lane == 0) ct[H_CODOK] = 0;
@@ -2433,7 +2498,10 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   // precompute overwrite it (M1, M2, A); the whole stage is wave 0's again
   if (tasked) {
     stopAll();
-    helperWait(ct, [](int v) { return v == HS_DONE; });
+    if (helperWait(ct, [](int v) { return v == HS_DONE; }, GW_COLLECT) < 0) {
+      protocolAbort(snap, cache, lane);
+      return;
+    }
     stage = stageAll;
     stageCap = stageCapAll;
   }
@@ -2642,7 +2710,7 @@ __device__ __forceinline__ void helperTask(const ModelDev& md, double* ct, const
     }
     if (!pOpen) break;
     // only the PGS fallback is open, waiting for the warm start
-    if (spinExpired(t0, it)) {
+    if (guardForced(ct, GW_HELPER_WARM) || protocolFailed(ct) || spinExpired(t0, it)) {
       protocolFail(ct);
       break;
     }
@@ -2658,7 +2726,7 @@ __device__ void helperWave(const ModelDev& md, double* s, const Layout& L, int l
   (void)g_stamp;
   s = lds<true>(s);
   double* ct = s + L.ct;
-  const int st = helperWait(ct, [](int v) { return v == HS_TASK || v == HS_SKIP; });
+  const int st = helperWait(ct, [](int v) { return v == HS_TASK || v == HS_SKIP; }, GW_HELPER_TASK);
   if (st < 0) return;  // (the deadlock guard expired: wave 0 goes on alone)
   if (st == HS_TASK) {
     // the cascade's Dantzig is on the world's critical path: the helper
@@ -2681,7 +2749,7 @@ __device__ void helperWave(const ModelDev& md, double* s, const Layout& L, int l
   }
   __builtin_amdgcn_s_setprio(0);
   helperPost(ct, HS_DONE, lane);
-  helperWait(ct, [](int v) { return v != HS_DONE; });
+  helperWait(ct, [](int v) { return v != HS_DONE; }, GW_HELPER_IDLE);
 }
 
 // wave 0's end of a world's protocol: post SKIP if no task went out, collect
@@ -2690,7 +2758,7 @@ __device__ void helperWave(const ModelDev& md, double* s, const Layout& L, int l
 __device__ __forceinline__ void helperRetire(double* s, const Layout& L, int lane) {
   double* ct = lds<true>(s) + L.ct;
   if (helperState(ct) == HS_IDLE) helperPost(ct, HS_SKIP, lane);
-  helperWait(ct, [](int v) { return v == HS_DONE; });
+  helperWait(ct, [](int v) { return v == HS_DONE; }, GW_RETIRE);
   helperPost(ct, HS_IDLE, lane);
 }
 

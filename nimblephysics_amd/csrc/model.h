@@ -75,6 +75,11 @@ struct ModelDev {
   // (contact.cuh pinvColumnsMfma) when the factor has full rank; 0: the
   // per-column solves (NIMBLE_AMD_PINV_MFMA=0, measurements)
   int pinvMfma;
+  // the deadlock guard's test switch (contact.cuh GW_*): the waits at the
+  // sites in guardSites expire at once in the worlds env with env %
+  // guardStride == guardOffset (NIMBLE_AMD_GUARD_TEST="sites:stride:offset",
+  // tests only; guardSites 0 in every other run)
+  int guardSites, guardStride, guardOffset;
   // kept-contact capacity of the contact stage (<= NIMBLE_MAX_CONTACTS)
   int maxContacts;
   // candidate pairs (i < j) after BodyNodeCollisionFilter, in detector order

@@ -317,7 +317,11 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
   if (helperOn) {
     if (threadIdx.x == 0) {
       int* hf = reinterpret_cast<int*>(s + L.ct + H_HELPER);
-      hf[0] = HS_IDLE; hf[1] = 0; hf[2] = 0; hf[3] = 0;
+      // hf[2]: the deadlock guard's forced-expiry sites for this world (the
+      // tests' NIMBLE_AMD_GUARD_TEST; 0 otherwise)
+      const int gs = md.guardSites;
+      hf[0] = HS_IDLE; hf[1] = 0; hf[3] = 0;
+      hf[2] = (gs != 0 && (R == 1 || !(gs & GW_ONE_ROW_ONLY)) && env % md.guardStride == md.guardOffset) ? gs : 0;
       *collideFlag(s + L.ct) = CS_IDLE;
     }
     __syncthreads();  // the one barrier both waves take: flags initialised
@@ -337,7 +341,7 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
 #endif
         if (R == 1) {
           // (the deadlock guard expired: wave 0 detects the contacts itself)
-          if (collideWait(ct, CS_GO)) {
+          if (collideWait(ct, CS_GO, GW_HELPER_GO)) {
 #ifdef NIMBLE_STAGE_TIMING
             collideWorld<true>(md, lds<true>(s), L, lane, snapshot + (size_t)env * snapDoubles + snEdge(n),
                                snapshot + (size_t)env * snapDoubles + snStamps(n));

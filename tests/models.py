@@ -8,10 +8,11 @@ from nimblephysics_amd.workloads import (atlas_world, cartpole_world, half_cheet
 from nimblephysics_amd.workloads import _fk_world  # noqa: F401
 
 
-def box_world(size=(0.4, 0.3, 0.2), friction=1.0, mass=1.0):
+def box_world(size=(0.4, 0.3, 0.2), friction=1.0, mass=1.0, ground=True):
     """A free box over a static ground box (top face at y = 0) -- the small
     contact world the reference's own LCP / gradient tests use
-    (unittests/comprehensive/test_Contacts.cpp style)."""
+    (unittests/comprehensive/test_Contacts.cpp style); without the ground
+    with ground=False (the contact-free step of the same box)."""
     from nimblephysics_amd import dynamics as D
     w = nimble.World()
     w.setGravity([0, -9.81, 0])
@@ -24,6 +25,8 @@ def box_world(size=(0.4, 0.3, 0.2), friction=1.0, mass=1.0):
     b.createShapeNode(D.BoxShape(list(size)), collision=True)
     b.setFrictionCoeff(friction)
     w.addSkeleton(box)
+    if not ground:
+        return w
     ground = D.Skeleton("ground")
     gj, gb = ground.createWeldJointAndBodyNodePair()
     T = np.eye(4)

@@ -294,3 +294,55 @@ def test_bench_atlas_lds_fits_four_worlds_per_cu():
     fwd, bwd = wave_emu.lds_bytes(models.atlas_world(True))
     assert fwd <= 40 * 1024, fwd
     assert bwd <= 40 * 1024, bwd
+
+
+# contact.cuh GW_* wait sites, and what the forced expiry does to the world:
+# "abort" -- wave 0 abandons the contact step (snapshot: no contacts, no rows;
+# the contact-free step), "complete" -- the step is the oracle's but flagged,
+# "either" -- which one depends on where wave 0 is when the helper gives up
+GUARD_SITES = {"helper_go": (1, "abort"), "collide_done": (2, "abort"), "board": (8, "abort"),
+               "collect": (32, "abort"), "helper_task": (64, "abort"), "helper_idle": (256, "either"),
+               "retire": (512, "complete")}
+
+
+@pytest.mark.parametrize("site", sorted(GUARD_SITES))
+def test_guard_forced_expiry_emulated(site):
+    """The deadlock guard's failure paths, run on purpose (NIMBLE_AMD_GUARD_TEST:
+    the wait at one site expires at once in the targeted worlds, contact.cuh
+    GW_*): four box-on-ground worlds at rest on the PGS fallback, the
+    frictionless PGS, the short-circuit and Dantzig, worlds 1 and 3 (the
+    frictionless PGS and Dantzig, both with the helper on the task board)
+    targeted.  The launch drains (the emulated waves all reach their exits,
+    under ASan); exactly the targeted worlds carry NIMBLE_STATUS_PROTOCOL; a
+    targeted world either abandons its contact step (no contacts and rows in
+    the snapshot, the contact-free step -- nothing the helper may still write
+    is read) or, for a late failure, completes it as the oracle does; every
+    other world equals the oracle."""
+    from nimblephysics_amd import _native
+    bit, expect = GUARD_SITES[site]
+    world = models.box_world()
+    st, f = models.box_states("rest", 8, seed=8)
+    st, f = st[:4], f[:4]
+    ow = O.OracleWorld(world)
+    ref = ow.forward(st, f)
+    assert [O.lcp_flags(ow, b)[0] for b in range(4)] == [0, 0, 1, 0]  # (P, F, C, D)
+    g = np.random.default_rng(3).standard_normal(st.shape)
+    rgs, rgf = ow.backward(g)
+    free = O.OracleWorld(models.box_world(ground=False)).forward(st, f)
+    nxt, gs, gf, head = wave_emu.step(world, st, f, g, {"NIMBLE_AMD_GUARD_TEST": f"{bit}:2:1"}, timeout=600)
+    for i in range(4):
+        status = int(head[i, 5])
+        if i % 2 == 0:
+            assert not status & _native.ST_PROTOCOL, (site, i, status)
+            assert np.abs(nxt[i] - ref[i]).max() <= 1e-12, (site, i)
+            assert np.abs(gs[i] - rgs[i]).max() <= 1e-9 * np.abs(rgs[i]).max(), (site, i)
+            continue
+        assert status & _native.ST_PROTOCOL, (site, i, status)
+        aborted = head[i, 0] == 0 and head[i, 1] == 0
+        assert expect == "either" or aborted == (expect == "abort"), (site, i, head[i, :8])
+        if aborted:
+            assert status == _native.ST_PROTOCOL and not head[i, 2:5].any(), (site, i, head[i, :8])
+            assert np.abs(nxt[i] - free[i]).max() <= 1e-12, (site, i)
+        else:
+            assert np.abs(nxt[i] - ref[i]).max() <= 1e-12, (site, i)
+        assert np.isfinite(gs[i]).all() and np.isfinite(gf[i]).all()

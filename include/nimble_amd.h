@@ -33,9 +33,14 @@ enum nimble_joint_type {
   NIMBLE_JOINT_WELD = 0,      /* dart/dynamics/WeldJoint.hpp      0 dof */
   NIMBLE_JOINT_REVOLUTE = 1,  /* dart/dynamics/RevoluteJoint.cpp  1 dof */
   NIMBLE_JOINT_PRISMATIC = 2, /* dart/dynamics/PrismaticJoint.cpp 1 dof */
-  NIMBLE_JOINT_FREE = 3       /* dart/dynamics/FreeJoint.cpp      6 dof
+  NIMBLE_JOINT_FREE = 3,      /* dart/dynamics/FreeJoint.cpp      6 dof
                                  (built with DART_USE_IDENTITY_JACOBIAN,
                                  dart/CMakeLists.txt:184) */
+  NIMBLE_JOINT_BALL = 4,      /* dart/dynamics/BallJoint.cpp      3 dof: exponential
+                                 coordinates, identity Jacobian (as FREE's
+                                 rotational part) */
+  NIMBLE_JOINT_TRANSLATIONAL = 5 /* dart/dynamics/TranslationalJoint.cpp 3 dof
+                                 (R3 space: q is the joint frame's offset) */
 };
 
 /* Collision shape types (dart/collision/dart/DARTCollide.cpp:5030 collide()). */

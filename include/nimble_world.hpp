@@ -206,6 +206,18 @@ class FreeJoint : public Joint {
   using Properties = Joint::Properties;
   FreeJoint(Skeleton* s, const Properties& p) : Joint(s, NIMBLE_JOINT_FREE, 6, p) {}
 };
+/* BallJoint (BallJoint.cpp: exponential coordinates, identity Jacobian) and
+ * TranslationalJoint (TranslationalJoint.cpp: R3 offset), 3 dofs each */
+class BallJoint : public Joint {
+ public:
+  using Properties = Joint::Properties;
+  BallJoint(Skeleton* s, const Properties& p) : Joint(s, NIMBLE_JOINT_BALL, 3, p) {}
+};
+class TranslationalJoint : public Joint {
+ public:
+  using Properties = Joint::Properties;
+  TranslationalJoint(Skeleton* s, const Properties& p) : Joint(s, NIMBLE_JOINT_TRANSLATIONAL, 3, p) {}
+};
 /* RevoluteJoint / PrismaticJoint::setAxis normalise the axis */
 class RevoluteJoint : public Joint {
  public:

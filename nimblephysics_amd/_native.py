@@ -304,7 +304,7 @@ def flop_estimate(world, rows: float = 0.0, clamping: float = 0.0) -> dict:
     nb, n = int(d["num_bodies"]), int(d["num_dofs"])
     parent = list(d["parent"])
     jt = list(d["joint_type"])
-    ndof = [0 if t == 0 else (6 if t == 3 else 1) for t in jt]
+    ndof = [{0: 0, 1: 1, 2: 1, 3: 6, 4: 3, 5: 3}[int(t)] for t in jt]
     anc = []
     for b in range(nb):
         s = {b}

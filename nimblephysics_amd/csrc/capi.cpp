@@ -151,7 +151,8 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
     m.parent[b] = p;
     m.jtype[b] = d->joint_type[b];
     m.dof0[b] = d->dof_offset[b];
-    m.ndof[b] = m.jtype[b] == NIMBLE_JOINT_WELD ? 0 : (m.jtype[b] == NIMBLE_JOINT_FREE ? 6 : 1);
+    m.ndof[b] = jointDofs(m.jtype[b]);
+    if (m.ndof[b] < 0) { delete w; return fail(NIMBLE_ERR_INVALID, "unknown joint type"); }
     m.depth[b] = p >= 0 ? m.depth[p] + 1 : 0;
     if (m.depth[b] > m.maxDepth) m.maxDepth = m.depth[b];
     m.anc[b] = (p >= 0 ? m.anc[p] : 0ull) | (1ull << b);
@@ -169,8 +170,10 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
     m.restitution[b] = d->restitution[b];
     for (int k = 0; k < m.ndof[b]; k++) m.dofBody[m.dof0[b] + k] = b;
     dofCount += m.ndof[b];
-    if (m.jtype[b] == NIMBLE_JOINT_FREE) {
-      if (m.numFree >= 8) { delete w; return fail(NIMBLE_ERR_UNSUPPORTED, "more than 8 free joints"); }
+    // the joints whose posPos / velPos blocks are central differences of the
+    // position integration (FreeJoint.cpp:965 / :987, BallJoint.cpp:368 / :390)
+    if (m.jtype[b] == NIMBLE_JOINT_FREE || m.jtype[b] == NIMBLE_JOINT_BALL) {
+      if (m.numFree >= 8) { delete w; return fail(NIMBLE_ERR_UNSUPPORTED, "more than 8 free / ball joints"); }
       m.freeBody[m.numFree++] = b;
     }
   }

@@ -549,6 +549,8 @@ dynamics::SkeletonPtr readSkeleton(const XmlNode* sk) {
     else if (jt == "revolute") jb = skel->createJointAndBodyNodePair<dynamics::RevoluteJoint>(parent, jp, bp);
     else if (jt == "prismatic") jb = skel->createJointAndBodyNodePair<dynamics::PrismaticJoint>(parent, jp, bp);
     else if (jt == "free") jb = skel->createJointAndBodyNodePair<dynamics::FreeJoint>(parent, jp, bp);
+    else if (jt == "ball") jb = skel->createJointAndBodyNodePair<dynamics::BallJoint>(parent, jp, bp);
+    else if (jt == "translational") jb = skel->createJointAndBodyNodePair<dynamics::TranslationalJoint>(parent, jp, bp);
     else throw std::invalid_argument("skel joint type " + jt + " is not on the timestep hot path");
     dynamics::Joint* j = jb.first;
     const Isometry3 parentWorld = jj.parent.empty() ? Isometry3::Identity() : bodies.at(jj.parent).init;

@@ -7,6 +7,17 @@
 
 #include "../../include/nimble_amd.h"
 
+// generalized coordinates of a joint type (-1: unknown)
+inline int jointDofs(int jt) {
+  switch (jt) {
+    case NIMBLE_JOINT_WELD: return 0;
+    case NIMBLE_JOINT_REVOLUTE: case NIMBLE_JOINT_PRISMATIC: return 1;
+    case NIMBLE_JOINT_BALL: case NIMBLE_JOINT_TRANSLATIONAL: return 3;
+    case NIMBLE_JOINT_FREE: return 6;
+    default: return -1;
+  }
+}
+
 #define NB_MAX NIMBLE_MAX_BODIES
 #define ND_MAX NIMBLE_MAX_DOFS
 #define NS_MAX NIMBLE_MAX_SHAPES

@@ -138,6 +138,21 @@ DEV void freeIntegrate(const double* q, const double* v, double dt, double* out)
   for (int r = 0; r < 3; r++) out[3 + r] = R[r * 3] * l[0] + R[r * 3 + 1] * l[1] + R[r * 3 + 2] * l[2] + q[3 + r];
 }
 
+// BallJoint::integratePositionsExplicit (dart/dynamics/BallJoint.cpp:333) with
+// DART_USE_IDENTITY_JACOBIAN: convertToPositions(R(q) * R(dq dt)) -- the
+// rotational half of freeIntegrate, the same operations
+DEV void ballIntegrate(const double* q, const double* v, double dt, double* out) {
+  double R[9], Rd[9], wd[3] = {v[0] * dt, v[1] * dt, v[2] * dt};
+  expMapRot(q, R);
+  expMapRot(wd, Rd);
+  double Rn[9];
+#pragma unroll
+  for (int r = 0; r < 3; r++)
+#pragma unroll
+    for (int c = 0; c < 3; c++) Rn[r * 3 + c] = R[r * 3] * Rd[c] + R[r * 3 + 1] * Rd[3 + c] + R[r * 3 + 2] * Rd[6 + c];
+  logMap(Rn, out);
+}
+
 // ---------------------------------------------------------------------------
 // The FreeJoint finite-difference blocks (FreeJoint.cpp:965 eps 1e-6, :987
 // eps 1e-7) difference two position integrations 2 eps apart, so the last

@@ -58,12 +58,19 @@ __device__ __forceinline__ void kinematics(const ModelDev& md, double* s, const 
       Q[8] = t * a[0] * a[2] - sn * a[1]; Q[9] = t * a[1] * a[2] + sn * a[0]; Q[10] = c + t * a[2] * a[2];
     } else if (jt == NIMBLE_JOINT_PRISMATIC) {
       Q[3] = a[0] * q[o]; Q[7] = a[1] * q[o]; Q[11] = a[2] * q[o];
-    } else if (jt == NIMBLE_JOINT_FREE) {
+    } else if (jt == NIMBLE_JOINT_FREE || jt == NIMBLE_JOINT_BALL) {
+      // FreeJoint::convertToTransform / BallJoint::convertToRotation
+      // (FreeJoint.cpp:74, BallJoint.cpp:91): expMapRot of the exponential
+      // coordinates (+ the translation for the free joint)
       double R[9];
       expMapRot(q + o, R);
-      Q[0] = R[0]; Q[1] = R[1]; Q[2] = R[2]; Q[3] = q[o + 3];
-      Q[4] = R[3]; Q[5] = R[4]; Q[6] = R[5]; Q[7] = q[o + 4];
-      Q[8] = R[6]; Q[9] = R[7]; Q[10] = R[8]; Q[11] = q[o + 5];
+      const bool fr = jt == NIMBLE_JOINT_FREE;
+      Q[0] = R[0]; Q[1] = R[1]; Q[2] = R[2]; Q[3] = fr ? q[o + 3] : 0.0;
+      Q[4] = R[3]; Q[5] = R[4]; Q[6] = R[5]; Q[7] = fr ? q[o + 4] : 0.0;
+      Q[8] = R[6]; Q[9] = R[7]; Q[10] = R[8]; Q[11] = fr ? q[o + 5] : 0.0;
+    } else if (jt == NIMBLE_JOINT_TRANSLATIONAL) {
+      // TranslationalJoint::updateRelativeTransform (TranslationalJoint.cpp:127)
+      Q[3] = q[o]; Q[7] = q[o + 1]; Q[11] = q[o + 2];
     }
     double T[12];
     tmul(md.Tpj[b], Q, T);
@@ -89,6 +96,9 @@ __device__ __forceinline__ void kinematics(const ModelDev& md, double* s, const 
     double loc[6] = {0, 0, 0, 0, 0, 0};
     if (jt == NIMBLE_JOINT_REVOLUTE) { loc[0] = a[0]; loc[1] = a[1]; loc[2] = a[2]; }
     else if (jt == NIMBLE_JOINT_PRISMATIC) { loc[3] = a[0]; loc[4] = a[1]; loc[5] = a[2]; }
+    // TranslationalJoint.cpp:142: [0; e_k]; free / ball (identity Jacobian,
+    // FreeJoint.cpp:536, BallJoint.cpp:446): e_k
+    else if (jt == NIMBLE_JOINT_TRANSLATIONAL) loc[3 + k - md.dof0[b]] = 1.0;
     else loc[k - md.dof0[b]] = 1.0;
     double TwC[12];
     tmul(s + L.Tw + 12 * b, md.Tcj[b], TwC);
@@ -456,10 +466,17 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
       const int jt = md.jtype[b];
       if (jt == NIMBLE_JOINT_REVOLUTE || jt == NIMBLE_JOINT_PRISMATIC) {
         out[o] = s[L.q + o] + vint[o] * md.dt;
+      } else if (jt == NIMBLE_JOINT_TRANSLATIONAL) {
+        // math::integratePosition<R3Space> (GenericJoint::integratePositions)
+        for (int i = 0; i < 3; i++) out[o + i] = s[L.q + o + i] + vint[o + i] * md.dt;
       } else if (jt == NIMBLE_JOINT_FREE) {
         double r[6];
         freeIntegrate(s + L.q + o, vint + o, md.dt, r);
         for (int i = 0; i < 6; i++) out[o + i] = r[i];
+      } else if (jt == NIMBLE_JOINT_BALL) {
+        double r[3];
+        ballIntegrate(s + L.q + o, vint + o, md.dt, r);
+        for (int i = 0; i < 3; i++) out[o + i] = r[i];
       }
     }
     WSYNC();
@@ -512,6 +529,40 @@ nimble_forward_wide_kernel(const ModelDev* __restrict__ mdp, Layout L, const dou
   if (!(st & ST_DEFERRED)) return;  // (whole workgroup)
   forwardWorld<2>(mdp, L, state, forces, lcpCache, nextState, snapshot, snapDoubles, cacheDoubles, 1 << 30, env,
                   false);
+}
+
+// posPos^T gp and velPos^T gp of one free (ND = 6) or ball (ND = 3) joint at
+// dof offset o, added to lane k's gq / gvOut: 4 ND lanes run one perturbed
+// integration each into fd (spatial.cuh fdFreeIntegrate: the oracle's
+// operation sequence; a ball joint's translation inputs are zero)
+template <int ND>
+__device__ __forceinline__ void fdBlocksVjp(const double* s, const Layout& L, int o, double dt, int lane, int k,
+                                            double* fd, double& gq, double& gvOut) {
+  if (lane < 4 * ND) {
+    const int which = lane / (2 * ND);  // 0: wrt pos, 1: wrt vel
+    const int i = (lane % (2 * ND)) / 2;
+    const double sign = (lane % 2) ? -1.0 : 1.0;
+    const double eps = which == 0 ? 1e-6 : 1e-7;
+    double qq[6] = {0, 0, 0, 0, 0, 0}, vv[6] = {0, 0, 0, 0, 0, 0}, r[6];
+    for (int j = 0; j < ND; j++) { qq[j] = s[L.q + o + j]; vv[j] = s[L.v + o + j]; }
+    if (which == 0) qq[i] += sign * eps; else vv[i] += sign * eps;
+    fdFreeIntegrate(qq, vv, dt, r);
+    for (int j = 0; j < 6; j++) fd[lane * 6 + j] = r[j];
+  }
+  WSYNC();
+  if (k >= o && k < o + ND) {
+    const int i = k - o;
+    double pp = 0.0, vp = 0.0;
+    for (int r = 0; r < ND; r++) {
+      const double jp = (fd[(i * 2) * 6 + r] - fd[(i * 2 + 1) * 6 + r]) / (2 * 1e-6);
+      const double jv = (fd[(2 * ND + i * 2) * 6 + r] - fd[(2 * ND + i * 2 + 1) * 6 + r]) / (2 * 1e-7);
+      pp += jp * s[L.gp + o + r];
+      vp += jv * s[L.gp + o + r];
+    }
+    gq += pp;
+    gvOut += vp;
+  }
+  WSYNC();
 }
 
 // ---------------------------------------------------------------------------
@@ -730,7 +781,8 @@ __device__ __forceinline__ void backwardItems(const ModelDev* __restrict__ mdp, 
       }
       // position generator Z (world twist of the subtree per unit q_k)
       const double* Sk = s + L.Sw + 6 * k;
-      if (md.jtype[b] == NIMBLE_JOINT_FREE) {
+      // (ball joints: the free joint's rotational half, BallJoint.cpp:282)
+      if (md.jtype[b] == NIMBLE_JOINT_FREE || md.jtype[b] == NIMBLE_JOINT_BALL) {
         const int o = md.dof0[b];
         const int c = k - o;
         double xi[6] = {0, 0, 0, 0, 0, 0};
@@ -767,8 +819,10 @@ __device__ __forceinline__ void backwardItems(const ModelDev* __restrict__ mdp, 
       gvOut = s[L.gv + k] - dt * accV - dt * md.damping[k] * wk - dt * dt * md.spring[k] * wk;
       gt = dt * wk;
       if (nc > 0) gvOut -= P.NV[k * NV_COLS + NV_MU];
-      // posPos^T gp and velPos^T gp for 1-dof joints: identity / dt * identity
-      if (md.ndof[b] == 1) {
+      // posPos^T gp and velPos^T gp for the Euclidean joints (revolute,
+      // prismatic, translational: GenericJoint::getPosPosJacobian /
+      // getVelPosJacobian): identity / dt * identity
+      if (md.jtype[b] != NIMBLE_JOINT_FREE && md.jtype[b] != NIMBLE_JOINT_BALL) {
         gq += s[L.gp + k];
         gvOut += dt * s[L.gp + k];
       }
@@ -903,37 +957,19 @@ __device__ __forceinline__ void backwardItems(const ModelDev* __restrict__ mdp, 
       }
       WSYNC();
     }
-    // FreeJoint posPos / velPos blocks: central differences exactly as
-    // FreeJoint::finiteDifferencePosPosJacobian / VelPosJacobian
-    // (FreeJoint.cpp:965, :987); 24 lanes, one perturbed integration each.
+    // FreeJoint / BallJoint posPos / velPos blocks: central differences
+    // exactly as FreeJoint::finiteDifferencePosPosJacobian / VelPosJacobian
+    // (FreeJoint.cpp:965, :987) and BallJoint's (BallJoint.cpp:368, :390);
+    // 4 ND lanes (ND = 6 / 3 coordinates), one perturbed integration each.  A
+    // ball joint's integration is the free joint's rotational half (the same
+    // operations; its translation inputs zero, outputs unused)
     double* fd = s + L.scratch;
     for (int f = 0; f < md.numFree; f++) {
       const int b = md.freeBody[f], o = md.dof0[b];
-      if (lane < 24) {
-        const int which = lane / 12;      // 0: wrt pos, 1: wrt vel
-        const int i = (lane % 12) / 2;
-        const double sign = (lane % 2) ? -1.0 : 1.0;
-        const double eps = which == 0 ? 1e-6 : 1e-7;
-        double qq[6], vv[6], r[6];
-        for (int j = 0; j < 6; j++) { qq[j] = s[L.q + o + j]; vv[j] = s[L.v + o + j]; }
-        if (which == 0) qq[i] += sign * eps; else vv[i] += sign * eps;
-        fdFreeIntegrate(qq, vv, dt, r);  // (the oracle's operation sequence: spatial.cuh fd*)
-        for (int j = 0; j < 6; j++) fd[lane * 6 + j] = r[j];
-      }
-      WSYNC();
-      if (k >= o && k < o + 6) {
-        const int i = k - o;
-        double pp = 0.0, vp = 0.0;
-        for (int r = 0; r < 6; r++) {
-          const double jp = (fd[(i * 2) * 6 + r] - fd[(i * 2 + 1) * 6 + r]) / (2 * 1e-6);
-          const double jv = (fd[(12 + i * 2) * 6 + r] - fd[(12 + i * 2 + 1) * 6 + r]) / (2 * 1e-7);
-          pp += jp * s[L.gp + o + r];
-          vp += jv * s[L.gp + o + r];
-        }
-        gq += pp;
-        gvOut += vp;
-      }
-      WSYNC();
+      if (md.jtype[b] == NIMBLE_JOINT_FREE)
+        fdBlocksVjp<6>(s, L, o, dt, lane, k, fd, gq, gvOut);
+      else
+        fdBlocksVjp<3>(s, L, o, dt, lane, k, fd, gq, gvOut);
     }
     if (k < n) {
       if (unitRow < 0) {

@@ -26,6 +26,8 @@ JOINT_WELD = 0
 JOINT_REVOLUTE = 1
 JOINT_PRISMATIC = 2
 JOINT_FREE = 3
+JOINT_BALL = 4           # BallJoint.cpp: exponential coordinates, identity Jacobian
+JOINT_TRANSLATIONAL = 5  # TranslationalJoint.cpp: R3 offset
 
 SHAPE_BOX = 0
 SHAPE_SPHERE = 1
@@ -207,7 +209,8 @@ class Joint:
         self.dof_offset = 0
 
     def getNumDofs(self) -> int:
-        return {JOINT_WELD: 0, JOINT_REVOLUTE: 1, JOINT_PRISMATIC: 1, JOINT_FREE: 6}[self.kind]
+        return {JOINT_WELD: 0, JOINT_REVOLUTE: 1, JOINT_PRISMATIC: 1, JOINT_FREE: 6, JOINT_BALL: 3,
+                JOINT_TRANSLATIONAL: 3}[self.kind]
 
     def getName(self):
         return self.name
@@ -369,6 +372,12 @@ class Skeleton:
 
     def createFreeJointAndBodyNodePair(self, parent=None, joint_name=None, body_name=None):
         return self._create(JOINT_FREE, parent, joint_name, body_name)
+
+    def createBallJointAndBodyNodePair(self, parent=None, joint_name=None, body_name=None):
+        return self._create(JOINT_BALL, parent, joint_name, body_name)
+
+    def createTranslationalJointAndBodyNodePair(self, parent=None, joint_name=None, body_name=None):
+        return self._create(JOINT_TRANSLATIONAL, parent, joint_name, body_name)
 
     def createWeldJointAndBodyNodePair(self, parent=None, joint_name=None, body_name=None):
         return self._create(JOINT_WELD, parent, joint_name, body_name)

@@ -100,7 +100,7 @@ def read_skeleton(sk_el) -> dyn.Skeleton:
     created: Dict[str, dyn.BodyNode] = {}
     pending = list(joints)
     kinds = {"weld": dyn.JOINT_WELD, "revolute": dyn.JOINT_REVOLUTE, "prismatic": dyn.JOINT_PRISMATIC,
-             "free": dyn.JOINT_FREE}
+             "free": dyn.JOINT_FREE, "ball": dyn.JOINT_BALL, "translational": dyn.JOINT_TRANSLATIONAL}
 
     def create(jel, parent, child):
         jt = jel.get("type")

@@ -49,7 +49,10 @@ World::World(const nimble_world_desc* d) {
     B.jtype = d->joint_type[b];
     B.dof0 = d->dof_offset[b];
     B.mobile = d->skeleton_mobile[b] != 0;
-    B.ndof = B.jtype == NIMBLE_JOINT_WELD ? 0 : (B.jtype == NIMBLE_JOINT_FREE ? 6 : 1);
+    // (WeldJoint 0, Revolute / Prismatic 1, Ball / Translational 3, Free 6)
+    B.ndof = B.jtype == NIMBLE_JOINT_WELD ? 0
+             : B.jtype == NIMBLE_JOINT_FREE ? 6
+             : (B.jtype == NIMBLE_JOINT_BALL || B.jtype == NIMBLE_JOINT_TRANSLATIONAL) ? 3 : 1;
     auto loadIso = [](const double* t, Iso<double>& T) {
       for (int r = 0; r < 3; r++) {
         for (int c = 0; c < 3; c++) T.R(r, c) = t[r * 4 + c];
@@ -136,6 +139,17 @@ void jointTransform(const Body& B, const S* q, Iso<S>& T, M6<S>& Sj /* 6 x ndof,
     Q.R = expMapRot(w);
     for (int i = 0; i < 3; i++) Q.p[i] = q[3 + i];
     for (int i = 0; i < 6; i++) local(i, i) = S(1.0);
+  } else if (B.jtype == NIMBLE_JOINT_BALL) {
+    // BallJoint::updateRelativeTransform (BallJoint.cpp:422, convertToRotation
+    // = expMapRot :91) and, with DART_USE_IDENTITY_JACOBIAN, the Jacobian
+    // getAdTMatrix(T_cj).leftCols<3>() (:446)
+    V3<S> w{{q[0], q[1], q[2]}};
+    Q.R = expMapRot(w);
+    for (int i = 0; i < 3; i++) local(i, i) = S(1.0);
+  } else if (B.jtype == NIMBLE_JOINT_TRANSLATIONAL) {
+    // TranslationalJoint::updateRelativeTransform / updateRelativeJacobian
+    // (TranslationalJoint.cpp:127, :138): Translation(q), [0; R_cj]
+    for (int i = 0; i < 3; i++) { Q.p[i] = q[i]; local(3 + i, i) = S(1.0); }
   }
   T = compose(compose(Tpj, Q), inverse(Tcj));
   // S = Ad(T_cj) * local  (AdTAngular / AdTLinear / getAdTMatrix)
@@ -372,20 +386,32 @@ void World::integratePositionsExplicit(const double* q, const double* v, double 
       V3<double> pn = add(mul(R, ld), V3<double>{{q[o + 3], q[o + 4], q[o + 5]}});
       V3<double> lg = logMap(Rn);
       for (int i = 0; i < 3; i++) { out[o + i] = lg[i]; out[o + 3 + i] = pn[i]; }
+    } else if (B.jtype == NIMBLE_JOINT_BALL) {
+      // BallJoint::integratePositionsExplicit (BallJoint.cpp:333), identity-J:
+      // convertToPositions(convertToRotation(q) * convertToRotation(dq * dt))
+      V3<double> w{{q[o], q[o + 1], q[o + 2]}};
+      V3<double> wd{{v[o] * dtt, v[o + 1] * dtt, v[o + 2] * dtt}};
+      V3<double> lg = logMap(mul(expMapRot(w), expMapRot(wd)));
+      for (int i = 0; i < 3; i++) out[o + i] = lg[i];
+    } else if (B.jtype == NIMBLE_JOINT_TRANSLATIONAL) {
+      for (int i = 0; i < 3; i++) out[o + i] = q[o + i] + v[o + i] * dtt;  // integratePosition<R3Space>
     }
   }
 }
 
 // Skeleton::getPosPosJac / getVelPosJac (Skeleton.cpp:9291, :9310):
-// identity / dt*identity for R1 joints, central finite differences for the
-// FreeJoint (FreeJoint.cpp:965 EPS=1e-6, :987 EPS=1e-7).
+// identity / dt*identity for the Euclidean joints (R1 / R3 spaces: revolute,
+// prismatic, translational), central finite differences for the FreeJoint
+// (FreeJoint.cpp:965 EPS=1e-6, :987 EPS=1e-7) and the BallJoint
+// (BallJoint.cpp:368 EPS=1e-6, :390 EPS=1e-7).
 void World::posPosJac(const double* q, const double* v, double* J) const {
   std::fill(J, J + n * n, 0.0);
   for (int b = 0; b < nb; b++) {
     const Body& B = bodies[b];
     int o = B.dof0;
-    if (B.ndof == 1) J[o * n + o] = 1.0;
     if (B.jtype == NIMBLE_JOINT_FREE) freeJointFD(q + o, v + o, true, J, o);
+    else if (B.jtype == NIMBLE_JOINT_BALL) ballJointFD(q + o, v + o, true, J, o);
+    else for (int i = 0; i < B.ndof; i++) J[(o + i) * n + o + i] = 1.0;
   }
 }
 void World::velPosJac(const double* q, const double* v, double* J) const {
@@ -393,8 +419,9 @@ void World::velPosJac(const double* q, const double* v, double* J) const {
   for (int b = 0; b < nb; b++) {
     const Body& B = bodies[b];
     int o = B.dof0;
-    if (B.ndof == 1) J[o * n + o] = dt;
     if (B.jtype == NIMBLE_JOINT_FREE) freeJointFD(q + o, v + o, false, J, o);
+    else if (B.jtype == NIMBLE_JOINT_BALL) ballJointFD(q + o, v + o, false, J, o);
+    else for (int i = 0; i < B.ndof; i++) J[(o + i) * n + o + i] = dt;
   }
 }
 //------------------------------------------------------------------------------
@@ -551,6 +578,25 @@ static void fdFreeIntegrate(const double* q, const double* v, double dt, double*
   const double l[3] = {v[3] * dt, v[4] * dt, v[5] * dt};
   fdLogMap(Rn, out);
   for (int r = 0; r < 3; r++) out[3 + r] = R[r * 3] * l[0] + R[r * 3 + 1] * l[1] + R[r * 3 + 2] * l[2] + q[3 + r];
+}
+
+// BallJoint::finiteDifferencePosPosJacobian / VelPosJacobian (BallJoint.cpp:368,
+// :390): the same central differences of its integration, which is the free
+// joint's rotational half (BallJoint.cpp:333 vs FreeJoint.cpp:920) -- evaluated
+// by fdFreeIntegrate with zero translation inputs, whose rotation outputs do
+// not depend on them
+void World::ballJointFD(const double* q3, const double* v3, bool wrtPos, double* J, int o) const {
+  const double EPS = wrtPos ? 1e-6 : 1e-7;
+  for (int i = 0; i < 3; i++) {
+    double pq[6], pv[6], plus[6], minus[6];
+    for (int j = 0; j < 6; j++) { pq[j] = j < 3 ? q3[j] : 0.0; pv[j] = j < 3 ? v3[j] : 0.0; }
+    if (wrtPos) pq[i] += EPS; else pv[i] += EPS;
+    fdFreeIntegrate(pq, pv, dt, plus);
+    for (int j = 0; j < 3; j++) { pq[j] = q3[j]; pv[j] = v3[j]; }
+    if (wrtPos) pq[i] -= EPS; else pv[i] -= EPS;
+    fdFreeIntegrate(pq, pv, dt, minus);
+    for (int r = 0; r < 3; r++) J[(o + r) * n + (o + i)] = (plus[r] - minus[r]) / (2 * EPS);
+  }
 }
 
 void World::freeJointFD(const double* q6, const double* v6, bool wrtPos, double* J, int o) const {

@@ -115,6 +115,7 @@ struct World {
   void posPosJac(const double* q, const double* v, double* J) const;
   void velPosJac(const double* q, const double* v, double* J) const;
   void freeJointFD(const double* q6, const double* v6, bool wrtPos, double* J, int o) const;
+  void ballJointFD(const double* q3, const double* v3, bool wrtPos, double* J, int o) const;
   void jacobianOfC(const double* q, const double* v, bool wrtPos, double* dC) const;
   void jacobianOfMy(const double* q, const double* y, double* dMy) const;
 

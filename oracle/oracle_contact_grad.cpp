@@ -36,14 +36,15 @@ static void cross3(const double* a, const double* b, double* o) {
 }
 
 // World screw axis for position (Joint::getWorldAxisScrewForPosition,
-// Joint.cpp:1167 with FreeJoint's position-space Jacobian FreeJoint.cpp:790)
+// Joint.cpp:1167 with FreeJoint's position-space Jacobian FreeJoint.cpp:790;
+// BallJoint's, BallJoint.cpp:282, is its rotational half)
 static void positionScrew(const World& w, const Kin<double>& k, const double* q, int dof, double* Z) {
   const int b = w.dofBody[dof];
   const Body& B = w.bodies[b];
   const int c = dof - B.dof0;
   V6<double> xi;
   for (int i = 0; i < 6; i++) xi[i] = 0.0;
-  if (B.jtype == NIMBLE_JOINT_FREE) {
+  if (B.jtype == NIMBLE_JOINT_FREE || B.jtype == NIMBLE_JOINT_BALL) {
     const double* th = q + B.dof0;
     V3<double> t{{th[0], th[1], th[2]}};
     if (c < 3) {
@@ -447,7 +448,10 @@ static void constraintForcesJacobian(const World& w, const Kin<double>& k, const
       // screw-axis gradient: k's joint at or above r's joint
       const int bk = w.dofBody[kk], br = w.dofBody[r];
       if (w.isAncestorOrSelf(bk, br)) {
-        if (bk != br || w.bodies[bk].jtype == NIMBLE_JOINT_FREE) {
+        // (a multi-dof joint's axes move with its own coordinates; a 1-dof
+        // joint's axis does not, and a translational joint's pure
+        // translations give ad(Z, S) = 0 either way)
+        if (bk != br || w.bodies[bk].ndof > 1) {
           V6<double> zz, ss;
           for (int i = 0; i < 6; i++) { zz[i] = Z[i]; ss[i] = S[i]; }
           V6<double> g = ad(zz, ss);

@@ -518,3 +518,72 @@ def pipe_box_states(case, order, batch, seed=0):
     st[:, 6:] = 0.2 * rng.standard_normal((batch, 6))
     f = rng.standard_normal((batch, 6))
     return st, f
+
+
+def ball_world(ground=True):
+    """A rig exercising the 3-dof joints: a base box on a TranslationalJoint
+    (root), a leg hanging from it on a BallJoint, a foot box on a revolute
+    ankle (z axis) at the leg's end, and an arm on a second BallJoint at the
+    base's side; the foot rests on a static ground box (top face at y = 0)
+    when `ground`.  (BallJoint.cpp / TranslationalJoint.cpp, identity
+    Jacobian build.)"""
+    from nimblephysics_amd import dynamics as D
+
+    def tr(x, y, z):
+        T = np.eye(4)
+        T[:3, 3] = [x, y, z]
+        return T
+
+    def box_inertia(b, m, sx, sy, sz):
+        b.setMass(m)
+        b.setMomentOfInertia(m * (sy * sy + sz * sz) / 12, m * (sx * sx + sz * sz) / 12, m * (sx * sx + sy * sy) / 12)
+
+    w = nimble.World()
+    w.setGravity([0, -9.81, 0])
+    rig = D.Skeleton("rig")
+    _, base = rig.createTranslationalJointAndBodyNodePair(body_name="base")
+    box_inertia(base, 2.0, 0.3, 0.2, 0.3)
+    base.createShapeNode(D.BoxShape([0.3, 0.2, 0.3]), collision=True)
+    hip, leg = rig.createBallJointAndBodyNodePair(base, joint_name="hip", body_name="leg")
+    hip.setTransformFromParentBodyNode(tr(0, -0.15, 0))
+    hip.setTransformFromChildBodyNode(tr(0, 0.2, 0))
+    box_inertia(leg, 1.0, 0.1, 0.4, 0.1)
+    leg.createShapeNode(D.BoxShape([0.1, 0.4, 0.1]), collision=True)
+    ankle, foot = rig.createRevoluteJointAndBodyNodePair(leg, joint_name="ankle", body_name="foot")
+    ankle.setAxis([0, 0, 1])
+    ankle.setTransformFromParentBodyNode(tr(0, -0.2, 0))
+    ankle.setTransformFromChildBodyNode(tr(0, 0.05, 0))
+    box_inertia(foot, 0.5, 0.2, 0.1, 0.3)
+    foot.createShapeNode(D.BoxShape([0.2, 0.1, 0.3]), collision=True)
+    shoulder, arm = rig.createBallJointAndBodyNodePair(base, joint_name="shoulder", body_name="arm")
+    shoulder.setTransformFromParentBodyNode(tr(0.15, 0, 0))
+    shoulder.setTransformFromChildBodyNode(tr(-0.12, 0, 0))
+    box_inertia(arm, 0.3, 0.24, 0.05, 0.05)
+    arm.createShapeNode(D.BoxShape([0.24, 0.05, 0.05]), collision=True)
+    w.addSkeleton(rig)
+    if ground:
+        g = D.Skeleton("ground")
+        gj, gb = g.createWeldJointAndBodyNodePair()
+        gj.setTransformFromParentBodyNode(tr(0, -0.05, 0))
+        gb.createShapeNode(D.BoxShape([10.0, 0.1, 10.0]), collision=True)
+        g.setMobile(False)
+        w.addSkeleton(g)
+    return w
+
+
+def ball_states(batch, seed=0, contact=True):
+    """ball_world states: the base at the height where the foot's sole is
+    ~1 mm into the ground (0.65 m) when `contact`, else 0.3 m higher; small
+    hip / ankle rotations, a random shoulder rotation (up to ~1 rad), small
+    velocities, random forces.  Dofs: base x y z, hip 3, ankle, shoulder 3."""
+    rng = np.random.default_rng(seed)
+    q = np.zeros((batch, 10))
+    v = 0.05 * rng.standard_normal((batch, 10))
+    q[:, 0] = 0.01 * rng.standard_normal(batch)
+    q[:, 1] = (0.649 if contact else 0.95) + 2e-4 * rng.standard_normal(batch)
+    q[:, 2] = 0.01 * rng.standard_normal(batch)
+    q[:, 3:6] = 0.01 * rng.standard_normal((batch, 3))
+    q[:, 6] = 0.01 * rng.standard_normal(batch)
+    q[:, 7:10] = 0.6 * rng.standard_normal((batch, 3))
+    f = 0.5 * rng.standard_normal((batch, 10))
+    return np.concatenate([q, v], axis=1), f

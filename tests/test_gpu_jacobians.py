@@ -32,10 +32,10 @@ def _fd_mask(world):
     n = world.getNumDofs()
     mask = np.zeros((2 * n, 2 * n), dtype=bool)
     for b, jt in enumerate(d["joint_type"]):
-        if int(jt) == 3:
-            o = int(d["dof_offset"][b])
-            mask[o:o + 6, o:o + 6] = True          # posPos
-            mask[o:o + 6, n + o:n + o + 6] = True  # velPos
+        if int(jt) in (3, 4):  # FreeJoint (6 coordinates), BallJoint (3: BallJoint.cpp:368, :390)
+            o, k = int(d["dof_offset"][b]), 6 if int(jt) == 3 else 3
+            mask[o:o + k, o:o + k] = True          # posPos
+            mask[o:o + k, n + o:n + o + k] = True  # velPos
     return mask
 
 

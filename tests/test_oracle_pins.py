@@ -558,3 +558,57 @@ def test_lcp_path_reproduces_the_step(oracle_built):
             assert got == want, (b, got[:6], want[:6])
             checked += 1
     assert checked > 20
+
+
+@pytest.mark.parametrize("contact", [False, True])
+def test_ball_translational_gradients_vs_finite_differences(oracle_built, contact):
+    """The 3-dof joints (BallJoint.cpp: exponential coordinates, identity
+    Jacobian, finite-difference posPos / velPos blocks :368 / :390;
+    TranslationalJoint.cpp: R3 offset, identity blocks): the oracle's
+    analytic gradients of a rig with a translational root, two ball joints
+    and a revolute ankle against central differences of its own step, in
+    the air and with the foot on the ground (contact gradients through the
+    ball joints' position screws and same-joint screw-axis terms)."""
+    w = models.ball_world(ground=contact)
+    st, f = models.ball_states(4, seed=3, contact=contact)
+    assert w.getNumDofs() == 10
+    o = O.OracleWorld(w)
+    o.forward(st, f)
+    if contact:
+        assert all(o.num_contacts(b) > 0 for b in range(4))
+    for b in range(2):
+        g = np.random.default_rng(10 + b).standard_normal(st.shape[1])
+        gs, gf, fd_s, fd_f = _fd_check(w, st[b], f[b], g)
+        assert np.abs(gs - fd_s).max() <= 1e-6 * np.abs(fd_s).max(), (b, np.abs(gs - fd_s).max())
+        assert np.abs(gf - fd_f).max() <= 1e-6 * np.abs(fd_f).max(), (b, np.abs(gf - fd_f).max())
+
+
+def test_ball_joint_integration_matches_rotation_composition(oracle_built):
+    """BallJoint::integratePositionsExplicit (BallJoint.cpp:333) in the
+    oracle's contact-free step: the next exponential coordinates of a ball
+    joint are log(exp(q) exp(v dt)) of the step's velocity (parallel
+    position / velocity update: the pre-step velocity), and a translational
+    joint's are q + v dt -- checked against scipy-free numpy Rodrigues."""
+    w = models.ball_world(ground=False)
+    st, f = models.ball_states(3, seed=9, contact=False)
+    nxt = O.OracleWorld(w).forward(st, f)
+    dt = w.getTimeStep() if hasattr(w, "getTimeStep") else w.dt
+
+    def expm(r):
+        th = np.linalg.norm(r)
+        K = np.array([[0, -r[2], r[1]], [r[2], 0, -r[0]], [-r[1], r[0], 0]])
+        if th < 1e-12:
+            return np.eye(3) + K
+        return np.eye(3) + np.sin(th) / th * K + (1 - np.cos(th)) / th ** 2 * K @ K
+
+    def logm(R):
+        c = np.clip((np.trace(R) - 1) / 2, -1, 1)
+        th = np.arccos(c)
+        return th / (2 * np.sin(th)) * np.array([R[2, 1] - R[1, 2], R[0, 2] - R[2, 0], R[1, 0] - R[0, 1]])
+    n = 10
+    for b in range(3):
+        q, v = st[b, :n], st[b, n:]
+        assert np.allclose(nxt[b, 0:3], q[0:3] + v[0:3] * dt, rtol=0, atol=1e-15)
+        for o in (3, 7):
+            want = logm(expm(q[o:o + 3]) @ expm(v[o:o + 3] * dt))
+            assert np.allclose(nxt[b, o:o + 3], want, rtol=0, atol=1e-12), (b, o)

@@ -346,3 +346,26 @@ def test_guard_forced_expiry_emulated(site):
         else:
             assert np.abs(nxt[i] - ref[i]).max() <= 1e-12, (site, i)
         assert np.isfinite(gs[i]).all() and np.isfinite(gf[i]).all()
+
+
+@pytest.mark.parametrize("contact", [False, True])
+def test_ball_rig_step_emulated(contact):
+    """The 3-dof joints through the emulated kernels (ball / translational
+    local transforms, motion subspaces, integrations, position screws and the
+    ball joints' FD blocks in the backward) against the oracle."""
+    world = models.ball_world(ground=contact)
+    st, f = models.ball_states(8, seed=21, contact=contact)
+    st, f = st[:2], f[:2]
+    g = np.random.default_rng(4).standard_normal(st.shape)
+    ow = O.OracleWorld(world)
+    ref = ow.forward(st, f)
+    rgs, rgf = ow.backward(g)
+    nxt, gs, gf, head = wave_emu.step(world, st, f, g, timeout=900)
+    if contact:
+        assert (head[:, 0] > 0).all()
+    for i in range(2):
+        fl = O.lcp_flags(ow, i)
+        assert (head[i, 6], head[i, 7], head[i, 4]) == (fl[0], fl[1], fl[2]), i
+    assert np.abs(nxt - ref).max() <= 1e-12 * max(1.0, np.abs(ref).max())
+    assert np.abs(gs - rgs).max() <= 1e-9 * np.abs(rgs).max()
+    assert np.abs(gf - rgf).max() <= 1e-9 * np.abs(rgf).max()

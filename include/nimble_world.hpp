@@ -157,6 +157,13 @@ class ShapeNode {
   Isometry3 mT;
 };
 
+/* Host-side joint kinds beyond the C-ABI's (nimble_joint_type): products of
+ * elementary axis rotations / translations, which World::describe() hands to
+ * the device as the equivalent chain of 1-dof joints through massless frames
+ * (the same transform as a function of q, hence the same motion subspace,
+ * dynamics, Euclidean integration and posPos / velPos blocks). */
+enum { kJointUniversal = 6, kJointEuler = 7, kJointPlanar = 8 };
+
 /* dart/dynamics/Joint.hpp + GenericJoint per-dof properties */
 class Joint {
  public:
@@ -186,6 +193,7 @@ class Joint {
  protected:
   Joint(Skeleton* skel, int type, int dofs, const Properties& p);
   void changed();
+  friend struct JointChainAccess;
   friend class simulation::World;
   friend class Skeleton;
   Skeleton* mSkel;
@@ -193,6 +201,12 @@ class Joint {
   std::string mName;
   Isometry3 mTp, mTc;
   Vector3s mAxis{{1, 0, 0}};
+  /* UniversalJoint's second axis; EulerJoint's axis order (XYZ 0, ZYX 1, ZXY
+   * 2, XZY 3) and flip map; PlanarJoint's translation and rotation axes */
+  Vector3s mAxis2{{0, 1, 0}};
+  int mOrder = 0;
+  Vector3s mFlip{{1, 1, 1}};
+  Vector3s mTrans1{{1, 0, 0}}, mTrans2{{0, 1, 0}}, mRot{{0, 0, 1}};
   VectorXs mDamping, mSpring, mRest, mPosLo, mPosHi, mVelLo, mVelHi, mForceLo, mForceHi;
   std::size_t mDofOffset = 0;
 };
@@ -217,6 +231,39 @@ class TranslationalJoint : public Joint {
  public:
   using Properties = Joint::Properties;
   TranslationalJoint(Skeleton* s, const Properties& p) : Joint(s, NIMBLE_JOINT_TRANSLATIONAL, 3, p) {}
+};
+/* UniversalJoint.cpp:193 T_pj AngleAxis(q0, axis1) AngleAxis(q1, axis2)
+ * T_cj^-1 (UniversalJointAspect defaults: axes x, y; normalised) */
+class UniversalJoint : public Joint {
+ public:
+  using Properties = Joint::Properties;
+  UniversalJoint(Skeleton* s, const Properties& p) : Joint(s, kJointUniversal, 2, p) {}
+  void setAxis1(const Vector3s& axis);
+  void setAxis2(const Vector3s& axis);
+  Vector3s getAxis1() const { return mAxis; }
+  Vector3s getAxis2() const { return mAxis2; }
+};
+/* EulerJoint.cpp:1333 T_pj euler_<order>(q .* flip) T_cj^-1 (Geometry.cpp
+ * eulerXYZToMatrix = Rx Ry Rz, ZYX = Rz Ry Rx, ZXY = Rz Rx Ry, XZY = Rx Rz Ry) */
+class EulerJoint : public Joint {
+ public:
+  using Properties = Joint::Properties;
+  enum class AxisOrder { XYZ = 0, ZYX = 1, ZXY = 2, XZY = 3 };
+  EulerJoint(Skeleton* s, const Properties& p) : Joint(s, kJointEuler, 3, p) {}
+  void setAxisOrder(AxisOrder order);
+  AxisOrder getAxisOrder() const { return static_cast<AxisOrder>(mOrder); }
+  void setFlipAxisMap(const Vector3s& flip);
+};
+/* PlanarJoint.cpp:296 T_pj Trans(t1 q0) Trans(t2 q1) expAngular(r q2) T_cj^-1
+ * (PlanarJointAspect.cpp:88: the XY plane by default) */
+class PlanarJoint : public Joint {
+ public:
+  using Properties = Joint::Properties;
+  PlanarJoint(Skeleton* s, const Properties& p) : Joint(s, kJointPlanar, 3, p) {}
+  void setXYPlane();
+  void setYZPlane();
+  void setZXPlane();
+  void setArbitraryPlane(const Vector3s& transAxis1, const Vector3s& transAxis2);
 };
 /* RevoluteJoint / PrismaticJoint::setAxis normalise the axis */
 class RevoluteJoint : public Joint {

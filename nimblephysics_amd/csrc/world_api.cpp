@@ -61,6 +61,61 @@ static Vector3s normalized(const Vector3s& a) {
   if (!(l > 0)) throw std::invalid_argument("setAxis: zero axis");
   return {a[0] / l, a[1] / l, a[2] / l};
 }
+void UniversalJoint::setAxis1(const Vector3s& axis) { mAxis = normalized(axis); changed(); }
+void UniversalJoint::setAxis2(const Vector3s& axis) { mAxis2 = normalized(axis); changed(); }
+void EulerJoint::setAxisOrder(AxisOrder order) { mOrder = static_cast<int>(order); changed(); }
+void EulerJoint::setFlipAxisMap(const Vector3s& flip) { mFlip = flip; changed(); }
+void PlanarJoint::setXYPlane() { mTrans1 = {{1, 0, 0}}; mTrans2 = {{0, 1, 0}}; mRot = {{0, 0, 1}}; changed(); }
+void PlanarJoint::setYZPlane() { mTrans1 = {{0, 1, 0}}; mTrans2 = {{0, 0, 1}}; mRot = {{1, 0, 0}}; changed(); }
+void PlanarJoint::setZXPlane() { mTrans1 = {{0, 0, 1}}; mTrans2 = {{1, 0, 0}}; mRot = {{0, 1, 0}}; changed(); }
+// PlanarJointUniqueProperties::setArbitraryPlane: normalised, the second axis
+// orthogonalised against the first, rotation about their cross product
+void PlanarJoint::setArbitraryPlane(const Vector3s& transAxis1, const Vector3s& transAxis2) {
+  const Vector3s t1 = normalized(transAxis1);
+  Vector3s t2 = normalized(transAxis2);
+  const double d = t1[0] * t2[0] + t1[1] * t2[1] + t1[2] * t2[2];
+  if (std::fabs(d) > 1e-6) t2 = normalized({{t2[0] - d * t1[0], t2[1] - d * t1[1], t2[2] - d * t1[2]}});
+  mTrans1 = t1;
+  mTrans2 = t2;
+  mRot = normalized({{t1[1] * t2[2] - t1[2] * t2[1], t1[2] * t2[0] - t1[0] * t2[2], t1[0] * t2[1] - t1[1] * t2[0]}});
+  changed();
+}
+
+// The device model's 1-dof elements of a joint (as dynamics.Joint.chain in
+// the Python mirror): a compound joint's elementary transforms in series,
+// the first with the joint's parent transform, the last with its child
+// transform, identity frames between them
+struct ChainElem {
+  int type;
+  Vector3s axis;
+  Isometry3 tp, tc;
+};
+struct JointChainAccess {
+  static std::vector<ChainElem> chain(const Joint& j);
+};
+std::vector<ChainElem> JointChainAccess::chain(const Joint& j) {
+  std::vector<std::pair<int, Vector3s>> el;
+  const Vector3s ex{{1, 0, 0}}, ey{{0, 1, 0}}, ez{{0, 0, 1}};
+  const Vector3s unit[3] = {ex, ey, ez};
+  if (j.type() == kJointUniversal) {
+    el = {{NIMBLE_JOINT_REVOLUTE, j.mAxis}, {NIMBLE_JOINT_REVOLUTE, j.mAxis2}};
+  } else if (j.type() == kJointEuler) {
+    static const int order[4][3] = {{0, 1, 2}, {2, 1, 0}, {2, 0, 1}, {0, 2, 1}};  // XYZ ZYX ZXY XZY
+    for (int i = 0; i < 3; i++) {
+      const Vector3s& u = unit[order[j.mOrder][i]];
+      el.push_back({NIMBLE_JOINT_REVOLUTE, {{u[0] * j.mFlip[i], u[1] * j.mFlip[i], u[2] * j.mFlip[i]}}});
+    }
+  } else if (j.type() == kJointPlanar) {
+    el = {{NIMBLE_JOINT_PRISMATIC, j.mTrans1}, {NIMBLE_JOINT_PRISMATIC, j.mTrans2}, {NIMBLE_JOINT_REVOLUTE, j.mRot}};
+  } else {
+    return {ChainElem{j.type(), j.mAxis, j.mTp, j.mTc}};
+  }
+  std::vector<ChainElem> out;
+  for (std::size_t i = 0; i < el.size(); i++)
+    out.push_back(ChainElem{el[i].first, el[i].second, i == 0 ? j.mTp : Isometry3::Identity(),
+                            i + 1 == el.size() ? j.mTc : Isometry3::Identity()});
+  return out;
+}
 void RevoluteJoint::setAxis(const Vector3s& axis) { mAxis = normalized(axis); changed(); }
 void PrismaticJoint::setAxis(const Vector3s& axis) { mAxis = normalized(axis); changed(); }
 
@@ -193,33 +248,50 @@ const nimble_world_desc& World::describe() {
   int bodyBase = 0, dofBase = 0, nb = 0;
   for (std::size_t si = 0; si < mSkels.size(); si++) {
     const auto& s = *mSkels[si];
+    // every body's 1-dof chain (compound joints: massless frames before the
+    // body itself) and the model index of the body
+    std::vector<std::vector<dynamics::ChainElem>> chains;
+    std::vector<int> index;
+    int next = bodyBase;
+    for (const auto& bp : s.mBodies) {
+      chains.push_back(dynamics::JointChainAccess::chain(*bp->mJoint));
+      next += (int)chains.back().size();
+      index.push_back(next - 1);
+    }
     for (std::size_t k = 0; k < s.mBodies.size(); k++) {
       const auto& b = *s.mBodies[k];
       const auto& j = *b.mJoint;
       int parent = -1;
       for (std::size_t q = 0; q < s.mBodies.size(); q++)
-        if (s.mBodies[q].get() == b.mParent) parent = bodyBase + (int)q;
+        if (s.mBodies[q].get() == b.mParent) parent = index[q];
       if (b.mParent && parent < 0) throw std::invalid_argument("describe: parent body of another skeleton");
-      mI32[PARENT].push_back(parent);
-      mI32[SKEL].push_back((int32_t)si);
-      mI32[JTYPE].push_back(j.mType);
-      mI32[DOFOFF].push_back(dofBase + (int32_t)j.mDofOffset);
-      mI32[MOBILE].push_back(s.mMobile ? 1 : 0);
-      mF64[TP].insert(mF64[TP].end(), j.mTp.m, j.mTp.m + 12);
-      mF64[TC].insert(mF64[TC].end(), j.mTc.m, j.mTc.m + 12);
-      mF64[AXIS].insert(mF64[AXIS].end(), j.mAxis.begin(), j.mAxis.end());
-      mF64[MASS].push_back(b.mMass);
-      mF64[COM].insert(mF64[COM].end(), b.mCom.begin(), b.mCom.end());
-      mF64[MOMENT].insert(mF64[MOMENT].end(), b.mMoment.begin(), b.mMoment.end());
-      mF64[FRIC].push_back(b.mFriction);
-      mF64[REST].push_back(b.mRestitution);
+      const auto& ch = chains[k];
+      for (std::size_t e = 0; e < ch.size(); e++) {
+        const bool self = e + 1 == ch.size();  // (the others: massless frames)
+        mI32[PARENT].push_back(e == 0 ? parent : nb - 1);
+        mI32[SKEL].push_back((int32_t)si);
+        mI32[JTYPE].push_back(ch[e].type);
+        mI32[DOFOFF].push_back(dofBase + (int32_t)j.mDofOffset + (int32_t)e);
+        mI32[MOBILE].push_back(s.mMobile ? 1 : 0);
+        mF64[TP].insert(mF64[TP].end(), ch[e].tp.m, ch[e].tp.m + 12);
+        mF64[TC].insert(mF64[TC].end(), ch[e].tc.m, ch[e].tc.m + 12);
+        mF64[AXIS].insert(mF64[AXIS].end(), ch[e].axis.begin(), ch[e].axis.end());
+        mF64[MASS].push_back(self ? b.mMass : 0.0);
+        const Vector3s zero3{{0, 0, 0}};
+        const Vector3s& com = self ? b.mCom : zero3;
+        mF64[COM].insert(mF64[COM].end(), com.begin(), com.end());
+        for (int t = 0; t < 6; t++) mF64[MOMENT].push_back(self ? b.mMoment[t] : 0.0);
+        mF64[FRIC].push_back(b.mFriction);
+        mF64[REST].push_back(b.mRestitution);
+        if (!self) nb++;
+      }
       auto app = [&](int key, const VectorXs& v) { mF64[key].insert(mF64[key].end(), v.begin(), v.end()); };
       app(DAMP, j.mDamping); app(SPRING, j.mSpring); app(RESTPOS, j.mRest);
       app(PLO, j.mPosLo); app(PHI, j.mPosHi); app(VLO, j.mVelLo); app(VHI, j.mVelHi);
       app(FLO, j.mForceLo); app(FHI, j.mForceHi);
       for (const auto& node : b.mShapes) {
         if (!node->mCollision) continue;
-        mI32[SHAPEBODY].push_back(bodyBase + (int32_t)k);
+        mI32[SHAPEBODY].push_back((int32_t)index[k]);
         shapeType.push_back(node->mShape->kind());
         const Vector3s& sz = node->mShape->size();
         mF64[SSHAPE].insert(mF64[SSHAPE].end(), sz.begin(), sz.end());
@@ -231,7 +303,7 @@ const nimble_world_desc& World::describe() {
       }
       nb++;
     }
-    bodyBase += (int)s.mBodies.size();
+    bodyBase = next;
     dofBase += (int)s.getNumDofs();
   }
   if (nb > NIMBLE_MAX_BODIES || dofBase > NIMBLE_MAX_DOFS || (int)shapeType.size() > NIMBLE_MAX_SHAPES)
@@ -393,8 +465,9 @@ bool World::massSelection(std::vector<double>& S) const {
   for (const auto& e : mTunedMass) massOnly = massOnly && e.second == Entry::INERTIA_MASS;
   if (massOnly) return true;
   const std::vector<int> idx = massBodyIndices();
-  std::size_t nb = 0;
-  for (const auto& sk : mSkels) nb += sk->mBodies.size();
+  std::size_t nb = 0;  // the device model's bodies (compound joints' massless frames included)
+  for (const auto& sk : mSkels)
+    for (const auto& b : sk->mBodies) nb += dynamics::JointChainAccess::chain(*b->mJoint).size();
   const std::size_t dims = getMassDims();
   S.assign(nb * 10 * dims, 0.0);
   std::size_t col = 0;
@@ -423,11 +496,14 @@ std::vector<int> World::massBodyIndices() const {
   std::vector<int> idx;
   for (const auto& e : mTunedMass) {
     const dynamics::BodyNode* t = e.first;
+    // (the device model's index: compound joints' massless frames come
+    // before their body, see describe())
     int base = 0, found = -1;
     for (const auto& sk : mSkels) {
-      for (std::size_t k = 0; k < sk->mBodies.size(); k++)
-        if (sk->mBodies[k].get() == t) found = base + (int)k;
-      base += (int)sk->mBodies.size();
+      for (std::size_t k = 0; k < sk->mBodies.size(); k++) {
+        base += (int)dynamics::JointChainAccess::chain(*sk->mBodies[k]->mJoint).size();
+        if (sk->mBodies[k].get() == t) found = base - 1;
+      }
     }
     idx.push_back(found);
   }

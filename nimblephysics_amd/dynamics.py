@@ -28,6 +28,17 @@ JOINT_PRISMATIC = 2
 JOINT_FREE = 3
 JOINT_BALL = 4           # BallJoint.cpp: exponential coordinates, identity Jacobian
 JOINT_TRANSLATIONAL = 5  # TranslationalJoint.cpp: R3 offset
+# Multi-dof joints whose relative transform is a product of elementary axis
+# rotations / translations with constant axes: the device model steps each as
+# the equivalent chain of 1-dof joints through massless frames (Joint.chain),
+# which has the same transform, motion subspace (velocities are the
+# coordinate rates, GenericJoint), Euclidean integration and identity posPos /
+# velPos blocks as the reference's joint
+JOINT_UNIVERSAL = 6  # UniversalJoint.cpp:193: T_pj R(axis1, q0) R(axis2, q1) T_cj^-1
+JOINT_EULER = 7      # EulerJoint.cpp:1333, :242: T_pj euler_<order>(q * flip) T_cj^-1
+JOINT_PLANAR = 8     # PlanarJoint.cpp:296: T_pj Trans(t1 q0) Trans(t2 q1) R(r, q2) T_cj^-1
+COMPOUND_JOINTS = (JOINT_UNIVERSAL, JOINT_EULER, JOINT_PLANAR)
+_EULER_AXES = {"XYZ": (0, 1, 2), "ZYX": (2, 1, 0), "ZXY": (2, 0, 1), "XZY": (0, 2, 1)}  # Geometry.cpp:1767 ff.
 
 SHAPE_BOX = 0
 SHAPE_SPHERE = 1
@@ -207,10 +218,93 @@ class Joint:
         self.force_hi = np.full(n, INF)
         self.initial_positions = np.zeros(n)
         self.dof_offset = 0
+        self.axis1, self.axis2 = np.array([1.0, 0.0, 0.0]), np.array([0.0, 1.0, 0.0])
+        self.axis_order, self.flip = "XYZ", np.ones(3)
+        self.trans1, self.trans2, self.rot = np.array([1.0, 0, 0]), np.array([0, 1.0, 0]), np.array([0, 0, 1.0])
 
     def getNumDofs(self) -> int:
         return {JOINT_WELD: 0, JOINT_REVOLUTE: 1, JOINT_PRISMATIC: 1, JOINT_FREE: 6, JOINT_BALL: 3,
-                JOINT_TRANSLATIONAL: 3}[self.kind]
+                JOINT_TRANSLATIONAL: 3, JOINT_UNIVERSAL: 2, JOINT_EULER: 3, JOINT_PLANAR: 3}[self.kind]
+
+    # --- UniversalJoint / EulerJoint / PlanarJoint properties (defaults as
+    # UniversalJointAspect: axes x, y; EulerJointAspect: XYZ, no flips;
+    # PlanarJointAspect: the XY plane) and their 1-dof chains
+    def setAxis1(self, axis):
+        a = np.asarray(axis, dtype=np.float64)
+        self.axis1 = a / np.linalg.norm(a)
+        _model_changed(self.skel)
+
+    def setAxis2(self, axis):
+        a = np.asarray(axis, dtype=np.float64)
+        self.axis2 = a / np.linalg.norm(a)
+        _model_changed(self.skel)
+
+    def getAxis1(self):
+        return self.axis1.copy()
+
+    def getAxis2(self):
+        return self.axis2.copy()
+
+    def setAxisOrder(self, order):
+        order = getattr(order, "name", order)
+        if order not in _EULER_AXES:
+            raise ValueError(f"EulerJoint axis order {order!r}")
+        self.axis_order = order
+        _model_changed(self.skel)
+
+    def getAxisOrder(self):
+        return self.axis_order
+
+    def setFlipAxisMap(self, flip):
+        self.flip = np.asarray(flip, dtype=np.float64).reshape(3).copy()
+        _model_changed(self.skel)
+
+    def _set_plane(self, t1, t2, r):
+        self.trans1, self.trans2, self.rot = (np.asarray(v, dtype=np.float64) for v in (t1, t2, r))
+        _model_changed(self.skel)
+
+    def setXYPlane(self):  # PlanarJointAspect.cpp:88
+        self._set_plane([1, 0, 0], [0, 1, 0], [0, 0, 1])
+
+    def setYZPlane(self):
+        self._set_plane([0, 1, 0], [0, 0, 1], [1, 0, 0])
+
+    def setZXPlane(self):
+        self._set_plane([0, 0, 1], [1, 0, 0], [0, 1, 0])
+
+    def setArbitraryPlane(self, transAxis1, transAxis2):
+        """PlanarJointUniqueProperties::setArbitraryPlane: normalised, the
+        second axis orthogonalised against the first, rotation about their
+        cross product."""
+        t1 = np.asarray(transAxis1, dtype=np.float64)
+        t1 = t1 / np.linalg.norm(t1)
+        t2 = np.asarray(transAxis2, dtype=np.float64)
+        t2 = t2 / np.linalg.norm(t2)
+        d = float(t1 @ t2)
+        if abs(d) > 1e-6:
+            t2 = t2 - d * t1
+            t2 = t2 / np.linalg.norm(t2)
+        r = np.cross(t1, t2)
+        self._set_plane(t1, t2, r / np.linalg.norm(r))
+
+    def chain(self):
+        """The joint as 1-dof joints in series, [(kind, axis, T_parent,
+        T_child)]: the first takes the joint's parent transform, the last its
+        child transform, the frames between are the identity (the product of
+        the elementary transforms is the reference's relative transform)."""
+        if self.kind == JOINT_UNIVERSAL:
+            elems = [(JOINT_REVOLUTE, self.axis1), (JOINT_REVOLUTE, self.axis2)]
+        elif self.kind == JOINT_EULER:
+            elems = [(JOINT_REVOLUTE, np.eye(3)[a] * self.flip[i]) for i, a in enumerate(_EULER_AXES[self.axis_order])]
+        elif self.kind == JOINT_PLANAR:
+            elems = [(JOINT_PRISMATIC, self.trans1), (JOINT_PRISMATIC, self.trans2), (JOINT_REVOLUTE, self.rot)]
+        else:
+            return [(self.kind, self.axis, self.T_parent, self.T_child)]
+        out = []
+        for i, (k, a) in enumerate(elems):
+            out.append((k, np.asarray(a, dtype=np.float64), self.T_parent if i == 0 else np.eye(4),
+                        self.T_child if i == len(elems) - 1 else np.eye(4)))
+        return out
 
     def getName(self):
         return self.name
@@ -378,6 +472,15 @@ class Skeleton:
 
     def createTranslationalJointAndBodyNodePair(self, parent=None, joint_name=None, body_name=None):
         return self._create(JOINT_TRANSLATIONAL, parent, joint_name, body_name)
+
+    def createUniversalJointAndBodyNodePair(self, parent=None, joint_name=None, body_name=None):
+        return self._create(JOINT_UNIVERSAL, parent, joint_name, body_name)
+
+    def createEulerJointAndBodyNodePair(self, parent=None, joint_name=None, body_name=None):
+        return self._create(JOINT_EULER, parent, joint_name, body_name)
+
+    def createPlanarJointAndBodyNodePair(self, parent=None, joint_name=None, body_name=None):
+        return self._create(JOINT_PLANAR, parent, joint_name, body_name)
 
     def createWeldJointAndBodyNodePair(self, parent=None, joint_name=None, body_name=None):
         return self._create(JOINT_WELD, parent, joint_name, body_name)

@@ -283,7 +283,7 @@ class World:
         num_bodies]); otherwise a [num_bodies * 10, getMassDims()] matrix
         taking nimble_backward_inertia's INERTIA_FULL-ordered parameters to
         the mass vector (COM_MU: the beta-weighted COM components)."""
-        order = [b for s in self.skeletons for b in s.bodies]
+        order = [e[2] for e in self._model_bodies()]
         idx = [next(i for i, o in enumerate(order) if o is b) for b, _, _, _ in self._mass_tuned]
         if all(k == "INERTIA_MASS" for _, k, _, _ in self._mass_tuned):
             return True, idx
@@ -302,24 +302,36 @@ class World:
                 col += 1
         return False, S
 
+    def _model_bodies(self):
+        """The device model's bodies in order: (skeleton index, skeleton,
+        BodyNode or None, owning BodyNode, chain element): every BodyNode, a
+        UniversalJoint / EulerJoint / PlanarJoint child preceded by the
+        massless frames of its 1-dof chain (dynamics.Joint.chain; None in the
+        third field), the chain's last element on the BodyNode itself."""
+        out = []
+        for si, s in enumerate(self.skeletons):
+            for b in s.bodies:
+                ch = b.joint.chain()
+                for k, e in enumerate(ch):
+                    out.append((si, s, b if k == len(ch) - 1 else None, b, e))
+        return out
+
     def _mass_body_indices(self):
         """Global body index (device model order) of each tuned mass entry."""
-        order = [b for s in self.skeletons for b in s.bodies]
+        order = [e[2] for e in self._model_bodies()]
         return [next(i for i, o in enumerate(order) if o is b) for b, _, _, _ in self._mass_tuned]
 
     # --- flattening -----------------------------------------------------------------------
     def desc_arrays(self) -> Dict[str, np.ndarray]:
-        bodies = []
-        for si, s in enumerate(self.skeletons):
-            for b in s.bodies:
-                bodies.append((si, s, b))
-        nb = len(bodies)
+        model = self._model_bodies()
+        nb = len(model)
         n = self.getNumDofs()
         if nb > NIMBLE_MAX_BODIES or n > NIMBLE_MAX_DOFS:
             raise ValueError(f"model too large: {nb} bodies / {n} dofs (max {NIMBLE_MAX_BODIES}/{NIMBLE_MAX_DOFS})")
         index = {}
-        for k, (si, s, b) in enumerate(bodies):
-            index[id(b)] = k
+        for k, (si, s, b, owner, _) in enumerate(model):
+            if b is not None:
+                index[id(b)] = k
         dof_base = {}
         c = 0
         for s in self.skeletons:
@@ -332,21 +344,27 @@ class World:
         A: Dict[str, list] = {k: [] for k in (
             "parent", "skeleton", "joint_type", "dof_offset", "skeleton_mobile", "T_parent_joint",
             "T_child_joint", "axis", "mass", "com", "moment", "friction", "restitution")}
-        for si, s, b in bodies:
-            j = b.joint
-            A["parent"].append(index[id(b.parent)] if b.parent is not None else -1)
+        prev = None
+        for k, (si, s, b, owner, (kind, axis, Tp, Tc)) in enumerate(model):
+            j = owner.joint
+            first = prev is None or prev[3] is not owner
+            pos = 0 if first else pos + 1
+            # (a chain's first element hangs from the owner's parent, the
+            # others from the previous element's massless frame)
+            A["parent"].append((index[id(owner.parent)] if owner.parent is not None else -1) if first else k - 1)
             A["skeleton"].append(si)
-            A["joint_type"].append(j.kind)
-            A["dof_offset"].append(dof_base[id(s)] + j.dof_offset)
+            A["joint_type"].append(kind)
+            A["dof_offset"].append(dof_base[id(s)] + j.dof_offset + pos)
             A["skeleton_mobile"].append(1 if s.mobile else 0)
-            A["T_parent_joint"].append(t12(j.T_parent))
-            A["T_child_joint"].append(t12(j.T_child))
-            A["axis"].append(j.axis)
-            A["mass"].append(b.mass)
-            A["com"].append(b.com)
-            A["moment"].append(b.moment)
-            A["friction"].append(b.friction)
-            A["restitution"].append(b.restitution)
+            A["T_parent_joint"].append(t12(Tp))
+            A["T_child_joint"].append(t12(Tc))
+            A["axis"].append(axis)
+            A["mass"].append(b.mass if b is not None else 0.0)
+            A["com"].append(b.com if b is not None else np.zeros(3))
+            A["moment"].append(b.moment if b is not None else np.zeros(6))
+            A["friction"].append(owner.friction)
+            A["restitution"].append(owner.restitution)
+            prev = (si, s, b, owner)
         per_dof = {k: [] for k in ("damping", "spring", "rest_position", "pos_lower", "pos_upper", "vel_lower",
                                     "vel_upper", "force_lower", "force_upper")}
         attr = {"damping": "damping", "spring": "spring", "rest_position": "rest", "pos_lower": "pos_lo",
@@ -357,7 +375,9 @@ class World:
                 for k, a in attr.items():
                     per_dof[k].extend(list(getattr(b.joint, a)))
         shapes = []
-        for si, s, b in bodies:
+        for si, s, b, _, _ in model:
+            if b is None:
+                continue
             for node in b.shape_nodes:
                 if node.collision:
                     shapes.append((index[id(b)], node))

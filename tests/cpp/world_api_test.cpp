@@ -77,9 +77,97 @@ static simulation::WorldPtr pendulumWorld() {
   return world;
 }
 
+static Isometry3 tr(double x, double y, double z) {
+  Isometry3 T = Isometry3::Identity();
+  T.setTranslation({x, y, z});
+  return T;
+}
+static void boxBody(dynamics::BodyNode* b, double m, double sx, double sy, double sz) {
+  b->setMass(m);
+  b->setMomentOfInertia(m * (sy * sy + sz * sz) / 12, m * (sx * sx + sz * sz) / 12, m * (sx * sx + sy * sy) / 12);
+  b->createShapeNodeWith<dynamics::CollisionAspect>(std::make_shared<dynamics::BoxShape>(Vector3s{sx, sy, sz}));
+}
+static void addGround(simulation::WorldPtr& world) {
+  auto ground = dynamics::Skeleton::create("ground");
+  auto gp = ground->createJointAndBodyNodePair<dynamics::WeldJoint>();
+  gp.first->setTransformFromParentBodyNode(tr(0, -0.05, 0));
+  gp.second->createShapeNodeWith<dynamics::CollisionAspect>(std::make_shared<dynamics::BoxShape>(Vector3s{10.0, 0.1, 10.0}));
+  ground->setMobile(false);
+  world->addSkeleton(ground);
+}
+
+// tests/models.py ball_world: translational root, two ball joints, a revolute ankle
+static simulation::WorldPtr ballWorld() {
+  auto world = simulation::World::create();
+  world->setGravity({0, -9.81, 0});
+  auto rig = dynamics::Skeleton::create("rig");
+  dynamics::Joint::Properties jp;
+  dynamics::BodyNode::Properties bp;
+  bp.mName = "base";
+  auto base = rig->createJointAndBodyNodePair<dynamics::TranslationalJoint>(nullptr, jp, bp);
+  boxBody(base.second, 2.0, 0.3, 0.2, 0.3);
+  jp.mName = "hip";
+  bp.mName = "leg";
+  auto leg = rig->createJointAndBodyNodePair<dynamics::BallJoint>(base.second, jp, bp);
+  leg.first->setTransformFromParentBodyNode(tr(0, -0.15, 0));
+  leg.first->setTransformFromChildBodyNode(tr(0, 0.2, 0));
+  boxBody(leg.second, 1.0, 0.1, 0.4, 0.1);
+  jp.mName = "ankle";
+  bp.mName = "foot";
+  auto foot = rig->createJointAndBodyNodePair<dynamics::RevoluteJoint>(leg.second, jp, bp);
+  foot.first->setAxis({0, 0, 1});
+  foot.first->setTransformFromParentBodyNode(tr(0, -0.2, 0));
+  foot.first->setTransformFromChildBodyNode(tr(0, 0.05, 0));
+  boxBody(foot.second, 0.5, 0.2, 0.1, 0.3);
+  jp.mName = "shoulder";
+  bp.mName = "arm";
+  auto arm = rig->createJointAndBodyNodePair<dynamics::BallJoint>(base.second, jp, bp);
+  arm.first->setTransformFromParentBodyNode(tr(0.15, 0, 0));
+  arm.first->setTransformFromChildBodyNode(tr(-0.12, 0, 0));
+  boxBody(arm.second, 0.3, 0.24, 0.05, 0.05);
+  world->addSkeleton(rig);
+  addGround(world);
+  return world;
+}
+
+// tests/models.py compound_world: planar root, universal shoulder, Euler (ZYX,
+// flipped y) wrist
+static simulation::WorldPtr compoundWorld() {
+  auto world = simulation::World::create();
+  world->setGravity({0, -9.81, 0});
+  auto rig = dynamics::Skeleton::create("rig");
+  dynamics::Joint::Properties jp;
+  dynamics::BodyNode::Properties bp;
+  bp.mName = "sled";
+  auto sled = rig->createJointAndBodyNodePair<dynamics::PlanarJoint>(nullptr, jp, bp);
+  sled.first->setXYPlane();
+  boxBody(sled.second, 2.0, 0.4, 0.2, 0.4);
+  jp.mName = "shoulder";
+  bp.mName = "arm";
+  auto arm = rig->createJointAndBodyNodePair<dynamics::UniversalJoint>(sled.second, jp, bp);
+  arm.first->setAxis1({0, 0, 1});
+  arm.first->setAxis2({1, 0, 0});
+  arm.first->setTransformFromParentBodyNode(tr(0, -0.1, 0));
+  arm.first->setTransformFromChildBodyNode(tr(0, 0.25, 0));
+  boxBody(arm.second, 0.8, 0.1, 0.5, 0.1);
+  jp.mName = "wrist";
+  bp.mName = "hand";
+  auto hand = rig->createJointAndBodyNodePair<dynamics::EulerJoint>(arm.second, jp, bp);
+  hand.first->setAxisOrder(dynamics::EulerJoint::AxisOrder::ZYX);
+  hand.first->setFlipAxisMap({1.0, -1.0, 1.0});
+  hand.first->setTransformFromParentBodyNode(tr(0, -0.25, 0));
+  hand.first->setTransformFromChildBodyNode(tr(0, 0.06, 0));
+  boxBody(hand.second, 0.4, 0.2, 0.12, 0.2);
+  world->addSkeleton(rig);
+  addGround(world);
+  return world;
+}
+
 static simulation::WorldPtr makeWorld(const std::string& name) {
   if (name == "box") return boxWorld();
   if (name == "pendulum") return pendulumWorld();
+  if (name == "ballrig") return ballWorld();
+  if (name == "compound") return compoundWorld();
   throw std::invalid_argument("unknown world " + name);
 }
 

@@ -587,3 +587,63 @@ def ball_states(batch, seed=0, contact=True):
     q[:, 7:10] = 0.6 * rng.standard_normal((batch, 3))
     f = 0.5 * rng.standard_normal((batch, 10))
     return np.concatenate([q, v], axis=1), f
+
+
+def compound_world(ground=True):
+    """A rig on the reference's compound joints: a sled on a PlanarJoint
+    (root, XY plane: x, y translation, rotation about z), an arm hanging
+    from it on a UniversalJoint (axes z, x), a hand on an EulerJoint (ZYX,
+    flip map (1, -1, 1)) at the arm's end, resting on a static ground box
+    (top face at y = 0) when `ground`."""
+    from nimblephysics_amd import dynamics as D
+
+    def tr(x, y, z):
+        T = np.eye(4)
+        T[:3, 3] = [x, y, z]
+        return T
+
+    def box(b, m, sx, sy, sz):
+        b.setMass(m)
+        b.setMomentOfInertia(m * (sy * sy + sz * sz) / 12, m * (sx * sx + sz * sz) / 12, m * (sx * sx + sy * sy) / 12)
+        b.createShapeNode(D.BoxShape([sx, sy, sz]), collision=True)
+
+    w = nimble.World()
+    w.setGravity([0, -9.81, 0])
+    rig = D.Skeleton("rig")
+    pj, sled = rig.createPlanarJointAndBodyNodePair(body_name="sled")
+    pj.setXYPlane()
+    box(sled, 2.0, 0.4, 0.2, 0.4)
+    uj, arm = rig.createUniversalJointAndBodyNodePair(sled, joint_name="shoulder", body_name="arm")
+    uj.setAxis1([0, 0, 1])
+    uj.setAxis2([1, 0, 0])
+    uj.setTransformFromParentBodyNode(tr(0, -0.1, 0))
+    uj.setTransformFromChildBodyNode(tr(0, 0.25, 0))
+    box(arm, 0.8, 0.1, 0.5, 0.1)
+    ej, hand = rig.createEulerJointAndBodyNodePair(arm, joint_name="wrist", body_name="hand")
+    ej.setAxisOrder("ZYX")
+    ej.setFlipAxisMap([1.0, -1.0, 1.0])
+    ej.setTransformFromParentBodyNode(tr(0, -0.25, 0))
+    ej.setTransformFromChildBodyNode(tr(0, 0.06, 0))
+    box(hand, 0.4, 0.2, 0.12, 0.2)
+    w.addSkeleton(rig)
+    if ground:
+        g = D.Skeleton("ground")
+        gj, gb = g.createWeldJointAndBodyNodePair()
+        gj.setTransformFromParentBodyNode(tr(0, -0.05, 0))
+        gb.createShapeNode(D.BoxShape([10.0, 0.1, 10.0]), collision=True)
+        g.setMobile(False)
+        w.addSkeleton(g)
+    return w
+
+
+def compound_states(batch, seed=0, contact=True):
+    """compound_world states (dofs: sled x y rot, shoulder 2, wrist 3): the
+    hand's sole ~1 mm into the ground (sled at 0.719 m) when `contact`, else
+    0.3 m higher; small rotations, small velocities, random forces."""
+    rng = np.random.default_rng(seed)
+    q = 0.01 * rng.standard_normal((batch, 8))
+    v = 0.05 * rng.standard_normal((batch, 8))
+    q[:, 1] = (0.719 if contact else 1.02) + 2e-4 * rng.standard_normal(batch)
+    q[:, 5:8] = 0.01 * rng.standard_normal((batch, 3))
+    f = 0.5 * rng.standard_normal((batch, 8))
+    return np.concatenate([q, v], axis=1), f

@@ -21,20 +21,30 @@ from test_gpu_jacobians import _batched, _fd_mask, _jac_err
 
 pytestmark = pytest.mark.gpu
 
+# UniversalJoint / EulerJoint / PlanarJoint go to the device as their 1-dof
+# chains through massless frames (dynamics.Joint.chain); the chains'
+# transforms are pinned to the reference's formulas and the oracle's
+# gradients to central differences in test_oracle_pins.py (compound_*)
+RIGS = {"ball": (models.ball_world, models.ball_states), "compound": (models.compound_world, models.compound_states)}
 
+
+@pytest.mark.parametrize("rig", sorted(RIGS))
 @pytest.mark.parametrize("contact", [False, True])
-def test_ball_rig_parity(contact):
-    world = models.ball_world(ground=contact)
-    st, f = models.ball_states(128, seed=21, contact=contact)
+def test_rig_parity(rig, contact):
+    make, states = RIGS[rig]
+    world = make(ground=contact)
+    st, f = states(128, seed=21, contact=contact)
     ow, snap = _parity(world, st, f)
     if contact:
         assert (snap[:, 0] > 0).mean() > 0.9  # the foot on the ground
 
 
+@pytest.mark.parametrize("rig", sorted(RIGS))
 @pytest.mark.parametrize("contact", [False, True])
-def test_ball_rig_jacobians(contact):
-    world = models.ball_world(ground=contact)
-    st, f = models.ball_states(32, seed=5, contact=contact)
+def test_rig_jacobians(rig, contact):
+    make, states = RIGS[rig]
+    world = make(ground=contact)
+    st, f = states(32, seed=5, contact=contact)
     ow = O.OracleWorld(world)
     ow.forward(st, f)
     RJ, RF = ow.jacobians()
@@ -42,7 +52,7 @@ def test_ball_rig_jacobians(contact):
     J = snap.getStateJacobian(world).cpu().numpy()
     F = snap.getActionJacobian(world).cpu().numpy()
     mask = _fd_mask(world)
-    assert mask.sum() == 2 * 2 * 9  # two ball joints: 3 x 3 posPos and velPos blocks each
+    assert mask.sum() == (2 * 2 * 9 if rig == "ball" else 0)  # ball joints: 3 x 3 posPos and velPos blocks
     checked = 0
     for b in range(st.shape[0]):
         fl = O.lcp_flags(ow, b)

@@ -612,3 +612,59 @@ def test_ball_joint_integration_matches_rotation_composition(oracle_built):
         for o in (3, 7):
             want = logm(expm(q[o:o + 3]) @ expm(v[o:o + 3] * dt))
             assert np.allclose(nxt[b, o:o + 3], want, rtol=0, atol=1e-12), (b, o)
+
+
+def _rot(axis, a):
+    axis = np.asarray(axis, dtype=np.float64)
+    K = np.array([[0, -axis[2], axis[1]], [axis[2], 0, -axis[0]], [-axis[1], axis[0], 0]])
+    return np.eye(3) + np.sin(a) * K + (1 - np.cos(a)) * K @ K
+
+
+def _iso(R=np.eye(3), p=(0, 0, 0)):
+    T = np.eye(4)
+    T[:3, :3] = R
+    T[:3, 3] = p
+    return T
+
+
+def test_compound_joint_transforms_match_reference_formulas(oracle_built):
+    """The 1-dof chains the device model steps UniversalJoint, EulerJoint and
+    PlanarJoint as (dynamics.Joint.chain) against the reference's relative
+    transforms: PlanarJoint.cpp:296 T_pj Trans(t1 q0) Trans(t2 q1)
+    expAngular(r q2) T_cj^-1, UniversalJoint.cpp:193 T_pj AngleAxis(q0, a1)
+    AngleAxis(q1, a2) T_cj^-1, EulerJoint.cpp:1333 with eulerZYXToMatrix(q *
+    flip) = Rz Ry Rx (Geometry.cpp) -- the world transforms of the rig's real
+    bodies at random coordinates.  The transform as a function of q fixes the
+    motion subspace (GenericJoint velocities are the coordinate rates), the
+    mass matrix and the bias forces, so the chain is the reference's joint."""
+    w = models.compound_world(ground=False)
+    o = O.OracleWorld(w)
+    rng = np.random.default_rng(4)
+    for _ in range(5):
+        q = rng.standard_normal(8)
+        Tw = o.body_transforms(q)  # device-model bodies: sled chain 0-2, arm chain 3-4, hand chain 5-7
+        sled = _iso(_rot([0, 0, 1], q[2]), [q[0], q[1], 0.0])
+        arm = sled @ _iso(p=[0, -0.1, 0]) @ _iso(_rot([0, 0, 1], q[3]) @ _rot([1, 0, 0], q[4])) @ _iso(p=[0, -0.25, 0])
+        a = q[5:8] * np.array([1.0, -1.0, 1.0])
+        hand = arm @ _iso(p=[0, -0.25, 0]) @ _iso(_rot([0, 0, 1], a[0]) @ _rot([0, 1, 0], a[1]) @ _rot([1, 0, 0], a[2])) \
+            @ _iso(p=[0, -0.06, 0])
+        for k, T in ((2, sled), (4, arm), (7, hand)):
+            assert np.abs(Tw[k] - T[:3, :4]).max() <= 1e-13, (k, np.abs(Tw[k] - T[:3, :4]).max())
+
+
+@pytest.mark.parametrize("contact", [False, True])
+def test_compound_gradients_vs_finite_differences(oracle_built, contact):
+    """UniversalJoint / EulerJoint / PlanarJoint (as their 1-dof chains): the
+    oracle's analytic gradients of the compound rig against central
+    differences of its own step, in the air and with the hand on the ground."""
+    w = models.compound_world(ground=contact)
+    st, f = models.compound_states(4, seed=3, contact=contact)
+    o = O.OracleWorld(w)
+    o.forward(st, f)
+    if contact:
+        assert all(o.num_contacts(b) > 0 for b in range(4))
+    for b in range(2):
+        g = np.random.default_rng(20 + b).standard_normal(st.shape[1])
+        gs, gf, fd_s, fd_f = _fd_check(w, st[b], f[b], g)
+        assert np.abs(gs - fd_s).max() <= 1e-6 * np.abs(fd_s).max(), (b, np.abs(gs - fd_s).max())
+        assert np.abs(gf - fd_f).max() <= 1e-6 * np.abs(fd_f).max(), (b, np.abs(gf - fd_f).max())

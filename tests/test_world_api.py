@@ -60,7 +60,8 @@ def pendulum_world():
     return w
 
 
-WORLDS = {"box": models.box_world, "pendulum": pendulum_world}
+WORLDS = {"box": models.box_world, "pendulum": pendulum_world, "ballrig": models.ball_world,
+          "compound": models.compound_world}
 
 
 @pytest.mark.parametrize("name", sorted(WORLDS))
@@ -74,10 +75,14 @@ def test_cpp_world_describes_like_python(name):
         assert np.array_equal(a.reshape(-1), b.reshape(-1)), k
 
 
-def _inputs(world, seed):
+def _inputs(world, seed, name=None):
     n = world.getNumDofs()
     rng = np.random.default_rng(seed)
-    if n == 6:  # the box resting ~1 mm into the ground
+    rigs = {"ballrig": models.ball_states, "compound": models.compound_states}
+    if name in rigs:  # the rig's foot / hand on the ground
+        st, f = rigs[name](1, seed=seed)
+        st, f = st[0], f[0]
+    elif n == 6:  # the box resting ~1 mm into the ground
         st, f = models.box_states("rest", 1, seed=seed)
         st, f = st[0], f[0]
     else:
@@ -93,7 +98,7 @@ def test_cpp_world_steps_match_oracle(name):
     from oracle.oracle import OracleWorld
     world = WORLDS[name]()
     n = world.getNumDofs()
-    st, f, g = _inputs(world, 3)
+    st, f, g = _inputs(world, 3, name)
     txt = " ".join(repr(float(x)) for x in np.concatenate([st, f, g]))
     out = _run("step", name, stdin=txt)
     ow = OracleWorld(world)

@@ -415,8 +415,10 @@ def measure(wl, batch, steps, warmup, dist, rank, ws, dev, gather):
     dom = "backward" if bwd_ms >= fwd_ms else "forward"
     dom_ms = max(bwd_ms, fwd_ms)
     achieved = flops[dom] * batch / (dom_ms * 1e-3) / 1e12
-    traffic, traffic_src = pmc_traffic(wl, [f"nimble_{dom}_kernel"] + ([f"nimble_{dom}_wide_kernel"]
-                                                                      if wl == "atlas_mesh" else []), batch)
+    # (models with mesh colliders run the one-row forward as its mesh instance)
+    one_row = "nimble_forward_mesh_kernel" if (dom == "forward" and wl == "atlas_mesh") else f"nimble_{dom}_kernel"
+    traffic, traffic_src = pmc_traffic(wl, [one_row] + ([f"nimble_{dom}_wide_kernel"] if wl == "atlas_mesh" else []),
+                                       batch)
     out.update(cstats=cstats, fwd_ms=fwd_ms, bwd_ms=bwd_ms, dom=dom, achieved=achieved, flops=flops,
                traffic=traffic, traffic_src=traffic_src)
     sc = cstats.get("solver_counts")
@@ -453,12 +455,13 @@ def roofline(r, wl):
 def mesh_report(args, mesh):
     """The `atlas_mesh` object: the reference atlas_bench's own model."""
     mf = mesh["flops"]
-    kern = {"forward": "nimble_forward_kernel + nimble_forward_wide_kernel",
+    kern = {"forward": "nimble_forward_mesh_kernel + nimble_forward_wide_kernel",
             "backward": "nimble_backward_kernel + nimble_backward_wide_kernel"}[mesh["dom"]]
     out = {"workload": mesh["wl_name"], "metric": mesh["metric"], "value": mesh["value"], "unit": "timesteps/s",
            "ms_per_step": mesh["ms_per_step"], "steps": min(args.steps, 20),
            "kernels_ms": {"forward": mesh["fwd_ms"], "backward": mesh["bwd_ms"],
-                          "note": "forward = nimble_forward_kernel + nimble_forward_wide_kernel (the worlds the "
+                          "note": "forward = nimble_forward_mesh_kernel (the one-row forward's instance for models "
+                                  "with mesh colliders) + nimble_forward_wide_kernel (the worlds the "
                                   "one-row kernel defers), backward likewise; per-kernel split in "
                                   "profiles/*kernel_stats_atlas_mesh*"},
            "contacts_per_world": mesh["cstats"]["contacts"], "lcp_rows_per_world": mesh["cstats"]["rows"],

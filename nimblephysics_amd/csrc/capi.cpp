@@ -50,6 +50,8 @@ struct nimble_world {
 
 extern "C" __global__ void nimble_forward_kernel(const ModelDev*, Layout, const double*, const double*, double*,
                                                  double*, double*, int, int, int, int);
+extern "C" __global__ void nimble_forward_mesh_kernel(const ModelDev*, Layout, const double*, const double*, double*,
+                                                      double*, double*, int, int, int, int);
 extern "C" __global__ void nimble_forward_wide_kernel(const ModelDev*, Layout, const double*, const double*, double*,
                                                       double*, double*, int, int, int);
 extern "C" __global__ void nimble_backward_kernel(const ModelDev*, int, const double*, const double*,
@@ -481,10 +483,18 @@ int nimble_forward(nimble_world_t w, int32_t batch, const double* state, const d
     // (contact.cuh deferEntry): only their counters are reset here
     if (wide && largestFirst)
       HIP_TRY(hipMemsetAsync(snapshot + (size_t)b0 * w->snapDoubles + SN_DEFERCNT, 0, DEFER_BUCKETS * sizeof(int), st));
-    hipLaunchKernelGGL(nimble_forward_kernel, dim3(cnt), dim3(fwdThreads), lds, st, w->dev, w->fwd,
-                       state + b0 * 2 * n, forces + b0 * n, lcp_cache + (size_t)b0 * w->cacheDoubles,
-                       next_state + b0 * 2 * n, snapshot + (size_t)b0 * w->snapDoubles, w->snapDoubles,
-                       w->cacheDoubles, w->fwdDeferRows, wide && largestFirst ? 1 : 0);
+    // (models with mesh colliders: the instance with the mesh-box narrow
+    // phase inlined on the helper)
+    if (w->host.hasMesh)
+      hipLaunchKernelGGL(nimble_forward_mesh_kernel, dim3(cnt), dim3(fwdThreads), lds, st, w->dev, w->fwd,
+                         state + b0 * 2 * n, forces + b0 * n, lcp_cache + (size_t)b0 * w->cacheDoubles,
+                         next_state + b0 * 2 * n, snapshot + (size_t)b0 * w->snapDoubles, w->snapDoubles,
+                         w->cacheDoubles, w->fwdDeferRows, wide && largestFirst ? 1 : 0);
+    else
+      hipLaunchKernelGGL(nimble_forward_kernel, dim3(cnt), dim3(fwdThreads), lds, st, w->dev, w->fwd,
+                         state + b0 * 2 * n, forces + b0 * n, lcp_cache + (size_t)b0 * w->cacheDoubles,
+                         next_state + b0 * 2 * n, snapshot + (size_t)b0 * w->snapDoubles, w->snapDoubles,
+                         w->cacheDoubles, w->fwdDeferRows, wide && largestFirst ? 1 : 0);
     HIP_TRY(hipGetLastError());
     // the worlds whose LCP pool the one-row kernel does not hold on chip (or
     // more rows than the test threshold): stepped by the big-LDS wide kernel

@@ -206,6 +206,10 @@ __device__ __forceinline__ void codFactorR(typename Space<kLds>::dptr Ain, typen
   double* A = c.A;
   const int m = c.m, n = c.n, ld = c.ld;
   double maxPivot = 0.0;
+  // the step the rank-revealing stop ended the QR at (kmax: no stop); the
+  // diagonal past it is unreduced and not R's, so the rank count below
+  // does not read it
+  int stopK = c.kmax;
 #ifndef NIMBLE_COD_LDS_ONLY
   if (m <= 24 && n <= 64) {
     WSYNC();
@@ -251,6 +255,7 @@ __device__ __forceinline__ void codFactorR(typename Space<kLds>::dptr Ain, typen
       if (k > 0 && piv <= 2.220446049250313e-16 * c.kmax * maxPiv) {
         for (int kk = k + lane; kk < c.kmax; kk += WAVE) c.vn[kk] = -1.0;
         WSYNC();
+        stopK = k;
         break;
       }
       maxPiv = piv > maxPiv ? piv : maxPiv;
@@ -433,7 +438,7 @@ rankAndRz:
 #pragma unroll
   for (int s = 0; s < R; s++) {
     const int k = rowAt(s, lane);
-    dkk[s] = k < c.kmax ? fabs(A[k * ld + k]) : 0.0;
+    dkk[s] = k < stopK ? fabs(A[k * ld + k]) : 0.0;
     ndkk[s] = -dkk[s];
   }
   maxPivot = -waveMinR(ndkk);

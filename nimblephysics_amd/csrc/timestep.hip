@@ -313,7 +313,7 @@ __device__ __forceinline__ void coreDynamics(const ModelDev& md, double* s, cons
 // leaves a world whose LCP has more than `deferRows` rows (> 64: more than
 // 21 frictional contacts) to the R = 2 kernel launched after it, which
 // steps only those worlds, from the same inputs.
-template <int R>
+template <int R, bool kMesh = false>
 __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, const Layout& L,
                                              const double* __restrict__ state, const double* __restrict__ forces,
                                              double* __restrict__ lcpCache, double* __restrict__ nextState,
@@ -353,10 +353,10 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
           // (the deadlock guard expired: wave 0 detects the contacts itself)
           if (collideWait(ct, CS_GO, GW_HELPER_GO)) {
 #ifdef NIMBLE_STAGE_TIMING
-            collideWorld<true>(md, lds<true>(s), L, lane, snapshot + (size_t)env * snapDoubles + snEdge(n),
-                               snapshot + (size_t)env * snapDoubles + snStamps(n));
+            collideWorld<kMesh>(md, lds<true>(s), L, lane, snapshot + (size_t)env * snapDoubles + snEdge(n),
+                                snapshot + (size_t)env * snapDoubles + snStamps(n));
 #else
-            collideWorld<true>(md, lds<true>(s), L, lane, snapshot + (size_t)env * snapDoubles + snEdge(n));
+            collideWorld<kMesh>(md, lds<true>(s), L, lane, snapshot + (size_t)env * snapDoubles + snEdge(n));
 #endif
             collidePost(ct, CS_DONE, lane);
           }
@@ -492,6 +492,21 @@ nimble_forward_kernel(const ModelDev* __restrict__ mdp, Layout L, const double* 
                       int cacheDoubles, int deferRows, int deferLists) {
   forwardWorld<1>(mdp, L, state, forces, lcpCache, nextState, snapshot, snapDoubles, cacheDoubles, deferRows,
                   blockIdx.x, deferLists != 0);
+}
+
+// the same step for models with mesh colliders: the helper wave's collision
+// pass with the mesh-box narrow phase inlined (out of line, its prologue
+// saved ~92 callee-saved VGPRs per lane on every mesh pair near contact).  A
+// separate instance because the inlined collider raises the kernel's
+// register pressure everywhere: with it the mesh-free models' forward
+// spilled 115 instead of 43 VGPRs (Scratch_Size 1,872 vs 1,504 B/lane)
+extern "C" __global__ void __launch_bounds__(2 * WAVE) __attribute__((amdgpu_waves_per_eu(2)))
+nimble_forward_mesh_kernel(const ModelDev* __restrict__ mdp, Layout L, const double* __restrict__ state,
+                           const double* __restrict__ forces, double* __restrict__ lcpCache,
+                           double* __restrict__ nextState, double* __restrict__ snapshot, int snapDoubles,
+                           int cacheDoubles, int deferRows, int deferLists) {
+  forwardWorld<1, true>(mdp, L, state, forces, lcpCache, nextState, snapshot, snapDoubles, cacheDoubles, deferRows,
+                        blockIdx.x, deferLists != 0);
 }
 
 // the worlds nimble_forward_kernel deferred (snapshot status ST_DEFERRED),

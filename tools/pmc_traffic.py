@@ -36,7 +36,8 @@ def main():
     wl = sys.argv[4] if len(sys.argv) > 4 else "atlas"
     out = sys.argv[5] if len(sys.argv) > 5 else "profiles/pmc_traffic.json"
     res = {}
-    for k in ("nimble_forward_kernel", "nimble_backward_kernel", "nimble_forward_wide_kernel", "nimble_backward_wide_kernel"):
+    for k in ("nimble_forward_kernel", "nimble_forward_mesh_kernel", "nimble_backward_kernel",
+              "nimble_forward_wide_kernel", "nimble_backward_wide_kernel"):
         fe = [v for n, v in load(fdir, "FETCH_SIZE") if k in n]
         wr = [v for n, v in load(wdir, "WRITE_SIZE") if k in n]
         if not fe or not wr:

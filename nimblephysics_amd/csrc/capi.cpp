@@ -79,6 +79,7 @@ static int ldsPoolRows(const ModelDev& m, int mcap) {
 
 static Layout makeLayout(const ModelDev& m, bool backward, int poolRows) {
   Layout L{};
+  L.early = -1;
   int o = 0;
   auto take = [&](int count) { int r = o; o += (count + 1) & ~1; return r; };
   const int n = m.n, nb = m.nb;
@@ -102,13 +103,16 @@ static Layout makeLayout(const ModelDev& m, bool backward, int poolRows) {
     L.V = take(6 * nb); L.A = take(6 * nb); L.F = take(6 * nb);
     L.IC = -1;  // composite inertias are not needed by the adjoint backward
   } else {
-    // V, A, IC, F last: after the dynamics they are dead and the contact
-    // stage (narrow-phase buffers, then the LCP pool) reuses the space
+    // V, A, IC, F in one area with the contact stage (narrow-phase buffers,
+    // then the LCP pool): after the dynamics they are dead and the pool
+    // reuses the space.  The dynamics buffers sit at the area's far end and
+    // the narrow-phase buffers at its start, so that the helper wave can run
+    // the collision detection, and then build the LCP rows in the pool's
+    // leading rows slots (contact.cuh EA_*), while wave 0 is still in the
+    // dynamics.
     const int dyn = 54 * nb;
-    L.V = o; L.A = o + 6 * nb; L.IC = o + 12 * nb; L.F = o + 48 * nb;
     L.poolCap = 0;
     int area = dyn;
-    L.cscr = o + dyn;
     if (m.numPairs > 0) {
       const int cs = collideScratchDoubles(m.pairChunk, m.hasMesh != 0);
       if (dyn + cs > area) area = dyn + cs;
@@ -117,7 +121,18 @@ static Layout makeLayout(const ModelDev& m, bool backward, int poolRows) {
         if (L.poolCap > area) area = L.poolCap;
       }
     }
+    area = (area + 1) & ~1;
     L.pool = o;
+    L.cscr = o;
+    const int dynOff = area - dyn;
+    L.V = o + dynOff; L.A = L.V + 6 * nb; L.IC = L.V + 12 * nb; L.F = L.V + 48 * nb;
+    // the helper's early rows: when the pool's rows slots for its largest
+    // on-chip LCP end before the dynamics buffers (NIMBLE_AMD_EARLY_ROWS=0:
+    // off, for measurements)
+    L.early = -1;
+    const char* ee = getenv("NIMBLE_AMD_EARLY_ROWS");
+    if (m.numPairs > 0 && poolRows > 0 && fwdPoolRowsDoubles(poolRows, n) <= dynOff && !(ee && atoi(ee) == 0))
+      L.early = 1;
     take(area);
   }
   L.total = o;
@@ -388,8 +403,8 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
               w->wideLds, w->fwdWide.stageCap, need, mc, w->fwdDeferRows);
   }
   if (getenv("NIMBLE_AMD_VERBOSE"))
-    fprintf(stderr, "nimble_amd: LDS forward %d B (pool rows %d), backward %d B (pool rows %d), max rows %d\n",
-            w->fwd.total * 8, fwdRows, w->bwd.total * 8, bwdRows, mcap);
+    fprintf(stderr, "nimble_amd: LDS forward %d B (pool rows %d, early rows at %d), backward %d B (pool rows %d), max rows %d\n",
+            w->fwd.total * 8, fwdRows, w->fwd.early, w->bwd.total * 8, bwdRows, mcap);
   const int poolRows = fwdRows < bwdRows ? fwdRows : bwdRows;
   w->poolRows = poolRows;
   w->maxRows = mcap;

@@ -312,21 +312,35 @@ struct FwdPool {
   double* scr;  // >= 10 m + 2 n + 16
 };
 
+// (rows first: J^T, the rows' directions, boxes and restitution and the int
+// vectors take the pool's first n m + 10 m doubles, which in the one-row
+// kernel lie clear of the dynamics buffers -- the helper's early rows, EA_*)
 __device__ inline void carveFwd(double* base, int m, int n, FwdPool& P) {
   double* p = base;
   P.cols = p; p += n * m;
   P.massed = P.cols;  // Y = L^-1 J^T overwrites J^T in place
-  P.A = p; p += m * m;
-  P.M1 = p; p += m * m;
-  P.M2 = p; p += m * (m | 1);  // Dantzig's L with an odd leading dimension
   // plain member assignments (no pointer-to-member tables) keep the
   // pointers' provenance visible, so LDS-laundered bases stay LDS
   P.lo = p; p += m;
   P.hi = p; p += m;
+  P.rest = p; p += m;
+  P.dvec = p; p += 3 * m;
+  int* ip = reinterpret_cast<int*>(p);
+  P.fi = ip; ip += m;
+  P.rowC = ip; ip += m;
+  P.rowDir = ip; ip += m;
+  P.mapping = ip; ip += m;
+  P.clampIdx = ip; ip += m;
+  P.ubIdx = ip; ip += m;
+  P.clampRow = ip; ip += m;
+  P.cl = ip; ip += m;
+  p += 4 * m;
+  P.A = p; p += m * m;
+  P.M1 = p; p += m * m;
+  P.M2 = p; p += m * (m | 1);  // Dantzig's L with an odd leading dimension
   P.b = p; p += m;
   P.X = p; p += m;
   P.aCol = p; p += m;
-  P.rest = p; p += m;
   P.pen = p; p += m;
   P.relVel = p; p += m;
   P.fc = p; p += m;
@@ -341,17 +355,6 @@ __device__ inline void carveFwd(double* base, int m, int n, FwdPool& P) {
   // penetration-correction terms, dead after the row setup)
   P.xp = P.xc;
   P.xf = P.pen;
-  P.dvec = p; p += 3 * m;
-  int* ip = reinterpret_cast<int*>(p);
-  P.fi = ip; ip += m;
-  P.mapping = ip; ip += m;
-  P.clampIdx = ip; ip += m;
-  P.ubIdx = ip; ip += m;
-  P.rowC = ip; ip += m;
-  P.rowDir = ip; ip += m;
-  P.clampRow = ip; ip += m;
-  P.cl = ip; ip += m;
-  p += 4 * m;
   P.scr = p;
 }
 
@@ -504,6 +507,9 @@ __device__ __forceinline__ bool protocolFailed(double* ct) {
 #define GW_HELPER_IDLE 256  // helper: wave 0 took its DONE
 #define GW_RETIRE 512       // wave 0: the helper's DONE at the world's end
 #define GW_ONE_ROW_ONLY 1024  // (modifier) the sites in the one-row kernel only, not in the wide kernel
+#define GW_EARLY_B 2048       // helper: wave 0 has formed b (early rows, one-row kernel)
+#define GW_EARLY_ROWS 4096    // wave 0: the helper's early rows
+#define GW_EARLY_A 8192       // wave 0: the helper's A = Y^T Y
 __device__ __forceinline__ bool guardForced(double* ct, int site) { return (uni(helperFlags(ct)[2]) & site) != 0; }
 // spin with s_sleep until pred(state); -1 when the guard expired (or was
 // forced at `site`, or the partner failed)
@@ -560,7 +566,7 @@ __device__ __forceinline__ void boardPost(double* ct, int mode, bool warmFinal, 
 
 // Collision detection on the helper wave.  collideWorld only reads the
 // body transforms (kinematics) and writes the contact header / list and its
-// own scratch past the dynamics buffers, so it overlaps wave 0's composite
+// own scratch clear of the dynamics buffers, so it overlaps wave 0's composite
 // inertias, mass matrix, Cholesky factor and unconstrained velocity.  Per
 // world: wave 0 posts CS_GO after the kinematics, the helper answers CS_DONE,
 // wave 0 takes the contacts and resets to CS_IDLE before the next world.
@@ -580,6 +586,51 @@ __device__ __forceinline__ bool collideWait(double* ct, int want, int site) {
   const long long t0 = spinClock();
   for (int it = 0;; it++) {
     if (uni(__hip_atomic_load(collideFlag(ct), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == want) return true;
+    if (protocolFailed(ct) || spinExpired(t0, it)) {
+      protocolFail(ct);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// Early rows (one-row kernel): the helper wave is idle from the end of the
+// collision detection until A is built, while wave 0 is still in the
+// composites, the mass matrix, its Cholesky factor and the unconstrained
+// solve.  So, once the contacts are final, the helper builds the LCP rows and
+// J^T in the LDS pool -- their slots come first in the pool (carveFwd) and
+// the one-row kernel's layout puts the dynamics buffers at the far end of the
+// pool area (capi.cpp makeLayout, Layout::early), so they are clear of
+// everything wave 0 still uses.  Wave 0 forms b = -J v1 from that J^T and
+// posts HF_B (helperFlags(ct)[1], which the board's mode overwrites later);
+// the helper then forms Y = L^-1 J^T in its place and A = Y^T Y, and wave 0,
+// through the penetration terms meanwhile, meets a built A.  Same
+// operations in the same order on the same operands as wave 0's own path,
+// so the same bits.  The helper's progress is the second int of H_COLLIDE
+// (written by the helper only; EA_NONE is stored before its CS_DONE):
+#define EA_PENDING 0  // contacts final, rows in progress
+#define EA_NONE 1     // not taken: wave 0 builds the rows itself
+#define EA_ROWS 2     // rows + J^T in the pool
+#define EA_A 3        // Y and A formed
+#define HF_B 3        // helperFlags(ct)[1] before the board: wave 0 has read J^T (b formed), dynamics done
+__device__ __forceinline__ int* earlyFlag(double* ct) { return reinterpret_cast<int*>(ct + H_COLLIDE) + 1; }
+__device__ __forceinline__ void earlyPost(double* ct, int state, int lane) {
+  if (lane == 0) __hip_atomic_store(earlyFlag(ct), state, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ int earlyState(double* ct) {
+  return uni(__hip_atomic_load(earlyFlag(ct), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+// spin until pred() (the early hand-off's waits, both waves); false when the
+// deadlock guard expired (or was forced at `site`, or the partner failed)
+template <class Pred>
+__device__ __forceinline__ bool earlyWait(double* ct, Pred pred, int site) {
+  if (guardForced(ct, site)) {
+    protocolFail(ct);
+    return false;
+  }
+  const long long t0 = spinClock();
+  for (int it = 0;; it++) {
+    if (pred()) return true;
     if (protocolFailed(ct) || spinExpired(t0, it)) {
       protocolFail(ct);
       return false;
@@ -655,7 +706,7 @@ __device__ __forceinline__ void collideWorld(const ModelDev& md, double* s, cons
                                              double* snapEdge, double* g_stamp = nullptr) {
   (void)g_stamp;
   double* ct = s + L.ct;
-  double* dropped = s + L.cscr;                         // past the dynamics buffers
+  double* dropped = s + L.cscr;                         // clear of the dynamics buffers
   double* pairbuf = dropped + CT_MAX_DROPPED * DROP_REC;
   if (lane == 0) { ct[H_NCON] = 0; ct[H_NDROP] = 0; ct[H_STATUS] = 0; }
   WSYNC();
@@ -928,6 +979,117 @@ __device__ inline double rowForceEntry(const ModelDev& md, const double* s, cons
   if (md.reactive[ba] && ((md.anc[ba] >> body) & 1ull)) val += sdot;
   if (md.reactive[bb] && ((md.anc[bb] >> body) & 1ull)) val -= sdot;
   return val;
+}
+
+// the LCP rows' per-row data and J^T (n x m, row i = dof i): the pool's
+struct RowsOut {
+  double *cols, *dvec, *lo, *hi, *rest;
+  int *fi, *rowC, *rowDir;
+};
+// rows (ContactConstraint: normal + 2 tangents with friction), lane =
+// contact; a contact's first row is its rank among the rows of the contacts
+// before it (popcount of the frictional ones).  Then J^T: lane = dof, loop
+// over the rows; the row's contact data are wave-uniform (rowForceEntry's
+// arithmetic, without a division-based (dof, row) unranking per element).
+// `rest` receives the row's restitution coefficient.
+__device__ __forceinline__ void buildRows(const ModelDev& md, const double* s, const Layout& L, const double* ct,
+                                          int nCon, int m, const RowsOut& O, int lane) {
+  const int n = md.n;
+  {
+    const int c = lane;
+    const bool live = c < nCon;
+    const double* rec = ct + CT_CONTACTS + (live ? c : 0) * CREC;
+    const int ba = (int)rec[8], bb = (int)rec[9];
+    const double mu = fmin(md.friction[ba], md.friction[bb]);
+    const double restC = md.restitution[ba] * md.restitution[bb];
+    const bool fr = live && mu > 1e-3;
+    const unsigned long long frm = __ballot(fr);  // (the whole wave: cross-lane ops stay out of divergent code)
+    if (live) {
+      int r = c + 2 * __popcll(frm & ((1ull << c) - 1ull));
+      const int base = r;
+      O.rowC[r] = c; O.rowDir[r] = 0;
+      for (int i = 0; i < 3; i++) O.dvec[3 * r + i] = rec[3 + i];
+      O.lo[r] = 0.0; O.hi[r] = __builtin_inf(); O.fi[r] = -1;
+      O.rest[r] = restC > 1e-3 ? restC : 0.0;
+      r++;
+      if (fr) {
+        double t1[3], t2[3];
+        tangentBasisODE(rec + 3, t1, t2);
+        for (int k = 0; k < 2; k++) {
+          O.rowC[r] = c; O.rowDir[r] = 1 + k;
+          for (int i = 0; i < 3; i++) O.dvec[3 * r + i] = k == 0 ? t1[i] : t2[i];
+          O.lo[r] = -mu; O.hi[r] = mu; O.fi[r] = base; O.rest[r] = 0.0;
+          r++;
+        }
+      }
+    }
+  }
+  WSYNC();
+  for (int i = lane; i < n; i += WAVE) {
+    const int body = md.dofBody[i];
+    double S[6];
+    for (int q = 0; q < 6; q++) S[q] = s[L.Sw + 6 * i + q];
+    for (int j = 0; j < m; j++) {
+      const double* rec = ct + CT_CONTACTS + uni(O.rowC[j]) * CREC;
+      const double* d = O.dvec + 3 * j;
+      double wr[6];
+      cross3(rec, d, wr);
+      wr[3] = d[0]; wr[4] = d[1]; wr[5] = d[2];
+      const double sdot = dot6(S, wr);
+      const int ba = uni((int)rec[8]), bb = uni((int)rec[9]);
+      double val = 0.0;
+      if (md.reactive[ba] && ((md.anc[ba] >> body) & 1ull)) val += sdot;
+      if (md.reactive[bb] && ((md.anc[bb] >> body) & 1ull)) val -= sdot;
+      O.cols[i * m + j] = val;
+    }
+  }
+  WSYNC();
+}
+
+// b = -J v1 (lane = row; J^T in `cols`)
+__device__ __forceinline__ void rowsRhs(const double* cols, const double* v1, double* b, int n, int m, int lane) {
+  for (int r = lane; r < m; r += WAVE) {
+    double acc = 0;
+#pragma unroll 8
+    for (int i = 0; i < n; i++) acc += cols[i * m + r] * v1[i];
+    b[r] = -acc;
+  }
+  WSYNC();
+}
+
+// Y = L^-1 J^T in place (J^T in Y) by columns (lane = column j): element
+// (i, j) receives -L_ik Y_kj for k = 0 .. i-1 in order and is then scaled by
+// 1/L_ii -- the same operation sequence as the row-by-row elimination,
+// without its two barriers per row.  (Eight columns per pass held in
+// registers with lane = dof row, readlane-broadcast like cholSolveReg,
+// measured 1.5x slower here.)  The L and Y operands of each 8-step block are
+// loaded together before its multiply-adds (LDS latency once per block; left
+// to the scheduler, every multiply-add waited on its own two loads: ~55k
+// clocks for the Atlas LCP).  Same operations in the same order.
+__device__ __forceinline__ void formY(double* Y, const double* Lm, const double* dinv, int n, int m, int lane) {
+  for (int j = lane; j < m; j += WAVE) {
+    for (int i = 0; i < n; i++) {
+      double acc = Y[i * m + j];
+      const double* Li = Lm + tri(i, 0);
+      int k = 0;
+      for (; k + 8 <= i; k += 8) {
+        double lv[8], yv[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          lv[u] = Li[k + u];
+          yv[u] = Y[(k + u) * m + j];
+        }
+        // (all sixteen issued before any is consumed)
+#pragma unroll
+        for (int u = 0; u < 8; u++) asm volatile("" : "+v"(lv[u]), "+v"(yv[u]));
+#pragma unroll
+        for (int u = 0; u < 8; u++) acc -= lv[u] * yv[u];
+      }
+      for (; k < i; k++) acc -= Li[k] * Y[k * m + j];
+      Y[i * m + j] = acc * dinv[i];
+    }
+  }
+  WSYNC();
 }
 
 // ---------------------------------------------------------------------------
@@ -2048,115 +2210,24 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   // (the pair counts are dead: the solvers' tally starts here, before any
   // task goes out to the helper)
   if (lane < 4) tallyOf(ct)[lane] = 0;
-  // rows (ContactConstraint: normal + 2 tangents with friction), lane =
-  // contact; a contact's first row is its rank among the rows of the
-  // contacts before it (popcount of the frictional ones)
-  {
-    const int c = lane;
-    const bool live = c < nCon;
-    const double* rec = ct + CT_CONTACTS + (live ? c : 0) * CREC;
-    const int ba = (int)rec[8], bb = (int)rec[9];
-    const double mu = fmin(md.friction[ba], md.friction[bb]);
-    const double restC = md.restitution[ba] * md.restitution[bb];
-    const bool fr = live && mu > 1e-3;
-    const unsigned long long frm = __ballot(fr);  // (the whole wave: cross-lane ops stay out of divergent code)
-    if (live) {
-    int r = c + 2 * __popcll(frm & ((1ull << c) - 1ull));
-    const int base = r;
-    P.rowC[r] = c; P.rowDir[r] = 0;
-    for (int i = 0; i < 3; i++) P.dvec[3 * r + i] = rec[3 + i];
-    P.lo[r] = 0.0; P.hi[r] = __builtin_inf(); P.fi[r] = -1;
-    P.rest[r] = restC > 1e-3 ? restC : 0.0;
-    r++;
-    if (fr) {
-      double t1[3], t2[3];
-      tangentBasisODE(rec + 3, t1, t2);
-      for (int k = 0; k < 2; k++) {
-        P.rowC[r] = c; P.rowDir[r] = 1 + k;
-        for (int i = 0; i < 3; i++) P.dvec[3 * r + i] = k == 0 ? t1[i] : t2[i];
-        P.lo[r] = -mu; P.hi[r] = mu; P.fi[r] = base; P.rest[r] = 0.0;
-        r++;
-      }
+  // the helper builds the rows and A (early rows, see EA_*): EA_NONE when it
+  // does not (stored before its CS_DONE, which wave 0 has taken)
+  const bool early = kLds && R == 1 && kK == 0 && helperOn && earlyState(ct) != EA_NONE;
+  if (early) {
+    if (!earlyWait(ct, [&]() { return earlyState(ct) >= EA_ROWS; }, GW_EARLY_ROWS)) {
+      protocolAbort(snap, cache, lane);
+      return;
     }
-    }
+  } else {
+    buildRows(md, s, L, ct, nCon, m, RowsOut{P.cols, P.dvec, P.lo, P.hi, P.rest, P.fi, P.rowC, P.rowDir}, lane);
   }
-  WSYNC();
-  // J^T (n x m, row i = dof i): lane = dof, loop over the rows; the row's
-  // contact data are wave-uniform (rowForceEntry's arithmetic, without a
-  // division-based (dof, row) unranking per element)
-  for (int i = lane; i < n; i += WAVE) {
-    const int body = md.dofBody[i];
-    double S[6];
-    for (int q = 0; q < 6; q++) S[q] = s[L.Sw + 6 * i + q];
-    for (int j = 0; j < m; j++) {
-      const double* rec = ct + CT_CONTACTS + uni(P.rowC[j]) * CREC;
-      const double* d = P.dvec + 3 * j;
-      double wr[6];
-      cross3(rec, d, wr);
-      wr[3] = d[0]; wr[4] = d[1]; wr[5] = d[2];
-      const double sdot = dot6(S, wr);
-      const int ba = uni((int)rec[8]), bb = uni((int)rec[9]);
-      double val = 0.0;
-      if (md.reactive[ba] && ((md.anc[ba] >> body) & 1ull)) val += sdot;
-      if (md.reactive[bb] && ((md.anc[bb] >> body) & 1ull)) val -= sdot;
-      P.cols[i * m + j] = val;
-    }
-  }
-  WSYNC();
   STAMP(2);
-  // Y = L^-1 J^T (row-parallel forward substitution; `massed` holds Y), so
-  // that A = J Minv J^T = Y^T Y and Minv J^T x = L^-T (Y x)
-  // b = -J v1 first: Y = L^-1 J^T is formed in place of J^T
-  for (int r = lane; r < m; r += WAVE) {
-    double acc = 0;
-#pragma unroll 8
-    for (int i = 0; i < n; i++) acc += P.cols[i * m + r] * v1[i];
-    P.b[r] = -acc;
-  }
-  WSYNC();
+  // b = -J v1 first: Y = L^-1 J^T is formed in place of J^T, so that
+  // A = J Minv J^T = Y^T Y and Minv J^T x = L^-T (Y x)
+  rowsRhs(P.cols, v1, P.b, n, m, lane);
+  if (early && lane == 0)  // (J^T read: the helper may overwrite it with Y)
+    __hip_atomic_store(helperFlags(ct) + 1, HF_B, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   STAMP(86);
-  {
-    // Y = L^-1 J^T by columns (lane = column j): element (i, j) receives
-    // -L_ik Y_kj for k = 0 .. i-1 in order and is then scaled by 1/L_ii --
-    // the same operation sequence as the row-by-row elimination, without
-    // its two barriers per row.  (Eight columns per pass held in registers
-    // with lane = dof row, readlane-broadcast like cholSolveReg, measured
-    // 1.5x slower here.)
-    // The L and Y operands of each 8-step block are loaded together before
-    // its multiply-adds (LDS latency once per block; left to the scheduler,
-    // every multiply-add waited on its own two loads: ~55k clocks for the
-    // Atlas LCP).  Same operations in the same order.
-    double* Y = P.massed;
-    for (int j = lane; j < m; j += WAVE) {
-      for (int i = 0; i < n; i++) {
-        double acc = Y[i * m + j];
-        const double* Li = Lm + tri(i, 0);
-        int k = 0;
-        for (; k + 8 <= i; k += 8) {
-          double lv[8], yv[8];
-#pragma unroll
-          for (int u = 0; u < 8; u++) {
-            lv[u] = Li[k + u];
-            yv[u] = Y[(k + u) * m + j];
-          }
-          // (all sixteen issued before any is consumed)
-#pragma unroll
-          for (int u = 0; u < 8; u++) asm volatile("" : "+v"(lv[u]), "+v"(yv[u]));
-#pragma unroll
-          for (int u = 0; u < 8; u++) acc -= lv[u] * yv[u];
-        }
-        for (; k < i; k++) acc -= Li[k] * Y[k * m + j];
-        Y[i * m + j] = acc * s[L.dinv + i];
-      }
-    }
-    WSYNC();
-    STAMP(87);
-    // A = Y^T Y on the matrix cores (the LCP matrix J Minv J^T)
-    gramMfma(Y, P.A, n, m, lane);
-    WSYNC();
-    STAMP(88);
-  }
-
   // penetration correction / restitution bounce of the normal rows (lane = row)
   for (int r = lane; r < m; r += WAVE) {
     P.pen[r] = 0.0;
@@ -2175,6 +2246,20 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
     P.b[r] += bv;
   }
   WSYNC();
+  if (early) {
+    if (!earlyWait(ct, [&]() { return earlyState(ct) == EA_A; }, GW_EARLY_A)) {
+      protocolAbort(snap, cache, lane);
+      return;
+    }
+    STAMP(87);
+  } else {
+    formY(P.massed, Lm, s + L.dinv, n, m, lane);
+    STAMP(87);
+    // A = Y^T Y on the matrix cores (the LCP matrix J Minv J^T)
+    gramMfma(P.massed, P.A, n, m, lane);
+    WSYNC();
+  }
+  STAMP(88);
   for (int j = lane; j < m; j += WAVE) {
     double acc = 0;
 #pragma unroll 8
@@ -2584,6 +2669,46 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
 // slots per lane, the pool P on chip (kLds) or in HBM; Dantzig's LDL^T factor
 // and scatter vector at Ldz / scrDz (LDS: the pool's M2 / xh2, or the wide
 // kernel's stage), the PGS fallback's reduced matrix at Mred.
+// The helper's end of the collision hand-off in the one-row kernel (see
+// EA_*): posts CS_DONE, then, when the world's LCP will run in the LDS pool
+// (wave 0 takes the same decision from the same contacts), builds the rows
+// and J^T there, and once wave 0 has formed b from them forms Y and A.
+// (deferRows: the kernel's threshold -- a world wave 0 defers to the wide
+// kernel never reaches the b hand-off, so the helper does not take it)
+__device__ __forceinline__ void helperEarly(const ModelDev& md, double* s, const Layout& L, int lane, int deferRows) {
+  double* ct = s + L.ct;
+  const int n = md.n;
+  const int nCon = uni((int)ct[H_NCON]);
+  bool fr = false;
+  if (lane < nCon) {
+    const double* rec = ct + CT_CONTACTS + lane * CREC;
+    fr = fmin(md.friction[(int)rec[8]], md.friction[(int)rec[9]]) > 1e-3;
+  }
+  const int m = nCon + 2 * __popcll(__ballot(fr));
+  const bool take = L.early > 0 && nCon > 0 && m <= WAVE && m <= deferRows && fwdPoolDoubles(m, n) <= L.poolCap;
+  if (!take) {
+    if (lane == 0) *earlyFlag(ct) = EA_NONE;  // (published by the release of CS_DONE)
+    collidePost(ct, CS_DONE, lane);
+    return;
+  }
+  collidePost(ct, CS_DONE, lane);
+  // (the world's critical path until A is built)
+  __builtin_amdgcn_s_setprio(2);
+  FwdPool P;
+  carveFwd(s + L.pool, m, n, P);
+  buildRows(md, s, L, ct, nCon, m, RowsOut{P.cols, P.dvec, P.lo, P.hi, P.rest, P.fi, P.rowC, P.rowDir}, lane);
+  earlyPost(ct, EA_ROWS, lane);
+  if (earlyWait(ct, [&]() {
+        return uni(__hip_atomic_load(helperFlags(ct) + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == HF_B;
+      }, GW_EARLY_B)) {
+    formY(P.massed, s + L.M, s + L.dinv, n, m, lane);
+    gramMfma(P.massed, P.A, n, m, lane);
+    WSYNC();
+    earlyPost(ct, EA_A, lane);
+  }
+  __builtin_amdgcn_s_setprio(0);
+}
+
 template <bool kLds, int R, bool kPL = false>
 __device__ __forceinline__ void helperTask(const ModelDev& md, double* ct, const FwdPool& Pin, int m, int lane,
                                            lds_double* Ldz, lds_double* scrDz, typename Space<kLds>::dptr Mred,

@@ -31,13 +31,18 @@ struct Layout {
   int ct, v1, pool, poolCap, dinv;
   // offset (doubles) of the dynamics cache inside each world's snapshot
   int snDyn;
-  // forward: narrow-phase scratch (dropped list + pair buffers), placed past
-  // the dynamics buffers V/A/IC/F so the helper wave can run the collision
-  // detection while wave 0 is still in the dynamics
+  // forward: narrow-phase scratch (dropped list + pair buffers), at the
+  // start of the area whose far end holds the dynamics buffers V/A/IC/F, so
+  // the helper wave can run the collision detection while wave 0 is still in
+  // the dynamics
   int cscr;
   // forward, wide kernels only: an LDS stage (offset, capacity in doubles)
   // for the COD factorisations of off-chip LCP pools (0: none)
   int stage, stageCap;
+  // forward, one-row kernel: 1 when the pool's rows slots
+  // (fwdPoolRowsDoubles) lie clear of the dynamics buffers, so that the
+  // helper may build the rows during the dynamics (contact.cuh EA_*); else -1
+  int early;
   int total;
 };
 

@@ -33,7 +33,7 @@
 #define MESH_PAIR_SCRATCH (16 * 64)
 // the forward's header + kept contacts live in Layout::ct; the dropped list
 // and the per-pair narrow-phase buffers (a mesh pair's records and scratch)
-// live at the start of the alias area past the dynamics buffers
+// live at the start of the alias area, clear of the dynamics buffers at its end
 __host__ __device__ inline int ctDoubles(int maxContacts) { return CT_CONTACTS + maxContacts * CREC; }
 __host__ __device__ inline int pairBufRecs(int pairChunk, bool mesh) {
   return mesh ? (MESH_PAIR_RECS > 8 * pairChunk ? MESH_PAIR_RECS : 8 * pairChunk) : 8 * pairChunk;
@@ -100,6 +100,11 @@ __host__ __device__ inline int snapWorkspaceOffset(int n) { return snStamps(n) +
 // (+24: codFactor's register path stages a 24-double column in the scratch)
 __host__ __device__ inline int fwdPoolDoubles(int m, int n) { return n * m + 3 * m * m + 33 * m + 2 * n + 72; }
 __host__ __device__ inline int bwdPoolDoubles(int m, int n) { return n * m + 24 * m + NV_COLS * n + 64; }
+
+// the rows' slots at the head of the forward pool (contact.cuh carveFwd: J^T,
+// boxes, restitution, directions, the int vectors), which the helper's early
+// rows write while wave 0 is still in the dynamics
+__host__ __device__ inline int fwdPoolRowsDoubles(int m, int n) { return n * m + 10 * m; }
 
 #define fwdPoolDoublesHost fwdPoolDoubles
 #define bwdPoolDoublesHost bwdPoolDoubles

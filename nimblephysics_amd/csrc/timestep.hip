@@ -333,6 +333,7 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
       hf[0] = HS_IDLE; hf[1] = 0; hf[3] = 0;
       hf[2] = (gs != 0 && (R == 1 || !(gs & GW_ONE_ROW_ONLY)) && env % md.guardStride == md.guardOffset) ? gs : 0;
       *collideFlag(s + L.ct) = CS_IDLE;
+      *earlyFlag(s + L.ct) = EA_PENDING;
     }
     __syncthreads();  // the one barrier both waves take: flags initialised
     if (threadIdx.x >= WAVE) {
@@ -358,7 +359,8 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
 #else
             collideWorld<kMesh>(md, lds<true>(s), L, lane, snapshot + (size_t)env * snapDoubles + snEdge(n));
 #endif
-            collidePost(ct, CS_DONE, lane);
+            // CS_DONE, then the early rows, Y and A (EA_*)
+            helperEarly(md, lds<true>(s), L, lane, deferRows);
           }
         }  // (the wide kernel's worlds come with the one-row kernel's contacts)
 #ifdef NIMBLE_STAGE_TIMING

@@ -34,7 +34,10 @@ STRIDE, OFFSET = 3, 1
 # site -> (GW_* mask, on every world's path, what a flagged world does)
 SITES = {"helper_go": (1, True, "abort"), "collide_done": (2, True, "abort"), "board": (8, False, "abort"),
          "collect": (32, False, "abort"), "helper_task": (64, True, "either"), "helper_idle": (256, True, "either"),
-         "retire": (512, True, "complete")}
+         "retire": (512, True, "complete"),
+         # the early rows' hand-off (one-row kernel, LCP in the LDS pool): the
+         # helper waiting for wave 0's dynamics, wave 0 for the rows and for A
+         "early_dyn": (2048, False, "abort"), "early_rows": (4096, False, "abort"), "early_a": (8192, False, "abort")}
 _base = {}
 
 

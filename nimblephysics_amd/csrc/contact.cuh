@@ -1059,34 +1059,57 @@ __device__ __forceinline__ void rowsRhs(const double* cols, const double* v1, do
 
 // Y = L^-1 J^T in place (J^T in Y) by columns (lane = column j): element
 // (i, j) receives -L_ik Y_kj for k = 0 .. i-1 in order and is then scaled by
-// 1/L_ii -- the same operation sequence as the row-by-row elimination,
-// without its two barriers per row.  (Eight columns per pass held in
-// registers with lane = dof row, readlane-broadcast like cholSolveReg,
-// measured 1.5x slower here.)  The L and Y operands of each 8-step block are
-// loaded together before its multiply-adds (LDS latency once per block; left
-// to the scheduler, every multiply-add waited on its own two loads: ~55k
-// clocks for the Atlas LCP).  Same operations in the same order.
+// 1/L_ii -- the same operation sequence as the row-by-row elimination.  Rows
+// in blocks of eight with their accumulators in registers: each earlier row
+// k (its Y_kj final, loaded once) updates the eight accumulators at once --
+// eight independent multiply-adds instead of one dependent chain per row --
+// then the block's own triangle in order, its Y values kept in registers.
+// Every element still sees its k terms in ascending order, so the same bits
+// as the row-at-a-time loop (which waited on each row's stored Y before the
+// next row's loads: ~33k clocks for the Atlas LCP's 33 x 24).
 __device__ __forceinline__ void formY(double* Y, const double* Lm, const double* dinv, int n, int m, int lane) {
   for (int j = lane; j < m; j += WAVE) {
-    for (int i = 0; i < n; i++) {
-      double acc = Y[i * m + j];
-      const double* Li = Lm + tri(i, 0);
-      int k = 0;
-      for (; k + 8 <= i; k += 8) {
-        double lv[8], yv[8];
+    for (int i0 = 0; i0 < n; i0 += 8) {
+      double acc[8], yb[8];
+      // (rows past n: clamped to row n - 1, their results unused)
+      int ro[8];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-          lv[u] = Li[k + u];
-          yv[u] = Y[(k + u) * m + j];
-        }
-        // (all sixteen issued before any is consumed)
-#pragma unroll
-        for (int u = 0; u < 8; u++) asm volatile("" : "+v"(lv[u]), "+v"(yv[u]));
-#pragma unroll
-        for (int u = 0; u < 8; u++) acc -= lv[u] * yv[u];
+      for (int u = 0; u < 8; u++) {
+        const int i = i0 + u < n ? i0 + u : n - 1;
+        ro[u] = tri(i, 0);
+        acc[u] = Y[i * m + j];
       }
-      for (; k < i; k++) acc -= Li[k] * Y[k * m + j];
-      Y[i * m + j] = acc * dinv[i];
+      // (four rows k per pass: their 36 loads issued before the 32
+      // multiply-adds, so the LDS latency is paid once per pass; i0 is a
+      // multiple of 8)
+      for (int k = 0; k < i0; k += 4) {
+        double yv[4], lv[4][8];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          yv[q] = Y[(k + q) * m + j];
+#pragma unroll
+          for (int u = 0; u < 8; u++) lv[q][u] = Lm[ro[u] + k + q];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          asm volatile("" : "+v"(yv[q]));
+#pragma unroll
+          for (int u = 0; u < 8; u++) asm volatile("" : "+v"(lv[q][u]));
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+#pragma unroll
+          for (int u = 0; u < 8; u++) acc[u] -= lv[q][u] * yv[q];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        if (i0 + u < n) {
+#pragma unroll
+          for (int v = 0; v < u; v++) acc[u] -= Lm[ro[u] + i0 + v] * yb[v];
+          yb[u] = acc[u] * dinv[i0 + u];
+          Y[(i0 + u) * m + j] = yb[u];
+        }
+      }
     }
   }
   WSYNC();

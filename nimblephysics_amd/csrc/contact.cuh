@@ -445,6 +445,8 @@ __device__ __forceinline__ void gramMfma(const double* Y, double* A, int n, int 
 #define HS_TASK 1
 #define HS_SKIP 2
 #define HS_DONE 3
+#define HS_POST 4      // (one-row kernel) wave 0's post-answer share for the helper, see contactLcp
+#define HS_POSTDONE 5  // ... done
 #define BD_G 0        // warm start final (P.xc): 1
 #define BD_D 1        // Dantzig: 0 running, 1 ok + valid, 2 failed, 3 not run (reduce merges)
 #define BD_PCLAIM 2   // PGS fallback: 0 unclaimed, 1 wave 0, 2 helper
@@ -510,6 +512,7 @@ __device__ __forceinline__ bool protocolFailed(double* ct) {
 #define GW_EARLY_B 2048       // helper: wave 0 has formed b (early rows, one-row kernel)
 #define GW_EARLY_ROWS 4096    // wave 0: the helper's early rows
 #define GW_EARLY_A 8192       // wave 0: the helper's A = Y^T Y
+#define GW_POST 16384         // wave 0: the helper's post-answer share (impulse, snapshot rows)
 __device__ __forceinline__ bool guardForced(double* ct, int site) { return (uni(helperFlags(ct)[2]) & site) != 0; }
 // spin with s_sleep until pred(state); -1 when the guard expired (or was
 // forced at `site`, or the partner failed)
@@ -2083,6 +2086,47 @@ __device__ void frictionlessPgsR(const double* PA, const double* Pb, const doubl
   }
 }
 
+// impulses (applyConstraintImpulses + computeImpulseForwardDynamics): the
+// velocity change u = Minv J^T x = L^-T (Y x) on lane i < n (and the
+// pre-impulse velocity into the snapshot)
+__device__ __forceinline__ double impulseDelta(const double* Y, const double* Xf, const double* Lm, const double* dinv,
+                                               const double* v1, double* snap, int n, int m, int lane) {
+  double u = 0.0;
+  if (lane < n) {
+#pragma unroll 4
+    for (int j = 0; j < m; j++) u += Y[lane * m + j] * Xf[j];
+    snap[SN_VF + lane] = v1[lane];
+  }
+  for (int k = n - 1; k >= 0; k--) {
+    const double uk = rdl(u, k) * dinv[k];
+    if (lane == k) u = uk;
+    else if (lane < k) u -= Lm[tri(k, lane)] * uk;
+  }
+  return u;
+}
+
+// the snapshot's contacts, rows, clamping impulses and unconstrained
+// acceleration
+__device__ __forceinline__ void snapshotRows(const FwdPool& P, const double* ct, const double* ddq, double* snap,
+                                             int nCon, int m, int nc, int n, int lane) {
+  for (int t = lane; t < nCon * CREC; t += WAVE) snap[SN_CONTACTS + t] = ct[CT_CONTACTS + t];
+  for (int j = lane; j < m; j += WAVE) {
+    double* rr = snap + SN_ROWS + j * SN_ROWREC;
+    rr[RR_CONTACT] = P.rowC[j];
+    rr[RR_DIR] = P.rowDir[j];
+    for (int i = 0; i < 3; i++) rr[RR_D + i] = P.dvec[3 * j + i];
+    rr[RR_B] = P.b[j];
+    rr[RR_X] = P.X[j];
+    rr[RR_MAP] = P.mapping[j];
+    rr[RR_CIDX] = P.clampIdx[j];
+    rr[RR_UIDX] = P.ubIdx[j];
+    rr[RR_EVAL] = P.Eval[j];
+    rr[RR_BOUNCE] = 1.0 + P.rest[j];
+  }
+  for (int i = lane; i < nc; i += WAVE) snap[SN_FC + i] = P.fc[i];
+  for (int i = lane; i < n; i += WAVE) snap[snYf(n) + i] = ddq[i];
+}
+
 // ---------------------------------------------------------------------------
 // The whole constraint stage of one world (World.cpp:254 runConstraintEngine
 // on the hot path): rows, A = J Minv J^T, b, LCP with the short-circuit,
@@ -2626,43 +2670,35 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   }
   const double* Xf = std2 ? P.X : P.xc;
   STAMP(8);
-  // impulses (applyConstraintImpulses + computeImpulseForwardDynamics):
-  // v1 += Minv J^T x = L^-T (Y x)
-  {
-    double u = 0.0;
-    if (lane < n) {
-#pragma unroll 4
-      for (int j = 0; j < m; j++) u += P.massed[lane * m + j] * Xf[j];
-      snap[SN_VF + lane] = v1[lane];
-    }
-    for (int k = n - 1; k >= 0; k--) {
-      const double uk = rdl(u, k) * s[L.dinv + k];
-      if (lane == k) u = uk;
-      else if (lane < k) u -= Lm[tri(k, lane)] * uk;
-    }
+  const int nc = uni((int)ct[H_NC]);
+  // The post-answer work in two shares (one-row kernel): the helper forms
+  // the impulse's velocity change into s + L.rhs (dead since the dynamics)
+  // and writes the snapshot's contacts and rows (HS_POST; the flag tells it
+  // which x the step keeps) while wave 0 runs the backward precompute --
+  // disjoint pool slots -- then wave 0 adds the change to v1.  Nothing of
+  // the state, the cache or the snapshot header is the helper's, so a
+  // protocol failure still leaves the contact-free step.
+  const bool postSplit = kLds && R == 1 && kK == 0 && helperOn;
+  if (postSplit) {
+    if (lane == 0) helperFlags(ct)[1] = std2 ? 1 : 0;
+    helperPost(ct, HS_POST, lane);
+  } else {
+    const double u = impulseDelta(P.massed, Xf, Lm, s + L.dinv, v1, snap, n, m, lane);
     WSYNC();
     if (lane < n) v1[lane] += u;
+    snapshotRows(P, ct, ddq, snap, nCon, m, nc, n, lane);
   }
   if (lane == 0) cache[0] = m;
   for (int i = lane; i < m; i += WAVE) cache[1 + i] = Xf[i];
-  for (int t = lane; t < nCon * CREC; t += WAVE) snap[SN_CONTACTS + t] = ct[CT_CONTACTS + t];
-  for (int j = lane; j < m; j += WAVE) {
-    double* rr = snap + SN_ROWS + j * SN_ROWREC;
-    rr[RR_CONTACT] = P.rowC[j];
-    rr[RR_DIR] = P.rowDir[j];
-    for (int i = 0; i < 3; i++) rr[RR_D + i] = P.dvec[3 * j + i];
-    rr[RR_B] = P.b[j];
-    rr[RR_X] = P.X[j];
-    rr[RR_MAP] = P.mapping[j];
-    rr[RR_CIDX] = P.clampIdx[j];
-    rr[RR_UIDX] = P.ubIdx[j];
-    rr[RR_EVAL] = P.Eval[j];
-    rr[RR_BOUNCE] = 1.0 + P.rest[j];
-  }
-  const int nc = uni((int)ct[H_NC]);
-  for (int i = lane; i < nc; i += WAVE) snap[SN_FC + i] = P.fc[i];
-  for (int i = lane; i < n; i += WAVE) snap[snYf(n) + i] = ddq[i];
   backwardPrecompute<kLds, R, kK>(md, sIn, md.lay[0], lane, poolIn, m, cfm, snap, sp<true>(ct), stage, stageCap);  // (not inlined)
+  if (postSplit) {
+    if (helperWait(ct, [](int v) { return v == HS_POSTDONE; }, GW_POST) < 0) {
+      protocolAbort(snap, cache, lane);
+      return;
+    }
+    if (lane < n) v1[lane] += s[L.rhs + lane];
+    WSYNC();
+  }
   if (lane == 0) {
     snap[SN_NCON] = nCon;
     snap[SN_M] = m;
@@ -2866,16 +2902,40 @@ __device__ __forceinline__ void helperTask(const ModelDev& md, double* ct, const
   }
 }
 
+// the helper's post-answer share (HS_POST, see contactLcp), then its end of
+// the world: POSTDONE, and wait until wave 0 has taken it
+__device__ __forceinline__ void helperPostShare(const ModelDev& md, double* s, const Layout& L, double* ct, double* snap,
+                                                int lane) {
+  const int n = md.n;
+  const int m = uni((int)ct[H_M]), nCon = uni((int)ct[H_NCON]), nc = uni((int)ct[H_NC]);
+  const bool std2 = uni(helperFlags(ct)[1]) != 0;
+  FwdPool P;
+  carveFwd(s + L.pool, m, n, P);
+  snap = gbl(snap);
+  const double u = impulseDelta(P.massed, std2 ? P.X : P.xc, s + L.M, s + L.dinv, s + L.v1, snap, n, m, lane);
+  if (lane < n) s[L.rhs + lane] = u;
+  snapshotRows(P, ct, s + L.x, snap, nCon, m, nc, n, lane);
+  helperPost(ct, HS_POSTDONE, lane);
+  helperWait(ct, [](int v) { return v != HS_POSTDONE; }, GW_HELPER_IDLE);
+}
+
 // kWide: the wide kernel's helper (both board modes); the one-row kernel's
 // only ever sees HB_LDS_POOL (a separate, smaller function: the wide mode's
 // registers made every call save ~160 callee-saved VGPRs to scratch)
+// (snap: the world's snapshot, for the one-row kernel's post-answer share)
 template <bool kWide>
-__device__ void helperWave(const ModelDev& md, double* s, const Layout& L, int lane, double* g_stamp, double* hbmPool) {
+__device__ void helperWave(const ModelDev& md, double* s, const Layout& L, int lane, double* g_stamp, double* hbmPool,
+                           double* snap) {
   (void)g_stamp;
   s = lds<true>(s);
   double* ct = s + L.ct;
-  const int st = helperWait(ct, [](int v) { return v == HS_TASK || v == HS_SKIP; }, GW_HELPER_TASK);
+  int st = helperWait(ct, [](int v) { return v == HS_TASK || v == HS_SKIP || (!kWide && v == HS_POST); },
+                      GW_HELPER_TASK);
   if (st < 0) return;  // (the deadlock guard expired: wave 0 goes on alone)
+  if (!kWide && st == HS_POST) {  // (no task went out)
+    helperPostShare(md, s, L, ct, snap, lane);
+    return;
+  }
   if (st == HS_TASK) {
     // the cascade's Dantzig is on the world's critical path: the helper
     // competes for issue with the other world's step wave on its SIMD
@@ -2897,7 +2957,8 @@ __device__ void helperWave(const ModelDev& md, double* s, const Layout& L, int l
   }
   __builtin_amdgcn_s_setprio(0);
   helperPost(ct, HS_DONE, lane);
-  helperWait(ct, [](int v) { return v != HS_DONE; }, GW_HELPER_IDLE);
+  st = helperWait(ct, [](int v) { return v != HS_DONE; }, GW_HELPER_IDLE);
+  if (!kWide && st == HS_POST) helperPostShare(md, s, L, ct, snap, lane);
 }
 
 // wave 0's end of a world's protocol: post SKIP if no task went out, collect
@@ -2906,7 +2967,8 @@ __device__ void helperWave(const ModelDev& md, double* s, const Layout& L, int l
 __device__ __forceinline__ void helperRetire(double* s, const Layout& L, int lane) {
   double* ct = lds<true>(s) + L.ct;
   if (helperState(ct) == HS_IDLE) helperPost(ct, HS_SKIP, lane);
-  helperWait(ct, [](int v) { return v == HS_DONE; }, GW_RETIRE);
+  // (POSTDONE: a post-answer share taken, the helper has answered already)
+  helperWait(ct, [](int v) { return v == HS_DONE || v == HS_POSTDONE; }, GW_RETIRE);
   helperPost(ct, HS_IDLE, lane);
 }
 

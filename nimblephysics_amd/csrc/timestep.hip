@@ -370,7 +370,8 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
 #endif
         // (the world's HBM LCP pool, the wide kernel's off-chip cascade)
         double* hbmPool = snapshot + (size_t)env * snapDoubles + snapWorkspaceOffset(n);
-        helperWave<(R > 1)>(md, s, md.lay[0], lane, hstamp, hbmPool);  // not inlined: the model's copy of L, not the argument's
+        helperWave<(R > 1)>(md, s, md.lay[0], lane, hstamp, hbmPool,
+                            snapshot + (size_t)env * snapDoubles);  // not inlined: the model's copy of L, not the argument's
       }
       return;
     }

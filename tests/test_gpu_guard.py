@@ -33,11 +33,17 @@ pytestmark = pytest.mark.gpu
 STRIDE, OFFSET = 3, 1
 # site -> (GW_* mask, on every world's path, what a flagged world does)
 SITES = {"helper_go": (1, True, "abort"), "collide_done": (2, True, "abort"), "board": (8, False, "abort"),
-         "collect": (32, False, "abort"), "helper_task": (64, True, "either"), "helper_idle": (256, True, "either"),
+         "collect": (32, False, "abort"), "helper_task": (64, True, "either"),
+         # (the helper's last wait: its failure there can come after wave 0
+         # has written the world's status -- a world that then shows no flag
+         # is bit-identical to the unforced run, which _check verifies)
+         "helper_idle": (256, False, "either"),
          "retire": (512, True, "complete"),
          # the early rows' hand-off (one-row kernel, LCP in the LDS pool): the
-         # helper waiting for wave 0's dynamics, wave 0 for the rows and for A
-         "early_dyn": (2048, False, "abort"), "early_rows": (4096, False, "abort"), "early_a": (8192, False, "abort")}
+         # helper waiting for wave 0's b, wave 0 for the rows and for A
+         "early_b": (2048, False, "abort"), "early_rows": (4096, False, "abort"), "early_a": (8192, False, "abort"),
+         # wave 0 waiting for the helper's post-answer share (impulse, snapshot rows)
+         "post": (16384, False, "abort")}
 _base = {}
 
 

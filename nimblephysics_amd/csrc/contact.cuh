@@ -1746,10 +1746,27 @@ __device__ __forceinline__ void pinvColumnsMfma(const lds_double* F, const lds_d
 // matrices it uses), computed here where A = J Minv J^T is on chip:
 // A_c, A_c_ub_E, Q = A_c^T Minv A_c_ub_E + cfm I, pinv(Q) (COD) and the
 // rank-deficiency flag ||I - Q Q^+||^2 >= 1e-18.
+// A_c and A_c_ub_E of the clamping rows into the snapshot (n x n_c each):
+// J^T columns re-evaluated from the rows' contacts and directions
+__device__ __forceinline__ void snapshotAc(const ModelDev& md, const double* s, const Layout& L, const FwdPool& P,
+                                          const double* cts, double* AcG, double* AcubEG, int m, int nc, int n,
+                                          int lane) {
+  for (int t = lane; t < n * nc; t += WAVE) {
+    const int i = t / nc, c = t % nc;
+    const int r = P.clampRow[c];
+    const double a = rowForceEntry(md, s, L, cts + P.rowC[r] * CREC, P.dvec + 3 * r, i);
+    double ae = a;
+    for (int u = r + 1; u <= r + 2 && u < m; u++)
+      if (P.mapping[u] == r) ae += P.Eval[u] * rowForceEntry(md, s, L, cts + P.rowC[u] * CREC, P.dvec + 3 * u, i);
+    AcG[t] = a;
+    AcubEG[t] = ae;
+  }
+}
+
 template <bool kLds, int R = 1, int kK = 0>  // (kK: as devConstruct)
 __device__ void backwardPrecompute(const ModelDev& md, lds_double* sIn, const Layout& L, int lane,
                                    typename Space<kLds>::dptr poolIn, int m, double cfm, double* snap, lds_double* ctIn,
-                                   lds_double* stage = nullptr, int stageCap = 0) {
+                                   lds_double* stage = nullptr, int stageCap = 0, bool acByHelper = false) {
   const int n = md.n;
   double* s = (double*)sIn;
   double* ct = (double*)ctIn;
@@ -1769,17 +1786,9 @@ __device__ void backwardPrecompute(const ModelDev& md, lds_double* sIn, const La
   double* QG = snap + snQ(n);
   const double* cts = s + L.ct + CT_CONTACTS;
   // A_c, A_c_ub_E (global): J^T columns re-evaluated (the on-chip copy of J^T
-  // was overwritten by Y)
-  for (int t = lane; t < n * nc; t += WAVE) {
-    const int i = t / nc, c = t % nc;
-    const int r = P.clampRow[c];
-    const double a = rowForceEntry(md, s, L, cts + P.rowC[r] * CREC, P.dvec + 3 * r, i);
-    double ae = a;
-    for (int u = r + 1; u <= r + 2 && u < m; u++)
-      if (P.mapping[u] == r) ae += P.Eval[u] * rowForceEntry(md, s, L, cts + P.rowC[u] * CREC, P.dvec + 3 * u, i);
-    AcG[t] = a;
-    AcubEG[t] = ae;
-  }
+  // was overwritten by Y); the helper's post-answer share in the one-row
+  // kernel (acByHelper)
+  if (!acByHelper) snapshotAc(md, s, L, P, cts, AcG, AcubEG, m, nc, n, lane);
   STAMP(46);
   STAMP(47);
   // Q into M1 (kept) and M2 (factored)
@@ -2673,7 +2682,8 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   const int nc = uni((int)ct[H_NC]);
   // The post-answer work in two shares (one-row kernel): the helper forms
   // the impulse's velocity change into s + L.rhs (dead since the dynamics)
-  // and writes the snapshot's contacts and rows (HS_POST; the flag tells it
+  // and writes the snapshot's contacts and rows and the clamping rows' J^T
+  // columns A_c, A_c_ub_E (HS_POST; the flag tells it
   // which x the step keeps) while wave 0 runs the backward precompute --
   // disjoint pool slots -- then wave 0 adds the change to v1.  Nothing of
   // the state, the cache or the snapshot header is the helper's, so a
@@ -2690,7 +2700,8 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   }
   if (lane == 0) cache[0] = m;
   for (int i = lane; i < m; i += WAVE) cache[1 + i] = Xf[i];
-  backwardPrecompute<kLds, R, kK>(md, sIn, md.lay[0], lane, poolIn, m, cfm, snap, sp<true>(ct), stage, stageCap);  // (not inlined)
+  backwardPrecompute<kLds, R, kK>(md, sIn, md.lay[0], lane, poolIn, m, cfm, snap, sp<true>(ct), stage, stageCap,
+                                  postSplit);  // (not inlined)
   if (postSplit) {
     if (helperWait(ct, [](int v) { return v == HS_POSTDONE; }, GW_POST) < 0) {
       protocolAbort(snap, cache, lane);
@@ -2915,6 +2926,7 @@ __device__ __forceinline__ void helperPostShare(const ModelDev& md, double* s, c
   const double u = impulseDelta(P.massed, std2 ? P.X : P.xc, s + L.M, s + L.dinv, s + L.v1, snap, n, m, lane);
   if (lane < n) s[L.rhs + lane] = u;
   snapshotRows(P, ct, s + L.x, snap, nCon, m, nc, n, lane);
+  if (nc > 0) snapshotAc(md, s, L, P, s + L.ct + CT_CONTACTS, snap + snAc(n), snap + snAcubE(n), m, nc, n, lane);
   helperPost(ct, HS_POSTDONE, lane);
   helperWait(ct, [](int v) { return v != HS_POSTDONE; }, GW_HELPER_IDLE);
 }

@@ -510,6 +510,7 @@ __device__ __forceinline__ bool protocolFailed(double* ct) {
 #define GW_RETIRE 512       // wave 0: the helper's DONE at the world's end
 #define GW_ONE_ROW_ONLY 1024  // (modifier) the sites in the one-row kernel only, not in the wide kernel
 #define GW_EARLY_B 2048       // helper: wave 0 has formed b (early rows, one-row kernel)
+#define GW_EARLY_DYN 32768    // helper: wave 0's dynamics done (early rows)
 #define GW_EARLY_ROWS 4096    // wave 0: the helper's early rows
 #define GW_EARLY_A 8192       // wave 0: the helper's A = Y^T Y
 #define GW_POST 16384         // wave 0: the helper's post-answer share (impulse, snapshot rows)
@@ -604,10 +605,12 @@ __device__ __forceinline__ bool collideWait(double* ct, int want, int site) {
 // J^T in the LDS pool -- their slots come first in the pool (carveFwd) and
 // the one-row kernel's layout puts the dynamics buffers at the far end of the
 // pool area (capi.cpp makeLayout, Layout::early), so they are clear of
-// everything wave 0 still uses.  Wave 0 forms b = -J v1 from that J^T and
-// posts HF_B (helperFlags(ct)[1], which the board's mode overwrites later);
-// the helper then forms Y = L^-1 J^T in its place and A = Y^T Y, and wave 0,
-// through the penetration terms meanwhile, meets a built A.  Same
+// everything wave 0 still uses.  Once wave 0's dynamics are done (HF_DYN in
+// helperFlags(ct)[1], which the board's mode overwrites later) the helper
+// forms Y = L^-1 J^T into M1 (+ M2, free until the cascade) and A = Y^T Y;
+// wave 0 forms b = -J v1 from J^T meanwhile and posts HF_B, after which the
+// helper moves Y into J^T's place; wave 0, through the penetration terms,
+// meets a built A.  Same
 // operations in the same order on the same operands as wave 0's own path,
 // so the same bits.  The helper's progress is the second int of H_COLLIDE
 // (written by the helper only; EA_NONE is stored before its CS_DONE):
@@ -615,7 +618,11 @@ __device__ __forceinline__ bool collideWait(double* ct, int want, int site) {
 #define EA_NONE 1     // not taken: wave 0 builds the rows itself
 #define EA_ROWS 2     // rows + J^T in the pool
 #define EA_A 3        // Y and A formed
-#define HF_B 3        // helperFlags(ct)[1] before the board: wave 0 has read J^T (b formed), dynamics done
+#define HF_DYN 2      // helperFlags(ct)[1] before the board: wave 0's dynamics are done (Cholesky final)
+#define HF_B 3        // ... and b formed: J^T read
+__device__ __forceinline__ void dynDonePost(double* ct, int lane) {
+  if (lane == 0) __hip_atomic_store(helperFlags(ct) + 1, HF_DYN, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 __device__ __forceinline__ int* earlyFlag(double* ct) { return reinterpret_cast<int*>(ct + H_COLLIDE) + 1; }
 __device__ __forceinline__ void earlyPost(double* ct, int state, int lane) {
   if (lane == 0) __hip_atomic_store(earlyFlag(ct), state, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1070,7 +1077,9 @@ __device__ __forceinline__ void rowsRhs(const double* cols, const double* v1, do
 // Every element still sees its k terms in ascending order, so the same bits
 // as the row-at-a-time loop (which waited on each row's stored Y before the
 // next row's loads: ~33k clocks for the Atlas LCP's 33 x 24).
-__device__ __forceinline__ void formY(double* Y, const double* Lm, const double* dinv, int n, int m, int lane) {
+// (Jt: J^T, n x m; Y: the result, in place when Y == Jt)
+__device__ __forceinline__ void formY(double* Y, const double* Jt, const double* Lm, const double* dinv, int n, int m,
+                                      int lane) {
   for (int j = lane; j < m; j += WAVE) {
     for (int i0 = 0; i0 < n; i0 += 8) {
       double acc[8], yb[8];
@@ -1080,7 +1089,7 @@ __device__ __forceinline__ void formY(double* Y, const double* Lm, const double*
       for (int u = 0; u < 8; u++) {
         const int i = i0 + u < n ? i0 + u : n - 1;
         ro[u] = tri(i, 0);
-        acc[u] = Y[i * m + j];
+        acc[u] = Jt[i * m + j];
       }
       // (four rows k per pass: their 36 loads issued before the 32
       // multiply-adds, so the LDS latency is paid once per pass; i0 is a
@@ -2329,7 +2338,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
     }
     STAMP(87);
   } else {
-    formY(P.massed, Lm, s + L.dinv, n, m, lane);
+    formY(P.massed, P.cols, Lm, s + L.dinv, n, m, lane);
     STAMP(87);
     // A = Y^T Y on the matrix cores (the LCP matrix J Minv J^T)
     gramMfma(P.massed, P.A, n, m, lane);
@@ -2768,13 +2777,31 @@ __device__ __forceinline__ void helperEarly(const ModelDev& md, double* s, const
   carveFwd(s + L.pool, m, n, P);
   buildRows(md, s, L, ct, nCon, m, RowsOut{P.cols, P.dvec, P.lo, P.hi, P.rest, P.fi, P.rowC, P.rowDir}, lane);
   earlyPost(ct, EA_ROWS, lane);
-  if (earlyWait(ct, [&]() {
-        return uni(__hip_atomic_load(helperFlags(ct) + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == HF_B;
-      }, GW_EARLY_B)) {
-    formY(P.massed, s + L.M, s + L.dinv, n, m, lane);
-    gramMfma(P.massed, P.A, n, m, lane);
-    WSYNC();
-    earlyPost(ct, EA_A, lane);
+  // Y into M1 (+ M2, free until the cascade; when they hold n x m) while
+  // wave 0 still needs J^T for b, A = Y^T Y from there, and Y moves into
+  // J^T's place once wave 0 has b; otherwise Y in place after b
+  double* Yt = P.M1;
+  const bool aside = n * m <= m * m + m * (m | 1);
+  auto flagAtLeast = [&](int v) {
+    return uni(__hip_atomic_load(helperFlags(ct) + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) >= v;
+  };
+  if (earlyWait(ct, [&]() { return flagAtLeast(HF_DYN); }, GW_EARLY_DYN)) {
+    if (aside) {
+      formY(Yt, P.cols, s + L.M, s + L.dinv, n, m, lane);
+      gramMfma(Yt, P.A, n, m, lane);
+      WSYNC();
+    }
+    if (earlyWait(ct, [&]() { return flagAtLeast(HF_B); }, GW_EARLY_B)) {
+      if (aside) {
+        for (int t = lane; t < n * m; t += WAVE) P.massed[t] = Yt[t];
+        WSYNC();
+      } else {
+        formY(P.massed, P.cols, s + L.M, s + L.dinv, n, m, lane);
+        gramMfma(P.massed, P.A, n, m, lane);
+        WSYNC();
+      }
+      earlyPost(ct, EA_A, lane);
+    }
   }
   __builtin_amdgcn_s_setprio(0);
 }

@@ -419,6 +419,9 @@ __device__ __forceinline__ void forwardWorld(const ModelDev* __restrict__ mdp, c
     cholesky(s + L.M, s + L.dinv, md.n, lane);
     STAMP(17);
     dynCacheCopy(md, s, L, snapshot + (size_t)env * snapDoubles + L.snDyn, true, lane);
+    // V, A, IC, F dead, the Cholesky factor final: the helper's early rows
+    // may turn into Y and A (contact.cuh EA_*)
+    if (helperOn) dynDonePost(lds<true>(s) + L.ct, lane);
     STAMP(11);
     }
     // rhs = tau + spring + damping - C   (GenericJoint::updateTotalForceDynamic)

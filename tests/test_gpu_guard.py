@@ -41,7 +41,7 @@ SITES = {"helper_go": (1, True, "abort"), "collide_done": (2, True, "abort"), "b
          "retire": (512, True, "complete"),
          # the early rows' hand-off (one-row kernel, LCP in the LDS pool): the
          # helper waiting for wave 0's b, wave 0 for the rows and for A
-         "early_b": (2048, False, "abort"), "early_rows": (4096, False, "abort"), "early_a": (8192, False, "abort"),
+         "early_b": (2048, False, "abort"), "early_dyn": (32768, False, "abort"), "early_rows": (4096, False, "abort"), "early_a": (8192, False, "abort"),
          # wave 0 waiting for the helper's post-answer share (impulse, snapshot rows)
          "post": (16384, False, "abort")}
 _base = {}

@@ -302,7 +302,7 @@ def test_bench_atlas_lds_fits_four_worlds_per_cu():
 # "either" -- which one depends on where wave 0 is when the helper gives up
 GUARD_SITES = {"helper_go": (1, "abort"), "collide_done": (2, "abort"), "board": (8, "abort"),
                "collect": (32, "abort"), "helper_task": (64, "abort"), "helper_idle": (256, "either"),
-               "retire": (512, "complete"), "early_b": (2048, "abort"), "early_rows": (4096, "abort"),
+               "retire": (512, "complete"), "early_b": (2048, "abort"), "early_dyn": (32768, "abort"), "early_rows": (4096, "abort"),
                "early_a": (8192, "abort"), "post": (16384, "abort")}
 
 

@@ -1078,8 +1078,8 @@ __device__ __forceinline__ void rowsRhs(const double* cols, const double* v1, do
 // as the row-at-a-time loop (which waited on each row's stored Y before the
 // next row's loads: ~33k clocks for the Atlas LCP's 33 x 24).
 // (Jt: J^T, n x m; Y: the result, in place when Y == Jt)
-__device__ __forceinline__ void formY(double* Y, const double* Jt, const double* Lm, const double* dinv, int n, int m,
-                                      int lane) {
+__device__ __forceinline__ void formYWide(double* Y, const double* Jt, const double* Lm, const double* dinv, int n,
+                                          int m, int lane) {
   for (int j = lane; j < m; j += WAVE) {
     for (int i0 = 0; i0 < n; i0 += 8) {
       double acc[8], yb[8];
@@ -1125,6 +1125,86 @@ __device__ __forceinline__ void formY(double* Y, const double* Jt, const double*
     }
   }
   WSYNC();
+}
+
+// Up to 32 columns: the wave's two halves share each 8-row block, lane = 32 h
+// + column, half h holding rows i0 + 4 h .. i0 + 4 h + 3 -- half the
+// accumulators and L loads per earlier row.  The block's triangle: half 0's
+// four rows, then half 1's (their terms from half 0's rows first, through
+// LDS), each element's terms still in ascending k.
+__device__ __forceinline__ void formY(double* Y, const double* Jt, const double* Lm, const double* dinv, int n, int m,
+                                      int lane) {
+  if (m > 32) {
+    formYWide(Y, Jt, Lm, dinv, n, m, lane);
+    return;
+  }
+  const int h = lane >> 5, j = lane & 31;
+  const bool live = j < m;
+  const int jc = live ? j : 0;
+  for (int i0 = 0; i0 < n; i0 += 8) {
+    double acc[4], yb[4];
+    int ro[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int r = i0 + 4 * h + u;
+      const int i = r < n ? r : n - 1;  // (rows past n: clamped, results unused)
+      ro[u] = tri(i, 0);
+      acc[u] = Jt[i * m + jc];
+    }
+    // rows before the block, four per pass (i0 is a multiple of 8)
+    for (int k = 0; k < i0; k += 4) {
+      double yv[4], lv[4][4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        yv[q] = Y[(k + q) * m + jc];
+#pragma unroll
+        for (int u = 0; u < 4; u++) lv[q][u] = Lm[ro[u] + k + q];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        asm volatile("" : "+v"(yv[q]));
+#pragma unroll
+        for (int u = 0; u < 4; u++) asm volatile("" : "+v"(lv[q][u]));
+      }
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int u = 0; u < 4; u++) acc[u] -= lv[q][u] * yv[q];
+    }
+    // half 0's rows
+    if (h == 0) {
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        if (i0 + u < n) {
+#pragma unroll
+          for (int v = 0; v < u; v++) acc[u] -= Lm[ro[u] + i0 + v] * yb[v];
+          yb[u] = acc[u] * dinv[i0 + u];
+          if (live) Y[(i0 + u) * m + j] = yb[u];
+        }
+      }
+    }
+    WSYNC();
+    // half 1's rows: half 0's four rows' terms, then their own triangle
+    if (h == 1 && i0 + 4 < n) {
+      double y0[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) y0[q] = Y[(i0 + q) * m + jc];
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int u = 0; u < 4; u++) acc[u] -= Lm[ro[u] + i0 + q] * y0[q];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        if (i0 + 4 + u < n) {
+#pragma unroll
+          for (int v = 0; v < u; v++) acc[u] -= Lm[ro[u] + i0 + 4 + v] * yb[v];
+          yb[u] = acc[u] * dinv[i0 + 4 + u];
+          if (live) Y[(i0 + 4 + u) * m + j] = yb[u];
+        }
+      }
+    }
+    WSYNC();
+  }
 }
 
 // ---------------------------------------------------------------------------

@@ -1,5 +1,6 @@
 // Y = L^-1 J^T micro-benchmark (contact.cuh formY, the LCP rows' massed
 // columns): n = 33 dofs, m = 24 rows, one problem per 64-lane wave in LDS,
+// (blocked: formYWide; halves: formY's two-half form for <= 32 columns)
 // against the row-at-a-time loop it replaced (kept here as the reference:
 // the results must be bit-identical).  Clocks per call, solo and at 2048
 // waves (two per SIMD).  Prints JSON.
@@ -49,7 +50,8 @@ extern "C" __global__ void __launch_bounds__(64) formy_bench(double* out, int n,
   __syncthreads();
   const long long t0 = __builtin_amdgcn_s_memtime();
   if (variant == 0) formYRows(Y, Lm, dinv, n, m, lane);
-  else formY(Y, Lm, dinv, n, m, lane);
+  else if (variant == 1) formYWide(Y, Y, Lm, dinv, n, m, lane);
+  else formY(Y, Y, Lm, dinv, n, m, lane);
   const long long t1 = __builtin_amdgcn_s_memtime();
   for (int t = lane; t < n * m; t += 64) out[(size_t)w * (n * m + 1) + 1 + t] = Y[t];
   if (lane == 0) out[(size_t)w * (n * m + 1)] = (double)(t1 - t0);
@@ -59,9 +61,10 @@ int main() {
   const int n = 33, m = 24, rec = n * m + 1;
   double* d;
   hipMalloc(&d, (size_t)2048 * rec * sizeof(double));
-  std::vector<double> h[2];
+  std::vector<double> h[3];
   std::printf("{");
-  for (int v = 0; v < 2; v++) {
+  const char* names[3] = {"rows", "blocked", "halves"};
+  for (int v = 0; v < 3; v++) {
     for (int B : {1, 2048}) {
       for (int rep = 0; rep < 2; rep++) hipLaunchKernelGGL(formy_bench, dim3(B), dim3(64), 0, 0, d, n, m, v);
       hipDeviceSynchronize();
@@ -69,13 +72,15 @@ int main() {
       hipMemcpy(o.data(), d, o.size() * sizeof(double), hipMemcpyDeviceToHost);
       double clk = 0;
       for (int w = 0; w < B; w++) clk += o[(size_t)w * rec];
-      std::printf("%s\"%s_%s\": %.0f", (v || B > 1) ? ", " : "", v ? "blocked" : "rows", B == 1 ? "solo" : "2048", clk / B);
+      std::printf("%s\"%s_%s\": %.0f", (v || B > 1) ? ", " : "", names[v], B == 1 ? "solo" : "2048", clk / B);
       if (B == 2048) h[v] = o;
     }
   }
-  size_t diff = 0;
-  for (size_t i = 0; i < h[0].size(); i++)
+  size_t diff = 0, diff2 = 0;
+  for (size_t i = 0; i < h[0].size(); i++) {
     if (i % rec && h[0][i] != h[1][i]) diff++;
-  std::printf(", \"elements_differing\": %zu}\n", diff);
+    if (i % rec && h[0][i] != h[2][i]) diff2++;
+  }
+  std::printf(", \"elements_differing\": %zu, \"elements_differing_halves\": %zu}\n", diff, diff2);
   return 0;
 }

@@ -270,15 +270,38 @@ __device__ __forceinline__ void dynCacheCopy(const ModelDev& md, double* s, cons
   const int n = md.n, nb = md.nb;
   const int seg[6][2] = {{L.Tw, 12 * nb}, {L.Sw, 6 * n}, {L.V, 6 * nb},
                          {L.M, n * (n + 1) / 2}, {L.dinv, n}, {L.rhs, n}};
-  int o = 0;
-  for (int k = 0; k < 6; k++) {
-    const int base = seg[k][0], cnt = seg[k][1];
-    if (base < 0) { o += cnt; continue; }  // region not kept in this kernel's LDS
-    if (store)
-      for (int t = lane; t < cnt; t += WAVE) cache[o + t] = s[base + t];
-    else
-      for (int t = lane; t < cnt; t += WAVE) s[base + t] = cache[o + t];
-    o += cnt;
+  if (store) {
+    int o = 0;
+    for (int k = 0; k < 6; k++) {
+      const int base = seg[k][0], cnt = seg[k][1];
+      if (base >= 0)  // (else: region not kept in this kernel's LDS)
+        for (int t = lane; t < cnt; t += WAVE) cache[o + t] = s[base + t];
+      o += cnt;
+    }
+  } else {
+    // the load: eight elements per lane in flight (one HBM latency per 512
+    // doubles instead of one per 64: the backward's load of the 1,455-double
+    // Atlas cache took ~21k clocks one pass at a time), each element mapped
+    // to its region by the segment ends (every region is kept on load)
+    const int total = dynCacheDoubles(n, nb);
+    const int e0 = 12 * nb, e1 = e0 + 6 * n, e2 = e1 + 6 * nb, e3 = e2 + n * (n + 1) / 2, e4 = e3 + n;
+    for (int t0 = lane; t0 < total; t0 += 8 * WAVE) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int t = t0 + u * WAVE;
+        v[u] = t < total ? cache[t] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int t = t0 + u * WAVE;
+        if (t < total) {
+          const int base = t < e0 ? L.Tw : t < e1 ? L.Sw - e0 : t < e2 ? L.V - e1 : t < e3 ? L.M - e2
+                         : t < e4 ? L.dinv - e3 : L.rhs - e4;
+          s[base + t] = v[u];
+        }
+      }
+    }
   }
   WSYNC();
 }

@@ -5,6 +5,7 @@ construct-like matrices (Q = Y^T Y of rank r <= n, and full-rank ones).
   python tools/micro/cod_bench.py run     # GPU box: clocks, rank, solution
   python tools/micro/cod_bench.py mfma    # GPU box: QR phase split + MFMA rank-4 update
   python tools/micro/cod_bench.py wide    # GPU box: the two-slot LDS factorisation at 64..100
+  python tools/micro/cod_bench.py ab      # GPU box: register QR vs dbg/libcod_reg_old.so (a previous build)
 """
 import ctypes as C
 import os
@@ -176,5 +177,31 @@ def wide(P=512, seed=1):
     print(json.dumps(res, indent=1))
 
 
+def ab(old=os.path.join(ROOT, "dbg", "libcod_reg_old.so")):
+    """A/B of the register QR against a previous build of it (same problems):
+    clocks at n = 24 and whether factor outputs (solution, rank) are
+    bit-identical."""
+    import torch
+    n, A, b = problems()
+    P = len(n)
+    dev = torch.device("cuda:0")
+    T = [torch.tensor(x, device=dev) for x in (n, A, b)]
+    s = torch.cuda.current_stream().cuda_stream
+    res = {}
+    for k, lib in (("old", old), ("new", LIBS["reg"])):
+        L = C.CDLL(lib)
+        out = torch.zeros((P, REC), dtype=torch.float64, device=dev)
+        for _ in range(3):
+            assert L.cod_bench_launch(C.c_int(P), C.c_int(NMAX), *[C.c_void_p(t.data_ptr()) for t in T],
+                                      C.c_void_p(out.data_ptr()), C.c_int(REC), C.c_void_p(s)) == 0
+        torch.cuda.synchronize()
+        res[k] = out.cpu().numpy()
+        sel = n == 24
+        print(f"{k}: n=24 factor clocks {res[k][sel, 0].mean():.0f}, solve {res[k][sel, 1].mean():.0f}")
+    same = np.array_equal(np.nan_to_num(res["old"][:, 8:]), np.nan_to_num(res["new"][:, 8:])) and \
+        np.array_equal(res["old"][:, 2], res["new"][:, 2])
+    print(f"bit-identical solutions and ranks: {same}")
+
+
 if __name__ == "__main__":
-    {"build": build, "run": run, "mfma": mfma, "wide": wide}[sys.argv[1] if len(sys.argv) > 1 else "run"]()
+    {"build": build, "run": run, "mfma": mfma, "wide": wide, "ab": ab}[sys.argv[1] if len(sys.argv) > 1 else "run"]()

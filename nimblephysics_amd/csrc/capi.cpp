@@ -242,6 +242,8 @@ int nimble_world_create(const nimble_world_desc* d, nimble_world_t* out) {
   // NIMBLE_AMD_HELPER_PRIO (measurements): the helper's priority on the task board
   m.helperPrio = 0;
   if (const char* e = getenv("NIMBLE_AMD_HELPER_PRIO")) m.helperPrio = atoi(e) & 3;
+  m.postSplit = 1;
+  if (const char* e = getenv("NIMBLE_AMD_POST_SPLIT")) m.postSplit = atoi(e) != 0;
   m.pinvMfma = 1;
   if (const char* e = getenv("NIMBLE_AMD_PINV_MFMA")) m.pinvMfma = atoi(e) != 0 ? 1 : 0;
   // NIMBLE_AMD_GUARD_TEST="sites:stride:offset" (tests only): force the

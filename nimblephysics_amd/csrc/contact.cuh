@@ -2777,7 +2777,7 @@ __device__ __forceinline__ void contactLcp(const ModelDev& md, lds_double* sIn, 
   // disjoint pool slots -- then wave 0 adds the change to v1.  Nothing of
   // the state, the cache or the snapshot header is the helper's, so a
   // protocol failure still leaves the contact-free step.
-  const bool postSplit = kLds && R == 1 && kK == 0 && helperOn;
+  const bool postSplit = kLds && R == 1 && kK == 0 && helperOn && md.postSplit;
   if (postSplit) {
     if (lane == 0) helperFlags(ct)[1] = std2 ? 1 : 0;
     helperPost(ct, HS_POST, lane);

@@ -87,6 +87,9 @@ struct ModelDev {
   // issue priority (s_setprio) of the forward's helper wave while it runs
   // its share of the LCP cascade (the collision detection runs at 0)
   int helperPrio;
+  // the forward's post-answer work in two shares (contact.cuh HS_POST; 0:
+  // wave 0 alone, NIMBLE_AMD_POST_SPLIT=0, for tests and measurements)
+  int postSplit;
   // backwardPrecompute's pinv(Q) of the wide worlds as blocked MFMA products
   // (contact.cuh pinvColumnsMfma) when the factor has full rank; 0: the
   // per-column solves (NIMBLE_AMD_PINV_MFMA=0, measurements)
